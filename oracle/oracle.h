@@ -1,0 +1,104 @@
+/* oracle/oracle.h — TEST INFRASTRUCTURE ONLY. CPU restatements used as the parity checker.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load liboracle.so. */
+#ifndef CORRO_ORACLE_H
+#define CORRO_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { OF_INTEGER = 1, OF_REAL = 2, OF_TEXT = 3, OF_BLOB = 4, OF_NULL = 5 };
+
+/* Column-change batch, SoA, application order = index order (same field order as
+ * corro_changes in include/corro_hip.h). table_cid = (table << 16) | cid, cid 0 = sentinel '-1'. */
+typedef struct {
+    uint64_t n;
+    const uint64_t *pk;
+    const uint32_t *table_cid;
+    const int64_t *col_version;
+    const int64_t *db_version;
+    const uint32_t *cl;
+    const uint32_t *seq;
+    const uint32_t *site;      /* site ordinal */
+    const uint64_t *val0;      /* INTEGER bits / REAL bits / TEXT,BLOB bytes 0..7 big-endian */
+    const uint64_t *val1;      /* optional: TEXT,BLOB bytes 8..15 big-endian */
+    const uint8_t *val_type;   /* optional: OF_* (NULL = all INTEGER) */
+    const uint8_t *val_len;    /* optional: TEXT/BLOB length (<= 16) */
+    const uint64_t *ts;        /* optional: changeset timestamp (NTP64) */
+} of_changes;
+
+typedef struct {
+    uint64_t *pk;
+    uint32_t *table_cid;
+    int64_t *col_version;
+    int64_t *db_version;
+    int64_t *cl;
+    uint32_t *seq;
+    uint32_t *site;
+    uint64_t *ts;
+    uint64_t *val0;
+    uint64_t *val1;
+    uint8_t *val_type;
+    uint8_t *val_len;
+} of_rows;
+
+typedef struct of_state of_state;
+
+of_state *of_new(const uint8_t *site_ids, uint32_t nsites);
+void of_free(of_state *s);
+void of_apply(of_state *s, const of_changes *in, uint8_t *impact_out);
+uint64_t of_count(const of_state *s);
+uint64_t of_export(const of_state *s, of_rows *out);
+void of_db_versions(const of_state *s, int64_t *out);
+
+/* ---- sync need diff (corro-types/src/sync.rs:127-249), CSR over (pair, actor) entries ---- */
+typedef struct {
+    uint64_t n;                 /* entries */
+    const uint64_t *their_head; /* > 0 (entries with head 0 / self actor are skipped by the caller) */
+    const int64_t *our_head;    /* -1 = we have no head for the actor */
+    const uint64_t *tn_off;     /* their need ranges: [tn_off[e], tn_off[e+1]) */
+    const uint64_t *tn_start, *tn_end;
+    const uint64_t *tp_off;     /* their partial versions */
+    const uint64_t *tp_ver;
+    const uint64_t *tps_off;    /* per their partial k: seq ranges [tps_off[k], tps_off[k+1]) */
+    const uint64_t *tps_start, *tps_end;
+    const uint64_t *on_off;     /* our need ranges */
+    const uint64_t *on_start, *on_end;
+    const uint64_t *op_off;     /* our partial versions */
+    const uint64_t *op_ver;
+    const uint64_t *ops_off;
+    const uint64_t *ops_start, *ops_end;
+} of_sync_entries;
+
+typedef struct {
+    /* count pass writes per-entry totals; fill pass writes the CSR */
+    uint64_t *need_count;   /* per entry: number of SyncNeedV1 */
+    uint64_t *seq_count;    /* per entry: number of seq ranges over its partial needs */
+    /* fill pass (offsets = exclusive scans of the counts) */
+    const uint64_t *need_off, *seq_off;
+    uint8_t *kind;          /* 0 = Full, 1 = Partial */
+    uint64_t *start, *end;  /* Full: versions start..=end; Partial: version in start, seq ranges in [sr_off[k], sr_off[k+1]) */
+    uint64_t *sr_off;       /* per need: absolute offset of its first seq range (size = total needs) */
+    uint64_t *sr_n;         /* per need: number of seq ranges */
+    uint64_t *s_start, *s_end;
+} of_needs_out;
+
+void of_needs(const of_sync_entries *in, of_needs_out *out, int fill);
+
+/* ---- gap bookkeeping (corro-types/src/agent.rs:1108-1235) ---- */
+typedef struct of_booked of_booked;
+of_booked *of_booked_new(void);
+void of_booked_free(of_booked *b);
+/* insert_db of the RangeInclusiveSet built from `n` ranges; returns 0 on success */
+int of_booked_insert_db(of_booked *b, const uint64_t *start, const uint64_t *end, uint64_t n);
+/* needed ranges -> out (caller sized by of_booked_needed_len) */
+uint64_t of_booked_needed_len(const of_booked *b);
+void of_booked_needed(const of_booked *b, uint64_t *start, uint64_t *end);
+int64_t of_booked_max(const of_booked *b);  /* -1 = None */
+int of_booked_contains(const of_booked *b, uint64_t version);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

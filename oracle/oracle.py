@@ -1,0 +1,224 @@
+"""ctypes binding for liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, and only
+as the checker (or the timed CPU baseline). The product (corrosion_amd) never touches it.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+OF_INTEGER, OF_REAL, OF_TEXT, OF_BLOB, OF_NULL = 1, 2, 3, 4, 5
+
+_u64p = C.POINTER(C.c_uint64)
+
+
+class _Changes(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("pk", C.c_void_p), ("table_cid", C.c_void_p),
+                ("col_version", C.c_void_p), ("db_version", C.c_void_p), ("cl", C.c_void_p),
+                ("seq", C.c_void_p), ("site", C.c_void_p), ("val0", C.c_void_p),
+                ("val1", C.c_void_p), ("val_type", C.c_void_p), ("val_len", C.c_void_p),
+                ("ts", C.c_void_p)]
+
+
+class _Rows(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("pk", "table_cid", "col_version", "db_version", "cl",
+                                          "seq", "site", "ts", "val0", "val1", "val_type",
+                                          "val_len")]
+
+
+class _SyncEntries(C.Structure):
+    _fields_ = [("n", C.c_uint64)] + [(k, C.c_void_p) for k in (
+        "their_head", "our_head", "tn_off", "tn_start", "tn_end", "tp_off", "tp_ver", "tps_off",
+        "tps_start", "tps_end", "on_off", "on_start", "on_end", "op_off", "op_ver", "ops_off",
+        "ops_start", "ops_end")]
+
+
+class _NeedsOut(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("need_count", "seq_count", "need_off", "seq_off", "kind",
+                                          "start", "end", "sr_off", "sr_n", "s_start", "s_end")]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.of_new.restype = C.c_void_p
+        L.of_new.argtypes = [C.c_void_p, C.c_uint32]
+        L.of_free.argtypes = [C.c_void_p]
+        L.of_apply.argtypes = [C.c_void_p, C.POINTER(_Changes), C.c_void_p]
+        L.of_count.restype = C.c_uint64
+        L.of_count.argtypes = [C.c_void_p]
+        L.of_export.restype = C.c_uint64
+        L.of_export.argtypes = [C.c_void_p, C.POINTER(_Rows)]
+        L.of_db_versions.argtypes = [C.c_void_p, C.c_void_p]
+        L.of_needs.argtypes = [C.POINTER(_SyncEntries), C.POINTER(_NeedsOut), C.c_int]
+        L.of_booked_new.restype = C.c_void_p
+        L.of_booked_free.argtypes = [C.c_void_p]
+        L.of_booked_insert_db.restype = C.c_int
+        L.of_booked_insert_db.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.of_booked_needed_len.restype = C.c_uint64
+        L.of_booked_needed_len.argtypes = [C.c_void_p]
+        L.of_booked_needed.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.of_booked_max.restype = C.c_int64
+        L.of_booked_max.argtypes = [C.c_void_p]
+        L.of_booked_contains.restype = C.c_int
+        L.of_booked_contains.argtypes = [C.c_void_p, C.c_uint64]
+        _lib = L
+    return _lib
+
+
+BATCH_DTYPES = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64,
+                "db_version": np.int64, "cl": np.uint32, "seq": np.uint32, "site": np.uint32,
+                "val0": np.uint64, "val1": np.uint64, "val_type": np.uint8, "val_len": np.uint8,
+                "ts": np.uint64}
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def _changes_struct(batch, keep):
+    n = len(batch["pk"])
+    s = _Changes()
+    s.n = n
+    for k, dt in BATCH_DTYPES.items():
+        a = batch.get(k)
+        if a is not None:
+            a = np.ascontiguousarray(a, dtype=dt)
+            assert len(a) == n, k
+            keep.append(a)
+        setattr(s, k, _ptr(a))
+    return s
+
+
+class Fold:
+    """Sequential cr-sqlite merge fold (crsql_changes INSERT per change)."""
+
+    def __init__(self, site_ids):
+        site_ids = np.ascontiguousarray(site_ids, dtype=np.uint8).reshape(-1, 16)
+        self._sites = site_ids
+        self.nsites = site_ids.shape[0]
+        self._h = lib().of_new(site_ids.ctypes.data, self.nsites)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().of_free(self._h)
+            self._h = None
+
+    def apply(self, batch):
+        keep = []
+        s = _changes_struct(batch, keep)
+        imp = np.zeros(max(s.n, 1), dtype=np.uint8)
+        lib().of_apply(self._h, C.byref(s), imp.ctypes.data)
+        return imp[: s.n]
+
+    def export(self):
+        m = lib().of_count(self._h)
+        out = {"pk": np.zeros(m, np.uint64), "table_cid": np.zeros(m, np.uint32),
+               "col_version": np.zeros(m, np.int64), "db_version": np.zeros(m, np.int64),
+               "cl": np.zeros(m, np.int64), "seq": np.zeros(m, np.uint32),
+               "site": np.zeros(m, np.uint32), "ts": np.zeros(m, np.uint64),
+               "val0": np.zeros(m, np.uint64), "val1": np.zeros(m, np.uint64),
+               "val_type": np.zeros(m, np.uint8), "val_len": np.zeros(m, np.uint8)}
+        r = _Rows()
+        for k, a in out.items():
+            setattr(r, k, a.ctypes.data if m else None)
+        if m:
+            got = lib().of_export(self._h, C.byref(r))
+            assert got == m
+        return out
+
+    def db_versions(self):
+        out = np.zeros(max(self.nsites, 1), np.int64)
+        lib().of_db_versions(self._h, out.ctypes.data)
+        return out[: self.nsites]
+
+
+SYNC_KEYS_U64 = ("their_head", "tn_off", "tn_start", "tn_end", "tp_off", "tp_ver", "tps_off",
+                 "tps_start", "tps_end", "on_off", "on_start", "on_end", "op_off", "op_ver",
+                 "ops_off", "ops_start", "ops_end")
+
+
+def needs(entries):
+    """compute_available_needs over CSR entries (dict of numpy arrays). Returns CSR result dict."""
+    keep = []
+    s = _SyncEntries()
+    n = len(entries["their_head"])
+    s.n = n
+    for k in SYNC_KEYS_U64:
+        a = np.ascontiguousarray(entries[k], dtype=np.uint64)
+        keep.append(a)
+        setattr(s, k, a.ctypes.data if a.size else None)
+    oh = np.ascontiguousarray(entries["our_head"], dtype=np.int64)
+    keep.append(oh)
+    s.our_head = oh.ctypes.data if oh.size else None
+    nc = np.zeros(max(n, 1), np.uint64)
+    sc = np.zeros(max(n, 1), np.uint64)
+    o = _NeedsOut()
+    o.need_count = nc.ctypes.data
+    o.seq_count = sc.ctypes.data
+    lib().of_needs(C.byref(s), C.byref(o), 0)
+    nc, sc = nc[:n], sc[:n]
+    need_off = np.zeros(n + 1, np.uint64)
+    seq_off = np.zeros(n + 1, np.uint64)
+    need_off[1:] = np.cumsum(nc)
+    seq_off[1:] = np.cumsum(sc)
+    T, Ts = int(need_off[-1]), int(seq_off[-1])
+    res = {"need_off": need_off, "seq_off": seq_off,
+           "kind": np.zeros(max(T, 1), np.uint8), "start": np.zeros(max(T, 1), np.uint64),
+           "end": np.zeros(max(T, 1), np.uint64), "sr_off": np.zeros(max(T, 1), np.uint64),
+           "sr_n": np.zeros(max(T, 1), np.uint64), "s_start": np.zeros(max(Ts, 1), np.uint64),
+           "s_end": np.zeros(max(Ts, 1), np.uint64)}
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        setattr(o, k, res[k].ctypes.data)
+    lib().of_needs(C.byref(s), C.byref(o), 1)
+    for k in ("kind", "start", "end", "sr_off", "sr_n"):
+        res[k] = res[k][:T]
+    for k in ("s_start", "s_end"):
+        res[k] = res[k][:Ts]
+    return res
+
+
+class Booked:
+    """BookedVersions gap bookkeeping (agent.rs:1108-1235, :1353-1362)."""
+
+    def __init__(self):
+        self._h = lib().of_booked_new()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().of_booked_free(self._h)
+            self._h = None
+
+    def insert_db(self, ranges):
+        s = np.array([r[0] for r in ranges], np.uint64)
+        e = np.array([r[1] for r in ranges], np.uint64)
+        return lib().of_booked_insert_db(self._h, s.ctypes.data, e.ctypes.data, len(ranges))
+
+    def needed(self):
+        m = lib().of_booked_needed_len(self._h)
+        s = np.zeros(max(m, 1), np.uint64)
+        e = np.zeros(max(m, 1), np.uint64)
+        lib().of_booked_needed(self._h, s.ctypes.data, e.ctypes.data)
+        return [(int(s[i]), int(e[i])) for i in range(m)]
+
+    def max(self):
+        v = lib().of_booked_max(self._h)
+        return None if v < 0 else int(v)
+
+    def contains(self, v):
+        return bool(lib().of_booked_contains(self._h, v))

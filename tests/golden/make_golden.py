@@ -1,0 +1,161 @@
+"""Transcribe the reference's known-answer vectors for this path into JSON fixtures.
+
+Run: python tests/golden/make_golden.py   (writes merge_kats.json, sync_kats.json, gaps_kats.json)
+
+Sources (data only, no reference code is copied):
+  * merge_kats   — SURVEY.md Appendix A.5 KAT table K1..K18 + its "additional probe facts"
+                   (cr-sqlite 0.17.0 results recorded during the survey) and the conflict example in
+                   /root/reference/doc/crdts.md:166-245 ('started' beats 'destroyed' at col_version 2).
+  * sync_kats    — the four assertions of test_compute_available_needs,
+                   /root/reference/crates/corro-types/src/sync.rs:386-500.
+  * gaps_kats    — the insert/expect_gaps steps of test_booked_insert_db,
+                   /root/reference/crates/corro-types/src/agent.rs:1605-1868.
+
+Merge-case notation: table t(id INTEGER PK, a, b, c); cid 0 = sentinel '-1', a=1, b=2, c=3.
+Sites sN = sixteen bytes of value N. A change is [cid, value, col_version, db_version, site, cl];
+value = {"t": "int"|"real"|"text"|"blob"|"null", "v": ...}. `impacted` is the cumulative
+crsql_rows_impacted() after each insert (one transaction).
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def I(v):
+    return {"t": "int", "v": v}
+
+
+def R(v):
+    return {"t": "real", "v": v}
+
+
+def T(v):
+    return {"t": "text", "v": v}
+
+
+def B(hexs):
+    return {"t": "blob", "v": hexs}
+
+
+N = {"t": "null", "v": None}
+S = 0  # sentinel cid
+
+MERGE = [
+    # name, input changes, expected final rows (cid, val, cv, dbv, site, cl), impacted, source
+    ("K1 first write cl=1", [[1, I(5), 1, 7, 1, 1]], [[1, I(5), 1, 7, 1, 1]], [1]),
+    ("K2 equal colv, bigger value wins", [[1, I(5), 1, 7, 1, 1], [1, I(6), 1, 3, 2, 1]],
+     [[1, I(6), 1, 3, 2, 1]], [1, 2]),
+    ("K3 equal colv, smaller value loses", [[1, I(6), 1, 3, 2, 1], [1, I(4), 1, 9, 2, 1]],
+     [[1, I(6), 1, 3, 2, 1]], [1, 1]),
+    ("K4 higher colv beats bigger value", [[1, I(9), 1, 7, 1, 1], [1, I(1), 2, 3, 2, 1]],
+     [[1, I(1), 2, 3, 2, 1]], [1, 2]),
+    ("K5 equal value+colv: bigger site wins",
+     [[1, I(5), 1, 7, 2, 1], [1, I(5), 1, 3, 1, 1], [1, I(5), 1, 4, 3, 1]],
+     [[1, I(5), 1, 4, 3, 1]], [1, 1, 2]),
+    ("K6 type rank INTEGER > REAL", [[1, R(5.5), 1, 7, 1, 1], [1, I(5), 1, 8, 2, 1]],
+     [[1, I(5), 1, 8, 2, 1]], [1, 2]),
+    ("K7 REAL loses to INTEGER", [[1, I(5), 1, 7, 1, 1], [1, R(5.5), 1, 8, 2, 1]],
+     [[1, I(5), 1, 7, 1, 1]], [1, 1]),
+    ("K8 NULL loses", [[1, I(5), 1, 7, 1, 1], [1, N, 1, 8, 2, 1]],
+     [[1, I(5), 1, 7, 1, 1]], [1, 1]),
+    ("K9 BLOB memcmp", [[3, B("6162"), 1, 7, 1, 1], [3, B("62"), 1, 8, 2, 1]],
+     [[3, B("62"), 1, 8, 2, 1]], [1, 2]),
+    ("K10 remote delete drops row", [[1, I(5), 1, 1, 1, 1], [S, N, 2, 2, 2, 2]],
+     [[S, N, 2, 2, 2, 2]], [1, 2]),
+    ("K11 stale col after delete ignored", [[S, N, 2, 2, 2, 2], [1, I(5), 9, 1, 1, 1]],
+     [[S, N, 2, 2, 2, 2]], [1, 1]),
+    ("K12 resurrect via column after delete",
+     [[1, I(5), 4, 1, 1, 1], [S, N, 2, 2, 2, 2], [1, I(7), 1, 3, 3, 3]],
+     [[S, N, 3, 3, 3, 3], [1, I(7), 1, 3, 3, 3]], [1, 2, 4]),
+    ("K13 missed-delete resurrect zeroes colv", [[1, I(5), 9, 1, 1, 1], [2, I(7), 1, 3, 3, 3]],
+     [[S, N, 3, 3, 3, 3], [1, I(5), 0, 1, 1, 3], [2, I(7), 1, 3, 3, 3]], [1, 3]),
+    ("K14 same as K13, reversed order", [[2, I(7), 1, 3, 3, 3], [1, I(5), 9, 1, 1, 1]],
+     [[S, N, 3, 3, 3, 3], [2, I(7), 1, 3, 3, 3]], [2, 2]),
+    ("K15 first write cl=3 creates sentinel", [[1, I(5), 1, 3, 3, 3]],
+     [[S, N, 3, 3, 3, 3], [1, I(5), 1, 3, 3, 3]], [2]),
+    ("K16 pk-only sentinel cl=1", [[S, N, 1, 2, 2, 1]], [[S, N, 1, 2, 2, 1]], [1]),
+    ("K17 sentinel cl=1 after column = no-op", [[1, I(5), 1, 1, 1, 1], [S, N, 1, 2, 2, 1]],
+     [[1, I(5), 1, 1, 1, 1]], [1, 1]),
+    ("K18 equal delete twice = no-op", [[S, N, 2, 2, 2, 2], [S, N, 2, 5, 3, 2]],
+     [[S, N, 2, 2, 2, 2]], [1, 1]),
+    ("P1 identical duplicate from the same site: no impact",
+     [[1, I(5), 1, 7, 1, 1], [1, I(5), 1, 7, 1, 1]], [[1, I(5), 1, 7, 1, 1]], [1, 1]),
+    ("P2 sentinel resurrect cv=7 cl=3 stores sentinel cv 7 (row cl reads 7)",
+     [[S, N, 2, 1, 1, 2], [S, N, 7, 2, 2, 3]], [[S, N, 7, 2, 2, 7]], [1, 2]),
+    ("D1 doc/crdts.md: 'started' beats 'destroyed' at equal col_version",
+     [[1, T("meow"), 1, 1, 5, 1], [2, T("destroyed"), 2, 5, 6, 1], [2, T("started"), 2, 3, 5, 1]],
+     [[1, T("meow"), 1, 1, 5, 1], [2, T("started"), 2, 3, 5, 1]], [1, 2, 3]),
+    ("D2 doc/crdts.md reverse direction: 'destroyed' loses to 'started'",
+     [[1, T("meow"), 1, 1, 5, 1], [2, T("started"), 2, 3, 5, 1], [2, T("destroyed"), 2, 5, 6, 1]],
+     [[1, T("meow"), 1, 1, 5, 1], [2, T("started"), 2, 3, 5, 1]], [1, 2, 2]),
+]
+
+# crsql_db_versions after {s3 dbv3 applied; s2 dbv17 ignored (cl<L);
+# s1 dbv21 lost on value; s4 dbv30 sentinel no-op} = {s1:21, s2:17, s3:3, s4:30}
+DBV = {
+    "name": "crsql_db_versions records every inserted change, losers included",
+    "changes": [[1, I(5), 1, 3, 3, 3], [1, I(9), 5, 17, 2, 1], [1, I(4), 1, 21, 1, 3],
+                [S, N, 3, 30, 4, 3]],
+    "db_versions": {"1": 21, "2": 17, "3": 3, "4": 30},
+}
+
+# sync.rs:386-500 (actor1 heads/needs; one actor)
+SYNC = [
+    {"name": "heads only", "our": {"head": 10, "need": [], "partials": {}},
+     "their": {"head": 13, "need": [], "partials": {}},
+     "expect": [["full", 11, 13]]},
+    {"name": "our needs inside their haves", "our": {"head": 10, "need": [[2, 5], [7, 7]], "partials": {}},
+     "their": {"head": 13, "need": [], "partials": {}},
+     "expect": [["full", 2, 5], ["full", 7, 7], ["full", 11, 13]]},
+    {"name": "our partial, they have the version",
+     "our": {"head": 10, "need": [[2, 5], [7, 7]], "partials": {"9": [[100, 120], [130, 132]]}},
+     "their": {"head": 13, "need": [], "partials": {}},
+     "expect": [["full", 2, 5], ["full", 7, 7], ["partial", 9, [[100, 120], [130, 132]]],
+                ["full", 11, 13]]},
+    {"name": "both partial: intersect with their seq haves",
+     "our": {"head": 10, "need": [[2, 5], [7, 7]], "partials": {"9": [[100, 120], [130, 132]]}},
+     "their": {"head": 13, "need": [], "partials": {"9": [[100, 110], [130, 130]]}},
+     "expect": [["full", 2, 5], ["full", 7, 7], ["partial", 9, [[111, 120], [131, 132]]],
+                ["full", 11, 13]]},
+]
+
+# agent.rs:1605-1868: sequences of insert_db(set) -> expected gaps; "reset" starts a new
+# BookedVersions; final max checked by expect_gaps (agent.rs:1911-1915)
+GAPS = [
+    {"insert": [[1, 20]], "gaps": []},
+    {"insert": [[1, 10]], "gaps": []},
+    {"reset": True},
+    {"insert": [[1, 1], [4, 4]], "gaps": [[2, 3]]},
+    {"insert": [[3, 3], [2, 2]], "gaps": []},
+    {"reset": True},
+    {"insert": [[5, 20]], "gaps": [[1, 4]]},
+    {"insert": [[6, 7]], "gaps": [[1, 4]]},
+    {"insert": [[3, 7]], "gaps": [[1, 2]]},
+    {"insert": [[1, 2]], "gaps": []},
+    {"insert": [[25, 25]], "gaps": [[21, 24]]},
+    {"insert": [[30, 35]], "gaps": [[21, 24], [26, 29]]},
+    {"insert": [[19, 22]], "gaps": [[23, 24], [26, 29]]},
+    {"insert": [[24, 25]], "gaps": [[23, 23], [26, 29]]},
+    {"insert": [[23, 27]], "gaps": [[28, 29]]},
+    {"insert": [[1, 20]], "gaps": [[28, 29]]},
+    {"insert": [[27, 30]], "gaps": []},
+    {"insert": [[40, 45]], "gaps": None},
+    {"insert": [[50, 55]], "gaps": None},
+    {"insert": [[38, 47]], "gaps": [[36, 37], [48, 49]]},
+]
+
+
+def main():
+    merge = [{"name": n, "changes": c, "rows": r, "impacted": imp} for (n, c, r, imp) in MERGE]
+    with open(os.path.join(HERE, "merge_kats.json"), "w") as f:
+        json.dump({"source": "SURVEY.md App. A.5 + doc/crdts.md:166-245", "cases": merge,
+                   "db_versions_case": DBV}, f, indent=1)
+    with open(os.path.join(HERE, "sync_kats.json"), "w") as f:
+        json.dump({"source": "corro-types/src/sync.rs:386-500", "cases": SYNC}, f, indent=1)
+    with open(os.path.join(HERE, "gaps_kats.json"), "w") as f:
+        json.dump({"source": "corro-types/src/agent.rs:1605-1868", "steps": GAPS}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+"""Pin the CPU oracle against the reference's own known-answer vectors (no GPU)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests._util import batch_from_changes, expected_rows, load_golden, rows_to_tuples, site_table
+from tests.sync_util import decode_needs, entries_from_pairs, kat_expect
+
+MERGE = load_golden("merge_kats.json")
+
+
+@pytest.mark.parametrize("case", MERGE["cases"], ids=[c["name"][:3] for c in MERGE["cases"]])
+def test_oracle_merge_kats(case):
+    f = O.Fold(site_table())
+    imp = f.apply(batch_from_changes(case["changes"]))
+    got = [t[:11] for t in rows_to_tuples(f.export())]
+    assert got == expected_rows(case["rows"])
+    assert list(np.cumsum(imp)) == case["impacted"]
+
+
+def test_oracle_db_versions():
+    c = MERGE["db_versions_case"]
+    f = O.Fold(site_table())
+    f.apply(batch_from_changes(c["changes"]))
+    dv = f.db_versions()
+    for site, v in c["db_versions"].items():
+        assert dv[int(site)] == v
+    assert dv[0] == -1
+
+
+def test_oracle_merge_kats_as_one_batch_over_many_pks():
+    """All KATs at once, each on its own pk, interleaved: per-pk results must not change."""
+    f = O.Fold(site_table())
+    parts, exp = [], []
+    for i, case in enumerate(MERGE["cases"]):
+        parts.append(batch_from_changes(case["changes"], pk=100 + i))
+        exp += expected_rows(case["rows"], pk=100 + i)
+    # interleave round-robin, keeping per-pk order
+    order = []
+    idx = [0] * len(parts)
+    while any(idx[j] < len(parts[j]["pk"]) for j in range(len(parts))):
+        for j in range(len(parts)):
+            if idx[j] < len(parts[j]["pk"]):
+                order.append((j, idx[j]))
+                idx[j] += 1
+    batch = {k: np.array([parts[j][k][i] for j, i in order], dtype=parts[0][k].dtype) for k in parts[0]}
+    f.apply(batch)
+    assert [t[:11] for t in rows_to_tuples(f.export())] == sorted(exp)
+
+
+SYNC = load_golden("sync_kats.json")
+
+
+@pytest.mark.parametrize("case", SYNC["cases"], ids=[c["name"] for c in SYNC["cases"]])
+def test_oracle_sync_kats(case):
+    ent = entries_from_pairs([(case["our"], case["their"])])
+    res = O.needs(ent)
+    assert decode_needs(res, 1)[0] == kat_expect(case["expect"])
+
+
+def test_oracle_gaps_kats():
+    steps = load_golden("gaps_kats.json")["steps"]
+    b, allv = O.Booked(), []
+    for st in steps:
+        if st.get("reset"):
+            b, allv = O.Booked(), []
+            continue
+        assert b.insert_db(st["insert"]) == 0
+        allv += st["insert"]
+        if st["gaps"] is not None:
+            assert b.needed() == [tuple(g) for g in st["gaps"]]
+            for s, e in st["gaps"]:
+                for v in range(s, e + 1):
+                    assert not b.contains(v)
+        for s, e in allv:
+            for v in range(s, e + 1):
+                if st["gaps"] is not None and any(gs <= v <= ge for gs, ge in st["gaps"]):
+                    continue
+                assert b.contains(v)
+        assert b.max() == max(e for _, e in allv)
