@@ -1,0 +1,123 @@
+"""ctypes binding of libcorro_hip.so (the C ABI declared in include/corro_hip.h).
+
+The product path has exactly one implementation: the HIP library. There is no CPU fallback;
+loading fails loudly if the library is missing, and compute calls fail with CORRO_E_NO_DEVICE
+when no gfx950 device is visible.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcorro_hip.so")
+
+CORRO_OK = 0
+ERRORS = {-1: "CORRO_E_INVALID", -2: "CORRO_E_NOMEM", -3: "CORRO_E_DEVICE",
+          -4: "CORRO_E_UNKNOWN_TABLE", -5: "CORRO_E_UNKNOWN_COLUMN", -6: "CORRO_E_RANGE",
+          -7: "CORRO_E_NO_DEVICE"}
+CORRO_MEM_HOST, CORRO_MEM_DEVICE = 0, 1
+
+# every symbol include/corro_hip.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "corro_last_error", "corro_abi_version", "corro_device_count", "corro_ctx_create",
+    "corro_ctx_destroy", "corro_lookup_cid", "corro_site_register", "corro_site_count",
+    "corro_apply_batch", "corro_state_count", "corro_state_export", "corro_state_reset",
+    "corro_db_versions", "corro_compute_needs", "corro_booked_new", "corro_booked_free",
+    "corro_booked_insert_db", "corro_booked_needed", "corro_booked_last", "corro_booked_contains",
+    "corro_booked_contains_all", "corro_ctx_set_profiling", "corro_last_timings",
+]
+
+
+class CorroError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class TableDesc(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("ncols", C.c_uint32), ("col_names", C.POINTER(C.c_char_p))]
+
+
+class Changes(C.Structure):
+    _fields_ = [("n", C.c_uint64)] + [(k, C.c_void_p) for k in (
+        "pk", "table_cid", "col_version", "db_version", "cl", "seq", "site", "val0", "val1",
+        "val_type", "val_len", "ts")]
+
+
+class ApplyOut(C.Structure):
+    _fields_ = [("impact", C.c_void_p)]
+
+
+class Rows(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("pk", "table_cid", "col_version", "db_version", "cl",
+                                          "seq", "site", "ts", "val0", "val1", "val_type",
+                                          "val_len")]
+
+
+class SyncEntries(C.Structure):
+    _fields_ = [("n", C.c_uint64)] + [(k, C.c_void_p) for k in (
+        "their_head", "our_head", "tn_off", "tn_start", "tn_end", "tp_off", "tp_ver", "tps_off",
+        "tps_start", "tps_end", "on_off", "on_start", "on_end", "op_off", "op_ver", "ops_off",
+        "ops_start", "ops_end")]
+
+
+class NeedsOut(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("need_count", "seq_count", "need_off", "seq_off", "kind",
+                                          "start", "end", "sr_off", "sr_n", "s_start", "s_end")]
+
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree libcorro_hip.so. Raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `python -m corrosion_amd.build` "
+                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+    sig = {
+        "corro_last_error": (C.c_char_p, []),
+        "corro_abi_version": (i32, []),
+        "corro_device_count": (i32, [vp]),
+        "corro_ctx_create": (i32, [vp, u32, u64, i32, vp]),
+        "corro_ctx_destroy": (None, [vp]),
+        "corro_lookup_cid": (i32, [vp, C.c_char_p, C.c_char_p, vp]),
+        "corro_site_register": (i32, [vp, vp, u64, vp]),
+        "corro_site_count": (i32, [vp, vp]),
+        "corro_apply_batch": (i32, [vp, C.POINTER(Changes), i32, C.POINTER(ApplyOut)]),
+        "corro_state_count": (i32, [vp, vp]),
+        "corro_state_export": (i32, [vp, C.POINTER(Rows), u64, vp]),
+        "corro_state_reset": (i32, [vp]),
+        "corro_db_versions": (i32, [vp, vp, u32]),
+        "corro_compute_needs": (i32, [vp, C.POINTER(SyncEntries), i32, C.POINTER(NeedsOut), i32]),
+        "corro_booked_new": (i32, [vp]),
+        "corro_booked_free": (None, [vp]),
+        "corro_booked_insert_db": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp, vp, u64, vp]),
+        "corro_booked_needed": (i32, [vp, vp, vp, u64, vp]),
+        "corro_booked_last": (i32, [vp, vp]),
+        "corro_booked_contains": (i32, [vp, u64, vp]),
+        "corro_booked_contains_all": (i32, [vp, u64, u64, vp]),
+        "corro_ctx_set_profiling": (i32, [vp, i32]),
+        "corro_last_timings": (i32, [vp, vp, u32, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != CORRO_OK:
+        raise CorroError(rc, lib().corro_last_error().decode(errors="replace"))
+    return rc
+
+
+def device_count():
+    c = C.c_int(0)
+    check(lib().corro_device_count(C.byref(c)))
+    return c.value

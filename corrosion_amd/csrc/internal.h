@@ -1,0 +1,104 @@
+// Internal declarations shared by the libcorro_hip.so translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "corro_hip.h"
+
+namespace corro {
+
+// Thread-local last error (corro_last_error).
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define CORRO_HIP_TRY(expr)                                                              \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return ::corro::fail(CORRO_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// One staged / state record: a column change or a clock row (64 B, 16-B aligned so a lane moves
+// it with four dwordx4 accesses). `pos` orders records of one row: prior-state rows use their
+// index inside the bucket's state slice (< 2^31), batch changes use BATCH_POS | batch index.
+struct __attribute__((aligned(16))) Rec {
+    uint64_t pk;
+    int64_t cv;    // col_version (sentinel: causal length)
+    int64_t dbv;   // db_version
+    uint64_t v0;   // value word 0
+    uint64_t v1;   // value word 1 (TEXT/BLOB bytes 8..15)
+    uint32_t tcid; // table << 16 | cid
+    uint32_t cl;   // change: causal length; state row: row causal length
+    uint32_t seq;
+    uint32_t site; // site ordinal
+    uint32_t pos;
+    uint32_t meta; // type | len << 8
+};
+static_assert(sizeof(Rec) == 64, "Rec must be 64 bytes");
+
+constexpr uint32_t BATCH_POS = 0x80000000u;
+
+// Growable device buffer.
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t want);
+    void release();
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct Table {
+    std::string name;
+    std::vector<std::string> cols;
+};
+
+}  // namespace corro
+
+struct corro_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<corro::Table> tables;
+    std::map<std::string, uint32_t> table_index;
+
+    // sites (crsql_site_id analogue): ordinal -> 16 bytes; rank = memcmp order
+    std::vector<std::array<uint8_t, 16>> sites;
+    std::map<std::array<uint8_t, 16>, uint32_t> site_ordinal;
+    corro::DevBuf d_site_rank;   // u32 per ordinal
+    corro::DevBuf d_dbv;         // u64 per ordinal: max db_version + 1 (0 = never seen)
+    corro::DevBuf d_dbv_batch;   // per-batch staging of the above
+    size_t dbv_cap = 0;
+
+    // bucket layout
+    uint32_t log2B = 0;
+    uint32_t B = 0;
+    // state (clock rows), double buffered; per-bucket slices
+    corro::DevBuf d_state[2], d_state_ts[2];
+    corro::DevBuf d_state_off, d_state_cnt, d_state_flags;     // current
+    corro::DevBuf d_out_off, d_out_cnt, d_out_flags;           // next
+    int cur = 0;
+    uint64_t state_total = 0;     // clock rows in the current state
+    bool track_ts = false;
+
+    // per-batch scratch
+    corro::DevBuf d_in;           // staged device copy of a host batch
+    corro::DevBuf d_hist;         // ntiles x B
+    corro::DevBuf d_new_cnt, d_stage_off, d_bflags;
+    corro::DevBuf d_stage;        // staged Recs
+    corro::DevBuf d_misc;         // counters: [0] error bits, [1] overflow count, [2] out total, [3] wide flag
+    corro::DevBuf d_ovf_list;     // overflow buckets
+    corro::DevBuf d_ovf_scratch;
+    corro::DevBuf d_impact;
+    corro::DevBuf d_export;
+    corro::DevBuf d_needs;        // sync-need scratch
+    corro::DevBuf d_ncols;        // u16 column count per table
+    uint64_t *h_misc = nullptr;   // pinned
+    // stage timing
+    bool profiling = false;
+    hipEvent_t ev[8] = {};
+    float last_ms[6] = {};
+};

@@ -1,0 +1,790 @@
+// Device code of the batched causal-length + LWW merge (the crsql_changes INSERT loop of
+// process_complete_version, /root/reference/crates/corro-agent/src/agent/util.rs:1222-1262).
+//
+// Pipeline for one batch of N column changes:
+//   k_hist     tile-local LDS histogram of the (table, pk) bucket of every change; one coalesced
+//              row of counts per tile (no global atomics); per-site crsql_db_versions maxima;
+//              input validation (unknown cid / site, out-of-range encodings).
+//   k_colscan  per bucket, exclusive prefix over tiles -> each tile owns a disjoint slice of the
+//              bucket (deterministic slices, no atomics).
+//   k_plan     one workgroup: bucket slice offsets for the staged batch and the next state.
+//   k_scatter  re-read the SoA batch, stage each change as one 64-B record in its bucket slice.
+//   k_merge    one workgroup per bucket: prior clock rows of the bucket (as a prefix of the
+//              application order) + its staged changes ->
+//                fast body  (all rows cl = 1, no sentinels): per-cell argmax of
+//                           (col_version, value, site_id rank, -position) by LDS 64-bit
+//                           atomic-max stages; order independent (SURVEY App. A.2 reduction).
+//                general    sort by (row, position) in LDS, then one lane per row folds the
+//                           cr-sqlite rules in application order (App. A.1), exactly.
+//              Buckets larger than LDS go to k_merge_ovf (same general body on global scratch).
+#pragma once
+#include "internal.h"
+
+namespace corro {
+
+constexpr int HIST_THREADS = 512;
+constexpr int MERGE_THREADS = 512;
+constexpr int FAST_R = 5;                              // records per thread, fast body
+constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 2560
+constexpr int FAST_SLOTS = 8192;                       // pow2 >= 2 * CAP_FAST
+constexpr int CAP_GEN = 2048;                          // records, general body in LDS
+constexpr int GEN_SLOTS = 4096;
+constexpr int OVF_THREADS = 1024;
+
+struct BatchDev {
+    const uint64_t *pk;
+    const uint32_t *tcid;
+    const int64_t *cv;
+    const int64_t *dbv;
+    const uint32_t *cl;
+    const uint32_t *seq;
+    const uint32_t *site;
+    const uint64_t *v0;
+    const uint64_t *v1;
+    const uint8_t *vt;
+    const uint8_t *vl;
+    const uint64_t *ts;
+    uint32_t n;
+};
+
+struct MergeArgs {
+    const Rec *prior;
+    const uint64_t *prior_off;
+    const uint32_t *prior_cnt;
+    const uint32_t *prior_flags;
+    const uint64_t *prior_ts;
+    const Rec *stage;
+    const uint32_t *stage_off;
+    const uint32_t *new_cnt;
+    const uint32_t *bflags;   // bit per bucket: batch has a non-(cl=1 column) change there
+    const uint64_t *batch_ts;
+    Rec *out;
+    uint64_t *out_ts;
+    const uint64_t *out_off;
+    uint32_t *out_cnt;
+    uint32_t *out_flags;
+    const uint32_t *site_rank;
+    uint32_t nsites;
+    uint8_t *impact;
+    unsigned long long *misc;  // [0] error bits [1] overflow buckets [2] rows written [3] wide values
+    uint32_t *ovf_list;
+    uint32_t force_general;
+    uint32_t track_ts;
+};
+
+// misc[0] error bits
+constexpr uint32_t ERR_NAME = 1u, ERR_SITE = 2u, ERR_RANGE = 4u, ERR_VALUE = 8u;
+
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+// Bucket of a row (table, pk): the top log2B bits of a 64-bit mix. Rows never straddle buckets, so
+// every causal-length interaction of a row (delete/resurrect zeroing) stays inside one workgroup.
+__host__ __device__ inline uint32_t bucket_of(uint32_t table, uint64_t pk, uint32_t log2B) {
+    if (log2B == 0) return 0;
+    uint64_t h = mix64(pk + 0x9E3779B97F4A7C15ULL * (uint64_t)(table + 1));
+    return (uint32_t)(h >> (64 - log2B));
+}
+
+__device__ inline uint32_t cell_hash(uint64_t pk, uint32_t tcid) {
+    return (uint32_t)mix64(pk * 0xD6E8FEB86659FD93ULL + tcid);
+}
+
+__device__ inline uint32_t row_hash(uint64_t pk, uint32_t table) {
+    return (uint32_t)mix64(pk * 0xA0761D6478BD642FULL + table + 0x51);
+}
+
+// --- value order: type rank INTEGER > REAL > TEXT > BLOB > NULL ---------------
+__device__ inline uint32_t vtype(uint32_t meta) { return meta & 0xFFu; }
+__device__ inline uint32_t vlen(uint32_t meta) { return (meta >> 8) & 0xFFu; }
+
+// order-preserving unsigned key of value word 0 within one storage class
+__device__ inline uint64_t vkey0(uint32_t type, uint64_t v0) {
+    switch (type) {
+    case CORRO_INTEGER: return v0 ^ 0x8000000000000000ULL;
+    case CORRO_REAL:
+        if (v0 == 0x8000000000000000ULL) v0 = 0;  // -0.0 == 0.0
+        return (v0 >> 63) ? ~v0 : (v0 | 0x8000000000000000ULL);
+    case CORRO_TEXT:
+    case CORRO_BLOB: return v0;
+    default: return 0;
+    }
+}
+
+// >0: a greater, <0: b greater, 0: equal
+__device__ inline int value_cmp(const Rec &a, const Rec &b) {
+    uint32_t ta = vtype(a.meta), tb = vtype(b.meta);
+    if (ta != tb) return (5 - (int)ta) > (5 - (int)tb) ? 1 : -1;
+    if (ta == CORRO_NULL) return 0;
+    uint64_t ka = vkey0(ta, a.v0), kb = vkey0(tb, b.v0);
+    if (ka != kb) return ka > kb ? 1 : -1;
+    if (ta == CORRO_TEXT || ta == CORRO_BLOB) {
+        if (a.v1 != b.v1) return a.v1 > b.v1 ? 1 : -1;
+        uint32_t la = vlen(a.meta), lb = vlen(b.meta);
+        if (la != lb) return la > lb ? 1 : -1;
+    }
+    return 0;
+}
+
+__device__ inline uint32_t site_rank_of(const MergeArgs &a, uint32_t site) {
+    return site < a.nsites ? a.site_rank[site] : 0u;
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(HIST_THREADS)
+k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t *__restrict__ hist_out,
+       uint32_t *__restrict__ bflags, unsigned long long *__restrict__ dbv_batch, uint32_t nsites,
+       const uint16_t *__restrict__ ncols, uint32_t ntables, unsigned long long *misc) {
+    extern __shared__ uint32_t sm[];
+    const uint32_t B = 1u << log2B;
+    const uint32_t nfl = (B + 31) / 32;
+    uint32_t *hist = sm;
+    uint32_t *fl = sm + B;
+    for (uint32_t i = threadIdx.x; i < B + nfl; i += blockDim.x) sm[i] = 0;
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * tile;
+    const uint32_t end = min(in.n, begin + tile);
+    uint32_t err = 0, wide = 0;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t base = begin; base < end; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const bool act = i < end;
+        uint32_t site = 0xFFFFFFFFu;
+        uint64_t dbv = 0;
+        if (act) {
+            const uint64_t pk = in.pk[i];
+            const uint32_t tc = in.tcid[i];
+            const uint32_t cl = in.cl[i];
+            const uint32_t t = tc >> 16, cid = tc & 0xFFFFu;
+            const uint32_t b = bucket_of(t, pk, log2B);
+            atomicAdd(&hist[b], 1u);
+            if (cl != 1u || cid == 0) atomicOr(&fl[b >> 5], 1u << (b & 31));
+            site = in.site[i];
+            dbv = (uint64_t)in.dbv[i];
+            if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
+            if (site >= nsites) err |= ERR_SITE;
+            const int64_t cv = in.cv[i];
+            if ((cid == 0 || (cl & 1u) == 0) && (cv < 0 || cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
+            if ((int64_t)dbv < 0) err |= ERR_RANGE;
+            if (in.vt) {
+                const uint32_t ty = in.vt[i];
+                if (ty < 1 || ty > 5) err |= ERR_VALUE;
+                if (ty != CORRO_INTEGER) wide = 1;
+                if (ty == CORRO_REAL) {
+                    const uint64_t v = in.v0[i];
+                    if (((v >> 52) & 0x7FF) == 0x7FF && (v & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
+                }
+                if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && in.vl && in.vl[i] > 16) err |= ERR_VALUE;
+            }
+        }
+        // crsql_db_versions: one atomic per run of equal (site, db_version) inside the wave
+        const uint32_t psite = __shfl_up(site, 1);
+        const unsigned long long pdbv = __shfl_up((unsigned long long)dbv, 1);
+        if (act && site < nsites && (lane == 0 || psite != site || pdbv != dbv))
+            atomicMax(&dbv_batch[site], (unsigned long long)dbv + 1ULL);
+    }
+    if (err) atomicOr(&misc[0], (unsigned long long)err);
+    if (wide) atomicOr(&misc[3], 1ULL);
+    __syncthreads();
+    uint32_t *row = hist_out + (size_t)blockIdx.x * B;
+    for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) row[b] = hist[b];
+    for (uint32_t w = threadIdx.x; w < nfl; w += blockDim.x)
+        if (fl[w]) atomicOr(&bflags[w], fl[w]);
+}
+
+// per bucket: exclusive prefix of the tile counts (in place) and the bucket total
+__global__ void k_colscan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t B,
+                          uint32_t *__restrict__ new_cnt) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    uint32_t run = 0;
+    uint32_t t = 0;
+    for (; t + 4 <= ntiles; t += 4) {
+        uint32_t c[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) c[k] = hist[(size_t)(t + k) * B + b];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hist[(size_t)(t + k) * B + b] = run;
+            run += c[k];
+        }
+    }
+    for (; t < ntiles; t++) {
+        const size_t k = (size_t)t * B + b;
+        const uint32_t c = hist[k];
+        hist[k] = run;
+        run += c;
+    }
+    new_cnt[b] = run;
+}
+
+// one 1024-thread workgroup: stage_off = excl-scan(new_cnt); out_off = excl-scan(prior + 2*new)
+__global__ void __launch_bounds__(1024)
+k_plan(const uint32_t *__restrict__ new_cnt, const uint32_t *__restrict__ prior_cnt, uint32_t B,
+       uint32_t *__restrict__ stage_off, uint64_t *__restrict__ out_off) {
+    __shared__ uint64_t s_a[1024];
+    __shared__ uint64_t s_b[1024];
+    const uint32_t per = (B + 1023) / 1024;
+    const uint32_t lo = min(B, threadIdx.x * per), hi = min(B, lo + per);
+    uint64_t sa = 0, sb = 0;
+    for (uint32_t b = lo; b < hi; b++) {
+        sa += new_cnt[b];
+        sb += (uint64_t)prior_cnt[b] + 2ULL * new_cnt[b];
+    }
+    s_a[threadIdx.x] = sa;
+    s_b[threadIdx.x] = sb;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        uint64_t xa = 0, xb = 0;
+        if (threadIdx.x >= d) {
+            xa = s_a[threadIdx.x - d];
+            xb = s_b[threadIdx.x - d];
+        }
+        __syncthreads();
+        s_a[threadIdx.x] += xa;
+        s_b[threadIdx.x] += xb;
+        __syncthreads();
+    }
+    uint64_t ra = s_a[threadIdx.x] - sa, rb = s_b[threadIdx.x] - sb;
+    for (uint32_t b = lo; b < hi; b++) {
+        stage_off[b] = (uint32_t)ra;
+        out_off[b] = rb;
+        ra += new_cnt[b];
+        rb += (uint64_t)prior_cnt[b] + 2ULL * new_cnt[b];
+    }
+}
+
+__device__ inline void store_rec(Rec *dst, const Rec &r) {
+    const uint4 *s = reinterpret_cast<const uint4 *>(&r);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+    d[3] = s[3];
+}
+
+__device__ inline Rec load_rec(const Rec *src) {
+    Rec r;
+    const uint4 *s = reinterpret_cast<const uint4 *>(src);
+    uint4 *d = reinterpret_cast<uint4 *>(&r);
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+    d[3] = s[3];
+    return r;
+}
+
+__global__ void __launch_bounds__(HIST_THREADS)
+k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict__ hist_off,
+          const uint32_t *__restrict__ stage_off, Rec *__restrict__ stage) {
+    extern __shared__ uint32_t cur[];
+    const uint32_t B = 1u << log2B;
+    const uint32_t *row = hist_off + (size_t)blockIdx.x * B;
+    for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) cur[b] = stage_off[b] + row[b];
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * tile;
+    const uint32_t end = min(in.n, begin + tile);
+    for (uint32_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
+        Rec r;
+        r.pk = in.pk[i];
+        r.cv = in.cv[i];
+        r.dbv = in.dbv[i];
+        r.v0 = in.v0[i];
+        r.v1 = in.v1 ? in.v1[i] : 0ULL;
+        r.tcid = in.tcid[i];
+        r.cl = in.cl[i];
+        r.seq = in.seq[i];
+        r.site = in.site[i];
+        r.pos = BATCH_POS | i;
+        const uint32_t ty = in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER;
+        const uint32_t ln = in.vl ? (uint32_t)in.vl[i] : 0u;
+        r.meta = ty | (ln << 8);
+        const uint32_t b = bucket_of(r.tcid >> 16, r.pk, log2B);
+        const uint32_t idx = atomicAdd(&cur[b], 1u);
+        store_rec(stage + idx, r);
+    }
+}
+
+// ------------------------------------------------------------------------ merge bodies
+struct BucketView {
+    const Rec *prior;   // already offset to the bucket
+    const Rec *fresh;   // staged batch records of the bucket
+    uint32_t np, nn;
+    const uint64_t *prior_ts;  // offset to the bucket (or null)
+    __device__ inline const Rec *at(uint32_t i) const { return i < np ? prior + i : fresh + (i - np); }
+};
+
+__device__ inline uint64_t rec_ts(const MergeArgs &a, const BucketView &v, const Rec &r) {
+    if (r.pos & BATCH_POS) return a.batch_ts ? a.batch_ts[r.pos & 0x7FFFFFFFu] : 0ULL;
+    return v.prior_ts ? v.prior_ts[r.pos] : 0ULL;
+}
+
+// Arrays used by the general (sequential-rule) body. They point into LDS (k_merge) or into a
+// global scratch slice (k_merge_ovf); the code is the same.
+struct GenArrays {
+    uint64_t *pk;
+    int64_t *cv;
+    uint32_t *tc;
+    uint32_t *cl;
+    uint32_t *pos;
+    uint32_t *own;   // row hash slots: owner record + 1
+    uint64_t *key;   // sort keys: row << 32 | pos
+    uint32_t *val;   // sort payload: record index
+    uint32_t *ccid;  // per-run cell scratch
+    uint32_t *csrc;
+    int64_t *ccv;
+    uint32_t slots;  // pow2
+    uint32_t P;      // pow2 >= n
+};
+
+__device__ inline void gen_emit(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts,
+                                uint32_t *outcnt, uint32_t *flag, const GenArrays &g, uint32_t s,
+                                uint32_t ncell, bool hs, int64_t scv, uint32_t ssrc) {
+    const int64_t L = hs ? scv : (ncell ? 1 : 0);
+    const uint32_t cnt = (hs ? 1u : 0u) + ncell;
+    if (cnt == 0) return;
+    uint32_t base = atomicAdd(outcnt, cnt);
+    if (hs || L != 1) atomicOr(flag, 1u);
+    uint32_t k = base;
+    if (hs) {
+        Rec r = load_rec(v.at(ssrc));
+        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+        r.tcid &= 0xFFFF0000u;
+        r.cv = scv;
+        r.cl = (uint32_t)L;
+        r.v0 = 0;
+        r.v1 = 0;
+        r.meta = CORRO_NULL;
+        r.pos = k;
+        store_rec(outb + k, r);
+        if (a.track_ts) outts[k] = ts;
+        k++;
+    }
+    for (uint32_t c = 0; c < ncell; c++) {
+        Rec r = load_rec(v.at(g.csrc[s + c]));
+        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+        r.cv = g.ccv[s + c];
+        r.cl = (uint32_t)L;
+        r.pos = k;
+        store_rec(outb + k, r);
+        if (a.track_ts) outts[k] = ts;
+        k++;
+    }
+}
+
+__device__ inline void gen_set_cell(const GenArrays &g, uint32_t s, uint32_t &ncell, uint32_t cid,
+                                    uint32_t x, int64_t cv) {
+    for (uint32_t c = 0; c < ncell; c++) {
+        if (g.ccid[s + c] == cid) {
+            g.csrc[s + c] = x;
+            g.ccv[s + c] = cv;
+            return;
+        }
+    }
+    g.ccid[s + ncell] = cid;
+    g.csrc[s + ncell] = x;
+    g.ccv[s + ncell] = cv;
+    ncell++;
+}
+
+// Fold one row's records (sorted positions [s, e)) through the cr-sqlite rules, then emit.
+__device__ inline void gen_fold_row(const MergeArgs &a, const BucketView &v, Rec *outb,
+                                    uint64_t *outts, uint32_t *outcnt, uint32_t *flag,
+                                    const GenArrays &g, uint32_t s, uint32_t n) {
+    const uint32_t row = (uint32_t)(g.key[s] >> 32);
+    uint32_t ncell = 0;
+    bool hs = false;
+    int64_t scv = 0;
+    uint32_t ssrc = 0;
+    for (uint32_t j = s; j < n && (uint32_t)(g.key[j] >> 32) == row; j++) {
+        const uint32_t x = g.val[j];
+        const uint32_t cl = g.cl[x];
+        const uint32_t cid = g.tc[x] & 0xFFFFu;
+        const int64_t cv = g.cv[x];
+        const uint32_t pos = g.pos[x];
+        const int64_t L = hs ? scv : (ncell ? 1 : 0);
+        const int64_t lcl = (int64_t)cl;
+        uint32_t imp = 0;
+        if (lcl < L) {
+            // rule 1: stale causal length
+        } else if ((cl & 1u) == 0) {  // rule 2: delete
+            if (lcl != L) {
+                ncell = 0;
+                hs = true;
+                scv = cv;
+                ssrc = x;
+                imp = 1;
+            }
+        } else if (cid == 0) {  // rule 3: pk-only insert / resurrect
+            if (lcl > L) {
+                for (uint32_t c = 0; c < ncell; c++) g.ccv[s + c] = 0;
+                hs = true;
+                scv = cv;
+                ssrc = x;
+                imp = 1;
+            }
+        } else if (lcl > L) {  // rule 4: column change that needs a resurrect
+            if (L > 0 || cl > 1) {
+                for (uint32_t c = 0; c < ncell; c++) g.ccv[s + c] = 0;
+                hs = true;
+                scv = lcl;
+                ssrc = x;
+                imp = 1;
+            }
+            gen_set_cell(g, s, ncell, cid, x, cv);
+            imp += 1;
+        } else {  // cl == L: last-writer-wins
+            int found = -1;
+            for (uint32_t c = 0; c < ncell; c++)
+                if (g.ccid[s + c] == cid) {
+                    found = (int)c;
+                    break;
+                }
+            bool win = true;
+            if (found >= 0) {
+                const int64_t lcv = g.ccv[s + found];
+                if (cv != lcv) {
+                    win = cv > lcv;
+                } else {
+                    const Rec xr = load_rec(v.at(x));
+                    const Rec lr = load_rec(v.at(g.csrc[s + found]));
+                    const int vc = value_cmp(xr, lr);
+                    if (vc != 0) win = vc > 0;
+                    else win = site_rank_of(a, xr.site) > site_rank_of(a, lr.site);
+                }
+            }
+            if (win) {
+                gen_set_cell(g, s, ncell, cid, x, cv);
+                imp = 1;
+            }
+        }
+        if (a.impact && (pos & BATCH_POS)) a.impact[pos & 0x7FFFFFFFu] = (uint8_t)imp;
+    }
+    gen_emit(a, v, outb, outts, outcnt, flag, g, s, ncell, hs, scv, ssrc);
+}
+
+// The general body for one bucket, executed by the whole workgroup (nth threads).
+__device__ inline void gen_body(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts,
+                                uint32_t *outcnt, uint32_t *flag, const GenArrays &g, bool fields_loaded) {
+    const uint32_t n = v.np + v.nn;
+    const uint32_t tid = threadIdx.x, nth = blockDim.x;
+    if (!fields_loaded) {
+        for (uint32_t i = tid; i < n; i += nth) {
+            const Rec *r = v.at(i);
+            g.pk[i] = r->pk;
+            g.cv[i] = r->cv;
+            g.tc[i] = r->tcid;
+            g.cl[i] = r->cl;
+            g.pos[i] = r->pos;
+        }
+    }
+    for (uint32_t i = tid; i < g.slots; i += nth) g.own[i] = 0;
+    __syncthreads();
+    // group records by row (table, pk): open addressing, owner = first claimer
+    const uint32_t mask = g.slots - 1;
+    for (uint32_t i = tid; i < n; i += nth) {
+        const uint64_t pk = g.pk[i];
+        const uint32_t t = g.tc[i] >> 16;
+        uint32_t slot = row_hash(pk, t) & mask;
+        uint32_t row;
+        while (true) {
+            const uint32_t o = atomicCAS(&g.own[slot], 0u, i + 1);
+            if (o == 0) {
+                row = i;
+                break;
+            }
+            if (g.pk[o - 1] == pk && (g.tc[o - 1] >> 16) == t) {
+                row = o - 1;
+                break;
+            }
+            slot = (slot + 1) & mask;
+        }
+        g.key[i] = ((uint64_t)row << 32) | g.pos[i];
+        g.val[i] = i;
+    }
+    for (uint32_t i = n + tid; i < g.P; i += nth) {
+        g.key[i] = ~0ULL;
+        g.val[i] = 0;
+    }
+    __syncthreads();
+    // bitonic sort of (row, position)
+    for (uint32_t k = 2; k <= g.P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < g.P; i += nth) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t x = g.key[i], y = g.key[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        g.key[i] = y;
+                        g.key[ixj] = x;
+                        const uint32_t t = g.val[i];
+                        g.val[i] = g.val[ixj];
+                        g.val[ixj] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // one lane per row, in application order
+    for (uint32_t i = tid; i < n; i += nth) {
+        if (i == 0 || (g.key[i] >> 32) != (g.key[i - 1] >> 32))
+            gen_fold_row(a, v, outb, outts, outcnt, flag, g, i, n);
+    }
+}
+
+__device__ inline uint32_t next_pow2(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+constexpr size_t FAST_LDS = (size_t)CAP_FAST * (8 + 4) + (size_t)FAST_SLOTS * 4 + (size_t)CAP_FAST * 8 * 2;
+constexpr size_t GEN_LDS = (size_t)CAP_GEN * (8 + 8 + 4 + 4 + 4) + (size_t)GEN_SLOTS * 4 +
+                           (size_t)CAP_GEN * (8 + 4) + (size_t)CAP_GEN * (4 + 4 + 8);
+constexpr size_t MERGE_LDS = FAST_LDS > GEN_LDS ? FAST_LDS : GEN_LDS;
+
+__global__ void __launch_bounds__(MERGE_THREADS)
+k_merge(MergeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[MERGE_LDS];
+    __shared__ uint32_t s_outcnt, s_flag;
+    const uint32_t b = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    BucketView v;
+    v.np = a.prior_cnt[b];
+    v.nn = a.new_cnt[b];
+    v.prior = a.prior + a.prior_off[b];
+    v.fresh = a.stage + a.stage_off[b];
+    v.prior_ts = a.prior_ts ? a.prior_ts + a.prior_off[b] : nullptr;
+    const uint32_t n = v.np + v.nn;
+    Rec *outb = a.out + a.out_off[b];
+    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    if (n == 0) {
+        if (tid == 0) {
+            a.out_cnt[b] = 0;
+            a.out_flags[b] = 0;
+        }
+        return;
+    }
+    const bool general = a.force_general || a.prior_flags[b] || ((a.bflags[b >> 5] >> (b & 31)) & 1u);
+    if ((general && n > (uint32_t)CAP_GEN) || (!general && n > (uint32_t)CAP_FAST)) {
+        if (tid == 0) {
+            const unsigned long long k = atomicAdd(&a.misc[1], 1ULL);
+            a.ovf_list[k] = b;
+        }
+        return;
+    }
+    if (tid == 0) {
+        s_outcnt = 0;
+        s_flag = 0;
+    }
+    if (general) {
+        GenArrays g;
+        uint8_t *p = smem;
+        g.pk = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
+        g.cv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
+        g.key = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
+        g.ccv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
+        g.tc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+        g.cl = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+        g.pos = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+        g.val = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+        g.ccid = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+        g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+        g.own = reinterpret_cast<uint32_t *>(p);
+        g.slots = GEN_SLOTS;
+        g.P = next_pow2(n);
+        gen_body(a, v, outb, outts, &s_outcnt, &s_flag, g, false);
+    } else {
+        // ---------------- fast body: every row has causal length 1 and no sentinel ----------------
+        uint8_t *p = smem;
+        uint64_t *s_pk = reinterpret_cast<uint64_t *>(p); p += CAP_FAST * 8;
+        uint64_t *s_k0 = reinterpret_cast<uint64_t *>(p); p += CAP_FAST * 8;
+        uint64_t *s_k1 = reinterpret_cast<uint64_t *>(p); p += CAP_FAST * 8;
+        uint32_t *s_tc = reinterpret_cast<uint32_t *>(p); p += CAP_FAST * 4;
+        uint32_t *s_own = reinterpret_cast<uint32_t *>(p);
+        Rec r[FAST_R];
+        uint32_t cell[FAST_R];
+        bool alive[FAST_R];
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            const uint32_t i = k * MERGE_THREADS + tid;
+            alive[k] = i < n;
+            if (alive[k]) {
+                r[k] = load_rec(v.at(i));
+                s_pk[i] = r[k].pk;
+                s_tc[i] = r[k].tcid;
+            }
+        }
+        for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            const uint32_t i = k * MERGE_THREADS + tid;
+            cell[k] = 0;
+            if (alive[k]) {
+                uint32_t slot = cell_hash(r[k].pk, r[k].tcid) & (FAST_SLOTS - 1);
+                while (true) {
+                    const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
+                    if (o == 0) {
+                        cell[k] = i;
+                        s_k0[i] = 0;
+                        s_k1[i] = 0;
+                        break;
+                    }
+                    if (s_pk[o - 1] == r[k].pk && s_tc[o - 1] == r[k].tcid) {
+                        cell[k] = o - 1;
+                        break;
+                    }
+                    slot = (slot + 1) & (FAST_SLOTS - 1);
+                }
+            }
+        }
+        __syncthreads();
+        // argmax stages over the key (col_version, value, site rank, -position)
+        const bool wide = a.misc[3] != 0;
+        const int nstages = wide ? 6 : 3;
+        for (int st = 0; st < nstages; st++) {
+            uint64_t *kc = (st & 1) ? s_k1 : s_k0;
+            uint64_t *kn = (st & 1) ? s_k0 : s_k1;
+            uint64_t w[FAST_R];
+#pragma unroll
+            for (int k = 0; k < FAST_R; k++) {
+                w[k] = 0;
+                if (!alive[k]) continue;
+                const uint32_t ty = vtype(r[k].meta);
+                const int which = wide ? st : (st == 0 ? 0 : (st == 1 ? 2 : 5));
+                switch (which) {
+                case 0: w[k] = (uint64_t)r[k].cv ^ 0x8000000000000000ULL; break;
+                case 1: w[k] = 5u - ty; break;
+                case 2: w[k] = vkey0(ty, r[k].v0); break;
+                case 3: w[k] = (ty == CORRO_TEXT || ty == CORRO_BLOB) ? r[k].v1 : 0; break;
+                case 4: w[k] = (ty == CORRO_TEXT || ty == CORRO_BLOB) ? vlen(r[k].meta) : 0; break;
+                default:
+                    w[k] = ((uint64_t)site_rank_of(a, r[k].site) << 32) | (uint64_t)(~r[k].pos);
+                    break;
+                }
+                atomicMax(reinterpret_cast<unsigned long long *>(&kc[cell[k]]), (unsigned long long)w[k]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < FAST_R; k++) {
+                const uint32_t i = k * MERGE_THREADS + tid;
+                if (alive[k]) {
+                    alive[k] = kc[cell[k]] == w[k];
+                }
+                if (i < n && cell[k] == i) kn[i] = 0;
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            if (!alive[k]) continue;
+            const uint32_t o = atomicAdd(&s_outcnt, 1u);
+            Rec x = r[k];
+            const uint64_t ts = a.track_ts ? rec_ts(a, v, x) : 0ULL;
+            x.cl = 1;
+            x.pos = o;
+            store_rec(outb + o, x);
+            if (a.track_ts) outts[o] = ts;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.out_cnt[b] = s_outcnt;
+        a.out_flags[b] = s_flag;
+        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+    }
+}
+
+// Oversized buckets: the general body on a global scratch slice. One workgroup per bucket.
+__global__ void __launch_bounds__(OVF_THREADS)
+k_merge_ovf(MergeArgs a, const uint64_t *__restrict__ scratch_off, uint8_t *__restrict__ scratch) {
+    __shared__ uint32_t s_outcnt, s_flag;
+    const uint32_t b = a.ovf_list[blockIdx.x];
+    BucketView v;
+    v.np = a.prior_cnt[b];
+    v.nn = a.new_cnt[b];
+    v.prior = a.prior + a.prior_off[b];
+    v.fresh = a.stage + a.stage_off[b];
+    v.prior_ts = a.prior_ts ? a.prior_ts + a.prior_off[b] : nullptr;
+    const uint32_t n = v.np + v.nn;
+    Rec *outb = a.out + a.out_off[b];
+    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    if (threadIdx.x == 0) {
+        s_outcnt = 0;
+        s_flag = 0;
+    }
+    const uint32_t P = next_pow2(n), slots = next_pow2(2 * n);
+    uint8_t *p = scratch + scratch_off[blockIdx.x];
+    GenArrays g;
+    g.key = reinterpret_cast<uint64_t *>(p); p += (size_t)P * 8;
+    g.pk = reinterpret_cast<uint64_t *>(p); p += (size_t)n * 8;
+    g.cv = reinterpret_cast<int64_t *>(p); p += (size_t)n * 8;
+    g.ccv = reinterpret_cast<int64_t *>(p); p += (size_t)n * 8;
+    g.val = reinterpret_cast<uint32_t *>(p); p += (size_t)P * 4;
+    g.own = reinterpret_cast<uint32_t *>(p); p += (size_t)slots * 4;
+    g.tc = reinterpret_cast<uint32_t *>(p); p += (size_t)n * 4;
+    g.cl = reinterpret_cast<uint32_t *>(p); p += (size_t)n * 4;
+    g.pos = reinterpret_cast<uint32_t *>(p); p += (size_t)n * 4;
+    g.ccid = reinterpret_cast<uint32_t *>(p); p += (size_t)n * 4;
+    g.csrc = reinterpret_cast<uint32_t *>(p);
+    g.slots = slots;
+    g.P = P;
+    gen_body(a, v, outb, outts, &s_outcnt, &s_flag, g, false);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.out_cnt[b] = s_outcnt;
+        a.out_flags[b] = s_flag;
+        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+    }
+}
+
+// size of the k_merge_ovf scratch slice for a bucket of n records (16-B aligned)
+__host__ __device__ inline uint64_t ovf_scratch_bytes(uint64_t n) {
+    uint64_t P = 1, S = 1;
+    while (P < n) P <<= 1;
+    while (S < 2 * n) S <<= 1;
+    const uint64_t bytes = P * 8 + n * 24 + P * 4 + S * 4 + n * 20;
+    return (bytes + 15) & ~15ULL;
+}
+
+// crsql_db_versions fold after a successful batch
+__global__ void k_dbv_fold(unsigned long long *__restrict__ dbv, const unsigned long long *__restrict__ batch,
+                           uint32_t nsites) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nsites && batch[i] > dbv[i]) dbv[i] = batch[i];
+}
+
+// export: bucket slices -> dense SoA rows
+__global__ void k_export(const Rec *__restrict__ st, const uint64_t *__restrict__ st_ts,
+                         const uint64_t *__restrict__ off, const uint32_t *__restrict__ cnt,
+                         const uint64_t *__restrict__ dense, corro_rows o) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t n = cnt[b];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const Rec r = load_rec(st + off[b] + i);
+        const uint64_t k = dense[b] + i;
+        o.pk[k] = r.pk;
+        o.table_cid[k] = r.tcid;
+        o.col_version[k] = r.cv;
+        o.db_version[k] = r.dbv;
+        o.cl[k] = (int64_t)r.cl;
+        o.seq[k] = r.seq;
+        o.site[k] = r.site;
+        o.ts[k] = st_ts ? st_ts[off[b] + i] : 0ULL;
+        o.val0[k] = r.v0;
+        o.val1[k] = r.v1;
+        o.val_type[k] = (uint8_t)vtype(r.meta);
+        o.val_len[k] = (uint8_t)vlen(r.meta);
+    }
+}
+
+}  // namespace corro

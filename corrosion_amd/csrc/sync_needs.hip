@@ -1,0 +1,313 @@
+// Batched SyncStateV1::compute_available_needs (/root/reference/crates/corro-types/src/sync.rs:127-249)
+// over CSR (node-pair, actor) entries: one lane per entry, two passes (count, fill).
+//
+// Per entry, with `holes` = their need ranges ∪ {their partial versions}:
+//   haves = {1..=head} − holes                                   (sync.rs:141-162)
+//   Full(r ∩ h) for every our-need range r, for every maximal haves range h overlapping r,
+//     in our range order, ascending inside each                   (sync.rs:164-174)
+//   for every our partial (v, seqs):                              (sync.rs:176-226)
+//     v ∈ haves                -> Partial(v, seqs)
+//     else they have partial v -> Partial(v, seqs ∩ ({0..=max end} − their seqs)) if non-empty
+//   Full(our_head+1..=head) if head > our_head, Full(1..=head) if we have no head (sync.rs:229-245)
+// "maximal haves range" is realised by a sweep that jumps over holes, so no set is materialised.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace corro {
+
+struct SyncDev {
+    uint64_t n;
+    const uint64_t *their_head;
+    const int64_t *our_head;
+    const uint64_t *tn_off, *tn_start, *tn_end;
+    const uint64_t *tp_off, *tp_ver;
+    const uint64_t *tps_off, *tps_start, *tps_end;
+    const uint64_t *on_off, *on_start, *on_end;
+    const uint64_t *op_off, *op_ver;
+    const uint64_t *ops_off, *ops_start, *ops_end;
+};
+
+// Holes of an entry's version space: their need ranges [tn] and their partial versions [tp].
+struct VerHoles {
+    const uint64_t *hs, *he;  // ranges
+    uint64_t h0, h1;
+    const uint64_t *pv;       // points
+    uint64_t p0, p1;
+    // if x lies in a hole, return the hole end (max over holes containing x) else return false
+    __device__ inline bool covering(uint64_t x, uint64_t &end) const {
+        bool hit = false;
+        for (uint64_t k = h0; k < h1; k++)
+            if (hs[k] <= x && x <= he[k] && (!hit || he[k] > end)) {
+                end = he[k];
+                hit = true;
+            }
+        for (uint64_t k = p0; k < p1; k++)
+            if (pv[k] == x && (!hit || x > end)) {
+                end = x;
+                hit = true;
+            }
+        return hit;
+    }
+    // smallest hole start > x (UINT64_MAX if none)
+    __device__ inline uint64_t next_start(uint64_t x) const {
+        uint64_t m = ~0ULL;
+        for (uint64_t k = h0; k < h1; k++)
+            if (hs[k] > x && hs[k] < m) m = hs[k];
+        for (uint64_t k = p0; k < p1; k++)
+            if (pv[k] > x && pv[k] < m) m = pv[k];
+        return m;
+    }
+};
+
+struct SeqHoles {
+    const uint64_t *hs, *he;
+    uint64_t h0, h1;
+    __device__ inline bool covering(uint64_t x, uint64_t &end) const {
+        bool hit = false;
+        for (uint64_t k = h0; k < h1; k++)
+            if (hs[k] <= x && x <= he[k] && (!hit || he[k] > end)) {
+                end = he[k];
+                hit = true;
+            }
+        return hit;
+    }
+    __device__ inline uint64_t next_start(uint64_t x) const {
+        uint64_t m = ~0ULL;
+        for (uint64_t k = h0; k < h1; k++)
+            if (hs[k] > x && hs[k] < m) m = hs[k];
+        return m;
+    }
+};
+
+// Visit maximal pieces of ([lo, hi] ∩ universe[ulo, uhi]) − holes in ascending order.
+template <class H, class F>
+__device__ inline void sweep(const H &holes, uint64_t lo, uint64_t hi, uint64_t ulo, uint64_t uhi, F &&emit) {
+    uint64_t x = lo > ulo ? lo : ulo;
+    const uint64_t top = hi < uhi ? hi : uhi;
+    while (x <= top) {
+        uint64_t e;
+        if (holes.covering(x, e)) {
+            if (e >= top) return;
+            x = e + 1;
+            continue;
+        }
+        const uint64_t ns = holes.next_start(x);
+        const uint64_t pe = (ns == ~0ULL || ns - 1 > top) ? top : ns - 1;
+        emit(x, pe);
+        if (pe >= top) return;
+        x = pe + 1;
+    }
+}
+
+__global__ void k_needs(SyncDev in, corro_needs_out o, int fill) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= in.n) return;
+    const uint64_t head = in.their_head[e];
+    VerHoles vh{in.tn_start, in.tn_end, in.tn_off[e], in.tn_off[e + 1], in.tp_ver, in.tp_off[e], in.tp_off[e + 1]};
+    uint64_t nn = 0, ns = 0;
+    const uint64_t nbase = fill ? o.need_off[e] : 0, sbase = fill ? o.seq_off[e] : 0;
+    auto full = [&](uint64_t s, uint64_t t) {
+        if (fill) {
+            const uint64_t k = nbase + nn;
+            o.kind[k] = 0;
+            o.start[k] = s;
+            o.end[k] = t;
+            o.sr_off[k] = sbase + ns;
+            o.sr_n[k] = 0;
+        }
+        nn++;
+    };
+    for (uint64_t k = in.on_off[e]; k < in.on_off[e + 1]; k++) sweep(vh, in.on_start[k], in.on_end[k], 1, head, full);
+
+    for (uint64_t k = in.op_off[e]; k < in.op_off[e + 1]; k++) {
+        const uint64_t v = in.op_ver[k];
+        uint64_t dummy;
+        const bool have = v >= 1 && v <= head && !vh.covering(v, dummy);
+        const uint64_t q0 = in.ops_off[k], q1 = in.ops_off[k + 1];
+        if (have) {
+            if (fill) {
+                const uint64_t q = nbase + nn;
+                o.kind[q] = 1;
+                o.start[q] = v;
+                o.end[q] = v;
+                o.sr_off[q] = sbase + ns;
+                o.sr_n[q] = q1 - q0;
+                for (uint64_t j = q0; j < q1; j++) {
+                    o.s_start[sbase + ns + (j - q0)] = in.ops_start[j];
+                    o.s_end[sbase + ns + (j - q0)] = in.ops_end[j];
+                }
+            }
+            ns += q1 - q0;
+            nn++;
+            continue;
+        }
+        int64_t tk = -1;
+        for (uint64_t j = in.tp_off[e]; j < in.tp_off[e + 1]; j++)
+            if (in.tp_ver[j] == v) {
+                tk = (int64_t)j;
+                break;
+            }
+        if (tk < 0) continue;
+        bool have_end = false;
+        uint64_t end = 0;
+        for (uint64_t j = in.tps_off[tk]; j < in.tps_off[tk + 1]; j++)
+            if (!have_end || in.tps_end[j] > end) {
+                end = in.tps_end[j];
+                have_end = true;
+            }
+        for (uint64_t j = q0; j < q1; j++)
+            if (!have_end || in.ops_end[j] > end) {
+                end = in.ops_end[j];
+                have_end = true;
+            }
+        if (!have_end) continue;
+        SeqHoles sh{in.tps_start, in.tps_end, in.tps_off[tk], in.tps_off[tk + 1]};
+        const uint64_t first = sbase + ns;
+        uint64_t cnt = 0;
+        auto piece = [&](uint64_t s, uint64_t t) {
+            if (fill) {
+                o.s_start[first + cnt] = s;
+                o.s_end[first + cnt] = t;
+            }
+            cnt++;
+        };
+        for (uint64_t j = q0; j < q1; j++) sweep(sh, in.ops_start[j], in.ops_end[j], 0, end, piece);
+        if (cnt) {
+            if (fill) {
+                const uint64_t q = nbase + nn;
+                o.kind[q] = 1;
+                o.start[q] = v;
+                o.end[q] = v;
+                o.sr_off[q] = first;
+                o.sr_n[q] = cnt;
+            }
+            nn++;
+            ns += cnt;
+        }
+    }
+    const int64_t ours = in.our_head[e];
+    if (ours < 0) full(1, head);
+    else if (head > (uint64_t)ours) full((uint64_t)ours + 1, head);
+    if (!fill) {
+        o.need_count[e] = nn;
+        o.seq_count[e] = ns;
+    }
+}
+
+}  // namespace corro
+
+using namespace corro;
+
+extern "C" int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in, int mem, corro_needs_out *out,
+                                   int pass) {
+    if (!ctx || !in || !out) return fail(CORRO_E_INVALID, "NULL argument");
+    if (pass != 0 && pass != 1) return fail(CORRO_E_INVALID, "pass must be 0 or 1");
+    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
+    const uint64_t n = in->n;
+    if (n == 0) return CORRO_OK;
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    SyncDev d{};
+    d.n = n;
+    corro_needs_out od = *out;
+    if (mem == CORRO_MEM_DEVICE) {
+        d.their_head = in->their_head; d.our_head = in->our_head;
+        d.tn_off = in->tn_off; d.tn_start = in->tn_start; d.tn_end = in->tn_end;
+        d.tp_off = in->tp_off; d.tp_ver = in->tp_ver;
+        d.tps_off = in->tps_off; d.tps_start = in->tps_start; d.tps_end = in->tps_end;
+        d.on_off = in->on_off; d.on_start = in->on_start; d.on_end = in->on_end;
+        d.op_off = in->op_off; d.op_ver = in->op_ver;
+        d.ops_off = in->ops_off; d.ops_start = in->ops_start; d.ops_end = in->ops_end;
+    } else {
+        // element counts of every CSR array
+        const uint64_t ntn = in->tn_off[n], ntp = in->tp_off[n], nop = in->op_off[n], non = in->on_off[n];
+        const uint64_t ntps = ntp ? in->tps_off[ntp] : 0, nops = nop ? in->ops_off[nop] : 0;
+        struct F { const void *src; uint64_t cnt; const void **dst; };
+        F f[] = {{in->their_head, n, (const void **)&d.their_head}, {in->our_head, n, (const void **)&d.our_head},
+                 {in->tn_off, n + 1, (const void **)&d.tn_off},     {in->tn_start, ntn, (const void **)&d.tn_start},
+                 {in->tn_end, ntn, (const void **)&d.tn_end},       {in->tp_off, n + 1, (const void **)&d.tp_off},
+                 {in->tp_ver, ntp, (const void **)&d.tp_ver},       {in->tps_off, ntp + 1, (const void **)&d.tps_off},
+                 {in->tps_start, ntps, (const void **)&d.tps_start}, {in->tps_end, ntps, (const void **)&d.tps_end},
+                 {in->on_off, n + 1, (const void **)&d.on_off},     {in->on_start, non, (const void **)&d.on_start},
+                 {in->on_end, non, (const void **)&d.on_end},       {in->op_off, n + 1, (const void **)&d.op_off},
+                 {in->op_ver, nop, (const void **)&d.op_ver},       {in->ops_off, nop + 1, (const void **)&d.ops_off},
+                 {in->ops_start, nops, (const void **)&d.ops_start}, {in->ops_end, nops, (const void **)&d.ops_end}};
+        uint64_t total = 0;
+        for (size_t i = 0; i < sizeof(f) / sizeof(f[0]); i++) {
+            // nested offsets (tps_off / ops_off) may be NULL when there are no partials
+            if (!f[i].src && ((i == 7 && ntp == 0) || (i == 15 && nop == 0))) f[i].cnt = 0;
+            if (!f[i].src && f[i].cnt) return fail(CORRO_E_INVALID, "a required sync entry array is NULL");
+            total += ((f[i].cnt * 8 + 255) / 256) * 256;
+        }
+        // outputs
+        uint64_t tneeds = 0, tseqs = 0;
+        if (pass == 1) {
+            tneeds = out->need_off[n];
+            tseqs = out->seq_off[n];
+        }
+        const uint64_t out_bytes = pass == 0 ? 2 * ((n * 8 + 255) / 256) * 256
+                                             : 2 * (((n + 1) * 8 + 255) / 256) * 256 + ((tneeds + 255) / 256) * 256 +
+                                                   4 * ((tneeds * 8 + 255) / 256) * 256 +
+                                                   2 * ((tseqs * 8 + 255) / 256) * 256;
+        if (int rc = ctx->d_needs.ensure(total + out_bytes + 4096)) return rc;
+        uint8_t *p = ctx->d_needs.as<uint8_t>();
+        for (auto &x : f) {
+            *x.dst = p;
+            if (x.cnt && x.src) CORRO_HIP_TRY(hipMemcpyAsync(p, x.src, x.cnt * 8, hipMemcpyHostToDevice, s));
+            p += ((x.cnt * 8 + 255) / 256) * 256;
+        }
+        auto carve = [&](uint64_t bytes) {
+            uint8_t *q = p;
+            p += ((bytes + 255) / 256) * 256;
+            return q;
+        };
+        if (pass == 0) {
+            od.need_count = (uint64_t *)carve(n * 8);
+            od.seq_count = (uint64_t *)carve(n * 8);
+        } else {
+            uint64_t *no = (uint64_t *)carve((n + 1) * 8), *so = (uint64_t *)carve((n + 1) * 8);
+            CORRO_HIP_TRY(hipMemcpyAsync(no, out->need_off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+            CORRO_HIP_TRY(hipMemcpyAsync(so, out->seq_off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+            od.need_off = no;
+            od.seq_off = so;
+            od.kind = (uint8_t *)carve(tneeds);
+            od.start = (uint64_t *)carve(tneeds * 8);
+            od.end = (uint64_t *)carve(tneeds * 8);
+            od.sr_off = (uint64_t *)carve(tneeds * 8);
+            od.sr_n = (uint64_t *)carve(tneeds * 8);
+            od.s_start = (uint64_t *)carve(tseqs * 8);
+            od.s_end = (uint64_t *)carve(tseqs * 8);
+        }
+    }
+    const uint32_t threads = 256;
+    const uint64_t blocks = (n + threads - 1) / threads;
+    if (blocks > 0x7FFFFFFFULL) return fail(CORRO_E_RANGE, "too many sync entries");
+    hipLaunchKernelGGL(k_needs, dim3((uint32_t)blocks), dim3(threads), 0, s, d, od, pass);
+    CORRO_HIP_TRY(hipGetLastError());
+    if (mem == CORRO_MEM_HOST) {
+        if (pass == 0) {
+            CORRO_HIP_TRY(hipMemcpyAsync(out->need_count, od.need_count, n * 8, hipMemcpyDeviceToHost, s));
+            CORRO_HIP_TRY(hipMemcpyAsync(out->seq_count, od.seq_count, n * 8, hipMemcpyDeviceToHost, s));
+        } else {
+            const uint64_t tneeds = out->need_off[n], tseqs = out->seq_off[n];
+            if (tneeds) {
+                CORRO_HIP_TRY(hipMemcpyAsync(out->kind, od.kind, tneeds, hipMemcpyDeviceToHost, s));
+                CORRO_HIP_TRY(hipMemcpyAsync(out->start, od.start, tneeds * 8, hipMemcpyDeviceToHost, s));
+                CORRO_HIP_TRY(hipMemcpyAsync(out->end, od.end, tneeds * 8, hipMemcpyDeviceToHost, s));
+                CORRO_HIP_TRY(hipMemcpyAsync(out->sr_off, od.sr_off, tneeds * 8, hipMemcpyDeviceToHost, s));
+                CORRO_HIP_TRY(hipMemcpyAsync(out->sr_n, od.sr_n, tneeds * 8, hipMemcpyDeviceToHost, s));
+            }
+            if (tseqs) {
+                CORRO_HIP_TRY(hipMemcpyAsync(out->s_start, od.s_start, tseqs * 8, hipMemcpyDeviceToHost, s));
+                CORRO_HIP_TRY(hipMemcpyAsync(out->s_end, od.s_end, tseqs * 8, hipMemcpyDeviceToHost, s));
+            }
+        }
+    }
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}

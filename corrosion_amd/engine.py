@@ -1,0 +1,156 @@
+"""MergeEngine: the device-resident replacement of cr-sqlite's `crsql_changes` merge.
+
+One MergeEngine corresponds to one corrosion writer connection with the CRR schema applied
+(corro-types/src/agent.rs:480-482 single writer; schema.rs:362-363 crsql_as_crr). `apply` is the
+batched form of the per-change loop in process_complete_version
+(/root/reference/crates/corro-agent/src/agent/util.rs:1222-1262): changes are applied in index
+order, exactly as consecutive `INSERT INTO crsql_changes` statements would be.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+BATCH_FIELDS = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64,
+                "db_version": np.int64, "cl": np.uint32, "seq": np.uint32, "site": np.uint32,
+                "val0": np.uint64, "val1": np.uint64, "val_type": np.uint8, "val_len": np.uint8,
+                "ts": np.uint64}
+REQUIRED = ("pk", "table_cid", "col_version", "db_version", "cl", "seq", "site", "val0")
+ROW_FIELDS = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64,
+              "db_version": np.int64, "cl": np.int64, "seq": np.uint32, "site": np.uint32,
+              "ts": np.uint64, "val0": np.uint64, "val1": np.uint64, "val_type": np.uint8,
+              "val_len": np.uint8}
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+class MergeEngine:
+    def __init__(self, schema, capacity_hint=1 << 20, device=0):
+        """schema: {table_name: [column names]} in table order (cid k = column k-1, cid 0 = '-1')."""
+        lib = L.lib()
+        self.schema = list(schema.items())
+        descs = (L.TableDesc * max(1, len(self.schema)))()
+        self._keep = []
+        for i, (name, cols) in enumerate(self.schema):
+            arr = (C.c_char_p * max(1, len(cols)))(*[c.encode() for c in cols])
+            self._keep.append(arr)
+            descs[i].name = name.encode()
+            descs[i].ncols = len(cols)
+            descs[i].col_names = C.cast(arr, C.POINTER(C.c_char_p))
+        h = C.c_void_p()
+        L.check(lib.corro_ctx_create(descs, len(self.schema), capacity_hint, device, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().corro_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---- schema / sites -------------------------------------------------------------------
+    def lookup(self, table, cid):
+        out = C.c_uint32()
+        L.check(L.lib().corro_lookup_cid(self._h, table.encode(), cid.encode(), C.byref(out)))
+        return out.value
+
+    def register_sites(self, site_ids):
+        ids = np.ascontiguousarray(site_ids, dtype=np.uint8).reshape(-1, 16)
+        ords = np.zeros(max(1, ids.shape[0]), np.uint32)
+        L.check(L.lib().corro_site_register(self._h, ids.ctypes.data, ids.shape[0], ords.ctypes.data))
+        return ords[: ids.shape[0]]
+
+    def site_count(self):
+        c = C.c_uint32()
+        L.check(L.lib().corro_site_count(self._h, C.byref(c)))
+        return c.value
+
+    # ---- merge ------------------------------------------------------------------------------
+    def apply(self, batch, impact=False):
+        """Merge a batch (dict of numpy arrays on the host, or of torch tensors on the GPU).
+
+        Returns the per-change crsql_rows_impacted() growth when impact=True, else None."""
+        for k in REQUIRED:
+            if k not in batch or batch[k] is None:
+                raise ValueError(f"batch lacks required field {k!r}")
+        s = L.Changes()
+        keep = []
+        on_dev = _is_torch(batch["pk"])
+        n = int(batch["pk"].shape[0])
+        s.n = n
+        for k, dt in BATCH_FIELDS.items():
+            a = batch.get(k)
+            if a is None:
+                setattr(s, k, None)
+                continue
+            if on_dev:
+                if not a.is_cuda or not a.is_contiguous() or a.element_size() != np.dtype(dt).itemsize:
+                    raise ValueError(f"device field {k} must be a contiguous CUDA tensor of {np.dtype(dt)}")
+                if int(a.shape[0]) != n:
+                    raise ValueError(f"field {k} has {a.shape[0]} elements, expected {n}")
+                setattr(s, k, a.data_ptr() if n else None)
+            else:
+                a = np.ascontiguousarray(a, dtype=dt)
+                if a.shape[0] != n:
+                    raise ValueError(f"field {k} has {a.shape[0]} elements, expected {n}")
+                keep.append(a)
+                setattr(s, k, a.ctypes.data if n else None)
+        out = L.ApplyOut()
+        imp = None
+        if impact:
+            imp = np.zeros(max(n, 1), np.uint8)
+            out.impact = imp.ctypes.data
+        if on_dev:
+            import torch
+            torch.cuda.current_stream().synchronize()
+        L.check(L.lib().corro_apply_batch(self._h, C.byref(s), L.CORRO_MEM_DEVICE if on_dev else L.CORRO_MEM_HOST,
+                                          C.byref(out)))
+        return imp[:n] if impact else None
+
+    def count(self):
+        c = C.c_uint64()
+        L.check(L.lib().corro_state_count(self._h, C.byref(c)))
+        return c.value
+
+    def reset(self):
+        L.check(L.lib().corro_state_reset(self._h))
+
+    def export(self):
+        """crsql_changes rows (unspecified order) as a dict of numpy arrays."""
+        m = self.count()
+        out = {k: np.zeros(max(m, 1), dt) for k, dt in ROW_FIELDS.items()}
+        r = L.Rows()
+        for k, a in out.items():
+            setattr(r, k, a.ctypes.data)
+        w = C.c_uint64()
+        L.check(L.lib().corro_state_export(self._h, C.byref(r), max(m, 1), C.byref(w)))
+        return {k: a[: w.value] for k, a in out.items()}
+
+    def db_versions(self):
+        n = self.site_count()
+        out = np.zeros(max(n, 1), np.int64)
+        L.check(L.lib().corro_db_versions(self._h, out.ctypes.data, n))
+        return out[:n]
+
+    # ---- timing (HIP events on the engine stream) ---------------------------------------
+    def set_profiling(self, on=True):
+        L.check(L.lib().corro_ctx_set_profiling(self._h, 1 if on else 0))
+
+    def last_timings(self):
+        """ms per stage of the last apply: hist, colscan, plan, scatter, merge, overflow"""
+        arr = (C.c_float * 8)()
+        n = C.c_uint32()
+        L.check(L.lib().corro_last_timings(self._h, arr, 8, C.byref(n)))
+        names = ["k_hist", "k_colscan", "k_plan", "k_scatter", "k_merge", "k_merge_ovf"]
+        return {names[i]: arr[i] for i in range(min(n.value, len(names)))}
+
+    # ---- sync need diff -------------------------------------------------------------------
+    def compute_needs(self, entries):
+        """Batched compute_available_needs over CSR entries (see corrosion_amd.sync)."""
+        from .sync import _needs_host
+        return _needs_host(self, entries)

@@ -1,0 +1,217 @@
+/*
+ * corro_hip.h — C ABI of the MI355X batched CRDT merge engine (libcorro_hip.so).
+ *
+ * This is the boundary a `corro-hip` Rust crate binds (see INTEGRATION.md for the `extern "C"`
+ * block). It replaces, for corrosion's apply hot path, the per-change SQL loop
+ *     for change in changes { INSERT INTO crsql_changes (...); SELECT crsql_rows_impacted(); }
+ * in process_complete_version (/root/reference/crates/corro-agent/src/agent/util.rs:1222-1262),
+ * i.e. cr-sqlite's `crsql_changes` xUpdate merge (prebuilt crsqlite-linux-x86_64.so, entry
+ * `sqlite3_crsqlite_init`, loaded at corro-types/src/sqlite.rs:121-139), plus the sync
+ * bookkeeping arithmetic of corro-types (SyncStateV1::compute_available_needs, sync.rs:127-249;
+ * VersionsSnapshot::compute_gaps_change/insert_db, agent.rs:1108-1235).
+ *
+ * Conventions
+ *   - Every function returns an int status: CORRO_OK (0) or a negative corro_status.
+ *     corro_last_error() returns a NUL-terminated description of the last failure on the
+ *     calling thread.
+ *   - All pointers are plain host (or, where `mem` says so, device) pointers; sizes are counts of
+ *     elements. No callbacks; no ownership transfer: the caller owns every buffer it passes.
+ *   - A context is thread-compatible, not thread-safe: one context per writer, mirroring the
+ *     single SQLite writer of the reference (corro-types/src/agent.rs:480-482, setup.rs:97).
+ *   - The library never falls back to a CPU path: without a usable gfx950 device every compute
+ *     entry point fails with CORRO_E_NO_DEVICE.
+ */
+#ifndef CORRO_HIP_H
+#define CORRO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CORRO_HIP_ABI_VERSION 1
+
+typedef enum {
+    CORRO_OK = 0,
+    CORRO_E_INVALID = -1,        /* bad argument / malformed input */
+    CORRO_E_NOMEM = -2,          /* host or device allocation failed */
+    CORRO_E_DEVICE = -3,         /* HIP runtime error */
+    CORRO_E_UNKNOWN_TABLE = -4,  /* "no such table" (the INSERT would fail: util.rs:839-860) */
+    CORRO_E_UNKNOWN_COLUMN = -5, /* unknown cid: cr-sqlite raises "SQL logic error" */
+    CORRO_E_RANGE = -6,          /* value outside the engine's fixed-width encoding */
+    CORRO_E_NO_DEVICE = -7       /* no HIP device visible */
+} corro_status;
+
+/* SQLite storage classes, numbered like corro-api-types ColumnType (lib.rs:300-307) */
+enum { CORRO_INTEGER = 1, CORRO_REAL = 2, CORRO_TEXT = 3, CORRO_BLOB = 4, CORRO_NULL = 5 };
+
+/* Where a batch's arrays live */
+enum { CORRO_MEM_HOST = 0, CORRO_MEM_DEVICE = 1 };
+
+typedef struct corro_ctx corro_ctx;
+
+/* One CRR table: its name and non-pk column names. cid k (1-based) = col_names[k-1];
+ * cid 0 is cr-sqlite's row sentinel "-1" (corro-api-types/src/lib.rs:748-751). */
+typedef struct {
+    const char *name;
+    uint32_t ncols;
+    const char *const *col_names;
+} corro_table_desc;
+
+/*
+ * A batch of column changes (corro-types/src/change.rs:19-30 `Change`), struct-of-arrays,
+ * application order = index order: actors ascending by 16-byte id, changesets in arrival
+ * order, changes in vector order (util.rs:705,765,782,1222). Required arrays: pk, table_cid,
+ * col_version, db_version, cl, seq, site, val0. Optional (NULL): val1, val_type, val_len, ts.
+ *
+ *   pk          row key: the table's single INTEGER pk value, or a host-interned key of the
+ *               packed pk bytes (pubsub.rs:2304-2358), like cr-sqlite's `__crsql_key`
+ *   table_cid   (table_index << 16) | cid, cid 0 = sentinel "-1"
+ *   cl          causal length (< 2^32); sentinel changes and even-cl changes need
+ *               0 <= col_version < 2^32 (their col_version becomes the row's causal length)
+ *   seq         CrsqlSeq (< 2^32)
+ *   site        site ordinal from corro_site_register (crsql_site_id.ordinal analogue)
+ *   val0/val1   INTEGER: i64 bits in val0. REAL: f64 bits in val0 (NaN not allowed).
+ *               TEXT/BLOB (<= 16 bytes): bytes 0..7 / 8..15 big-endian, zero padded.
+ *   val_type    CORRO_* storage class (NULL array = all INTEGER)
+ *   val_len     TEXT/BLOB byte length
+ *   ts          changeset timestamp (NTP64), bound per change as in util.rs:1244
+ */
+typedef struct {
+    uint64_t n;
+    const uint64_t *pk;
+    const uint32_t *table_cid;
+    const int64_t *col_version;
+    const int64_t *db_version;
+    const uint32_t *cl;
+    const uint32_t *seq;
+    const uint32_t *site;
+    const uint64_t *val0;
+    const uint64_t *val1;
+    const uint8_t *val_type;
+    const uint8_t *val_len;
+    const uint64_t *ts;
+} corro_changes;
+
+/* Per-batch outputs (all optional, host pointers, n elements each) */
+typedef struct {
+    /* crsql_rows_impacted() growth caused by each change (0, 1 or 2), util.rs:1246-1260 */
+    uint8_t *impact;
+} corro_apply_out;
+
+/* crsql_changes read-back rows (table, pk, cid, val, col_version, db_version, site_id, cl, seq, ts) */
+typedef struct {
+    uint64_t *pk;
+    uint32_t *table_cid;
+    int64_t *col_version;
+    int64_t *db_version;
+    int64_t *cl;
+    uint32_t *seq;
+    uint32_t *site;
+    uint64_t *ts;
+    uint64_t *val0;
+    uint64_t *val1;
+    uint8_t *val_type;
+    uint8_t *val_len;
+} corro_rows;
+
+/* ------------------------------------------------------------------ context */
+
+const char *corro_last_error(void);
+int corro_abi_version(void);
+/* number of visible HIP devices (0 if none); does not initialise a context */
+int corro_device_count(int *count);
+
+/* Create an engine bound to a schema. `capacity_hint` = expected clock rows + changes per
+ * apply (sizes the bucket table); `device` = HIP ordinal. Mirrors CrConn::init + apply_schema. */
+int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t capacity_hint,
+                     int device, corro_ctx **out);
+void corro_ctx_destroy(corro_ctx *ctx);
+
+/* Resolve Change.table / Change.cid strings. Unknown names -> CORRO_E_UNKNOWN_TABLE/_COLUMN. */
+int corro_lookup_cid(corro_ctx *ctx, const char *table, const char *cid, uint32_t *table_cid);
+
+/* Register 16-byte site ids (ActorId bytes), returning stable ordinals (existing ids keep theirs).
+ * The engine orders sites by memcmp of the bytes for the merge-equal-values tie-break. */
+int corro_site_register(corro_ctx *ctx, const uint8_t *site_ids, uint64_t n, uint32_t *ordinals);
+int corro_site_count(corro_ctx *ctx, uint32_t *count);
+
+/* ------------------------------------------------------------------ merge */
+
+/* Merge one batch into the device state (equivalent to one INSERT INTO crsql_changes per change,
+ * in index order). `mem` says where the arrays live. Synchronous: returns after the state is
+ * resident and outputs are written. */
+int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out);
+
+/* Clock rows currently in the state (sentinels included). */
+int corro_state_count(corro_ctx *ctx, uint64_t *count);
+/* Copy the state out in crsql_changes form, unspecified row order; `cap` = capacity of `out`. */
+int corro_state_export(corro_ctx *ctx, corro_rows *out, uint64_t cap, uint64_t *written);
+/* Drop all merged state (keeps schema, sites and crsql_db_versions). */
+int corro_state_reset(corro_ctx *ctx);
+/* crsql_db_versions: per-site max db_version over every merged change, -1 = never seen. */
+int corro_db_versions(corro_ctx *ctx, int64_t *out, uint32_t nsites);
+
+/* Stage timing with HIP events recorded on the engine's stream (for roofline reporting).
+ * corro_last_timings returns milliseconds of the last apply per stage:
+ * [0] k_hist [1] k_colscan [2] k_plan [3] k_scatter [4] k_merge [5] k_merge_ovf (0 if not run). */
+int corro_ctx_set_profiling(corro_ctx *ctx, int on);
+int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count);
+
+/* ------------------------------------------------------------------ sync need diff */
+
+/* CSR over (node-pair, actor) entries of two SyncStateV1 (sync.rs:79-87). One entry = one
+ * `(actor_id, head)` of other.heads that compute_available_needs does not skip (actor !=
+ * self.actor_id and head != 0, sync.rs:133-140). Partials must be listed per entry in the
+ * order the caller wants them emitted (ascending version = canonical HashMap order). */
+typedef struct {
+    uint64_t n;
+    const uint64_t *their_head;
+    const int64_t *our_head;  /* -1 = None */
+    const uint64_t *tn_off, *tn_start, *tn_end;               /* other.need[a] */
+    const uint64_t *tp_off, *tp_ver;                           /* other.partial_need[a] keys */
+    const uint64_t *tps_off, *tps_start, *tps_end;             /* ... their seq ranges */
+    const uint64_t *on_off, *on_start, *on_end;                /* self.need[a] */
+    const uint64_t *op_off, *op_ver;                           /* self.partial_need[a] keys */
+    const uint64_t *ops_off, *ops_start, *ops_end;             /* ... our seq ranges */
+} corro_sync_entries;
+
+/* Output CSR of HashMap<ActorId, Vec<SyncNeedV1>> (sync.rs:252-264). Two passes:
+ * pass 0 fills need_count/seq_count per entry; the caller scans them into need_off/seq_off
+ * (n+1 entries each) and allocates; pass 1 fills the rest. */
+typedef struct {
+    uint64_t *need_count, *seq_count;       /* pass 0, n each */
+    const uint64_t *need_off, *seq_off;     /* pass 1 inputs, n+1 each */
+    uint8_t *kind;                          /* 0 Full{versions: start..=end}, 1 Partial{version: start} */
+    uint64_t *start, *end;
+    uint64_t *sr_off, *sr_n;                /* Partial seq ranges: [sr_off, sr_off+sr_n) */
+    uint64_t *s_start, *s_end;
+} corro_needs_out;
+
+/* mem = CORRO_MEM_HOST or CORRO_MEM_DEVICE for BOTH `in` arrays and `out` arrays. */
+int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in, int mem,
+                        corro_needs_out *out, int pass);
+
+/* ------------------------------------------------------------------ gap bookkeeping */
+
+/* BookedVersions (agent.rs:1260-1458): needed gaps, max, partials' presence. Host-side. */
+typedef struct corro_booked corro_booked;
+int corro_booked_new(corro_booked **out);
+void corro_booked_free(corro_booked *b);
+/* VersionsSnapshot::insert_db with `n` applied version ranges. Returns the gap rows to DELETE
+ * (removed) and INSERT (inserted) in __corro_bookkeeping_gaps (agent.rs:1120-1163); pass NULL
+ * buffers with caps 0 to only apply. *n_removed / *n_inserted receive the full counts. */
+int corro_booked_insert_db(corro_booked *b, const uint64_t *start, const uint64_t *end, uint64_t n,
+                           uint64_t *rm_start, uint64_t *rm_end, uint64_t rm_cap, uint64_t *n_removed,
+                           uint64_t *in_start, uint64_t *in_end, uint64_t in_cap, uint64_t *n_inserted);
+int corro_booked_needed(corro_booked *b, uint64_t *start, uint64_t *end, uint64_t cap, uint64_t *count);
+int corro_booked_last(corro_booked *b, int64_t *max);     /* -1 = None */
+int corro_booked_contains(corro_booked *b, uint64_t version, int *result);
+int corro_booked_contains_all(corro_booked *b, uint64_t start, uint64_t end, int *result);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CORRO_HIP_H */

@@ -1,0 +1,157 @@
+"""Seeded synthetic changesets for the BASELINE.json configs (SURVEY.md §8(d) "Concrete inputs").
+
+All batches are SoA dicts in application order (actors ascending by 16-byte id, then version, then
+seq — util.rs:705,765,782,1222). numpy variants feed tests and the CPU baseline; the torch variant
+builds config 2 directly in HBM for bench.py.
+"""
+import numpy as np
+
+MASK64 = (1 << 64) - 1
+
+
+def splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & MASK64
+    z = x
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+    return z ^ (z >> 31)
+
+
+def config_seed(cfg):
+    return splitmix64(0xC0DE0000 + cfg)
+
+
+def site_ids(n, seed):
+    """n distinct random 16-byte actor ids, sorted ascending (ordinal == rank)."""
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    ids = np.unique(ids, axis=0)
+    while ids.shape[0] < n:
+        extra = rng.integers(0, 256, size=(n - ids.shape[0], 16), dtype=np.uint8)
+        ids = np.unique(np.concatenate([ids, extra]), axis=0)
+    return ids[:n]
+
+
+def uniform_batch(n, nactors, npk, ncols, seed, cv_max=8, tie_frac=0.125, per_version=64, table=0,
+                  pk_base=1):
+    """Config 1/2 shape: cl = 1, INTEGER values, pk uniform in [pk_base, pk_base+npk)."""
+    rng = np.random.default_rng(seed)
+    per_actor = -(-n // nactors)
+    i = np.arange(n, dtype=np.int64)
+    site = (i // per_actor).astype(np.uint32)
+    local = i % per_actor
+    dbv = (local // per_version + 1).astype(np.int64)
+    seq = (local % per_version).astype(np.uint32)
+    pk = (rng.integers(0, npk, size=n, dtype=np.int64) + pk_base).astype(np.uint64)
+    cid = rng.integers(1, ncols + 1, size=n, dtype=np.int64)
+    tcid = ((table << 16) | cid).astype(np.uint32)
+    cv = rng.integers(1, cv_max + 1, size=n, dtype=np.int64)
+    val = rng.integers(-(1 << 62), 1 << 62, size=n, dtype=np.int64)
+    ties = rng.random(n) < tie_frac
+    val[ties] = rng.integers(0, 8, size=int(ties.sum()), dtype=np.int64)
+    return {"pk": pk, "table_cid": tcid, "col_version": cv, "db_version": dbv,
+            "cl": np.ones(n, np.uint32), "seq": seq, "site": site, "val0": val.view(np.uint64)}
+
+
+def _zipf_pk(rng, n, npk, s):
+    # bounded Zipf over [1, npk] by inverse CDF on a table
+    ranks = np.arange(1, npk + 1, dtype=np.float64)
+    w = ranks ** (-s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    u = rng.random(n)
+    return (np.searchsorted(cdf, u) + 1).astype(np.uint64)
+
+
+def adversarial_batch(n, nactors, ntables, npk, seed, zipf=1.1, sentinel_frac=0.3, wide=True,
+                      malformed=False, per_version=50, max_cl=6):
+    """Config 5 shape (scaled): Zipf pks, deletes/resurrects, mixed INTEGER + 16-byte BLOB columns.
+
+    Schema per table: (id INTEGER PK, i0 INTEGER, i1 INTEGER, b0 BLOB, b1 BLOB) -> cids 1..4.
+    Well-formed unless malformed=True: sentinel changes carry col_version == cl and
+    NULL; column changes carry odd cl. With wide=True some values are REAL/TEXT/NULL too."""
+    rng = np.random.default_rng(seed)
+    per_actor = -(-n // nactors)
+    i = np.arange(n, dtype=np.int64)
+    site = (i // per_actor).astype(np.uint32)
+    local = i % per_actor
+    dbv = (local // per_version + 1).astype(np.int64)
+    seq = (local % per_version).astype(np.uint32)
+    table = rng.integers(0, ntables, size=n, dtype=np.int64)
+    pk = _zipf_pk(rng, n, npk, zipf) if zipf else rng.integers(1, npk + 1, size=n).astype(np.uint64)
+    sent = rng.random(n) < sentinel_frac
+    cid = np.where(sent, 0, rng.integers(1, 5, size=n, dtype=np.int64))
+    cl = rng.integers(1, max_cl + 1, size=n, dtype=np.int64)
+    if not malformed:
+        cl = np.where(sent, cl, cl | 1)  # column changes: odd causal length
+    cv = rng.integers(1, 6, size=n, dtype=np.int64)
+    if not malformed:
+        cv = np.where(sent, cl, cv)
+    vt = np.full(n, 1, np.uint8)
+    v0 = rng.integers(-(1 << 62), 1 << 62, size=n, dtype=np.int64).view(np.uint64)
+    ties = rng.random(n) < 0.3
+    v0[ties] = rng.integers(0, 4, size=int(ties.sum())).astype(np.uint64)
+    v1 = np.zeros(n, np.uint64)
+    vl = np.zeros(n, np.uint8)
+    blob = (cid == 3) | (cid == 4)
+    vt[blob] = 4
+    vl[blob] = 16
+    v1[blob] = rng.integers(0, 1 << 63, size=int(blob.sum()), dtype=np.int64).astype(np.uint64)
+    bt = blob & (rng.random(n) < 0.3)
+    v1[bt] = rng.integers(0, 3, size=int(bt.sum())).astype(np.uint64)
+    v0[bt] = rng.integers(0, 3, size=int(bt.sum())).astype(np.uint64)
+    if wide:
+        r = rng.random(n)
+        real = (~blob) & (r < 0.1)
+        vt[real] = 2
+        v0[real] = rng.choice(np.array([0.0, -0.0, 1.5, -2.25, 5.0], np.float64), size=int(real.sum())).view(np.uint64)
+        text = (~blob) & (r >= 0.1) & (r < 0.2)
+        vt[text] = 3
+        lens = rng.integers(0, 17, size=int(text.sum()))
+        vl[text] = lens
+        raw = rng.integers(97, 100, size=(int(text.sum()), 16), dtype=np.uint8)
+        for k in range(raw.shape[0]):
+            raw[k, lens[k]:] = 0
+        v0[text] = raw[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+        v1[text] = raw[:, 8:].copy().view(">u8").reshape(-1).astype(np.uint64)
+        nul = (~blob) & (r >= 0.2) & (r < 0.25)
+        vt[nul] = 5
+        v0[nul] = 0
+    vt[sent] = 5
+    v0[sent] = 0
+    v1[sent] = 0
+    vl[sent] = 0
+    tcid = ((table << 16) | cid).astype(np.uint32)
+    return {"pk": pk, "table_cid": tcid, "col_version": cv.astype(np.int64), "db_version": dbv,
+            "cl": cl.astype(np.uint32), "seq": seq, "site": site, "val0": v0, "val1": v1,
+            "val_type": vt, "val_len": vl, "ts": (dbv.astype(np.uint64) << np.uint64(20)) + site.astype(np.uint64)}
+
+
+ADV_COLS = ["i0", "i1", "b0", "b1"]
+
+
+def adversarial_schema(ntables):
+    return {f"t{k}": list(ADV_COLS) for k in range(ntables)}
+
+
+def uniform_batch_torch(n, nactors, npk, ncols, seed, device="cuda", cv_max=8, per_version=64):
+    """Config 2 generated in HBM (torch), same distribution as uniform_batch."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
+    per_actor = -(-n // nactors)
+    i = torch.arange(n, device=device, dtype=torch.int64)
+    site = (i // per_actor).to(torch.int32)
+    local = i % per_actor
+    dbv = local // per_version + 1
+    seq = (local % per_version).to(torch.int32)
+    pk = torch.randint(0, npk, (n,), device=device, generator=g, dtype=torch.int64) + 1
+    cid = torch.randint(1, ncols + 1, (n,), device=device, generator=g, dtype=torch.int64)
+    cv = torch.randint(1, cv_max + 1, (n,), device=device, generator=g, dtype=torch.int64)
+    val = torch.randint(-(1 << 62), 1 << 62, (n,), device=device, generator=g, dtype=torch.int64)
+    ties = torch.rand(n, device=device, generator=g) < 0.125
+    small = torch.randint(0, 8, (n,), device=device, generator=g, dtype=torch.int64)
+    val = torch.where(ties, small, val)
+    return {"pk": pk.contiguous(), "table_cid": cid.to(torch.int32).contiguous(), "col_version": cv.contiguous(),
+            "db_version": dbv.contiguous(), "cl": torch.ones(n, device=device, dtype=torch.int32),
+            "seq": seq.contiguous(), "site": site.contiguous(), "val0": val.contiguous()}

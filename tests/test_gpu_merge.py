@@ -1,0 +1,193 @@
+"""GPU parity of the batched merge (libcorro_hip.so through the C ABI) against the CPU oracle
+restatement of cr-sqlite's crsql_changes INSERT (oracle/crsql_fold.c) and the golden KATs.
+Bar: bit-exact crsql_changes rows, impacts and crsql_db_versions."""
+import numpy as np
+import pytest
+
+import synth
+from oracle import oracle as O
+from tests._util import batch_from_changes, expected_rows, load_golden, rows_to_tuples, site_table
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA_T = {"t": ["a", "b", "c"]}
+MERGE = load_golden("merge_kats.json")
+
+
+def engine(schema, cap=1 << 16, sites=None):
+    import corrosion_amd as ca
+    e = ca.MergeEngine(schema, capacity_hint=cap)
+    e.register_sites(site_table() if sites is None else sites)
+    return e
+
+
+def compare(eng, fold, with_ts=False):
+    got = rows_to_tuples(eng.export(), with_ts=with_ts)
+    exp = rows_to_tuples(fold.export(), with_ts=with_ts)
+    assert len(got) == len(exp)
+    assert got == exp
+    nd = fold.nsites
+    assert list(eng.db_versions()[:nd]) == list(fold.db_versions())
+
+
+@pytest.mark.parametrize("case", MERGE["cases"], ids=[c["name"][:3] for c in MERGE["cases"]])
+def test_kats_gpu(case):
+    e = engine(SCHEMA_T)
+    imp = e.apply(batch_from_changes(case["changes"]), impact=True)
+    got = [t[:11] for t in rows_to_tuples(e.export())]
+    assert got == expected_rows(case["rows"])
+    assert list(np.cumsum(imp)) == case["impacted"]
+
+
+@pytest.mark.parametrize("case", MERGE["cases"], ids=[c["name"][:3] for c in MERGE["cases"]])
+def test_kats_gpu_one_change_per_batch(case):
+    """Folding batch-by-batch equals one batch (state is the prefix of application order)."""
+    e = engine(SCHEMA_T)
+    b = batch_from_changes(case["changes"])
+    for i in range(len(b["pk"])):
+        e.apply({k: v[i:i + 1] for k, v in b.items()})
+    assert [t[:11] for t in rows_to_tuples(e.export())] == expected_rows(case["rows"])
+
+
+def test_kats_gpu_no_impact_path():
+    """Without impact output the fast/general split is used; results identical."""
+    for case in MERGE["cases"]:
+        e = engine(SCHEMA_T)
+        e.apply(batch_from_changes(case["changes"]))
+        assert [t[:11] for t in rows_to_tuples(e.export())] == expected_rows(case["rows"]), case["name"]
+
+
+def test_db_versions_gpu():
+    c = MERGE["db_versions_case"]
+    e = engine(SCHEMA_T)
+    e.apply(batch_from_changes(c["changes"]))
+    dv = e.db_versions()
+    for site, v in c["db_versions"].items():
+        assert dv[int(site)] == v
+    assert dv[0] == -1
+
+
+@pytest.mark.parametrize("n,npk,seed", [(1000, 50, 1), (20000, 3000, 2), (200000, 40000, 3)])
+def test_uniform_cl1_vs_oracle(n, npk, seed):
+    sites = synth.site_ids(16, seed)
+    b = synth.uniform_batch(n, 16, npk, 4, seed)
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=n, sites=sites)
+    f = O.Fold(sites)
+    e.apply(b)
+    f.apply(b)
+    compare(e, f)
+
+
+@pytest.mark.parametrize("malformed", [False, True])
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_adversarial_vs_oracle(seed, malformed):
+    sites = synth.site_ids(8, seed)
+    b = synth.adversarial_batch(30000, 8, 3, 400, seed, malformed=malformed)
+    e = engine(synth.adversarial_schema(3), cap=30000, sites=sites)
+    f = O.Fold(sites)
+    imp_e = e.apply(b, impact=True)
+    imp_f = f.apply(b)
+    compare(e, f, with_ts=True)
+    assert np.array_equal(imp_e, imp_f)
+
+
+def test_adversarial_multi_batch_fold():
+    """Several batches in sequence (prior state as prefix), with and without impact output."""
+    seed = 21
+    sites = synth.site_ids(8, seed)
+    e = engine(synth.adversarial_schema(2), cap=20000, sites=sites)
+    f = O.Fold(sites)
+    for k in range(6):
+        b = synth.adversarial_batch(5000, 8, 2, 300, seed + k)
+        if k % 2:
+            assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+        else:
+            e.apply(b)
+            f.apply(b)
+        compare(e, f, with_ts=True)
+
+
+def test_mixed_cl1_then_adversarial():
+    """Fast-path state (cl=1 rows) then deletes/resurrects on the same rows."""
+    seed = 31
+    sites = synth.site_ids(8, seed)
+    e = engine(synth.adversarial_schema(1), cap=50000, sites=sites)
+    f = O.Fold(sites)
+    b1 = synth.uniform_batch(40000, 8, 2000, 4, seed)
+    b1["table_cid"] = (b1["table_cid"] & 0xFFFF).astype(np.uint32)
+    e.apply(b1)
+    f.apply(b1)
+    compare(e, f)
+    b2 = synth.adversarial_batch(20000, 8, 1, 2000, seed + 1, zipf=0, wide=False)
+    e.apply(b2)
+    f.apply(b2)
+    compare(e, f, with_ts=False)
+
+
+def test_hot_rows_overflow_buckets():
+    """Zipf-hot rows make buckets larger than LDS: the global-scratch path must agree."""
+    seed = 41
+    sites = synth.site_ids(8, seed)
+    b = synth.adversarial_batch(60000, 8, 1, 50, seed, zipf=1.1)
+    e = engine(synth.adversarial_schema(1), cap=64, sites=sites)  # tiny bucket table
+    f = O.Fold(sites)
+    assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+    compare(e, f, with_ts=True)
+
+
+def test_fast_path_overflow_cl1():
+    seed = 42
+    sites = synth.site_ids(4, seed)
+    b = synth.uniform_batch(50000, 4, 20000, 3, seed)
+    e = engine(SCHEMA_T, cap=64, sites=sites)
+    f = O.Fold(sites)
+    e.apply(b)
+    f.apply(b)
+    compare(e, f)
+
+
+def test_device_resident_batch():
+    import torch
+    seed = 51
+    sites = synth.site_ids(16, seed)
+    b = synth.uniform_batch(100000, 16, 10000, 4, seed)
+    dev = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                               (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda() for k, v in b.items()}
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=100000, sites=sites)
+    f = O.Fold(sites)
+    e.apply(dev)
+    f.apply(b)
+    compare(e, f)
+
+
+def test_reset_and_reapply():
+    seed = 61
+    sites = synth.site_ids(4, seed)
+    b = synth.uniform_batch(10000, 4, 1000, 3, seed)
+    e = engine(SCHEMA_T, cap=10000, sites=sites)
+    e.apply(b)
+    first = rows_to_tuples(e.export())
+    e.reset()
+    assert e.count() == 0
+    e.apply(b)
+    assert rows_to_tuples(e.export()) == first
+
+
+def test_errors_leave_state_untouched():
+    import corrosion_amd as ca
+    e = engine(SCHEMA_T)
+    b = batch_from_changes([[1, {"t": "int", "v": 5}, 1, 7, 1, 1]])
+    e.apply(b)
+    before = rows_to_tuples(e.export())
+    bad = batch_from_changes([[7, {"t": "int", "v": 5}, 2, 8, 1, 1]])  # cid 7 does not exist
+    with pytest.raises(ca.CorroError) as ex:
+        e.apply(bad)
+    assert ex.value.code == -5
+    assert rows_to_tuples(e.export()) == before
+    bad = batch_from_changes([[1, {"t": "int", "v": 5}, 2, 8, 99, 1]])  # unknown site ordinal
+    with pytest.raises(ca.CorroError):
+        e.apply(bad)
+    assert rows_to_tuples(e.export()) == before
+    assert e.lookup("t", "b") == 2 and e.lookup("t", "-1") == 0
+    with pytest.raises(ca.CorroError):
+        e.lookup("t", "zz")

@@ -1,0 +1,67 @@
+"""GPU parity of the batched need diff (k_needs via corro_compute_needs) against the oracle and
+the reference's own test_compute_available_needs assertions (sync.rs:386-500)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests._util import load_golden
+from tests.sync_util import decode_needs, entries_from_pairs, kat_expect
+
+pytestmark = pytest.mark.gpu
+SYNC = load_golden("sync_kats.json")
+
+
+def _engine():
+    import corrosion_amd as ca
+    return ca.MergeEngine({"t": ["a"]}, capacity_hint=1024)
+
+
+@pytest.mark.parametrize("case", SYNC["cases"], ids=[c["name"] for c in SYNC["cases"]])
+def test_sync_kats_gpu(case):
+    e = _engine()
+    ent = entries_from_pairs([(case["our"], case["their"])])
+    assert decode_needs(e.compute_needs(ent), 1)[0] == kat_expect(case["expect"])
+
+
+def test_sync_state_api_gpu():
+    import corrosion_amd as ca
+    e = _engine()
+    a1 = b"\x01" * 16
+    ours = ca.SyncStateV1(actor_id=b"\x00" * 16, heads={a1: 10}, need={a1: [(2, 5), (7, 7)]},
+                          partial_need={a1: {9: [(100, 120), (130, 132)]}})
+    theirs = ca.SyncStateV1(actor_id=b"\x02" * 16, heads={a1: 13, b"\x00" * 16: 4},
+                            partial_need={a1: {9: [(100, 110), (130, 130)]}})
+    got = ours.compute_available_needs(theirs, e)
+    assert got == {a1: [ca.Full(2, 5), ca.Full(7, 7), ca.Partial(9, ((111, 120), (131, 132))), ca.Full(11, 13)]}
+
+
+def random_side(rng, with_head=True):
+    head = int(rng.integers(1, 200))
+    need, x = [], 1
+    for _ in range(int(rng.poisson(2))):
+        s = x + int(rng.integers(1, 30))
+        e = s + int(rng.geometric(0.1))
+        need.append([s, e])
+        x = e + 2
+    partials = {}
+    for _ in range(int(rng.integers(0, 3))):
+        v = int(rng.integers(1, head + 10))
+        rs, y = [], int(rng.integers(0, 5))
+        for _ in range(int(rng.integers(0, 4))):
+            a = y + int(rng.integers(0, 20))
+            b = a + int(rng.integers(0, 20))
+            rs.append([a, b])
+            y = b + 2
+        partials[str(v)] = rs
+    return {"head": head if with_head else None, "need": need, "partials": partials}
+
+
+def test_sync_random_vs_oracle():
+    rng = np.random.default_rng(5)
+    pairs = [(random_side(rng, with_head=rng.random() < 0.9), random_side(rng)) for _ in range(5000)]
+    ent = entries_from_pairs(pairs)
+    e = _engine()
+    got = e.compute_needs(ent)
+    exp = O.needs(ent)
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        assert np.array_equal(got[k], exp[k]), k
