@@ -357,7 +357,6 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_dbv_batch.p, 0, (size_t)nsites * 8, s));
     if (out && out->impact) CORRO_HIP_TRY(hipMemsetAsync(ctx->d_impact.p, 0, n, s));
 
-    const DevBuf &d_ncols = ctx->d_ncols;
     unsigned long long *misc = ctx->d_misc.as<unsigned long long>();
     const bool prof = ctx->profiling;
     auto mark = [&](int i) {
@@ -365,11 +364,8 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     };
     for (float &m : ctx->last_ms) m = 0.f;
     mark(0);
-    const size_t hist_lds = (size_t)B * 4 + (size_t)((B + 31) / 32) * 4;
-    hipLaunchKernelGGL(k_hist, dim3(ntiles), dim3(HIST_THREADS), hist_lds, s, bd, tile, log2B,
-                       ctx->d_hist.as<uint32_t>(), ctx->d_bflags.as<uint32_t>(),
-                       ctx->d_dbv_batch.as<unsigned long long>(), nsites, d_ncols.as<uint16_t>(),
-                       (uint32_t)ctx->tables.size(), misc);
+    hipLaunchKernelGGL(k_hist, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B,
+                       ctx->d_hist.as<uint32_t>());
     CORRO_HIP_TRY(hipGetLastError());
     mark(1);
     hipLaunchKernelGGL(k_colscan, dim3((B + 255) / 256), dim3(256), 0, s, ctx->d_hist.as<uint32_t>(), ntiles, B,
@@ -379,8 +375,10 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
                        ctx->d_state_cnt.as<uint32_t>(), B, ctx->d_stage_off.as<uint32_t>(),
                        ctx->d_out_off.as<uint64_t>());
     mark(3);
-    hipLaunchKernelGGL(k_scatter, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B,
-                       ctx->d_hist.as<uint32_t>(), ctx->d_stage_off.as<uint32_t>(), ctx->d_stage.as<Rec>());
+    hipLaunchKernelGGL(k_scatter, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4 + ((B + 31) / 32) * 4, s, bd, tile,
+                       log2B, ctx->d_hist.as<uint32_t>(), ctx->d_stage_off.as<uint32_t>(), ctx->d_stage.as<Rec>(),
+                       ctx->d_bflags.as<uint32_t>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites,
+                       ctx->d_ncols.as<uint16_t>(), (uint32_t)ctx->tables.size(), misc);
     CORRO_HIP_TRY(hipGetLastError());
     mark(4);
 
@@ -407,6 +405,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     a.ovf_list = ctx->d_ovf_list.as<uint32_t>();
     a.force_general = (out && out->impact) ? 1u : 0u;
     a.track_ts = ctx->track_ts ? 1u : 0u;
+    a.state_wide = ctx->state_wide ? 1u : 0u;
     hipLaunchKernelGGL(k_merge, dim3(B), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
     mark(5);
@@ -452,6 +451,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     std::swap(ctx->d_state_flags, ctx->d_out_flags);
     ctx->cur = nxt;
     ctx->state_total = ctx->h_misc[2];
+    if (ctx->h_misc[3]) ctx->state_wide = true;
     return CORRO_OK;
 }
 

@@ -83,6 +83,7 @@ struct corro_ctx {
     int cur = 0;
     uint64_t state_total = 0;     // clock rows in the current state
     bool track_ts = false;
+    bool state_wide = false;      // some clock row holds a non-INTEGER value
 
     // per-batch scratch
     corro::DevBuf d_in;           // staged device copy of a host batch

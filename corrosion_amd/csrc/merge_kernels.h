@@ -2,13 +2,14 @@
 // process_complete_version, /root/reference/crates/corro-agent/src/agent/util.rs:1222-1262).
 //
 // Pipeline for one batch of N column changes:
-//   k_hist     tile-local LDS histogram of the (table, pk) bucket of every change; one coalesced
-//              row of counts per tile (no global atomics); per-site crsql_db_versions maxima;
-//              input validation (unknown cid / site, out-of-range encodings).
+//   k_hist     tile-local LDS histogram of the (table, pk) bucket of every change (reads pk and
+//              table_cid only); one coalesced row of counts per tile (no global atomics).
 //   k_colscan  per bucket, exclusive prefix over tiles -> each tile owns a disjoint slice of the
 //              bucket (deterministic slices, no atomics).
 //   k_plan     one workgroup: bucket slice offsets for the staged batch and the next state.
-//   k_scatter  re-read the SoA batch, stage each change as one 64-B record in its bucket slice.
+//   k_scatter  re-read the SoA batch, stage each change as one 64-B record in its bucket slice;
+//              per-bucket "general" bits, per-site crsql_db_versions maxima, input validation
+//              (unknown cid / site, out-of-range encodings).
 //   k_merge    one workgroup per bucket: prior clock rows of the bucket (as a prefix of the
 //              application order) + its staged changes ->
 //                fast body  (all rows cl = 1, no sentinels): per-cell argmax of
@@ -24,8 +25,8 @@ namespace corro {
 
 constexpr int HIST_THREADS = 512;
 constexpr int MERGE_THREADS = 512;
-constexpr int FAST_R = 5;                              // records per thread, fast body
-constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 2560
+constexpr int FAST_R = 7;                              // records per thread, fast body
+constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 3584
 constexpr int FAST_SLOTS = 8192;                       // pow2 >= 2 * CAP_FAST
 constexpr int CAP_GEN = 2048;                          // records, general body in LDS
 constexpr int GEN_SLOTS = 4096;
@@ -70,6 +71,7 @@ struct MergeArgs {
     uint32_t *ovf_list;
     uint32_t force_general;
     uint32_t track_ts;
+    uint32_t state_wide;       // prior state holds non-INTEGER values
 };
 
 // misc[0] error bits
@@ -137,65 +139,20 @@ __device__ inline uint32_t site_rank_of(const MergeArgs &a, uint32_t site) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Tile histogram of row buckets. Reads only pk + table_cid (12 B per change).
 __global__ void __launch_bounds__(HIST_THREADS)
-k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t *__restrict__ hist_out,
-       uint32_t *__restrict__ bflags, unsigned long long *__restrict__ dbv_batch, uint32_t nsites,
-       const uint16_t *__restrict__ ncols, uint32_t ntables, unsigned long long *misc) {
-    extern __shared__ uint32_t sm[];
+k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t *__restrict__ hist_out) {
+    extern __shared__ uint32_t hist[];
     const uint32_t B = 1u << log2B;
-    const uint32_t nfl = (B + 31) / 32;
-    uint32_t *hist = sm;
-    uint32_t *fl = sm + B;
-    for (uint32_t i = threadIdx.x; i < B + nfl; i += blockDim.x) sm[i] = 0;
+    for (uint32_t i = threadIdx.x; i < B; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     const uint32_t begin = blockIdx.x * tile;
     const uint32_t end = min(in.n, begin + tile);
-    uint32_t err = 0, wide = 0;
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t base = begin; base < end; base += blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
-        const bool act = i < end;
-        uint32_t site = 0xFFFFFFFFu;
-        uint64_t dbv = 0;
-        if (act) {
-            const uint64_t pk = in.pk[i];
-            const uint32_t tc = in.tcid[i];
-            const uint32_t cl = in.cl[i];
-            const uint32_t t = tc >> 16, cid = tc & 0xFFFFu;
-            const uint32_t b = bucket_of(t, pk, log2B);
-            atomicAdd(&hist[b], 1u);
-            if (cl != 1u || cid == 0) atomicOr(&fl[b >> 5], 1u << (b & 31));
-            site = in.site[i];
-            dbv = (uint64_t)in.dbv[i];
-            if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
-            if (site >= nsites) err |= ERR_SITE;
-            const int64_t cv = in.cv[i];
-            if ((cid == 0 || (cl & 1u) == 0) && (cv < 0 || cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
-            if ((int64_t)dbv < 0) err |= ERR_RANGE;
-            if (in.vt) {
-                const uint32_t ty = in.vt[i];
-                if (ty < 1 || ty > 5) err |= ERR_VALUE;
-                if (ty != CORRO_INTEGER) wide = 1;
-                if (ty == CORRO_REAL) {
-                    const uint64_t v = in.v0[i];
-                    if (((v >> 52) & 0x7FF) == 0x7FF && (v & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
-                }
-                if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && in.vl && in.vl[i] > 16) err |= ERR_VALUE;
-            }
-        }
-        // crsql_db_versions: one atomic per run of equal (site, db_version) inside the wave
-        const uint32_t psite = __shfl_up(site, 1);
-        const unsigned long long pdbv = __shfl_up((unsigned long long)dbv, 1);
-        if (act && site < nsites && (lane == 0 || psite != site || pdbv != dbv))
-            atomicMax(&dbv_batch[site], (unsigned long long)dbv + 1ULL);
-    }
-    if (err) atomicOr(&misc[0], (unsigned long long)err);
-    if (wide) atomicOr(&misc[3], 1ULL);
+    for (uint32_t i = begin + threadIdx.x; i < end; i += blockDim.x)
+        atomicAdd(&hist[bucket_of(in.tcid[i] >> 16, in.pk[i], log2B)], 1u);
     __syncthreads();
     uint32_t *row = hist_out + (size_t)blockIdx.x * B;
     for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) row[b] = hist[b];
-    for (uint32_t w = threadIdx.x; w < nfl; w += blockDim.x)
-        if (fl[w]) atomicOr(&bflags[w], fl[w]);
 }
 
 // per bucket: exclusive prefix of the tile counts (in place) and the bucket total
@@ -280,35 +237,137 @@ __device__ inline Rec load_rec(const Rec *src) {
     return r;
 }
 
+// Wave-cooperative store of one 64-B record per lane to base[idx] (all 64 lanes must call it).
+// A 4x4 transpose across lanes {l, l+16, l+32, l+48} (v_permlane32_swap + v_permlane16_swap) lets
+// store instruction k write the four 16-B quads of the records of lanes l+16k from four lanes, so
+// every instruction writes 16 whole 64-B records instead of 64 scattered 16-B pieces.
+__device__ inline void swap32(uint32_t &a, uint32_t &b) {
+    auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+}
+__device__ inline void swap16(uint32_t &a, uint32_t &b) {
+    auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+}
+__device__ inline void store_rec_wave(Rec *base, uint32_t idx, const Rec &r, bool valid) {
+    uint4 q[4];
+    const uint4 *src = reinterpret_cast<const uint4 *>(&r);
+    q[0] = src[0];
+    q[1] = src[1];
+    q[2] = src[2];
+    q[3] = src[3];
+    swap32(q[0].x, q[2].x); swap32(q[0].y, q[2].y); swap32(q[0].z, q[2].z); swap32(q[0].w, q[2].w);
+    swap32(q[1].x, q[3].x); swap32(q[1].y, q[3].y); swap32(q[1].z, q[3].z); swap32(q[1].w, q[3].w);
+    swap16(q[0].x, q[1].x); swap16(q[0].y, q[1].y); swap16(q[0].z, q[1].z); swap16(q[0].w, q[1].w);
+    swap16(q[2].x, q[3].x); swap16(q[2].y, q[3].y); swap16(q[2].z, q[3].z); swap16(q[2].w, q[3].w);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = lane >> 4, l = lane & 15;
+    const int v = valid ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int srcl = (int)l + 16 * k;
+        const uint32_t sidx = __shfl(idx, srcl);
+        const int sv = __shfl(v, srcl);
+        if (sv) reinterpret_cast<uint4 *>(base + sidx)[j] = q[k];
+    }
+}
+
+__device__ inline unsigned long long wave_max_u64(unsigned long long x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long y = __shfl_xor(x, d);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+// Stage every change of the tile as one 64-B record in its bucket slice. Also: per-bucket
+// "general" bits (a change with cl != 1 or a sentinel), crsql_db_versions maxima and validation.
 __global__ void __launch_bounds__(HIST_THREADS)
 k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict__ hist_off,
-          const uint32_t *__restrict__ stage_off, Rec *__restrict__ stage) {
+          const uint32_t *__restrict__ stage_off, Rec *__restrict__ stage, uint32_t *__restrict__ bflags,
+          unsigned long long *__restrict__ dbv_batch, uint32_t nsites, const uint16_t *__restrict__ ncols,
+          uint32_t ntables, unsigned long long *misc) {
     extern __shared__ uint32_t cur[];
     const uint32_t B = 1u << log2B;
+    const uint32_t nfl = (B + 31) / 32;
+    uint32_t *fl = cur + B;
     const uint32_t *row = hist_off + (size_t)blockIdx.x * B;
     for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) cur[b] = stage_off[b] + row[b];
+    for (uint32_t w = threadIdx.x; w < nfl; w += blockDim.x) fl[w] = 0;
     __syncthreads();
     const uint32_t begin = blockIdx.x * tile;
     const uint32_t end = min(in.n, begin + tile);
-    for (uint32_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t err = 0, wide = 0;
+    // crsql_db_versions: per-wave run of one site (a tile is a contiguous slice of the application
+    // order, so a wave sees one actor's changesets for long stretches)
+    uint32_t run_site = 0xFFFFFFFFu;
+    unsigned long long run_max = 0;
+    for (uint32_t base = begin; base < end; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const bool act = i < end;
         Rec r;
-        r.pk = in.pk[i];
-        r.cv = in.cv[i];
-        r.dbv = in.dbv[i];
-        r.v0 = in.v0[i];
-        r.v1 = in.v1 ? in.v1[i] : 0ULL;
-        r.tcid = in.tcid[i];
-        r.cl = in.cl[i];
-        r.seq = in.seq[i];
-        r.site = in.site[i];
-        r.pos = BATCH_POS | i;
-        const uint32_t ty = in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER;
-        const uint32_t ln = in.vl ? (uint32_t)in.vl[i] : 0u;
-        r.meta = ty | (ln << 8);
-        const uint32_t b = bucket_of(r.tcid >> 16, r.pk, log2B);
-        const uint32_t idx = atomicAdd(&cur[b], 1u);
-        store_rec(stage + idx, r);
+        r.site = 0xFFFFFFFFu;
+        r.dbv = 0;
+        uint32_t idx = 0;
+        if (act) {
+            r.pk = in.pk[i];
+            r.cv = in.cv[i];
+            r.dbv = in.dbv[i];
+            r.v0 = in.v0[i];
+            r.v1 = in.v1 ? in.v1[i] : 0ULL;
+            r.tcid = in.tcid[i];
+            r.cl = in.cl[i];
+            r.seq = in.seq[i];
+            r.site = in.site[i];
+            r.pos = BATCH_POS | i;
+            const uint32_t ty = in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER;
+            const uint32_t ln = in.vl ? (uint32_t)in.vl[i] : 0u;
+            r.meta = ty | (ln << 8);
+            const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
+            const uint32_t b = bucket_of(t, r.pk, log2B);
+            idx = atomicAdd(&cur[b], 1u);
+            if (r.cl != 1u || cid == 0) atomicOr(&fl[b >> 5], 1u << (b & 31));
+            if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
+            if (r.site >= nsites) err |= ERR_SITE;
+            if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
+            if (r.dbv < 0) err |= ERR_RANGE;
+            if (ty != CORRO_INTEGER) {
+                wide = 1;
+                if (ty < 1 || ty > 5) err |= ERR_VALUE;
+                if (ty == CORRO_REAL && ((r.v0 >> 52) & 0x7FF) == 0x7FF && (r.v0 & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
+                if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) err |= ERR_VALUE;
+            }
+        }
+        store_rec_wave(stage, idx, r, act);
+        // db_versions
+        const uint32_t site0 = __shfl(r.site, 0);
+        const unsigned long long dv = act ? (unsigned long long)r.dbv + 1ULL : 0ULL;
+        if (__all(!act || r.site == site0)) {
+            const unsigned long long m = wave_max_u64(dv);
+            if (site0 == run_site) {
+                run_max = m > run_max ? m : run_max;
+            } else {
+                if (lane == 0 && run_site < nsites) atomicMax(&dbv_batch[run_site], run_max);
+                run_site = site0;
+                run_max = m;
+            }
+        } else {
+            const uint32_t psite = __shfl_up(r.site, 1);
+            const unsigned long long pdv = __shfl_up(dv, 1);
+            if (act && r.site < nsites && (lane == 0 || psite != r.site || pdv != dv))
+                atomicMax(&dbv_batch[r.site], dv);
+        }
     }
+    if (lane == 0 && run_site < nsites) atomicMax(&dbv_batch[run_site], run_max);
+    if (err) atomicOr(&misc[0], (unsigned long long)err);
+    if (wide) atomicOr(&misc[3], 1ULL);
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < nfl; w += blockDim.x)
+        if (fl[w]) atomicOr(&bflags[w], fl[w]);
 }
 
 // ------------------------------------------------------------------------ merge bodies
@@ -649,7 +708,7 @@ k_merge(MergeArgs a) {
         }
         __syncthreads();
         // argmax stages over the key (col_version, value, site rank, -position)
-        const bool wide = a.misc[3] != 0;
+        const bool wide = a.state_wide || a.misc[3] != 0;
         const int nstages = wide ? 6 : 3;
         for (int st = 0; st < nstages; st++) {
             uint64_t *kc = (st & 1) ? s_k1 : s_k0;
@@ -686,14 +745,15 @@ k_merge(MergeArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < FAST_R; k++) {
-            if (!alive[k]) continue;
-            const uint32_t o = atomicAdd(&s_outcnt, 1u);
+            uint32_t o = 0;
             Rec x = r[k];
-            const uint64_t ts = a.track_ts ? rec_ts(a, v, x) : 0ULL;
-            x.cl = 1;
-            x.pos = o;
-            store_rec(outb + o, x);
-            if (a.track_ts) outts[o] = ts;
+            if (alive[k]) {
+                o = atomicAdd(&s_outcnt, 1u);
+                if (a.track_ts) outts[o] = rec_ts(a, v, x);
+                x.cl = 1;
+                x.pos = o;
+            }
+            store_rec_wave(outb, o, x, alive[k]);
         }
     }
     __syncthreads();
