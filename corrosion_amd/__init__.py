@@ -10,3 +10,4 @@ from ._lib import CorroError, device_count, lib  # noqa: F401
 from .bookkeeping import BookedVersions  # noqa: F401
 from .engine import MergeEngine  # noqa: F401
 from .sync import Full, Partial, SyncStateV1, batch_compute_available_needs  # noqa: F401
+from . import agent  # noqa: F401

@@ -24,7 +24,15 @@ EXPORTS = [
     "corro_db_versions", "corro_compute_needs", "corro_booked_new", "corro_booked_free",
     "corro_booked_insert_db", "corro_booked_needed", "corro_booked_last", "corro_booked_contains",
     "corro_booked_contains_all", "corro_ctx_set_profiling", "corro_last_timings",
+    "corro_bookie_new", "corro_bookie_free", "corro_process_multiple_changes",
+    "corro_bookie_take_ready", "corro_process_fully_buffered", "corro_bookie_last",
+    "corro_bookie_needed", "corro_bookie_contains_all", "corro_bookie_partial",
+    "corro_generate_sync",
 ]
+
+CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
+KNOWN = {0: "skipped", 1: "current", 2: "cleared", 3: "partial"}
+CORRO_TCID_UNKNOWN = 0xFFFFFFFF
 
 
 class CorroError(RuntimeError):
@@ -65,6 +73,24 @@ class NeedsOut(C.Structure):
                                           "start", "end", "sr_off", "sr_n", "s_start", "s_end")]
 
 
+class Changeset(C.Structure):
+    _fields_ = [("actor_id", C.c_void_p), ("site", C.c_uint32), ("kind", C.c_uint32),
+                ("version_start", C.c_uint64), ("version_end", C.c_uint64), ("seq_start", C.c_uint64),
+                ("seq_end", C.c_uint64), ("last_seq", C.c_uint64), ("ts", C.c_uint64),
+                ("change_off", C.c_uint64), ("change_count", C.c_uint64)]
+
+
+class ProcessOut(C.Structure):
+    _fields_ = [("known", C.c_void_p), ("impactful", C.c_void_p), ("n_ready", C.c_uint64)]
+
+
+class SyncState(C.Structure):
+    _fields_ = [("n_actors", C.c_uint64), ("n_need", C.c_uint64), ("n_partials", C.c_uint64),
+                ("n_pseqs", C.c_uint64)] + [(k, C.c_void_p) for k in (
+        "actor_ids", "heads", "need_off", "need_start", "need_end", "partial_off", "partial_ver",
+        "pseq_off", "pseq_start", "pseq_end")]
+
+
 _lib = None
 
 
@@ -102,6 +128,16 @@ def lib():
         "corro_booked_contains_all": (i32, [vp, u64, u64, vp]),
         "corro_ctx_set_profiling": (i32, [vp, i32]),
         "corro_last_timings": (i32, [vp, vp, u32, vp]),
+        "corro_bookie_new": (i32, [vp]),
+        "corro_bookie_free": (None, [vp]),
+        "corro_process_multiple_changes": (i32, [vp, vp, vp, u64, C.POINTER(Changes), C.POINTER(ProcessOut)]),
+        "corro_bookie_take_ready": (i32, [vp, vp, vp, u64, vp]),
+        "corro_process_fully_buffered": (i32, [vp, vp, vp, u64, vp]),
+        "corro_bookie_last": (i32, [vp, vp, vp]),
+        "corro_bookie_needed": (i32, [vp, vp, vp, vp, u64, vp]),
+        "corro_bookie_contains_all": (i32, [vp, vp, u64, u64, i32, u64, u64, vp]),
+        "corro_bookie_partial": (i32, [vp, vp, u64, vp, vp, u64, vp, vp]),
+        "corro_generate_sync": (i32, [vp, vp, C.POINTER(SyncState), i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

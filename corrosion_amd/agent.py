@@ -1,0 +1,252 @@
+"""Mirror of corrosion's apply entry points over the device engine.
+
+Types mirror corro-types: `Change` (change.rs:19-30), `ChangeV1` / `Changeset::{Full, Empty,
+EmptySet}` (broadcast.rs:114-148); functions mirror corro-agent/src/agent/util.rs:
+`process_multiple_changes` (:691), `process_fully_buffered_changes` (:541) and corro-types
+`generate_sync` (sync.rs:284). All logic runs in libcorro_hip.so (csrc/agent.cpp + the HIP merge);
+this module converts the Python objects to the C ABI structs and back.
+"""
+import ctypes as C
+import struct
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+from .engine import MergeEngine
+from .sync import SyncStateV1
+
+
+@dataclass
+class Change:
+    table: str
+    pk: int                 # single INTEGER primary key value (row key)
+    cid: str                # column name, "-1" = row sentinel
+    val: object             # None | int | float | str | bytes  (SqliteValue)
+    col_version: int
+    db_version: int
+    seq: int
+    site_id: bytes          # 16 bytes
+    cl: int
+
+
+@dataclass
+class Full:
+    version: int
+    changes: list
+    seqs: tuple             # (start, end) inclusive
+    last_seq: int
+    ts: int = 0
+
+
+@dataclass
+class Empty:
+    versions: tuple         # (start, end) inclusive
+    ts: int = None
+
+
+@dataclass
+class EmptySet:
+    versions: list
+    ts: int = 0
+
+
+@dataclass
+class ChangeV1:
+    actor_id: bytes
+    changeset: object
+
+
+def encode_value(v):
+    """SqliteValue -> (type, val0, val1, len) of the engine's fixed-width value encoding."""
+    if v is None:
+        return L_NULL, 0, 0, 0
+    if isinstance(v, bool) or isinstance(v, int):
+        return 1, int(v) & 0xFFFFFFFFFFFFFFFF, 0, 0
+    if isinstance(v, float):
+        if v != v:
+            return L_NULL, 0, 0, 0  # SQLite binds NaN as NULL
+        return 2, struct.unpack("<Q", struct.pack("<d", v))[0], 0, 0
+    b = v.encode() if isinstance(v, str) else bytes(v)
+    if len(b) > 16:
+        raise L.CorroError(-6, "TEXT/BLOB values longer than 16 bytes are outside the engine encoding")
+    p = b + b"\0" * (16 - len(b))
+    return (3 if isinstance(v, str) else 4), int.from_bytes(p[:8], "big"), int.from_bytes(p[8:], "big"), len(b)
+
+
+L_NULL = 5
+
+
+@dataclass
+class Processed:
+    known: list                               # per ChangeV1: "skipped" | "current" | "cleared" | "partial" | error code
+    impactful: list = field(default_factory=list)  # per ChangeV1: impactful Change list (Full only)
+    ready: list = field(default_factory=list)      # (actor, version) now fully buffered
+
+
+class Bookie:
+    def __init__(self):
+        h = C.c_void_p()
+        L.check(L.lib().corro_bookie_new(C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            L.lib().corro_bookie_free(self._h)
+            self._h = None
+
+    def last(self, actor):
+        v = C.c_int64()
+        L.check(L.lib().corro_bookie_last(self._h, actor, C.byref(v)))
+        return None if v.value < 0 else v.value
+
+    def needed(self, actor):
+        c = C.c_uint64()
+        L.check(L.lib().corro_bookie_needed(self._h, actor, None, None, 0, C.byref(c)))
+        s = np.zeros(max(1, c.value), np.uint64)
+        e = np.zeros(max(1, c.value), np.uint64)
+        L.check(L.lib().corro_bookie_needed(self._h, actor, s.ctypes.data, e.ctypes.data, c.value, C.byref(c)))
+        return [(int(s[i]), int(e[i])) for i in range(c.value)]
+
+    def contains_all(self, actor, versions, seqs=None):
+        r = C.c_int()
+        L.check(L.lib().corro_bookie_contains_all(self._h, actor, versions[0], versions[1], 1 if seqs else 0,
+                                                   seqs[0] if seqs else 0, seqs[1] if seqs else 0, C.byref(r)))
+        return bool(r.value)
+
+    def partial(self, actor, version):
+        """(seq ranges, last_seq) of a partially received version, or None."""
+        c, last = C.c_uint64(), C.c_int64()
+        s = np.zeros(64, np.uint64)
+        e = np.zeros(64, np.uint64)
+        L.check(L.lib().corro_bookie_partial(self._h, actor, version, s.ctypes.data, e.ctypes.data, 64,
+                                             C.byref(c), C.byref(last)))
+        if last.value < 0:
+            return None
+        return [(int(s[i]), int(e[i])) for i in range(min(c.value, 64))], int(last.value)
+
+
+class Agent:
+    """One node's writer: the device merge engine + its Bookie (agent.rs:480-482 single writer)."""
+
+    def __init__(self, schema, capacity_hint=1 << 20, device=0, actor_id=b"\0" * 16):
+        self.engine = MergeEngine(schema, capacity_hint=capacity_hint, device=device)
+        self.bookie = Bookie()
+        self.actor_id = actor_id
+
+    def site(self, site_id):
+        return int(self.engine.register_sites(np.frombuffer(site_id, np.uint8).reshape(1, 16))[0])
+
+    def process_multiple_changes(self, changes):
+        """changes: list of ChangeV1 (or (ChangeV1, source, instant) tuples) in arrival order."""
+        changes = [c[0] if isinstance(c, tuple) else c for c in changes]
+        ncs = len(changes)
+        rows = []
+        descs = (L.Changeset * max(1, ncs))()
+        actor_bufs = []
+        for i, cv1 in enumerate(changes):
+            cs = cv1.changeset
+            d = descs[i]
+            ab = C.create_string_buffer(bytes(cv1.actor_id), 16)
+            actor_bufs.append(ab)
+            d.actor_id = C.addressof(ab)
+            d.site = self.site(cv1.actor_id)
+            d.change_off = len(rows)
+            if isinstance(cs, Full):
+                d.kind = L.CORRO_CS_FULL
+                d.version_start = d.version_end = cs.version
+                d.seq_start, d.seq_end = cs.seqs
+                d.last_seq = cs.last_seq
+                d.ts = cs.ts or 0
+                d.change_count = len(cs.changes)
+                rows.extend(cs.changes)
+            elif isinstance(cs, Empty):
+                d.kind = L.CORRO_CS_EMPTY
+                d.version_start, d.version_end = cs.versions
+                d.ts = cs.ts or 0
+            else:
+                d.kind = L.CORRO_CS_EMPTY_SET
+                d.ts = cs.ts or 0
+        n = len(rows)
+        arr = {k: np.zeros(max(1, n), dt) for k, dt in (
+            ("pk", np.uint64), ("table_cid", np.uint32), ("col_version", np.int64), ("db_version", np.int64),
+            ("cl", np.uint32), ("seq", np.uint32), ("site", np.uint32), ("val0", np.uint64),
+            ("val1", np.uint64), ("val_type", np.uint8), ("val_len", np.uint8))}
+        for j, ch in enumerate(rows):
+            try:
+                tc = self.engine.lookup(ch.table, ch.cid)
+            except L.CorroError:
+                tc = L.CORRO_TCID_UNKNOWN
+            t, v0, v1, ln = encode_value(ch.val)
+            arr["pk"][j] = ch.pk & 0xFFFFFFFFFFFFFFFF
+            arr["table_cid"][j] = tc
+            arr["col_version"][j] = ch.col_version
+            arr["db_version"][j] = ch.db_version
+            arr["cl"][j] = ch.cl
+            arr["seq"][j] = ch.seq
+            arr["site"][j] = self.site(ch.site_id)
+            arr["val0"][j], arr["val1"][j], arr["val_type"][j], arr["val_len"][j] = v0, v1, t, ln
+        s = L.Changes()
+        s.n = n
+        for k, a in arr.items():
+            setattr(s, k, a.ctypes.data)
+        s.ts = None
+        known = np.zeros(max(1, ncs), np.int32)
+        imp = np.zeros(max(1, n), np.uint8)
+        out = L.ProcessOut()
+        out.known = known.ctypes.data
+        out.impactful = imp.ctypes.data
+        L.check(L.lib().corro_process_multiple_changes(self.engine._h, self.bookie._h, descs, ncs, C.byref(s),
+                                                       C.byref(out)))
+        res = Processed(known=[L.KNOWN.get(int(k), int(k)) for k in known[:ncs]])
+        for i, cv1 in enumerate(changes):
+            cs = cv1.changeset
+            if isinstance(cs, Full):
+                off = descs[i].change_off
+                res.impactful.append([c for k, c in enumerate(cs.changes) if imp[off + k]])
+            else:
+                res.impactful.append([])
+        res.ready = self.take_ready()
+        return res
+
+    def take_ready(self):
+        c = C.c_uint64()
+        L.check(L.lib().corro_bookie_take_ready(self.bookie._h, None, None, 0, C.byref(c)))
+        if c.value == 0:
+            return []
+        a = np.zeros((c.value, 16), np.uint8)
+        v = np.zeros(c.value, np.uint64)
+        L.check(L.lib().corro_bookie_take_ready(self.bookie._h, a.ctypes.data, v.ctypes.data, c.value, C.byref(c)))
+        return [(bytes(a[k]), int(v[k])) for k in range(c.value)]
+
+    def process_fully_buffered_changes(self, actor, version):
+        r = C.c_int()
+        L.check(L.lib().corro_process_fully_buffered(self.engine._h, self.bookie._h, actor, version, C.byref(r)))
+        return bool(r.value)
+
+    def generate_sync(self):
+        lib = L.lib()
+        st = L.SyncState()
+        L.check(lib.corro_generate_sync(self.bookie._h, self.actor_id, C.byref(st), 0))
+        na, nn, npr, ns = st.n_actors, st.n_need, st.n_partials, st.n_pseqs
+        bufs = {"actor_ids": np.zeros(max(1, 16 * na), np.uint8), "heads": np.zeros(max(1, na), np.uint64),
+                "need_off": np.zeros(na + 1, np.uint64), "need_start": np.zeros(max(1, nn), np.uint64),
+                "need_end": np.zeros(max(1, nn), np.uint64), "partial_off": np.zeros(na + 1, np.uint64),
+                "partial_ver": np.zeros(max(1, npr), np.uint64), "pseq_off": np.zeros(npr + 1, np.uint64),
+                "pseq_start": np.zeros(max(1, ns), np.uint64), "pseq_end": np.zeros(max(1, ns), np.uint64)}
+        for k, a in bufs.items():
+            setattr(st, k, a.ctypes.data)
+        L.check(lib.corro_generate_sync(self.bookie._h, self.actor_id, C.byref(st), 1))
+        state = SyncStateV1(actor_id=self.actor_id)
+        for i in range(na):
+            a = bytes(bufs["actor_ids"][16 * i:16 * i + 16])
+            state.heads[a] = int(bufs["heads"][i])
+            need = [(int(bufs["need_start"][k]), int(bufs["need_end"][k]))
+                    for k in range(int(bufs["need_off"][i]), int(bufs["need_off"][i + 1]))]
+            if need:
+                state.need[a] = need
+            for p in range(int(bufs["partial_off"][i]), int(bufs["partial_off"][i + 1])):
+                seqs = [(int(bufs["pseq_start"][k]), int(bufs["pseq_end"][k]))
+                        for k in range(int(bufs["pseq_off"][p]), int(bufs["pseq_off"][p + 1]))]
+                state.partial_need.setdefault(a, {})[int(bufs["partial_ver"][p])] = seqs
+        return state

@@ -455,6 +455,26 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     return CORRO_OK;
 }
 
+}  // extern "C"
+
+namespace corro {
+// crsql_set_db_version(site, v) for an empty complete changeset (util.rs:1040-1050)
+int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version) {
+    if (site >= ctx->sites.size()) return fail(CORRO_E_INVALID, "unregistered site ordinal");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    uint64_t cur = 0;
+    uint64_t *p = ctx->d_dbv.as<uint64_t>() + site;
+    CORRO_HIP_TRY(hipMemcpy(&cur, p, 8, hipMemcpyDeviceToHost));
+    if (version + 1 > cur) {
+        const uint64_t nv = version + 1;
+        CORRO_HIP_TRY(hipMemcpy(p, &nv, 8, hipMemcpyHostToDevice));
+    }
+    return CORRO_OK;
+}
+}  // namespace corro
+
+extern "C" {
+
 int corro_ctx_set_profiling(corro_ctx *ctx, int on) {
     if (!ctx) return fail(CORRO_E_INVALID, "NULL argument");
     ctx->profiling = on != 0;

@@ -211,6 +211,76 @@ int corro_booked_last(corro_booked *b, int64_t *max);     /* -1 = None */
 int corro_booked_contains(corro_booked *b, uint64_t version, int *result);
 int corro_booked_contains_all(corro_booked *b, uint64_t start, uint64_t end, int *result);
 
+/* ------------------------------------------------------------------ process_multiple_changes */
+
+/* Bookie (corro-types/src/agent.rs:1546-1598): BookedVersions per actor, plus the buffered
+ * changes / seq bookkeeping of incomplete versions (__corro_buffered_changes,
+ * __corro_seq_bookkeeping, agent.rs:290-322). Host-side. */
+typedef struct corro_bookie corro_bookie;
+
+enum { CORRO_CS_FULL = 0, CORRO_CS_EMPTY = 1, CORRO_CS_EMPTY_SET = 2 };
+/* KnownDbVersion outcome per changeset (agent.rs:1085-1090); negative = corro_status of a
+ * version that was rolled back (its SAVEPOINT, util.rs:839-860) */
+enum { CORRO_KNOWN_SKIPPED = 0, CORRO_KNOWN_CURRENT = 1, CORRO_KNOWN_CLEARED = 2, CORRO_KNOWN_PARTIAL = 3 };
+/* table_cid value a caller uses for a Change whose table/cid did not resolve */
+#define CORRO_TCID_UNKNOWN 0xFFFFFFFFu
+
+/* One ChangeV1 (broadcast.rs:114-148): its actor and changeset header; its changes are
+ * [change_off, change_off + change_count) of the batch arrays. */
+typedef struct {
+    const uint8_t *actor_id;   /* 16 bytes */
+    uint32_t site;             /* site ordinal of actor_id (corro_site_register) */
+    uint32_t kind;             /* CORRO_CS_* */
+    uint64_t version_start;    /* Full: version; Empty: versions.start */
+    uint64_t version_end;      /* Empty: versions.end */
+    uint64_t seq_start, seq_end, last_seq;  /* Full */
+    uint64_t ts;               /* changeset timestamp, bound to each change (util.rs:1244) */
+    uint64_t change_off, change_count;
+} corro_changeset;
+
+typedef struct {
+    int32_t *known;       /* per changeset: CORRO_KNOWN_* or negative status */
+    uint8_t *impactful;   /* optional, per change: kept in Changeset::Full(impactful) */
+    uint64_t n_ready;     /* partial versions that became complete (corro_bookie_take_ready) */
+} corro_process_out;
+
+int corro_bookie_new(corro_bookie **out);
+void corro_bookie_free(corro_bookie *b);
+
+/* process_multiple_changes (corro-agent/src/agent/util.rs:691-1037) for `ncs` ChangeV1 in arrival
+ * order: dedup passes against the bookie, actors in ActorId byte order, empty versions to
+ * crsql_set_db_version, incomplete versions buffered, ONE corro_apply_batch for all complete
+ * versions, impactful changes with the transaction-cumulative crsql_rows_impacted() semantics,
+ * then per-actor gap bookkeeping and partial tracking. `in` holds every change (host arrays);
+ * unresolved names carry table_cid = CORRO_TCID_UNKNOWN. */
+int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
+                                   const corro_changes *in, corro_process_out *out);
+/* (actor, version) pairs whose buffered seqs are complete; cap < count = sizing call */
+int corro_bookie_take_ready(corro_bookie *bk, uint8_t *actors, uint64_t *versions, uint64_t cap, uint64_t *count);
+/* process_fully_buffered_changes (util.rs:541-688) */
+int corro_process_fully_buffered(corro_ctx *ctx, corro_bookie *bk, const uint8_t *actor_id, uint64_t version,
+                                 int *impacted);
+
+int corro_bookie_last(corro_bookie *bk, const uint8_t *actor_id, int64_t *max);
+int corro_bookie_needed(corro_bookie *bk, const uint8_t *actor_id, uint64_t *start, uint64_t *end, uint64_t cap,
+                        uint64_t *count);
+int corro_bookie_contains_all(corro_bookie *bk, const uint8_t *actor_id, uint64_t start, uint64_t end,
+                              int has_seqs, uint64_t seq_start, uint64_t seq_end, int *result);
+int corro_bookie_partial(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t *start,
+                         uint64_t *end, uint64_t cap, uint64_t *count, int64_t *last_seq);
+
+/* generate_sync (corro-types/src/sync.rs:284-333) as CSR over actors with a known head:
+ * heads, needed ranges, and for every non-complete partial the seq gaps over 0..=last_seq. */
+typedef struct {
+    uint64_t n_actors, n_need, n_partials, n_pseqs;    /* pass 0 output */
+    uint8_t *actor_ids;                                /* 16 * n_actors */
+    uint64_t *heads;                                   /* n_actors */
+    uint64_t *need_off, *need_start, *need_end;        /* n_actors + 1, n_need, n_need */
+    uint64_t *partial_off, *partial_ver;               /* n_actors + 1, n_partials */
+    uint64_t *pseq_off, *pseq_start, *pseq_end;        /* n_partials + 1, n_pseqs, n_pseqs */
+} corro_sync_state;
+int corro_generate_sync(corro_bookie *bk, const uint8_t *self_actor, corro_sync_state *out, int pass);
+
 #ifdef __cplusplus
 }
 #endif

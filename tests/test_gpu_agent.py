@@ -1,0 +1,185 @@
+"""process_multiple_changes through the C ABI (csrc/agent.cpp + the HIP merge), restating the
+reference's own apply-path tests:
+  test_process_multiple_changes  corro-agent/src/agent/tests.rs:1001-1182
+  process_failed_changes         corro-agent/src/agent/tests.rs:877-999
+The reference drives real agents; here `Node` plays ta1: versions of 4 column changes
+(table tests3: text, text2, num, num2; tests.rs:1326-1340) read back like get_rows
+(tests.rs:1264-1324): a cleared version is a Full changeset with no changes, seqs 0..=4, last_seq 4.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+COLS = ["text", "text2", "num", "num2"]
+SCHEMA = {"tests": ["text"], "tests3": COLS}
+TA1 = bytes(range(1, 17))
+TA2 = bytes([0xAA] * 16)
+
+
+class Node:
+    """ta1: each insert_rows version writes row id=i of tests3 (4 changes, seq 0..3)."""
+
+    def __init__(self, actor):
+        self.actor = actor
+        self.version = 0
+        self.rows = {}       # version -> list of Change (current clock rows with that db_version)
+        self.cells = {}      # (pk, cid) -> (version, col_version)
+
+    def insert_rows(self, start, n):
+        from corrosion_amd.agent import Change
+        for i in range(start, n + 1):
+            self.version += 1
+            v = self.version
+            for k, c in enumerate(COLS):
+                old = self.cells.get((i, c))
+                cv = 1 if old is None else old[1] + 1
+                if old is not None:
+                    self.rows[old[0]] = [x for x in self.rows[old[0]] if not (x.pk == i and x.cid == c)]
+                self.cells[(i, c)] = (v, cv)
+                val = f"t{i}-{v}"[:16] if k < 2 else i * 1000 + v
+                self.rows.setdefault(v, []).append(
+                    Change("tests3", i, c, val, cv, v, k, self.actor, 1))
+
+    def get_rows(self, spec):
+        from corrosion_amd.agent import ChangeV1, Full
+        out = []
+        for (vs, ve), seqs in spec:
+            for v in range(vs, ve + 1):
+                ch = sorted(self.rows.get(v, []), key=lambda c: c.seq)
+                last = len(ch) - 1 if ch else 4
+                if seqs is not None:
+                    ch = [c for c in ch if seqs[0] <= c.seq <= seqs[1]]
+                    s = seqs
+                else:
+                    s = (0, last)
+                out.append(ChangeV1(self.actor, Full(v, ch, s, last, ts=1000 + v)))
+        return out
+
+
+def agent():
+    import corrosion_amd as ca
+    return ca.agent.Agent(SCHEMA, capacity_hint=1 << 12)
+
+
+def state_rows(a):
+    rows = a.engine.export()
+    return {(int(rows["pk"][i]), int(rows["table_cid"][i]) & 0xFFFF): (int(rows["db_version"][i]), int(rows["site"][i]))
+            for i in range(len(rows["pk"]))}
+
+
+def check(a, complete=(), gap=(), partials=(), cleared=()):
+    bk = a.bookie
+    needed = bk.needed(TA1)
+    for vs, ve in complete:
+        for v in range(vs, ve + 1):
+            assert not any(s <= v <= e for s, e in needed), v
+    for (vs, ve), (ss, se) in partials:
+        for v in range(vs, ve + 1):
+            assert not any(s <= v <= e for s, e in needed), v
+            p = bk.partial(TA1, v)
+            assert p is not None and p[0] == [(ss, se)], (v, p)
+    for vs, ve in gap:
+        assert (vs, ve) in needed, (vs, ve, needed)
+    site = a.site(TA1)
+    st = state_rows(a)
+    for vs, ve in cleared:
+        for v in range(vs, ve + 1):
+            assert not any(d == v and s == site for d, s in st.values()), v
+
+
+def test_process_multiple_changes_reference_sequence():
+    ta1, ta2 = Node(TA1), agent()
+    ta1.insert_rows(1, 50)
+    r = ta2.process_multiple_changes(ta1.get_rows([((1, 5), None)]))
+    assert r.known == ["current"] * 5
+    check(ta2, complete=[(1, 5)])
+    ta2.process_multiple_changes(ta1.get_rows([((9, 10), None)]))
+    check(ta2, gap=[(6, 8)])
+    r = ta2.process_multiple_changes(ta1.get_rows([((20, 20), None), ((15, 16), (0, 0))]))
+    assert r.known == ["current", "partial", "partial"]
+    check(ta2, gap=[(11, 14), (17, 19)], partials=[((15, 16), (0, 0))])
+    ta1.insert_rows(21, 25)  # clears versions 21-25 on ta1 (rewritten as 51-55)
+    r = ta2.process_multiple_changes(ta1.get_rows([((21, 21), None), ((25, 25), None)]))
+    assert r.known == ["cleared", "cleared"]
+    check(ta2, cleared=[(21, 21), (25, 25)])
+    r = ta2.process_multiple_changes(ta1.get_rows([((14, 18), None), ((15, 16), (1, 3)), ((23, 24), None)]))
+    assert r.known == ["current"] * 5 + ["skipped", "skipped", "cleared", "cleared"]
+    check(ta2, complete=[(14, 18), (15, 16)], gap=[(11, 13), (19, 19), (22, 22)], cleared=[(23, 25)])
+    ta2.process_multiple_changes(ta1.get_rows([((6, 8), None), ((11, 19), None), ((22, 22), None)]))
+    check(ta2, complete=[(1, 20)], cleared=[(21, 25)])
+    assert ta2.bookie.needed(TA1) == []
+    assert ta2.bookie.last(TA1) == 25
+    # generate_sync: head 25, nothing needed, complete partials not reported (sync.rs:313-318)
+    st = ta2.generate_sync()
+    assert st.heads == {TA1: 25} and st.need == {} and st.partial_need == {}
+    # every merged cell of rows 1..20 carries ta1's db_version of its last write
+    site = ta2.site(TA1)
+    rows = state_rows(ta2)
+    for pk in range(1, 21):
+        for cid in range(1, 5):
+            assert rows[(pk, cid)] == (ta1.cells[(pk, COLS[cid - 1])][0], site)
+
+
+def test_duplicate_and_known_changesets_are_skipped():
+    ta1, ta2 = Node(TA1), agent()
+    ta1.insert_rows(1, 3)
+    batch = ta1.get_rows([((1, 3), None)])
+    r = ta2.process_multiple_changes(batch + batch)
+    assert r.known == ["current"] * 3 + ["skipped"] * 3
+    r = ta2.process_multiple_changes(batch)
+    assert r.known == ["skipped"] * 3
+
+
+def test_partial_versions_complete_then_apply_buffered():
+    """Incomplete versions are buffered; once every seq is in, process_fully_buffered_changes
+    merges them (util.rs:541-688, :968-1008)."""
+    ta1, ta2 = Node(TA1), agent()
+    ta1.insert_rows(1, 2)
+    r = ta2.process_multiple_changes(ta1.get_rows([((1, 1), (0, 1))]))
+    assert r.known == ["partial"] and r.ready == []
+    assert state_rows(ta2) == {}
+    st = ta2.generate_sync()
+    assert st.partial_need == {TA1: {1: [(2, 3)]}}
+    r = ta2.process_multiple_changes(ta1.get_rows([((1, 1), (2, 3))]))
+    assert r.known == ["partial"] and r.ready == [(TA1, 1)]
+    assert ta2.process_fully_buffered_changes(TA1, 1)
+    rows = state_rows(ta2)
+    assert len(rows) == 4 and all(v[0] == 1 for v in rows.values())
+    assert ta2.bookie.contains_all(TA1, (1, 1), (0, 3))
+
+
+def test_process_failed_changes_rolls_back_only_the_bad_version():
+    """tests.rs:877-999: a changeset with an unknown cid is rolled back; the others apply."""
+    from corrosion_amd.agent import Change, ChangeV1, Full
+    ta2node = Node(TA2)
+    for i in range(1, 6):
+        ta2node.version += 1
+        ta2node.rows[i] = [Change("tests", i, "text", "service-text", 1, i, 0, TA2, 1)]
+    good = ta2node.get_rows([((1, 5), None)])
+    bad_actor = bytes.fromhex("0000000000000000a716446655440000")
+    change6 = Change("tests", 6, "text", "six", 1, 6, 0, bad_actor, 1)
+    bad = Change("tests", 6, "nonexistent", "six", 1, 6, 1, bad_actor, 1)
+    ta1 = agent()
+    r = ta1.process_multiple_changes([ChangeV1(bad_actor, Full(1, [change6, bad], (0, 1), 1))] + good)
+    assert r.known[0] == -5 and r.known[1:] == ["current"] * 5
+    rows = state_rows(ta1)
+    site = ta1.site(TA2)
+    for i in range(1, 6):
+        assert rows[(i, 1)] == (i, site)
+    assert (6, 1) not in rows
+
+
+def test_impactful_changes_follow_cumulative_rows_impacted():
+    """A losing change that starts a version still counts as impactful when earlier versions of
+    the same transaction impacted rows (util.rs:1218-1261 with cumulative crsql_rows_impacted)."""
+    from corrosion_amd.agent import Change, ChangeV1, Full
+    a = agent()
+    A, Bs = bytes([1] * 16), bytes([2] * 16)
+    v1 = ChangeV1(A, Full(1, [Change("tests", 1, "text", "b", 5, 1, 0, A, 1)], (0, 0), 0))
+    v2 = ChangeV1(Bs, Full(1, [Change("tests", 1, "text", "a", 1, 1, 0, Bs, 1),
+                                Change("tests", 1, "text", "a", 1, 1, 1, Bs, 1)], (0, 1), 1))
+    r = a.process_multiple_changes([v1, v2])
+    assert r.known == ["current", "current"]
+    assert len(r.impactful[0]) == 1
+    assert [c.seq for c in r.impactful[1]] == [0]   # first change of v2: cumulative counter > 0
