@@ -406,7 +406,11 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     a.force_general = (out && out->impact) ? 1u : 0u;
     a.track_ts = ctx->track_ts ? 1u : 0u;
     a.state_wide = ctx->state_wide ? 1u : 0u;
-    hipLaunchKernelGGL(k_merge, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_merge_fast<false>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+    CORRO_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_merge_fast<true>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+    CORRO_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_merge_gen, dim3(B), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
     mark(5);
     CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, 4 * 8, hipMemcpyDeviceToHost, s));

@@ -10,13 +10,13 @@
 //   k_scatter  re-read the SoA batch, stage each change as one 64-B record in its bucket slice;
 //              per-bucket "general" bits, per-site crsql_db_versions maxima, input validation
 //              (unknown cid / site, out-of-range encodings).
-//   k_merge    one workgroup per bucket: prior clock rows of the bucket (as a prefix of the
-//              application order) + its staged changes ->
-//                fast body  (all rows cl = 1, no sentinels): per-cell argmax of
-//                           (col_version, value, site_id rank, -position) by LDS 64-bit
-//                           atomic-max stages; order independent (SURVEY App. A.2 reduction).
-//                general    sort by (row, position) in LDS, then one lane per row folds the
-//                           cr-sqlite rules in application order (App. A.1), exactly.
+//   k_merge_fast / k_merge_gen   one workgroup per bucket: prior clock rows of the bucket (as a
+//              prefix of the application order) + its staged changes ->
+//                fast  (all rows cl = 1, no sentinels): per-cell argmax of
+//                      (col_version, value, site_id rank, -position) by LDS 64-bit atomic-max
+//                      stages; order independent (SURVEY App. A.2 reduction). 2 WGs/CU.
+//                gen   sort by (row, position) in LDS, then one lane per row folds the
+//                      cr-sqlite rules in application order (App. A.1), exactly.
 //              Buckets larger than LDS go to k_merge_ovf (same general body on global scratch).
 #pragma once
 #include "internal.h"
@@ -25,9 +25,9 @@ namespace corro {
 
 constexpr int HIST_THREADS = 512;
 constexpr int MERGE_THREADS = 512;
-constexpr int FAST_R = 7;                              // records per thread, fast body
-constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 3584
-constexpr int FAST_SLOTS = 8192;                       // pow2 >= 2 * CAP_FAST
+constexpr int FAST_R = 6;                              // records per thread, fast body
+constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 3072
+constexpr int FAST_SLOTS = 4096;                       // cell table (distinct cells <= records)
 constexpr int CAP_GEN = 2048;                          // records, general body in LDS
 constexpr int GEN_SLOTS = 4096;
 constexpr int OVF_THREADS = 1024;
@@ -605,26 +605,45 @@ __device__ inline uint32_t next_pow2(uint32_t x) {
     return p;
 }
 
-constexpr size_t FAST_LDS = (size_t)CAP_FAST * (8 + 4) + (size_t)FAST_SLOTS * 4 + (size_t)CAP_FAST * 8 * 2;
 constexpr size_t GEN_LDS = (size_t)CAP_GEN * (8 + 8 + 4 + 4 + 4) + (size_t)GEN_SLOTS * 4 +
                            (size_t)CAP_GEN * (8 + 4) + (size_t)CAP_GEN * (4 + 4 + 8);
-constexpr size_t MERGE_LDS = FAST_LDS > GEN_LDS ? FAST_LDS : GEN_LDS;
 
-__global__ void __launch_bounds__(MERGE_THREADS)
-k_merge(MergeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[MERGE_LDS];
-    __shared__ uint32_t s_outcnt, s_flag;
-    const uint32_t b = blockIdx.x;
-    const uint32_t tid = threadIdx.x;
-    BucketView v;
+__device__ inline void bucket_view(const MergeArgs &a, uint32_t b, BucketView &v) {
     v.np = a.prior_cnt[b];
     v.nn = a.new_cnt[b];
     v.prior = a.prior + a.prior_off[b];
     v.fresh = a.stage + a.stage_off[b];
     v.prior_ts = a.prior_ts ? a.prior_ts + a.prior_off[b] : nullptr;
+}
+
+__device__ inline bool bucket_general(const MergeArgs &a, uint32_t b) {
+    return a.force_general || a.prior_flags[b] || ((a.bflags[b >> 5] >> (b & 31)) & 1u);
+}
+
+__device__ inline void push_overflow(const MergeArgs &a, uint32_t b) {
+    const unsigned long long k = atomicAdd(&a.misc[1], 1ULL);
+    a.ovf_list[k] = b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fast body: every row of the bucket has causal length 1 and no sentinel, so the merge is a
+// per-cell argmax of (col_version, value order, site-id rank, -position). Registers keep only the
+// stage keys of FAST_R records per thread; the full 64-B record of each winner is re-read (L2)
+// for the output. LDS: cell keys + one stage array + the open-addressing cell table (76 KB, two
+// workgroups per CU).
+template <bool WIDE>
+__global__ void __launch_bounds__(MERGE_THREADS, 4)
+k_merge_fast(MergeArgs a) {
+    __shared__ uint64_t s_pk[CAP_FAST];
+    __shared__ uint64_t s_k[CAP_FAST];
+    __shared__ uint32_t s_tc[CAP_FAST];
+    __shared__ uint32_t s_own[FAST_SLOTS];
+    __shared__ uint32_t s_outcnt;
+    const uint32_t b = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    BucketView v;
+    bucket_view(a, b, v);
     const uint32_t n = v.np + v.nn;
-    Rec *outb = a.out + a.out_off[b];
-    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
     if (n == 0) {
         if (tid == 0) {
             a.out_cnt[b] = 0;
@@ -632,130 +651,156 @@ k_merge(MergeArgs a) {
         }
         return;
     }
-    const bool general = a.force_general || a.prior_flags[b] || ((a.bflags[b >> 5] >> (b & 31)) & 1u);
-    if ((general && n > (uint32_t)CAP_GEN) || (!general && n > (uint32_t)CAP_FAST)) {
-        if (tid == 0) {
-            const unsigned long long k = atomicAdd(&a.misc[1], 1ULL);
-            a.ovf_list[k] = b;
-        }
+    if (bucket_general(a, b)) return;  // k_merge_gen
+    // two instantiations are launched; the one matching the batch's value classes runs
+    const bool wide = a.state_wide || a.misc[3] != 0;
+    if (wide != WIDE) return;
+    if (n > (uint32_t)CAP_FAST) {
+        if (tid == 0) push_overflow(a, b);
         return;
     }
+    Rec *outb = a.out + a.out_off[b];
+    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], rp[FAST_R];
+    uint32_t meta[FAST_R], cell[FAST_R];
+    bool alive[FAST_R];
+    if (tid == 0) s_outcnt = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        alive[k] = i < n;
+        cell[k] = 0;
+        if (alive[k]) {
+            const Rec r = load_rec(v.at(i));
+            s_pk[i] = r.pk;
+            s_tc[i] = r.tcid;
+            cv[k] = (uint64_t)r.cv ^ 0x8000000000000000ULL;
+            v0[k] = r.v0;
+            v1[k] = WIDE ? r.v1 : 0;
+            meta[k] = WIDE ? r.meta : (uint32_t)CORRO_INTEGER;
+            rp[k] = ((uint64_t)site_rank_of(a, r.site) << 32) | (uint64_t)(~r.pos);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (!alive[k]) continue;
+        const uint64_t pk = s_pk[i];
+        const uint32_t tc = s_tc[i];
+        uint32_t slot = cell_hash(pk, tc) & (FAST_SLOTS - 1);
+        while (true) {
+            const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
+            if (o == 0) {
+                cell[k] = i;
+                s_k[i] = 0;
+                break;
+            }
+            if (s_pk[o - 1] == pk && s_tc[o - 1] == tc) {
+                cell[k] = o - 1;
+                break;
+            }
+            slot = (slot + 1) & (FAST_SLOTS - 1);
+        }
+    }
+    __syncthreads();
+    // argmax stages: INTEGER-only: col_version, value, site|pos. Mixed: + rank, word 1, length.
+    constexpr int nstages = WIDE ? 6 : 3;
+#pragma unroll
+    for (int st = 0; st < nstages; st++) {
+        const int which = WIDE ? st : (st == 0 ? 0 : (st == 1 ? 2 : 5));
+        uint64_t w[FAST_R];
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            w[k] = 0;
+            if (!alive[k]) continue;
+            const uint32_t ty = WIDE ? vtype(meta[k]) : (uint32_t)CORRO_INTEGER;
+            const bool tb = ty == CORRO_TEXT || ty == CORRO_BLOB;
+            switch (which) {
+            case 0: w[k] = cv[k]; break;
+            case 1: w[k] = 5u - ty; break;
+            case 2: w[k] = vkey0(ty, v0[k]); break;
+            case 3: w[k] = tb ? v1[k] : 0; break;
+            case 4: w[k] = tb ? vlen(meta[k]) : 0; break;
+            default: w[k] = rp[k]; break;
+            }
+            atomicMax(reinterpret_cast<unsigned long long *>(&s_k[cell[k]]), (unsigned long long)w[k]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++)
+            if (alive[k]) alive[k] = s_k[cell[k]] == w[k];
+        __syncthreads();
+        if (st + 1 < nstages) {
+#pragma unroll
+            for (int k = 0; k < FAST_R; k++) {
+                const uint32_t i = k * MERGE_THREADS + tid;
+                if (i < n && cell[k] == i) s_k[i] = 0;
+            }
+            __syncthreads();
+        }
+    }
+    // winners: re-read the record, write the clock row (wave-cooperative 64-B stores)
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        uint32_t o = 0;
+        Rec x;
+        if (alive[k]) {
+            x = load_rec(v.at(i));
+            o = atomicAdd(&s_outcnt, 1u);
+            if (a.track_ts) outts[o] = rec_ts(a, v, x);
+            x.cl = 1;
+            x.pos = o;
+        }
+        store_rec_wave(outb, o, x, alive[k]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.out_cnt[b] = s_outcnt;
+        a.out_flags[b] = 0;
+        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+    }
+}
+
+// General body in LDS: sort (row, position), one lane per row folds the cr-sqlite rules.
+__global__ void __launch_bounds__(MERGE_THREADS)
+k_merge_gen(MergeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[GEN_LDS];
+    __shared__ uint32_t s_outcnt, s_flag;
+    const uint32_t b = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    BucketView v;
+    bucket_view(a, b, v);
+    const uint32_t n = v.np + v.nn;
+    if (n == 0 || !bucket_general(a, b)) return;  // k_merge_fast
+    if (n > (uint32_t)CAP_GEN) {
+        if (tid == 0) push_overflow(a, b);
+        return;
+    }
+    Rec *outb = a.out + a.out_off[b];
+    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
     if (tid == 0) {
         s_outcnt = 0;
         s_flag = 0;
     }
-    if (general) {
-        GenArrays g;
-        uint8_t *p = smem;
-        g.pk = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
-        g.cv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
-        g.key = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
-        g.ccv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
-        g.tc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-        g.cl = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-        g.pos = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-        g.val = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-        g.ccid = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-        g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-        g.own = reinterpret_cast<uint32_t *>(p);
-        g.slots = GEN_SLOTS;
-        g.P = next_pow2(n);
-        gen_body(a, v, outb, outts, &s_outcnt, &s_flag, g, false);
-    } else {
-        // ---------------- fast body: every row has causal length 1 and no sentinel ----------------
-        uint8_t *p = smem;
-        uint64_t *s_pk = reinterpret_cast<uint64_t *>(p); p += CAP_FAST * 8;
-        uint64_t *s_k0 = reinterpret_cast<uint64_t *>(p); p += CAP_FAST * 8;
-        uint64_t *s_k1 = reinterpret_cast<uint64_t *>(p); p += CAP_FAST * 8;
-        uint32_t *s_tc = reinterpret_cast<uint32_t *>(p); p += CAP_FAST * 4;
-        uint32_t *s_own = reinterpret_cast<uint32_t *>(p);
-        Rec r[FAST_R];
-        uint32_t cell[FAST_R];
-        bool alive[FAST_R];
-#pragma unroll
-        for (int k = 0; k < FAST_R; k++) {
-            const uint32_t i = k * MERGE_THREADS + tid;
-            alive[k] = i < n;
-            if (alive[k]) {
-                r[k] = load_rec(v.at(i));
-                s_pk[i] = r[k].pk;
-                s_tc[i] = r[k].tcid;
-            }
-        }
-        for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < FAST_R; k++) {
-            const uint32_t i = k * MERGE_THREADS + tid;
-            cell[k] = 0;
-            if (alive[k]) {
-                uint32_t slot = cell_hash(r[k].pk, r[k].tcid) & (FAST_SLOTS - 1);
-                while (true) {
-                    const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
-                    if (o == 0) {
-                        cell[k] = i;
-                        s_k0[i] = 0;
-                        s_k1[i] = 0;
-                        break;
-                    }
-                    if (s_pk[o - 1] == r[k].pk && s_tc[o - 1] == r[k].tcid) {
-                        cell[k] = o - 1;
-                        break;
-                    }
-                    slot = (slot + 1) & (FAST_SLOTS - 1);
-                }
-            }
-        }
-        __syncthreads();
-        // argmax stages over the key (col_version, value, site rank, -position)
-        const bool wide = a.state_wide || a.misc[3] != 0;
-        const int nstages = wide ? 6 : 3;
-        for (int st = 0; st < nstages; st++) {
-            uint64_t *kc = (st & 1) ? s_k1 : s_k0;
-            uint64_t *kn = (st & 1) ? s_k0 : s_k1;
-            uint64_t w[FAST_R];
-#pragma unroll
-            for (int k = 0; k < FAST_R; k++) {
-                w[k] = 0;
-                if (!alive[k]) continue;
-                const uint32_t ty = vtype(r[k].meta);
-                const int which = wide ? st : (st == 0 ? 0 : (st == 1 ? 2 : 5));
-                switch (which) {
-                case 0: w[k] = (uint64_t)r[k].cv ^ 0x8000000000000000ULL; break;
-                case 1: w[k] = 5u - ty; break;
-                case 2: w[k] = vkey0(ty, r[k].v0); break;
-                case 3: w[k] = (ty == CORRO_TEXT || ty == CORRO_BLOB) ? r[k].v1 : 0; break;
-                case 4: w[k] = (ty == CORRO_TEXT || ty == CORRO_BLOB) ? vlen(r[k].meta) : 0; break;
-                default:
-                    w[k] = ((uint64_t)site_rank_of(a, r[k].site) << 32) | (uint64_t)(~r[k].pos);
-                    break;
-                }
-                atomicMax(reinterpret_cast<unsigned long long *>(&kc[cell[k]]), (unsigned long long)w[k]);
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < FAST_R; k++) {
-                const uint32_t i = k * MERGE_THREADS + tid;
-                if (alive[k]) {
-                    alive[k] = kc[cell[k]] == w[k];
-                }
-                if (i < n && cell[k] == i) kn[i] = 0;
-            }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int k = 0; k < FAST_R; k++) {
-            uint32_t o = 0;
-            Rec x = r[k];
-            if (alive[k]) {
-                o = atomicAdd(&s_outcnt, 1u);
-                if (a.track_ts) outts[o] = rec_ts(a, v, x);
-                x.cl = 1;
-                x.pos = o;
-            }
-            store_rec_wave(outb, o, x, alive[k]);
-        }
-    }
+    GenArrays g;
+    uint8_t *p = smem;
+    g.pk = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
+    g.cv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
+    g.key = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
+    g.ccv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
+    g.tc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+    g.cl = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+    g.pos = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+    g.val = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+    g.ccid = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+    g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+    g.own = reinterpret_cast<uint32_t *>(p);
+    g.slots = GEN_SLOTS;
+    g.P = next_pow2(n);
+    gen_body(a, v, outb, outts, &s_outcnt, &s_flag, g, false);
     __syncthreads();
     if (tid == 0) {
         a.out_cnt[b] = s_outcnt;
