@@ -6,9 +6,9 @@ Workload = BASELINE.json configs[1]: 64M (2^26) column changes, 1 table with 4 I
 generated directly in HBM. One step = one `process_multiple_changes`-sized apply of the whole
 batch into an empty state (state reset + corro_apply_batch), inputs already resident in HBM.
 
-Multi-GPU (torchrun): every rank owns a disjoint pk shard of the same size (hash sharding with
-no data-path collective: each row merges independently); weak scaling. The only
-collectives are the timing barriers and the max-over-ranks reduction.
+Multi-GPU (torchrun, one process per GPU): every rank holds 64M changes over the whole pk space;
+one step = stable pk-hash partition by owner rank (HIP) + one all-to-all-v exchange (RCCL over
+xGMI) + the local merge of the owned rows; weak scaling (per-GPU input fixed).
 
 Prints ONE JSON line (rank 0).
 """
@@ -83,15 +83,17 @@ def main():
     eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=n, device=local)
     sites = synth.site_ids(N_ACTORS, 1)
     eng.register_sites(sites)
-    batch = synth.uniform_batch_torch(n, N_ACTORS, N_PK, N_COLS, seed=synth.config_seed(2) + rank, device=dev)
-    # disjoint pk shard per rank (rows merge independently)
-    batch["pk"] += rank * N_PK
+    batch = synth.uniform_batch_torch(n, N_ACTORS, N_PK * world, N_COLS, seed=synth.config_seed(2) + rank, device=dev)
     torch.cuda.synchronize()
     eng.set_profiling(True)
+    from corrosion_amd.dist import distributed_apply
 
     def step():
         eng.reset()
-        eng.apply(batch)
+        if world > 1:
+            distributed_apply(eng, batch)
+        else:
+            eng.apply(batch)
 
     for _ in range(args.warmup):
         step()
@@ -137,8 +139,9 @@ def main():
             "dtype": "int64",
             "data": "synthetic (seeded, generated in HBM)",
             "config": {"workload": "config 2: 64M column-changes, 1 table x 4 INTEGER cols, 1000 actors, "
-                                   "uniform pk in [1,2^22], cl=1, sort-free bucket merge",
-                       "changes_per_gpu": n, "cells_per_gpu": int(cells), "parallelism": f"pk-shard x{world}"},
+                                   "uniform pk in [1,2^22] per GPU, cl=1, bucket merge"
+                                   + ("" if world == 1 else "; + pk-hash partition and RCCL all-to-all per step"),
+                       "changes_per_gpu": n, "cells_per_gpu": int(cells), "parallelism": f"pk-hash x{world}"},
             "roofline": {"bound": "hbm", "kernel": "apply pipeline: " + "+".join(k for k in kern if kern[k] > 0),
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -27,7 +27,7 @@ EXPORTS = [
     "corro_bookie_new", "corro_bookie_free", "corro_process_multiple_changes",
     "corro_bookie_take_ready", "corro_process_fully_buffered", "corro_bookie_last",
     "corro_bookie_needed", "corro_bookie_contains_all", "corro_bookie_partial",
-    "corro_generate_sync",
+    "corro_generate_sync", "corro_partition_ranks",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -138,6 +138,7 @@ def lib():
         "corro_bookie_contains_all": (i32, [vp, vp, u64, u64, i32, u64, u64, vp]),
         "corro_bookie_partial": (i32, [vp, vp, u64, vp, vp, u64, vp, vp]),
         "corro_generate_sync": (i32, [vp, vp, C.POINTER(SyncState), i32]),
+        "corro_partition_ranks": (i32, [vp, C.POINTER(Changes), u32, C.POINTER(Changes), vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

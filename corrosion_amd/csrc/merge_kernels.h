@@ -20,6 +20,7 @@
 //              Buckets larger than LDS go to k_merge_ovf (same general body on global scratch).
 #pragma once
 #include "internal.h"
+#include "rowhash.h"
 
 namespace corro {
 
@@ -31,22 +32,6 @@ constexpr int FAST_SLOTS = 4096;                       // cell table (distinct c
 constexpr int CAP_GEN = 2048;                          // records, general body in LDS
 constexpr int GEN_SLOTS = 4096;
 constexpr int OVF_THREADS = 1024;
-
-struct BatchDev {
-    const uint64_t *pk;
-    const uint32_t *tcid;
-    const int64_t *cv;
-    const int64_t *dbv;
-    const uint32_t *cl;
-    const uint32_t *seq;
-    const uint32_t *site;
-    const uint64_t *v0;
-    const uint64_t *v1;
-    const uint8_t *vt;
-    const uint8_t *vl;
-    const uint64_t *ts;
-    uint32_t n;
-};
 
 struct MergeArgs {
     const Rec *prior;
@@ -76,23 +61,6 @@ struct MergeArgs {
 
 // misc[0] error bits
 constexpr uint32_t ERR_NAME = 1u, ERR_SITE = 2u, ERR_RANGE = 4u, ERR_VALUE = 8u;
-
-__host__ __device__ inline uint64_t mix64(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdULL;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ULL;
-    x ^= x >> 33;
-    return x;
-}
-
-// Bucket of a row (table, pk): the top log2B bits of a 64-bit mix. Rows never straddle buckets, so
-// every causal-length interaction of a row (delete/resurrect zeroing) stays inside one workgroup.
-__host__ __device__ inline uint32_t bucket_of(uint32_t table, uint64_t pk, uint32_t log2B) {
-    if (log2B == 0) return 0;
-    uint64_t h = mix64(pk + 0x9E3779B97F4A7C15ULL * (uint64_t)(table + 1));
-    return (uint32_t)(h >> (64 - log2B));
-}
 
 __device__ inline uint32_t cell_hash(uint64_t pk, uint32_t tcid) {
     return (uint32_t)mix64(pk * 0xD6E8FEB86659FD93ULL + tcid);

@@ -1,0 +1,171 @@
+// pk-hash partition of a change batch across the ranks of one node.
+//
+// Each row (table, pk) is owned by exactly one rank, so after one all-to-all exchange every rank
+// merges its rows independently. The partition is STABLE: a rank receives its changes in the
+// sender's order, and with senders concatenated by rank the application order of the global batch
+// (actors by id, then arrival) is preserved for every row.
+//
+// rank_of(table, pk) uses the LOW 32 bits of the same 64-bit mix whose top bits pick the merge
+// bucket (merge_kernels.h bucket_of), so a rank's rows still spread over all of its buckets.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "internal.h"
+#include "rowhash.h"
+
+namespace corro {
+
+constexpr int PART_THREADS = 256;
+constexpr int PART_MAX_RANKS = 64;
+
+__host__ __device__ inline uint32_t rank_of(uint32_t table, uint64_t pk, uint32_t nranks) {
+    const uint64_t h = mix64(pk + 0x9E3779B97F4A7C15ULL * (uint64_t)(table + 1));
+    return (uint32_t)(h & 0xFFFFFFFFULL) % nranks;
+}
+
+// per tile: count of changes per destination rank
+__global__ void __launch_bounds__(PART_THREADS)
+k_part_count(BatchDev in, uint32_t tile, uint32_t nranks, uint32_t *__restrict__ counts) {
+    __shared__ uint32_t c[PART_MAX_RANKS];
+    for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) c[r] = 0;
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * tile, end = min(in.n, begin + tile);
+    for (uint32_t i = begin + threadIdx.x; i < end; i += blockDim.x)
+        atomicAdd(&c[rank_of(in.tcid[i] >> 16, in.pk[i], nranks)], 1u);
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) counts[(size_t)blockIdx.x * nranks + r] = c[r];
+}
+
+// one workgroup: counts[t][r] -> absolute output position of tile t's first change for rank r;
+// totals[r] = changes for rank r
+__global__ void k_part_scan(uint32_t *__restrict__ counts, uint32_t ntiles, uint32_t nranks,
+                            uint64_t *__restrict__ totals) {
+    __shared__ uint64_t base[PART_MAX_RANKS];
+    if (threadIdx.x < nranks) {
+        const uint32_t r = threadIdx.x;
+        uint64_t run = 0;
+        for (uint32_t t = 0; t < ntiles; t++) {
+            const uint32_t x = counts[(size_t)t * nranks + r];
+            counts[(size_t)t * nranks + r] = (uint32_t)run;
+            run += x;
+        }
+        totals[r] = run;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t run = 0;
+        for (uint32_t r = 0; r < nranks; r++) {
+            base[r] = run;
+            run += totals[r];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nranks)
+        for (uint32_t t = 0; t < ntiles; t++) counts[(size_t)t * nranks + threadIdx.x] += (uint32_t)base[threadIdx.x];
+}
+
+struct BatchOut {
+    uint64_t *pk;
+    uint32_t *tcid;
+    int64_t *cv;
+    int64_t *dbv;
+    uint32_t *cl;
+    uint32_t *seq;
+    uint32_t *site;
+    uint64_t *v0;
+    uint64_t *v1;
+    uint8_t *vt;
+    uint8_t *vl;
+    uint64_t *ts;
+};
+
+// stable scatter: chunks of PART_THREADS changes in order; wave ballots rank lanes per destination
+__global__ void __launch_bounds__(PART_THREADS)
+k_part_scatter(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restrict__ offs, BatchOut o) {
+    __shared__ uint32_t run[PART_MAX_RANKS];
+    __shared__ uint32_t wcnt[PART_THREADS / 64][PART_MAX_RANKS];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) run[r] = offs[(size_t)blockIdx.x * nranks + r];
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * tile, end = min(in.n, begin + tile);
+    const uint64_t lt = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+    for (uint32_t base = begin; base < end; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const bool act = i < end;
+        const uint32_t d = act ? rank_of(in.tcid[i] >> 16, in.pk[i], nranks) : 0xFFFFFFFFu;
+        uint32_t my_rank = 0;
+        for (uint32_t r = 0; r < nranks; r++) {
+            const uint64_t m = __ballot(d == r);
+            if (d == r) my_rank = __popcll(m & lt);
+            if (lane == 0) wcnt[w][r] = __popcll(m);
+        }
+        __syncthreads();
+        uint32_t pos = 0;
+        if (act) {
+            pos = run[d] + my_rank;
+            for (uint32_t ww = 0; ww < w; ww++) pos += wcnt[ww][d];
+            o.pk[pos] = in.pk[i];
+            o.tcid[pos] = in.tcid[i];
+            o.cv[pos] = in.cv[i];
+            o.dbv[pos] = in.dbv[i];
+            o.cl[pos] = in.cl[i];
+            o.seq[pos] = in.seq[i];
+            o.site[pos] = in.site[i];
+            o.v0[pos] = in.v0[i];
+            if (o.v1) o.v1[pos] = in.v1 ? in.v1[i] : 0ULL;
+            if (o.vt) o.vt[pos] = in.vt ? in.vt[i] : (uint8_t)CORRO_INTEGER;
+            if (o.vl) o.vl[pos] = in.vl ? in.vl[i] : 0;
+            if (o.ts) o.ts[pos] = in.ts ? in.ts[i] : 0ULL;
+        }
+        __syncthreads();
+        if (threadIdx.x < nranks) {
+            uint32_t add = 0;
+            for (uint32_t ww = 0; ww < PART_THREADS / 64; ww++) add += wcnt[ww][threadIdx.x];
+            run[threadIdx.x] += add;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace corro
+
+using namespace corro;
+
+extern "C" int corro_partition_ranks(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, corro_changes *out,
+                                     uint64_t *counts) {
+    if (!ctx || !in || !out || !counts) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nranks == 0 || nranks > (uint32_t)PART_MAX_RANKS) return fail(CORRO_E_RANGE, "1..64 ranks");
+    if (in->n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
+    if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
+        !in->val0 || !out->pk || !out->table_cid || !out->col_version || !out->db_version || !out->cl ||
+        !out->seq || !out->site || !out->val0)
+        return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    for (uint32_t r = 0; r < nranks; r++) counts[r] = 0;
+    const uint32_t n = (uint32_t)in->n;
+    if (n == 0) return CORRO_OK;
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    BatchDev bd{in->pk, in->table_cid, in->col_version, in->db_version, in->cl, in->seq, in->site, in->val0,
+                in->val1, in->val_type, in->val_len, in->ts, n};
+    BatchOut bo{const_cast<uint64_t *>(out->pk),     const_cast<uint32_t *>(out->table_cid),
+                const_cast<int64_t *>(out->col_version), const_cast<int64_t *>(out->db_version),
+                const_cast<uint32_t *>(out->cl),     const_cast<uint32_t *>(out->seq),
+                const_cast<uint32_t *>(out->site),   const_cast<uint64_t *>(out->val0),
+                const_cast<uint64_t *>(out->val1),   const_cast<uint8_t *>(out->val_type),
+                const_cast<uint8_t *>(out->val_len), const_cast<uint64_t *>(out->ts)};
+    uint32_t ntiles = std::max<uint32_t>(1, std::min<uint32_t>(2048, (n + 8191) / 8192));
+    uint32_t tile = (n + ntiles - 1) / ntiles;
+    tile = (tile + PART_THREADS - 1) / PART_THREADS * PART_THREADS;
+    ntiles = (n + tile - 1) / tile;
+    if (int rc = ctx->d_part.ensure((size_t)ntiles * nranks * 4 + nranks * 8 + 256)) return rc;
+    uint32_t *d_counts = ctx->d_part.as<uint32_t>();
+    uint64_t *d_tot = reinterpret_cast<uint64_t *>(ctx->d_part.as<uint8_t>() + (((size_t)ntiles * nranks * 4 + 255) / 256) * 256);
+    hipLaunchKernelGGL(k_part_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, d_tot);
+    hipLaunchKernelGGL(k_part_scatter, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts, bo);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipMemcpyAsync(counts, d_tot, nranks * 8ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}

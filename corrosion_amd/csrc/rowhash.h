@@ -1,0 +1,43 @@
+// Shared device-side definitions: the SoA batch view and the row hash that places a row
+// (table, pk) in a merge bucket (top bits) and on an owner rank (low bits).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace corro {
+
+struct BatchDev {
+    const uint64_t *pk;
+    const uint32_t *tcid;
+    const int64_t *cv;
+    const int64_t *dbv;
+    const uint32_t *cl;
+    const uint32_t *seq;
+    const uint32_t *site;
+    const uint64_t *v0;
+    const uint64_t *v1;
+    const uint8_t *vt;
+    const uint8_t *vl;
+    const uint64_t *ts;
+    uint32_t n;
+};
+
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+// Bucket of a row (table, pk): the top log2B bits of a 64-bit mix. Rows never straddle buckets, so
+// every causal-length interaction of a row (delete/resurrect zeroing) stays inside one workgroup.
+__host__ __device__ inline uint32_t bucket_of(uint32_t table, uint64_t pk, uint32_t log2B) {
+    if (log2B == 0) return 0;
+    uint64_t h = mix64(pk + 0x9E3779B97F4A7C15ULL * (uint64_t)(table + 1));
+    return (uint32_t)(h >> (64 - log2B));
+}
+
+}  // namespace corro

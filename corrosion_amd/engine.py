@@ -149,6 +149,31 @@ class MergeEngine:
         names = ["k_hist", "k_colscan", "k_plan", "k_scatter", "k_merge", "k_merge_ovf"]
         return {names[i]: arr[i] for i in range(min(n.value, len(names)))}
 
+    # ---- multi-GPU ingest -----------------------------------------------------------------
+    def partition(self, batch, nranks):
+        """Stable pk-hash partition of a device batch by owner rank (corro_partition_ranks).
+        Returns (partitioned dict of device tensors, per-rank counts list)."""
+        import torch
+        n = int(batch["pk"].shape[0])
+        s, o = L.Changes(), L.Changes()
+        s.n = o.n = n
+        out = {}
+        for k in BATCH_FIELDS:
+            a = batch.get(k)
+            if a is None:
+                setattr(s, k, None)
+                setattr(o, k, None)
+                continue
+            if not a.is_cuda or not a.is_contiguous():
+                raise ValueError(f"field {k} must be a contiguous CUDA tensor")
+            out[k] = torch.empty_like(a)
+            setattr(s, k, a.data_ptr() if n else None)
+            setattr(o, k, out[k].data_ptr() if n else None)
+        counts = np.zeros(max(1, nranks), np.uint64)
+        torch.cuda.current_stream().synchronize()
+        L.check(L.lib().corro_partition_ranks(self._h, C.byref(s), nranks, C.byref(o), counts.ctypes.data))
+        return out, [int(c) for c in counts[:nranks]]
+
     # ---- sync need diff -------------------------------------------------------------------
     def compute_needs(self, entries):
         """Batched compute_available_needs over CSR entries (see corrosion_amd.sync)."""

@@ -160,6 +160,16 @@ int corro_db_versions(corro_ctx *ctx, int64_t *out, uint32_t nsites);
 int corro_ctx_set_profiling(corro_ctx *ctx, int on);
 int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count);
 
+/* ------------------------------------------------------------------ multi-GPU ingest */
+
+/* Stable partition of a DEVICE-resident batch by owner rank, rank_of(table, pk) = low 32 bits of
+ * the row hash mod nranks: `out` (device arrays, in->n each; optional arrays may be
+ * NULL) receives the changes grouped by destination rank, each group in input order; counts[r]
+ * (host) = changes for rank r. Followed by one all-to-all exchange (RCCL), receivers concatenate
+ * by source rank, which preserves the application order of every row. 1 <= nranks <= 64. */
+int corro_partition_ranks(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, corro_changes *out,
+                          uint64_t *counts);
+
 /* ------------------------------------------------------------------ sync need diff */
 
 /* CSR over (node-pair, actor) entries of two SyncStateV1 (sync.rs:79-87). One entry = one

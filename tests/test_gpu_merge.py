@@ -209,3 +209,22 @@ def test_exported_state_reapplied_reproduces_itself():
     e2 = engine(synth.adversarial_schema(2), cap=20000, sites=sites)
     e2.apply(replay)
     assert rows_to_tuples(e2.export(), with_ts=True) == rows_to_tuples(rows, with_ts=True)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_partition_ranks_stable(nranks):
+    """corro_partition_ranks == stable partition by rank_of (host mirror)."""
+    import torch
+    from corrosion_amd.dist import rank_of_np
+    seed = 81
+    b = synth.adversarial_batch(50000, 8, 3, 5000, seed, zipf=0)
+    dev = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                               (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda() for k, v in b.items()}
+    e = engine(synth.adversarial_schema(3), cap=50000, sites=synth.site_ids(8, seed))
+    parts, counts = e.partition(dev, nranks)
+    dest = rank_of_np(b["table_cid"], b["pk"], nranks)
+    order = np.argsort(dest, kind="stable")
+    assert counts == np.bincount(dest, minlength=nranks).tolist()
+    for k, v in b.items():
+        got = parts[k].cpu().numpy().view(v.dtype)
+        assert np.array_equal(got, v[order]), k
