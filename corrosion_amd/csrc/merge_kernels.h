@@ -116,8 +116,26 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t *__restrict__ hist_o
     __syncthreads();
     const uint32_t begin = blockIdx.x * tile;
     const uint32_t end = min(in.n, begin + tile);
-    for (uint32_t i = begin + threadIdx.x; i < end; i += blockDim.x)
-        atomicAdd(&hist[bucket_of(in.tcid[i] >> 16, in.pk[i], log2B)], 1u);
+    // HIST_U changes per lane in flight: one CU holds a single 128-KB-LDS workgroup, so memory
+    // level parallelism has to come from each lane
+    constexpr int HIST_U = 8;
+    for (uint32_t base = begin; base < end; base += blockDim.x * HIST_U) {
+        uint64_t pk[HIST_U];
+        uint32_t tc[HIST_U];
+#pragma unroll
+        for (int k = 0; k < HIST_U; k++) {
+            const uint32_t i = base + k * blockDim.x + threadIdx.x;
+            if (i < end) {
+                pk[k] = in.pk[i];
+                tc[k] = in.tcid[i];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < HIST_U; k++) {
+            const uint32_t i = base + k * blockDim.x + threadIdx.x;
+            if (i < end) atomicAdd(&hist[bucket_of(tc[k] >> 16, pk[k], log2B)], 1u);
+        }
+    }
     __syncthreads();
     uint32_t *row = hist_out + (size_t)blockIdx.x * B;
     for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) row[b] = hist[b];
@@ -274,60 +292,75 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict
     // order, so a wave sees one actor's changesets for long stretches)
     uint32_t run_site = 0xFFFFFFFFu;
     unsigned long long run_max = 0;
-    for (uint32_t base = begin; base < end; base += blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
-        const bool act = i < end;
-        Rec r;
-        r.site = 0xFFFFFFFFu;
-        r.dbv = 0;
-        uint32_t idx = 0;
-        if (act) {
-            r.pk = in.pk[i];
-            r.cv = in.cv[i];
-            r.dbv = in.dbv[i];
-            r.v0 = in.v0[i];
-            r.v1 = in.v1 ? in.v1[i] : 0ULL;
-            r.tcid = in.tcid[i];
-            r.cl = in.cl[i];
-            r.seq = in.seq[i];
-            r.site = in.site[i];
-            r.pos = BATCH_POS | i;
-            const uint32_t ty = in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER;
-            const uint32_t ln = in.vl ? (uint32_t)in.vl[i] : 0u;
-            r.meta = ty | (ln << 8);
-            const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
-            const uint32_t b = bucket_of(t, r.pk, log2B);
-            idx = atomicAdd(&cur[b], 1u);
-            if (r.cl != 1u || cid == 0) atomicOr(&fl[b >> 5], 1u << (b & 31));
-            if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
-            if (r.site >= nsites) err |= ERR_SITE;
-            if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
-            if (r.dbv < 0) err |= ERR_RANGE;
-            if (ty != CORRO_INTEGER) {
-                wide = 1;
-                if (ty < 1 || ty > 5) err |= ERR_VALUE;
-                if (ty == CORRO_REAL && ((r.v0 >> 52) & 0x7FF) == 0x7FF && (r.v0 & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
-                if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) err |= ERR_VALUE;
+    // SCAT_U changes per lane: all their loads are issued before any is consumed (one 132-KB-LDS
+    // workgroup per CU, so memory-level parallelism must come from each lane)
+    constexpr int SCAT_U = 4;
+    for (uint32_t base = begin; base < end; base += blockDim.x * SCAT_U) {
+        Rec rr[SCAT_U];
+#pragma unroll
+        for (int u = 0; u < SCAT_U; u++) {
+            const uint32_t i = base + u * blockDim.x + threadIdx.x;
+            Rec &r = rr[u];
+            r.site = 0xFFFFFFFFu;
+            r.dbv = 0;
+            if (i < end) {
+                r.pk = in.pk[i];
+                r.cv = in.cv[i];
+                r.dbv = in.dbv[i];
+                r.v0 = in.v0[i];
+                r.v1 = in.v1 ? in.v1[i] : 0ULL;
+                r.tcid = in.tcid[i];
+                r.cl = in.cl[i];
+                r.seq = in.seq[i];
+                r.site = in.site[i];
+                r.pos = BATCH_POS | i;
+                const uint32_t ty = in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER;
+                const uint32_t ln = in.vl ? (uint32_t)in.vl[i] : 0u;
+                r.meta = ty | (ln << 8);
             }
         }
-        store_rec_wave(stage, idx, r, act);
-        // db_versions
-        const uint32_t site0 = __shfl(r.site, 0);
-        const unsigned long long dv = act ? (unsigned long long)r.dbv + 1ULL : 0ULL;
-        if (__all(!act || r.site == site0)) {
-            const unsigned long long m = wave_max_u64(dv);
-            if (site0 == run_site) {
-                run_max = m > run_max ? m : run_max;
-            } else {
-                if (lane == 0 && run_site < nsites) atomicMax(&dbv_batch[run_site], run_max);
-                run_site = site0;
-                run_max = m;
+#pragma unroll
+        for (int u = 0; u < SCAT_U; u++) {
+            const uint32_t i = base + u * blockDim.x + threadIdx.x;
+            const bool act = i < end;
+            const Rec &r = rr[u];
+            uint32_t idx = 0;
+            if (act) {
+                const uint32_t ty = vtype(r.meta), ln = vlen(r.meta);
+                const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
+                const uint32_t b = bucket_of(t, r.pk, log2B);
+                idx = atomicAdd(&cur[b], 1u);
+                if (r.cl != 1u || cid == 0) atomicOr(&fl[b >> 5], 1u << (b & 31));
+                if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
+                if (r.site >= nsites) err |= ERR_SITE;
+                if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
+                if (r.dbv < 0) err |= ERR_RANGE;
+                if (ty != CORRO_INTEGER) {
+                    wide = 1;
+                    if (ty < 1 || ty > 5) err |= ERR_VALUE;
+                    if (ty == CORRO_REAL && ((r.v0 >> 52) & 0x7FF) == 0x7FF && (r.v0 & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
+                    if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) err |= ERR_VALUE;
+                }
             }
-        } else {
-            const uint32_t psite = __shfl_up(r.site, 1);
-            const unsigned long long pdv = __shfl_up(dv, 1);
-            if (act && r.site < nsites && (lane == 0 || psite != r.site || pdv != dv))
-                atomicMax(&dbv_batch[r.site], dv);
+            store_rec_wave(stage, idx, r, act);
+            // db_versions
+            const uint32_t site0 = __shfl(r.site, 0);
+            const unsigned long long dv = act ? (unsigned long long)r.dbv + 1ULL : 0ULL;
+            if (__all(!act || r.site == site0)) {
+                const unsigned long long m = wave_max_u64(dv);
+                if (site0 == run_site) {
+                    run_max = m > run_max ? m : run_max;
+                } else {
+                    if (lane == 0 && run_site < nsites) atomicMax(&dbv_batch[run_site], run_max);
+                    run_site = site0;
+                    run_max = m;
+                }
+            } else {
+                const uint32_t psite = __shfl_up(r.site, 1);
+                const unsigned long long pdv = __shfl_up(dv, 1);
+                if (act && r.site < nsites && (lane == 0 || psite != r.site || pdv != dv))
+                    atomicMax(&dbv_batch[r.site], dv);
+            }
         }
     }
     if (lane == 0 && run_site < nsites) atomicMax(&dbv_batch[run_site], run_max);
