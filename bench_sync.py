@@ -1,0 +1,99 @@
+"""Config-4 benchmark: batched SyncStateV1 need diff (compute_available_needs) on MI355X.
+
+BASELINE.json configs[3]: 1M node-pair sync states, 64 sparse actors per pair from a 100k-actor
+universe -> 64M (pair, actor) entries, generated in HBM (synth.sync_entries_torch). One step =
+corro_compute_needs count pass + device offset scan + fill pass. Algorithmic bytes:
+16 B per input range (ours.need, theirs.need, partial seq ranges) + 16 B per head pair + 8 B per
+partial version + 16 B per output range. Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_baseline(ent_dev, sample):
+    """oracle/ranges.c compute_available_needs on the first `sample` entries (kind 'port', 1 core)."""
+    import numpy as np
+    from oracle import oracle as O
+    cut = {}
+    n = sample
+    for k in ("their_head", "our_head"):
+        cut[k] = ent_dev[k][:n].cpu().numpy()
+    for side in ("tn", "on", "tp", "op"):
+        off = ent_dev[f"{side}_off"][: n + 1].cpu().numpy()
+        cut[f"{side}_off"] = off
+        m = int(off[-1])
+        if side in ("tn", "on"):
+            cut[f"{side}_start"] = ent_dev[f"{side}_start"][:m].cpu().numpy()
+            cut[f"{side}_end"] = ent_dev[f"{side}_end"][:m].cpu().numpy()
+        else:
+            cut[f"{side}_ver"] = ent_dev[f"{side}_ver"][:m].cpu().numpy()
+            so = ent_dev[f"{side}s_off"][: m + 1].cpu().numpy()
+            cut[f"{side}s_off"] = so
+            cut[f"{side}s_start"] = ent_dev[f"{side}s_start"][: int(so[-1])].cpu().numpy()
+            cut[f"{side}s_end"] = ent_dev[f"{side}s_end"][: int(so[-1])].cpu().numpy()
+    cut = {k: np.ascontiguousarray(v) for k, v in cut.items()}
+    t0 = time.perf_counter()
+    O.needs(cut)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "entries/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} (pair, actor) entries, oracle/ranges.c count+fill passes in {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=1_000_000)
+    ap.add_argument("--actors-per-pair", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    args = ap.parse_args()
+
+    import torch
+    import synth
+    import corrosion_amd as ca
+    from corrosion_amd.sync import _needs_device
+
+    dev = torch.device("cuda", 0)
+    eng = ca.MergeEngine({"t": ["a"]}, capacity_hint=1024)
+    ent = synth.sync_entries_torch(args.pairs, args.actors_per_pair, synth.config_seed(4), device=dev)
+    torch.cuda.synchronize()
+    eng.set_profiling(True)
+    for _ in range(args.warmup):
+        res = _needs_device(eng, ent)
+    kt = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = _needs_device(eng, ent)
+        tm = eng.last_timings(apply_only=False)
+        kt += tm["k_needs_count"] + tm["k_needs_fill"]
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    kt /= args.steps
+    E = int(ent["their_head"].shape[0])
+    in_ranges = sum(int(ent[k].shape[0]) for k in ("tn_start", "on_start", "tps_start", "ops_start"))
+    pvers = int(ent["tp_ver"].shape[0] + ent["op_ver"].shape[0])
+    out_ranges = int(res["start"].shape[0] + res["s_start"].shape[0])
+    alg = 16 * in_ranges + 16 * E + 8 * pvers + 16 * out_ranges
+    achieved = alg / (kt * 1e-3) / 1e9
+    line = {"metric": "SyncStateV1 need diff: node-pairs/s (config 4)", "value": args.pairs / dt,
+            "unit": "node-pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3, "higher_is_better": True, "dtype": "u64", "data": "synthetic (HBM)",
+            "config": {"workload": "config 4", "pairs": args.pairs, "entries": E, "input_ranges": in_ranges,
+                       "output_needs": int(res["start"].shape[0]), "output_seq_ranges": int(res["s_start"].shape[0])},
+            "entries_per_s": E / dt,
+            "roofline": {"bound": "hbm", "kernel": "k_needs (count + fill)", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernels_ms": kt},
+            "cpu_baseline": cpu_baseline(ent, min(args.cpu_sample, E))}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -362,7 +362,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     auto mark = [&](int i) {
         if (prof) (void)hipEventRecord(ctx->ev[i], s);
     };
-    for (float &m : ctx->last_ms) m = 0.f;
+    for (int k = 0; k < 6; k++) ctx->last_ms[k] = 0.f;
     mark(0);
     hipLaunchKernelGGL(k_hist, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B,
                        ctx->d_hist.as<uint32_t>());
@@ -487,7 +487,7 @@ int corro_ctx_set_profiling(corro_ctx *ctx, int on) {
 
 int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count) {
     if (!ctx || !count || (!ms && cap)) return fail(CORRO_E_INVALID, "NULL argument");
-    const uint32_t n = 6;
+    const uint32_t n = 8;
     for (uint32_t i = 0; i < n && i < cap; i++) ms[i] = ctx->last_ms[i];
     *count = n;
     return CORRO_OK;

@@ -102,5 +102,5 @@ struct corro_ctx {
     // stage timing
     bool profiling = false;
     hipEvent_t ev[8] = {};
-    float last_ms[6] = {};
+    float last_ms[8] = {};        // apply stages [0..5], k_needs count [6], k_needs fill [7]
 };

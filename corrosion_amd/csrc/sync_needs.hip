@@ -287,7 +287,9 @@ extern "C" int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in,
     const uint32_t threads = 256;
     const uint64_t blocks = (n + threads - 1) / threads;
     if (blocks > 0x7FFFFFFFULL) return fail(CORRO_E_RANGE, "too many sync entries");
+    if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[0], s));
     hipLaunchKernelGGL(k_needs, dim3((uint32_t)blocks), dim3(threads), 0, s, d, od, pass);
+    if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
     CORRO_HIP_TRY(hipGetLastError());
     if (mem == CORRO_MEM_HOST) {
         if (pass == 0) {
@@ -309,5 +311,6 @@ extern "C" int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in,
         }
     }
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (ctx->profiling) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[6 + pass], ctx->ev[0], ctx->ev[1]));
     return CORRO_OK;
 }

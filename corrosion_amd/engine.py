@@ -141,12 +141,15 @@ class MergeEngine:
     def set_profiling(self, on=True):
         L.check(L.lib().corro_ctx_set_profiling(self._h, 1 if on else 0))
 
-    def last_timings(self):
-        """ms per stage of the last apply: hist, colscan, plan, scatter, merge, overflow"""
+    def last_timings(self, apply_only=True):
+        """ms per stage of the last apply: hist, colscan, plan, scatter, merge (fast + general
+        kernels), overflow; with apply_only=False also the last sync-need count/fill kernels."""
         arr = (C.c_float * 8)()
         n = C.c_uint32()
         L.check(L.lib().corro_last_timings(self._h, arr, 8, C.byref(n)))
         names = ["k_hist", "k_colscan", "k_plan", "k_scatter", "k_merge", "k_merge_ovf"]
+        if not apply_only:
+            names += ["k_needs_count", "k_needs_fill"]
         return {names[i]: arr[i] for i in range(min(n.value, len(names)))}
 
     # ---- multi-GPU ingest -----------------------------------------------------------------

@@ -136,6 +136,46 @@ def _needs_host(engine, ent):
     return res
 
 
+def _needs_device(engine, ent):
+    """corro_compute_needs on device-resident CSR entries (dict of CUDA int64 tensors).
+    Returns the CSR result as CUDA tensors (two passes, offsets scanned on the device)."""
+    import torch
+    lib = L.lib()
+    n = int(ent["their_head"].shape[0])
+    dev = ent["their_head"].device
+    s = L.SyncEntries()
+    s.n = n
+    for k, _ in L.SyncEntries._fields_[1:]:
+        a = ent[k]
+        setattr(s, k, a.data_ptr() if a.numel() else None)
+    nc = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+    sc = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+    o = L.NeedsOut()
+    o.need_count, o.seq_count = nc.data_ptr(), sc.data_ptr()
+    torch.cuda.current_stream().synchronize()
+    L.check(lib.corro_compute_needs(engine._h, C.byref(s), L.CORRO_MEM_DEVICE, C.byref(o), 0))
+    need_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    seq_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    need_off[1:] = torch.cumsum(nc[:n], 0)
+    seq_off[1:] = torch.cumsum(sc[:n], 0)
+    T, Ts = int(need_off[-1].item()), int(seq_off[-1].item())
+    res = {"need_off": need_off, "seq_off": seq_off,
+           "kind": torch.zeros(max(T, 1), dtype=torch.uint8, device=dev)}
+    for k in ("start", "end", "sr_off", "sr_n"):
+        res[k] = torch.zeros(max(T, 1), dtype=torch.int64, device=dev)
+    for k in ("s_start", "s_end"):
+        res[k] = torch.zeros(max(Ts, 1), dtype=torch.int64, device=dev)
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        setattr(o, k, res[k].data_ptr())
+    torch.cuda.current_stream().synchronize()
+    L.check(lib.corro_compute_needs(engine._h, C.byref(s), L.CORRO_MEM_DEVICE, C.byref(o), 1))
+    for k in ("kind", "start", "end", "sr_off", "sr_n"):
+        res[k] = res[k][:T]
+    for k in ("s_start", "s_end"):
+        res[k] = res[k][:Ts]
+    return res
+
+
 def decode(res, index, npairs):
     out = [dict() for _ in range(npairs)]
     for e, (p, actor) in enumerate(index):

@@ -155,3 +155,74 @@ def uniform_batch_torch(n, nactors, npk, ncols, seed, device="cuda", cv_max=8, p
     return {"pk": pk.contiguous(), "table_cid": cid.to(torch.int32).contiguous(), "col_version": cv.contiguous(),
             "db_version": dbv.contiguous(), "cl": torch.ones(n, device=device, dtype=torch.int32),
             "seq": seq.contiguous(), "site": site.contiguous(), "val0": val.contiguous()}
+
+
+def sync_entries_torch(npairs, actors_per_pair, seed, device="cuda", max_head=1_000_000,
+                       need_rate=2.0, need_len=20, partial_frac=0.05):
+    """Config 4 generated in HBM: npairs node-pair states, each with
+    `actors_per_pair` sparse actors -> one CSR entry per (pair, actor). Per side: head uniform in
+    [1, max_head] (ours absent 10 %), Poisson(need_rate) disjoint non-adjacent need ranges of
+    geometric length (mean need_len); 5 % of entries carry a partial version (1-3 seq ranges in
+    [0, 1000]), half of them at the same version on both sides."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
+    E = npairs * actors_per_pair
+    i64 = torch.int64
+
+    def ranges(cnt, gap_mean, len_mean, base):
+        R = int(cnt.sum().item())
+        off = torch.zeros(E + 1, dtype=i64, device=device)
+        off[1:] = torch.cumsum(cnt, 0)
+        if R == 0:
+            z = torch.zeros(0, dtype=i64, device=device)
+            return off, z, z
+        ent = torch.repeat_interleave(torch.arange(E, device=device), cnt)
+        gap = torch.empty(R, device=device).geometric_(1.0 / gap_mean, generator=g).to(i64) + 1
+        ln = torch.empty(R, device=device).geometric_(1.0 / len_mean, generator=g).to(i64)
+        step = gap + ln
+        cs = torch.cumsum(step, 0)
+        first = off[:-1][ent]
+        prior = torch.where(first > 0, cs[(first - 1).clamp(min=0)], torch.zeros_like(first))
+        seg = cs - prior                      # segmented inclusive cumsum per entry
+        end = seg + base
+        start = end - ln + 1
+        return off, start, end
+
+    their_head = torch.randint(1, max_head + 1, (E,), device=device, generator=g)
+    our_head = torch.randint(1, max_head + 1, (E,), device=device, generator=g)
+    our_head = torch.where(torch.rand(E, device=device, generator=g) < 0.1, torch.full_like(our_head, -1), our_head)
+    tn_cnt = torch.poisson(torch.full((E,), need_rate, device=device), generator=g).to(i64)
+    on_cnt = torch.poisson(torch.full((E,), need_rate, device=device), generator=g).to(i64)
+    span = max(1, max_head // 20)
+    tn_off, tn_s, tn_e = ranges(tn_cnt, span // 4 + 2, need_len, 0)
+    on_off, on_s, on_e = ranges(on_cnt, span // 4 + 2, need_len, 0)
+
+    def partials(shared_ver):
+        has = torch.rand(E, device=device, generator=g) < partial_frac
+        cnt = has.to(i64)
+        off = torch.zeros(E + 1, dtype=i64, device=device)
+        off[1:] = torch.cumsum(cnt, 0)
+        ids = torch.nonzero(has).flatten()
+        ver = torch.where(torch.rand(ids.numel(), device=device, generator=g) < 0.5, shared_ver[ids],
+                          (torch.rand(ids.numel(), device=device, generator=g) * their_head[ids]).to(i64) + 1)
+        scnt = torch.randint(1, 4, (ids.numel(),), device=device, generator=g)
+        soff = torch.zeros(ids.numel() + 1, dtype=i64, device=device)
+        soff[1:] = torch.cumsum(scnt, 0)
+        S = int(soff[-1].item())
+        pid = torch.repeat_interleave(torch.arange(ids.numel(), device=device), scnt)
+        gap = torch.randint(0, 200, (S,), device=device, generator=g) + 2
+        ln = torch.randint(0, 150, (S,), device=device, generator=g)
+        cs = torch.cumsum(gap + ln, 0)
+        first = soff[:-1][pid]
+        prior = torch.where(first > 0, cs[(first - 1).clamp(min=0)], torch.zeros_like(first))
+        e_ = cs - prior
+        return off, ver, soff, e_ - ln, e_
+
+    shared = (torch.rand(E, device=device, generator=g) * their_head).to(i64) + 1
+    tp_off, tp_ver, tps_off, tps_s, tps_e = partials(shared)
+    op_off, op_ver, ops_off, ops_s, ops_e = partials(shared)
+    return {"their_head": their_head, "our_head": our_head, "tn_off": tn_off, "tn_start": tn_s, "tn_end": tn_e,
+            "tp_off": tp_off, "tp_ver": tp_ver, "tps_off": tps_off, "tps_start": tps_s, "tps_end": tps_e,
+            "on_off": on_off, "on_start": on_s, "on_end": on_e, "op_off": op_off, "op_ver": op_ver,
+            "ops_off": ops_off, "ops_start": ops_s, "ops_end": ops_e}

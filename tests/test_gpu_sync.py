@@ -65,3 +65,17 @@ def test_sync_random_vs_oracle():
     exp = O.needs(ent)
     for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
         assert np.array_equal(got[k], exp[k]), k
+
+
+def test_sync_device_resident_config4_shape_vs_oracle():
+    """Config-4-shaped entries generated in HBM, need diff on device, checked against the oracle."""
+    import torch
+    import synth
+    from corrosion_amd.sync import _needs_device
+    ent = synth.sync_entries_torch(3000, 16, 9, device="cuda")
+    e = _engine()
+    got = _needs_device(e, ent)
+    host = {k: v.cpu().numpy() for k, v in ent.items()}
+    exp = O.needs(host)
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        assert np.array_equal(got[k].cpu().numpy().astype(np.uint64), exp[k].astype(np.uint64)), k
