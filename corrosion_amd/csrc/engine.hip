@@ -316,6 +316,12 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     if (mem == CORRO_MEM_HOST) {
         TRY(stage_host_batch(ctx, in, bd));
     } else {
+        // k_scatter reads pairs of changes with 16-B (64-bit fields) / 8-B (32-bit fields) loads
+        auto misaligned = [](const void *p, uintptr_t a) { return p && ((uintptr_t)p % a) != 0; };
+        if (misaligned(in->pk, 16) || misaligned(in->col_version, 16) || misaligned(in->db_version, 16) ||
+            misaligned(in->val0, 16) || misaligned(in->val1, 16) || misaligned(in->table_cid, 8) ||
+            misaligned(in->cl, 8) || misaligned(in->seq, 8) || misaligned(in->site, 8))
+            return fail(CORRO_E_INVALID, "device batch arrays must be 16-byte (64-bit fields) / 8-byte aligned");
         bd.pk = in->pk;
         bd.tcid = in->table_cid;
         bd.cv = in->col_version;

@@ -295,33 +295,61 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict
     // SCAT_U changes per lane: all their loads are issued before any is consumed (one 132-KB-LDS
     // workgroup per CU, so memory-level parallelism must come from each lane)
     constexpr int SCAT_U = 4;
+    // (tiles start at multiples of 2 * blockDim.x, so pairs (2t, 2t+1) are 16-B aligned)
     for (uint32_t base = begin; base < end; base += blockDim.x * SCAT_U) {
         Rec rr[SCAT_U];
 #pragma unroll
-        for (int u = 0; u < SCAT_U; u++) {
-            const uint32_t i = base + u * blockDim.x + threadIdx.x;
-            Rec &r = rr[u];
-            r.site = 0xFFFFFFFFu;
-            r.dbv = 0;
-            if (i < end) {
-                r.pk = in.pk[i];
-                r.cv = in.cv[i];
-                r.dbv = in.dbv[i];
-                r.v0 = in.v0[i];
-                r.v1 = in.v1 ? in.v1[i] : 0ULL;
-                r.tcid = in.tcid[i];
-                r.cl = in.cl[i];
-                r.seq = in.seq[i];
-                r.site = in.site[i];
-                r.pos = BATCH_POS | i;
-                const uint32_t ty = in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER;
-                const uint32_t ln = in.vl ? (uint32_t)in.vl[i] : 0u;
-                r.meta = ty | (ln << 8);
+        for (int p = 0; p < SCAT_U / 2; p++) {
+            // each lane loads two consecutive changes with 16-B (8-B for 32-bit fields) accesses
+            const uint32_t i = base + p * 2 * blockDim.x + 2 * threadIdx.x;
+            Rec &a = rr[2 * p], &b = rr[2 * p + 1];
+            a.site = b.site = 0xFFFFFFFFu;
+            a.dbv = b.dbv = 0;
+            if (i + 1 < end) {
+                const ulonglong2 pk = *reinterpret_cast<const ulonglong2 *>(in.pk + i);
+                const longlong2 cv = *reinterpret_cast<const longlong2 *>(in.cv + i);
+                const longlong2 dbv = *reinterpret_cast<const longlong2 *>(in.dbv + i);
+                const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(in.v0 + i);
+                const uint2 tc = *reinterpret_cast<const uint2 *>(in.tcid + i);
+                const uint2 cl = *reinterpret_cast<const uint2 *>(in.cl + i);
+                const uint2 sq = *reinterpret_cast<const uint2 *>(in.seq + i);
+                const uint2 st = *reinterpret_cast<const uint2 *>(in.site + i);
+                a.pk = pk.x; b.pk = pk.y;
+                a.cv = cv.x; b.cv = cv.y;
+                a.dbv = dbv.x; b.dbv = dbv.y;
+                a.v0 = v0.x; b.v0 = v0.y;
+                a.tcid = tc.x; b.tcid = tc.y;
+                a.cl = cl.x; b.cl = cl.y;
+                a.seq = sq.x; b.seq = sq.y;
+                a.site = st.x; b.site = st.y;
+                if (in.v1) {
+                    const ulonglong2 v1 = *reinterpret_cast<const ulonglong2 *>(in.v1 + i);
+                    a.v1 = v1.x; b.v1 = v1.y;
+                } else {
+                    a.v1 = b.v1 = 0;
+                }
+                a.meta = in.vt ? ((uint32_t)in.vt[i] | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8)) : (uint32_t)CORRO_INTEGER;
+                b.meta = in.vt ? ((uint32_t)in.vt[i + 1] | ((in.vl ? (uint32_t)in.vl[i + 1] : 0u) << 8))
+                               : (uint32_t)CORRO_INTEGER;
+                a.pos = BATCH_POS | i;
+                b.pos = BATCH_POS | (i + 1);
+            } else if (i < end) {
+                a.pk = in.pk[i];
+                a.cv = in.cv[i];
+                a.dbv = in.dbv[i];
+                a.v0 = in.v0[i];
+                a.v1 = in.v1 ? in.v1[i] : 0ULL;
+                a.tcid = in.tcid[i];
+                a.cl = in.cl[i];
+                a.seq = in.seq[i];
+                a.site = in.site[i];
+                a.pos = BATCH_POS | i;
+                a.meta = in.vt ? ((uint32_t)in.vt[i] | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8)) : (uint32_t)CORRO_INTEGER;
             }
         }
 #pragma unroll
         for (int u = 0; u < SCAT_U; u++) {
-            const uint32_t i = base + u * blockDim.x + threadIdx.x;
+            const uint32_t i = base + (u / 2) * 2 * blockDim.x + 2 * threadIdx.x + (u & 1);
             const bool act = i < end;
             const Rec &r = rr[u];
             uint32_t idx = 0;
@@ -379,6 +407,32 @@ struct BucketView {
     const uint64_t *prior_ts;  // offset to the bucket (or null)
     __device__ inline const Rec *at(uint32_t i) const { return i < np ? prior + i : fresh + (i - np); }
 };
+
+// Wave-cooperative load of the 64 records [wave_base, wave_base + 64) of a bucket (lane L gets
+// record wave_base + L; records >= n read as zero). Load instruction k reads the 1 KB of records
+// wave_base + 16k .. +15 with one 16-B quad per lane (fully coalesced); the same 4x4 lane
+// transpose as store_rec_wave (an involution) then gives every lane its own record.
+__device__ inline Rec load_rec_wave(const BucketView &v, uint32_t wave_base, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = lane >> 4, l = lane & 15;
+    uint4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t ri = wave_base + l + 16 * k;
+        q[k] = ri < n ? reinterpret_cast<const uint4 *>(v.at(ri))[j] : make_uint4(0, 0, 0, 0);
+    }
+    swap32(q[0].x, q[2].x); swap32(q[0].y, q[2].y); swap32(q[0].z, q[2].z); swap32(q[0].w, q[2].w);
+    swap32(q[1].x, q[3].x); swap32(q[1].y, q[3].y); swap32(q[1].z, q[3].z); swap32(q[1].w, q[3].w);
+    swap16(q[0].x, q[1].x); swap16(q[0].y, q[1].y); swap16(q[0].z, q[1].z); swap16(q[0].w, q[1].w);
+    swap16(q[2].x, q[3].x); swap16(q[2].y, q[3].y); swap16(q[2].z, q[3].z); swap16(q[2].w, q[3].w);
+    Rec r;
+    uint4 *d = reinterpret_cast<uint4 *>(&r);
+    d[0] = q[0];
+    d[1] = q[1];
+    d[2] = q[2];
+    d[3] = q[3];
+    return r;
+}
 
 __device__ inline uint64_t rec_ts(const MergeArgs &a, const BucketView &v, const Rec &r) {
     if (r.pos & BATCH_POS) return a.batch_ts ? a.batch_ts[r.pos & 0x7FFFFFFFu] : 0ULL;
@@ -672,8 +726,8 @@ k_merge_fast(MergeArgs a) {
         const uint32_t i = k * MERGE_THREADS + tid;
         alive[k] = i < n;
         cell[k] = 0;
+        const Rec r = load_rec_wave(v, k * MERGE_THREADS + (tid & ~63u), n);
         if (alive[k]) {
-            const Rec r = load_rec(v.at(i));
             s_pk[i] = r.pk;
             s_tc[i] = r.tcid;
             cv[k] = (uint64_t)r.cv ^ 0x8000000000000000ULL;

@@ -110,9 +110,13 @@ def test_process_multiple_changes_reference_sequence():
     check(ta2, complete=[(1, 20)], cleared=[(21, 25)])
     assert ta2.bookie.needed(TA1) == []
     assert ta2.bookie.last(TA1) == 25
-    # generate_sync: head 25, nothing needed, complete partials not reported (sync.rs:313-318)
+    # generate_sync: head 25, nothing needed. Versions 15/16 arrived complete after their seq-0
+    # partials; the reference only drops in-memory partials inside removed gap ranges
+    # (agent.rs:1130-1136), so their stale partials (seqs {0}, last_seq 3) stay and generate_sync
+    # still lists seqs 1..=3 for them (sync.rs:311-326).
     st = ta2.generate_sync()
-    assert st.heads == {TA1: 25} and st.need == {} and st.partial_need == {}
+    assert st.heads == {TA1: 25} and st.need == {}
+    assert st.partial_need == {TA1: {15: [(1, 3)], 16: [(1, 3)]}}
     # every merged cell of rows 1..20 carries ta1's db_version of its last write
     site = ta2.site(TA1)
     rows = state_rows(ta2)
