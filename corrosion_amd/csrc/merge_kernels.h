@@ -171,35 +171,63 @@ __global__ void k_colscan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t
 __global__ void __launch_bounds__(1024)
 k_plan(const uint32_t *__restrict__ new_cnt, const uint32_t *__restrict__ prior_cnt, uint32_t B,
        uint32_t *__restrict__ stage_off, uint64_t *__restrict__ out_off) {
-    __shared__ uint64_t s_a[1024];
-    __shared__ uint64_t s_b[1024];
-    const uint32_t per = (B + 1023) / 1024;
-    const uint32_t lo = min(B, threadIdx.x * per), hi = min(B, lo + per);
-    uint64_t sa = 0, sb = 0;
-    for (uint32_t b = lo; b < hi; b++) {
-        sa += new_cnt[b];
-        sb += (uint64_t)prior_cnt[b] + 2ULL * new_cnt[b];
-    }
-    s_a[threadIdx.x] = sa;
-    s_b[threadIdx.x] = sb;
+    // chunks of 4096 buckets: 4 consecutive buckets per lane (coalesced 16-B loads), wave scans
+    // by shuffles, one LDS round for the 16 wave totals, a running carry across chunks
+    __shared__ uint64_t w_a[16], w_b[16];
+    __shared__ uint64_t carry_a, carry_b;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry_a = carry_b = 0;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        uint64_t xa = 0, xb = 0;
-        if (threadIdx.x >= d) {
-            xa = s_a[threadIdx.x - d];
-            xb = s_b[threadIdx.x - d];
+    for (uint32_t c0 = 0; c0 < B; c0 += 4096) {
+        const uint32_t b0 = c0 + 4 * threadIdx.x;
+        uint32_t nc[4] = {0, 0, 0, 0}, pc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (b0 + k < B) {
+                nc[k] = new_cnt[b0 + k];
+                pc[k] = prior_cnt[b0 + k];
+            }
+        uint64_t sa = 0, sb = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            sa += nc[k];
+            sb += (uint64_t)pc[k] + 2ULL * nc[k];
+        }
+        uint64_t ia = sa, ib = sb;  // inclusive wave scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t xa = __shfl_up(ia, d), xb = __shfl_up(ib, d);
+            if (lane >= (uint32_t)d) {
+                ia += xa;
+                ib += xb;
+            }
+        }
+        if (lane == 63) {
+            w_a[w] = ia;
+            w_b[w] = ib;
         }
         __syncthreads();
-        s_a[threadIdx.x] += xa;
-        s_b[threadIdx.x] += xb;
+        uint64_t ra = carry_a + ia - sa, rb = carry_b + ib - sb;
+        for (uint32_t ww = 0; ww < w; ww++) {
+            ra += w_a[ww];
+            rb += w_b[ww];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (b0 + k < B) {
+                stage_off[b0 + k] = (uint32_t)ra;
+                out_off[b0 + k] = rb;
+                ra += nc[k];
+                rb += (uint64_t)pc[k] + 2ULL * nc[k];
+            }
         __syncthreads();
-    }
-    uint64_t ra = s_a[threadIdx.x] - sa, rb = s_b[threadIdx.x] - sb;
-    for (uint32_t b = lo; b < hi; b++) {
-        stage_off[b] = (uint32_t)ra;
-        out_off[b] = rb;
-        ra += new_cnt[b];
-        rb += (uint64_t)prior_cnt[b] + 2ULL * new_cnt[b];
+        if (threadIdx.x == 0) {
+            for (int ww = 0; ww < 16; ww++) {
+                carry_a += w_a[ww];
+                carry_b += w_b[ww];
+            }
+        }
+        __syncthreads();
     }
 }
 

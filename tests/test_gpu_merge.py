@@ -228,3 +228,43 @@ def test_partition_ranks_stable(nranks):
     for k, v in b.items():
         got = parts[k].cpu().numpy().view(v.dtype)
         assert np.array_equal(got, v[order]), k
+
+
+def test_config1_cpu_reference_workload():
+    """BASELINE configs[0]: 100k changes from 4 actors into one 3-column table, pk in [1, 10k]."""
+    sites = synth.site_ids(4, synth.config_seed(1))
+    b = synth.uniform_batch(100_000, 4, 10_000, 3, synth.config_seed(1), per_version=50)
+    e = engine(SCHEMA_T, cap=100_000, sites=sites)
+    f = O.Fold(sites)
+    assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+    compare(e, f)
+
+
+@pytest.mark.slow
+def test_config5_adversarial_scaled():
+    """BASELINE configs[4] shape at 1M changes: 8 tables, Zipf(1.1) pks over 2^20, 30 % sentinel
+    deletes/resurrects, mixed INTEGER/REAL/TEXT/NULL + 16-byte BLOB values, 1000 actors."""
+    seed = synth.config_seed(5)
+    sites = synth.site_ids(1000, seed)
+    b = synth.adversarial_batch(1_000_000, 1000, 8, 1 << 20, seed)
+    e = engine(synth.adversarial_schema(8), cap=1_000_000, sites=sites)
+    f = O.Fold(sites)
+    e.apply(b)
+    f.apply(b)
+    compare(e, f, with_ts=True)
+
+
+@pytest.mark.slow
+def test_config2_distribution_4m_vs_oracle():
+    """Config 2's distribution (1000 actors, 4 cols, pk space 2^22) at 4M changes, device input."""
+    import torch
+    seed = synth.config_seed(2)
+    sites = synth.site_ids(1000, 1)
+    b = synth.uniform_batch(1 << 22, 1000, 1 << 22, 4, seed)
+    dev = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                               (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda() for k, v in b.items()}
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=1 << 22, sites=sites)
+    f = O.Fold(sites)
+    e.apply(dev)
+    f.apply(b)
+    compare(e, f)
