@@ -57,6 +57,34 @@ def cpu_baseline(seconds_target=15.0):
                       f"folded by oracle/crsql_fold.c in {dt:.2f} s"}
 
 
+PIPELINE_KERNELS = ("k_hist", "k_colscan", "k_plan", "k_scatter", "k_merge_fast", "k_merge_gen", "k_merge_ovf")
+
+
+def pmc_traffic_per_apply():
+    """HBM bytes per apply from the committed rocprofv3 PMC passes (profiles/*_pmc_{FETCH,WRITE}_SIZE.csv,
+    collected by scripts/gpu_prof.sh on this bench): sum over the pipeline kernels of
+    2 x FETCH_SIZE (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md §HBM) +
+    WRITE_SIZE, in KiB -> bytes, averaged per dispatch. None when the files are absent."""
+    import csv
+    import glob
+    from collections import defaultdict
+    out = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{counter}.csv")))
+        if not files:
+            return None, None
+        tot, disp = defaultdict(float), defaultdict(set)
+        for r in csv.DictReader(open(files[-1])):
+            name = r["Kernel_Name"]
+            k = next((p for p in PIPELINE_KERNELS if p in name), None)
+            if k and r["Counter_Name"] == counter:
+                tot[k] += float(r["Counter_Value"])
+                disp[k].add(r["Dispatch_Id"])
+        out[counter] = sum(tot[k] / len(disp[k]) for k in tot)
+        src = os.path.basename(files[-1])
+    return (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024.0, src
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,6 +152,7 @@ def main():
     achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
 
     if rank == 0:
+        traffic, traffic_src = pmc_traffic_per_apply()
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline()
         line = {
             "metric": "merged column-changes/sec (node) at 1/2/4/8 GPUs + % of HBM BW roofline",
@@ -144,7 +173,7 @@ def main():
                        "changes_per_gpu": n, "cells_per_gpu": int(cells), "parallelism": f"pk-hash x{world}"},
             "roofline": {"bound": "hbm", "kernel": "apply pipeline: " + "+".join(k for k in kern if kern[k] > 0),
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_apply": alg_bytes, "pipeline_ms": pipe_ms,
                          "kernels_ms": kern, "dominant": dominant},
             "cpu_baseline": cpu,

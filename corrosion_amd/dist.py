@@ -38,6 +38,10 @@ def exchange(parts, counts, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     dev = next(iter(parts.values())).device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        # gloo has no device all-to-all: stage through host memory (rehearsals on a 1-GPU box)
+        got = exchange({k: v.cpu() for k, v in parts.items()}, counts, group)
+        return {k: v.to(dev) for k, v in got.items()}
     send = torch.tensor(counts, dtype=torch.int64, device=dev)
     recv = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_to_all_single(recv, send, group=group)

@@ -25,6 +25,7 @@ __device__ inline uint64_t mix64(uint64_t x) {
 __device__ inline void swap32(uint32_t &a, uint32_t &b) { auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false); a = r[0]; b = r[1]; }
 __device__ inline void swap16(uint32_t &a, uint32_t &b) { auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false); a = r[0]; b = r[1]; }
 
+template <bool NT>
 __device__ inline void store64_wave(uint4 *base, uint32_t idx, uint4 q0, uint4 q1, uint4 q2, uint4 q3) {
     uint4 q[4] = {q0, q1, q2, q3};
     swap32(q[0].x, q[2].x); swap32(q[0].y, q[2].y); swap32(q[0].z, q[2].z); swap32(q[0].w, q[2].w);
@@ -35,7 +36,10 @@ __device__ inline void store64_wave(uint4 *base, uint32_t idx, uint4 q0, uint4 q
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint32_t sidx = __shfl(idx, (int)l + 16 * k);
-        base[(size_t)sidx * 4 + j] = q[k];
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u t = {q[k].x, q[k].y, q[k].z, q[k].w};
+        if (NT) __builtin_nontemporal_store(t, reinterpret_cast<v4u *>(&base[(size_t)sidx * 4 + j]));
+        else base[(size_t)sidx * 4 + j] = q[k];
     }
 }
 
@@ -54,7 +58,7 @@ __global__ void k_stage(const uint64_t *pk, const int64_t *cv, const int64_t *db
             q1 = make_uint4((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)v, (uint32_t)(v >> 32));
             q2 = make_uint4(0, 0, tc[i], cl[i]);
             q3 = make_uint4(seq[i], site[i], i, 1);
-            if (mode == 0) d = i;
+            if (mode == 0 || mode == 3) d = i;
             else if (mode == 1) {
                 const uint32_t bk = (uint32_t)(mix64(p) >> 49);  // 32K buckets
                 const uint32_t per = n >> 15;
@@ -63,7 +67,8 @@ __global__ void k_stage(const uint64_t *pk, const int64_t *cv, const int64_t *db
                 d = (uint32_t)(mix64(i) & ((1u << lgn) - 1));    // not a bijection; fine for bandwidth
             }
         }
-        store64_wave(out, d, q0, q1, q2, q3);
+        if (mode >= 3) store64_wave<true>(out, d, q0, q1, q2, q3);
+        else store64_wave<false>(out, d, q0, q1, q2, q3);
     }
 }
 
@@ -120,8 +125,9 @@ int main(int argc, char **argv) {
                            (uint32_t *)in[7], sink, n);
     });
     time_it("read records 64B", 64.0 * n, [&] { hipLaunchKernelGGL(k_read_rec, grid, blk, 0, 0, out, sink, n); });
-    const char *names[3] = {"stage 48B->64B sequential", "stage 48B->64B bucket slices", "stage 48B->64B random"};
-    for (int mode = 0; mode < 3; mode++)
+    const char *names[5] = {"stage 48B->64B sequential", "stage 48B->64B bucket slices", "stage 48B->64B random",
+                            "stage sequential, nt stores", "stage random, nt stores"};
+    for (int mode = 0; mode < 5; mode++)
         time_it(names[mode], 112.0 * n, [&] {
             hipLaunchKernelGGL(k_stage, grid, blk, 0, 0, (uint64_t *)in[0], (int64_t *)in[1], (int64_t *)in[2],
                                (uint64_t *)in[3], (uint32_t *)in[4], (uint32_t *)in[5], (uint32_t *)in[6],
