@@ -744,8 +744,8 @@ k_merge_fast(MergeArgs a) {
     }
     Rec *outb = a.out + a.out_off[b];
     uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
-    uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], rp[FAST_R];
-    uint32_t meta[FAST_R], cell[FAST_R];
+    uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], rp[FAST_R], dbv[FAST_R];
+    uint32_t meta[FAST_R], cell[FAST_R], seq[FAST_R], site[FAST_R];
     bool alive[FAST_R];
     if (tid == 0) s_outcnt = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
@@ -763,6 +763,11 @@ k_merge_fast(MergeArgs a) {
             v1[k] = WIDE ? r.v1 : 0;
             meta[k] = WIDE ? r.meta : (uint32_t)CORRO_INTEGER;
             rp[k] = ((uint64_t)site_rank_of(a, r.site) << 32) | (uint64_t)(~r.pos);
+            if (!WIDE) {  // INTEGER-only: keep the whole clock row in registers (no re-read)
+                dbv[k] = (uint64_t)r.dbv;
+                seq[k] = r.seq;
+                site[k] = r.site;
+            }
         }
     }
     __syncthreads();
@@ -831,7 +836,20 @@ k_merge_fast(MergeArgs a) {
         uint32_t o = 0;
         Rec x;
         if (alive[k]) {
-            x = load_rec(v.at(i));
+            if (WIDE) {
+                x = load_rec(v.at(i));
+            } else {
+                x.pk = s_pk[i];
+                x.cv = (int64_t)(cv[k] ^ 0x8000000000000000ULL);
+                x.dbv = (int64_t)dbv[k];
+                x.v0 = v0[k];
+                x.v1 = 0;
+                x.tcid = s_tc[i];
+                x.seq = seq[k];
+                x.site = site[k];
+                x.pos = ~(uint32_t)rp[k];
+                x.meta = CORRO_INTEGER;
+            }
             o = atomicAdd(&s_outcnt, 1u);
             if (a.track_ts) outts[o] = rec_ts(a, v, x);
             x.cl = 1;
