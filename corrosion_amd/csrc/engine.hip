@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -85,7 +86,9 @@ static int ctx_prepare_device(corro_ctx *ctx) {
     for (auto &e : ctx->ev) CORRO_HIP_TRY(hipEventCreate(&e));
     const size_t lds_max = 160 * 1024;
     CORRO_HIP_TRY(hipFuncSetAttribute((const void *)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
-    CORRO_HIP_TRY(hipFuncSetAttribute((const void *)k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
+    for (const void *f : {(const void *)k_scatter<true, true>, (const void *)k_scatter<true, false>,
+                          (const void *)k_scatter<false, true>, (const void *)k_scatter<false, false>})
+        CORRO_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
     return CORRO_OK;
 }
 
@@ -135,6 +138,8 @@ int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t 
     if (!rc) rc = ctx->d_bflags.ensure(((B + 31) / 32) * 4ULL);
     if (!rc) rc = ctx->d_misc.ensure(8 * 8);
     if (!rc) rc = ctx->d_ovf_list.ensure(B * 4ULL);
+    if (!rc) rc = ctx->d_gen_list.ensure(B * 4ULL);
+    if (!rc) rc = ctx->d_wide_list.ensure(B * 4ULL);
     if (!rc) rc = ctx->d_state[0].ensure(64);
     if (!rc) rc = ctx->d_state[1].ensure(64);
     if (rc != CORRO_OK) {
@@ -170,7 +175,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_state_ts[0], &ctx->d_state_ts[1], &ctx->d_state_off, &ctx->d_state_cnt,
                       &ctx->d_state_flags, &ctx->d_out_off, &ctx->d_out_cnt, &ctx->d_out_flags, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_ovf_scratch, &ctx->d_impact, &ctx->d_export,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_scratch, &ctx->d_impact, &ctx->d_export,
                       &ctx->d_needs, &ctx->d_ncols, &ctx->d_part};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
@@ -344,8 +349,13 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
         ctx->track_ts = true;
     }
 
-    // tiles: about 2 waves of 256 workgroups over the batch
-    uint32_t ntiles = std::max<uint32_t>(1, std::min<uint32_t>(512, (n + 4095) / 4096));
+    // tiles: one workgroup per CU (the 128-KB LDS histogram admits one), 256 CUs
+    static const uint32_t tiles_max = [] {
+        const char *e = std::getenv("CORRO_HIP_TILES");  // tuning knob for experiments
+        const long v = e ? std::atol(e) : 0;
+        return v > 0 && v <= 4096 ? (uint32_t)v : TILES_MAX;
+    }();
+    uint32_t ntiles = std::max<uint32_t>(1, std::min<uint32_t>(tiles_max, (n + 4095) / 4096));
     uint32_t tile = (n + ntiles - 1) / ntiles;
     tile = (tile + HIST_THREADS - 1) / HIST_THREADS * HIST_THREADS;
     ntiles = (n + tile - 1) / tile;
@@ -370,7 +380,8 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     };
     for (int k = 0; k < 6; k++) ctx->last_ms[k] = 0.f;
     mark(0);
-    hipLaunchKernelGGL(k_hist, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B,
+    const uint32_t one_table = ctx->tables.size() == 1 ? 1u : 0u;
+    hipLaunchKernelGGL(k_hist, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B, one_table,
                        ctx->d_hist.as<uint32_t>());
     CORRO_HIP_TRY(hipGetLastError());
     mark(1);
@@ -381,10 +392,17 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
                        ctx->d_state_cnt.as<uint32_t>(), B, ctx->d_stage_off.as<uint32_t>(),
                        ctx->d_out_off.as<uint64_t>());
     mark(3);
-    hipLaunchKernelGGL(k_scatter, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4 + ((B + 31) / 32) * 4, s, bd, tile,
-                       log2B, ctx->d_hist.as<uint32_t>(), ctx->d_stage_off.as<uint32_t>(), ctx->d_stage.as<Rec>(),
-                       ctx->d_bflags.as<uint32_t>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites,
-                       ctx->d_ncols.as<uint16_t>(), (uint32_t)ctx->tables.size(), misc);
+    {
+        static const bool nt_stores = std::getenv("CORRO_HIP_NT") && std::atoi(std::getenv("CORRO_HIP_NT")) != 0;
+        const bool plain = !bd.v1 && !bd.vt && !bd.vl;
+        auto kern = plain ? (nt_stores ? k_scatter<true, true> : k_scatter<true, false>)
+                          : (nt_stores ? k_scatter<false, true> : k_scatter<false, false>);
+        hipLaunchKernelGGL(kern, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4 + ((B + 31) / 32) * 4, s, bd,
+                           tile, log2B, one_table, ctx->d_hist.as<uint32_t>(), ctx->d_stage_off.as<uint32_t>(),
+                           ctx->d_stage.as<Rec>(), ctx->d_bflags.as<uint32_t>(),
+                           ctx->d_dbv_batch.as<unsigned long long>(), nsites, ctx->d_ncols.as<uint16_t>(),
+                           (uint32_t)ctx->tables.size(), misc);
+    }
     CORRO_HIP_TRY(hipGetLastError());
     mark(4);
 
@@ -412,11 +430,13 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     a.force_general = (out && out->impact) ? 1u : 0u;
     a.track_ts = ctx->track_ts ? 1u : 0u;
     a.state_wide = ctx->state_wide ? 1u : 0u;
-    hipLaunchKernelGGL(k_merge_fast<false>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+    a.gen_list = ctx->d_gen_list.as<uint32_t>();
+    a.wide_list = ctx->d_wide_list.as<uint32_t>();
+    hipLaunchKernelGGL(k_merge_fast_int, dim3(B), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_merge_fast<true>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_merge_fast_wide, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_merge_gen, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_merge_gen, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
     mark(5);
     CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, 4 * 8, hipMemcpyDeviceToHost, s));

@@ -90,8 +90,10 @@ struct corro_ctx {
     corro::DevBuf d_hist;         // ntiles x B
     corro::DevBuf d_new_cnt, d_stage_off, d_bflags;
     corro::DevBuf d_stage;        // staged Recs
-    corro::DevBuf d_misc;         // counters: [0] error bits, [1] overflow count, [2] out total, [3] wide flag
+    corro::DevBuf d_misc;         // counters: [0] error bits, [1] overflow count, [2] out total, [3] wide flag, [4] general queue, [5] wide queue
     corro::DevBuf d_ovf_list;     // overflow buckets
+    corro::DevBuf d_gen_list;     // buckets queued for the general body
+    corro::DevBuf d_wide_list;    // buckets queued for the mixed-type fast body
     corro::DevBuf d_ovf_scratch;
     corro::DevBuf d_impact;
     corro::DevBuf d_export;

@@ -10,8 +10,9 @@
 //   k_scatter  re-read the SoA batch, stage each change as one 64-B record in its bucket slice;
 //              per-bucket "general" bits, per-site crsql_db_versions maxima, input validation
 //              (unknown cid / site, out-of-range encodings).
-//   k_merge_fast / k_merge_gen   one workgroup per bucket: prior clock rows of the bucket (as a
-//              prefix of the application order) + its staged changes ->
+//   k_merge_fast_int (one workgroup per bucket) triages buckets and runs the INTEGER fast body;
+//   k_merge_fast_wide / k_merge_gen work through the queues it fills. Per bucket: prior clock rows
+//              of the bucket (as a prefix of the application order) + its staged changes ->
 //                fast  (all rows cl = 1, no sentinels): per-cell argmax of
 //                      (col_version, value, site_id rank, -position) by LDS 64-bit atomic-max
 //                      stages; order independent (SURVEY App. A.2 reduction). 2 WGs/CU.
@@ -25,6 +26,7 @@
 namespace corro {
 
 constexpr int HIST_THREADS = 512;
+constexpr uint32_t TILES_MAX = 256;                    // hist/scatter tiles: one per CU
 constexpr int MERGE_THREADS = 512;
 constexpr int FAST_R = 6;                              // records per thread, fast body
 constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 3072
@@ -53,7 +55,10 @@ struct MergeArgs {
     uint32_t nsites;
     uint8_t *impact;
     unsigned long long *misc;  // [0] error bits [1] overflow buckets [2] rows written [3] wide values
+                               // [4] general buckets [5] wide fast buckets
     uint32_t *ovf_list;
+    uint32_t *gen_list;        // buckets for k_merge_gen (pushed by k_merge_fast_int)
+    uint32_t *wide_list;       // buckets for k_merge_fast_wide
     uint32_t force_general;
     uint32_t track_ts;
     uint32_t state_wide;       // prior state holds non-INTEGER values
@@ -107,9 +112,11 @@ __device__ inline uint32_t site_rank_of(const MergeArgs &a, uint32_t site) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Tile histogram of row buckets. Reads only pk + table_cid (12 B per change).
+// Tile histogram of row buckets. Reads only pk + table_cid (12 B per change), or only pk when the
+// schema has one table (every change's bucket then uses table 0; k_scatter does the same and
+// reports a bad table id as an error).
 __global__ void __launch_bounds__(HIST_THREADS)
-k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t *__restrict__ hist_out) {
+k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t *__restrict__ hist_out) {
     extern __shared__ uint32_t hist[];
     const uint32_t B = 1u << log2B;
     for (uint32_t i = threadIdx.x; i < B; i += blockDim.x) hist[i] = 0;
@@ -117,18 +124,17 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t *__restrict__ hist_o
     const uint32_t begin = blockIdx.x * tile;
     const uint32_t end = min(in.n, begin + tile);
     // HIST_U changes per lane in flight: one CU holds a single 128-KB-LDS workgroup, so memory
-    // level parallelism has to come from each lane
+    // level parallelism has to come from each lane. Loads are unconditional (clamped index) so
+    // that all of them are issued before the first wait.
     constexpr int HIST_U = 8;
     for (uint32_t base = begin; base < end; base += blockDim.x * HIST_U) {
         uint64_t pk[HIST_U];
         uint32_t tc[HIST_U];
 #pragma unroll
         for (int k = 0; k < HIST_U; k++) {
-            const uint32_t i = base + k * blockDim.x + threadIdx.x;
-            if (i < end) {
-                pk[k] = in.pk[i];
-                tc[k] = in.tcid[i];
-            }
+            const uint32_t i = min(base + k * blockDim.x + threadIdx.x, end - 1);
+            pk[k] = in.pk[i];
+            tc[k] = one_table ? 0u : in.tcid[i];
         }
 #pragma unroll
         for (int k = 0; k < HIST_U; k++) {
@@ -167,67 +173,90 @@ __global__ void k_colscan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t
     new_cnt[b] = run;
 }
 
-// one 1024-thread workgroup: stage_off = excl-scan(new_cnt); out_off = excl-scan(prior + 2*new)
+// one 1024-thread workgroup: stage_off = excl-scan(new_cnt); out_off = excl-scan(prior + 2*new).
+// Every lane sums its run of `per` consecutive buckets with all loads issued at once (one memory
+// latency for the whole scan), the lane sums are scanned by wave shuffles + one LDS round, and the
+// lane re-reads its run (L2-resident now) to write the offsets.
+constexpr uint32_t PLAN_PER = 32;  // B <= 1024 * PLAN_PER = 2^15 (B is a power of two)
 __global__ void __launch_bounds__(1024)
 k_plan(const uint32_t *__restrict__ new_cnt, const uint32_t *__restrict__ prior_cnt, uint32_t B,
        uint32_t *__restrict__ stage_off, uint64_t *__restrict__ out_off) {
-    // chunks of 4096 buckets: 4 consecutive buckets per lane (coalesced 16-B loads), wave scans
-    // by shuffles, one LDS round for the 16 wave totals, a running carry across chunks
     __shared__ uint64_t w_a[16], w_b[16];
-    __shared__ uint64_t carry_a, carry_b;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) carry_a = carry_b = 0;
+    // B is a power of two: runs of per = B / 1024 buckets (16-B aligned when per >= 4)
+    const uint32_t per = B >= 1024 ? B / 1024 : 1u;  // <= PLAN_PER
+    const uint32_t b0 = threadIdx.x * per;
+    const uint32_t cnt = b0 < B ? per : 0u;
+    uint64_t sa = 0, sb = 0;
+    if (per >= 4) {
+        uint4 x[PLAN_PER / 4], y[PLAN_PER / 4];
+#pragma unroll
+        for (uint32_t k = 0; k < PLAN_PER / 4; k++) {
+            const uint32_t kk = min(k, per / 4 - 1);
+            x[k] = reinterpret_cast<const uint4 *>(new_cnt + b0)[kk];
+            y[k] = reinterpret_cast<const uint4 *>(prior_cnt + b0)[kk];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PLAN_PER / 4; k++)
+            if (4 * k < per) {
+                sa += (uint64_t)x[k].x + x[k].y + x[k].z + x[k].w;
+                sb += (uint64_t)y[k].x + y[k].y + y[k].z + y[k].w;
+            }
+        sb += 2 * sa;
+    } else {
+        for (uint32_t k = 0; k < cnt; k++) {
+            sa += new_cnt[b0 + k];
+            sb += (uint64_t)prior_cnt[b0 + k] + 2ULL * new_cnt[b0 + k];
+        }
+    }
+    uint64_t ia = sa, ib = sb;  // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t xa = __shfl_up(ia, d), xb = __shfl_up(ib, d);
+        if (lane >= (uint32_t)d) {
+            ia += xa;
+            ib += xb;
+        }
+    }
+    if (lane == 63) {
+        w_a[w] = ia;
+        w_b[w] = ib;
+    }
     __syncthreads();
-    for (uint32_t c0 = 0; c0 < B; c0 += 4096) {
-        const uint32_t b0 = c0 + 4 * threadIdx.x;
-        uint32_t nc[4] = {0, 0, 0, 0}, pc[4] = {0, 0, 0, 0};
+    uint64_t ra = ia - sa, rb = ib - sb;
+    for (uint32_t ww = 0; ww < w; ww++) {
+        ra += w_a[ww];
+        rb += w_b[ww];
+    }
+    if (per >= 4) {
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (b0 + k < B) {
-                nc[k] = new_cnt[b0 + k];
-                pc[k] = prior_cnt[b0 + k];
-            }
-        uint64_t sa = 0, sb = 0;
+        for (uint32_t k = 0; k < PLAN_PER / 4; k++) {
+            if (4 * k >= per) break;
+            // re-read the run (L2-resident): holding it across the scan would spill
+            const uint4 xk = reinterpret_cast<const uint4 *>(new_cnt + b0)[k];
+            const uint4 yk = reinterpret_cast<const uint4 *>(prior_cnt + b0)[k];
+            const uint32_t xs[4] = {xk.x, xk.y, xk.z, xk.w}, ys[4] = {yk.x, yk.y, yk.z, yk.w};
+            uint32_t so[4];
+            uint64_t oo[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            sa += nc[k];
-            sb += (uint64_t)pc[k] + 2ULL * nc[k];
-        }
-        uint64_t ia = sa, ib = sb;  // inclusive wave scan
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t xa = __shfl_up(ia, d), xb = __shfl_up(ib, d);
-            if (lane >= (uint32_t)d) {
-                ia += xa;
-                ib += xb;
+            for (int e = 0; e < 4; e++) {
+                so[e] = (uint32_t)ra;
+                oo[e] = rb;
+                ra += xs[e];
+                rb += (uint64_t)ys[e] + 2ULL * xs[e];
             }
+            reinterpret_cast<uint4 *>(stage_off + b0)[k] = make_uint4(so[0], so[1], so[2], so[3]);
+            reinterpret_cast<ulonglong2 *>(out_off + b0)[2 * k] = make_ulonglong2(oo[0], oo[1]);
+            reinterpret_cast<ulonglong2 *>(out_off + b0)[2 * k + 1] = make_ulonglong2(oo[2], oo[3]);
         }
-        if (lane == 63) {
-            w_a[w] = ia;
-            w_b[w] = ib;
+    } else {
+        for (uint32_t k = 0; k < cnt; k++) {
+            const uint32_t xn = new_cnt[b0 + k], yp = prior_cnt[b0 + k];
+            stage_off[b0 + k] = (uint32_t)ra;
+            out_off[b0 + k] = rb;
+            ra += xn;
+            rb += (uint64_t)yp + 2ULL * xn;
         }
-        __syncthreads();
-        uint64_t ra = carry_a + ia - sa, rb = carry_b + ib - sb;
-        for (uint32_t ww = 0; ww < w; ww++) {
-            ra += w_a[ww];
-            rb += w_b[ww];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (b0 + k < B) {
-                stage_off[b0 + k] = (uint32_t)ra;
-                out_off[b0 + k] = rb;
-                ra += nc[k];
-                rb += (uint64_t)pc[k] + 2ULL * nc[k];
-            }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int ww = 0; ww < 16; ww++) {
-                carry_a += w_a[ww];
-                carry_b += w_b[ww];
-            }
-        }
-        __syncthreads();
     }
 }
 
@@ -265,6 +294,7 @@ __device__ inline void swap16(uint32_t &a, uint32_t &b) {
     a = r[0];
     b = r[1];
 }
+template <bool NT = false>
 __device__ inline void store_rec_wave(Rec *base, uint32_t idx, const Rec &r, bool valid) {
     uint4 q[4];
     const uint4 *src = reinterpret_cast<const uint4 *>(&r);
@@ -284,7 +314,16 @@ __device__ inline void store_rec_wave(Rec *base, uint32_t idx, const Rec &r, boo
         const int srcl = (int)l + 16 * k;
         const uint32_t sidx = __shfl(idx, srcl);
         const int sv = __shfl(v, srcl);
-        if (sv) reinterpret_cast<uint4 *>(base + sidx)[j] = q[k];
+        if (sv) {
+            uint4 *dst = reinterpret_cast<uint4 *>(base + sidx) + j;
+            if (NT) {
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                const v4u t = {q[k].x, q[k].y, q[k].z, q[k].w};
+                __builtin_nontemporal_store(t, reinterpret_cast<v4u *>(dst));
+            } else {
+                *dst = q[k];
+            }
+        }
     }
 }
 
@@ -299,8 +338,11 @@ __device__ inline unsigned long long wave_max_u64(unsigned long long x) {
 
 // Stage every change of the tile as one 64-B record in its bucket slice. Also: per-bucket
 // "general" bits (a change with cl != 1 or a sentinel), crsql_db_versions maxima and validation.
+// PLAIN: the batch has no val1/val_type/val_len arrays (INTEGER values) -- loads are unconditional
+// (clamped) so all of an iteration's loads are in flight together. NT: non-temporal record stores.
+template <bool PLAIN, bool NT>
 __global__ void __launch_bounds__(HIST_THREADS)
-k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict__ hist_off,
+k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const uint32_t *__restrict__ hist_off,
           const uint32_t *__restrict__ stage_off, Rec *__restrict__ stage, uint32_t *__restrict__ bflags,
           unsigned long long *__restrict__ dbv_batch, uint32_t nsites, const uint16_t *__restrict__ ncols,
           uint32_t ntables, unsigned long long *misc) {
@@ -324,8 +366,39 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict
     // workgroup per CU, so memory-level parallelism must come from each lane)
     constexpr int SCAT_U = 4;
     // (tiles start at multiples of 2 * blockDim.x, so pairs (2t, 2t+1) are 16-B aligned)
+    // the PLAIN path needs an even tile length (pairs never straddle the tile end)
+    const bool plain = PLAIN && ((end - begin) & 1u) == 0;
     for (uint32_t base = begin; base < end; base += blockDim.x * SCAT_U) {
         Rec rr[SCAT_U];
+        if (plain) {
+#pragma unroll
+            for (int p = 0; p < SCAT_U / 2; p++) {
+                const uint32_t i = base + p * 2 * blockDim.x + 2 * threadIdx.x;
+                const uint32_t ic = min(i, end - 2);
+                Rec &a = rr[2 * p], &b = rr[2 * p + 1];
+                const ulonglong2 pk = *reinterpret_cast<const ulonglong2 *>(in.pk + ic);
+                const longlong2 cv = *reinterpret_cast<const longlong2 *>(in.cv + ic);
+                const longlong2 dbv = *reinterpret_cast<const longlong2 *>(in.dbv + ic);
+                const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(in.v0 + ic);
+                const uint2 tc = *reinterpret_cast<const uint2 *>(in.tcid + ic);
+                const uint2 cl = *reinterpret_cast<const uint2 *>(in.cl + ic);
+                const uint2 sq = *reinterpret_cast<const uint2 *>(in.seq + ic);
+                const uint2 st = *reinterpret_cast<const uint2 *>(in.site + ic);
+                const bool ok = i < end;
+                a.pk = pk.x; b.pk = pk.y;
+                a.cv = cv.x; b.cv = cv.y;
+                a.dbv = ok ? dbv.x : 0; b.dbv = ok ? dbv.y : 0;
+                a.v0 = v0.x; b.v0 = v0.y;
+                a.v1 = b.v1 = 0;
+                a.tcid = tc.x; b.tcid = tc.y;
+                a.cl = cl.x; b.cl = cl.y;
+                a.seq = sq.x; b.seq = sq.y;
+                a.site = ok ? st.x : 0xFFFFFFFFu; b.site = ok ? st.y : 0xFFFFFFFFu;
+                a.meta = b.meta = (uint32_t)CORRO_INTEGER;
+                a.pos = BATCH_POS | i;
+                b.pos = BATCH_POS | (i + 1);
+            }
+        } else {
 #pragma unroll
         for (int p = 0; p < SCAT_U / 2; p++) {
             // each lane loads two consecutive changes with 16-B (8-B for 32-bit fields) accesses
@@ -375,6 +448,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict
                 a.meta = in.vt ? ((uint32_t)in.vt[i] | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8)) : (uint32_t)CORRO_INTEGER;
             }
         }
+        }
 #pragma unroll
         for (int u = 0; u < SCAT_U; u++) {
             const uint32_t i = base + (u / 2) * 2 * blockDim.x + 2 * threadIdx.x + (u & 1);
@@ -384,7 +458,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict
             if (act) {
                 const uint32_t ty = vtype(r.meta), ln = vlen(r.meta);
                 const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
-                const uint32_t b = bucket_of(t, r.pk, log2B);
+                const uint32_t b = bucket_of(one_table ? 0u : t, r.pk, log2B);
                 idx = atomicAdd(&cur[b], 1u);
                 if (r.cl != 1u || cid == 0) atomicOr(&fl[b >> 5], 1u << (b & 31));
                 if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
@@ -398,7 +472,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, const uint32_t *__restrict
                     if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) err |= ERR_VALUE;
                 }
             }
-            store_rec_wave(stage, idx, r, act);
+            store_rec_wave<NT>(stage, idx, r, act);
             // db_versions
             const uint32_t site0 = __shfl(r.site, 0);
             const unsigned long long dv = act ? (unsigned long long)r.dbv + 1ULL : 0ULL;
@@ -449,6 +523,34 @@ __device__ inline Rec load_rec_wave(const BucketView &v, uint32_t wave_base, uin
         const uint32_t ri = wave_base + l + 16 * k;
         q[k] = ri < n ? reinterpret_cast<const uint4 *>(v.at(ri))[j] : make_uint4(0, 0, 0, 0);
     }
+    swap32(q[0].x, q[2].x); swap32(q[0].y, q[2].y); swap32(q[0].z, q[2].z); swap32(q[0].w, q[2].w);
+    swap32(q[1].x, q[3].x); swap32(q[1].y, q[3].y); swap32(q[1].z, q[3].z); swap32(q[1].w, q[3].w);
+    swap16(q[0].x, q[1].x); swap16(q[0].y, q[1].y); swap16(q[0].z, q[1].z); swap16(q[0].w, q[1].w);
+    swap16(q[2].x, q[3].x); swap16(q[2].y, q[3].y); swap16(q[2].z, q[3].z); swap16(q[2].w, q[3].w);
+    Rec r;
+    uint4 *d = reinterpret_cast<uint4 *>(&r);
+    d[0] = q[0];
+    d[1] = q[1];
+    d[2] = q[2];
+    d[3] = q[3];
+    return r;
+}
+
+// Issue-only half of load_rec_wave: the four coalesced 16-B loads of lane L for records
+// [wave_base, wave_base + 64), with the record index clamped to n - 1 (no branch, so a caller can
+// issue the loads of several groups before the first wait). rec_from_wave_quads finishes the job.
+__device__ inline void load_rec_wave_raw(const BucketView &v, uint32_t wave_base, uint32_t n, uint4 q[4]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = lane >> 4, l = lane & 15;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t ri = min(wave_base + l + 16 * k, n - 1);
+        const Rec *p = ri < v.np ? v.prior + ri : v.fresh + (ri - v.np);
+        q[k] = reinterpret_cast<const uint4 *>(p)[j];
+    }
+}
+
+__device__ inline Rec rec_from_wave_quads(uint4 q[4]) {
     swap32(q[0].x, q[2].x); swap32(q[0].y, q[2].y); swap32(q[0].z, q[2].z); swap32(q[0].w, q[2].w);
     swap32(q[1].x, q[3].x); swap32(q[1].y, q[3].y); swap32(q[1].z, q[3].z); swap32(q[1].w, q[3].w);
     swap16(q[0].x, q[1].x); swap16(q[0].y, q[1].y); swap16(q[0].z, q[1].z); swap16(q[0].w, q[1].w);
@@ -715,61 +817,50 @@ __device__ inline void push_overflow(const MergeArgs &a, uint32_t b) {
 // for the output. LDS: cell keys + one stage array + the open-addressing cell table (76 KB, two
 // workgroups per CU).
 template <bool WIDE>
-__global__ void __launch_bounds__(MERGE_THREADS, 4)
-k_merge_fast(MergeArgs a) {
+__device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketView &v) {
     __shared__ uint64_t s_pk[CAP_FAST];
     __shared__ uint64_t s_k[CAP_FAST];
     __shared__ uint32_t s_tc[CAP_FAST];
     __shared__ uint32_t s_own[FAST_SLOTS];
     __shared__ uint32_t s_outcnt;
-    const uint32_t b = blockIdx.x;
     const uint32_t tid = threadIdx.x;
-    BucketView v;
-    bucket_view(a, b, v);
     const uint32_t n = v.np + v.nn;
-    if (n == 0) {
-        if (tid == 0) {
-            a.out_cnt[b] = 0;
-            a.out_flags[b] = 0;
-        }
-        return;
-    }
-    if (bucket_general(a, b)) return;  // k_merge_gen
-    // two instantiations are launched; the one matching the batch's value classes runs
-    const bool wide = a.state_wide || a.misc[3] != 0;
-    if (wide != WIDE) return;
-    if (n > (uint32_t)CAP_FAST) {
-        if (tid == 0) push_overflow(a, b);
-        return;
-    }
     Rec *outb = a.out + a.out_off[b];
     uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
     uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], rp[FAST_R], dbv[FAST_R];
     uint32_t meta[FAST_R], cell[FAST_R], seq[FAST_R], site[FAST_R];
     bool alive[FAST_R];
+    // every record load of this lane is issued before the first wait (one memory latency per
+    // bucket instead of one per record group), then the site-rank lookups as one more batch
+    uint4 q[FAST_R][4];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
     if (tid == 0) s_outcnt = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    uint32_t srank[FAST_R];
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * MERGE_THREADS + tid;  // < CAP_FAST: stores of dead lanes are harmless
         alive[k] = i < n;
         cell[k] = 0;
-        const Rec r = load_rec_wave(v, k * MERGE_THREADS + (tid & ~63u), n);
-        if (alive[k]) {
-            s_pk[i] = r.pk;
-            s_tc[i] = r.tcid;
-            cv[k] = (uint64_t)r.cv ^ 0x8000000000000000ULL;
-            v0[k] = r.v0;
-            v1[k] = WIDE ? r.v1 : 0;
-            meta[k] = WIDE ? r.meta : (uint32_t)CORRO_INTEGER;
-            rp[k] = ((uint64_t)site_rank_of(a, r.site) << 32) | (uint64_t)(~r.pos);
-            if (!WIDE) {  // INTEGER-only: keep the whole clock row in registers (no re-read)
-                dbv[k] = (uint64_t)r.dbv;
-                seq[k] = r.seq;
-                site[k] = r.site;
-            }
+        const Rec r = rec_from_wave_quads(q[k]);
+        s_pk[i] = r.pk;
+        s_tc[i] = r.tcid;
+        cv[k] = (uint64_t)r.cv ^ 0x8000000000000000ULL;
+        v0[k] = r.v0;
+        v1[k] = WIDE ? r.v1 : 0;
+        meta[k] = WIDE ? r.meta : (uint32_t)CORRO_INTEGER;
+        rp[k] = (uint64_t)(~r.pos);
+        site[k] = r.site;
+        if (!WIDE) {  // INTEGER-only: keep the whole clock row in registers (no re-read)
+            dbv[k] = (uint64_t)r.dbv;
+            seq[k] = r.seq;
         }
     }
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) srank[k] = a.site_rank[site[k] < a.nsites ? site[k] : 0u];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) rp[k] |= (uint64_t)(site[k] < a.nsites ? srank[k] : 0u) << 32;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -865,17 +956,70 @@ k_merge_fast(MergeArgs a) {
     }
 }
 
-// General body in LDS: sort (row, position), one lane per row folds the cr-sqlite rules.
-__global__ void __launch_bounds__(MERGE_THREADS)
-k_merge_gen(MergeArgs a) {
+// Bucket triage + the INTEGER fast body (one workgroup per bucket). General buckets and, for a
+// batch with non-INTEGER values, every fast bucket are queued for the list-driven kernels below,
+// so those launch a few hundred workgroups instead of one per bucket.
+__global__ void __launch_bounds__(MERGE_THREADS, 4)
+k_merge_fast_int(MergeArgs a) {
+    const uint32_t b = blockIdx.x;
+    // every per-bucket word is loaded up front (independent scalar loads, one latency)
+    BucketView v;
+    v.np = a.prior_cnt[b];
+    v.nn = a.new_cnt[b];
+    const uint64_t poff = a.prior_off[b];
+    const uint32_t soff = a.stage_off[b];
+    const uint32_t pflag = a.prior_flags[b];
+    const uint32_t bword = a.bflags[b >> 5];
+    const unsigned long long wide = a.misc[3];
+    v.prior = a.prior + poff;
+    v.fresh = a.stage + soff;
+    v.prior_ts = a.prior_ts ? a.prior_ts + poff : nullptr;
+    const uint32_t n = v.np + v.nn;
+    if (n == 0) {
+        if (threadIdx.x == 0) {
+            a.out_cnt[b] = 0;
+            a.out_flags[b] = 0;
+        }
+        return;
+    }
+    if (a.force_general || pflag || ((bword >> (b & 31)) & 1u)) {
+        if (threadIdx.x == 0) a.gen_list[atomicAdd(&a.misc[4], 1ULL)] = b;
+        return;
+    }
+    if (n > (uint32_t)CAP_FAST) {
+        if (threadIdx.x == 0) push_overflow(a, b);
+        return;
+    }
+    if (a.state_wide || wide != 0) {
+        if (threadIdx.x == 0) a.wide_list[atomicAdd(&a.misc[5], 1ULL)] = b;
+        return;
+    }
+    fast_body<false>(a, b, v);
+}
+
+constexpr uint32_t LIST_GRID = 512;
+
+__global__ void __launch_bounds__(MERGE_THREADS, 4)
+k_merge_fast_wide(MergeArgs a) {
+    const uint32_t cnt = (uint32_t)a.misc[5];
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+        const uint32_t b = a.wide_list[k];
+        BucketView v;
+        bucket_view(a, b, v);
+        fast_body<true>(a, b, v);
+        __syncthreads();
+    }
+}
+
+// General body in LDS for one queued bucket: sort (row, position), one lane per row folds the
+// cr-sqlite rules. Buckets larger than LDS are passed on to k_merge_ovf.
+__device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[GEN_LDS];
     __shared__ uint32_t s_outcnt, s_flag;
-    const uint32_t b = blockIdx.x;
     const uint32_t tid = threadIdx.x;
     BucketView v;
     bucket_view(a, b, v);
     const uint32_t n = v.np + v.nn;
-    if (n == 0 || !bucket_general(a, b)) return;  // k_merge_fast
     if (n > (uint32_t)CAP_GEN) {
         if (tid == 0) push_overflow(a, b);
         return;
@@ -907,6 +1051,15 @@ k_merge_gen(MergeArgs a) {
         a.out_cnt[b] = s_outcnt;
         a.out_flags[b] = s_flag;
         atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+    }
+}
+
+__global__ void __launch_bounds__(MERGE_THREADS)
+k_merge_gen(MergeArgs a) {
+    const uint32_t cnt = (uint32_t)a.misc[4];
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+        gen_bucket(a, a.gen_list[k]);
+        __syncthreads();
     }
 }
 
