@@ -73,7 +73,7 @@ def pmc_traffic_per_apply():
     from collections import defaultdict
     out = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{counter}.csv")))
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_{counter}.csv")))
         if not files:
             return None, None
         tot, disp = defaultdict(float), defaultdict(set)
