@@ -67,15 +67,19 @@ def main():
     eng.set_profiling(True)
     for _ in range(args.warmup):
         res = _needs_device(eng, ent)
-    kt = 0.0
+    kt = kc = kf = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = _needs_device(eng, ent)
         tm = eng.last_timings(apply_only=False)
+        kc += tm["k_needs_count"]
+        kf += tm["k_needs_fill"]
         kt += tm["k_needs_count"] + tm["k_needs_fill"]
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     kt /= args.steps
+    kc /= args.steps
+    kf /= args.steps
     E = int(ent["their_head"].shape[0])
     in_ranges = sum(int(ent[k].shape[0]) for k in ("tn_start", "on_start", "tps_start", "ops_start"))
     pvers = int(ent["tp_ver"].shape[0] + ent["op_ver"].shape[0])
@@ -90,7 +94,7 @@ def main():
             "entries_per_s": E / dt,
             "roofline": {"bound": "hbm", "kernel": "k_needs (count + fill)", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernels_ms": kt},
+                         "kernels_ms": kt, "count_pass_ms": kc, "fill_pass_ms": kf},
             "cpu_baseline": cpu_baseline(ent, min(args.cpu_sample, E))}
     print(json.dumps(line), flush=True)
 

@@ -6,6 +6,7 @@ when no gfx950 device is visible.
 """
 import ctypes as C
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libcorro_hip.so")
@@ -94,6 +95,24 @@ class SyncState(C.Structure):
 _lib = None
 
 
+def _torch_runtime_first():
+    """The PyTorch-ROCm wheel bundles its own HIP/HSA runtime (torch/lib/libamdhip64.so, no
+    soname) next to the system one libcorro_hip.so links (libamdhip64.so.7), so a process that
+    uses both holds two runtimes. They coexist when PyTorch initialises the device first (device
+    pointers are process-wide KFD addresses), but PyTorch cannot find the device once the other
+    runtime has initialised it. So when PyTorch is installed it is imported and initialises the
+    device first; C callers of the library never load it."""
+    import importlib.util
+    if "torch" not in sys.modules and importlib.util.find_spec("torch") is None:
+        return
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:  # noqa: BLE001 -- torch is an optional neighbour, never a requirement
+        pass
+
+
 def lib():
     """Load the in-tree libcorro_hip.so. Raises if it is missing (no fallback)."""
     global _lib
@@ -102,6 +121,7 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: run `python -m corrosion_amd.build` "
                           "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    _torch_runtime_first()
     L = C.CDLL(LIB_PATH)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
     sig = {

@@ -32,9 +32,24 @@ struct SyncDev {
     const uint64_t *ops_off, *ops_start, *ops_end;
 };
 
+// Array views indexed by GLOBAL CSR index k: element k lives at p[k - base] (base = the start of
+// the workgroup's staged segment when p points into LDS, 0 for global memory). The bias is applied
+// to the index, never to the pointer: an LDS pointer moved outside the LDS window is not a valid
+// flat address.
+struct V64 {
+    const uint64_t *p;
+    uint64_t base;
+    __device__ inline uint64_t operator[](uint64_t k) const { return p[k - base]; }
+};
+template <class T> struct WView {
+    T *p;
+    uint64_t base;
+    __device__ inline T &operator[](uint64_t k) const { return p[k - base]; }
+};
+
 // Holes of an entry's version space: their need ranges [tn] and their partial versions [tp].
 struct VerHoles {
-    const uint64_t *hs, *he;  // ranges
+    V64 hs, he;               // ranges
     uint64_t h0, h1;
     const uint64_t *pv;       // points
     uint64_t p0, p1;
@@ -65,7 +80,7 @@ struct VerHoles {
 };
 
 struct SeqHoles {
-    const uint64_t *hs, *he;
+    V64 hs, he;
     uint64_t h0, h1;
     __device__ inline bool covering(uint64_t x, uint64_t &end) const {
         bool hit = false;
@@ -104,98 +119,182 @@ __device__ inline void sweep(const H &holes, uint64_t lo, uint64_t hi, uint64_t 
     }
 }
 
-__global__ void k_needs(SyncDev in, corro_needs_out o, int fill) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= in.n) return;
-    const uint64_t head = in.their_head[e];
-    VerHoles vh{in.tn_start, in.tn_end, in.tn_off[e], in.tn_off[e + 1], in.tp_ver, in.tp_off[e], in.tp_off[e + 1]};
-    uint64_t nn = 0, ns = 0;
-    const uint64_t nbase = fill ? o.need_off[e] : 0, sbase = fill ? o.seq_off[e] : 0;
-    auto full = [&](uint64_t s, uint64_t t) {
-        if (fill) {
-            const uint64_t k = nbase + nn;
-            o.kind[k] = 0;
-            o.start[k] = s;
-            o.end[k] = t;
-            o.sr_off[k] = sbase + ns;
-            o.sr_n[k] = 0;
-        }
-        nn++;
-    };
-    for (uint64_t k = in.on_off[e]; k < in.on_off[e + 1]; k++) sweep(vh, in.on_start[k], in.on_end[k], 1, head, full);
+// One workgroup = NEEDS_T consecutive entries, one lane per entry. The workgroup's CSR segments of
+// their/our need ranges are contiguous, so they are staged into LDS with coalesced 16-B loads
+// (lanes then walk LDS, not scattered global lines); in the fill pass the workgroup's output
+// range [need_off[e0], need_off[e1]) is contiguous too, so outputs are assembled in LDS and
+// written out coalesced. Segments larger than the LDS caps fall back to global memory (same code,
+// generic pointers). Partials (5 % of entries) are read from global memory directly.
+constexpr uint32_t NEEDS_T = 256;
+constexpr uint32_t NEEDS_CAP_R = 640;    // staged ranges per side (avg 2 per entry -> 512, sd ~32)
+constexpr uint32_t NEEDS_CAP_O = 960;    // staged output needs (avg ~2.5 per entry -> ~650); 3 WGs/CU
 
-    for (uint64_t k = in.op_off[e]; k < in.op_off[e + 1]; k++) {
-        const uint64_t v = in.op_ver[k];
-        uint64_t dummy;
-        const bool have = v >= 1 && v <= head && !vh.covering(v, dummy);
-        const uint64_t q0 = in.ops_off[k], q1 = in.ops_off[k + 1];
-        if (have) {
-            if (fill) {
-                const uint64_t q = nbase + nn;
-                o.kind[q] = 1;
-                o.start[q] = v;
-                o.end[q] = v;
-                o.sr_off[q] = sbase + ns;
-                o.sr_n[q] = q1 - q0;
-                for (uint64_t j = q0; j < q1; j++) {
-                    o.s_start[sbase + ns + (j - q0)] = in.ops_start[j];
-                    o.s_end[sbase + ns + (j - q0)] = in.ops_end[j];
-                }
-            }
-            ns += q1 - q0;
-            nn++;
-            continue;
+__device__ inline void stage_ranges(const uint64_t *gs, const uint64_t *ge, uint64_t lo, uint64_t cnt, uint64_t *ls,
+                                    uint64_t *le) {
+    // 16-B loads of pairs of ranges starting at an even global index (the CSR arrays are
+    // 16-B aligned: corro_compute_needs checks device pointers)
+    const uint64_t a0 = lo & ~1ULL;
+    const uint64_t npair = (lo + cnt - a0 + 1) / 2;
+    for (uint64_t q = threadIdx.x; q < npair; q += blockDim.x) {
+        const uint64_t g = a0 + 2 * q;
+        ulonglong2 s2, e2;
+        if (g + 1 < lo + cnt) {  // never read past the segment (it may end the array)
+            s2 = *reinterpret_cast<const ulonglong2 *>(gs + g);
+            e2 = *reinterpret_cast<const ulonglong2 *>(ge + g);
+        } else {
+            s2.x = gs[g];
+            e2.x = ge[g];
+            s2.y = e2.y = 0;
         }
-        int64_t tk = -1;
-        for (uint64_t j = in.tp_off[e]; j < in.tp_off[e + 1]; j++)
-            if (in.tp_ver[j] == v) {
-                tk = (int64_t)j;
-                break;
-            }
-        if (tk < 0) continue;
-        bool have_end = false;
-        uint64_t end = 0;
-        for (uint64_t j = in.tps_off[tk]; j < in.tps_off[tk + 1]; j++)
-            if (!have_end || in.tps_end[j] > end) {
-                end = in.tps_end[j];
-                have_end = true;
-            }
-        for (uint64_t j = q0; j < q1; j++)
-            if (!have_end || in.ops_end[j] > end) {
-                end = in.ops_end[j];
-                have_end = true;
-            }
-        if (!have_end) continue;
-        SeqHoles sh{in.tps_start, in.tps_end, in.tps_off[tk], in.tps_off[tk + 1]};
-        const uint64_t first = sbase + ns;
-        uint64_t cnt = 0;
-        auto piece = [&](uint64_t s, uint64_t t) {
-            if (fill) {
-                o.s_start[first + cnt] = s;
-                o.s_end[first + cnt] = t;
-            }
-            cnt++;
-        };
-        for (uint64_t j = q0; j < q1; j++) sweep(sh, in.ops_start[j], in.ops_end[j], 0, end, piece);
-        if (cnt) {
-            if (fill) {
-                const uint64_t q = nbase + nn;
-                o.kind[q] = 1;
-                o.start[q] = v;
-                o.end[q] = v;
-                o.sr_off[q] = first;
-                o.sr_n[q] = cnt;
-            }
-            nn++;
-            ns += cnt;
+        if (g >= lo && g < lo + cnt) {
+            ls[g - lo] = s2.x;
+            le[g - lo] = e2.x;
+        }
+        if (g + 1 >= lo && g + 1 < lo + cnt) {
+            ls[g + 1 - lo] = s2.y;
+            le[g + 1 - lo] = e2.y;
         }
     }
-    const int64_t ours = in.our_head[e];
-    if (ours < 0) full(1, head);
-    else if (head > (uint64_t)ours) full((uint64_t)ours + 1, head);
-    if (!fill) {
-        o.need_count[e] = nn;
-        o.seq_count[e] = ns;
+}
+
+template <bool FILL>
+__global__ void __launch_bounds__(NEEDS_T) k_needs(SyncDev in, corro_needs_out o) {
+    __shared__ uint64_t l_tns[NEEDS_CAP_R], l_tne[NEEDS_CAP_R], l_ons[NEEDS_CAP_R], l_one[NEEDS_CAP_R];
+    __shared__ uint64_t l_start[FILL ? NEEDS_CAP_O : 1], l_end[FILL ? NEEDS_CAP_O : 1];
+    __shared__ uint64_t l_sro[FILL ? NEEDS_CAP_O : 1], l_srn[FILL ? NEEDS_CAP_O : 1];
+    __shared__ uint8_t l_kind[FILL ? NEEDS_CAP_O : 1];
+    const uint64_t e0 = (uint64_t)blockIdx.x * NEEDS_T;
+    const uint64_t e1 = min(in.n, e0 + NEEDS_T);
+    const uint64_t e = e0 + threadIdx.x;
+    const bool live = e < in.n;
+    // per-lane words first, so their latency overlaps the staging below
+    const uint64_t el = live ? e : e0;
+    const uint64_t head = in.their_head[el];
+    const int64_t ours = in.our_head[el];
+    const uint64_t tne0 = in.tn_off[el], tne1 = in.tn_off[el + 1], one0 = in.on_off[el], one1 = in.on_off[el + 1];
+    const uint64_t tpe0 = in.tp_off[el], tpe1 = in.tp_off[el + 1], ope0 = in.op_off[el], ope1 = in.op_off[el + 1];
+    const uint64_t nbase = FILL ? o.need_off[el] : 0, sbase = FILL ? o.seq_off[el] : 0;
+    // workgroup segments (uniform scalar loads)
+    const uint64_t tn_lo = in.tn_off[e0], tn_hi = in.tn_off[e1];
+    const uint64_t on_lo = in.on_off[e0], on_hi = in.on_off[e1];
+    const bool tn_lds = tn_hi - tn_lo <= NEEDS_CAP_R, on_lds = on_hi - on_lo <= NEEDS_CAP_R;
+    if (tn_lds) stage_ranges(in.tn_start, in.tn_end, tn_lo, tn_hi - tn_lo, l_tns, l_tne);
+    if (on_lds) stage_ranges(in.on_start, in.on_end, on_lo, on_hi - on_lo, l_ons, l_one);
+    uint64_t o_lo = 0, o_hi = 0;
+    bool o_lds = false;
+    if (FILL) {
+        o_lo = o.need_off[e0];
+        o_hi = o.need_off[e1];
+        o_lds = o_hi - o_lo <= NEEDS_CAP_O;
+    }
+    __syncthreads();
+    // views indexed by the global CSR index
+    const V64 tns{tn_lds ? l_tns : in.tn_start, tn_lds ? tn_lo : 0}, tne{tn_lds ? l_tne : in.tn_end, tn_lds ? tn_lo : 0};
+    const V64 ons{on_lds ? l_ons : in.on_start, on_lds ? on_lo : 0}, one{on_lds ? l_one : in.on_end, on_lds ? on_lo : 0};
+    const uint64_t ob = o_lds ? o_lo : 0;
+    const WView<uint8_t> okind{o_lds ? l_kind : o.kind, ob};
+    const WView<uint64_t> ostart{o_lds ? l_start : o.start, ob}, oend{o_lds ? l_end : o.end, ob};
+    const WView<uint64_t> osro{o_lds ? l_sro : o.sr_off, ob}, osrn{o_lds ? l_srn : o.sr_n, ob};
+
+    if (live) {
+        VerHoles vh{tns, tne, tne0, tne1, in.tp_ver, tpe0, tpe1};
+        uint64_t nn = 0, ns = 0;
+        auto full = [&](uint64_t s, uint64_t t) {
+            if (FILL) {
+                const uint64_t k = nbase + nn;
+                okind[k] = 0;
+                ostart[k] = s;
+                oend[k] = t;
+                osro[k] = sbase + ns;
+                osrn[k] = 0;
+            }
+            nn++;
+        };
+        for (uint64_t k = one0; k < one1; k++) sweep(vh, ons[k], one[k], 1, head, full);
+
+        for (uint64_t k = ope0; k < ope1; k++) {
+            const uint64_t v = in.op_ver[k];
+            uint64_t dummy;
+            const bool have = v >= 1 && v <= head && !vh.covering(v, dummy);
+            const uint64_t q0 = in.ops_off[k], q1 = in.ops_off[k + 1];
+            if (have) {
+                if (FILL) {
+                    const uint64_t q = nbase + nn;
+                    okind[q] = 1;
+                    ostart[q] = v;
+                    oend[q] = v;
+                    osro[q] = sbase + ns;
+                    osrn[q] = q1 - q0;
+                    for (uint64_t j = q0; j < q1; j++) {
+                        o.s_start[sbase + ns + (j - q0)] = in.ops_start[j];
+                        o.s_end[sbase + ns + (j - q0)] = in.ops_end[j];
+                    }
+                }
+                ns += q1 - q0;
+                nn++;
+                continue;
+            }
+            int64_t tk = -1;
+            for (uint64_t j = tpe0; j < tpe1; j++)
+                if (in.tp_ver[j] == v) {
+                    tk = (int64_t)j;
+                    break;
+                }
+            if (tk < 0) continue;
+            bool have_end = false;
+            uint64_t end = 0;
+            for (uint64_t j = in.tps_off[tk]; j < in.tps_off[tk + 1]; j++)
+                if (!have_end || in.tps_end[j] > end) {
+                    end = in.tps_end[j];
+                    have_end = true;
+                }
+            for (uint64_t j = q0; j < q1; j++)
+                if (!have_end || in.ops_end[j] > end) {
+                    end = in.ops_end[j];
+                    have_end = true;
+                }
+            if (!have_end) continue;
+            SeqHoles sh{V64{in.tps_start, 0}, V64{in.tps_end, 0}, in.tps_off[tk], in.tps_off[tk + 1]};
+            const uint64_t first = sbase + ns;
+            uint64_t cnt = 0;
+            auto piece = [&](uint64_t s, uint64_t t) {
+                if (FILL) {
+                    o.s_start[first + cnt] = s;
+                    o.s_end[first + cnt] = t;
+                }
+                cnt++;
+            };
+            for (uint64_t j = q0; j < q1; j++) sweep(sh, in.ops_start[j], in.ops_end[j], 0, end, piece);
+            if (cnt) {
+                if (FILL) {
+                    const uint64_t q = nbase + nn;
+                    okind[q] = 1;
+                    ostart[q] = v;
+                    oend[q] = v;
+                    osro[q] = first;
+                    osrn[q] = cnt;
+                }
+                nn++;
+                ns += cnt;
+            }
+        }
+        if (ours < 0) full(1, head);
+        else if (head > (uint64_t)ours) full((uint64_t)ours + 1, head);
+        if (!FILL) {
+            o.need_count[e] = nn;
+            o.seq_count[e] = ns;
+        }
+    }
+    if (FILL && o_lds) {
+        __syncthreads();
+        const uint64_t m = o_hi - o_lo;
+        for (uint64_t k = threadIdx.x; k < m; k += NEEDS_T) {
+            o.start[o_lo + k] = l_start[k];
+            o.end[o_lo + k] = l_end[k];
+            o.sr_off[o_lo + k] = l_sro[k];
+            o.sr_n[o_lo + k] = l_srn[k];
+            o.kind[o_lo + k] = l_kind[k];
+        }
     }
 }
 
@@ -216,6 +315,10 @@ extern "C" int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in,
     d.n = n;
     corro_needs_out od = *out;
     if (mem == CORRO_MEM_DEVICE) {
+        for (const void *q : {(const void *)in->tn_start, (const void *)in->tn_end, (const void *)in->on_start,
+                              (const void *)in->on_end})
+            if (q && ((uintptr_t)q % 16) != 0)
+                return fail(CORRO_E_INVALID, "device need-range arrays must be 16-byte aligned");
         d.their_head = in->their_head; d.our_head = in->our_head;
         d.tn_off = in->tn_off; d.tn_start = in->tn_start; d.tn_end = in->tn_end;
         d.tp_off = in->tp_off; d.tp_ver = in->tp_ver;
@@ -284,11 +387,13 @@ extern "C" int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in,
             od.s_end = (uint64_t *)carve(tseqs * 8);
         }
     }
-    const uint32_t threads = 256;
-    const uint64_t blocks = (n + threads - 1) / threads;
+    const uint64_t blocks = (n + NEEDS_T - 1) / NEEDS_T;
     if (blocks > 0x7FFFFFFFULL) return fail(CORRO_E_RANGE, "too many sync entries");
     if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[0], s));
-    hipLaunchKernelGGL(k_needs, dim3((uint32_t)blocks), dim3(threads), 0, s, d, od, pass);
+    if (pass == 0)
+        hipLaunchKernelGGL(k_needs<false>, dim3((uint32_t)blocks), dim3(NEEDS_T), 0, s, d, od);
+    else
+        hipLaunchKernelGGL(k_needs<true>, dim3((uint32_t)blocks), dim3(NEEDS_T), 0, s, d, od);
     if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
     CORRO_HIP_TRY(hipGetLastError());
     if (mem == CORRO_MEM_HOST) {
