@@ -366,12 +366,16 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     TRY(ctx->d_stage.ensure((size_t)n * sizeof(Rec)));
     TRY(ctx->d_state[nxt].ensure(out_cap * sizeof(Rec)));
     if (ctx->track_ts) TRY(ctx->d_state_ts[nxt].ensure(out_cap * 8));
-    if (out && out->impact) TRY(ctx->d_impact.ensure(n));
+    // impact output: a device batch gets its flags written straight into the caller's device
+    // buffer; a host batch through a device staging buffer + one copy
+    const bool imp_dev = out && out->impact && mem == CORRO_MEM_DEVICE;
+    if (out && out->impact && !imp_dev) TRY(ctx->d_impact.ensure(n));
+    uint8_t *imp_buf = !(out && out->impact) ? nullptr : (imp_dev ? out->impact : ctx->d_impact.as<uint8_t>());
 
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_bflags.p, 0, ((B + 31) / 32) * 4ULL, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_dbv_batch.p, 0, (size_t)nsites * 8, s));
-    if (out && out->impact) CORRO_HIP_TRY(hipMemsetAsync(ctx->d_impact.p, 0, n, s));
+    if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 0, n, s));
 
     unsigned long long *misc = ctx->d_misc.as<unsigned long long>();
     const bool prof = ctx->profiling;
@@ -424,17 +428,26 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     a.out_flags = ctx->d_out_flags.as<uint32_t>();
     a.site_rank = ctx->d_site_rank.as<uint32_t>();
     a.nsites = nsites;
-    a.impact = (out && out->impact) ? ctx->d_impact.as<uint8_t>() : nullptr;
+    a.impact = imp_buf;
     a.misc = misc;
     a.ovf_list = ctx->d_ovf_list.as<uint32_t>();
-    a.force_general = (out && out->impact) ? 1u : 0u;
+    // CORRO_HIP_FORCE_GENERAL=1 sends every bucket through the sequential body (cross-checks)
+    static const bool force_general = std::getenv("CORRO_HIP_FORCE_GENERAL") &&
+                                      std::atoi(std::getenv("CORRO_HIP_FORCE_GENERAL")) != 0;
+    a.force_general = force_general ? 1u : 0u;
     a.track_ts = ctx->track_ts ? 1u : 0u;
     a.state_wide = ctx->state_wide ? 1u : 0u;
     a.gen_list = ctx->d_gen_list.as<uint32_t>();
     a.wide_list = ctx->d_wide_list.as<uint32_t>();
-    hipLaunchKernelGGL(k_merge_fast_int, dim3(B), dim3(MERGE_THREADS), 0, s, a);
-    CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_merge_fast_wide, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+    if (a.impact) {
+        hipLaunchKernelGGL(k_merge_fast_int<true>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+        CORRO_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_merge_fast_wide<true>, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_merge_fast_int<false>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+        CORRO_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_merge_fast_wide<false>, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+    }
     CORRO_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_merge_gen, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
@@ -471,7 +484,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     }
     hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
                        ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites);
-    if (out && out->impact)
+    if (out && out->impact && !imp_dev)
         CORRO_HIP_TRY(hipMemcpyAsync(out->impact, ctx->d_impact.p, n, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
 

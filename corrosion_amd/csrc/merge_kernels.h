@@ -59,7 +59,7 @@ struct MergeArgs {
     uint32_t *ovf_list;
     uint32_t *gen_list;        // buckets for k_merge_gen (pushed by k_merge_fast_int)
     uint32_t *wide_list;       // buckets for k_merge_fast_wide
-    uint32_t force_general;
+    uint32_t force_general;    // route every non-empty bucket through the sequential general body
     uint32_t track_ts;
     uint32_t state_wide;       // prior state holds non-INTEGER values
 };
@@ -956,10 +956,216 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     }
 }
 
+// Same per-cell merge with per-change crsql_rows_impacted() growth (impact output requested: the
+// agent path, util.rs:1246-1262). With every cl = 1 and no sentinel (App. A.1 rule 4 with L <= 1)
+// change i grows the counter by exactly 1 iff it is the first change of its cell in application
+// order or its key (col_version, value, site id) is strictly greater than every earlier one: a
+// strict prefix maximum. The cell's final winner is the maximum key, earliest among equals. Both
+// are decided per change by one walk over the cell's member list (counting sort of the bucket's
+// records by cell in LDS), so no atomic argmax stages are needed. One workgroup per CU (LDS).
+__device__ inline int value_cmp_f(uint32_t ma, uint64_t a0, uint64_t a1, uint32_t mb, uint64_t b0, uint64_t b1) {
+    const uint32_t ta = vtype(ma), tb = vtype(mb);
+    if (ta != tb) return (5 - (int)ta) > (5 - (int)tb) ? 1 : -1;
+    if (ta == CORRO_NULL) return 0;
+    const uint64_t ka = vkey0(ta, a0), kb = vkey0(tb, b0);
+    if (ka != kb) return ka > kb ? 1 : -1;
+    if (ta == CORRO_TEXT || ta == CORRO_BLOB) {
+        if (a1 != b1) return a1 > b1 ? 1 : -1;
+        const uint32_t la = vlen(ma), lb = vlen(mb);
+        if (la != lb) return la > lb ? 1 : -1;
+    }
+    return 0;
+}
+
+template <bool WIDE>
+__device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const BucketView &v) {
+    __shared__ uint64_t s_pk[CAP_FAST];      // cell hashing: pk; then the biased col_version keys
+    __shared__ uint32_t s_tc[CAP_FAST];      // cell hashing: table_cid; then site ranks
+    __shared__ uint32_t s_own[FAST_SLOTS];   // cell hashing: slot owners; then member counts/offsets
+    __shared__ uint64_t s_v0[CAP_FAST];
+    __shared__ uint32_t s_pos[CAP_FAST];
+    __shared__ uint16_t s_list[CAP_FAST];
+    __shared__ uint64_t s_v1[WIDE ? CAP_FAST : 1];
+    __shared__ uint32_t s_meta[WIDE ? CAP_FAST : 1];
+    __shared__ uint32_t s_wsum[MERGE_THREADS / 64];
+    __shared__ uint32_t s_outcnt;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = v.np + v.nn;
+    Rec *outb = a.out + a.out_off[b];
+    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], pk[FAST_R], dbv[FAST_R];
+    uint32_t meta[FAST_R], cell[FAST_R], seq[FAST_R], site[FAST_R], pos[FAST_R], rank[FAST_R], tc[FAST_R];
+    bool alive[FAST_R];
+    uint4 q[FAST_R][4];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    if (tid == 0) s_outcnt = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        alive[k] = i < n;
+        cell[k] = 0;
+        const Rec r = rec_from_wave_quads(q[k]);
+        pk[k] = r.pk;
+        tc[k] = r.tcid;
+        s_pk[i] = r.pk;
+        s_tc[i] = r.tcid;
+        cv[k] = (uint64_t)r.cv ^ 0x8000000000000000ULL;
+        v0[k] = r.v0;
+        v1[k] = WIDE ? r.v1 : 0;
+        meta[k] = WIDE ? r.meta : (uint32_t)CORRO_INTEGER;
+        pos[k] = r.pos;
+        site[k] = r.site;
+        dbv[k] = (uint64_t)r.dbv;
+        seq[k] = r.seq;
+    }
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) rank[k] = a.site_rank[site[k] < a.nsites ? site[k] : 0u];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) rank[k] = site[k] < a.nsites ? rank[k] : 0u;
+    __syncthreads();
+    // 1. cells: open addressing on (pk, table_cid), owner = first claimer
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (!alive[k]) continue;
+        uint32_t slot = cell_hash(pk[k], tc[k]) & (FAST_SLOTS - 1);
+        while (true) {
+            const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
+            if (o == 0) {
+                cell[k] = i;
+                break;
+            }
+            if (s_pk[o - 1] == pk[k] && s_tc[o - 1] == tc[k]) {
+                cell[k] = o - 1;
+                break;
+            }
+            slot = (slot + 1) & (FAST_SLOTS - 1);
+        }
+    }
+    __syncthreads();
+    // 2. member counts per owner (s_own reused), keys into LDS
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (!alive[k]) continue;
+        s_pk[i] = cv[k];
+        s_tc[i] = rank[k];
+        s_v0[i] = v0[k];
+        s_pos[i] = pos[k];
+        if (WIDE) {
+            s_v1[i] = v1[k];
+            s_meta[i] = meta[k];
+        }
+        atomicAdd(&s_own[cell[k]], 1u);
+    }
+    __syncthreads();
+    // 3. exclusive scan of the counts over owner index [0, n): FAST_R consecutive per thread
+    {
+        const uint32_t i0 = tid * FAST_R;
+        uint32_t c[FAST_R], loc = 0;
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            c[k] = i0 + k < n ? s_own[i0 + k] : 0u;
+            loc += c[k];
+        }
+        const uint32_t lane = tid & 63, w = tid >> 6;
+        uint32_t inc = loc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        if (lane == 63) s_wsum[w] = inc;
+        __syncthreads();
+        uint32_t run = inc - loc;
+        for (uint32_t ww = 0; ww < w; ww++) run += s_wsum[ww];
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++)
+            if (i0 + k < n) {
+                s_own[i0 + k] = run;
+                run += c[k];
+            }
+    }
+    __syncthreads();
+    uint32_t mbeg[FAST_R];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) mbeg[k] = alive[k] ? s_own[cell[k]] : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (alive[k]) s_list[atomicAdd(&s_own[cell[k]], 1u)] = (uint16_t)i;
+    }
+    __syncthreads();
+    // 4. one walk over the cell's members per change: impact (strict prefix max) and winner
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (!alive[k]) continue;
+        const uint32_t mend = s_own[cell[k]];
+        bool imp = true, win = true;
+        for (uint32_t m = mbeg[k]; m < mend; m++) {
+            const uint32_t j = s_list[m];
+            if (j == i) continue;
+            int c;
+            const uint64_t cj = s_pk[j];
+            if (cj != cv[k]) {
+                c = cj > cv[k] ? 1 : -1;
+            } else {
+                c = WIDE ? value_cmp_f(s_meta[j], s_v0[j], s_v1[j], meta[k], v0[k], v1[k])
+                         : (s_v0[j] != v0[k] ? (((s_v0[j] ^ 0x8000000000000000ULL) > (v0[k] ^ 0x8000000000000000ULL)) ? 1 : -1) : 0);
+                if (c == 0) {
+                    const uint32_t rj = s_tc[j];
+                    c = rj != rank[k] ? (rj > rank[k] ? 1 : -1) : 0;
+                }
+            }
+            const bool earlier = s_pos[j] < pos[k];
+            if (earlier && c >= 0) imp = false;             // an earlier change already holds >= key
+            if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
+        }
+        if (a.impact && (pos[k] & BATCH_POS)) a.impact[pos[k] & 0x7FFFFFFFu] = imp ? 1 : 0;
+        alive[k] = win;
+    }
+    // 5. winners: the clock row (wave-cooperative 64-B stores)
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        uint32_t o = 0;
+        Rec x;
+        if (alive[k]) {
+            x.pk = pk[k];
+            x.cv = (int64_t)(cv[k] ^ 0x8000000000000000ULL);
+            x.dbv = (int64_t)dbv[k];
+            x.v0 = v0[k];
+            x.v1 = v1[k];
+            x.tcid = tc[k];
+            x.seq = seq[k];
+            x.site = site[k];
+            x.pos = pos[k];
+            x.meta = meta[k];
+            o = atomicAdd(&s_outcnt, 1u);
+            if (a.track_ts) outts[o] = rec_ts(a, v, x);
+            x.cl = 1;
+            x.pos = o;
+        }
+        store_rec_wave(outb, o, x, alive[k]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.out_cnt[b] = s_outcnt;
+        a.out_flags[b] = 0;
+        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+    }
+}
+
 // Bucket triage + the INTEGER fast body (one workgroup per bucket). General buckets and, for a
 // batch with non-INTEGER values, every fast bucket are queued for the list-driven kernels below,
 // so those launch a few hundred workgroups instead of one per bucket.
-__global__ void __launch_bounds__(MERGE_THREADS, 4)
+template <bool IMPACT>
+__global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
 k_merge_fast_int(MergeArgs a) {
     const uint32_t b = blockIdx.x;
     // every per-bucket word is loaded up front (independent scalar loads, one latency)
@@ -994,19 +1200,26 @@ k_merge_fast_int(MergeArgs a) {
         if (threadIdx.x == 0) a.wide_list[atomicAdd(&a.misc[5], 1ULL)] = b;
         return;
     }
-    fast_body<false>(a, b, v);
+    if (IMPACT)
+        fast_body_impact<false>(a, b, v);
+    else
+        fast_body<false>(a, b, v);
 }
 
 constexpr uint32_t LIST_GRID = 512;
 
-__global__ void __launch_bounds__(MERGE_THREADS, 4)
+template <bool IMPACT>
+__global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
 k_merge_fast_wide(MergeArgs a) {
     const uint32_t cnt = (uint32_t)a.misc[5];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
         const uint32_t b = a.wide_list[k];
         BucketView v;
         bucket_view(a, b, v);
-        fast_body<true>(a, b, v);
+        if (IMPACT)
+            fast_body_impact<true>(a, b, v);
+        else
+            fast_body<true>(a, b, v);
         __syncthreads();
     }
 }

@@ -74,7 +74,8 @@ class MergeEngine:
     def apply(self, batch, impact=False):
         """Merge a batch (dict of numpy arrays on the host, or of torch tensors on the GPU).
 
-        Returns the per-change crsql_rows_impacted() growth when impact=True, else None."""
+        Returns the per-change crsql_rows_impacted() growth when impact=True (a numpy array for a
+        host batch, a CUDA uint8 tensor for a device batch), else None."""
         for k in REQUIRED:
             if k not in batch or batch[k] is None:
                 raise ValueError(f"batch lacks required field {k!r}")
@@ -103,8 +104,13 @@ class MergeEngine:
         out = L.ApplyOut()
         imp = None
         if impact:
-            imp = np.zeros(max(n, 1), np.uint8)
-            out.impact = imp.ctypes.data
+            if on_dev:  # device batch -> device impact flags (written in place, no copy)
+                import torch
+                imp = torch.zeros(max(n, 1), dtype=torch.uint8, device=batch["pk"].device)
+                out.impact = imp.data_ptr()
+            else:
+                imp = np.zeros(max(n, 1), np.uint8)
+                out.impact = imp.ctypes.data
         if on_dev:
             import torch
             torch.cuda.current_stream().synchronize()

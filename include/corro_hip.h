@@ -97,7 +97,8 @@ typedef struct {
 
 /* Per-batch outputs (all optional, host pointers, n elements each) */
 typedef struct {
-    /* crsql_rows_impacted() growth caused by each change (0, 1 or 2), util.rs:1246-1260 */
+    /* crsql_rows_impacted() growth caused by each change (0, 1 or 2), util.rs:1246-1260; NULL =
+     * not wanted. Host memory for a CORRO_MEM_HOST batch, device memory for CORRO_MEM_DEVICE. */
     uint8_t *impact;
 } corro_apply_out;
 

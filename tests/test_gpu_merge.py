@@ -268,3 +268,47 @@ def test_config2_distribution_4m_vs_oracle():
     e.apply(dev)
     f.apply(b)
     compare(e, f)
+
+
+@pytest.mark.parametrize("n,npk,seed", [(3000, 200, 31), (60000, 9000, 32), (400000, 100000, 33)])
+def test_uniform_cl1_impacts_fast_path_vs_oracle(n, npk, seed):
+    """cl = 1 batches with impact output take the fast body's member-walk variant (not the
+    sequential body): per-change crsql_rows_impacted growth and the merged state must match the
+    oracle, across batches (prior state as the first member of a cell)."""
+    sites = synth.site_ids(16, seed)
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=n, sites=sites)
+    f = O.Fold(sites)
+    for k in range(3):
+        b = synth.uniform_batch(n, 16, npk, 4, seed * 10 + k)
+        assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+    compare(e, f)
+
+
+def test_wide_cl1_impacts_fast_path_vs_oracle():
+    """Mixed value classes (INTEGER/REAL/TEXT/BLOB/NULL), every cl = 1, no sentinel: the wide fast
+    body with impact output, several batches."""
+    seed = 34
+    sites = synth.site_ids(8, seed)
+    e = engine(synth.adversarial_schema(2), cap=40000, sites=sites)
+    f = O.Fold(sites)
+    for k in range(3):
+        b = synth.adversarial_batch(40000, 8, 2, 3000, seed + k, zipf=0, sentinel_frac=0.0, max_cl=1)
+        assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+    compare(e, f, with_ts=True)
+
+
+def test_device_batch_device_impacts_vs_oracle():
+    """Device-resident batch with impact output: the flags land in a device tensor (no copy)."""
+    import torch
+    seed = 35
+    sites = synth.site_ids(16, seed)
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=200000, sites=sites)
+    f = O.Fold(sites)
+    for k in range(2):
+        b = synth.uniform_batch(200000, 16, 30000, 4, seed + k)
+        dev = {key: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                                     (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda() for key, v in b.items()}
+        imp = e.apply(dev, impact=True)
+        assert imp.is_cuda and imp.dtype == torch.uint8
+        assert np.array_equal(imp.cpu().numpy(), f.apply(b))
+    compare(e, f)

@@ -79,3 +79,34 @@ def test_sync_device_resident_config4_shape_vs_oracle():
     exp = O.needs(host)
     for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
         assert np.array_equal(got[k].cpu().numpy().astype(np.uint64), exp[k].astype(np.uint64)), k
+
+
+def _dense_side(rng, nranges, head):
+    need, x = [], 1
+    for _ in range(nranges):
+        s = x + int(rng.integers(1, 4))
+        e = s + int(rng.integers(0, 3))
+        need.append([s, e])
+        x = e + 2
+    return {"head": head, "need": need, "partials": {}}
+
+
+@pytest.mark.parametrize("dense", ["theirs", "ours", "both"])
+def test_sync_lds_caps_exceeded_vs_oracle(dense):
+    """Workgroups whose staged need ranges (> 640 per side) or outputs (> 960 needs) exceed the LDS
+    caps of k_needs take the global-memory path; mixed with normal workgroups in one launch."""
+    rng = np.random.default_rng(11)
+    pairs = []
+    for i in range(1200):
+        heavy = 256 <= i < 768  # two whole workgroups of heavy entries
+        nt = 12 if heavy and dense in ("theirs", "both") else int(rng.poisson(2))
+        no = 12 if heavy and dense in ("ours", "both") else int(rng.poisson(2))
+        their = _dense_side(rng, nt, 300)
+        our = _dense_side(rng, no, int(rng.integers(1, 100)))
+        pairs.append((our, their))
+    ent = entries_from_pairs(pairs)
+    e = _engine()
+    got = e.compute_needs(ent)
+    exp = O.needs(ent)
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        assert np.array_equal(got[k], exp[k]), k
