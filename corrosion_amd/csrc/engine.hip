@@ -56,6 +56,84 @@ using namespace corro;
         if (rc_ != CORRO_OK) return rc_; \
     } while (0)
 
+namespace corro {
+int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t *ko, const uint32_t *vi,
+                   uint32_t *vo, uint32_t n, uint32_t end_bit, hipStream_t s);
+
+// Oversized buckets (after the first merge pass queued them): prep -> device-wide sort by (bucket
+// base + row, position) -> parallel row fold -> [sort of the candidates -> impacts].
+static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) {
+    hipStream_t s = ctx->stream;
+    const uint32_t B = ctx->B;
+    std::vector<uint32_t> list(novf), pc(B), nc(B);
+    CORRO_HIP_TRY(hipMemcpy(list.data(), ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost));
+    CORRO_HIP_TRY(hipMemcpy(pc.data(), ctx->d_state_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
+    CORRO_HIP_TRY(hipMemcpy(nc.data(), ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> soff(novf);
+    std::vector<uint32_t> kb(novf);
+    uint64_t tot = 0, keys = 0;
+    for (uint64_t k = 0; k < novf; k++) {
+        const uint64_t n = (uint64_t)pc[list[k]] + nc[list[k]];
+        soff[k] = tot;
+        tot += ovf_scratch_bytes(n);
+        kb[k] = (uint32_t)keys;
+        keys += n;
+        if (keys >= (1ULL << 31)) return fail(CORRO_E_RANGE, "oversized buckets hold more than 2^31 records");
+    }
+    // key high halves are < keys; one spare value above them so ~0 (not a candidate) sorts last
+    uint32_t end_bit = 33;
+    while ((1ULL << (end_bit - 32)) <= keys) end_bit++;
+    size_t temp = 0;
+    TRY(ovf_sort_pairs(nullptr, &temp, nullptr, nullptr, nullptr, nullptr, (uint32_t)keys, end_bit, s));
+    auto al = [](uint64_t x) { return (x + 255) & ~255ULL; };
+    const uint64_t sort_bytes = 4 * al(keys * 8) + 4 * al(keys * 4) + al(novf * 8) + 2 * al(novf * 4) + al(temp);
+    TRY(ctx->d_ovf_scratch.ensure(tot + 256));
+    TRY(ctx->d_ovf_sort.ensure(sort_bytes + 256));
+    uint8_t *q = ctx->d_ovf_sort.as<uint8_t>();
+    auto carve = [&](uint64_t bytes) {
+        uint8_t *r = q;
+        q += al(bytes);
+        return r;
+    };
+    OvfArgs o{};
+    o.scratch = ctx->d_ovf_scratch.as<uint8_t>();
+    o.key = (uint64_t *)carve(keys * 8);
+    o.key_s = (uint64_t *)carve(keys * 8);
+    o.ckey = (uint64_t *)carve(keys * 8);
+    o.ckey_s = (uint64_t *)carve(keys * 8);
+    o.val = (uint32_t *)carve(keys * 4);
+    o.val_s = (uint32_t *)carve(keys * 4);
+    o.cval = (uint32_t *)carve(keys * 4);
+    o.cval_s = (uint32_t *)carve(keys * 4);
+    uint64_t *d_soff = (uint64_t *)carve(novf * 8);
+    uint32_t *d_kb = (uint32_t *)carve(novf * 4);
+    o.ccnt = (uint32_t *)carve(novf * 4);
+    void *d_temp = carve(temp);
+    o.soff = d_soff;
+    o.koff = d_kb;
+    CORRO_HIP_TRY(hipMemcpyAsync(d_soff, soff.data(), novf * 8, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(d_kb, kb.data(), novf * 4, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemsetAsync(o.ccnt, 0, novf * 4, s));
+    if (prof) (void)hipEventRecord(ctx->ev[6], s);
+    const dim3 grid((uint32_t)novf), blk(OVF_THREADS);
+    hipLaunchKernelGGL(k_ovf_prep, grid, blk, 0, s, a, o);
+    CORRO_HIP_TRY(hipGetLastError());
+    TRY(ovf_sort_pairs(d_temp, &temp, o.key, o.key_s, o.val, o.val_s, (uint32_t)keys, end_bit, s));
+    hipLaunchKernelGGL(k_ovf_fold_a, grid, blk, 0, s, a, o);
+    CORRO_HIP_TRY(hipGetLastError());
+    if (a.impact) {
+        TRY(ovf_sort_pairs(d_temp, &temp, o.ckey, o.ckey_s, o.cval, o.cval_s, (uint32_t)keys, end_bit, s));
+        hipLaunchKernelGGL(k_ovf_fold_b, grid, blk, 0, s, a, o);
+        CORRO_HIP_TRY(hipGetLastError());
+    }
+    if (prof) (void)hipEventRecord(ctx->ev[7], s);
+    CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, a.misc, 4 * 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (prof) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[5], ctx->ev[6], ctx->ev[7]));
+    return CORRO_OK;
+}
+}  // namespace corro
+
 extern "C" {
 
 const char *corro_last_error(void) { return g_last_error.c_str(); }
@@ -175,7 +253,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_state_ts[0], &ctx->d_state_ts[1], &ctx->d_state_off, &ctx->d_state_cnt,
                       &ctx->d_state_flags, &ctx->d_out_off, &ctx->d_out_cnt, &ctx->d_out_flags, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_scratch, &ctx->d_impact, &ctx->d_export,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_scratch, &ctx->d_ovf_sort, &ctx->d_impact, &ctx->d_export,
                       &ctx->d_needs, &ctx->d_ncols, &ctx->d_part};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
@@ -459,29 +537,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
         for (int i = 0; i < 5; i++) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[i], ctx->ev[i], ctx->ev[i + 1]));
 
     const uint64_t novf = ctx->h_misc[1];
-    if (novf) {
-        std::vector<uint32_t> list(novf), pc(B), nc(B);
-        CORRO_HIP_TRY(hipMemcpy(list.data(), ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost));
-        CORRO_HIP_TRY(hipMemcpy(pc.data(), ctx->d_state_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
-        CORRO_HIP_TRY(hipMemcpy(nc.data(), ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
-        std::vector<uint64_t> soff(novf);
-        uint64_t tot = 0;
-        for (uint64_t k = 0; k < novf; k++) {
-            soff[k] = tot;
-            tot += ovf_scratch_bytes((uint64_t)pc[list[k]] + nc[list[k]]);
-        }
-        TRY(ctx->d_ovf_scratch.ensure(tot + novf * 8 + 256));
-        uint8_t *base = ctx->d_ovf_scratch.as<uint8_t>();
-        uint64_t *d_soff = reinterpret_cast<uint64_t *>(base + ((tot + 255) / 256) * 256);
-        CORRO_HIP_TRY(hipMemcpyAsync(d_soff, soff.data(), novf * 8, hipMemcpyHostToDevice, s));
-        mark(6);
-        hipLaunchKernelGGL(k_merge_ovf, dim3((uint32_t)novf), dim3(OVF_THREADS), 0, s, a, d_soff, base);
-        CORRO_HIP_TRY(hipGetLastError());
-        mark(7);
-        CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, 4 * 8, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
-        if (prof) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[5], ctx->ev[6], ctx->ev[7]));
-    }
+    if (novf) TRY(run_overflow(ctx, a, novf, prof));
     hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
                        ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites);
     if (out && out->impact && !imp_dev)

@@ -312,3 +312,23 @@ def test_device_batch_device_impacts_vs_oracle():
         assert imp.is_cuda and imp.dtype == torch.uint8
         assert np.array_equal(imp.cpu().numpy(), f.apply(b))
     compare(e, f)
+
+
+@pytest.mark.parametrize("malformed", [False, True])
+@pytest.mark.parametrize("impact", [False, True])
+def test_parallel_row_fold_overflow_vs_oracle(malformed, impact):
+    """Overflow buckets run the parallel row fold (segmented scans over the row's changes, a walk
+    over its records only); rows outside App. A.3 (malformed) keep the sequential fold in the same
+    bucket. Zipf-hot rows with up to 12 causal-length epochs, several batches (prior state as a
+    prefix), impacts on and off."""
+    seed = 71 + (2 if malformed else 0) + (1 if impact else 0)
+    sites = synth.site_ids(8, seed)
+    e = engine(synth.adversarial_schema(3), cap=64, sites=sites)  # one bucket: everything overflows
+    f = O.Fold(sites)
+    for k in range(3):
+        b = synth.adversarial_batch(30000, 8, 3, 300, seed * 10 + k, zipf=1.1, malformed=malformed, max_cl=12)
+        got = e.apply(b, impact=impact)
+        ref = f.apply(b)
+        if impact:
+            assert np.array_equal(got, ref), f"impacts differ in batch {k}"
+    compare(e, f, with_ts=True)
