@@ -28,7 +28,7 @@ EXPORTS = [
     "corro_bookie_new", "corro_bookie_free", "corro_process_multiple_changes",
     "corro_bookie_take_ready", "corro_process_fully_buffered", "corro_bookie_last",
     "corro_bookie_needed", "corro_bookie_contains_all", "corro_bookie_partial",
-    "corro_generate_sync", "corro_partition_ranks",
+    "corro_generate_sync", "corro_partition_ranks", "corro_scan_offsets",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -139,6 +139,7 @@ def lib():
         "corro_state_reset": (i32, [vp]),
         "corro_db_versions": (i32, [vp, vp, u32]),
         "corro_compute_needs": (i32, [vp, C.POINTER(SyncEntries), i32, C.POINTER(NeedsOut), i32]),
+        "corro_scan_offsets": (i32, [vp, vp, vp, u64]),
         "corro_booked_new": (i32, [vp]),
         "corro_booked_free": (None, [vp]),
         "corro_booked_insert_db": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp, vp, u64, vp]),

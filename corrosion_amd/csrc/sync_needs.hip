@@ -36,20 +36,25 @@ struct SyncDev {
 // the workgroup's staged segment when p points into LDS, 0 for global memory). The bias is applied
 // to the index, never to the pointer: an LDS pointer moved outside the LDS window is not a valid
 // flat address.
-struct V64 {
+// SPACE tags the instantiation (0 global, 1 LDS): a workgroup picks one uniformly, so every
+// access in an instantiation has a single known address space (LDS views compile to ds_read /
+// ds_write; a view that could be either would be a flat access, issued through the vector memory
+// pipeline lane by lane).
+template <int SPACE> struct V64S {
     const uint64_t *p;
     uint64_t base;
     __device__ inline uint64_t operator[](uint64_t k) const { return p[k - base]; }
 };
-template <class T> struct WView {
+using V64 = V64S<0>;
+template <class T, int SPACE = 0> struct WView {
     T *p;
     uint64_t base;
     __device__ inline T &operator[](uint64_t k) const { return p[k - base]; }
 };
 
 // Holes of an entry's version space: their need ranges [tn] and their partial versions [tp].
-struct VerHoles {
-    V64 hs, he;               // ranges
+template <class V> struct VerHolesT {
+    V hs, he;                 // ranges
     uint64_t h0, h1;
     const uint64_t *pv;       // points
     uint64_t p0, p1;
@@ -188,16 +193,10 @@ __global__ void __launch_bounds__(NEEDS_T) k_needs(SyncDev in, corro_needs_out o
         o_lds = o_hi - o_lo <= NEEDS_CAP_O;
     }
     __syncthreads();
-    // views indexed by the global CSR index
-    const V64 tns{tn_lds ? l_tns : in.tn_start, tn_lds ? tn_lo : 0}, tne{tn_lds ? l_tne : in.tn_end, tn_lds ? tn_lo : 0};
-    const V64 ons{on_lds ? l_ons : in.on_start, on_lds ? on_lo : 0}, one{on_lds ? l_one : in.on_end, on_lds ? on_lo : 0};
-    const uint64_t ob = o_lds ? o_lo : 0;
-    const WView<uint8_t> okind{o_lds ? l_kind : o.kind, ob};
-    const WView<uint64_t> ostart{o_lds ? l_start : o.start, ob}, oend{o_lds ? l_end : o.end, ob};
-    const WView<uint64_t> osro{o_lds ? l_sro : o.sr_off, ob}, osrn{o_lds ? l_srn : o.sr_n, ob};
-
-    if (live) {
-        VerHoles vh{tns, tne, tne0, tne1, in.tp_ver, tpe0, tpe1};
+    // the per-lane walk, instantiated once for LDS-staged views and once for global ones
+    auto lane = [&](auto tns, auto tne, auto ons, auto one, auto okind, auto ostart, auto oend, auto osro,
+                    auto osrn) {
+        VerHolesT<decltype(tns)> vh{tns, tne, tne0, tne1, in.tp_ver, tpe0, tpe1};
         uint64_t nn = 0, ns = 0;
         auto full = [&](uint64_t s, uint64_t t) {
             if (FILL) {
@@ -284,8 +283,20 @@ __global__ void __launch_bounds__(NEEDS_T) k_needs(SyncDev in, corro_needs_out o
             o.need_count[e] = nn;
             o.seq_count[e] = ns;
         }
+    };
+    const bool all_lds = tn_lds && on_lds && (!FILL || o_lds);
+    if (live) {
+        if (all_lds) {
+            lane(V64S<1>{l_tns, tn_lo}, V64S<1>{l_tne, tn_lo}, V64S<1>{l_ons, on_lo}, V64S<1>{l_one, on_lo},
+                 WView<uint8_t, 1>{l_kind, o_lo}, WView<uint64_t, 1>{l_start, o_lo}, WView<uint64_t, 1>{l_end, o_lo},
+                 WView<uint64_t, 1>{l_sro, o_lo}, WView<uint64_t, 1>{l_srn, o_lo});
+        } else {
+            lane(V64{in.tn_start, 0}, V64{in.tn_end, 0}, V64{in.on_start, 0}, V64{in.on_end, 0},
+                 WView<uint8_t>{o.kind, 0}, WView<uint64_t>{o.start, 0}, WView<uint64_t>{o.end, 0},
+                 WView<uint64_t>{o.sr_off, 0}, WView<uint64_t>{o.sr_n, 0});
+        }
     }
-    if (FILL && o_lds) {
+    if (FILL && all_lds) {
         __syncthreads();
         const uint64_t m = o_hi - o_lo;
         for (uint64_t k = threadIdx.x; k < m; k += NEEDS_T) {

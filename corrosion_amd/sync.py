@@ -148,23 +148,24 @@ def _needs_device(engine, ent):
     for k, _ in L.SyncEntries._fields_[1:]:
         a = ent[k]
         setattr(s, k, a.data_ptr() if a.numel() else None)
-    nc = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
-    sc = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+    nc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)  # pass 0 writes every entry
+    sc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     o = L.NeedsOut()
     o.need_count, o.seq_count = nc.data_ptr(), sc.data_ptr()
     torch.cuda.current_stream().synchronize()
     L.check(lib.corro_compute_needs(engine._h, C.byref(s), L.CORRO_MEM_DEVICE, C.byref(o), 0))
-    need_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    seq_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    need_off[1:] = torch.cumsum(nc[:n], 0)
-    seq_off[1:] = torch.cumsum(sc[:n], 0)
+    need_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    seq_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    L.check(lib.corro_scan_offsets(engine._h, nc.data_ptr(), need_off.data_ptr(), n))
+    L.check(lib.corro_scan_offsets(engine._h, sc.data_ptr(), seq_off.data_ptr(), n))
     T, Ts = int(need_off[-1].item()), int(seq_off[-1].item())
+    # pass 1 writes every output element: no fill needed
     res = {"need_off": need_off, "seq_off": seq_off,
-           "kind": torch.zeros(max(T, 1), dtype=torch.uint8, device=dev)}
+           "kind": torch.empty(max(T, 1), dtype=torch.uint8, device=dev)}
     for k in ("start", "end", "sr_off", "sr_n"):
-        res[k] = torch.zeros(max(T, 1), dtype=torch.int64, device=dev)
+        res[k] = torch.empty(max(T, 1), dtype=torch.int64, device=dev)
     for k in ("s_start", "s_end"):
-        res[k] = torch.zeros(max(Ts, 1), dtype=torch.int64, device=dev)
+        res[k] = torch.empty(max(Ts, 1), dtype=torch.int64, device=dev)
     for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
         setattr(o, k, res[k].data_ptr())
     torch.cuda.current_stream().synchronize()

@@ -204,6 +204,9 @@ typedef struct {
 /* mem = CORRO_MEM_HOST or CORRO_MEM_DEVICE for BOTH `in` arrays and `out` arrays. */
 int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in, int mem,
                         corro_needs_out *out, int pass);
+/* Device helper between the two passes: offsets[0] = 0, offsets[k+1] = counts[0] + ... + counts[k]
+ * (n + 1 outputs), for device-resident need_count / seq_count. */
+int corro_scan_offsets(corro_ctx *ctx, const uint64_t *counts, uint64_t *offsets, uint64_t n);
 
 /* ------------------------------------------------------------------ gap bookkeeping */
 
