@@ -60,8 +60,12 @@ namespace corro {
 int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t *ko, const uint32_t *vi,
                    uint32_t *vo, uint32_t n, uint32_t end_bit, hipStream_t s);
 
-// Oversized buckets (after the first merge pass queued them): prep -> device-wide sort by (bucket
-// base + row, position) -> parallel row fold -> [sort of the candidates -> impacts].
+int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStream_t s);
+
+// Oversized buckets (after the first merge pass queued them), all at once and device-wide (the
+// phases of ovf_kernels.h): fields + row ids -> sort by (bucket base + row, position) -> L scan ->
+// classify -> epoch scan -> candidate keys -> sort -> argmax / group-start scans -> link -> walk
+// -> [impacts] -> per-bucket counts.
 static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) {
     hipStream_t s = ctx->stream;
     const uint32_t B = ctx->B;
@@ -69,63 +73,98 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     CORRO_HIP_TRY(hipMemcpy(list.data(), ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost));
     CORRO_HIP_TRY(hipMemcpy(pc.data(), ctx->d_state_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
     CORRO_HIP_TRY(hipMemcpy(nc.data(), ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
-    std::vector<uint64_t> soff(novf);
-    std::vector<uint32_t> kb(novf);
-    uint64_t tot = 0, keys = 0;
+    std::vector<uint32_t> koff(novf + 1), soff(novf);
+    uint64_t K = 0, S = 0;
     for (uint64_t k = 0; k < novf; k++) {
         const uint64_t n = (uint64_t)pc[list[k]] + nc[list[k]];
-        soff[k] = tot;
-        tot += ovf_scratch_bytes(n);
-        kb[k] = (uint32_t)keys;
-        keys += n;
-        if (keys >= (1ULL << 31)) return fail(CORRO_E_RANGE, "oversized buckets hold more than 2^31 records");
+        uint64_t sl = 1;
+        while (sl < 2 * n) sl <<= 1;
+        koff[k] = (uint32_t)K;
+        soff[k] = (uint32_t)S;
+        K += n;
+        S += sl;
+        if (K >= (1ULL << 31) || S >= (1ULL << 32))
+            return fail(CORRO_E_RANGE, "oversized buckets hold more than 2^31 records");
     }
-    // key high halves are < keys; one spare value above them so ~0 (not a candidate) sorts last
-    uint32_t end_bit = 33;
-    while ((1ULL << (end_bit - 32)) <= keys) end_bit++;
-    size_t temp = 0;
-    TRY(ovf_sort_pairs(nullptr, &temp, nullptr, nullptr, nullptr, nullptr, (uint32_t)keys, end_bit, s));
+    koff[novf] = (uint32_t)K;
+    // row ids (< K) take rb bits with one spare value above them, so that ~0 sorts last
+    uint32_t rb = 1;
+    while ((1ULL << rb) <= K) rb++;
+    const uint32_t key_bits = 32 + rb;
+    const uint32_t ckey_bits = std::min<uint32_t>(64, rb + OVF_EP_BITS + 16);
     auto al = [](uint64_t x) { return (x + 255) & ~255ULL; };
-    const uint64_t sort_bytes = 4 * al(keys * 8) + 4 * al(keys * 4) + al(novf * 8) + 2 * al(novf * 4) + al(temp);
-    TRY(ctx->d_ovf_scratch.ensure(tot + 256));
-    TRY(ctx->d_ovf_sort.ensure(sort_bytes + 256));
-    uint8_t *q = ctx->d_ovf_sort.as<uint8_t>();
-    auto carve = [&](uint64_t bytes) {
-        uint8_t *r = q;
-        q += al(bytes);
+    // pass 0 sizes the arrays, pass 1 carves them out of d_ovf_sort
+    OvfDev d{};
+    d.G = (uint32_t)novf;
+    d.K = (uint32_t)K;
+    uint64_t bytes = 0;
+    uint8_t *base = nullptr;
+    auto take = [&](uint64_t n) {
+        uint8_t *r = base ? base + bytes : nullptr;
+        bytes += al(n);
         return r;
     };
-    OvfArgs o{};
-    o.scratch = ctx->d_ovf_scratch.as<uint8_t>();
-    o.key = (uint64_t *)carve(keys * 8);
-    o.key_s = (uint64_t *)carve(keys * 8);
-    o.ckey = (uint64_t *)carve(keys * 8);
-    o.ckey_s = (uint64_t *)carve(keys * 8);
-    o.val = (uint32_t *)carve(keys * 4);
-    o.val_s = (uint32_t *)carve(keys * 4);
-    o.cval = (uint32_t *)carve(keys * 4);
-    o.cval_s = (uint32_t *)carve(keys * 4);
-    uint64_t *d_soff = (uint64_t *)carve(novf * 8);
-    uint32_t *d_kb = (uint32_t *)carve(novf * 4);
-    o.ccnt = (uint32_t *)carve(novf * 4);
-    void *d_temp = carve(temp);
-    o.soff = d_soff;
-    o.koff = d_kb;
-    CORRO_HIP_TRY(hipMemcpyAsync(d_soff, soff.data(), novf * 8, hipMemcpyHostToDevice, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(d_kb, kb.data(), novf * 4, hipMemcpyHostToDevice, s));
-    CORRO_HIP_TRY(hipMemsetAsync(o.ccnt, 0, novf * 4, s));
-    if (prof) (void)hipEventRecord(ctx->ev[6], s);
-    const dim3 grid((uint32_t)novf), blk(OVF_THREADS);
-    hipLaunchKernelGGL(k_ovf_prep, grid, blk, 0, s, a, o);
-    CORRO_HIP_TRY(hipGetLastError());
-    TRY(ovf_sort_pairs(d_temp, &temp, o.key, o.key_s, o.val, o.val_s, (uint32_t)keys, end_bit, s));
-    hipLaunchKernelGGL(k_ovf_fold_a, grid, blk, 0, s, a, o);
-    CORRO_HIP_TRY(hipGetLastError());
-    if (a.impact) {
-        TRY(ovf_sort_pairs(d_temp, &temp, o.ckey, o.ckey_s, o.cval, o.cval_s, (uint32_t)keys, end_bit, s));
-        hipLaunchKernelGGL(k_ovf_fold_b, grid, blk, 0, s, a, o);
-        CORRO_HIP_TRY(hipGetLastError());
+    void *d_temp = nullptr;
+    size_t temp = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        bytes = 0;
+        d.koff = (const uint32_t *)take((novf + 1) * 4);
+        d.slot_off = (const uint32_t *)take(novf * 4);
+        d.ocnt = (uint32_t *)take(novf * 4);
+        d.oflag = (uint32_t *)take(novf * 4);
+        d.slots = (uint32_t *)take(S * 4);
+        uint64_t **u64s[] = {&d.pk, &d.vk0, &d.vk1, &d.key, &d.key_s, &d.ckey, &d.ckey_s};
+        for (uint64_t **p : u64s) *p = (uint64_t *)take(K * 8);
+        d.cv = (int64_t *)take(K * 8);
+        d.ccv = (int64_t *)take(K * 8);
+        uint32_t **u32s[] = {&d.tc,    &d.cl,     &d.pos,   &d.vmeta, &d.srank, &d.val,    &d.val_s, &d.rowid,
+                             &d.cl_s,  &d.lx,     &d.recf,  &d.epc,   &d.kind,  &d.pb,     &d.rstart, &d.rbad,
+                             &d.rnrec, &d.recs,   &d.head,  &d.scid,  &d.spos,  &d.sz,     &d.ccid,  &d.csrc,
+                             &d.cval,  &d.cval_s, &d.cbest, &d.cgs,   &d.nxt,   &d.fstg};
+        for (uint32_t **p : u32s) *p = (uint32_t *)take(K * 4);
+        if (pass == 0) {
+            size_t t0 = 0, t1 = 0, t2 = 0;
+            TRY(ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, d.K, key_bits, s));
+            TRY(ovf_sort_pairs(nullptr, &t1, nullptr, nullptr, nullptr, nullptr, d.K, ckey_bits, s));
+            TRY(ovf_scans(nullptr, &t2, d, 0, s));
+            temp = std::max(std::max(t0, t1), t2);
+        }
+        d_temp = take(temp);
+        if (pass == 0) {
+            TRY(ctx->d_ovf_sort.ensure(bytes + 256));
+            base = ctx->d_ovf_sort.as<uint8_t>();
+        }
     }
+    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.koff, koff.data(), (novf + 1) * 4, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.slot_off, soff.data(), novf * 4, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemsetAsync(d.ocnt, 0, novf * 4, s));
+    CORRO_HIP_TRY(hipMemsetAsync(d.oflag, 0, novf * 4, s));
+    CORRO_HIP_TRY(hipMemsetAsync(d.slots, 0, S * 4, s));
+    if (prof) (void)hipEventRecord(ctx->ev[6], s);
+    const dim3 blk(256), grid((uint32_t)std::min<uint64_t>((K + 255) / 256, 8192));
+    auto launched = [&]() -> int {
+        CORRO_HIP_TRY(hipGetLastError());
+        return CORRO_OK;
+    };
+    hipLaunchKernelGGL(k_ovf_load, grid, blk, 0, s, a, d);
+    hipLaunchKernelGGL(k_ovf_rowhash, grid, blk, 0, s, d);
+    TRY(launched());
+    TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.key_s, d.val, d.val_s, d.K, key_bits, s));
+    hipLaunchKernelGGL(k_ovf_gather, grid, blk, 0, s, d);
+    TRY(launched());
+    TRY(ovf_scans(d_temp, &temp, d, 0, s));
+    hipLaunchKernelGGL(k_ovf_classify, grid, blk, 0, s, a, d);
+    TRY(launched());
+    TRY(ovf_scans(d_temp, &temp, d, 1, s));
+    hipLaunchKernelGGL(k_ovf_epochs, grid, blk, 0, s, d);
+    TRY(launched());
+    TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.ckey_s, d.cval, d.cval_s, d.K, ckey_bits, s));
+    TRY(ovf_scans(d_temp, &temp, d, 2, s));
+    hipLaunchKernelGGL(k_ovf_link, grid, blk, 0, s, d);
+    hipLaunchKernelGGL(k_ovf_walk, grid, blk, 0, s, a, d);
+    if (a.impact) hipLaunchKernelGGL(k_ovf_impacts, grid, blk, 0, s, a, d);
+    hipLaunchKernelGGL(k_ovf_finish, dim3((uint32_t)((novf + 255) / 256)), blk, 0, s, a, d);
+    TRY(launched());
     if (prof) (void)hipEventRecord(ctx->ev[7], s);
     CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, a.misc, 4 * 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
@@ -253,7 +292,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_state_ts[0], &ctx->d_state_ts[1], &ctx->d_state_off, &ctx->d_state_cnt,
                       &ctx->d_state_flags, &ctx->d_out_off, &ctx->d_out_cnt, &ctx->d_out_flags, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_scratch, &ctx->d_ovf_sort, &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export,
                       &ctx->d_needs, &ctx->d_ncols, &ctx->d_part};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);

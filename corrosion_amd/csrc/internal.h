@@ -94,8 +94,7 @@ struct corro_ctx {
     corro::DevBuf d_ovf_list;     // overflow buckets
     corro::DevBuf d_gen_list;     // buckets queued for the general body
     corro::DevBuf d_wide_list;    // buckets queued for the mixed-type fast body
-    corro::DevBuf d_ovf_scratch;
-    corro::DevBuf d_ovf_sort;     // overflow path: sort arrays, offsets, rocPRIM temp
+    corro::DevBuf d_ovf_sort;     // overflow path: its device-wide arrays, offsets, rocPRIM temp
     corro::DevBuf d_scan_tmp;     // corro_scan_offsets: rocPRIM temp
     corro::DevBuf d_impact;
     corro::DevBuf d_export;

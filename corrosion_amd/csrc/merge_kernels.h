@@ -18,8 +18,8 @@
 //                      stages; order independent (SURVEY App. A.2 reduction). 2 WGs/CU.
 //                gen   sort by (row, position) in LDS, then one lane per row folds the
 //                      cr-sqlite rules in application order (App. A.1), exactly.
-//              Buckets larger than LDS go to the overflow path (k_ovf_*: parallel row fold on
-//              global scratch around device-wide segmented sorts).
+//              Buckets larger than LDS, or holding a long row, go to the overflow path
+//              (ovf_kernels.h: a parallel row fold over all of them at once, device-wide).
 #pragma once
 #include "internal.h"
 #include "rowhash.h"
@@ -34,7 +34,6 @@ constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 3072
 constexpr int FAST_SLOTS = 4096;                       // cell table (distinct cells <= records)
 constexpr int CAP_GEN = 2048;                          // records, general body in LDS
 constexpr int GEN_SLOTS = 4096;
-constexpr int OVF_THREADS = 1024;
 constexpr uint32_t LONG_ROW = 128;                     // rows this long leave the LDS body
 
 struct MergeArgs {
@@ -132,7 +131,7 @@ __device__ inline uint32_t site_rank_of(const MergeArgs &a, uint32_t site) {
 // Tile histogram of row buckets. Reads only pk + table_cid (12 B per change), or only pk when the
 // schema has one table (every change's bucket then uses table 0; k_scatter does the same and
 // reports a bad table id as an error).
-__global__ void __launch_bounds__(HIST_THREADS)
+static __global__ void __launch_bounds__(HIST_THREADS)
 k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t *__restrict__ hist_out) {
     extern __shared__ uint32_t hist[];
     const uint32_t B = 1u << log2B;
@@ -165,7 +164,7 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t 
 }
 
 // per bucket: exclusive prefix of the tile counts (in place) and the bucket total
-__global__ void k_colscan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t B,
+static __global__ void k_colscan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t B,
                           uint32_t *__restrict__ new_cnt) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
@@ -195,7 +194,7 @@ __global__ void k_colscan(uint32_t *__restrict__ hist, uint32_t ntiles, uint32_t
 // latency for the whole scan), the lane sums are scanned by wave shuffles + one LDS round, and the
 // lane re-reads its run (L2-resident now) to write the offsets.
 constexpr uint32_t PLAN_PER = 32;  // B <= 1024 * PLAN_PER = 2^15 (B is a power of two)
-__global__ void __launch_bounds__(1024)
+static __global__ void __launch_bounds__(1024)
 k_plan(const uint32_t *__restrict__ new_cnt, const uint32_t *__restrict__ prior_cnt, uint32_t B,
        uint32_t *__restrict__ stage_off, uint64_t *__restrict__ out_off) {
     __shared__ uint64_t w_a[16], w_b[16];
@@ -358,7 +357,7 @@ __device__ inline unsigned long long wave_max_u64(unsigned long long x) {
 // PLAIN: the batch has no val1/val_type/val_len arrays (INTEGER values) -- loads are unconditional
 // (clamped) so all of an iteration's loads are in flight together. NT: non-temporal record stores.
 template <bool PLAIN, bool NT>
-__global__ void __launch_bounds__(HIST_THREADS)
+static __global__ void __launch_bounds__(HIST_THREADS)
 k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const uint32_t *__restrict__ hist_off,
           const uint32_t *__restrict__ stage_off, Rec *__restrict__ stage, uint32_t *__restrict__ bflags,
           unsigned long long *__restrict__ dbv_batch, uint32_t nsites, const uint16_t *__restrict__ ncols,
@@ -829,303 +828,6 @@ __device__ inline void gen_body(const MergeArgs &a, const BucketView &v, Rec *ou
     }
 }
 
-}  // namespace corro
-#include "rowfold.h"
-namespace corro {
-
-// Lexicographic cell key (col_version, value order, site rank) of record x; `zeroed` = the carried
-// cell of a resurrected row (col_version 0, value and metadata kept). >0: a greater.
-__device__ inline int rf_cmp(const GenArrays &g, const FoldArrays &F, uint32_t xa, bool za, uint32_t xb, bool zb) {
-    const int64_t ca = za ? 0 : g.cv[xa], cb = zb ? 0 : g.cv[xb];
-    if (ca != cb) return ca > cb ? 1 : -1;
-    const int vc = value_cmp_f(F.vmeta[xa], F.vk0[xa], F.vk1[xa], F.vmeta[xb], F.vk0[xb], F.vk1[xb]);
-    if (vc != 0) return vc;
-    if (F.srank[xa] != F.srank[xb]) return F.srank[xa] > F.srank[xb] ? 1 : -1;
-    return 0;
-}
-
-// atomicMax(&base[key], val) for the active lanes of a wave, with lanes that share a key (a hot
-// row's cell) combined by a wave reduction first: a few rounds of "leader's key, max over the
-// lanes with it, one atomic", then plain per-lane atomics for what is left. All lanes call it.
-__device__ inline void wave_grouped_max(uint64_t *base, uint32_t key, uint64_t val, bool active) {
-    const uint32_t lane = threadIdx.x & 63;
-    for (int round = 0; round < 4; round++) {
-        const uint64_t act = __ballot(active);
-        if (!act) return;
-        const int leader = __ffsll((unsigned long long)act) - 1;
-        const uint32_t lk = __shfl(key, leader);
-        const bool mine = active && key == lk;
-        const unsigned long long m = wave_max_u64(mine ? val : 0ULL);
-        if ((int)lane == leader) atomicMax(reinterpret_cast<unsigned long long *>(&base[lk]), m);
-        if (mine) active = false;
-    }
-    if (active) atomicMax(reinterpret_cast<unsigned long long *>(&base[key]), (unsigned long long)val);
-}
-
-// Emit the clock rows of one row folded by the record walk (see rowfold.h).
-__device__ inline void rf_emit(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts, uint32_t *outcnt,
-                               uint32_t *flag, const GenArrays &g, const FoldArrays &F, uint32_t j0, uint32_t ncell,
-                               uint32_t rpos) {
-    const uint32_t xr = g.val[rpos];
-    const uint32_t clr = g.cl[xr], cidr = g.tc[xr] & 0xFFFFu;
-    const bool hs = !(cidr != 0 && clr == 1 && F.lx[rpos] == 0);
-    const int64_t scv = cidr == 0 ? g.cv[xr] : (int64_t)clr;
-    const int64_t rowcl = hs ? scv : 1;
-    const bool cells = (clr & 1u) != 0;  // L_final = the last record's cl
-    const uint32_t cnt = (hs ? 1u : 0u) + (cells ? ncell : 0u);
-    if (cnt == 0) return;
-    uint32_t k = atomicAdd(outcnt, cnt);
-    if (hs || rowcl != 1) atomicOr(flag, 1u);
-    if (hs) {
-        Rec r = load_rec(v.at(xr));
-        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
-        r.tcid &= 0xFFFF0000u;
-        r.cv = scv;
-        r.cl = (uint32_t)rowcl;
-        r.v0 = 0;
-        r.v1 = 0;
-        r.meta = CORRO_NULL;
-        r.pos = k;
-        store_rec(outb + k, r);
-        if (a.track_ts) outts[k] = ts;
-        k++;
-    }
-    if (!cells) return;
-    for (uint32_t c = 0; c < ncell; c++) {
-        Rec r = load_rec(v.at(g.val[F.spos[j0 + c]]));
-        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
-        if (F.sz[j0 + c]) r.cv = 0;
-        r.cl = (uint32_t)rowcl;
-        r.pos = k;
-        store_rec(outb + k, r);
-        if (a.track_ts) outts[k] = ts;
-        k++;
-    }
-}
-
-// The parallel row fold of a sorted bucket (gen_sort done). s_f / s_m: 2 x blockDim words of LDS.
-__device__ inline void rowfold_a(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts,
-                                 uint32_t *outcnt, uint32_t *flag, const GenArrays &g, const FoldArrays &F,
-                                 uint32_t *s_f, uint32_t *s_m, uint32_t *s_ncand, uint32_t *ncand_out) {
-    const uint32_t n = v.np + v.nn;
-    const uint32_t tid = threadIdx.x, nth = blockDim.x;
-    auto row_of = [&](uint32_t j) { return (uint32_t)(g.key[j] >> 32) - F.kbase; };
-    auto starts = [&](uint32_t j) { return j == 0 || row_of(j) != row_of(j - 1); };
-    // per record: value words, meta, site rank; per row: init
-    for (uint32_t i = tid; i < n; i += nth) {
-        const Rec r = load_rec(v.at(i));
-        F.vk0[i] = r.v0;
-        F.vk1[i] = r.v1;
-        F.vmeta[i] = r.meta;
-        F.srank[i] = site_rank_of(a, r.site);
-        F.rbad[i] = 0;
-        F.rnrec[i] = 0;
-        F.head[i] = 0;
-    }
-    for (uint32_t i = tid; i < F.gslots; i += nth) F.gslot[i] = 0;
-    if (tid == 0) *s_ncand = 0;
-    __syncthreads();
-    for (uint32_t j = tid; j < n; j += nth)
-        if (starts(j)) F.rstart[row_of(j)] = j;
-    // 1. L before every change: segmented exclusive max-scan of cl
-    rf_seg_scan(
-        n, 0u, [&](uint32_t j) { return g.cl[g.val[j]]; }, [](uint32_t x, uint32_t y) { return x > y ? x : y; },
-        starts, [&](uint32_t j, uint32_t e) { F.lx[j] = e; }, s_f, s_m);
-    // 2. classification, record impacts, malformed rows
-    for (uint32_t j = tid; j < n; j += nth) {
-        const uint32_t x = g.val[j];
-        const uint32_t cl = g.cl[x], L = F.lx[j], cid = g.tc[x] & 0xFFFFu;
-        const uint32_t kd = cl > L ? 1u : ((cl == L && cid != 0 && (cl & 1u)) ? 2u : 0u);
-        F.kind[j] = kd;
-        const uint32_t pos = g.pos[x];
-        // outside App. A.3: a sentinel / even-cl change whose col_version is not its cl, or prior
-        // cells kept under an even causal length (left by such a history): sequential fold
-        if (((cid == 0 || (cl & 1u) == 0) && g.cv[x] != (int64_t)cl) || (!(pos & BATCH_POS) && cid != 0 && !(cl & 1u)))
-            atomicOr(&F.rbad[row_of(j)], 1u);
-        if (a.impact && (pos & BATCH_POS) && kd != 2)
-            a.impact[pos & 0x7FFFFFFFu] = kd == 0 ? 0 : ((cid != 0 && (cl & 1u) && (L > 0 || cl > 1)) ? 2 : 1);
-    }
-    __syncthreads();
-    // 3. epochs: segmented count of records; the row's record list
-    rf_seg_scan(
-        n, 0u, [&](uint32_t j) { return F.kind[j] == 1 ? 1u : 0u; }, [](uint32_t x, uint32_t y) { return x + y; },
-        starts,
-        [&](uint32_t j, uint32_t e) {
-            const uint32_t inc = e + (F.kind[j] == 1 ? 1u : 0u);
-            F.ep[j] = inc ? inc - 1 : RF_NONE;
-            if (F.kind[j] == 1) {
-                const uint32_t row = row_of(j);
-                F.recs[F.rstart[row] + inc - 1] = j;
-                atomicMax(&F.rnrec[row], inc);
-            }
-        },
-        s_f, s_m);
-    // 4. groups (row, epoch, cid) of the candidates; argmax stages
-    const uint32_t gmask = F.gslots - 1;
-    for (uint32_t j = tid; j < n; j += nth) {
-        if (F.kind[j] != 2) continue;
-        const uint32_t row = row_of(j), ep = F.ep[j], cid = g.tc[g.val[j]] & 0xFFFFu;
-        uint32_t slot = (uint32_t)mix64(((uint64_t)row << 32 | ep) * 0x9E3779B97F4A7C15ULL + cid) & gmask;
-        while (true) {
-            uint32_t o = __hip_atomic_load(&F.gslot[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (o == 0) o = atomicCAS(&F.gslot[slot], 0u, j + 1);
-            if (o == 0) {
-                F.gid[j] = j;
-                F.gk[j] = 0;
-                break;
-            }
-            const uint32_t oj = o - 1;
-            if (row_of(oj) == row && F.ep[oj] == ep && (g.tc[g.val[oj]] & 0xFFFFu) == cid) {
-                F.gid[j] = oj;
-                break;
-            }
-            slot = (slot + 1) & gmask;
-        }
-        F.alive[j] = 1;
-    }
-    __syncthreads();
-    for (int st = 0; st < 6; st++) {
-        for (uint32_t jb = 0; jb < n; jb += nth) {  // whole waves iterate together (wave reductions)
-            const uint32_t j = jb + tid;
-            const bool act = j < n && F.kind[j] == 2 && F.alive[j];
-            if (!__any(act)) continue;
-            const uint32_t x = act ? g.val[j] : 0u;
-            const uint32_t ty = vtype(F.vmeta[x]);
-            const bool tb = ty == CORRO_TEXT || ty == CORRO_BLOB;
-            uint64_t w;
-            switch (st) {
-            case 0: w = (uint64_t)g.cv[x] ^ 0x8000000000000000ULL; break;
-            case 1: w = 5u - ty; break;
-            case 2: w = vkey0(ty, F.vk0[x]); break;
-            case 3: w = tb ? F.vk1[x] : 0; break;
-            case 4: w = tb ? vlen(F.vmeta[x]) : 0; break;
-            default: w = ((uint64_t)F.srank[x] << 32) | (uint64_t)(~g.pos[x]); break;
-            }
-            wave_grouped_max(F.gk, act ? F.gid[j] : 0u, w, act);
-            if (act) {
-                F.fst[j] = (uint32_t)(w >> 32);  // stash the stage key (both halves) for the compare
-                F.win[j] = (uint32_t)w;
-            }
-        }
-        __syncthreads();
-        for (uint32_t j = tid; j < n; j += nth) {
-            if (F.kind[j] != 2 || !F.alive[j]) continue;
-            const uint64_t w = ((uint64_t)F.fst[j] << 32) | F.win[j];
-            F.alive[j] = F.gk[F.gid[j]] == w;
-        }
-        __syncthreads();
-        for (uint32_t j = tid; j < n; j += nth)
-            if (F.kind[j] == 2 && F.gid[j] == j) F.gk[j] = 0;
-        __syncthreads();
-    }
-    for (uint32_t j = tid; j < n; j += nth)
-        if (F.kind[j] == 2 && F.alive[j]) F.win[F.gid[j]] = j;
-    __syncthreads();
-    // link each group into its epoch's record
-    for (uint32_t j = tid; j < n; j += nth) {
-        if (F.kind[j] != 2 || F.gid[j] != j) continue;
-        const uint32_t rec = F.recs[F.rstart[row_of(j)] + F.ep[j]];
-        F.nxt[j] = atomicExch(&F.head[rec], j + 1);
-    }
-    __syncthreads();
-    // 5. one lane per well-formed row walks its records (few) and emits
-    for (uint32_t j0 = tid; j0 < n; j0 += nth) {
-        if (!starts(j0)) continue;
-        const uint32_t row = row_of(j0);
-        if (F.rbad[row]) continue;
-        const uint32_t nrec = F.rnrec[row];
-        uint32_t ncell = 0;
-        for (uint32_t k = 0; k < nrec; k++) {
-            const uint32_t R = F.recs[j0 + k];
-            const uint32_t xR = g.val[R];
-            if ((g.cl[xR] & 1u) == 0) {
-                ncell = 0;
-                continue;
-            }
-            for (uint32_t c = 0; c < ncell; c++) F.sz[j0 + c] = 1;
-            auto set = [&](uint32_t cid, uint32_t pos, uint32_t z) {
-                for (uint32_t c = 0; c < ncell; c++)
-                    if (F.scid[j0 + c] == cid) {
-                        F.spos[j0 + c] = pos;
-                        F.sz[j0 + c] = z;
-                        return;
-                    }
-                F.scid[j0 + ncell] = cid;
-                F.spos[j0 + ncell] = pos;
-                F.sz[j0 + ncell] = z;
-                ncell++;
-            };
-            const uint32_t cidR = g.tc[xR] & 0xFFFFu;
-            if (cidR != 0) set(cidR, R, 0);
-            for (uint32_t h = F.head[R]; h; h = F.nxt[h - 1]) {
-                const uint32_t g0 = h - 1;
-                const uint32_t cid = g.tc[g.val[g0]] & 0xFFFFu;
-                int found = -1;
-                for (uint32_t c = 0; c < ncell; c++)
-                    if (F.scid[j0 + c] == cid) {
-                        found = (int)c;
-                        break;
-                    }
-                const uint32_t w = F.win[g0];
-                F.fst[g0] = found < 0 ? 0u : ((F.spos[j0 + found] + 1) | (F.sz[j0 + found] << 31));
-                if (found < 0 || rf_cmp(g, F, g.val[w], false, g.val[F.spos[j0 + found]], F.sz[j0 + found] != 0) > 0)
-                    set(cid, w, 0);
-            }
-        }
-        if (nrec) rf_emit(a, v, outb, outts, outcnt, flag, g, F, j0, ncell, F.recs[j0 + nrec - 1]);
-    }
-    __syncthreads();
-    // candidate sort keys for the impact pass (rowfold_b): (base + group) << 32 | position, or ~0
-    // (sorts after every bucket); the bucket's candidate count goes to *ncand_out
-    if (a.impact) {
-        if (tid == 0) *s_ncand = 0;
-        __syncthreads();
-        for (uint32_t jb = 0; jb < n; jb += nth) {
-            const uint32_t j = jb + tid;
-            const bool c = j < n && F.kind[j] == 2 && !F.rbad[row_of(j)];
-            if (j < n) {
-                F.ckey[j] = c ? (((uint64_t)(F.kbase + F.gid[j]) << 32) | j) : ~0ULL;
-                F.cval[j] = j;
-            }
-            const uint64_t bal = __ballot(c);
-            if ((tid & 63) == 0 && bal) atomicAdd(s_ncand, (uint32_t)__popcll(bal));
-        }
-        __syncthreads();
-        if (tid == 0) *ncand_out = *s_ncand;
-    }
-    // 7. rows outside App. A.3 keep the sequential fold (it writes their impacts too)
-    for (uint32_t j0 = tid; j0 < n; j0 += nth)
-        if (starts(j0) && F.rbad[row_of(j0)]) gen_fold_row(a, v, outb, outts, outcnt, flag, g, j0, n);
-}
-
-
-// Impact pass of the parallel fold: F.ckey / F.cval point at the bucket's nc candidates sorted by
-// (group, position) (a device-wide radix sort between the two launches); a segmented
-// prefix argmax over them decides each candidate's impact (strict prefix maximum of its cell
-// within its epoch, seeded by the epoch's first element).
-__device__ inline void rowfold_b(const MergeArgs &a, const GenArrays &g, const FoldArrays &F, uint32_t nc,
-                                 uint32_t *s_f, uint32_t *s_m) {
-    rf_seg_scan(
-        nc, RF_NONE, [&](uint32_t q) { return F.cval[q]; },
-        [&](uint32_t x, uint32_t y) {
-            if (x == RF_NONE) return y;
-            if (y == RF_NONE) return x;
-            return rf_cmp(g, F, g.val[y], false, g.val[x], false) > 0 ? y : x;
-        },
-        [&](uint32_t q) { return q == 0 || (F.ckey[q] >> 32) != (F.ckey[q - 1] >> 32); },
-        [&](uint32_t q, uint32_t prev) {
-            const uint32_t j = F.cval[q];
-            const uint32_t x = g.val[j];
-            const uint32_t pos = g.pos[x];
-            if (!(pos & BATCH_POS)) return;
-            bool imp = prev == RF_NONE || rf_cmp(g, F, x, false, g.val[prev], false) > 0;
-            const uint32_t fs = F.fst[F.gid[j]];
-            if (imp && fs) imp = rf_cmp(g, F, x, false, g.val[(fs & 0x7FFFFFFFu) - 1], (fs >> 31) != 0) > 0;
-            a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
-        },
-        s_f, s_m);
-}
-
 __device__ inline uint32_t next_pow2(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;
@@ -1493,7 +1195,7 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
 // batch with non-INTEGER values, every fast bucket are queued for the list-driven kernels below,
 // so those launch a few hundred workgroups instead of one per bucket.
 template <bool IMPACT>
-__global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
+static __global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
 k_merge_fast_int(MergeArgs a) {
     const uint32_t b = blockIdx.x;
     // every per-bucket word is loaded up front (independent scalar loads, one latency)
@@ -1537,7 +1239,7 @@ k_merge_fast_int(MergeArgs a) {
 constexpr uint32_t LIST_GRID = 512;
 
 template <bool IMPACT>
-__global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
+static __global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
 k_merge_fast_wide(MergeArgs a) {
     const uint32_t cnt = (uint32_t)a.misc[5];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
@@ -1590,7 +1292,7 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
     if (tid == 0) s_long = 0;
     gen_sort(v, g, false);
     // a row longer than LONG_ROW would serialise this bucket on one lane: the overflow path
-    // folds it with workgroup-wide scans instead (rowfold.h)
+    // folds it with device-wide scans instead (ovf_kernels.h)
     for (uint32_t j = LONG_ROW + tid; j < n; j += blockDim.x)
         if ((g.key[j] >> 32) == (g.key[j - LONG_ROW] >> 32)) s_long = 1;
     __syncthreads();
@@ -1609,7 +1311,7 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
     }
 }
 
-__global__ void __launch_bounds__(MERGE_THREADS)
+static __global__ void __launch_bounds__(MERGE_THREADS)
 k_merge_gen(MergeArgs a) {
     const uint32_t cnt = (uint32_t)a.misc[4];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
@@ -1618,106 +1320,15 @@ k_merge_gen(MergeArgs a) {
     }
 }
 
-// Oversized buckets (Zipf-hot rows): one workgroup per bucket over a global scratch slice, in
-// three launches around device-wide segmented radix sorts (rocPRIM, csrc/ovf_sort.hip):
-//   k_ovf_prep    fields + row keys (row << 32 | position) of every record
-//   [sort by (row, position), all oversized buckets at once]
-//   k_ovf_fold_a  the parallel row fold (rowfold.h), emission; candidate keys for the impacts
-//   [sort the candidates by (group, position)]                    (impact output only)
-//   k_ovf_fold_b  candidate impacts
-struct OvfArgs {
-    const uint64_t *soff;    // scratch slice offset per oversized bucket
-    uint8_t *scratch;
-    const uint32_t *koff;    // offset of the bucket's records in the sort arrays
-    uint32_t *ccnt;          // candidates per bucket (impact pass)
-    uint64_t *key, *key_s;   // (base + row, position) keys, unsorted / sorted
-    uint32_t *val, *val_s;
-    uint64_t *ckey, *ckey_s; // candidate keys, unsorted / sorted
-    uint32_t *cval, *cval_s;
-};
-
-__device__ inline uint32_t ovf_bucket(const MergeArgs &a, const OvfArgs &o, BucketView &v, GenArrays &g,
-                                      FoldArrays &F, bool sorted_keys) {
-    const uint32_t b = a.ovf_list[blockIdx.x];
-    bucket_view(a, b, v);
-    const uint32_t n = v.np + v.nn;
-    carve_ovf(o.scratch + o.soff[blockIdx.x], n, &g, &F);
-    const uint32_t k0 = o.koff[blockIdx.x];
-    F.kbase = k0;
-    g.key = (sorted_keys ? o.key_s : o.key) + k0;
-    g.val = (sorted_keys ? o.val_s : o.val) + k0;
-    F.ckey = o.ckey + k0;
-    F.cval = o.cval + k0;
-    return b;
-}
-
-__global__ void __launch_bounds__(OVF_THREADS) k_ovf_prep(MergeArgs a, OvfArgs o) {
-    BucketView v;
-    GenArrays g;
-    FoldArrays F;
-    ovf_bucket(a, o, v, g, F, false);
-    gen_rowkeys(v, g, false);
-    __syncthreads();
-    const uint32_t n = v.np + v.nn;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) g.key[i] += (uint64_t)F.kbase << 32;
-}
-
-__global__ void __launch_bounds__(OVF_THREADS) k_ovf_fold_a(MergeArgs a, OvfArgs o) {
-    __shared__ uint32_t s_outcnt, s_flag, s_ncand;
-    __shared__ uint32_t s_f[2 * OVF_THREADS], s_m[2 * OVF_THREADS];
-    BucketView v;
-    GenArrays g;
-    FoldArrays F;
-    const uint32_t b = ovf_bucket(a, o, v, g, F, true);
-    if (threadIdx.x == 0) {
-        s_outcnt = 0;
-        s_flag = 0;
-    }
-    Rec *outb = a.out + a.out_off[b];
-    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
-    rowfold_a(a, v, outb, outts, &s_outcnt, &s_flag, g, F, s_f, s_m, &s_ncand, o.ccnt + blockIdx.x);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a.out_cnt[b] = s_outcnt;
-        a.out_flags[b] = s_flag;
-        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
-    }
-}
-
-// the candidates of every bucket were sorted together: bucket k's are the ccnt[k] after those of
-// buckets 0..k-1
-__global__ void __launch_bounds__(OVF_THREADS) k_ovf_fold_b(MergeArgs a, OvfArgs o) {
-    __shared__ uint32_t s_start;
-    __shared__ uint32_t s_f[2 * OVF_THREADS], s_m[2 * OVF_THREADS];
-    BucketView v;
-    GenArrays g;
-    FoldArrays F;
-    ovf_bucket(a, o, v, g, F, true);
-    if (threadIdx.x == 0) {
-        uint32_t st = 0;
-        for (uint32_t k = 0; k < blockIdx.x; k++) st += o.ccnt[k];
-        s_start = st;
-    }
-    __syncthreads();
-    F.ckey = o.ckey_s + s_start;
-    F.cval = o.cval_s + s_start;
-    rowfold_b(a, g, F, o.ccnt[blockIdx.x], s_f, s_m);
-}
-
-// size of the overflow scratch slice for a bucket of n records (256-B aligned)
-__host__ __device__ inline uint64_t ovf_scratch_bytes(uint64_t n) {
-    return (carve_ovf(nullptr, n, nullptr, nullptr) + 255) & ~255ULL;
-}
-
 // crsql_db_versions fold after a successful batch
-__global__ void k_dbv_fold(unsigned long long *__restrict__ dbv, const unsigned long long *__restrict__ batch,
+static __global__ void k_dbv_fold(unsigned long long *__restrict__ dbv, const unsigned long long *__restrict__ batch,
                            uint32_t nsites) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nsites && batch[i] > dbv[i]) dbv[i] = batch[i];
 }
 
 // export: bucket slices -> dense SoA rows
-__global__ void k_export(const Rec *__restrict__ st, const uint64_t *__restrict__ st_ts,
+static __global__ void k_export(const Rec *__restrict__ st, const uint64_t *__restrict__ st_ts,
                          const uint64_t *__restrict__ off, const uint32_t *__restrict__ cnt,
                          const uint64_t *__restrict__ dense, corro_rows o) {
     const uint32_t b = blockIdx.x;
@@ -1741,3 +1352,5 @@ __global__ void k_export(const Rec *__restrict__ st, const uint64_t *__restrict_
 }
 
 }  // namespace corro
+
+#include "ovf_kernels.h"

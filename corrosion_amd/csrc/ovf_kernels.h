@@ -1,0 +1,355 @@
+// Overflow path, device-wide: the buckets too large for a workgroup's LDS, or holding a long row
+// (Zipf-hot rows: tens of thousands of changes in one row), are folded by kernels that span the
+// whole GPU, so a bucket of a million changes is not one CU's work, and a hot row is not a chain
+// of dependent loads in one lane. Every per-record / per-position / per-row array is global,
+// indexed by the bucket's base offset kb (prefix of the oversized buckets' sizes) plus the local
+// index; rows are identified by kb + their owner record.
+//
+// Parallel row fold. Per row, with changes sorted by application position
+// (prior state first, as a prefix):
+//   L_i     = exclusive running max of cl                          (segmented max-scan)
+//   kind_i  = record (cl_i > L_i) | candidate (cl_i == L_i, odd, column change) | no-op
+//   epoch_i = index of the last record at or before i              (segmented count)
+//   W(e, c) = argmax over the epoch's candidates of cid c of (col_version, value, site id),
+//             earliest on ties                                     (segmented argmax-scan)
+//   walk over records: a delete drops the cells, an odd record zeroes them (cv -> 0, value and
+//   metadata kept) and a column record then sets its own cell; each W(e, c) replaces the carried
+//   cell when strictly greater.
+//   impacts: records 1 (2 for a column record that resurrects), candidates 1 iff strictly greater
+//   than the epoch's first element of their cell and every earlier candidate of it, else 0.
+// This equals cr-sqlite's sequential rules (App. A.1) whenever every sentinel and even-cl change
+// carries col_version == cl (App. A.3, what cr-sqlite itself produces): L then only grows by max.
+// Rows that break it (or have more than 2^OVF_EP_BITS epochs) keep the sequential fold
+// (gen_fold_row). The formulation was checked against the oracle on random batches on the CPU
+// (tools/proto_rowfold.py); tests/test_gpu_merge.py checks this implementation.
+//
+// Phases:
+//   k_ovf_load, k_ovf_rowhash       fields; row ids (open addressing per bucket, read-before-CAS)
+//   radix sort by (kb + row, position)                                  [prims.hip, rocPRIM]
+//   k_ovf_gather                    cl in sorted order, row starts
+//   exclusive max-scan of cl by row -> L                                [rocPRIM scan_by_key]
+//   k_ovf_classify                  record / candidate / no-op, record impacts, App. A.3 check
+//   inclusive count of records by row -> epoch
+//   k_ovf_epochs                    the row's record list; candidate keys (row, epoch, cid)
+//   stable radix sort of the candidates by (row, epoch, cid): a group keeps application order
+//   inclusive argmax-scan by group (-> W and every prefix), min-scan of the index (group start)
+//   k_ovf_link                      each group's end is linked under its epoch's record
+//   k_ovf_walk                      one thread per row: the walk over its records, emission;
+//                                   rows outside App. A.3 run the sequential fold instead
+//   k_ovf_impacts                   candidate impacts (strict prefix max, seeded by the epoch's
+//                                   first element of the cell)
+//   k_ovf_finish                    per-bucket counts and flags
+#pragma once
+
+namespace corro {
+
+constexpr uint32_t OVF_EP_BITS = 17;  // epochs per row in a candidate key (beyond: sequential)
+
+struct OvfDev {
+    uint32_t G, K;              // oversized buckets, their records
+    const uint32_t *koff;       // [G + 1] bucket base offsets
+    const uint32_t *slot_off;   // [G] row-hash slot region, next_pow2(2 n) words each
+    // per record (kb + i)
+    uint64_t *pk;
+    int64_t *cv;
+    uint64_t *vk0, *vk1;
+    uint32_t *tc, *cl, *pos, *vmeta, *srank;
+    // per sorted position
+    uint64_t *key, *key_s;
+    uint32_t *val, *val_s;      // local record index
+    uint32_t *rowid, *cl_s, *lx, *recf, *epc, *kind, *pb;
+    // per row (global row id)
+    uint32_t *rstart, *rbad, *rnrec, *recs, *head;
+    uint32_t *scid, *spos, *sz;  // walk state at [rstart, rstart + ncell)
+    uint32_t *ccid, *csrc;       // sequential-fold scratch (GenArrays)
+    int64_t *ccv;
+    // candidates
+    uint64_t *ckey, *ckey_s;
+    uint32_t *cval, *cval_s, *cbest, *cgs, *nxt, *fstg;
+    uint32_t *slots;
+    uint32_t *ocnt, *oflag;     // [G]
+};
+
+__device__ inline uint32_t ovf_bucket_of(const OvfDev &d, uint32_t r) {
+    uint32_t lo = 0, hi = d.G;  // koff[lo] <= r < koff[hi]
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (d.koff[m] <= r) lo = m;
+        else hi = m;
+    }
+    return lo;
+}
+
+// Cell key of the record behind sorted position p (zeroed: the carried cell of a resurrected row).
+__device__ inline int ovf_cmp(const OvfDev &d, uint32_t pa, bool za, uint32_t pb, bool zb) {
+    const uint32_t xa = d.koff[d.pb[pa]] + d.val_s[pa], xb = d.koff[d.pb[pb]] + d.val_s[pb];
+    const int64_t ca = za ? 0 : d.cv[xa], cb = zb ? 0 : d.cv[xb];
+    if (ca != cb) return ca > cb ? 1 : -1;
+    const int vc = value_cmp_f(d.vmeta[xa], d.vk0[xa], d.vk1[xa], d.vmeta[xb], d.vk0[xb], d.vk1[xb]);
+    if (vc != 0) return vc;
+    if (d.srank[xa] != d.srank[xb]) return d.srank[xa] > d.srank[xb] ? 1 : -1;
+    return 0;
+}
+
+// argmax by cell key over sorted positions, the earlier one on ties (x precedes y)
+struct OvfArgmax {
+    OvfDev d;
+    __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const {
+        return ovf_cmp(d, y, false, x, false) > 0 ? y : x;
+    }
+};
+
+#define OVF_LOOP(i, N) for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (N); i += gridDim.x * blockDim.x)
+
+static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
+    OVF_LOOP(r, d.K) {
+        const uint32_t b = ovf_bucket_of(d, r);
+        BucketView v;
+        bucket_view(a, a.ovf_list[b], v);
+        const Rec x = load_rec(v.at(r - d.koff[b]));
+        d.pk[r] = x.pk;
+        d.cv[r] = x.cv;
+        d.vk0[r] = x.v0;
+        d.vk1[r] = x.v1;
+        d.tc[r] = x.tcid;
+        d.cl[r] = x.cl;
+        d.pos[r] = x.pos;
+        d.vmeta[r] = x.meta;
+        d.srank[r] = site_rank_of(a, x.site);
+    }
+}
+
+static __global__ void k_ovf_rowhash(OvfDev d) {
+    OVF_LOOP(r, d.K) {
+        const uint32_t b = ovf_bucket_of(d, r);
+        const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
+        uint32_t S = 1;
+        while (S < 2 * n) S <<= 1;
+        uint32_t *slots = d.slots + d.slot_off[b];
+        const uint64_t pk = d.pk[r];
+        const uint32_t t = d.tc[r] >> 16;
+        uint32_t slot = row_hash(pk, t) & (S - 1), owner;
+        while (true) {
+            // read first: a hot row's slot is claimed once and then only read
+            uint32_t o = __hip_atomic_load(&slots[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (o == 0) o = atomicCAS(&slots[slot], 0u, r - kb + 1);
+            if (o == 0) {
+                owner = r - kb;
+                break;
+            }
+            if (d.pk[kb + o - 1] == pk && (d.tc[kb + o - 1] >> 16) == t) {
+                owner = o - 1;
+                break;
+            }
+            slot = (slot + 1) & (S - 1);
+        }
+        d.key[r] = ((uint64_t)(kb + owner) << 32) | d.pos[r];
+        d.val[r] = r - kb;
+    }
+}
+
+static __global__ void k_ovf_gather(OvfDev d) {
+    OVF_LOOP(p, d.K) {
+        const uint32_t row = (uint32_t)(d.key_s[p] >> 32);
+        const uint32_t b = ovf_bucket_of(d, p);  // buckets stay contiguous after the sort
+        d.pb[p] = b;
+        d.rowid[p] = row;
+        d.cl_s[p] = d.cl[d.koff[b] + d.val_s[p]];
+        d.head[p] = 0;
+        d.fstg[p] = 0;
+        if (p == 0 || (uint32_t)(d.key_s[p - 1] >> 32) != row) {
+            d.rstart[row] = p;
+            d.rbad[row] = 0;
+            d.rnrec[row] = 0;
+        }
+    }
+}
+
+static __global__ void k_ovf_classify(MergeArgs a, OvfDev d) {
+    OVF_LOOP(p, d.K) {
+        const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
+        const uint32_t cl = d.cl_s[p], L = d.lx[p], cid = d.tc[x] & 0xFFFFu, pos = d.pos[x];
+        const uint32_t kd = cl > L ? 1u : ((cl == L && cid != 0 && (cl & 1u)) ? 2u : 0u);
+        d.kind[p] = kd;
+        d.recf[p] = kd == 1 ? 1u : 0u;
+        // outside App. A.3 (see rowfold.h): the sequential fold takes the row
+        if (((cid == 0 || (cl & 1u) == 0) && d.cv[x] != (int64_t)cl) || (!(pos & BATCH_POS) && cid != 0 && !(cl & 1u)))
+            atomicOr(&d.rbad[d.rowid[p]], 1u);
+        if (a.impact && (pos & BATCH_POS) && kd != 2)
+            a.impact[pos & 0x7FFFFFFFu] = kd == 0 ? 0 : ((cid != 0 && (cl & 1u) && (L > 0 || cl > 1)) ? 2 : 1);
+    }
+}
+
+static __global__ void k_ovf_epochs(OvfDev d) {
+    OVF_LOOP(p, d.K) {
+        const uint32_t row = d.rowid[p], c = d.epc[p], kd = d.kind[p];
+        if (kd == 1) {
+            d.recs[d.rstart[row] + c - 1] = p;
+            atomicMax(&d.rnrec[row], c);
+        }
+        uint64_t k = ~0ULL;
+        if (kd == 2) {
+            const uint32_t ep = c - 1;  // a candidate always follows its row's first record
+            const uint32_t cid = d.tc[d.koff[d.pb[p]] + d.val_s[p]] & 0xFFFFu;
+            if (ep >= (1u << OVF_EP_BITS)) atomicOr(&d.rbad[row], 1u);
+            else k = ((uint64_t)row << (OVF_EP_BITS + 16)) | ((uint64_t)ep << 16) | cid;
+        }
+        d.ckey[p] = k;
+        d.cval[p] = p;
+    }
+}
+
+static __global__ void k_ovf_link(OvfDev d) {
+    OVF_LOOP(q, d.K) {
+        const uint64_t k = d.ckey_s[q];
+        if (k == ~0ULL || (q + 1 < d.K && d.ckey_s[q + 1] == k)) continue;
+        const uint32_t row = (uint32_t)(k >> (OVF_EP_BITS + 16));
+        const uint32_t ep = (uint32_t)(k >> 16) & ((1u << OVF_EP_BITS) - 1);
+        const uint32_t R = d.recs[d.rstart[row] + ep];
+        d.nxt[q] = atomicExch(&d.head[R], q + 1);
+    }
+}
+
+// clock rows of one walked row (rf_emit on the global arrays)
+__device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b, const BucketView &v, uint32_t j0,
+                                uint32_t ncell, uint32_t rpos) {
+    const uint32_t kb = d.koff[b];
+    const uint32_t xr = kb + d.val_s[rpos];
+    const uint32_t clr = d.cl[xr], cidr = d.tc[xr] & 0xFFFFu;
+    const bool hs = !(cidr != 0 && clr == 1 && d.lx[rpos] == 0);
+    const int64_t scv = cidr == 0 ? d.cv[xr] : (int64_t)clr;
+    const int64_t rowcl = hs ? scv : 1;
+    const bool cells = (clr & 1u) != 0;
+    const uint32_t cnt = (hs ? 1u : 0u) + (cells ? ncell : 0u);
+    if (cnt == 0) return;
+    const uint32_t bb = a.ovf_list[b];
+    Rec *outb = a.out + a.out_off[bb];
+    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[bb] : nullptr;
+    uint32_t k = atomicAdd(&d.ocnt[b], cnt);
+    if (hs || rowcl != 1) atomicOr(&d.oflag[b], 1u);
+    if (hs) {
+        Rec r = load_rec(v.at(d.val_s[rpos]));
+        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+        r.tcid &= 0xFFFF0000u;
+        r.cv = scv;
+        r.cl = (uint32_t)rowcl;
+        r.v0 = 0;
+        r.v1 = 0;
+        r.meta = CORRO_NULL;
+        r.pos = k;
+        store_rec(outb + k, r);
+        if (a.track_ts) outts[k] = ts;
+        k++;
+    }
+    if (!cells) return;
+    for (uint32_t c = 0; c < ncell; c++) {
+        Rec r = load_rec(v.at(d.val_s[d.spos[j0 + c]]));
+        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+        if (d.sz[j0 + c]) r.cv = 0;
+        r.cl = (uint32_t)rowcl;
+        r.pos = k;
+        store_rec(outb + k, r);
+        if (a.track_ts) outts[k] = ts;
+        k++;
+    }
+}
+
+static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
+    OVF_LOOP(j0, d.K) {
+        const uint32_t row = d.rowid[j0];
+        if (j0 > 0 && d.rowid[j0 - 1] == row) continue;  // one thread per row
+        const uint32_t b = d.pb[j0];
+        const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
+        BucketView v;
+        bucket_view(a, a.ovf_list[b], v);
+        if (d.rbad[row]) {  // outside App. A.3: the sequential fold on this bucket's views
+            GenArrays g;
+            g.key = d.key_s + kb;
+            g.val = d.val_s + kb;
+            g.pk = d.pk + kb;
+            g.cv = d.cv + kb;
+            g.tc = d.tc + kb;
+            g.cl = d.cl + kb;
+            g.pos = d.pos + kb;
+            g.ccid = d.ccid + kb;
+            g.csrc = d.csrc + kb;
+            g.ccv = d.ccv + kb;
+            g.own = nullptr;
+            g.slots = 0;
+            g.P = n;
+            const uint32_t bb = a.ovf_list[b];
+            gen_fold_row(a, v, a.out + a.out_off[bb], a.out_ts ? a.out_ts + a.out_off[bb] : nullptr, &d.ocnt[b],
+                         &d.oflag[b], g, j0 - kb, n);
+            continue;
+        }
+        const uint32_t nrec = d.rnrec[row];
+        uint32_t ncell = 0;
+        for (uint32_t k = 0; k < nrec; k++) {
+            const uint32_t R = d.recs[j0 + k];
+            const uint32_t xR = kb + d.val_s[R];
+            if ((d.cl[xR] & 1u) == 0) {
+                ncell = 0;
+                continue;
+            }
+            for (uint32_t c = 0; c < ncell; c++) d.sz[j0 + c] = 1;
+            auto set = [&](uint32_t cid, uint32_t p, uint32_t z) {
+                for (uint32_t c = 0; c < ncell; c++)
+                    if (d.scid[j0 + c] == cid) {
+                        d.spos[j0 + c] = p;
+                        d.sz[j0 + c] = z;
+                        return;
+                    }
+                d.scid[j0 + ncell] = cid;
+                d.spos[j0 + ncell] = p;
+                d.sz[j0 + ncell] = z;
+                ncell++;
+            };
+            const uint32_t cidR = d.tc[xR] & 0xFFFFu;
+            if (cidR != 0) set(cidR, R, 0);
+            for (uint32_t h = d.head[R]; h; h = d.nxt[h - 1]) {
+                const uint32_t qe = h - 1;  // the group's last candidate
+                const uint32_t cid = (uint32_t)(d.ckey_s[qe] & 0xFFFFu);
+                int found = -1;
+                for (uint32_t c = 0; c < ncell; c++)
+                    if (d.scid[j0 + c] == cid) {
+                        found = (int)c;
+                        break;
+                    }
+                d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((d.spos[j0 + found] + 1) | (d.sz[j0 + found] << 31));
+                const uint32_t w = d.cbest[qe];
+                if (found < 0 || ovf_cmp(d, w, false, d.spos[j0 + found], d.sz[j0 + found] != 0) > 0) set(cid, w, 0);
+            }
+        }
+        if (nrec) ovf_emit(a, d, b, v, j0, ncell, d.recs[j0 + nrec - 1]);
+    }
+}
+
+static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
+    OVF_LOOP(q, d.K) {
+        const uint64_t k = d.ckey_s[q];
+        if (k == ~0ULL) continue;
+        const uint32_t row = (uint32_t)(k >> (OVF_EP_BITS + 16));
+        if (d.rbad[row]) continue;
+        const uint32_t p = d.cval_s[q];
+        const uint32_t pos = d.pos[d.koff[d.pb[p]] + d.val_s[p]];
+        if (!(pos & BATCH_POS)) continue;
+        const bool first = q == 0 || d.ckey_s[q - 1] != k;
+        bool imp = first || ovf_cmp(d, p, false, d.cbest[q - 1], false) > 0;
+        const uint32_t fs = d.fstg[d.cgs[q]];
+        if (imp && fs) imp = ovf_cmp(d, p, false, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0) > 0;
+        a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
+    }
+}
+
+static __global__ void k_ovf_finish(MergeArgs a, OvfDev d) {
+    OVF_LOOP(b, d.G) {
+        const uint32_t bb = a.ovf_list[b];
+        a.out_cnt[bb] = d.ocnt[b];
+        a.out_flags[bb] = d.oflag[b];
+        atomicAdd(&a.misc[2], (unsigned long long)d.ocnt[b]);
+    }
+}
+
+#undef OVF_LOOP
+
+}  // namespace corro

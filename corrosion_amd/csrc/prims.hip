@@ -10,8 +10,11 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_scan_by_key.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "internal.h"
+#include "merge_kernels.h"
 
 namespace corro {
 
@@ -20,6 +23,51 @@ int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t 
                    uint32_t *vo, uint32_t n, uint32_t end_bit, hipStream_t s) {
     const hipError_t e = rocprim::radix_sort_pairs(temp, *temp_bytes, ki, ko, vi, vo, n, 0u, end_bit, s);
     if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("radix sort: ") + hipGetErrorString(e));
+    return CORRO_OK;
+}
+
+struct OvfMax {
+    __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return x > y ? x : y; }
+};
+struct OvfMin {
+    __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return x < y ? x : y; }
+};
+
+// Segmented scans of the device-wide overflow path (ovf_kernels.h): which = 0 L (exclusive max of
+// cl by row), 1 epoch counts (inclusive count of records by row), 2 running argmax and group start
+// of the candidates by group. temp == nullptr -> *temp_bytes = the largest size any of them needs.
+int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStream_t s) {
+    const size_t K = d.K;
+    hipError_t e = hipSuccess;
+    const rocprim::counting_iterator<uint32_t> idx(0u);
+    if (!temp) {
+        size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        e = rocprim::exclusive_scan_by_key(nullptr, t0, d.rowid, d.cl_s, d.lx, 0u, K, OvfMax{},
+                                           rocprim::equal_to<uint32_t>(), s);
+        if (e == hipSuccess)
+            e = rocprim::inclusive_scan_by_key(nullptr, t1, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
+                                               rocprim::equal_to<uint32_t>(), s);
+        if (e == hipSuccess)
+            e = rocprim::inclusive_scan_by_key(nullptr, t2, d.ckey_s, d.cval_s, d.cbest, K, OvfArgmax{d},
+                                               rocprim::equal_to<uint64_t>(), s);
+        if (e == hipSuccess)
+            e = rocprim::inclusive_scan_by_key(nullptr, t3, d.ckey_s, idx, d.cgs, K, OvfMin{},
+                                               rocprim::equal_to<uint64_t>(), s);
+        *temp_bytes = std::max(std::max(t0, t1), std::max(t2, t3));
+    } else if (which == 0) {
+        e = rocprim::exclusive_scan_by_key(temp, *temp_bytes, d.rowid, d.cl_s, d.lx, 0u, K, OvfMax{},
+                                           rocprim::equal_to<uint32_t>(), s);
+    } else if (which == 1) {
+        e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
+                                           rocprim::equal_to<uint32_t>(), s);
+    } else {
+        e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, d.cval_s, d.cbest, K, OvfArgmax{d},
+                                           rocprim::equal_to<uint64_t>(), s);
+        if (e == hipSuccess)
+            e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, idx, d.cgs, K, OvfMin{},
+                                               rocprim::equal_to<uint64_t>(), s);
+    }
+    if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("segmented scan: ") + hipGetErrorString(e));
     return CORRO_OK;
 }
 
