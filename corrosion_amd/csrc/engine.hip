@@ -117,6 +117,11 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
         for (uint64_t **p : u64s) *p = (uint64_t *)take(K * 8);
         d.cv = (int64_t *)take(K * 8);
         d.ccv = (int64_t *)take(K * 8);
+        d.qcv = (int64_t *)take(K * 8);
+        d.qk0 = (uint64_t *)take(K * 8);
+        d.qk1 = (uint64_t *)take(K * 8);
+        d.qm = (uint32_t *)take(K * 4);
+        d.qsr = (uint32_t *)take(K * 4);
         uint32_t **u32s[] = {&d.tc,    &d.cl,     &d.pos,   &d.vmeta, &d.srank, &d.val,    &d.val_s, &d.rowid,
                              &d.cl_s,  &d.lx,     &d.recf,  &d.epc,   &d.kind,  &d.pb,     &d.rstart, &d.rbad,
                              &d.rnrec, &d.recs,   &d.head,  &d.scid,  &d.spos,  &d.sz,     &d.ccid,  &d.csrc,
@@ -159,6 +164,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     hipLaunchKernelGGL(k_ovf_epochs, grid, blk, 0, s, d);
     TRY(launched());
     TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.ckey_s, d.cval, d.cval_s, d.K, ckey_bits, s));
+    hipLaunchKernelGGL(k_ovf_cgather, grid, blk, 0, s, d);
+    TRY(launched());
     TRY(ovf_scans(d_temp, &temp, d, 2, s));
     hipLaunchKernelGGL(k_ovf_link, grid, blk, 0, s, d);
     hipLaunchKernelGGL(k_ovf_walk, grid, blk, 0, s, a, d);

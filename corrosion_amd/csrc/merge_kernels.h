@@ -600,7 +600,7 @@ struct GenArrays {
     uint32_t *csrc;
     int64_t *ccv;
     uint32_t slots;  // pow2
-    uint32_t P;      // pow2 >= n
+    uint32_t P;      // records
 };
 
 __device__ inline void gen_emit(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts,
@@ -786,52 +786,103 @@ __device__ inline void gen_rowkeys(const BucketView &v, const GenArrays &g, bool
     }
 }
 
-__device__ inline void gen_sort(const BucketView &v, const GenArrays &g, bool fields_loaded) {
+// Group the bucket's records by row, each row's records in application order: afterwards
+// g.key[j] = row << 32 | pos and g.val[j] = record index for j < n, a row's records contiguous.
+// A counting sort by row owner (LDS histogram, block scan, scatter through g.own), then every
+// record moves to its rank by position within its row: a handful of barriers instead of a
+// bitonic network's 66. Returns (in *s_long) whether some row is longer than LONG_ROW; g.ccid /
+// g.csrc are free again afterwards (the fold's cell scratch). C = ceil(n / blockDim.x) <= GEN_C.
+constexpr uint32_t GEN_C = (CAP_GEN + MERGE_THREADS - 1) / MERGE_THREADS;
+
+__device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32_t *s_wsum, uint32_t *s_long) {
     const uint32_t n = v.np + v.nn;
     const uint32_t tid = threadIdx.x, nth = blockDim.x;
-    gen_rowkeys(v, g, fields_loaded);
-    for (uint32_t i = n + tid; i < g.P; i += nth) {
-        g.key[i] = ~0ULL;
-        g.val[i] = 0;
+    for (uint32_t i = tid; i < n; i += nth) g.ccid[i] = 0;
+    gen_rowkeys(v, g, false);  // (its barrier orders the zeroing above)
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += nth) atomicAdd(&g.ccid[(uint32_t)(g.key[i] >> 32)], 1u);
+    __syncthreads();
+    // exclusive scan of the counts over owner index: GEN_C consecutive per thread
+    {
+        const uint32_t i0 = tid * GEN_C;
+        uint32_t c[GEN_C], loc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < GEN_C; k++) {
+            c[k] = i0 + k < n ? g.ccid[i0 + k] : 0u;
+            loc += c[k];
+        }
+        const uint32_t lane = tid & 63, w = tid >> 6;
+        uint32_t inc = loc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        if (lane == 63) s_wsum[w] = inc;
+        __syncthreads();
+        uint32_t run = inc - loc;
+        for (uint32_t ww = 0; ww < w; ww++) run += s_wsum[ww];
+#pragma unroll
+        for (uint32_t k = 0; k < GEN_C; k++)
+            if (i0 + k < n) {
+                g.csrc[i0 + k] = run;
+                run += c[k];
+            }
     }
     __syncthreads();
-    // bitonic sort of (row, position)
-    for (uint32_t k = 2; k <= g.P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = tid; i < g.P; i += nth) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t x = g.key[i], y = g.key[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((x > y) == up) {
-                        g.key[i] = y;
-                        g.key[ixj] = x;
-                        const uint32_t t = g.val[i];
-                        g.val[i] = g.val[ixj];
-                        g.val[ixj] = t;
-                    }
-                }
-            }
-            __syncthreads();
+    // scatter record indices by row (g.own: the row table is dead; GEN_SLOTS >= CAP_GEN)
+    for (uint32_t i = tid; i < n; i += nth) g.own[atomicAdd(&g.csrc[(uint32_t)(g.key[i] >> 32)], 1u)] = i;
+    __syncthreads();
+    uint64_t kk[GEN_C];
+#pragma unroll
+    for (uint32_t k = 0; k < GEN_C; k++) {
+        const uint32_t j = k * nth + tid;
+        if (j < n) {
+            kk[k] = g.key[g.own[j]];
         }
     }
-}
-
-__device__ inline void gen_body(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts,
-                                uint32_t *outcnt, uint32_t *flag, const GenArrays &g, bool fields_loaded) {
-    const uint32_t n = v.np + v.nn;
-    gen_sort(v, g, fields_loaded);
-    // one lane per row, in application order
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        if (i == 0 || (g.key[i] >> 32) != (g.key[i - 1] >> 32))
-            gen_fold_row(a, v, outb, outts, outcnt, flag, g, i, n);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < GEN_C; k++) {
+        const uint32_t j = k * nth + tid;
+        if (j < n) {
+            g.key[j] = kk[k];
+            g.val[j] = g.own[j];
+        }
     }
-}
-
-__device__ inline uint32_t next_pow2(uint32_t x) {
-    uint32_t p = 1;
-    while (p < x) p <<= 1;
-    return p;
+    __syncthreads();
+    // each row's records by position: a record's rank in its row is the number of the row's
+    // records with a smaller key (positions are distinct), counted by every lane at once -- no
+    // dependent chain, a row of c records costs its lanes c LDS reads each (csrc[r] is now the
+    // row's end, ccid[r] its length)
+    uint32_t dst[GEN_C], vv[GEN_C];
+#pragma unroll
+    for (uint32_t k = 0; k < GEN_C; k++) {
+        const uint32_t j = k * nth + tid;
+        dst[k] = 0xFFFFFFFFu;
+        if (j < n) {
+            const uint64_t key = g.key[j];
+            const uint32_t r = (uint32_t)(key >> 32), c = g.ccid[r];
+            if (c > LONG_ROW) {  // the bucket goes to the overflow path
+                *s_long = 1;
+                continue;
+            }
+            const uint32_t s = g.csrc[r] - c;
+            uint32_t rank = 0;
+            for (uint32_t t = s; t < s + c; t++) rank += g.key[t] < key ? 1u : 0u;
+            kk[k] = key;
+            vv[k] = g.val[j];
+            dst[k] = s + rank;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < GEN_C; k++)
+        if (dst[k] != 0xFFFFFFFFu) {
+            g.key[dst[k]] = kk[k];
+            g.val[dst[k]] = vv[k];
+        }
+    __syncthreads();
 }
 
 constexpr size_t GEN_LDS = (size_t)CAP_GEN * (8 + 8 + 4 + 4 + 4) + (size_t)GEN_SLOTS * 4 +
@@ -1287,15 +1338,12 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
     g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
     g.own = reinterpret_cast<uint32_t *>(p);
     g.slots = GEN_SLOTS;
-    g.P = next_pow2(n);
-    __shared__ uint32_t s_long;
+    g.P = n;
+    __shared__ uint32_t s_long, s_wsum[MERGE_THREADS / 64];
     if (tid == 0) s_long = 0;
-    gen_sort(v, g, false);
     // a row longer than LONG_ROW would serialise this bucket on one lane: the overflow path
     // folds it with device-wide scans instead (ovf_kernels.h)
-    for (uint32_t j = LONG_ROW + tid; j < n; j += blockDim.x)
-        if ((g.key[j] >> 32) == (g.key[j - LONG_ROW] >> 32)) s_long = 1;
-    __syncthreads();
+    gen_group(v, g, s_wsum, &s_long);
     if (s_long) {
         if (tid == 0) push_overflow(a, b);
         return;

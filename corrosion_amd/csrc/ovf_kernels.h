@@ -32,6 +32,7 @@
 //   inclusive count of records by row -> epoch
 //   k_ovf_epochs                    the row's record list; candidate keys (row, epoch, cid)
 //   stable radix sort of the candidates by (row, epoch, cid): a group keeps application order
+//   k_ovf_cgather                   the candidates' cell keys in candidate-sorted order
 //   inclusive argmax-scan by group (-> W and every prefix), min-scan of the index (group start)
 //   k_ovf_link                      each group's end is linked under its epoch's record
 //   k_ovf_walk                      one thread per row: the walk over its records, emission;
@@ -66,6 +67,10 @@ struct OvfDev {
     // candidates
     uint64_t *ckey, *ckey_s;
     uint32_t *cval, *cval_s, *cbest, *cgs, *nxt, *fstg;
+    // candidates' cell keys gathered in candidate-sorted order (the argmax scan reads neighbours)
+    int64_t *qcv;
+    uint64_t *qk0, *qk1;
+    uint32_t *qm, *qsr;
     uint32_t *slots;
     uint32_t *ocnt, *oflag;     // [G]
 };
@@ -80,22 +85,39 @@ __device__ inline uint32_t ovf_bucket_of(const OvfDev &d, uint32_t r) {
     return lo;
 }
 
-// Cell key of the record behind sorted position p (zeroed: the carried cell of a resurrected row).
-__device__ inline int ovf_cmp(const OvfDev &d, uint32_t pa, bool za, uint32_t pb, bool zb) {
-    const uint32_t xa = d.koff[d.pb[pa]] + d.val_s[pa], xb = d.koff[d.pb[pb]] + d.val_s[pb];
-    const int64_t ca = za ? 0 : d.cv[xa], cb = zb ? 0 : d.cv[xb];
-    if (ca != cb) return ca > cb ? 1 : -1;
-    const int vc = value_cmp_f(d.vmeta[xa], d.vk0[xa], d.vk1[xa], d.vmeta[xb], d.vk0[xb], d.vk1[xb]);
+// Cell key (col_version, value order, site rank) of a change; `z` = the carried cell of a
+// resurrected row (col_version 0, value and metadata kept).
+struct OvfKey {
+    int64_t cv;
+    uint64_t k0, k1;
+    uint32_t m, sr;
+};
+
+// by sorted position p
+__device__ inline OvfKey ovf_key_p(const OvfDev &d, uint32_t p, bool z) {
+    const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
+    return OvfKey{z ? 0 : d.cv[x], d.vk0[x], d.vk1[x], d.vmeta[x], d.srank[x]};
+}
+
+// by candidate-sorted index q
+__device__ inline OvfKey ovf_key_q(const OvfDev &d, uint32_t q) {
+    return OvfKey{d.qcv[q], d.qk0[q], d.qk1[q], d.qm[q], d.qsr[q]};
+}
+
+// >0: a greater
+__device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b) {
+    if (a.cv != b.cv) return a.cv > b.cv ? 1 : -1;
+    const int vc = value_cmp_f(a.m, a.k0, a.k1, b.m, b.k0, b.k1);
     if (vc != 0) return vc;
-    if (d.srank[xa] != d.srank[xb]) return d.srank[xa] > d.srank[xb] ? 1 : -1;
+    if (a.sr != b.sr) return a.sr > b.sr ? 1 : -1;
     return 0;
 }
 
-// argmax by cell key over sorted positions, the earlier one on ties (x precedes y)
+// argmax by cell key over candidate-sorted indices, the earlier one on ties (x precedes y)
 struct OvfArgmax {
     OvfDev d;
     __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const {
-        return ovf_cmp(d, y, false, x, false) > 0 ? y : x;
+        return ovf_kcmp(ovf_key_q(d, y), ovf_key_q(d, x)) > 0 ? y : x;
     }
 };
 
@@ -120,6 +142,7 @@ static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
 }
 
 static __global__ void k_ovf_rowhash(OvfDev d) {
+    const uint32_t lane = threadIdx.x & 63;
     OVF_LOOP(r, d.K) {
         const uint32_t b = ovf_bucket_of(d, r);
         const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
@@ -128,21 +151,39 @@ static __global__ void k_ovf_rowhash(OvfDev d) {
         uint32_t *slots = d.slots + d.slot_off[b];
         const uint64_t pk = d.pk[r];
         const uint32_t t = d.tc[r] >> 16;
-        uint32_t slot = row_hash(pk, t) & (S - 1), owner;
-        while (true) {
-            // read first: a hot row's slot is claimed once and then only read
-            uint32_t o = __hip_atomic_load(&slots[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (o == 0) o = atomicCAS(&slots[slot], 0u, r - kb + 1);
-            if (o == 0) {
-                owner = r - kb;
-                break;
+        auto probe = [&]() -> uint32_t {
+            uint32_t slot = row_hash(pk, t) & (S - 1);
+            while (true) {
+                // a plain read first: a claimed slot is only read afterwards
+                uint32_t o = slots[slot];
+                if (o == 0) o = atomicCAS(&slots[slot], 0u, r - kb + 1);
+                if (o == 0) return r - kb;
+                if (d.pk[kb + o - 1] == pk && (d.tc[kb + o - 1] >> 16) == t) return o - 1;
+                slot = (slot + 1) & (S - 1);
             }
-            if (d.pk[kb + o - 1] == pk && (d.tc[kb + o - 1] >> 16) == t) {
-                owner = o - 1;
-                break;
+        };
+        // A Zipf-hot row fills whole waves, and all of its lanes start at once: every one of them
+        // would read the unclaimed slot and CAS it, a chain of serialised same-address atomics
+        // as long as the row. Lanes of one wave that share a row let one leader probe for them.
+        bool todo = true;
+        uint32_t owner = 0;
+        for (int round = 0; round < 2; round++) {
+            const uint64_t act = __ballot(todo);
+            if (!act) break;
+            const int leader = __ffsll((unsigned long long)act) - 1;
+            const uint64_t lpk = __shfl(pk, leader);
+            const uint32_t lt = __shfl(t, leader);
+            const bool mine = todo && pk == lpk && t == lt;
+            if (__popcll(__ballot(mine)) < 8) break;  // (wave-uniform) not a hot row
+            uint32_t o = 0;
+            if ((int)lane == leader) o = probe();
+            o = __shfl(o, leader);
+            if (mine) {
+                owner = o;
+                todo = false;
             }
-            slot = (slot + 1) & (S - 1);
         }
+        if (todo) owner = probe();
         d.key[r] = ((uint64_t)(kb + owner) << 32) | d.pos[r];
         d.val[r] = r - kb;
     }
@@ -196,6 +237,18 @@ static __global__ void k_ovf_epochs(OvfDev d) {
         }
         d.ckey[p] = k;
         d.cval[p] = p;
+    }
+}
+
+static __global__ void k_ovf_cgather(OvfDev d) {
+    OVF_LOOP(q, d.K) {
+        const uint32_t p = d.cval_s[q];
+        const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
+        d.qcv[q] = d.cv[x];
+        d.qk0[q] = d.vk0[x];
+        d.qk1[q] = d.vk1[x];
+        d.qm[q] = d.vmeta[x];
+        d.qsr[q] = d.srank[x];
     }
 }
 
@@ -316,8 +369,10 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
                         break;
                     }
                 d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((d.spos[j0 + found] + 1) | (d.sz[j0 + found] << 31));
-                const uint32_t w = d.cbest[qe];
-                if (found < 0 || ovf_cmp(d, w, false, d.spos[j0 + found], d.sz[j0 + found] != 0) > 0) set(cid, w, 0);
+                const uint32_t wq = d.cbest[qe];
+                if (found < 0 ||
+                    ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(d, d.spos[j0 + found], d.sz[j0 + found] != 0)) > 0)
+                    set(cid, d.cval_s[wq], 0);
             }
         }
         if (nrec) ovf_emit(a, d, b, v, j0, ncell, d.recs[j0 + nrec - 1]);
@@ -334,9 +389,10 @@ static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
         const uint32_t pos = d.pos[d.koff[d.pb[p]] + d.val_s[p]];
         if (!(pos & BATCH_POS)) continue;
         const bool first = q == 0 || d.ckey_s[q - 1] != k;
-        bool imp = first || ovf_cmp(d, p, false, d.cbest[q - 1], false) > 0;
+        const OvfKey kq = ovf_key_q(d, q);
+        bool imp = first || ovf_kcmp(kq, ovf_key_q(d, d.cbest[q - 1])) > 0;
         const uint32_t fs = d.fstg[d.cgs[q]];
-        if (imp && fs) imp = ovf_cmp(d, p, false, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0) > 0;
+        if (imp && fs) imp = ovf_kcmp(kq, ovf_key_p(d, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0)) > 0;
         a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
     }
 }

@@ -1,5 +1,5 @@
 // Device-wide primitives from rocPRIM, kept in one translation unit (rocPRIM is heavy to compile):
-// the overflow path's radix sort and the exclusive scan that turns per-entry need counts into CSR
+// the overflow path's radix sorts and segmented scans, and the exclusive scan that turns per-entry need counts into CSR
 // offsets for corro_compute_needs' second pass.
 //
 // Radix sort (overflow path): Keys carry the bucket's base offset in
@@ -35,7 +35,8 @@ struct OvfMin {
 
 // Segmented scans of the device-wide overflow path (ovf_kernels.h): which = 0 L (exclusive max of
 // cl by row), 1 epoch counts (inclusive count of records by row), 2 running argmax and group start
-// of the candidates by group. temp == nullptr -> *temp_bytes = the largest size any of them needs.
+// of the candidates by group, both over candidate-sorted indices. temp == nullptr -> *temp_bytes =
+// the largest size any of them needs.
 int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStream_t s) {
     const size_t K = d.K;
     hipError_t e = hipSuccess;
@@ -48,7 +49,7 @@ int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStr
             e = rocprim::inclusive_scan_by_key(nullptr, t1, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
                                                rocprim::equal_to<uint32_t>(), s);
         if (e == hipSuccess)
-            e = rocprim::inclusive_scan_by_key(nullptr, t2, d.ckey_s, d.cval_s, d.cbest, K, OvfArgmax{d},
+            e = rocprim::inclusive_scan_by_key(nullptr, t2, d.ckey_s, idx, d.cbest, K, OvfArgmax{d},
                                                rocprim::equal_to<uint64_t>(), s);
         if (e == hipSuccess)
             e = rocprim::inclusive_scan_by_key(nullptr, t3, d.ckey_s, idx, d.cgs, K, OvfMin{},
@@ -61,7 +62,7 @@ int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStr
         e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
                                            rocprim::equal_to<uint32_t>(), s);
     } else {
-        e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, d.cval_s, d.cbest, K, OvfArgmax{d},
+        e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, idx, d.cbest, K, OvfArgmax{d},
                                            rocprim::equal_to<uint64_t>(), s);
         if (e == hipSuccess)
             e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, idx, d.cgs, K, OvfMin{},

@@ -18,4 +18,7 @@ if [ -n "$SYNC" ]; then
   run sync_pmc_FETCH 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/sync_pmc_FETCH -o run -- python bench_sync.py --steps 2 --warmup 1 --cpu-sample 1000
   run sync_pmc_WRITE 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/sync_pmc_WRITE -o run -- python bench_sync.py --steps 2 --warmup 1 --cpu-sample 1000
 fi
+if [ -n "$C5" ]; then
+  run c5_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/c5_trace -o run -- python tools/bench_config5.py --sizes 16000000
+fi
 echo "=== done"
