@@ -91,12 +91,16 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     uint32_t rb = 1;
     while ((1ULL << rb) <= K) rb++;
     const uint32_t key_bits = 32 + rb;
-    const uint32_t ckey_bits = std::min<uint32_t>(64, rb + OVF_EP_BITS + 16);
+    uint32_t maxc = 0, cid_bits = 1;
+    for (const auto &t : ctx->tables) maxc = std::max<uint32_t>(maxc, (uint32_t)t.cols.size());
+    while ((1u << cid_bits) <= maxc) cid_bits++;
+    const uint32_t ckey_bits = rb + cid_bits;
     auto al = [](uint64_t x) { return (x + 255) & ~255ULL; };
     // pass 0 sizes the arrays, pass 1 carves them out of d_ovf_sort
     OvfDev d{};
     d.G = (uint32_t)novf;
     d.K = (uint32_t)K;
+    d.cid_bits = cid_bits;
     uint64_t bytes = 0;
     uint8_t *base = nullptr;
     auto take = [&](uint64_t n) {
@@ -162,6 +166,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     TRY(launched());
     TRY(ovf_scans(d_temp, &temp, d, 1, s));
     hipLaunchKernelGGL(k_ovf_epochs, grid, blk, 0, s, d);
+    hipLaunchKernelGGL(k_ovf_ckeys, grid, blk, 0, s, d);
     TRY(launched());
     TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.ckey_s, d.cval, d.cval_s, d.K, ckey_bits, s));
     hipLaunchKernelGGL(k_ovf_cgather, grid, blk, 0, s, d);

@@ -626,15 +626,23 @@ __device__ inline void gen_emit(const MergeArgs &a, const BucketView &v, Rec *ou
         if (a.track_ts) outts[k] = ts;
         k++;
     }
-    for (uint32_t c = 0; c < ncell; c++) {
-        Rec r = load_rec(v.at(g.csrc[s + c]));
-        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
-        r.cv = g.ccv[s + c];
-        r.cl = (uint32_t)L;
-        r.pos = k;
-        store_rec(outb + k, r);
-        if (a.track_ts) outts[k] = ts;
-        k++;
+    // four cells at a time, their loads issued together (clamped, so no branch splits them)
+    constexpr uint32_t EU = 4;
+    for (uint32_t c0 = 0; c0 < ncell; c0 += EU) {
+        Rec r[EU];
+#pragma unroll
+        for (uint32_t u = 0; u < EU; u++) r[u] = load_rec(v.at(g.csrc[s + min(c0 + u, ncell - 1)]));
+#pragma unroll
+        for (uint32_t u = 0; u < EU; u++) {
+            if (c0 + u >= ncell) break;
+            const uint64_t ts = a.track_ts ? rec_ts(a, v, r[u]) : 0ULL;
+            r[u].cv = g.ccv[s + c0 + u];
+            r[u].cl = (uint32_t)L;
+            r[u].pos = k;
+            store_rec(outb + k, r[u]);
+            if (a.track_ts) outts[k] = ts;
+            k++;
+        }
     }
 }
 

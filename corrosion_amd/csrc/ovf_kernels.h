@@ -19,8 +19,7 @@
 //   than the epoch's first element of their cell and every earlier candidate of it, else 0.
 // This equals cr-sqlite's sequential rules (App. A.1) whenever every sentinel and even-cl change
 // carries col_version == cl (App. A.3, what cr-sqlite itself produces): L then only grows by max.
-// Rows that break it (or have more than 2^OVF_EP_BITS epochs) keep the sequential fold
-// (gen_fold_row). The formulation was checked against the oracle on random batches on the CPU
+// Rows that break it keep the sequential fold (gen_fold_row). The formulation was checked against the oracle on random batches on the CPU
 // (tools/proto_rowfold.py); tests/test_gpu_merge.py checks this implementation.
 //
 // Phases:
@@ -30,8 +29,8 @@
 //   exclusive max-scan of cl by row -> L                                [rocPRIM scan_by_key]
 //   k_ovf_classify                  record / candidate / no-op, record impacts, App. A.3 check
 //   inclusive count of records by row -> epoch
-//   k_ovf_epochs                    the row's record list; candidate keys (row, epoch, cid)
-//   stable radix sort of the candidates by (row, epoch, cid): a group keeps application order
+//   k_ovf_epochs, k_ovf_ckeys       the row's record list; candidate keys (epoch's record, cid)
+//   stable radix sort of the candidates by (epoch, cid): a group keeps application order
 //   k_ovf_cgather                   the candidates' cell keys in candidate-sorted order
 //   inclusive argmax-scan by group (-> W and every prefix), min-scan of the index (group start)
 //   k_ovf_link                      each group's end is linked under its epoch's record
@@ -44,10 +43,9 @@
 
 namespace corro {
 
-constexpr uint32_t OVF_EP_BITS = 17;  // epochs per row in a candidate key (beyond: sequential)
-
 struct OvfDev {
     uint32_t G, K;              // oversized buckets, their records
+    uint32_t cid_bits;          // a candidate key is (epoch's record position) << cid_bits | cid
     const uint32_t *koff;       // [G + 1] bucket base offsets
     const uint32_t *slot_off;   // [G] row-hash slot region, next_pow2(2 n) words each
     // per record (kb + i)
@@ -129,6 +127,7 @@ static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
         BucketView v;
         bucket_view(a, a.ovf_list[b], v);
         const Rec x = load_rec(v.at(r - d.koff[b]));
+        d.pb[r] = b;  // (buckets stay contiguous after the sort: also the bucket of position r)
         d.pk[r] = x.pk;
         d.cv[r] = x.cv;
         d.vk0[r] = x.v0;
@@ -144,7 +143,7 @@ static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
 static __global__ void k_ovf_rowhash(OvfDev d) {
     const uint32_t lane = threadIdx.x & 63;
     OVF_LOOP(r, d.K) {
-        const uint32_t b = ovf_bucket_of(d, r);
+        const uint32_t b = d.pb[r];
         const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
         uint32_t S = 1;
         while (S < 2 * n) S <<= 1;
@@ -192,8 +191,7 @@ static __global__ void k_ovf_rowhash(OvfDev d) {
 static __global__ void k_ovf_gather(OvfDev d) {
     OVF_LOOP(p, d.K) {
         const uint32_t row = (uint32_t)(d.key_s[p] >> 32);
-        const uint32_t b = ovf_bucket_of(d, p);  // buckets stay contiguous after the sort
-        d.pb[p] = b;
+        const uint32_t b = d.pb[p];
         d.rowid[p] = row;
         d.cl_s[p] = d.cl[d.koff[b] + d.val_s[p]];
         d.head[p] = 0;
@@ -223,17 +221,23 @@ static __global__ void k_ovf_classify(MergeArgs a, OvfDev d) {
 
 static __global__ void k_ovf_epochs(OvfDev d) {
     OVF_LOOP(p, d.K) {
-        const uint32_t row = d.rowid[p], c = d.epc[p], kd = d.kind[p];
-        if (kd == 1) {
-            d.recs[d.rstart[row] + c - 1] = p;
-            atomicMax(&d.rnrec[row], c);
-        }
+        if (d.kind[p] != 1) continue;
+        const uint32_t row = d.rowid[p], c = d.epc[p];
+        d.recs[d.rstart[row] + c - 1] = p;
+        atomicMax(&d.rnrec[row], c);
+    }
+}
+
+// candidate keys: (position of the epoch's record, cid), ~0 for the rest (sorts last). The record
+// position names (row, epoch) in log2(K) bits, so the sort has few digits to go through.
+static __global__ void k_ovf_ckeys(OvfDev d) {
+    const uint32_t cmask = (1u << d.cid_bits) - 1;
+    OVF_LOOP(p, d.K) {
         uint64_t k = ~0ULL;
-        if (kd == 2) {
-            const uint32_t ep = c - 1;  // a candidate always follows its row's first record
-            const uint32_t cid = d.tc[d.koff[d.pb[p]] + d.val_s[p]] & 0xFFFFu;
-            if (ep >= (1u << OVF_EP_BITS)) atomicOr(&d.rbad[row], 1u);
-            else k = ((uint64_t)row << (OVF_EP_BITS + 16)) | ((uint64_t)ep << 16) | cid;
+        if (d.kind[p] == 2) {  // a candidate always follows its row's first record
+            const uint32_t R = d.recs[d.rstart[d.rowid[p]] + d.epc[p] - 1];
+            const uint32_t cid = d.tc[d.koff[d.pb[p]] + d.val_s[p]] & cmask;
+            k = ((uint64_t)R << d.cid_bits) | cid;
         }
         d.ckey[p] = k;
         d.cval[p] = p;
@@ -256,10 +260,7 @@ static __global__ void k_ovf_link(OvfDev d) {
     OVF_LOOP(q, d.K) {
         const uint64_t k = d.ckey_s[q];
         if (k == ~0ULL || (q + 1 < d.K && d.ckey_s[q + 1] == k)) continue;
-        const uint32_t row = (uint32_t)(k >> (OVF_EP_BITS + 16));
-        const uint32_t ep = (uint32_t)(k >> 16) & ((1u << OVF_EP_BITS) - 1);
-        const uint32_t R = d.recs[d.rstart[row] + ep];
-        d.nxt[q] = atomicExch(&d.head[R], q + 1);
+        d.nxt[q] = atomicExch(&d.head[(uint32_t)(k >> d.cid_bits)], q + 1);
     }
 }
 
@@ -361,7 +362,7 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
             if (cidR != 0) set(cidR, R, 0);
             for (uint32_t h = d.head[R]; h; h = d.nxt[h - 1]) {
                 const uint32_t qe = h - 1;  // the group's last candidate
-                const uint32_t cid = (uint32_t)(d.ckey_s[qe] & 0xFFFFu);
+                const uint32_t cid = (uint32_t)d.ckey_s[qe] & ((1u << d.cid_bits) - 1);
                 int found = -1;
                 for (uint32_t c = 0; c < ncell; c++)
                     if (d.scid[j0 + c] == cid) {
@@ -383,8 +384,7 @@ static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
     OVF_LOOP(q, d.K) {
         const uint64_t k = d.ckey_s[q];
         if (k == ~0ULL) continue;
-        const uint32_t row = (uint32_t)(k >> (OVF_EP_BITS + 16));
-        if (d.rbad[row]) continue;
+        if (d.rbad[d.rowid[(uint32_t)(k >> d.cid_bits)]]) continue;
         const uint32_t p = d.cval_s[q];
         const uint32_t pos = d.pos[d.koff[d.pb[p]] + d.val_s[p]];
         if (!(pos & BATCH_POS)) continue;
