@@ -323,3 +323,140 @@ uint64_t of_export(const of_state *s, of_rows *o) {
 void of_db_versions(const of_state *s, int64_t *out) {
     memcpy(out, s->dbv, sizeof(int64_t) * s->nsites);
 }
+
+/* ---- pk-sharded fold (SURVEY.md §8(d) CPU baseline (ii), and the checker at >= 512M changes) ----
+ * Rows merge independently, so S shard states, each owning the rows whose
+ * mix64(table, pk) falls in it, folded by S threads over their changes in application order, give
+ * exactly the sequential fold's rows and impacts; crsql_db_versions is the per-site max over shards. */
+#include <pthread.h>
+
+static uint32_t shard_of(uint32_t table, uint64_t pk, uint32_t nshards) {
+    return (uint32_t)(((mix64(pk ^ ((uint64_t)table << 48) ^ table) >> 32) * nshards) >> 32);
+}
+
+typedef struct {
+    of_state **shards;
+    uint32_t nshards, nthreads, t;
+    const of_changes *in;
+    uint8_t *impact;
+    uint8_t *sid;        /* shard id per change */
+    uint64_t *counts;    /* [nthreads][nshards] */
+    uint64_t *offs;      /* [nthreads][nshards] start of this slice's run in idx */
+    uint32_t *idx;       /* change indices grouped by shard, application order within a shard */
+    uint64_t *shard_off; /* [nshards + 1] */
+    int phase;
+} sh_job;
+
+static void *sh_worker(void *p) {
+    sh_job *j = (sh_job *)p;
+    uint64_t n = j->in->n;
+    uint64_t lo = n * j->t / j->nthreads, hi = n * (j->t + 1) / j->nthreads;
+    if (j->phase == 0) {
+        uint64_t *c = j->counts + (size_t)j->t * j->nshards;
+        for (uint64_t i = lo; i < hi; i++) {
+            uint32_t s = shard_of(j->in->table_cid[i] >> 16, j->in->pk[i], j->nshards);
+            j->sid[i] = (uint8_t)s;
+            c[s]++;
+        }
+    } else if (j->phase == 1) {
+        uint64_t *o = j->offs + (size_t)j->t * j->nshards;
+        for (uint64_t i = lo; i < hi; i++) j->idx[o[j->sid[i]]++] = (uint32_t)i;
+    } else {
+        for (uint32_t s = j->t; s < j->nshards; s += j->nthreads) {
+            of_state *st = j->shards[s];
+            for (uint64_t k = j->shard_off[s]; k < j->shard_off[s + 1]; k++) {
+                uint64_t i = j->idx[k];
+                int imp = apply_one(st, j->in, i);
+                if (j->impact) j->impact[i] = (uint8_t)imp;
+            }
+        }
+    }
+    return NULL;
+}
+
+static void sh_run(sh_job *base, uint32_t nthreads, int phase) {
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+    sh_job *jobs = (sh_job *)malloc(sizeof(sh_job) * nthreads);
+    for (uint32_t t = 0; t < nthreads; t++) {
+        jobs[t] = *base; jobs[t].t = t; jobs[t].phase = phase;
+        pthread_create(&th[t], NULL, sh_worker, &jobs[t]);
+    }
+    for (uint32_t t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(jobs); free(th);
+}
+
+/* Apply one batch to `nshards` (<= 256) shard states with `nthreads` threads. Returns 0, or -1 if
+ * the batch exceeds 2^32-1 changes. */
+int of_apply_sharded(of_state **shards, uint32_t nshards, const of_changes *in, uint8_t *impact_out,
+                     uint32_t nthreads) {
+    if (in->n >= (1ULL << 32) || nshards == 0 || nshards > 256) return -1;
+    if (nthreads == 0) nthreads = 1;
+    sh_job b;
+    memset(&b, 0, sizeof(b));
+    b.shards = shards; b.nshards = nshards; b.nthreads = nthreads; b.in = in; b.impact = impact_out;
+    b.sid = (uint8_t *)malloc(in->n + 1);
+    b.counts = (uint64_t *)calloc((size_t)nthreads * nshards, sizeof(uint64_t));
+    b.offs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nthreads * nshards);
+    b.idx = (uint32_t *)malloc(sizeof(uint32_t) * (in->n + 1));
+    b.shard_off = (uint64_t *)malloc(sizeof(uint64_t) * (nshards + 1));
+    sh_run(&b, nthreads, 0);
+    uint64_t run = 0;  /* shard-major, slice-minor: stable in application order */
+    for (uint32_t s = 0; s < nshards; s++) {
+        b.shard_off[s] = run;
+        for (uint32_t t = 0; t < nthreads; t++) {
+            b.offs[(size_t)t * nshards + s] = run;
+            run += b.counts[(size_t)t * nshards + s];
+        }
+    }
+    b.shard_off[nshards] = run;
+    sh_run(&b, nthreads, 1);
+    sh_run(&b, nthreads, 2);
+    free(b.sid); free(b.counts); free(b.offs); free(b.idx); free(b.shard_off);
+    return 0;
+}
+
+/* ---- order-independent digest of crsql_changes rows (checksum of per-row checksums) ---- */
+static uint64_t row_hash(uint64_t pk, uint32_t tcid, int64_t cv, int64_t dbv, int64_t cl, uint32_t seq,
+                         uint32_t site, uint64_t ts, uint8_t vt, uint8_t vl, uint64_t v0, uint64_t v1) {
+    uint64_t h = mix64(pk + 0x9E3779B97F4A7C15ULL);
+    h = mix64(h ^ tcid);
+    h = mix64(h ^ (uint64_t)cv);
+    h = mix64(h ^ (uint64_t)dbv);
+    h = mix64(h ^ (uint64_t)cl);
+    h = mix64(h ^ (((uint64_t)seq << 32) | site));
+    h = mix64(h ^ ts);
+    h = mix64(h ^ (((uint64_t)vt << 8) | vl));
+    h = mix64(h ^ v0);
+    h = mix64(h ^ v1);
+    return h;
+}
+
+/* out[0] = rows, out[1] = sum of row hashes, out[2] = xor of rotated row hashes */
+static void digest_add(uint64_t out[3], uint64_t h) {
+    out[0]++; out[1] += h; out[2] ^= (h << 17) | (h >> 47);
+}
+
+void of_rows_digest(const of_rows *o, uint64_t n, uint64_t out[3]) {
+    out[0] = out[1] = out[2] = 0;
+    for (uint64_t k = 0; k < n; k++)
+        digest_add(out, row_hash(o->pk[k], o->table_cid[k], o->col_version[k], o->db_version[k], o->cl[k],
+                                 o->seq[k], o->site[k], o->ts[k], o->val_type[k], o->val_len[k],
+                                 o->val0[k], o->val1[k]));
+}
+
+/* digest of the rows of_export would emit (any order) */
+void of_state_digest(const of_state *s, uint64_t out[3]) {
+    for (uint64_t i = 0; i < s->cap; i++) {
+        const of_row *r = &s->rows[i];
+        if (!r->used) continue;
+        int64_t L = row_L(r);
+        if (r->has_sent)
+            digest_add(out, row_hash(r->pk, r->table << 16, r->sent.cv, r->sent.dbv, L, r->sent.seq, r->sent.site,
+                                     r->sent.ts, OF_NULL, 0, 0, 0));
+        for (uint32_t k = 0; k < r->ncells; k++) {
+            const of_cell *c = &r->cells[k];
+            digest_add(out, row_hash(r->pk, (r->table << 16) | c->cid, c->cv, c->dbv, L, c->seq, c->site, c->ts,
+                                     c->vtype, c->vlen, c->v0, c->v1));
+        }
+    }
+}

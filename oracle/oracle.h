@@ -51,6 +51,13 @@ void of_apply(of_state *s, const of_changes *in, uint8_t *impact_out);
 uint64_t of_count(const of_state *s);
 uint64_t of_export(const of_state *s, of_rows *out);
 void of_db_versions(const of_state *s, int64_t *out);
+/* pk-sharded parallel fold: shards[s] owns the rows hashed to s (<= 256 shards) */
+int of_apply_sharded(of_state **shards, uint32_t nshards, const of_changes *in, uint8_t *impact_out,
+                     uint32_t nthreads);
+/* order-independent digests: {rows, sum of row hashes, xor of rotated row hashes}; state digests
+ * accumulate into out (so shard digests add up), row-array digests overwrite it */
+void of_state_digest(const of_state *s, uint64_t out[3]);
+void of_rows_digest(const of_rows *o, uint64_t n, uint64_t out[3]);
 
 /* ---- sync need diff (corro-types/src/sync.rs:127-249), CSR over (pair, actor) entries ---- */
 typedef struct {

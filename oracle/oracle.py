@@ -65,6 +65,10 @@ def lib():
         L.of_export.restype = C.c_uint64
         L.of_export.argtypes = [C.c_void_p, C.POINTER(_Rows)]
         L.of_db_versions.argtypes = [C.c_void_p, C.c_void_p]
+        L.of_apply_sharded.restype = C.c_int
+        L.of_apply_sharded.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_Changes), C.c_void_p, C.c_uint32]
+        L.of_state_digest.argtypes = [C.c_void_p, C.c_void_p]
+        L.of_rows_digest.argtypes = [C.POINTER(_Rows), C.c_uint64, C.c_void_p]
         L.of_needs.argtypes = [C.POINTER(_SyncEntries), C.POINTER(_NeedsOut), C.c_int]
         L.of_booked_new.restype = C.c_void_p
         L.of_booked_free.argtypes = [C.c_void_p]
@@ -146,6 +150,66 @@ class Fold:
         out = np.zeros(max(self.nsites, 1), np.int64)
         lib().of_db_versions(self._h, out.ctypes.data)
         return out[: self.nsites]
+
+
+class ShardedFold:
+    """The same fold over `nshards` pk-hash shards with `nthreads` threads (of_apply_sharded):
+    rows merge independently, so results equal Fold's. Used as the multi-core CPU baseline and as
+    the checker at >= 512M changes (compared through digests)."""
+
+    def __init__(self, site_ids, nshards=16, nthreads=16):
+        site_ids = np.ascontiguousarray(site_ids, dtype=np.uint8).reshape(-1, 16)
+        self.nsites = site_ids.shape[0]
+        self.nthreads = nthreads
+        self._hs = (C.c_void_p * nshards)(*[lib().of_new(site_ids.ctypes.data, self.nsites) for _ in range(nshards)])
+        self.nshards = nshards
+
+    def __del__(self):
+        if getattr(self, "_hs", None) is not None:
+            for h in self._hs:
+                lib().of_free(h)
+            self._hs = None
+
+    def apply(self, batch, impact=True):
+        keep = []
+        s = _changes_struct(batch, keep)
+        imp = np.zeros(max(s.n, 1), dtype=np.uint8) if impact else None
+        rc = lib().of_apply_sharded(self._hs, self.nshards, C.byref(s), imp.ctypes.data if impact else None,
+                                    self.nthreads)
+        assert rc == 0, "batch too large for the sharded fold"
+        return imp[: s.n] if impact else None
+
+    def digest(self):
+        out = np.zeros(3, np.uint64)
+        for h in self._hs:
+            lib().of_state_digest(h, out.ctypes.data)
+        return tuple(int(x) for x in out)
+
+    def db_versions(self):
+        acc = np.full(max(self.nsites, 1), -1, np.int64)
+        out = np.zeros(max(self.nsites, 1), np.int64)
+        for h in self._hs:
+            lib().of_db_versions(h, out.ctypes.data)
+            np.maximum(acc, out, out=acc)
+        return acc[: self.nsites]
+
+
+def rows_digest(rows):
+    """Digest of crsql_changes rows given as arrays (e.g. MergeEngine.export()), comparable with
+    ShardedFold.digest(): (rows, sum of row hashes, xor of rotated row hashes)."""
+    m = len(rows["pk"])
+    dts = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64, "db_version": np.int64,
+           "cl": np.int64, "seq": np.uint32, "site": np.uint32, "ts": np.uint64, "val0": np.uint64,
+           "val1": np.uint64, "val_type": np.uint8, "val_len": np.uint8}
+    r = _Rows()
+    keep = []
+    for k, dt in dts.items():
+        a = np.ascontiguousarray(rows[k], dtype=dt)
+        keep.append(a)
+        setattr(r, k, a.ctypes.data if m else None)
+    out = np.zeros(3, np.uint64)
+    lib().of_rows_digest(C.byref(r), m, out.ctypes.data)
+    return tuple(int(x) for x in out)
 
 
 SYNC_KEYS_U64 = ("their_head", "tn_off", "tn_start", "tn_end", "tp_off", "tp_ver", "tps_off",

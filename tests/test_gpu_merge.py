@@ -332,3 +332,29 @@ def test_parallel_row_fold_overflow_vs_oracle(malformed, impact):
         if impact:
             assert np.array_equal(got, ref), f"impacts differ in batch {k}"
     compare(e, f, with_ts=True)
+
+
+@pytest.mark.slow
+def test_config2_full_size_vs_sharded_oracle():
+    """Config 2 at its full size (2^26 changes, pk space 2^22, 1000 actors) generated in HBM, with
+    impact flags: all 2^26 impacts equal, rows equal through the order-independent digest of every
+    output field, db_versions equal (checker: the oracle's pk-sharded fold on the host cores).
+    tools/parity_scale.py runs the same check at 2^29 changes (profiles/r01_parity_512m.json)."""
+    import torch
+    sites = synth.site_ids(1000, 1)
+    b = synth.uniform_batch_torch(1 << 26, 1000, 1 << 22, 4, seed=synth.config_seed(2), device="cuda")
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=1 << 26, sites=sites)
+    imp = e.apply(b, impact=True).cpu().numpy()
+    hb = {k: v.cpu().numpy() for k, v in b.items()}
+    del b
+    torch.cuda.empty_cache()
+    for k in ("table_cid", "cl", "seq", "site"):
+        hb[k] = hb[k].view(np.uint32)
+    for k in ("pk", "val0"):
+        hb[k] = hb[k].view(np.uint64)
+    f = O.ShardedFold(sites, nshards=64, nthreads=16)
+    ref = f.apply(hb)
+    assert np.array_equal(imp, ref)
+    assert O.rows_digest(e.export()) == f.digest()
+    assert np.array_equal(e.db_versions(), f.db_versions())
+    e.close()

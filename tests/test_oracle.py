@@ -78,3 +78,33 @@ def test_oracle_gaps_kats():
                     continue
                 assert b.contains(v)
         assert b.max() == max(e for _, e in allv)
+
+
+@pytest.mark.parametrize("nshards,nthreads", [(1, 1), (7, 3), (16, 8)])
+def test_sharded_fold_equals_sequential_fold(nshards, nthreads):
+    """The pk-sharded parallel fold (CPU baseline / 512M checker) reproduces the sequential fold:
+    same impacts, same rows (digest and exported rows), same crsql_db_versions."""
+    import synth
+    sites = synth.site_ids(8, 3)
+    batches = [synth.adversarial_batch(30000, 8, 2, 400, 11), synth.uniform_batch(30000, 8, 500, 4, 12),
+               synth.adversarial_batch(20000, 8, 2, 400, 13, malformed=True)]
+    f = O.Fold(sites)
+    g = O.ShardedFold(sites, nshards=nshards, nthreads=nthreads)
+    for b in batches:
+        assert np.array_equal(f.apply(b), g.apply(b))
+    assert g.digest() == O.rows_digest(f.export())
+    assert np.array_equal(g.db_versions(), f.db_versions())
+
+
+def test_rows_digest_detects_a_single_field_change():
+    import synth
+    f = O.Fold(synth.site_ids(4, 1))
+    f.apply(synth.uniform_batch(5000, 4, 300, 4, 3))
+    rows = f.export()
+    d0 = O.rows_digest(rows)
+    perm = np.random.default_rng(0).permutation(len(rows["pk"]))
+    assert O.rows_digest({k: v[perm] for k, v in rows.items()}) == d0  # order-independent
+    for k in rows:
+        r2 = {kk: vv.copy() for kk, vv in rows.items()}
+        r2[k][17] ^= 1
+        assert O.rows_digest(r2) != d0, k
