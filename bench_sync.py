@@ -2,7 +2,8 @@
 
 BASELINE.json configs[3]: 1M node-pair sync states, 64 sparse actors per pair from a 100k-actor
 universe -> 64M (pair, actor) entries, generated in HBM (synth.sync_entries_torch). One step =
-corro_compute_needs count pass + device offset scan + fill pass. Algorithmic bytes:
+corro_compute_needs count pass + device offset scan + fill pass (default), or with --one-pass
+corro_compute_needs_onepass. Algorithmic bytes:
 16 B per input range (ours.need, theirs.need, partial seq ranges) + 16 B per head pair + 8 B per
 partial version + 16 B per output range. Prints one JSON line.
 """
@@ -53,12 +54,15 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--one-pass", action="store_true",
+                    help="corro_compute_needs_onepass (decoupled look-back) instead of count + fill passes")
     args = ap.parse_args()
 
     import torch
     import synth
     import corrosion_amd as ca
-    from corrosion_amd.sync import _needs_device
+    from corrosion_amd.sync import _needs_device, _needs_device_1pass
+    run = _needs_device_1pass if args.one_pass else _needs_device
 
     dev = torch.device("cuda", 0)
     eng = ca.MergeEngine({"t": ["a"]}, capacity_hint=1024)
@@ -66,11 +70,11 @@ def main():
     torch.cuda.synchronize()
     eng.set_profiling(True)
     for _ in range(args.warmup):
-        res = _needs_device(eng, ent)
+        res = run(eng, ent)
     kt = kc = kf = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = _needs_device(eng, ent)
+        res = run(eng, ent)
         tm = eng.last_timings(apply_only=False)
         kc += tm["k_needs_count"]
         kf += tm["k_needs_fill"]
@@ -92,7 +96,7 @@ def main():
             "config": {"workload": "config 4", "pairs": args.pairs, "entries": E, "input_ranges": in_ranges,
                        "output_needs": int(res["start"].shape[0]), "output_seq_ranges": int(res["s_start"].shape[0])},
             "entries_per_s": E / dt,
-            "roofline": {"bound": "hbm", "kernel": "k_needs (count + fill)", "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": "k_needs1 (one pass)" if args.one_pass else "k_needs (count + fill)", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernels_ms": kt, "count_pass_ms": kc, "fill_pass_ms": kf},
             "cpu_baseline": cpu_baseline(ent, min(args.cpu_sample, E))}

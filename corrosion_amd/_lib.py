@@ -29,6 +29,7 @@ EXPORTS = [
     "corro_bookie_take_ready", "corro_process_fully_buffered", "corro_bookie_last",
     "corro_bookie_needed", "corro_bookie_contains_all", "corro_bookie_partial",
     "corro_generate_sync", "corro_partition_ranks", "corro_scan_offsets",
+    "corro_compute_needs_onepass", "corro_needs_bound",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -140,6 +141,8 @@ def lib():
         "corro_db_versions": (i32, [vp, vp, u32]),
         "corro_compute_needs": (i32, [vp, C.POINTER(SyncEntries), i32, C.POINTER(NeedsOut), i32]),
         "corro_scan_offsets": (i32, [vp, vp, vp, u64]),
+        "corro_compute_needs_onepass": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsOut), u64, u64, vp]),
+        "corro_needs_bound": (i32, [vp, C.POINTER(SyncEntries), i32, vp, vp]),
         "corro_booked_new": (i32, [vp]),
         "corro_booked_free": (None, [vp]),
         "corro_booked_insert_db": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp, vp, u64, vp]),

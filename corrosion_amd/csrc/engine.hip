@@ -305,7 +305,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_state_flags, &ctx->d_out_off, &ctx->d_out_cnt, &ctx->d_out_flags, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
                       &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export,
-                      &ctx->d_needs, &ctx->d_ncols, &ctx->d_part};
+                      &ctx->d_needs, &ctx->d_needs1, &ctx->d_ncols, &ctx->d_part};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     for (auto &e : ctx->ev)

@@ -99,6 +99,7 @@ struct corro_ctx {
     corro::DevBuf d_impact;
     corro::DevBuf d_export;
     corro::DevBuf d_needs;        // sync-need scratch
+    corro::DevBuf d_needs1;       // one-pass need diff: look-back status words + ticket
     corro::DevBuf d_ncols;        // u16 column count per table
     corro::DevBuf d_part;         // partition counts
     uint64_t *h_misc = nullptr;   // pinned

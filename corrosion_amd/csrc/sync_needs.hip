@@ -56,7 +56,7 @@ template <class T, int SPACE = 0> struct WView {
 template <class V> struct VerHolesT {
     V hs, he;                 // ranges
     uint64_t h0, h1;
-    const uint64_t *pv;       // points
+    V pv;                     // points
     uint64_t p0, p1;
     // if x lies in a hole, return the hole end (max over holes containing x) else return false
     __device__ inline bool covering(uint64_t x, uint64_t &end) const {
@@ -84,8 +84,8 @@ template <class V> struct VerHolesT {
     }
 };
 
-struct SeqHoles {
-    V64 hs, he;
+template <class V> struct SeqHolesT {
+    V hs, he;
     uint64_t h0, h1;
     __device__ inline bool covering(uint64_t x, uint64_t &end) const {
         bool hit = false;
@@ -124,15 +124,18 @@ __device__ inline void sweep(const H &holes, uint64_t lo, uint64_t hi, uint64_t 
     }
 }
 
-// One workgroup = NEEDS_T consecutive entries, one lane per entry. The workgroup's CSR segments of
-// their/our need ranges are contiguous, so they are staged into LDS with coalesced 16-B loads
-// (lanes then walk LDS, not scattered global lines); in the fill pass the workgroup's output
-// range [need_off[e0], need_off[e1]) is contiguous too, so outputs are assembled in LDS and
-// written out coalesced. Segments larger than the LDS caps fall back to global memory (same code,
-// generic pointers). Partials (5 % of entries) are read from global memory directly.
+// One workgroup = NEEDS_T consecutive entries, one lane per entry. Every CSR segment a workgroup
+// touches is contiguous (their/our need ranges, their/our partial versions, their seq offsets and
+// seq ranges), so all of them are staged into LDS up front — one wave of coalesced loads per
+// segment, three dependent latencies in total (offsets -> nested offsets -> ranges) — and the lanes
+// then walk LDS only. In the fill pass the workgroup's output range is contiguous too, so outputs
+// are assembled in LDS and written out coalesced. A workgroup with any segment above its LDS cap
+// runs the same walk on global memory instead (views over global arrays).
 constexpr uint32_t NEEDS_T = 256;
-constexpr uint32_t NEEDS_CAP_R = 640;    // staged ranges per side (avg 2 per entry -> 512, sd ~32)
-constexpr uint32_t NEEDS_CAP_O = 960;    // staged output needs (avg ~2.5 per entry -> ~650); 3 WGs/CU
+constexpr uint32_t NEEDS_CAP_R = 576;    // staged need ranges per side (avg 2 per entry -> 512, sd ~23)
+constexpr uint32_t NEEDS_CAP_O = 800;    // staged output needs (avg ~2.55 per entry -> ~650, sd ~30)
+constexpr uint32_t NEEDS_CAP_P = 64;     // staged partial versions per side (5 % of entries -> ~13)
+constexpr uint32_t NEEDS_CAP_S = 160;    // staged partial seq ranges per side (~2 per partial -> ~26)
 
 __device__ inline void stage_ranges(const uint64_t *gs, const uint64_t *ge, uint64_t lo, uint64_t cnt, uint64_t *ls,
                                     uint64_t *le) {
@@ -162,150 +165,447 @@ __device__ inline void stage_ranges(const uint64_t *gs, const uint64_t *ge, uint
     }
 }
 
+__device__ inline void stage_words(const uint64_t *g, uint64_t lo, uint64_t cnt, uint64_t *l) {
+    for (uint64_t q = threadIdx.x; q < cnt; q += blockDim.x) l[q] = g[lo + q];
+}
+
+// Per-lane words of one entry.
+struct EntryHdr {
+    uint64_t head;
+    int64_t ours;
+    uint64_t tne0, tne1, one0, one1, tpe0, tpe1, ope0, ope1;
+};
+
+__device__ inline EntryHdr load_entry(const SyncDev &in, uint64_t e) {
+    EntryHdr h;
+    h.head = in.their_head[e];
+    h.ours = in.our_head[e];
+    h.tne0 = in.tn_off[e]; h.tne1 = in.tn_off[e + 1];
+    h.one0 = in.on_off[e]; h.one1 = in.on_off[e + 1];
+    h.tpe0 = in.tp_off[e]; h.tpe1 = in.tp_off[e + 1];
+    h.ope0 = in.op_off[e]; h.ope1 = in.op_off[e + 1];
+    return h;
+}
+
+// Every input array an entry walk reads, as views of one address space.
+template <class V> struct InViews {
+    V tns, tne, ons, one;          // need ranges
+    V tpv, tpso, tpss, tpse;       // their partial versions, seq offsets, seq ranges
+    V opv, opso, opss, opse;       // ours
+};
+
+// The walk of one entry (sync.rs:141-245). Counts its needs (nn) and partial seq ranges (ns); with
+// FILL also writes them: needs at [nbase, nbase + nn) through the o* views, seq ranges straight to
+// global memory at [sbase, sbase + ns).
+template <bool FILL, class V, class VK, class VU>
+__device__ inline void walk_entry(const corro_needs_out &o, const EntryHdr &h, const InViews<V> &iv, VK okind,
+                                  VU ostart, VU oend, VU osro, VU osrn, uint64_t nbase, uint64_t sbase,
+                                  uint64_t &nn_out, uint64_t &ns_out) {
+    const uint64_t head = h.head;
+    VerHolesT<V> vh{iv.tns, iv.tne, h.tne0, h.tne1, iv.tpv, h.tpe0, h.tpe1};
+    uint64_t nn = 0, ns = 0;
+    auto full = [&](uint64_t s, uint64_t t) {
+        if (FILL) {
+            const uint64_t k = nbase + nn;
+            okind[k] = 0;
+            ostart[k] = s;
+            oend[k] = t;
+            osro[k] = sbase + ns;
+            osrn[k] = 0;
+        }
+        nn++;
+    };
+    for (uint64_t k = h.one0; k < h.one1; k++) sweep(vh, iv.ons[k], iv.one[k], 1, head, full);
+
+    for (uint64_t k = h.ope0; k < h.ope1; k++) {
+        const uint64_t v = iv.opv[k];
+        uint64_t dummy;
+        const bool have = v >= 1 && v <= head && !vh.covering(v, dummy);
+        const uint64_t q0 = iv.opso[k], q1 = iv.opso[k + 1];
+        if (have) {
+            if (FILL) {
+                const uint64_t q = nbase + nn;
+                okind[q] = 1;
+                ostart[q] = v;
+                oend[q] = v;
+                osro[q] = sbase + ns;
+                osrn[q] = q1 - q0;
+                for (uint64_t j = q0; j < q1; j++) {
+                    o.s_start[sbase + ns + (j - q0)] = iv.opss[j];
+                    o.s_end[sbase + ns + (j - q0)] = iv.opse[j];
+                }
+            }
+            ns += q1 - q0;
+            nn++;
+            continue;
+        }
+        int64_t tk = -1;
+        for (uint64_t j = h.tpe0; j < h.tpe1; j++)
+            if (iv.tpv[j] == v) {
+                tk = (int64_t)j;
+                break;
+            }
+        if (tk < 0) continue;
+        const uint64_t t0 = iv.tpso[tk], t1 = iv.tpso[tk + 1];
+        bool have_end = false;
+        uint64_t end = 0;
+        for (uint64_t j = t0; j < t1; j++)
+            if (!have_end || iv.tpse[j] > end) {
+                end = iv.tpse[j];
+                have_end = true;
+            }
+        for (uint64_t j = q0; j < q1; j++)
+            if (!have_end || iv.opse[j] > end) {
+                end = iv.opse[j];
+                have_end = true;
+            }
+        if (!have_end) continue;
+        SeqHolesT<V> sh{iv.tpss, iv.tpse, t0, t1};
+        const uint64_t first = sbase + ns;
+        uint64_t cnt = 0;
+        auto piece = [&](uint64_t s, uint64_t t) {
+            if (FILL) {
+                o.s_start[first + cnt] = s;
+                o.s_end[first + cnt] = t;
+            }
+            cnt++;
+        };
+        for (uint64_t j = q0; j < q1; j++) sweep(sh, iv.opss[j], iv.opse[j], 0, end, piece);
+        if (cnt) {
+            if (FILL) {
+                const uint64_t q = nbase + nn;
+                okind[q] = 1;
+                ostart[q] = v;
+                oend[q] = v;
+                osro[q] = first;
+                osrn[q] = cnt;
+            }
+            nn++;
+            ns += cnt;
+        }
+    }
+    if (h.ours < 0) full(1, head);
+    else if (head > (uint64_t)h.ours) full((uint64_t)h.ours + 1, head);
+    nn_out = nn;
+    ns_out = ns;
+}
+
+// LDS of one need workgroup: the staged inputs ...
+struct NeedsLds {
+    uint64_t tns[NEEDS_CAP_R], tne[NEEDS_CAP_R], ons[NEEDS_CAP_R], one[NEEDS_CAP_R];
+    uint64_t tpv[NEEDS_CAP_P], tpso[NEEDS_CAP_P + 1], tpss[NEEDS_CAP_S], tpse[NEEDS_CAP_S];
+    uint64_t opv[NEEDS_CAP_P], opso[NEEDS_CAP_P + 1], opss[NEEDS_CAP_S], opse[NEEDS_CAP_S];
+};
+// ... and, when outputs are staged (NEEDS_OSTAGE), the output needs.
+struct NeedsOutLds {
+    uint64_t start[NEEDS_CAP_O], end[NEEDS_CAP_O], sro[NEEDS_CAP_O], srn[NEEDS_CAP_O];
+    uint8_t kind[NEEDS_CAP_O];
+};
+
+// Segment bounds of one workgroup [e0, e1) (global CSR indices).
+struct WgSegs {
+    uint64_t tn_lo, tn_hi, on_lo, on_hi, tp_lo, tp_hi, op_lo, op_hi, tps_lo, tps_hi, ops_lo, ops_hi;
+    bool lds;
+};
+
+// Stage every input segment of the workgroup into LDS (or decide that one does not fit).
+// Ends with __syncthreads().
+__device__ inline WgSegs stage_inputs(const SyncDev &in, uint64_t e0, uint64_t e1, NeedsLds &L) {
+    WgSegs g;
+    g.tn_lo = in.tn_off[e0]; g.tn_hi = in.tn_off[e1];
+    g.on_lo = in.on_off[e0]; g.on_hi = in.on_off[e1];
+    g.tp_lo = in.tp_off[e0]; g.tp_hi = in.tp_off[e1];
+    g.op_lo = in.op_off[e0]; g.op_hi = in.op_off[e1];
+    const bool fit1 = g.tn_hi - g.tn_lo <= NEEDS_CAP_R && g.on_hi - g.on_lo <= NEEDS_CAP_R &&
+                      g.tp_hi - g.tp_lo <= NEEDS_CAP_P && g.op_hi - g.op_lo <= NEEDS_CAP_P;
+    g.tps_lo = g.tps_hi = g.ops_lo = g.ops_hi = 0;
+    g.lds = false;
+    if (!fit1) return g;  // uniform: no barrier skipped by part of the workgroup
+    // nested offsets of the partial segments (uniform loads; NULL arrays only when empty)
+    if (g.tp_hi > g.tp_lo) {
+        g.tps_lo = in.tps_off[g.tp_lo];
+        g.tps_hi = in.tps_off[g.tp_hi];
+    }
+    if (g.op_hi > g.op_lo) {
+        g.ops_lo = in.ops_off[g.op_lo];
+        g.ops_hi = in.ops_off[g.op_hi];
+    }
+    stage_ranges(in.tn_start, in.tn_end, g.tn_lo, g.tn_hi - g.tn_lo, L.tns, L.tne);
+    stage_ranges(in.on_start, in.on_end, g.on_lo, g.on_hi - g.on_lo, L.ons, L.one);
+    if (g.tp_hi > g.tp_lo) {
+        stage_words(in.tp_ver, g.tp_lo, g.tp_hi - g.tp_lo, L.tpv);
+        stage_words(in.tps_off, g.tp_lo, g.tp_hi - g.tp_lo + 1, L.tpso);
+    }
+    if (g.op_hi > g.op_lo) {
+        stage_words(in.op_ver, g.op_lo, g.op_hi - g.op_lo, L.opv);
+        stage_words(in.ops_off, g.op_lo, g.op_hi - g.op_lo + 1, L.opso);
+    }
+    g.lds = g.tps_hi - g.tps_lo <= NEEDS_CAP_S && g.ops_hi - g.ops_lo <= NEEDS_CAP_S;
+    if (g.lds) {
+        stage_words(in.tps_start, g.tps_lo, g.tps_hi - g.tps_lo, L.tpss);
+        stage_words(in.tps_end, g.tps_lo, g.tps_hi - g.tps_lo, L.tpse);
+        stage_words(in.ops_start, g.ops_lo, g.ops_hi - g.ops_lo, L.opss);
+        stage_words(in.ops_end, g.ops_lo, g.ops_hi - g.ops_lo, L.opse);
+    }
+    __syncthreads();
+    return g;
+}
+
+// Run walk_entry on LDS views when the inputs are staged (and, with FILL, the outputs fit),
+// else on global views.
+template <bool FILL>
+__device__ inline void walk_dispatch(const SyncDev &in, const corro_needs_out &o, const EntryHdr &h, NeedsLds &L,
+                                     NeedsOutLds *Lo, const WgSegs &g, uint64_t o_lo, uint64_t nbase, uint64_t sbase,
+                                     uint64_t &nn, uint64_t &ns) {
+    if (g.lds && (!FILL || !Lo)) {  // staged inputs, outputs (if any) straight to global memory
+        using VL = V64S<1>;
+        const InViews<VL> iv{VL{L.tns, g.tn_lo},  VL{L.tne, g.tn_lo},  VL{L.ons, g.on_lo},  VL{L.one, g.on_lo},
+                             VL{L.tpv, g.tp_lo},  VL{L.tpso, g.tp_lo}, VL{L.tpss, g.tps_lo}, VL{L.tpse, g.tps_lo},
+                             VL{L.opv, g.op_lo},  VL{L.opso, g.op_lo}, VL{L.opss, g.ops_lo}, VL{L.opse, g.ops_lo}};
+        walk_entry<FILL>(o, h, iv, WView<uint8_t>{o.kind, 0}, WView<uint64_t>{o.start, 0}, WView<uint64_t>{o.end, 0},
+                         WView<uint64_t>{o.sr_off, 0}, WView<uint64_t>{o.sr_n, 0}, nbase, sbase, nn, ns);
+    } else if (g.lds) {
+        using VL = V64S<1>;
+        const InViews<VL> iv{VL{L.tns, g.tn_lo},  VL{L.tne, g.tn_lo},  VL{L.ons, g.on_lo},  VL{L.one, g.on_lo},
+                             VL{L.tpv, g.tp_lo},  VL{L.tpso, g.tp_lo}, VL{L.tpss, g.tps_lo}, VL{L.tpse, g.tps_lo},
+                             VL{L.opv, g.op_lo},  VL{L.opso, g.op_lo}, VL{L.opss, g.ops_lo}, VL{L.opse, g.ops_lo}};
+        NeedsOutLds &O = *Lo;
+        walk_entry<FILL>(o, h, iv, WView<uint8_t, 1>{O.kind, o_lo}, WView<uint64_t, 1>{O.start, o_lo},
+                         WView<uint64_t, 1>{O.end, o_lo}, WView<uint64_t, 1>{O.sro, o_lo},
+                         WView<uint64_t, 1>{O.srn, o_lo}, nbase, sbase, nn, ns);
+    } else {
+        const InViews<V64> iv{V64{in.tn_start, 0}, V64{in.tn_end, 0},  V64{in.on_start, 0},  V64{in.on_end, 0},
+                              V64{in.tp_ver, 0},   V64{in.tps_off, 0}, V64{in.tps_start, 0}, V64{in.tps_end, 0},
+                              V64{in.op_ver, 0},   V64{in.ops_off, 0}, V64{in.ops_start, 0}, V64{in.ops_end, 0}};
+        walk_entry<FILL>(o, h, iv, WView<uint8_t>{o.kind, 0}, WView<uint64_t>{o.start, 0}, WView<uint64_t>{o.end, 0},
+                         WView<uint64_t>{o.sr_off, 0}, WView<uint64_t>{o.sr_n, 0}, nbase, sbase, nn, ns);
+    }
+}
+
+__device__ inline void flush_needs(const corro_needs_out &o, const NeedsOutLds &L, uint64_t o_lo, uint64_t m) {
+    for (uint64_t k = threadIdx.x; k < m; k += NEEDS_T) {
+        o.start[o_lo + k] = L.start[k];
+        o.end[o_lo + k] = L.end[k];
+        o.sr_off[o_lo + k] = L.sro[k];
+        o.sr_n[o_lo + k] = L.srn[k];
+        o.kind[o_lo + k] = L.kind[k];
+    }
+}
+
+// Output staging in LDS costs ~33 B of LDS per output need (3 -> 2 workgroups per CU); writing
+// straight from the lanes keeps 6 workgroups per CU resident, which hides more latency.
+#ifndef NEEDS_OSTAGE
+#define NEEDS_OSTAGE 0
+#endif
+template <bool FILL> struct OutStage { __device__ NeedsOutLds *get() { return nullptr; } };
+#if NEEDS_OSTAGE
+template <> struct OutStage<true> {
+    __device__ NeedsOutLds *get() {
+        __shared__ NeedsOutLds Lo;
+        return &Lo;
+    }
+};
+#endif
+
+// Two-pass form (corro_compute_needs): pass 0 counts, pass 1 fills at caller-scanned offsets.
 template <bool FILL>
 __global__ void __launch_bounds__(NEEDS_T) k_needs(SyncDev in, corro_needs_out o) {
-    __shared__ uint64_t l_tns[NEEDS_CAP_R], l_tne[NEEDS_CAP_R], l_ons[NEEDS_CAP_R], l_one[NEEDS_CAP_R];
-    __shared__ uint64_t l_start[FILL ? NEEDS_CAP_O : 1], l_end[FILL ? NEEDS_CAP_O : 1];
-    __shared__ uint64_t l_sro[FILL ? NEEDS_CAP_O : 1], l_srn[FILL ? NEEDS_CAP_O : 1];
-    __shared__ uint8_t l_kind[FILL ? NEEDS_CAP_O : 1];
+    __shared__ NeedsLds L;
     const uint64_t e0 = (uint64_t)blockIdx.x * NEEDS_T;
     const uint64_t e1 = min(in.n, e0 + NEEDS_T);
     const uint64_t e = e0 + threadIdx.x;
     const bool live = e < in.n;
     // per-lane words first, so their latency overlaps the staging below
-    const uint64_t el = live ? e : e0;
-    const uint64_t head = in.their_head[el];
-    const int64_t ours = in.our_head[el];
-    const uint64_t tne0 = in.tn_off[el], tne1 = in.tn_off[el + 1], one0 = in.on_off[el], one1 = in.on_off[el + 1];
-    const uint64_t tpe0 = in.tp_off[el], tpe1 = in.tp_off[el + 1], ope0 = in.op_off[el], ope1 = in.op_off[el + 1];
-    const uint64_t nbase = FILL ? o.need_off[el] : 0, sbase = FILL ? o.seq_off[el] : 0;
-    // workgroup segments (uniform scalar loads)
-    const uint64_t tn_lo = in.tn_off[e0], tn_hi = in.tn_off[e1];
-    const uint64_t on_lo = in.on_off[e0], on_hi = in.on_off[e1];
-    const bool tn_lds = tn_hi - tn_lo <= NEEDS_CAP_R, on_lds = on_hi - on_lo <= NEEDS_CAP_R;
-    if (tn_lds) stage_ranges(in.tn_start, in.tn_end, tn_lo, tn_hi - tn_lo, l_tns, l_tne);
-    if (on_lds) stage_ranges(in.on_start, in.on_end, on_lo, on_hi - on_lo, l_ons, l_one);
+    const EntryHdr h = load_entry(in, live ? e : e0);
+    const uint64_t nbase = FILL ? o.need_off[live ? e : e0] : 0, sbase = FILL ? o.seq_off[live ? e : e0] : 0;
     uint64_t o_lo = 0, o_hi = 0;
-    bool o_lds = false;
     if (FILL) {
         o_lo = o.need_off[e0];
         o_hi = o.need_off[e1];
-        o_lds = o_hi - o_lo <= NEEDS_CAP_O;
+    }
+    const WgSegs g = stage_inputs(in, e0, e1, L);
+    NeedsOutLds *Lo = OutStage<FILL>().get();
+    if (o_hi - o_lo > NEEDS_CAP_O) Lo = nullptr;
+    uint64_t nn = 0, ns = 0;
+    if (live) walk_dispatch<FILL>(in, o, h, L, Lo, g, o_lo, nbase, sbase, nn, ns);
+    if (!FILL && live) {
+        o.need_count[e] = nn;
+        o.seq_count[e] = ns;
+    }
+    if (FILL && g.lds && Lo) {
+        __syncthreads();
+        flush_needs(o, *Lo, o_lo, o_hi - o_lo);
+    }
+}
+
+// ---- one-pass form (corro_compute_needs_onepass) ----------------------------------------------
+// Each workgroup counts its entries' needs / seq ranges from LDS-staged inputs, scans them across
+// the workgroup, obtains the global prefix of every earlier workgroup by a decoupled look-back
+// over per-workgroup status words (one chain for needs, one for seq ranges), then re-walks the
+// LDS-resident inputs writing its outputs at the now-known offsets. Inputs are read from HBM once.
+// Workgroups take their logical index from a ticket counter, so a workgroup only ever waits on
+// workgroups that are already running (no dependence on dispatch order).
+constexpr uint64_t ST_A = 1ULL << 62, ST_P = 2ULL << 62, ST_VAL = (1ULL << 62) - 1;
+
+__device__ inline uint64_t st_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline uint64_t wave_sum(uint64_t v) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+// Called by one whole wave: sums of both chains over workgroups [0, wg). Status words of one
+// workgroup are adjacent (needs, seqs) and published together, so one look-back serves both.
+// Each lane inspects LB_PER consecutive predecessors, so one round covers 64 * LB_PER of them (the
+// statuses sit in the device-coherent level, a round trip costs ~1-2 us: a wide window makes the
+// inclusive-prefix frontier advance that many workgroups per round trip).
+constexpr int LB_PER = 1;
+__device__ inline void lookback2(const uint64_t *st, int64_t wg, uint64_t &xn, uint64_t &xs) {
+    const int lane = threadIdx.x & 63;
+    xn = xs = 0;
+    int64_t base = wg - 1;  // nearest predecessor not yet summed
+    while (true) {
+        // lane's chunk: predecessors base - (lane * LB_PER + j), nearest first. Sum the run of
+        // aggregates up to the first non-aggregate; a P (inclusive prefix) ends the look-back, an
+        // X (not yet published, or the two words caught mid-update) stops the run there.
+        uint64_t an = 0, as = 0;
+        int first = LB_PER;
+        bool isp = false;
+#pragma unroll
+        for (int j = 0; j < LB_PER; j++) {
+            const int64_t idx = base - (lane * LB_PER + j);
+            const uint64_t vn = idx >= 0 ? st_load(&st[2 * idx]) : ST_P;
+            const uint64_t vs = idx >= 0 ? st_load(&st[2 * idx + 1]) : ST_P;
+            const uint64_t sn = vn >> 62;
+            const bool agg = sn == 1 && (vs >> 62) == 1;
+            const bool pre = sn == 2 && (vs >> 62) == 2;
+            if (first == LB_PER) {
+                if (agg || pre) {
+                    an += vn & ST_VAL;
+                    as += vs & ST_VAL;
+                }
+                if (!agg) {
+                    first = j;
+                    isp = pre;
+                }
+            }
+        }
+        const unsigned long long stop = __ballot(first < LB_PER);
+        if (!stop) {
+            xn += wave_sum(an);
+            xs += wave_sum(as);
+            base -= 64 * LB_PER;
+            continue;
+        }
+        const int k = __ffsll(stop) - 1;
+        if (lane > k) an = as = 0;
+        xn += wave_sum(an);
+        xs += wave_sum(as);
+        const bool kp = __shfl(isp ? 1 : 0, k);
+        if (kp) return;
+        const int kf = __shfl(first, k);
+        base -= k * LB_PER + kf;  // resume at the unpublished predecessor
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+struct Needs1Args {
+    uint64_t *st;        // 2 status words per workgroup (zeroed)
+    uint64_t *ticket;    // [0] ticket counter (zeroed), [1] totals: needs, [2] seq ranges
+    uint64_t need_cap, seq_cap;
+};
+
+__global__ void __launch_bounds__(NEEDS_T) k_needs1(SyncDev in, corro_needs_out o, Needs1Args a) {
+    __shared__ NeedsLds L;
+    __shared__ uint64_t s_wn[NEEDS_T / 64], s_ws[NEEDS_T / 64];
+    __shared__ uint64_t s_base[2];
+    __shared__ uint64_t s_wg;
+    if (threadIdx.x == 0) s_wg = atomicAdd((unsigned long long *)a.ticket, 1ULL);
+    __syncthreads();
+    const uint64_t wg = s_wg;
+    const uint64_t e0 = wg * NEEDS_T;
+    const uint64_t e1 = min(in.n, e0 + NEEDS_T);
+    const uint64_t e = e0 + threadIdx.x;
+    const bool live = e < in.n;
+    const EntryHdr h = load_entry(in, live ? e : e0);
+    const WgSegs g = stage_inputs(in, e0, e1, L);
+    // count walk (no output)
+    uint64_t nn = 0, ns = 0;
+    if (live) walk_dispatch<false>(in, o, h, L, nullptr, g, 0, 0, 0, nn, ns);
+    // workgroup exclusive scan of (nn, ns)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t in_n = nn, in_s = ns;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t yn = __shfl_up(in_n, d), ys = __shfl_up(in_s, d);
+        if (lane >= d) {
+            in_n += yn;
+            in_s += ys;
+        }
+    }
+    if (lane == 63) {
+        s_wn[wv] = in_n;
+        s_ws[wv] = in_s;
     }
     __syncthreads();
-    // the per-lane walk, instantiated once for LDS-staged views and once for global ones
-    auto lane = [&](auto tns, auto tne, auto ons, auto one, auto okind, auto ostart, auto oend, auto osro,
-                    auto osrn) {
-        VerHolesT<decltype(tns)> vh{tns, tne, tne0, tne1, in.tp_ver, tpe0, tpe1};
-        uint64_t nn = 0, ns = 0;
-        auto full = [&](uint64_t s, uint64_t t) {
-            if (FILL) {
-                const uint64_t k = nbase + nn;
-                okind[k] = 0;
-                ostart[k] = s;
-                oend[k] = t;
-                osro[k] = sbase + ns;
-                osrn[k] = 0;
-            }
-            nn++;
-        };
-        for (uint64_t k = one0; k < one1; k++) sweep(vh, ons[k], one[k], 1, head, full);
-
-        for (uint64_t k = ope0; k < ope1; k++) {
-            const uint64_t v = in.op_ver[k];
-            uint64_t dummy;
-            const bool have = v >= 1 && v <= head && !vh.covering(v, dummy);
-            const uint64_t q0 = in.ops_off[k], q1 = in.ops_off[k + 1];
-            if (have) {
-                if (FILL) {
-                    const uint64_t q = nbase + nn;
-                    okind[q] = 1;
-                    ostart[q] = v;
-                    oend[q] = v;
-                    osro[q] = sbase + ns;
-                    osrn[q] = q1 - q0;
-                    for (uint64_t j = q0; j < q1; j++) {
-                        o.s_start[sbase + ns + (j - q0)] = in.ops_start[j];
-                        o.s_end[sbase + ns + (j - q0)] = in.ops_end[j];
-                    }
-                }
-                ns += q1 - q0;
-                nn++;
-                continue;
-            }
-            int64_t tk = -1;
-            for (uint64_t j = tpe0; j < tpe1; j++)
-                if (in.tp_ver[j] == v) {
-                    tk = (int64_t)j;
-                    break;
-                }
-            if (tk < 0) continue;
-            bool have_end = false;
-            uint64_t end = 0;
-            for (uint64_t j = in.tps_off[tk]; j < in.tps_off[tk + 1]; j++)
-                if (!have_end || in.tps_end[j] > end) {
-                    end = in.tps_end[j];
-                    have_end = true;
-                }
-            for (uint64_t j = q0; j < q1; j++)
-                if (!have_end || in.ops_end[j] > end) {
-                    end = in.ops_end[j];
-                    have_end = true;
-                }
-            if (!have_end) continue;
-            SeqHoles sh{V64{in.tps_start, 0}, V64{in.tps_end, 0}, in.tps_off[tk], in.tps_off[tk + 1]};
-            const uint64_t first = sbase + ns;
-            uint64_t cnt = 0;
-            auto piece = [&](uint64_t s, uint64_t t) {
-                if (FILL) {
-                    o.s_start[first + cnt] = s;
-                    o.s_end[first + cnt] = t;
-                }
-                cnt++;
-            };
-            for (uint64_t j = q0; j < q1; j++) sweep(sh, in.ops_start[j], in.ops_end[j], 0, end, piece);
-            if (cnt) {
-                if (FILL) {
-                    const uint64_t q = nbase + nn;
-                    okind[q] = 1;
-                    ostart[q] = v;
-                    oend[q] = v;
-                    osro[q] = first;
-                    osrn[q] = cnt;
-                }
-                nn++;
-                ns += cnt;
-            }
+    uint64_t pre_n = 0, pre_s = 0, tot_n = 0, tot_s = 0;
+    for (int w = 0; w < (int)(NEEDS_T / 64); w++) {
+        if (w < wv) {
+            pre_n += s_wn[w];
+            pre_s += s_ws[w];
         }
-        if (ours < 0) full(1, head);
-        else if (head > (uint64_t)ours) full((uint64_t)ours + 1, head);
-        if (!FILL) {
-            o.need_count[e] = nn;
-            o.seq_count[e] = ns;
-        }
-    };
-    const bool all_lds = tn_lds && on_lds && (!FILL || o_lds);
-    if (live) {
-        if (all_lds) {
-            lane(V64S<1>{l_tns, tn_lo}, V64S<1>{l_tne, tn_lo}, V64S<1>{l_ons, on_lo}, V64S<1>{l_one, on_lo},
-                 WView<uint8_t, 1>{l_kind, o_lo}, WView<uint64_t, 1>{l_start, o_lo}, WView<uint64_t, 1>{l_end, o_lo},
-                 WView<uint64_t, 1>{l_sro, o_lo}, WView<uint64_t, 1>{l_srn, o_lo});
+        tot_n += s_wn[w];
+        tot_s += s_ws[w];
+    }
+    const uint64_t lex_n = pre_n + in_n - nn, lex_s = pre_s + in_s - ns;
+    // publish the aggregate, look back for the prefix, publish the inclusive prefix
+    if (wv == 0) {
+        uint64_t bn = 0, bs = 0;
+        if (wg == 0) {
+            if (lane == 0) {
+                st_store(&a.st[0], ST_P | tot_n);
+                st_store(&a.st[1], ST_P | tot_s);
+            }
         } else {
-            lane(V64{in.tn_start, 0}, V64{in.tn_end, 0}, V64{in.on_start, 0}, V64{in.on_end, 0},
-                 WView<uint8_t>{o.kind, 0}, WView<uint64_t>{o.start, 0}, WView<uint64_t>{o.end, 0},
-                 WView<uint64_t>{o.sr_off, 0}, WView<uint64_t>{o.sr_n, 0});
+            if (lane == 0) {
+                st_store(&a.st[2 * wg], ST_A | tot_n);
+                st_store(&a.st[2 * wg + 1], ST_A | tot_s);
+            }
+            lookback2(a.st, (int64_t)wg, bn, bs);
+            if (lane == 0) {
+                st_store(&a.st[2 * wg], ST_P | (bn + tot_n));
+                st_store(&a.st[2 * wg + 1], ST_P | (bs + tot_s));
+            }
+        }
+        if (lane == 0) {
+            s_base[0] = bn;
+            s_base[1] = bs;
         }
     }
-    if (FILL && all_lds) {
+    __syncthreads();
+    const uint64_t wbn = s_base[0], wbs = s_base[1];
+    if (live) {
+        const_cast<uint64_t *>(o.need_off)[e] = wbn + lex_n;
+        const_cast<uint64_t *>(o.seq_off)[e] = wbs + lex_s;
+    }
+    if (e1 == in.n && threadIdx.x == 0) {  // last workgroup: closing offsets and totals
+        const_cast<uint64_t *>(o.need_off)[in.n] = wbn + tot_n;
+        const_cast<uint64_t *>(o.seq_off)[in.n] = wbs + tot_s;
+        a.ticket[1] = wbn + tot_n;
+        a.ticket[2] = wbs + tot_s;
+    }
+    // capacity guard: a workgroup whose outputs would not fit writes none (the host reports the
+    // totals and the caller re-runs with them)
+    if (wbn + tot_n > a.need_cap || wbs + tot_s > a.seq_cap) return;
+    NeedsOutLds *Lo = OutStage<true>().get();
+    if (tot_n > NEEDS_CAP_O) Lo = nullptr;
+    if (live) walk_dispatch<true>(in, o, h, L, Lo, g, wbn, wbn + lex_n, wbs + lex_s, nn, ns);
+    if (g.lds && Lo) {
         __syncthreads();
-        const uint64_t m = o_hi - o_lo;
-        for (uint64_t k = threadIdx.x; k < m; k += NEEDS_T) {
-            o.start[o_lo + k] = l_start[k];
-            o.end[o_lo + k] = l_end[k];
-            o.sr_off[o_lo + k] = l_sro[k];
-            o.sr_n[o_lo + k] = l_srn[k];
-            o.kind[o_lo + k] = l_kind[k];
-        }
+        flush_needs(o, *Lo, wbn, tot_n);
     }
 }
 
@@ -428,5 +728,87 @@ extern "C" int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in,
     }
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     if (ctx->profiling) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[6 + pass], ctx->ev[0], ctx->ev[1]));
+    return CORRO_OK;
+}
+
+extern "C" int corro_needs_bound(corro_ctx *ctx, const corro_sync_entries *in, int mem, uint64_t *need_cap,
+                                 uint64_t *seq_cap) {
+    if (!ctx || !in || !need_cap || !seq_cap) return fail(CORRO_E_INVALID, "NULL argument");
+    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
+    const uint64_t n = in->n;
+    if (n == 0) {
+        *need_cap = *seq_cap = 0;
+        return CORRO_OK;
+    }
+    uint64_t w[6] = {0, 0, 0, 0, 0, 0};  // tn, on, tp, op totals, then tps, ops totals
+    const uint64_t *offs[4] = {in->tn_off, in->on_off, in->tp_off, in->op_off};
+    for (int i = 0; i < 4; i++) {
+        if (!offs[i]) return fail(CORRO_E_INVALID, "a required offset array is NULL");
+        if (mem == CORRO_MEM_HOST) w[i] = offs[i][n];
+        else CORRO_HIP_TRY(hipMemcpy(&w[i], offs[i] + n, 8, hipMemcpyDeviceToHost));
+    }
+    const uint64_t *soffs[2] = {in->tps_off, in->ops_off};
+    const uint64_t sidx[2] = {w[2], w[3]};
+    for (int i = 0; i < 2; i++) {
+        if (!sidx[i]) continue;
+        if (!soffs[i]) return fail(CORRO_E_INVALID, "a partial seq offset array is NULL");
+        if (mem == CORRO_MEM_HOST) w[4 + i] = soffs[i][sidx[i]];
+        else CORRO_HIP_TRY(hipMemcpy(&w[4 + i], soffs[i] + sidx[i], 8, hipMemcpyDeviceToHost));
+    }
+    // Full pieces <= our ranges + holes (their ranges + their partial versions) + 1 tail per entry,
+    // plus one Partial per our partial version; seq pieces <= our + their partial seq ranges.
+    // Exact for disjoint need ranges (RangeInclusiveSet output); the one-pass call reports the
+    // true totals if overlapping ranges ever exceed it.
+    *need_cap = w[0] + w[1] + w[2] + w[3] + n;
+    *seq_cap = w[4] + w[5];
+    return CORRO_OK;
+}
+
+extern "C" int corro_compute_needs_onepass(corro_ctx *ctx, const corro_sync_entries *in, corro_needs_out *out,
+                                         uint64_t need_cap, uint64_t seq_cap, uint64_t *totals) {
+    if (!ctx || !in || !out || !totals) return fail(CORRO_E_INVALID, "NULL argument");
+    const uint64_t n = in->n;
+    totals[0] = totals[1] = 0;
+    if (n == 0) return CORRO_OK;
+    if (!out->need_off || !out->seq_off) return fail(CORRO_E_INVALID, "need_off / seq_off are NULL");
+    if ((need_cap && (!out->kind || !out->start || !out->end || !out->sr_off || !out->sr_n)) ||
+        (seq_cap && (!out->s_start || !out->s_end)))
+        return fail(CORRO_E_INVALID, "an output array is NULL");
+    for (const void *q : {(const void *)in->tn_start, (const void *)in->tn_end, (const void *)in->on_start,
+                          (const void *)in->on_end})
+        if (q && ((uintptr_t)q % 16) != 0) return fail(CORRO_E_INVALID, "device need-range arrays must be 16-byte aligned");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const uint64_t blocks = (n + NEEDS_T - 1) / NEEDS_T;
+    if (blocks > 0x7FFFFFFFULL) return fail(CORRO_E_RANGE, "too many sync entries");
+    const size_t scratch = (2 * blocks + 4) * 8;
+    if (int rc = ctx->d_needs1.ensure(scratch)) return rc;
+    uint64_t *ticket = ctx->d_needs1.as<uint64_t>();
+    Needs1Args a{ticket + 4, ticket, need_cap, seq_cap};
+    SyncDev d{};
+    d.n = n;
+    d.their_head = in->their_head; d.our_head = in->our_head;
+    d.tn_off = in->tn_off; d.tn_start = in->tn_start; d.tn_end = in->tn_end;
+    d.tp_off = in->tp_off; d.tp_ver = in->tp_ver;
+    d.tps_off = in->tps_off; d.tps_start = in->tps_start; d.tps_end = in->tps_end;
+    d.on_off = in->on_off; d.on_start = in->on_start; d.on_end = in->on_end;
+    d.op_off = in->op_off; d.op_ver = in->op_ver;
+    d.ops_off = in->ops_off; d.ops_start = in->ops_start; d.ops_end = in->ops_end;
+    CORRO_HIP_TRY(hipMemsetAsync(ticket, 0, scratch, s));
+    if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    hipLaunchKernelGGL(k_needs1, dim3((uint32_t)blocks), dim3(NEEDS_T), 0, s, d, *out, a);
+    if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    CORRO_HIP_TRY(hipGetLastError());
+    uint64_t t[2];
+    CORRO_HIP_TRY(hipMemcpyAsync(t, ticket + 1, 16, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (ctx->profiling) {
+        CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[6], ctx->ev[0], ctx->ev[1]));
+        ctx->last_ms[7] = 0.f;
+    }
+    totals[0] = t[0];
+    totals[1] = t[1];
+    if (t[0] > need_cap || t[1] > seq_cap)
+        return fail(CORRO_E_RANGE, "need output exceeds the given capacity (totals hold the sizes to re-run with)");
     return CORRO_OK;
 }

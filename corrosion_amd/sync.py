@@ -177,6 +177,52 @@ def _needs_device(engine, ent):
     return res
 
 
+def _needs_device_1pass(engine, ent):
+    """corro_compute_needs_onepass on device-resident CSR entries: one kernel, every input read once
+    (outputs sized by corro_needs_bound; re-run at the exact totals in the never-expected case of
+    overlapping need ranges exceeding it). Returns the same CSR dict as _needs_device."""
+    import torch
+    lib = L.lib()
+    n = int(ent["their_head"].shape[0])
+    dev = ent["their_head"].device
+    s = L.SyncEntries()
+    s.n = n
+    for k, _ in L.SyncEntries._fields_[1:]:
+        a = ent[k]
+        setattr(s, k, a.data_ptr() if a.numel() else None)
+    torch.cuda.current_stream().synchronize()
+    ncap, scap = C.c_uint64(), C.c_uint64()
+    L.check(lib.corro_needs_bound(engine._h, C.byref(s), L.CORRO_MEM_DEVICE, C.byref(ncap), C.byref(scap)))
+    caps = [ncap.value, scap.value]
+    while True:
+        res = {"need_off": torch.empty(n + 1, dtype=torch.int64, device=dev),
+               "seq_off": torch.empty(n + 1, dtype=torch.int64, device=dev),
+               "kind": torch.empty(max(caps[0], 1), dtype=torch.uint8, device=dev)}
+        for k in ("start", "end", "sr_off", "sr_n"):
+            res[k] = torch.empty(max(caps[0], 1), dtype=torch.int64, device=dev)
+        for k in ("s_start", "s_end"):
+            res[k] = torch.empty(max(caps[1], 1), dtype=torch.int64, device=dev)
+        o = L.NeedsOut()
+        for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+            setattr(o, k, res[k].data_ptr())
+        tot = (C.c_uint64 * 2)()
+        rc = lib.corro_compute_needs_onepass(engine._h, C.byref(s), C.byref(o), caps[0], caps[1], tot)
+        if rc == -6 and (tot[0] > caps[0] or tot[1] > caps[1]):
+            caps = [tot[0], tot[1]]
+            continue
+        L.check(rc)
+        break
+    if n == 0:
+        res["need_off"].zero_()
+        res["seq_off"].zero_()
+    T, Ts = tot[0], tot[1]
+    for k in ("kind", "start", "end", "sr_off", "sr_n"):
+        res[k] = res[k][:T]
+    for k in ("s_start", "s_end"):
+        res[k] = res[k][:Ts]
+    return res
+
+
 def decode(res, index, npairs):
     out = [dict() for _ in range(npairs)]
     for e, (p, actor) in enumerate(index):

@@ -204,6 +204,18 @@ typedef struct {
 /* mem = CORRO_MEM_HOST or CORRO_MEM_DEVICE for BOTH `in` arrays and `out` arrays. */
 int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in, int mem,
                         corro_needs_out *out, int pass);
+/* One-pass form for DEVICE-resident entries and outputs: reads every input once (the count and
+ * the fill walk share LDS-staged inputs; workgroup offsets come from a decoupled look-back).
+ * Here out->need_off / out->seq_off (n+1 each) are OUTPUTS (written, like pass 0 + scan);
+ * kind/start/end/sr_off/sr_n hold need_cap elements, s_start/s_end seq_cap elements.
+ * totals[0] = needs, totals[1] = seq ranges (host memory). If a total exceeds its cap the call
+ * returns CORRO_E_RANGE, writes no payload past the cap, and totals still hold the exact sizes to
+ * re-run with. corro_needs_bound gives caps that always suffice for disjoint need ranges. */
+int corro_compute_needs_onepass(corro_ctx *ctx, const corro_sync_entries *in, corro_needs_out *out,
+                              uint64_t need_cap, uint64_t seq_cap, uint64_t *totals);
+/* Output-size bound from the entry CSR sizes (reads 6 words): needs <= our + their need ranges +
+ * their partial versions + our partial versions + entries; seq ranges <= all partial seq ranges. */
+int corro_needs_bound(corro_ctx *ctx, const corro_sync_entries *in, int mem, uint64_t *need_cap, uint64_t *seq_cap);
 /* Device helper between the two passes: offsets[0] = 0, offsets[k+1] = counts[0] + ... + counts[k]
  * (n + 1 outputs), for device-resident need_count / seq_count. */
 int corro_scan_offsets(corro_ctx *ctx, const uint64_t *counts, uint64_t *offsets, uint64_t n);

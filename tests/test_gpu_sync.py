@@ -110,3 +110,92 @@ def test_sync_lds_caps_exceeded_vs_oracle(dense):
     exp = O.needs(ent)
     for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
         assert np.array_equal(got[k], exp[k]), k
+
+
+# ---- one-pass form (corro_compute_needs_onepass: decoupled look-back, inputs read once) ----------
+
+def _to_dev(ent):
+    import torch
+    return {k: torch.from_numpy(np.ascontiguousarray(v).view(np.int64)).cuda() for k, v in ent.items()}
+
+
+def _check_1pass(ent_host, exp=None):
+    from corrosion_amd.sync import _needs_device_1pass
+    got = _needs_device_1pass(_engine(), _to_dev(ent_host))
+    exp = O.needs(ent_host) if exp is None else exp
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        assert np.array_equal(got[k].cpu().numpy().astype(np.uint64), exp[k].astype(np.uint64)), k
+
+
+@pytest.mark.parametrize("case", SYNC["cases"], ids=[c["name"] for c in SYNC["cases"]])
+def test_sync_kats_gpu_1pass(case):
+    from corrosion_amd.sync import _needs_device_1pass
+    ent = entries_from_pairs([(case["our"], case["their"])])
+    got = {k: v.cpu().numpy().astype(np.uint64) for k, v in _needs_device_1pass(_engine(), _to_dev(ent)).items()}
+    assert decode_needs(got, 1)[0] == kat_expect(case["expect"])
+
+
+def test_sync_random_vs_oracle_1pass():
+    rng = np.random.default_rng(6)
+    pairs = [(random_side(rng, with_head=rng.random() < 0.9), random_side(rng)) for _ in range(40000)]
+    _check_1pass(entries_from_pairs(pairs))   # 157 workgroups: look-back spans several waves
+
+
+def test_sync_config4_shape_1pass_equals_two_pass():
+    """Config-4-shaped entries in HBM (600K entries, 2344 workgroups): the one-pass kernel's CSR
+    equals the two-pass kernel's and the oracle's."""
+    import synth
+    from corrosion_amd.sync import _needs_device, _needs_device_1pass
+    ent = synth.sync_entries_torch(20000, 30, 21, device="cuda")
+    e = _engine()
+    a = _needs_device(e, ent)
+    b = _needs_device_1pass(e, ent)
+    for k in a:
+        assert a[k].shape == b[k].shape and bool((a[k] == b[k]).all()), k
+    exp = O.needs({k: v.cpu().numpy() for k, v in ent.items()})
+    for k in ("need_off", "kind", "start", "s_end"):
+        assert np.array_equal(b[k].cpu().numpy().astype(np.uint64), exp[k].astype(np.uint64)), k
+
+
+@pytest.mark.parametrize("dense", ["theirs", "ours", "both"])
+def test_sync_lds_caps_exceeded_1pass(dense):
+    rng = np.random.default_rng(12)
+    pairs = []
+    for i in range(1200):
+        heavy = 256 <= i < 768
+        nt = 12 if heavy and dense in ("theirs", "both") else int(rng.poisson(2))
+        no = 12 if heavy and dense in ("ours", "both") else int(rng.poisson(2))
+        pairs.append((_dense_side(rng, no, int(rng.integers(1, 100))), _dense_side(rng, nt, 300)))
+    _check_1pass(entries_from_pairs(pairs))
+
+
+def test_sync_1pass_capacity_error_reports_totals():
+    """Caps below the output size: CORRO_E_RANGE, the exact totals, no write past the caps; the
+    wrapper's re-run at those totals gives the oracle's result (here with overlapping our-need
+    ranges, which the RangeInclusiveSet-based bound does not cover)."""
+    import ctypes as C
+    import torch
+    import corrosion_amd._lib as L
+    their = {"head": 400, "need": [[k, k] for k in range(3, 390, 4)], "partials": {}}
+    our = {"head": None, "need": [[1, 395]] * 6, "partials": {}}
+    ent = entries_from_pairs([(our, their)] * 300)
+    _check_1pass(ent)
+    d = _to_dev(ent)
+    e = _engine()
+    s = L.SyncEntries()
+    s.n = len(ent["their_head"])
+    for k, _ in L.SyncEntries._fields_[1:]:
+        setattr(s, k, d[k].data_ptr() if d[k].numel() else None)
+    o = L.NeedsOut()
+    guard = torch.full((64,), 7, dtype=torch.int64, device="cuda")
+    bufs = {k: torch.zeros(s.n + 1, dtype=torch.int64, device="cuda") for k in ("need_off", "seq_off")}
+    for k in ("need_off", "seq_off"):
+        setattr(o, k, bufs[k].data_ptr())
+    for k in ("kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        setattr(o, k, guard.data_ptr())
+    tot = (C.c_uint64 * 2)()
+    rc = L.lib().corro_compute_needs_onepass(e._h, C.byref(s), C.byref(o), 0, 0, tot)
+    assert rc == -6
+    exp = O.needs(ent)
+    assert tot[0] == int(exp["need_off"][-1]) and tot[1] == int(exp["seq_off"][-1])
+    assert bool((guard == 7).all())
