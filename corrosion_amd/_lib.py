@@ -29,7 +29,8 @@ EXPORTS = [
     "corro_bookie_take_ready", "corro_process_fully_buffered", "corro_bookie_last",
     "corro_bookie_needed", "corro_bookie_contains_all", "corro_bookie_partial",
     "corro_generate_sync", "corro_partition_ranks", "corro_scan_offsets",
-    "corro_compute_needs_onepass", "corro_needs_bound",
+    "corro_compute_needs_onepass", "corro_needs_bound", "corro_extract_changes",
+    "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -68,6 +69,15 @@ class SyncEntries(C.Structure):
         "their_head", "our_head", "tn_off", "tn_start", "tn_end", "tp_off", "tp_ver", "tps_off",
         "tps_start", "tps_end", "on_off", "on_start", "on_end", "op_off", "op_ver", "ops_off",
         "ops_start", "ops_end")]
+
+
+class ExtractIn(C.Structure):
+    _fields_ = [("n", C.c_uint64)] + [(k, C.c_void_p) for k in ("site", "start", "end", "seq_start", "seq_end")]
+
+
+class ExtractOut(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("grp_count", "row_count", "grp_off", "row_off", "version", "last_seq",
+                                          "ts", "grp_row_off", "grp_rows")] + [("rows", Rows)]
 
 
 class NeedsOut(C.Structure):
@@ -143,6 +153,10 @@ def lib():
         "corro_scan_offsets": (i32, [vp, vp, vp, u64]),
         "corro_compute_needs_onepass": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsOut), u64, u64, vp]),
         "corro_needs_bound": (i32, [vp, C.POINTER(SyncEntries), i32, vp, vp]),
+        "corro_bookie_seq_bookkeeping": (i32, [vp, vp, u64, vp, vp, u64, vp, vp, vp]),
+        "corro_bookie_buffered_versions": (i32, [vp, vp, u64, u64, vp, u64, vp]),
+        "corro_bookie_buffered": (i32, [vp, vp, u64, u64, u64, C.POINTER(Rows), u64, vp]),
+        "corro_extract_changes": (i32, [vp, C.POINTER(ExtractIn), i32, C.POINTER(ExtractOut), i32]),
         "corro_booked_new": (i32, [vp]),
         "corro_booked_free": (None, [vp]),
         "corro_booked_insert_db": (i32, [vp, vp, vp, u64, vp, vp, u64, vp, vp, vp, u64, vp]),

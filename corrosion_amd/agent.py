@@ -133,9 +133,17 @@ class Agent:
         self.engine = MergeEngine(schema, capacity_hint=capacity_hint, device=device)
         self.bookie = Bookie()
         self.actor_id = actor_id
+        self.site_ids = {}      # ordinal -> 16-byte site id (crsql_site_id)
 
     def site(self, site_id):
-        return int(self.engine.register_sites(np.frombuffer(site_id, np.uint8).reshape(1, 16))[0])
+        o = int(self.engine.register_sites(np.frombuffer(bytes(site_id), np.uint8).reshape(1, 16))[0])
+        self.site_ids[o] = bytes(site_id)
+        return o
+
+    def handle_needs(self, needs, max_buf_size=None):
+        """Answer (actor_id, SyncNeedV1) needs from this node's state (serve.handle_needs)."""
+        from . import serve
+        return serve.handle_needs(self, needs, max_buf_size or serve.MAX_CHANGES_BYTES_PER_MESSAGE)
 
     def process_multiple_changes(self, changes):
         """changes: list of ChangeV1 (or (ChangeV1, source, instant) tuples) in arrival order."""

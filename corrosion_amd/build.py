@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcorro_hip.so")
-SOURCES = ["engine.hip", "sync_needs.hip", "partition.hip", "prims.hip", "booked.cpp", "agent.cpp"]
+SOURCES = ["engine.hip", "sync_needs.hip", "partition.hip", "prims.hip", "extract.hip", "booked.cpp", "agent.cpp"]
 HEADERS = ["internal.h", "merge_kernels.h", "ovf_kernels.h", "ranges.h", "booked.h", "rowhash.h"]
 ARCH = "gfx950"
 
@@ -28,6 +28,8 @@ def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = []
     objs = []
     for src in SOURCES:
         obj = os.path.join(CSRC, src + ".o")
@@ -38,8 +40,12 @@ def build(force=False, verbose=False):
                    "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.check_call(cmd)
+        jobs.append(cmd)
         objs.append(obj)
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS") or os.cpu_count() or 1)))
+    with ThreadPoolExecutor(workers) as ex:
+        for f in [ex.submit(subprocess.check_call, c) for c in jobs]:
+            f.result()
     tmp = LIB + ".tmp"
     subprocess.check_call([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)
     os.replace(tmp, LIB)

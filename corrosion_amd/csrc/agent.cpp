@@ -11,6 +11,7 @@
 //   process_fully_buffered_changes :541-688   (apply a version once all its seqs arrived)
 // and generate_sync (corro-types/src/sync.rs:284-333). The merge itself is corro_apply_batch.
 #include <array>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <optional>
@@ -407,6 +408,85 @@ int corro_bookie_contains_all(corro_bookie *bk, const uint8_t *actor_id, uint64_
     }
     Range sq{seq_start, seq_end};
     *result = it->second.contains_all(start, end, has_seqs ? &sq : nullptr);
+    return CORRO_OK;
+}
+
+// __corro_seq_bookkeeping rows of one (actor, version) as handle_need reads them
+// (corro-agent/src/api/peer/mod.rs:505-511, :640-667): seq ranges, last_seq (-1 = no rows), ts.
+int corro_bookie_seq_bookkeeping(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t *start,
+                                 uint64_t *end, uint64_t cap, uint64_t *count, int64_t *last_seq, uint64_t *ts) {
+    if (!bk || !actor_id || !count || !last_seq || !ts) return fail(CORRO_E_INVALID, "NULL argument");
+    *count = 0;
+    *last_seq = -1;
+    *ts = 0;
+    auto so = bk->site_of.find(actor_of(actor_id));
+    if (so == bk->site_of.end()) return CORRO_OK;
+    auto it = bk->seqbook.find({so->second, version});
+    if (it == bk->seqbook.end()) return CORRO_OK;
+    std::vector<Range> rs = it->second.ranges;
+    std::sort(rs.begin(), rs.end());
+    uint64_t k = 0;
+    for (const Range &r : rs) {
+        if (k < cap && start && end) {
+            start[k] = r.first;
+            end[k] = r.second;
+        }
+        k++;
+    }
+    *count = k;
+    *last_seq = (int64_t)it->second.last_seq;
+    *ts = it->second.ts;
+    return CORRO_OK;
+}
+
+// versions of `actor` in [vstart, vend] with buffered rows (the EXISTS(__corro_buffered_changes)
+// probe of handle_need, peer/mod.rs:466-492), ascending; *count = all of them, at most cap written.
+int corro_bookie_buffered_versions(corro_bookie *bk, const uint8_t *actor_id, uint64_t vstart, uint64_t vend,
+                                   uint64_t *versions, uint64_t cap, uint64_t *count) {
+    if (!bk || !actor_id || !count || (cap && !versions)) return fail(CORRO_E_INVALID, "NULL argument");
+    *count = 0;
+    auto so = bk->site_of.find(actor_of(actor_id));
+    if (so == bk->site_of.end() || vstart > vend || vstart > (uint64_t)INT64_MAX) return CORRO_OK;
+    uint64_t k = 0;
+    for (auto it = bk->buffered.lower_bound({so->second, (int64_t)vstart}); it != bk->buffered.end(); ++it) {
+        if (it->first.first != so->second || (uint64_t)it->first.second > vend) break;
+        if (it->second.empty()) continue;
+        if (k < cap) versions[k] = (uint64_t)it->first.second;
+        k++;
+    }
+    *count = k;
+    return CORRO_OK;
+}
+
+// __corro_buffered_changes rows of (actor, version) with seq in [seq_start, seq_end], seq
+// ascending (peer/mod.rs:513-531, :672-693). *count = all matching rows; at most cap are written.
+int corro_bookie_buffered(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t seq_start,
+                          uint64_t seq_end, corro_rows *o, uint64_t cap, uint64_t *count) {
+    if (!bk || !actor_id || !count || (cap && !o)) return fail(CORRO_E_INVALID, "NULL argument");
+    *count = 0;
+    auto so = bk->site_of.find(actor_of(actor_id));
+    if (so == bk->site_of.end()) return CORRO_OK;
+    auto it = bk->buffered.find({so->second, (int64_t)version});
+    if (it == bk->buffered.end() || seq_start > seq_end || seq_start > 0xFFFFFFFFULL) return CORRO_OK;
+    const uint32_t hi = seq_end > 0xFFFFFFFFULL ? 0xFFFFFFFFu : (uint32_t)seq_end;
+    uint64_t k = 0;
+    for (auto r = it->second.lower_bound((uint32_t)seq_start); r != it->second.end() && r->first <= hi; ++r, ++k) {
+        if (k >= cap) continue;
+        const HostRow &h = r->second;
+        if (o->pk) o->pk[k] = h.pk;
+        if (o->table_cid) o->table_cid[k] = h.tcid;
+        if (o->col_version) o->col_version[k] = h.cv;
+        if (o->db_version) o->db_version[k] = h.dbv;
+        if (o->cl) o->cl[k] = h.cl;
+        if (o->seq) o->seq[k] = h.seq;
+        if (o->site) o->site[k] = h.site;
+        if (o->ts) o->ts[k] = h.ts;
+        if (o->val0) o->val0[k] = h.v0;
+        if (o->val1) o->val1[k] = h.v1;
+        if (o->val_type) o->val_type[k] = h.vt;
+        if (o->val_len) o->val_len[k] = h.vl;
+    }
+    *count = k;
     return CORRO_OK;
 }
 

@@ -305,7 +305,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_state_flags, &ctx->d_out_off, &ctx->d_out_cnt, &ctx->d_out_flags, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
                       &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export,
-                      &ctx->d_needs, &ctx->d_needs1, &ctx->d_ncols, &ctx->d_part};
+                      &ctx->d_needs, &ctx->d_needs1, &ctx->d_xidx, &ctx->d_xout, &ctx->d_ncols, &ctx->d_part};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     for (auto &e : ctx->ev)
@@ -601,6 +601,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     std::swap(ctx->d_state_flags, ctx->d_out_flags);
     ctx->cur = nxt;
     ctx->state_total = ctx->h_misc[2];
+    ctx->state_epoch++;
     if (ctx->h_misc[3]) ctx->state_wide = true;
     return CORRO_OK;
 }
@@ -653,6 +654,7 @@ int corro_state_reset(corro_ctx *ctx) {
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_state_flags.p, 0, ctx->B * 4ULL, ctx->stream));
     CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->state_total = 0;
+    ctx->state_epoch++;
     return CORRO_OK;
 }
 

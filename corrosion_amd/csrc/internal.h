@@ -52,6 +52,13 @@ struct DevBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// Pointers into corro_ctx::d_xidx (extract.hip): the (site, db_version, seq) index of the state.
+struct XIdxPtrs {
+    uint64_t *hkey = nullptr;
+    uint32_t *seq = nullptr, *ref = nullptr, *gid = nullptr, *gstart = nullptr, *glast = nullptr;
+    uint64_t *gts = nullptr;
+};
+
 struct Table {
     std::string name;
     std::vector<std::string> cols;
@@ -100,6 +107,13 @@ struct corro_ctx {
     corro::DevBuf d_export;
     corro::DevBuf d_needs;        // sync-need scratch
     corro::DevBuf d_needs1;       // one-pass need diff: look-back status words + ticket
+    corro::DevBuf d_xidx;         // changeset extraction: state index + its build scratch
+    corro::DevBuf d_xout;         // changeset extraction: staged needs / outputs
+    corro::XIdxPtrs x;
+    uint64_t state_epoch = 0;     // bumped by every state change (apply, reset)
+    uint64_t xidx_epoch = ~0ULL;  // epoch the extraction index was built for
+    uint32_t x_db = 1, x_groups = 0;
+    uint64_t x_max_dbv = 0;
     corro::DevBuf d_ncols;        // u16 column count per table
     corro::DevBuf d_part;         // partition counts
     uint64_t *h_misc = nullptr;   // pinned

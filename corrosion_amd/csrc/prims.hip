@@ -26,6 +26,14 @@ int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t 
     return CORRO_OK;
 }
 
+// inclusive scan of u32 (extraction index group ids); temp == nullptr -> *temp_bytes = size needed
+int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, uint32_t *out, uint32_t n,
+                            hipStream_t s) {
+    const hipError_t e = rocprim::inclusive_scan(temp, *temp_bytes, in, out, (size_t)n, rocprim::plus<uint32_t>(), s);
+    if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("scan: ") + hipGetErrorString(e));
+    return CORRO_OK;
+}
+
 struct OvfMax {
     __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return x > y ? x : y; }
 };

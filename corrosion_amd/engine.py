@@ -183,6 +183,86 @@ class MergeEngine:
         L.check(L.lib().corro_partition_ranks(self._h, C.byref(s), nranks, C.byref(o), counts.ctypes.data))
         return out, [int(c) for c in counts[:nranks]]
 
+    # ---- changeset extraction (server side of a sync need) ---------------------------------
+    def extract_changes(self, needs):
+        """crsql_changes rows per need (corro_extract_changes): needs = {"site": u32[], "start":
+        u64[], "end": u64[], optional "seq_start"/"seq_end": u32[]} as numpy arrays (host) or CUDA
+        tensors (device). Returns grp_off/row_off (n+1), per group version/last_seq/ts/grp_row_off/
+        grp_rows, and "rows" (crsql_changes fields), groups of a need in DESCENDING version order."""
+        lib = L.lib()
+        on_dev = _is_torch(needs["site"])
+        n = int(needs["site"].shape[0])
+        s = L.ExtractIn()
+        s.n = n
+        keep = []
+        for k, dt in (("site", np.uint32), ("start", np.uint64), ("end", np.uint64), ("seq_start", np.uint32),
+                      ("seq_end", np.uint32)):
+            a = needs.get(k)
+            if a is None:
+                setattr(s, k, None)
+                continue
+            if on_dev:
+                if not a.is_cuda or not a.is_contiguous() or a.element_size() != np.dtype(dt).itemsize:
+                    raise ValueError(f"device need field {k} must be a contiguous CUDA tensor of {np.dtype(dt)}")
+                setattr(s, k, a.data_ptr() if n else None)
+            else:
+                a = np.ascontiguousarray(a, dtype=dt)
+                keep.append(a)
+                setattr(s, k, a.ctypes.data if n else None)
+        mem = L.CORRO_MEM_DEVICE if on_dev else L.CORRO_MEM_HOST
+        if on_dev:
+            import torch
+            dev = needs["site"].device
+
+            def alloc(cnt, dt):
+                tdt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint32: torch.int32,
+                       np.uint8: torch.uint8}[dt]
+                return torch.empty(max(cnt, 1), dtype=tdt, device=dev)
+
+            def ptr(a):
+                return a.data_ptr()
+            torch.cuda.current_stream().synchronize()
+        else:
+            def alloc(cnt, dt):
+                return np.zeros(max(cnt, 1), dt)
+
+            def ptr(a):
+                return a.ctypes.data
+        o = L.ExtractOut()
+        gc, rc = alloc(n, np.uint64), alloc(n, np.uint64)
+        o.grp_count, o.row_count = ptr(gc), ptr(rc)
+        if n:
+            L.check(lib.corro_extract_changes(self._h, C.byref(s), mem, C.byref(o), 0))
+        if on_dev:
+            import torch
+            go = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            ro = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            go[1:] = torch.cumsum(gc[:n], 0)
+            ro[1:] = torch.cumsum(rc[:n], 0)
+            G, R = int(go[-1].item()), int(ro[-1].item())
+        else:
+            go = np.zeros(n + 1, np.uint64)
+            ro = np.zeros(n + 1, np.uint64)
+            go[1:] = np.cumsum(gc[:n])
+            ro[1:] = np.cumsum(rc[:n])
+            G, R = int(go[-1]), int(ro[-1])
+        res = {"grp_off": go, "row_off": ro, "version": alloc(G, np.int64), "last_seq": alloc(G, np.uint64),
+               "ts": alloc(G, np.uint64), "grp_row_off": alloc(G, np.uint64), "grp_rows": alloc(G, np.uint64)}
+        rows = {k: alloc(R, dt) for k, dt in ROW_FIELDS.items()}
+        o.grp_off, o.row_off = ptr(go), ptr(ro)
+        for k in ("version", "last_seq", "ts", "grp_row_off", "grp_rows"):
+            setattr(o, k, ptr(res[k]))
+        for k, a in rows.items():
+            setattr(o.rows, k, ptr(a))
+        if n:
+            if on_dev:
+                torch.cuda.current_stream().synchronize()
+            L.check(lib.corro_extract_changes(self._h, C.byref(s), mem, C.byref(o), 1))
+        for k in ("version", "last_seq", "ts", "grp_row_off", "grp_rows"):
+            res[k] = res[k][:G]
+        res["rows"] = {k: a[:R] for k, a in rows.items()}
+        return res
+
     # ---- sync need diff -------------------------------------------------------------------
     def compute_needs(self, entries):
         """Batched compute_available_needs over CSR entries (see corrosion_amd.sync)."""

@@ -220,6 +220,39 @@ int corro_needs_bound(corro_ctx *ctx, const corro_sync_entries *in, int mem, uin
  * (n + 1 outputs), for device-resident need_count / seq_count. */
 int corro_scan_offsets(corro_ctx *ctx, const uint64_t *counts, uint64_t *offsets, uint64_t n);
 
+/* ------------------------------------------------------------------ changeset extraction */
+
+/* Server side of a sync need (handle_need, corro-agent/src/api/peer/mod.rs:371-727): for every
+ * need, the state's crsql_changes rows WHERE site_id = site AND db_version BETWEEN start AND end
+ * [AND seq BETWEEN seq_start AND seq_end], grouped by db_version in DESCENDING order (:385-394),
+ * rows of a group by seq ASCENDING (:423-431, :603-611). A Full need is one entry; a Partial need
+ * is one entry per seq range with start = end = version. Ties on seq inside a version come out in
+ * an unspecified order (as the SQL leaves them). */
+typedef struct {
+    uint64_t n;
+    const uint32_t *site;                   /* actor site ordinal */
+    const uint64_t *start, *end;            /* db_version range, inclusive */
+    const uint32_t *seq_start, *seq_end;    /* optional row filter: both NULL = every seq */
+} corro_extract_in;
+
+/* Two passes, like corro_compute_needs: pass 0 fills grp_count / row_count per need; the caller
+ * scans them into grp_off / row_off (n+1 each) and allocates; pass 1 fills the rest. Per group:
+ * db_version, last_seq = MAX(seq) and ts = MAX(ts) over ALL of that version's rows (the GROUP BY
+ * query, not the seq-filtered rows), and its rows [grp_row_off, grp_row_off + grp_rows). Row
+ * arrays left NULL are not written. */
+typedef struct {
+    uint64_t *grp_count, *row_count;        /* pass 0, n each */
+    const uint64_t *grp_off, *row_off;      /* pass 1 inputs, n+1 each */
+    int64_t *version;
+    uint64_t *last_seq, *ts;
+    uint64_t *grp_row_off, *grp_rows;
+    corro_rows rows;
+} corro_extract_out;
+
+/* mem = CORRO_MEM_HOST or CORRO_MEM_DEVICE for both. The state index behind it is rebuilt on the
+ * first call after the state changed (one radix sort of the clock rows). */
+int corro_extract_changes(corro_ctx *ctx, const corro_extract_in *in, int mem, corro_extract_out *out, int pass);
+
 /* ------------------------------------------------------------------ gap bookkeeping */
 
 /* BookedVersions (agent.rs:1260-1458): needed gaps, max, partials' presence. Host-side. */
@@ -294,6 +327,18 @@ int corro_bookie_contains_all(corro_bookie *bk, const uint8_t *actor_id, uint64_
                               int has_seqs, uint64_t seq_start, uint64_t seq_end, int *result);
 int corro_bookie_partial(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t *start,
                          uint64_t *end, uint64_t cap, uint64_t *count, int64_t *last_seq);
+/* __corro_seq_bookkeeping rows of (actor, version) as handle_need reads them (peer/mod.rs:505-511,
+ * :640-667): seq ranges (ascending), last_seq (-1 = none), ts. */
+int corro_bookie_seq_bookkeeping(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t *start,
+                                 uint64_t *end, uint64_t cap, uint64_t *count, int64_t *last_seq, uint64_t *ts);
+/* Versions of actor in [vstart, vend] holding buffered rows, ascending (handle_need's
+ * EXISTS(__corro_buffered_changes) probe, peer/mod.rs:466-492). */
+int corro_bookie_buffered_versions(corro_bookie *bk, const uint8_t *actor_id, uint64_t vstart, uint64_t vend,
+                                   uint64_t *versions, uint64_t cap, uint64_t *count);
+/* __corro_buffered_changes rows of (actor, version) with seq in [seq_start, seq_end], seq
+ * ascending (peer/mod.rs:513-531, :672-693); *count = matching rows, at most cap written. */
+int corro_bookie_buffered(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t seq_start,
+                          uint64_t seq_end, corro_rows *out, uint64_t cap, uint64_t *count);
 
 /* generate_sync (corro-types/src/sync.rs:284-333) as CSR over actors with a known head:
  * heads, needed ranges, and for every non-complete partial the seq gaps over 0..=last_seq. */

@@ -286,3 +286,36 @@ class Booked:
 
     def contains(self, v):
         return bool(lib().of_booked_contains(self._h, v))
+
+
+def extract_changes(rows, needs):
+    """Changeset extraction on exported crsql_changes rows (numpy restatement of handle_need's two
+    queries, corro-agent/src/api/peer/mod.rs:385-394 and :423-431 / :603-611): per need, the
+    versions of `site` in [start, end] present in the rows, DESCENDING, each with MAX(seq) and
+    MAX(ts) over the version's rows and its rows with seq in the optional [seq_start, seq_end],
+    by seq ascending (ties by (table_cid, pk), the canonical form the tests compare in). Returns a
+    list per need of (version, last_seq, ts, row index array)."""
+    site = np.asarray(rows["site"]).astype(np.int64)
+    dbv = np.asarray(rows["db_version"]).astype(np.int64)
+    order = np.lexsort((np.asarray(rows["pk"]), np.asarray(rows["table_cid"]), np.asarray(rows["seq"]), dbv, site))
+    ks, kd = site[order], dbv[order]
+    out = []
+    for e in range(len(needs["site"])):
+        a, s0, e0 = int(needs["site"][e]), int(needs["start"][e]), int(needs["end"][e])
+        lo = np.searchsorted(ks, a, "left")
+        hi = np.searchsorted(ks, a, "right")
+        sub = order[lo:hi]
+        d = kd[lo:hi]
+        l2, h2 = np.searchsorted(d, s0, "left"), np.searchsorted(d, e0, "right")
+        sub, d = sub[l2:h2], d[l2:h2]
+        groups = []
+        for v in sorted(set(d.tolist()), reverse=True):
+            g = sub[d == v]
+            last = int(np.asarray(rows["seq"])[g].max())
+            ts = int(np.asarray(rows["ts"])[g].max())
+            if needs.get("seq_start") is not None:
+                sq = np.asarray(rows["seq"])[g]
+                g = g[(sq >= int(needs["seq_start"][e])) & (sq <= int(needs["seq_end"][e]))]
+            groups.append((v, last, ts, g))
+        out.append(groups)
+    return out

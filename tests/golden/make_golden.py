@@ -10,6 +10,9 @@ Sources (data only, no reference code is copied):
                    /root/reference/crates/corro-types/src/sync.rs:386-500.
   * gaps_kats    — the insert/expect_gaps steps of test_booked_insert_db,
                    /root/reference/crates/corro-types/src/agent.rs:1605-1868.
+  * chunker_kats — the cases of test_change_chunker, /root/reference/crates/corro-types/src/change.rs:
+                   266-401: Change { seq, ..Default::default() } (empty table/cid/pk, Null value), so
+                   every change's estimated_byte_size is the same; max_buf_size is given in changes.
 
 Merge-case notation: table t(id INTEGER PK, a, b, c); cid 0 = sentinel '-1', a=1, b=2, c=3.
 Sites sN = sixteen bytes of value N. A change is [cid, value, col_version, db_version, site, cl];
@@ -146,6 +149,24 @@ GAPS = [
 ]
 
 
+# (seqs of the input changes, start_seq, last_seq, max_buf_size in multiples of one change's size
+#  or an absolute byte count, expected chunks as (seqs of changes, start, end))
+CHUNKER = [
+    {"name": "empty iterator", "input": [], "start": 0, "last": 100, "max_bytes": 50,
+     "chunks": [[[], 0, 100]]},
+    {"name": "2 iterations", "input": [0, 1, 2], "start": 0, "last": 100, "max_changes": 2,
+     "chunks": [[[0, 1], 0, 1], [[2], 2, 100]]},
+    {"name": "last seq reached", "input": [0, 1], "start": 0, "last": 0, "max_changes": 1,
+     "chunks": [[[0], 0, 0]]},
+    {"name": "gaps", "input": [0, 2], "start": 0, "last": 100, "max_changes": 2,
+     "chunks": [[[0, 2], 0, 100]]},
+    {"name": "gaps, send all", "input": [2, 4, 7, 8], "start": 0, "last": 100, "max_bytes": 100000,
+     "chunks": [[[2, 4, 7, 8], 0, 100]]},
+    {"name": "gaps, two chunks", "input": [2, 4, 7, 8], "start": 0, "last": 10, "max_changes": 2,
+     "chunks": [[[2, 4], 0, 4], [[7, 8], 5, 10]]},
+]
+
+
 def main():
     merge = [{"name": n, "changes": c, "rows": r, "impacted": imp} for (n, c, r, imp) in MERGE]
     with open(os.path.join(HERE, "merge_kats.json"), "w") as f:
@@ -155,6 +176,8 @@ def main():
         json.dump({"source": "corro-types/src/sync.rs:386-500", "cases": SYNC}, f, indent=1)
     with open(os.path.join(HERE, "gaps_kats.json"), "w") as f:
         json.dump({"source": "corro-types/src/agent.rs:1605-1868", "steps": GAPS}, f, indent=1)
+    with open(os.path.join(HERE, "chunker_kats.json"), "w") as f:
+        json.dump({"source": "corro-types/src/change.rs:266-401", "cases": CHUNKER}, f, indent=1)
 
 
 if __name__ == "__main__":
