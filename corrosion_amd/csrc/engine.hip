@@ -634,7 +634,7 @@ int corro_ctx_set_profiling(corro_ctx *ctx, int on) {
 
 int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count) {
     if (!ctx || !count || (!ms && cap)) return fail(CORRO_E_INVALID, "NULL argument");
-    const uint32_t n = 8;
+    const uint32_t n = 9;
     for (uint32_t i = 0; i < n && i < cap; i++) ms[i] = ctx->last_ms[i];
     *count = n;
     return CORRO_OK;

@@ -57,8 +57,28 @@ struct XIndex {
     uint64_t *gts;      // MAX(ts) per group
 };
 
-// max db_version and max seq over the state's clock rows
-__global__ void k_xmax(const Rec *st, const uint64_t *off, const uint32_t *cnt, unsigned long long *mx) {
+// max db_version and max seq over the state's clock rows: per-bucket maxima (no contended
+// atomics: one word per block), then one block folds them
+__device__ inline void block_max2(uint64_t &a, uint64_t &b) {
+    __shared__ uint64_t sa[16], sb[16];
+    for (int d = 32; d >= 1; d >>= 1) {
+        a = max(a, (uint64_t)__shfl_xor(a, d));
+        b = max(b, (uint64_t)__shfl_xor(b, d));
+    }
+    const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sa[w] = a;
+        sb[w] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (uint32_t k = 1; k < nw; k++) {
+            a = max(a, sa[k]);
+            b = max(b, sb[k]);
+        }
+}
+
+__global__ void k_xmax(const Rec *st, const uint64_t *off, const uint32_t *cnt, uint64_t *part) {
     const uint32_t b = blockIdx.x;
     const uint32_t n = cnt[b];
     uint64_t md = 0, ms = 0;
@@ -67,13 +87,23 @@ __global__ void k_xmax(const Rec *st, const uint64_t *off, const uint32_t *cnt, 
         md = max(md, (uint64_t)r.dbv);
         ms = max(ms, (uint64_t)r.seq);
     }
-    for (int d = 32; d >= 1; d >>= 1) {
-        md = max(md, (uint64_t)__shfl_xor(md, d));
-        ms = max(ms, (uint64_t)__shfl_xor(ms, d));
+    block_max2(md, ms);
+    if (threadIdx.x == 0) {
+        part[2 * b] = md;
+        part[2 * b + 1] = ms;
     }
-    if ((threadIdx.x & 63) == 0 && n) {
-        atomicMax(&mx[0], (unsigned long long)md);
-        atomicMax(&mx[1], (unsigned long long)ms);
+}
+
+__global__ void k_xmax_fold(const uint64_t *part, uint32_t B, uint64_t *mx) {
+    uint64_t md = 0, ms = 0;
+    for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) {
+        md = max(md, part[2 * b]);
+        ms = max(ms, part[2 * b + 1]);
+    }
+    block_max2(md, ms);
+    if (threadIdx.x == 0) {
+        mx[0] = md;
+        mx[1] = ms;
     }
 }
 
@@ -141,6 +171,23 @@ __global__ void k_xgmeta(XIndex x, const uint64_t *st_ts, uint32_t G) {
     if (st_ts)
         for (uint32_t i = a; i < b; i++) t = max(t, st_ts[x.ref[i]]);
     x.gts[g] = t;
+}
+
+// clustered copy of the clock rows in index order (and their ts): extraction then reads each
+// group's rows as one contiguous run instead of one random 64-B line per row
+__global__ void k_xcluster(const Rec *st, const uint64_t *st_ts, const uint32_t *ref, uint64_t m, Rec *crec,
+                           uint64_t *cts) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t g = ref[i];
+    const Rec r = x_load(st + g);
+    uint4 *o = reinterpret_cast<uint4 *>(crec + i);
+    const uint4 *q = reinterpret_cast<const uint4 *>(&r);
+    o[0] = q[0];
+    o[1] = q[1];
+    o[2] = q[2];
+    o[3] = q[3];
+    if (cts) cts[i] = st_ts ? st_ts[g] : 0ULL;
 }
 
 // ---- extraction ----------------------------------------------------------------------------
@@ -218,7 +265,7 @@ struct XOut {
     const uint64_t *grp_off, *row_off;
     int64_t *version;
     uint64_t *last_seq, *ts, *grp_row_off, *grp_rows;
-    uint32_t *grp_src;   // scratch: first sorted index of the group's (filtered) rows
+    uint32_t *out_src;   // scratch: index-order position of every output row
     corro_rows rows;
 };
 
@@ -248,35 +295,32 @@ __global__ void k_xfill(XIndex x, XParams p, XNeeds nd, XOut o) {
         o.ts[k] = x.gts[g];
         o.grp_row_off[k] = cur;
         o.grp_rows[k] = b - a;
-        o.grp_src[k] = a;
+        for (uint32_t i = a; i < b; i++) o.out_src[cur + (i - a)] = i;
         cur += b - a;
         k++;
     }
 }
 
-// one wave per output group: rows gathered from the state, seq ascending
-__global__ void k_xgather(XIndex x, const Rec *st, const uint64_t *st_ts, XOut o, uint64_t G) {
-    const uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (k >= G) return;
-    const uint64_t n = o.grp_rows[k], src = o.grp_src[k], dst = o.grp_row_off[k];
-    for (uint64_t j = threadIdx.x & 63; j < n; j += 64) {
-        const uint32_t g = x.ref[src + j];
-        const Rec r = x_load(st + g);
-        const uint64_t q = dst + j;
-        const corro_rows &w = o.rows;
-        if (w.pk) w.pk[q] = r.pk;
-        if (w.table_cid) w.table_cid[q] = r.tcid;
-        if (w.col_version) w.col_version[q] = r.cv;
-        if (w.db_version) w.db_version[q] = r.dbv;
-        if (w.cl) w.cl[q] = (int64_t)r.cl;
-        if (w.seq) w.seq[q] = r.seq;
-        if (w.site) w.site[q] = r.site;
-        if (w.ts) w.ts[q] = st_ts ? st_ts[g] : 0ULL;
-        if (w.val0) w.val0[q] = r.v0;
-        if (w.val1) w.val1[q] = r.v1;
-        if (w.val_type) w.val_type[q] = (uint8_t)(r.meta & 0xFFu);
-        if (w.val_len) w.val_len[q] = (uint8_t)((r.meta >> 8) & 0xFFu);
-    }
+// one thread per output row: rows copied from the index's clustered copy (runs of a group are
+// contiguous there), into crsql_changes form
+__global__ void k_xgather(const Rec *crec, const uint64_t *cts, XOut o, uint64_t R) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= R) return;
+    const uint32_t i = o.out_src[q];
+    const Rec r = x_load(crec + i);
+    const corro_rows &w = o.rows;
+    if (w.pk) w.pk[q] = r.pk;
+    if (w.table_cid) w.table_cid[q] = r.tcid;
+    if (w.col_version) w.col_version[q] = r.cv;
+    if (w.db_version) w.db_version[q] = r.dbv;
+    if (w.cl) w.cl[q] = (int64_t)r.cl;
+    if (w.seq) w.seq[q] = r.seq;
+    if (w.site) w.site[q] = r.site;
+    if (w.ts) w.ts[q] = cts ? cts[i] : 0ULL;
+    if (w.val0) w.val0[q] = r.v0;
+    if (w.val1) w.val1[q] = r.v1;
+    if (w.val_type) w.val_type[q] = (uint8_t)(r.meta & 0xFFu);
+    if (w.val_len) w.val_len[q] = (uint8_t)((r.meta >> 8) & 0xFFu);
 }
 
 uint32_t bits_for(uint64_t v) {
@@ -294,6 +338,7 @@ int ensure_index(corro_ctx *ctx, XIndex &x, XParams &p) {
     if (m >= (1ULL << 32)) return fail(CORRO_E_RANGE, "extraction index holds at most 2^32-1 clock rows");
     const uint32_t B = ctx->B;
     if (ctx->xidx_epoch != ctx->state_epoch) {
+        if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[2], s));
         const Rec *st = ctx->d_state[ctx->cur].as<Rec>();
         const uint64_t *off = ctx->d_state_off.as<uint64_t>();
         const uint32_t *cnt = ctx->d_state_cnt.as<uint32_t>();
@@ -304,8 +349,9 @@ int ensure_index(corro_ctx *ctx, XIndex &x, XParams &p) {
                 return rc;
             if (int rc = prim_inclusive_scan_u32(nullptr, &scan_tmp, nullptr, nullptr, (uint32_t)m, s)) return rc;
         }
-        const size_t idx_bytes = al(m * 8) + 5 * al(m * 4 + 4) + al(m * 8 + 8);
-        const size_t scr_bytes = 2 * al(m * 8) + al(m * 4) + al(B * 8ULL) + 256 + al(std::max(sort_tmp, scan_tmp) + 256);
+        const size_t idx_bytes = al(m * 8) + 5 * al(m * 4 + 4) + al(m * 8 + 8) + al(m * 64) + al(m * 8);
+        const size_t scr_bytes = 2 * al(m * 8) + al(m * 4) + al(B * 8ULL) + al(B * 16ULL) + 256 +
+                                 al(std::max(sort_tmp, scan_tmp) + 256);
         if (int rc = ctx->d_xidx.ensure(idx_bytes + scr_bytes)) return rc;
         uint8_t *q = ctx->d_xidx.as<uint8_t>();
         auto carve = [&](size_t bytes) {
@@ -320,10 +366,13 @@ int ensure_index(corro_ctx *ctx, XIndex &x, XParams &p) {
         ctx->x.gstart = (uint32_t *)carve(m * 4 + 4);
         ctx->x.glast = (uint32_t *)carve(m * 4 + 4);
         ctx->x.gts = (uint64_t *)carve(m * 8 + 8);
+        ctx->x.crec = (Rec *)carve(m * 64);
+        ctx->x.cts = (uint64_t *)carve(m * 8);
         uint64_t *kin = (uint64_t *)carve(m * 8), *kout = (uint64_t *)carve(m * 8);
         uint32_t *rin = (uint32_t *)carve(m * 4);
         uint64_t *d_dense = (uint64_t *)carve(B * 8ULL);
-        unsigned long long *mx = (unsigned long long *)carve(256);
+        uint64_t *part = (uint64_t *)carve(B * 16ULL);
+        uint64_t *mx = (uint64_t *)carve(256);
         void *tmp = carve(std::max(sort_tmp, scan_tmp) + 256);
         XIndex X{ctx->x.hkey, ctx->x.seq, ctx->x.ref, ctx->x.gid, ctx->x.gstart, ctx->x.glast, ctx->x.gts};
         uint64_t hm[2] = {0, 0};
@@ -340,8 +389,8 @@ int ensure_index(corro_ctx *ctx, XIndex &x, XParams &p) {
             }
             if (run != m) return fail(CORRO_E_DEVICE, "internal: state count mismatch");
             CORRO_HIP_TRY(hipMemcpyAsync(d_dense, dense.data(), B * 8ULL, hipMemcpyHostToDevice, s));
-            CORRO_HIP_TRY(hipMemsetAsync(mx, 0, 16, s));
-            hipLaunchKernelGGL(k_xmax, dim3(B), dim3(256), 0, s, st, off, cnt, mx);
+            hipLaunchKernelGGL(k_xmax, dim3(B), dim3(256), 0, s, st, off, cnt, part);
+            hipLaunchKernelGGL(k_xmax_fold, dim3(1), dim3(1024), 0, s, part, B, mx);
             CORRO_HIP_TRY(hipMemcpyAsync(hm, mx, 16, hipMemcpyDeviceToHost, s));
             CORRO_HIP_TRY(hipStreamSynchronize(s));
             db = bits_for(hm[0]);
@@ -369,7 +418,14 @@ int ensure_index(corro_ctx *ctx, XIndex &x, XParams &p) {
             G += 1;
             const uint64_t *sts = ctx->track_ts ? ctx->d_state_ts[ctx->cur].as<uint64_t>() : nullptr;
             hipLaunchKernelGGL(k_xgmeta, dim3((G + 255) / 256), dim3(256), 0, s, X, sts, G);
+            hipLaunchKernelGGL(k_xcluster, dim3(mb), dim3(256), 0, s, st, sts, X.ref, m, ctx->x.crec,
+                               sts ? ctx->x.cts : nullptr);
             CORRO_HIP_TRY(hipGetLastError());
+        }
+        if (ctx->profiling) {
+            CORRO_HIP_TRY(hipEventRecord(ctx->ev[3], s));
+            CORRO_HIP_TRY(hipEventSynchronize(ctx->ev[3]));
+            CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[8], ctx->ev[2], ctx->ev[3]));
         }
         ctx->x_db = db;
         ctx->x_max_dbv = hm[0];
@@ -414,13 +470,13 @@ extern "C" int corro_extract_changes(corro_ctx *ctx, const corro_extract_in *in,
             CORRO_HIP_TRY(hipMemcpy(&R, out->row_off + n, 8, hipMemcpyDeviceToHost));
         }
     }
-    // device scratch: staged needs (host mode), outputs (host mode), grp_src
+    // device scratch: staged needs (host mode), outputs (host mode), out_src
     const bool has_seq = in->seq_start != nullptr;
     size_t need_bytes = mem == CORRO_MEM_HOST ? al(n * 4) + 2 * al(n * 8) + (has_seq ? 2 * al(n * 4) : 0) : 0;
     size_t out_bytes = 0;
     if (mem == CORRO_MEM_HOST)
         out_bytes = pass == 0 ? 2 * al(n * 8) : 2 * al((n + 1) * 8) + 5 * al(G * 8) + al(R * 8) * 7 + al(R * 4) * 3 + al(R) * 2;
-    const size_t src_bytes = pass == 1 ? al(G * 4 + 4) : 0;
+    const size_t src_bytes = pass == 1 ? al(R * 4 + 4) : 0;
     if (int rc = ctx->d_xout.ensure(need_bytes + out_bytes + src_bytes + 1024)) return rc;
     uint8_t *q = ctx->d_xout.as<uint8_t>();
     auto carve = [&](size_t bytes) {
@@ -462,7 +518,7 @@ extern "C" int corro_extract_changes(corro_ctx *ctx, const corro_extract_in *in,
         }
     } else {
         XOut o{};
-        o.grp_src = (uint32_t *)carve(G * 4 + 4);
+        o.out_src = (uint32_t *)carve(R * 4 + 4);
         if (mem == CORRO_MEM_DEVICE) {
             o.grp_off = out->grp_off;
             o.row_off = out->row_off;
@@ -499,11 +555,9 @@ extern "C" int corro_extract_changes(corro_ctx *ctx, const corro_extract_in *in,
             w.val_len = h.val_len ? (uint8_t *)carve(R) : nullptr;
         }
         hipLaunchKernelGGL(k_xfill, dim3(nb), dim3(256), 0, s, x, p, nd, o);
-        if (G) {
-            const uint64_t *sts = ctx->track_ts ? ctx->d_state_ts[ctx->cur].as<uint64_t>() : nullptr;
-            hipLaunchKernelGGL(k_xgather, dim3((uint32_t)((G + 3) / 4)), dim3(256), 0, s, x,
-                               ctx->d_state[ctx->cur].as<Rec>(), sts, o, G);
-        }
+        if (R)
+            hipLaunchKernelGGL(k_xgather, dim3((uint32_t)((R + 255) / 256)), dim3(256), 0, s, ctx->x.crec,
+                               ctx->track_ts ? ctx->x.cts : nullptr, o, R);
         if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
         CORRO_HIP_TRY(hipGetLastError());
         if (mem == CORRO_MEM_HOST) {

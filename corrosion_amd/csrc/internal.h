@@ -57,6 +57,8 @@ struct XIdxPtrs {
     uint64_t *hkey = nullptr;
     uint32_t *seq = nullptr, *ref = nullptr, *gid = nullptr, *gstart = nullptr, *glast = nullptr;
     uint64_t *gts = nullptr;
+    Rec *crec = nullptr;         // clock rows in index order (clustered copy)
+    uint64_t *cts = nullptr;     // their ts (when the state tracks ts)
 };
 
 struct Table {
@@ -120,5 +122,5 @@ struct corro_ctx {
     // stage timing
     bool profiling = false;
     hipEvent_t ev[8] = {};
-    float last_ms[8] = {};        // apply stages [0..5], k_needs count [6], k_needs fill [7]
+    float last_ms[9] = {};        // apply stages [0..5], k_needs / extract count [6], fill [7], extract index build [8]
 };

@@ -149,13 +149,14 @@ class MergeEngine:
 
     def last_timings(self, apply_only=True):
         """ms per stage of the last apply: hist, colscan, plan, scatter, merge (fast + general
-        kernels), overflow; with apply_only=False also the last sync-need count/fill kernels."""
-        arr = (C.c_float * 8)()
+        kernels), overflow; with apply_only=False also the last sync-need / extraction count and fill
+        kernels and the last extraction index build."""
+        arr = (C.c_float * 9)()
         n = C.c_uint32()
-        L.check(L.lib().corro_last_timings(self._h, arr, 8, C.byref(n)))
+        L.check(L.lib().corro_last_timings(self._h, arr, 9, C.byref(n)))
         names = ["k_hist", "k_colscan", "k_plan", "k_scatter", "k_merge", "k_merge_ovf"]
         if not apply_only:
-            names += ["k_needs_count", "k_needs_fill"]
+            names += ["k_needs_count", "k_needs_fill", "extract_index"]
         return {names[i]: arr[i] for i in range(min(n.value, len(names)))}
 
     # ---- multi-GPU ingest -----------------------------------------------------------------

@@ -157,7 +157,8 @@ int corro_db_versions(corro_ctx *ctx, int64_t *out, uint32_t nsites);
 
 /* Stage timing with HIP events recorded on the engine's stream (for roofline reporting).
  * corro_last_timings returns milliseconds of the last apply per stage:
- * [0] k_hist [1] k_colscan [2] k_plan [3] k_scatter [4] k_merge [5] k_merge_ovf (0 if not run). */
+ * [0] k_hist [1] k_colscan [2] k_plan [3] k_scatter [4] k_merge [5] k_merge_ovf (0 if not run),
+ * [6] / [7] the last need-diff or extraction count / fill pass, [8] the last extraction index build. */
 int corro_ctx_set_profiling(corro_ctx *ctx, int on);
 int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count);
 
