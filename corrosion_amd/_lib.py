@@ -16,6 +16,7 @@ ERRORS = {-1: "CORRO_E_INVALID", -2: "CORRO_E_NOMEM", -3: "CORRO_E_DEVICE",
           -4: "CORRO_E_UNKNOWN_TABLE", -5: "CORRO_E_UNKNOWN_COLUMN", -6: "CORRO_E_RANGE",
           -7: "CORRO_E_NO_DEVICE"}
 CORRO_MEM_HOST, CORRO_MEM_DEVICE = 0, 1
+CORRO_PAYLOAD_SYNC, CORRO_PAYLOAD_UNI = 0, 1
 
 # every symbol include/corro_hip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -31,6 +32,7 @@ EXPORTS = [
     "corro_generate_sync", "corro_partition_ranks", "corro_scan_offsets",
     "corro_compute_needs_onepass", "corro_needs_bound", "corro_extract_changes",
     "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
+    "corro_decode_frames", "corro_site_ids",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -90,6 +92,12 @@ class Changeset(C.Structure):
                 ("version_start", C.c_uint64), ("version_end", C.c_uint64), ("seq_start", C.c_uint64),
                 ("seq_end", C.c_uint64), ("last_seq", C.c_uint64), ("ts", C.c_uint64),
                 ("change_off", C.c_uint64), ("change_count", C.c_uint64)]
+
+
+class Decoded(C.Structure):
+    _fields_ = [("nframes", C.c_uint64), ("nchanges", C.c_uint64), ("nsets", C.c_uint64), ("cs", C.c_void_p),
+                ("actor_ids", C.c_void_p), ("status", C.c_void_p), ("changes", Changes), ("set_start", C.c_void_p),
+                ("set_end", C.c_void_p)]
 
 
 class ProcessOut(C.Structure):
@@ -154,6 +162,8 @@ def lib():
         "corro_compute_needs_onepass": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsOut), u64, u64, vp]),
         "corro_needs_bound": (i32, [vp, C.POINTER(SyncEntries), i32, vp, vp]),
         "corro_bookie_seq_bookkeeping": (i32, [vp, vp, u64, vp, vp, u64, vp, vp, vp]),
+        "corro_site_ids": (i32, [vp, vp, u32, vp]),
+        "corro_decode_frames": (i32, [vp, C.c_char_p, u64, i32, i32, C.POINTER(Decoded), i32]),
         "corro_bookie_buffered_versions": (i32, [vp, vp, u64, u64, vp, u64, vp]),
         "corro_bookie_buffered": (i32, [vp, vp, u64, u64, u64, C.POINTER(Rows), u64, vp]),
         "corro_extract_changes": (i32, [vp, C.POINTER(ExtractIn), i32, C.POINTER(ExtractOut), i32]),

@@ -217,6 +217,37 @@ class Agent:
         res.ready = self.take_ready()
         return res
 
+    def process_frames(self, buf, payload=0):
+        """Wire bytes -> merge: decode length-delimited changeset frames on the GPU
+        (corro_decode_frames) and feed the decoded batch to process_multiple_changes as it is.
+        Frames with a non-zero decode status are not applied. Returns (Processed over the applied
+        frames, per-frame decode status)."""
+        dec = self.engine.decode_frames(buf, payload)
+        keep = [i for i in range(dec["nframes"]) if dec["status"][i] == 0]
+        descs = (L.Changeset * max(1, len(keep)))()
+        for j, i in enumerate(keep):
+            C.memmove(C.byref(descs[j]), C.byref(dec["cs"][i]), C.sizeof(L.Changeset))
+            if descs[j].kind == L.CORRO_CS_EMPTY_SET:
+                descs[j].change_off = descs[j].change_count = 0
+        self.site_ids = dict(enumerate(self.engine.site_ids()))   # the decoder may have registered sites
+        ch = dec["changes"]
+        n = len(ch["pk"])
+        s = L.Changes()
+        s.n = n
+        for k, a in ch.items():
+            setattr(s, k, a.ctypes.data if n else None)
+        known = np.zeros(max(1, len(keep)), np.int32)
+        imp = np.zeros(max(1, n), np.uint8)
+        out = L.ProcessOut()
+        out.known = known.ctypes.data
+        out.impactful = imp.ctypes.data
+        L.check(L.lib().corro_process_multiple_changes(self.engine._h, self.bookie._h, descs, len(keep), C.byref(s),
+                                                       C.byref(out)))
+        res = Processed(known=[L.KNOWN.get(int(k), int(k)) for k in known[:len(keep)]])
+        res.impact = imp[:n]
+        res.ready = self.take_ready()
+        return res, dec["status"]
+
     def take_ready(self):
         c = C.c_uint64()
         L.check(L.lib().corro_bookie_take_ready(self.bookie._h, None, None, 0, C.byref(c)))

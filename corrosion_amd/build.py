@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcorro_hip.so")
-SOURCES = ["engine.hip", "sync_needs.hip", "partition.hip", "prims.hip", "extract.hip", "booked.cpp", "agent.cpp"]
+SOURCES = ["engine.hip", "sync_needs.hip", "partition.hip", "prims.hip", "extract.hip", "wire.hip", "booked.cpp", "agent.cpp"]
 HEADERS = ["internal.h", "merge_kernels.h", "ovf_kernels.h", "ranges.h", "booked.h", "rowhash.h"]
 ARCH = "gfx950"
 

@@ -305,7 +305,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_state_flags, &ctx->d_out_off, &ctx->d_out_cnt, &ctx->d_out_flags, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
                       &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export,
-                      &ctx->d_needs, &ctx->d_needs1, &ctx->d_xidx, &ctx->d_xout, &ctx->d_ncols, &ctx->d_part};
+                      &ctx->d_needs, &ctx->d_needs1, &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites, &ctx->d_ncols, &ctx->d_part};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     for (auto &e : ctx->ev)
@@ -378,6 +378,14 @@ int corro_site_register(corro_ctx *ctx, const uint8_t *site_ids, uint64_t n, uin
         if (ordinals) ordinals[i] = ord;
     }
     if (added) return upload_site_tables(ctx);
+    return CORRO_OK;
+}
+
+int corro_site_ids(corro_ctx *ctx, uint8_t *ids, uint32_t cap, uint32_t *count) {
+    if (!ctx || !count || (cap && !ids)) return fail(CORRO_E_INVALID, "NULL argument");
+    const uint32_t n = (uint32_t)ctx->sites.size();
+    for (uint32_t i = 0; i < n && i < cap; i++) std::memcpy(ids + 16ULL * i, ctx->sites[i].data(), 16);
+    *count = n;
     return CORRO_OK;
 }
 

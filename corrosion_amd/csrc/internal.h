@@ -116,6 +116,15 @@ struct corro_ctx {
     uint64_t xidx_epoch = ~0ULL;  // epoch the extraction index was built for
     uint32_t x_db = 1, x_groups = 0;
     uint64_t x_max_dbv = 0;
+    corro::DevBuf d_wire;         // wire decode: frame bytes, headers, staged outputs
+    corro::DevBuf d_wire_schema;  // wire decode: table / column names
+    corro::DevBuf d_wire_sites;   // wire decode: hash of the registered site ids
+    bool wire_schema_ready = false;
+    const uint8_t *wire_names = nullptr;
+    const uint32_t *wire_toff = nullptr, *wire_tlen = nullptr, *wire_tbase = nullptr, *wire_tn = nullptr,
+                   *wire_coff = nullptr, *wire_clen = nullptr;
+    size_t wire_sites_n = 0;
+    uint32_t wire_hmask = 0;
     corro::DevBuf d_ncols;        // u16 column count per table
     corro::DevBuf d_part;         // partition counts
     uint64_t *h_misc = nullptr;   // pinned

@@ -1,0 +1,633 @@
+// Wire decode: length-delimited frames of speedy-encoded changesets ->
+// the SoA batch + changeset headers that corro_process_multiple_changes / corro_apply_batch take.
+//
+// Reference: frames are tokio LengthDelimitedCodec (u32 big-endian length + payload,
+// corro-agent/src/api/peer/mod.rs:917-929, corro-types/src/sync.rs:366-376); payloads are
+// SyncMessage::V1(SyncMessageV1::Changeset(ChangeV1)) (sync.rs:19-30) or
+// UniPayload::V1 { Broadcast(BroadcastV1::Change(ChangeV1)), cluster_id } (broadcast.rs:41-52,
+// 93-96), read with speedy's derived layout (u32 enum tags, u32 length prefixes, little endian;
+// corrosion_amd/wire.py restates it); ChangeV1 / Changeset / Change: broadcast.rs:114-148,
+// change.rs:19-30; SqliteValue's own encoding: corro-api-types/src/lib.rs:615-680; packed pks:
+// unpack_columns (corro-types/src/pubsub.rs:2396-2451).
+//
+// Kernels:
+//   k_wire_hdr     one lane per frame: message tags, actor, changeset variant and its fixed
+//                  header (Full: version + change count; Empty: versions + optional ts; EmptySet:
+//                  ranges + ts)
+//   k_wire_decode  one 64-lane workgroup per Full frame: the frame is staged into LDS with
+//                  coalesced loads, lane 0 walks the variable-length changes once to record each
+//                  change's offset (and reads the trailing seqs / last_seq / ts), then all lanes
+//                  decode changes in parallel: table / column names matched against the schema,
+//                  pk unpacked, value to the engine's fixed-width encoding, site id to its ordinal
+//                  through a device hash of the registered sites.
+// Unknown site ids are collected; the host registers them (corro_site_register) and re-runs the
+// decode, so ordinals match the engine's site table. Unknown table / column names give
+// table_cid = CORRO_TCID_UNKNOWN (the host rolls that version back, as the failing INSERT's
+// SAVEPOINT does, util.rs:839-860).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace corro {
+namespace {
+
+constexpr uint32_t WIRE_LDS = 16384;      // frame bytes staged per workgroup
+constexpr uint32_t WIRE_OFFS = 1024;      // change offsets kept in LDS
+constexpr int32_t ST_NOT_CHANGESET = 1;   // a frame that is not a changeset message (skipped)
+
+__device__ inline uint64_t wmix(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33; return x;
+}
+
+struct WireDev {
+    const uint8_t *buf;
+    const uint64_t *foff;     // frame payload offsets
+    const uint32_t *flen;     // frame payload lengths
+    uint32_t nframes, kind;   // kind: 0 sync message, 1 uni payload
+    // per frame header (out)
+    int32_t *status;
+    uint32_t *cs_kind, *nchg, *nset, *chg_start, *site;
+    uint64_t *v0, *v1, *s0, *s1, *last, *ts;
+    uint8_t *actor;           // 16 per frame
+    const uint64_t *chg_off, *set_off;   // pass 1 inputs
+    uint64_t *set_start, *set_end;
+    // schema
+    const uint8_t *names;
+    const uint32_t *tname_off, *tname_len, *tcol_base, *tncols, *cname_off, *cname_len;
+    uint32_t ntables;
+    // sites
+    const uint64_t *hlo, *hhi;
+    const uint32_t *hord;
+    uint32_t hmask;
+    uint8_t *unknown;         // 16 per unknown site slot
+    unsigned long long *nunknown;
+    uint32_t unknown_cap;
+    // outputs (SoA)
+    corro_changes out;
+    uint32_t *chg_rel;        // scratch: per change offset within its frame (frames with > WIRE_OFFS changes)
+};
+
+// little-endian / big-endian readers over any byte pointer, bounds-checked against end
+struct Rd {
+    const uint8_t *p;
+    uint32_t pos, end;
+    bool bad;
+    __device__ inline bool need(uint32_t n) {
+        if (pos + n > end || pos + n < pos) bad = true;
+        return !bad;
+    }
+    __device__ inline uint64_t le(uint32_t n) {
+        if (!need(n)) return 0;
+        uint64_t v = 0;
+        for (uint32_t i = 0; i < n; i++) v |= (uint64_t)p[pos + i] << (8 * i);
+        pos += n;
+        return v;
+    }
+    __device__ inline uint32_t u32() { return (uint32_t)le(4); }
+    __device__ inline uint64_t u64() { return le(8); }
+};
+
+__device__ inline uint32_t site_lookup(const WireDev &d, uint64_t lo, uint64_t hi) {
+    if (d.hmask == 0) return 0xFFFFFFFFu;
+    uint32_t h = (uint32_t)wmix(lo ^ (hi * 0x9E3779B97F4A7C15ULL)) & d.hmask;
+    while (true) {
+        const uint32_t o = d.hord[h];
+        if (o == 0xFFFFFFFFu) return o;
+        if (d.hlo[h] == lo && d.hhi[h] == hi) return o;
+        h = (h + 1) & d.hmask;
+    }
+}
+
+__device__ inline void note_unknown(const WireDev &d, uint64_t lo, uint64_t hi) {
+    const unsigned long long k = atomicAdd(d.nunknown, 1ULL);
+    if (k < d.unknown_cap) {
+        uint64_t *u = reinterpret_cast<uint64_t *>(d.unknown + 16 * k);
+        u[0] = lo;
+        u[1] = hi;
+    }
+}
+
+__global__ void k_wire_hdr(WireDev d) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= d.nframes) return;
+    Rd r{d.buf + d.foff[f], 0, d.flen[f], false};
+    int32_t st = 0;
+    uint32_t kind = 0, nchg = 0, nset = 0, cstart = 0;
+    uint64_t v0 = 0, v1 = 0, ts = 0;
+    if (d.kind == 0) {
+        if (r.u32() != 0 || r.u32() != 1) st = ST_NOT_CHANGESET;   // SyncMessage::V1, ::Changeset
+    } else {
+        if (r.u32() != 0 || r.u32() != 0 || r.u32() != 0) st = ST_NOT_CHANGESET;  // UniPayload::V1/Broadcast/Change
+    }
+    uint64_t alo = 0, ahi = 0;
+    if (!st) {
+        alo = r.u64();
+        ahi = r.u64();
+        kind = r.u32();
+        if (kind == 0) {            // Empty { versions, ts: Option<Timestamp> (default_on_eof) }
+            v0 = r.u64();
+            v1 = r.u64();
+            if (!r.bad && r.pos < r.end) {
+                const uint32_t some = (uint32_t)r.le(1);
+                if (some == 1) ts = r.u64();
+                else if (some != 0) st = CORRO_E_INVALID;
+            }
+        } else if (kind == 1) {     // Full { version, changes, ... } (the rest follows the changes)
+            v0 = v1 = r.u64();
+            nchg = r.u32();
+            cstart = r.pos;
+        } else if (kind == 2) {     // EmptySet { versions: Vec<RangeInclusive>, ts }
+            nset = r.u32();
+            const uint64_t body = (uint64_t)nset * 16;
+            if (!r.need(body > 0xFFFFFFFFULL ? 0xFFFFFFFFu : (uint32_t)body)) nset = 0;
+            else r.pos += (uint32_t)body;
+            ts = r.u64();
+        } else {
+            st = CORRO_E_INVALID;
+        }
+        if (r.bad) st = CORRO_E_INVALID;
+    }
+    d.status[f] = st;
+    d.cs_kind[f] = kind;
+    d.nchg[f] = st ? 0 : nchg;
+    d.nset[f] = st ? 0 : nset;
+    d.chg_start[f] = cstart;
+    d.v0[f] = v0;
+    d.v1[f] = v1;
+    d.ts[f] = ts;
+    d.s0[f] = d.s1[f] = d.last[f] = 0;
+    uint64_t *a = reinterpret_cast<uint64_t *>(d.actor + 16 * (uint64_t)f);
+    a[0] = alo;
+    a[1] = ahi;
+    uint32_t so = 0xFFFFFFFFu;
+    if (!st) {
+        so = site_lookup(d, alo, ahi);
+        if (so == 0xFFFFFFFFu) note_unknown(d, alo, ahi);
+    }
+    d.site[f] = so;
+}
+
+// EmptySet ranges (pass 1)
+__global__ void k_wire_sets(WireDev d) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= d.nframes || d.status[f] || d.cs_kind[f] != 2) return;
+    Rd r{d.buf + d.foff[f], 0, d.flen[f], false};
+    r.pos = (d.kind == 0 ? 8 : 12) + 16 + 4 + 4;
+    const uint64_t o = d.set_off[f];
+    for (uint32_t k = 0; k < d.nset[f]; k++) {
+        d.set_start[o + k] = r.u64();
+        d.set_end[o + k] = r.u64();
+    }
+}
+
+__device__ inline bool name_eq(const uint8_t *a, uint32_t alen, const uint8_t *b, uint32_t blen) {
+    if (alen != blen) return false;
+    for (uint32_t i = 0; i < alen; i++)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+__global__ void __launch_bounds__(64) k_wire_decode(WireDev d) {
+    __shared__ uint8_t s_buf[WIRE_LDS];
+    __shared__ uint32_t s_off[WIRE_OFFS];
+    __shared__ int32_t s_bad;
+    const uint32_t f = blockIdx.x;
+    if (d.status[f] || d.cs_kind[f] != 1) return;   // uniform per workgroup
+    const uint32_t len = d.flen[f], n = d.nchg[f];
+    const uint8_t *g = d.buf + d.foff[f];
+    const bool lds = len <= WIRE_LDS;
+    if (lds) {
+        // coalesced staging: 8-byte words where aligned, bytes at the ragged ends
+        const uintptr_t base = reinterpret_cast<uintptr_t>(g);
+        const uint32_t head = (uint32_t)std::min<uintptr_t>((8 - (base & 7)) & 7, len);
+        for (uint32_t i = threadIdx.x; i < head; i += 64) s_buf[i] = g[i];
+        const uint32_t nw = (len - head) / 8;
+        const uint64_t *gw = reinterpret_cast<const uint64_t *>(g + head);
+        for (uint32_t w = threadIdx.x; w < nw; w += 64) {
+            const uint64_t x = gw[w];
+            for (int b = 0; b < 8; b++) s_buf[head + 8 * w + b] = (uint8_t)(x >> (8 * b));
+        }
+        for (uint32_t i = head + 8 * nw + threadIdx.x; i < len; i += 64) s_buf[i] = g[i];
+    }
+    __syncthreads();
+    const uint8_t *p = lds ? s_buf : g;
+    const bool off_lds = n <= WIRE_OFFS;
+    const uint64_t co = d.chg_off[f];
+    if (threadIdx.x == 0) {
+        // the walk: offsets of the variable-length changes, then the Full tail
+        Rd r{p, d.chg_start[f], len, false};
+        for (uint32_t k = 0; k < n && !r.bad; k++) {
+            if (off_lds) s_off[k] = r.pos;
+            else d.chg_rel[co + k] = r.pos;
+            for (int s = 0; s < 2; s++) {        // table, pk
+                const uint32_t l = r.u32();
+                if (r.need(l)) r.pos += l;
+            }
+            const uint32_t lc = r.u32();         // cid
+            if (r.need(lc)) r.pos += lc;
+            const uint32_t tag = (uint32_t)r.le(1);
+            if (tag == 1 || tag == 2) r.pos += 8;
+            else if (tag == 3 || tag == 4) {
+                const uint32_t l = r.u32();
+                if (r.need(l)) r.pos += l;
+            } else if (tag != 0) r.bad = true;
+            r.need(48);                          // col_version, db_version, seq, site_id, cl
+            r.pos += 48;
+        }
+        d.s0[f] = r.u64();
+        d.s1[f] = r.u64();
+        d.last[f] = r.u64();
+        d.ts[f] = r.u64();
+        s_bad = r.bad ? 1 : 0;
+        if (!off_lds) __threadfence_block();
+    }
+    __syncthreads();
+    if (s_bad) {
+        if (threadIdx.x == 0) d.status[f] = CORRO_E_INVALID;
+        return;
+    }
+    const uint64_t ts = d.ts[f];
+    int32_t err = 0;
+    for (uint32_t k = threadIdx.x; k < n; k += 64) {
+        Rd r{p, off_lds ? s_off[k] : d.chg_rel[co + k], len, false};
+        const uint32_t lt = r.u32();
+        const uint32_t pt = r.pos;
+        r.pos += lt;
+        const uint32_t lp = r.u32();
+        const uint32_t pp = r.pos;
+        r.pos += lp;
+        const uint32_t lc = r.u32();
+        const uint32_t pc = r.pos;
+        r.pos += lc;
+        // table / column names
+        uint32_t tcid = CORRO_TCID_UNKNOWN;
+        for (uint32_t t = 0; t < d.ntables; t++) {
+            if (!name_eq(p + pt, lt, d.names + d.tname_off[t], d.tname_len[t])) continue;
+            if (lc == 2 && p[pc] == '-' && p[pc + 1] == '1') {
+                tcid = t << 16;
+            } else {
+                for (uint32_t c = 0; c < d.tncols[t]; c++) {
+                    const uint32_t ci = d.tcol_base[t] + c;
+                    if (name_eq(p + pc, lc, d.names + d.cname_off[ci], d.cname_len[ci])) {
+                        tcid = (t << 16) | (c + 1);
+                        break;
+                    }
+                }
+            }
+            break;
+        }
+        // pk: one packed INTEGER column (unpack_columns: get_int sign-extends big-endian bytes)
+        uint64_t pk = 0;
+        if (lp < 2 || p[pp] != 1 || (p[pp + 1] & 7) != 1 || (uint32_t)(p[pp + 1] >> 3) + 2 != lp ||
+            (p[pp + 1] >> 3) > 8) {
+            err = CORRO_E_RANGE;
+        } else {
+            const uint32_t nb = p[pp + 1] >> 3;
+            for (uint32_t i = 0; i < nb; i++) pk = (pk << 8) | p[pp + 2 + i];
+            if (nb && nb < 8 && (pk >> (8 * nb - 1)) & 1) pk |= ~0ULL << (8 * nb);
+        }
+        // value -> (type, val0, val1, len)
+        const uint32_t tag = (uint32_t)r.le(1);
+        uint32_t vt = CORRO_NULL, vl = 0;
+        uint64_t w0 = 0, w1 = 0;
+        if (tag == 1) {
+            vt = CORRO_INTEGER;
+            w0 = r.u64();
+        } else if (tag == 2) {
+            w0 = r.u64();
+            const bool nan = ((w0 >> 52) & 0x7FF) == 0x7FF && (w0 & 0xFFFFFFFFFFFFFULL);
+            if (nan) w0 = 0;             // SQLite binds NaN as NULL
+            else vt = CORRO_REAL;
+        } else if (tag == 3 || tag == 4) {
+            const uint32_t l = r.u32();
+            vt = tag == 3 ? CORRO_TEXT : CORRO_BLOB;
+            if (l > 16) err = CORRO_E_RANGE;
+            vl = l > 16 ? 16 : l;
+            for (uint32_t i = 0; i < vl; i++) {
+                const uint64_t b = p[r.pos + i];
+                if (i < 8) w0 |= b << (8 * (7 - i));
+                else w1 |= b << (8 * (15 - i));
+            }
+            r.pos += l;
+        }
+        const int64_t cv = (int64_t)r.u64();
+        const uint64_t dbv = r.u64();
+        const uint64_t seq = r.u64();
+        const uint64_t slo = r.u64(), shi = r.u64();
+        const int64_t cl = (int64_t)r.u64();
+        if (seq > 0xFFFFFFFFULL || cl < 0 || cl > 0xFFFFFFFFLL || dbv > (uint64_t)INT64_MAX) err = CORRO_E_RANGE;
+        uint32_t so = site_lookup(d, slo, shi);
+        if (so == 0xFFFFFFFFu) note_unknown(d, slo, shi);
+        const uint64_t q = co + k;
+        const corro_changes &o = d.out;
+        const_cast<uint64_t *>(o.pk)[q] = pk;
+        const_cast<uint32_t *>(o.table_cid)[q] = tcid;
+        const_cast<int64_t *>(o.col_version)[q] = cv;
+        const_cast<int64_t *>(o.db_version)[q] = (int64_t)dbv;
+        const_cast<uint32_t *>(o.cl)[q] = (uint32_t)cl;
+        const_cast<uint32_t *>(o.seq)[q] = (uint32_t)seq;
+        const_cast<uint32_t *>(o.site)[q] = so;
+        const_cast<uint64_t *>(o.val0)[q] = w0;
+        if (o.val1) const_cast<uint64_t *>(o.val1)[q] = w1;
+        if (o.val_type) const_cast<uint8_t *>(o.val_type)[q] = (uint8_t)vt;
+        if (o.val_len) const_cast<uint8_t *>(o.val_len)[q] = (uint8_t)vl;
+        if (o.ts) const_cast<uint64_t *>(o.ts)[q] = ts;
+    }
+    if (err) atomicMin(&d.status[f], err);
+}
+
+size_t al(size_t b) { return ((b + 255) / 256) * 256; }
+
+uint64_t hmix(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33; return x;
+}
+
+// device copies of the schema names (once) and of the site hash (whenever sites were added)
+int wire_tables(corro_ctx *ctx) {
+    if (!ctx->wire_schema_ready) {
+        std::vector<uint8_t> names;
+        std::vector<uint32_t> toff, tlen, tbase, tn, coff, clen;
+        for (const auto &t : ctx->tables) {
+            toff.push_back((uint32_t)names.size());
+            tlen.push_back((uint32_t)t.name.size());
+            names.insert(names.end(), t.name.begin(), t.name.end());
+            tbase.push_back((uint32_t)coff.size());
+            tn.push_back((uint32_t)t.cols.size());
+            for (const auto &c : t.cols) {
+                coff.push_back((uint32_t)names.size());
+                clen.push_back((uint32_t)c.size());
+                names.insert(names.end(), c.begin(), c.end());
+            }
+        }
+        const size_t nt = toff.size(), nc = coff.size();
+        const size_t bytes = al(names.size() + 1) + 4 * al(nt * 4 + 4) + 2 * al(nc * 4 + 4);
+        if (int rc = ctx->d_wire_schema.ensure(bytes)) return rc;
+        uint8_t *q = ctx->d_wire_schema.as<uint8_t>();
+        auto put = [&](const void *src, size_t b) -> uint8_t * {
+            uint8_t *r = q;
+            if (b && hipMemcpy(r, src, b, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+            q += al(b + 4);
+            return r;
+        };
+        ctx->wire_names = put(names.data(), names.size());
+        ctx->wire_toff = (uint32_t *)put(toff.data(), nt * 4);
+        ctx->wire_tlen = (uint32_t *)put(tlen.data(), nt * 4);
+        ctx->wire_tbase = (uint32_t *)put(tbase.data(), nt * 4);
+        ctx->wire_tn = (uint32_t *)put(tn.data(), nt * 4);
+        ctx->wire_coff = (uint32_t *)put(coff.data(), nc * 4);
+        ctx->wire_clen = (uint32_t *)put(clen.data(), nc * 4);
+        if (!ctx->wire_names) return fail(CORRO_E_DEVICE, "upload of the schema names failed");
+        ctx->wire_schema_ready = true;
+    }
+    if (ctx->wire_sites_n != ctx->sites.size() || !ctx->d_wire_sites.p) {
+        const size_t n = ctx->sites.size();
+        uint32_t H = 16;
+        while (H < 2 * n) H <<= 1;
+        std::vector<uint64_t> lo(H, 0), hi(H, 0);
+        std::vector<uint32_t> ord(H, 0xFFFFFFFFu);
+        for (size_t i = 0; i < n; i++) {
+            uint64_t a, b;
+            std::memcpy(&a, ctx->sites[i].data(), 8);
+            std::memcpy(&b, ctx->sites[i].data() + 8, 8);
+            uint32_t h = (uint32_t)hmix(a ^ (b * 0x9E3779B97F4A7C15ULL)) & (H - 1);
+            while (ord[h] != 0xFFFFFFFFu) h = (h + 1) & (H - 1);
+            lo[h] = a;
+            hi[h] = b;
+            ord[h] = (uint32_t)i;
+        }
+        if (int rc = ctx->d_wire_sites.ensure(al(H * 8ULL) * 2 + al(H * 4ULL))) return rc;
+        uint8_t *q = ctx->d_wire_sites.as<uint8_t>();
+        CORRO_HIP_TRY(hipMemcpy(q, lo.data(), H * 8ULL, hipMemcpyHostToDevice));
+        CORRO_HIP_TRY(hipMemcpy(q + al(H * 8ULL), hi.data(), H * 8ULL, hipMemcpyHostToDevice));
+        CORRO_HIP_TRY(hipMemcpy(q + 2 * al(H * 8ULL), ord.data(), H * 4ULL, hipMemcpyHostToDevice));
+        ctx->wire_hmask = H - 1;
+        ctx->wire_sites_n = n;
+    }
+    return CORRO_OK;
+}
+
+}  // namespace
+}  // namespace corro
+
+using namespace corro;
+
+extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t len, int payload, int mem,
+                                   corro_decoded *out, int pass) {
+    if (!ctx || (!buf && len) || !out) return fail(CORRO_E_INVALID, "NULL argument");
+    if (payload != CORRO_PAYLOAD_SYNC && payload != CORRO_PAYLOAD_UNI) return fail(CORRO_E_INVALID, "bad payload kind");
+    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
+    if (pass != 0 && pass != 1) return fail(CORRO_E_INVALID, "pass must be 0 or 1");
+    if (len >= (1ULL << 32)) return fail(CORRO_E_RANGE, "at most 4 GiB of frames per call");
+    // frame scan (host: the length prefixes are a sequential chain)
+    std::vector<uint64_t> foff;
+    std::vector<uint32_t> flen;
+    uint64_t pos = 0;
+    while (pos + 4 <= len) {
+        const uint32_t l = ((uint32_t)buf[pos] << 24) | ((uint32_t)buf[pos + 1] << 16) | ((uint32_t)buf[pos + 2] << 8) |
+                           (uint32_t)buf[pos + 3];
+        if (pos + 4 + l > len) return fail(CORRO_E_INVALID, "truncated frame");
+        foff.push_back(pos + 4);
+        flen.push_back(l);
+        pos += 4 + (uint64_t)l;
+    }
+    if (pos != len) return fail(CORRO_E_INVALID, "trailing bytes after the last frame");
+    const uint32_t F = (uint32_t)foff.size();
+    if (pass == 0) {
+        out->nframes = F;
+        out->nchanges = out->nsets = 0;
+    } else if (out->nframes != F) {
+        return fail(CORRO_E_INVALID, "nframes differs from pass 0");
+    }
+    if (F == 0) return CORRO_OK;
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    if (int rc = wire_tables(ctx)) return rc;
+    const uint64_t NC = pass == 1 ? out->nchanges : 0, NS = pass == 1 ? out->nsets : 0;
+    const uint32_t ucap = 4096;
+    // scratch: bytes, frame index, headers, offsets, unknown sites, outputs staged for host mode
+    const size_t hdr = 6 * al(F * 4ULL) + 6 * al(F * 8ULL) + al(F * 16ULL);
+    const size_t outb = (mem == CORRO_MEM_HOST && pass == 1) ? (al(NC * 8) * 6 + al(NC * 4) * 4 + al(NC) * 2) : 0;
+    const size_t need = al(len) + al(F * 8ULL) + al(F * 4ULL) + hdr + 2 * al((F + 1) * 8ULL) + al(NC * 4 + 4) +
+                        al(ucap * 16ULL) + 256 + outb + 2 * al(NS * 8 + 8);
+    if (int rc = ctx->d_wire.ensure(need)) return rc;
+    uint8_t *q = ctx->d_wire.as<uint8_t>();
+    auto carve = [&](size_t b) {
+        uint8_t *r = q;
+        q += al(b);
+        return r;
+    };
+    WireDev d{};
+    uint8_t *dbuf = carve(len);
+    uint64_t *dfoff = (uint64_t *)carve(F * 8ULL);
+    uint32_t *dflen = (uint32_t *)carve(F * 4ULL);
+    d.buf = dbuf;
+    d.foff = dfoff;
+    d.flen = dflen;
+    d.nframes = F;
+    d.kind = (uint32_t)payload;
+    d.status = (int32_t *)carve(F * 4ULL);
+    d.cs_kind = (uint32_t *)carve(F * 4ULL);
+    d.nchg = (uint32_t *)carve(F * 4ULL);
+    d.nset = (uint32_t *)carve(F * 4ULL);
+    d.chg_start = (uint32_t *)carve(F * 4ULL);
+    d.site = (uint32_t *)carve(F * 4ULL);
+    d.v0 = (uint64_t *)carve(F * 8ULL);
+    d.v1 = (uint64_t *)carve(F * 8ULL);
+    d.s0 = (uint64_t *)carve(F * 8ULL);
+    d.s1 = (uint64_t *)carve(F * 8ULL);
+    d.last = (uint64_t *)carve(F * 8ULL);
+    d.ts = (uint64_t *)carve(F * 8ULL);
+    d.actor = carve(F * 16ULL);
+    uint64_t *dchg = (uint64_t *)carve((F + 1) * 8ULL), *dset = (uint64_t *)carve((F + 1) * 8ULL);
+    d.chg_off = dchg;
+    d.set_off = dset;
+    d.chg_rel = (uint32_t *)carve(NC * 4 + 4);
+    d.unknown = carve(ucap * 16ULL);
+    d.nunknown = (unsigned long long *)carve(256);
+    d.unknown_cap = ucap;
+    d.names = ctx->wire_names;
+    d.tname_off = ctx->wire_toff;
+    d.tname_len = ctx->wire_tlen;
+    d.tcol_base = ctx->wire_tbase;
+    d.tncols = ctx->wire_tn;
+    d.cname_off = ctx->wire_coff;
+    d.cname_len = ctx->wire_clen;
+    d.ntables = (uint32_t)ctx->tables.size();
+    CORRO_HIP_TRY(hipMemcpyAsync(dbuf, buf, len, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(dfoff, foff.data(), F * 8ULL, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(dflen, flen.data(), F * 4ULL, hipMemcpyHostToDevice, s));
+    // outputs
+    corro_changes o{};
+    uint64_t *dss = nullptr, *dse = nullptr;
+    if (pass == 1) {
+        if (mem == CORRO_MEM_DEVICE) {
+            o = out->changes;
+            dss = out->set_start;
+            dse = out->set_end;
+        } else {
+            o.pk = (uint64_t *)carve(NC * 8);
+            o.col_version = (int64_t *)carve(NC * 8);
+            o.db_version = (int64_t *)carve(NC * 8);
+            o.val0 = (uint64_t *)carve(NC * 8);
+            o.val1 = (uint64_t *)carve(NC * 8);
+            o.ts = (uint64_t *)carve(NC * 8);
+            o.table_cid = (uint32_t *)carve(NC * 4);
+            o.cl = (uint32_t *)carve(NC * 4);
+            o.seq = (uint32_t *)carve(NC * 4);
+            o.site = (uint32_t *)carve(NC * 4);
+            o.val_type = (uint8_t *)carve(NC);
+            o.val_len = (uint8_t *)carve(NC);
+            dss = (uint64_t *)carve(NS * 8 + 8);
+            dse = (uint64_t *)carve(NS * 8 + 8);
+        }
+        if (NC && (!o.pk || !o.table_cid || !o.col_version || !o.db_version || !o.cl || !o.seq || !o.site || !o.val0))
+            return fail(CORRO_E_INVALID, "a required change output array is NULL");
+        if (NS && (!dss || !dse)) return fail(CORRO_E_INVALID, "EmptySet range outputs are NULL");
+    }
+    d.out = o;
+    d.set_start = dss;
+    d.set_end = dse;
+    std::vector<int32_t> st(F);
+    std::vector<uint32_t> kind(F), nchg(F), nset(F), site(F);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if (int rc = wire_tables(ctx)) return rc;
+        uint8_t *sq = ctx->d_wire_sites.as<uint8_t>();
+        const uint32_t H = ctx->wire_hmask + 1;
+        d.hlo = (const uint64_t *)sq;
+        d.hhi = (const uint64_t *)(sq + al(H * 8ULL));
+        d.hord = (const uint32_t *)(sq + 2 * al(H * 8ULL));
+        d.hmask = ctx->wire_hmask;
+        CORRO_HIP_TRY(hipMemsetAsync(d.nunknown, 0, 8, s));
+        if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[0], s));
+        hipLaunchKernelGGL(k_wire_hdr, dim3((F + 255) / 256), dim3(256), 0, s, d);
+        CORRO_HIP_TRY(hipGetLastError());
+        CORRO_HIP_TRY(hipMemcpyAsync(st.data(), d.status, F * 4ULL, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(kind.data(), d.cs_kind, F * 4ULL, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(nchg.data(), d.nchg, F * 4ULL, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(nset.data(), d.nset, F * 4ULL, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        std::vector<uint64_t> co(F + 1, 0), so(F + 1, 0);
+        for (uint32_t f = 0; f < F; f++) {
+            co[f + 1] = co[f] + nchg[f];
+            so[f + 1] = so[f] + nset[f];
+        }
+        if (pass == 0) {
+            out->nchanges = co[F];
+            out->nsets = so[F];
+            return CORRO_OK;
+        }
+        if (co[F] != NC || so[F] != NS) return fail(CORRO_E_INVALID, "sizes differ from pass 0");
+        CORRO_HIP_TRY(hipMemcpyAsync(dchg, co.data(), (F + 1) * 8ULL, hipMemcpyHostToDevice, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(dset, so.data(), (F + 1) * 8ULL, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_wire_sets, dim3((F + 255) / 256), dim3(256), 0, s, d);
+        hipLaunchKernelGGL(k_wire_decode, dim3(F), dim3(64), 0, s, d);
+        if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
+        CORRO_HIP_TRY(hipGetLastError());
+        uint64_t nu = 0;
+        CORRO_HIP_TRY(hipMemcpyAsync(&nu, d.nunknown, 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        if (ctx->profiling) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[7], ctx->ev[0], ctx->ev[1]));
+        if (nu == 0) break;
+        if (attempt == 1) return fail(CORRO_E_DEVICE, "internal: sites still unknown after registering them");
+        // register every site id seen but not yet known, then decode again with the new table
+        const uint64_t take = std::min<uint64_t>(nu, ucap);
+        std::vector<uint8_t> ids(take * 16);
+        CORRO_HIP_TRY(hipMemcpy(ids.data(), d.unknown, take * 16, hipMemcpyDeviceToHost));
+        if (int rc = corro_site_register(ctx, ids.data(), take, nullptr)) return rc;
+        if (nu > ucap) attempt = -1;  // more unknown ids than one pass collects: keep going
+    }
+    // headers -> host
+    std::vector<uint64_t> v0(F), v1(F), s0(F), s1(F), last(F), ts(F);
+    std::vector<uint8_t> actor(F * 16ULL);
+    CORRO_HIP_TRY(hipMemcpyAsync(st.data(), d.status, F * 4ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(site.data(), d.site, F * 4ULL, hipMemcpyDeviceToHost, s));
+    struct H8 { std::vector<uint64_t> *h; uint64_t *dv; } h8[] = {{&v0, d.v0}, {&v1, d.v1}, {&s0, d.s0}, {&s1, d.s1},
+                                                                  {&last, d.last}, {&ts, d.ts}};
+    for (auto &x : h8) CORRO_HIP_TRY(hipMemcpyAsync(x.h->data(), x.dv, F * 8ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(actor.data(), d.actor, F * 16ULL, hipMemcpyDeviceToHost, s));
+    if (mem == CORRO_MEM_HOST && NC) {
+        const corro_changes &h = out->changes;
+        struct Cp { const void *dst; const void *src; size_t b; } cp[] = {
+            {h.pk, o.pk, NC * 8},         {h.col_version, o.col_version, NC * 8}, {h.db_version, o.db_version, NC * 8},
+            {h.val0, o.val0, NC * 8},     {h.val1, o.val1, NC * 8},               {h.ts, o.ts, NC * 8},
+            {h.table_cid, o.table_cid, NC * 4}, {h.cl, o.cl, NC * 4},             {h.seq, o.seq, NC * 4},
+            {h.site, o.site, NC * 4},     {h.val_type, o.val_type, NC},           {h.val_len, o.val_len, NC}};
+        for (auto &c : cp)
+            if (c.dst) CORRO_HIP_TRY(hipMemcpyAsync(const_cast<void *>(c.dst), c.src, c.b, hipMemcpyDeviceToHost, s));
+    }
+    if (mem == CORRO_MEM_HOST && NS) {
+        CORRO_HIP_TRY(hipMemcpyAsync(out->set_start, dss, NS * 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(out->set_end, dse, NS * 8, hipMemcpyDeviceToHost, s));
+    }
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    uint64_t coff = 0, soff = 0;
+    for (uint32_t f = 0; f < F; f++) {
+        corro_changeset &c = out->cs[f];
+        std::memcpy(out->actor_ids + 16ULL * f, actor.data() + 16ULL * f, 16);
+        c.actor_id = out->actor_ids + 16ULL * f;
+        c.site = site[f];
+        // speedy variant index (Empty 0, Full 1, EmptySet 2) -> CORRO_CS_*
+        c.kind = kind[f] == 0 ? CORRO_CS_EMPTY : (kind[f] == 1 ? CORRO_CS_FULL : CORRO_CS_EMPTY_SET);
+        c.version_start = v0[f];
+        c.version_end = v1[f];
+        c.seq_start = s0[f];
+        c.seq_end = s1[f];
+        c.last_seq = last[f];
+        c.ts = ts[f];
+        c.change_off = kind[f] == 2 ? soff : coff;
+        c.change_count = kind[f] == 2 ? nset[f] : nchg[f];
+        coff += nchg[f];
+        soff += nset[f];
+        if (out->status) out->status[f] = st[f];
+    }
+    return CORRO_OK;
+}

@@ -65,6 +65,14 @@ class MergeEngine:
         L.check(L.lib().corro_site_register(self._h, ids.ctypes.data, ids.shape[0], ords.ctypes.data))
         return ords[: ids.shape[0]]
 
+    def site_ids(self):
+        """Registered 16-byte site ids by ordinal (crsql_site_id)."""
+        c = C.c_uint32()
+        L.check(L.lib().corro_site_ids(self._h, None, 0, C.byref(c)))
+        buf = np.zeros(max(1, 16 * c.value), np.uint8)
+        L.check(L.lib().corro_site_ids(self._h, buf.ctypes.data, c.value, C.byref(c)))
+        return [bytes(buf[16 * i:16 * i + 16]) for i in range(c.value)]
+
     def site_count(self):
         c = C.c_uint32()
         L.check(L.lib().corro_site_count(self._h, C.byref(c)))
@@ -183,6 +191,31 @@ class MergeEngine:
         torch.cuda.current_stream().synchronize()
         L.check(L.lib().corro_partition_ranks(self._h, C.byref(s), nranks, C.byref(o), counts.ctypes.data))
         return out, [int(c) for c in counts[:nranks]]
+
+    # ---- wire decode ------------------------------------------------------------------------
+    def decode_frames(self, buf, payload=0):
+        """Decode length-delimited speedy frames (corro_decode_frames; payload 0 = SyncMessage,
+        1 = UniPayload) on the GPU. Returns {"cs": ctypes array of corro_changeset (one per
+        frame), "status": int32[], "changes": SoA dict (host numpy), "set_start"/"set_end"}."""
+        lib = L.lib()
+        buf = bytes(buf)
+        d = L.Decoded()
+        L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, L.CORRO_MEM_HOST, C.byref(d), 0))
+        F, NC, NS = d.nframes, d.nchanges, d.nsets
+        cs = (L.Changeset * max(F, 1))()
+        actors = (C.c_uint8 * max(16 * F, 16))()
+        status = np.zeros(max(F, 1), np.int32)
+        ch = {k: np.zeros(max(NC, 1), dt) for k, dt in BATCH_FIELDS.items()}
+        ss, se = np.zeros(max(NS, 1), np.uint64), np.zeros(max(NS, 1), np.uint64)
+        d.cs, d.actor_ids, d.status = C.addressof(cs), C.addressof(actors), status.ctypes.data
+        d.changes.n = NC
+        for k, a in ch.items():
+            setattr(d.changes, k, a.ctypes.data)
+        d.set_start, d.set_end = ss.ctypes.data, se.ctypes.data
+        if F:
+            L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, L.CORRO_MEM_HOST, C.byref(d), 1))
+        return {"cs": cs, "nframes": F, "actors": actors, "status": status[:F],
+                "changes": {k: a[:NC] for k, a in ch.items()}, "set_start": ss[:NS], "set_end": se[:NS]}
 
     # ---- changeset extraction (server side of a sync need) ---------------------------------
     def extract_changes(self, needs):

@@ -233,11 +233,11 @@ def _subtract(ranges, holes):
 def handle_needs(agent, needs, max_buf_size=MAX_CHANGES_BYTES_PER_MESSAGE):
     """handle_need (peer/mod.rs:371-727) for a list of (actor_id, SyncNeedV1) at once.
 
-    Change.site_id comes from agent.site_ids (ordinal -> 16 bytes). Returns, per need,
+    Change.site_id comes from the engine's site table (ordinal -> 16 bytes). Returns, per need,
     the list of ChangeV1 messages in the order the reference sends them. The crsql_changes
     queries of every need run as ONE batched device extraction."""
     eng = agent.engine
-    site_ids = agent.site_ids
+    site_ids = dict(enumerate(eng.site_ids()))
     # one extraction entry per crsql_changes query
     ent_site, ent_s, ent_e, ent_ss, ent_se, owner = [], [], [], [], [], []
     plan = []

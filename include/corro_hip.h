@@ -138,6 +138,8 @@ int corro_lookup_cid(corro_ctx *ctx, const char *table, const char *cid, uint32_
  * The engine orders sites by memcmp of the bytes for the merge-equal-values tie-break. */
 int corro_site_register(corro_ctx *ctx, const uint8_t *site_ids, uint64_t n, uint32_t *ordinals);
 int corro_site_count(corro_ctx *ctx, uint32_t *count);
+/* The registered 16-byte site ids by ordinal (at most cap written; *count = all). */
+int corro_site_ids(corro_ctx *ctx, uint8_t *ids, uint32_t cap, uint32_t *count);
 
 /* ------------------------------------------------------------------ merge */
 
@@ -352,6 +354,34 @@ typedef struct {
     uint64_t *pseq_off, *pseq_start, *pseq_end;        /* n_partials + 1, n_pseqs, n_pseqs */
 } corro_sync_state;
 int corro_generate_sync(corro_bookie *bk, const uint8_t *self_actor, corro_sync_state *out, int pass);
+
+/* ------------------------------------------------------------------ wire decode */
+
+/* Decode length-delimited frames (tokio LengthDelimitedCodec: u32 big-endian length + payload,
+ * api/peer/mod.rs:917-929) of speedy-encoded changeset messages on the GPU:
+ * CORRO_PAYLOAD_SYNC = SyncMessage::V1(SyncMessageV1::Changeset(ChangeV1)) (sync.rs:19-30),
+ * CORRO_PAYLOAD_UNI = UniPayload::V1 { Broadcast(BroadcastV1::Change(ChangeV1)), .. }
+ * (broadcast.rs:41-52, uni.rs:63). `buf` is host memory. Two passes: pass 0 sets nframes /
+ * nchanges / nsets; the caller allocates; pass 1 fills one corro_changeset per frame (cs[i],
+ * actor_id pointing into actor_ids) and the changes as one SoA batch (arrays on `mem`, the shape
+ * corro_process_multiple_changes / corro_apply_batch take; ts = the changeset's ts). EmptySet
+ * ranges go to set_start/set_end at [change_off, change_off + change_count) of their frame.
+ * status[i]: 0 ok, 1 not a changeset message (skipped), CORRO_E_INVALID malformed, CORRO_E_RANGE a
+ * value outside the engine encoding (TEXT/BLOB > 16 bytes, a pk that is not one packed INTEGER,
+ * seq or cl beyond 32 bits); the changes of a frame with status != 0 are unspecified. Unknown
+ * table/column names give table_cid = CORRO_TCID_UNKNOWN; site ids not yet registered are
+ * registered (corro_site_register) so every site field is a valid ordinal. */
+enum { CORRO_PAYLOAD_SYNC = 0, CORRO_PAYLOAD_UNI = 1 };
+typedef struct {
+    uint64_t nframes, nchanges, nsets;      /* pass 0 outputs, pass 1 inputs */
+    corro_changeset *cs;                    /* host, nframes */
+    uint8_t *actor_ids;                     /* host, 16 * nframes */
+    int32_t *status;                        /* host, nframes (optional) */
+    corro_changes changes;                  /* nchanges each (mem); val1/val_type/val_len/ts optional */
+    uint64_t *set_start, *set_end;          /* nsets each (mem) */
+} corro_decoded;
+int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t len, int payload, int mem, corro_decoded *out,
+                        int pass);
 
 #ifdef __cplusplus
 }
