@@ -61,12 +61,14 @@ int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t 
                    uint32_t *vo, uint32_t n, uint32_t end_bit, hipStream_t s);
 
 int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStream_t s);
+int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, uint32_t *out, uint32_t n,
+                            hipStream_t s);
 
 // Oversized buckets (after the first merge pass queued them), all at once and device-wide (the
 // phases of ovf_kernels.h): fields + row ids -> sort by (bucket base + row, position) -> L scan ->
 // classify -> epoch scan -> candidate keys -> sort -> argmax / group-start scans -> link -> walk
 // -> [impacts] -> per-bucket counts.
-static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) {
+static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nbatch, bool prof) {
     hipStream_t s = ctx->stream;
     const uint32_t B = ctx->B;
     std::vector<uint32_t> list(novf), pc(B), nc(B);
@@ -74,9 +76,10 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     CORRO_HIP_TRY(hipMemcpy(pc.data(), ctx->d_state_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
     CORRO_HIP_TRY(hipMemcpy(nc.data(), ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
     std::vector<uint32_t> koff(novf + 1), soff(novf);
-    uint64_t K = 0, S = 0;
+    uint64_t K = 0, S = 0, PM = 0;
     for (uint64_t k = 0; k < novf; k++) {
         const uint64_t n = (uint64_t)pc[list[k]] + nc[list[k]];
+        PM = std::max<uint64_t>(PM, pc[list[k]]);
         uint64_t sl = 1;
         while (sl < 2 * n) sl <<= 1;
         koff[k] = (uint32_t)K;
@@ -90,7 +93,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     // row ids (< K) take rb bits with one spare value above them, so that ~0 sorts last
     uint32_t rb = 1;
     while ((1ULL << rb) <= K) rb++;
-    const uint32_t key_bits = 32 + rb;
+    // compact positions: prior slice index < PM, batch change i -> PM + i
+    uint32_t pbits = 1;
+    while ((1ULL << pbits) < PM + nbatch) pbits++;
     uint32_t maxc = 0, cid_bits = 1;
     for (const auto &t : ctx->tables) maxc = std::max<uint32_t>(maxc, (uint32_t)t.cols.size());
     while ((1u << cid_bits) <= maxc) cid_bits++;
@@ -101,6 +106,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     d.G = (uint32_t)novf;
     d.K = (uint32_t)K;
     d.cid_bits = cid_bits;
+    d.rshift = pbits;
+    d.pm = (uint32_t)PM;
     uint64_t bytes = 0;
     uint8_t *base = nullptr;
     auto take = [&](uint64_t n) {
@@ -121,22 +128,19 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
         for (uint64_t **p : u64s) *p = (uint64_t *)take(K * 8);
         d.cv = (int64_t *)take(K * 8);
         d.ccv = (int64_t *)take(K * 8);
-        d.qcv = (int64_t *)take(K * 8);
-        d.qk0 = (uint64_t *)take(K * 8);
-        d.qk1 = (uint64_t *)take(K * 8);
-        d.qm = (uint32_t *)take(K * 4);
-        d.qsr = (uint32_t *)take(K * 4);
+        d.qkey = (OvfKey *)take(K * sizeof(OvfKey));
         uint32_t **u32s[] = {&d.tc,    &d.cl,     &d.pos,   &d.vmeta, &d.srank, &d.val,    &d.val_s, &d.rowid,
                              &d.cl_s,  &d.lx,     &d.recf,  &d.epc,   &d.kind,  &d.pb,     &d.rstart, &d.rbad,
                              &d.rnrec, &d.recs,   &d.head,  &d.scid,  &d.spos,  &d.sz,     &d.ccid,  &d.csrc,
                              &d.cval,  &d.cval_s, &d.cbest, &d.cgs,   &d.nxt,   &d.fstg};
         for (uint32_t **p : u32s) *p = (uint32_t *)take(K * 4);
         if (pass == 0) {
-            size_t t0 = 0, t1 = 0, t2 = 0;
-            TRY(ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, d.K, key_bits, s));
+            size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+            TRY(ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, d.K, 64, s));
             TRY(ovf_sort_pairs(nullptr, &t1, nullptr, nullptr, nullptr, nullptr, d.K, ckey_bits, s));
             TRY(ovf_scans(nullptr, &t2, d, 0, s));
-            temp = std::max(std::max(t0, t1), t2);
+            TRY(prim_inclusive_scan_u32(nullptr, &t3, nullptr, nullptr, d.K, s));
+            temp = std::max(std::max(t0, t1), std::max(t2, t3));
         }
         d_temp = take(temp);
         if (pass == 0) {
@@ -157,6 +161,21 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, bool prof) 
     };
     hipLaunchKernelGGL(k_ovf_load, grid, blk, 0, s, a, d);
     hipLaunchKernelGGL(k_ovf_rowhash, grid, blk, 0, s, d);
+    TRY(launched());
+    // dense row ids: the row count sizes the sort's key
+    TRY(prim_inclusive_scan_u32(d_temp, &temp, d.recf, d.epc, d.K, s));
+    uint32_t nrows = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&nrows, d.epc + (K - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    uint32_t rbits = 1;
+    while ((1ULL << rbits) < nrows) rbits++;
+    const uint32_t key_bits = rbits + pbits;
+    if (key_bits > 64) return fail(CORRO_E_RANGE, "overflow sort key exceeds 64 bits");
+    static const bool dbg = std::getenv("CORRO_HIP_OVF_DEBUG") != nullptr;
+    if (dbg)
+        fprintf(stderr, "[corro ovf] buckets %llu records %llu rows %u key bits %u (+%u) cand key bits %u\n",
+                (unsigned long long)novf, (unsigned long long)K, nrows, key_bits, rbits, ckey_bits);
+    hipLaunchKernelGGL(k_ovf_rowkey, grid, blk, 0, s, d);
     TRY(launched());
     TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.key_s, d.val, d.val_s, d.K, key_bits, s));
     hipLaunchKernelGGL(k_ovf_gather, grid, blk, 0, s, d);
@@ -596,7 +615,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
         for (int i = 0; i < 5; i++) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[i], ctx->ev[i], ctx->ev[i + 1]));
 
     const uint64_t novf = ctx->h_misc[1];
-    if (novf) TRY(run_overflow(ctx, a, novf, prof));
+    if (novf) TRY(run_overflow(ctx, a, novf, n, prof));
     hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
                        ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites);
     if (out && out->impact && !imp_dev)

@@ -601,6 +601,7 @@ struct GenArrays {
     int64_t *ccv;
     uint32_t slots;  // pow2
     uint32_t P;      // records
+    uint32_t rshift; // row = key >> rshift (32 in LDS; the overflow path's compact keys use fewer)
 };
 
 __device__ inline void gen_emit(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts,
@@ -665,12 +666,12 @@ __device__ inline void gen_set_cell(const GenArrays &g, uint32_t s, uint32_t &nc
 __device__ inline void gen_fold_row(const MergeArgs &a, const BucketView &v, Rec *outb,
                                     uint64_t *outts, uint32_t *outcnt, uint32_t *flag,
                                     const GenArrays &g, uint32_t s, uint32_t n) {
-    const uint32_t row = (uint32_t)(g.key[s] >> 32);
+    const uint32_t row = (uint32_t)(g.key[s] >> g.rshift);
     uint32_t ncell = 0;
     bool hs = false;
     int64_t scv = 0;
     uint32_t ssrc = 0;
-    for (uint32_t j = s; j < n && (uint32_t)(g.key[j] >> 32) == row; j++) {
+    for (uint32_t j = s; j < n && (uint32_t)(g.key[j] >> g.rshift) == row; j++) {
         const uint32_t x = g.val[j];
         const uint32_t cl = g.cl[x];
         const uint32_t cid = g.tc[x] & 0xFFFFu;
@@ -1346,6 +1347,7 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
     g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
     g.own = reinterpret_cast<uint32_t *>(p);
     g.slots = GEN_SLOTS;
+    g.rshift = 32;
     g.P = n;
     __shared__ uint32_t s_long, s_wsum[MERGE_THREADS / 64];
     if (tid == 0) s_long = 0;

@@ -23,8 +23,9 @@
 // (tools/proto_rowfold.py); tests/test_gpu_merge.py checks this implementation.
 //
 // Phases:
-//   k_ovf_load, k_ovf_rowhash       fields; row ids (open addressing per bucket, read-before-CAS)
-//   radix sort by (kb + row, position)                                  [prims.hip, rocPRIM]
+//   k_ovf_load, k_ovf_rowhash       fields; row owners (open addressing per bucket, read-before-CAS)
+//   scan of owner flags, k_ovf_rowkey  dense row ids, compact positions
+//   radix sort by (row, position)                                       [prims.hip, rocPRIM]
 //   k_ovf_gather                    cl in sorted order, row starts
 //   exclusive max-scan of cl by row -> L                                [rocPRIM scan_by_key]
 //   k_ovf_classify                  record / candidate / no-op, record impacts, App. A.3 check
@@ -32,7 +33,8 @@
 //   k_ovf_epochs, k_ovf_ckeys       the row's record list; candidate keys (epoch's record, cid)
 //   stable radix sort of the candidates by (epoch, cid): a group keeps application order
 //   k_ovf_cgather                   the candidates' cell keys in candidate-sorted order
-//   inclusive argmax-scan by group (-> W and every prefix), min-scan of the index (group start)
+//   inclusive argmax-scan by group (-> W and every prefix) over the gathered 32-B keys; group
+//   start = plain max-scan of the group heads' indices [prims.hip]
 //   k_ovf_link                      each group's end is linked under its epoch's record
 //   k_ovf_walk                      one thread per row: the walk over its records, emission;
 //                                   rows outside App. A.3 run the sequential fold instead
@@ -43,9 +45,19 @@
 
 namespace corro {
 
+// Cell key (col_version, value order, site rank) of a change; `z` = the carried cell of a
+// resurrected row (col_version 0, value and metadata kept). 32 B: two 16-B loads from one line.
+struct alignas(16) OvfKey {
+    int64_t cv;
+    uint64_t k0, k1;
+    uint32_t m, sr;
+};
+
 struct OvfDev {
     uint32_t G, K;              // oversized buckets, their records
     uint32_t cid_bits;          // a candidate key is (epoch's record position) << cid_bits | cid
+    uint32_t rshift;            // a record's sort key is dense row << rshift | compact position
+    uint32_t pm;                // compact position of batch change i: pm + i (prior rows: their slice index < pm)
     const uint32_t *koff;       // [G + 1] bucket base offsets
     const uint32_t *slot_off;   // [G] row-hash slot region, next_pow2(2 n) words each
     // per record (kb + i)
@@ -66,9 +78,7 @@ struct OvfDev {
     uint64_t *ckey, *ckey_s;
     uint32_t *cval, *cval_s, *cbest, *cgs, *nxt, *fstg;
     // candidates' cell keys gathered in candidate-sorted order (the argmax scan reads neighbours)
-    int64_t *qcv;
-    uint64_t *qk0, *qk1;
-    uint32_t *qm, *qsr;
+    OvfKey *qkey;
     uint32_t *slots;
     uint32_t *ocnt, *oflag;     // [G]
 };
@@ -83,14 +93,6 @@ __device__ inline uint32_t ovf_bucket_of(const OvfDev &d, uint32_t r) {
     return lo;
 }
 
-// Cell key (col_version, value order, site rank) of a change; `z` = the carried cell of a
-// resurrected row (col_version 0, value and metadata kept).
-struct OvfKey {
-    int64_t cv;
-    uint64_t k0, k1;
-    uint32_t m, sr;
-};
-
 // by sorted position p
 __device__ inline OvfKey ovf_key_p(const OvfDev &d, uint32_t p, bool z) {
     const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
@@ -99,7 +101,7 @@ __device__ inline OvfKey ovf_key_p(const OvfDev &d, uint32_t p, bool z) {
 
 // by candidate-sorted index q
 __device__ inline OvfKey ovf_key_q(const OvfDev &d, uint32_t q) {
-    return OvfKey{d.qcv[q], d.qk0[q], d.qk1[q], d.qm[q], d.qsr[q]};
+    return d.qkey[q];
 }
 
 // >0: a greater
@@ -113,10 +115,8 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b) {
 
 // argmax by cell key over candidate-sorted indices, the earlier one on ties (x precedes y)
 struct OvfArgmax {
-    OvfDev d;
-    __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const {
-        return ovf_kcmp(ovf_key_q(d, y), ovf_key_q(d, x)) > 0 ? y : x;
-    }
+    const OvfKey *q;
+    __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return ovf_kcmp(q[y], q[x]) > 0 ? y : x; }
 };
 
 #define OVF_LOOP(i, N) for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (N); i += gridDim.x * blockDim.x)
@@ -183,20 +183,34 @@ static __global__ void k_ovf_rowhash(OvfDev d) {
             }
         }
         if (todo) owner = probe();
-        d.key[r] = ((uint64_t)(kb + owner) << 32) | d.pos[r];
+        d.rowid[r] = owner;  // (scratch until the sort)
+        d.recf[r] = owner == r - kb ? 1u : 0u;
         d.val[r] = r - kb;
+    }
+}
+
+// Sort keys: rows numbered densely (inclusive scan of the owner flags, in epc) and positions
+// compacted (prior rows first, then the batch in application order), so the radix sort goes
+// through log2(rows) + log2(prior + batch) bits instead of 32 + 32.
+static __global__ void k_ovf_rowkey(OvfDev d) {
+    OVF_LOOP(r, d.K) {
+        const uint32_t kb = d.koff[d.pb[r]];
+        const uint64_t row = d.epc[kb + d.rowid[r]] - 1u;
+        const uint32_t pos = d.pos[r];
+        const uint64_t cp = (pos & BATCH_POS) ? (uint64_t)d.pm + (pos & 0x7FFFFFFFu) : (uint64_t)pos;
+        d.key[r] = (row << d.rshift) | cp;
     }
 }
 
 static __global__ void k_ovf_gather(OvfDev d) {
     OVF_LOOP(p, d.K) {
-        const uint32_t row = (uint32_t)(d.key_s[p] >> 32);
+        const uint32_t row = (uint32_t)(d.key_s[p] >> d.rshift);
         const uint32_t b = d.pb[p];
         d.rowid[p] = row;
         d.cl_s[p] = d.cl[d.koff[b] + d.val_s[p]];
         d.head[p] = 0;
         d.fstg[p] = 0;
-        if (p == 0 || (uint32_t)(d.key_s[p - 1] >> 32) != row) {
+        if (p == 0 || (uint32_t)(d.key_s[p - 1] >> d.rshift) != row) {
             d.rstart[row] = p;
             d.rbad[row] = 0;
             d.rnrec[row] = 0;
@@ -248,11 +262,7 @@ static __global__ void k_ovf_cgather(OvfDev d) {
     OVF_LOOP(q, d.K) {
         const uint32_t p = d.cval_s[q];
         const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
-        d.qcv[q] = d.cv[x];
-        d.qk0[q] = d.vk0[x];
-        d.qk1[q] = d.vk1[x];
-        d.qm[q] = d.vmeta[x];
-        d.qsr[q] = d.srank[x];
+        d.qkey[q] = OvfKey{d.cv[x], d.vk0[x], d.vk1[x], d.vmeta[x], d.srank[x]};
     }
 }
 
@@ -330,6 +340,7 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
             g.ccv = d.ccv + kb;
             g.own = nullptr;
             g.slots = 0;
+            g.rshift = d.rshift;
             g.P = n;
             const uint32_t bb = a.ovf_list[b];
             gen_fold_row(a, v, a.out + a.out_off[bb], a.out_ts ? a.out_ts + a.out_off[bb] : nullptr, &d.ocnt[b],

@@ -12,6 +12,7 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_scan_by_key.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "internal.h"
 #include "merge_kernels.h"
@@ -37,18 +38,23 @@ int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, 
 struct OvfMax {
     __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return x > y ? x : y; }
 };
-struct OvfMin {
-    __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return x < y ? x : y; }
+
+// group start of candidate-sorted index q: the last group head at or before q (heads' indices
+// increase, so a plain max-scan of "q if head else 0" finds it; no keys are compared in the scan)
+struct OvfHead {
+    const uint64_t *k;
+    __device__ inline uint32_t operator()(uint32_t q) const { return (q == 0 || k[q - 1] != k[q]) ? q : 0u; }
 };
 
 // Segmented scans of the device-wide overflow path (ovf_kernels.h): which = 0 L (exclusive max of
-// cl by row), 1 epoch counts (inclusive count of records by row), 2 running argmax and group start
-// of the candidates by group, both over candidate-sorted indices. temp == nullptr -> *temp_bytes =
-// the largest size any of them needs.
+// cl by row), 1 epoch counts (inclusive count of records by row), 2 running argmax (by group) and
+// group start (plain max-scan) of the candidates, over candidate-sorted indices. temp == nullptr ->
+// *temp_bytes = the largest size any of them needs.
 int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStream_t s) {
     const size_t K = d.K;
     hipError_t e = hipSuccess;
     const rocprim::counting_iterator<uint32_t> idx(0u);
+    const auto heads = rocprim::make_transform_iterator(idx, OvfHead{d.ckey_s});
     if (!temp) {
         size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
         e = rocprim::exclusive_scan_by_key(nullptr, t0, d.rowid, d.cl_s, d.lx, 0u, K, OvfMax{},
@@ -57,11 +63,9 @@ int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStr
             e = rocprim::inclusive_scan_by_key(nullptr, t1, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
                                                rocprim::equal_to<uint32_t>(), s);
         if (e == hipSuccess)
-            e = rocprim::inclusive_scan_by_key(nullptr, t2, d.ckey_s, idx, d.cbest, K, OvfArgmax{d},
+            e = rocprim::inclusive_scan_by_key(nullptr, t2, d.ckey_s, idx, d.cbest, K, OvfArgmax{d.qkey},
                                                rocprim::equal_to<uint64_t>(), s);
-        if (e == hipSuccess)
-            e = rocprim::inclusive_scan_by_key(nullptr, t3, d.ckey_s, idx, d.cgs, K, OvfMin{},
-                                               rocprim::equal_to<uint64_t>(), s);
+        if (e == hipSuccess) e = rocprim::inclusive_scan(nullptr, t3, heads, d.cgs, K, OvfMax{}, s);
         *temp_bytes = std::max(std::max(t0, t1), std::max(t2, t3));
     } else if (which == 0) {
         e = rocprim::exclusive_scan_by_key(temp, *temp_bytes, d.rowid, d.cl_s, d.lx, 0u, K, OvfMax{},
@@ -70,11 +74,9 @@ int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStr
         e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
                                            rocprim::equal_to<uint32_t>(), s);
     } else {
-        e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, idx, d.cbest, K, OvfArgmax{d},
+        e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, idx, d.cbest, K, OvfArgmax{d.qkey},
                                            rocprim::equal_to<uint64_t>(), s);
-        if (e == hipSuccess)
-            e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, idx, d.cgs, K, OvfMin{},
-                                               rocprim::equal_to<uint64_t>(), s);
+        if (e == hipSuccess) e = rocprim::inclusive_scan(temp, *temp_bytes, heads, d.cgs, K, OvfMax{}, s);
     }
     if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("segmented scan: ") + hipGetErrorString(e));
     return CORRO_OK;
