@@ -140,6 +140,12 @@ class Agent:
         self.site_ids[o] = bytes(site_id)
         return o
 
+    def change_queue(self, **kw):
+        """handle_changes' batching loop in front of this agent (queue.ChangeQueue): apply each batch
+        it returns with process_multiple_changes, then report it with job_done()."""
+        from .queue import ChangeQueue
+        return ChangeQueue(self.actor_id, self.bookie.contains_all, **kw)
+
     def handle_needs(self, needs, max_buf_size=None):
         """Answer (actor_id, SyncNeedV1) needs from this node's state (serve.handle_needs)."""
         from . import serve

@@ -187,3 +187,23 @@ def test_impactful_changes_follow_cumulative_rows_impacted():
     assert r.known == ["current", "current"]
     assert len(r.impactful[0]) == 1
     assert [c.seq for c in r.impactful[1]] == [0]   # first change of v2: cumulative counter > 0
+
+
+def test_loadshed_handle_changes():
+    """handlers.rs:931-1000 through the real Agent and Bookie: apply_queue_len 1,
+    processing_queue_len 3, the writer busy while 10..1 arrive: 6..=10 and 1..=3 are applied,
+    4 and 5 were displaced from the queue and never are."""
+    from corrosion_amd.agent import Change, ChangeV1, Full
+    a = agent()
+    other = bytes([0x55] * 16)
+    q = a.change_queue(apply_queue_len=1, processing_queue_len=3)
+    running = []
+    for i in range(10, 0, -1):
+        ch = Change("tests", i, "text", "two override", 1, i, 0, TA1, 1)
+        running += q.recv(ChangeV1(other, Full(i, [ch], (0, 0), 0, ts=1)))
+    assert len(running) == 5 and q.dropped == 2
+    while running:
+        a.process_multiple_changes(running.pop(0))
+        running += q.job_done()
+    assert a.bookie.contains_all(other, (6, 10)) and a.bookie.contains_all(other, (1, 3))
+    assert not a.bookie.contains_all(other, (5, 5)) and not a.bookie.contains_all(other, (4, 4))
