@@ -63,6 +63,8 @@ int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t 
 int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStream_t s);
 int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, uint32_t *out, uint32_t n,
                             hipStream_t s);
+int ovf_scan_tiles(void *temp, size_t *temp_bytes, const OvfDev &d, const CsAgg *in, CsAgg *out, uint32_t n,
+                   hipStream_t s);
 
 // Oversized buckets (after the first merge pass queued them), all at once and device-wide (the
 // phases of ovf_kernels.h): fields + row ids -> sort by (bucket base + row, position) -> L scan ->
@@ -117,6 +119,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     };
     void *d_temp = nullptr;
     size_t temp = 0;
+    uint32_t nt = 0, *cs_first = nullptr;
+    CsAgg *cs_agg = nullptr, *cs_incl = nullptr;
     for (int pass = 0; pass < 2; pass++) {
         bytes = 0;
         d.koff = (const uint32_t *)take((novf + 1) * 4);
@@ -140,8 +144,14 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
             TRY(ovf_sort_pairs(nullptr, &t1, nullptr, nullptr, nullptr, nullptr, d.K, ckey_bits, s));
             TRY(ovf_scans(nullptr, &t2, d, 0, s));
             TRY(prim_inclusive_scan_u32(nullptr, &t3, nullptr, nullptr, d.K, s));
-            temp = std::max(std::max(t0, t1), std::max(t2, t3));
+            size_t t4 = 0;
+            TRY(ovf_scan_tiles(nullptr, &t4, d, nullptr, nullptr, (uint32_t)((K + CS_TILE - 1) / CS_TILE), s));
+            temp = std::max(std::max(std::max(t0, t1), std::max(t2, t3)), t4);
         }
+        nt = (uint32_t)((K + CS_TILE - 1) / CS_TILE);
+        cs_agg = (CsAgg *)take(nt * 8ULL);
+        cs_incl = (CsAgg *)take(nt * 8ULL);
+        cs_first = (uint32_t *)take(nt * 4ULL);
         d_temp = take(temp);
         if (pass == 0) {
             TRY(ctx->d_ovf_sort.ensure(bytes + 256));
@@ -187,13 +197,32 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     hipLaunchKernelGGL(k_ovf_epochs, grid, blk, 0, s, d);
     hipLaunchKernelGGL(k_ovf_ckeys, grid, blk, 0, s, d);
     TRY(launched());
-    TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.ckey_s, d.cval, d.cval_s, d.K, ckey_bits, s));
-    hipLaunchKernelGGL(k_ovf_cgather, grid, blk, 0, s, d);
+    // only the candidates are sorted (a minority of the records): compact them first
+    TRY(prim_inclusive_scan_u32(d_temp, &temp, d.slots, d.slots + K, d.K, s));
+    uint32_t ncand = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&ncand, d.slots + K + (K - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    hipLaunchKernelGGL(k_ovf_ccompact, grid, blk, 0, s, d);
     TRY(launched());
-    TRY(ovf_scans(d_temp, &temp, d, 2, s));
-    hipLaunchKernelGGL(k_ovf_link, grid, blk, 0, s, d);
+    if (ncand) TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.ckey_s, d.val, d.cval_s, ncand, ckey_bits, s));
+    if (ncand < K) CORRO_HIP_TRY(hipMemsetAsync(d.ckey_s + ncand, 0xFF, (K - ncand) * 8, s));
+    if (dbg) fprintf(stderr, "[corro ovf] candidates %u\n", ncand);
+    d.ncand = ncand;
+    const dim3 cgrid((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((ncand + 255) / 256, 8192)));
+    hipLaunchKernelGGL(k_ovf_cgather, cgrid, blk, 0, s, d);
+    TRY(launched());
+    if (ncand) {
+        const uint32_t ntc = (ncand + CS_TILE - 1) / CS_TILE;  // <= nt
+        hipLaunchKernelGGL(k_cscan_tile, dim3(ntc), dim3(CS_T), 0, s, d, cs_agg, cs_first);
+        TRY(launched());
+        TRY(ovf_scan_tiles(d_temp, &temp, d, cs_agg, cs_incl, ntc, s));
+        hipLaunchKernelGGL(k_cscan_fix, dim3(ntc), dim3(CS_T), 0, s, d, cs_incl, cs_first);
+    }
+    TRY(launched());
+    if (ncand) TRY(ovf_scans(d_temp, &temp, d, 2, s));
+    hipLaunchKernelGGL(k_ovf_link, cgrid, blk, 0, s, d);
     hipLaunchKernelGGL(k_ovf_walk, grid, blk, 0, s, a, d);
-    if (a.impact) hipLaunchKernelGGL(k_ovf_impacts, grid, blk, 0, s, a, d);
+    if (a.impact) hipLaunchKernelGGL(k_ovf_impacts, cgrid, blk, 0, s, a, d);
     hipLaunchKernelGGL(k_ovf_finish, dim3((uint32_t)((novf + 255) / 256)), blk, 0, s, a, d);
     TRY(launched());
     if (prof) (void)hipEventRecord(ctx->ev[7], s);

@@ -31,10 +31,13 @@
 //   k_ovf_classify                  record / candidate / no-op, record impacts, App. A.3 check
 //   inclusive count of records by row -> epoch
 //   k_ovf_epochs, k_ovf_ckeys       the row's record list; candidate keys (epoch's record, cid)
-//   stable radix sort of the candidates by (epoch, cid): a group keeps application order
+//   k_ovf_ccompact                  the candidates compacted (scan of flags), then a stable radix
+//                                   sort by (epoch, cid): a group keeps application order; the
+//                                   rest of the sorted key array is ~0
 //   k_ovf_cgather                   the candidates' cell keys in candidate-sorted order
-//   inclusive argmax-scan by group (-> W and every prefix) over the gathered 32-B keys; group
-//   start = plain max-scan of the group heads' indices [prims.hip]
+//   k_cscan_*                       inclusive argmax-scan by group (-> W and every prefix), keys
+//                                   compared in registers; group start = plain max-scan of the
+//                                   group heads' indices [prims.hip]
 //   k_ovf_link                      each group's end is linked under its epoch's record
 //   k_ovf_walk                      one thread per row: the walk over its records, emission;
 //                                   rows outside App. A.3 run the sequential fold instead
@@ -58,6 +61,7 @@ struct OvfDev {
     uint32_t cid_bits;          // a candidate key is (epoch's record position) << cid_bits | cid
     uint32_t rshift;            // a record's sort key is dense row << rshift | compact position
     uint32_t pm;                // compact position of batch change i: pm + i (prior rows: their slice index < pm)
+    uint32_t ncand;             // candidates: candidate-sorted indices [0, ncand) (the rest of ckey_s is ~0)
     const uint32_t *koff;       // [G + 1] bucket base offsets
     const uint32_t *slot_off;   // [G] row-hash slot region, next_pow2(2 n) words each
     // per record (kb + i)
@@ -112,12 +116,6 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b) {
     if (a.sr != b.sr) return a.sr > b.sr ? 1 : -1;
     return 0;
 }
-
-// argmax by cell key over candidate-sorted indices, the earlier one on ties (x precedes y)
-struct OvfArgmax {
-    const OvfKey *q;
-    __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return ovf_kcmp(q[y], q[x]) > 0 ? y : x; }
-};
 
 #define OVF_LOOP(i, N) for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (N); i += gridDim.x * blockDim.x)
 
@@ -254,12 +252,22 @@ static __global__ void k_ovf_ckeys(OvfDev d) {
             k = ((uint64_t)R << d.cid_bits) | cid;
         }
         d.ckey[p] = k;
-        d.cval[p] = p;
+        d.slots[p] = k != ~0ULL ? 1u : 0u;  // (the row-hash slots are free by now)
+    }
+}
+
+// candidates only, in order (inclusive scan of the flags at slots + K), for the candidate sort
+static __global__ void k_ovf_ccompact(OvfDev d) {
+    OVF_LOOP(p, d.K) {
+        if (!d.slots[p]) continue;
+        const uint32_t j = d.slots[d.K + p] - 1;
+        d.key[j] = d.ckey[p];
+        d.val[j] = p;
     }
 }
 
 static __global__ void k_ovf_cgather(OvfDev d) {
-    OVF_LOOP(q, d.K) {
+    OVF_LOOP(q, d.ncand) {
         const uint32_t p = d.cval_s[q];
         const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
         d.qkey[q] = OvfKey{d.cv[x], d.vk0[x], d.vk1[x], d.vmeta[x], d.srank[x]};
@@ -267,9 +275,9 @@ static __global__ void k_ovf_cgather(OvfDev d) {
 }
 
 static __global__ void k_ovf_link(OvfDev d) {
-    OVF_LOOP(q, d.K) {
+    OVF_LOOP(q, d.ncand) {
         const uint64_t k = d.ckey_s[q];
-        if (k == ~0ULL || (q + 1 < d.K && d.ckey_s[q + 1] == k)) continue;
+        if (q + 1 < d.ncand && d.ckey_s[q + 1] == k) continue;
         d.nxt[q] = atomicExch(&d.head[(uint32_t)(k >> d.cid_bits)], q + 1);
     }
 }
@@ -392,9 +400,8 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
 }
 
 static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
-    OVF_LOOP(q, d.K) {
+    OVF_LOOP(q, d.ncand) {
         const uint64_t k = d.ckey_s[q];
-        if (k == ~0ULL) continue;
         if (d.rbad[d.rowid[(uint32_t)(k >> d.cid_bits)]]) continue;
         const uint32_t p = d.cval_s[q];
         const uint32_t pos = d.pos[d.koff[d.pb[p]] + d.val_s[p]];
@@ -415,6 +422,152 @@ static __global__ void k_ovf_finish(MergeArgs a, OvfDev d) {
         a.out_flags[bb] = d.oflag[b];
         atomicAdd(&a.misc[2], (unsigned long long)d.ocnt[b]);
     }
+}
+
+// Running argmax of the candidates by group (cbest): a segmented scan with the 32-B keys compared
+// in registers. k_cscan_tile: each wave scans 8 chunks of 64 consecutive candidates (coalesced
+// loads, shuffle scan, carry from chunk to chunk), the workgroup combines its 4 waves; every
+// element after the tile's first group head is final. The tile aggregates are scanned by rocPRIM
+// (prims.hip, a few thousand entries), then k_cscan_fix gives each tile's leading open group its
+// carry.
+constexpr uint32_t CS_T = 256, CS_W = CS_T / 64, CS_C = 8, CS_TILE = CS_T * CS_C;
+
+struct CsAgg {
+    uint32_t head;  // a group starts inside
+    uint32_t best;  // running argmax of the last group (~0u: none)
+};
+
+// x precedes y; ~0u = none. The later one only when strictly greater (earliest on ties).
+__device__ inline uint32_t cs_pick(const OvfKey *qk, uint32_t x, uint32_t y) {
+    if (x == ~0u) return y;
+    if (y == ~0u) return x;
+    return ovf_kcmp(qk[y], qk[x]) > 0 ? y : x;
+}
+
+struct CsComb {
+    const OvfKey *qk;
+    __device__ inline CsAgg operator()(const CsAgg &a, const CsAgg &b) const {
+        return b.head ? b : CsAgg{a.head, cs_pick(qk, a.best, b.best)};
+    }
+};
+
+__device__ inline OvfKey shfl_up_key(const OvfKey &k, int off) {
+    OvfKey r;
+    r.cv = __shfl_up(k.cv, off);
+    r.k0 = __shfl_up(k.k0, off);
+    r.k1 = __shfl_up(k.k1, off);
+    r.m = __shfl_up(k.m, off);
+    r.sr = __shfl_up(k.sr, off);
+    return r;
+}
+
+__device__ inline OvfKey shfl_key(const OvfKey &k, int src) {
+    OvfKey r;
+    r.cv = __shfl(k.cv, src);
+    r.k0 = __shfl(k.k0, src);
+    r.k1 = __shfl(k.k1, src);
+    r.m = __shfl(k.m, src);
+    r.sr = __shfl(k.sr, src);
+    return r;
+}
+
+static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tagg, uint32_t *tfirst) {
+    __shared__ uint32_t s_head[CS_W], s_best[CS_W], s_first[CS_W];
+    __shared__ OvfKey s_key[CS_W];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t t0 = blockIdx.x * CS_TILE, base = t0 + w * (CS_C * 64);
+    if (d.ckey_s[t0] == ~0ULL) {  // the non-candidates' key sorts last: no cbest is read there
+        if (threadIdx.x == 0) {
+            tagg[blockIdx.x] = CsAgg{1u, ~0u};
+            tfirst[blockIdx.x] = 0;
+        }
+        return;
+    }
+    uint32_t res[CS_C];
+    bool open[CS_C];
+    uint32_t ch = 0, cb = ~0u, first = CS_C * 64;  // wave carry: head seen, best; first head offset
+    OvfKey ck{};
+#pragma unroll
+    for (uint32_t c = 0; c < CS_C; c++) {
+        const uint32_t q = base + c * 64 + lane;
+        const bool valid = q < d.K;
+        uint32_t h = 0, b = ~0u;
+        OvfKey k{};
+        if (valid) {
+            const uint64_t kk = d.ckey_s[q];
+            h = (q == 0 || d.ckey_s[q - 1] != kk) ? 1u : 0u;
+            b = q;
+            k = d.qkey[q];
+        }
+        const uint64_t hb = __ballot(h != 0);
+        if (hb && first == CS_C * 64) first = c * 64 + (uint32_t)(__ffsll((unsigned long long)hb) - 1);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t lh = __shfl_up(h, off), lb = __shfl_up(b, off);
+            const OvfKey lk = shfl_up_key(k, off);
+            if ((int)lane >= off && !h) {
+                h = lh;
+                if (lb != ~0u && (b == ~0u || !(ovf_kcmp(k, lk) > 0))) {
+                    b = lb;
+                    k = lk;
+                }
+            }
+        }
+        if (!h && cb != ~0u && (b == ~0u || !(ovf_kcmp(k, ck) > 0))) {
+            b = cb;
+            k = ck;
+        }
+        res[c] = b;
+        open[c] = !h && !ch;
+        ch |= __shfl(h, 63);
+        cb = __shfl(b, 63);
+        ck = shfl_key(k, 63);
+    }
+    if (lane == 0) {
+        s_head[w] = ch;
+        s_best[w] = cb;
+        s_key[w] = ck;
+        s_first[w] = w * (CS_C * 64) + first;
+    }
+    __syncthreads();
+    // carry from the earlier waves of the tile
+    uint32_t pb = ~0u;
+    for (uint32_t v = 0; v < w; v++) {
+        if (s_head[v]) pb = s_best[v];
+        else if (s_best[v] != ~0u && (pb == ~0u || ovf_kcmp(s_key[v], d.qkey[pb]) > 0)) pb = s_best[v];
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < CS_C; c++) {
+        const uint32_t q = base + c * 64 + lane;
+        if (q >= d.K) continue;
+        d.cbest[q] = open[c] ? cs_pick(d.qkey, pb, res[c]) : res[c];
+    }
+    if (threadIdx.x == 0) {
+        CsAgg agg{0u, ~0u};
+        uint32_t f = CS_TILE;
+        for (uint32_t v = 0; v < CS_W; v++) {
+            if (s_head[v]) {
+                agg.head = 1;
+                agg.best = s_best[v];
+                if (f == CS_TILE) f = s_first[v];
+            } else {
+                agg.best = cs_pick(d.qkey, agg.best, s_best[v]);
+            }
+        }
+        tagg[blockIdx.x] = agg;
+        tfirst[blockIdx.x] = f;
+    }
+}
+
+// tincl: inclusive scan of the tile aggregates; tile t's leading open group takes tincl[t - 1]
+static __global__ void __launch_bounds__(CS_T) k_cscan_fix(OvfDev d, const CsAgg *tincl, const uint32_t *tfirst) {
+    const uint32_t t = blockIdx.x;
+    if (t == 0) return;
+    const uint32_t c = tincl[t - 1].best;
+    const uint32_t t0 = t * CS_TILE;
+    if (c == ~0u || d.ckey_s[t0] == ~0ULL) return;
+    const uint32_t e = min(d.K, t0 + tfirst[t]);
+    for (uint32_t q = t0 + threadIdx.x; q < e; q += CS_T) d.cbest[q] = cs_pick(d.qkey, c, d.cbest[q]);
 }
 
 #undef OVF_LOOP

@@ -47,8 +47,8 @@ struct OvfHead {
 };
 
 // Segmented scans of the device-wide overflow path (ovf_kernels.h): which = 0 L (exclusive max of
-// cl by row), 1 epoch counts (inclusive count of records by row), 2 running argmax (by group) and
-// group start (plain max-scan) of the candidates, over candidate-sorted indices. temp == nullptr ->
+// cl by row), 1 epoch counts (inclusive count of records by row), 2 group start of the candidates
+// (plain max-scan over candidate-sorted indices; their running argmax is k_cscan_* in ovf_kernels.h). temp == nullptr ->
 // *temp_bytes = the largest size any of them needs.
 int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStream_t s) {
     const size_t K = d.K;
@@ -56,17 +56,14 @@ int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStr
     const rocprim::counting_iterator<uint32_t> idx(0u);
     const auto heads = rocprim::make_transform_iterator(idx, OvfHead{d.ckey_s});
     if (!temp) {
-        size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        size_t t0 = 0, t1 = 0, t3 = 0;
         e = rocprim::exclusive_scan_by_key(nullptr, t0, d.rowid, d.cl_s, d.lx, 0u, K, OvfMax{},
                                            rocprim::equal_to<uint32_t>(), s);
         if (e == hipSuccess)
             e = rocprim::inclusive_scan_by_key(nullptr, t1, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
                                                rocprim::equal_to<uint32_t>(), s);
-        if (e == hipSuccess)
-            e = rocprim::inclusive_scan_by_key(nullptr, t2, d.ckey_s, idx, d.cbest, K, OvfArgmax{d.qkey},
-                                               rocprim::equal_to<uint64_t>(), s);
         if (e == hipSuccess) e = rocprim::inclusive_scan(nullptr, t3, heads, d.cgs, K, OvfMax{}, s);
-        *temp_bytes = std::max(std::max(t0, t1), std::max(t2, t3));
+        *temp_bytes = std::max(std::max(t0, t1), t3);
     } else if (which == 0) {
         e = rocprim::exclusive_scan_by_key(temp, *temp_bytes, d.rowid, d.cl_s, d.lx, 0u, K, OvfMax{},
                                            rocprim::equal_to<uint32_t>(), s);
@@ -74,11 +71,17 @@ int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStr
         e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.rowid, d.recf, d.epc, K, rocprim::plus<uint32_t>(),
                                            rocprim::equal_to<uint32_t>(), s);
     } else {
-        e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, d.ckey_s, idx, d.cbest, K, OvfArgmax{d.qkey},
-                                           rocprim::equal_to<uint64_t>(), s);
-        if (e == hipSuccess) e = rocprim::inclusive_scan(temp, *temp_bytes, heads, d.cgs, K, OvfMax{}, s);
+        e = rocprim::inclusive_scan(temp, *temp_bytes, heads, d.cgs, (size_t)d.ncand, OvfMax{}, s);
     }
     if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("segmented scan: ") + hipGetErrorString(e));
+    return CORRO_OK;
+}
+
+// inclusive segmented scan of the candidate argmax's tile aggregates (k_cscan_tile)
+int ovf_scan_tiles(void *temp, size_t *temp_bytes, const OvfDev &d, const CsAgg *in, CsAgg *out, uint32_t n,
+                   hipStream_t s) {
+    const hipError_t e = rocprim::inclusive_scan(temp, *temp_bytes, in, out, (size_t)n, CsComb{d.qkey}, s);
+    if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("tile scan: ") + hipGetErrorString(e));
     return CORRO_OK;
 }
 
