@@ -315,7 +315,7 @@ int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t 
     if (!rc) rc = ctx->d_bflags.ensure(((B + 31) / 32) * 4ULL);
     if (!rc) rc = ctx->d_misc.ensure(8 * 8);
     if (!rc) rc = ctx->d_ovf_list.ensure(B * 4ULL);
-    if (!rc) rc = ctx->d_gen_list.ensure(B * 4ULL);
+    if (!rc) rc = ctx->d_gen_list.ensure(3 * B * 4ULL);
     if (!rc) rc = ctx->d_wide_list.ensure(B * 4ULL);
     if (!rc) rc = ctx->d_state[0].ensure(64);
     if (!rc) rc = ctx->d_state[1].ensure(64);
@@ -633,6 +633,10 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
         CORRO_HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_merge_fast_wide<false>, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
     }
+    CORRO_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_merge_gen_small, dim3(std::min(B, 4 * LIST_GRID)), dim3(GEN_SMALL_THREADS), 0, s, a, B);
+    CORRO_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_merge_gen_mid, dim3(std::min(B, 2 * LIST_GRID)), dim3(GEN_SMALL_THREADS), 0, s, a, B);
     CORRO_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_merge_gen, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());

@@ -56,9 +56,9 @@ struct MergeArgs {
     uint32_t nsites;
     uint8_t *impact;
     unsigned long long *misc;  // [0] error bits [1] overflow buckets [2] rows written [3] wide values
-                               // [4] general buckets [5] wide fast buckets
+                               // [4] general buckets [5] wide fast buckets [6] small, [7] mid general buckets
     uint32_t *ovf_list;
-    uint32_t *gen_list;        // buckets for k_merge_gen (pushed by k_merge_fast_int)
+    uint32_t *gen_list;        // [B] buckets for k_merge_gen, then k_merge_gen_small, k_merge_gen_mid
     uint32_t *wide_list;       // buckets for k_merge_fast_wide
     uint32_t force_general;    // route every non-empty bucket through the sequential general body
     uint32_t track_ts;
@@ -801,8 +801,23 @@ __device__ inline void gen_rowkeys(const BucketView &v, const GenArrays &g, bool
 // record moves to its rank by position within its row: a handful of barriers instead of a
 // bitonic network's 66. Returns (in *s_long) whether some row is longer than LONG_ROW; g.ccid /
 // g.csrc are free again afterwards (the fold's cell scratch). C = ceil(n / blockDim.x) <= GEN_C.
-constexpr uint32_t GEN_C = (CAP_GEN + MERGE_THREADS - 1) / MERGE_THREADS;
+// The general body comes in two sizes: CAP_GEN records (one 131 KB workgroup per CU) and
+// CAP_GEN_SMALL (32 KB, 256 threads, four per CU) and CAP_GEN_MID (64 KB, 256 threads, two per CU)
+// for the many small general buckets, so that their barrier- and latency-bound phases overlap
+// across workgroups.
+constexpr uint32_t CAP_GEN_SMALL = 512, CAP_GEN_MID = 1024;
 
+constexpr uint32_t GEN_SMALL_THREADS = 256;
+
+template <uint32_t CAP, uint32_t THREADS = MERGE_THREADS>
+struct GenCfg {
+    static constexpr uint32_t C = (CAP + THREADS - 1) / THREADS;  // records per thread
+    static constexpr uint32_t SLOTS = 2 * CAP;                                // row table (pow2 >= CAP)
+    static constexpr size_t LDS = (size_t)CAP * (8 + 8 + 4 + 4 + 4) + (size_t)SLOTS * 4 + (size_t)CAP * (8 + 4) +
+                                  (size_t)CAP * (4 + 4 + 8);
+};
+
+template <uint32_t GEN_C>
 __device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32_t *s_wsum, uint32_t *s_long) {
     const uint32_t n = v.np + v.nn;
     const uint32_t tid = threadIdx.x, nth = blockDim.x;
@@ -894,8 +909,7 @@ __device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32
     __syncthreads();
 }
 
-constexpr size_t GEN_LDS = (size_t)CAP_GEN * (8 + 8 + 4 + 4 + 4) + (size_t)GEN_SLOTS * 4 +
-                           (size_t)CAP_GEN * (8 + 4) + (size_t)CAP_GEN * (4 + 4 + 8);
+static_assert(GenCfg<CAP_GEN>::SLOTS == GEN_SLOTS, "row table of the large general body");
 
 __device__ inline void bucket_view(const MergeArgs &a, uint32_t b, BucketView &v) {
     v.np = a.prior_cnt[b];
@@ -1279,7 +1293,14 @@ k_merge_fast_int(MergeArgs a) {
         return;
     }
     if (a.force_general || pflag || ((bword >> (b & 31)) & 1u)) {
-        if (threadIdx.x == 0) a.gen_list[atomicAdd(&a.misc[4], 1ULL)] = b;
+        if (threadIdx.x == 0) {
+            if (n <= CAP_GEN_SMALL)
+                a.gen_list[gridDim.x + atomicAdd(&a.misc[6], 1ULL)] = b;  // (grid = one WG per bucket)
+            else if (n <= CAP_GEN_MID)
+                a.gen_list[2 * gridDim.x + atomicAdd(&a.misc[7], 1ULL)] = b;
+            else
+                a.gen_list[atomicAdd(&a.misc[4], 1ULL)] = b;
+        }
         return;
     }
     if (n > (uint32_t)CAP_FAST) {
@@ -1316,14 +1337,16 @@ k_merge_fast_wide(MergeArgs a) {
 
 // General body in LDS for one queued bucket: sort (row, position), one lane per row folds the
 // cr-sqlite rules. Buckets larger than LDS are passed on to the overflow path (k_ovf_*).
+template <uint32_t CAP, uint32_t THREADS>
 __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[GEN_LDS];
+    using Cfg = GenCfg<CAP, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[Cfg::LDS];
     __shared__ uint32_t s_outcnt, s_flag;
     const uint32_t tid = threadIdx.x;
     BucketView v;
     bucket_view(a, b, v);
     const uint32_t n = v.np + v.nn;
-    if (n > (uint32_t)CAP_GEN) {
+    if (n > CAP) {
         if (tid == 0) push_overflow(a, b);
         return;
     }
@@ -1335,25 +1358,25 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
     }
     GenArrays g;
     uint8_t *p = smem;
-    g.pk = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
-    g.cv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
-    g.key = reinterpret_cast<uint64_t *>(p); p += CAP_GEN * 8;
-    g.ccv = reinterpret_cast<int64_t *>(p); p += CAP_GEN * 8;
-    g.tc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-    g.cl = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-    g.pos = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-    g.val = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-    g.ccid = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
-    g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP_GEN * 4;
+    g.pk = reinterpret_cast<uint64_t *>(p); p += CAP * 8;
+    g.cv = reinterpret_cast<int64_t *>(p); p += CAP * 8;
+    g.key = reinterpret_cast<uint64_t *>(p); p += CAP * 8;
+    g.ccv = reinterpret_cast<int64_t *>(p); p += CAP * 8;
+    g.tc = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.cl = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.pos = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.val = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.ccid = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
     g.own = reinterpret_cast<uint32_t *>(p);
-    g.slots = GEN_SLOTS;
+    g.slots = Cfg::SLOTS;
     g.rshift = 32;
     g.P = n;
     __shared__ uint32_t s_long, s_wsum[MERGE_THREADS / 64];
     if (tid == 0) s_long = 0;
     // a row longer than LONG_ROW would serialise this bucket on one lane: the overflow path
     // folds it with device-wide scans instead (ovf_kernels.h)
-    gen_group(v, g, s_wsum, &s_long);
+    gen_group<Cfg::C>(v, g, s_wsum, &s_long);
     if (s_long) {
         if (tid == 0) push_overflow(a, b);
         return;
@@ -1373,7 +1396,27 @@ static __global__ void __launch_bounds__(MERGE_THREADS)
 k_merge_gen(MergeArgs a) {
     const uint32_t cnt = (uint32_t)a.misc[4];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
-        gen_bucket(a, a.gen_list[k]);
+        gen_bucket<CAP_GEN, MERGE_THREADS>(a, a.gen_list[k]);
+        __syncthreads();
+    }
+}
+
+// general buckets of at most CAP_GEN_MID records (queued at gen_list + 2B, count misc[7])
+static __global__ void __launch_bounds__(GEN_SMALL_THREADS, 2)
+k_merge_gen_mid(MergeArgs a, uint32_t B) {
+    const uint32_t cnt = (uint32_t)a.misc[7];
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+        gen_bucket<CAP_GEN_MID, GEN_SMALL_THREADS>(a, a.gen_list[2 * B + k]);
+        __syncthreads();
+    }
+}
+
+// general buckets of at most CAP_GEN_SMALL records (queued at gen_list + B, count misc[6])
+static __global__ void __launch_bounds__(GEN_SMALL_THREADS, 4)
+k_merge_gen_small(MergeArgs a, uint32_t B) {
+    const uint32_t cnt = (uint32_t)a.misc[6];
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+        gen_bucket<CAP_GEN_SMALL, GEN_SMALL_THREADS>(a, a.gen_list[B + k]);
         __syncthreads();
     }
 }
