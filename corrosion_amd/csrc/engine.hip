@@ -180,6 +180,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     uint32_t rbits = 1;
     while ((1ULL << rbits) < nrows) rbits++;
     const uint32_t key_bits = rbits + pbits;
+    d.nrows = nrows;
     if (key_bits > 64) return fail(CORRO_E_RANGE, "overflow sort key exceeds 64 bits");
     static const bool dbg = std::getenv("CORRO_HIP_OVF_DEBUG") != nullptr;
     if (dbg)
@@ -221,7 +222,10 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     TRY(launched());
     if (ncand) TRY(ovf_scans(d_temp, &temp, d, 2, s));
     hipLaunchKernelGGL(k_ovf_link, cgrid, blk, 0, s, d);
-    hipLaunchKernelGGL(k_ovf_walk, grid, blk, 0, s, a, d);
+    // carried cells in registers when no table has WALK_MAXC or more columns (cids 1..ncols)
+    auto walk = maxc + 1 <= WALK_MAXC ? k_ovf_walk<true> : k_ovf_walk<false>;
+    hipLaunchKernelGGL(walk, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nrows + 255) / 256, 8192))),
+                       blk, 0, s, a, d);
     if (a.impact) hipLaunchKernelGGL(k_ovf_impacts, cgrid, blk, 0, s, a, d);
     hipLaunchKernelGGL(k_ovf_finish, dim3((uint32_t)((novf + 255) / 256)), blk, 0, s, a, d);
     TRY(launched());

@@ -62,6 +62,7 @@ struct OvfDev {
     uint32_t rshift;            // a record's sort key is dense row << rshift | compact position
     uint32_t pm;                // compact position of batch change i: pm + i (prior rows: their slice index < pm)
     uint32_t ncand;             // candidates: candidate-sorted indices [0, ncand) (the rest of ckey_s is ~0)
+    uint32_t nrows;             // rows (dense ids [0, nrows))
     const uint32_t *koff;       // [G + 1] bucket base offsets
     const uint32_t *slot_off;   // [G] row-hash slot region, next_pow2(2 n) words each
     // per record (kb + i)
@@ -282,9 +283,80 @@ static __global__ void k_ovf_link(OvfDev d) {
     }
 }
 
-// clock rows of one walked row (rf_emit on the global arrays)
-__device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b, const BucketView &v, uint32_t j0,
-                                uint32_t ncell, uint32_t rpos) {
+// The walk's carried cells (cid, source position, zeroed flag) for one row, in insertion order:
+// in registers when every table has fewer than WALK_MAXC columns (dynamic indices resolved by
+// unrolled compares, so nothing goes to scratch), else in the global scratch at the row's start.
+constexpr uint32_t WALK_MAXC = 8;
+
+template <bool REG>
+struct WalkCells;
+
+template <>
+struct WalkCells<true> {
+    uint32_t cid_[WALK_MAXC], pos_[WALK_MAXC], z_[WALK_MAXC];
+    __device__ inline WalkCells(const OvfDev &, uint32_t) {}
+    __device__ inline uint32_t pos(uint32_t c) const {
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < WALK_MAXC; i++) r = i == c ? pos_[i] : r;
+        return r;
+    }
+    __device__ inline uint32_t z(uint32_t c) const {
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < WALK_MAXC; i++) r = i == c ? z_[i] : r;
+        return r;
+    }
+    __device__ inline void zero_all() {
+#pragma unroll
+        for (uint32_t i = 0; i < WALK_MAXC; i++) z_[i] = 1;
+    }
+    __device__ inline int find(uint32_t cid, uint32_t n) const {
+        int f = -1;
+#pragma unroll
+        for (uint32_t i = 0; i < WALK_MAXC; i++)
+            if (f < 0 && i < n && cid_[i] == cid) f = (int)i;
+        return f;
+    }
+    __device__ inline void put(uint32_t c, uint32_t cid, uint32_t p, uint32_t zz) {
+#pragma unroll
+        for (uint32_t i = 0; i < WALK_MAXC; i++)
+            if (i == c) {
+                cid_[i] = cid;
+                pos_[i] = p;
+                z_[i] = zz;
+            }
+    }
+};
+
+template <>
+struct WalkCells<false> {
+    uint32_t *cid_, *pos_, *z_;
+    __device__ inline WalkCells(const OvfDev &d, uint32_t j0) : cid_(d.scid + j0), pos_(d.spos + j0), z_(d.sz + j0) {}
+    __device__ inline uint32_t pos(uint32_t c) const { return pos_[c]; }
+    __device__ inline uint32_t z(uint32_t c) const { return z_[c]; }
+    uint32_t n_ = 0;
+    __device__ inline void zero_all() {
+        for (uint32_t c = 0; c < n_; c++) z_[c] = 1;
+    }
+    __device__ inline int find(uint32_t cid, uint32_t n) {
+        n_ = n;
+        for (uint32_t c = 0; c < n; c++)
+            if (cid_[c] == cid) return (int)c;
+        return -1;
+    }
+    __device__ inline void put(uint32_t c, uint32_t cid, uint32_t p, uint32_t zz) {
+        cid_[c] = cid;
+        pos_[c] = p;
+        z_[c] = zz;
+        if (c + 1 > n_) n_ = c + 1;
+    }
+};
+
+// clock rows of one walked row (rf_emit on the carried cells)
+template <bool REG>
+__device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b, const BucketView &v,
+                                const WalkCells<REG> &cells_, uint32_t ncell, uint32_t rpos) {
     const uint32_t kb = d.koff[b];
     const uint32_t xr = kb + d.val_s[rpos];
     const uint32_t clr = d.cl[xr], cidr = d.tc[xr] & 0xFFFFu;
@@ -315,9 +387,9 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b,
     }
     if (!cells) return;
     for (uint32_t c = 0; c < ncell; c++) {
-        Rec r = load_rec(v.at(d.val_s[d.spos[j0 + c]]));
+        Rec r = load_rec(v.at(d.val_s[cells_.pos(c)]));
         const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
-        if (d.sz[j0 + c]) r.cv = 0;
+        if (cells_.z(c)) r.cv = 0;
         r.cl = (uint32_t)rowcl;
         r.pos = k;
         store_rec(outb + k, r);
@@ -326,10 +398,10 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b,
     }
 }
 
+template <bool REG>
 static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
-    OVF_LOOP(j0, d.K) {
-        const uint32_t row = d.rowid[j0];
-        if (j0 > 0 && d.rowid[j0 - 1] == row) continue;  // one thread per row
+    OVF_LOOP(row, d.nrows) {  // one thread per row (dense ids), every lane busy
+        const uint32_t j0 = d.rstart[row];
         const uint32_t b = d.pb[j0];
         const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
         BucketView v;
@@ -357,24 +429,32 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
         }
         const uint32_t nrec = d.rnrec[row];
         uint32_t ncell = 0;
-        for (uint32_t k = 0; k < nrec; k++) {
+        WalkCells<REG> cs(d, j0);
+        // A delete record (even cl) drops every cell, so without impacts (which need every epoch's
+        // carried cells, fstg) the walk starts at the row's last delete: hot rows skip their history.
+        uint32_t k0 = 0;
+        if (!a.impact)
+            for (uint32_t k = nrec; k-- > 0;)
+                if ((d.cl[kb + d.val_s[d.recs[j0 + k]]] & 1u) == 0) {
+                    k0 = k;
+                    break;
+                }
+        for (uint32_t k = k0; k < nrec; k++) {
             const uint32_t R = d.recs[j0 + k];
             const uint32_t xR = kb + d.val_s[R];
             if ((d.cl[xR] & 1u) == 0) {
                 ncell = 0;
                 continue;
             }
-            for (uint32_t c = 0; c < ncell; c++) d.sz[j0 + c] = 1;
+            cs.find(0xFFFFFFFFu, ncell);  // (sizes the global store's zeroing)
+            cs.zero_all();
             auto set = [&](uint32_t cid, uint32_t p, uint32_t z) {
-                for (uint32_t c = 0; c < ncell; c++)
-                    if (d.scid[j0 + c] == cid) {
-                        d.spos[j0 + c] = p;
-                        d.sz[j0 + c] = z;
-                        return;
-                    }
-                d.scid[j0 + ncell] = cid;
-                d.spos[j0 + ncell] = p;
-                d.sz[j0 + ncell] = z;
+                const int f = cs.find(cid, ncell);
+                if (f >= 0) {
+                    cs.put((uint32_t)f, cid, p, z);
+                    return;
+                }
+                cs.put(ncell, cid, p, z);
                 ncell++;
             };
             const uint32_t cidR = d.tc[xR] & 0xFFFFu;
@@ -382,20 +462,14 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
             for (uint32_t h = d.head[R]; h; h = d.nxt[h - 1]) {
                 const uint32_t qe = h - 1;  // the group's last candidate
                 const uint32_t cid = (uint32_t)d.ckey_s[qe] & ((1u << d.cid_bits) - 1);
-                int found = -1;
-                for (uint32_t c = 0; c < ncell; c++)
-                    if (d.scid[j0 + c] == cid) {
-                        found = (int)c;
-                        break;
-                    }
-                d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((d.spos[j0 + found] + 1) | (d.sz[j0 + found] << 31));
+                const int found = cs.find(cid, ncell);
+                const uint32_t fp = found < 0 ? 0u : cs.pos((uint32_t)found), fz = found < 0 ? 0u : cs.z((uint32_t)found);
+                d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((fp + 1) | (fz << 31));
                 const uint32_t wq = d.cbest[qe];
-                if (found < 0 ||
-                    ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(d, d.spos[j0 + found], d.sz[j0 + found] != 0)) > 0)
-                    set(cid, d.cval_s[wq], 0);
+                if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(d, fp, fz != 0)) > 0) set(cid, d.cval_s[wq], 0);
             }
         }
-        if (nrec) ovf_emit(a, d, b, v, j0, ncell, d.recs[j0 + nrec - 1]);
+        if (nrec) ovf_emit<REG>(a, d, b, v, cs, ncell, d.recs[j0 + nrec - 1]);
     }
 }
 
