@@ -1265,11 +1265,188 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
     }
 }
 
+// The INTEGER form of fast_body_impact in 76 KB of LDS (two workgroups per CU instead of one): a
+// cell's members are placed in application order (each member's rank among its cell's positions),
+// so "earlier" is the member index and no position array is kept for the walk; the hashing arrays
+// are reused for the ordered keys.
+__device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, const BucketView &v) {
+    __shared__ uint64_t s_a[CAP_FAST];      // hashing: pk; then the cell-ordered biased col_versions
+    __shared__ uint32_t s_b[CAP_FAST];      // hashing: table_cid; then positions by member slot; then site ranks
+    __shared__ uint64_t s_c[CAP_FAST];      // cell-ordered values
+    __shared__ uint32_t s_own[FAST_SLOTS];  // hashing: slot owners; then member counts / offsets / ends
+    __shared__ uint32_t s_wsum[MERGE_THREADS / 64];
+    __shared__ uint32_t s_outcnt;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = v.np + v.nn;
+    Rec *outb = a.out + a.out_off[b];
+    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    uint64_t cv[FAST_R], v0[FAST_R], pk[FAST_R], dbv[FAST_R];
+    uint32_t cell[FAST_R], seq[FAST_R], site[FAST_R], pos[FAST_R], rank[FAST_R], tc[FAST_R];
+    uint32_t md[FAST_R];  // member range begin | own member slot << 16 (both < CAP_FAST); end = s_own[cell]
+    bool alive[FAST_R];
+    uint4 q[FAST_R][4];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    if (tid == 0) s_outcnt = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        alive[k] = i < n;
+        cell[k] = 0;
+        const Rec r = rec_from_wave_quads(q[k]);
+        pk[k] = r.pk;
+        tc[k] = r.tcid;
+        s_a[i] = r.pk;
+        s_b[i] = r.tcid;
+        cv[k] = (uint64_t)r.cv ^ 0x8000000000000000ULL;
+        v0[k] = r.v0 ^ 0x8000000000000000ULL;  // INTEGER order as unsigned
+        pos[k] = r.pos;
+        site[k] = r.site;
+        dbv[k] = (uint64_t)r.dbv;
+        seq[k] = r.seq;
+    }
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) rank[k] = a.site_rank[site[k] < a.nsites ? site[k] : 0u];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) rank[k] = site[k] < a.nsites ? rank[k] : 0u;
+    __syncthreads();
+    // 1. cells: open addressing on (pk, table_cid), owner = first claimer
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (!alive[k]) continue;
+        uint32_t slot = cell_hash(pk[k], tc[k]) & (FAST_SLOTS - 1);
+        while (true) {
+            const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
+            if (o == 0) {
+                cell[k] = i;
+                break;
+            }
+            if (s_a[o - 1] == pk[k] && s_b[o - 1] == tc[k]) {
+                cell[k] = o - 1;
+                break;
+            }
+            slot = (slot + 1) & (FAST_SLOTS - 1);
+        }
+    }
+    __syncthreads();
+    // 2. member counts per owner, exclusive scan -> offsets
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) atomicAdd(&s_own[cell[k]], 1u);
+    __syncthreads();
+    {
+        const uint32_t i0 = tid * FAST_R;
+        uint32_t c[FAST_R], loc = 0;
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            c[k] = i0 + k < n ? s_own[i0 + k] : 0u;
+            loc += c[k];
+        }
+        const uint32_t lane = tid & 63, w = tid >> 6;
+        uint32_t inc = loc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        if (lane == 63) s_wsum[w] = inc;
+        __syncthreads();
+        uint32_t run = inc - loc;
+        for (uint32_t ww = 0; ww < w; ww++) run += s_wsum[ww];
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++)
+            if (i0 + k < n) {
+                s_own[i0 + k] = run;
+                run += c[k];
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) md[k] = alive[k] ? s_own[cell[k]] : 0u;
+    __syncthreads();
+    // 3. positions by member slot, then each member's rank among its cell's positions
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) s_b[atomicAdd(&s_own[cell[k]], 1u)] = pos[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        if (!alive[k]) continue;
+        const uint32_t mb = md[k], me = s_own[cell[k]];
+        uint32_t r = 0;
+        for (uint32_t m = mb; m < me; m++) r += s_b[m] < pos[k] ? 1u : 0u;  // positions are distinct
+        md[k] = mb | ((mb + r) << 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) {
+            const uint32_t d = md[k] >> 16;
+            s_a[d] = cv[k];
+            s_c[d] = v0[k];
+            s_b[d] = rank[k];
+        }
+    __syncthreads();
+    // 4. one walk over the cell's members (application order) per change: impact (strict prefix
+    // maximum) and winner (maximum, earliest among equals)
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        if (!alive[k]) continue;
+        bool imp = true, win = true;
+        const uint32_t mb = md[k] & 0xFFFFu, d = md[k] >> 16, me = s_own[cell[k]];
+        for (uint32_t m = mb; m < me; m++) {
+            if (m == d) continue;
+            const uint64_t cj = s_a[m], vj = s_c[m];
+            const uint32_t rj = s_b[m];
+            const int c = cj != cv[k] ? (cj > cv[k] ? 1 : -1)
+                                      : (vj != v0[k] ? (vj > v0[k] ? 1 : -1) : (rj != rank[k] ? (rj > rank[k] ? 1 : -1) : 0));
+            const bool earlier = m < d;
+            if (earlier && c >= 0) imp = false;             // an earlier change already holds >= key
+            if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
+        }
+        if (a.impact && (pos[k] & BATCH_POS)) a.impact[pos[k] & 0x7FFFFFFFu] = imp ? 1 : 0;
+        alive[k] = win;
+    }
+    // 5. winners: the clock row (wave-cooperative 64-B stores)
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        uint32_t o = 0;
+        Rec x;
+        if (alive[k]) {
+            x.pk = pk[k];
+            x.cv = (int64_t)(cv[k] ^ 0x8000000000000000ULL);
+            x.dbv = (int64_t)dbv[k];
+            x.v0 = v0[k] ^ 0x8000000000000000ULL;
+            x.v1 = 0;
+            x.tcid = tc[k];
+            x.seq = seq[k];
+            x.site = site[k];
+            x.pos = pos[k];
+            x.meta = CORRO_INTEGER;
+            o = atomicAdd(&s_outcnt, 1u);
+            if (a.track_ts) outts[o] = rec_ts(a, v, x);
+            x.cl = 1;
+            x.pos = o;
+        }
+        store_rec_wave(outb, o, x, alive[k]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.out_cnt[b] = s_outcnt;
+        a.out_flags[b] = 0;
+        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+    }
+}
+
 // Bucket triage + the INTEGER fast body (one workgroup per bucket). General buckets and, for a
 // batch with non-INTEGER values, every fast bucket are queued for the list-driven kernels below,
 // so those launch a few hundred workgroups instead of one per bucket.
 template <bool IMPACT>
-static __global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
+static __global__ void __launch_bounds__(MERGE_THREADS, 4)
 k_merge_fast_int(MergeArgs a) {
     const uint32_t b = blockIdx.x;
     // every per-bucket word is loaded up front (independent scalar loads, one latency)
@@ -1311,8 +1488,8 @@ k_merge_fast_int(MergeArgs a) {
         if (threadIdx.x == 0) a.wide_list[atomicAdd(&a.misc[5], 1ULL)] = b;
         return;
     }
-    if (IMPACT)
-        fast_body_impact<false>(a, b, v);
+    if constexpr (IMPACT)
+        fast_body_impact_int(a, b, v);
     else
         fast_body<false>(a, b, v);
 }
