@@ -128,12 +128,12 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         d.ocnt = (uint32_t *)take(novf * 4);
         d.oflag = (uint32_t *)take(novf * 4);
         d.slots = (uint32_t *)take(S * 4);
-        uint64_t **u64s[] = {&d.pk, &d.vk0, &d.vk1, &d.key, &d.key_s, &d.ckey, &d.ckey_s};
+        uint64_t **u64s[] = {&d.pk, &d.key, &d.key_s, &d.ckey, &d.ckey_s};
         for (uint64_t **p : u64s) *p = (uint64_t *)take(K * 8);
         d.cv = (int64_t *)take(K * 8);
         d.ccv = (int64_t *)take(K * 8);
         d.qkey = (OvfKey *)take(K * sizeof(OvfKey));
-        uint32_t **u32s[] = {&d.tc,    &d.cl,     &d.pos,   &d.vmeta, &d.srank, &d.val,    &d.val_s, &d.rowid,
+        uint32_t **u32s[] = {&d.tc,    &d.cl,     &d.pos,   &d.val,    &d.val_s, &d.rowid,
                              &d.cl_s,  &d.lx,     &d.recf,  &d.epc,   &d.kind,  &d.pb,     &d.rstart, &d.rbad,
                              &d.rnrec, &d.recs,   &d.head,  &d.scid,  &d.spos,  &d.sz,     &d.ccid,  &d.csrc,
                              &d.cval,  &d.cval_s, &d.cbest, &d.cgs,   &d.nxt,   &d.fstg};
@@ -210,7 +210,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     if (dbg) fprintf(stderr, "[corro ovf] candidates %u\n", ncand);
     d.ncand = ncand;
     const dim3 cgrid((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((ncand + 255) / 256, 8192)));
-    hipLaunchKernelGGL(k_ovf_cgather, cgrid, blk, 0, s, d);
+    hipLaunchKernelGGL(k_ovf_cgather, cgrid, blk, 0, s, a, d);
     TRY(launched());
     if (ncand) {
         const uint32_t ntc = (ncand + CS_TILE - 1) / CS_TILE;  // <= nt

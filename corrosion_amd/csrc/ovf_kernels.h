@@ -68,8 +68,7 @@ struct OvfDev {
     // per record (kb + i)
     uint64_t *pk;
     int64_t *cv;
-    uint64_t *vk0, *vk1;
-    uint32_t *tc, *cl, *pos, *vmeta, *srank;
+    uint32_t *tc, *cl, *pos;
     // per sorted position
     uint64_t *key, *key_s;
     uint32_t *val, *val_s;      // local record index
@@ -99,9 +98,18 @@ __device__ inline uint32_t ovf_bucket_of(const OvfDev &d, uint32_t r) {
 }
 
 // by sorted position p
-__device__ inline OvfKey ovf_key_p(const OvfDev &d, uint32_t p, bool z) {
-    const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
-    return OvfKey{z ? 0 : d.cv[x], d.vk0[x], d.vk1[x], d.vmeta[x], d.srank[x]};
+// (the value words, metadata and site of a record are read from its staged 64-B record: only
+// candidates and carried cells need them, a small part of the overflow records)
+__device__ inline OvfKey ovf_key_rec(const MergeArgs &a, const OvfDev &d, uint32_t p, bool z) {
+    const uint32_t b = d.pb[p];
+    BucketView v;
+    bucket_view(a, a.ovf_list[b], v);
+    const Rec r = load_rec(v.at(d.val_s[p]));
+    return OvfKey{z ? 0 : r.cv, r.v0, r.v1, r.meta, site_rank_of(a, r.site)};
+}
+
+__device__ inline OvfKey ovf_key_p(const MergeArgs &a, const OvfDev &d, uint32_t p, bool z) {
+    return ovf_key_rec(a, d, p, z);
 }
 
 // by candidate-sorted index q
@@ -129,13 +137,9 @@ static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
         d.pb[r] = b;  // (buckets stay contiguous after the sort: also the bucket of position r)
         d.pk[r] = x.pk;
         d.cv[r] = x.cv;
-        d.vk0[r] = x.v0;
-        d.vk1[r] = x.v1;
         d.tc[r] = x.tcid;
         d.cl[r] = x.cl;
         d.pos[r] = x.pos;
-        d.vmeta[r] = x.meta;
-        d.srank[r] = site_rank_of(a, x.site);
     }
 }
 
@@ -267,11 +271,9 @@ static __global__ void k_ovf_ccompact(OvfDev d) {
     }
 }
 
-static __global__ void k_ovf_cgather(OvfDev d) {
+static __global__ void k_ovf_cgather(MergeArgs a, OvfDev d) {
     OVF_LOOP(q, d.ncand) {
-        const uint32_t p = d.cval_s[q];
-        const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
-        d.qkey[q] = OvfKey{d.cv[x], d.vk0[x], d.vk1[x], d.vmeta[x], d.srank[x]};
+        d.qkey[q] = ovf_key_rec(a, d, d.cval_s[q], false);
     }
 }
 
@@ -466,7 +468,7 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
                 const uint32_t fp = found < 0 ? 0u : cs.pos((uint32_t)found), fz = found < 0 ? 0u : cs.z((uint32_t)found);
                 d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((fp + 1) | (fz << 31));
                 const uint32_t wq = d.cbest[qe];
-                if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(d, fp, fz != 0)) > 0) set(cid, d.cval_s[wq], 0);
+                if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(a, d, fp, fz != 0)) > 0) set(cid, d.cval_s[wq], 0);
             }
         }
         if (nrec) ovf_emit<REG>(a, d, b, v, cs, ncell, d.recs[j0 + nrec - 1]);
@@ -484,7 +486,7 @@ static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
         const OvfKey kq = ovf_key_q(d, q);
         bool imp = first || ovf_kcmp(kq, ovf_key_q(d, d.cbest[q - 1])) > 0;
         const uint32_t fs = d.fstg[d.cgs[q]];
-        if (imp && fs) imp = ovf_kcmp(kq, ovf_key_p(d, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0)) > 0;
+        if (imp && fs) imp = ovf_kcmp(kq, ovf_key_p(a, d, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0)) > 0;
         a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
     }
 }
