@@ -640,7 +640,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     CORRO_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_merge_gen_small, dim3(std::min(B, 4 * LIST_GRID)), dim3(GEN_SMALL_THREADS), 0, s, a, B);
     CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_merge_gen_mid, dim3(std::min(B, 2 * LIST_GRID)), dim3(GEN_SMALL_THREADS), 0, s, a, B);
+    hipLaunchKernelGGL(k_merge_gen_mid, dim3(std::min(B, 2 * LIST_GRID)), dim3(MERGE_THREADS), 0, s, a, B);
     CORRO_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_merge_gen, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());

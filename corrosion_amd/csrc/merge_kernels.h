@@ -1579,11 +1579,11 @@ k_merge_gen(MergeArgs a) {
 }
 
 // general buckets of at most CAP_GEN_MID records (queued at gen_list + 2B, count misc[7])
-static __global__ void __launch_bounds__(GEN_SMALL_THREADS, 2)
+static __global__ void __launch_bounds__(MERGE_THREADS, 4)
 k_merge_gen_mid(MergeArgs a, uint32_t B) {
     const uint32_t cnt = (uint32_t)a.misc[7];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
-        gen_bucket<CAP_GEN_MID, GEN_SMALL_THREADS>(a, a.gen_list[2 * B + k]);
+        gen_bucket<CAP_GEN_MID, MERGE_THREADS>(a, a.gen_list[2 * B + k]);
         __syncthreads();
     }
 }
