@@ -1,38 +1,48 @@
 """Headline benchmark: merged column-changes/s of the batched crsql_changes merge on MI355X.
 
-Workload = BASELINE.json configs[1]: 64M (2^26) column changes, 1 table with 4 INTEGER columns,
-1000 actors, pk uniform in [1, 2^22], col_version uniform [1, 8], 1/8 of values from {0..7}
-(value ties), cl = 1, 64 changes per version per actor. Synthetic data
-generated directly in HBM. One step = one `process_multiple_changes`-sized apply of the whole
-batch into an empty state (state reset + corro_apply_batch), inputs already resident in HBM.
+N = 1 (default): BASELINE.json configs[1] = config 2 -- 64M (2^26) column changes, 1 table with 4
+INTEGER columns, 1000 actors, pk uniform in [1, 2^22], col_version uniform [1, 8], 1/8 of values
+from {0..7} (value ties), cl = 1, 64 changes per version per actor.
+Synthetic data generated directly in HBM. One step = one `process_multiple_changes`-sized apply of
+the whole batch into an empty state (state reset + corro_apply_batch), inputs resident in HBM.
 
-Multi-GPU (torchrun, one process per GPU): rows are owned by pk hash
-(corro_partition_ranks' rank_of), every row merges independently, so each rank merges the ~64M
-changes of ITS rows with no collective on the data path (weak scaling: per-GPU work fixed; the
-batch each rank holds is the owner-routed ingest of config 3, routed when it is built, outside the
-timed region). `--exchange` instead times partition + RCCL all-to-all-v + merge per step for
-batches that arrive mixed on every GPU (the ingest-exchange variant, reported in DESIGN.md §6).
+N > 1: `python bench.py --gpus N` launches N fresh ranks itself (one process per GPU; the parent
+never touches the GPU) unless it already runs under torchrun (WORLD_SIZE set). Default workload is
+config 3, STRONG scaling: 2^29 global changes (pk space 2^25, same distribution), the batch arriving
+rank-major (rank r holds the global slice r). One step = pk-hash partition into packed 48-B records
+(HIP) + ONE RCCL all-to-all-v of the records over xGMI + unpack + the local merge of the owned rows
+-- the exchange is inside the timed region and also reported as `exchange_ms`. The owner-routed
+figure (each rank merging only its own rows, no collective on the data path) is reported beside it
+as `owner_routed`. `--mode weak` keeps 64M changes per GPU instead.
+
+Roofline: algorithmic bytes (48 B per change + 48 B per output cell) over the apply
+pipeline's device time (HIP events on the engine's stream). `traffic` = HBM bytes per apply from
+rocprofv3 PMC passes (FETCH_SIZE x 2 per the gfx950 correction, + WRITE_SIZE) that this script runs
+on itself, in child processes, before it touches the GPU.
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 N_CHANGES = 1 << 26
+N_GLOBAL_C3 = 1 << 29
 N_ACTORS = 1000
 N_PK = 1 << 22
+N_PK_C3 = 1 << 25
 N_COLS = 4
 ALG_BYTES_PER_CHANGE = 48  # pk 8, table_cid 4, col_version 8, db_version 8, cl 4, seq 4, site 4, value 8
 ALG_BYTES_PER_CELL = 48
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8 TB/s spec
+METRIC = "merged column-changes/sec (node) at 1/2/4/8 GPUs + % of HBM BW roofline"
 
 
 def cpu_baseline(batch_dev, seconds_target=15.0):
@@ -78,171 +88,286 @@ def cpu_baseline(batch_dev, seconds_target=15.0):
                             "sample": f"{n} changes of the config-2 distribution folded sequentially in {dt:.2f} s"}}
 
 
-PIPELINE_KERNELS = ("k_hist", "k_colscan", "k_plan", "k_scatter", "k_merge_fast", "k_merge_gen", "k_merge_ovf")
+# ------------------------------------------------------------------------------------- PMC traffic
+def _ours(kernel_name):
+    """Kernels of the apply pipeline (the library's own and the rocPRIM sorts it launches), not the
+    synthetic-data generation or torch's memsets."""
+    return kernel_name.startswith("k_") or "corro" in kernel_name or "rocprim" in kernel_name
 
 
-def pmc_traffic_per_apply():
-    """HBM bytes per apply from the committed rocprofv3 PMC passes (profiles/*_pmc_{FETCH,WRITE}_SIZE.csv,
-    collected by scripts/gpu_prof.sh on this bench): sum over the pipeline kernels of
-    2 x FETCH_SIZE (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md §HBM) +
-    WRITE_SIZE, in KiB -> bytes, averaged per dispatch. None when the files are absent."""
+def _read_counter(dirname, counter):
     import csv
     import glob
-    from collections import defaultdict
-    out = {}
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        return None
+    tot = 0.0
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == counter and _ours(r.get("Kernel_Name", "")):
+                tot += float(r["Counter_Value"])
+    return tot
+
+
+def pmc_traffic_live(changes, applies=3, timeout=240):
+    """HBM bytes per apply measured now: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: they do
+    not fit one pass) over a child run of this bench doing `applies` applies of the same workload.
+    Counters are KiB; FETCH_SIZE is doubled (gfx950 reports half of wide coalesced reads,
+    MI355X_MICROARCH.md §HBM). Runs BEFORE this process touches the GPU. Returns (bytes or None,
+    note)."""
+    import shutil
+    import tempfile
+    rp = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if not rp:
+        return None, "rocprofv3 not found"
+    tmp = os.environ.get("TMPDIR") or "/tmp"
+    got = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_{counter}.csv")))
-        if not files:
-            return None, None
-        tot, disp = defaultdict(float), defaultdict(set)
-        for r in csv.DictReader(open(files[-1])):
-            name = r["Kernel_Name"]
-            k = next((p for p in PIPELINE_KERNELS if p in name), None)
-            if k and r["Counter_Name"] == counter:
-                tot[k] += float(r["Counter_Value"])
-                disp[k].add(r["Dispatch_Id"])
-        out[counter] = sum(tot[k] / len(disp[k]) for k in tot)
-        src = os.path.basename(files[-1])
-    return (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024.0, src
+        d = tempfile.mkdtemp(prefix="corro_pmc_", dir=tmp)
+        cmd = ["timeout", "-k", "10", "-s", "KILL", str(timeout), rp, "--pmc", counter, "--output-format", "csv",
+               "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
+               "--changes", str(changes), "--steps", str(applies - 1), "--warmup", "1"]
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout + 30)
+        except subprocess.TimeoutExpired:
+            return None, f"rocprofv3 --pmc {counter} timed out"
+        v = _read_counter(d, counter)
+        shutil.rmtree(d, ignore_errors=True)
+        if r.returncode != 0 or v is None:
+            return None, f"rocprofv3 --pmc {counter} rc={r.returncode}: {r.stderr.decode(errors='replace')[-300:]}"
+        got[counter] = v / applies
+    return (2 * got["FETCH_SIZE"] + got["WRITE_SIZE"]) * 1024.0, \
+        f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes run by bench.py on itself ({applies} applies each)"
 
 
+# ----------------------------------------------------------------------------------- self-launch
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """One fresh process per GPU (this parent never initialises the GPU): RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* as torchrun sets them. Returns the worst exit code."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+# ------------------------------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--changes", type=int, default=N_CHANGES)
+    ap.add_argument("--changes", type=int, default=None,
+                    help="N=1: changes per apply (default 2^26); N>1 strong: global changes (default 2^29)")
+    ap.add_argument("--mode", choices=("strong", "weak"), default="strong",
+                    help="N>1: strong = config 3 (2^29 global, exchange timed); weak = 64M per GPU, owner-routed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--exchange", action="store_true",
-                    help="N>1: time partition + RCCL all-to-all + merge (batches arrive mixed on every GPU)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and not args.pmc_child:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
+    rank = int(os.environ.get("RANK", "0"))
+
+    traffic, traffic_note = None, "not measured (--no-pmc)"
+    if world == 1 and not args.pmc_child and not args.no_pmc and rank == 0:
+        traffic, traffic_note = pmc_traffic_live(args.changes or N_CHANGES)
+
+    if world == 1:
+        run_single(args, traffic, traffic_note)
+    else:
+        run_multi(args, world, rank)
+
+
+def run_single(args, traffic, traffic_note):
     import torch
-    import torch.distributed as dist
     import synth
     import corrosion_amd as ca
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # CORRO_BENCH_BACKEND=gloo rehearses the N>1 code path with several ranks on one GPU
-    backend = os.environ.get("CORRO_BENCH_BACKEND", "nccl")
-    if backend == "gloo":
-        local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    sdev = dev if backend == "nccl" else torch.device("cpu")  # where scalar reductions run
-
-    n = args.changes
-    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=n, device=local)
-    sites = synth.site_ids(N_ACTORS, 1)
-    eng.register_sites(sites)
-    seed = synth.config_seed(2) + rank
-    if world == 1 or args.exchange:
-        batch = synth.uniform_batch_torch(n, N_ACTORS, N_PK * world, N_COLS, seed=seed, device=dev)
-    else:
-        # owner-routed ingest: keep this rank's rows out of `world` chunks of candidates drawn over
-        # the whole node's pk space (untimed setup)
-        own = []
-        for c in range(world):
-            cand = synth.uniform_batch_torch(n, N_ACTORS, N_PK * world, N_COLS, seed=seed * 1000 + c, device=dev)
-            parts, counts = eng.partition(cand, world)
-            lo = sum(counts[:rank])
-            own.append({k: v[lo:lo + counts[rank]].clone() for k, v in parts.items()})
-            del cand, parts
-        batch = {k: torch.cat([o[k] for o in own]).contiguous() for k in own[0]}
-        del own
-        torch.cuda.empty_cache()
-    n_local = int(batch["pk"].shape[0])
+    n = args.changes or N_CHANGES
+    dev = torch.device("cuda", 0)
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=n, device=0)
+    eng.register_sites(synth.site_ids(N_ACTORS, 1))
+    batch = synth.uniform_batch_torch(n, N_ACTORS, N_PK, N_COLS, seed=synth.config_seed(2), device=dev)
     torch.cuda.synchronize()
     eng.set_profiling(True)
-    from corrosion_amd.dist import distributed_apply
-
     # the batch's C-ABI descriptor (device pointers and sizes) is built once: a Rust caller hands
     # the same struct over; every step still resets the state and runs the whole apply
     prep = eng.prepare(batch)
 
     def step():
         eng.reset()
-        if world > 1 and args.exchange:
-            distributed_apply(eng, batch)
-        else:
-            eng.apply_prepared(prep)
+        eng.apply_prepared(prep)
 
     for _ in range(args.warmup):
         step()
-    cells = eng.count()
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
+    if args.pmc_child:
+        for _ in range(args.steps):
+            step()
         torch.cuda.synchronize()
-
+        eng.close()
+        return
+    cells = eng.count()
     kern = {}
-    barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         for k, v in eng.last_timings().items():
             kern[k] = kern.get(k, 0.0) + v
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern = {k: v / args.steps for k, v in kern.items()}
+    pipe_ms = sum(kern.values())
+    alg_bytes = ALG_BYTES_PER_CHANGE * n + ALG_BYTES_PER_CELL * cells
+    achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
+    cpu = None if args.no_cpu_baseline else cpu_baseline(batch)
+    line = {
+        "metric": METRIC,
+        "value": n / dt * args.steps,
+        "unit": "merged column-changes/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded, generated in HBM)",
+        "config": {"workload": "config 2: 64M column-changes, 1 table x 4 INTEGER cols, 1000 actors, uniform pk in "
+                               "[1,2^22], cl=1, one apply into an empty state per step",
+                   "changes": n, "cells": int(cells), "parallelism": "1 GPU"},
+        "roofline": {"bound": "hbm", "kernel": "apply pipeline: " + "+".join(k for k in kern if kern[k] > 0),
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_note,
+                     "traffic_ratio": (traffic / alg_bytes) if traffic else None,
+                     "alg_bytes_per_apply": alg_bytes, "pipeline_ms": pipe_ms, "kernels_ms": kern,
+                     "dominant": max(kern, key=kern.get)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    eng.close()
+
+
+def run_multi(args, world, rank):
+    import torch
+    import torch.distributed as dist
+    import synth
+    import corrosion_amd as ca
+    from corrosion_amd.dist import exchange_records, verify_sites
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    # CORRO_BENCH_BACKEND=gloo rehearses the N>1 code path with several ranks on one GPU
+    backend = os.environ.get("CORRO_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", local)
+    sdev = dev if backend == "nccl" else torch.device("cpu")   # where scalar reductions run
+    strong = args.mode == "strong"
+    if strong:
+        G = args.changes or N_GLOBAL_C3
+        lo, hi = rank * G // world, (rank + 1) * G // world
+        npk = N_PK_C3
+    else:
+        G = (args.changes or N_CHANGES) * world
+        lo, hi = rank * G // world, (rank + 1) * G // world
+        npk = N_PK * world
+    n_local = hi - lo
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=max(n_local, 1), device=local)
+    eng.register_sites(synth.site_ids(N_ACTORS, 1))
+    verify_sites(eng)
+    # rank r holds the global batch's slice r (rank-major = application order)
+    batch = synth.uniform_batch_torch(n_local, N_ACTORS, npk, N_COLS, seed=synth.config_seed(3) + rank, device=dev,
+                                      offset=lo, global_n=G)
+    torch.cuda.synchronize()
+
+    def barrier():
+        dist.barrier()
+        torch.cuda.synchronize()
+
+    ex_ms = []
+
+    def step():
+        eng.reset()
+        t0 = time.perf_counter()
+        recs, rb, counts, _ = eng.partition_packed(batch, world)
+        got, _rc = exchange_records(recs, rb, counts)
+        mine = eng.unpack_records(got, rb)
+        torch.cuda.synchronize()
+        ex_ms.append((time.perf_counter() - t0) * 1e3)
+        eng.apply(mine)
+        return mine
+
+    for _ in range(args.warmup):
+        mine = step()
+    barrier()
+    ex_ms.clear()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mine = step()
     barrier()
     dt = time.perf_counter() - t0
-    total = n_local * world if args.exchange else n_local
-    if world > 1:
-        t = torch.tensor([dt], device=sdev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        if not args.exchange:
-            tot = torch.tensor([n_local], device=sdev, dtype=torch.int64)
-            dist.all_reduce(tot)
-            total = int(tot.item())
-    kern = {k: v / args.steps for k, v in kern.items()}
-    pipe_ms = sum(v for k, v in kern.items())
-    dominant = max(kern, key=kern.get)
-    # per-GPU algorithmic bytes of one merge (with --exchange the merged slice is the received one,
-    # of the same expected size as the local batch)
-    alg_bytes = ALG_BYTES_PER_CHANGE * n_local + ALG_BYTES_PER_CELL * cells
-    achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
-
+    # owner-routed: the received batch IS this rank's owner-routed ingest; merge it alone
+    prep = eng.prepare(mine)
+    eng.reset()
+    eng.apply_prepared(prep)
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.reset()
+        eng.apply_prepared(prep)
+    barrier()
+    dt_own = time.perf_counter() - t1
+    stats = torch.tensor([dt, dt_own, sum(ex_ms) / max(1, len(ex_ms))], device=sdev, dtype=torch.float64)
+    dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    dt, dt_own, exm = (float(x) for x in stats.tolist())
     if rank == 0:
-        traffic, traffic_src = pmc_traffic_per_apply()
-        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(batch)
         line = {
-            "metric": "merged column-changes/sec (node) at 1/2/4/8 GPUs + % of HBM BW roofline",
-            "value": total / dt * args.steps,
+            "metric": METRIC,
+            "value": G / dt * args.steps,
             "unit": "merged column-changes/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded, generated in HBM)",
-            "config": {"workload": "config 2: 64M column-changes, 1 table x 4 INTEGER cols, 1000 actors, "
-                                   "uniform pk in [1,2^22] per GPU, cl=1, bucket merge"
-                                   + ("" if world == 1 else
-                                      ("; + pk-hash partition and RCCL all-to-all per step" if args.exchange else
-                                       "; rows owned by pk hash, each rank merges its own rows (no data-path collective)")),
-                       "changes_per_gpu": n_local, "total_changes": total, "cells_per_gpu": int(cells),
-                       "parallelism": f"pk-hash x{world}" + (" + all-to-all" if world > 1 and args.exchange else "")},
-            "roofline": {"bound": "hbm", "kernel": "apply pipeline: " + "+".join(k for k in kern if kern[k] > 0),
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "alg_bytes_per_apply": alg_bytes, "pipeline_ms": pipe_ms,
-                         "kernels_ms": kern, "dominant": dominant},
-            "cpu_baseline": cpu,
+            "config": {"workload": ("config 3: 2^29 global column-changes (pk space 2^25, 1000 actors, 4 INTEGER cols, "
+                                    "cl=1) arriving rank-major; per step: pk-hash partition into 48-B records + one "
+                                    "all-to-all-v + unpack + merge of the owned rows") if strong else
+                                   ("64M column-changes per GPU arriving on every GPU; per step: partition + one "
+                                    "all-to-all-v + merge"),
+                       "total_changes": G, "changes_per_gpu": n_local,
+                       "parallelism": f"pk-hash x{world}, {backend} all-to-all"},
+            "exchange_ms": exm,
+            "owner_routed": {"value": G / dt_own * args.steps, "ms_per_step": dt_own / args.steps * 1e3,
+                             "note": "each rank merges only its own rows (the received batch), no collective"},
         }
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

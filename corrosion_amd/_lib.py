@@ -32,7 +32,8 @@ EXPORTS = [
     "corro_generate_sync", "corro_partition_ranks", "corro_scan_offsets",
     "corro_compute_needs_onepass", "corro_needs_bound", "corro_extract_changes",
     "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
-    "corro_decode_frames", "corro_site_ids",
+    "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
+    "corro_unpack_records",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -187,6 +188,9 @@ def lib():
         "corro_bookie_partial": (i32, [vp, vp, u64, vp, vp, u64, vp, vp]),
         "corro_generate_sync": (i32, [vp, vp, C.POINTER(SyncState), i32]),
         "corro_partition_ranks": (i32, [vp, C.POINTER(Changes), u32, C.POINTER(Changes), vp]),
+        "corro_packed_record_bytes": (i32, [C.POINTER(Changes), vp]),
+        "corro_partition_packed": (i32, [vp, C.POINTER(Changes), u32, vp, vp, vp]),
+        "corro_unpack_records": (i32, [vp, vp, u64, u32, C.POINTER(Changes)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

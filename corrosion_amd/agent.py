@@ -117,13 +117,16 @@ class Bookie:
     def partial(self, actor, version):
         """(seq ranges, last_seq) of a partially received version, or None."""
         c, last = C.c_uint64(), C.c_int64()
-        s = np.zeros(64, np.uint64)
-        e = np.zeros(64, np.uint64)
-        L.check(L.lib().corro_bookie_partial(self._h, actor, version, s.ctypes.data, e.ctypes.data, 64,
-                                             C.byref(c), C.byref(last)))
+        # sizing call first (cap 0), then the ranges: a version may hold any number of seq ranges
+        L.check(L.lib().corro_bookie_partial(self._h, actor, version, None, None, 0, C.byref(c), C.byref(last)))
         if last.value < 0:
             return None
-        return [(int(s[i]), int(e[i])) for i in range(min(c.value, 64))], int(last.value)
+        n = int(c.value)
+        s = np.zeros(max(n, 1), np.uint64)
+        e = np.zeros(max(n, 1), np.uint64)
+        L.check(L.lib().corro_bookie_partial(self._h, actor, version, s.ctypes.data, e.ctypes.data, n,
+                                             C.byref(c), C.byref(last)))
+        return [(int(s[i]), int(e[i])) for i in range(n)], int(last.value)
 
 
 class Agent:

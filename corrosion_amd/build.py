@@ -15,13 +15,27 @@ HEADERS = ["internal.h", "merge_kernels.h", "ovf_kernels.h", "ranges.h", "booked
 ARCH = "gfx950"
 
 
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}"]
+STAMP = LIB + ".srchash"
+
+
+def _source_hash():
+    """sha256 over every source, header and the build flags: the library is rebuilt when any of
+    them changes, whatever the files' mtimes (a copied tree keeps a valid build)."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS + SOURCES).encode())
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "corro_hip.h")]
+    for d in deps:
+        with open(d, "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
 def _stale():
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(STAMP):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(ROOT, "include", "corro_hip.h"))
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(STAMP) as f:
+        return f.read().strip() != _source_hash()
 
 
 def build(force=False, verbose=False):
@@ -35,8 +49,8 @@ def build(force=False, verbose=False):
         obj = os.path.join(CSRC, src + ".o")
         # (-Wno-unused-function: the host pass of a .hip file reports the static kernels of a shared
         # header that the file does not launch itself)
-        cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}",
-               "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", os.path.join(CSRC, src),
+                                 "-o", obj]
         if src.endswith(".cpp"):
             cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "-Wall", "-x", "c++",
                    "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]
@@ -53,6 +67,8 @@ def build(force=False, verbose=False):
     os.replace(tmp, LIB)
     for o in objs:
         os.remove(o)
+    with open(STAMP, "w") as f:
+        f.write(_source_hash())
     return LIB
 
 

@@ -105,14 +105,26 @@ HostRow row_at(const corro_changes *in, uint64_t i, uint64_t ts) {
 
 // process_incomplete_version (util.rs:1053-1186): buffer the rows, merge the seq range into the
 // seq bookkeeping. Returns the PartialVersion (seqs = the merged range only) or an error.
-int process_incomplete(corro_bookie *bk, const corro_changeset &cs, const corro_changes *in,
-                       corro::PartialVersion &out) {
-    for (uint64_t k = 0; k < cs.change_count; k++) {
-        const HostRow r = row_at(in, cs.change_off + k, cs.ts);
-        auto &slot = bk->buffered[{r.site, r.dbv}];
-        slot.emplace(r.seq, r);  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
+// Writes of one process_multiple_changes call that must not outlive a failed call: the reference
+// makes them inside the call's single transaction (util.rs:749, :936), so they are staged here and
+// applied only once the merge and the gap bookkeeping have succeeded.
+struct Staged {
+    std::vector<std::pair<uint32_t, uint64_t>> set_dbv;                      // crsql_set_db_version
+    std::vector<HostRow> buffered;                                            // __corro_buffered_changes
+    std::map<std::pair<uint32_t, uint64_t>, SeqBook> seqbook;                 // __corro_seq_bookkeeping
+    SeqBook &seq(const corro_bookie *bk, uint32_t site, uint64_t version) {
+        auto it = seqbook.find({site, version});
+        if (it != seqbook.end()) return it->second;
+        auto b = bk->seqbook.find({site, version});
+        return seqbook.emplace(std::make_pair(site, version), b == bk->seqbook.end() ? SeqBook{} : b->second)
+            .first->second;
     }
-    SeqBook &sb = bk->seqbook[{cs.site, cs.version_start}];
+};
+
+int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset &cs, const corro_changes *in,
+                       corro::PartialVersion &out) {
+    for (uint64_t k = 0; k < cs.change_count; k++) st.buffered.push_back(row_at(in, cs.change_off + k, cs.ts));
+    SeqBook &sb = st.seq(bk, cs.site, cs.version_start);
     const uint64_t s = cs.seq_start, e = cs.seq_end;
     RangeSet merged;
     std::vector<Range> keep;
@@ -204,6 +216,7 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     }
 
     // pass 2 (util.rs:765-884): per actor, in order
+    Staged st;
     Batch batch;
     std::vector<std::pair<uint64_t, uint64_t>> applied;  // (changeset, first batch row)
     std::map<ActorId, std::vector<std::pair<Range, std::optional<corro::PartialVersion>>>> processed;
@@ -235,10 +248,7 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
             std::optional<corro::PartialVersion> partial;
             if (is_complete(c) && is_empty(c)) {
                 // process_empty_version only when end > booked max (util.rs:810-824)
-                if (!had_max || v.second > max) {
-                    int rc = corro::set_db_version(ctx, c.site, v.second);
-                    if (rc != CORRO_OK) return rc;
-                }
+                if (!had_max || v.second > max) st.set_dbv.emplace_back(c.site, v.second);
                 out->known[i] = CORRO_KNOWN_CLEARED;
             } else {
                 if (seqs && seqs->second < seqs->first) continue;  // invalid seqs (util.rs:826-831)
@@ -255,7 +265,7 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
                     out->known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
                 } else {
                     corro::PartialVersion p;
-                    if (process_incomplete(bk, c, in, p) != CORRO_OK) {
+                    if (process_incomplete(bk, st, c, in, p) != CORRO_OK) {
                         out->known[i] = CORRO_E_INVALID;
                         continue;
                     }
@@ -268,6 +278,26 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
         }
     }
 
+    // gap bookkeeping first, on copies of the actors' Booked (VersionsSnapshot, agent.rs:1108-1235): an
+    // INSERT that would violate __corro_bookkeeping_gaps' key fails the whole call before the merge
+    // has touched the state, as the transaction's rollback would undo it (util.rs:894-936)
+    std::map<ActorId, corro::Booked> next;
+    std::vector<std::pair<ActorId, uint64_t>> ready;
+    for (auto &[actor, list] : processed) {
+        corro::Booked nb = bk->actors[actor];
+        RangeSet versions;
+        for (auto &e : list) versions.insert(e.first.first, e.first.second);
+        if (!nb.insert_db(versions, nullptr, nullptr))
+            return fail(CORRO_E_INVALID, "UNIQUE constraint failed: __corro_bookkeeping_gaps.start");
+        for (auto &e : list) {
+            if (!e.second) continue;
+            const uint64_t version = e.first.first;
+            const corro::PartialVersion &p = nb.insert_partial(version, *e.second);
+            if (p.seqs.gaps(0, p.last_seq).empty()) ready.emplace_back(actor, version);
+        }
+        next.emplace(actor, std::move(nb));
+    }
+
     // the merge: one batch in application order
     std::vector<uint8_t> impact(batch.size(), 0);
     if (batch.size()) {
@@ -275,8 +305,19 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
         corro_apply_out ao{};
         ao.impact = impact.data();
         int rc = corro_apply_batch(ctx, &view, CORRO_MEM_HOST, &ao);
-        if (rc != CORRO_OK) return rc;  // the transaction fails as a whole (util.rs:849-855)
+        if (rc != CORRO_OK) {  // the transaction fails as a whole (util.rs:849-855)
+            for (uint64_t i = 0; i < ncs; i++) out->known[i] = CORRO_KNOWN_SKIPPED;
+            return rc;
+        }
     }
+    // commit: everything below only records what the successful transaction did
+    for (const auto &[site, version] : st.set_dbv) {
+        int rc = corro::set_db_version(ctx, site, version);
+        if (rc != CORRO_OK) return rc;
+    }
+    for (const HostRow &r : st.buffered)  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
+        bk->buffered[{r.site, r.dbv}].emplace(r.seq, r);
+    for (auto &[key, sb] : st.seqbook) bk->seqbook[key] = sb;
     // impactful changes: crsql_rows_impacted() is cumulative over the transaction, while
     // last_rows_impacted restarts at 0 for every version (util.rs:1218-1261)
     uint64_t cum = 0;
@@ -299,25 +340,10 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
         // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303)
         clear_buffered(bk, c.site, c.version_start, c.version_start);
     }
-
-    // per-actor gap snapshot + commit, then partials (util.rs:894-1008)
-    out->n_ready = 0;
-    for (auto &[actor, list] : processed) {
-        corro::Booked &booked = bk->actors[actor];
-        RangeSet versions;
-        for (auto &e : list) versions.insert(e.first.first, e.first.second);
-        if (!booked.insert_db(versions, nullptr, nullptr))
-            return fail(CORRO_E_INVALID, "UNIQUE constraint failed: __corro_bookkeeping_gaps.start");
-        for (auto &e : list) {
-            if (!e.second) continue;
-            const uint64_t version = e.first.first;
-            const corro::PartialVersion &p = booked.insert_partial(version, *e.second);
-            if (p.seqs.gaps(0, p.last_seq).empty()) {
-                bk->ready.emplace_back(actor, version);
-                out->n_ready++;
-            }
-        }
-    }
+    // per-actor gap snapshot commit, then partials (util.rs:936-1008)
+    for (auto &[actor, nb] : next) bk->actors[actor] = std::move(nb);
+    for (auto &r : ready) bk->ready.push_back(r);
+    out->n_ready = ready.size();
     return CORRO_OK;
 }
 
@@ -352,6 +378,11 @@ int corro_process_fully_buffered(corro_ctx *ctx, corro_bookie *bk, const uint8_t
     auto rows = bk->buffered.find({site, (int64_t)version});
     if (rows != bk->buffered.end())
         for (auto &kv : rows->second) batch.push(kv.second);  // ORDER BY db_version, seq
+    RangeSet v;
+    v.insert(version, version);
+    corro::Booked nb = booked;  // committed only with the merge (one transaction, util.rs:560-676)
+    if (!nb.insert_db(v, nullptr, nullptr))
+        return fail(CORRO_E_INVALID, "UNIQUE constraint failed: __corro_bookkeeping_gaps.start");
     std::vector<uint8_t> impact(batch.size(), 0);
     if (batch.size()) {
         corro_changes view = batch.view();
@@ -361,10 +392,7 @@ int corro_process_fully_buffered(corro_ctx *ctx, corro_bookie *bk, const uint8_t
         if (rc != CORRO_OK) return rc;
     }
     clear_buffered(bk, site, version, version);
-    RangeSet v;
-    v.insert(version, version);
-    if (!booked.insert_db(v, nullptr, nullptr))
-        return fail(CORRO_E_INVALID, "UNIQUE constraint failed: __corro_bookkeeping_gaps.start");
+    booked = std::move(nb);
     uint64_t total = 0;
     for (uint8_t x : impact) total += x;
     if (impacted) *impacted = total > 0;

@@ -491,46 +491,14 @@ static int error_from_bits(uint64_t bits) {
     return fail(CORRO_E_INVALID, "malformed value (type, length or NaN REAL)");
 }
 
-int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out) {
-    if (!ctx || !in) return fail(CORRO_E_INVALID, "NULL argument");
-    if (in->n == 0) return CORRO_OK;
-    if (in->n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
-    if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
-        !in->val0)
-        return fail(CORRO_E_INVALID, "a required batch array is NULL");
-    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
-    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+// One apply of a device-resident chunk (bd: n changes in application order) into the state.
+// imp_buf: device impact flags of this chunk (or null). Returns with the state committed.
+static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     hipStream_t s = ctx->stream;
-    const uint32_t n = (uint32_t)in->n;
+    const uint32_t n = bd.n;
     const uint32_t B = ctx->B, log2B = ctx->log2B;
     const uint32_t nsites = (uint32_t)ctx->sites.size();
-    if (nsites == 0) return fail(CORRO_E_INVALID, "no sites registered");
-
-    BatchDev bd{};
-    if (mem == CORRO_MEM_HOST) {
-        TRY(stage_host_batch(ctx, in, bd));
-    } else {
-        // k_scatter reads pairs of changes with 16-B (64-bit fields) / 8-B (32-bit fields) loads
-        auto misaligned = [](const void *p, uintptr_t a) { return p && ((uintptr_t)p % a) != 0; };
-        if (misaligned(in->pk, 16) || misaligned(in->col_version, 16) || misaligned(in->db_version, 16) ||
-            misaligned(in->val0, 16) || misaligned(in->val1, 16) || misaligned(in->table_cid, 8) ||
-            misaligned(in->cl, 8) || misaligned(in->seq, 8) || misaligned(in->site, 8))
-            return fail(CORRO_E_INVALID, "device batch arrays must be 16-byte (64-bit fields) / 8-byte aligned");
-        bd.pk = in->pk;
-        bd.tcid = in->table_cid;
-        bd.cv = in->col_version;
-        bd.dbv = in->db_version;
-        bd.cl = in->cl;
-        bd.seq = in->seq;
-        bd.site = in->site;
-        bd.v0 = in->val0;
-        bd.v1 = in->val1;
-        bd.vt = in->val_type;
-        bd.vl = in->val_len;
-        bd.ts = in->ts;
-    }
-    bd.n = n;
-    if (in->ts && !ctx->track_ts) {
+    if (bd.ts && !ctx->track_ts) {
         // timestamps start being tracked: give the current state zero timestamps
         const size_t cap_rows = ctx->d_state[ctx->cur].bytes / sizeof(Rec);
         TRY(ctx->d_state_ts[ctx->cur].ensure(std::max<size_t>(cap_rows, 1) * 8));
@@ -555,11 +523,6 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     TRY(ctx->d_stage.ensure((size_t)n * sizeof(Rec)));
     TRY(ctx->d_state[nxt].ensure(out_cap * sizeof(Rec)));
     if (ctx->track_ts) TRY(ctx->d_state_ts[nxt].ensure(out_cap * 8));
-    // impact output: a device batch gets its flags written straight into the caller's device
-    // buffer; a host batch through a device staging buffer + one copy
-    const bool imp_dev = out && out->impact && mem == CORRO_MEM_DEVICE;
-    if (out && out->impact && !imp_dev) TRY(ctx->d_impact.ensure(n));
-    uint8_t *imp_buf = !(out && out->impact) ? nullptr : (imp_dev ? out->impact : ctx->d_impact.as<uint8_t>());
 
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_bflags.p, 0, ((B + 31) / 32) * 4ULL, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
@@ -655,8 +618,6 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     if (novf) TRY(run_overflow(ctx, a, novf, n, prof));
     hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
                        ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites);
-    if (out && out->impact && !imp_dev)
-        CORRO_HIP_TRY(hipMemcpyAsync(out->impact, ctx->d_impact.p, n, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
 
     // commit: the next state becomes current
@@ -667,6 +628,93 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     ctx->state_total = ctx->h_misc[2];
     ctx->state_epoch++;
     if (ctx->h_misc[3]) ctx->state_wide = true;
+    return CORRO_OK;
+}
+
+// Changes per chunk: the bucket count sizes the merge for ~2048 records per bucket, so a larger
+// batch is applied as consecutive chunks of it, in application order -- the same result as one
+// apply, since the merge is a left fold over the changes (each INSERT sees the state its
+// predecessors left). The whole batch is validated before the first chunk commits.
+static uint64_t chunk_changes(const corro_ctx *ctx) {
+    const char *e = std::getenv("CORRO_HIP_CHUNK");  // tests: force chunking of small batches
+    const uint64_t env = e ? (uint64_t)std::atoll(e) : 0ULL;
+    if (env) return std::max<uint64_t>(1024, env & ~1023ULL);
+    return std::max<uint64_t>(1ULL << 16, (uint64_t)ctx->B * 2048ULL);
+}
+
+int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out) {
+    if (!ctx || !in) return fail(CORRO_E_INVALID, "NULL argument");
+    if (in->n == 0) return CORRO_OK;
+    if (in->n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
+    if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
+        !in->val0)
+        return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const uint32_t n = (uint32_t)in->n;
+    const uint32_t nsites = (uint32_t)ctx->sites.size();
+    if (nsites == 0) return fail(CORRO_E_INVALID, "no sites registered");
+
+    BatchDev bd{};
+    if (mem == CORRO_MEM_HOST) {
+        TRY(stage_host_batch(ctx, in, bd));
+    } else {
+        // k_scatter reads pairs of changes with 16-B (64-bit fields) / 8-B (32-bit fields) loads
+        auto misaligned = [](const void *p, uintptr_t a) { return p && ((uintptr_t)p % a) != 0; };
+        if (misaligned(in->pk, 16) || misaligned(in->col_version, 16) || misaligned(in->db_version, 16) ||
+            misaligned(in->val0, 16) || misaligned(in->val1, 16) || misaligned(in->table_cid, 8) ||
+            misaligned(in->cl, 8) || misaligned(in->seq, 8) || misaligned(in->site, 8))
+            return fail(CORRO_E_INVALID, "device batch arrays must be 16-byte (64-bit fields) / 8-byte aligned");
+        bd.pk = in->pk;
+        bd.tcid = in->table_cid;
+        bd.cv = in->col_version;
+        bd.dbv = in->db_version;
+        bd.cl = in->cl;
+        bd.seq = in->seq;
+        bd.site = in->site;
+        bd.v0 = in->val0;
+        bd.v1 = in->val1;
+        bd.vt = in->val_type;
+        bd.vl = in->val_len;
+        bd.ts = in->ts;
+    }
+    bd.n = n;
+    // impact output: a device batch gets its flags written straight into the caller's device
+    // buffer; a host batch through a device staging buffer + one copy
+    const bool imp_dev = out && out->impact && mem == CORRO_MEM_DEVICE;
+    if (out && out->impact && !imp_dev) TRY(ctx->d_impact.ensure(n));
+    uint8_t *imp_buf = !(out && out->impact) ? nullptr : (imp_dev ? out->impact : ctx->d_impact.as<uint8_t>());
+
+    const uint64_t chunk = chunk_changes(ctx);
+    if (n > chunk) {
+        CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
+        hipLaunchKernelGGL(k_validate, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, bd,
+                           nsites, ctx->d_ncols.as<uint16_t>(), (uint32_t)ctx->tables.size(),
+                           ctx->d_misc.as<unsigned long long>());
+        CORRO_HIP_TRY(hipGetLastError());
+        CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, ctx->d_misc.p, 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        if (ctx->h_misc[0]) return error_from_bits(ctx->h_misc[0]);
+    }
+    float ms[6] = {};
+    for (uint64_t off = 0; off < n; off += chunk) {
+        BatchDev c = bd;
+        const uint32_t m = (uint32_t)std::min<uint64_t>(chunk, n - off);
+        auto adv = [&](auto *&p) {
+            if (p) p += off;
+        };
+        adv(c.pk), adv(c.tcid), adv(c.cv), adv(c.dbv), adv(c.cl), adv(c.seq), adv(c.site), adv(c.v0), adv(c.v1);
+        adv(c.vt), adv(c.vl), adv(c.ts);
+        c.n = m;
+        TRY(apply_chunk(ctx, c, imp_buf ? imp_buf + off : nullptr));
+        for (int k = 0; k < 6; k++) ms[k] += ctx->last_ms[k];
+    }
+    for (int k = 0; k < 6; k++) ctx->last_ms[k] = ms[k];
+    if (out && out->impact && !imp_dev) {
+        CORRO_HIP_TRY(hipMemcpyAsync(out->impact, ctx->d_impact.p, n, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+    }
     return CORRO_OK;
 }
 

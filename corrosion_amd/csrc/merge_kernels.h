@@ -1598,6 +1598,36 @@ k_merge_gen_small(MergeArgs a, uint32_t B) {
     }
 }
 
+// Validation of a whole batch before a chunked apply commits its first chunk (the checks k_scatter
+// makes per chunk; a batch is applied all or nothing).
+static __global__ void k_validate(BatchDev in, uint32_t nsites, const uint16_t *__restrict__ ncols, uint32_t ntables,
+                                  unsigned long long *misc) {
+    uint32_t err = 0, wide = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < in.n; i += gridDim.x * blockDim.x) {
+        const uint32_t tc = in.tcid[i], t = tc >> 16, cid = tc & 0xFFFFu, cl = in.cl[i];
+        const int64_t cv = in.cv[i];
+        if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
+        if (in.site[i] >= nsites) err |= ERR_SITE;
+        if ((cid == 0 || (cl & 1u) == 0) && (cv < 0 || cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
+        if (in.dbv[i] < 0) err |= ERR_RANGE;
+        if (in.vt) {
+            const uint32_t ty = in.vt[i], ln = in.vl ? in.vl[i] : 0u;
+            if (ty != CORRO_INTEGER) {
+                wide = 1;
+                const uint64_t v0 = in.v0[i];
+                if (ty < 1 || ty > 5) err |= ERR_VALUE;
+                if (ty == CORRO_REAL && ((v0 >> 52) & 0x7FF) == 0x7FF && (v0 & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
+                if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) err |= ERR_VALUE;
+            }
+        }
+    }
+    if (__any(err != 0)) {
+        for (int d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d);
+        if ((threadIdx.x & 63) == 0) atomicOr(&misc[0], (unsigned long long)err);
+    }
+    if (__any(wide != 0) && (threadIdx.x & 63) == 0) atomicOr(&misc[3], 1ULL);
+}
+
 // crsql_db_versions fold after a successful batch
 static __global__ void k_dbv_fold(unsigned long long *__restrict__ dbv, const unsigned long long *__restrict__ batch,
                            uint32_t nsites) {

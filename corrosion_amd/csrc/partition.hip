@@ -9,6 +9,7 @@
 // bucket (merge_kernels.h bucket_of), so a rank's rows still spread over all of its buckets.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "internal.h"
@@ -128,6 +129,102 @@ k_part_scatter(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__re
     }
 }
 
+// Packed-record exchange format (one all-to-all of whole records instead of one per SoA field):
+// PLAIN batches (INTEGER values, no val1/val_type/val_len/ts arrays) use the 48-B record of
+// SURVEY §8(d); others a 80-B record that carries every optional field.
+struct __attribute__((aligned(16))) PackedRec48 {
+    uint64_t pk;
+    int64_t cv, dbv;
+    uint64_t v0;
+    uint32_t tcid, cl, seq, site;
+};
+struct __attribute__((aligned(16))) PackedRec80 {
+    uint64_t pk;
+    int64_t cv, dbv;
+    uint64_t v0, v1, ts;
+    uint32_t tcid, cl, seq, site, meta, pad[3];
+};
+static_assert(sizeof(PackedRec48) == 48 && sizeof(PackedRec80) == 80, "packed record sizes");
+
+// stable scatter of whole records (same ranking as k_part_scatter); perm[pos] = source index
+template <bool PLAIN>
+__global__ void __launch_bounds__(PART_THREADS)
+k_part_pack(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restrict__ offs, void *__restrict__ out,
+            uint32_t *__restrict__ perm) {
+    __shared__ uint32_t run[PART_MAX_RANKS];
+    __shared__ uint32_t wcnt[PART_THREADS / 64][PART_MAX_RANKS];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) run[r] = offs[(size_t)blockIdx.x * nranks + r];
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * tile, end = min(in.n, begin + tile);
+    const uint64_t lt = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+    for (uint32_t base = begin; base < end; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const bool act = i < end;
+        const uint32_t ic = act ? i : begin;
+        const uint64_t pk = in.pk[ic];
+        const uint32_t tc = in.tcid[ic];
+        const uint32_t d = act ? rank_of(tc >> 16, pk, nranks) : 0xFFFFFFFFu;
+        uint32_t my_rank = 0;
+        for (uint32_t r = 0; r < nranks; r++) {
+            const uint64_t m = __ballot(d == r);
+            if (d == r) my_rank = __popcll(m & lt);
+            if (lane == 0) wcnt[w][r] = __popcll(m);
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t pos = run[d] + my_rank;
+            for (uint32_t ww = 0; ww < w; ww++) pos += wcnt[ww][d];
+            if (PLAIN) {
+                PackedRec48 r{pk, in.cv[i], in.dbv[i], in.v0[i], tc, in.cl[i], in.seq[i], in.site[i]};
+                static_cast<PackedRec48 *>(out)[pos] = r;
+            } else {
+                PackedRec80 r{};
+                r.pk = pk;
+                r.cv = in.cv[i];
+                r.dbv = in.dbv[i];
+                r.v0 = in.v0[i];
+                r.v1 = in.v1 ? in.v1[i] : 0ULL;
+                r.ts = in.ts ? in.ts[i] : 0ULL;
+                r.tcid = tc;
+                r.cl = in.cl[i];
+                r.seq = in.seq[i];
+                r.site = in.site[i];
+                r.meta = (in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER) | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8);
+                static_cast<PackedRec80 *>(out)[pos] = r;
+            }
+            if (perm) perm[pos] = i;
+        }
+        __syncthreads();
+        if (threadIdx.x < nranks) {
+            uint32_t add = 0;
+            for (uint32_t ww = 0; ww < PART_THREADS / 64; ww++) add += wcnt[ww][threadIdx.x];
+            run[threadIdx.x] += add;
+        }
+        __syncthreads();
+    }
+}
+
+// received records (source-rank order) -> the SoA batch corro_apply_batch takes
+template <bool PLAIN>
+__global__ void k_unpack(const void *__restrict__ recs, uint32_t n, BatchOut o) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (PLAIN) {
+            const PackedRec48 r = static_cast<const PackedRec48 *>(recs)[i];
+            o.pk[i] = r.pk; o.cv[i] = r.cv; o.dbv[i] = r.dbv; o.v0[i] = r.v0;
+            o.tcid[i] = r.tcid; o.cl[i] = r.cl; o.seq[i] = r.seq; o.site[i] = r.site;
+        } else {
+            const PackedRec80 r = static_cast<const PackedRec80 *>(recs)[i];
+            o.pk[i] = r.pk; o.cv[i] = r.cv; o.dbv[i] = r.dbv; o.v0[i] = r.v0;
+            o.tcid[i] = r.tcid; o.cl[i] = r.cl; o.seq[i] = r.seq; o.site[i] = r.site;
+            if (o.v1) o.v1[i] = r.v1;
+            if (o.ts) o.ts[i] = r.ts;
+            if (o.vt) o.vt[i] = (uint8_t)(r.meta & 0xFFu);
+            if (o.vl) o.vl[i] = (uint8_t)(r.meta >> 8);
+        }
+    }
+}
+
 }  // namespace corro
 
 using namespace corro;
@@ -166,6 +263,83 @@ extern "C" int corro_partition_ranks(corro_ctx *ctx, const corro_changes *in, ui
     hipLaunchKernelGGL(k_part_scatter, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts, bo);
     CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipMemcpyAsync(counts, d_tot, nranks * 8ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+static int part_tiles(corro_ctx *ctx, uint32_t n, uint32_t nranks, uint32_t &ntiles, uint32_t &tile, uint32_t *&d_counts,
+                      uint64_t *&d_tot) {
+    ntiles = std::max<uint32_t>(1, std::min<uint32_t>(2048, (n + 8191) / 8192));
+    tile = (n + ntiles - 1) / ntiles;
+    tile = (tile + PART_THREADS - 1) / PART_THREADS * PART_THREADS;
+    ntiles = (n + tile - 1) / tile;
+    if (int rc = ctx->d_part.ensure((size_t)ntiles * nranks * 4 + nranks * 8 + 256)) return rc;
+    d_counts = ctx->d_part.as<uint32_t>();
+    d_tot = reinterpret_cast<uint64_t *>(ctx->d_part.as<uint8_t>() + (((size_t)ntiles * nranks * 4 + 255) / 256) * 256);
+    return CORRO_OK;
+}
+
+extern "C" int corro_packed_record_bytes(const corro_changes *in, uint32_t *bytes) {
+    if (!in || !bytes) return fail(CORRO_E_INVALID, "NULL argument");
+    *bytes = (!in->val1 && !in->val_type && !in->val_len && !in->ts) ? 48u : 80u;
+    return CORRO_OK;
+}
+
+extern "C" int corro_partition_packed(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, void *out,
+                                      uint32_t *perm, uint64_t *counts) {
+    if (!ctx || !in || !out || !counts) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nranks == 0 || nranks > (uint32_t)PART_MAX_RANKS) return fail(CORRO_E_RANGE, "1..64 ranks");
+    if (in->n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
+    if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
+        !in->val0)
+        return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    if ((uintptr_t)out % 16) return fail(CORRO_E_INVALID, "packed records must be 16-byte aligned");
+    for (uint32_t r = 0; r < nranks; r++) counts[r] = 0;
+    const uint32_t n = (uint32_t)in->n;
+    if (n == 0) return CORRO_OK;
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    BatchDev bd{in->pk, in->table_cid, in->col_version, in->db_version, in->cl, in->seq, in->site, in->val0,
+                in->val1, in->val_type, in->val_len, in->ts, n};
+    uint32_t ntiles, tile, *d_counts;
+    uint64_t *d_tot;
+    if (int rc = part_tiles(ctx, n, nranks, ntiles, tile, d_counts, d_tot)) return rc;
+    const bool plain = !in->val1 && !in->val_type && !in->val_len && !in->ts;
+    hipLaunchKernelGGL(k_part_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, d_tot);
+    if (plain)
+        hipLaunchKernelGGL(k_part_pack<true>, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts, out, perm);
+    else
+        hipLaunchKernelGGL(k_part_pack<false>, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts, out, perm);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipMemcpyAsync(counts, d_tot, nranks * 8ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+extern "C" int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n, uint32_t rec_bytes,
+                                    corro_changes *out) {
+    if (!ctx || (!recs && n) || !out) return fail(CORRO_E_INVALID, "NULL argument");
+    if (rec_bytes != 48 && rec_bytes != 80) return fail(CORRO_E_INVALID, "record size must be 48 or 80 bytes");
+    if (n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
+    if (n == 0) return CORRO_OK;
+    if (!out->pk || !out->table_cid || !out->col_version || !out->db_version || !out->cl || !out->seq ||
+        !out->site || !out->val0)
+        return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    BatchOut bo{const_cast<uint64_t *>(out->pk),     const_cast<uint32_t *>(out->table_cid),
+                const_cast<int64_t *>(out->col_version), const_cast<int64_t *>(out->db_version),
+                const_cast<uint32_t *>(out->cl),     const_cast<uint32_t *>(out->seq),
+                const_cast<uint32_t *>(out->site),   const_cast<uint64_t *>(out->val0),
+                const_cast<uint64_t *>(out->val1),   const_cast<uint8_t *>(out->val_type),
+                const_cast<uint8_t *>(out->val_len), const_cast<uint64_t *>(out->ts)};
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+    if (rec_bytes == 48)
+        hipLaunchKernelGGL(k_unpack<true>, dim3(grid), dim3(256), 0, s, recs, (uint32_t)n, bo);
+    else
+        hipLaunchKernelGGL(k_unpack<false>, dim3(grid), dim3(256), 0, s, recs, (uint32_t)n, bo);
+    CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;
 }

@@ -143,6 +143,10 @@ __global__ void k_wire_hdr(WireDev d) {
             v0 = v1 = r.u64();
             nchg = r.u32();
             cstart = r.pos;
+            // the count is untrusted: the smallest encoded change is 61 bytes (three u32 length
+            // prefixes, a value tag and 48 bytes of fixed fields), so a count the frame cannot hold
+            // is malformed (and must not size the caller's allocations)
+            if (!r.bad && (uint64_t)nchg * 61 > (uint64_t)(r.end - r.pos)) st = CORRO_E_INVALID;
         } else if (kind == 2) {     // EmptySet { versions: Vec<RangeInclusive>, ts }
             nset = r.u32();
             const uint64_t body = (uint64_t)nset * 16;

@@ -1,11 +1,19 @@
 """Node-level multi-GPU merge: one process per GPU, rows sharded by pk hash.
 
-Ingest on every rank: stable partition by owner rank (HIP kernel, corro_partition_ranks) ->
-one all-to-all-v exchange per SoA field (torch.distributed, RCCL over xGMI on the GPU box) ->
-concatenation by source rank (preserves every row's application order when the global batch is
-rank-major) -> local merge. No further communication: rows merge independently; per-site
-crsql_db_versions maxima reduce with one tiny all-reduce(max) when asked.
+Ingest on every rank: stable partition by owner rank into whole packed records (HIP kernel,
+corro_partition_packed: 48 B per INTEGER change, the §8(d) record) -> ONE all-to-all-v of records
+(torch.distributed: RCCL over xGMI on the GPU box, gloo in CPU rehearsals) after one all-to-all of
+the per-rank counts -> the received records, concatenated by source rank, unpacked to the SoA batch
+(corro_unpack_records) -> local merge. Concatenation by source rank preserves every row's
+application order when the global batch is rank-major. No further communication: rows merge
+independently; per-site crsql_db_versions maxima reduce with one tiny all-reduce(max) when asked.
+
+Site ordinals are per-engine, so the exchange is only meaningful between engines whose site tables
+are identical (same 16-byte ids at the same ordinals): `verify_sites` all-gathers a digest of the
+table and raises when a rank differs.
 """
+import hashlib
+
 import numpy as np
 
 MASK64 = (1 << 64) - 1
@@ -30,23 +38,29 @@ def rank_of_np(table_cid, pk, nranks):
     return ((h & np.uint64(0xFFFFFFFF)) % np.uint64(nranks)).astype(np.int64)
 
 
-def exchange(parts, counts, group=None):
-    """All-to-all-v of a rank-partitioned batch. `parts`: dict of 1-D tensors grouped by
-    destination rank; `counts`: per-destination sizes. Returns the received dict (source-rank
-    order) — works on CUDA tensors with nccl (RCCL) and on CPU tensors with gloo."""
+def _counts_exchange(counts, dev, group):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    send = torch.tensor(counts, dtype=torch.int64, device=dev)
+    recv = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, send, group=group)
+    return [int(c) for c in recv.tolist()]
+
+
+def exchange(parts, counts, group=None):
+    """All-to-all-v of a rank-partitioned SoA batch, one collective per field (kept for batches a
+    caller partitioned itself). `parts`: dict of 1-D tensors grouped by destination rank; `counts`:
+    per-destination sizes. Returns the received dict (source-rank order)."""
+    import torch
+    import torch.distributed as dist
     dev = next(iter(parts.values())).device
     if dev.type == "cuda" and dist.get_backend(group) == "gloo":
         # gloo has no device all-to-all: stage through host memory (rehearsals on a 1-GPU box)
         got = exchange({k: v.cpu() for k, v in parts.items()}, counts, group)
         return {k: v.to(dev) for k, v in got.items()}
-    send = torch.tensor(counts, dtype=torch.int64, device=dev)
-    recv = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(recv, send, group=group)
+    out_splits = _counts_exchange(counts, dev, group)
     in_splits = [int(c) for c in counts]
-    out_splits = [int(c) for c in recv.tolist()]
     total = sum(out_splits)
     out = {}
     for k, a in parts.items():
@@ -56,12 +70,71 @@ def exchange(parts, counts, group=None):
     return out
 
 
-def distributed_apply(engine, batch, group=None, impact=False):
-    """Partition by owner rank, exchange, merge the owned rows into this rank's engine."""
+def exchange_records(recs, rec_bytes, counts, group=None):
+    """ONE all-to-all-v of packed records (uint8 tensor, grouped by destination rank, `counts`
+    records each). Returns (received uint8 tensor in source-rank order, received counts)."""
+    import torch
+    import torch.distributed as dist
+    dev = recs.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        got, rc = exchange_records(recs.cpu(), rec_bytes, counts, group)
+        return got.to(dev), rc
+    rcounts = _counts_exchange(counts, dev, group)
+    out = torch.empty(sum(rcounts) * rec_bytes, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(out, recs, [c * rec_bytes for c in rcounts], [int(c) * rec_bytes for c in counts],
+                           group=group)
+    return out, rcounts
+
+
+def site_digest(engine):
+    """sha256 of the engine's site table (16-byte ids in ordinal order)."""
+    return hashlib.sha256(b"".join(engine.site_ids())).digest()
+
+
+def verify_sites(engine, group=None):
+    """Raise unless every rank's engine holds the same site table (ids at the same ordinals): the
+    packed records carry site ordinals, which would otherwise land under the wrong site id and
+    break the merge-equal-values tie-break."""
+    import torch.distributed as dist
+    mine = site_digest(engine)
+    got = [None] * dist.get_world_size(group)
+    dist.all_gather_object(got, mine, group=group)
+    bad = [r for r, d in enumerate(got) if d != mine]
+    if bad:
+        raise RuntimeError(f"site tables differ between ranks {bad} and this one: register the same site ids "
+                           "in the same order on every rank before exchanging changes")
+
+
+def distributed_apply(engine, batch, group=None, impact=False, verify=True):
+    """Partition by owner rank into packed records, exchange them with one all-to-all, merge the
+    owned rows into this rank's engine. With impact=True returns the crsql_rows_impacted() growth
+    of THIS rank's input changes, in the caller's order (a second, 1-byte-per-change all-to-all
+    sends every flag back to its sender, and the partition's permutation restores the order)."""
+    import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     if world == 1:
-        return engine.apply(batch, impact=impact), None
-    parts, counts = engine.partition(batch, world)
-    mine = exchange(parts, counts, group)
-    return engine.apply(mine, impact=impact), mine
+        return engine.apply(batch, impact=impact)
+    if verify:
+        n_sites = engine.site_count()
+        if getattr(engine, "_sites_verified", None) != n_sites:
+            verify_sites(engine, group)
+            engine._sites_verified = n_sites
+    recs, rb, counts, perm = engine.partition_packed(batch, world, with_perm=impact)
+    got, rcounts = exchange_records(recs, rb, counts, group)
+    mine = engine.unpack_records(got, rb)
+    imp = engine.apply(mine, impact=impact)
+    if not impact:
+        return None
+    # flags back to the senders (reverse split sizes), then into the caller's order
+    dev = imp.device
+    back = torch.empty(sum(counts), dtype=torch.uint8, device=dev)
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        b2 = torch.empty(sum(counts), dtype=torch.uint8)
+        dist.all_to_all_single(b2, imp[:sum(rcounts)].cpu(), [int(c) for c in counts], rcounts, group=group)
+        back = b2.to(dev)
+    else:
+        dist.all_to_all_single(back, imp[:sum(rcounts)].contiguous(), [int(c) for c in counts], rcounts, group=group)
+    out = torch.empty_like(back)
+    out[perm.long()] = back
+    return out

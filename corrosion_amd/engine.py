@@ -27,6 +27,15 @@ def _is_torch(x):
     return type(x).__module__.startswith("torch")
 
 
+def _int_dtype_ok(t, dt):
+    """A device field's tensor must be an integer type of the field's width (signed or unsigned: the
+    C ABI reads the bits); a float, bool or wider/narrower tensor is rejected, not reinterpreted."""
+    import torch
+    ok = {8: (torch.int64, getattr(torch, "uint64", None)), 4: (torch.int32, getattr(torch, "uint32", None)),
+          2: (torch.int16, getattr(torch, "uint16", None)), 1: (torch.uint8, torch.int8)}
+    return t.dtype in ok.get(np.dtype(dt).itemsize, ())
+
+
 class MergeEngine:
     def __init__(self, schema, capacity_hint=1 << 20, device=0):
         """schema: {table_name: [column names]} in table order (cid k = column k-1, cid 0 = '-1')."""
@@ -104,8 +113,9 @@ class MergeEngine:
                 setattr(s, k, None)
                 continue
             if on_dev:
-                if not a.is_cuda or not a.is_contiguous() or a.element_size() != np.dtype(dt).itemsize:
-                    raise ValueError(f"device field {k} must be a contiguous CUDA tensor of {np.dtype(dt)}")
+                if not a.is_cuda or not a.is_contiguous() or not _int_dtype_ok(a, dt):
+                    raise ValueError(f"device field {k} must be a contiguous CUDA integer tensor of {np.dtype(dt)} width "
+                                     f"(got {a.dtype})")
                 if int(a.shape[0]) != n:
                     raise ValueError(f"field {k} has {a.shape[0]} elements, expected {n}")
                 setattr(s, k, a.data_ptr() if n else None)
@@ -204,6 +214,55 @@ class MergeEngine:
         L.check(L.lib().corro_partition_ranks(self._h, C.byref(s), nranks, C.byref(o), counts.ctypes.data))
         return out, [int(c) for c in counts[:nranks]]
 
+    def _device_changes(self, batch):
+        n = int(batch["pk"].shape[0])
+        s = L.Changes()
+        s.n = n
+        for k, dt in BATCH_FIELDS.items():
+            a = batch.get(k)
+            if a is None:
+                setattr(s, k, None)
+                continue
+            if not a.is_cuda or not a.is_contiguous() or not _int_dtype_ok(a, dt) or int(a.shape[0]) != n:
+                raise ValueError(f"field {k} must be a contiguous CUDA integer tensor of {n} x {np.dtype(dt)} width")
+            setattr(s, k, a.data_ptr() if n else None)
+        return s
+
+    def partition_packed(self, batch, nranks, with_perm=False):
+        """Stable pk-hash partition of a device batch into whole packed records grouped by owner
+        rank (corro_partition_packed): returns (uint8 CUDA tensor of n * rec_bytes, rec_bytes,
+        per-rank counts, perm or None) -- one tensor, so one all-to-all moves every field."""
+        import torch
+        s = self._device_changes(batch)
+        n = int(s.n)
+        rb = C.c_uint32()
+        L.check(L.lib().corro_packed_record_bytes(C.byref(s), C.byref(rb)))
+        recs = torch.empty(max(n, 1) * rb.value, dtype=torch.uint8, device=batch["pk"].device)
+        perm = torch.empty(max(n, 1), dtype=torch.int32, device=batch["pk"].device) if with_perm else None
+        counts = np.zeros(max(1, nranks), np.uint64)
+        torch.cuda.current_stream().synchronize()
+        L.check(L.lib().corro_partition_packed(self._h, C.byref(s), nranks, recs.data_ptr(),
+                                               perm.data_ptr() if perm is not None else None, counts.ctypes.data))
+        return recs[:n * rb.value], rb.value, [int(c) for c in counts[:nranks]], (perm[:n] if perm is not None else None)
+
+    def unpack_records(self, recs, rec_bytes, out=None):
+        """Packed records (a uint8 CUDA tensor) -> SoA device batch (corro_unpack_records)."""
+        import torch
+        n = int(recs.numel()) // rec_bytes
+        dev = recs.device
+        if out is None:
+            tdt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}
+            keys = [k for k in BATCH_FIELDS if k in REQUIRED or rec_bytes == 80]
+            out = {k: torch.empty(max(n, 1), dtype=tdt[BATCH_FIELDS[k]], device=dev)[:n] for k in keys}
+        s = L.Changes()
+        s.n = n
+        for k in BATCH_FIELDS:
+            a = out.get(k)
+            setattr(s, k, a.data_ptr() if (a is not None and n) else None)
+        torch.cuda.current_stream().synchronize()
+        L.check(L.lib().corro_unpack_records(self._h, recs.data_ptr() if n else None, n, rec_bytes, C.byref(s)))
+        return out
+
     # ---- wire decode ------------------------------------------------------------------------
     def decode_frames(self, buf, payload=0):
         """Decode length-delimited speedy frames (corro_decode_frames; payload 0 = SyncMessage,
@@ -248,8 +307,9 @@ class MergeEngine:
                 setattr(s, k, None)
                 continue
             if on_dev:
-                if not a.is_cuda or not a.is_contiguous() or a.element_size() != np.dtype(dt).itemsize:
-                    raise ValueError(f"device need field {k} must be a contiguous CUDA tensor of {np.dtype(dt)}")
+                if not a.is_cuda or not a.is_contiguous() or not _int_dtype_ok(a, dt):
+                    raise ValueError(f"device need field {k} must be a contiguous CUDA integer tensor of "
+                                     f"{np.dtype(dt)} width (got {a.dtype})")
                 setattr(s, k, a.data_ptr() if n else None)
             else:
                 a = np.ascontiguousarray(a, dtype=dt)

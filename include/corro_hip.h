@@ -174,6 +174,19 @@ int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count)
 int corro_partition_ranks(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, corro_changes *out,
                           uint64_t *counts);
 
+/* The same partition as whole packed records, for ONE all-to-all of records per exchange (instead
+ * of one per SoA field): `out` (device, 16-B aligned) receives in->n records grouped by destination
+ * rank, each group in input order. Records are 48 B (pk, col_version, db_version,
+ * val0, table_cid, cl, seq, site) when the batch has no val1/val_type/val_len/ts arrays, else 80 B
+ * (every field); corro_packed_record_bytes says which. perm (optional, device, in->n) receives the
+ * source index of every packed record (to return per-change results to the sender's order). */
+int corro_packed_record_bytes(const corro_changes *in, uint32_t *bytes);
+int corro_partition_packed(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, void *out, uint32_t *perm,
+                           uint64_t *counts);
+/* Received records (concatenated by source rank) -> the SoA batch corro_apply_batch takes (device
+ * arrays, n each; optional arrays may be NULL). rec_bytes = 48 or 80. */
+int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n, uint32_t rec_bytes, corro_changes *out);
+
 /* ------------------------------------------------------------------ sync need diff */
 
 /* CSR over (node-pair, actor) entries of two SyncStateV1 (sync.rs:79-87). One entry = one

@@ -134,13 +134,16 @@ def adversarial_schema(ntables):
     return {f"t{k}": list(ADV_COLS) for k in range(ntables)}
 
 
-def uniform_batch_torch(n, nactors, npk, ncols, seed, device="cuda", cv_max=8, per_version=64):
-    """Config 2 generated in HBM (torch), same distribution as uniform_batch."""
+def uniform_batch_torch(n, nactors, npk, ncols, seed, device="cuda", cv_max=8, per_version=64, offset=0,
+                        global_n=None):
+    """Config 2 generated in HBM (torch), same distribution as uniform_batch. `offset` / `global_n`
+    generate the slice [offset, offset + n) of a global batch of global_n changes (config 3's
+    rank-major batch: actors, versions and seqs numbered over the whole batch)."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
-    per_actor = -(-n // nactors)
-    i = torch.arange(n, device=device, dtype=torch.int64)
+    per_actor = -(-(global_n or n) // nactors)
+    i = torch.arange(offset, offset + n, device=device, dtype=torch.int64)
     site = (i // per_actor).to(torch.int32)
     local = i % per_actor
     dbv = local // per_version + 1

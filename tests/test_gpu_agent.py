@@ -207,3 +207,33 @@ def test_loadshed_handle_changes():
         running += q.job_done()
     assert a.bookie.contains_all(other, (6, 10)) and a.bookie.contains_all(other, (1, 3))
     assert not a.bookie.contains_all(other, (5, 5)) and not a.bookie.contains_all(other, (4, 4))
+
+
+def test_failed_call_leaves_bookkeeping_untouched():
+    """one call holding an empty version (crsql_set_db_version), an incomplete version
+    (buffered rows + seq bookkeeping) and a complete version whose sentinel col_version is outside
+    the engine encoding: the merge fails, and -- as the reference's single transaction rolls back
+    (util.rs:749, :849-855, :936) -- nothing of the call remains: no db_version bump, no buffered
+    rows or partial, no gap bookkeeping."""
+    import corrosion_amd as ca
+    from corrosion_amd.agent import Change, ChangeV1, Empty, Full
+    a = agent()
+    X, Y, Z = bytes([3] * 16), bytes([4] * 16), bytes([5] * 16)
+    for s in (X, Y, Z):
+        a.site(s)
+    dbv0 = list(a.engine.db_versions())
+    empty = ChangeV1(X, Empty((1, 5)))
+    part = ChangeV1(Y, Full(1, [Change("tests", 1, "text", "p", 1, 1, 0, Y, 1)], (0, 0), 3, ts=1))
+    poison = ChangeV1(Z, Full(1, [Change("tests", 2, "-1", None, 1 << 33, 1, 0, Z, 2)], (0, 0), 0, ts=1))
+    with pytest.raises(ca.CorroError):
+        a.process_multiple_changes([empty, part, poison])
+    assert list(a.engine.db_versions()) == dbv0
+    assert a.bookie.partial(Y, 1) is None
+    assert a.bookie.last(X) is None and a.bookie.last(Y) is None and a.bookie.last(Z) is None
+    assert state_rows(a) == {}
+    st = a.generate_sync()
+    assert st.heads == {} and st.partial_need == {}
+    # the same call without the poisoned version goes through
+    r = a.process_multiple_changes([empty, part])
+    assert r.known == ["cleared", "partial"]
+    assert a.bookie.partial(Y, 1) is not None and a.bookie.last(X) == 5

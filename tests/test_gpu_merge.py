@@ -358,3 +358,41 @@ def test_config2_full_size_vs_sharded_oracle():
     assert O.rows_digest(e.export()) == f.digest()
     assert np.array_equal(e.db_versions(), f.db_versions())
     e.close()
+
+
+@pytest.mark.parametrize("impact", [False, True])
+def test_chunked_apply_equals_one_apply(monkeypatch, impact):
+    """A batch larger than the merge's chunk is applied as consecutive chunks in application order:
+    the left fold makes that the same result as one apply (forced here with a 4096-change chunk)."""
+    monkeypatch.setenv("CORRO_HIP_CHUNK", "4096")
+    seed = 61
+    sites = synth.site_ids(8, seed)
+    b = synth.adversarial_batch(50000, 8, 2, 700, seed)
+    e = engine(synth.adversarial_schema(2), cap=50000, sites=sites)
+    f = O.Fold(sites)
+    got = e.apply(b, impact=impact)
+    want = f.apply(b)
+    if impact:
+        assert np.array_equal(got, want)
+    compare(e, f, with_ts=True)
+
+
+def test_chunked_apply_validates_before_the_first_chunk(monkeypatch):
+    """An error in the LAST chunk of a chunked apply leaves the state as it was: the whole batch is
+    validated before any chunk commits."""
+    import corrosion_amd as ca
+    monkeypatch.setenv("CORRO_HIP_CHUNK", "4096")
+    seed = 62
+    sites = synth.site_ids(8, seed)
+    e = engine(synth.adversarial_schema(1), cap=1 << 14, sites=sites)
+    e.apply(synth.adversarial_batch(3000, 8, 1, 300, seed))
+    before = rows_to_tuples(e.export(), with_ts=True)
+    dv = list(e.db_versions())
+    b = synth.adversarial_batch(20000, 8, 1, 300, seed + 1)
+    b["table_cid"] = b["table_cid"].copy()
+    b["table_cid"][-1] = 7  # cid 7 of table 0 does not exist
+    with pytest.raises(ca.CorroError) as ex:
+        e.apply(b)
+    assert ex.value.code == -5
+    assert rows_to_tuples(e.export(), with_ts=True) == before
+    assert list(e.db_versions()) == dv

@@ -116,10 +116,15 @@ def test_decode_large_frames_and_errors():
                                                                             ACT[3], 1)], (0, 0), 0, ts=1)))
     text_pk = wire.encode_sync_changeset(ChangeV1(ACT[3], Full(5, [Change("users", b"\x01\x03\x01a", "name", "y", 1, 5,
                                                                           0, ACT[3], 1)], (0, 0), 0, ts=1)))
-    buf = b"".join(wire.frame(x) for x in (wire.encode_sync_changeset(big), clock, good, trunc, long_text, text_pk))
+    # a Full changeset that claims 2^32-1 changes in a 25-byte body: malformed, and sizes nothing
+    huge = struct.pack("<II", 0, 1) + bytes(ACT[4]) + struct.pack("<IQI", 1, 7, 0xFFFFFFFF)
+    buf = b"".join(wire.frame(x) for x in (wire.encode_sync_changeset(big), clock, good, trunc, long_text, text_pk,
+                                           huge))
     eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 14)
     dec = eng.decode_frames(buf)
-    assert list(dec["status"]) == [0, 1, 0, -1, -6, -6]
+    assert list(dec["status"]) == [0, 1, 0, -1, -6, -6, -1]
+    assert dec["cs"][6].change_count == 0
+    assert len(dec["changes"]["pk"]) <= 1500 + 200 + 5 + 1 + 1
     cs0 = dec["cs"][0]
     assert cs0.change_count == 1500 and cs0.last_seq == 1499 and cs0.ts == 5
     for k in (0, 777, 1499):
