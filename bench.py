@@ -235,6 +235,7 @@ def run_single(args, traffic, traffic_note):
     pipe_ms = sum(kern.values())
     alg_bytes = ALG_BYTES_PER_CHANGE * n + ALG_BYTES_PER_CELL * cells
     achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
+    steady = steady_state(eng, prep, n, dev, dt / args.steps * 1e3, cells)
     cpu = None if args.no_cpu_baseline else cpu_baseline(batch)
     line = {
         "metric": METRIC,
@@ -259,9 +260,34 @@ def run_single(args, traffic, traffic_note):
                      "alg_bytes_per_apply": alg_bytes, "pipeline_ms": pipe_ms, "kernels_ms": kern,
                      "dominant": max(kern, key=kern.get)},
         "cpu_baseline": cpu,
+        "steady_state": steady,
     }
     print(json.dumps(line), flush=True)
     eng.close()
+
+
+def steady_state(eng, prep, n, dev, empty_ms, cells, reps=3):
+    """The same-size config-2 batch (another seed) applied into the populated state the headline
+    batch leaves (16.5M cells): the in-place row store's apply cost against the empty-state one."""
+    import torch
+    import synth
+    other = synth.uniform_batch_torch(n, N_ACTORS, N_PK, N_COLS, seed=synth.config_seed(2) + 1, device=dev)
+    prep2 = eng.prepare(other)
+    ms = []
+    for _ in range(reps):
+        eng.reset()
+        eng.apply_prepared(prep)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.apply_prepared(prep2)
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) * 1e3)
+    ms.sort()
+    med = ms[len(ms) // 2]
+    del other, prep2
+    return {"ms": med, "state_cells_before": int(cells), "ratio_vs_empty_state": med / empty_ms,
+            "note": "a second 64M config-2 batch applied into the ~16.5M-cell state of the first (median of "
+                    f"{reps}); empty-state step = reset + apply"}
 
 
 def run_multi(args, world, rank):

@@ -33,7 +33,8 @@ EXPORTS = [
     "corro_compute_needs_onepass", "corro_needs_bound", "corro_extract_changes",
     "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
-    "corro_unpack_records",
+    "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
+    "corro_pk_canonical",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -191,6 +192,10 @@ def lib():
         "corro_packed_record_bytes": (i32, [C.POINTER(Changes), vp]),
         "corro_partition_packed": (i32, [vp, C.POINTER(Changes), u32, vp, vp, vp]),
         "corro_unpack_records": (i32, [vp, vp, u64, u32, C.POINTER(Changes)]),
+        "corro_table_set_pk_interned": (i32, [vp, u32, i32]),
+        "corro_pk_keys": (i32, [vp, u32, vp, vp, u64, vp]),
+        "corro_pk_bytes": (i32, [vp, u32, vp, u64, vp, u64, vp]),
+        "corro_pk_canonical": (i32, [C.c_char_p, u64, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -20,7 +20,7 @@ from .sync import SyncStateV1
 @dataclass
 class Change:
     table: str
-    pk: int                 # single INTEGER primary key value (row key)
+    pk: object              # INTEGER pk value, or pack_columns bytes (interned tables: any pk)
     cid: str                # column name, "-1" = row sentinel
     val: object             # None | int | float | str | bytes  (SqliteValue)
     col_version: int
@@ -132,11 +132,31 @@ class Bookie:
 class Agent:
     """One node's writer: the device merge engine + its Bookie (agent.rs:480-482 single writer)."""
 
-    def __init__(self, schema, capacity_hint=1 << 20, device=0, actor_id=b"\0" * 16):
-        self.engine = MergeEngine(schema, capacity_hint=capacity_hint, device=device)
+    def __init__(self, schema, capacity_hint=1 << 20, device=0, actor_id=b"\0" * 16, interned=()):
+        self.engine = MergeEngine(schema, capacity_hint=capacity_hint, device=device, interned=interned)
         self.bookie = Bookie()
         self.actor_id = actor_id
         self.site_ids = {}      # ordinal -> 16-byte site id (crsql_site_id)
+
+    def row_keys(self, changes):
+        """Row keys of the changes' primary keys: an INTEGER pk is its own key; an interned table's
+        pk (pack_columns bytes, or an int packed as one INTEGER column) goes through corro_pk_keys."""
+        from .wire import pack_int_pk, unpack_int_pk
+        keys = np.zeros(len(changes), np.uint64)
+        by_table = {}
+        for j, ch in enumerate(changes):
+            if ch.table in self.engine.interned:
+                packed = bytes(ch.pk) if isinstance(ch.pk, (bytes, bytearray)) else pack_int_pk(ch.pk)
+                by_table.setdefault(ch.table, ([], []))
+                by_table[ch.table][0].append(j)
+                by_table[ch.table][1].append(packed)
+            elif isinstance(ch.pk, (bytes, bytearray)):
+                keys[j] = unpack_int_pk(bytes(ch.pk)) & 0xFFFFFFFFFFFFFFFF
+            else:
+                keys[j] = ch.pk & 0xFFFFFFFFFFFFFFFF
+        for table, (idx, packed) in by_table.items():
+            keys[idx] = self.engine.pk_keys(table, packed)
+        return keys
 
     def site(self, site_id):
         o = int(self.engine.register_sites(np.frombuffer(bytes(site_id), np.uint8).reshape(1, 16))[0])
@@ -189,13 +209,13 @@ class Agent:
             ("pk", np.uint64), ("table_cid", np.uint32), ("col_version", np.int64), ("db_version", np.int64),
             ("cl", np.uint32), ("seq", np.uint32), ("site", np.uint32), ("val0", np.uint64),
             ("val1", np.uint64), ("val_type", np.uint8), ("val_len", np.uint8))}
+        arr["pk"][:n] = self.row_keys(rows)
         for j, ch in enumerate(rows):
             try:
                 tc = self.engine.lookup(ch.table, ch.cid)
             except L.CorroError:
                 tc = L.CORRO_TCID_UNKNOWN
             t, v0, v1, ln = encode_value(ch.val)
-            arr["pk"][j] = ch.pk & 0xFFFFFFFFFFFFFFFF
             arr["table_cid"][j] = tc
             arr["col_version"][j] = ch.col_version
             arr["db_version"][j] = ch.db_version

@@ -10,8 +10,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcorro_hip.so")
-SOURCES = ["engine.hip", "sync_needs.hip", "partition.hip", "prims.hip", "extract.hip", "wire.hip", "booked.cpp", "agent.cpp"]
-HEADERS = ["internal.h", "merge_kernels.h", "ovf_kernels.h", "ranges.h", "booked.h", "rowhash.h"]
+SOURCES = ["engine.hip", "sync_needs.hip", "partition.hip", "prims.hip", "extract.hip", "wire.hip", "booked.cpp", "agent.cpp",
+           "pkeys.hip"]
+HEADERS = ["internal.h", "merge_kernels.h", "ovf_kernels.h", "ranges.h", "booked.h", "rowhash.h", "rowstore.h"]
 ARCH = "gfx950"
 
 
@@ -41,6 +42,7 @@ def _stale():
 def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
+    src_hash = _source_hash()  # of the sources this build compiles (not of later edits)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     from concurrent.futures import ThreadPoolExecutor
     jobs = []
@@ -68,7 +70,7 @@ def build(force=False, verbose=False):
     for o in objs:
         os.remove(o)
     with open(STAMP, "w") as f:
-        f.write(_source_hash())
+        f.write(src_hash)
     return LIB
 
 

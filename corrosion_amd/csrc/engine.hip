@@ -66,50 +66,54 @@ int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, 
 int ovf_scan_tiles(void *temp, size_t *temp_bytes, const OvfDev &d, const CsAgg *in, CsAgg *out, uint32_t n,
                    hipStream_t s);
 
-// Oversized buckets (after the first merge pass queued them), all at once and device-wide (the
-// phases of ovf_kernels.h): fields + row ids -> sort by (bucket base + row, position) -> L scan ->
-// classify -> epoch scan -> candidate keys -> sort -> argmax / group-start scans -> link -> walk
-// -> [impacts] -> per-bucket counts.
+int grow_regions(corro_ctx *ctx, uint32_t new_log2S);
+int grow_heap(corro_ctx *ctx, uint64_t want_records);
+RowStore row_store(corro_ctx *ctx);
+
+// Oversized buckets (queued by a merge round), all at once and device-wide (the phases of
+// ovf_kernels.h): batch fields + row ids -> region lookups (prior records appended, new rows
+// counted; the store grows here if they do not fit, before anything is written) -> sort by (row,
+// position) -> L scan -> classify -> epoch scan -> candidate keys -> sort -> argmax / group-start
+// scans -> link -> walk (rows written back to the heap) -> [impacts] -> region fill counts.
 static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nbatch, bool prof) {
     hipStream_t s = ctx->stream;
     const uint32_t B = ctx->B;
-    std::vector<uint32_t> list(novf), pc(B), nc(B);
+    std::vector<uint32_t> list(novf), nc(B);
     CORRO_HIP_TRY(hipMemcpy(list.data(), ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost));
-    CORRO_HIP_TRY(hipMemcpy(pc.data(), ctx->d_state_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
     CORRO_HIP_TRY(hipMemcpy(nc.data(), ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
     std::vector<uint32_t> koff(novf + 1), soff(novf);
-    uint64_t K = 0, S = 0, PM = 0;
+    uint64_t Kb = 0, S = 0;
     for (uint64_t k = 0; k < novf; k++) {
-        const uint64_t n = (uint64_t)pc[list[k]] + nc[list[k]];
-        PM = std::max<uint64_t>(PM, pc[list[k]]);
+        const uint64_t n = nc[list[k]];
         uint64_t sl = 1;
         while (sl < 2 * n) sl <<= 1;
-        koff[k] = (uint32_t)K;
+        koff[k] = (uint32_t)Kb;
         soff[k] = (uint32_t)S;
-        K += n;
+        Kb += n;
         S += sl;
-        if (K >= (1ULL << 31) || S >= (1ULL << 32))
-            return fail(CORRO_E_RANGE, "oversized buckets hold more than 2^31 records");
     }
-    koff[novf] = (uint32_t)K;
-    // row ids (< K) take rb bits with one spare value above them, so that ~0 sorts last
-    uint32_t rb = 1;
-    while ((1ULL << rb) <= K) rb++;
-    // compact positions: prior slice index < PM, batch change i -> PM + i
+    koff[novf] = (uint32_t)Kb;
+    // prior records: at most one heap row per batch row, at most the whole state
+    const uint64_t Kmax = Kb + std::min<uint64_t>(ctx->state_total, Kb * (uint64_t)ctx->max_stride);
+    if (Kmax >= (1ULL << 31) || S >= (1ULL << 32))
+        return fail(CORRO_E_RANGE, "oversized buckets hold more than 2^31 records");
+    // compact positions: prior slots [0, pm), batch change i -> pm + i
+    const uint32_t pm = ctx->max_stride;
     uint32_t pbits = 1;
-    while ((1ULL << pbits) < PM + nbatch) pbits++;
-    uint32_t maxc = 0, cid_bits = 1;
-    for (const auto &t : ctx->tables) maxc = std::max<uint32_t>(maxc, (uint32_t)t.cols.size());
-    while ((1u << cid_bits) <= maxc) cid_bits++;
+    while ((1ULL << pbits) < pm + nbatch) pbits++;
+    uint32_t rb = 1;  // record positions (< Kmax) with one spare value above them, so that ~0 sorts last
+    while ((1ULL << rb) <= Kmax) rb++;
+    uint32_t cid_bits = 1;
+    while ((1u << cid_bits) <= ctx->max_stride - 1) cid_bits++;
     const uint32_t ckey_bits = rb + cid_bits;
     auto al = [](uint64_t x) { return (x + 255) & ~255ULL; };
     // pass 0 sizes the arrays, pass 1 carves them out of d_ovf_sort
     OvfDev d{};
     d.G = (uint32_t)novf;
-    d.K = (uint32_t)K;
+    d.K = (uint32_t)Kmax;
+    d.Kb = (uint32_t)Kb;
     d.cid_bits = cid_bits;
-    d.rshift = pbits;
-    d.pm = (uint32_t)PM;
+    d.pm = pm;
     uint64_t bytes = 0;
     uint8_t *base = nullptr;
     auto take = [&](uint64_t n) {
@@ -121,23 +125,28 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     size_t temp = 0;
     uint32_t nt = 0, *cs_first = nullptr;
     CsAgg *cs_agg = nullptr, *cs_incl = nullptr;
+    const uint64_t K = Kmax, R = std::max<uint64_t>(Kb, 1);
     for (int pass = 0; pass < 2; pass++) {
         bytes = 0;
         d.koff = (const uint32_t *)take((novf + 1) * 4);
         d.slot_off = (const uint32_t *)take(novf * 4);
-        d.ocnt = (uint32_t *)take(novf * 4);
-        d.oflag = (uint32_t *)take(novf * 4);
-        d.slots = (uint32_t *)take(S * 4);
+        d.bnew = (uint32_t *)take(novf * 4);
+        d.bnrec = (uint32_t *)take(novf * 4);
+        d.slots = (uint32_t *)take(std::max<uint64_t>(S, 2 * K) * 4);
         uint64_t **u64s[] = {&d.pk, &d.key, &d.key_s, &d.ckey, &d.ckey_s};
         for (uint64_t **p : u64s) *p = (uint64_t *)take(K * 8);
         d.cv = (int64_t *)take(K * 8);
         d.ccv = (int64_t *)take(K * 8);
         d.qkey = (OvfKey *)take(K * sizeof(OvfKey));
-        uint32_t **u32s[] = {&d.tc,    &d.cl,     &d.pos,   &d.val,    &d.val_s, &d.rowid,
-                             &d.cl_s,  &d.lx,     &d.recf,  &d.epc,   &d.kind,  &d.pb,     &d.rstart, &d.rbad,
-                             &d.rnrec, &d.recs,   &d.head,  &d.scid,  &d.spos,  &d.sz,     &d.ccid,  &d.csrc,
-                             &d.cval,  &d.cval_s, &d.cbest, &d.cgs,   &d.nxt,   &d.fstg};
+        d.pkey = (OvfKey *)take((K - Kb + 1) * sizeof(OvfKey));
+        uint32_t **u32s[] = {&d.tc,    &d.cl,    &d.pos,   &d.src,   &d.val,   &d.val_s, &d.rowid, &d.cl_s,
+                             &d.lx,    &d.recf,  &d.epc,   &d.kind,  &d.pb,    &d.rstart, &d.rbad, &d.rnrec,
+                             &d.recs,  &d.head,  &d.scid,  &d.spos,  &d.sz,    &d.ccid,  &d.csrc,  &d.cval,
+                             &d.cval_s, &d.cbest, &d.cgs,  &d.nxt,   &d.fstg};
         for (uint32_t **p : u32s) *p = (uint32_t *)take(K * 4);
+        uint32_t **rows[] = {&d.rowner, &d.rb, &d.rheap, &d.rprior, &d.rpoff};
+        for (uint32_t **p : rows) *p = (uint32_t *)take(R * 4);
+        d.rbits = (uint64_t *)take(R * 16);
         if (pass == 0) {
             size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
             TRY(ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, d.K, 64, s));
@@ -160,33 +169,63 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     }
     CORRO_HIP_TRY(hipMemcpyAsync((void *)d.koff, koff.data(), (novf + 1) * 4, hipMemcpyHostToDevice, s));
     CORRO_HIP_TRY(hipMemcpyAsync((void *)d.slot_off, soff.data(), novf * 4, hipMemcpyHostToDevice, s));
-    CORRO_HIP_TRY(hipMemsetAsync(d.ocnt, 0, novf * 4, s));
-    CORRO_HIP_TRY(hipMemsetAsync(d.oflag, 0, novf * 4, s));
+    CORRO_HIP_TRY(hipMemsetAsync(d.bnew, 0, novf * 4, s));
+    CORRO_HIP_TRY(hipMemsetAsync(d.bnrec, 0, novf * 4, s));
     CORRO_HIP_TRY(hipMemsetAsync(d.slots, 0, S * 4, s));
     if (prof) (void)hipEventRecord(ctx->ev[6], s);
-    const dim3 blk(256), grid((uint32_t)std::min<uint64_t>((K + 255) / 256, 8192));
+    auto grid_for = [](uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192))); };
+    const dim3 blk(256), gridb = grid_for(Kb);
     auto launched = [&]() -> int {
         CORRO_HIP_TRY(hipGetLastError());
         return CORRO_OK;
     };
-    hipLaunchKernelGGL(k_ovf_load, grid, blk, 0, s, a, d);
-    hipLaunchKernelGGL(k_ovf_rowhash, grid, blk, 0, s, d);
+    hipLaunchKernelGGL(k_ovf_load, gridb, blk, 0, s, a, d);
+    hipLaunchKernelGGL(k_ovf_rowhash, gridb, blk, 0, s, d);
     TRY(launched());
     // dense row ids: the row count sizes the sort's key
-    TRY(prim_inclusive_scan_u32(d_temp, &temp, d.recf, d.epc, d.K, s));
+    TRY(prim_inclusive_scan_u32(d_temp, &temp, d.recf, d.epc, d.Kb, s));
     uint32_t nrows = 0;
-    CORRO_HIP_TRY(hipMemcpyAsync(&nrows, d.epc + (K - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&nrows, d.epc + (Kb - 1), 4, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    d.nrows = nrows;
+    // every row looked up in its region; prior records counted, new rows counted per bucket
+    hipLaunchKernelGGL(k_ovf_lookup, gridb, blk, 0, s, a, d);
+    TRY(launched());
+    TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
+    uint32_t P = 0;
+    std::vector<uint32_t> bnew(novf), bnrec(novf), used(B);
+    CORRO_HIP_TRY(hipMemcpyAsync(&P, d.rpoff + (nrows - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(bnew.data(), d.bnew, novf * 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(bnrec.data(), d.bnrec, novf * 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(used.data(), ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost, s));
+    unsigned long long top = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&top, ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (Kb + (uint64_t)P > Kmax) return fail(CORRO_E_DEVICE, "internal: overflow prior records exceed their bound");
+    // room for the new rows (region fill, heap) before the walk writes anything
+    uint64_t need_heap = 0;
+    uint32_t need_log2S = ctx->log2S;
+    for (uint64_t k = 0; k < novf; k++) {
+        need_heap += bnrec[k];
+        const uint64_t want = (uint64_t)used[list[k]] + bnew[k];
+        while (want > ((7ULL << need_log2S) >> 3)) need_log2S++;
+    }
+    if (need_log2S != ctx->log2S) TRY(grow_regions(ctx, need_log2S));
+    if (top + need_heap > ctx->heap_cap) TRY(grow_heap(ctx, top + need_heap));
+    a.rs = row_store(ctx);
+    d.K = (uint32_t)(Kb + P);
+    const dim3 grid = grid_for(d.K);
     uint32_t rbits = 1;
     while ((1ULL << rbits) < nrows) rbits++;
     const uint32_t key_bits = rbits + pbits;
-    d.nrows = nrows;
+    d.rshift = pbits;
     if (key_bits > 64) return fail(CORRO_E_RANGE, "overflow sort key exceeds 64 bits");
     static const bool dbg = std::getenv("CORRO_HIP_OVF_DEBUG") != nullptr;
     if (dbg)
-        fprintf(stderr, "[corro ovf] buckets %llu records %llu rows %u key bits %u (+%u) cand key bits %u\n",
-                (unsigned long long)novf, (unsigned long long)K, nrows, key_bits, rbits, ckey_bits);
-    hipLaunchKernelGGL(k_ovf_rowkey, grid, blk, 0, s, d);
+        fprintf(stderr, "[corro ovf] buckets %llu batch records %llu prior %u rows %u key bits %u (+%u) cand key bits %u\n",
+                (unsigned long long)novf, (unsigned long long)Kb, P, nrows, key_bits, rbits, ckey_bits);
+    hipLaunchKernelGGL(k_ovf_pload, grid_for(nrows), blk, 0, s, a, d);
+    hipLaunchKernelGGL(k_ovf_rowkey, gridb, blk, 0, s, d);
     TRY(launched());
     TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.key_s, d.val, d.val_s, d.K, key_bits, s));
     hipLaunchKernelGGL(k_ovf_gather, grid, blk, 0, s, d);
@@ -199,17 +238,17 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     hipLaunchKernelGGL(k_ovf_ckeys, grid, blk, 0, s, d);
     TRY(launched());
     // only the candidates are sorted (a minority of the records): compact them first
-    TRY(prim_inclusive_scan_u32(d_temp, &temp, d.slots, d.slots + K, d.K, s));
+    TRY(prim_inclusive_scan_u32(d_temp, &temp, d.slots, d.slots + d.K, d.K, s));
     uint32_t ncand = 0;
-    CORRO_HIP_TRY(hipMemcpyAsync(&ncand, d.slots + K + (K - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&ncand, d.slots + d.K + (d.K - 1), 4, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     hipLaunchKernelGGL(k_ovf_ccompact, grid, blk, 0, s, d);
     TRY(launched());
     if (ncand) TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.ckey_s, d.val, d.cval_s, ncand, ckey_bits, s));
-    if (ncand < K) CORRO_HIP_TRY(hipMemsetAsync(d.ckey_s + ncand, 0xFF, (K - ncand) * 8, s));
+    if (ncand < d.K) CORRO_HIP_TRY(hipMemsetAsync(d.ckey_s + ncand, 0xFF, (d.K - ncand) * 8ULL, s));
     if (dbg) fprintf(stderr, "[corro ovf] candidates %u\n", ncand);
     d.ncand = ncand;
-    const dim3 cgrid((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((ncand + 255) / 256, 8192)));
+    const dim3 cgrid = grid_for(ncand);
     hipLaunchKernelGGL(k_ovf_cgather, cgrid, blk, 0, s, a, d);
     TRY(launched());
     if (ncand) {
@@ -223,14 +262,12 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     if (ncand) TRY(ovf_scans(d_temp, &temp, d, 2, s));
     hipLaunchKernelGGL(k_ovf_link, cgrid, blk, 0, s, d);
     // carried cells in registers when no table has WALK_MAXC or more columns (cids 1..ncols)
-    auto walk = maxc + 1 <= WALK_MAXC ? k_ovf_walk<true> : k_ovf_walk<false>;
-    hipLaunchKernelGGL(walk, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nrows + 255) / 256, 8192))),
-                       blk, 0, s, a, d);
+    auto walk = ctx->max_stride <= WALK_MAXC ? k_ovf_walk<true> : k_ovf_walk<false>;
+    hipLaunchKernelGGL(walk, grid_for(nrows), blk, 0, s, a, d);
     if (a.impact) hipLaunchKernelGGL(k_ovf_impacts, cgrid, blk, 0, s, a, d);
-    hipLaunchKernelGGL(k_ovf_finish, dim3((uint32_t)((novf + 255) / 256)), blk, 0, s, a, d);
+    hipLaunchKernelGGL(k_ovf_finish, grid_for(novf), blk, 0, s, a, d);
     TRY(launched());
     if (prof) (void)hipEventRecord(ctx->ev[7], s);
-    CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, a.misc, 4 * 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     if (prof) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[5], ctx->ev[6], ctx->ev[7]));
     return CORRO_OK;
@@ -263,7 +300,7 @@ static int ctx_prepare_device(corro_ctx *ctx) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(CORRO_E_NO_DEVICE, std::string("libcorro_hip is built for gfx950, device is ") + prop.gcnArchName);
     CORRO_HIP_TRY(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    CORRO_HIP_TRY(hipHostMalloc((void **)&ctx->h_misc, 8 * sizeof(uint64_t), hipHostMallocDefault));
+    CORRO_HIP_TRY(hipHostMalloc((void **)&ctx->h_misc, MISC_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     for (auto &e : ctx->ev) CORRO_HIP_TRY(hipEventCreate(&e));
     const size_t lds_max = 160 * 1024;
     CORRO_HIP_TRY(hipFuncSetAttribute((const void *)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
@@ -272,6 +309,111 @@ static int ctx_prepare_device(corro_ctx *ctx) {
         CORRO_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
     return CORRO_OK;
 }
+
+}  // extern "C"
+
+// Initial row-store sizes from the capacity hint (expected changes per apply): regions at about half
+// fill for hint/4 rows, a heap of hint/2 records; both grow on demand.
+static int store_alloc(corro_ctx *ctx, uint64_t capacity_hint) {
+    const uint32_t B = ctx->B;
+    const uint64_t rows = std::max<uint64_t>(1024, capacity_hint / 4);
+    uint32_t lg = 4;
+    while (((uint64_t)B << lg) < 2 * rows && lg < 20) lg++;
+    ctx->log2S = lg;
+    TRY(ctx->d_ent.ensure(((size_t)B << lg) * sizeof(RowEnt)));
+    TRY(ctx->d_used.ensure(B * 4ULL));
+    TRY(ctx->d_gen.ensure(B * 4ULL));
+    TRY(ctx->d_heap_top.ensure(8));
+    ctx->heap_cap = std::max<uint64_t>(1ULL << 16, capacity_hint / 2);
+    TRY(ctx->d_heap.ensure(ctx->heap_cap * sizeof(Rec)));
+    return CORRO_OK;
+}
+
+static int store_clear(corro_ctx *ctx) {
+    hipStream_t s = ctx->stream;
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_ent.p, 0, ((size_t)ctx->B << ctx->log2S) * sizeof(RowEnt), s));
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_used.p, 0, ctx->B * 4ULL, s));
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_gen.p, 0, ctx->B * 4ULL, s));
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_heap_top.p, 0, 8, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    ctx->state_total = 0;
+    ctx->state_epoch++;
+    return CORRO_OK;
+}
+
+namespace corro {
+RowStore row_store(corro_ctx *ctx) {
+    RowStore rs{};
+    rs.ent = ctx->d_ent.as<RowEnt>();
+    rs.used = ctx->d_used.as<uint32_t>();
+    rs.gen = ctx->d_gen.as<uint32_t>();
+    rs.heap = ctx->d_heap.as<Rec>();
+    rs.heap_ts = ctx->track_ts ? ctx->d_heap_ts.as<uint64_t>() : nullptr;
+    rs.heap_top = ctx->d_heap_top.as<unsigned long long>();
+    rs.heap_cap = ctx->heap_cap;
+    rs.log2S = ctx->log2S;
+    rs.fill = (uint32_t)((7ULL << ctx->log2S) >> 3);
+    rs.stride = ctx->d_stride.as<uint16_t>();
+    return rs;
+}
+
+// Regions rehashed to 2^new_log2S slots (between merge rounds / before an overflow walk: no apply
+// writes are in flight). Entry indices change; heap indices and presence bits move with the rows.
+int grow_regions(corro_ctx *ctx, uint32_t new_log2S) {
+    if (new_log2S <= ctx->log2S) return CORRO_OK;
+    if (new_log2S > 26) return fail(CORRO_E_NOMEM, "row store regions would exceed 2^26 slots");
+    hipStream_t s = ctx->stream;
+    DevBuf nb;
+    TRY(nb.ensure(((size_t)ctx->B << new_log2S) * sizeof(RowEnt)));
+    CORRO_HIP_TRY(hipMemsetAsync(nb.p, 0, ((size_t)ctx->B << new_log2S) * sizeof(RowEnt), s));
+    const uint32_t old_log2S = ctx->log2S;
+    DevBuf old = ctx->d_ent;
+    ctx->d_ent = nb;
+    nb.p = nullptr;
+    ctx->log2S = new_log2S;
+    hipLaunchKernelGGL(k_rehash, dim3(ctx->B), dim3(256), 0, s, old.as<RowEnt>(), old_log2S, row_store(ctx));
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    old.release();
+    return CORRO_OK;
+}
+
+// Heap reallocated to hold at least want_records (doubling), contents copied.
+int grow_heap(corro_ctx *ctx, uint64_t want_records) {
+    if (want_records <= ctx->heap_cap) return CORRO_OK;
+    uint64_t cap = ctx->heap_cap;
+    while (cap < want_records) cap *= 2;
+    if (cap > (1ULL << 32)) cap = 1ULL << 32;
+    if (cap < want_records) return fail(CORRO_E_RANGE, "row store heap would exceed 2^32 records");
+    hipStream_t s = ctx->stream;
+    unsigned long long top = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&top, ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    top = std::min<unsigned long long>(top, ctx->heap_cap);
+    DevBuf nh;
+    TRY(nh.ensure(cap * sizeof(Rec)));
+    CORRO_HIP_TRY(hipMemcpyAsync(nh.p, ctx->d_heap.p, top * sizeof(Rec), hipMemcpyDeviceToDevice, s));
+    DevBuf nts;
+    if (ctx->track_ts) {
+        TRY(nts.ensure(cap * 8));
+        CORRO_HIP_TRY(hipMemsetAsync(nts.p, 0, cap * 8, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(nts.p, ctx->d_heap_ts.p, top * 8, hipMemcpyDeviceToDevice, s));
+    }
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    ctx->d_heap.release();
+    ctx->d_heap = nh;
+    nh.p = nullptr;
+    if (ctx->track_ts) {
+        ctx->d_heap_ts.release();
+        ctx->d_heap_ts = nts;
+        nts.p = nullptr;
+    }
+    ctx->heap_cap = cap;
+    return CORRO_OK;
+}
+}  // namespace corro
+
+extern "C" {
 
 int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t capacity_hint, int device,
                      corro_ctx **out) {
@@ -286,13 +428,14 @@ int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t 
             delete ctx;
             return fail(CORRO_E_INVALID, "table name is NULL");
         }
-        if (tables[t].ncols > 65535) {
+        if (tables[t].ncols > MAX_COLS) {
             delete ctx;
-            return fail(CORRO_E_RANGE, "at most 65535 columns per table");
+            return fail(CORRO_E_RANGE, "at most 127 non-pk columns per table (the row store's presence bits)");
         }
         Table tb;
         tb.name = tables[t].name;
         for (uint32_t c = 0; c < tables[t].ncols; c++) tb.cols.emplace_back(tables[t].col_names[c]);
+        ctx->max_stride = std::max<uint32_t>(ctx->max_stride, tables[t].ncols + 1);
         ctx->table_index[tb.name] = t;
         ctx->tables.push_back(std::move(tb));
     }
@@ -308,42 +451,37 @@ int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t 
         return rc;
     }
     const uint32_t B = ctx->B;
-    rc = ctx->d_state_off.ensure(B * 8ULL);
-    if (!rc) rc = ctx->d_state_cnt.ensure(B * 4ULL);
-    if (!rc) rc = ctx->d_state_flags.ensure(B * 4ULL);
-    if (!rc) rc = ctx->d_out_off.ensure(B * 8ULL);
-    if (!rc) rc = ctx->d_out_cnt.ensure(B * 4ULL);
-    if (!rc) rc = ctx->d_out_flags.ensure(B * 4ULL);
-    if (!rc) rc = ctx->d_new_cnt.ensure(B * 4ULL);
+    rc = ctx->d_new_cnt.ensure(B * 4ULL);
     if (!rc) rc = ctx->d_stage_off.ensure(B * 4ULL);
     if (!rc) rc = ctx->d_bflags.ensure(((B + 31) / 32) * 4ULL);
-    if (!rc) rc = ctx->d_misc.ensure(8 * 8);
+    if (!rc) rc = ctx->d_misc.ensure(MISC_WORDS * 8);
     if (!rc) rc = ctx->d_ovf_list.ensure(B * 4ULL);
     if (!rc) rc = ctx->d_gen_list.ensure(3 * B * 4ULL);
     if (!rc) rc = ctx->d_wide_list.ensure(B * 4ULL);
-    if (!rc) rc = ctx->d_state[0].ensure(64);
-    if (!rc) rc = ctx->d_state[1].ensure(64);
+    if (!rc) rc = ctx->d_defer.ensure(B * 4ULL);
+    if (!rc) rc = ctx->d_relist.ensure(B * 4ULL);
+    if (!rc) rc = store_alloc(ctx, capacity_hint);
     if (rc != CORRO_OK) {
         corro_ctx_destroy(ctx);
         return rc;
     }
     {
-        std::vector<uint16_t> ncols(ctx->tables.size() + 1, 0);
-        for (size_t t = 0; t < ctx->tables.size(); t++) ncols[t] = (uint16_t)ctx->tables[t].cols.size();
+        std::vector<uint16_t> ncols(ctx->tables.size() + 1, 0), stride(ctx->tables.size() + 1, 1);
+        for (size_t t = 0; t < ctx->tables.size(); t++) {
+            ncols[t] = (uint16_t)ctx->tables[t].cols.size();
+            stride[t] = (uint16_t)(ctx->tables[t].cols.size() + 1);
+        }
         rc = ctx->d_ncols.ensure(ncols.size() * 2);
-        if (rc == CORRO_OK && hipMemcpy(ctx->d_ncols.p, ncols.data(), ncols.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+        if (!rc) rc = ctx->d_stride.ensure(stride.size() * 2);
+        if (rc == CORRO_OK &&
+            (hipMemcpy(ctx->d_ncols.p, ncols.data(), ncols.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(ctx->d_stride.p, stride.data(), stride.size() * 2, hipMemcpyHostToDevice) != hipSuccess))
             rc = fail(CORRO_E_DEVICE, "upload of the schema failed");
+        if (rc == CORRO_OK) rc = store_clear(ctx);
         if (rc != CORRO_OK) {
             corro_ctx_destroy(ctx);
             return rc;
         }
-    }
-    (void)hipMemsetAsync(ctx->d_state_off.p, 0, B * 8ULL, ctx->stream);
-    (void)hipMemsetAsync(ctx->d_state_cnt.p, 0, B * 4ULL, ctx->stream);
-    (void)hipMemsetAsync(ctx->d_state_flags.p, 0, B * 4ULL, ctx->stream);
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
-        corro_ctx_destroy(ctx);
-        return fail(CORRO_E_DEVICE, "stream synchronize failed");
     }
     *out = ctx;
     return CORRO_OK;
@@ -352,12 +490,14 @@ int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t 
 void corro_ctx_destroy(corro_ctx *ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    DevBuf *bufs[] = {&ctx->d_site_rank, &ctx->d_dbv, &ctx->d_dbv_batch, &ctx->d_state[0], &ctx->d_state[1],
-                      &ctx->d_state_ts[0], &ctx->d_state_ts[1], &ctx->d_state_off, &ctx->d_state_cnt,
-                      &ctx->d_state_flags, &ctx->d_out_off, &ctx->d_out_cnt, &ctx->d_out_flags, &ctx->d_in,
+    DevBuf *bufs[] = {&ctx->d_site_rank, &ctx->d_dbv, &ctx->d_dbv_batch, &ctx->d_ent, &ctx->d_used, &ctx->d_gen,
+                      &ctx->d_heap, &ctx->d_heap_ts, &ctx->d_heap_top, &ctx->d_stride, &ctx->d_defer,
+                      &ctx->d_relist, &ctx->d_dense, &ctx->d_dense_ts, &ctx->d_dense_view, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export,
-                      &ctx->d_needs, &ctx->d_needs1, &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites, &ctx->d_ncols, &ctx->d_part};
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort,
+                      &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
+                      &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
+                      &ctx->d_ncols, &ctx->d_part};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     for (auto &e : ctx->ev)
@@ -493,16 +633,18 @@ static int error_from_bits(uint64_t bits) {
 
 // One apply of a device-resident chunk (bd: n changes in application order) into the state.
 // imp_buf: device impact flags of this chunk (or null). Returns with the state committed.
+// Merge rounds: the first covers every bucket; a bucket that could not take its new rows (region
+// or heap full) deferred itself before writing anything, the store grows, and the next round
+// merges only the deferred buckets.
 static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     hipStream_t s = ctx->stream;
     const uint32_t n = bd.n;
     const uint32_t B = ctx->B, log2B = ctx->log2B;
     const uint32_t nsites = (uint32_t)ctx->sites.size();
     if (bd.ts && !ctx->track_ts) {
-        // timestamps start being tracked: give the current state zero timestamps
-        const size_t cap_rows = ctx->d_state[ctx->cur].bytes / sizeof(Rec);
-        TRY(ctx->d_state_ts[ctx->cur].ensure(std::max<size_t>(cap_rows, 1) * 8));
-        CORRO_HIP_TRY(hipMemsetAsync(ctx->d_state_ts[ctx->cur].p, 0, std::max<size_t>(cap_rows, 1) * 8, s));
+        // timestamps start being tracked: the state so far has zero timestamps
+        TRY(ctx->d_heap_ts.ensure(ctx->heap_cap * 8));
+        CORRO_HIP_TRY(hipMemsetAsync(ctx->d_heap_ts.p, 0, ctx->heap_cap * 8, s));
         ctx->track_ts = true;
     }
 
@@ -517,15 +659,10 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     tile = (tile + HIST_THREADS - 1) / HIST_THREADS * HIST_THREADS;
     ntiles = (n + tile - 1) / tile;
 
-    const int nxt = ctx->cur ^ 1;
-    const uint64_t out_cap = ctx->state_total + 2ULL * n;
     TRY(ctx->d_hist.ensure((size_t)ntiles * B * 4));
     TRY(ctx->d_stage.ensure((size_t)n * sizeof(Rec)));
-    TRY(ctx->d_state[nxt].ensure(out_cap * sizeof(Rec)));
-    if (ctx->track_ts) TRY(ctx->d_state_ts[nxt].ensure(out_cap * 8));
-
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_bflags.p, 0, ((B + 31) / 32) * 4ULL, s));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, MISC_WORDS * 8, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_dbv_batch.p, 0, (size_t)nsites * 8, s));
     if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 0, n, s));
 
@@ -544,9 +681,8 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     hipLaunchKernelGGL(k_colscan, dim3((B + 255) / 256), dim3(256), 0, s, ctx->d_hist.as<uint32_t>(), ntiles, B,
                        ctx->d_new_cnt.as<uint32_t>());
     mark(2);
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, ctx->d_new_cnt.as<uint32_t>(),
-                       ctx->d_state_cnt.as<uint32_t>(), B, ctx->d_stage_off.as<uint32_t>(),
-                       ctx->d_out_off.as<uint64_t>());
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, ctx->d_new_cnt.as<uint32_t>(), B,
+                       ctx->d_stage_off.as<uint32_t>());
     mark(3);
     {
         static const bool nt_stores = std::getenv("CORRO_HIP_NT") && std::atoi(std::getenv("CORRO_HIP_NT")) != 0;
@@ -563,71 +699,105 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     mark(4);
 
     MergeArgs a{};
-    a.prior = ctx->d_state[ctx->cur].as<Rec>();
-    a.prior_off = ctx->d_state_off.as<uint64_t>();
-    a.prior_cnt = ctx->d_state_cnt.as<uint32_t>();
-    a.prior_flags = ctx->d_state_flags.as<uint32_t>();
-    a.prior_ts = ctx->track_ts && ctx->state_total ? ctx->d_state_ts[ctx->cur].as<uint64_t>() : nullptr;
     a.stage = ctx->d_stage.as<Rec>();
     a.stage_off = ctx->d_stage_off.as<uint32_t>();
     a.new_cnt = ctx->d_new_cnt.as<uint32_t>();
     a.bflags = ctx->d_bflags.as<uint32_t>();
     a.batch_ts = bd.ts;
-    a.out = ctx->d_state[nxt].as<Rec>();
-    a.out_ts = ctx->track_ts ? ctx->d_state_ts[nxt].as<uint64_t>() : nullptr;
-    a.out_off = ctx->d_out_off.as<uint64_t>();
-    a.out_cnt = ctx->d_out_cnt.as<uint32_t>();
-    a.out_flags = ctx->d_out_flags.as<uint32_t>();
+    a.rs = row_store(ctx);
     a.site_rank = ctx->d_site_rank.as<uint32_t>();
     a.nsites = nsites;
     a.impact = imp_buf;
     a.misc = misc;
     a.ovf_list = ctx->d_ovf_list.as<uint32_t>();
+    a.gen_list = ctx->d_gen_list.as<uint32_t>();
+    a.wide_list = ctx->d_wide_list.as<uint32_t>();
+    a.defer_list = ctx->d_defer.as<uint32_t>();
+    a.bucket_list = nullptr;
+    a.B = B;
     // CORRO_HIP_FORCE_GENERAL=1 sends every bucket through the sequential body (cross-checks)
     static const bool force_general = std::getenv("CORRO_HIP_FORCE_GENERAL") &&
                                       std::atoi(std::getenv("CORRO_HIP_FORCE_GENERAL")) != 0;
     a.force_general = force_general ? 1u : 0u;
     a.track_ts = ctx->track_ts ? 1u : 0u;
     a.state_wide = ctx->state_wide ? 1u : 0u;
-    a.gen_list = ctx->d_gen_list.as<uint32_t>();
-    a.wide_list = ctx->d_wide_list.as<uint32_t>();
-    if (a.impact) {
-        hipLaunchKernelGGL(k_merge_fast_int<true>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+    uint32_t nblocks = B;
+    float merge_ms = 0.f, ovf_ms = 0.f;
+    for (int round = 0;; round++) {
+        if (round > 40) return fail(CORRO_E_NOMEM, "internal: the row store did not take the batch's rows");
+        // a batch that failed validation (k_scatter's error bits) is never merged
+        if (round == 0) {
+            CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, 8, hipMemcpyDeviceToHost, s));
+            CORRO_HIP_TRY(hipStreamSynchronize(s));
+            if (ctx->h_misc[0]) return error_from_bits(ctx->h_misc[0]);
+            if (prof)
+                for (int i = 0; i < 4; i++) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[i], ctx->ev[i], ctx->ev[i + 1]));
+        }
+        mark(4);
+        if (a.impact) {
+            hipLaunchKernelGGL(k_merge_fast_int<true>, dim3(nblocks), dim3(MERGE_THREADS), 0, s, a);
+            CORRO_HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(k_merge_fast_wide<true>, dim3(std::min(nblocks, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(k_merge_fast_int<false>, dim3(nblocks), dim3(MERGE_THREADS), 0, s, a);
+            CORRO_HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(k_merge_fast_wide<false>, dim3(std::min(nblocks, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+        }
         CORRO_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_merge_fast_wide<true>, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(k_merge_fast_int<false>, dim3(B), dim3(MERGE_THREADS), 0, s, a);
+        hipLaunchKernelGGL(k_merge_gen_small, dim3(std::min(nblocks, 4 * LIST_GRID)), dim3(GEN_SMALL_THREADS), 0, s, a);
         CORRO_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_merge_fast_wide<false>, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+        hipLaunchKernelGGL(k_merge_gen_mid, dim3(std::min(nblocks, 2 * LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+        CORRO_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_merge_gen, dim3(std::min(nblocks, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+        CORRO_HIP_TRY(hipGetLastError());
+        mark(5);
+        CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, MISC_WORDS * 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        if (prof) {
+            float ms = 0.f;
+            CORRO_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[4], ctx->ev[5]));
+            merge_ms += ms;
+        }
+        const uint64_t novf = ctx->h_misc[MISC_OVF];
+        if (novf) {
+            TRY(run_overflow(ctx, a, novf, n, prof));
+            ovf_ms += ctx->last_ms[5];
+        }
+        const uint64_t ndefer = ctx->h_misc[MISC_DEFER];
+        if (!ndefer) break;
+        // grow what ran out, then merge the deferred buckets again
+        const uint64_t why = ctx->h_misc[MISC_DEFER_WHY];
+        if (why & DEFER_REGION) TRY(grow_regions(ctx, ctx->log2S + 1));
+        if (why & DEFER_HEAP) {
+            unsigned long long top = 0;
+            CORRO_HIP_TRY(hipMemcpy(&top, ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost));
+            TRY(grow_heap(ctx, std::max<uint64_t>(ctx->heap_cap * 2, top + (top >> 2))));
+        }
+        CORRO_HIP_TRY(hipMemcpyAsync(ctx->d_relist.p, ctx->d_defer.p, ndefer * 4, hipMemcpyDeviceToDevice, s));
+        for (int w : {MISC_OVF, MISC_GEN, MISC_WIDEQ, MISC_GEN_SMALL, MISC_GEN_MID, MISC_DEFER, MISC_DEFER_WHY})
+            CORRO_HIP_TRY(hipMemsetAsync(misc + w, 0, 8, s));
+        a.rs = row_store(ctx);
+        a.bucket_list = ctx->d_relist.as<uint32_t>();
+        nblocks = (uint32_t)ndefer;
     }
-    CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_merge_gen_small, dim3(std::min(B, 4 * LIST_GRID)), dim3(GEN_SMALL_THREADS), 0, s, a, B);
-    CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_merge_gen_mid, dim3(std::min(B, 2 * LIST_GRID)), dim3(MERGE_THREADS), 0, s, a, B);
-    CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_merge_gen, dim3(std::min(B, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
-    CORRO_HIP_TRY(hipGetLastError());
-    mark(5);
-    CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, 4 * 8, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipStreamSynchronize(s));
-    if (ctx->h_misc[0]) return error_from_bits(ctx->h_misc[0]);
-    if (prof)
-        for (int i = 0; i < 5; i++) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[i], ctx->ev[i], ctx->ev[i + 1]));
-
-    const uint64_t novf = ctx->h_misc[1];
-    if (novf) TRY(run_overflow(ctx, a, novf, n, prof));
+    if (prof) {
+        ctx->last_ms[4] = merge_ms;
+        ctx->last_ms[5] = ovf_ms;
+    }
     hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
                        ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites);
+    CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, MISC_WORDS * 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
-
-    // commit: the next state becomes current
-    std::swap(ctx->d_state_off, ctx->d_out_off);
-    std::swap(ctx->d_state_cnt, ctx->d_out_cnt);
-    std::swap(ctx->d_state_flags, ctx->d_out_flags);
-    ctx->cur = nxt;
-    ctx->state_total = ctx->h_misc[2];
+    ctx->state_total += ctx->h_misc[MISC_LIVE];  // (a signed delta in two's complement)
     ctx->state_epoch++;
-    if (ctx->h_misc[3]) ctx->state_wide = true;
+    if (ctx->h_misc[MISC_WIDE]) ctx->state_wide = true;
+    // keep the regions under half full for the next batch
+    uint64_t rows_cap = ((uint64_t)B << ctx->log2S) / 2;
+    if (ctx->state_total > rows_cap) {
+        uint32_t lg = ctx->log2S;
+        while (((uint64_t)B << lg) / 2 < ctx->state_total && lg < 26) lg++;
+        TRY(grow_regions(ctx, lg));
+    }
     return CORRO_OK;
 }
 
@@ -721,6 +891,46 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
 }  // extern "C"
 
 namespace corro {
+// The state's clock records as one dense array (+ ts), split into pseudo-buckets of 4096 records
+// for the extraction index's per-bucket kernels; rebuilt once per state epoch.
+int state_dense_view(corro_ctx *ctx, DenseView &v) {
+    const uint64_t m = ctx->state_total;
+    const uint32_t chunk = 4096;
+    const uint32_t nb = (uint32_t)std::max<uint64_t>(1, (m + chunk - 1) / chunk);
+    hipStream_t s = ctx->stream;
+    if (ctx->dense_epoch != ctx->state_epoch) {
+        TRY(ctx->d_dense.ensure(std::max<uint64_t>(m, 1) * sizeof(Rec)));
+        if (ctx->track_ts) TRY(ctx->d_dense_ts.ensure(std::max<uint64_t>(m, 1) * 8));
+        TRY(ctx->d_dense_view.ensure(nb * 12ULL + 256));
+        std::vector<uint64_t> off(nb);
+        std::vector<uint32_t> cnt(nb);
+        for (uint32_t b = 0; b < nb; b++) {
+            off[b] = (uint64_t)b * chunk;
+            cnt[b] = (uint32_t)std::min<uint64_t>(chunk, m - std::min<uint64_t>(m, off[b]));
+        }
+        uint8_t *p = ctx->d_dense_view.as<uint8_t>();
+        CORRO_HIP_TRY(hipMemcpyAsync(p, off.data(), nb * 8ULL, hipMemcpyHostToDevice, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(p + nb * 8ULL, cnt.data(), nb * 4ULL, hipMemcpyHostToDevice, s));
+        unsigned long long *c = (unsigned long long *)(p + ((nb * 12ULL + 7) / 8) * 8);
+        CORRO_HIP_TRY(hipMemsetAsync(c, 0, 8, s));
+        const uint64_t nent = (uint64_t)ctx->B << ctx->log2S;
+        if (m)
+            hipLaunchKernelGGL(k_materialize, dim3((uint32_t)std::min<uint64_t>((nent + 255) / 256, 8192)), dim3(256),
+                               0, s, row_store(ctx), nent, c, ctx->d_dense.as<Rec>(),
+                               ctx->track_ts ? ctx->d_dense_ts.as<uint64_t>() : nullptr);
+        CORRO_HIP_TRY(hipGetLastError());
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        ctx->dense_epoch = ctx->state_epoch;
+    }
+    uint8_t *p = ctx->d_dense_view.as<uint8_t>();
+    v.st = ctx->d_dense.as<Rec>();
+    v.ts = ctx->track_ts ? ctx->d_dense_ts.as<uint64_t>() : nullptr;
+    v.off = (const uint64_t *)p;
+    v.cnt = (const uint32_t *)(p + nb * 8ULL);
+    v.nb = nb;
+    return CORRO_OK;
+}
+
 // crsql_set_db_version(site, v) for an empty complete changeset (util.rs:1040-1050)
 int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version) {
     if (site >= ctx->sites.size()) return fail(CORRO_E_INVALID, "unregistered site ordinal");
@@ -761,13 +971,7 @@ int corro_state_count(corro_ctx *ctx, uint64_t *count) {
 int corro_state_reset(corro_ctx *ctx) {
     if (!ctx) return fail(CORRO_E_INVALID, "NULL argument");
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_state_cnt.p, 0, ctx->B * 4ULL, ctx->stream));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_state_off.p, 0, ctx->B * 8ULL, ctx->stream));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_state_flags.p, 0, ctx->B * 4ULL, ctx->stream));
-    CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
-    ctx->state_total = 0;
-    ctx->state_epoch++;
-    return CORRO_OK;
+    return store_clear(ctx);
 }
 
 int corro_state_export(corro_ctx *ctx, corro_rows *o, uint64_t cap, uint64_t *written) {
@@ -778,19 +982,9 @@ int corro_state_export(corro_ctx *ctx, corro_rows *o, uint64_t cap, uint64_t *wr
     if (m == 0) return CORRO_OK;
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    const uint32_t B = ctx->B;
-    std::vector<uint32_t> cnt(B);
-    CORRO_HIP_TRY(hipMemcpy(cnt.data(), ctx->d_state_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
-    std::vector<uint64_t> dense(B);
-    uint64_t run = 0;
-    for (uint32_t b = 0; b < B; b++) {
-        dense[b] = run;
-        run += cnt[b];
-    }
-    if (run != m) return fail(CORRO_E_DEVICE, "internal: state count mismatch");
-    // device SoA: 8*6 + 4*3 + 1*2 bytes per row
+    // device SoA: 8*7 + 4*3 + 1*2 bytes per row
     const size_t per = 8 * 7 + 4 * 3 + 2;
-    TRY(ctx->d_export.ensure(m * per + B * 8 + 4096));
+    TRY(ctx->d_export.ensure(m * per + 13 * 256 + 256));
     uint8_t *p = ctx->d_export.as<uint8_t>();
     corro_rows d{};
     auto carve = [&](size_t elem) {
@@ -810,12 +1004,16 @@ int corro_state_export(corro_ctx *ctx, corro_rows *o, uint64_t cap, uint64_t *wr
     d.site = (uint32_t *)carve(4);
     d.val_type = (uint8_t *)carve(1);
     d.val_len = (uint8_t *)carve(1);
-    uint64_t *d_dense = (uint64_t *)p;
-    CORRO_HIP_TRY(hipMemcpyAsync(d_dense, dense.data(), B * 8ULL, hipMemcpyHostToDevice, s));
-    const uint64_t *sts = ctx->track_ts ? ctx->d_state_ts[ctx->cur].as<uint64_t>() : nullptr;
-    hipLaunchKernelGGL(k_export, dim3(B), dim3(256), 0, s, ctx->d_state[ctx->cur].as<Rec>(), sts,
-                       ctx->d_state_off.as<uint64_t>(), ctx->d_state_cnt.as<uint32_t>(), d_dense, d);
+    unsigned long long *cnt = (unsigned long long *)p;
+    CORRO_HIP_TRY(hipMemsetAsync(cnt, 0, 8, s));
+    const uint64_t nent = (uint64_t)ctx->B << ctx->log2S;
+    hipLaunchKernelGGL(k_export, dim3((uint32_t)std::min<uint64_t>((nent + 255) / 256, 8192)), dim3(256), 0, s,
+                       row_store(ctx), nent, cnt, d);
     CORRO_HIP_TRY(hipGetLastError());
+    unsigned long long got = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&got, cnt, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (got != m) return fail(CORRO_E_DEVICE, "internal: state count mismatch");
     struct C { void *dst; const void *src; size_t elem; } cp[] = {
         {o->pk, d.pk, 8},         {o->col_version, d.col_version, 8}, {o->db_version, d.db_version, 8},
         {o->cl, d.cl, 8},         {o->ts, d.ts, 8},                   {o->val0, d.val0, 8},

@@ -33,6 +33,7 @@ int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t 
                    uint32_t *vo, uint32_t n, uint32_t end_bit, hipStream_t s);
 int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, uint32_t *out, uint32_t n,
                             hipStream_t s);
+int state_dense_view(corro_ctx *ctx, DenseView &v);
 
 namespace {
 
@@ -336,12 +337,15 @@ int ensure_index(corro_ctx *ctx, XIndex &x, XParams &p) {
     hipStream_t s = ctx->stream;
     const uint64_t m = ctx->state_total;
     if (m >= (1ULL << 32)) return fail(CORRO_E_RANGE, "extraction index holds at most 2^32-1 clock rows");
-    const uint32_t B = ctx->B;
     if (ctx->xidx_epoch != ctx->state_epoch) {
         if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[2], s));
-        const Rec *st = ctx->d_state[ctx->cur].as<Rec>();
-        const uint64_t *off = ctx->d_state_off.as<uint64_t>();
-        const uint32_t *cnt = ctx->d_state_cnt.as<uint32_t>();
+        // the row store's clock records, materialised densely in pseudo-buckets
+        DenseView dv{};
+        if (int rc = state_dense_view(ctx, dv)) return rc;
+        const uint32_t B = dv.nb;
+        const Rec *st = dv.st;
+        const uint64_t *off = dv.off;
+        const uint32_t *cnt = dv.cnt;
         // scratch: keys in/out, refs in, dense offsets, max words; rocPRIM temp after
         size_t sort_tmp = 0, scan_tmp = 0;
         if (m) {
@@ -416,7 +420,7 @@ int ensure_index(corro_ctx *ctx, XIndex &x, XParams &p) {
             CORRO_HIP_TRY(hipMemcpyAsync(&G, X.gid + (m - 1), 4, hipMemcpyDeviceToHost, s));
             CORRO_HIP_TRY(hipStreamSynchronize(s));
             G += 1;
-            const uint64_t *sts = ctx->track_ts ? ctx->d_state_ts[ctx->cur].as<uint64_t>() : nullptr;
+            const uint64_t *sts = dv.ts;
             hipLaunchKernelGGL(k_xgmeta, dim3((G + 255) / 256), dim3(256), 0, s, X, sts, G);
             hipLaunchKernelGGL(k_xcluster, dim3(mb), dim3(256), 0, s, st, sts, X.ref, m, ctx->x.crec,
                                sts ? ctx->x.cts : nullptr);

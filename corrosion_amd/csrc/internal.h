@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "corro_hip.h"
@@ -61,10 +62,29 @@ struct XIdxPtrs {
     uint64_t *cts = nullptr;     // their ts (when the state tracks ts)
 };
 
+// The state as dense clock records in pseudo-buckets (engine.hip state_dense_view).
+struct DenseView {
+    const Rec *st;
+    const uint64_t *ts;
+    const uint64_t *off;
+    const uint32_t *cnt;
+    uint32_t nb;
+};
+
 struct Table {
     std::string name;
     std::vector<std::string> cols;
 };
+
+// Row keys of one table's primary keys (pkeys.cpp): interned tables key rows by a dense id of the
+// canonical packed pk (cr-sqlite's __crsql_key / <t>__crsql_pks), others by the INTEGER pk itself.
+struct PkTable {
+    bool interned = false;
+    std::unordered_map<std::string, uint64_t> ids;
+    std::vector<std::string> keys;
+};
+bool pk_canonical(const uint8_t *p, uint64_t len, std::string &out, bool *single_int, int64_t *ival);
+std::string pack_int_pk(int64_t v);
 
 }  // namespace corro
 
@@ -72,6 +92,7 @@ struct corro_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::vector<corro::Table> tables;
+    std::vector<corro::PkTable> pk;  // per table
     std::map<std::string, uint32_t> table_index;
 
     // sites (crsql_site_id analogue): ordinal -> 16 bytes; rank = memcmp order
@@ -85,21 +106,28 @@ struct corro_ctx {
     // bucket layout
     uint32_t log2B = 0;
     uint32_t B = 0;
-    // state (clock rows), double buffered; per-bucket slices
-    corro::DevBuf d_state[2], d_state_ts[2];
-    corro::DevBuf d_state_off, d_state_cnt, d_state_flags;     // current
-    corro::DevBuf d_out_off, d_out_cnt, d_out_flags;           // next
-    int cur = 0;
-    uint64_t state_total = 0;     // clock rows in the current state
+    // state: the row store (rowstore.h), updated in place by every apply
+    corro::DevBuf d_ent;          // RowEnt[B << log2S]
+    corro::DevBuf d_used, d_gen;  // u32[B]: region fill, region holds a sentinel row
+    corro::DevBuf d_heap, d_heap_ts;
+    corro::DevBuf d_heap_top;     // u64 records handed out
+    corro::DevBuf d_stride;       // u16 per table: ncols + 1
+    uint32_t log2S = 0;
+    uint64_t heap_cap = 0;        // records
+    uint32_t max_stride = 1;
+    uint64_t state_total = 0;     // clock records in the state
     bool track_ts = false;
     bool state_wide = false;      // some clock row holds a non-INTEGER value
+    corro::DevBuf d_defer, d_relist;  // deferred buckets of a merge round, the re-merge list
+    corro::DevBuf d_dense, d_dense_ts, d_dense_view;  // materialised state (extraction), its pseudo-buckets
+    uint64_t dense_epoch = ~0ULL;
 
     // per-batch scratch
     corro::DevBuf d_in;           // staged device copy of a host batch
     corro::DevBuf d_hist;         // ntiles x B
     corro::DevBuf d_new_cnt, d_stage_off, d_bflags;
     corro::DevBuf d_stage;        // staged Recs
-    corro::DevBuf d_misc;         // counters: [0] error bits, [1] overflow count, [2] out total, [3] wide flag, [4] general queue, [5] wide queue
+    corro::DevBuf d_misc;         // counters (merge_kernels.h MISC_*)
     corro::DevBuf d_ovf_list;     // overflow buckets
     corro::DevBuf d_gen_list;     // buckets queued for the general body
     corro::DevBuf d_wide_list;    // buckets queued for the mixed-type fast body
@@ -127,7 +155,7 @@ struct corro_ctx {
     uint32_t wire_hmask = 0;
     corro::DevBuf d_ncols;        // u16 column count per table
     corro::DevBuf d_part;         // partition counts
-    uint64_t *h_misc = nullptr;   // pinned
+    uint64_t *h_misc = nullptr;   // pinned, 16 words
     // stage timing
     bool profiling = false;
     hipEvent_t ev[8] = {};

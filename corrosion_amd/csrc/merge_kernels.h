@@ -23,6 +23,7 @@
 #pragma once
 #include "internal.h"
 #include "rowhash.h"
+#include "rowstore.h"
 
 namespace corro {
 
@@ -37,33 +38,31 @@ constexpr int GEN_SLOTS = 4096;
 constexpr uint32_t LONG_ROW = 128;                     // rows this long leave the LDS body
 
 struct MergeArgs {
-    const Rec *prior;
-    const uint64_t *prior_off;
-    const uint32_t *prior_cnt;
-    const uint32_t *prior_flags;
-    const uint64_t *prior_ts;
     const Rec *stage;
     const uint32_t *stage_off;
     const uint32_t *new_cnt;
     const uint32_t *bflags;   // bit per bucket: batch has a non-(cl=1 column) change there
     const uint64_t *batch_ts;
-    Rec *out;
-    uint64_t *out_ts;
-    const uint64_t *out_off;
-    uint32_t *out_cnt;
-    uint32_t *out_flags;
+    RowStore rs;              // the state (rowstore.h), updated in place
     const uint32_t *site_rank;
     uint32_t nsites;
     uint8_t *impact;
-    unsigned long long *misc;  // [0] error bits [1] overflow buckets [2] rows written [3] wide values
-                               // [4] general buckets [5] wide fast buckets [6] small, [7] mid general buckets
+    unsigned long long *misc;  // see MISC_* below
     uint32_t *ovf_list;
     uint32_t *gen_list;        // [B] buckets for k_merge_gen, then k_merge_gen_small, k_merge_gen_mid
     uint32_t *wide_list;       // buckets for k_merge_fast_wide
+    uint32_t *defer_list;      // buckets that could not take their new rows (re-merged after growth)
+    const uint32_t *bucket_list;  // a re-merge: workgroup k takes bucket bucket_list[k] (null: k itself)
+    uint32_t B;
     uint32_t force_general;    // route every non-empty bucket through the sequential general body
     uint32_t track_ts;
-    uint32_t state_wide;       // prior state holds non-INTEGER values
+    uint32_t state_wide;       // the state holds non-INTEGER values
 };
+
+// misc words
+constexpr int MISC_ERR = 0, MISC_OVF = 1, MISC_LIVE = 2, MISC_WIDE = 3, MISC_GEN = 4, MISC_WIDEQ = 5,
+              MISC_GEN_SMALL = 6, MISC_GEN_MID = 7, MISC_DEFER = 8, MISC_DEFER_WHY = 9, MISC_WORDS = 16;
+constexpr unsigned long long DEFER_REGION = 1, DEFER_HEAP = 2;
 
 // misc[0] error bits
 constexpr uint32_t ERR_NAME = 1u, ERR_SITE = 2u, ERR_RANGE = 4u, ERR_VALUE = 8u;
@@ -189,89 +188,57 @@ static __global__ void k_colscan(uint32_t *__restrict__ hist, uint32_t ntiles, u
     new_cnt[b] = run;
 }
 
-// one 1024-thread workgroup: stage_off = excl-scan(new_cnt); out_off = excl-scan(prior + 2*new).
-// Every lane sums its run of `per` consecutive buckets with all loads issued at once (one memory
-// latency for the whole scan), the lane sums are scanned by wave shuffles + one LDS round, and the
-// lane re-reads its run (L2-resident now) to write the offsets.
+// one 1024-thread workgroup: stage_off = excl-scan(new_cnt). Every lane sums its run of `per`
+// consecutive buckets with all loads issued at once (one memory latency for the whole scan), the
+// lane sums are scanned by wave shuffles + one LDS round, and the lane re-reads its run (L2-resident
+// now) to write the offsets.
 constexpr uint32_t PLAN_PER = 32;  // B <= 1024 * PLAN_PER = 2^15 (B is a power of two)
 static __global__ void __launch_bounds__(1024)
-k_plan(const uint32_t *__restrict__ new_cnt, const uint32_t *__restrict__ prior_cnt, uint32_t B,
-       uint32_t *__restrict__ stage_off, uint64_t *__restrict__ out_off) {
-    __shared__ uint64_t w_a[16], w_b[16];
+k_plan(const uint32_t *__restrict__ new_cnt, uint32_t B, uint32_t *__restrict__ stage_off) {
+    __shared__ uint64_t w_a[16];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // B is a power of two: runs of per = B / 1024 buckets (16-B aligned when per >= 4)
     const uint32_t per = B >= 1024 ? B / 1024 : 1u;  // <= PLAN_PER
     const uint32_t b0 = threadIdx.x * per;
     const uint32_t cnt = b0 < B ? per : 0u;
-    uint64_t sa = 0, sb = 0;
+    uint64_t sa = 0;
     if (per >= 4) {
-        uint4 x[PLAN_PER / 4], y[PLAN_PER / 4];
+        uint4 x[PLAN_PER / 4];
 #pragma unroll
-        for (uint32_t k = 0; k < PLAN_PER / 4; k++) {
-            const uint32_t kk = min(k, per / 4 - 1);
-            x[k] = reinterpret_cast<const uint4 *>(new_cnt + b0)[kk];
-            y[k] = reinterpret_cast<const uint4 *>(prior_cnt + b0)[kk];
-        }
+        for (uint32_t k = 0; k < PLAN_PER / 4; k++) x[k] = reinterpret_cast<const uint4 *>(new_cnt + b0)[min(k, per / 4 - 1)];
 #pragma unroll
         for (uint32_t k = 0; k < PLAN_PER / 4; k++)
-            if (4 * k < per) {
-                sa += (uint64_t)x[k].x + x[k].y + x[k].z + x[k].w;
-                sb += (uint64_t)y[k].x + y[k].y + y[k].z + y[k].w;
-            }
-        sb += 2 * sa;
+            if (4 * k < per) sa += (uint64_t)x[k].x + x[k].y + x[k].z + x[k].w;
     } else {
-        for (uint32_t k = 0; k < cnt; k++) {
-            sa += new_cnt[b0 + k];
-            sb += (uint64_t)prior_cnt[b0 + k] + 2ULL * new_cnt[b0 + k];
-        }
+        for (uint32_t k = 0; k < cnt; k++) sa += new_cnt[b0 + k];
     }
-    uint64_t ia = sa, ib = sb;  // inclusive wave scan
+    uint64_t ia = sa;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t xa = __shfl_up(ia, d), xb = __shfl_up(ib, d);
-        if (lane >= (uint32_t)d) {
-            ia += xa;
-            ib += xb;
-        }
+        const uint64_t xa = __shfl_up(ia, d);
+        if (lane >= (uint32_t)d) ia += xa;
     }
-    if (lane == 63) {
-        w_a[w] = ia;
-        w_b[w] = ib;
-    }
+    if (lane == 63) w_a[w] = ia;
     __syncthreads();
-    uint64_t ra = ia - sa, rb = ib - sb;
-    for (uint32_t ww = 0; ww < w; ww++) {
-        ra += w_a[ww];
-        rb += w_b[ww];
-    }
+    uint64_t ra = ia - sa;
+    for (uint32_t ww = 0; ww < w; ww++) ra += w_a[ww];
     if (per >= 4) {
 #pragma unroll
         for (uint32_t k = 0; k < PLAN_PER / 4; k++) {
             if (4 * k >= per) break;
-            // re-read the run (L2-resident): holding it across the scan would spill
             const uint4 xk = reinterpret_cast<const uint4 *>(new_cnt + b0)[k];
-            const uint4 yk = reinterpret_cast<const uint4 *>(prior_cnt + b0)[k];
-            const uint32_t xs[4] = {xk.x, xk.y, xk.z, xk.w}, ys[4] = {yk.x, yk.y, yk.z, yk.w};
+            const uint32_t xs[4] = {xk.x, xk.y, xk.z, xk.w};
             uint32_t so[4];
-            uint64_t oo[4];
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 so[e] = (uint32_t)ra;
-                oo[e] = rb;
                 ra += xs[e];
-                rb += (uint64_t)ys[e] + 2ULL * xs[e];
             }
             reinterpret_cast<uint4 *>(stage_off + b0)[k] = make_uint4(so[0], so[1], so[2], so[3]);
-            reinterpret_cast<ulonglong2 *>(out_off + b0)[2 * k] = make_ulonglong2(oo[0], oo[1]);
-            reinterpret_cast<ulonglong2 *>(out_off + b0)[2 * k + 1] = make_ulonglong2(oo[2], oo[3]);
         }
     } else {
         for (uint32_t k = 0; k < cnt; k++) {
-            const uint32_t xn = new_cnt[b0 + k], yp = prior_cnt[b0 + k];
             stage_off[b0 + k] = (uint32_t)ra;
-            out_off[b0 + k] = rb;
-            ra += xn;
-            rb += (uint64_t)yp + 2ULL * xn;
+            ra += new_cnt[b0 + k];
         }
     }
 }
@@ -476,7 +443,8 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                 const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
                 const uint32_t b = bucket_of(one_table ? 0u : t, r.pk, log2B);
                 idx = atomicAdd(&cur[b], 1u);
-                if (r.cl != 1u || cid == 0) atomicOr(&fl[b >> 5], 1u << (b & 31));
+                // (the fast bodies keep a row's presence bits in one word: cids 1..63)
+                if (r.cl != 1u || cid == 0 || cid >= 64) atomicOr(&fl[b >> 5], 1u << (b & 31));
                 if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
                 if (r.site >= nsites) err |= ERR_SITE;
                 if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
@@ -518,51 +486,30 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
 }
 
 // ------------------------------------------------------------------------ merge bodies
+// A bucket's records: its staged batch changes [0, nn) and, in the general body, the prior clock
+// records of the rows they touch [nn, nn + np) (heap records, named by hix[x - nn]).
 struct BucketView {
-    const Rec *prior;   // already offset to the bucket
-    const Rec *fresh;   // staged batch records of the bucket
-    uint32_t np, nn;
-    const uint64_t *prior_ts;  // offset to the bucket (or null)
-    __device__ inline const Rec *at(uint32_t i) const { return i < np ? prior + i : fresh + (i - np); }
+    const Rec *fresh;
+    uint32_t nn, np;
+    const Rec *heap;
+    const uint32_t *hix;
+    const uint64_t *heap_ts;
+    __device__ inline const Rec *at(uint32_t i) const { return i < nn ? fresh + i : heap + hix[i - nn]; }
+    __device__ inline uint64_t prior_ts(const Rec &r) const { return heap_ts ? heap_ts[r.pos] : 0ULL; }
 };
 
-// Wave-cooperative load of the 64 records [wave_base, wave_base + 64) of a bucket (lane L gets
-// record wave_base + L; records >= n read as zero). Load instruction k reads the 1 KB of records
-// wave_base + 16k .. +15 with one 16-B quad per lane (fully coalesced); the same 4x4 lane
-// transpose as store_rec_wave (an involution) then gives every lane its own record.
-__device__ inline Rec load_rec_wave(const BucketView &v, uint32_t wave_base, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t j = lane >> 4, l = lane & 15;
-    uint4 q[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t ri = wave_base + l + 16 * k;
-        q[k] = ri < n ? reinterpret_cast<const uint4 *>(v.at(ri))[j] : make_uint4(0, 0, 0, 0);
-    }
-    swap32(q[0].x, q[2].x); swap32(q[0].y, q[2].y); swap32(q[0].z, q[2].z); swap32(q[0].w, q[2].w);
-    swap32(q[1].x, q[3].x); swap32(q[1].y, q[3].y); swap32(q[1].z, q[3].z); swap32(q[1].w, q[3].w);
-    swap16(q[0].x, q[1].x); swap16(q[0].y, q[1].y); swap16(q[0].z, q[1].z); swap16(q[0].w, q[1].w);
-    swap16(q[2].x, q[3].x); swap16(q[2].y, q[3].y); swap16(q[2].z, q[3].z); swap16(q[2].w, q[3].w);
-    Rec r;
-    uint4 *d = reinterpret_cast<uint4 *>(&r);
-    d[0] = q[0];
-    d[1] = q[1];
-    d[2] = q[2];
-    d[3] = q[3];
-    return r;
-}
-
-// Issue-only half of load_rec_wave: the four coalesced 16-B loads of lane L for records
-// [wave_base, wave_base + 64), with the record index clamped to n - 1 (no branch, so a caller can
-// issue the loads of several groups before the first wait). rec_from_wave_quads finishes the job.
-__device__ inline void load_rec_wave_raw(const BucketView &v, uint32_t wave_base, uint32_t n, uint4 q[4]) {
+// Issue-only half of a wave-cooperative record load: the four coalesced 16-B loads of lane L for
+// staged records [wave_base, wave_base + 64), the record index clamped to n - 1 (no branch, so a
+// caller can issue the loads of several groups before the first wait). Load instruction k reads
+// the 1 KB of records wave_base + 16k .. +15 with one 16-B quad per lane; rec_from_wave_quads (the
+// 4x4 lane transpose of store_rec_wave, an involution) gives every lane its own record.
+__device__ inline void load_rec_wave_raw(const Rec *fresh, uint32_t wave_base, uint32_t n, uint4 q[4]) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = lane >> 4, l = lane & 15;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint32_t ri = min(wave_base + l + 16 * k, n - 1);
-        const Rec *p = ri < v.np ? v.prior + ri : v.fresh + (ri - v.np);
-        q[k] = reinterpret_cast<const uint4 *>(p)[j];
+        q[k] = reinterpret_cast<const uint4 *>(fresh + ri)[j];
     }
 }
 
@@ -580,13 +527,25 @@ __device__ inline Rec rec_from_wave_quads(uint4 q[4]) {
     return r;
 }
 
-__device__ inline uint64_t rec_ts(const MergeArgs &a, const BucketView &v, const Rec &r) {
+template <class V>
+__device__ inline uint64_t rec_ts(const MergeArgs &a, const V &v, const Rec &r) {
     if (r.pos & BATCH_POS) return a.batch_ts ? a.batch_ts[r.pos & 0x7FFFFFFFu] : 0ULL;
-    return v.prior_ts ? v.prior_ts[r.pos] : 0ULL;
+    return v.prior_ts(r);
 }
 
-// Arrays used by the general (sequential-rule) body. They point into LDS (k_merge) or into a
-// global scratch slice (overflow path); the code is the same.
+__device__ inline void push_overflow(const MergeArgs &a, uint32_t b) {
+    const unsigned long long k = atomicAdd(&a.misc[MISC_OVF], 1ULL);
+    a.ovf_list[k] = b;
+}
+
+__device__ inline void push_defer(const MergeArgs &a, uint32_t b, unsigned long long why) {
+    const unsigned long long k = atomicAdd(&a.misc[MISC_DEFER], 1ULL);
+    a.defer_list[k] = b;
+    atomicOr(&a.misc[MISC_DEFER_WHY], why);
+}
+
+// Arrays used by the general (sequential-rule) body. They point into LDS (gen_bucket) or into a
+// global scratch (overflow path); the code is the same.
 struct GenArrays {
     uint64_t *pk;
     int64_t *cv;
@@ -594,25 +553,29 @@ struct GenArrays {
     uint32_t *cl;
     uint32_t *pos;
     uint32_t *own;   // row hash slots: owner record + 1
-    uint64_t *key;   // sort keys: row << 32 | pos
+    uint64_t *key;   // sort keys: row << rshift | position
     uint32_t *val;   // sort payload: record index
     uint32_t *ccid;  // per-run cell scratch
     uint32_t *csrc;
     int64_t *ccv;
+    uint32_t *rheap; // LDS body, per row owner: heap index of the row's slot 0
+    uint32_t *rent;  // LDS body, per row owner: region entry (ROW_NONE: a new row)
+    uint32_t *hix;   // LDS body: heap index of prior record x (x >= nn)
     uint32_t slots;  // pow2
     uint32_t P;      // records
     uint32_t rshift; // row = key >> rshift (32 in LDS; the overflow path's compact keys use fewer)
 };
 
-__device__ inline void gen_emit(const MergeArgs &a, const BucketView &v, Rec *outb, uint64_t *outts,
-                                uint32_t *outcnt, uint32_t *flag, const GenArrays &g, uint32_t s,
-                                uint32_t ncell, bool hs, int64_t scv, uint32_t ssrc) {
+// Write a folded row into its heap slots: the sentinel clock (slot 0) and the cells (slot cid),
+// every one with the row's causal length; `bits` receives the presence bits. Each written slot's
+// source is the batch change that set it or the slot's own prior record, loaded before the store.
+template <class V>
+__device__ inline uint32_t heap_write_row(const MergeArgs &a, const V &v, const GenArrays &g, uint32_t s,
+                                          uint32_t ncell, bool hs, int64_t scv, uint32_t ssrc, uint32_t hb,
+                                          uint64_t bits[2]) {
     const int64_t L = hs ? scv : (ncell ? 1 : 0);
-    const uint32_t cnt = (hs ? 1u : 0u) + ncell;
-    if (cnt == 0) return;
-    uint32_t base = atomicAdd(outcnt, cnt);
-    if (hs || L != 1) atomicOr(flag, 1u);
-    uint32_t k = base;
+    bits[0] = bits[1] = 0;
+    uint32_t cnt = 0;
     if (hs) {
         Rec r = load_rec(v.at(ssrc));
         const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
@@ -622,10 +585,11 @@ __device__ inline void gen_emit(const MergeArgs &a, const BucketView &v, Rec *ou
         r.v0 = 0;
         r.v1 = 0;
         r.meta = CORRO_NULL;
-        r.pos = k;
-        store_rec(outb + k, r);
-        if (a.track_ts) outts[k] = ts;
-        k++;
+        r.pos = hb;
+        store_rec(a.rs.heap + hb, r);
+        if (a.track_ts) a.rs.heap_ts[hb] = ts;
+        bits[0] |= 1ULL;
+        cnt++;
     }
     // four cells at a time, their loads issued together (clamped, so no branch splits them)
     constexpr uint32_t EU = 4;
@@ -637,14 +601,17 @@ __device__ inline void gen_emit(const MergeArgs &a, const BucketView &v, Rec *ou
         for (uint32_t u = 0; u < EU; u++) {
             if (c0 + u >= ncell) break;
             const uint64_t ts = a.track_ts ? rec_ts(a, v, r[u]) : 0ULL;
+            const uint32_t cid = r[u].tcid & 0xFFFFu;
             r[u].cv = g.ccv[s + c0 + u];
             r[u].cl = (uint32_t)L;
-            r[u].pos = k;
-            store_rec(outb + k, r[u]);
-            if (a.track_ts) outts[k] = ts;
-            k++;
+            r[u].pos = hb + cid;
+            store_rec(a.rs.heap + hb + cid, r[u]);
+            if (a.track_ts) a.rs.heap_ts[hb + cid] = ts;
+            bits[cid >> 6] |= 1ULL << (cid & 63);
+            cnt++;
         }
     }
+    return cnt;
 }
 
 __device__ inline void gen_set_cell(const GenArrays &g, uint32_t s, uint32_t &ncell, uint32_t cid,
@@ -662,10 +629,11 @@ __device__ inline void gen_set_cell(const GenArrays &g, uint32_t s, uint32_t &nc
     ncell++;
 }
 
-// Fold one row's records (sorted positions [s, e)) through the cr-sqlite rules, then emit.
-__device__ inline void gen_fold_row(const MergeArgs &a, const BucketView &v, Rec *outb,
-                                    uint64_t *outts, uint32_t *outcnt, uint32_t *flag,
-                                    const GenArrays &g, uint32_t s, uint32_t n) {
+// Fold one row's records (sorted positions [s, e)) through the cr-sqlite rules,
+// then hand the result to the emitter.
+template <class V, class E>
+__device__ inline void gen_fold_row(const MergeArgs &a, const V &v, E &em, const GenArrays &g, uint32_t s,
+                                    uint32_t n) {
     const uint32_t row = (uint32_t)(g.key[s] >> g.rshift);
     uint32_t ncell = 0;
     bool hs = false;
@@ -747,28 +715,15 @@ __device__ inline void gen_fold_row(const MergeArgs &a, const BucketView &v, Rec
         }
         if (a.impact && (pos & BATCH_POS)) a.impact[pos & 0x7FFFFFFFu] = (uint8_t)imp;
     }
-    gen_emit(a, v, outb, outts, outcnt, flag, g, s, ncell, hs, scv, ssrc);
+    em.emit(a, v, g, s, row, ncell, hs, scv, ssrc);
 }
 
-// The general body for one bucket, executed by the whole workgroup (nth threads).
-// Load the bucket's fields, group its records by row and sort them by (row, position): after
-// this, g.key[j] = row << 32 | pos and g.val[j] = record index for sorted positions j < n.
-__device__ inline void gen_rowkeys(const BucketView &v, const GenArrays &g, bool fields_loaded) {
-    const uint32_t n = v.np + v.nn;
+// Group the records [0, n) by row with an LDS open-addressing table (owner = first claimer):
+// afterwards g.key[i] = owner << 32 | pos and g.val[i] = i.
+__device__ inline void gen_rowkeys(const GenArrays &g, uint32_t n) {
     const uint32_t tid = threadIdx.x, nth = blockDim.x;
-    if (!fields_loaded) {
-        for (uint32_t i = tid; i < n; i += nth) {
-            const Rec *r = v.at(i);
-            g.pk[i] = r->pk;
-            g.cv[i] = r->cv;
-            g.tc[i] = r->tcid;
-            g.cl[i] = r->cl;
-            g.pos[i] = r->pos;
-        }
-    }
     for (uint32_t i = tid; i < g.slots; i += nth) g.own[i] = 0;
     __syncthreads();
-    // group records by row (table, pk): open addressing, owner = first claimer
     const uint32_t mask = g.slots - 1;
     for (uint32_t i = tid; i < n; i += nth) {
         const uint64_t pk = g.pk[i];
@@ -795,37 +750,14 @@ __device__ inline void gen_rowkeys(const BucketView &v, const GenArrays &g, bool
     }
 }
 
-// Group the bucket's records by row, each row's records in application order: afterwards
-// g.key[j] = row << 32 | pos and g.val[j] = record index for j < n, a row's records contiguous.
-// A counting sort by row owner (LDS histogram, block scan, scatter through g.own), then every
-// record moves to its rank by position within its row: a handful of barriers instead of a
-// bitonic network's 66. Returns (in *s_long) whether some row is longer than LONG_ROW; g.ccid /
-// g.csrc are free again afterwards (the fold's cell scratch). C = ceil(n / blockDim.x) <= GEN_C.
-// The general body comes in two sizes: CAP_GEN records (one 131 KB workgroup per CU) and
-// CAP_GEN_SMALL (32 KB, 256 threads, four per CU) and CAP_GEN_MID (64 KB, 256 threads, two per CU)
-// for the many small general buckets, so that their barrier- and latency-bound phases overlap
-// across workgroups.
-constexpr uint32_t CAP_GEN_SMALL = 512, CAP_GEN_MID = 1024;
-
-constexpr uint32_t GEN_SMALL_THREADS = 256;
-
-template <uint32_t CAP, uint32_t THREADS = MERGE_THREADS>
-struct GenCfg {
-    static constexpr uint32_t C = (CAP + THREADS - 1) / THREADS;  // records per thread
-    static constexpr uint32_t SLOTS = 2 * CAP;                                // row table (pow2 >= CAP)
-    static constexpr size_t LDS = (size_t)CAP * (8 + 8 + 4 + 4 + 4) + (size_t)SLOTS * 4 + (size_t)CAP * (8 + 4) +
-                                  (size_t)CAP * (4 + 4 + 8);
-};
-
+// Counting sort of the records [0, n) by row owner (counts already in g.ccid[owner], zero for
+// non-owners), then every record moves to its rank by position within its row: a handful of
+// barriers instead of a bitonic network. Afterwards g.key[j] / g.val[j] for sorted j, a row's
+// records contiguous in application order; g.ccid / g.csrc are free again (the fold's cell
+// scratch). C = ceil(n / blockDim.x) <= GEN_C.
 template <uint32_t GEN_C>
-__device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32_t *s_wsum, uint32_t *s_long) {
-    const uint32_t n = v.np + v.nn;
+__device__ inline void gen_sort_rows(const GenArrays &g, uint32_t n, uint32_t *s_wsum) {
     const uint32_t tid = threadIdx.x, nth = blockDim.x;
-    for (uint32_t i = tid; i < n; i += nth) g.ccid[i] = 0;
-    gen_rowkeys(v, g, false);  // (its barrier orders the zeroing above)
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += nth) atomicAdd(&g.ccid[(uint32_t)(g.key[i] >> 32)], 1u);
-    __syncthreads();
     // exclusive scan of the counts over owner index: GEN_C consecutive per thread
     {
         const uint32_t i0 = tid * GEN_C;
@@ -854,16 +786,14 @@ __device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32
             }
     }
     __syncthreads();
-    // scatter record indices by row (g.own: the row table is dead; GEN_SLOTS >= CAP_GEN)
+    // scatter record indices by row (g.own: the row table is dead; SLOTS >= CAP)
     for (uint32_t i = tid; i < n; i += nth) g.own[atomicAdd(&g.csrc[(uint32_t)(g.key[i] >> 32)], 1u)] = i;
     __syncthreads();
     uint64_t kk[GEN_C];
 #pragma unroll
     for (uint32_t k = 0; k < GEN_C; k++) {
         const uint32_t j = k * nth + tid;
-        if (j < n) {
-            kk[k] = g.key[g.own[j]];
-        }
+        if (j < n) kk[k] = g.key[g.own[j]];
     }
     __syncthreads();
 #pragma unroll
@@ -876,9 +806,8 @@ __device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32
     }
     __syncthreads();
     // each row's records by position: a record's rank in its row is the number of the row's
-    // records with a smaller key (positions are distinct), counted by every lane at once -- no
-    // dependent chain, a row of c records costs its lanes c LDS reads each (csrc[r] is now the
-    // row's end, ccid[r] its length)
+    // records with a smaller key (positions are distinct), counted by every lane at once (csrc[r]
+    // is now the row's end, ccid[r] its length)
     uint32_t dst[GEN_C], vv[GEN_C];
 #pragma unroll
     for (uint32_t k = 0; k < GEN_C; k++) {
@@ -887,10 +816,6 @@ __device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32
         if (j < n) {
             const uint64_t key = g.key[j];
             const uint32_t r = (uint32_t)(key >> 32), c = g.ccid[r];
-            if (c > LONG_ROW) {  // the bucket goes to the overflow path
-                *s_long = 1;
-                continue;
-            }
             const uint32_t s = g.csrc[r] - c;
             uint32_t rank = 0;
             for (uint32_t t = s; t < s + c; t++) rank += g.key[t] < key ? 1u : 0u;
@@ -909,42 +834,309 @@ __device__ inline void gen_group(const BucketView &v, const GenArrays &g, uint32
     __syncthreads();
 }
 
-static_assert(GenCfg<CAP_GEN>::SLOTS == GEN_SLOTS, "row table of the large general body");
+// The general body comes in three sizes: CAP_GEN records (one 155 KB workgroup per CU), CAP_GEN_MID
+// (78 KB, two per CU) and CAP_GEN_SMALL (39 KB, 256 threads, four per CU) for the many small general
+// buckets, so that their barrier- and latency-bound phases overlap across workgroups.
+constexpr uint32_t CAP_GEN_SMALL = 512, CAP_GEN_MID = 1024;
+constexpr uint32_t GEN_SMALL_THREADS = 256;
+
+template <uint32_t CAP, uint32_t THREADS = MERGE_THREADS>
+struct GenCfg {
+    static constexpr uint32_t C = (CAP + THREADS - 1) / THREADS;  // records per thread
+    static constexpr uint32_t SLOTS = 2 * CAP;                    // row table (pow2 >= CAP)
+    static constexpr size_t LDS = (size_t)CAP * (8 + 8 + 4 + 4 + 4) + (size_t)SLOTS * 4 + (size_t)CAP * (8 + 4) +
+                                  (size_t)CAP * (4 + 4 + 8) + (size_t)CAP * (4 + 4 + 4);
+};
+static_assert(GenCfg<CAP_GEN>::LDS + 256 <= 160 * 1024, "large general body must fit the CU's LDS");
+
+// Emission of the LDS general body: the row's heap slot (allocated before the fold for a new row),
+// its region entry inserted (new row) or its presence bits replaced.
+struct LdsEmit {
+    uint32_t b;
+    uint32_t *emitted, *general;
+    __device__ inline void emit(const MergeArgs &a, const BucketView &v, const GenArrays &g, uint32_t s, uint32_t row,
+                                uint32_t ncell, bool hs, int64_t scv, uint32_t ssrc) {
+        const uint32_t hb = g.rheap[row], e = g.rent[row];
+        if (e == ROW_NONE && !hs && ncell == 0) return;  // a new row the batch left empty (cl 0)
+        uint64_t bits[2];
+        const uint32_t cnt = heap_write_row(a, v, g, s, ncell, hs, scv, ssrc, hb, bits);
+        if (e == ROW_NONE) {
+            rs_insert(a.rs, b, g.pk[row], g.tc[row] >> 16, hb, bits);
+        } else {
+            a.rs.ent[e].bits[0] = bits[0];
+            a.rs.ent[e].bits[1] = bits[1];
+        }
+        atomicAdd(emitted, cnt);
+        if (hs) *general = 1;
+    }
+};
 
 __device__ inline void bucket_view(const MergeArgs &a, uint32_t b, BucketView &v) {
-    v.np = a.prior_cnt[b];
-    v.nn = a.new_cnt[b];
-    v.prior = a.prior + a.prior_off[b];
     v.fresh = a.stage + a.stage_off[b];
-    v.prior_ts = a.prior_ts ? a.prior_ts + a.prior_off[b] : nullptr;
+    v.nn = a.new_cnt[b];
+    v.np = 0;
+    v.heap = a.rs.heap;
+    v.hix = nullptr;
+    v.heap_ts = a.rs.heap_ts;
 }
 
-__device__ inline bool bucket_general(const MergeArgs &a, uint32_t b) {
-    return a.force_general || a.prior_flags[b] || ((a.bflags[b >> 5] >> (b & 31)) & 1u);
-}
-
-__device__ inline void push_overflow(const MergeArgs &a, uint32_t b) {
-    const unsigned long long k = atomicAdd(&a.misc[1], 1ULL);
-    a.ovf_list[k] = b;
+// General body in LDS for one queued bucket. Its rows' prior clock records are looked up in the
+// region and gathered into LDS as the prefix of each row, the records sorted by (row, position),
+// one lane per row folds the cr-sqlite rules, and each row is written back to its heap slot.
+// A bucket whose batch + prior records exceed CAP moves on to the next size (NEXT_Q: the queue of
+// the mid / large body, or the device-wide overflow path from the large one), as does one that
+// holds a row longer than LONG_ROW (straight to the overflow path). All of these decisions, and a
+// region or heap that cannot take the bucket's new rows (deferred), come before any write.
+template <uint32_t CAP, uint32_t THREADS, int NEXT_Q>
+__device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
+    using Cfg = GenCfg<CAP, THREADS>;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[Cfg::LDS];
+    __shared__ uint32_t s_np, s_nrow, s_nrec, s_fail, s_emit, s_gen, s_wsum[THREADS / 64];
+    __shared__ unsigned long long s_hbase;
+    const uint32_t tid = threadIdx.x;
+    BucketView v;
+    bucket_view(a, b, v);
+    const uint32_t nn = v.nn;
+    auto pass_on = [&](int q) {
+        if (q == 0) push_overflow(a, b);
+        else if (q == 1) a.gen_list[2 * a.B + atomicAdd(&a.misc[MISC_GEN_MID], 1ULL)] = b;
+        else a.gen_list[atomicAdd(&a.misc[MISC_GEN], 1ULL)] = b;
+    };
+    if (nn > CAP) {
+        if (tid == 0) pass_on(NEXT_Q);
+        return;
+    }
+    if (tid == 0) {
+        s_np = s_nrow = s_nrec = s_fail = s_emit = s_gen = 0;
+    }
+    GenArrays g;
+    uint8_t *p = smem;
+    g.pk = reinterpret_cast<uint64_t *>(p); p += CAP * 8;
+    g.cv = reinterpret_cast<int64_t *>(p); p += CAP * 8;
+    g.key = reinterpret_cast<uint64_t *>(p); p += CAP * 8;
+    g.ccv = reinterpret_cast<int64_t *>(p); p += CAP * 8;
+    g.tc = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.cl = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.pos = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.val = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.ccid = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.rheap = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.rent = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.hix = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
+    g.own = reinterpret_cast<uint32_t *>(p);
+    g.slots = Cfg::SLOTS;
+    g.rshift = 32;
+    v.hix = g.hix;
+    // 1. the batch records' fields; counts per row start at zero
+    for (uint32_t i = tid; i < nn; i += THREADS) {
+        const Rec *r = v.fresh + i;
+        g.pk[i] = r->pk;
+        g.cv[i] = r->cv;
+        g.tc[i] = r->tcid;
+        g.cl[i] = r->cl;
+        g.pos[i] = r->pos;
+    }
+    for (uint32_t i = tid; i < CAP; i += THREADS) g.ccid[i] = 0;
+    // 2. rows (its barrier orders the loads above)
+    gen_rowkeys(g, nn);
+    __syncthreads();
+    for (uint32_t i = tid; i < nn; i += THREADS) atomicAdd(&g.ccid[(uint32_t)(g.key[i] >> 32)], 1u);
+    __syncthreads();
+    // 3. each row owner looks its row up (read-only) and gathers its prior clock records
+    for (uint32_t i = tid; i < nn; i += THREADS) {
+        if ((uint32_t)(g.key[i] >> 32) != i) continue;
+        const uint32_t t = g.tc[i] >> 16;
+        const uint32_t e = rs_lookup(a.rs, b, g.pk[i], t);
+        g.rent[i] = e;
+        if (e == ROW_NONE) {
+            g.rheap[i] = atomicAdd(&s_nrec, (uint32_t)a.rs.stride[t]);  // offset until the allocation
+            atomicAdd(&s_nrow, 1u);
+            if (g.ccid[i] > LONG_ROW) s_fail = 3;
+            continue;
+        }
+        const RowEnt re = a.rs.ent[e];
+        g.rheap[i] = re.heap;
+        const uint32_t pc = row_popc(re.bits);
+        if (g.ccid[i] + pc > LONG_ROW) s_fail = 3;
+        const uint32_t off = atomicAdd(&s_np, pc);
+        if (nn + off + pc > CAP) continue;  // the bucket moves on (step 4)
+        g.ccid[i] += pc;
+        uint32_t k = nn + off;
+        for (int w = 0; w < 2; w++)
+            for (uint64_t m = re.bits[w]; m; m &= m - 1) {
+                const uint32_t c = 64 * w + (uint32_t)__ffsll((unsigned long long)m) - 1;
+                const Rec *pr = a.rs.heap + re.heap + c;
+                g.pk[k] = g.pk[i];
+                g.cv[k] = pr->cv;
+                g.tc[k] = pr->tcid;
+                g.cl[k] = pr->cl;
+                g.pos[k] = c;  // prior records sort first in their row (sentinel, then cells)
+                g.hix[k - nn] = re.heap + c;
+                g.key[k] = ((uint64_t)i << 32) | c;
+                g.val[k] = k;
+                k++;
+            }
+    }
+    __syncthreads();
+    // 4. decisions before any write: long row -> overflow; too many records -> the next size;
+    //    region or heap without room for the new rows -> deferred
+    if (tid == 0) {
+        if (s_fail == 3) {
+            push_overflow(a, b);
+        } else if (nn + s_np > CAP) {
+            pass_on(NEXT_Q);
+            s_fail = 2;
+        } else {
+            bool ok = a.rs.used[b] + s_nrow <= a.rs.fill;
+            unsigned long long h = 0;
+            if (ok && s_nrec) {
+                h = rs_heap_alloc(a.rs, s_nrec);
+                ok = h != ~0ULL;
+            }
+            if (!ok) {
+                push_defer(a, b, a.rs.used[b] + s_nrow <= a.rs.fill ? DEFER_HEAP : DEFER_REGION);
+                s_fail = 1;
+            } else {
+                a.rs.used[b] += s_nrow;
+                s_hbase = h;
+            }
+        }
+    }
+    __syncthreads();
+    if (s_fail) return;
+    const uint32_t n = nn + s_np;
+    for (uint32_t i = tid; i < nn; i += THREADS)
+        if ((uint32_t)(g.key[i] >> 32) == i && g.rent[i] == ROW_NONE) g.rheap[i] += (uint32_t)s_hbase;
+    // 5. records by row, in application order (prior first)
+    gen_sort_rows<Cfg::C>(g, n, s_wsum);
+    // 6. fold + write back
+    LdsEmit em{b, &s_emit, &s_gen};
+    for (uint32_t i = tid; i < n; i += THREADS)
+        if (i == 0 || (g.key[i] >> 32) != (g.key[i - 1] >> 32)) gen_fold_row(a, v, em, g, i, n);
+    __syncthreads();
+    if (tid == 0) {
+        atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)((long long)s_emit - (long long)s_np));
+        if (s_gen) a.rs.gen[b] = 1;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fast body: every row of the bucket has causal length 1 and no sentinel, so the merge is a
-// per-cell argmax of (col_version, value order, site-id rank, -position). Registers keep only the
-// stage keys of FAST_R records per thread; the full 64-B record of each winner is re-read (L2)
-// for the output. LDS: cell keys + one stage array + the open-addressing cell table (76 KB, two
-// workgroups per CU).
+// Fast bodies: every row of the bucket has causal length 1 and no sentinel, in the batch and in
+// the region, so the merge is a per-cell argmax of (col_version, value order, site-id rank,
+// -position) over the batch, then one comparison with the cell's prior clock in the heap (the
+// prior is earlier in application order: it keeps ties). Rows of the winners are resolved in the
+// region (lookups, then inserts of new rows once the region and heap are known to have room).
+
+// Row resolution shared by the fast bodies, run by the whole workgroup after the batch winners
+// (alive) are known. s_own: FAST_SLOTS words of LDS scratch; keys of record i: s_pk[i] and
+// s_tc[i] >> 16. Leaves row[k] (record index of the row's owner), the owner's heap index in
+// s_heap[owner] and its prior presence word in s_bits[owner]; owner lanes keep their region entry
+// in ent[k]. Returns false when the bucket was deferred (nothing written).
+template <int R>
+__device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, const bool (&alive)[R], uint32_t (&row)[R],
+                                 uint32_t (&ent)[R], const uint64_t *s_pk, const uint32_t *s_tc, uint32_t *s_own,
+                                 uint32_t *s_heap, uint64_t *s_bits, uint32_t *s_ctl, unsigned long long *s_hbase) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    if (tid == 0) s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        row[k] = 0;
+        ent[k] = ROW_NONE;
+        if (!alive[k]) continue;
+        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint64_t pk = s_pk[i];
+        const uint32_t t = s_tc[i] >> 16;
+        uint32_t slot = row_hash(pk, t) & (FAST_SLOTS - 1);
+        while (true) {
+            uint32_t o = __hip_atomic_load(&s_own[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (o == 0) o = atomicCAS(&s_own[slot], 0u, i + 1);
+            if (o == 0) {
+                row[k] = i;
+                break;
+            }
+            if (s_pk[o - 1] == pk && (s_tc[o - 1] >> 16) == t) {
+                row[k] = o - 1;
+                break;
+            }
+            slot = (slot + 1) & (FAST_SLOTS - 1);
+        }
+    }
+    __syncthreads();
+    // owners: read-only lookups; new rows counted (their heap offsets in s_heap until allocation)
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (!alive[k] || row[k] != i) continue;
+        const uint32_t t = s_tc[i] >> 16;
+        const uint32_t e = rs_lookup(a.rs, b, s_pk[i], t);
+        if (e != ROW_NONE) {
+            s_heap[i] = a.rs.ent[e].heap;
+            s_bits[i] = a.rs.ent[e].bits[0];
+            ent[k] = e;
+        } else {
+            s_heap[i] = atomicAdd(&s_ctl[1], (uint32_t)a.rs.stride[t]);
+            s_bits[i] = 0;
+            atomicAdd(&s_ctl[0], 1u);
+            ent[k] = ROW_NONE - 1;  // marks "owner of a new row"
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        bool ok = a.rs.used[b] + s_ctl[0] <= a.rs.fill;
+        unsigned long long h = 0;
+        if (ok && s_ctl[1]) {
+            h = rs_heap_alloc(a.rs, s_ctl[1]);
+            ok = h != ~0ULL;
+        }
+        if (!ok) {
+            push_defer(a, b, a.rs.used[b] + s_ctl[0] <= a.rs.fill ? DEFER_HEAP : DEFER_REGION);
+            s_ctl[2] = 1;
+        } else {
+            a.rs.used[b] += s_ctl[0];
+            *s_hbase = h;
+        }
+    }
+    __syncthreads();
+    if (s_ctl[2]) return false;
+    // new rows: heap slot, region entry (presence bits published at the end)
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (ent[k] != ROW_NONE - 1) continue;
+        const uint32_t hb = (uint32_t)*s_hbase + s_heap[i];
+        s_heap[i] = hb;
+        const uint64_t z[2] = {0, 0};
+        ent[k] = rs_insert(a.rs, b, s_pk[i], s_tc[i] >> 16, hb, z);
+    }
+    __syncthreads();
+    return true;
+}
+
+// prior clock of a cell vs the batch winner's key: > 0 when the winner is greater
+__device__ inline int prior_cmp_int(const MergeArgs &a, const Rec &pr, uint64_t cvb, uint64_t v0b, uint32_t rank) {
+    const uint64_t pcv = (uint64_t)pr.cv ^ 0x8000000000000000ULL, pv = pr.v0 ^ 0x8000000000000000ULL;
+    if (cvb != pcv) return cvb > pcv ? 1 : -1;
+    if (v0b != pv) return v0b > pv ? 1 : -1;
+    const uint32_t pr_rank = site_rank_of(a, pr.site);
+    return rank != pr_rank ? (rank > pr_rank ? 1 : -1) : 0;
+}
+
+// Fast body without impact output. Registers keep only the stage keys of FAST_R records per thread;
+// the full 64-B record of a winner is re-read (L2) for the wide form. LDS: cell keys + one stage
+// array + the open-addressing cell table (76 KB, two workgroups per CU).
 template <bool WIDE>
 __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketView &v) {
     __shared__ uint64_t s_pk[CAP_FAST];
     __shared__ uint64_t s_k[CAP_FAST];
     __shared__ uint32_t s_tc[CAP_FAST];
     __shared__ uint32_t s_own[FAST_SLOTS];
-    __shared__ uint32_t s_outcnt;
+    __shared__ uint32_t s_ctl[4];
+    __shared__ unsigned long long s_hbase, s_live;
     const uint32_t tid = threadIdx.x;
-    const uint32_t n = v.np + v.nn;
-    Rec *outb = a.out + a.out_off[b];
-    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    const uint32_t n = v.nn;
     uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], rp[FAST_R], dbv[FAST_R];
     uint32_t meta[FAST_R], cell[FAST_R], seq[FAST_R], site[FAST_R];
     bool alive[FAST_R];
@@ -952,8 +1144,8 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     // bucket instead of one per record group), then the site-rank lookups as one more batch
     uint4 q[FAST_R][4];
 #pragma unroll
-    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
-    if (tid == 0) s_outcnt = 0;
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    if (tid == 0) s_live = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
     uint32_t srank[FAST_R];
 #pragma unroll
@@ -1038,15 +1230,48 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
             __syncthreads();
         }
     }
-    // winners: re-read the record, write the clock row (wave-cooperative 64-B stores)
+    // rows of the winners (s_own: row table, then heap indices; s_k: presence words)
+    uint32_t row[FAST_R], ent[FAST_R];
+    if (!fast_rows<FAST_R>(a, b, alive, row, ent, s_pk, s_tc, s_own, s_own, s_k, s_ctl, &s_hbase)) return;
+    // winners vs the prior clock of their cell; new cells set their presence bit
+    uint32_t hb[FAST_R];
+    uint32_t nlive = 0;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        hb[k] = 0;
+        if (!alive[k]) continue;
+        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t c = s_tc[i] & 0xFFFFu;
+        hb[k] = s_own[row[k]] + c;
+        if ((s_k[row[k]] >> c) & 1ULL) {
+            const Rec pr = load_rec(a.rs.heap + hb[k]);
+            int cmp;
+            if (WIDE) {
+                Rec x = load_rec(v.fresh + i);
+                cmp = (int64_t)(cv[k] ^ 0x8000000000000000ULL) != pr.cv
+                          ? ((int64_t)(cv[k] ^ 0x8000000000000000ULL) > pr.cv ? 1 : -1)
+                          : value_cmp(x, pr);
+                if (cmp == 0) {
+                    const uint32_t rk = (uint32_t)(rp[k] >> 32), prk = site_rank_of(a, pr.site);
+                    cmp = rk != prk ? (rk > prk ? 1 : -1) : 0;
+                }
+            } else {
+                cmp = prior_cmp_int(a, pr, cv[k], v0[k] ^ 0x8000000000000000ULL, (uint32_t)(rp[k] >> 32));
+            }
+            if (cmp <= 0) alive[k] = false;  // the prior clock is earlier: it keeps ties
+        } else {
+            atomicOr(reinterpret_cast<unsigned long long *>(&s_k[row[k]]), 1ULL << c);
+            nlive++;
+        }
+    }
+    // winners: the clock row into its heap slot (wave-cooperative 64-B stores)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
-        uint32_t o = 0;
         Rec x;
         if (alive[k]) {
             if (WIDE) {
-                x = load_rec(v.at(i));
+                x = load_rec(v.fresh + i);
             } else {
                 x.pk = s_pk[i];
                 x.cv = (int64_t)(cv[k] ^ 0x8000000000000000ULL);
@@ -1059,51 +1284,53 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
                 x.pos = ~(uint32_t)rp[k];
                 x.meta = CORRO_INTEGER;
             }
-            o = atomicAdd(&s_outcnt, 1u);
-            if (a.track_ts) outts[o] = rec_ts(a, v, x);
+            if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
             x.cl = 1;
-            x.pos = o;
+            x.pos = hb[k];
         }
-        store_rec_wave(outb, o, x, alive[k]);
+        store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
     }
+    if (nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
-    if (tid == 0) {
-        a.out_cnt[b] = s_outcnt;
-        a.out_flags[b] = 0;
-        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+    // owners publish the rows' presence bits
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_k[i];
     }
+    if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
 }
 
 // Same per-cell merge with per-change crsql_rows_impacted() growth (impact output requested: the
 // agent path, util.rs:1246-1262). With every cl = 1 and no sentinel (App. A.1 rule 4 with L <= 1)
-// change i grows the counter by exactly 1 iff it is the first change of its cell in application
-// order or its key (col_version, value, site id) is strictly greater than every earlier one: a
-// strict prefix maximum. The cell's final winner is the maximum key, earliest among equals. Both
-// are decided per change by one walk over the cell's member list (counting sort of the bucket's
-// records by cell in LDS), so no atomic argmax stages are needed. One workgroup per CU (LDS).
-template <bool WIDE>
-__device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const BucketView &v) {
+// change i grows the counter by exactly 1 iff its key (col_version, value, site id) is strictly
+// greater than the cell's prior clock (if any) and than every earlier change of the cell in the
+// batch: a strict prefix maximum. The cell's new clock is the batch maximum (earliest among equals)
+// when it beats the prior. Decided per change by one walk over the cell's member list (counting
+// sort of the bucket's records by cell in LDS). Mixed value classes; one workgroup per CU (LDS).
+__device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, const BucketView &v) {
     __shared__ uint64_t s_pk[CAP_FAST];      // cell hashing: pk; then the biased col_version keys
     __shared__ uint32_t s_tc[CAP_FAST];      // cell hashing: table_cid; then site ranks
-    __shared__ uint32_t s_own[FAST_SLOTS];   // cell hashing: slot owners; then member counts/offsets
-    __shared__ uint64_t s_v0[CAP_FAST];
+    __shared__ uint32_t s_own[FAST_SLOTS];   // cell / row hashing; heap indices; member counts/offsets
+    __shared__ uint64_t s_v0[CAP_FAST];      // row presence words; then values
     __shared__ uint32_t s_pos[CAP_FAST];
     __shared__ uint16_t s_list[CAP_FAST];
-    __shared__ uint64_t s_v1[WIDE ? CAP_FAST : 1];
-    __shared__ uint32_t s_meta[WIDE ? CAP_FAST : 1];
+    __shared__ uint64_t s_v1[CAP_FAST];
+    __shared__ uint32_t s_meta[CAP_FAST];
     __shared__ uint32_t s_wsum[MERGE_THREADS / 64];
-    __shared__ uint32_t s_outcnt;
+    __shared__ uint32_t s_ctl[4];
+    __shared__ unsigned long long s_hbase, s_live;
     const uint32_t tid = threadIdx.x;
-    const uint32_t n = v.np + v.nn;
-    Rec *outb = a.out + a.out_off[b];
-    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    const uint32_t n = v.nn;
     uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], pk[FAST_R], dbv[FAST_R];
     uint32_t meta[FAST_R], cell[FAST_R], seq[FAST_R], site[FAST_R], pos[FAST_R], rank[FAST_R], tc[FAST_R];
+    uint32_t row[FAST_R], ent[FAST_R], hb[FAST_R];
     bool alive[FAST_R];
+    uint32_t flags = 0;  // bit 2k: beats the prior clock; bit 2k+1: the cell had no prior clock
     uint4 q[FAST_R][4];
 #pragma unroll
-    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
-    if (tid == 0) s_outcnt = 0;
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    if (tid == 0) s_live = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1117,8 +1344,8 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
         s_tc[i] = r.tcid;
         cv[k] = (uint64_t)r.cv ^ 0x8000000000000000ULL;
         v0[k] = r.v0;
-        v1[k] = WIDE ? r.v1 : 0;
-        meta[k] = WIDE ? r.meta : (uint32_t)CORRO_INTEGER;
+        v1[k] = r.v1;
+        meta[k] = r.meta;
         pos[k] = r.pos;
         site[k] = r.site;
         dbv[k] = (uint64_t)r.dbv;
@@ -1149,6 +1376,28 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
         }
     }
     __syncthreads();
+    // 1b. rows of every change, prior clocks: does the change beat its cell's prior?
+    if (!fast_rows<FAST_R>(a, b, alive, row, ent, s_pk, s_tc, s_own, s_own, s_v0, s_ctl, &s_hbase)) return;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        hb[k] = 0;
+        if (!alive[k]) continue;
+        const uint32_t c = tc[k] & 0xFFFFu;
+        hb[k] = s_own[row[k]] + c;
+        if ((s_v0[row[k]] >> c) & 1ULL) {
+            const Rec pr = load_rec(a.rs.heap + hb[k]);
+            const int64_t bcv = (int64_t)(cv[k] ^ 0x8000000000000000ULL);
+            int cmp = bcv != pr.cv ? (bcv > pr.cv ? 1 : -1) : value_cmp_f(meta[k], v0[k], v1[k], pr.meta, pr.v0, pr.v1);
+            if (cmp == 0) {
+                const uint32_t prk = site_rank_of(a, pr.site);
+                cmp = rank[k] != prk ? (rank[k] > prk ? 1 : -1) : 0;
+            }
+            if (cmp > 0) flags |= 1u << (2 * k);
+        } else {
+            flags |= 3u << (2 * k);
+        }
+    }
+    __syncthreads();
     // 2. member counts per owner (s_own reused), keys into LDS
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
     __syncthreads();
@@ -1160,10 +1409,8 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
         s_tc[i] = rank[k];
         s_v0[i] = v0[k];
         s_pos[i] = pos[k];
-        if (WIDE) {
-            s_v1[i] = v1[k];
-            s_meta[i] = meta[k];
-        }
+        s_v1[i] = v1[k];
+        s_meta[i] = meta[k];
         atomicAdd(&s_own[cell[k]], 1u);
     }
     __syncthreads();
@@ -1211,7 +1458,7 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
         const uint32_t i = k * MERGE_THREADS + tid;
         if (!alive[k]) continue;
         const uint32_t mend = s_own[cell[k]];
-        bool imp = true, win = true;
+        bool imp = (flags >> (2 * k)) & 1u, win = imp;
         for (uint32_t m = mbeg[k]; m < mend; m++) {
             const uint32_t j = s_list[m];
             if (j == i) continue;
@@ -1220,8 +1467,7 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
             if (cj != cv[k]) {
                 c = cj > cv[k] ? 1 : -1;
             } else {
-                c = WIDE ? value_cmp_f(s_meta[j], s_v0[j], s_v1[j], meta[k], v0[k], v1[k])
-                         : (s_v0[j] != v0[k] ? (((s_v0[j] ^ 0x8000000000000000ULL) > (v0[k] ^ 0x8000000000000000ULL)) ? 1 : -1) : 0);
+                c = value_cmp_f(s_meta[j], s_v0[j], s_v1[j], meta[k], v0[k], v1[k]);
                 if (c == 0) {
                     const uint32_t rj = s_tc[j];
                     c = rj != rank[k] ? (rj > rank[k] ? 1 : -1) : 0;
@@ -1234,10 +1480,17 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
         if (a.impact && (pos[k] & BATCH_POS)) a.impact[pos[k] & 0x7FFFFFFFu] = imp ? 1 : 0;
         alive[k] = win;
     }
-    // 5. winners: the clock row (wave-cooperative 64-B stores)
+    __syncthreads();
+    // 5. winners: the clock row into its heap slot; presence bits of new cells (s_v0 per owner)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        uint32_t o = 0;
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (ent[k] != ROW_NONE && row[k] == i) s_v0[i] = a.rs.ent[ent[k]].bits[0];
+    }
+    __syncthreads();
+    uint32_t nlive = 0;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
         Rec x;
         if (alive[k]) {
             x.pk = pk[k];
@@ -1250,44 +1503,50 @@ __device__ inline void fast_body_impact(const MergeArgs &a, uint32_t b, const Bu
             x.site = site[k];
             x.pos = pos[k];
             x.meta = meta[k];
-            o = atomicAdd(&s_outcnt, 1u);
-            if (a.track_ts) outts[o] = rec_ts(a, v, x);
+            if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
             x.cl = 1;
-            x.pos = o;
+            x.pos = hb[k];
+            if ((flags >> (2 * k + 1)) & 1u) {
+                atomicOr(reinterpret_cast<unsigned long long *>(&s_v0[row[k]]), 1ULL << (tc[k] & 0xFFFFu));
+                nlive++;
+            }
         }
-        store_rec_wave(outb, o, x, alive[k]);
+        store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
     }
+    if (nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
-    if (tid == 0) {
-        a.out_cnt[b] = s_outcnt;
-        a.out_flags[b] = 0;
-        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_v0[i];
     }
+    if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
 }
 
-// The INTEGER form of fast_body_impact in 76 KB of LDS (two workgroups per CU instead of one): a
+// The INTEGER form of the impact body in 76 KB of LDS (two workgroups per CU instead of one): a
 // cell's members are placed in application order (each member's rank among its cell's positions),
 // so "earlier" is the member index and no position array is kept for the walk; the hashing arrays
 // are reused for the ordered keys.
 __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, const BucketView &v) {
     __shared__ uint64_t s_a[CAP_FAST];      // hashing: pk; then the cell-ordered biased col_versions
     __shared__ uint32_t s_b[CAP_FAST];      // hashing: table_cid; then positions by member slot; then site ranks
-    __shared__ uint64_t s_c[CAP_FAST];      // cell-ordered values
-    __shared__ uint32_t s_own[FAST_SLOTS];  // hashing: slot owners; then member counts / offsets / ends
+    __shared__ uint64_t s_c[CAP_FAST];      // row presence words; then cell-ordered values; then presence words
+    __shared__ uint32_t s_own[FAST_SLOTS];  // cell / row hashing; heap indices; member counts / offsets / ends
     __shared__ uint32_t s_wsum[MERGE_THREADS / 64];
-    __shared__ uint32_t s_outcnt;
+    __shared__ uint32_t s_ctl[4];
+    __shared__ unsigned long long s_hbase, s_live;
     const uint32_t tid = threadIdx.x;
-    const uint32_t n = v.np + v.nn;
-    Rec *outb = a.out + a.out_off[b];
-    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
+    const uint32_t n = v.nn;
     uint64_t cv[FAST_R], v0[FAST_R], pk[FAST_R], dbv[FAST_R];
     uint32_t cell[FAST_R], seq[FAST_R], site[FAST_R], pos[FAST_R], rank[FAST_R], tc[FAST_R];
     uint32_t md[FAST_R];  // member range begin | own member slot << 16 (both < CAP_FAST); end = s_own[cell]
+    uint32_t row[FAST_R], ent[FAST_R], hb[FAST_R];
+    uint32_t flags = 0;   // bit 2k: beats the prior clock; bit 2k+1: the cell had no prior clock
     bool alive[FAST_R];
     uint4 q[FAST_R][4];
 #pragma unroll
-    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
-    if (tid == 0) s_outcnt = 0;
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    if (tid == 0) s_live = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1328,6 +1587,22 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
                 break;
             }
             slot = (slot + 1) & (FAST_SLOTS - 1);
+        }
+    }
+    __syncthreads();
+    // 1b. rows of every change, prior clocks: does the change beat its cell's prior?
+    if (!fast_rows<FAST_R>(a, b, alive, row, ent, s_a, s_b, s_own, s_own, s_c, s_ctl, &s_hbase)) return;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        hb[k] = 0;
+        if (!alive[k]) continue;
+        const uint32_t c = tc[k] & 0xFFFFu;
+        hb[k] = s_own[row[k]] + c;
+        if ((s_c[row[k]] >> c) & 1ULL) {
+            const Rec pr = load_rec(a.rs.heap + hb[k]);
+            if (prior_cmp_int(a, pr, cv[k], v0[k], rank[k]) > 0) flags |= 1u << (2 * k);
+        } else {
+            flags |= 3u << (2 * k);
         }
     }
     __syncthreads();
@@ -1392,11 +1667,11 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
         }
     __syncthreads();
     // 4. one walk over the cell's members (application order) per change: impact (strict prefix
-    // maximum) and winner (maximum, earliest among equals)
+    // maximum, above the prior clock) and winner (maximum, earliest among equals, above the prior)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         if (!alive[k]) continue;
-        bool imp = true, win = true;
+        bool imp = (flags >> (2 * k)) & 1u, win = imp;
         const uint32_t mb = md[k] & 0xFFFFu, d = md[k] >> 16, me = s_own[cell[k]];
         for (uint32_t m = mb; m < me; m++) {
             if (m == d) continue;
@@ -1411,10 +1686,17 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
         if (a.impact && (pos[k] & BATCH_POS)) a.impact[pos[k] & 0x7FFFFFFFu] = imp ? 1 : 0;
         alive[k] = win;
     }
-    // 5. winners: the clock row (wave-cooperative 64-B stores)
+    __syncthreads();
+    // 5. winners: the clock row into its heap slot; presence bits of new cells (s_c per owner)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        uint32_t o = 0;
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (ent[k] != ROW_NONE && row[k] == i) s_c[i] = a.rs.ent[ent[k]].bits[0];
+    }
+    __syncthreads();
+    uint32_t nlive = 0;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
         Rec x;
         if (alive[k]) {
             x.pk = pk[k];
@@ -1427,56 +1709,53 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
             x.site = site[k];
             x.pos = pos[k];
             x.meta = CORRO_INTEGER;
-            o = atomicAdd(&s_outcnt, 1u);
-            if (a.track_ts) outts[o] = rec_ts(a, v, x);
+            if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
             x.cl = 1;
-            x.pos = o;
+            x.pos = hb[k];
+            if ((flags >> (2 * k + 1)) & 1u) {
+                atomicOr(reinterpret_cast<unsigned long long *>(&s_c[row[k]]), 1ULL << (tc[k] & 0xFFFFu));
+                nlive++;
+            }
         }
-        store_rec_wave(outb, o, x, alive[k]);
+        store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
     }
+    if (nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
-    if (tid == 0) {
-        a.out_cnt[b] = s_outcnt;
-        a.out_flags[b] = 0;
-        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_c[i];
     }
+    if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
+}
+
+__device__ inline uint32_t bucket_of_block(const MergeArgs &a) {
+    return a.bucket_list ? a.bucket_list[blockIdx.x] : blockIdx.x;
 }
 
 // Bucket triage + the INTEGER fast body (one workgroup per bucket). General buckets and, for a
-// batch with non-INTEGER values, every fast bucket are queued for the list-driven kernels below,
-// so those launch a few hundred workgroups instead of one per bucket.
+// batch or state with non-INTEGER values, every fast bucket are queued for the list-driven kernels
+// below, so those launch a few hundred workgroups instead of one per bucket.
 template <bool IMPACT>
 static __global__ void __launch_bounds__(MERGE_THREADS, 4)
 k_merge_fast_int(MergeArgs a) {
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = bucket_of_block(a);
     // every per-bucket word is loaded up front (independent scalar loads, one latency)
     BucketView v;
-    v.np = a.prior_cnt[b];
-    v.nn = a.new_cnt[b];
-    const uint64_t poff = a.prior_off[b];
-    const uint32_t soff = a.stage_off[b];
-    const uint32_t pflag = a.prior_flags[b];
+    bucket_view(a, b, v);
+    const uint32_t rgen = a.rs.gen[b];
     const uint32_t bword = a.bflags[b >> 5];
-    const unsigned long long wide = a.misc[3];
-    v.prior = a.prior + poff;
-    v.fresh = a.stage + soff;
-    v.prior_ts = a.prior_ts ? a.prior_ts + poff : nullptr;
-    const uint32_t n = v.np + v.nn;
-    if (n == 0) {
-        if (threadIdx.x == 0) {
-            a.out_cnt[b] = 0;
-            a.out_flags[b] = 0;
-        }
-        return;
-    }
-    if (a.force_general || pflag || ((bword >> (b & 31)) & 1u)) {
+    const unsigned long long wide = a.misc[MISC_WIDE];
+    const uint32_t n = v.nn;
+    if (n == 0) return;
+    if (a.force_general || rgen || ((bword >> (b & 31)) & 1u)) {
         if (threadIdx.x == 0) {
             if (n <= CAP_GEN_SMALL)
-                a.gen_list[gridDim.x + atomicAdd(&a.misc[6], 1ULL)] = b;  // (grid = one WG per bucket)
+                a.gen_list[a.B + atomicAdd(&a.misc[MISC_GEN_SMALL], 1ULL)] = b;
             else if (n <= CAP_GEN_MID)
-                a.gen_list[2 * gridDim.x + atomicAdd(&a.misc[7], 1ULL)] = b;
+                a.gen_list[2 * a.B + atomicAdd(&a.misc[MISC_GEN_MID], 1ULL)] = b;
             else
-                a.gen_list[atomicAdd(&a.misc[4], 1ULL)] = b;
+                a.gen_list[atomicAdd(&a.misc[MISC_GEN], 1ULL)] = b;
         }
         return;
     }
@@ -1485,7 +1764,7 @@ k_merge_fast_int(MergeArgs a) {
         return;
     }
     if (a.state_wide || wide != 0) {
-        if (threadIdx.x == 0) a.wide_list[atomicAdd(&a.misc[5], 1ULL)] = b;
+        if (threadIdx.x == 0) a.wide_list[atomicAdd(&a.misc[MISC_WIDEQ], 1ULL)] = b;
         return;
     }
     if constexpr (IMPACT)
@@ -1499,101 +1778,44 @@ constexpr uint32_t LIST_GRID = 512;
 template <bool IMPACT>
 static __global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
 k_merge_fast_wide(MergeArgs a) {
-    const uint32_t cnt = (uint32_t)a.misc[5];
+    const uint32_t cnt = (uint32_t)a.misc[MISC_WIDEQ];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
         const uint32_t b = a.wide_list[k];
         BucketView v;
         bucket_view(a, b, v);
         if (IMPACT)
-            fast_body_impact<true>(a, b, v);
+            fast_body_impact_wide(a, b, v);
         else
             fast_body<true>(a, b, v);
         __syncthreads();
     }
 }
 
-// General body in LDS for one queued bucket: sort (row, position), one lane per row folds the
-// cr-sqlite rules. Buckets larger than LDS are passed on to the overflow path (k_ovf_*).
-template <uint32_t CAP, uint32_t THREADS>
-__device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
-    using Cfg = GenCfg<CAP, THREADS>;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[Cfg::LDS];
-    __shared__ uint32_t s_outcnt, s_flag;
-    const uint32_t tid = threadIdx.x;
-    BucketView v;
-    bucket_view(a, b, v);
-    const uint32_t n = v.np + v.nn;
-    if (n > CAP) {
-        if (tid == 0) push_overflow(a, b);
-        return;
-    }
-    Rec *outb = a.out + a.out_off[b];
-    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[b] : nullptr;
-    if (tid == 0) {
-        s_outcnt = 0;
-        s_flag = 0;
-    }
-    GenArrays g;
-    uint8_t *p = smem;
-    g.pk = reinterpret_cast<uint64_t *>(p); p += CAP * 8;
-    g.cv = reinterpret_cast<int64_t *>(p); p += CAP * 8;
-    g.key = reinterpret_cast<uint64_t *>(p); p += CAP * 8;
-    g.ccv = reinterpret_cast<int64_t *>(p); p += CAP * 8;
-    g.tc = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
-    g.cl = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
-    g.pos = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
-    g.val = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
-    g.ccid = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
-    g.csrc = reinterpret_cast<uint32_t *>(p); p += CAP * 4;
-    g.own = reinterpret_cast<uint32_t *>(p);
-    g.slots = Cfg::SLOTS;
-    g.rshift = 32;
-    g.P = n;
-    __shared__ uint32_t s_long, s_wsum[MERGE_THREADS / 64];
-    if (tid == 0) s_long = 0;
-    // a row longer than LONG_ROW would serialise this bucket on one lane: the overflow path
-    // folds it with device-wide scans instead (ovf_kernels.h)
-    gen_group<Cfg::C>(v, g, s_wsum, &s_long);
-    if (s_long) {
-        if (tid == 0) push_overflow(a, b);
-        return;
-    }
-    for (uint32_t i = tid; i < n; i += blockDim.x)
-        if (i == 0 || (g.key[i] >> 32) != (g.key[i - 1] >> 32))
-            gen_fold_row(a, v, outb, outts, &s_outcnt, &s_flag, g, i, n);
-    __syncthreads();
-    if (tid == 0) {
-        a.out_cnt[b] = s_outcnt;
-        a.out_flags[b] = s_flag;
-        atomicAdd(&a.misc[2], (unsigned long long)s_outcnt);
-    }
-}
-
 static __global__ void __launch_bounds__(MERGE_THREADS)
 k_merge_gen(MergeArgs a) {
-    const uint32_t cnt = (uint32_t)a.misc[4];
+    const uint32_t cnt = (uint32_t)a.misc[MISC_GEN];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
-        gen_bucket<CAP_GEN, MERGE_THREADS>(a, a.gen_list[k]);
+        gen_bucket<CAP_GEN, MERGE_THREADS, 0>(a, a.gen_list[k]);
         __syncthreads();
     }
 }
 
-// general buckets of at most CAP_GEN_MID records (queued at gen_list + 2B, count misc[7])
+// general buckets of at most CAP_GEN_MID records (queued at gen_list + 2B)
 static __global__ void __launch_bounds__(MERGE_THREADS, 4)
-k_merge_gen_mid(MergeArgs a, uint32_t B) {
-    const uint32_t cnt = (uint32_t)a.misc[7];
+k_merge_gen_mid(MergeArgs a) {
+    const uint32_t cnt = (uint32_t)a.misc[MISC_GEN_MID];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
-        gen_bucket<CAP_GEN_MID, MERGE_THREADS>(a, a.gen_list[2 * B + k]);
+        gen_bucket<CAP_GEN_MID, MERGE_THREADS, 2>(a, a.gen_list[2 * a.B + k]);
         __syncthreads();
     }
 }
 
-// general buckets of at most CAP_GEN_SMALL records (queued at gen_list + B, count misc[6])
+// general buckets of at most CAP_GEN_SMALL records (queued at gen_list + B)
 static __global__ void __launch_bounds__(GEN_SMALL_THREADS, 4)
-k_merge_gen_small(MergeArgs a, uint32_t B) {
-    const uint32_t cnt = (uint32_t)a.misc[6];
+k_merge_gen_small(MergeArgs a) {
+    const uint32_t cnt = (uint32_t)a.misc[MISC_GEN_SMALL];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
-        gen_bucket<CAP_GEN_SMALL, GEN_SMALL_THREADS>(a, a.gen_list[B + k]);
+        gen_bucket<CAP_GEN_SMALL, GEN_SMALL_THREADS, 1>(a, a.gen_list[a.B + k]);
         __syncthreads();
     }
 }
@@ -1635,27 +1857,80 @@ static __global__ void k_dbv_fold(unsigned long long *__restrict__ dbv, const un
     if (i < nsites && batch[i] > dbv[i]) dbv[i] = batch[i];
 }
 
-// export: bucket slices -> dense SoA rows
-static __global__ void k_export(const Rec *__restrict__ st, const uint64_t *__restrict__ st_ts,
-                         const uint64_t *__restrict__ off, const uint32_t *__restrict__ cnt,
-                         const uint64_t *__restrict__ dense, corro_rows o) {
-    const uint32_t b = blockIdx.x;
-    const uint32_t n = cnt[b];
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const Rec r = load_rec(st + off[b] + i);
-        const uint64_t k = dense[b] + i;
+// Export / materialisation: every present clock record of the row store, row by row (rows in slot
+// order; a row's records sentinel first, then by cid), each with the row's causal length. Output
+// slots come from one atomic per wave (a wave-level prefix sum of the rows' record counts).
+template <class F>
+__device__ inline void for_each_state_record(const RowStore &rs, uint64_t nent, unsigned long long *count, F &&f) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < nent; base += stride) {
+        const uint64_t e = base + lane;
+        RowEnt re{};
+        if (e < nent) re = rs.ent[e];
+        const bool ok = re.tag != 0;
+        const uint32_t cnt = ok ? row_popc(re.bits) : 0u;
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        const uint32_t tot = __shfl(inc, 63);
+        unsigned long long w0 = 0;
+        if (lane == 63 && tot) w0 = atomicAdd(count, (unsigned long long)tot);
+        w0 = __shfl(w0, 63);
+        if (!cnt) continue;
+        unsigned long long k = w0 + inc - cnt;
+        const int64_t L = (re.bits[0] & 1ULL) ? rs.heap[re.heap].cv : 1;
+        for (int w = 0; w < 2; w++)
+            for (uint64_t m = re.bits[w]; m; m &= m - 1) {
+                const uint32_t c = 64 * w + (uint32_t)__ffsll((unsigned long long)m) - 1;
+                f(k++, re.heap + c, L);
+            }
+    }
+}
+
+static __global__ void k_export(RowStore rs, uint64_t nent, unsigned long long *count, corro_rows o) {
+    for_each_state_record(rs, nent, count, [&](unsigned long long k, uint32_t h, int64_t L) {
+        const Rec r = load_rec(rs.heap + h);
         o.pk[k] = r.pk;
         o.table_cid[k] = r.tcid;
         o.col_version[k] = r.cv;
         o.db_version[k] = r.dbv;
-        o.cl[k] = (int64_t)r.cl;
+        o.cl[k] = L;
         o.seq[k] = r.seq;
         o.site[k] = r.site;
-        o.ts[k] = st_ts ? st_ts[off[b] + i] : 0ULL;
+        o.ts[k] = rs.heap_ts ? rs.heap_ts[h] : 0ULL;
         o.val0[k] = r.v0;
         o.val1[k] = r.v1;
         o.val_type[k] = (uint8_t)vtype(r.meta);
         o.val_len[k] = (uint8_t)vlen(r.meta);
+    });
+}
+
+// dense copy of the state's clock records (64-B Recs with cl = the row's causal length, pos = the
+// dense index) + their ts, for the extraction index
+static __global__ void k_materialize(RowStore rs, uint64_t nent, unsigned long long *count, Rec *out,
+                                     uint64_t *out_ts) {
+    for_each_state_record(rs, nent, count, [&](unsigned long long k, uint32_t h, int64_t L) {
+        Rec r = load_rec(rs.heap + h);
+        r.cl = (uint32_t)L;
+        r.pos = (uint32_t)k;
+        store_rec(out + k, r);
+        if (out_ts) out_ts[k] = rs.heap_ts ? rs.heap_ts[h] : 0ULL;
+    });
+}
+
+// Growth: every entry of the old regions re-inserted into regions of twice the slots (a row keeps
+// its region: the region is its bucket). One workgroup per old region.
+static __global__ void k_rehash(const RowEnt *__restrict__ old_ent, uint32_t old_log2S, RowStore rs) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t S = 1u << old_log2S;
+    for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
+        const RowEnt re = old_ent[((size_t)b << old_log2S) + s];
+        if (re.tag == 0) continue;
+        rs_insert(rs, b, re.pk, re.tag - 1, re.heap, re.bits);
     }
 }
 

@@ -1,9 +1,11 @@
 // Overflow path, device-wide: the buckets too large for a workgroup's LDS, or holding a long row
 // (Zipf-hot rows: tens of thousands of changes in one row), are folded by kernels that span the
 // whole GPU, so a bucket of a million changes is not one CU's work, and a hot row is not a chain
-// of dependent loads in one lane. Every per-record / per-position / per-row array is global,
-// indexed by the bucket's base offset kb (prefix of the oversized buckets' sizes) plus the local
-// index; rows are identified by kb + their owner record.
+// of dependent loads in one lane. Every per-record / per-position / per-row array is global.
+// Records [0, Kb) are the oversized buckets' batch changes (bucket k at koff[k]); their rows get
+// dense ids (bucket-major), each row is looked up once in its region, and the prior clock records
+// of the rows found are appended as records [Kb, K) (read from the heap), so the sort by (row,
+// position) places them first in their row -- the prior state as a prefix of the application order.
 //
 // Parallel row fold. Per row, with changes sorted by application position
 // (prior state first, as a prefix):
@@ -24,7 +26,10 @@
 //
 // Phases:
 //   k_ovf_load, k_ovf_rowhash       fields; row owners (open addressing per bucket, read-before-CAS)
-//   scan of owner flags, k_ovf_rowkey  dense row ids, compact positions
+//   scan of owner flags               dense row ids
+//   k_ovf_lookup, scan, k_ovf_pload   each row looked up in its region (new rows counted per bucket
+//                                     for the host's capacity check), prior records appended
+//   k_ovf_rowkey                      compact positions (prior: slot index < pm; batch: pm + i)
 //   radix sort by (row, position)                                       [prims.hip, rocPRIM]
 //   k_ovf_gather                    cl in sorted order, row starts
 //   exclusive max-scan of cl by row -> L                                [rocPRIM scan_by_key]
@@ -39,11 +44,12 @@
 //                                   compared in registers; group start = plain max-scan of the
 //                                   group heads' indices [prims.hip]
 //   k_ovf_link                      each group's end is linked under its epoch's record
-//   k_ovf_walk                      one thread per row: the walk over its records, emission;
-//                                   rows outside App. A.3 run the sequential fold instead
+//   k_ovf_walk                      one thread per row: the walk over its records, the row written
+//                                   back to its heap slot (found or inserted in its region); rows
+//                                   outside App. A.3 run the sequential fold instead
 //   k_ovf_impacts                   candidate impacts (strict prefix max, seeded by the epoch's
 //                                   first element of the cell)
-//   k_ovf_finish                    per-bucket counts and flags
+//   k_ovf_finish                    region fill counts
 #pragma once
 
 namespace corro {
@@ -57,24 +63,28 @@ struct alignas(16) OvfKey {
 };
 
 struct OvfDev {
-    uint32_t G, K;              // oversized buckets, their records
+    uint32_t G, K;              // oversized buckets, their records (batch + prior)
+    uint32_t Kb;                // batch records [0, Kb); prior records [Kb, K)
     uint32_t cid_bits;          // a candidate key is (epoch's record position) << cid_bits | cid
     uint32_t rshift;            // a record's sort key is dense row << rshift | compact position
-    uint32_t pm;                // compact position of batch change i: pm + i (prior rows: their slice index < pm)
+    uint32_t pm;                // compact position of batch change i: pm + i (prior records: slot < pm)
     uint32_t ncand;             // candidates: candidate-sorted indices [0, ncand) (the rest of ckey_s is ~0)
     uint32_t nrows;             // rows (dense ids [0, nrows))
-    const uint32_t *koff;       // [G + 1] bucket base offsets
+    const uint32_t *koff;       // [G + 1] bucket base offsets of the batch records
     const uint32_t *slot_off;   // [G] row-hash slot region, next_pow2(2 n) words each
-    // per record (kb + i)
+    // per record (global index)
     uint64_t *pk;
     int64_t *cv;
     uint32_t *tc, *cl, *pos;
+    uint32_t *src;              // batch record: its staged index; prior record: its heap index
     // per sorted position
     uint64_t *key, *key_s;
-    uint32_t *val, *val_s;      // local record index
+    uint32_t *val, *val_s;      // global record index
     uint32_t *rowid, *cl_s, *lx, *recf, *epc, *kind, *pb;
-    // per row (global row id)
+    // per row (dense id)
     uint32_t *rstart, *rbad, *rnrec, *recs, *head;
+    uint32_t *rowner, *rb, *rheap, *rprior, *rpoff;  // owner record, bucket, prior heap slot, prior records
+    uint64_t *rbits;                                 // [2 * nrows] prior presence bits
     uint32_t *scid, *spos, *sz;  // walk state at [rstart, rstart + ncell)
     uint32_t *ccid, *csrc;       // sequential-fold scratch (GenArrays)
     int64_t *ccv;
@@ -83,8 +93,22 @@ struct OvfDev {
     uint32_t *cval, *cval_s, *cbest, *cgs, *nxt, *fstg;
     // candidates' cell keys gathered in candidate-sorted order (the argmax scan reads neighbours)
     OvfKey *qkey;
+    OvfKey *pkey;                // [K - Kb] the prior records' keys, read before the walk rewrites their slots
     uint32_t *slots;
-    uint32_t *ocnt, *oflag;     // [G]
+    uint32_t *bnew, *bnrec;      // [G] new rows / their heap records per bucket
+};
+
+// a record's 64-B source: the staged batch change or the prior heap record
+__device__ inline const Rec *ovf_rec(const MergeArgs &a, const OvfDev &d, uint32_t x) {
+    return x < d.Kb ? a.stage + d.src[x] : a.rs.heap + d.src[x];
+}
+
+// the view gen_fold_row / heap_write_row read records through (record = global index)
+struct OvfView {
+    const MergeArgs *a;
+    const OvfDev *d;
+    __device__ inline const Rec *at(uint32_t x) const { return ovf_rec(*a, *d, x); }
+    __device__ inline uint64_t prior_ts(const Rec &r) const { return a->rs.heap_ts ? a->rs.heap_ts[r.pos] : 0ULL; }
 };
 
 __device__ inline uint32_t ovf_bucket_of(const OvfDev &d, uint32_t r) {
@@ -98,13 +122,16 @@ __device__ inline uint32_t ovf_bucket_of(const OvfDev &d, uint32_t r) {
 }
 
 // by sorted position p
-// (the value words, metadata and site of a record are read from its staged 64-B record: only
+// (the value words, metadata and site of a record are read from its 64-B source record: only
 // candidates and carried cells need them, a small part of the overflow records)
 __device__ inline OvfKey ovf_key_rec(const MergeArgs &a, const OvfDev &d, uint32_t p, bool z) {
-    const uint32_t b = d.pb[p];
-    BucketView v;
-    bucket_view(a, a.ovf_list[b], v);
-    const Rec r = load_rec(v.at(d.val_s[p]));
+    const uint32_t x = d.val_s[p];
+    if (x >= d.Kb) {  // a prior clock: its heap slot may already hold the row's new value
+        OvfKey k = d.pkey[x - d.Kb];
+        if (z) k.cv = 0;
+        return k;
+    }
+    const Rec r = load_rec(ovf_rec(a, d, x));
     return OvfKey{z ? 0 : r.cv, r.v0, r.v1, r.meta, site_rank_of(a, r.site)};
 }
 
@@ -129,12 +156,12 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b) {
 #define OVF_LOOP(i, N) for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (N); i += gridDim.x * blockDim.x)
 
 static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
-    OVF_LOOP(r, d.K) {
+    OVF_LOOP(r, d.Kb) {
         const uint32_t b = ovf_bucket_of(d, r);
-        BucketView v;
-        bucket_view(a, a.ovf_list[b], v);
-        const Rec x = load_rec(v.at(r - d.koff[b]));
-        d.pb[r] = b;  // (buckets stay contiguous after the sort: also the bucket of position r)
+        const uint32_t si = a.stage_off[a.ovf_list[b]] + (r - d.koff[b]);
+        const Rec x = load_rec(a.stage + si);
+        d.pb[r] = b;
+        d.src[r] = si;
         d.pk[r] = x.pk;
         d.cv[r] = x.cv;
         d.tc[r] = x.tcid;
@@ -145,7 +172,7 @@ static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
 
 static __global__ void k_ovf_rowhash(OvfDev d) {
     const uint32_t lane = threadIdx.x & 63;
-    OVF_LOOP(r, d.K) {
+    OVF_LOOP(r, d.Kb) {
         const uint32_t b = d.pb[r];
         const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
         uint32_t S = 1;
@@ -188,29 +215,84 @@ static __global__ void k_ovf_rowhash(OvfDev d) {
         if (todo) owner = probe();
         d.rowid[r] = owner;  // (scratch until the sort)
         d.recf[r] = owner == r - kb ? 1u : 0u;
-        d.val[r] = r - kb;
+        d.val[r] = r;
     }
 }
 
-// Sort keys: rows numbered densely (inclusive scan of the owner flags, in epc) and positions
-// compacted (prior rows first, then the batch in application order), so the radix sort goes
-// through log2(rows) + log2(prior + batch) bits instead of 32 + 32.
+// Each row (its owner record, dense id from the scan of owner flags in epc) looked up in its region:
+// prior records counted, new rows counted per bucket (the host checks the region and heap have
+// room before anything is written). The removed prior records leave the live count here; the walk
+// adds what it writes back.
+static __global__ void k_ovf_lookup(MergeArgs a, OvfDev d) {
+    OVF_LOOP(r, d.Kb) {
+        if (!d.recf[r]) continue;
+        const uint32_t row = d.epc[r] - 1u;
+        const uint32_t b = d.pb[r], t = d.tc[r] >> 16;
+        d.rowner[row] = r;
+        d.rb[row] = b;
+        const uint32_t e = rs_lookup(a.rs, a.ovf_list[b], d.pk[r], t);
+        if (e == ROW_NONE) {
+            d.rheap[row] = ROW_NONE;
+            d.rprior[row] = 0;
+            d.rbits[2 * row] = d.rbits[2 * row + 1] = 0;
+            atomicAdd(&d.bnew[b], 1u);
+            atomicAdd(&d.bnrec[b], (uint32_t)a.rs.stride[t]);
+        } else {
+            const RowEnt re = a.rs.ent[e];
+            const uint32_t pc = row_popc(re.bits);
+            d.rheap[row] = re.heap;
+            d.rprior[row] = pc;
+            d.rbits[2 * row] = re.bits[0];
+            d.rbits[2 * row + 1] = re.bits[1];
+            atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)(-(long long)pc));
+        }
+    }
+}
+
+// prior records of every found row appended at [Kb + rpoff[row] - pc, Kb + rpoff[row]) (rpoff:
+// inclusive scan of the rows' prior counts)
+static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
+    OVF_LOOP(row, d.nrows) {
+        const uint32_t pc = d.rprior[row];
+        if (!pc) continue;
+        const uint32_t hb = d.rheap[row], own = d.rowner[row];
+        uint32_t r = d.Kb + d.rpoff[row] - pc;
+        for (int w = 0; w < 2; w++)
+            for (uint64_t m = d.rbits[2 * row + w]; m; m &= m - 1) {
+                const uint32_t c = 64 * w + (uint32_t)__ffsll((unsigned long long)m) - 1;
+                const Rec pr = load_rec(a.rs.heap + hb + c);
+                d.pk[r] = d.pk[own];
+                d.cv[r] = pr.cv;
+                d.tc[r] = pr.tcid;
+                d.cl[r] = pr.cl;
+                d.pkey[r - d.Kb] = OvfKey{pr.cv, pr.v0, pr.v1, pr.meta, site_rank_of(a, pr.site)};
+                d.pos[r] = c;  // compact position < pm: before the batch
+                d.src[r] = hb + c;
+                d.key[r] = ((uint64_t)row << d.rshift) | c;
+                d.val[r] = r;
+                r++;
+            }
+    }
+}
+
+// Sort keys of the batch records: rows numbered densely (inclusive scan of the owner flags, in epc)
+// and positions compacted (prior slots [0, pm), then the batch in application order), so the radix
+// sort goes through log2(rows) + log2(pm + batch) bits instead of 32 + 32.
 static __global__ void k_ovf_rowkey(OvfDev d) {
-    OVF_LOOP(r, d.K) {
+    OVF_LOOP(r, d.Kb) {
         const uint32_t kb = d.koff[d.pb[r]];
         const uint64_t row = d.epc[kb + d.rowid[r]] - 1u;
         const uint32_t pos = d.pos[r];
-        const uint64_t cp = (pos & BATCH_POS) ? (uint64_t)d.pm + (pos & 0x7FFFFFFFu) : (uint64_t)pos;
-        d.key[r] = (row << d.rshift) | cp;
+        d.key[r] = (row << d.rshift) | ((uint64_t)d.pm + (pos & 0x7FFFFFFFu));
     }
 }
 
 static __global__ void k_ovf_gather(OvfDev d) {
     OVF_LOOP(p, d.K) {
         const uint32_t row = (uint32_t)(d.key_s[p] >> d.rshift);
-        const uint32_t b = d.pb[p];
         d.rowid[p] = row;
-        d.cl_s[p] = d.cl[d.koff[b] + d.val_s[p]];
+        d.pb[p] = d.rb[row];
+        d.cl_s[p] = d.cl[d.val_s[p]];
         d.head[p] = 0;
         d.fstg[p] = 0;
         if (p == 0 || (uint32_t)(d.key_s[p - 1] >> d.rshift) != row) {
@@ -223,7 +305,7 @@ static __global__ void k_ovf_gather(OvfDev d) {
 
 static __global__ void k_ovf_classify(MergeArgs a, OvfDev d) {
     OVF_LOOP(p, d.K) {
-        const uint32_t x = d.koff[d.pb[p]] + d.val_s[p];
+        const uint32_t x = d.val_s[p];
         const uint32_t cl = d.cl_s[p], L = d.lx[p], cid = d.tc[x] & 0xFFFFu, pos = d.pos[x];
         const uint32_t kd = cl > L ? 1u : ((cl == L && cid != 0 && (cl & 1u)) ? 2u : 0u);
         d.kind[p] = kd;
@@ -253,7 +335,7 @@ static __global__ void k_ovf_ckeys(OvfDev d) {
         uint64_t k = ~0ULL;
         if (d.kind[p] == 2) {  // a candidate always follows its row's first record
             const uint32_t R = d.recs[d.rstart[d.rowid[p]] + d.epc[p] - 1];
-            const uint32_t cid = d.tc[d.koff[d.pb[p]] + d.val_s[p]] & cmask;
+            const uint32_t cid = d.tc[d.val_s[p]] & cmask;
             k = ((uint64_t)R << d.cid_bits) | cid;
         }
         d.ckey[p] = k;
@@ -355,12 +437,45 @@ struct WalkCells<false> {
     }
 };
 
-// clock rows of one walked row (rf_emit on the carried cells)
+// The row's heap slot: its prior one, or a fresh one for a new row (the host made room), and its
+// region entry: looked up for a row that existed before the apply, inserted for a new one
+// (k_ovf_lookup told them apart; rowstore.h says why the two never interfere). Returns the entry.
+__device__ inline uint32_t ovf_row_slot(const MergeArgs &a, const OvfDev &d, uint32_t row, uint32_t &hb) {
+    const uint32_t bb = a.ovf_list[d.rb[row]], own = d.rowner[row], t = d.tc[own] >> 16;
+    hb = d.rheap[row];
+    if (hb != ROW_NONE) return rs_lookup(a.rs, bb, d.pk[own], t);
+    hb = (uint32_t)atomicAdd(a.rs.heap_top, (unsigned long long)a.rs.stride[t]);
+    const uint64_t z[2] = {0, 0};
+    return rs_insert(a.rs, bb, d.pk[own], t, hb, z);
+}
+
+__device__ inline void ovf_publish(const MergeArgs &a, const OvfDev &d, uint32_t row, uint32_t e,
+                                   const uint64_t bits[2], uint32_t cnt, bool hs) {
+    a.rs.ent[e].bits[0] = bits[0];
+    a.rs.ent[e].bits[1] = bits[1];
+    atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)cnt);
+    if (hs) a.rs.gen[a.ovf_list[d.rb[row]]] = 1;
+}
+
+// emitter of the sequential fold when it runs here (rows outside App. A.3)
+struct OvfEmit {
+    const OvfDev *d;
+    __device__ inline void emit(const MergeArgs &a, const OvfView &v, const GenArrays &g, uint32_t s, uint32_t row,
+                                uint32_t ncell, bool hs, int64_t scv, uint32_t ssrc) {
+        if (d->rheap[row] == ROW_NONE && !hs && ncell == 0) return;
+        uint32_t hb;
+        const uint32_t e = ovf_row_slot(a, *d, row, hb);
+        uint64_t bits[2];
+        const uint32_t cnt = heap_write_row(a, v, g, s, ncell, hs, scv, ssrc, hb, bits);
+        ovf_publish(a, *d, row, e, bits, cnt, hs);
+    }
+};
+
+// clock rows of one walked row (rf_emit on the carried cells) into its heap slot
 template <bool REG>
-__device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b, const BucketView &v,
-                                const WalkCells<REG> &cells_, uint32_t ncell, uint32_t rpos) {
-    const uint32_t kb = d.koff[b];
-    const uint32_t xr = kb + d.val_s[rpos];
+__device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t row, const WalkCells<REG> &cells_,
+                                uint32_t ncell, uint32_t rpos) {
+    const uint32_t xr = d.val_s[rpos];
     const uint32_t clr = d.cl[xr], cidr = d.tc[xr] & 0xFFFFu;
     const bool hs = !(cidr != 0 && clr == 1 && d.lx[rpos] == 0);
     const int64_t scv = cidr == 0 ? d.cv[xr] : (int64_t)clr;
@@ -368,13 +483,12 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b,
     const bool cells = (clr & 1u) != 0;
     const uint32_t cnt = (hs ? 1u : 0u) + (cells ? ncell : 0u);
     if (cnt == 0) return;
-    const uint32_t bb = a.ovf_list[b];
-    Rec *outb = a.out + a.out_off[bb];
-    uint64_t *outts = a.out_ts ? a.out_ts + a.out_off[bb] : nullptr;
-    uint32_t k = atomicAdd(&d.ocnt[b], cnt);
-    if (hs || rowcl != 1) atomicOr(&d.oflag[b], 1u);
+    uint32_t hb;
+    const uint32_t e = ovf_row_slot(a, d, row, hb);
+    const OvfView v{&a, &d};
+    uint64_t bits[2] = {0, 0};
     if (hs) {
-        Rec r = load_rec(v.at(d.val_s[rpos]));
+        Rec r = load_rec(ovf_rec(a, d, xr));
         const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
         r.tcid &= 0xFFFF0000u;
         r.cv = scv;
@@ -382,51 +496,49 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t b,
         r.v0 = 0;
         r.v1 = 0;
         r.meta = CORRO_NULL;
-        r.pos = k;
-        store_rec(outb + k, r);
-        if (a.track_ts) outts[k] = ts;
-        k++;
+        r.pos = hb;
+        store_rec(a.rs.heap + hb, r);
+        if (a.track_ts) a.rs.heap_ts[hb] = ts;
+        bits[0] |= 1ULL;
     }
-    if (!cells) return;
-    for (uint32_t c = 0; c < ncell; c++) {
-        Rec r = load_rec(v.at(d.val_s[cells_.pos(c)]));
-        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
-        if (cells_.z(c)) r.cv = 0;
-        r.cl = (uint32_t)rowcl;
-        r.pos = k;
-        store_rec(outb + k, r);
-        if (a.track_ts) outts[k] = ts;
-        k++;
+    if (cells) {
+        for (uint32_t c = 0; c < ncell; c++) {
+            Rec r = load_rec(ovf_rec(a, d, d.val_s[cells_.pos(c)]));
+            const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+            const uint32_t cid = r.tcid & 0xFFFFu;
+            if (cells_.z(c)) r.cv = 0;
+            r.cl = (uint32_t)rowcl;
+            r.pos = hb + cid;
+            store_rec(a.rs.heap + hb + cid, r);
+            if (a.track_ts) a.rs.heap_ts[hb + cid] = ts;
+            bits[cid >> 6] |= 1ULL << (cid & 63);
+        }
     }
+    ovf_publish(a, d, row, e, bits, cnt, hs);
 }
 
 template <bool REG>
 static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
     OVF_LOOP(row, d.nrows) {  // one thread per row (dense ids), every lane busy
         const uint32_t j0 = d.rstart[row];
-        const uint32_t b = d.pb[j0];
-        const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
-        BucketView v;
-        bucket_view(a, a.ovf_list[b], v);
-        if (d.rbad[row]) {  // outside App. A.3: the sequential fold on this bucket's views
-            GenArrays g;
-            g.key = d.key_s + kb;
-            g.val = d.val_s + kb;
-            g.pk = d.pk + kb;
-            g.cv = d.cv + kb;
-            g.tc = d.tc + kb;
-            g.cl = d.cl + kb;
-            g.pos = d.pos + kb;
-            g.ccid = d.ccid + kb;
-            g.csrc = d.csrc + kb;
-            g.ccv = d.ccv + kb;
+        if (d.rbad[row]) {  // outside App. A.3: the sequential fold over the row's sorted records
+            GenArrays g{};
+            g.key = d.key_s;
+            g.val = d.val_s;
+            g.pk = d.pk;
+            g.cv = d.cv;
+            g.tc = d.tc;
+            g.cl = d.cl;
+            g.pos = d.pos;
+            g.ccid = d.ccid;
+            g.csrc = d.csrc;
+            g.ccv = d.ccv;
             g.own = nullptr;
             g.slots = 0;
             g.rshift = d.rshift;
-            g.P = n;
-            const uint32_t bb = a.ovf_list[b];
-            gen_fold_row(a, v, a.out + a.out_off[bb], a.out_ts ? a.out_ts + a.out_off[bb] : nullptr, &d.ocnt[b],
-                         &d.oflag[b], g, j0 - kb, n);
+            g.P = d.K;
+            OvfEmit em{&d};
+            gen_fold_row(a, OvfView{&a, &d}, em, g, j0, d.K);
             continue;
         }
         const uint32_t nrec = d.rnrec[row];
@@ -437,13 +549,13 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
         uint32_t k0 = 0;
         if (!a.impact)
             for (uint32_t k = nrec; k-- > 0;)
-                if ((d.cl[kb + d.val_s[d.recs[j0 + k]]] & 1u) == 0) {
+                if ((d.cl[d.val_s[d.recs[j0 + k]]] & 1u) == 0) {
                     k0 = k;
                     break;
                 }
         for (uint32_t k = k0; k < nrec; k++) {
             const uint32_t R = d.recs[j0 + k];
-            const uint32_t xR = kb + d.val_s[R];
+            const uint32_t xR = d.val_s[R];
             if ((d.cl[xR] & 1u) == 0) {
                 ncell = 0;
                 continue;
@@ -471,7 +583,7 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
                 if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(a, d, fp, fz != 0)) > 0) set(cid, d.cval_s[wq], 0);
             }
         }
-        if (nrec) ovf_emit<REG>(a, d, b, v, cs, ncell, d.recs[j0 + nrec - 1]);
+        if (nrec) ovf_emit<REG>(a, d, row, cs, ncell, d.recs[j0 + nrec - 1]);
     }
 }
 
@@ -480,7 +592,7 @@ static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
         const uint64_t k = d.ckey_s[q];
         if (d.rbad[d.rowid[(uint32_t)(k >> d.cid_bits)]]) continue;
         const uint32_t p = d.cval_s[q];
-        const uint32_t pos = d.pos[d.koff[d.pb[p]] + d.val_s[p]];
+        const uint32_t pos = d.pos[d.val_s[p]];
         if (!(pos & BATCH_POS)) continue;
         const bool first = q == 0 || d.ckey_s[q - 1] != k;
         const OvfKey kq = ovf_key_q(d, q);
@@ -492,12 +604,7 @@ static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
 }
 
 static __global__ void k_ovf_finish(MergeArgs a, OvfDev d) {
-    OVF_LOOP(b, d.G) {
-        const uint32_t bb = a.ovf_list[b];
-        a.out_cnt[bb] = d.ocnt[b];
-        a.out_flags[bb] = d.oflag[b];
-        atomicAdd(&a.misc[2], (unsigned long long)d.ocnt[b]);
-    }
+    OVF_LOOP(b, d.G) a.rs.used[a.ovf_list[b]] += d.bnew[b];
 }
 
 // Running argmax of the candidates by group (cbest): a segmented scan with the 32-B keys compared

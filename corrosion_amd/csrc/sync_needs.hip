@@ -215,7 +215,20 @@ __device__ inline void walk_entry(const corro_needs_out &o, const EntryHdr &h, c
         }
         nn++;
     };
-    for (uint64_t k = h.one0; k < h.one1; k++) sweep(vh, iv.ons[k], iv.one[k], 1, head, full);
+    for (uint64_t k = h.one0; k < h.one1; k++) {
+        const uint64_t s = iv.ons[k], t = iv.one[k];
+        if (s > t) {
+            // an inverted (empty) range, which no RangeInclusiveSet holds but a peer's message may:
+            // rangemap's overlapping(s..=t) yields every stored range with end >= s and start <= t,
+            // i.e. a have range spanning [t, s], and the reference then pushes Full(s..=t) as is
+            if (t >= 1 && s <= head) {
+                uint64_t dummy;
+                if (!vh.covering(t, dummy) && vh.next_start(t) > s) full(s, t);
+            }
+            continue;
+        }
+        sweep(vh, s, t, 1, head, full);
+    }
 
     for (uint64_t k = h.ope0; k < h.ope1; k++) {
         const uint64_t v = iv.opv[k];

@@ -37,8 +37,10 @@ def _int_dtype_ok(t, dt):
 
 
 class MergeEngine:
-    def __init__(self, schema, capacity_hint=1 << 20, device=0):
-        """schema: {table_name: [column names]} in table order (cid k = column k-1, cid 0 = '-1')."""
+    def __init__(self, schema, capacity_hint=1 << 20, device=0, interned=()):
+        """schema: {table_name: [column names]} in table order (cid k = column k-1, cid 0 = '-1').
+        interned: tables whose primary key is not one INTEGER column (BLOB / TEXT / composite pks):
+        their rows are keyed by corro_pk_keys' interned ids of the packed pk bytes."""
         lib = L.lib()
         self.schema = list(schema.items())
         descs = (L.TableDesc * max(1, len(self.schema)))()
@@ -53,6 +55,9 @@ class MergeEngine:
         L.check(lib.corro_ctx_create(descs, len(self.schema), capacity_hint, device, C.byref(h)))
         self._h = h
         self.device = device
+        self.interned = set()
+        for name in interned:
+            self.set_pk_interned(name)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -86,6 +91,50 @@ class MergeEngine:
         c = C.c_uint32()
         L.check(L.lib().corro_site_count(self._h, C.byref(c)))
         return c.value
+
+    # ---- primary keys ---------------------------------------------------------------------
+    def table_index(self, table):
+        if isinstance(table, int):
+            return table
+        for i, (name, _cols) in enumerate(self.schema):
+            if name == table:
+                return i
+        raise L.CorroError(-4, f"no such table: {table}")
+
+    def set_pk_interned(self, table, on=True):
+        t = self.table_index(table)
+        L.check(L.lib().corro_table_set_pk_interned(self._h, t, 1 if on else 0))
+        name = self.schema[t][0]
+        (self.interned.add if on else self.interned.discard)(name)
+
+    def pk_keys(self, table, packed):
+        """Row keys of packed pks (a list of bytes, pack_columns encoding) of one table."""
+        t = self.table_index(table)
+        lens = np.array([len(b) for b in packed], np.uint64)
+        off = np.zeros(len(packed) + 1, np.uint64)
+        off[1:] = np.cumsum(lens)
+        buf = np.frombuffer(b"".join(bytes(b) for b in packed) or b"\0", np.uint8)
+        keys = np.zeros(max(1, len(packed)), np.uint64)
+        L.check(L.lib().corro_pk_keys(self._h, t, buf.ctypes.data, off.ctypes.data, len(packed), keys.ctypes.data))
+        return keys[:len(packed)]
+
+    def pk_bytes(self, table, keys):
+        """Canonical packed pk bytes of row keys of one table."""
+        t = self.table_index(table)
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        n = len(keys)
+        off = np.zeros(n + 1, np.uint64)
+        cap = 64 * n + 64
+        while True:
+            buf = np.zeros(cap, np.uint8)
+            rc = L.lib().corro_pk_bytes(self._h, t, keys.ctypes.data, n, buf.ctypes.data, cap, off.ctypes.data)
+            if rc == 0:
+                break
+            if rc != -6 or int(off[n]) <= cap:
+                L.check(rc)
+            cap = int(off[n])
+        raw = buf.tobytes()
+        return [raw[int(off[i]):int(off[i + 1])] for i in range(n)]
 
     # ---- merge ------------------------------------------------------------------------------
     def apply(self, batch, impact=False):

@@ -153,7 +153,10 @@ def rows_to_changes(engine, site_ids, rows, lo, hi):
         tc = int(rows["table_cid"][k])
         t, cid = tc >> 16, tc & 0xFFFF
         name, cols = engine.schema[t]
-        out.append(Change(table=name, pk=int(rows["pk"][k]), cid="-1" if cid == 0 else cols[cid - 1],
+        pk = int(rows["pk"][k])
+        if name in engine.interned:  # the canonical packed pk of the row (cr-sqlite's t__crsql_pks)
+            pk = engine.pk_bytes(t, [pk])[0]
+        out.append(Change(table=name, pk=pk, cid="-1" if cid == 0 else cols[cid - 1],
                           val=_decode_value(rows["val_type"][k], rows["val0"][k], rows["val1"][k], rows["val_len"][k]),
                           col_version=int(rows["col_version"][k]), db_version=int(rows["db_version"][k]),
                           seq=int(rows["seq"][k]), site_id=site_ids[int(rows["site"][k])], cl=int(rows["cl"][k])))

@@ -66,8 +66,9 @@ typedef struct {
  * order, changes in vector order (util.rs:705,765,782,1222). Required arrays: pk, table_cid,
  * col_version, db_version, cl, seq, site, val0. Optional (NULL): val1, val_type, val_len, ts.
  *
- *   pk          row key: the table's single INTEGER pk value, or a host-interned key of the
- *               packed pk bytes (pubsub.rs:2304-2358), like cr-sqlite's `__crsql_key`
+ *   pk          row key: the table's single INTEGER pk value, or for an interned table the key
+ *               corro_pk_keys gives its packed pk bytes (pubsub.rs:2304-2358), like cr-sqlite's
+ *               `__crsql_key`
  *   table_cid   (table_index << 16) | cid, cid 0 = sentinel "-1"
  *   cl          causal length (< 2^32); sentinel changes and even-cl changes need
  *               0 <= col_version < 2^32 (their col_version becomes the row's causal length)
@@ -140,6 +141,26 @@ int corro_site_register(corro_ctx *ctx, const uint8_t *site_ids, uint64_t n, uin
 int corro_site_count(corro_ctx *ctx, uint32_t *count);
 /* The registered 16-byte site ids by ordinal (at most cap written; *count = all). */
 int corro_site_ids(corro_ctx *ctx, uint8_t *ids, uint32_t cap, uint32_t *count);
+
+/* ------------------------------------------------------------------ primary keys */
+
+/* A Change's pk is pack_columns bytes (corro-types/src/pubsub.rs:2304-2358). A table whose primary
+ * key is one INTEGER column keys its rows by that integer (the default). Any other table (a BLOB,
+ * TEXT, REAL or composite primary key -- corro-tests' testsblob and wide, corro-tests/src/lib.rs:13-53)
+ * is marked interned before its first change: its rows are keyed by a dense id per table, handed out
+ * in first-seen order for the CANONICAL packed bytes (unpacked and re-packed as pack_columns packs,
+ * so non-canonical encodings of one key name one row, as cr-sqlite's __crsql_key does). */
+int corro_table_set_pk_interned(corro_ctx *ctx, uint32_t table, int interned);
+/* The canonical form of one packed pk (no context, no device): unpack_columns then pack_columns. */
+int corro_pk_canonical(const uint8_t *bytes, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *out_len);
+/* n packed pks of `table` -> row keys (the corro_changes.pk values): pk i = bytes[off[i], off[i+1]).
+ * CORRO_E_INVALID for a malformed encoding, CORRO_E_RANGE for a non-INTEGER pk of a table not interned. */
+int corro_pk_keys(corro_ctx *ctx, uint32_t table, const uint8_t *bytes, const uint64_t *off, uint64_t n,
+                  uint64_t *keys);
+/* Row keys of `table` -> canonical packed pk bytes (export, extraction): key i's bytes at
+ * [out_off[i], out_off[i+1]); out_off holds n + 1 entries; CORRO_E_RANGE if cap < out_off[n]. */
+int corro_pk_bytes(corro_ctx *ctx, uint32_t table, const uint64_t *keys, uint64_t n, uint8_t *bytes, uint64_t cap,
+                   uint64_t *out_off);
 
 /* ------------------------------------------------------------------ merge */
 

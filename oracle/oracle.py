@@ -257,6 +257,57 @@ def needs(entries):
     return res
 
 
+def needs_parallel(entries, nthreads=16, chunk=1 << 20):
+    """needs() over entry chunks on `nthreads` host threads (the C fold releases the GIL): the CSR
+    offsets stay absolute, so a chunk is the per-entry arrays offset by its first entry."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(entries["their_head"])
+    keep = {k: np.ascontiguousarray(entries[k], dtype=np.uint64) for k in SYNC_KEYS_U64}
+    keep["our_head"] = np.ascontiguousarray(entries["our_head"], dtype=np.int64)
+    per_entry = ("their_head", "our_head", "tn_off", "tp_off", "on_off", "op_off")
+    nc = np.zeros(max(n, 1), np.uint64)
+    sc = np.zeros(max(n, 1), np.uint64)
+
+    def run(a, b, fill, res=None):
+        s = _SyncEntries()
+        s.n = b - a
+        for k in SYNC_KEYS_U64 + ("our_head",):
+            arr = keep[k]
+            off = a * arr.itemsize if k in per_entry else 0
+            setattr(s, k, arr.ctypes.data + off if arr.size else None)
+        o = _NeedsOut()
+        o.need_count = nc.ctypes.data + 8 * a
+        o.seq_count = sc.ctypes.data + 8 * a
+        if fill:
+            for k in ("kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+                setattr(o, k, res[k].ctypes.data)
+            o.need_off = res["need_off"].ctypes.data + 8 * a
+            o.seq_off = res["seq_off"].ctypes.data + 8 * a
+        lib().of_needs(C.byref(s), C.byref(o), 1 if fill else 0)
+
+    spans = [(a, min(n, a + chunk)) for a in range(0, n, chunk)]
+    with ThreadPoolExecutor(nthreads) as ex:
+        list(ex.map(lambda ab: run(ab[0], ab[1], False), spans))
+    nc, sc = nc[:n], sc[:n]
+    need_off = np.zeros(n + 1, np.uint64)
+    seq_off = np.zeros(n + 1, np.uint64)
+    need_off[1:] = np.cumsum(nc)
+    seq_off[1:] = np.cumsum(sc)
+    T, Ts = int(need_off[-1]), int(seq_off[-1])
+    res = {"need_off": need_off, "seq_off": seq_off,
+           "kind": np.zeros(max(T, 1), np.uint8), "start": np.zeros(max(T, 1), np.uint64),
+           "end": np.zeros(max(T, 1), np.uint64), "sr_off": np.zeros(max(T, 1), np.uint64),
+           "sr_n": np.zeros(max(T, 1), np.uint64), "s_start": np.zeros(max(Ts, 1), np.uint64),
+           "s_end": np.zeros(max(Ts, 1), np.uint64)}
+    with ThreadPoolExecutor(nthreads) as ex:
+        list(ex.map(lambda ab: run(ab[0], ab[1], True, res), spans))
+    for k in ("kind", "start", "end", "sr_off", "sr_n"):
+        res[k] = res[k][:T]
+    for k in ("s_start", "s_end"):
+        res[k] = res[k][:Ts]
+    return res
+
+
 class Booked:
     """BookedVersions gap bookkeeping (agent.rs:1108-1235, :1353-1362)."""
 

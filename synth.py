@@ -181,8 +181,10 @@ def sync_entries_torch(npairs, actors_per_pair, seed, device="cuda", max_head=1_
             z = torch.zeros(0, dtype=i64, device=device)
             return off, z, z
         ent = torch.repeat_interleave(torch.arange(E, device=device), cnt)
-        gap = torch.empty(R, device=device).geometric_(1.0 / gap_mean, generator=g).to(i64) + 1
-        ln = torch.empty(R, device=device).geometric_(1.0 / len_mean, generator=g).to(i64)
+        # (a float geometric sample can round to 0: clamp, so ranges are non-empty and non-adjacent as
+        # generate_sync's RangeInclusiveSet gives them)
+        gap = torch.empty(R, device=device).geometric_(1.0 / gap_mean, generator=g).to(i64).clamp(min=1) + 1
+        ln = torch.empty(R, device=device).geometric_(1.0 / len_mean, generator=g).to(i64).clamp(min=1)
         step = gap + ln
         cs = torch.cumsum(step, 0)
         first = off[:-1][ent]

@@ -61,3 +61,26 @@ def kat_expect(expect):
         else:
             out.append(("partial", x[1], [tuple(r) for r in x[2]]))
     return out
+
+
+def pairs_from_cases(cases):
+    """tests/golden/sync_inverted_cases.json entries -> (our, their) pairs for entries_from_pairs."""
+    pairs = []
+    for c in cases:
+        x = c["in"]
+        our = {"head": None if x["our_head"] < 0 else x["our_head"], "need": x["our_need"],
+               "partials": {str(v): r for v, r in x["our_partials"]}}
+        their = {"head": x["their_head"], "need": x["their_need"],
+                 "partials": {str(v): r for v, r in x["their_partials"]}}
+        pairs.append((our, their))
+    return pairs
+
+
+def expected_from_cases(cases):
+    out = []
+    for c in cases:
+        lst = []
+        for kind, s, e, seqs in c["oracle"]:
+            lst.append(("full", s, e) if kind == 0 else ("partial", s, [tuple(r) for r in seqs]))
+        out.append(lst)
+    return out

@@ -92,3 +92,31 @@ def test_booked_matches_oracle_random():
             assert p.last() == o.max()
             for v in range(1, 70):
                 assert p.contains_version(v) == o.contains(v)
+
+
+def _canon(b):
+    import ctypes as C
+    out = (C.c_uint8 * 256)()
+    n = C.c_uint64()
+    rc = L.lib().corro_pk_canonical(bytes(b), len(b), out, 256, C.byref(n))
+    return None if rc else bytes(out[:n.value])
+
+
+def test_pk_canonical_form():
+    """pack_columns / unpack_columns (pubsub.rs:2304-2451) round trip, quirks included: integers in the
+    fewest bytes num_bytes_needed_i64 gives (0 -> no bytes, negatives -> 8), TEXT/BLOB length in
+    num_bytes_needed_i32 bytes; a non-canonical encoding of one key canonicalises to the same bytes."""
+    assert _canon(b"\x01\x09\x01") == b"\x01\x09\x01"                      # Integer(1)
+    assert _canon(b"\x01\x01") == b"\x01\x01"                              # Integer(0): no int bytes
+    assert _canon(b"\x01\x21\x00\x00\x00\x01") == b"\x01\x09\x01"          # 1 in 4 bytes -> 1 byte
+    assert _canon(b"\x01\x11\x01\x00") == b"\x01\x11\x01\x00"              # Integer(256): 2 bytes
+    assert _canon(b"\x01\x09\xff") == b"\x01\x41" + b"\xff" * 8            # get_int sign-extends: -1 -> 8 bytes
+    assert _canon(b"\x01\x0b\x02ab") == b"\x01\x0b\x02ab"                  # Text("ab")
+    blob16 = bytes(range(16))
+    assert _canon(b"\x01\x0c\x10" + blob16) == b"\x01\x0c\x10" + blob16    # Blob(16 bytes)
+    comp = b"\x02\x0c\x08" + b"\x00" * 7 + b"\x05" + b"\x0b\x01" + b"5"      # (Blob(be 5), Text("5")): wide's pk
+    assert _canon(comp) == comp
+    assert _canon(b"\x01\x02" + b"\x80" + b"\x00" * 7) == b"\x01\x02" + b"\x00" * 8  # REAL -0.0 == 0.0
+    assert _canon(b"\x01\x05") == b"\x01\x05"                              # NULL
+    assert _canon(b"\x01\x0b\x05ab") is None                               # length past the end
+    assert _canon(b"\x01\x07") is None                                     # no such column type

@@ -396,3 +396,59 @@ def test_chunked_apply_validates_before_the_first_chunk(monkeypatch):
     assert ex.value.code == -5
     assert rows_to_tuples(e.export(), with_ts=True) == before
     assert list(e.db_versions()) == dv
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_fast_path_folds_into_prior_state(wide):
+    """cl=1 batches applied one after another into a growing state (the in-place row store): every
+    cell's prior clock is compared with the batch winner, impacts count the prior as the earliest
+    member of the cell; alternating impact / no-impact applies, INTEGER and mixed value classes."""
+    seed = 81
+    sites = synth.site_ids(16, seed)
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=40000, sites=sites)
+    f = O.Fold(sites)
+    for k in range(6):
+        b = synth.uniform_batch(40000, 16, 6000, 4, seed + k)
+        if wide and k % 3 == 2:  # some TEXT / REAL values (the mixed-class fast bodies)
+            rng = np.random.default_rng(seed + k)
+            m = rng.random(len(b["pk"])) < 0.3
+            b["val_type"] = np.where(m, np.uint8(3), np.uint8(1)).astype(np.uint8)
+            b["val_len"] = np.where(m, np.uint8(5), np.uint8(0)).astype(np.uint8)
+            b["val1"] = np.zeros(len(b["pk"]), np.uint64)
+            # 5-byte TEXT: big-endian bytes in val0, zero padded
+            b["val0"] = np.where(m, b["val0"] & np.uint64(0xFFFFFFFFFF000000), b["val0"]).astype(np.uint64)
+        if k % 2:
+            assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+        else:
+            e.apply(b)
+            f.apply(b)
+        compare(e, f)
+
+
+def test_store_growth_defers_and_regrows():
+    """A state far larger than the capacity hint: buckets whose region or the heap cannot take their
+    new rows defer before writing, the row store grows, the deferred buckets merge again --
+    bit-exact rows and impacts (fast bodies, chunked applies)."""
+    seed = 83
+    sites = synth.site_ids(16, seed)
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=1 << 16, sites=sites)
+    f = O.Fold(sites)
+    b = synth.uniform_batch(150000, 16, 30000, 4, seed)
+    assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+    compare(e, f)
+    b = synth.uniform_batch(150000, 16, 90000, 4, seed + 1)
+    e.apply(b)
+    f.apply(b)
+    compare(e, f)
+
+
+def test_general_path_grows_regions():
+    """The same growth through the general and overflow bodies (sentinels, Zipf-hot rows)."""
+    seed = 84
+    sites = synth.site_ids(8, seed)
+    e = engine(synth.adversarial_schema(2), cap=1 << 12, sites=sites)
+    f = O.Fold(sites)
+    for k in range(3):
+        b = synth.adversarial_batch(60000, 8, 2, 20000, seed + k, zipf=0.6)
+        assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+        compare(e, f, with_ts=True)

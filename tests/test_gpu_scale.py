@@ -1,0 +1,92 @@
+"""Full-size parity (the north-star criterion and BASELINE's stated sizes), in the GPU suite:
+
+  * config 3: 2^29 = 536,870,912 column changes (pk space 2^25, 1000 actors, 4 INTEGER columns,
+    cl = 1), merged on one MI355X as ONE batch, and as 8 consecutive 2^26 batches folded into one
+    state (each batch into the state the previous ones left: the in-place row store), checked against
+    the oracle's pk-sharded fold (oracle/crsql_fold.c of_apply_sharded, the sequential rules run per
+    shard on the host cores): every impact flag, the crsql_changes rows through an order-independent
+    digest of every output field (row count, sum and xor of per-row 64-bit hashes), crsql_db_versions;
+  * config 4: 1M node pairs x 64 sparse actors from a 100k-actor universe (64M need-diff entries),
+    the device need diff against the oracle restatement (oracle/ranges.c, threaded over entry
+    chunks), every output array equal.
+The oracle is the checker only."""
+import time
+
+import numpy as np
+import pytest
+
+import synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N3, PK3, ACT = 1 << 29, 1 << 25, 1000
+
+
+def _host(b):
+    hb = {k: v.cpu().numpy() for k, v in b.items()}
+    for k in ("table_cid", "cl", "seq", "site"):
+        hb[k] = hb[k].view(np.uint32)
+    for k in ("pk", "val0"):
+        hb[k] = hb[k].view(np.uint64)
+    return hb
+
+
+def _config3(batches):
+    import torch
+    import corrosion_amd as ca
+    sites = synth.site_ids(ACT, 1)
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=N3 // batches, device=0)
+    eng.register_sites(sites)
+    fold = O.ShardedFold(sites, nshards=64, nthreads=16)
+    per = N3 // batches
+    t_gpu = []
+    for k in range(batches):
+        b = synth.uniform_batch_torch(per, ACT, PK3, 4, seed=synth.config_seed(3) + k, device="cuda")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        imp = eng.apply(b, impact=True)
+        torch.cuda.synchronize()
+        t_gpu.append(time.perf_counter() - t0)
+        imp = imp.cpu().numpy()
+        hb = _host(b)
+        del b
+        torch.cuda.empty_cache()
+        ref = fold.apply(hb)
+        assert np.array_equal(imp, ref), f"batch {k}: impact flags differ"
+        del hb, imp, ref
+    rows = eng.export()
+    dg = O.rows_digest(rows)
+    del rows
+    assert dg == fold.digest()
+    assert np.array_equal(eng.db_versions(), fold.db_versions())
+    print(f"config 3, {batches} batch(es): {dg[0]} clock rows bit-exact; GPU apply s per batch "
+          + ", ".join(f"{t:.3f}" for t in t_gpu))
+    eng.close()
+
+
+def test_config3_512m_one_batch_vs_sharded_oracle():
+    _config3(1)
+
+
+def test_config3_512m_eight_batch_fold_vs_sharded_oracle():
+    _config3(8)
+
+
+def test_config4_full_size_vs_oracle():
+    import torch
+    import corrosion_amd as ca
+    from corrosion_amd.sync import _needs_device
+    ent = synth.sync_entries_torch(1_000_000, 64, synth.config_seed(4), device="cuda")
+    e = ca.MergeEngine({"t": ["a"]}, capacity_hint=1024)
+    got = _needs_device(e, ent)
+    host = {k: v.cpu().numpy() for k, v in ent.items()}
+    del ent
+    torch.cuda.empty_cache()
+    exp = O.needs_parallel(host, nthreads=16)
+    assert len(host["their_head"]) == 64_000_000
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        g = got[k].cpu().numpy() if hasattr(got[k], "cpu") else got[k]
+        assert np.array_equal(g.view(exp[k].dtype) if g.dtype != exp[k].dtype and g.itemsize == exp[k].itemsize
+                              else g, exp[k]), k
+    e.close()

@@ -199,3 +199,12 @@ def test_sync_1pass_capacity_error_reports_totals():
     exp = O.needs(ent)
     assert tot[0] == int(exp["need_off"][-1]) and tot[1] == int(exp["seq_off"][-1])
     assert bool((guard == 7).all())
+
+
+def test_inverted_our_need_ranges_vs_fixture():
+    """The three config-4 entries (found at full size) whose our-need list holds an inverted range."""
+    from tests.sync_util import expected_from_cases, pairs_from_cases
+    cases = load_golden("sync_inverted_cases.json")["cases"]
+    e = _engine()
+    got = decode_needs(e.compute_needs(entries_from_pairs(pairs_from_cases(cases))), len(cases))
+    assert got == expected_from_cases(cases)

@@ -108,3 +108,26 @@ def test_rows_digest_detects_a_single_field_change():
         r2 = {kk: vv.copy() for kk, vv in rows.items()}
         r2[k][17] ^= 1
         assert O.rows_digest(r2) != d0, k
+
+
+def test_needs_parallel_equals_needs():
+    """The threaded chunked need diff (the full-size config-4 checker) equals the single pass."""
+    from tests.sync_util import entries_from_pairs
+    from tests.test_gpu_sync import random_side
+    rng = np.random.default_rng(17)
+    pairs = [(random_side(rng, with_head=rng.random() < 0.9), random_side(rng)) for _ in range(3000)]
+    ent = entries_from_pairs(pairs)
+    a = O.needs(ent)
+    b = O.needs_parallel(ent, nthreads=4, chunk=257)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_inverted_our_need_ranges_fixture():
+    """Entries whose our-need list holds an inverted (empty) range, as a peer's message could:
+    the oracle keeps rangemap's overlapping() semantics (a have range spanning [t, s] yields
+    Full(s..=t)); the fixture pins that output for the GPU test."""
+    from tests.sync_util import decode_needs, entries_from_pairs, expected_from_cases, pairs_from_cases
+    cases = load_golden("sync_inverted_cases.json")["cases"]
+    ent = entries_from_pairs(pairs_from_cases(cases))
+    assert decode_needs(O.needs(ent), len(cases)) == expected_from_cases(cases)
