@@ -95,18 +95,28 @@ def _ours(kernel_name):
     return kernel_name.startswith("k_") or "corro" in kernel_name or "rocprim" in kernel_name
 
 
+def _short_kernel(name):
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
+    name = name.replace("void ", "").replace("corro::", "")
+    return "rocprim" if "rocprim" in name else name
+
+
 def _read_counter(dirname, counter):
+    """(total, {kernel: total}) of one counter over the pipeline's kernels, or None."""
     import csv
     import glob
     files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         return None
-    tot = 0.0
+    tot, per = 0.0, {}
     for f in files:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") == counter and _ours(r.get("Kernel_Name", "")):
-                tot += float(r["Counter_Value"])
-    return tot
+                v = float(r["Counter_Value"])
+                tot += v
+                k = _short_kernel(r["Kernel_Name"])
+                per[k] = per.get(k, 0.0) + v
+    return tot, per
 
 
 def pmc_traffic_live(changes, applies=3, timeout=240):
@@ -119,9 +129,9 @@ def pmc_traffic_live(changes, applies=3, timeout=240):
     import tempfile
     rp = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
     if not rp:
-        return None, "rocprofv3 not found"
+        return None, "rocprofv3 not found", None
     tmp = os.environ.get("TMPDIR") or "/tmp"
-    got = {}
+    got, per = {}, {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="corro_pmc_", dir=tmp)
         cmd = ["timeout", "-k", "10", "-s", "KILL", str(timeout), rp, "--pmc", counter, "--output-format", "csv",
@@ -130,14 +140,17 @@ def pmc_traffic_live(changes, applies=3, timeout=240):
         try:
             r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout + 30)
         except subprocess.TimeoutExpired:
-            return None, f"rocprofv3 --pmc {counter} timed out"
+            return None, f"rocprofv3 --pmc {counter} timed out", None
         v = _read_counter(d, counter)
         shutil.rmtree(d, ignore_errors=True)
         if r.returncode != 0 or v is None:
-            return None, f"rocprofv3 --pmc {counter} rc={r.returncode}: {r.stderr.decode(errors='replace')[-300:]}"
-        got[counter] = v / applies
+            return None, f"rocprofv3 --pmc {counter} rc={r.returncode}: {r.stderr.decode(errors='replace')[-300:]}", None
+        got[counter] = v[0] / applies
+        scale = (2.0 if counter == "FETCH_SIZE" else 1.0) * 1024.0 / applies
+        for k, x in v[1].items():
+            per.setdefault(k, {"fetch": 0.0, "write": 0.0})["fetch" if counter == "FETCH_SIZE" else "write"] = x * scale
     return (2 * got["FETCH_SIZE"] + got["WRITE_SIZE"]) * 1024.0, \
-        f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes run by bench.py on itself ({applies} applies each)"
+        f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes run by bench.py on itself ({applies} applies each)", per
 
 
 # ----------------------------------------------------------------------------------- self-launch
@@ -184,17 +197,17 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
 
-    traffic, traffic_note = None, "not measured (--no-pmc)"
+    traffic, traffic_note, traffic_kern = None, "not measured (--no-pmc)", None
     if world == 1 and not args.pmc_child and not args.no_pmc and rank == 0:
-        traffic, traffic_note = pmc_traffic_live(args.changes or N_CHANGES)
+        traffic, traffic_note, traffic_kern = pmc_traffic_live(args.changes or N_CHANGES)
 
     if world == 1:
-        run_single(args, traffic, traffic_note)
+        run_single(args, traffic, traffic_note, traffic_kern)
     else:
         run_multi(args, world, rank)
 
 
-def run_single(args, traffic, traffic_note):
+def run_single(args, traffic, traffic_note, traffic_kern=None):
     import torch
     import synth
     import corrosion_amd as ca
@@ -257,6 +270,8 @@ def run_single(args, traffic, traffic_note):
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_note,
                      "traffic_ratio": (traffic / alg_bytes) if traffic else None,
+                     "traffic_by_kernel": ({k: {"fetch": round(v["fetch"]), "write": round(v["write"])}
+                                            for k, v in sorted(traffic_kern.items())} if traffic_kern else None),
                      "alg_bytes_per_apply": alg_bytes, "pipeline_ms": pipe_ms, "kernels_ms": kern,
                      "dominant": max(kern, key=kern.get)},
         "cpu_baseline": cpu,

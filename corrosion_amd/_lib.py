@@ -23,7 +23,7 @@ EXPORTS = [
     "corro_last_error", "corro_abi_version", "corro_device_count", "corro_ctx_create",
     "corro_ctx_destroy", "corro_lookup_cid", "corro_site_register", "corro_site_count",
     "corro_apply_batch", "corro_state_count", "corro_state_export", "corro_state_reset",
-    "corro_db_versions", "corro_compute_needs", "corro_booked_new", "corro_booked_free",
+    "corro_db_versions", "corro_value_bytes", "corro_compute_needs", "corro_booked_new", "corro_booked_free",
     "corro_booked_insert_db", "corro_booked_needed", "corro_booked_last", "corro_booked_contains",
     "corro_booked_contains_all", "corro_ctx_set_profiling", "corro_last_timings",
     "corro_bookie_new", "corro_bookie_free", "corro_process_multiple_changes",
@@ -34,12 +34,13 @@ EXPORTS = [
     "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
     "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
-    "corro_pk_canonical",
+    "corro_pk_canonical", "corro_bookie_buffered_value",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
 KNOWN = {0: "skipped", 1: "current", 2: "cleared", 3: "partial"}
 CORRO_TCID_UNKNOWN = 0xFFFFFFFF
+CORRO_VAL_LONG = 255  # val_len of a TEXT/BLOB value longer than 16 bytes
 
 
 class CorroError(RuntimeError):
@@ -55,7 +56,7 @@ class TableDesc(C.Structure):
 class Changes(C.Structure):
     _fields_ = [("n", C.c_uint64)] + [(k, C.c_void_p) for k in (
         "pk", "table_cid", "col_version", "db_version", "cl", "seq", "site", "val0", "val1",
-        "val_type", "val_len", "ts")]
+        "val_type", "val_len", "ts", "val_off", "val_size", "val_data")] + [("val_data_len", C.c_uint64)]
 
 
 class ApplyOut(C.Structure):
@@ -148,6 +149,7 @@ def lib():
     sig = {
         "corro_last_error": (C.c_char_p, []),
         "corro_abi_version": (i32, []),
+        "corro_value_bytes": (i32, [vp, vp, u64, vp, u64, vp]),
         "corro_device_count": (i32, [vp]),
         "corro_ctx_create": (i32, [vp, u32, u64, i32, vp]),
         "corro_ctx_destroy": (None, [vp]),
@@ -168,6 +170,7 @@ def lib():
         "corro_decode_frames": (i32, [vp, C.c_char_p, u64, i32, i32, C.POINTER(Decoded), i32]),
         "corro_bookie_buffered_versions": (i32, [vp, vp, u64, u64, vp, u64, vp]),
         "corro_bookie_buffered": (i32, [vp, vp, u64, u64, u64, C.POINTER(Rows), u64, vp]),
+        "corro_bookie_buffered_value": (i32, [vp, vp, u64, u64, vp, u64, vp]),
         "corro_extract_changes": (i32, [vp, C.POINTER(ExtractIn), i32, C.POINTER(ExtractOut), i32]),
         "corro_booked_new": (i32, [vp]),
         "corro_booked_free": (None, [vp]),

@@ -57,8 +57,17 @@ class ChangeV1:
     changeset: object
 
 
+def value_bytes(v):
+    """The bytes of a TEXT/BLOB SqliteValue (None for other classes)."""
+    if v is None or isinstance(v, (bool, int, float)):
+        return None
+    return v.encode() if isinstance(v, str) else bytes(v)
+
+
 def encode_value(v):
-    """SqliteValue -> (type, val0, val1, len) of the engine's fixed-width value encoding."""
+    """SqliteValue -> (type, val0, val1, len) of the engine's fixed-width value encoding. A TEXT/BLOB
+    longer than 16 bytes gives len = CORRO_VAL_LONG and its first 8 bytes in val0: its bytes travel in
+    the batch's val_data (value_bytes)."""
     if v is None:
         return L_NULL, 0, 0, 0
     if isinstance(v, bool) or isinstance(v, int):
@@ -69,7 +78,9 @@ def encode_value(v):
         return 2, struct.unpack("<Q", struct.pack("<d", v))[0], 0, 0
     b = v.encode() if isinstance(v, str) else bytes(v)
     if len(b) > 16:
-        raise L.CorroError(-6, "TEXT/BLOB values longer than 16 bytes are outside the engine encoding")
+        if len(b) >= 1 << 24:
+            raise L.CorroError(-6, "TEXT/BLOB values of 16 MiB or more are outside the engine encoding")
+        return (3 if isinstance(v, str) else 4), int.from_bytes(b[:8], "big"), 0, L.CORRO_VAL_LONG
     p = b + b"\0" * (16 - len(b))
     return (3 if isinstance(v, str) else 4), int.from_bytes(p[:8], "big"), int.from_bytes(p[8:], "big"), len(b)
 
@@ -210,6 +221,8 @@ class Agent:
             ("cl", np.uint32), ("seq", np.uint32), ("site", np.uint32), ("val0", np.uint64),
             ("val1", np.uint64), ("val_type", np.uint8), ("val_len", np.uint8))}
         arr["pk"][:n] = self.row_keys(rows)
+        voff, vsz, data = np.zeros(max(1, n), np.uint64), np.zeros(max(1, n), np.uint32), []
+        dlen = 0
         for j, ch in enumerate(rows):
             try:
                 tc = self.engine.lookup(ch.table, ch.cid)
@@ -223,11 +236,19 @@ class Agent:
             arr["seq"][j] = ch.seq
             arr["site"][j] = self.site(ch.site_id)
             arr["val0"][j], arr["val1"][j], arr["val_type"][j], arr["val_len"][j] = v0, v1, t, ln
+            if ln == L.CORRO_VAL_LONG:
+                b = value_bytes(ch.val)
+                voff[j], vsz[j] = dlen, len(b)
+                data.append(b)
+                dlen += len(b)
         s = L.Changes()
         s.n = n
         for k, a in arr.items():
             setattr(s, k, a.ctypes.data)
         s.ts = None
+        if data:
+            blob = np.frombuffer(b"".join(data), np.uint8)
+            s.val_off, s.val_size, s.val_data, s.val_data_len = voff.ctypes.data, vsz.ctypes.data, blob.ctypes.data, dlen
         known = np.zeros(max(1, ncs), np.int32)
         imp = np.zeros(max(1, n), np.uint8)
         out = L.ProcessOut()

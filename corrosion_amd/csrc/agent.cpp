@@ -40,7 +40,10 @@ struct HostRow {  // one buffered change (__corro_buffered_changes row)
     int64_t cv, dbv;
     uint32_t tcid, cl, seq, site;
     uint8_t vt, vl;
+    std::string lv;  // a long TEXT/BLOB value's bytes (vl == CORRO_VAL_LONG)
 };
+
+bool is_long(uint8_t vt, uint8_t vl) { return vl == CORRO_VAL_LONG && (vt == CORRO_TEXT || vt == CORRO_BLOB); }
 
 struct SeqBook {  // __corro_seq_bookkeeping rows of one (site, version)
     std::vector<Range> ranges;
@@ -66,14 +69,22 @@ ActorId actor_of(const uint8_t *p) {
 }
 
 struct Batch {  // application-order SoA assembled on the host
-    std::vector<uint64_t> pk, v0, v1, ts;
+    std::vector<uint64_t> pk, v0, v1, ts, voff;
     std::vector<int64_t> cv, dbv;
-    std::vector<uint32_t> tcid, cl, seq, site;
+    std::vector<uint32_t> tcid, cl, seq, site, vsz;
     std::vector<uint8_t> vt, vl;
+    std::string data;  // long values' bytes
+    bool any_long = false;
     void push(const HostRow &r) {
         pk.push_back(r.pk); v0.push_back(r.v0); v1.push_back(r.v1); ts.push_back(r.ts);
         cv.push_back(r.cv); dbv.push_back(r.dbv); tcid.push_back(r.tcid); cl.push_back(r.cl);
         seq.push_back(r.seq); site.push_back(r.site); vt.push_back(r.vt); vl.push_back(r.vl);
+        voff.push_back(data.size());
+        vsz.push_back((uint32_t)r.lv.size());
+        if (is_long(r.vt, r.vl)) {
+            data += r.lv;
+            any_long = true;
+        }
     }
     size_t size() const { return pk.size(); }
     corro_changes view() const {
@@ -82,6 +93,12 @@ struct Batch {  // application-order SoA assembled on the host
         c.pk = pk.data(); c.table_cid = tcid.data(); c.col_version = cv.data(); c.db_version = dbv.data();
         c.cl = cl.data(); c.seq = seq.data(); c.site = site.data(); c.val0 = v0.data(); c.val1 = v1.data();
         c.val_type = vt.data(); c.val_len = vl.data(); c.ts = ts.data();
+        if (any_long) {
+            c.val_off = voff.data();
+            c.val_size = vsz.data();
+            c.val_data = reinterpret_cast<const uint8_t *>(data.data());
+            c.val_data_len = data.size();
+        }
         return c;
     }
 };
@@ -100,6 +117,10 @@ HostRow row_at(const corro_changes *in, uint64_t i, uint64_t ts) {
     r.vt = in->val_type ? in->val_type[i] : (uint8_t)CORRO_INTEGER;
     r.vl = in->val_len ? in->val_len[i] : 0;
     r.ts = in->ts ? in->ts[i] : ts;
+    // a long value whose span is malformed is passed on as it is (empty): the apply rejects it
+    if (is_long(r.vt, r.vl) && in->val_off && in->val_size && in->val_data && in->val_size[i] > 16 &&
+        in->val_off[i] <= in->val_data_len && in->val_size[i] <= in->val_data_len - in->val_off[i])
+        r.lv.assign(reinterpret_cast<const char *>(in->val_data + in->val_off[i]), in->val_size[i]);
     return r;
 }
 
@@ -515,6 +536,23 @@ int corro_bookie_buffered(corro_bookie *bk, const uint8_t *actor_id, uint64_t ve
         if (o->val_len) o->val_len[k] = h.vl;
     }
     *count = k;
+    return CORRO_OK;
+}
+
+// bytes of a buffered long value (the row of (actor, version, seq)); *len = its length (0: none)
+int corro_bookie_buffered_value(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t seq,
+                                uint8_t *out, uint64_t cap, uint64_t *len) {
+    if (!bk || !actor_id || !len || (cap && !out)) return fail(CORRO_E_INVALID, "NULL argument");
+    *len = 0;
+    auto so = bk->site_of.find(actor_of(actor_id));
+    if (so == bk->site_of.end() || seq > 0xFFFFFFFFULL) return CORRO_OK;
+    auto it = bk->buffered.find({so->second, (int64_t)version});
+    if (it == bk->buffered.end()) return CORRO_OK;
+    auto r = it->second.find((uint32_t)seq);
+    if (r == it->second.end()) return CORRO_OK;
+    const std::string &lv = r->second.lv;
+    *len = lv.size();
+    std::memcpy(out, lv.data(), std::min<uint64_t>(cap, lv.size()));
     return CORRO_OK;
 }
 

@@ -114,6 +114,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     d.Kb = (uint32_t)Kb;
     d.cid_bits = cid_bits;
     d.pm = pm;
+    d.arena = a.arena;
     uint64_t bytes = 0;
     uint8_t *base = nullptr;
     auto take = [&](uint64_t n) {
@@ -337,6 +338,7 @@ static int store_clear(corro_ctx *ctx) {
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_heap_top.p, 0, 8, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     ctx->state_total = 0;
+    ctx->arena_top = 0;
     ctx->state_epoch++;
     return CORRO_OK;
 }
@@ -355,6 +357,23 @@ RowStore row_store(corro_ctx *ctx) {
     rs.fill = (uint32_t)((7ULL << ctx->log2S) >> 3);
     rs.stride = ctx->d_stride.as<uint16_t>();
     return rs;
+}
+
+// Room for `add` more bytes in the value arena (contents kept: handles are offsets into it).
+static constexpr uint64_t ARENA_MAX = 1ULL << 40;  // a value handle holds a 40-bit offset
+static int arena_reserve(corro_ctx *ctx, uint64_t add) {
+    const uint64_t need = ctx->arena_top + add;
+    if (need > ARENA_MAX) return fail(CORRO_E_RANGE, "value arena would exceed 2^40 bytes");
+    if (need <= ctx->d_arena.bytes && ctx->d_arena.p) return CORRO_OK;
+    DevBuf nb;
+    TRY(nb.ensure(std::max<uint64_t>(need + (need >> 1), 1ULL << 20)));
+    if (ctx->arena_top)
+        CORRO_HIP_TRY(hipMemcpyAsync(nb.p, ctx->d_arena.p, ctx->arena_top, hipMemcpyDeviceToDevice, ctx->stream));
+    CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->d_arena.release();
+    ctx->d_arena = nb;
+    nb.p = nullptr;
+    return CORRO_OK;
 }
 
 // Regions rehashed to 2^new_log2S slots (between merge rounds / before an overflow walk: no apply
@@ -497,7 +516,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
-                      &ctx->d_ncols, &ctx->d_part};
+                      &ctx->d_ncols, &ctx->d_part, &ctx->d_arena};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     for (auto &e : ctx->ev)
@@ -592,10 +611,12 @@ static int stage_host_batch(corro_ctx *ctx, const corro_changes *in, BatchDev &b
     const uint64_t n = in->n;
     struct F { const void *src; size_t elem; const void **dst; };
     const void *pk = nullptr, *tc = nullptr, *cv = nullptr, *dbv = nullptr, *cl = nullptr, *seq = nullptr,
-               *site = nullptr, *v0 = nullptr, *v1 = nullptr, *vt = nullptr, *vl = nullptr, *ts = nullptr;
+               *site = nullptr, *v0 = nullptr, *v1 = nullptr, *vt = nullptr, *vl = nullptr, *ts = nullptr,
+               *voff = nullptr, *vsz = nullptr;
     F f[] = {{in->pk, 8, &pk},   {in->col_version, 8, &cv}, {in->db_version, 8, &dbv}, {in->val0, 8, &v0},
              {in->val1, 8, &v1}, {in->ts, 8, &ts},          {in->table_cid, 4, &tc},   {in->cl, 4, &cl},
-             {in->seq, 4, &seq}, {in->site, 4, &site},      {in->val_type, 1, &vt},    {in->val_len, 1, &vl}};
+             {in->seq, 4, &seq}, {in->site, 4, &site},      {in->val_type, 1, &vt},    {in->val_len, 1, &vl},
+             {in->val_off, 8, &voff}, {in->val_size, 4, &vsz}};
     size_t total = 0;
     for (auto &x : f)
         if (x.src) total += ((n * x.elem + 255) / 256) * 256;
@@ -620,6 +641,8 @@ static int stage_host_batch(corro_ctx *ctx, const corro_changes *in, BatchDev &b
     bd.vt = (const uint8_t *)vt;
     bd.vl = (const uint8_t *)vl;
     bd.ts = (const uint64_t *)ts;
+    bd.voff = (const uint64_t *)voff;
+    bd.vsz = (const uint32_t *)vsz;
     return CORRO_OK;
 }
 
@@ -721,6 +744,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     a.force_general = force_general ? 1u : 0u;
     a.track_ts = ctx->track_ts ? 1u : 0u;
     a.state_wide = ctx->state_wide ? 1u : 0u;
+    a.arena = ctx->d_arena.as<uint8_t>();
     uint32_t nblocks = B;
     float merge_ms = 0.f, ovf_ms = 0.f;
     for (int round = 0;; round++) {
@@ -848,8 +872,25 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
         bd.vt = in->val_type;
         bd.vl = in->val_len;
         bd.ts = in->ts;
+        bd.voff = in->val_off;
+        bd.vsz = in->val_size;
     }
     bd.n = n;
+    // long values: the batch's value bytes are appended to the arena once; every chunk's changes
+    // name their bytes relative to that base. A failed batch leaves them unreferenced.
+    if (in->val_off) {
+        if (!in->val_size || !in->val_type || !in->val_len || (in->val_data_len && !in->val_data))
+            return fail(CORRO_E_INVALID, "long values need val_size, val_type, val_len and val_data");
+        TRY(arena_reserve(ctx, in->val_data_len));
+        if (in->val_data_len)
+            CORRO_HIP_TRY(hipMemcpyAsync(ctx->d_arena.as<uint8_t>() + ctx->arena_top, in->val_data, in->val_data_len,
+                                         mem == CORRO_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
+        bd.arena = ctx->d_arena.as<uint8_t>();
+        bd.lbase = ctx->arena_top;
+        bd.ldata = in->val_data_len;
+        // (claimed before the first chunk: a chunk that commits may reference them)
+        ctx->arena_top = (ctx->arena_top + in->val_data_len + 7) & ~7ULL;
+    }
     // impact output: a device batch gets its flags written straight into the caller's device
     // buffer; a host batch through a device staging buffer + one copy
     const bool imp_dev = out && out->impact && mem == CORRO_MEM_DEVICE;
@@ -875,7 +916,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
             if (p) p += off;
         };
         adv(c.pk), adv(c.tcid), adv(c.cv), adv(c.dbv), adv(c.cl), adv(c.seq), adv(c.site), adv(c.v0), adv(c.v1);
-        adv(c.vt), adv(c.vl), adv(c.ts);
+        adv(c.vt), adv(c.vl), adv(c.ts), adv(c.voff), adv(c.vsz);
         c.n = m;
         TRY(apply_chunk(ctx, c, imp_buf ? imp_buf + off : nullptr));
         for (int k = 0; k < 6; k++) ms[k] += ctx->last_ms[k];
@@ -1023,6 +1064,47 @@ int corro_state_export(corro_ctx *ctx, corro_rows *o, uint64_t cap, uint64_t *wr
         if (c.dst) CORRO_HIP_TRY(hipMemcpyAsync(c.dst, c.src, m * c.elem, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     *written = m;
+    return CORRO_OK;
+}
+
+}  // extern "C"
+
+// value i's bytes (handle = offset << 24 | length) to out + off[i]: one workgroup per value
+static __global__ void k_gather_values(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ handles,
+                                       const uint64_t *__restrict__ off, uint64_t n, uint8_t *__restrict__ out) {
+    for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint64_t h = handles[i], src = h >> 24, len = h & 0xFFFFFFu, dst = off[i];
+        for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) out[dst + k] = arena[src + k];
+    }
+}
+
+extern "C" {
+
+int corro_value_bytes(corro_ctx *ctx, const uint64_t *handles, uint64_t n, uint8_t *bytes, uint64_t cap,
+                      uint64_t *out_off) {
+    if (!ctx || !out_off || (n && !handles) || (cap && !bytes)) return fail(CORRO_E_INVALID, "NULL argument");
+    out_off[0] = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t src = handles[i] >> 24, len = handles[i] & 0xFFFFFFu;
+        if (src + len > ctx->arena_top) return fail(CORRO_E_INVALID, "value handle outside the value arena");
+        out_off[i + 1] = out_off[i] + len;
+    }
+    const uint64_t total = out_off[n];
+    if (total > cap) return fail(CORRO_E_RANGE, "value bytes exceed cap");
+    if (total == 0) return CORRO_OK;
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    DevBuf &tmp = ctx->d_export;  // (scratch shared with corro_state_export)
+    TRY(tmp.ensure(16 * n + total + 256));
+    uint64_t *dh = tmp.as<uint64_t>(), *doff = dh + n;
+    uint8_t *dout = reinterpret_cast<uint8_t *>(doff + n);
+    CORRO_HIP_TRY(hipMemcpyAsync(dh, handles, 8 * n, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(doff, out_off, 8 * n, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_gather_values, dim3((uint32_t)std::min<uint64_t>(n, 4096)), dim3(256), 0, s,
+                       ctx->d_arena.as<uint8_t>(), dh, doff, n, dout);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipMemcpyAsync(bytes, dout, total, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;
 }
 

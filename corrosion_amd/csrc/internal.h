@@ -120,6 +120,8 @@ struct corro_ctx {
     bool state_wide = false;      // some clock row holds a non-INTEGER value
     corro::DevBuf d_defer, d_relist;  // deferred buckets of a merge round, the re-merge list
     corro::DevBuf d_dense, d_dense_ts, d_dense_view;  // materialised state (extraction), its pseudo-buckets
+    corro::DevBuf d_arena;        // long TEXT/BLOB value bytes (append-only; handles point into it)
+    uint64_t arena_top = 0;       // bytes in use
     uint64_t dense_epoch = ~0ULL;
 
     // per-batch scratch

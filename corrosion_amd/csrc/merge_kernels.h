@@ -57,6 +57,7 @@ struct MergeArgs {
     uint32_t force_general;    // route every non-empty bucket through the sequential general body
     uint32_t track_ts;
     uint32_t state_wide;       // the state holds non-INTEGER values
+    const uint8_t *arena;      // bytes of long TEXT/BLOB values (value handles point into it)
 };
 
 // misc words
@@ -92,34 +93,63 @@ __device__ inline uint64_t vkey0(uint32_t type, uint64_t v0) {
     }
 }
 
-// >0: a greater, <0: b greater, 0: equal
-__device__ inline int value_cmp(const Rec &a, const Rec &b) {
-    uint32_t ta = vtype(a.meta), tb = vtype(b.meta);
-    if (ta != tb) return (5 - (int)ta) > (5 - (int)tb) ? 1 : -1;
-    if (ta == CORRO_NULL) return 0;
-    uint64_t ka = vkey0(ta, a.v0), kb = vkey0(tb, b.v0);
-    if (ka != kb) return ka > kb ? 1 : -1;
-    if (ta == CORRO_TEXT || ta == CORRO_BLOB) {
-        if (a.v1 != b.v1) return a.v1 > b.v1 ? 1 : -1;
-        uint32_t la = vlen(a.meta), lb = vlen(b.meta);
-        if (la != lb) return la > lb ? 1 : -1;
+// A TEXT/BLOB value longer than 16 bytes (length field CORRO_VAL_LONG) keeps bytes 0..7 big-endian
+// in word 0 and a handle in word 1: (arena offset << 24) | byte length; its bytes live in the
+// value arena. Values of up to 16 bytes stay inline (words 0/1), so a long value is never equal to
+// an inline one.
+constexpr uint32_t VLEN_LONG = 255;
+__device__ inline bool is_long(uint32_t meta) { return vlen(meta) == VLEN_LONG; }
+__device__ inline uint64_t text_len(uint32_t meta, uint64_t w1) { return is_long(meta) ? (w1 & 0xFFFFFFu) : vlen(meta); }
+// byte k >= 8 of a TEXT/BLOB value (k < its length)
+__device__ inline uint32_t text_byte(uint32_t meta, uint64_t w1, const uint8_t *arena, uint64_t k) {
+    return is_long(meta) ? (uint32_t)arena[(w1 >> 24) + k] : (uint32_t)(w1 >> (8 * (15 - k))) & 0xFFu;
+}
+// TEXT/BLOB order past equal first words when either value is long: memcmp of bytes 8.. over the
+// common length, then the longer is greater (SQLite's BINARY collation / blob compare)
+__device__ __noinline__ int long_tail_cmp(uint32_t ma, uint64_t a1, uint32_t mb, uint64_t b1, const uint8_t *arena) {
+    const uint64_t la = text_len(ma, a1), lb = text_len(mb, b1), n = la < lb ? la : lb;
+    for (uint64_t k = 8; k < n; k++) {
+        const uint32_t x = text_byte(ma, a1, arena, k), y = text_byte(mb, b1, arena, k);
+        if (x != y) return x > y ? 1 : -1;
     }
-    return 0;
+    return la > lb ? 1 : (la < lb ? -1 : 0);
 }
 
-// value_cmp on loose fields (type|len meta, word 0, word 1)
-__device__ inline int value_cmp_f(uint32_t ma, uint64_t a0, uint64_t a1, uint32_t mb, uint64_t b0, uint64_t b1) {
+// value order on loose fields (type|len meta, word 0, word 1): >0: a greater, <0: b greater, 0: equal
+__device__ inline int value_cmp_f(uint32_t ma, uint64_t a0, uint64_t a1, uint32_t mb, uint64_t b0, uint64_t b1,
+                                  const uint8_t *arena) {
     const uint32_t ta = vtype(ma), tb = vtype(mb);
     if (ta != tb) return (5 - (int)ta) > (5 - (int)tb) ? 1 : -1;
     if (ta == CORRO_NULL) return 0;
     const uint64_t ka = vkey0(ta, a0), kb = vkey0(tb, b0);
     if (ka != kb) return ka > kb ? 1 : -1;
     if (ta == CORRO_TEXT || ta == CORRO_BLOB) {
+        if (is_long(ma) || is_long(mb)) return long_tail_cmp(ma, a1, mb, b1, arena);
         if (a1 != b1) return a1 > b1 ? 1 : -1;
         const uint32_t la = vlen(ma), lb = vlen(mb);
         if (la != lb) return la > lb ? 1 : -1;
     }
     return 0;
+}
+
+__device__ inline int value_cmp(const Rec &a, const Rec &b, const uint8_t *arena) {
+    return value_cmp_f(a.meta, a.v0, a.v1, b.meta, b.v0, b.v1, arena);
+}
+
+// A long value of change i (length field VLEN_LONG): validates its span and returns word 0 (bytes
+// 0..7 big-endian) and word 1 (the handle of its bytes in the arena). False = malformed.
+__device__ inline bool long_value(const BatchDev &in, uint32_t i, uint64_t &w0, uint64_t &w1) {
+    if (!in.voff || !in.vsz || !in.arena) return false;
+    const uint64_t off = in.voff[i];
+    const uint32_t sz = in.vsz[i];
+    if (sz <= 16 || sz >= (1u << 24) || off > in.ldata || sz > in.ldata - off) return false;
+    const uint8_t *p = in.arena + in.lbase + off;
+    uint64_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) w = (w << 8) | p[k];
+    w0 = w;
+    w1 = ((in.lbase + off) << 24) | sz;
+    return true;
 }
 
 __device__ inline uint32_t site_rank_of(const MergeArgs &a, uint32_t site) {
@@ -436,15 +466,18 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
         for (int u = 0; u < SCAT_U; u++) {
             const uint32_t i = base + (u / 2) * 2 * blockDim.x + 2 * threadIdx.x + (u & 1);
             const bool act = i < end;
-            const Rec &r = rr[u];
+            Rec &r = rr[u];
             uint32_t idx = 0;
             if (act) {
                 const uint32_t ty = vtype(r.meta), ln = vlen(r.meta);
                 const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
                 const uint32_t b = bucket_of(one_table ? 0u : t, r.pk, log2B);
                 idx = atomicAdd(&cur[b], 1u);
+                // long values: words from the arena; their buckets take the general body
+                const bool lv = !PLAIN && (ty == CORRO_TEXT || ty == CORRO_BLOB) && ln == VLEN_LONG;
+                if (lv && !long_value(in, i, r.v0, r.v1)) err |= ERR_VALUE;
                 // (the fast bodies keep a row's presence bits in one word: cids 1..63)
-                if (r.cl != 1u || cid == 0 || cid >= 64) atomicOr(&fl[b >> 5], 1u << (b & 31));
+                if (r.cl != 1u || cid == 0 || cid >= 64 || lv) atomicOr(&fl[b >> 5], 1u << (b & 31));
                 if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
                 if (r.site >= nsites) err |= ERR_SITE;
                 if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
@@ -453,7 +486,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                     wide = 1;
                     if (ty < 1 || ty > 5) err |= ERR_VALUE;
                     if (ty == CORRO_REAL && ((r.v0 >> 52) & 0x7FF) == 0x7FF && (r.v0 & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
-                    if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) err |= ERR_VALUE;
+                    if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16 && ln != VLEN_LONG) err |= ERR_VALUE;
                 }
             }
             store_rec_wave<NT>(stage, idx, r, act);
@@ -569,10 +602,13 @@ struct GenArrays {
 // Write a folded row into its heap slots: the sentinel clock (slot 0) and the cells (slot cid),
 // every one with the row's causal length; `bits` receives the presence bits. Each written slot's
 // source is the batch change that set it or the slot's own prior record, loaded before the store.
+// `general` is set when the row must keep fast bodies out of its region (it holds a sentinel clock
+// or a long value).
 template <class V>
 __device__ inline uint32_t heap_write_row(const MergeArgs &a, const V &v, const GenArrays &g, uint32_t s,
                                           uint32_t ncell, bool hs, int64_t scv, uint32_t ssrc, uint32_t hb,
-                                          uint64_t bits[2]) {
+                                          uint64_t bits[2], bool &general) {
+    general = hs;
     const int64_t L = hs ? scv : (ncell ? 1 : 0);
     bits[0] = bits[1] = 0;
     uint32_t cnt = 0;
@@ -608,6 +644,7 @@ __device__ inline uint32_t heap_write_row(const MergeArgs &a, const V &v, const 
             store_rec(a.rs.heap + hb + cid, r[u]);
             if (a.track_ts) a.rs.heap_ts[hb + cid] = ts;
             bits[cid >> 6] |= 1ULL << (cid & 63);
+            if (is_long(r[u].meta)) general = true;
             cnt++;
         }
     }
@@ -703,7 +740,7 @@ __device__ inline void gen_fold_row(const MergeArgs &a, const V &v, E &em, const
                 } else {
                     const Rec xr = load_rec(v.at(x));
                     const Rec lr = load_rec(v.at(g.csrc[s + found]));
-                    const int vc = value_cmp(xr, lr);
+                    const int vc = value_cmp(xr, lr, a.arena);
                     if (vc != 0) win = vc > 0;
                     else win = site_rank_of(a, xr.site) > site_rank_of(a, lr.site);
                 }
@@ -859,7 +896,8 @@ struct LdsEmit {
         const uint32_t hb = g.rheap[row], e = g.rent[row];
         if (e == ROW_NONE && !hs && ncell == 0) return;  // a new row the batch left empty (cl 0)
         uint64_t bits[2];
-        const uint32_t cnt = heap_write_row(a, v, g, s, ncell, hs, scv, ssrc, hb, bits);
+        bool gen;
+        const uint32_t cnt = heap_write_row(a, v, g, s, ncell, hs, scv, ssrc, hb, bits, gen);
         if (e == ROW_NONE) {
             rs_insert(a.rs, b, g.pk[row], g.tc[row] >> 16, hb, bits);
         } else {
@@ -867,7 +905,7 @@ struct LdsEmit {
             a.rs.ent[e].bits[1] = bits[1];
         }
         atomicAdd(emitted, cnt);
-        if (hs) *general = 1;
+        if (gen) *general = 1;
     }
 };
 
@@ -1250,7 +1288,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
                 Rec x = load_rec(v.fresh + i);
                 cmp = (int64_t)(cv[k] ^ 0x8000000000000000ULL) != pr.cv
                           ? ((int64_t)(cv[k] ^ 0x8000000000000000ULL) > pr.cv ? 1 : -1)
-                          : value_cmp(x, pr);
+                          : value_cmp(x, pr, a.arena);
                 if (cmp == 0) {
                     const uint32_t rk = (uint32_t)(rp[k] >> 32), prk = site_rank_of(a, pr.site);
                     cmp = rk != prk ? (rk > prk ? 1 : -1) : 0;
@@ -1387,7 +1425,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
         if ((s_v0[row[k]] >> c) & 1ULL) {
             const Rec pr = load_rec(a.rs.heap + hb[k]);
             const int64_t bcv = (int64_t)(cv[k] ^ 0x8000000000000000ULL);
-            int cmp = bcv != pr.cv ? (bcv > pr.cv ? 1 : -1) : value_cmp_f(meta[k], v0[k], v1[k], pr.meta, pr.v0, pr.v1);
+            int cmp = bcv != pr.cv ? (bcv > pr.cv ? 1 : -1) : value_cmp_f(meta[k], v0[k], v1[k], pr.meta, pr.v0, pr.v1, a.arena);
             if (cmp == 0) {
                 const uint32_t prk = site_rank_of(a, pr.site);
                 cmp = rank[k] != prk ? (rank[k] > prk ? 1 : -1) : 0;
@@ -1467,7 +1505,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
             if (cj != cv[k]) {
                 c = cj > cv[k] ? 1 : -1;
             } else {
-                c = value_cmp_f(s_meta[j], s_v0[j], s_v1[j], meta[k], v0[k], v1[k]);
+                c = value_cmp_f(s_meta[j], s_v0[j], s_v1[j], meta[k], v0[k], v1[k], a.arena);
                 if (c == 0) {
                     const uint32_t rj = s_tc[j];
                     c = rj != rank[k] ? (rj > rank[k] ? 1 : -1) : 0;
@@ -1839,7 +1877,10 @@ static __global__ void k_validate(BatchDev in, uint32_t nsites, const uint16_t *
                 const uint64_t v0 = in.v0[i];
                 if (ty < 1 || ty > 5) err |= ERR_VALUE;
                 if (ty == CORRO_REAL && ((v0 >> 52) & 0x7FF) == 0x7FF && (v0 & 0xFFFFFFFFFFFFFULL)) err |= ERR_VALUE;
-                if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) err |= ERR_VALUE;
+                if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln > 16) {
+                    uint64_t w0, w1;
+                    if (ln != VLEN_LONG || !long_value(in, i, w0, w1)) err |= ERR_VALUE;
+                }
             }
         }
     }

@@ -96,6 +96,7 @@ struct OvfDev {
     OvfKey *pkey;                // [K - Kb] the prior records' keys, read before the walk rewrites their slots
     uint32_t *slots;
     uint32_t *bnew, *bnrec;      // [G] new rows / their heap records per bucket
+    const uint8_t *arena;        // long value bytes (MergeArgs::arena)
 };
 
 // a record's 64-B source: the staged batch change or the prior heap record
@@ -145,9 +146,9 @@ __device__ inline OvfKey ovf_key_q(const OvfDev &d, uint32_t q) {
 }
 
 // >0: a greater
-__device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b) {
+__device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b, const uint8_t *arena) {
     if (a.cv != b.cv) return a.cv > b.cv ? 1 : -1;
-    const int vc = value_cmp_f(a.m, a.k0, a.k1, b.m, b.k0, b.k1);
+    const int vc = value_cmp_f(a.m, a.k0, a.k1, b.m, b.k0, b.k1, arena);
     if (vc != 0) return vc;
     if (a.sr != b.sr) return a.sr > b.sr ? 1 : -1;
     return 0;
@@ -449,12 +450,13 @@ __device__ inline uint32_t ovf_row_slot(const MergeArgs &a, const OvfDev &d, uin
     return rs_insert(a.rs, bb, d.pk[own], t, hb, z);
 }
 
+// general: the row holds a sentinel clock or a long value (fast bodies stay out of its region)
 __device__ inline void ovf_publish(const MergeArgs &a, const OvfDev &d, uint32_t row, uint32_t e,
-                                   const uint64_t bits[2], uint32_t cnt, bool hs) {
+                                   const uint64_t bits[2], uint32_t cnt, bool general) {
     a.rs.ent[e].bits[0] = bits[0];
     a.rs.ent[e].bits[1] = bits[1];
     atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)cnt);
-    if (hs) a.rs.gen[a.ovf_list[d.rb[row]]] = 1;
+    if (general) a.rs.gen[a.ovf_list[d.rb[row]]] = 1;
 }
 
 // emitter of the sequential fold when it runs here (rows outside App. A.3)
@@ -466,8 +468,9 @@ struct OvfEmit {
         uint32_t hb;
         const uint32_t e = ovf_row_slot(a, *d, row, hb);
         uint64_t bits[2];
-        const uint32_t cnt = heap_write_row(a, v, g, s, ncell, hs, scv, ssrc, hb, bits);
-        ovf_publish(a, *d, row, e, bits, cnt, hs);
+        bool gen;
+        const uint32_t cnt = heap_write_row(a, v, g, s, ncell, hs, scv, ssrc, hb, bits, gen);
+        ovf_publish(a, *d, row, e, bits, cnt, gen);
     }
 };
 
@@ -487,6 +490,7 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t ro
     const uint32_t e = ovf_row_slot(a, d, row, hb);
     const OvfView v{&a, &d};
     uint64_t bits[2] = {0, 0};
+    bool general = hs;
     if (hs) {
         Rec r = load_rec(ovf_rec(a, d, xr));
         const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
@@ -512,9 +516,10 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t ro
             store_rec(a.rs.heap + hb + cid, r);
             if (a.track_ts) a.rs.heap_ts[hb + cid] = ts;
             bits[cid >> 6] |= 1ULL << (cid & 63);
+            if (is_long(r.meta)) general = true;
         }
     }
-    ovf_publish(a, d, row, e, bits, cnt, hs);
+    ovf_publish(a, d, row, e, bits, cnt, general);
 }
 
 template <bool REG>
@@ -580,7 +585,7 @@ static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
                 const uint32_t fp = found < 0 ? 0u : cs.pos((uint32_t)found), fz = found < 0 ? 0u : cs.z((uint32_t)found);
                 d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((fp + 1) | (fz << 31));
                 const uint32_t wq = d.cbest[qe];
-                if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(a, d, fp, fz != 0)) > 0) set(cid, d.cval_s[wq], 0);
+                if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(a, d, fp, fz != 0), d.arena) > 0) set(cid, d.cval_s[wq], 0);
             }
         }
         if (nrec) ovf_emit<REG>(a, d, row, cs, ncell, d.recs[j0 + nrec - 1]);
@@ -596,9 +601,9 @@ static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
         if (!(pos & BATCH_POS)) continue;
         const bool first = q == 0 || d.ckey_s[q - 1] != k;
         const OvfKey kq = ovf_key_q(d, q);
-        bool imp = first || ovf_kcmp(kq, ovf_key_q(d, d.cbest[q - 1])) > 0;
+        bool imp = first || ovf_kcmp(kq, ovf_key_q(d, d.cbest[q - 1]), d.arena) > 0;
         const uint32_t fs = d.fstg[d.cgs[q]];
-        if (imp && fs) imp = ovf_kcmp(kq, ovf_key_p(a, d, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0)) > 0;
+        if (imp && fs) imp = ovf_kcmp(kq, ovf_key_p(a, d, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0), d.arena) > 0;
         a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
     }
 }
@@ -621,16 +626,17 @@ struct CsAgg {
 };
 
 // x precedes y; ~0u = none. The later one only when strictly greater (earliest on ties).
-__device__ inline uint32_t cs_pick(const OvfKey *qk, uint32_t x, uint32_t y) {
+__device__ inline uint32_t cs_pick(const OvfKey *qk, uint32_t x, uint32_t y, const uint8_t *arena) {
     if (x == ~0u) return y;
     if (y == ~0u) return x;
-    return ovf_kcmp(qk[y], qk[x]) > 0 ? y : x;
+    return ovf_kcmp(qk[y], qk[x], arena) > 0 ? y : x;
 }
 
 struct CsComb {
     const OvfKey *qk;
+    const uint8_t *arena;
     __device__ inline CsAgg operator()(const CsAgg &a, const CsAgg &b) const {
-        return b.head ? b : CsAgg{a.head, cs_pick(qk, a.best, b.best)};
+        return b.head ? b : CsAgg{a.head, cs_pick(qk, a.best, b.best, arena)};
     }
 };
 
@@ -690,13 +696,13 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tag
             const OvfKey lk = shfl_up_key(k, off);
             if ((int)lane >= off && !h) {
                 h = lh;
-                if (lb != ~0u && (b == ~0u || !(ovf_kcmp(k, lk) > 0))) {
+                if (lb != ~0u && (b == ~0u || !(ovf_kcmp(k, lk, d.arena) > 0))) {
                     b = lb;
                     k = lk;
                 }
             }
         }
-        if (!h && cb != ~0u && (b == ~0u || !(ovf_kcmp(k, ck) > 0))) {
+        if (!h && cb != ~0u && (b == ~0u || !(ovf_kcmp(k, ck, d.arena) > 0))) {
             b = cb;
             k = ck;
         }
@@ -717,13 +723,13 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tag
     uint32_t pb = ~0u;
     for (uint32_t v = 0; v < w; v++) {
         if (s_head[v]) pb = s_best[v];
-        else if (s_best[v] != ~0u && (pb == ~0u || ovf_kcmp(s_key[v], d.qkey[pb]) > 0)) pb = s_best[v];
+        else if (s_best[v] != ~0u && (pb == ~0u || ovf_kcmp(s_key[v], d.qkey[pb], d.arena) > 0)) pb = s_best[v];
     }
 #pragma unroll
     for (uint32_t c = 0; c < CS_C; c++) {
         const uint32_t q = base + c * 64 + lane;
         if (q >= d.K) continue;
-        d.cbest[q] = open[c] ? cs_pick(d.qkey, pb, res[c]) : res[c];
+        d.cbest[q] = open[c] ? cs_pick(d.qkey, pb, res[c], d.arena) : res[c];
     }
     if (threadIdx.x == 0) {
         CsAgg agg{0u, ~0u};
@@ -734,7 +740,7 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tag
                 agg.best = s_best[v];
                 if (f == CS_TILE) f = s_first[v];
             } else {
-                agg.best = cs_pick(d.qkey, agg.best, s_best[v]);
+                agg.best = cs_pick(d.qkey, agg.best, s_best[v], d.arena);
             }
         }
         tagg[blockIdx.x] = agg;
@@ -750,7 +756,7 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_fix(OvfDev d, const CsAgg
     const uint32_t t0 = t * CS_TILE;
     if (c == ~0u || d.ckey_s[t0] == ~0ULL) return;
     const uint32_t e = min(d.K, t0 + tfirst[t]);
-    for (uint32_t q = t0 + threadIdx.x; q < e; q += CS_T) d.cbest[q] = cs_pick(d.qkey, c, d.cbest[q]);
+    for (uint32_t q = t0 + threadIdx.x; q < e; q += CS_T) d.cbest[q] = cs_pick(d.qkey, c, d.cbest[q], d.arena);
 }
 
 #undef OVF_LOOP

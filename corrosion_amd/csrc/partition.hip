@@ -229,6 +229,24 @@ __global__ void k_unpack(const void *__restrict__ recs, uint32_t n, BatchOut o) 
 
 using namespace corro;
 
+static BatchDev batch_dev(const corro_changes *in, uint32_t n) {
+    BatchDev bd{};
+    bd.pk = in->pk;
+    bd.tcid = in->table_cid;
+    bd.cv = in->col_version;
+    bd.dbv = in->db_version;
+    bd.cl = in->cl;
+    bd.seq = in->seq;
+    bd.site = in->site;
+    bd.v0 = in->val0;
+    bd.v1 = in->val1;
+    bd.vt = in->val_type;
+    bd.vl = in->val_len;
+    bd.ts = in->ts;
+    bd.n = n;
+    return bd;
+}
+
 extern "C" int corro_partition_ranks(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, corro_changes *out,
                                      uint64_t *counts) {
     if (!ctx || !in || !out || !counts) return fail(CORRO_E_INVALID, "NULL argument");
@@ -238,13 +256,14 @@ extern "C" int corro_partition_ranks(corro_ctx *ctx, const corro_changes *in, ui
         !in->val0 || !out->pk || !out->table_cid || !out->col_version || !out->db_version || !out->cl ||
         !out->seq || !out->site || !out->val0)
         return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    if (in->val_off)
+        return fail(CORRO_E_RANGE, "long values are not exchanged between ranks (apply them on their owner)");
     for (uint32_t r = 0; r < nranks; r++) counts[r] = 0;
     const uint32_t n = (uint32_t)in->n;
     if (n == 0) return CORRO_OK;
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    BatchDev bd{in->pk, in->table_cid, in->col_version, in->db_version, in->cl, in->seq, in->site, in->val0,
-                in->val1, in->val_type, in->val_len, in->ts, n};
+    const BatchDev bd = batch_dev(in, n);
     BatchOut bo{const_cast<uint64_t *>(out->pk),     const_cast<uint32_t *>(out->table_cid),
                 const_cast<int64_t *>(out->col_version), const_cast<int64_t *>(out->db_version),
                 const_cast<uint32_t *>(out->cl),     const_cast<uint32_t *>(out->seq),
@@ -293,14 +312,15 @@ extern "C" int corro_partition_packed(corro_ctx *ctx, const corro_changes *in, u
     if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
         !in->val0)
         return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    if (in->val_off)
+        return fail(CORRO_E_RANGE, "long values are not exchanged between ranks (apply them on their owner)");
     if ((uintptr_t)out % 16) return fail(CORRO_E_INVALID, "packed records must be 16-byte aligned");
     for (uint32_t r = 0; r < nranks; r++) counts[r] = 0;
     const uint32_t n = (uint32_t)in->n;
     if (n == 0) return CORRO_OK;
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    BatchDev bd{in->pk, in->table_cid, in->col_version, in->db_version, in->cl, in->seq, in->site, in->val0,
-                in->val1, in->val_type, in->val_len, in->ts, n};
+    const BatchDev bd = batch_dev(in, n);
     uint32_t ntiles, tile, *d_counts;
     uint64_t *d_tot;
     if (int rc = part_tiles(ctx, n, nranks, ntiles, tile, d_counts, d_tot)) return rc;

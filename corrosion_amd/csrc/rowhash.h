@@ -20,6 +20,12 @@ struct BatchDev {
     const uint8_t *vt;
     const uint8_t *vl;
     const uint64_t *ts;
+    // long TEXT/BLOB values: val_off / val_size per change; the batch's val_data was copied to
+    // arena + lbase (ldata bytes) before the apply
+    const uint64_t *voff;
+    const uint32_t *vsz;
+    const uint8_t *arena;
+    uint64_t lbase, ldata;
     uint32_t n;
 };
 

@@ -15,7 +15,10 @@ from . import _lib as L
 BATCH_FIELDS = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64,
                 "db_version": np.int64, "cl": np.uint32, "seq": np.uint32, "site": np.uint32,
                 "val0": np.uint64, "val1": np.uint64, "val_type": np.uint8, "val_len": np.uint8,
-                "ts": np.uint64}
+                "ts": np.uint64, "val_off": np.uint64, "val_size": np.uint32}
+VAL_LONG = L.CORRO_VAL_LONG  # val_len of a TEXT/BLOB value longer than 16 bytes (bytes in "val_data")
+LONG_FIELDS = ("val_off", "val_size")
+FIXED_FIELDS = {k: v for k, v in BATCH_FIELDS.items() if k not in LONG_FIELDS}
 REQUIRED = ("pk", "table_cid", "col_version", "db_version", "cl", "seq", "site", "val0")
 ROW_FIELDS = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64,
               "db_version": np.int64, "cl": np.int64, "seq": np.uint32, "site": np.uint32,
@@ -174,6 +177,17 @@ class MergeEngine:
                     raise ValueError(f"field {k} has {a.shape[0]} elements, expected {n}")
                 keep.append(a)
                 setattr(s, k, a.ctypes.data if n else None)
+        data = batch.get("val_data")  # long values' bytes (val_off / val_size index them)
+        if data is not None:
+            if on_dev:
+                if not data.is_cuda or not data.is_contiguous() or data.dtype != __import__("torch").uint8:
+                    raise ValueError("device val_data must be a contiguous CUDA uint8 tensor")
+                s.val_data, s.val_data_len = (data.data_ptr() if data.numel() else None), int(data.numel())
+            else:
+                data = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else \
+                    np.ascontiguousarray(data, dtype=np.uint8)
+                keep.append(data)
+                s.val_data, s.val_data_len = (data.ctypes.data if data.size else None), int(data.size)
         out = L.ApplyOut()
         imp = None
         if impact:
@@ -214,7 +228,30 @@ class MergeEngine:
             setattr(r, k, a.ctypes.data)
         w = C.c_uint64()
         L.check(L.lib().corro_state_export(self._h, C.byref(r), max(m, 1), C.byref(w)))
-        return {k: a[: w.value] for k, a in out.items()}
+        rows = {k: a[: w.value] for k, a in out.items()}
+        rows["long_values"] = self.long_values(rows)
+        return rows
+
+    def value_bytes(self, handles):
+        """Bytes of long values by their handles (the val1 of rows with val_len == VAL_LONG)."""
+        h = np.ascontiguousarray(handles, dtype=np.uint64)
+        n = len(h)
+        off = np.zeros(n + 1, np.uint64)
+        total = int((h & np.uint64(0xFFFFFF)).sum()) if n else 0
+        buf = np.zeros(max(total, 1), np.uint8)
+        L.check(L.lib().corro_value_bytes(self._h, h.ctypes.data if n else None, n, buf.ctypes.data, total,
+                                          off.ctypes.data))
+        raw = buf.tobytes()
+        return [raw[int(off[i]):int(off[i + 1])] for i in range(n)]
+
+    def long_values(self, rows):
+        """{row index: bytes} for the rows (host arrays) that hold a long value."""
+        vl = np.asarray(rows["val_len"])
+        idx = np.nonzero(vl == VAL_LONG)[0]
+        if len(idx) == 0:
+            return {}
+        vals = self.value_bytes(np.asarray(rows["val1"])[idx])
+        return {int(i): v for i, v in zip(idx, vals)}
 
     def db_versions(self):
         n = self.site_count()
@@ -301,7 +338,7 @@ class MergeEngine:
         dev = recs.device
         if out is None:
             tdt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}
-            keys = [k for k in BATCH_FIELDS if k in REQUIRED or rec_bytes == 80]
+            keys = [k for k in FIXED_FIELDS if k in REQUIRED or rec_bytes == 80]
             out = {k: torch.empty(max(n, 1), dtype=tdt[BATCH_FIELDS[k]], device=dev)[:n] for k in keys}
         s = L.Changes()
         s.n = n
@@ -325,7 +362,7 @@ class MergeEngine:
         cs = (L.Changeset * max(F, 1))()
         actors = (C.c_uint8 * max(16 * F, 16))()
         status = np.zeros(max(F, 1), np.int32)
-        ch = {k: np.zeros(max(NC, 1), dt) for k, dt in BATCH_FIELDS.items()}
+        ch = {k: np.zeros(max(NC, 1), dt) for k, dt in FIXED_FIELDS.items()}
         ss, se = np.zeros(max(NS, 1), np.uint64), np.zeros(max(NS, 1), np.uint64)
         d.cs, d.actor_ids, d.status = C.addressof(cs), C.addressof(actors), status.ctypes.data
         d.changes.n = NC

@@ -134,8 +134,11 @@ def send_change_chunks(out, chunked, actor_id, version, last_seq, ts):
 
 # ---- rows -> Change objects -------------------------------------------------------------------
 
-def _decode_value(vt, v0, v1, ln):
+def _decode_value(vt, v0, v1, ln, long_bytes=None):
     vt = int(vt)
+    if vt in (3, 4) and int(ln) == L.CORRO_VAL_LONG:  # a long value: its bytes from the arena / bookie
+        b = long_bytes()
+        return b.decode() if vt == 3 else b
     if vt == 1:
         return struct.unpack("<q", struct.pack("<Q", int(v0)))[0]
     if vt == 2:
@@ -146,9 +149,13 @@ def _decode_value(vt, v0, v1, ln):
     return None
 
 
-def rows_to_changes(engine, site_ids, rows, lo, hi):
-    """crsql_changes rows [lo, hi) -> Change objects (table / cid names from the engine schema)."""
+def rows_to_changes(engine, site_ids, rows, lo, hi, long_bytes=None):
+    """crsql_changes rows [lo, hi) -> Change objects (table / cid names from the engine schema).
+    long_bytes(k): the bytes of row k's long value (default: its val1 handle in the engine's arena)."""
     out = []
+    if long_bytes is None:
+        def long_bytes(k):
+            return engine.value_bytes([int(rows["val1"][k])])[0]
     for k in range(lo, hi):
         tc = int(rows["table_cid"][k])
         t, cid = tc >> 16, tc & 0xFFFF
@@ -157,7 +164,8 @@ def rows_to_changes(engine, site_ids, rows, lo, hi):
         if name in engine.interned:  # the canonical packed pk of the row (cr-sqlite's t__crsql_pks)
             pk = engine.pk_bytes(t, [pk])[0]
         out.append(Change(table=name, pk=pk, cid="-1" if cid == 0 else cols[cid - 1],
-                          val=_decode_value(rows["val_type"][k], rows["val0"][k], rows["val1"][k], rows["val_len"][k]),
+                          val=_decode_value(rows["val_type"][k], rows["val0"][k], rows["val1"][k], rows["val_len"][k],
+                                            lambda: long_bytes(k)),
                           col_version=int(rows["col_version"][k]), db_version=int(rows["db_version"][k]),
                           seq=int(rows["seq"][k]), site_id=site_ids[int(rows["site"][k])], cl=int(rows["cl"][k])))
     return out
@@ -198,6 +206,18 @@ def _buffered_rows(bookie, actor, version, s, e):
         setattr(r, k, a.ctypes.data)
     L.check(L.lib().corro_bookie_buffered(bookie._h, actor, version, s, e, C.byref(r), c.value, C.byref(c)))
     return rows, c.value
+
+
+def _buffered_long(bookie, actor, version, rows):
+    """long_bytes for rows_to_changes over buffered rows: the bookie keeps their bytes."""
+    def get(k):
+        n = C.c_uint64()
+        seq = int(rows["seq"][k])
+        L.check(L.lib().corro_bookie_buffered_value(bookie._h, actor, version, seq, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(max(1, n.value))
+        L.check(L.lib().corro_bookie_buffered_value(bookie._h, actor, version, seq, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
+    return get
 
 
 def _in_ranges(ranges, v):
@@ -286,8 +306,8 @@ def handle_needs(agent, needs, max_buf_size=MAX_CHANGES_BYTES_PER_MESSAGE):
                 for v in buffered:
                     for (rs, re_), last_seq, ts in _seq_bookkeeping(agent.bookie, actor, v):
                         rows, m = _buffered_rows(agent.bookie, actor, v, rs, re_)
-                        send_change_chunks(out, ChunkedChanges(rows_to_changes(eng, site_ids, rows, 0, m), rs, re_,
-                                                               max_buf_size), actor, v, last_seq, ts)
+                        chg = rows_to_changes(eng, site_ids, rows, 0, m, _buffered_long(agent.bookie, actor, v, rows))
+                        send_change_chunks(out, ChunkedChanges(chg, rs, re_, max_buf_size), actor, v, last_seq, ts)
                 empties += _subtract([(s, e)], gaps + [(v, v) for v in buffered])
         elif kind == "partial":
             g = groups(k)
@@ -312,8 +332,9 @@ def handle_needs(agent, needs, max_buf_size=MAX_CHANGES_BYTES_PER_MESSAGE):
                                 continue
                             s, e = max(rs, qs), min(re_, qe)
                             rows, m = _buffered_rows(agent.bookie, actor, v, s, e)
-                            send_change_chunks(out, ChunkedChanges(rows_to_changes(eng, site_ids, rows, 0, m), s, e,
-                                                                   max_buf_size), actor, v, last_seq, ts)
+                            chg = rows_to_changes(eng, site_ids, rows, 0, m,
+                                                  _buffered_long(agent.bookie, actor, v, rows))
+                            send_change_chunks(out, ChunkedChanges(chg, s, e, max_buf_size), actor, v, last_seq, ts)
         for s, e in _subtract(empties, []):                    # :715-724
             out.append(ChangeV1(actor, Empty(versions=(s, e), ts=None)))
         out_all.append(out)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define CORRO_HIP_ABI_VERSION 1
+#define CORRO_HIP_ABI_VERSION 2
 
 typedef enum {
     CORRO_OK = 0,
@@ -77,9 +77,19 @@ typedef struct {
  *   val0/val1   INTEGER: i64 bits in val0. REAL: f64 bits in val0 (NaN not allowed).
  *               TEXT/BLOB (<= 16 bytes): bytes 0..7 / 8..15 big-endian, zero padded.
  *   val_type    CORRO_* storage class (NULL array = all INTEGER)
- *   val_len     TEXT/BLOB byte length
+ *   val_len     TEXT/BLOB byte length, or CORRO_VAL_LONG for a value longer than 16 bytes
  *   ts          changeset timestamp (NTP64), bound per change as in util.rs:1244
+ *   val_off / val_size / val_data / val_data_len
+ *               TEXT/BLOB values of any length (SqliteValue::Text(String) / Blob(Vec<u8>),
+ *               corro-api-types/src/lib.rs:419-429): a change with val_len == CORRO_VAL_LONG has its
+ *               bytes at val_data[val_off[i], val_off[i] + val_size[i]), 16 < val_size < 2^24
+ *               (val0/val1 are not read for it). val_data holds val_data_len bytes in the batch's
+ *               memory; val_off/val_size are read only for long values (other entries are
+ *               ignored). All NULL/0 when the batch has no long value. The engine keeps the bytes
+ *               in a device value arena; exported rows carry val_len == CORRO_VAL_LONG, val0 = bytes
+ *               0..7 big-endian and val1 = a value handle that corro_value_bytes resolves.
  */
+#define CORRO_VAL_LONG 255
 typedef struct {
     uint64_t n;
     const uint64_t *pk;
@@ -94,6 +104,10 @@ typedef struct {
     const uint8_t *val_type;
     const uint8_t *val_len;
     const uint64_t *ts;
+    const uint64_t *val_off;
+    const uint32_t *val_size;
+    const uint8_t *val_data;
+    uint64_t val_data_len;
 } corro_changes;
 
 /* Per-batch outputs (all optional, host pointers, n elements each) */
@@ -177,6 +191,13 @@ int corro_state_export(corro_ctx *ctx, corro_rows *out, uint64_t cap, uint64_t *
 int corro_state_reset(corro_ctx *ctx);
 /* crsql_db_versions: per-site max db_version over every merged change, -1 = never seen. */
 int corro_db_versions(corro_ctx *ctx, int64_t *out, uint32_t nsites);
+/* Bytes of long values named by value handles (the val1 of exported / extracted rows whose val_len
+ * is CORRO_VAL_LONG; a handle's low 24 bits are its length). Value i's bytes go to
+ * bytes[out_off[i], out_off[i+1]); out_off holds n + 1 entries (host). CORRO_E_RANGE if cap <
+ * out_off[n] (out_off is still filled), CORRO_E_INVALID for a handle outside the arena. Handles stay
+ * valid until corro_state_reset. */
+int corro_value_bytes(corro_ctx *ctx, const uint64_t *handles, uint64_t n, uint8_t *bytes, uint64_t cap,
+                      uint64_t *out_off);
 
 /* Stage timing with HIP events recorded on the engine's stream (for roofline reporting).
  * corro_last_timings returns milliseconds of the last apply per stage:
@@ -376,6 +397,11 @@ int corro_bookie_buffered_versions(corro_bookie *bk, const uint8_t *actor_id, ui
  * ascending (peer/mod.rs:513-531, :672-693); *count = matching rows, at most cap written. */
 int corro_bookie_buffered(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t seq_start,
                           uint64_t seq_end, corro_rows *out, uint64_t cap, uint64_t *count);
+/* Bytes of the buffered row (actor, version, seq) when it holds a long value (its corro_rows entry
+ * has val_len == CORRO_VAL_LONG and val1 = 0): *len = the length (0 = no such value), at most cap
+ * bytes copied. */
+int corro_bookie_buffered_value(corro_bookie *bk, const uint8_t *actor_id, uint64_t version, uint64_t seq,
+                                uint8_t *out, uint64_t cap, uint64_t *len);
 
 /* generate_sync (corro-types/src/sync.rs:284-333) as CSR over actors with a known head:
  * heads, needed ranges, and for every non-complete partial the seq gaps over 0..=last_seq. */

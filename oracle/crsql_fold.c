@@ -26,7 +26,9 @@
  *   crsql_db_versions[site] = max(.., db_version) for EVERY inserted change.
  *
  * Value order: type rank INTEGER > REAL > TEXT > BLOB > NULL; INTEGER signed,
- * REAL numeric (-0.0 == 0.0), TEXT/BLOB memcmp then length, NULL == NULL.
+ * REAL numeric (-0.0 == 0.0), TEXT/BLOB memcmp then length, NULL == NULL. TEXT/BLOB values have
+ * no length limit (SqliteValue::Text(String) / Blob(Vec<u8>), corro-api-types/src/lib.rs:419-429):
+ * values longer than 16 bytes are kept whole in a per-state byte arena and compared in full.
  *
  * Parity pinning: the KATs of SURVEY.md App. A.5 and the worked example in
  * /root/reference/doc/crdts.md:225-245 (tests/golden/merge_kats.json, tests/test_oracle.py).
@@ -63,6 +65,8 @@ struct of_state {
     int64_t *dbv;       /* per-site max db_version, -1 = absent */
     of_row *rows;
     uint64_t cap, nrows;
+    uint8_t *arena;     /* bytes of long values; a long cell's v1 = (offset << 24) | length */
+    uint64_t arena_len, arena_cap;
 };
 
 static uint64_t mix64(uint64_t x) {
@@ -86,7 +90,7 @@ of_state *of_new(const uint8_t *site_ids, uint32_t nsites) {
 void of_free(of_state *s) {
     if (!s) return;
     for (uint64_t i = 0; i < s->cap; i++) free(s->rows[i].cells);
-    free(s->rows); free(s->dbv); free(s->site_ids); free(s);
+    free(s->rows); free(s->dbv); free(s->site_ids); free(s->arena); free(s);
 }
 
 static of_row *find_row(of_state *s, uint32_t table, uint64_t pk, int create);
@@ -126,31 +130,109 @@ static int64_t row_L(const of_row *r) {
 
 static int rank_of(uint8_t t) { return 5 - (int)t; }  /* INTEGER(1)=4 ... NULL(5)=0 */
 
+/* A value as the merge compares it: short TEXT/BLOB bytes live big-endian in v0/v1 (zero padded,
+ * length vlen), a long one (vlen == OF_LONG) at lp[0, llen). */
+typedef struct {
+    uint8_t type, vlen;
+    uint64_t v0, v1;
+    const uint8_t *lp;
+    uint64_t llen;
+} of_val;
+
+static const uint8_t *val_bytes(const of_val *v, uint8_t buf[16], uint64_t *len) {
+    if (v->vlen == OF_LONG) { *len = v->llen; return v->lp; }
+    for (int k = 0; k < 8; k++) { buf[k] = (uint8_t)(v->v0 >> (56 - 8 * k)); buf[8 + k] = (uint8_t)(v->v1 >> (56 - 8 * k)); }
+    *len = v->vlen;
+    return buf;
+}
+
 /* compare incoming value a against local value b: >0 a greater, <0 b greater, 0 equal */
-static int value_cmp(uint8_t ta, uint64_t a0, uint64_t a1, uint8_t la,
-                     uint8_t tb, uint64_t b0, uint64_t b1, uint8_t lb) {
-    if (ta != tb) return rank_of(ta) > rank_of(tb) ? 1 : -1;
-    switch (ta) {
+static int value_cmp(const of_val *a, const of_val *b) {
+    if (a->type != b->type) return rank_of(a->type) > rank_of(b->type) ? 1 : -1;
+    switch (a->type) {
     case OF_INTEGER: {
-        int64_t x = (int64_t)a0, y = (int64_t)b0;
+        int64_t x = (int64_t)a->v0, y = (int64_t)b->v0;
         return x > y ? 1 : (x < y ? -1 : 0);
     }
     case OF_REAL: {
         double x, y;
-        memcpy(&x, &a0, 8); memcpy(&y, &b0, 8);
+        memcpy(&x, &a->v0, 8); memcpy(&y, &b->v0, 8);
         return x > y ? 1 : (x < y ? -1 : 0);
     }
     case OF_TEXT:
-    case OF_BLOB:
-        if (a0 != b0) return a0 > b0 ? 1 : -1;
-        if (a1 != b1) return a1 > b1 ? 1 : -1;
+    case OF_BLOB: {  /* memcmp over the common length, then the longer value is greater */
+        uint8_t ba[16], bb[16];
+        uint64_t la, lb;
+        const uint8_t *pa = val_bytes(a, ba, &la), *pb = val_bytes(b, bb, &lb);
+        int c = memcmp(pa, pb, la < lb ? la : lb);
+        if (c) return c > 0 ? 1 : -1;
         return la > lb ? 1 : (la < lb ? -1 : 0);
+    }
     default:
         return 0;  /* NULL == NULL */
     }
 }
 
-static void fill_cell(of_cell *c, const of_changes *in, uint64_t i) {
+static of_val in_val(const of_changes *in, uint64_t i) {
+    of_val v;
+    v.type = in->val_type ? in->val_type[i] : OF_INTEGER;
+    v.vlen = in->val_len ? in->val_len[i] : 0;
+    v.v0 = in->val0 ? in->val0[i] : 0;
+    v.v1 = in->val1 ? in->val1[i] : 0;
+    v.lp = NULL; v.llen = 0;
+    if (v.vlen == OF_LONG && (v.type == OF_TEXT || v.type == OF_BLOB)) {
+        v.lp = in->val_data + in->val_off[i];
+        v.llen = in->val_size[i];
+        v.v0 = 0;  /* bytes 0..7 big-endian (the caller's val0 is not read) */
+        for (int k = 0; k < 8; k++) v.v0 = (v.v0 << 8) | v.lp[k];
+        v.v1 = 0;
+    }
+    return v;
+}
+
+static of_val cell_val(const of_state *s, const of_cell *c) {
+    of_val v;
+    v.type = c->vtype; v.vlen = c->vlen; v.v0 = c->v0; v.v1 = c->v1;
+    v.lp = NULL; v.llen = 0;
+    if (c->vlen == OF_LONG) { v.lp = s->arena + (c->v1 >> 24); v.llen = c->v1 & 0xFFFFFFu; }
+    return v;
+}
+
+static uint64_t arena_put(of_state *s, const uint8_t *p, uint64_t len) {
+    if (s->arena_len + len > s->arena_cap) {
+        while (s->arena_len + len > s->arena_cap) s->arena_cap = s->arena_cap ? 2 * s->arena_cap : 4096;
+        s->arena = (uint8_t *)realloc(s->arena, s->arena_cap);
+    }
+    const uint64_t off = s->arena_len;
+    memcpy(s->arena + off, p, len);
+    s->arena_len += len;
+    return off;
+}
+
+uint64_t of_bytes_hash(const uint8_t *p, uint64_t len) {
+    uint64_t h = mix64(len + 0x2545F4914F6CDD1DULL);
+    uint64_t k = 0;
+    for (; k + 8 <= len; k += 8) {
+        uint64_t w;
+        memcpy(&w, p + k, 8);
+        h = mix64(h ^ w);
+    }
+    if (k < len) {
+        uint64_t w = 0;
+        memcpy(&w, p + k, len - k);
+        h = mix64(h ^ w ^ 0x9E3779B97F4A7C15ULL);
+    }
+    return h;
+}
+
+uint64_t of_value_bytes(const of_state *s, uint64_t handle, uint8_t *out, uint64_t cap) {
+    const uint64_t off = handle >> 24, len = handle & 0xFFFFFFu;
+    if (off + len > s->arena_len) return 0;
+    memcpy(out, s->arena + off, len < cap ? len : cap);
+    return len;
+}
+
+static void fill_cell(of_state *s, of_cell *c, const of_changes *in, uint64_t i) {
     c->cid = in->table_cid[i] & 0xFFFFu;
     c->cv = in->col_version[i];
     c->dbv = in->db_version[i];
@@ -161,6 +243,11 @@ static void fill_cell(of_cell *c, const of_changes *in, uint64_t i) {
     c->vlen = in->val_len ? in->val_len[i] : 0;
     c->v0 = in->val0 ? in->val0[i] : 0;
     c->v1 = in->val1 ? in->val1[i] : 0;
+    if (c->vlen == OF_LONG && (c->vtype == OF_TEXT || c->vtype == OF_BLOB)) {
+        const of_val v = in_val(in, i);
+        c->v0 = v.v0;
+        c->v1 = (arena_put(s, v.lp, v.llen) << 24) | v.llen;
+    }
 }
 
 static of_cell *find_cell(of_row *r, uint32_t cid) {
@@ -177,11 +264,23 @@ static of_cell *add_cell(of_row *r) {
     return &r->cells[r->ncells++];
 }
 
-static void set_cell(of_row *r, const of_changes *in, uint64_t i) {
+static void set_cell(of_state *s, of_row *r, const of_changes *in, uint64_t i) {
     uint32_t cid = in->table_cid[i] & 0xFFFFu;
     of_cell *c = find_cell(r, cid);
     if (!c) c = add_cell(r);
-    fill_cell(c, in, i);
+    fill_cell(s, c, in, i);
+}
+
+/* the sentinel clock takes change i's clock fields (never a value) */
+static void fill_sentinel(of_row *r, const of_changes *in, uint64_t i) {
+    of_cell *c = &r->sent;
+    c->cid = 0;
+    c->cv = in->col_version[i];
+    c->dbv = in->db_version[i];
+    c->site = in->site[i];
+    c->seq = in->seq[i];
+    c->ts = in->ts ? in->ts[i] : 0;
+    c->vtype = OF_NULL; c->vlen = 0; c->v0 = c->v1 = 0;
 }
 
 static void zero_cells(of_row *r) {
@@ -204,16 +303,14 @@ static int apply_one(of_state *s, const of_changes *in, uint64_t i) {
         if (cl == L) return 0;
         r->ncells = 0;
         r->has_sent = 1;
-        fill_cell(&r->sent, in, i);                         /* sentinel cv = x.cv */
-        r->sent.cid = 0; r->sent.vtype = OF_NULL; r->sent.v0 = r->sent.v1 = 0; r->sent.vlen = 0;
+        fill_sentinel(r, in, i);                            /* sentinel cv = x.cv */
         return 1;
     }
     if (cid == 0) {                                         /* rule 3: pk-only / resurrect */
         if (cl > L) {
             zero_cells(r);
             r->has_sent = 1;
-            fill_cell(&r->sent, in, i);
-            r->sent.cid = 0; r->sent.vtype = OF_NULL; r->sent.v0 = r->sent.v1 = 0; r->sent.vlen = 0;
+            fill_sentinel(r, in, i);
             return 1;
         }
         return 0;
@@ -223,12 +320,11 @@ static int apply_one(of_state *s, const of_changes *in, uint64_t i) {
         if (L > 0 || cl > 1) {
             zero_cells(r);
             r->has_sent = 1;
-            fill_cell(&r->sent, in, i);
+            fill_sentinel(r, in, i);
             r->sent.cv = cl;
-            r->sent.cid = 0; r->sent.vtype = OF_NULL; r->sent.v0 = r->sent.v1 = 0; r->sent.vlen = 0;
             imp = 1;
         }
-        set_cell(r, in, i);
+        set_cell(s, r, in, i);
         return imp + 1;
     }
     /* cl == L : last-writer-wins */
@@ -237,10 +333,8 @@ static int apply_one(of_state *s, const of_changes *in, uint64_t i) {
         int64_t cv = in->col_version[i];
         if (cv < c->cv) return 0;
         if (cv == c->cv) {
-            int vc = value_cmp(in->val_type ? in->val_type[i] : OF_INTEGER,
-                               in->val0 ? in->val0[i] : 0, in->val1 ? in->val1[i] : 0,
-                               in->val_len ? in->val_len[i] : 0,
-                               c->vtype, c->v0, c->v1, c->vlen);
+            const of_val a = in_val(in, i), b = cell_val(s, c);
+            int vc = value_cmp(&a, &b);
             if (vc < 0) return 0;
             if (vc == 0) {
                 /* merge-equal-values: bigger writer site id wins (memcmp of 16 bytes) */
@@ -250,7 +344,7 @@ static int apply_one(of_state *s, const of_changes *in, uint64_t i) {
             }
         }
     }
-    set_cell(r, in, i);
+    set_cell(s, r, in, i);
     return 1;
 }
 
@@ -455,8 +549,9 @@ void of_state_digest(const of_state *s, uint64_t out[3]) {
                                      r->sent.ts, OF_NULL, 0, 0, 0));
         for (uint32_t k = 0; k < r->ncells; k++) {
             const of_cell *c = &r->cells[k];
+            const uint64_t v1 = c->vlen == OF_LONG ? of_bytes_hash(s->arena + (c->v1 >> 24), c->v1 & 0xFFFFFFu) : c->v1;
             digest_add(out, row_hash(r->pk, (r->table << 16) | c->cid, c->cv, c->dbv, L, c->seq, c->site, c->ts,
-                                     c->vtype, c->vlen, c->v0, c->v1));
+                                     c->vtype, c->vlen, c->v0, v1));
         }
     }
 }

@@ -26,7 +26,15 @@ typedef struct {
     const uint8_t *val_type;   /* optional: OF_* (NULL = all INTEGER) */
     const uint8_t *val_len;    /* optional: TEXT/BLOB length (<= 16) */
     const uint64_t *ts;        /* optional: changeset timestamp (NTP64) */
+    /* optional: TEXT/BLOB values longer than 16 bytes. A change with val_len == OF_LONG holds its
+     * bytes at val_data[val_off[i], val_off[i] + val_size[i]) (17 <= val_size < 2^24). */
+    const uint64_t *val_off;
+    const uint32_t *val_size;
+    const uint8_t *val_data;
 } of_changes;
+
+/* val_len of a long value; in exported rows its val1 is a handle of_value_bytes resolves */
+#define OF_LONG 255
 
 typedef struct {
     uint64_t *pk;
@@ -51,11 +59,18 @@ void of_apply(of_state *s, const of_changes *in, uint8_t *impact_out);
 uint64_t of_count(const of_state *s);
 uint64_t of_export(const of_state *s, of_rows *out);
 void of_db_versions(const of_state *s, int64_t *out);
+/* bytes of a long value exported by of_export (val_len == OF_LONG, handle = its val1); returns the
+ * length, copies min(length, cap) bytes */
+uint64_t of_value_bytes(const of_state *s, uint64_t handle, uint8_t *out, uint64_t cap);
+/* content hash the digests use in place of a long value's handle */
+uint64_t of_bytes_hash(const uint8_t *p, uint64_t len);
 /* pk-sharded parallel fold: shards[s] owns the rows hashed to s (<= 256 shards) */
 int of_apply_sharded(of_state **shards, uint32_t nshards, const of_changes *in, uint8_t *impact_out,
                      uint32_t nthreads);
 /* order-independent digests: {rows, sum of row hashes, xor of rotated row hashes}; state digests
- * accumulate into out (so shard digests add up), row-array digests overwrite it */
+ * accumulate into out (so shard digests add up), row-array digests overwrite it. A long value
+ * enters a row hash as of_bytes_hash of its bytes: of_rows_digest expects the caller to have put
+ * that hash in val1 of every row with val_len == OF_LONG. */
 void of_state_digest(const of_state *s, uint64_t out[3]);
 void of_rows_digest(const of_rows *o, uint64_t n, uint64_t out[3]);
 

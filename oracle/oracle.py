@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 OF_INTEGER, OF_REAL, OF_TEXT, OF_BLOB, OF_NULL = 1, 2, 3, 4, 5
+OF_LONG = 255  # val_len of a TEXT/BLOB value longer than 16 bytes (bytes in val_data)
 
 _u64p = C.POINTER(C.c_uint64)
 
@@ -22,7 +23,8 @@ class _Changes(C.Structure):
                 ("col_version", C.c_void_p), ("db_version", C.c_void_p), ("cl", C.c_void_p),
                 ("seq", C.c_void_p), ("site", C.c_void_p), ("val0", C.c_void_p),
                 ("val1", C.c_void_p), ("val_type", C.c_void_p), ("val_len", C.c_void_p),
-                ("ts", C.c_void_p)]
+                ("ts", C.c_void_p), ("val_off", C.c_void_p), ("val_size", C.c_void_p),
+                ("val_data", C.c_void_p)]
 
 
 class _Rows(C.Structure):
@@ -69,6 +71,10 @@ def lib():
         L.of_apply_sharded.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_Changes), C.c_void_p, C.c_uint32]
         L.of_state_digest.argtypes = [C.c_void_p, C.c_void_p]
         L.of_rows_digest.argtypes = [C.POINTER(_Rows), C.c_uint64, C.c_void_p]
+        L.of_value_bytes.restype = C.c_uint64
+        L.of_value_bytes.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
+        L.of_bytes_hash.restype = C.c_uint64
+        L.of_bytes_hash.argtypes = [C.c_char_p, C.c_uint64]
         L.of_needs.argtypes = [C.POINTER(_SyncEntries), C.POINTER(_NeedsOut), C.c_int]
         L.of_booked_new.restype = C.c_void_p
         L.of_booked_free.argtypes = [C.c_void_p]
@@ -88,7 +94,7 @@ def lib():
 BATCH_DTYPES = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64,
                 "db_version": np.int64, "cl": np.uint32, "seq": np.uint32, "site": np.uint32,
                 "val0": np.uint64, "val1": np.uint64, "val_type": np.uint8, "val_len": np.uint8,
-                "ts": np.uint64}
+                "ts": np.uint64, "val_off": np.uint64, "val_size": np.uint32}
 
 
 def _ptr(a):
@@ -106,7 +112,18 @@ def _changes_struct(batch, keep):
             assert len(a) == n, k
             keep.append(a)
         setattr(s, k, _ptr(a))
+    data = batch.get("val_data")
+    if data is not None:
+        data = np.frombuffer(bytes(data) or b"\0", np.uint8) if not isinstance(data, np.ndarray) else data
+        keep.append(data)
+        s.val_data = data.ctypes.data
     return s
+
+
+def bytes_hash(b):
+    """of_bytes_hash: the content hash a long value enters the digests with."""
+    b = bytes(b)
+    return int(lib().of_bytes_hash(b, len(b)))
 
 
 class Fold:
@@ -144,7 +161,15 @@ class Fold:
         if m:
             got = lib().of_export(self._h, C.byref(r))
             assert got == m
+        out["long_values"] = {int(i): self.value_bytes(int(out["val1"][i]))
+                              for i in np.nonzero(out["val_len"] == OF_LONG)[0]}
         return out
+
+    def value_bytes(self, handle):
+        n = lib().of_value_bytes(self._h, handle, None, 0)
+        buf = C.create_string_buffer(max(n, 1))
+        lib().of_value_bytes(self._h, handle, buf, n)
+        return buf.raw[:n]
 
     def db_versions(self):
         out = np.zeros(max(self.nsites, 1), np.int64)
@@ -196,8 +221,15 @@ class ShardedFold:
 
 def rows_digest(rows):
     """Digest of crsql_changes rows given as arrays (e.g. MergeEngine.export()), comparable with
-    ShardedFold.digest(): (rows, sum of row hashes, xor of rotated row hashes)."""
+    ShardedFold.digest(): (rows, sum of row hashes, xor of rotated row hashes). Rows holding a long
+    value (val_len == OF_LONG) need its bytes in rows["long_values"] ({row index: bytes})."""
     m = len(rows["pk"])
+    longs = rows.get("long_values") or {}
+    if longs:
+        rows = dict(rows)
+        rows["val1"] = np.array(rows["val1"], dtype=np.uint64, copy=True)
+        for i, b in longs.items():
+            rows["val1"][i] = bytes_hash(b)
     dts = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64, "db_version": np.int64,
            "cl": np.int64, "seq": np.uint32, "site": np.uint32, "ts": np.uint64, "val0": np.uint64,
            "val1": np.uint64, "val_type": np.uint8, "val_len": np.uint8}

@@ -231,3 +231,38 @@ def sync_entries_torch(npairs, actors_per_pair, seed, device="cuda", max_head=1_
             "tp_off": tp_off, "tp_ver": tp_ver, "tps_off": tps_off, "tps_start": tps_s, "tps_end": tps_e,
             "on_off": on_off, "on_start": on_s, "on_end": on_e, "op_off": op_off, "op_ver": op_ver,
             "ops_off": ops_off, "ops_start": ops_s, "ops_end": ops_e}
+
+
+# long TEXT/BLOB values (> 16 bytes) that tie on their first 8 / 16 bytes, differ only past them, or
+# only in length -- the cases a prefix compare would get wrong
+LONG_POOL = [b"hello world, this is a long value", b"hello world, this is a long valuf",
+             b"hello world, this is a long value!", b"0123456789abcdef0", b"0123456789abcdef" * 9,
+             b"\0" * 17, b"\0" * 40, b"\0" * 16 + b"\1", bytes(range(200)), b"aaaaaaaaaaaaaaaaaaaaaaaaa"]
+
+
+def with_long_values(b, seed, frac=0.2, pool=LONG_POOL):
+    """A copy of batch b in which about `frac` of the column changes carry a long TEXT/BLOB value
+    (val_len 255, bytes in val_data at val_off / val_size)."""
+    rng = np.random.default_rng(seed)
+    n = len(b["pk"])
+    out = dict(b)
+    vt = np.array(b.get("val_type", np.ones(n, np.uint8)), np.uint8, copy=True)
+    vl = np.array(b.get("val_len", np.zeros(n, np.uint8)), np.uint8, copy=True)
+    v0 = np.array(b["val0"], np.uint64, copy=True)
+    v1 = np.array(b.get("val1", np.zeros(n, np.uint64)), np.uint64, copy=True)
+    pick = ((np.asarray(b["table_cid"]) & 0xFFFF) != 0) & (rng.random(n) < frac)
+    which = rng.integers(0, len(pool), size=n)
+    off, size = np.zeros(n, np.uint64), np.zeros(n, np.uint32)
+    data, dlen = [], 0
+    for i in np.nonzero(pick)[0]:
+        v = pool[which[i]]
+        vt[i] = 3 if (which[i] % 2 == 0) else 4
+        vl[i] = 255
+        v0[i] = int.from_bytes(v[:8], "big")
+        v1[i] = 0
+        off[i], size[i] = dlen, len(v)
+        data.append(v)
+        dlen += len(v)
+    out.update({"val_type": vt, "val_len": vl, "val0": v0, "val1": v1, "val_off": off, "val_size": size,
+                "val_data": np.frombuffer(b"".join(data) or b"\0", np.uint8)[:dlen]})
+    return out

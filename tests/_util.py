@@ -58,14 +58,54 @@ def batch_from_changes(changes, pk=1, table=0, seq0=0):
     return {k: np.array(v, dtype=dt[k]) for k, v in b.items()}
 
 
+LONG = 255  # val_len of a TEXT/BLOB value longer than 16 bytes
+
+
+def encode_values(vals):
+    """SqliteValues (None | int | float | str | bytes, any length) -> the batch's value fields:
+    val_type / val0 / val1 / val_len, plus val_off / val_size / val_data for values longer than 16
+    bytes (omitted when there are none)."""
+    n = len(vals)
+    out = {"val_type": np.zeros(n, np.uint8), "val0": np.zeros(n, np.uint64), "val1": np.zeros(n, np.uint64),
+           "val_len": np.zeros(n, np.uint8)}
+    off, size, data, dlen = np.zeros(n, np.uint64), np.zeros(n, np.uint32), [], 0
+    for i, v in enumerate(vals):
+        if v is None:
+            out["val_type"][i] = 5
+        elif isinstance(v, (bool, int)):
+            out["val_type"][i], out["val0"][i] = 1, int(v) & 0xFFFFFFFFFFFFFFFF
+        elif isinstance(v, float):
+            out["val_type"][i], out["val0"][i] = 2, struct.unpack("<Q", struct.pack("<d", v))[0]
+        else:
+            b = v.encode() if isinstance(v, str) else bytes(v)
+            out["val_type"][i] = 3 if isinstance(v, str) else 4
+            if len(b) > 16:
+                out["val0"][i], out["val_len"][i] = int.from_bytes(b[:8], "big"), LONG
+                off[i], size[i] = dlen, len(b)
+                data.append(b)
+                dlen += len(b)
+            else:
+                p = b.ljust(16, b"\0")
+                out["val0"][i], out["val1"][i] = int.from_bytes(p[:8], "big"), int.from_bytes(p[8:], "big")
+                out["val_len"][i] = len(b)
+    if data:
+        out["val_off"], out["val_size"] = off, size
+        out["val_data"] = np.frombuffer(b"".join(data), np.uint8)
+    return out
+
+
 def rows_to_tuples(rows, with_ts=False):
-    """exported state dict -> sorted list of comparable tuples"""
+    """exported state dict -> sorted list of comparable tuples (a long value compares by its bytes,
+    rows["long_values"])"""
     n = len(rows["pk"])
+    longs = rows.get("long_values") or {}
     out = []
     for i in range(n):
         t = int(rows["val_type"][i])
+        lv = t in (3, 4) and int(rows["val_len"][i]) == LONG
         tup = (int(rows["table_cid"][i]) >> 16, int(rows["pk"][i]), int(rows["table_cid"][i]) & 0xFFFF,
-               t, int(rows["val0"][i]) if t != 5 else 0, int(rows["val1"][i]) if t in (3, 4) else 0,
+               t, int(rows["val0"][i]) if t != 5 else 0,
+               (longs[i] if lv else int(rows["val1"][i])) if t in (3, 4) else 0,
                int(rows["val_len"][i]) if t in (3, 4) else 0, int(rows["col_version"][i]),
                int(rows["db_version"][i]), int(rows["site"][i]), int(rows["cl"][i]),
                int(rows["seq"][i]))

@@ -2,13 +2,15 @@
 (/root/reference/crates/corro-tests/src/lib.rs:13-53) -- tests, tests2, tests3 (INTEGER pk),
 testsblob (BLOB pk), testsbool, wide (composite BLOB + TEXT pk) -- merged through the C ABI with
 interned row keys (corro_pk_keys) and checked against the oracle on the same keys, bit-exact; the
-keys map back to the canonical packed pks (corro_pk_bytes)."""
+keys map back to the canonical packed pks (corro_pk_bytes). TEXT / BLOB column values have any
+length (SqliteValue, corro-api-types/src/lib.rs:419-429): values longer than 16 bytes go through
+the value arena and compare by their whole bytes."""
 import numpy as np
 import pytest
 
 import synth
 from oracle import oracle as O
-from tests._util import rows_to_tuples
+from tests._util import encode_values, rows_to_tuples
 
 pytestmark = pytest.mark.gpu
 
@@ -54,21 +56,27 @@ def _changes(rng, n, nsites):
         cl = cl if sent else (cl | 1)
         cv = cl if sent else int(rng.integers(1, 4))
         if sent:
-            vt, v0, v1, vl = 5, 0, 0, 0
+            val = None
         else:
             col = cols[cid - 1]
             if col in ("num", "num2", "int", "b"):
-                vt, v0, v1, vl = 1, int(rng.integers(0, 4)), 0, 0
+                val = int(rng.integers(0, 4))
             elif col == "float":
-                vt, v0, v1, vl = 2, int(np.float64(rng.integers(0, 3) * 0.5).view(np.uint64)), 0, 0
+                val = float(rng.integers(0, 3) * 0.5)
             elif col == "blob":
-                raw = bytes(rng.integers(0, 3, 16, dtype=np.uint8))
-                vt, v0, v1, vl = 4, int.from_bytes(raw[:8], "big"), int.from_bytes(raw[8:], "big"), 16
+                val = BLOBS[int(rng.integers(0, len(BLOBS)))]
             else:
-                s = f"v{int(rng.integers(0, 3))}".encode()
-                vt, v0, v1, vl = 3, int.from_bytes(s.ljust(8, b"\0"), "big"), 0, len(s)
-        rows.append((t, pk, cid, vt, v0, v1, vl, cv, int(rng.integers(1, 50)), int(rng.integers(0, nsites)), cl, i))
+                val = TEXTS[int(rng.integers(0, len(TEXTS)))]
+        rows.append((t, pk, cid, val, cv, int(rng.integers(1, 50)), int(rng.integers(0, nsites)), cl, i))
     return rows
+
+
+# short and long values that tie on their first 8 / 16 bytes, differ only past them, or only in length
+TEXTS = ["v0", "v1", "v2", "hello world, this is a long text value", "hello world, this is a long text valuf",
+         "hello world, this is a long text value!", "hello wo", "0123456789abcdef", "0123456789abcdef0",
+         "0123456789abcdef" * 20]
+BLOBS = [bytes(16), bytes(17), bytes(16) + b"\1", bytes([1, 2]) * 20, bytes([1, 2]) * 21, bytes([1, 2, 2]) * 7,
+         bytes(range(3)) * 5 + bytes([9])]
 
 
 def test_every_corro_tests_table_vs_oracle():
@@ -93,15 +101,13 @@ def test_every_corro_tests_table_vs_oracle():
                 keys[idx] = [unpack_int_pk(rows[j][1]) & 0xFFFFFFFFFFFFFFFF for j in idx]
         b = {"pk": keys,
              "table_cid": np.array([(tix[r[0]] << 16) | r[2] for r in rows], np.uint32),
-             "val_type": np.array([r[3] for r in rows], np.uint8),
-             "val0": np.array([r[4] for r in rows], np.uint64),
-             "val1": np.array([r[5] for r in rows], np.uint64),
-             "val_len": np.array([r[6] for r in rows], np.uint8),
-             "col_version": np.array([r[7] for r in rows], np.int64),
-             "db_version": np.array([r[8] for r in rows], np.int64),
-             "site": np.array([r[9] for r in rows], np.uint32),
-             "cl": np.array([r[10] for r in rows], np.uint32),
-             "seq": np.array([r[11] % 100 for r in rows], np.uint32)}
+             "col_version": np.array([r[4] for r in rows], np.int64),
+             "db_version": np.array([r[5] for r in rows], np.int64),
+             "site": np.array([r[6] for r in rows], np.uint32),
+             "cl": np.array([r[7] for r in rows], np.uint32),
+             "seq": np.array([r[8] % 100 for r in rows], np.uint32)}
+        b.update(encode_values([r[3] for r in rows]))
+        assert "val_data" in b
         assert np.array_equal(e.apply(b, impact=True), f.apply(b))
         assert rows_to_tuples(e.export()) == rows_to_tuples(f.export())
     # interned keys give back the canonical packed pks, every table's rows present

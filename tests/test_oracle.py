@@ -103,6 +103,7 @@ def test_rows_digest_detects_a_single_field_change():
     rows = f.export()
     d0 = O.rows_digest(rows)
     perm = np.random.default_rng(0).permutation(len(rows["pk"]))
+    rows.pop("long_values")
     assert O.rows_digest({k: v[perm] for k, v in rows.items()}) == d0  # order-independent
     for k in rows:
         r2 = {kk: vv.copy() for kk, vv in rows.items()}
@@ -131,3 +132,59 @@ def test_inverted_our_need_ranges_fixture():
     cases = load_golden("sync_inverted_cases.json")["cases"]
     ent = entries_from_pairs(pairs_from_cases(cases))
     assert decode_needs(O.needs(ent), len(cases)) == expected_from_cases(cases)
+
+
+LONG_POOL = ["v0", "same-prefix", "same-pre", "same-prefix-and-then-some", "same-prefix-and-then-somf",
+             "same-prefix-and-then-some-more", "0123456789abcdef", "0123456789abcdef0", "x" * 300,
+             b"\0" * 16, b"\0" * 17, b"\0" * 40, b"\0" * 16 + b"\1", bytes(range(64))]
+
+
+def _value_key(v):
+    """SQLite value order for TEXT/BLOB (memcmp, then length): Python's bytes order; TEXT > BLOB."""
+    return (1 if isinstance(v, str) else 0, v.encode() if isinstance(v, str) else bytes(v))
+
+
+def test_oracle_long_values_lww_order():
+    """Values of any length (SqliteValue::Text / Blob, corro-api-types/src/lib.rs:419-429): at equal
+    col_version the greater value wins by memcmp-then-length over the WHOLE value (not a 16-byte
+    prefix), and the state keeps every byte."""
+    from tests._util import encode_values
+    rng = np.random.default_rng(11)
+    n = 4000
+    vals = [LONG_POOL[int(rng.integers(0, len(LONG_POOL)))] for _ in range(n)]
+    pks = rng.integers(0, 40, n).astype(np.uint64)
+    b = encode_values(vals)
+    b.update({"pk": pks, "table_cid": np.ones(n, np.uint32), "col_version": np.ones(n, np.int64),
+              "db_version": np.arange(1, n + 1, dtype=np.int64), "cl": np.ones(n, np.uint32),
+              "seq": np.zeros(n, np.uint32), "site": (np.arange(n) % 3).astype(np.uint32)})
+    f = O.Fold(site_table(4))
+    imp = f.apply(b)
+    rows = f.export()
+    got = {int(rows["pk"][i]): i for i in range(len(rows["pk"]))}
+    for pk in range(40):
+        mine = [(v, j) for j, v in enumerate(vals) if pks[j] == pk]
+        if not mine:
+            continue
+        # winner: max value; among equal values the larger site id, then the earliest change
+        best = max(mine, key=lambda t: (_value_key(t[0]), t[1] % 3, -t[1]))
+        i = got[pk]
+        v = best[0]
+        raw = v.encode() if isinstance(v, str) else bytes(v)
+        if len(raw) > 16:
+            assert rows["val_len"][i] == O.OF_LONG and rows["long_values"][i] == raw
+        else:
+            assert rows["val_len"][i] == len(raw)
+        assert rows["db_version"][i] == best[1] + 1
+    # impacts: strict prefix maxima of (value, site) per pk
+    cur = {}
+    for j, v in enumerate(vals):
+        k = (_value_key(v), j % 3)
+        exp = 1 if (int(pks[j]) not in cur or k > cur[int(pks[j])]) else 0
+        if exp:
+            cur[int(pks[j])] = k
+        assert imp[j] == exp, j
+    # the digest sees the bytes: a copy of the rows with the same long values digests equal
+    assert O.rows_digest(rows)[0] == len(rows["pk"])
+    s = O.ShardedFold(site_table(4), nshards=4, nthreads=2)
+    s.apply(b)
+    assert s.digest() == O.rows_digest(rows)
