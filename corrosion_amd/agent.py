@@ -285,7 +285,10 @@ class Agent:
         s = L.Changes()
         s.n = n
         for k, a in ch.items():
-            setattr(s, k, a.ctypes.data if n else None)
+            if k == "val_data":
+                s.val_data, s.val_data_len = a.ctypes.data, a.size
+            else:
+                setattr(s, k, a.ctypes.data if n else None)
         known = np.zeros(max(1, len(keep)), np.int32)
         imp = np.zeros(max(1, n), np.uint8)
         out = L.ProcessOut()

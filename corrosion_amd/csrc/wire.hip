@@ -19,7 +19,11 @@
 //                  change's offset (and reads the trailing seqs / last_seq / ts), then all lanes
 //                  decode changes in parallel: table / column names matched against the schema,
 //                  pk unpacked, value to the engine's fixed-width encoding, site id to its ordinal
-//                  through a device hash of the registered sites.
+//                  through a device hash of the registered sites. A TEXT/BLOB longer than 16 bytes
+//                  stays in the frame bytes: the change names it by val_off / val_size (offsets in
+//                  the frame buffer, which becomes the batch's val_data). The pk of an interned table
+//                  (corro_table_set_pk_interned: BLOB / TEXT / composite pks) is left as a reference
+//                  to its packed bytes, which the host interns (corro_pk_keys) after the kernel.
 // Unknown site ids are collected; the host registers them (corro_site_register) and re-runs the
 // decode, so ordinals match the engine's site table. Unknown table / column names give
 // table_cid = CORRO_TCID_UNKNOWN (the host rolls that version back, as the failing INSERT's
@@ -72,6 +76,9 @@ struct WireDev {
     // outputs (SoA)
     corro_changes out;
     uint32_t *chg_rel;        // scratch: per change offset within its frame (frames with > WIRE_OFFS changes)
+    const uint8_t *interned;  // per table: 1 = rows keyed by interned pk bytes
+    uint64_t *pkref;          // per change: 0, or (buffer offset << 32 | length) of an interned pk
+    unsigned long long *nref, *nlong;  // interned pk references, long values
 };
 
 // little-endian / big-endian readers over any byte pointer, bounds-checked against end
@@ -287,11 +294,17 @@ __global__ void __launch_bounds__(64) k_wire_decode(WireDev d) {
             }
             break;
         }
-        // pk: one packed INTEGER column (unpack_columns: get_int sign-extends big-endian bytes)
+        // pk: one packed INTEGER column (unpack_columns: get_int sign-extends big-endian bytes), or
+        // for an interned table a reference to the packed bytes (the host interns them)
         uint64_t pk = 0;
-        if (lp < 2 || p[pp] != 1 || (p[pp + 1] & 7) != 1 || (uint32_t)(p[pp + 1] >> 3) + 2 != lp ||
-            (p[pp + 1] >> 3) > 8) {
-            err = CORRO_E_RANGE;
+        const uint64_t q = co + k;
+        const bool known = tcid != CORRO_TCID_UNKNOWN;
+        if (known && d.interned[tcid >> 16]) {
+            d.pkref[q] = ((d.foff[f] + pp) << 32) | lp;
+            atomicAdd(d.nref, 1ULL);
+        } else if (lp < 2 || p[pp] != 1 || (p[pp + 1] & 7) != 1 || (uint32_t)(p[pp + 1] >> 3) + 2 != lp ||
+                   (p[pp + 1] >> 3) > 8) {
+            if (known) err = CORRO_E_RANGE;  // (a change of an unknown table rolls its version back anyway)
         } else {
             const uint32_t nb = p[pp + 1] >> 3;
             for (uint32_t i = 0; i < nb; i++) pk = (pk << 8) | p[pp + 2 + i];
@@ -312,12 +325,22 @@ __global__ void __launch_bounds__(64) k_wire_decode(WireDev d) {
         } else if (tag == 3 || tag == 4) {
             const uint32_t l = r.u32();
             vt = tag == 3 ? CORRO_TEXT : CORRO_BLOB;
-            if (l > 16) err = CORRO_E_RANGE;
-            vl = l > 16 ? 16 : l;
-            for (uint32_t i = 0; i < vl; i++) {
+            const uint32_t nb = l > 16 ? 8 : l;
+            for (uint32_t i = 0; i < nb; i++) {
                 const uint64_t b = p[r.pos + i];
                 if (i < 8) w0 |= b << (8 * (7 - i));
                 else w1 |= b << (8 * (15 - i));
+            }
+            vl = l;
+            if (l > 16) {  // a long value: its bytes stay in the frame buffer
+                vl = CORRO_VAL_LONG;
+                if (!d.out.val_off || !d.out.val_size || l >= (1u << 24)) {
+                    err = CORRO_E_RANGE;
+                } else {
+                    const_cast<uint64_t *>(d.out.val_off)[q] = d.foff[f] + r.pos;
+                    const_cast<uint32_t *>(d.out.val_size)[q] = l;
+                    atomicAdd(d.nlong, 1ULL);
+                }
             }
             r.pos += l;
         }
@@ -329,7 +352,6 @@ __global__ void __launch_bounds__(64) k_wire_decode(WireDev d) {
         if (seq > 0xFFFFFFFFULL || cl < 0 || cl > 0xFFFFFFFFLL || dbv > (uint64_t)INT64_MAX) err = CORRO_E_RANGE;
         uint32_t so = site_lookup(d, slo, shi);
         if (so == 0xFFFFFFFFu) note_unknown(d, slo, shi);
-        const uint64_t q = co + k;
         const corro_changes &o = d.out;
         const_cast<uint64_t *>(o.pk)[q] = pk;
         const_cast<uint32_t *>(o.table_cid)[q] = tcid;
@@ -461,7 +483,8 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
     const size_t hdr = 6 * al(F * 4ULL) + 6 * al(F * 8ULL) + al(F * 16ULL);
     const size_t outb = (mem == CORRO_MEM_HOST && pass == 1) ? (al(NC * 8) * 6 + al(NC * 4) * 4 + al(NC) * 2) : 0;
     const size_t need = al(len) + al(F * 8ULL) + al(F * 4ULL) + hdr + 2 * al((F + 1) * 8ULL) + al(NC * 4 + 4) +
-                        al(ucap * 16ULL) + 256 + outb + 2 * al(NS * 8 + 8);
+                        al(ucap * 16ULL) + 256 + outb + 2 * al(NS * 8 + 8) + al(NC * 8 + 8) + al(NC * 12 + 12) +
+                        al(ctx->tables.size() + 1);
     if (int rc = ctx->d_wire.ensure(need)) return rc;
     uint8_t *q = ctx->d_wire.as<uint8_t>();
     auto carve = [&](size_t b) {
@@ -497,7 +520,17 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
     d.chg_rel = (uint32_t *)carve(NC * 4 + 4);
     d.unknown = carve(ucap * 16ULL);
     d.nunknown = (unsigned long long *)carve(256);
+    d.nref = d.nunknown + 1;
+    d.nlong = d.nunknown + 2;
     d.unknown_cap = ucap;
+    d.pkref = (uint64_t *)carve(NC * 8 + 8);
+    {
+        std::vector<uint8_t> fl(ctx->tables.size() + 1, 0);
+        for (size_t t = 0; t < ctx->tables.size() && t < ctx->pk.size(); t++) fl[t] = ctx->pk[t].interned ? 1 : 0;
+        uint8_t *dfl = carve(fl.size());
+        CORRO_HIP_TRY(hipMemcpyAsync(dfl, fl.data(), fl.size(), hipMemcpyHostToDevice, s));
+        d.interned = dfl;
+    }
     d.names = ctx->wire_names;
     d.tname_off = ctx->wire_toff;
     d.tname_len = ctx->wire_tlen;
@@ -532,6 +565,12 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
             o.val_len = (uint8_t *)carve(NC);
             dss = (uint64_t *)carve(NS * 8 + 8);
             dse = (uint64_t *)carve(NS * 8 + 8);
+            // long values' spans, when the caller takes them
+            uint8_t *lv = carve(NC * 12 + 12);
+            if (out->changes.val_off && out->changes.val_size) {
+                o.val_off = (uint64_t *)lv;
+                o.val_size = (uint32_t *)(lv + NC * 8 + 8);
+            }
         }
         if (NC && (!o.pk || !o.table_cid || !o.col_version || !o.db_version || !o.cl || !o.seq || !o.site || !o.val0))
             return fail(CORRO_E_INVALID, "a required change output array is NULL");
@@ -542,6 +581,8 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
     d.set_end = dse;
     std::vector<int32_t> st(F);
     std::vector<uint32_t> kind(F), nchg(F), nset(F), site(F);
+    std::vector<uint64_t> cofs(F + 1, 0);
+    uint64_t cnt3[3] = {0, 0, 0};  // unknown sites, interned pk references, long values
     for (int attempt = 0; attempt < 2; attempt++) {
         if (int rc = wire_tables(ctx)) return rc;
         uint8_t *sq = ctx->d_wire_sites.as<uint8_t>();
@@ -550,7 +591,8 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
         d.hhi = (const uint64_t *)(sq + al(H * 8ULL));
         d.hord = (const uint32_t *)(sq + 2 * al(H * 8ULL));
         d.hmask = ctx->wire_hmask;
-        CORRO_HIP_TRY(hipMemsetAsync(d.nunknown, 0, 8, s));
+        CORRO_HIP_TRY(hipMemsetAsync(d.nunknown, 0, 24, s));
+        if (NC) CORRO_HIP_TRY(hipMemsetAsync(d.pkref, 0, NC * 8, s));
         if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[0], s));
         hipLaunchKernelGGL(k_wire_hdr, dim3((F + 255) / 256), dim3(256), 0, s, d);
         CORRO_HIP_TRY(hipGetLastError());
@@ -570,15 +612,16 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
             return CORRO_OK;
         }
         if (co[F] != NC || so[F] != NS) return fail(CORRO_E_INVALID, "sizes differ from pass 0");
+        cofs = co;
         CORRO_HIP_TRY(hipMemcpyAsync(dchg, co.data(), (F + 1) * 8ULL, hipMemcpyHostToDevice, s));
         CORRO_HIP_TRY(hipMemcpyAsync(dset, so.data(), (F + 1) * 8ULL, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_wire_sets, dim3((F + 255) / 256), dim3(256), 0, s, d);
         hipLaunchKernelGGL(k_wire_decode, dim3(F), dim3(64), 0, s, d);
         if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
         CORRO_HIP_TRY(hipGetLastError());
-        uint64_t nu = 0;
-        CORRO_HIP_TRY(hipMemcpyAsync(&nu, d.nunknown, 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(cnt3, d.nunknown, 24, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipStreamSynchronize(s));
+        const uint64_t nu = cnt3[0];
         if (ctx->profiling) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[7], ctx->ev[0], ctx->ev[1]));
         if (nu == 0) break;
         if (attempt == 1) return fail(CORRO_E_DEVICE, "internal: sites still unknown after registering them");
@@ -604,7 +647,8 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
             {h.pk, o.pk, NC * 8},         {h.col_version, o.col_version, NC * 8}, {h.db_version, o.db_version, NC * 8},
             {h.val0, o.val0, NC * 8},     {h.val1, o.val1, NC * 8},               {h.ts, o.ts, NC * 8},
             {h.table_cid, o.table_cid, NC * 4}, {h.cl, o.cl, NC * 4},             {h.seq, o.seq, NC * 4},
-            {h.site, o.site, NC * 4},     {h.val_type, o.val_type, NC},           {h.val_len, o.val_len, NC}};
+            {h.site, o.site, NC * 4},     {h.val_type, o.val_type, NC},           {h.val_len, o.val_len, NC},
+            {cnt3[2] ? h.val_off : nullptr, o.val_off, NC * 8}, {cnt3[2] ? h.val_size : nullptr, o.val_size, NC * 4}};
         for (auto &c : cp)
             if (c.dst) CORRO_HIP_TRY(hipMemcpyAsync(const_cast<void *>(c.dst), c.src, c.b, hipMemcpyDeviceToHost, s));
     }
@@ -613,6 +657,46 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
         CORRO_HIP_TRY(hipMemcpyAsync(out->set_end, dse, NS * 8, hipMemcpyDeviceToHost, s));
     }
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    // long values: the frame bytes are the batch's val_data (host: the caller's own buffer)
+    corro_changes &oc = out->changes;
+    if (cnt3[2]) {
+        if (mem == CORRO_MEM_HOST) {
+            oc.val_data = buf;
+        } else {
+            if (!oc.val_data) return fail(CORRO_E_RANGE, "long values decoded: changes.val_data must hold len bytes");
+            CORRO_HIP_TRY(hipMemcpyAsync(const_cast<uint8_t *>(oc.val_data), dbuf, len, hipMemcpyDeviceToDevice, s));
+        }
+        oc.val_data_len = len;
+    } else if (pass == 1) {
+        oc.val_off = nullptr;
+        oc.val_size = nullptr;
+        oc.val_data = nullptr;
+        oc.val_data_len = 0;
+    }
+    // interned pks: their packed bytes -> row keys (corro_pk_keys), patched into the pk array
+    if (cnt3[1]) {
+        std::vector<uint64_t> ref(NC), pk(NC);
+        std::vector<uint32_t> tc(NC);
+        CORRO_HIP_TRY(hipMemcpyAsync(ref.data(), d.pkref, NC * 8, hipMemcpyDeviceToHost, s));
+        if (mem == CORRO_MEM_DEVICE) {
+            CORRO_HIP_TRY(hipMemcpyAsync(tc.data(), o.table_cid, NC * 4, hipMemcpyDeviceToHost, s));
+            CORRO_HIP_TRY(hipMemcpyAsync(pk.data(), o.pk, NC * 8, hipMemcpyDeviceToHost, s));
+        }
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        uint64_t *hp = mem == CORRO_MEM_HOST ? const_cast<uint64_t *>(oc.pk) : pk.data();
+        const uint32_t *ht = mem == CORRO_MEM_HOST ? oc.table_cid : tc.data();
+        uint32_t f = 0;
+        for (uint64_t q = 0; q < NC; q++) {
+            if (!ref[q]) continue;
+            while (cofs[f + 1] <= q) f++;
+            const uint64_t off[2] = {0, ref[q] & 0xFFFFFFFFu};
+            if (corro_pk_keys(ctx, ht[q] >> 16, buf + (ref[q] >> 32), off, 1, hp + q) != CORRO_OK)
+                st[f] = std::min(st[f], (int32_t)CORRO_E_INVALID);
+        }
+        if (mem == CORRO_MEM_DEVICE)
+            CORRO_HIP_TRY(hipMemcpyAsync(const_cast<uint64_t *>(oc.pk), pk.data(), NC * 8, hipMemcpyHostToDevice, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+    }
     uint64_t coff = 0, soff = 0;
     for (uint32_t f = 0; f < F; f++) {
         corro_changeset &c = out->cs[f];

@@ -362,7 +362,7 @@ class MergeEngine:
         cs = (L.Changeset * max(F, 1))()
         actors = (C.c_uint8 * max(16 * F, 16))()
         status = np.zeros(max(F, 1), np.int32)
-        ch = {k: np.zeros(max(NC, 1), dt) for k, dt in FIXED_FIELDS.items()}
+        ch = {k: np.zeros(max(NC, 1), dt) for k, dt in BATCH_FIELDS.items()}
         ss, se = np.zeros(max(NS, 1), np.uint64), np.zeros(max(NS, 1), np.uint64)
         d.cs, d.actor_ids, d.status = C.addressof(cs), C.addressof(actors), status.ctypes.data
         d.changes.n = NC
@@ -371,8 +371,14 @@ class MergeEngine:
         d.set_start, d.set_end = ss.ctypes.data, se.ctypes.data
         if F:
             L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, L.CORRO_MEM_HOST, C.byref(d), 1))
+        changes = {k: a[:NC] for k, a in ch.items()}
+        if d.changes.val_data:  # long values: offsets into the frame bytes
+            changes["val_data"] = np.frombuffer(buf, np.uint8)
+        else:
+            for k in LONG_FIELDS:
+                changes.pop(k)
         return {"cs": cs, "nframes": F, "actors": actors, "status": status[:F],
-                "changes": {k: a[:NC] for k, a in ch.items()}, "set_start": ss[:NS], "set_end": se[:NS]}
+                "changes": changes, "set_start": ss[:NS], "set_end": se[:NS]}
 
     # ---- changeset extraction (server side of a sync need) ---------------------------------
     def extract_changes(self, needs):

@@ -427,10 +427,15 @@ int corro_generate_sync(corro_bookie *bk, const uint8_t *self_actor, corro_sync_
  * corro_process_multiple_changes / corro_apply_batch take; ts = the changeset's ts). EmptySet
  * ranges go to set_start/set_end at [change_off, change_off + change_count) of their frame.
  * status[i]: 0 ok, 1 not a changeset message (skipped), CORRO_E_INVALID malformed, CORRO_E_RANGE a
- * value outside the engine encoding (TEXT/BLOB > 16 bytes, a pk that is not one packed INTEGER,
- * seq or cl beyond 32 bits); the changes of a frame with status != 0 are unspecified. Unknown
- * table/column names give table_cid = CORRO_TCID_UNKNOWN; site ids not yet registered are
- * registered (corro_site_register) so every site field is a valid ordinal. */
+ * value outside the engine encoding (a pk that is not one packed INTEGER in a table not marked
+ * interned, seq or cl beyond 32 bits, a TEXT/BLOB of 16 MiB or more, or one longer than 16 bytes
+ * when changes.val_off / val_size are NULL); the changes of a frame with status != 0 are
+ * unspecified. Unknown table/column names give table_cid = CORRO_TCID_UNKNOWN; site ids not yet
+ * registered are registered (corro_site_register) so every site field is a valid ordinal. Interned
+ * tables' pks are interned (corro_pk_keys). Long TEXT/BLOB values: pass 1 fills changes.val_off /
+ * val_size (caller arrays of nchanges, on `mem`) with offsets into the frame buffer, which becomes
+ * changes.val_data (host: `buf` itself; device: the caller's changes.val_data, len bytes, receives a
+ * copy) with val_data_len = len; with no long value decoded the four fields are set to NULL / 0. */
 enum { CORRO_PAYLOAD_SYNC = 0, CORRO_PAYLOAD_UNI = 1 };
 typedef struct {
     uint64_t nframes, nchanges, nsets;      /* pass 0 outputs, pass 1 inputs */

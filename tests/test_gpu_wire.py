@@ -29,9 +29,9 @@ def rand_changes(rng, n, actor, version):
         elif r < 0.55:
             val = float(rng.choice([0.0, -2.5, 1e300, 3.25]))
         elif r < 0.75:
-            val = "".join(chr(97 + int(x)) for x in rng.integers(0, 26, int(rng.integers(0, 17))))
-        elif r < 0.9:
-            val = bytes(rng.integers(0, 256, int(rng.integers(0, 17))).astype(np.uint8))
+            val = "".join(chr(97 + int(x)) for x in rng.integers(0, 26, int(rng.integers(0, 41))))
+        elif r < 0.9:  # (values past 16 bytes travel as val_off / val_size into the frame bytes)
+            val = bytes(rng.integers(0, 256, int(rng.integers(0, 41))).astype(np.uint8))
         else:
             val = None
         pk = int(rng.choice([int(rng.integers(0, 128)), int(rng.integers(-(1 << 40), 1 << 40)), 1 << 60]))
@@ -55,6 +55,13 @@ def got_fields(dec, i):
     c = dec["changes"]
     return tuple(int(c[k][i]) for k in ("pk", "table_cid", "col_version", "db_version", "cl", "seq", "site", "val0",
                                          "val1", "val_type", "val_len", "ts"))
+
+
+def got_long(dec, i):
+    """the bytes of decoded change i's long value (val_off / val_size into the frame buffer)"""
+    c = dec["changes"]
+    o, n = int(c["val_off"][i]), int(c["val_size"][i])
+    return bytes(c["val_data"][o:o + n])
 
 
 @pytest.mark.parametrize("payload", [wire.PAYLOAD_SYNC, wire.PAYLOAD_UNI])
@@ -89,6 +96,9 @@ def test_decode_roundtrip(payload):
             assert cs.change_count == len(x.changes)
             for k, ch in enumerate(x.changes):
                 assert got_fields(dec, cs.change_off + k) == expected_fields(eng, ch, x.ts), (i, k)
+                if dec["changes"]["val_len"][cs.change_off + k] == 255:
+                    raw = ch.val.encode() if isinstance(ch.val, str) else bytes(ch.val)
+                    assert got_long(dec, cs.change_off + k) == raw
         elif isinstance(x, Empty):
             assert (cs.kind, cs.version_start, cs.version_end, cs.ts) == (1, x.versions[0], x.versions[1], x.ts or 0)
         else:
@@ -102,7 +112,8 @@ def test_decode_roundtrip(payload):
 
 def test_decode_large_frames_and_errors():
     """A frame above the 16 KB LDS stage and with more than 1024 changes (global paths), a
-    non-changeset sync message, a truncated changeset, a 17-byte TEXT and a text pk."""
+    non-changeset sync message, a truncated changeset, a 17-byte TEXT (decoded as a long value)
+    and a text pk of a table not marked interned (outside the encoding)."""
     import corrosion_amd as ca
     import struct
     rng = np.random.default_rng(9)
@@ -122,7 +133,9 @@ def test_decode_large_frames_and_errors():
                                            huge))
     eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 14)
     dec = eng.decode_frames(buf)
-    assert list(dec["status"]) == [0, 1, 0, -1, -6, -6, -1]
+    assert list(dec["status"]) == [0, 1, 0, -1, 0, -6, -1]
+    i = dec["cs"][4].change_off
+    assert dec["changes"]["val_len"][i] == 255 and got_long(dec, i) == b"x" * 17
     assert dec["cs"][6].change_count == 0
     assert len(dec["changes"]["pk"]) <= 1500 + 200 + 5 + 1 + 1
     cs0 = dec["cs"][0]
@@ -165,12 +178,66 @@ def test_process_frames_equals_process_objects():
     ry, st = y.process_frames(wire.frames(msgs))
     assert (st == 0).all() and rx.known == ry.known
 
-    def canon(e):
-        r = e.export()
-        keys = ("table_cid", "pk", "val_type", "val0", "val1", "val_len", "col_version", "db_version", "site", "cl",
-                "seq", "ts")
-        return sorted(zip(*[r[k].tolist() for k in keys]))
     assert canon(x.engine) == canon(y.engine)
     assert list(x.engine.db_versions()) == list(y.engine.db_versions())
     for a in ACT[:3]:
         assert x.bookie.needed(a) == y.bookie.needed(a) and x.bookie.last(a) == y.bookie.last(a)
+
+
+def canon(e):
+    """the state's rows, comparable across engines: long values by their bytes, interned row keys
+    by their packed pks"""
+    r = e.export()
+    longs = r["long_values"]
+    keys = ("table_cid", "pk", "val_type", "val0", "val1", "val_len", "col_version", "db_version", "site", "cl",
+            "seq", "ts")
+    cols = [r[k].tolist() for k in keys]
+    for i, b in longs.items():
+        cols[4][i] = b
+    for t, (name, _c) in enumerate(e.schema):
+        if name in e.interned:
+            idx = [i for i, tc in enumerate(cols[0]) if tc >> 16 == t]
+            for i, pk in zip(idx, e.pk_bytes(t, [cols[1][i] for i in idx])):
+                cols[1][i] = pk
+    return sorted(zip(*cols), key=repr)
+
+
+WSCHEMA = {"tests": ["text"], "testsblob": ["text"], "wide": ["int", "float", "blob"]}
+
+
+def test_process_frames_interned_pks_and_long_values():
+    """corro-tests' BLOB-pk and composite-pk tables (corro-tests/src/lib.rs:32-52) over the wire:
+    interned pks and long values decoded on the GPU give the state the same objects give."""
+    import corrosion_amd as ca
+    rng = np.random.default_rng(12)
+    from tests.test_gpu_pk import _pack
+    msgs = []
+    for v in range(1, 80):
+        a = ACT[v % 3]
+        ch = []
+        for k in range(int(rng.integers(1, 25))):
+            t = ["tests", "testsblob", "wide"][int(rng.integers(0, 3))]
+            j = int(rng.integers(0, 30))
+            pk = j if t == "tests" else (_pack([bytes([j]) * (1 + j % 4)]) if t == "testsblob"
+                                         else _pack([j.to_bytes(8, "big"), str(j % 5)]))
+            cols = WSCHEMA[t]
+            cid = cols[int(rng.integers(0, len(cols)))]
+            if cid in ("text", "blob"):
+                n = int(rng.integers(0, 50))
+                val = "t" * n if cid == "text" else bytes([j]) * n
+            else:
+                val = int(rng.integers(0, 3)) if cid == "int" else 0.5
+            ch.append(Change(t, pk, cid, val, int(rng.integers(1, 3)), v, k, a, 1))
+        msgs.append(ChangeV1(a, Full(v, ch, (0, len(ch) - 1), len(ch) - 1, ts=v)))
+    x = ca.agent.Agent(WSCHEMA, capacity_hint=1 << 12, interned=("testsblob", "wide"))
+    y = ca.agent.Agent(WSCHEMA, capacity_hint=1 << 12, interned=("testsblob", "wide"))
+    for a in ACT:
+        x.site(a)
+        y.site(a)
+    rx = x.process_multiple_changes(msgs)
+    ry, st = y.process_frames(wire.frames(msgs))
+    assert (st == 0).all() and rx.known == ry.known
+    cx, cy = canon(x.engine), canon(y.engine)
+    assert cx == cy
+    assert any(isinstance(row[4], bytes) for row in cx)          # long values present
+    assert any(isinstance(row[1], bytes) for row in cx)          # interned pks present
