@@ -249,6 +249,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
     alg_bytes = ALG_BYTES_PER_CHANGE * n + ALG_BYTES_PER_CELL * cells
     achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
     steady = steady_state(eng, prep, n, dev, dt / args.steps * 1e3, cells)
+    e2e = host_batch_e2e(eng, batch, n)
     cpu = None if args.no_cpu_baseline else cpu_baseline(batch)
     line = {
         "metric": METRIC,
@@ -276,9 +277,33 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
                      "dominant": max(kern, key=kern.get)},
         "cpu_baseline": cpu,
         "steady_state": steady,
+        "end_to_end_h2d": e2e,
     }
     print(json.dumps(line), flush=True)
     eng.close()
+
+
+def host_batch_e2e(eng, batch, n, reps=3):
+    """SURVEY §8(d)'s end-to-end figure: the same batch handed over in host memory (numpy arrays, as
+    a Rust caller's Vec<Change> columns), so the apply includes the H2D copies of every field.
+    Never `value` (the contract measures device-resident inputs)."""
+    import torch
+    host = {k: v.cpu().numpy() for k, v in batch.items()}
+    prep = eng.prepare(host)
+    ms = []
+    for _ in range(reps):
+        eng.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.apply_prepared(prep)
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) * 1e3)
+    ms.sort()
+    med = ms[len(ms) // 2]
+    del host, prep
+    return {"ms": med, "changes_per_s": n / (med * 1e-3),
+            "note": "config-2 batch from pageable host memory (H2D of every SoA field inside the apply call), "
+                    f"empty state, median of {reps}"}
 
 
 def steady_state(eng, prep, n, dev, empty_ms, cells, reps=3):

@@ -325,7 +325,7 @@ static int store_alloc(corro_ctx *ctx, uint64_t capacity_hint) {
     TRY(ctx->d_used.ensure(B * 4ULL));
     TRY(ctx->d_gen.ensure(B * 4ULL));
     TRY(ctx->d_heap_top.ensure(8));
-    ctx->heap_cap = std::max<uint64_t>(1ULL << 16, capacity_hint / 2);
+    ctx->heap_cap = std::min<uint64_t>(1ULL << 31, std::max<uint64_t>(1ULL << 16, capacity_hint / 2));
     TRY(ctx->d_heap.ensure(ctx->heap_cap * sizeof(Rec)));
     return CORRO_OK;
 }
@@ -402,8 +402,9 @@ int grow_heap(corro_ctx *ctx, uint64_t want_records) {
     if (want_records <= ctx->heap_cap) return CORRO_OK;
     uint64_t cap = ctx->heap_cap;
     while (cap < want_records) cap *= 2;
-    if (cap > (1ULL << 32)) cap = 1ULL << 32;
-    if (cap < want_records) return fail(CORRO_E_RANGE, "row store heap would exceed 2^32 records");
+    // (heap indices stay below 2^31: the fast bodies mark a new row's heap offset with the top bit)
+    if (cap > (1ULL << 31)) cap = 1ULL << 31;
+    if (cap < want_records) return fail(CORRO_E_RANGE, "row store heap would exceed 2^31 records");
     hipStream_t s = ctx->stream;
     unsigned long long top = 0;
     CORRO_HIP_TRY(hipMemcpyAsync(&top, ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost, s));

@@ -1068,21 +1068,36 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
 
 // Row resolution shared by the fast bodies, run by the whole workgroup after the batch winners
 // (alive) are known. s_own: FAST_SLOTS words of LDS scratch; keys of record i: s_pk[i] and
-// s_tc[i] >> 16. Leaves row[k] (record index of the row's owner), the owner's heap index in
-// s_heap[owner] and its prior presence word in s_bits[owner]; owner lanes keep their region entry
-// in ent[k]. Returns false when the bucket was deferred (nothing written).
+// s_tc[i] >> 16. Leaves row[k] (record index of the row's owner), the owner's heap word in
+// s_heap[owner] (row_heap() gives the heap index) and its prior presence word in s_bits[owner];
+// owner lanes keep their region entry in ent[k] (a new row's is claimed here, after the bucket is
+// known to fit). The workgroup owns region b during the fast bodies, so the region is probed with
+// plain loads -- skipped altogether while the region is empty (used0 = its fill at apply start) --
+// and a new row claims the first empty slot its probe met with one CAS. Returns false when the
+// bucket was deferred (nothing written).
+__device__ inline uint32_t row_heap(uint32_t w, unsigned long long hbase) {
+    return (w & 0x80000000u) ? (uint32_t)hbase + (w & 0x7FFFFFFFu) : w;
+}
+
 template <int R>
-__device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, const bool (&alive)[R], uint32_t (&row)[R],
-                                 uint32_t (&ent)[R], const uint64_t *s_pk, const uint32_t *s_tc, uint32_t *s_own,
-                                 uint32_t *s_heap, uint64_t *s_bits, uint32_t *s_ctl, unsigned long long *s_hbase) {
+__device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0, const bool (&alive)[R],
+                                 uint32_t (&row)[R], uint32_t (&ent)[R], const uint64_t *s_pk, const uint32_t *s_tc,
+                                 uint32_t *s_own, uint32_t *s_heap, uint64_t *s_bits, uint32_t *s_ctl,
+                                 unsigned long long *s_hbase) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
     if (tid == 0) s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
     __syncthreads();
+    // rows: the first claimer owns a row and looks it up in the region at once (read-only; a new
+    // row's heap offset gets the top bit until the allocation). The heap words wait in registers
+    // until the row table (s_own, which s_heap may alias) is no longer probed.
+    uint32_t e0[R], hw[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
         row[k] = 0;
         ent[k] = ROW_NONE;
+        e0[k] = 0;
+        hw[k] = 0;
         if (!alive[k]) continue;
         const uint32_t i = k * MERGE_THREADS + tid;
         const uint64_t pk = s_pk[i];
@@ -1101,55 +1116,48 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, const bool (&al
             }
             slot = (slot + 1) & (FAST_SLOTS - 1);
         }
-    }
-    __syncthreads();
-    // owners: read-only lookups; new rows counted (their heap offsets in s_heap until allocation)
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
-        if (!alive[k] || row[k] != i) continue;
-        const uint32_t t = s_tc[i] >> 16;
-        const uint32_t e = rs_lookup(a.rs, b, s_pk[i], t);
+        if (row[k] != i) continue;
+        const uint32_t e = used0 ? rs_probe(a.rs, b, pk, t, e0[k]) : ROW_NONE;
+        if (!used0) e0[k] = region_slot(pk, t, a.rs.log2S);
         if (e != ROW_NONE) {
-            s_heap[i] = a.rs.ent[e].heap;
+            hw[k] = a.rs.ent[e].heap;
             s_bits[i] = a.rs.ent[e].bits[0];
             ent[k] = e;
         } else {
-            s_heap[i] = atomicAdd(&s_ctl[1], (uint32_t)a.rs.stride[t]);
+            hw[k] = 0x80000000u | atomicAdd(&s_ctl[1], (uint32_t)a.rs.stride[t]);
             s_bits[i] = 0;
             atomicAdd(&s_ctl[0], 1u);
             ent[k] = ROW_NONE - 1;  // marks "owner of a new row"
         }
     }
     __syncthreads();
+#pragma unroll
+    for (int k = 0; k < R; k++)
+        if (ent[k] != ROW_NONE) s_heap[k * MERGE_THREADS + tid] = hw[k];
     if (tid == 0) {
-        bool ok = a.rs.used[b] + s_ctl[0] <= a.rs.fill;
+        bool ok = used0 + s_ctl[0] <= a.rs.fill;
         unsigned long long h = 0;
         if (ok && s_ctl[1]) {
             h = rs_heap_alloc(a.rs, s_ctl[1]);
             ok = h != ~0ULL;
         }
         if (!ok) {
-            push_defer(a, b, a.rs.used[b] + s_ctl[0] <= a.rs.fill ? DEFER_HEAP : DEFER_REGION);
+            push_defer(a, b, used0 + s_ctl[0] <= a.rs.fill ? DEFER_HEAP : DEFER_REGION);
             s_ctl[2] = 1;
         } else {
-            a.rs.used[b] += s_ctl[0];
+            a.rs.used[b] = used0 + s_ctl[0];
             *s_hbase = h;
         }
     }
     __syncthreads();
     if (s_ctl[2]) return false;
-    // new rows: heap slot, region entry (presence bits published at the end)
+    // new rows: their region entries (presence bits published by the caller at the end)
 #pragma unroll
     for (int k = 0; k < R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
         if (ent[k] != ROW_NONE - 1) continue;
-        const uint32_t hb = (uint32_t)*s_hbase + s_heap[i];
-        s_heap[i] = hb;
-        const uint64_t z[2] = {0, 0};
-        ent[k] = rs_insert(a.rs, b, s_pk[i], s_tc[i] >> 16, hb, z);
+        ent[k] = rs_claim(a.rs, b, e0[k], s_pk[i], s_tc[i] >> 16, row_heap(hw[k], *s_hbase));
     }
-    __syncthreads();
     return true;
 }
 
@@ -1183,6 +1191,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     uint4 q[FAST_R][4];
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
     if (tid == 0) s_live = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
     uint32_t srank[FAST_R];
@@ -1270,7 +1279,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     }
     // rows of the winners (s_own: row table, then heap indices; s_k: presence words)
     uint32_t row[FAST_R], ent[FAST_R];
-    if (!fast_rows<FAST_R>(a, b, alive, row, ent, s_pk, s_tc, s_own, s_own, s_k, s_ctl, &s_hbase)) return;
+    if (!fast_rows<FAST_R>(a, b, used0, alive, row, ent, s_pk, s_tc, s_own, s_own, s_k, s_ctl, &s_hbase)) return;
     // winners vs the prior clock of their cell; new cells set their presence bit
     uint32_t hb[FAST_R];
     uint32_t nlive = 0;
@@ -1280,7 +1289,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         if (!alive[k]) continue;
         const uint32_t i = k * MERGE_THREADS + tid;
         const uint32_t c = s_tc[i] & 0xFFFFu;
-        hb[k] = s_own[row[k]] + c;
+        hb[k] = row_heap(s_own[row[k]], s_hbase) + c;
         if ((s_k[row[k]] >> c) & 1ULL) {
             const Rec pr = load_rec(a.rs.heap + hb[k]);
             int cmp;
@@ -1368,6 +1377,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     uint4 q[FAST_R][4];
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
     if (tid == 0) s_live = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
 #pragma unroll
@@ -1415,13 +1425,13 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     }
     __syncthreads();
     // 1b. rows of every change, prior clocks: does the change beat its cell's prior?
-    if (!fast_rows<FAST_R>(a, b, alive, row, ent, s_pk, s_tc, s_own, s_own, s_v0, s_ctl, &s_hbase)) return;
+    if (!fast_rows<FAST_R>(a, b, used0, alive, row, ent, s_pk, s_tc, s_own, s_own, s_v0, s_ctl, &s_hbase)) return;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
         if (!alive[k]) continue;
         const uint32_t c = tc[k] & 0xFFFFu;
-        hb[k] = s_own[row[k]] + c;
+        hb[k] = row_heap(s_own[row[k]], s_hbase) + c;
         if ((s_v0[row[k]] >> c) & 1ULL) {
             const Rec pr = load_rec(a.rs.heap + hb[k]);
             const int64_t bcv = (int64_t)(cv[k] ^ 0x8000000000000000ULL);
@@ -1584,6 +1594,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     uint4 q[FAST_R][4];
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
     if (tid == 0) s_live = 0;
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
 #pragma unroll
@@ -1629,13 +1640,13 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     }
     __syncthreads();
     // 1b. rows of every change, prior clocks: does the change beat its cell's prior?
-    if (!fast_rows<FAST_R>(a, b, alive, row, ent, s_a, s_b, s_own, s_own, s_c, s_ctl, &s_hbase)) return;
+    if (!fast_rows<FAST_R>(a, b, used0, alive, row, ent, s_a, s_b, s_own, s_own, s_c, s_ctl, &s_hbase)) return;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
         if (!alive[k]) continue;
         const uint32_t c = tc[k] & 0xFFFFu;
-        hb[k] = s_own[row[k]] + c;
+        hb[k] = row_heap(s_own[row[k]], s_hbase) + c;
         if ((s_c[row[k]] >> c) & 1ULL) {
             const Rec pr = load_rec(a.rs.heap + hb[k]);
             if (prior_cmp_int(a, pr, cv[k], v0[k], rank[k]) > 0) flags |= 1u << (2 * k);

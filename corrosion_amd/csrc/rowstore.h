@@ -69,6 +69,38 @@ __device__ inline uint32_t rs_lookup(const RowStore &rs, uint32_t b, uint64_t pk
     return ROW_NONE;
 }
 
+// rs_lookup that also reports the first empty slot its probe met (the slot a new row of this key
+// claims first), as a local slot index.
+__device__ inline uint32_t rs_probe(const RowStore &rs, uint32_t b, uint64_t pk, uint32_t table, uint32_t &empty) {
+    const uint32_t S = 1u << rs.log2S, m = S - 1;
+    const RowEnt *reg = rs.ent + ((size_t)b << rs.log2S);
+    uint32_t s = region_slot(pk, table, rs.log2S);
+    for (uint32_t k = 0; k < S; k++, s = (s + 1) & m) {
+        const uint32_t tag = reg[s].tag;
+        if (tag == 0) {
+            empty = s;
+            return ROW_NONE;
+        }
+        if (tag == table + 1 && reg[s].pk == pk) return (b << rs.log2S) | s;
+    }
+    empty = region_slot(pk, table, rs.log2S);
+    return ROW_NONE;
+}
+
+// rs_insert from a slot known to have been empty at the probe (one CAS when no other new row of
+// the workgroup took it); the entry's presence bits start at zero.
+__device__ inline uint32_t rs_claim(const RowStore &rs, uint32_t b, uint32_t s, uint64_t pk, uint32_t table,
+                                    uint32_t heap) {
+    const uint32_t m = (1u << rs.log2S) - 1;
+    RowEnt *reg = rs.ent + ((size_t)b << rs.log2S);
+    while (atomicCAS(&reg[s].tag, 0u, table + 1) != 0u) s = (s + 1) & m;
+    reg[s].pk = pk;
+    reg[s].heap = heap;
+    reg[s].bits[0] = 0;
+    reg[s].bits[1] = 0;
+    return (b << rs.log2S) | s;
+}
+
 // Claim an empty slot of region b for a row known to be absent. Inserters race each other only for
 // empty slots (one CAS on the tag); nothing looks a new row's slot up while it is written: a lookup
 // runs only for rows that existed when the apply began, and such a row's probe path (its home slot up

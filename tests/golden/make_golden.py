@@ -13,6 +13,18 @@ Sources (data only, no reference code is copied):
   * chunker_kats — the cases of test_change_chunker, /root/reference/crates/corro-types/src/change.rs:
                    266-401: Change { seq, ..Default::default() } (empty table/cid/pk, Null value), so
                    every change's estimated_byte_size is the same; max_buf_size is given in changes.
+  * agent_kats   — two end-to-end scenarios over corro-tests' TEST_SCHEMA
+                   (/root/reference/crates/corro-tests/src/lib.rs:13-53):
+                   process_failed_changes, /root/reference/crates/corro-agent/src/agent/tests.rs:
+                   877-999 (the bad-cid version rolled back alone; db_version / site of pks 1..5 as
+                   asserted at :970-992; pk 6 absent), and test_handle_need,
+                   /root/reference/crates/corro-agent/src/api/peer/mod.rs:1729-2321 (every
+                   process_multiple_changes call and every handle_need with the messages the test
+                   receives, in order). The reference draws the `wide` rows' int / float / blob from
+                   rand::thread_rng; fixed stand-ins are recorded here (the assertions compare the
+                   served changes with the applied ones, whatever their values). Change notation:
+                   [table, pk, cid, value, col_version, db_version, seq, cl], pk = an int (one packed
+                   INTEGER) or {"pack": [hex blob | {"text": s} | int, ...]} (pack_columns).
 
 Merge-case notation: table t(id INTEGER PK, a, b, c); cid 0 = sentinel '-1', a=1, b=2, c=3.
 Sites sN = sixteen bytes of value N. A change is [cid, value, col_version, db_version, site, cl];
@@ -167,6 +179,66 @@ CHUNKER = [
 ]
 
 
+def _hn_changes():
+    """test_handle_need's changes (peer/mod.rs:1757-1781, :1908-1918, :2040-2050, :2076-2108)."""
+    c1 = ["tests", 1, "text", T("one"), 1, 1, 0, 1]
+    c2 = ["tests", 2, "text", T("two"), 1, 2, 0, 1]
+    c3 = ["tests", 1, "text", T("one override"), 2, 3, 0, 1]
+    c4 = ["tests", 2, "text", T("two override"), 2, 4, 0, 1]
+    wide, seq = [], 0
+    for i in range(10):
+        grp = []
+        pk = {"pack": [i.to_bytes(8, "big").hex(), {"text": str(i)}]}
+        vals = [("int", I((i * 7919 - 31337) * 104729)), ("float", R(i * 0.125 - 0.5)),
+                ("blob", B(bytes((i * 37 + k * 11) % 256 for k in range(16)).hex()))]
+        for col, v in vals:
+            grp.append(["wide", pk, col, v, 1, 5, seq, 1])
+            seq += 1
+        wide.append(grp)
+    return c1, c2, c3, c4, wide
+
+
+def agent_kats():
+    ta2 = "11" * 16   # the serving agent's actor (ta2's site id in the reference test)
+    bad = "0000000000000000a716446655440000"  # Uuid 00000000-0000-0000-a716-446655440000
+    failed = {
+        "source": "corro-agent/src/agent/tests.rs:877-999",
+        "ta2": ta2, "bad_actor": bad,
+        # ta2's five INSERT OR REPLACE INTO tests (id, text) VALUES (i, 'service-text') versions
+        "good": [{"actor": ta2, "version": i, "changes": [["tests", i, "text", T("service-text"), 1, i, 0, 1]],
+                  "seqs": [0, 0], "last_seq": 0} for i in range(1, 6)],
+        "bad": {"actor": bad, "version": 1, "seqs": [0, 1], "last_seq": 1,
+                "changes": [["tests", 6, "text", T("six"), 1, 6, 0, 1], ["tests", 6, "nonexistent", T("six"), 1, 6, 1, 1]]},
+        # :970-992: crsql_changes db_version of pk i with site_id = ta2 is i; :994-998: no row 6
+        "expect_dbv": {str(i): i for i in range(1, 6)}, "expect_absent": [6],
+    }
+    c1, c2, c3, c4, wide = _hn_changes()
+    last = 29
+
+    def full(v, ch, seqs, last_seq=0):
+        return {"kind": "full", "version": v, "changes": ch, "seqs": seqs, "last_seq": last_seq}
+    flat = [c for g in wide for c in g]
+    steps = [
+        {"process": [full(1, [c1], [0, 0]), full(2, [c2], [0, 0])]},
+        {"need": {"full": [1, 1]}, "expect": [full(1, [c1], [0, 0])]},
+        {"need": {"partial": 2, "seqs": [[0, 0]]}, "expect": [full(2, [c2], [0, 0])]},
+        {"process": [full(3, [c3], [0, 0])]},
+        {"need": {"partial": 1, "seqs": [[0, 0]]}, "expect": [{"kind": "empty", "versions": [1, 1]}]},
+        {"need": {"full": [1, 6]}, "expect_prefix": [full(3, [c3], [0, 0]), full(2, [c2], [0, 0]),
+                                                     {"kind": "empty", "versions": [1, 1]}]},
+        {"process": [full(4, [c4], [0, 0])]},
+        {"process": [full(5, g, [g[0][6], g[-1][6]], last) for g in wide]},
+        {"need": {"full": [1, 1000]}, "expect_prefix": [full(4, [c4], [0, 0]), full(3, [c3], [0, 0]),
+                                                        full(5, flat, [0, last], last),
+                                                        {"kind": "empty", "versions": [1, 2]}]},
+        {"need": {"partial": 5, "seqs": [[4, 7]]}, "expect": [full(5, flat[4:8], [4, 7], last)]},
+        {"need": {"partial": 5, "seqs": [[2, 2], [15, 24]]},
+         "expect": [full(5, flat[2:3], [2, 2], last), full(5, flat[15:25], [15, 24], last)]},
+    ]
+    handle = {"source": "corro-agent/src/api/peer/mod.rs:1729-2321", "actor": "ab" * 16, "ts": 7, "steps": steps}
+    return {"process_failed_changes": failed, "handle_need": handle}
+
+
 def main():
     merge = [{"name": n, "changes": c, "rows": r, "impacted": imp} for (n, c, r, imp) in MERGE]
     with open(os.path.join(HERE, "merge_kats.json"), "w") as f:
@@ -178,6 +250,8 @@ def main():
         json.dump({"source": "corro-types/src/agent.rs:1605-1868", "steps": GAPS}, f, indent=1)
     with open(os.path.join(HERE, "chunker_kats.json"), "w") as f:
         json.dump({"source": "corro-types/src/change.rs:266-401", "cases": CHUNKER}, f, indent=1)
+    with open(os.path.join(HERE, "agent_kats.json"), "w") as f:
+        json.dump(agent_kats(), f, indent=1)
 
 
 if __name__ == "__main__":
