@@ -1066,57 +1066,63 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
 // prior is earlier in application order: it keeps ties). Rows of the winners are resolved in the
 // region (lookups, then inserts of new rows once the region and heap are known to have room).
 
-// Row resolution shared by the fast bodies, run by the whole workgroup after the batch winners
-// (alive) are known. s_own: FAST_SLOTS words of LDS scratch; keys of record i: s_pk[i] and
-// s_tc[i] >> 16. Leaves row[k] (record index of the row's owner), the owner's heap word in
-// s_heap[owner] (row_heap() gives the heap index) and its prior presence word in s_bits[owner];
-// owner lanes keep their region entry in ent[k] (a new row's is claimed here, after the bucket is
-// known to fit). The workgroup owns region b during the fast bodies, so the region is probed with
+// Cell and row of record i in one probe: the cell table (s_own, keys (pk, table_cid) of the claiming
+// record) is probed from the ROW's home slot, so the first record of the same row met in probe order
+// -- the same one for every record of the row, since a slot once claimed keeps its occupant and a
+// record claims the first empty slot it meets -- names the row (or record i, when it claims a slot
+// before meeting one). No second table, no second pass.
+__device__ inline void cell_row_claim(uint32_t *s_own, const uint64_t *s_pk, const uint32_t *s_tc, uint32_t i,
+                                      uint64_t pk, uint32_t tc, uint32_t &cell, uint32_t &row) {
+    const uint32_t t = tc >> 16;
+    uint32_t slot = row_hash(pk, t) & (FAST_SLOTS - 1);
+    uint32_t r = ~0u;
+    while (true) {
+        const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
+        if (o == 0) {
+            cell = i;
+            row = r == ~0u ? i : r;
+            return;
+        }
+        const uint32_t x = o - 1;
+        if (s_pk[x] == pk && (s_tc[x] >> 16) == t) {
+            if (r == ~0u) r = x;
+            if (s_tc[x] == tc) {
+                cell = x;
+                row = r;
+                return;
+            }
+        }
+        slot = (slot + 1) & (FAST_SLOTS - 1);
+    }
+}
+
+// Row resolution shared by the fast bodies, run by the whole workgroup once the cell table is no
+// longer probed (s_heap may alias it). row[k]: the row's record (cell_row_claim); the lane holding
+// it (valid, row[k] == i) looks the row up and keeps its region entry in ent[k]; the row's heap word
+// goes to s_heap[row] (row_heap() gives the heap index) and its prior presence word to
+// s_bits[row]. The workgroup owns region b during the fast bodies, so the region is probed with
 // plain loads -- skipped altogether while the region is empty (used0 = its fill at apply start) --
-// and a new row claims the first empty slot its probe met with one CAS. Returns false when the
-// bucket was deferred (nothing written).
+// and a new row claims the first empty slot its probe met with one CAS, after the bucket is known to
+// fit. Returns false when the bucket was deferred (nothing written). s_ctl[0..2] must be zero.
 __device__ inline uint32_t row_heap(uint32_t w, unsigned long long hbase) {
     return (w & 0x80000000u) ? (uint32_t)hbase + (w & 0x7FFFFFFFu) : w;
 }
 
 template <int R>
-__device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0, const bool (&alive)[R],
-                                 uint32_t (&row)[R], uint32_t (&ent)[R], const uint64_t *s_pk, const uint32_t *s_tc,
-                                 uint32_t *s_own, uint32_t *s_heap, uint64_t *s_bits, uint32_t *s_ctl,
-                                 unsigned long long *s_hbase) {
+__device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0, uint32_t n, const uint32_t (&row)[R],
+                                 uint32_t (&ent)[R], const uint64_t *s_pk, const uint32_t *s_tc, uint32_t *s_heap,
+                                 uint64_t *s_bits, uint32_t *s_ctl, unsigned long long *s_hbase) {
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
-    if (tid == 0) s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
-    __syncthreads();
-    // rows: the first claimer owns a row and looks it up in the region at once (read-only; a new
-    // row's heap offset gets the top bit until the allocation). The heap words wait in registers
-    // until the row table (s_own, which s_heap may alias) is no longer probed.
     uint32_t e0[R], hw[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
-        row[k] = 0;
+        const uint32_t i = k * MERGE_THREADS + tid;
         ent[k] = ROW_NONE;
         e0[k] = 0;
         hw[k] = 0;
-        if (!alive[k]) continue;
-        const uint32_t i = k * MERGE_THREADS + tid;
+        if (i >= n || row[k] != i) continue;
         const uint64_t pk = s_pk[i];
         const uint32_t t = s_tc[i] >> 16;
-        uint32_t slot = row_hash(pk, t) & (FAST_SLOTS - 1);
-        while (true) {
-            uint32_t o = __hip_atomic_load(&s_own[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (o == 0) o = atomicCAS(&s_own[slot], 0u, i + 1);
-            if (o == 0) {
-                row[k] = i;
-                break;
-            }
-            if (s_pk[o - 1] == pk && (s_tc[o - 1] >> 16) == t) {
-                row[k] = o - 1;
-                break;
-            }
-            slot = (slot + 1) & (FAST_SLOTS - 1);
-        }
-        if (row[k] != i) continue;
         const uint32_t e = used0 ? rs_probe(a.rs, b, pk, t, e0[k]) : ROW_NONE;
         if (!used0) e0[k] = region_slot(pk, t, a.rs.log2S);
         if (e != ROW_NONE) {
@@ -1184,7 +1190,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     const uint32_t tid = threadIdx.x;
     const uint32_t n = v.nn;
     uint64_t cv[FAST_R], v0[FAST_R], v1[FAST_R], rp[FAST_R], dbv[FAST_R];
-    uint32_t meta[FAST_R], cell[FAST_R], seq[FAST_R], site[FAST_R];
+    uint32_t meta[FAST_R], cell[FAST_R], seq[FAST_R], site[FAST_R], row[FAST_R];
     bool alive[FAST_R];
     // every record load of this lane is issued before the first wait (one memory latency per
     // bucket instead of one per record group), then the site-rank lookups as one more batch
@@ -1192,7 +1198,10 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
-    if (tid == 0) s_live = 0;
+    if (tid == 0) {
+        s_live = 0;
+        s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
+    }
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
     uint32_t srank[FAST_R];
 #pragma unroll
@@ -1222,23 +1231,10 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
+        row[k] = 0;
         if (!alive[k]) continue;
-        const uint64_t pk = s_pk[i];
-        const uint32_t tc = s_tc[i];
-        uint32_t slot = cell_hash(pk, tc) & (FAST_SLOTS - 1);
-        while (true) {
-            const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
-            if (o == 0) {
-                cell[k] = i;
-                s_k[i] = 0;
-                break;
-            }
-            if (s_pk[o - 1] == pk && s_tc[o - 1] == tc) {
-                cell[k] = o - 1;
-                break;
-            }
-            slot = (slot + 1) & (FAST_SLOTS - 1);
-        }
+        cell_row_claim(s_own, s_pk, s_tc, i, s_pk[i], s_tc[i], cell[k], row[k]);
+        if (cell[k] == i) s_k[i] = 0;
     }
     __syncthreads();
     // argmax stages: INTEGER-only: col_version, value, site|pos. Mixed: + rank, word 1, length.
@@ -1277,9 +1273,9 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
             __syncthreads();
         }
     }
-    // rows of the winners (s_own: row table, then heap indices; s_k: presence words)
-    uint32_t row[FAST_R], ent[FAST_R];
-    if (!fast_rows<FAST_R>(a, b, used0, alive, row, ent, s_pk, s_tc, s_own, s_own, s_k, s_ctl, &s_hbase)) return;
+    // rows (s_own: heap words by row record; s_k: presence words)
+    uint32_t ent[FAST_R];
+    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_k, s_ctl, &s_hbase)) return;
     // winners vs the prior clock of their cell; new cells set their presence bit
     uint32_t hb[FAST_R];
     uint32_t nlive = 0;
@@ -1378,7 +1374,10 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
-    if (tid == 0) s_live = 0;
+    if (tid == 0) {
+        s_live = 0;
+        s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
+    }
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1404,28 +1403,17 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) rank[k] = site[k] < a.nsites ? rank[k] : 0u;
     __syncthreads();
-    // 1. cells: open addressing on (pk, table_cid), owner = first claimer
+    // 1. cells and rows: open addressing on (pk, table_cid) from the row's home slot
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
+        row[k] = 0;
         if (!alive[k]) continue;
-        uint32_t slot = cell_hash(pk[k], tc[k]) & (FAST_SLOTS - 1);
-        while (true) {
-            const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
-            if (o == 0) {
-                cell[k] = i;
-                break;
-            }
-            if (s_pk[o - 1] == pk[k] && s_tc[o - 1] == tc[k]) {
-                cell[k] = o - 1;
-                break;
-            }
-            slot = (slot + 1) & (FAST_SLOTS - 1);
-        }
+        cell_row_claim(s_own, s_pk, s_tc, i, pk[k], tc[k], cell[k], row[k]);
     }
     __syncthreads();
-    // 1b. rows of every change, prior clocks: does the change beat its cell's prior?
-    if (!fast_rows<FAST_R>(a, b, used0, alive, row, ent, s_pk, s_tc, s_own, s_own, s_v0, s_ctl, &s_hbase)) return;
+    // 1b. row lookups, prior clocks: does the change beat its cell's prior?
+    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_v0, s_ctl, &s_hbase)) return;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
@@ -1595,7 +1583,10 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
-    if (tid == 0) s_live = 0;
+    if (tid == 0) {
+        s_live = 0;
+        s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
+    }
     for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1619,28 +1610,17 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) rank[k] = site[k] < a.nsites ? rank[k] : 0u;
     __syncthreads();
-    // 1. cells: open addressing on (pk, table_cid), owner = first claimer
+    // 1. cells and rows: open addressing on (pk, table_cid) from the row's home slot
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
+        row[k] = 0;
         if (!alive[k]) continue;
-        uint32_t slot = cell_hash(pk[k], tc[k]) & (FAST_SLOTS - 1);
-        while (true) {
-            const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
-            if (o == 0) {
-                cell[k] = i;
-                break;
-            }
-            if (s_a[o - 1] == pk[k] && s_b[o - 1] == tc[k]) {
-                cell[k] = o - 1;
-                break;
-            }
-            slot = (slot + 1) & (FAST_SLOTS - 1);
-        }
+        cell_row_claim(s_own, s_a, s_b, i, pk[k], tc[k], cell[k], row[k]);
     }
     __syncthreads();
-    // 1b. rows of every change, prior clocks: does the change beat its cell's prior?
-    if (!fast_rows<FAST_R>(a, b, used0, alive, row, ent, s_a, s_b, s_own, s_own, s_c, s_ctl, &s_hbase)) return;
+    // 1b. row lookups, prior clocks: does the change beat its cell's prior?
+    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase)) return;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
