@@ -319,7 +319,8 @@ static int store_alloc(corro_ctx *ctx, uint64_t capacity_hint) {
     const uint32_t B = ctx->B;
     const uint64_t rows = std::max<uint64_t>(1024, capacity_hint / 4);
     uint32_t lg = 4;
-    while (((uint64_t)B << lg) < 2 * rows && lg < 20) lg++;
+    // (region entries are named by 32-bit indices: B << log2S stays <= 2^31)
+    while (((uint64_t)B << lg) < 2 * rows && lg < 20 && ((uint64_t)B << (lg + 1)) <= (1ULL << 31)) lg++;
     ctx->log2S = lg;
     TRY(ctx->d_ent.ensure(((size_t)B << lg) * sizeof(RowEnt)));
     TRY(ctx->d_used.ensure(B * 4ULL));
@@ -380,7 +381,8 @@ static int arena_reserve(corro_ctx *ctx, uint64_t add) {
 // writes are in flight). Entry indices change; heap indices and presence bits move with the rows.
 int grow_regions(corro_ctx *ctx, uint32_t new_log2S) {
     if (new_log2S <= ctx->log2S) return CORRO_OK;
-    if (new_log2S > 26) return fail(CORRO_E_NOMEM, "row store regions would exceed 2^26 slots");
+    if (new_log2S > 26 || ((uint64_t)ctx->B << new_log2S) > (1ULL << 31))
+        return fail(CORRO_E_NOMEM, "row store regions would exceed 2^31 entries");
     hipStream_t s = ctx->stream;
     DevBuf nb;
     TRY(nb.ensure(((size_t)ctx->B << new_log2S) * sizeof(RowEnt)));
@@ -820,7 +822,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     uint64_t rows_cap = ((uint64_t)B << ctx->log2S) / 2;
     if (ctx->state_total > rows_cap) {
         uint32_t lg = ctx->log2S;
-        while (((uint64_t)B << lg) / 2 < ctx->state_total && lg < 26) lg++;
+        while (((uint64_t)B << lg) / 2 < ctx->state_total && lg < 26 && ((uint64_t)B << (lg + 1)) <= (1ULL << 31)) lg++;
         TRY(grow_regions(ctx, lg));
     }
     return CORRO_OK;

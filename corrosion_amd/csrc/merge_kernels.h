@@ -1097,22 +1097,67 @@ __device__ inline void cell_row_claim(uint32_t *s_own, const uint64_t *s_pk, con
 }
 
 // Row resolution shared by the fast bodies, run by the whole workgroup once the cell table is no
-// longer probed (s_heap may alias it). row[k]: the row's record (cell_row_claim); the lane holding
-// it (valid, row[k] == i) looks the row up and keeps its region entry in ent[k]; the row's heap word
-// goes to s_heap[row] (row_heap() gives the heap index) and its prior presence word to
-// s_bits[row]. The workgroup owns region b during the fast bodies, so the region is probed with
-// plain loads -- skipped altogether while the region is empty (used0 = its fill at apply start) --
-// and a new row claims the first empty slot its probe met with one CAS, after the bucket is known to
-// fit. Returns false when the bucket was deferred (nothing written). s_ctl[0..2] must be zero.
+// longer probed (s_heap aliases its first CAP_FAST words, the claim bitmap the rest). row[k]: the
+// row's record (cell_row_claim); the lane holding it (valid, row[k] == i) looks the row up and keeps
+// its region entry in ent[k]; the row's heap word goes to s_heap[row] (row_heap() gives the heap
+// index) and its prior presence word to s_bits[row]. The workgroup owns region b during the fast
+// bodies, so the region is probed with plain loads -- not at all while it is empty (used0 = its fill
+// at apply start) -- and a new row takes the first empty slot its probe met unless another new row
+// of the workgroup took it first, decided by an LDS bitmap of the region's slots: no global atomic,
+// the entry written with plain stores (regions larger than the bitmap claim by CAS). `counted`: the
+// region was empty and fast_rows_count / fast_rows_alloc already ran. Returns false when the bucket
+// was deferred (nothing written). s_ctl[0..2] must be zero on entry unless counted.
+constexpr uint32_t RS_BM_WORDS = FAST_SLOTS - CAP_FAST;  // claim bitmap: regions of up to 32768 slots
+
 __device__ inline uint32_t row_heap(uint32_t w, unsigned long long hbase) {
     return (w & 0x80000000u) ? (uint32_t)hbase + (w & 0x7FFFFFFFu) : w;
+}
+
+// Empty region: every row of the bucket is new, so rows and heap records are counted (and each row's
+// heap offset noted) right after the cell hashing; thread 0 allocates after the next barrier, its
+// latency hidden behind the argmax.
+template <int R>
+__device__ inline void fast_rows_count(const MergeArgs &a, uint32_t n, const uint32_t (&row)[R], const uint32_t *s_tc,
+                                       uint32_t *s_heap, uint32_t *s_ctl) {
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (i >= n || row[k] != i) continue;
+        s_heap[i] = 0x80000000u | atomicAdd(&s_ctl[1], (uint32_t)a.rs.stride[s_tc[i] >> 16]);
+        atomicAdd(&s_ctl[0], 1u);
+    }
+}
+
+// thread 0: the region fill check and the heap allocation of the bucket's new rows (s_ctl[0] rows,
+// s_ctl[1] records); s_ctl[2] = 1 when the bucket defers.
+__device__ inline void fast_rows_alloc(const MergeArgs &a, uint32_t b, uint32_t used0, uint32_t *s_ctl,
+                                       unsigned long long *s_hbase) {
+    bool ok = used0 + s_ctl[0] <= a.rs.fill;
+    unsigned long long h = 0;
+    if (ok && s_ctl[1]) {
+        h = rs_heap_alloc(a.rs, s_ctl[1]);
+        ok = h != ~0ULL;
+    }
+    if (!ok) {
+        push_defer(a, b, used0 + s_ctl[0] <= a.rs.fill ? DEFER_HEAP : DEFER_REGION);
+        s_ctl[2] = 1;
+    } else {
+        a.rs.used[b] = used0 + s_ctl[0];
+        *s_hbase = h;
+    }
 }
 
 template <int R>
 __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0, uint32_t n, const uint32_t (&row)[R],
                                  uint32_t (&ent)[R], const uint64_t *s_pk, const uint32_t *s_tc, uint32_t *s_heap,
-                                 uint64_t *s_bits, uint32_t *s_ctl, unsigned long long *s_hbase) {
+                                 uint64_t *s_bits, uint32_t *s_ctl, unsigned long long *s_hbase, bool counted) {
     const uint32_t tid = threadIdx.x;
+    const uint32_t S = 1u << a.rs.log2S;
+    uint32_t *s_bm = s_heap + CAP_FAST;
+    const bool lds_claim = S <= 32 * RS_BM_WORDS;
+    if (lds_claim)
+        for (uint32_t w = tid; w < (S + 31) / 32; w += MERGE_THREADS) s_bm[w] = 0;
     uint32_t e0[R], hw[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
@@ -1123,6 +1168,13 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
         if (i >= n || row[k] != i) continue;
         const uint64_t pk = s_pk[i];
         const uint32_t t = s_tc[i] >> 16;
+        if (counted) {  // an empty region: new, heap word noted by fast_rows_count
+            hw[k] = s_heap[i];
+            s_bits[i] = 0;
+            e0[k] = region_slot(pk, t, a.rs.log2S);
+            ent[k] = ROW_NONE - 1;
+            continue;
+        }
         const uint32_t e = used0 ? rs_probe(a.rs, b, pk, t, e0[k]) : ROW_NONE;
         if (!used0) e0[k] = region_slot(pk, t, a.rs.log2S);
         if (e != ROW_NONE) {
@@ -1137,32 +1189,41 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
         }
     }
     __syncthreads();
+    if (!counted) {
 #pragma unroll
-    for (int k = 0; k < R; k++)
-        if (ent[k] != ROW_NONE) s_heap[k * MERGE_THREADS + tid] = hw[k];
-    if (tid == 0) {
-        bool ok = used0 + s_ctl[0] <= a.rs.fill;
-        unsigned long long h = 0;
-        if (ok && s_ctl[1]) {
-            h = rs_heap_alloc(a.rs, s_ctl[1]);
-            ok = h != ~0ULL;
-        }
-        if (!ok) {
-            push_defer(a, b, used0 + s_ctl[0] <= a.rs.fill ? DEFER_HEAP : DEFER_REGION);
-            s_ctl[2] = 1;
-        } else {
-            a.rs.used[b] = used0 + s_ctl[0];
-            *s_hbase = h;
-        }
+        for (int k = 0; k < R; k++)
+            if (ent[k] != ROW_NONE) s_heap[k * MERGE_THREADS + tid] = hw[k];
+        if (tid == 0) fast_rows_alloc(a, b, used0, s_ctl, s_hbase);
+        __syncthreads();
     }
-    __syncthreads();
     if (s_ctl[2]) return false;
     // new rows: their region entries (presence bits published by the caller at the end)
 #pragma unroll
     for (int k = 0; k < R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
         if (ent[k] != ROW_NONE - 1) continue;
-        ent[k] = rs_claim(a.rs, b, e0[k], s_pk[i], s_tc[i] >> 16, row_heap(hw[k], *s_hbase));
+        const uint32_t t = s_tc[i] >> 16, hb = row_heap(hw[k], *s_hbase);
+        if (!lds_claim) {
+            ent[k] = rs_claim(a.rs, b, e0[k], s_pk[i], t, hb);
+            continue;
+        }
+        uint32_t sl = e0[k];
+        while (true) {
+            const uint32_t bit = 1u << (sl & 31);
+            // slot e0 was empty at the probe; a later one only if its tag says so (no other
+            // workgroup writes the region, and this one's claims all go through the bitmap)
+            if (!(atomicOr(&s_bm[sl >> 5], bit) & bit) &&
+                (sl == e0[k] || !used0 || a.rs.ent[((size_t)b << a.rs.log2S) + sl].tag == 0))
+                break;
+            sl = (sl + 1) & (S - 1);
+        }
+        const uint32_t e = (b << a.rs.log2S) | sl;
+        RowEnt &re = a.rs.ent[e];
+        re.pk = s_pk[i];
+        re.tag = t + 1;
+        re.heap = hb;
+        re.bits[1] = 0;
+        ent[k] = e;
     }
     return true;
 }
@@ -1237,6 +1298,8 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         if (cell[k] == i) s_k[i] = 0;
     }
     __syncthreads();
+    // an empty region: all rows new -- counted now, allocated behind the argmax
+    if (!used0) fast_rows_count<FAST_R>(a, n, row, s_tc, s_own, s_ctl);
     // argmax stages: INTEGER-only: col_version, value, site|pos. Mixed: + rank, word 1, length.
     constexpr int nstages = WIDE ? 6 : 3;
 #pragma unroll
@@ -1260,6 +1323,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
             atomicMax(reinterpret_cast<unsigned long long *>(&s_k[cell[k]]), (unsigned long long)w[k]);
         }
         __syncthreads();
+        if (st == 0 && !used0 && tid == 0) fast_rows_alloc(a, b, used0, s_ctl, &s_hbase);
 #pragma unroll
         for (int k = 0; k < FAST_R; k++)
             if (alive[k]) alive[k] = s_k[cell[k]] == w[k];
@@ -1275,7 +1339,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     }
     // rows (s_own: heap words by row record; s_k: presence words)
     uint32_t ent[FAST_R];
-    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_k, s_ctl, &s_hbase)) return;
+    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_k, s_ctl, &s_hbase, used0 == 0)) return;
     // winners vs the prior clock of their cell; new cells set their presence bit
     uint32_t hb[FAST_R];
     uint32_t nlive = 0;
@@ -1413,7 +1477,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     }
     __syncthreads();
     // 1b. row lookups, prior clocks: does the change beat its cell's prior?
-    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_v0, s_ctl, &s_hbase)) return;
+    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_v0, s_ctl, &s_hbase, false)) return;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
@@ -1620,7 +1684,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     }
     __syncthreads();
     // 1b. row lookups, prior clocks: does the change beat its cell's prior?
-    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase)) return;
+    if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase, false)) return;
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
