@@ -9,7 +9,8 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcorro_hip.so")
+# CORRO_HIP_LIB: an alternative build of the same library (diagnostic variants, tools/)
+LIB_PATH = os.environ.get("CORRO_HIP_LIB") or os.path.join(HERE, "libcorro_hip.so")
 
 CORRO_OK = 0
 ERRORS = {-1: "CORRO_E_INVALID", -2: "CORRO_E_NOMEM", -3: "CORRO_E_DEVICE",

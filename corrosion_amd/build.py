@@ -39,19 +39,26 @@ def _stale():
         return f.read().strip() != _source_hash()
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, out=None, defines=()):
+    """Build LIB (or, with `out`/`defines`, a variant of it at `out`: diagnostics only)."""
+    if out is not None:
+        return _build_to(out, list(defines), verbose)
     if not force and not _stale():
         return LIB
+    return _build_to(LIB, [], verbose, stamp=True)
+
+
+def _build_to(lib, defines, verbose, stamp=False):
     src_hash = _source_hash()  # of the sources this build compiles (not of later edits)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     from concurrent.futures import ThreadPoolExecutor
     jobs = []
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src + ".o")
+        obj = os.path.join(os.path.dirname(lib), os.path.basename(lib) + "." + src + ".o")
         # (-Wno-unused-function: the host pass of a .hip file reports the static kernels of a shared
         # header that the file does not launch itself)
-        cmd = [hipcc] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", os.path.join(CSRC, src),
+        cmd = [hipcc] + FLAGS + defines + ["-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", os.path.join(CSRC, src),
                                  "-o", obj]
         if src.endswith(".cpp"):
             cmd = [hipcc, "-O3", "-std=c++17", "-fPIC", "-Wall", "-x", "c++",
@@ -64,14 +71,15 @@ def build(force=False, verbose=False):
     with ThreadPoolExecutor(workers) as ex:
         for f in [ex.submit(subprocess.check_call, c) for c in jobs]:
             f.result()
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.check_call([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    with open(STAMP, "w") as f:
-        f.write(src_hash)
-    return LIB
+    if stamp:
+        with open(STAMP, "w") as f:
+            f.write(src_hash)
+    return lib
 
 
 if __name__ == "__main__":

@@ -816,6 +816,11 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, MISC_WORDS * 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     ctx->state_total += ctx->h_misc[MISC_LIVE];  // (a signed delta in two's complement)
+#if CORRO_DIAG & 64
+    fprintf(stderr, "DIAG phases (us per bucket, 100 MHz wall clock): %.3f %.3f %.3f %.3f %.3f %.3f\n",
+            ctx->h_misc[10] / 100.0 / B, ctx->h_misc[11] / 100.0 / B, ctx->h_misc[12] / 100.0 / B,
+            ctx->h_misc[13] / 100.0 / B, ctx->h_misc[14] / 100.0 / B, ctx->h_misc[15] / 100.0 / B);
+#endif
     ctx->state_epoch++;
     if (ctx->h_misc[MISC_WIDE]) ctx->state_wide = true;
     // keep the regions under half full for the next batch

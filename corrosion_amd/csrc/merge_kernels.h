@@ -27,6 +27,9 @@
 
 namespace corro {
 
+#ifndef CORRO_DIAG
+#define CORRO_DIAG 0
+#endif
 constexpr int HIST_THREADS = 512;
 constexpr uint32_t TILES_MAX = 256;                    // hist/scatter tiles: one per CU
 constexpr int MERGE_THREADS = 512;
@@ -1066,39 +1069,47 @@ __device__ inline void gen_bucket(const MergeArgs &a, uint32_t b) {
 // prior is earlier in application order: it keeps ties). Rows of the winners are resolved in the
 // region (lookups, then inserts of new rows once the region and heap are known to have room).
 
-// Cell and row of record i in one probe: the cell table (s_own, keys (pk, table_cid) of the claiming
-// record) is probed from the ROW's home slot, so the first record of the same row met in probe order
-// -- the same one for every record of the row, since a slot once claimed keeps its occupant and a
-// record claims the first empty slot it meets -- names the row (or record i, when it claims a slot
-// before meeting one). No second table, no second pass.
-__device__ inline void cell_row_claim(uint32_t *s_own, const uint64_t *s_pk, const uint32_t *s_tc, uint32_t i,
-                                      uint64_t pk, uint32_t tc, uint32_t &cell, uint32_t &row) {
-    const uint32_t t = tc >> 16;
+// Rows, then cells, in two short probes. Phase 1 (row_claim, every record): open addressing on the
+// row key (pk, table) in `s_rt` (FAST_SLOTS words that are free until phase 2 has run), entries =
+// claiming record + 1, an empty slot read plainly before it is claimed by CAS (lanes of one row mostly
+// meet its occupied home slot: broadcast reads, no serialised atomics); row = the row's first
+// claimant. Phase 2 (cell_claim, after a barrier): open addressing on the cell key (row claimant + 1,
+// cid) packed into one word with the claimant, so a probe compares words without reading s_pk/s_tc
+// (cid < 128: MAX_COLS; records < 4096). s_rt and s_own must be zero before phase 1.
+__device__ inline uint32_t row_claim(uint32_t *s_rt, const uint64_t *s_pk, const uint32_t *s_tc, uint32_t i, uint64_t pk,
+                                     uint32_t t) {
     uint32_t slot = row_hash(pk, t) & (FAST_SLOTS - 1);
-    uint32_t r = ~0u;
     while (true) {
-        const uint32_t o = atomicCAS(&s_own[slot], 0u, i + 1);
+        uint32_t o = __hip_atomic_load(&s_rt[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (o == 0) {
-            cell = i;
-            row = r == ~0u ? i : r;
-            return;
+            o = atomicCAS(&s_rt[slot], 0u, i + 1);
+            if (o == 0) return i;
         }
         const uint32_t x = o - 1;
-        if (s_pk[x] == pk && (s_tc[x] >> 16) == t) {
-            if (r == ~0u) r = x;
-            if (s_tc[x] == tc) {
-                cell = x;
-                row = r;
-                return;
-            }
+        if (s_pk[x] == pk && (s_tc[x] >> 16) == t) return x;
+        slot = (slot + 1) & (FAST_SLOTS - 1);
+    }
+}
+
+__device__ inline uint32_t cell_claim(uint32_t *s_own, uint32_t i, uint32_t row, uint32_t cid) {
+    static_assert(CAP_FAST <= 4096 && MAX_COLS < 128, "cell words: claimant in 12 bits, cid in 7");
+    const uint32_t key = ((row + 1) << 7) | (cid & 127u);
+    const uint32_t mine = (key << 12) | i;
+    uint32_t slot = (key * 0x9E3779B1u) >> (32 - 12);
+    while (true) {
+        uint32_t o = __hip_atomic_load(&s_own[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (o == 0) {
+            o = atomicCAS(&s_own[slot], 0u, mine);
+            if (o == 0) return i;
         }
+        if ((o >> 12) == key) return o & 0xFFFu;
         slot = (slot + 1) & (FAST_SLOTS - 1);
     }
 }
 
 // Row resolution shared by the fast bodies, run by the whole workgroup once the cell table is no
 // longer probed (s_heap aliases its first CAP_FAST words, the claim bitmap the rest). row[k]: the
-// row's record (cell_row_claim); the lane holding it (valid, row[k] == i) looks the row up and keeps
+// row's record (row_claim); the lane holding it (valid, row[k] == i) looks the row up and keeps
 // its region entry in ent[k]; the row's heap word goes to s_heap[row] (row_heap() gives the heap
 // index) and its prior presence word to s_bits[row]. The workgroup owns region b during the fast
 // bodies, so the region is probed with plain loads -- not at all while it is empty (used0 = its fill
@@ -1117,14 +1128,14 @@ __device__ inline uint32_t row_heap(uint32_t w, unsigned long long hbase) {
 // heap offset noted) right after the cell hashing; thread 0 allocates after the next barrier, its
 // latency hidden behind the argmax.
 template <int R>
-__device__ inline void fast_rows_count(const MergeArgs &a, uint32_t n, const uint32_t (&row)[R], const uint32_t *s_tc,
-                                       uint32_t *s_heap, uint32_t *s_ctl) {
+__device__ inline void fast_rows_count(uint32_t n, const uint32_t (&row)[R], const uint32_t (&strd)[R], uint32_t *s_heap,
+                                       uint32_t *s_ctl) {
     const uint32_t tid = threadIdx.x;
 #pragma unroll
     for (int k = 0; k < R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
         if (i >= n || row[k] != i) continue;
-        s_heap[i] = 0x80000000u | atomicAdd(&s_ctl[1], (uint32_t)a.rs.stride[s_tc[i] >> 16]);
+        s_heap[i] = 0x80000000u | atomicAdd(&s_ctl[1], strd[k]);
         atomicAdd(&s_ctl[0], 1u);
     }
 }
@@ -1136,7 +1147,11 @@ __device__ inline void fast_rows_alloc(const MergeArgs &a, uint32_t b, uint32_t 
     bool ok = used0 + s_ctl[0] <= a.rs.fill;
     unsigned long long h = 0;
     if (ok && s_ctl[1]) {
+#if CORRO_DIAG & 8
+        h = (unsigned long long)b * 640u;
+#else
         h = rs_heap_alloc(a.rs, s_ctl[1]);
+#endif
         ok = h != ~0ULL;
     }
     if (!ok) {
@@ -1202,6 +1217,10 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
     for (int k = 0; k < R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
         if (ent[k] != ROW_NONE - 1) continue;
+#if CORRO_DIAG & 2
+        ent[k] = ROW_NONE;
+        continue;
+#endif
         const uint32_t t = s_tc[i] >> 16, hb = row_heap(hw[k], *s_hbase);
         if (!lds_claim) {
             ent[k] = rs_claim(a.rs, b, e0[k], s_pk[i], t, hb);
@@ -1256,14 +1275,23 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     // every record load of this lane is issued before the first wait (one memory latency per
     // bucket instead of one per record group), then the site-rank lookups as one more batch
     uint4 q[FAST_R][4];
+#if CORRO_DIAG & 64
+    unsigned long long diag_t = wall_clock64();
+#define DIAG_MARK(k) do { if (tid == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&a.misc[10 + (k)], t_ - diag_t); diag_t = t_; } } while (0)
+#else
+#define DIAG_MARK(k) do { } while (0)
+#endif
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
     if (tid == 0) {
         s_live = 0;
-        s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
+        s_ctl[0] = s_ctl[1] = s_ctl[2] = s_ctl[3] = 0;
     }
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) {
+        s_own[i] = 0;
+        reinterpret_cast<uint32_t *>(s_k)[i] = 0;  // the row table of row_claim
+    }
     uint32_t srank[FAST_R];
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1284,22 +1312,36 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
             seq[k] = r.seq;
         }
     }
+    // site ranks and (for the rows an empty region gets) row strides: one more batch of loads
+    uint32_t strd[FAST_R];
 #pragma unroll
-    for (int k = 0; k < FAST_R; k++) srank[k] = a.site_rank[site[k] < a.nsites ? site[k] : 0u];
+    for (int k = 0; k < FAST_R; k++) {
+        srank[k] = a.site_rank[site[k] < a.nsites ? site[k] : 0u];
+        strd[k] = used0 ? 0u : (uint32_t)a.rs.stride[alive[k] ? s_tc[k * MERGE_THREADS + tid] >> 16 : 0u];
+    }
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) rp[k] |= (uint64_t)(site[k] < a.nsites ? srank[k] : 0u) << 32;
     __syncthreads();
+    DIAG_MARK(0);
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
         row[k] = 0;
         if (!alive[k]) continue;
-        cell_row_claim(s_own, s_pk, s_tc, i, s_pk[i], s_tc[i], cell[k], row[k]);
+        row[k] = row_claim(reinterpret_cast<uint32_t *>(s_k), s_pk, s_tc, i, s_pk[i], s_tc[i] >> 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * MERGE_THREADS + tid;
+        if (!alive[k]) continue;
+        cell[k] = cell_claim(s_own, i, row[k], s_tc[i]);
         if (cell[k] == i) s_k[i] = 0;
     }
     __syncthreads();
+    DIAG_MARK(1);
     // an empty region: all rows new -- counted now, allocated behind the argmax
-    if (!used0) fast_rows_count<FAST_R>(a, n, row, s_tc, s_own, s_ctl);
+    if (!used0) fast_rows_count<FAST_R>(n, row, strd, s_own, s_ctl);
     // argmax stages: INTEGER-only: col_version, value, site|pos. Mixed: + rank, word 1, length.
     constexpr int nstages = WIDE ? 6 : 3;
 #pragma unroll
@@ -1338,8 +1380,10 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         }
     }
     // rows (s_own: heap words by row record; s_k: presence words)
+    DIAG_MARK(2);
     uint32_t ent[FAST_R];
     if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_k, s_ctl, &s_hbase, used0 == 0)) return;
+    DIAG_MARK(3);
     // winners vs the prior clock of their cell; new cells set their presence bit
     uint32_t hb[FAST_R];
     uint32_t nlive = 0;
@@ -1395,10 +1439,21 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
             x.cl = 1;
             x.pos = hb[k];
         }
+#if CORRO_DIAG & 1
+        {   // DIAG: winners written compactly behind the bucket's heap base (timing only)
+            uint32_t o = 0;
+            if (alive[k]) o = atomicAdd(&s_ctl[3], 1u);
+            store_rec_wave(a.rs.heap, (uint32_t)s_hbase + o, x, alive[k]);
+        }
+#elif CORRO_DIAG & 4
+        (void)x;
+#else
         store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
+#endif
     }
     if (nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
+    DIAG_MARK(4);
     // owners publish the rows' presence bits
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1406,6 +1461,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_k[i];
     }
     if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
+    DIAG_MARK(5);
 }
 
 // Same per-cell merge with per-change crsql_rows_impacted() growth (impact output requested: the
@@ -1442,7 +1498,10 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
         s_live = 0;
         s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
     }
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) {
+        s_own[i] = 0;
+        reinterpret_cast<uint32_t *>(s_v0)[i] = 0;  // the row table of row_claim
+    }
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
@@ -1467,14 +1526,18 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) rank[k] = site[k] < a.nsites ? rank[k] : 0u;
     __syncthreads();
-    // 1. cells and rows: open addressing on (pk, table_cid) from the row's home slot
+    // 1. rows, then cells (row_claim / cell_claim)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
         row[k] = 0;
         if (!alive[k]) continue;
-        cell_row_claim(s_own, s_pk, s_tc, i, pk[k], tc[k], cell[k], row[k]);
+        row[k] = row_claim(reinterpret_cast<uint32_t *>(s_v0), s_pk, s_tc, i, pk[k], tc[k] >> 16);
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) cell[k] = cell_claim(s_own, k * MERGE_THREADS + tid, row[k], tc[k]);
     __syncthreads();
     // 1b. row lookups, prior clocks: does the change beat its cell's prior?
     if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_v0, s_ctl, &s_hbase, false)) return;
@@ -1651,7 +1714,10 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
         s_live = 0;
         s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
     }
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) {
+        s_own[i] = 0;
+        reinterpret_cast<uint32_t *>(s_c)[i] = 0;  // the row table of row_claim
+    }
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
@@ -1674,14 +1740,18 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) rank[k] = site[k] < a.nsites ? rank[k] : 0u;
     __syncthreads();
-    // 1. cells and rows: open addressing on (pk, table_cid) from the row's home slot
+    // 1. rows, then cells (row_claim / cell_claim)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
         row[k] = 0;
         if (!alive[k]) continue;
-        cell_row_claim(s_own, s_a, s_b, i, pk[k], tc[k], cell[k], row[k]);
+        row[k] = row_claim(reinterpret_cast<uint32_t *>(s_c), s_a, s_b, i, pk[k], tc[k] >> 16);
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) cell[k] = cell_claim(s_own, k * MERGE_THREADS + tid, row[k], tc[k]);
     __syncthreads();
     // 1b. row lookups, prior clocks: does the change beat its cell's prior?
     if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase, false)) return;
