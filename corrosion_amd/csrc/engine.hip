@@ -817,9 +817,11 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     ctx->state_total += ctx->h_misc[MISC_LIVE];  // (a signed delta in two's complement)
 #if CORRO_DIAG & 64
-    fprintf(stderr, "DIAG phases (us per bucket, 100 MHz wall clock): %.3f %.3f %.3f %.3f %.3f %.3f\n",
-            ctx->h_misc[10] / 100.0 / B, ctx->h_misc[11] / 100.0 / B, ctx->h_misc[12] / 100.0 / B,
-            ctx->h_misc[13] / 100.0 / B, ctx->h_misc[14] / 100.0 / B, ctx->h_misc[15] / 100.0 / B);
+    fprintf(stderr, "DIAG phases (us per bucket): load %.3f claims %.3f rows_count %.3f stage1 %.3f stages %.3f fast_rows %.3f winners %.3f publish %.3f\n",
+            ctx->h_misc[MISC_DIAG] / 100.0 / B, ctx->h_misc[MISC_DIAG + 1] / 100.0 / B,
+            ctx->h_misc[MISC_DIAG + 6] / 100.0 / B, ctx->h_misc[MISC_DIAG + 7] / 100.0 / B,
+            ctx->h_misc[MISC_DIAG + 2] / 100.0 / B, ctx->h_misc[MISC_DIAG + 3] / 100.0 / B,
+            ctx->h_misc[MISC_DIAG + 4] / 100.0 / B, ctx->h_misc[MISC_DIAG + 5] / 100.0 / B);
 #endif
     ctx->state_epoch++;
     if (ctx->h_misc[MISC_WIDE]) ctx->state_wide = true;

@@ -31,6 +31,9 @@ namespace corro {
 #define CORRO_DIAG 0
 #endif
 constexpr int HIST_THREADS = 512;
+// INTEGER fast body, two-stage argmax: every col_version of the batch in [0, CV_PACKED_LIMIT) and
+// at most 2^16 sites (k_scatter flags MISC_CVBIG otherwise)
+constexpr uint64_t CV_PACKED_LIMIT = 1ULL << 15;
 constexpr uint32_t TILES_MAX = 256;                    // hist/scatter tiles: one per CU
 constexpr int MERGE_THREADS = 512;
 constexpr int FAST_R = 6;                              // records per thread, fast body
@@ -65,7 +68,8 @@ struct MergeArgs {
 
 // misc words
 constexpr int MISC_ERR = 0, MISC_OVF = 1, MISC_LIVE = 2, MISC_WIDE = 3, MISC_GEN = 4, MISC_WIDEQ = 5,
-              MISC_GEN_SMALL = 6, MISC_GEN_MID = 7, MISC_DEFER = 8, MISC_DEFER_WHY = 9, MISC_WORDS = 16;
+              MISC_GEN_SMALL = 6, MISC_GEN_MID = 7, MISC_DEFER = 8, MISC_DEFER_WHY = 9, MISC_CVBIG = 10,
+              MISC_DIAG = 16, MISC_WORDS = 24;
 constexpr unsigned long long DEFER_REGION = 1, DEFER_HEAP = 2;
 
 // misc[0] error bits
@@ -322,15 +326,19 @@ __device__ inline void store_rec_wave(Rec *base, uint32_t idx, const Rec &r, boo
     swap32(q[1].x, q[3].x); swap32(q[1].y, q[3].y); swap32(q[1].z, q[3].z); swap32(q[1].w, q[3].w);
     swap16(q[0].x, q[1].x); swap16(q[0].y, q[1].y); swap16(q[0].z, q[1].z); swap16(q[0].w, q[1].w);
     swap16(q[2].x, q[3].x); swap16(q[2].y, q[3].y); swap16(q[2].z, q[3].z); swap16(q[2].w, q[3].w);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t j = lane >> 4, l = lane & 15;
-    const int v = valid ? 1 : 0;
+    // the destination indices ride the same transpose (no LDS permutes): after it, lane l + 16j
+    // holds in ix[k] the index of lane l + 16k's record (~0u: that lane stores nothing)
+    uint32_t ix[4];
+    ix[0] = ix[1] = ix[2] = ix[3] = valid ? idx : ~0u;
+    swap32(ix[0], ix[2]);
+    swap32(ix[1], ix[3]);
+    swap16(ix[0], ix[1]);
+    swap16(ix[2], ix[3]);
+    const uint32_t j = (threadIdx.x & 63) >> 4;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int srcl = (int)l + 16 * k;
-        const uint32_t sidx = __shfl(idx, srcl);
-        const int sv = __shfl(v, srcl);
-        if (sv) {
+        const uint32_t sidx = ix[k];
+        if (sidx != ~0u) {
             uint4 *dst = reinterpret_cast<uint4 *>(base + sidx) + j;
             if (NT) {
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -373,7 +381,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
     const uint32_t begin = blockIdx.x * tile;
     const uint32_t end = min(in.n, begin + tile);
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t err = 0, wide = 0;
+    uint32_t err = 0, wide = 0, cvbig = 0;
     // crsql_db_versions: per-wave run of one site (a tile is a contiguous slice of the application
     // order, so a wave sees one actor's changesets for long stretches)
     uint32_t run_site = 0xFFFFFFFFu;
@@ -485,6 +493,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                 if (r.site >= nsites) err |= ERR_SITE;
                 if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
                 if (r.dbv < 0) err |= ERR_RANGE;
+                if ((uint64_t)r.cv >= CV_PACKED_LIMIT) cvbig = 1;
                 if (ty != CORRO_INTEGER) {
                     wide = 1;
                     if (ty < 1 || ty > 5) err |= ERR_VALUE;
@@ -516,6 +525,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
     if (lane == 0 && run_site < nsites) atomicMax(&dbv_batch[run_site], run_max);
     if (err) atomicOr(&misc[0], (unsigned long long)err);
     if (wide) atomicOr(&misc[3], 1ULL);
+    if (__any(cvbig) && lane == 0) atomicOr(&misc[MISC_CVBIG], 1ULL);
     __syncthreads();
     for (uint32_t w = threadIdx.x; w < nfl; w += blockDim.x)
         if (fl[w]) atomicOr(&bflags[w], fl[w]);
@@ -1118,6 +1128,31 @@ __device__ inline uint32_t cell_claim(uint32_t *s_own, uint32_t i, uint32_t row,
 // the entry written with plain stores (regions larger than the bitmap claim by CAS). `counted`: the
 // region was empty and fast_rows_count / fast_rows_alloc already ran. Returns false when the bucket
 // was deferred (nothing written). s_ctl[0..2] must be zero on entry unless counted.
+// Wave-aggregated LDS counters: many lanes adding to one LDS word serialise (same-address atomics),
+// so a wave scans its lanes' amounts and one lane adds the total. Called by every lane of the wave.
+__device__ inline uint32_t wave_incl_scan(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    return x;
+}
+// ctr += sum of x over the wave; returns this lane's exclusive offset (old ctr + earlier lanes' x).
+__device__ inline uint32_t wave_lds_add(uint32_t *ctr, uint32_t x) {
+    const uint32_t inc = wave_incl_scan(x);
+    const uint32_t total = __shfl(inc, 63);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == 0 && total) base = atomicAdd(ctr, total);
+    return __shfl(base, 0) + inc - x;
+}
+__device__ inline uint32_t wave_sum_u32(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+    return x;
+}
+
 constexpr uint32_t RS_BM_WORDS = FAST_SLOTS - CAP_FAST;  // claim bitmap: regions of up to 32768 slots
 
 __device__ inline uint32_t row_heap(uint32_t w, unsigned long long hbase) {
@@ -1131,13 +1166,17 @@ template <int R>
 __device__ inline void fast_rows_count(uint32_t n, const uint32_t (&row)[R], const uint32_t (&strd)[R], uint32_t *s_heap,
                                        uint32_t *s_ctl) {
     const uint32_t tid = threadIdx.x;
+    uint32_t rows = 0;
 #pragma unroll
     for (int k = 0; k < R; k++) {
         const uint32_t i = k * MERGE_THREADS + tid;
-        if (i >= n || row[k] != i) continue;
-        s_heap[i] = 0x80000000u | atomicAdd(&s_ctl[1], strd[k]);
-        atomicAdd(&s_ctl[0], 1u);
+        const bool own = i < n && row[k] == i;
+        const uint32_t off = wave_lds_add(&s_ctl[1], own ? strd[k] : 0u);
+        if (own) s_heap[i] = 0x80000000u | off;
+        rows += own;
     }
+    rows = wave_sum_u32(rows);
+    if ((tid & 63) == 0 && rows) atomicAdd(&s_ctl[0], rows);
 }
 
 // thread 0: the region fill check and the heap allocation of the bucket's new rows (s_ctl[0] rows,
@@ -1197,11 +1236,22 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
             s_bits[i] = a.rs.ent[e].bits[0];
             ent[k] = e;
         } else {
-            hw[k] = 0x80000000u | atomicAdd(&s_ctl[1], (uint32_t)a.rs.stride[t]);
+            hw[k] = (uint32_t)a.rs.stride[t];  // (its heap offset below)
             s_bits[i] = 0;
-            atomicAdd(&s_ctl[0], 1u);
             ent[k] = ROW_NONE - 1;  // marks "owner of a new row"
         }
+    }
+    if (!counted) {  // heap offsets of the new rows, one LDS atomic per wave and k
+        uint32_t rows = 0;
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const bool nw = ent[k] == ROW_NONE - 1;
+            const uint32_t off = wave_lds_add(&s_ctl[1], nw ? hw[k] : 0u);
+            if (nw) hw[k] = 0x80000000u | off;
+            rows += nw;
+        }
+        rows = wave_sum_u32(rows);
+        if ((tid & 63) == 0 && rows) atomicAdd(&s_ctl[0], rows);
     }
     __syncthreads();
     if (!counted) {
@@ -1260,7 +1310,7 @@ __device__ inline int prior_cmp_int(const MergeArgs &a, const Rec &pr, uint64_t 
 // the full 64-B record of a winner is re-read (L2) for the wide form. LDS: cell keys + one stage
 // array + the open-addressing cell table (76 KB, two workgroups per CU).
 template <bool WIDE>
-__device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketView &v) {
+__device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketView &v, bool packed = false) {
     __shared__ uint64_t s_pk[CAP_FAST];
     __shared__ uint64_t s_k[CAP_FAST];
     __shared__ uint32_t s_tc[CAP_FAST];
@@ -1277,7 +1327,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     uint4 q[FAST_R][4];
 #if CORRO_DIAG & 64
     unsigned long long diag_t = wall_clock64();
-#define DIAG_MARK(k) do { if (tid == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&a.misc[10 + (k)], t_ - diag_t); diag_t = t_; } } while (0)
+#define DIAG_MARK(k) do { if (tid == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&a.misc[MISC_DIAG + (k)], t_ - diag_t); diag_t = t_; } } while (0)
 #else
 #define DIAG_MARK(k) do { } while (0)
 #endif
@@ -1312,15 +1362,14 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
             seq[k] = r.seq;
         }
     }
-    // site ranks and (for the rows an empty region gets) row strides: one more batch of loads
+    // site ranks (first needed by the last argmax stage) and, for the rows an empty region gets, row
+    // strides (needed after the claims): one more batch of loads, in flight during the claims
     uint32_t strd[FAST_R];
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         srank[k] = a.site_rank[site[k] < a.nsites ? site[k] : 0u];
         strd[k] = used0 ? 0u : (uint32_t)a.rs.stride[alive[k] ? s_tc[k * MERGE_THREADS + tid] >> 16 : 0u];
     }
-#pragma unroll
-    for (int k = 0; k < FAST_R; k++) rp[k] |= (uint64_t)(site[k] < a.nsites ? srank[k] : 0u) << 32;
     __syncthreads();
     DIAG_MARK(0);
 #pragma unroll
@@ -1338,14 +1387,47 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         cell[k] = cell_claim(s_own, i, row[k], s_tc[i]);
         if (cell[k] == i) s_k[i] = 0;
     }
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) rp[k] |= (uint64_t)(site[k] < a.nsites ? srank[k] : 0u) << 32;
     __syncthreads();
     DIAG_MARK(1);
     // an empty region: all rows new -- counted now, allocated behind the argmax
     if (!used0) fast_rows_count<FAST_R>(n, row, strd, s_own, s_ctl);
+    DIAG_MARK(6);
     // argmax stages: INTEGER-only: col_version, value, site|pos. Mixed: + rank, word 1, length.
+    // Packed INTEGER form (`packed`: col_versions < 2^15, sites <= 2^16): two stages, (cv 15 | value
+    // bits 63..16) then (1 | value bits 15..0 | site rank 16 | ~position 31): the second stage's keys
+    // all exceed the first's, so the cell words need no zeroing (and no barrier) in between.
+    if (!WIDE && packed) {
+        uint64_t w[FAST_R];
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            w[k] = ((cv[k] ^ 0x8000000000000000ULL) << 48) | (v0[k] ^ 0x8000000000000000ULL) >> 16;
+            if (alive[k]) atomicMax(reinterpret_cast<unsigned long long *>(&s_k[cell[k]]), (unsigned long long)w[k]);
+        }
+        __syncthreads();
+        DIAG_MARK(7);
+        if (!used0 && tid == 0) fast_rows_alloc(a, b, used0, s_ctl, &s_hbase);
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++)
+            if (alive[k]) alive[k] = s_k[cell[k]] == w[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            w[k] = (1ULL << 63) | (((v0[k] ^ 0x8000000000000000ULL) & 0xFFFFULL) << 47) | ((rp[k] >> 32) << 31) |
+                   ((uint64_t)(uint32_t)rp[k] & 0x7FFFFFFFULL);
+            if (alive[k]) atomicMax(reinterpret_cast<unsigned long long *>(&s_k[cell[k]]), (unsigned long long)w[k]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++)
+            if (alive[k]) alive[k] = s_k[cell[k]] == w[k];
+        __syncthreads();
+    }
     constexpr int nstages = WIDE ? 6 : 3;
 #pragma unroll
     for (int st = 0; st < nstages; st++) {
+        if (!WIDE && packed) break;
         const int which = WIDE ? st : (st == 0 ? 0 : (st == 1 ? 2 : 5));
         uint64_t w[FAST_R];
 #pragma unroll
@@ -1451,7 +1533,8 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
 #endif
     }
-    if (nlive) atomicAdd(&s_live, (unsigned long long)nlive);
+    nlive = wave_sum_u32(nlive);
+    if ((tid & 63) == 0 && nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
     DIAG_MARK(4);
     // owners publish the rows' presence bits
@@ -1676,7 +1759,8 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
         }
         store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
     }
-    if (nlive) atomicAdd(&s_live, (unsigned long long)nlive);
+    nlive = wave_sum_u32(nlive);
+    if ((tid & 63) == 0 && nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1882,7 +1966,8 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
         }
         store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
     }
-    if (nlive) atomicAdd(&s_live, (unsigned long long)nlive);
+    nlive = wave_sum_u32(nlive);
+    if ((tid & 63) == 0 && nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1908,7 +1993,7 @@ k_merge_fast_int(MergeArgs a) {
     bucket_view(a, b, v);
     const uint32_t rgen = a.rs.gen[b];
     const uint32_t bword = a.bflags[b >> 5];
-    const unsigned long long wide = a.misc[MISC_WIDE];
+    const unsigned long long wide = a.misc[MISC_WIDE], cvbig = a.misc[MISC_CVBIG];
     const uint32_t n = v.nn;
     if (n == 0) return;
     if (a.force_general || rgen || ((bword >> (b & 31)) & 1u)) {
@@ -1933,7 +2018,7 @@ k_merge_fast_int(MergeArgs a) {
     if constexpr (IMPACT)
         fast_body_impact_int(a, b, v);
     else
-        fast_body<false>(a, b, v);
+        fast_body<false>(a, b, v, cvbig == 0 && a.nsites <= 65536);
 }
 
 constexpr uint32_t LIST_GRID = 512;

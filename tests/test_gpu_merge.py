@@ -452,3 +452,20 @@ def test_general_path_grows_regions():
         b = synth.adversarial_batch(60000, 8, 2, 20000, seed + k, zipf=0.6)
         assert np.array_equal(e.apply(b, impact=True), f.apply(b))
         compare(e, f, with_ts=True)
+
+
+@pytest.mark.parametrize("cv_max,tie_frac", [(8, 0.5), ((1 << 15) - 1, 0.125), (1 << 15, 0.125), (1 << 40, 0.125)])
+def test_fast_body_argmax_forms_vs_oracle(cv_max, tie_frac):
+    """The INTEGER fast body without impacts takes the two-stage packed argmax while every
+    col_version of the batch is below 2^15 and the three-stage one otherwise (k_scatter's MISC_CVBIG
+    flag); both forms, value ties and col_version ties included, against the oracle over a fold."""
+    sites = synth.site_ids(40, 5)
+    e = engine({"t": ["a", "b", "c", "d"]}, cap=200000, sites=sites)
+    f = O.Fold(sites)
+    for k in range(3):
+        b = synth.uniform_batch(200000, 40, 20000, 4, 900 + k, cv_max=cv_max, tie_frac=tie_frac)
+        if cv_max > 8:  # col_version ties as well
+            b["col_version"][::3] = cv_max
+        e.apply(b)
+        f.apply(b)
+    compare(e, f)
