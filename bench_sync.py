@@ -47,6 +47,18 @@ def cpu_baseline(ent_dev, sample):
             "sample": f"first {n} (pair, actor) entries, oracle/ranges.c count+fill passes in {dt:.2f} s"}
 
 
+def _packed_seq_total(res):
+    """Seq ranges of a packed result, from the written need slots only."""
+    import torch
+    cnt = res["need_count"].to(torch.int64)
+    T = int(cnt.sum())
+    off = torch.zeros_like(cnt)
+    off[1:] = torch.cumsum(cnt, 0)[:-1]
+    slot = torch.repeat_interleave(res["need_off"] - off, cnt) + torch.arange(T, device=cnt.device)
+    hi = res["range"].view(-1, 2)[slot, 1]
+    return int(torch.where(res["kind"][slot] == 1, hi & 0xFFFFFF, 0).sum())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=1_000_000)
@@ -54,15 +66,17 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=200_000)
-    ap.add_argument("--one-pass", action="store_true",
-                    help="corro_compute_needs_onepass (decoupled look-back) instead of count + fill passes")
+    ap.add_argument("--mode", choices=("packed", "two-pass", "one-pass"), default="packed",
+                    help="packed: corro_compute_needs_packed (one pass into bound-reserved slots, 16-B need "
+                         "pairs); two-pass: corro_compute_needs count + fill; one-pass: "
+                         "corro_compute_needs_onepass (decoupled look-back)")
     args = ap.parse_args()
 
     import torch
     import synth
     import corrosion_amd as ca
-    from corrosion_amd.sync import _needs_device, _needs_device_1pass
-    run = _needs_device_1pass if args.one_pass else _needs_device
+    from corrosion_amd.sync import _needs_device, _needs_device_1pass, _needs_device_packed
+    run = {"packed": _needs_device_packed, "two-pass": _needs_device, "one-pass": _needs_device_1pass}[args.mode]
 
     dev = torch.device("cuda", 0)
     eng = ca.MergeEngine({"t": ["a"]}, capacity_hint=1024)
@@ -87,16 +101,23 @@ def main():
     E = int(ent["their_head"].shape[0])
     in_ranges = sum(int(ent[k].shape[0]) for k in ("tn_start", "on_start", "tps_start", "ops_start"))
     pvers = int(ent["tp_ver"].shape[0] + ent["op_ver"].shape[0])
-    out_ranges = int(res["start"].shape[0] + res["s_start"].shape[0])
+    if args.mode == "packed":
+        n_needs = int(res["need_count"].to(torch.int64).sum())
+        n_seqs = _packed_seq_total(res)  # (from the written slots only: the padding holds garbage)
+    else:
+        n_needs, n_seqs = int(res["start"].shape[0]), int(res["s_start"].shape[0])
+    out_ranges = n_needs + n_seqs
     alg = 16 * in_ranges + 16 * E + 8 * pvers + 16 * out_ranges
     achieved = alg / (kt * 1e-3) / 1e9
     line = {"metric": "SyncStateV1 need diff: node-pairs/s (config 4)", "value": args.pairs / dt,
             "unit": "node-pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt * 1e3, "higher_is_better": True, "dtype": "u64", "data": "synthetic (HBM)",
             "config": {"workload": "config 4", "pairs": args.pairs, "entries": E, "input_ranges": in_ranges,
-                       "output_needs": int(res["start"].shape[0]), "output_seq_ranges": int(res["s_start"].shape[0])},
+                       "output_needs": n_needs, "output_seq_ranges": n_seqs, "mode": args.mode},
             "entries_per_s": E / dt,
-            "roofline": {"bound": "hbm", "kernel": "k_needs1 (one pass)" if args.one_pass else "k_needs (count + fill)", "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": {"packed": "k_needs_packed (one pass)", "two-pass": "k_needs (count + fill)",
+                                                    "one-pass": "k_needs1 (one pass, look-back)"}[args.mode],
+                         "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernels_ms": kt, "count_pass_ms": kc, "fill_pass_ms": kf},
             "cpu_baseline": cpu_baseline(ent, min(args.cpu_sample, E))}

@@ -35,7 +35,7 @@ EXPORTS = [
     "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
     "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
-    "corro_pk_canonical", "corro_bookie_buffered_value",
+    "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -84,6 +84,10 @@ class ExtractIn(C.Structure):
 class ExtractOut(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("grp_count", "row_count", "grp_off", "row_off", "version", "last_seq",
                                           "ts", "grp_row_off", "grp_rows")] + [("rows", Rows)]
+
+
+class NeedsPackedOut(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("need_off", "need_count", "range", "kind", "s_start", "s_end")]
 
 
 class NeedsOut(C.Structure):
@@ -166,6 +170,7 @@ def lib():
         "corro_scan_offsets": (i32, [vp, vp, vp, u64]),
         "corro_compute_needs_onepass": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsOut), u64, u64, vp]),
         "corro_needs_bound": (i32, [vp, C.POINTER(SyncEntries), i32, vp, vp]),
+        "corro_compute_needs_packed": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsPackedOut), u64, u64]),
         "corro_bookie_seq_bookkeeping": (i32, [vp, vp, u64, vp, vp, u64, vp, vp, vp]),
         "corro_site_ids": (i32, [vp, vp, u32, vp]),
         "corro_decode_frames": (i32, [vp, C.c_char_p, u64, i32, i32, C.POINTER(Decoded), i32]),

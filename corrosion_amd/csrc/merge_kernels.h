@@ -1400,6 +1400,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     // all exceed the first's, so the cell words need no zeroing (and no barrier) in between.
     if (!WIDE && packed) {
         uint64_t w[FAST_R];
+        unsigned long long hraw = 0;
 #pragma unroll
         for (int k = 0; k < FAST_R; k++) {
             w[k] = ((cv[k] ^ 0x8000000000000000ULL) << 48) | (v0[k] ^ 0x8000000000000000ULL) >> 16;
@@ -1407,7 +1408,8 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         }
         __syncthreads();
         DIAG_MARK(7);
-        if (!used0 && tid == 0) fast_rows_alloc(a, b, used0, s_ctl, &s_hbase);
+        // the bucket's heap allocation: issued now, its result consumed after the second stage
+        if (!used0 && tid == 0 && s_ctl[1] && used0 + s_ctl[0] <= a.rs.fill) hraw = atomicAdd(a.rs.heap_top, (unsigned long long)s_ctl[1]);
 #pragma unroll
         for (int k = 0; k < FAST_R; k++)
             if (alive[k]) alive[k] = s_k[cell[k]] == w[k];
@@ -1423,6 +1425,17 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         for (int k = 0; k < FAST_R; k++)
             if (alive[k]) alive[k] = s_k[cell[k]] == w[k];
         __syncthreads();
+        if (!used0 && tid == 0) {  // (published to the workgroup by fast_rows' first barrier)
+            const unsigned long long need = s_ctl[1];
+            const bool room = used0 + s_ctl[0] <= a.rs.fill;
+            if (!room || (need && hraw + need > a.rs.heap_cap)) {
+                push_defer(a, b, room ? DEFER_HEAP : DEFER_REGION);
+                s_ctl[2] = 1;
+            } else {
+                a.rs.used[b] = used0 + s_ctl[0];
+                s_hbase = need ? hraw : 0;
+            }
+        }
     }
     constexpr int nstages = WIDE ? 6 : 3;
 #pragma unroll

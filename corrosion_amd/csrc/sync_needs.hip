@@ -197,22 +197,40 @@ template <class V> struct InViews {
 // The walk of one entry (sync.rs:141-245). Counts its needs (nn) and partial seq ranges (ns); with
 // FILL also writes them: needs at [nbase, nbase + nn) through the o* views, seq ranges straight to
 // global memory at [sbase, sbase + ns).
-template <bool FILL, class V, class VK, class VU>
-__device__ inline void walk_entry(const corro_needs_out &o, const EntryHdr &h, const InViews<V> &iv, VK okind,
-                                  VU ostart, VU oend, VU osro, VU osrn, uint64_t nbase, uint64_t sbase,
-                                  uint64_t &nn_out, uint64_t &ns_out) {
+// Output emitters of the fill walk. NeedsEmit: the five arrays of corro_needs_out (global or LDS
+// views); need q, seq-range slot j.
+template <class VK, class VU> struct NeedsEmit {
+    VK okind;
+    VU ostart, oend, osro, osrn;
+    uint64_t *s_start, *s_end;
+    __device__ inline void full(uint64_t q, uint64_t s, uint64_t t, uint64_t sr) const {
+        okind[q] = 0;
+        ostart[q] = s;
+        oend[q] = t;
+        osro[q] = sr;
+        osrn[q] = 0;
+    }
+    __device__ inline void partial(uint64_t q, uint64_t v, uint64_t sr, uint64_t cnt) const {
+        okind[q] = 1;
+        ostart[q] = v;
+        oend[q] = v;
+        osro[q] = sr;
+        osrn[q] = cnt;
+    }
+    __device__ inline void seq(uint64_t j, uint64_t s, uint64_t t) const {
+        s_start[j] = s;
+        s_end[j] = t;
+    }
+};
+
+template <bool FILL, class V, class E>
+__device__ inline void walk_entry(const EntryHdr &h, const InViews<V> &iv, const E &em, uint64_t nbase,
+                                  uint64_t sbase, uint64_t &nn_out, uint64_t &ns_out) {
     const uint64_t head = h.head;
     VerHolesT<V> vh{iv.tns, iv.tne, h.tne0, h.tne1, iv.tpv, h.tpe0, h.tpe1};
     uint64_t nn = 0, ns = 0;
     auto full = [&](uint64_t s, uint64_t t) {
-        if (FILL) {
-            const uint64_t k = nbase + nn;
-            okind[k] = 0;
-            ostart[k] = s;
-            oend[k] = t;
-            osro[k] = sbase + ns;
-            osrn[k] = 0;
-        }
+        if (FILL) em.full(nbase + nn, s, t, sbase + ns);
         nn++;
     };
     for (uint64_t k = h.one0; k < h.one1; k++) {
@@ -237,16 +255,8 @@ __device__ inline void walk_entry(const corro_needs_out &o, const EntryHdr &h, c
         const uint64_t q0 = iv.opso[k], q1 = iv.opso[k + 1];
         if (have) {
             if (FILL) {
-                const uint64_t q = nbase + nn;
-                okind[q] = 1;
-                ostart[q] = v;
-                oend[q] = v;
-                osro[q] = sbase + ns;
-                osrn[q] = q1 - q0;
-                for (uint64_t j = q0; j < q1; j++) {
-                    o.s_start[sbase + ns + (j - q0)] = iv.opss[j];
-                    o.s_end[sbase + ns + (j - q0)] = iv.opse[j];
-                }
+                em.partial(nbase + nn, v, sbase + ns, q1 - q0);
+                for (uint64_t j = q0; j < q1; j++) em.seq(sbase + ns + (j - q0), iv.opss[j], iv.opse[j]);
             }
             ns += q1 - q0;
             nn++;
@@ -277,22 +287,12 @@ __device__ inline void walk_entry(const corro_needs_out &o, const EntryHdr &h, c
         const uint64_t first = sbase + ns;
         uint64_t cnt = 0;
         auto piece = [&](uint64_t s, uint64_t t) {
-            if (FILL) {
-                o.s_start[first + cnt] = s;
-                o.s_end[first + cnt] = t;
-            }
+            if (FILL) em.seq(first + cnt, s, t);
             cnt++;
         };
         for (uint64_t j = q0; j < q1; j++) sweep(sh, iv.opss[j], iv.opse[j], 0, end, piece);
         if (cnt) {
-            if (FILL) {
-                const uint64_t q = nbase + nn;
-                okind[q] = 1;
-                ostart[q] = v;
-                oend[q] = v;
-                osro[q] = first;
-                osrn[q] = cnt;
-            }
+            if (FILL) em.partial(nbase + nn, v, first, cnt);
             nn++;
             ns += cnt;
         }
@@ -364,6 +364,11 @@ __device__ inline WgSegs stage_inputs(const SyncDev &in, uint64_t e0, uint64_t e
     return g;
 }
 
+__device__ inline NeedsEmit<WView<uint8_t>, WView<uint64_t>> gemit(const corro_needs_out &o) {
+    return {WView<uint8_t>{o.kind, 0},   WView<uint64_t>{o.start, 0}, WView<uint64_t>{o.end, 0},
+            WView<uint64_t>{o.sr_off, 0}, WView<uint64_t>{o.sr_n, 0}, o.s_start, o.s_end};
+}
+
 // Run walk_entry on LDS views when the inputs are staged (and, with FILL, the outputs fit),
 // else on global views.
 template <bool FILL>
@@ -375,23 +380,22 @@ __device__ inline void walk_dispatch(const SyncDev &in, const corro_needs_out &o
         const InViews<VL> iv{VL{L.tns, g.tn_lo},  VL{L.tne, g.tn_lo},  VL{L.ons, g.on_lo},  VL{L.one, g.on_lo},
                              VL{L.tpv, g.tp_lo},  VL{L.tpso, g.tp_lo}, VL{L.tpss, g.tps_lo}, VL{L.tpse, g.tps_lo},
                              VL{L.opv, g.op_lo},  VL{L.opso, g.op_lo}, VL{L.opss, g.ops_lo}, VL{L.opse, g.ops_lo}};
-        walk_entry<FILL>(o, h, iv, WView<uint8_t>{o.kind, 0}, WView<uint64_t>{o.start, 0}, WView<uint64_t>{o.end, 0},
-                         WView<uint64_t>{o.sr_off, 0}, WView<uint64_t>{o.sr_n, 0}, nbase, sbase, nn, ns);
+        walk_entry<FILL>(h, iv, gemit(o), nbase, sbase, nn, ns);
     } else if (g.lds) {
         using VL = V64S<1>;
         const InViews<VL> iv{VL{L.tns, g.tn_lo},  VL{L.tne, g.tn_lo},  VL{L.ons, g.on_lo},  VL{L.one, g.on_lo},
                              VL{L.tpv, g.tp_lo},  VL{L.tpso, g.tp_lo}, VL{L.tpss, g.tps_lo}, VL{L.tpse, g.tps_lo},
                              VL{L.opv, g.op_lo},  VL{L.opso, g.op_lo}, VL{L.opss, g.ops_lo}, VL{L.opse, g.ops_lo}};
         NeedsOutLds &O = *Lo;
-        walk_entry<FILL>(o, h, iv, WView<uint8_t, 1>{O.kind, o_lo}, WView<uint64_t, 1>{O.start, o_lo},
-                         WView<uint64_t, 1>{O.end, o_lo}, WView<uint64_t, 1>{O.sro, o_lo},
-                         WView<uint64_t, 1>{O.srn, o_lo}, nbase, sbase, nn, ns);
+        const NeedsEmit<WView<uint8_t, 1>, WView<uint64_t, 1>> em{
+            WView<uint8_t, 1>{O.kind, o_lo}, WView<uint64_t, 1>{O.start, o_lo}, WView<uint64_t, 1>{O.end, o_lo},
+            WView<uint64_t, 1>{O.sro, o_lo}, WView<uint64_t, 1>{O.srn, o_lo}, o.s_start, o.s_end};
+        walk_entry<FILL>(h, iv, em, nbase, sbase, nn, ns);
     } else {
         const InViews<V64> iv{V64{in.tn_start, 0}, V64{in.tn_end, 0},  V64{in.on_start, 0},  V64{in.on_end, 0},
                               V64{in.tp_ver, 0},   V64{in.tps_off, 0}, V64{in.tps_start, 0}, V64{in.tps_end, 0},
                               V64{in.op_ver, 0},   V64{in.ops_off, 0}, V64{in.ops_start, 0}, V64{in.ops_end, 0}};
-        walk_entry<FILL>(o, h, iv, WView<uint8_t>{o.kind, 0}, WView<uint64_t>{o.start, 0}, WView<uint64_t>{o.end, 0},
-                         WView<uint64_t>{o.sr_off, 0}, WView<uint64_t>{o.sr_n, 0}, nbase, sbase, nn, ns);
+        walk_entry<FILL>(h, iv, gemit(o), nbase, sbase, nn, ns);
     }
 }
 
@@ -622,6 +626,115 @@ __global__ void __launch_bounds__(NEEDS_T) k_needs1(SyncDev in, corro_needs_out 
     }
 }
 
+// ---- packed one-pass form (corro_compute_needs_packed) ---------------------------------------
+// No count pass and no look-back: a workgroup's outputs go to the slots its entries' output BOUNDS
+// reserve (corro_needs_bound, per entry: our + their need ranges + their + our partial versions + 1
+// need slots; our + their partial seq ranges seq slots -- prefix sums of the input CSR offsets, so
+// the workgroup reads them off its own segment bounds), compacted within the workgroup: count walk
+// over the LDS-staged inputs, workgroup scan, fill walk. Needs are written as one 16-B pair + a kind
+// byte (Partial: {version, first seq slot << 24 | seq ranges}), so a wave's stores cover whole lines.
+struct PackedEmit {
+    uint64_t *range;
+    uint8_t *kind;
+    uint64_t *s_start, *s_end;
+    __device__ inline void full(uint64_t q, uint64_t s, uint64_t t, uint64_t) const {
+        *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(s, t);
+        kind[q] = 0;
+    }
+    __device__ inline void partial(uint64_t q, uint64_t v, uint64_t sr, uint64_t cnt) const {
+        *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(v, (sr << 24) | cnt);
+        kind[q] = 1;
+    }
+    __device__ inline void seq(uint64_t j, uint64_t s, uint64_t t) const {
+        s_start[j] = s;
+        s_end[j] = t;
+    }
+};
+struct NullEmit {
+    __device__ inline void full(uint64_t, uint64_t, uint64_t, uint64_t) const {}
+    __device__ inline void partial(uint64_t, uint64_t, uint64_t, uint64_t) const {}
+    __device__ inline void seq(uint64_t, uint64_t, uint64_t) const {}
+};
+
+template <bool FILL, class E>
+__device__ inline void walk_inputs(const SyncDev &in, const EntryHdr &h, const NeedsLds &L, const WgSegs &g,
+                                   const E &em, uint64_t nbase, uint64_t sbase, uint64_t &nn, uint64_t &ns) {
+    if (g.lds) {
+        using VL = V64S<1>;
+        const InViews<VL> iv{VL{L.tns, g.tn_lo},  VL{L.tne, g.tn_lo},  VL{L.ons, g.on_lo},  VL{L.one, g.on_lo},
+                             VL{L.tpv, g.tp_lo},  VL{L.tpso, g.tp_lo}, VL{L.tpss, g.tps_lo}, VL{L.tpse, g.tps_lo},
+                             VL{L.opv, g.op_lo},  VL{L.opso, g.op_lo}, VL{L.opss, g.ops_lo}, VL{L.opse, g.ops_lo}};
+        walk_entry<FILL>(h, iv, em, nbase, sbase, nn, ns);
+    } else {
+        const InViews<V64> iv{V64{in.tn_start, 0}, V64{in.tn_end, 0},  V64{in.on_start, 0},  V64{in.on_end, 0},
+                              V64{in.tp_ver, 0},   V64{in.tps_off, 0}, V64{in.tps_start, 0}, V64{in.tps_end, 0},
+                              V64{in.op_ver, 0},   V64{in.ops_off, 0}, V64{in.ops_start, 0}, V64{in.ops_end, 0}};
+        walk_entry<FILL>(h, iv, em, nbase, sbase, nn, ns);
+    }
+}
+
+// err[0] |= 1: a workgroup's needs exceed its bound slots (overlapping input ranges); 2: a partial
+// with >= 2^24 seq ranges or a seq slot >= 2^40 (not representable in the packed word)
+__global__ void __launch_bounds__(NEEDS_T) k_needs_packed(SyncDev in, corro_needs_packed_out o, uint64_t need_slots,
+                                                          uint64_t seq_slots, unsigned long long *err) {
+    __shared__ NeedsLds L;
+    __shared__ uint64_t s_wn[NEEDS_T / 64], s_ws[NEEDS_T / 64];
+    const uint64_t e0 = (uint64_t)blockIdx.x * NEEDS_T;
+    const uint64_t e1 = min(in.n, e0 + NEEDS_T);
+    const uint64_t e = e0 + threadIdx.x;
+    const bool live = e < in.n;
+    const EntryHdr h = load_entry(in, live ? e : e0);
+    // the workgroup's bound slot windows (uniform loads, in flight with the staging)
+    const uint64_t tps0 = in.tps_off ? in.tps_off[in.tp_off[e0]] : 0, tps1 = in.tps_off ? in.tps_off[in.tp_off[e1]] : 0;
+    const uint64_t ops0 = in.ops_off ? in.ops_off[in.op_off[e0]] : 0, ops1 = in.ops_off ? in.ops_off[in.op_off[e1]] : 0;
+    const WgSegs g = stage_inputs(in, e0, e1, L);
+    const uint64_t bn0 = g.tn_lo + g.on_lo + g.tp_lo + g.op_lo + e0, bn1 = g.tn_hi + g.on_hi + g.tp_hi + g.op_hi + e1;
+    const uint64_t bs0 = tps0 + ops0, bs1 = tps1 + ops1;
+    uint64_t nn = 0, ns = 0;
+    if (live) walk_inputs<false>(in, h, L, g, NullEmit{}, 0, 0, nn, ns);
+    // workgroup exclusive scan of (nn, ns)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t in_n = nn, in_s = ns;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t yn = __shfl_up(in_n, d), ys = __shfl_up(in_s, d);
+        if (lane >= d) {
+            in_n += yn;
+            in_s += ys;
+        }
+    }
+    if (lane == 63) {
+        s_wn[wv] = in_n;
+        s_ws[wv] = in_s;
+    }
+    __syncthreads();
+    uint64_t pre_n = 0, pre_s = 0, tot_n = 0, tot_s = 0;
+#pragma unroll
+    for (int w = 0; w < (int)(NEEDS_T / 64); w++) {
+        if (w < wv) {
+            pre_n += s_wn[w];
+            pre_s += s_ws[w];
+        }
+        tot_n += s_wn[w];
+        tot_s += s_ws[w];
+    }
+    if (bn0 + tot_n > bn1 || bs0 + tot_s > bs1 || bn1 > need_slots || bs1 > seq_slots) {
+        if (threadIdx.x == 0) atomicOr(err, 1ULL);
+        return;  // uniform
+    }
+    if (bs1 >= (1ULL << 40) || __any(nn > 0xFFFFFFFFULL || ns >= (1ULL << 24))) {
+        if (threadIdx.x == 0) atomicOr(err, 2ULL);
+        return;
+    }
+    const uint64_t nbase = bn0 + pre_n + in_n - nn, sbase = bs0 + pre_s + in_s - ns;
+    if (live) {
+        o.need_off[e] = nbase;
+        o.need_count[e] = (uint32_t)nn;
+        const PackedEmit em{o.range, o.kind, o.s_start, o.s_end};
+        uint64_t n2 = 0, s2 = 0;
+        walk_inputs<true>(in, h, L, g, em, nbase, sbase, n2, s2);
+    }
+}
+
 }  // namespace corro
 
 using namespace corro;
@@ -823,5 +936,49 @@ extern "C" int corro_compute_needs_onepass(corro_ctx *ctx, const corro_sync_entr
     totals[1] = t[1];
     if (t[0] > need_cap || t[1] > seq_cap)
         return fail(CORRO_E_RANGE, "need output exceeds the given capacity (totals hold the sizes to re-run with)");
+    return CORRO_OK;
+}
+
+extern "C" int corro_compute_needs_packed(corro_ctx *ctx, const corro_sync_entries *in, corro_needs_packed_out *out,
+                                          uint64_t need_slots, uint64_t seq_slots) {
+    if (!ctx || !in || !out) return fail(CORRO_E_INVALID, "NULL argument");
+    const uint64_t n = in->n;
+    if (n == 0) return CORRO_OK;
+    if (!out->need_off || !out->need_count || (need_slots && (!out->range || !out->kind)) ||
+        (seq_slots && (!out->s_start || !out->s_end)))
+        return fail(CORRO_E_INVALID, "an output array is NULL");
+    if ((uintptr_t)out->range % 16) return fail(CORRO_E_INVALID, "range must be 16-byte aligned");
+    for (const void *q : {(const void *)in->tn_start, (const void *)in->tn_end, (const void *)in->on_start,
+                          (const void *)in->on_end})
+        if (q && ((uintptr_t)q % 16) != 0) return fail(CORRO_E_INVALID, "device need-range arrays must be 16-byte aligned");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const uint64_t blocks = (n + NEEDS_T - 1) / NEEDS_T;
+    if (blocks > 0x7FFFFFFFULL) return fail(CORRO_E_RANGE, "too many sync entries");
+    if (int rc = ctx->d_needs1.ensure(64)) return rc;
+    unsigned long long *err = ctx->d_needs1.as<unsigned long long>();
+    SyncDev d{};
+    d.n = n;
+    d.their_head = in->their_head; d.our_head = in->our_head;
+    d.tn_off = in->tn_off; d.tn_start = in->tn_start; d.tn_end = in->tn_end;
+    d.tp_off = in->tp_off; d.tp_ver = in->tp_ver;
+    d.tps_off = in->tps_off; d.tps_start = in->tps_start; d.tps_end = in->tps_end;
+    d.on_off = in->on_off; d.on_start = in->on_start; d.on_end = in->on_end;
+    d.op_off = in->op_off; d.op_ver = in->op_ver;
+    d.ops_off = in->ops_off; d.ops_start = in->ops_start; d.ops_end = in->ops_end;
+    CORRO_HIP_TRY(hipMemsetAsync(err, 0, 8, s));
+    if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    hipLaunchKernelGGL(k_needs_packed, dim3((uint32_t)blocks), dim3(NEEDS_T), 0, s, d, *out, need_slots, seq_slots, err);
+    if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    CORRO_HIP_TRY(hipGetLastError());
+    unsigned long long e = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&e, err, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (ctx->profiling) {
+        CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[6], ctx->ev[0], ctx->ev[1]));
+        ctx->last_ms[7] = 0.f;
+    }
+    if (e & 1) return fail(CORRO_E_RANGE, "needs exceed their bound slots (overlapping need ranges: use corro_compute_needs)");
+    if (e & 2) return fail(CORRO_E_RANGE, "a partial's seq ranges do not fit the packed need word");
     return CORRO_OK;
 }

@@ -223,6 +223,69 @@ def _needs_device_1pass(engine, ent):
     return res
 
 
+def _needs_device_packed(engine, ent):
+    """corro_compute_needs_packed on device-resident CSR entries: one kernel, no count pass; outputs
+    in the workgroup-padded packed layout (slots sized by corro_needs_bound). Returns CUDA tensors
+    need_off, need_count, range (2 per slot), kind, s_start, s_end."""
+    import torch
+    lib = L.lib()
+    n = int(ent["their_head"].shape[0])
+    dev = ent["their_head"].device
+    s = L.SyncEntries()
+    s.n = n
+    for k, _ in L.SyncEntries._fields_[1:]:
+        a = ent[k]
+        setattr(s, k, a.data_ptr() if a.numel() else None)
+    torch.cuda.current_stream().synchronize()
+    ncap, scap = C.c_uint64(), C.c_uint64()
+    L.check(lib.corro_needs_bound(engine._h, C.byref(s), L.CORRO_MEM_DEVICE, C.byref(ncap), C.byref(scap)))
+    res = {"need_off": torch.empty(max(n, 1), dtype=torch.int64, device=dev),
+           "need_count": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+           "range": torch.empty(2 * max(ncap.value, 1), dtype=torch.int64, device=dev),
+           "kind": torch.empty(max(ncap.value, 1), dtype=torch.uint8, device=dev),
+           "s_start": torch.empty(max(scap.value, 1), dtype=torch.int64, device=dev),
+           "s_end": torch.empty(max(scap.value, 1), dtype=torch.int64, device=dev)}
+    o = L.NeedsPackedOut()
+    for k in ("need_off", "need_count", "range", "kind", "s_start", "s_end"):
+        setattr(o, k, res[k].data_ptr())
+    L.check(lib.corro_compute_needs_packed(engine._h, C.byref(s), C.byref(o), ncap.value, scap.value))
+    res["need_off"], res["need_count"] = res["need_off"][:n], res["need_count"][:n]
+    return res
+
+
+def packed_to_csr(res):
+    """The packed layout as the CSR dict of corro_compute_needs (numpy, host): need_off / seq_off
+    (n+1), kind, start, end, sr_off, sr_n, s_start, s_end."""
+    import numpy as np
+    g = {k: (v.cpu().numpy() if hasattr(v, "cpu") else np.asarray(v)) for k, v in res.items()}
+    cnt = g["need_count"].astype(np.int64)
+    n = len(cnt)
+    need_off = np.zeros(n + 1, np.int64)
+    need_off[1:] = np.cumsum(cnt)
+    T = int(need_off[-1])
+    slot = np.repeat(g["need_off"].astype(np.int64) - need_off[:-1], cnt) + np.arange(T)
+    rng = g["range"].view(np.uint64).reshape(-1, 2)[slot]
+    kind = g["kind"][slot]
+    part = kind == 1
+    first = (rng[:, 1] >> np.uint64(24)).astype(np.int64)
+    sr_n = np.where(part, (rng[:, 1] & np.uint64(0xFFFFFF)).astype(np.int64), 0)
+    ent_of = np.repeat(np.arange(n), cnt)
+    seq_cnt = np.bincount(ent_of, weights=sr_n, minlength=n).astype(np.int64) if T else np.zeros(n, np.int64)
+    seq_off = np.zeros(n + 1, np.int64)
+    seq_off[1:] = np.cumsum(seq_cnt)
+    # seq ranges of the partials in need order, compacted
+    sr_off = np.zeros(T, np.int64)
+    sr_off[1:] = np.cumsum(sr_n)[:-1]
+    src = np.repeat(np.where(part, first, 0), sr_n) + (np.arange(int(sr_n.sum())) - np.repeat(sr_off, sr_n))
+    full_sr = np.zeros(T, np.int64)  # a Full need's sr_off: the seq ranges emitted before it
+    full_sr[:] = sr_off
+    return {"need_off": need_off, "seq_off": seq_off, "kind": kind,
+            "start": rng[:, 0].astype(np.int64),
+            "end": np.where(part, rng[:, 0], rng[:, 1]).astype(np.int64),
+            "sr_off": full_sr, "sr_n": sr_n,
+            "s_start": g["s_start"][src].astype(np.int64), "s_end": g["s_end"][src].astype(np.int64)}
+
+
 def decode(res, index, npairs):
     out = [dict() for _ in range(npairs)]
     for e, (p, actor) in enumerate(index):

@@ -90,3 +90,37 @@ def test_config4_full_size_vs_oracle():
         assert np.array_equal(g.view(exp[k].dtype) if g.dtype != exp[k].dtype and g.itemsize == exp[k].itemsize
                               else g, exp[k]), k
     e.close()
+
+
+def test_config4_full_size_packed_equals_two_pass():
+    """Config 4 at its stated size (1M node pairs x 64 actors = 64M entries): the packed one-pass
+    kernel's needs equal the two-pass kernel's (itself checked against the oracle above), compared
+    on the device slot by slot."""
+    import torch
+    import corrosion_amd as ca
+    from corrosion_amd.sync import _needs_device, _needs_device_packed
+    ent = synth.sync_entries_torch(1_000_000, 64, synth.config_seed(4), device="cuda")
+    e = ca.MergeEngine({"t": ["a"]}, capacity_hint=1024)
+    a = _needs_device(e, ent)
+    b = _needs_device_packed(e, ent)
+    del ent
+    cnt = b["need_count"].to(torch.int64)
+    assert bool((cnt == a["need_off"][1:] - a["need_off"][:-1]).all())
+    T = int(a["need_off"][-1])
+    slot = torch.repeat_interleave(b["need_off"] - a["need_off"][:-1], cnt) + torch.arange(T, device="cuda")
+    rng = b["range"].view(-1, 2)
+    kind = b["kind"][slot]
+    assert bool((kind == a["kind"]).all())
+    lo, hi = rng[slot, 0], rng[slot, 1]
+    part = kind == 1
+    assert bool((lo == a["start"]).all())
+    assert bool((torch.where(part, lo, hi) == a["end"]).all())
+    assert bool((torch.where(part, hi & 0xFFFFFF, 0) == a["sr_n"]).all())
+    first = torch.where(part, hi >> 24, 0)
+    sr = a["sr_n"]
+    Ts = int(sr.sum())
+    assert Ts == int(a["seq_off"][-1])
+    src = torch.repeat_interleave(first, sr) + (torch.arange(Ts, device="cuda")
+                                               - torch.repeat_interleave(a["sr_off"], sr))
+    assert bool((b["s_start"][src] == a["s_start"]).all()) and bool((b["s_end"][src] == a["s_end"]).all())
+    e.close()

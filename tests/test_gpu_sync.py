@@ -208,3 +208,62 @@ def test_inverted_our_need_ranges_vs_fixture():
     e = _engine()
     got = decode_needs(e.compute_needs(entries_from_pairs(pairs_from_cases(cases))), len(cases))
     assert got == expected_from_cases(cases)
+
+
+# ---- packed one-pass form (corro_compute_needs_packed: bound-reserved slots, no count pass) -----
+
+def _packed_csr(ent_dev):
+    from corrosion_amd.sync import _needs_device_packed, packed_to_csr
+    return packed_to_csr(_needs_device_packed(_engine(), ent_dev))
+
+
+def _check_packed(ent_host):
+    got = _packed_csr(_to_dev(ent_host))
+    exp = O.needs(ent_host)
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        assert np.array_equal(got[k].astype(np.uint64), exp[k].astype(np.uint64)), k
+
+
+@pytest.mark.parametrize("case", SYNC["cases"], ids=[c["name"] for c in SYNC["cases"]])
+def test_sync_kats_gpu_packed(case):
+    ent = entries_from_pairs([(case["our"], case["their"])])
+    assert decode_needs(_packed_csr(_to_dev(ent)), 1)[0] == kat_expect(case["expect"])
+
+
+def test_sync_random_vs_oracle_packed():
+    rng = np.random.default_rng(16)
+    pairs = [(random_side(rng, with_head=rng.random() < 0.9), random_side(rng)) for _ in range(40000)]
+    _check_packed(entries_from_pairs(pairs))
+
+
+@pytest.mark.parametrize("dense", ["theirs", "ours", "both"])
+def test_sync_lds_caps_exceeded_packed(dense):
+    """Workgroups whose segments exceed the LDS caps walk global memory; same result."""
+    rng = np.random.default_rng(13)
+    pairs = []
+    for i in range(1200):
+        heavy = 256 <= i < 768
+        nt = 12 if heavy and dense in ("theirs", "both") else int(rng.poisson(2))
+        no = 12 if heavy and dense in ("ours", "both") else int(rng.poisson(2))
+        pairs.append((_dense_side(rng, no, int(rng.integers(1, 100))), _dense_side(rng, nt, 300)))
+    _check_packed(entries_from_pairs(pairs))
+
+
+def test_sync_config4_shape_packed_vs_oracle():
+    import synth
+    ent = synth.sync_entries_torch(20000, 30, 22, device="cuda")
+    got = _packed_csr(ent)
+    exp = O.needs({k: v.cpu().numpy() for k, v in ent.items()})
+    for k in ("need_off", "seq_off", "kind", "start", "end", "sr_off", "sr_n", "s_start", "s_end"):
+        assert np.array_equal(got[k].astype(np.uint64), exp[k].astype(np.uint64)), k
+
+
+def test_sync_packed_overlapping_ranges_rejected():
+    """Overlapping our-need ranges (no RangeInclusiveSet produces them) can exceed the bound slots:
+    CORRO_E_RANGE instead of a write past a workgroup's slots."""
+    from corrosion_amd.sync import _needs_device_packed
+    their = {"head": 400, "need": [[k, k] for k in range(3, 390, 4)], "partials": {}}
+    our = {"head": None, "need": [[1, 395]] * 6, "partials": {}}
+    ent = entries_from_pairs([(our, their)] * 300)
+    with pytest.raises(RuntimeError, match="CORRO_E_RANGE"):
+        _needs_device_packed(_engine(), _to_dev(ent))
