@@ -162,7 +162,7 @@ def _free_port():
     return p
 
 
-def launch_ranks(n):
+def launch_ranks(n, script=None):
     """One fresh process per GPU (this parent never initialises the GPU): RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* as torchrun sets them. Returns the worst exit code."""
     port = str(_free_port())
@@ -170,7 +170,7 @@ def launch_ranks(n):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(script or __file__)] + sys.argv[1:], env=env))
     rcs = [p.wait() for p in procs]
     return max(rcs, key=abs)
 

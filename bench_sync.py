@@ -6,6 +6,11 @@ corro_compute_needs count pass + device offset scan + fill pass (default), or wi
 corro_compute_needs_onepass. Algorithmic bytes:
 16 B per input range (ours.need, theirs.need, partial seq ranges) + 16 B per head pair + 8 B per
 partial version + 16 B per output range. Prints one JSON line.
+
+--gpus N (SURVEY §8(e) last bullet): node pairs are independent, so the 1M pairs are sharded
+contiguously over N ranks (one process per GPU, launched by this script unless WORLD_SIZE is set)
+with no exchange on the data path: each rank diffs its own pairs and keeps its outputs (strong
+scaling; `value` = all pairs / the slowest rank's step, barrier + max over ranks).
 """
 import argparse
 import json
@@ -63,6 +68,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=1_000_000)
     ap.add_argument("--actors-per-pair", type=int, default=64)
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=200_000)
@@ -71,6 +77,11 @@ def main():
                          "pairs); two-pass: corro_compute_needs count + fill; one-pass: "
                          "corro_compute_needs_onepass (decoupled look-back)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from bench import launch_ranks
+        sys.exit(launch_ranks(args.gpus, __file__))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
 
     import torch
     import synth
@@ -78,14 +89,29 @@ def main():
     from corrosion_amd.sync import _needs_device, _needs_device_1pass, _needs_device_packed
     run = {"packed": _needs_device_packed, "two-pass": _needs_device, "one-pass": _needs_device_1pass}[args.mode]
 
-    dev = torch.device("cuda", 0)
-    eng = ca.MergeEngine({"t": ["a"]}, capacity_hint=1024)
-    ent = synth.sync_entries_torch(args.pairs, args.actors_per_pair, synth.config_seed(4), device=dev)
+    dist = None
+    local = 0
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("CORRO_BENCH_BACKEND", "nccl")
+        local = int(os.environ.get("LOCAL_RANK", str(rank))) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local)
+    eng = ca.MergeEngine({"t": ["a"]}, capacity_hint=1024, device=local)
+    pairs_local = (rank + 1) * args.pairs // world - rank * args.pairs // world
+    ent = synth.sync_entries_torch(pairs_local, args.actors_per_pair, synth.config_seed(4) + 7919 * rank, device=dev)
     torch.cuda.synchronize()
     eng.set_profiling(True)
     for _ in range(args.warmup):
         res = run(eng, ent)
     kt = kc = kf = 0.0
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = run(eng, ent)
@@ -94,7 +120,14 @@ def main():
         kf += tm["k_needs_fill"]
         kt += tm["k_needs_count"] + tm["k_needs_fill"]
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     dt = (time.perf_counter() - t0) / args.steps
+    if dist is not None:
+        x = torch.tensor([dt], dtype=torch.float64, device=dev if os.environ.get("CORRO_BENCH_BACKEND", "nccl") == "nccl"
+                         else "cpu")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        dt = float(x.item())
     kt /= args.steps
     kc /= args.steps
     kf /= args.steps
@@ -110,18 +143,25 @@ def main():
     alg = 16 * in_ranges + 16 * E + 8 * pvers + 16 * out_ranges
     achieved = alg / (kt * 1e-3) / 1e9
     line = {"metric": "SyncStateV1 need diff: node-pairs/s (config 4)", "value": args.pairs / dt,
-            "unit": "node-pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": dt * 1e3, "higher_is_better": True, "dtype": "u64", "data": "synthetic (HBM)",
-            "config": {"workload": "config 4", "pairs": args.pairs, "entries": E, "input_ranges": in_ranges,
-                       "output_needs": n_needs, "output_seq_ranges": n_seqs, "mode": args.mode},
-            "entries_per_s": E / dt,
+            "unit": "node-pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "strong" if world > 1 else "n/a",
+            "dtype": "u64", "data": "synthetic (HBM)",
+            "config": {"workload": "config 4", "pairs": args.pairs, "entries_rank0": E, "input_ranges_rank0": in_ranges,
+                       "output_needs_rank0": n_needs, "output_seq_ranges_rank0": n_seqs, "mode": args.mode,
+                       "parallelism": f"{world} rank(s), node pairs sharded, no exchange"},
+            "entries_per_s": E * world / dt,
             "roofline": {"bound": "hbm", "kernel": {"packed": "k_needs_packed (one pass)", "two-pass": "k_needs (count + fill)",
                                                     "one-pass": "k_needs1 (one pass, look-back)"}[args.mode],
                          "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernels_ms": kt, "count_pass_ms": kc, "fill_pass_ms": kf},
-            "cpu_baseline": cpu_baseline(ent, min(args.cpu_sample, E))}
-    print(json.dumps(line), flush=True)
+                         "kernels_ms": kt, "count_pass_ms": kc, "fill_pass_ms": kf}}
+    if rank == 0:
+        if world == 1:
+            line["cpu_baseline"] = cpu_baseline(ent, min(args.cpu_sample, E))
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -36,6 +36,7 @@ EXPORTS = [
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
     "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
+    "corro_booked_insert_db_batch",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -84,6 +85,16 @@ class ExtractIn(C.Structure):
 class ExtractOut(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("grp_count", "row_count", "grp_off", "row_off", "version", "last_seq",
                                           "ts", "grp_row_off", "grp_rows")] + [("rows", Rows)]
+
+
+class GapsIn(C.Structure):
+    _fields_ = [("n", C.c_uint64)] + [(k, C.c_void_p) for k in ("max", "gap_off", "gap_start", "gap_end",
+                                                                 "ver_off", "ver_start", "ver_end")]
+
+
+class GapsOut(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("max", "rm_count", "ins_count", "gap_count", "rm_start", "rm_end",
+                                          "ins_start", "ins_end", "new_start", "new_end", "status")]
 
 
 class NeedsPackedOut(C.Structure):
@@ -170,6 +181,7 @@ def lib():
         "corro_scan_offsets": (i32, [vp, vp, vp, u64]),
         "corro_compute_needs_onepass": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsOut), u64, u64, vp]),
         "corro_needs_bound": (i32, [vp, C.POINTER(SyncEntries), i32, vp, vp]),
+        "corro_booked_insert_db_batch": (i32, [vp, C.POINTER(GapsIn), C.POINTER(GapsOut)]),
         "corro_compute_needs_packed": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsPackedOut), u64, u64]),
         "corro_bookie_seq_bookkeeping": (i32, [vp, vp, u64, vp, vp, u64, vp, vp, vp]),
         "corro_site_ids": (i32, [vp, vp, u32, vp]),

@@ -65,3 +65,73 @@ class BookedVersions:
         r = C.c_int()
         L.check(L.lib().corro_booked_contains_all(self._h, start, end, C.byref(r)))
         return bool(r.value)
+
+
+def canonical_ranges(ranges):
+    """RangeInclusiveSet of (s, e) pairs: sorted, overlapping and touching ranges coalesced."""
+    out = []
+    for s, e in sorted((int(s), int(e)) for s, e in ranges):
+        if out and s <= out[-1][1] + 1:
+            if e > out[-1][1]:
+                out[-1][1] = e
+        else:
+            out.append([s, e])
+    return [tuple(r) for r in out]
+
+
+def insert_db_batch(engine, maxes, gaps, versions):
+    """corro_booked_insert_db_batch for len(maxes) actors at once on the engine's device.
+    maxes: per actor max or None; gaps / versions: per actor lists of (s, e) (versions are made a
+    RangeInclusiveSet first, as insert_db's caller builds one). Returns per actor
+    (max, removed rows, inserted rows, needed gaps, status)."""
+    import torch
+    lib = L.lib()
+    n = len(maxes)
+    dev = torch.device("cuda", engine.device) if hasattr(engine, "device") else torch.device("cuda")
+    versions = [canonical_ranges(v) for v in versions]
+
+    def csr(lists):
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in lists])
+        flat = [r for x in lists for r in x]
+        s = np.array([r[0] for r in flat], np.uint64)
+        e = np.array([r[1] for r in flat], np.uint64)
+        return off, s, e
+
+    def to_dev(a, dtype=torch.int64):
+        a = np.ascontiguousarray(a)
+        return torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev) if a.size else \
+            torch.zeros(1, dtype=dtype, device=dev)
+
+    goff, gs, ge = csr(gaps)
+    voff, vs, ve = csr(versions)
+    mx = np.array([-1 if m is None else int(m) for m in maxes], np.int64)
+    G, V = int(goff[-1]), int(voff[-1])
+    W = G + V + n
+    t = {"max": to_dev(mx), "gap_off": to_dev(goff), "gap_start": to_dev(gs), "gap_end": to_dev(ge),
+         "ver_off": to_dev(voff), "ver_start": to_dev(vs), "ver_end": to_dev(ve)}
+    o = {k: torch.zeros(max(1, sz), dtype=dt, device=dev) for k, sz, dt in
+         (("max", n, torch.int64), ("rm_count", n, torch.int64), ("ins_count", n, torch.int64),
+          ("gap_count", n, torch.int64), ("rm_start", G, torch.int64), ("rm_end", G, torch.int64),
+          ("ins_start", W, torch.int64), ("ins_end", W, torch.int64), ("new_start", W, torch.int64),
+          ("new_end", W, torch.int64), ("status", n, torch.int32))}
+    gi = L.GapsIn()
+    gi.n = n
+    for k in ("max", "gap_off", "gap_start", "gap_end", "ver_off", "ver_start", "ver_end"):
+        setattr(gi, k, t[k].data_ptr())
+    go = L.GapsOut()
+    for k in o:
+        setattr(go, k, o[k].data_ptr())
+    torch.cuda.synchronize(dev)
+    L.check(lib.corro_booked_insert_db_batch(engine._h, C.byref(gi), C.byref(go)))
+    h = {k: v.cpu().numpy() for k, v in o.items()}
+    res = []
+    for a in range(n):
+        rb, ib = int(goff[a]), int(goff[a] + voff[a]) + a
+        nr, ni, ng = int(h["rm_count"][a]), int(h["ins_count"][a]), int(h["gap_count"][a])
+        res.append((None if h["max"][a] < 0 else int(h["max"][a]),
+                    [(int(h["rm_start"][rb + i]), int(h["rm_end"][rb + i])) for i in range(nr)],
+                    [(int(h["ins_start"][ib + i]), int(h["ins_end"][ib + i])) for i in range(ni)],
+                    [(int(h["new_start"][ib + i]), int(h["new_end"][ib + i])) for i in range(ng)],
+                    int(h["status"][a])))
+    return res

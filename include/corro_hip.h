@@ -344,6 +344,32 @@ int corro_booked_last(corro_booked *b, int64_t *max);     /* -1 = None */
 int corro_booked_contains(corro_booked *b, uint64_t version, int *result);
 int corro_booked_contains_all(corro_booked *b, uint64_t start, uint64_t end, int *result);
 
+/* Batched insert_db on the device (csrc/gaps.hip): the same gap bookkeeping for n actors in one
+ * launch, one lane per actor, DEVICE memory throughout. Inputs per actor a: its BookedVersions max
+ * (-1 = None), its needed gaps [gap_off[a], gap_off[a+1]) and this call's applied versions
+ * [ver_off[a], ver_off[a+1]), both canonical RangeInclusiveSets (sorted, disjoint, non-touching).
+ * Outputs go to windows the input sizes reserve (no count pass): the DELETE rows at
+ * rm_*[gap_off[a] .. + rm_count[a]); the INSERT rows at ins_*[gap_off[a] + ver_off[a] + a .. +
+ * ins_count[a]) and the new needed gaps at new_*[the same base .. + gap_count[a]) (arrays of
+ * gap_off[n] and gap_off[n] + ver_off[n] + n elements). status[a]: 0 ok, -1 a non-canonical input
+ * (nothing written for that actor). Partials whose version lies in a DELETE row are the caller's to
+ * drop (insert_db's partials.remove, agent.rs:1148). */
+typedef struct {
+    uint64_t n;
+    const int64_t *max;
+    const uint64_t *gap_off, *gap_start, *gap_end;
+    const uint64_t *ver_off, *ver_start, *ver_end;
+} corro_gaps_in;
+typedef struct {
+    int64_t *max;
+    uint64_t *rm_count, *ins_count, *gap_count;
+    uint64_t *rm_start, *rm_end;
+    uint64_t *ins_start, *ins_end;
+    uint64_t *new_start, *new_end;
+    int32_t *status;
+} corro_gaps_out;
+int corro_booked_insert_db_batch(corro_ctx *ctx, const corro_gaps_in *in, corro_gaps_out *out);
+
 /* ------------------------------------------------------------------ process_multiple_changes */
 
 /* Bookie (corro-types/src/agent.rs:1546-1598): BookedVersions per actor, plus the buffered

@@ -2,6 +2,7 @@
 sentinel deletes/resurrects, mixed value classes) through the general merge path.
 Not the headline bench (bench.py measures configs[1]); prints one line per size."""
 import argparse
+import json
 import os
 import sys
 import time
@@ -46,6 +47,19 @@ def main():
         print(f"n={n} gen={gen:.1f}s apply={dt*1e3:.2f} ms (median of {args.reps}) rows={eng.count()} "
               f"({n/dt/1e6:.1f} M changes/s) stages={ {s: round(v, 3) for s, v in stages[k].items()} }",
               flush=True)
+        # config 5 prices 56 B per change and per output cell (16-B value keys)
+        cells = eng.count()
+        pipe = sum(stages[k].values())
+        alg = 56 * (n + cells)
+        print(json.dumps({"metric": "merged column-changes/s (config 5: adversarial)", "value": n / dt,
+                          "unit": "merged column-changes/s", "n_gpus": 1, "ms_per_apply": dt * 1e3,
+                          "impact": bool(args.impact), "dtype": "int64/16-B blob keys",
+                          "config": {"workload": "config 5", "changes": n, "cells": cells, "tables": 8,
+                                     "sentinel_frac": 0.3, "zipf": 1.1},
+                          "roofline": {"bound": "hbm", "kernel": "apply pipeline (sum of stages)",
+                                       "achieved": alg / (pipe * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                                       "frac": alg / (pipe * 1e-3) / 1e9 / 8000.0, "alg_bytes": alg,
+                                       "pipeline_ms": pipe, "stages_ms": stages[k]}}), flush=True)
         eng.close()
 
 
