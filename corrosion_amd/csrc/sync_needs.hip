@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <string>
 #include <vector>
 
@@ -626,6 +627,56 @@ __global__ void __launch_bounds__(NEEDS_T) k_needs1(SyncDev in, corro_needs_out 
     }
 }
 
+// Segment bounds of every workgroup boundary e = w * NEEDS_T (w = 0..nwg), computed by one tiny
+// pre-pass so a workgroup reads its whole CSR window -- including the nested partial-seq offsets, a
+// chain of two dependent loads -- with two 48-B loads (one latency) before staging its data.
+struct WgBound {
+    uint64_t tn, on, tp, op, tps, ops;
+};
+__global__ void __launch_bounds__(256) k_needs_bounds(SyncDev in, uint64_t nwg, WgBound *wb) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w > nwg) return;
+    const uint64_t e = min(in.n, w * NEEDS_T);
+    WgBound b;
+    b.tn = in.tn_off[e];
+    b.on = in.on_off[e];
+    b.tp = in.tp_off[e];
+    b.op = in.op_off[e];
+    b.tps = in.tps_off ? in.tps_off[b.tp] : 0;
+    b.ops = in.ops_off ? in.ops_off[b.op] : 0;
+    wb[w] = b;
+}
+
+// stage_inputs with the workgroup's bounds given (one latency fewer per nesting level).
+__device__ inline WgSegs stage_inputs_b(const SyncDev &in, const WgBound &b0, const WgBound &b1, NeedsLds &L) {
+    WgSegs g;
+    g.tn_lo = b0.tn; g.tn_hi = b1.tn;
+    g.on_lo = b0.on; g.on_hi = b1.on;
+    g.tp_lo = b0.tp; g.tp_hi = b1.tp;
+    g.op_lo = b0.op; g.op_hi = b1.op;
+    g.tps_lo = b0.tps; g.tps_hi = b1.tps;
+    g.ops_lo = b0.ops; g.ops_hi = b1.ops;
+    g.lds = g.tn_hi - g.tn_lo <= NEEDS_CAP_R && g.on_hi - g.on_lo <= NEEDS_CAP_R && g.tp_hi - g.tp_lo <= NEEDS_CAP_P &&
+            g.op_hi - g.op_lo <= NEEDS_CAP_P && g.tps_hi - g.tps_lo <= NEEDS_CAP_S && g.ops_hi - g.ops_lo <= NEEDS_CAP_S;
+    if (!g.lds) return g;  // uniform
+    stage_ranges(in.tn_start, in.tn_end, g.tn_lo, g.tn_hi - g.tn_lo, L.tns, L.tne);
+    stage_ranges(in.on_start, in.on_end, g.on_lo, g.on_hi - g.on_lo, L.ons, L.one);
+    if (g.tp_hi > g.tp_lo) {
+        stage_words(in.tp_ver, g.tp_lo, g.tp_hi - g.tp_lo, L.tpv);
+        stage_words(in.tps_off, g.tp_lo, g.tp_hi - g.tp_lo + 1, L.tpso);
+        stage_words(in.tps_start, g.tps_lo, g.tps_hi - g.tps_lo, L.tpss);
+        stage_words(in.tps_end, g.tps_lo, g.tps_hi - g.tps_lo, L.tpse);
+    }
+    if (g.op_hi > g.op_lo) {
+        stage_words(in.op_ver, g.op_lo, g.op_hi - g.op_lo, L.opv);
+        stage_words(in.ops_off, g.op_lo, g.op_hi - g.op_lo + 1, L.opso);
+        stage_words(in.ops_start, g.ops_lo, g.ops_hi - g.ops_lo, L.opss);
+        stage_words(in.ops_end, g.ops_lo, g.ops_hi - g.ops_lo, L.opse);
+    }
+    __syncthreads();
+    return g;
+}
+
 // ---- packed one-pass form (corro_compute_needs_packed) ---------------------------------------
 // No count pass and no look-back: a workgroup's outputs go to the slots its entries' output BOUNDS
 // reserve (corro_needs_bound, per entry: our + their need ranges + their + our partial versions + 1
@@ -676,22 +727,30 @@ __device__ inline void walk_inputs(const SyncDev &in, const EntryHdr &h, const N
 // err[0] |= 1: a workgroup's needs exceed its bound slots (overlapping input ranges); 2: a partial
 // with >= 2^24 seq ranges or a seq slot >= 2^40 (not representable in the packed word)
 __global__ void __launch_bounds__(NEEDS_T) k_needs_packed(SyncDev in, corro_needs_packed_out o, uint64_t need_slots,
-                                                          uint64_t seq_slots, unsigned long long *err) {
+                                                          uint64_t seq_slots, unsigned long long *err,
+                                                          const WgBound *__restrict__ wb) {
     __shared__ NeedsLds L;
     __shared__ uint64_t s_wn[NEEDS_T / 64], s_ws[NEEDS_T / 64];
+#if defined(CORRO_DIAG) && (CORRO_DIAG & 128)
+    unsigned long long dt0 = wall_clock64();
+#define NDIAG(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&err[1 + (k)], t_ - dt0); dt0 = t_; } } while (0)
+#else
+#define NDIAG(k) do { } while (0)
+#endif
     const uint64_t e0 = (uint64_t)blockIdx.x * NEEDS_T;
     const uint64_t e1 = min(in.n, e0 + NEEDS_T);
     const uint64_t e = e0 + threadIdx.x;
     const bool live = e < in.n;
     const EntryHdr h = load_entry(in, live ? e : e0);
-    // the workgroup's bound slot windows (uniform loads, in flight with the staging)
-    const uint64_t tps0 = in.tps_off ? in.tps_off[in.tp_off[e0]] : 0, tps1 = in.tps_off ? in.tps_off[in.tp_off[e1]] : 0;
-    const uint64_t ops0 = in.ops_off ? in.ops_off[in.op_off[e0]] : 0, ops1 = in.ops_off ? in.ops_off[in.op_off[e1]] : 0;
-    const WgSegs g = stage_inputs(in, e0, e1, L);
+    // the workgroup's CSR window (k_needs_bounds) also fixes its bound slot windows
+    const WgBound b0 = wb[blockIdx.x], b1 = wb[blockIdx.x + 1];
+    const WgSegs g = stage_inputs_b(in, b0, b1, L);
     const uint64_t bn0 = g.tn_lo + g.on_lo + g.tp_lo + g.op_lo + e0, bn1 = g.tn_hi + g.on_hi + g.tp_hi + g.op_hi + e1;
-    const uint64_t bs0 = tps0 + ops0, bs1 = tps1 + ops1;
+    const uint64_t bs0 = b0.tps + b0.ops, bs1 = b1.tps + b1.ops;
+    NDIAG(0);
     uint64_t nn = 0, ns = 0;
     if (live) walk_inputs<false>(in, h, L, g, NullEmit{}, 0, 0, nn, ns);
+    NDIAG(1);
     // workgroup exclusive scan of (nn, ns)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint64_t in_n = nn, in_s = ns;
@@ -726,6 +785,7 @@ __global__ void __launch_bounds__(NEEDS_T) k_needs_packed(SyncDev in, corro_need
         return;
     }
     const uint64_t nbase = bn0 + pre_n + in_n - nn, sbase = bs0 + pre_s + in_s - ns;
+    NDIAG(2);
     if (live) {
         o.need_off[e] = nbase;
         o.need_count[e] = (uint32_t)nn;
@@ -733,6 +793,7 @@ __global__ void __launch_bounds__(NEEDS_T) k_needs_packed(SyncDev in, corro_need
         uint64_t n2 = 0, s2 = 0;
         walk_inputs<true>(in, h, L, g, em, nbase, sbase, n2, s2);
     }
+    NDIAG(3);
 }
 
 }  // namespace corro
@@ -955,8 +1016,9 @@ extern "C" int corro_compute_needs_packed(corro_ctx *ctx, const corro_sync_entri
     hipStream_t s = ctx->stream;
     const uint64_t blocks = (n + NEEDS_T - 1) / NEEDS_T;
     if (blocks > 0x7FFFFFFFULL) return fail(CORRO_E_RANGE, "too many sync entries");
-    if (int rc = ctx->d_needs1.ensure(64)) return rc;
+    if (int rc = ctx->d_needs1.ensure(64 + (blocks + 1) * sizeof(WgBound))) return rc;
     unsigned long long *err = ctx->d_needs1.as<unsigned long long>();
+    WgBound *wb = reinterpret_cast<WgBound *>(ctx->d_needs1.as<uint8_t>() + 64);
     SyncDev d{};
     d.n = n;
     d.their_head = in->their_head; d.our_head = in->our_head;
@@ -966,9 +1028,11 @@ extern "C" int corro_compute_needs_packed(corro_ctx *ctx, const corro_sync_entri
     d.on_off = in->on_off; d.on_start = in->on_start; d.on_end = in->on_end;
     d.op_off = in->op_off; d.op_ver = in->op_ver;
     d.ops_off = in->ops_off; d.ops_start = in->ops_start; d.ops_end = in->ops_end;
-    CORRO_HIP_TRY(hipMemsetAsync(err, 0, 8, s));
+    CORRO_HIP_TRY(hipMemsetAsync(err, 0, 64, s));
     if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[0], s));
-    hipLaunchKernelGGL(k_needs_packed, dim3((uint32_t)blocks), dim3(NEEDS_T), 0, s, d, *out, need_slots, seq_slots, err);
+    hipLaunchKernelGGL(k_needs_bounds, dim3((uint32_t)((blocks + 1 + 255) / 256)), dim3(256), 0, s, d, blocks, wb);
+    hipLaunchKernelGGL(k_needs_packed, dim3((uint32_t)blocks), dim3(NEEDS_T), 0, s, d, *out, need_slots, seq_slots, err,
+                       (const WgBound *)wb);
     if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[1], s));
     CORRO_HIP_TRY(hipGetLastError());
     unsigned long long e = 0;
@@ -978,6 +1042,14 @@ extern "C" int corro_compute_needs_packed(corro_ctx *ctx, const corro_sync_entri
         CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[6], ctx->ev[0], ctx->ev[1]));
         ctx->last_ms[7] = 0.f;
     }
+#if defined(CORRO_DIAG) && (CORRO_DIAG & 128)
+    {
+        unsigned long long ph[5];
+        CORRO_HIP_TRY(hipMemcpy(ph, err, 40, hipMemcpyDeviceToHost));
+        fprintf(stderr, "NDIAG us per workgroup: staging %.3f count %.3f scan %.3f fill %.3f\n", ph[1] / 100.0 / blocks,
+                ph[2] / 100.0 / blocks, ph[3] / 100.0 / blocks, ph[4] / 100.0 / blocks);
+    }
+#endif
     if (e & 1) return fail(CORRO_E_RANGE, "needs exceed their bound slots (overlapping need ranges: use corro_compute_needs)");
     if (e & 2) return fail(CORRO_E_RANGE, "a partial's seq ranges do not fit the packed need word");
     return CORRO_OK;
