@@ -36,7 +36,7 @@ EXPORTS = [
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
     "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
-    "corro_booked_insert_db_batch",
+    "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -181,6 +181,8 @@ def lib():
         "corro_scan_offsets": (i32, [vp, vp, vp, u64]),
         "corro_compute_needs_onepass": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsOut), u64, u64, vp]),
         "corro_needs_bound": (i32, [vp, C.POINTER(SyncEntries), i32, vp, vp]),
+        "corro_affinity_of_type": (i32, [C.c_char_p]),
+        "corro_table_set_affinity": (i32, [vp, u32, vp, u32]),
         "corro_booked_insert_db_batch": (i32, [vp, C.POINTER(GapsIn), C.POINTER(GapsOut)]),
         "corro_compute_needs_packed": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsPackedOut), u64, u64]),
         "corro_bookie_seq_bookkeeping": (i32, [vp, vp, u64, vp, vp, u64, vp, vp, vp]),

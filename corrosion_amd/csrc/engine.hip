@@ -69,6 +69,7 @@ int ovf_scan_tiles(void *temp, size_t *temp_bytes, const OvfDev &d, const CsAgg 
 int grow_regions(corro_ctx *ctx, uint32_t new_log2S);
 int grow_heap(corro_ctx *ctx, uint64_t want_records);
 RowStore row_store(corro_ctx *ctx);
+int affinity_check(corro_ctx *ctx, const BatchDev &bd);  // affinity.hip
 
 // Oversized buckets (queued by a merge round), all at once and device-wide (the phases of
 // ovf_kernels.h): batch fields + row ids -> region lookups (prior records appended, new rows
@@ -519,7 +520,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
-                      &ctx->d_ncols, &ctx->d_part, &ctx->d_arena};
+                      &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     for (auto &e : ctx->ev)
@@ -907,6 +908,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     if (out && out->impact && !imp_dev) TRY(ctx->d_impact.ensure(n));
     uint8_t *imp_buf = !(out && out->impact) ? nullptr : (imp_dev ? out->impact : ctx->d_impact.as<uint8_t>());
 
+    TRY(affinity_check(ctx, bd));
     const uint64_t chunk = chunk_changes(ctx);
     if (n > chunk) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));

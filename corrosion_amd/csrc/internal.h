@@ -156,6 +156,9 @@ struct corro_ctx {
     size_t wire_sites_n = 0;
     uint32_t wire_hmask = 0;
     corro::DevBuf d_ncols;        // u16 column count per table
+    std::vector<uint8_t> aff;     // column affinity per (table, cid), (MAX_COLS + 1) per table
+    corro::DevBuf d_aff, d_affflag;
+    bool aff_any = false;         // some column has an affinity other than BLOB
     corro::DevBuf d_part;         // partition counts
     uint64_t *h_misc = nullptr;   // pinned, 16 words
     // stage timing

@@ -110,6 +110,15 @@ class MergeEngine:
         name = self.schema[t][0]
         (self.interned.add if on else self.interned.discard)(name)
 
+    # ---- column affinity -------------------------------------------------------------------
+    def set_column_types(self, table, decl_types):
+        """Register the table's declared column types (one per non-pk column, in cid order): their
+        SQLite affinities (corro_affinity_of_type) make the engine refuse values the affinity would
+        convert (corro_table_set_affinity)."""
+        t = self.table_index(table)
+        aff = np.array([L.lib().corro_affinity_of_type(str(d).encode()) for d in decl_types], np.uint8)
+        L.check(L.lib().corro_table_set_affinity(self._h, t, aff.ctypes.data if len(aff) else None, len(aff)))
+
     def pk_keys(self, table, packed):
         """Row keys of packed pks (a list of bytes, pack_columns encoding) of one table."""
         t = self.table_index(table)

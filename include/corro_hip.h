@@ -176,6 +176,21 @@ int corro_pk_keys(corro_ctx *ctx, uint32_t table, const uint8_t *bytes, const ui
 int corro_pk_bytes(corro_ctx *ctx, uint32_t table, const uint64_t *keys, uint64_t n, uint8_t *bytes, uint64_t cap,
                    uint64_t *out_off);
 
+/* ------------------------------------------------------------------ column affinity */
+
+/* SQLite column affinity. cr-sqlite stores a winning value through the base table,
+ * whose column affinity may convert it; the next change is then compared unconverted against the
+ * converted value. The engine merges values already in the class their column's affinity keeps (what
+ * corrosion's writers send) and REFUSES a batch holding a value the affinity would convert
+ * (CORRO_E_RANGE, nothing merged) instead of merging it inexactly. Without a registered affinity a
+ * column is BLOB (no conversion, no check). */
+enum { CORRO_AFF_BLOB = 0, CORRO_AFF_TEXT = 1, CORRO_AFF_NUMERIC = 2, CORRO_AFF_INTEGER = 3, CORRO_AFF_REAL = 4 };
+/* sqlite3AffinityType of a declared column type (schema.rs's column type names): INT -> INTEGER,
+ * CHAR/CLOB/TEXT -> TEXT, BLOB or none -> BLOB, REAL/FLOA/DOUB -> REAL, else NUMERIC. Host only. */
+int corro_affinity_of_type(const char *decl_type);
+/* aff[c - 1] = affinity of cid c, ncols = the table's column count. */
+int corro_table_set_affinity(corro_ctx *ctx, uint32_t table, const uint8_t *aff, uint32_t ncols);
+
 /* ------------------------------------------------------------------ merge */
 
 /* Merge one batch into the device state (equivalent to one INSERT INTO crsql_changes per change,

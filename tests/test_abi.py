@@ -120,3 +120,16 @@ def test_pk_canonical_form():
     assert _canon(b"\x01\x05") == b"\x01\x05"                              # NULL
     assert _canon(b"\x01\x0b\x05ab") is None                               # length past the end
     assert _canon(b"\x01\x07") is None                                     # no such column type
+
+
+def test_affinity_of_type_rules():
+    """sqlite3AffinityType's rule order (the column types of schema.rs): INT anywhere -> INTEGER
+    (so 'FLOATING POINT' is INTEGER), CHAR/CLOB/TEXT -> TEXT, BLOB or no type -> BLOB,
+    REAL/FLOA/DOUB -> REAL, anything else -> NUMERIC."""
+    import corrosion_amd._lib as L
+    f = L.lib().corro_affinity_of_type
+    cases = {b"INTEGER": 3, b"int": 3, b"BIGINT": 3, b"TEXT": 1, b"VARCHAR(10)": 1, b"CLOB": 1, b"BLOB": 0,
+             b"": 0, b"REAL": 4, b"DOUBLE PRECISION": 4, b"FLOAT": 4, b"NUMERIC": 2, b"BOOLEAN": 2,
+             b"DECIMAL(10,5)": 2, b"FLOATING POINT": 3, b"CHARINT": 3}
+    for t, a in cases.items():
+        assert f(t) == a, t
