@@ -249,6 +249,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
     alg_bytes = ALG_BYTES_PER_CHANGE * n + ALG_BYTES_PER_CELL * cells
     achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
     steady = steady_state(eng, prep, n, dev, dt / args.steps * 1e3, cells)
+    agent = agent_path(eng, batch, n)
     e2e = host_batch_e2e(eng, batch, n)
     cpu = None if args.no_cpu_baseline else cpu_baseline(batch)
     line = {
@@ -277,6 +278,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
                      "dominant": max(kern, key=kern.get)},
         "cpu_baseline": cpu,
         "steady_state": steady,
+        "agent_path": agent,
         "end_to_end_h2d": e2e,
     }
     print(json.dumps(line), flush=True)
@@ -328,6 +330,27 @@ def steady_state(eng, prep, n, dev, empty_ms, cells, reps=3):
     return {"ms": med, "state_cells_before": int(cells), "ratio_vs_empty_state": med / empty_ms,
             "note": "a second 64M config-2 batch applied into the ~16.5M-cell state of the first (median of "
                     f"{reps}); empty-state step = reset + apply"}
+
+
+def agent_path(eng, batch, n, reps=3):
+    """The same batch applied with per-change impact flags (crsql_rows_impacted growth: what
+    process_multiple_changes asks for, util.rs:1246-1262) into an empty state; median of `reps`."""
+    import torch
+    prep = eng.prepare(batch, impact=True)
+    ms = []
+    for _ in range(reps):
+        eng.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.apply_prepared(prep)
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) * 1e3)
+    ms.sort()
+    med = ms[len(ms) // 2]
+    stages = eng.last_timings()
+    del prep
+    return {"ms": med, "changes_per_s": n / (med * 1e-3), "merge_ms": stages.get("k_merge"),
+            "note": f"config-2 batch with impact flags (the agent path), reset + apply, median of {reps}"}
 
 
 def run_multi(args, world, rank):

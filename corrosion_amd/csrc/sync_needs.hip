@@ -726,7 +726,11 @@ __device__ inline void walk_inputs(const SyncDev &in, const EntryHdr &h, const N
 
 // err[0] |= 1: a workgroup's needs exceed its bound slots (overlapping input ranges); 2: a partial
 // with >= 2^24 seq ranges or a seq slot >= 2^40 (not representable in the packed word)
-__global__ void __launch_bounds__(NEEDS_T) k_needs_packed(SyncDev in, corro_needs_packed_out o, uint64_t need_slots,
+#ifndef NEEDS_PACKED_WAVES
+#define NEEDS_PACKED_WAVES 6  // waves per SIMD the compiler budgets registers for: LDS allows 6
+                              // workgroups per CU; at 6 (84 B of spills) 5.25 ms vs 6.92 ms at 4 (no spills)
+#endif
+__global__ void __launch_bounds__(NEEDS_T, NEEDS_PACKED_WAVES) k_needs_packed(SyncDev in, corro_needs_packed_out o, uint64_t need_slots,
                                                           uint64_t seq_slots, unsigned long long *err,
                                                           const WgBound *__restrict__ wb) {
     __shared__ NeedsLds L;

@@ -18,7 +18,8 @@ def child():
     eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=n, device=0)
     eng.register_sites(synth.site_ids(1000, 1))
     batch = synth.uniform_batch_torch(n, 1000, 1 << 22, 4, seed=synth.config_seed(2), device=dev)
-    prep = eng.prepare(batch) if hasattr(eng, "prepare") else None
+    impact = os.environ.get("DIAG_IMPACT") == "1"  # the agent path: per-change impact flags
+    prep = eng.prepare(batch, impact=impact) if hasattr(eng, "prepare") else None
     eng.set_profiling(True)
     acc = {}
     for it in range(8):
@@ -26,7 +27,7 @@ def child():
         if prep is not None:
             eng.apply_prepared(prep)
         else:
-            eng.apply(batch)
+            eng.apply(batch, impact=impact)
         torch.cuda.synchronize()
         if it >= 3:
             for k, v in eng.last_timings().items():
