@@ -119,7 +119,7 @@ def _read_counter(dirname, counter):
     return tot, per
 
 
-def pmc_traffic_live(changes, applies=3, timeout=240):
+def pmc_traffic_live(changes, applies=3, timeout=240, child_cmd=None):
     """HBM bytes per apply measured now: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: they do
     not fit one pass) over a child run of this bench doing `applies` applies of the same workload.
     Counters are KiB; FETCH_SIZE is doubled (gfx950 reports half of wide coalesced reads,
@@ -134,9 +134,10 @@ def pmc_traffic_live(changes, applies=3, timeout=240):
     got, per = {}, {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="corro_pmc_", dir=tmp)
+        child = child_cmd or [os.path.abspath(__file__), "--pmc-child", "--changes", str(changes), "--steps",
+                              str(applies - 1), "--warmup", "1"]
         cmd = ["timeout", "-k", "10", "-s", "KILL", str(timeout), rp, "--pmc", counter, "--output-format", "csv",
-               "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
-               "--changes", str(changes), "--steps", str(applies - 1), "--warmup", "1"]
+               "-d", d, "-o", "run", "--", sys.executable] + child
         try:
             r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout + 30)
         except subprocess.TimeoutExpired:

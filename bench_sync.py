@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--mode", choices=("packed", "two-pass", "one-pass"), default="packed",
                     help="packed: corro_compute_needs_packed (one pass into bound-reserved slots, 16-B need "
                          "pairs); two-pass: corro_compute_needs count + fill; one-pass: "
@@ -82,6 +84,19 @@ def main():
         sys.exit(launch_ranks(args.gpus, __file__))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    PMC_RUNS = 3
+    traffic = None
+    if world == 1 and not args.pmc_child and not args.no_pmc:
+        # HBM bytes per diff from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over a child run of this
+        # script doing PMC_RUNS diffs, before this process touches the GPU (bench.py's recipe)
+        from bench import pmc_traffic_live
+        child = [os.path.abspath(__file__), "--pmc-child", "--mode", args.mode, "--pairs", str(args.pairs),
+                 "--actors-per-pair", str(args.actors_per_pair)]
+        tb, note, per = pmc_traffic_live(0, applies=PMC_RUNS, child_cmd=child)
+        if per:  # the need-diff kernels only (the child's data generation runs torch / rocPRIM kernels)
+            per = {k: v for k, v in per.items() if k.startswith("k_needs") or k.startswith("k_scan")}
+            tb = sum(v["fetch"] + v["write"] for v in per.values())
+        traffic = {"bytes": tb, "source": note, "by_kernel": per}
 
     import torch
     import synth
@@ -105,6 +120,11 @@ def main():
     pairs_local = (rank + 1) * args.pairs // world - rank * args.pairs // world
     ent = synth.sync_entries_torch(pairs_local, args.actors_per_pair, synth.config_seed(4) + 7919 * rank, device=dev)
     torch.cuda.synchronize()
+    if args.pmc_child:  # exactly PMC_RUNS diffs, nothing else of ours
+        for _ in range(PMC_RUNS):
+            run(eng, ent)
+        torch.cuda.synchronize()
+        return
     eng.set_profiling(True)
     for _ in range(args.warmup):
         res = run(eng, ent)
@@ -153,7 +173,13 @@ def main():
             "roofline": {"bound": "hbm", "kernel": {"packed": "k_needs_packed (one pass)", "two-pass": "k_needs (count + fill)",
                                                     "one-pass": "k_needs1 (one pass, look-back)"}[args.mode],
                          "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic["bytes"] if traffic else None,
+                         "traffic_ratio": (traffic["bytes"] / alg) if traffic and traffic["bytes"] else None,
+                         "traffic_by_kernel": traffic["by_kernel"] if traffic else None,
+                         "alg_bytes": alg,
+                         "output_bytes": (17 * n_needs + 12 * E if args.mode == "packed" else 33 * n_needs + 32 * E)
+                         + 16 * n_seqs,
                          "kernels_ms": kt, "count_pass_ms": kc, "fill_pass_ms": kf}}
     if rank == 0:
         if world == 1:

@@ -522,8 +522,11 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t ro
     ovf_publish(a, d, row, e, bits, cnt, general);
 }
 
+#ifndef OVF_WALK_WAVES
+#define OVF_WALK_WAVES 4  // 6 or 8 (spilling) measured no faster on config 5
+#endif
 template <bool REG>
-static __global__ void k_ovf_walk(MergeArgs a, OvfDev d) {
+static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeArgs a, OvfDev d) {
     OVF_LOOP(row, d.nrows) {  // one thread per row (dense ids), every lane busy
         const uint32_t j0 = d.rstart[row];
         if (d.rbad[row]) {  // outside App. A.3: the sequential fold over the row's sorted records
