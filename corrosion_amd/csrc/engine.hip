@@ -315,10 +315,10 @@ static int ctx_prepare_device(corro_ctx *ctx) {
 }  // extern "C"
 
 // Initial row-store sizes from the capacity hint (expected changes per apply): regions at about half
-// fill for hint/4 rows, a heap of hint/2 records; both grow on demand.
+// fill for hint/16 rows, a heap of hint/2 records; both grow on demand.
 static int store_alloc(corro_ctx *ctx, uint64_t capacity_hint) {
     const uint32_t B = ctx->B;
-    const uint64_t rows = std::max<uint64_t>(1024, capacity_hint / 4);
+    const uint64_t rows = std::max<uint64_t>(1024, capacity_hint / 16);  // (~4 changes per row, half of them new)
     uint32_t lg = 4;
     // (region entries are named by 32-bit indices: B << log2S stays <= 2^31)
     while (((uint64_t)B << lg) < 2 * rows && lg < 20 && ((uint64_t)B << (lg + 1)) <= (1ULL << 31)) lg++;
@@ -337,9 +337,9 @@ static int store_clear(corro_ctx *ctx) {
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_ent.p, 0, ((size_t)ctx->B << ctx->log2S) * sizeof(RowEnt), s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_used.p, 0, ctx->B * 4ULL, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_gen.p, 0, ctx->B * 4ULL, s));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_heap_top.p, 0, 8, s));
-    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_heap_top.p, 0, 8, s));  // (stream-ordered before the next apply)
     ctx->state_total = 0;
+    ctx->state_rows = 0;
     ctx->arena_top = 0;
     ctx->state_epoch++;
     return CORRO_OK;
@@ -814,9 +814,12 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     }
     hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
                        ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites);
+    CORRO_HIP_TRY(hipMemsetAsync(misc + MISC_ROWS, 0, 8, s));
+    hipLaunchKernelGGL(k_sum_used, dim3(1), dim3(1024), 0, s, ctx->d_used.as<uint32_t>(), B, misc);
     CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, MISC_WORDS * 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     ctx->state_total += ctx->h_misc[MISC_LIVE];  // (a signed delta in two's complement)
+    ctx->state_rows = ctx->h_misc[MISC_ROWS];
 #if CORRO_DIAG & 64
     fprintf(stderr, "DIAG phases (us per bucket): load %.3f claims %.3f rows_count %.3f stage1 %.3f stages %.3f fast_rows %.3f winners %.3f publish %.3f\n",
             ctx->h_misc[MISC_DIAG] / 100.0 / B, ctx->h_misc[MISC_DIAG + 1] / 100.0 / B,
@@ -826,11 +829,12 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
 #endif
     ctx->state_epoch++;
     if (ctx->h_misc[MISC_WIDE]) ctx->state_wide = true;
-    // keep the regions under half full for the next batch
-    uint64_t rows_cap = ((uint64_t)B << ctx->log2S) / 2;
-    if (ctx->state_total > rows_cap) {
+    // keep the regions' average fill at most 5/8 for the next batch (rows, not clock records: a
+    // row's cells share one entry); growth takes them back to at most half
+    const uint64_t slots = (uint64_t)B << ctx->log2S;
+    if (ctx->state_rows * 8 > slots * 5) {
         uint32_t lg = ctx->log2S;
-        while (((uint64_t)B << lg) / 2 < ctx->state_total && lg < 26 && ((uint64_t)B << (lg + 1)) <= (1ULL << 31)) lg++;
+        while (((uint64_t)B << lg) / 2 < ctx->state_rows && lg < 26 && ((uint64_t)B << (lg + 1)) <= (1ULL << 31)) lg++;
         TRY(grow_regions(ctx, lg));
     }
     return CORRO_OK;

@@ -116,6 +116,7 @@ struct corro_ctx {
     uint64_t heap_cap = 0;        // records
     uint32_t max_stride = 1;
     uint64_t state_total = 0;     // clock records in the state
+    uint64_t state_rows = 0;      // rows (region entries) in the state
     bool track_ts = false;
     bool state_wide = false;      // some clock row holds a non-INTEGER value
     corro::DevBuf d_defer, d_relist;  // deferred buckets of a merge round, the re-merge list

@@ -69,7 +69,7 @@ struct MergeArgs {
 // misc words
 constexpr int MISC_ERR = 0, MISC_OVF = 1, MISC_LIVE = 2, MISC_WIDE = 3, MISC_GEN = 4, MISC_WIDEQ = 5,
               MISC_GEN_SMALL = 6, MISC_GEN_MID = 7, MISC_DEFER = 8, MISC_DEFER_WHY = 9, MISC_CVBIG = 10,
-              MISC_DIAG = 16, MISC_WORDS = 24;
+              MISC_ROWS = 11, MISC_DIAG = 16, MISC_WORDS = 24;
 constexpr unsigned long long DEFER_REGION = 1, DEFER_HEAP = 2;
 
 // misc[0] error bits
@@ -2083,6 +2083,15 @@ k_merge_gen_small(MergeArgs a) {
 
 // Validation of a whole batch before a chunked apply commits its first chunk (the checks k_scatter
 // makes per chunk; a batch is applied all or nothing).
+// Rows in the state after an apply: the sum of the regions' entry counts (sizes the regions).
+static __global__ void __launch_bounds__(1024) k_sum_used(const uint32_t *__restrict__ used, uint32_t B,
+                                                          unsigned long long *misc) {
+    unsigned long long t = 0;
+    for (uint32_t b = threadIdx.x; b < B; b += 1024) t += used[b];
+    for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d);
+    if ((threadIdx.x & 63) == 0 && t) atomicAdd(&misc[MISC_ROWS], t);
+}
+
 static __global__ void k_validate(BatchDev in, uint32_t nsites, const uint16_t *__restrict__ ncols, uint32_t ntables,
                                   unsigned long long *misc) {
     uint32_t err = 0, wide = 0;
