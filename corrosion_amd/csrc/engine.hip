@@ -763,13 +763,13 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         }
         mark(4);
         if (a.impact) {
-            hipLaunchKernelGGL(k_merge_fast_int<true>, dim3(nblocks), dim3(MERGE_THREADS), 0, s, a);
+            hipLaunchKernelGGL(k_merge_fast_int<true>, dim3(nblocks), dim3(FAST_T), 0, s, a);
             CORRO_HIP_TRY(hipGetLastError());
-            hipLaunchKernelGGL(k_merge_fast_wide<true>, dim3(std::min(nblocks, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+            hipLaunchKernelGGL(k_merge_fast_wide<true>, dim3(std::min(nblocks, LIST_GRID)), dim3(FAST_T), 0, s, a);
         } else {
-            hipLaunchKernelGGL(k_merge_fast_int<false>, dim3(nblocks), dim3(MERGE_THREADS), 0, s, a);
+            hipLaunchKernelGGL(k_merge_fast_int<false>, dim3(nblocks), dim3(FAST_T), 0, s, a);
             CORRO_HIP_TRY(hipGetLastError());
-            hipLaunchKernelGGL(k_merge_fast_wide<false>, dim3(std::min(nblocks, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
+            hipLaunchKernelGGL(k_merge_fast_wide<false>, dim3(std::min(nblocks, LIST_GRID)), dim3(FAST_T), 0, s, a);
         }
         CORRO_HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_merge_gen_small, dim3(std::min(nblocks, 4 * LIST_GRID)), dim3(GEN_SMALL_THREADS), 0, s, a);

@@ -36,8 +36,14 @@ constexpr int HIST_THREADS = 512;
 constexpr uint64_t CV_PACKED_LIMIT = 1ULL << 15;
 constexpr uint32_t TILES_MAX = 256;                    // hist/scatter tiles: one per CU
 constexpr int MERGE_THREADS = 512;
-constexpr int FAST_R = 6;                              // records per thread, fast body
-constexpr int CAP_FAST = MERGE_THREADS * FAST_R;       // 3072
+#ifndef CORRO_FAST_T
+#define CORRO_FAST_T 512
+#endif
+constexpr int FAST_T = CORRO_FAST_T;                   // threads of a fast-body workgroup
+constexpr int CAP_FAST = 3072;                         // records a fast body holds
+constexpr int FAST_R = CAP_FAST / FAST_T;              // records per thread
+static_assert(FAST_R * FAST_T == CAP_FAST, "FAST_T must divide CAP_FAST");
+constexpr int FAST_WAVES_EU = 2 * (FAST_T / 64) / 4;  // two workgroups per CU (LDS)
 constexpr int FAST_SLOTS = 4096;                       // cell table (distinct cells <= records)
 constexpr int CAP_GEN = 2048;                          // records, general body in LDS
 constexpr int GEN_SLOTS = 4096;
@@ -1169,7 +1175,7 @@ __device__ inline void fast_rows_count(uint32_t n, const uint32_t (&row)[R], con
     uint32_t rows = 0;
 #pragma unroll
     for (int k = 0; k < R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         const bool own = i < n && row[k] == i;
         const uint32_t off = wave_lds_add(&s_ctl[1], own ? strd[k] : 0u);
         if (own) s_heap[i] = 0x80000000u | off;
@@ -1211,11 +1217,11 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
     uint32_t *s_bm = s_heap + CAP_FAST;
     const bool lds_claim = S <= 32 * RS_BM_WORDS;
     if (lds_claim)
-        for (uint32_t w = tid; w < (S + 31) / 32; w += MERGE_THREADS) s_bm[w] = 0;
+        for (uint32_t w = tid; w < (S + 31) / 32; w += FAST_T) s_bm[w] = 0;
     uint32_t e0[R], hw[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         ent[k] = ROW_NONE;
         e0[k] = 0;
         hw[k] = 0;
@@ -1257,7 +1263,7 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
     if (!counted) {
 #pragma unroll
         for (int k = 0; k < R; k++)
-            if (ent[k] != ROW_NONE) s_heap[k * MERGE_THREADS + tid] = hw[k];
+            if (ent[k] != ROW_NONE) s_heap[k * FAST_T + tid] = hw[k];
         if (tid == 0) fast_rows_alloc(a, b, used0, s_ctl, s_hbase);
         __syncthreads();
     }
@@ -1265,7 +1271,7 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
     // new rows: their region entries (presence bits published by the caller at the end)
 #pragma unroll
     for (int k = 0; k < R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (ent[k] != ROW_NONE - 1) continue;
 #if CORRO_DIAG & 2
         ent[k] = ROW_NONE;
@@ -1332,20 +1338,20 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
 #define DIAG_MARK(k) do { } while (0)
 #endif
 #pragma unroll
-    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * FAST_T + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
     if (tid == 0) {
         s_live = 0;
         s_ctl[0] = s_ctl[1] = s_ctl[2] = s_ctl[3] = 0;
     }
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) {
+    for (uint32_t i = tid; i < FAST_SLOTS; i += FAST_T) {
         s_own[i] = 0;
         reinterpret_cast<uint32_t *>(s_k)[i] = 0;  // the row table of row_claim
     }
     uint32_t srank[FAST_R];
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;  // < CAP_FAST: stores of dead lanes are harmless
+        const uint32_t i = k * FAST_T + tid;  // < CAP_FAST: stores of dead lanes are harmless
         alive[k] = i < n;
         cell[k] = 0;
         const Rec r = rec_from_wave_quads(q[k]);
@@ -1368,13 +1374,13 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         srank[k] = a.site_rank[site[k] < a.nsites ? site[k] : 0u];
-        strd[k] = used0 ? 0u : (uint32_t)a.rs.stride[alive[k] ? s_tc[k * MERGE_THREADS + tid] >> 16 : 0u];
+        strd[k] = used0 ? 0u : (uint32_t)a.rs.stride[alive[k] ? s_tc[k * FAST_T + tid] >> 16 : 0u];
     }
     __syncthreads();
     DIAG_MARK(0);
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         row[k] = 0;
         if (!alive[k]) continue;
         row[k] = row_claim(reinterpret_cast<uint32_t *>(s_k), s_pk, s_tc, i, s_pk[i], s_tc[i] >> 16);
@@ -1382,7 +1388,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (!alive[k]) continue;
         cell[k] = cell_claim(s_own, i, row[k], s_tc[i]);
         if (cell[k] == i) s_k[i] = 0;
@@ -1468,7 +1474,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         if (st + 1 < nstages) {
 #pragma unroll
             for (int k = 0; k < FAST_R; k++) {
-                const uint32_t i = k * MERGE_THREADS + tid;
+                const uint32_t i = k * FAST_T + tid;
                 if (i < n && cell[k] == i) s_k[i] = 0;
             }
             __syncthreads();
@@ -1486,7 +1492,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
         if (!alive[k]) continue;
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         const uint32_t c = s_tc[i] & 0xFFFFu;
         hb[k] = row_heap(s_own[row[k]], s_hbase) + c;
         if ((s_k[row[k]] >> c) & 1ULL) {
@@ -1513,7 +1519,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     // winners: the clock row into its heap slot (wave-cooperative 64-B stores)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         Rec x;
         if (alive[k]) {
             if (WIDE) {
@@ -1553,7 +1559,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
     // owners publish the rows' presence bits
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_k[i];
     }
     if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
@@ -1576,7 +1582,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     __shared__ uint16_t s_list[CAP_FAST];
     __shared__ uint64_t s_v1[CAP_FAST];
     __shared__ uint32_t s_meta[CAP_FAST];
-    __shared__ uint32_t s_wsum[MERGE_THREADS / 64];
+    __shared__ uint32_t s_wsum[FAST_T / 64];
     __shared__ uint32_t s_ctl[4];
     __shared__ unsigned long long s_hbase, s_live;
     const uint32_t tid = threadIdx.x;
@@ -1588,19 +1594,19 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     uint32_t flags = 0;  // bit 2k: beats the prior clock; bit 2k+1: the cell had no prior clock
     uint4 q[FAST_R][4];
 #pragma unroll
-    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * FAST_T + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
     if (tid == 0) {
         s_live = 0;
         s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
     }
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) {
+    for (uint32_t i = tid; i < FAST_SLOTS; i += FAST_T) {
         s_own[i] = 0;
         reinterpret_cast<uint32_t *>(s_v0)[i] = 0;  // the row table of row_claim
     }
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         alive[k] = i < n;
         cell[k] = 0;
         const Rec r = rec_from_wave_quads(q[k]);
@@ -1625,7 +1631,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     // 1. rows, then cells (row_claim / cell_claim)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         row[k] = 0;
         if (!alive[k]) continue;
         row[k] = row_claim(reinterpret_cast<uint32_t *>(s_v0), s_pk, s_tc, i, pk[k], tc[k] >> 16);
@@ -1633,7 +1639,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++)
-        if (alive[k]) cell[k] = cell_claim(s_own, k * MERGE_THREADS + tid, row[k], tc[k]);
+        if (alive[k]) cell[k] = cell_claim(s_own, k * FAST_T + tid, row[k], tc[k]);
     __syncthreads();
     // 1b. row lookups, prior clocks: does the change beat its cell's prior?
     if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_pk, s_tc, s_own, s_v0, s_ctl, &s_hbase, false)) return;
@@ -1658,11 +1664,11 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     }
     __syncthreads();
     // 2. member counts per owner (s_own reused), keys into LDS
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += FAST_T) s_own[i] = 0;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (!alive[k]) continue;
         s_pk[i] = cv[k];
         s_tc[i] = rank[k];
@@ -1707,14 +1713,14 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (alive[k]) s_list[atomicAdd(&s_own[cell[k]], 1u)] = (uint16_t)i;
     }
     __syncthreads();
     // 4. one walk over the cell's members per change: impact (strict prefix max) and winner
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (!alive[k]) continue;
         const uint32_t mend = s_own[cell[k]];
         bool imp = (flags >> (2 * k)) & 1u, win = imp;
@@ -1743,7 +1749,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     // 5. winners: the clock row into its heap slot; presence bits of new cells (s_v0 per owner)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (ent[k] != ROW_NONE && row[k] == i) s_v0[i] = a.rs.ent[ent[k]].bits[0];
     }
     __syncthreads();
@@ -1777,7 +1783,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_v0[i];
     }
     if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
@@ -1792,7 +1798,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     __shared__ uint32_t s_b[CAP_FAST];      // hashing: table_cid; then positions by member slot; then site ranks
     __shared__ uint64_t s_c[CAP_FAST];      // row presence words; then cell-ordered values; then presence words
     __shared__ uint32_t s_own[FAST_SLOTS];  // cell / row hashing; heap indices; member counts / offsets / ends
-    __shared__ uint32_t s_wsum[MERGE_THREADS / 64];
+    __shared__ uint32_t s_wsum[FAST_T / 64];
     __shared__ uint32_t s_ctl[4];
     __shared__ unsigned long long s_hbase, s_live;
     const uint32_t tid = threadIdx.x;
@@ -1805,19 +1811,19 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     bool alive[FAST_R];
     uint4 q[FAST_R][4];
 #pragma unroll
-    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * MERGE_THREADS + (tid & ~63u), n, q[k]);
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * FAST_T + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
     if (tid == 0) {
         s_live = 0;
         s_ctl[0] = s_ctl[1] = s_ctl[2] = 0;
     }
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) {
+    for (uint32_t i = tid; i < FAST_SLOTS; i += FAST_T) {
         s_own[i] = 0;
         reinterpret_cast<uint32_t *>(s_c)[i] = 0;  // the row table of row_claim
     }
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         alive[k] = i < n;
         cell[k] = 0;
         const Rec r = rec_from_wave_quads(q[k]);
@@ -1840,7 +1846,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     // 1. rows, then cells (row_claim / cell_claim)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         row[k] = 0;
         if (!alive[k]) continue;
         row[k] = row_claim(reinterpret_cast<uint32_t *>(s_c), s_a, s_b, i, pk[k], tc[k] >> 16);
@@ -1848,7 +1854,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++)
-        if (alive[k]) cell[k] = cell_claim(s_own, k * MERGE_THREADS + tid, row[k], tc[k]);
+        if (alive[k]) cell[k] = cell_claim(s_own, k * FAST_T + tid, row[k], tc[k]);
     __syncthreads();
     // 1b. row lookups, prior clocks: does the change beat its cell's prior?
     if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase, false)) return;
@@ -1867,7 +1873,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     }
     __syncthreads();
     // 2. member counts per owner, exclusive scan -> offsets
-    for (uint32_t i = tid; i < FAST_SLOTS; i += MERGE_THREADS) s_own[i] = 0;
+    for (uint32_t i = tid; i < FAST_SLOTS; i += FAST_T) s_own[i] = 0;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++)
@@ -1950,7 +1956,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     // 5. winners: the clock row into its heap slot; presence bits of new cells (s_c per owner)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (ent[k] != ROW_NONE && row[k] == i) s_c[i] = a.rs.ent[ent[k]].bits[0];
     }
     __syncthreads();
@@ -1984,7 +1990,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
-        const uint32_t i = k * MERGE_THREADS + tid;
+        const uint32_t i = k * FAST_T + tid;
         if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_c[i];
     }
     if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
@@ -1998,7 +2004,7 @@ __device__ inline uint32_t bucket_of_block(const MergeArgs &a) {
 // batch or state with non-INTEGER values, every fast bucket are queued for the list-driven kernels
 // below, so those launch a few hundred workgroups instead of one per bucket.
 template <bool IMPACT>
-static __global__ void __launch_bounds__(MERGE_THREADS, 4)
+static __global__ void __launch_bounds__(FAST_T, FAST_WAVES_EU)
 k_merge_fast_int(MergeArgs a) {
     const uint32_t b = bucket_of_block(a);
     // every per-bucket word is loaded up front (independent scalar loads, one latency)
@@ -2037,7 +2043,7 @@ k_merge_fast_int(MergeArgs a) {
 constexpr uint32_t LIST_GRID = 512;
 
 template <bool IMPACT>
-static __global__ void __launch_bounds__(MERGE_THREADS, IMPACT ? 2 : 4)
+static __global__ void __launch_bounds__(FAST_T, IMPACT ? FAST_WAVES_EU / 2 : FAST_WAVES_EU)
 k_merge_fast_wide(MergeArgs a) {
     const uint32_t cnt = (uint32_t)a.misc[MISC_WIDEQ];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
