@@ -37,6 +37,7 @@ EXPORTS = [
     "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
     "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity",
+    "corro_ctx_metrics", "corro_table_committed",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -85,6 +86,12 @@ class ExtractIn(C.Structure):
 class ExtractOut(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("grp_count", "row_count", "grp_off", "row_off", "version", "last_seq",
                                           "ts", "grp_row_off", "grp_rows")] + [("rows", Rows)]
+
+
+class Metrics(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("applies", "changes", "overflow_rounds", "deferred_rounds",
+                                          "region_growths", "heap_growths", "state_rows", "state_records",
+                                          "max_batch")] + [("apply_seconds", C.c_double)]
 
 
 class GapsIn(C.Structure):
@@ -182,6 +189,8 @@ def lib():
         "corro_compute_needs_onepass": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsOut), u64, u64, vp]),
         "corro_needs_bound": (i32, [vp, C.POINTER(SyncEntries), i32, vp, vp]),
         "corro_affinity_of_type": (i32, [C.c_char_p]),
+        "corro_ctx_metrics": (i32, [vp, C.POINTER(Metrics)]),
+        "corro_table_committed": (i32, [vp, u32, vp]),
         "corro_table_set_affinity": (i32, [vp, u32, vp, u32]),
         "corro_booked_insert_db_batch": (i32, [vp, C.POINTER(GapsIn), C.POINTER(GapsOut)]),
         "corro_compute_needs_packed": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsPackedOut), u64, u64]),

@@ -23,6 +23,9 @@
 #include "booked.h"
 #include "corro_hip.h"
 
+// engine.hip: adds per-table committed counts to the context (corro_table_committed)
+void corro_detail_add_committed(corro_ctx *ctx, const uint64_t *counts, size_t n);
+
 namespace corro {
 int fail(int code, const std::string &msg);
 int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version);
@@ -336,8 +339,17 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
         int rc = corro::set_db_version(ctx, site, version);
         if (rc != CORRO_OK) return rc;
     }
-    for (const HostRow &r : st.buffered)  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
+    // corro.changes.committed{table} (util.rs:533-535): every buffered change of an incomplete
+    // version (:1101-1105), every impactful change of a complete one (:1254-1258, below)
+    std::vector<uint64_t> committed;
+    auto commit_count = [&](uint32_t tcid) {
+        if ((tcid >> 16) >= committed.size()) committed.resize((tcid >> 16) + 1, 0);
+        committed[tcid >> 16]++;
+    };
+    for (const HostRow &r : st.buffered) {  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
         bk->buffered[{r.site, r.dbv}].emplace(r.seq, r);
+        commit_count(r.tcid);
+    }
     for (auto &[key, sb] : st.seqbook) bk->seqbook[key] = sb;
     // impactful changes: crsql_rows_impacted() is cumulative over the transaction, while
     // last_rows_impacted restarts at 0 for every version (util.rs:1218-1261)
@@ -354,6 +366,7 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
             if (hit) {
                 any = true;
                 if (out->impactful) out->impactful[c.change_off + k] = 1;
+                commit_count(in->table_cid[c.change_off + k]);
             }
         }
         out->known[ci] = any ? CORRO_KNOWN_CURRENT : CORRO_KNOWN_CLEARED;
@@ -365,6 +378,7 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     for (auto &[actor, nb] : next) bk->actors[actor] = std::move(nb);
     for (auto &r : ready) bk->ready.push_back(r);
     out->n_ready = ready.size();
+    corro_detail_add_committed(ctx, committed.data(), committed.size());
     return CORRO_OK;
 }
 

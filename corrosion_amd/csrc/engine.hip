@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -382,6 +383,7 @@ static int arena_reserve(corro_ctx *ctx, uint64_t add) {
 // writes are in flight). Entry indices change; heap indices and presence bits move with the rows.
 int grow_regions(corro_ctx *ctx, uint32_t new_log2S) {
     if (new_log2S <= ctx->log2S) return CORRO_OK;
+    ctx->metrics.region_growths++;
     if (new_log2S > 26 || ((uint64_t)ctx->B << new_log2S) > (1ULL << 31))
         return fail(CORRO_E_NOMEM, "row store regions would exceed 2^31 entries");
     hipStream_t s = ctx->stream;
@@ -403,6 +405,7 @@ int grow_regions(corro_ctx *ctx, uint32_t new_log2S) {
 // Heap reallocated to hold at least want_records (doubling), contents copied.
 int grow_heap(corro_ctx *ctx, uint64_t want_records) {
     if (want_records <= ctx->heap_cap) return CORRO_OK;
+    ctx->metrics.heap_growths++;
     uint64_t cap = ctx->heap_cap;
     while (cap < want_records) cap *= 2;
     // (heap indices stay below 2^31: the fast bodies mark a new row's heap offset with the top bit)
@@ -789,12 +792,14 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         const uint64_t novf = ctx->h_misc[MISC_OVF];
         if (novf) {
             TRY(run_overflow(ctx, a, novf, n, prof));
+            ctx->metrics.overflow_rounds++;
             ovf_ms += ctx->last_ms[5];
         }
         const uint64_t ndefer = ctx->h_misc[MISC_DEFER];
         if (!ndefer) break;
         // grow what ran out, then merge the deferred buckets again
         const uint64_t why = ctx->h_misc[MISC_DEFER_WHY];
+        ctx->metrics.deferred_rounds++;
         if (why & DEFER_REGION) TRY(grow_regions(ctx, ctx->log2S + 1));
         if (why & DEFER_HEAP) {
             unsigned long long top = 0;
@@ -851,9 +856,24 @@ static uint64_t chunk_changes(const corro_ctx *ctx) {
     return std::max<uint64_t>(1ULL << 16, (uint64_t)ctx->B * 2048ULL);
 }
 
+static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out);
+
 int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out) {
     if (!ctx || !in) return fail(CORRO_E_INVALID, "NULL argument");
     if (in->n == 0) return CORRO_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = apply_batch_impl(ctx, in, mem, out);
+    if (rc == CORRO_OK) {
+        corro_metrics &m = ctx->metrics;
+        m.applies++;
+        m.changes += in->n;
+        m.max_batch = std::max<uint64_t>(m.max_batch, in->n);
+        m.apply_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return rc;
+}
+
+static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out) {
     if (in->n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
     if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
         !in->val0)
@@ -1022,6 +1042,30 @@ int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count)
 int corro_state_count(corro_ctx *ctx, uint64_t *count) {
     if (!ctx || !count) return fail(CORRO_E_INVALID, "NULL argument");
     *count = ctx->state_total;
+    return CORRO_OK;
+}
+
+int corro_ctx_metrics(corro_ctx *ctx, corro_metrics *out) {
+    if (!ctx || !out) return fail(CORRO_E_INVALID, "NULL argument");
+    *out = ctx->metrics;
+    out->state_rows = ctx->state_rows;
+    out->state_records = ctx->state_total;
+    return CORRO_OK;
+}
+
+}  // extern "C"
+
+void corro_detail_add_committed(corro_ctx *ctx, const uint64_t *counts, size_t n) {
+    if (ctx->committed.size() < ctx->tables.size()) ctx->committed.resize(ctx->tables.size(), 0);
+    for (size_t t = 0; t < n && t < ctx->committed.size(); t++) ctx->committed[t] += counts[t];
+}
+
+extern "C" {
+
+int corro_table_committed(corro_ctx *ctx, uint32_t table, uint64_t *count) {
+    if (!ctx || !count) return fail(CORRO_E_INVALID, "NULL argument");
+    if (table >= ctx->tables.size()) return fail(CORRO_E_UNKNOWN_TABLE, "no such table");
+    *count = table < ctx->committed.size() ? ctx->committed[table] : 0;
     return CORRO_OK;
 }
 

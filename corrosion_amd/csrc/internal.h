@@ -117,6 +117,8 @@ struct corro_ctx {
     uint32_t max_stride = 1;
     uint64_t state_total = 0;     // clock records in the state
     uint64_t state_rows = 0;      // rows (region entries) in the state
+    corro_metrics metrics{};      // cumulative counters (corro_ctx_metrics)
+    std::vector<uint64_t> committed;  // per table: changes committed by corro_process_multiple_changes
     bool track_ts = false;
     bool state_wide = false;      // some clock row holds a non-INTEGER value
     corro::DevBuf d_defer, d_relist;  // deferred buckets of a merge round, the re-merge list

@@ -110,6 +110,19 @@ class MergeEngine:
         name = self.schema[t][0]
         (self.interned.add if on else self.interned.discard)(name)
 
+    # ---- metrics -----------------------------------------------------------------------------
+    def metrics(self):
+        """Cumulative counters (corro_ctx_metrics) as a dict."""
+        m = L.Metrics()
+        L.check(L.lib().corro_ctx_metrics(self._h, C.byref(m)))
+        return {k: getattr(m, k) for k, _ in L.Metrics._fields_}
+
+    def committed(self, table):
+        """corro.changes.committed for one table (corro_table_committed)."""
+        c = C.c_uint64()
+        L.check(L.lib().corro_table_committed(self._h, self.table_index(table), C.byref(c)))
+        return c.value
+
     # ---- column affinity -------------------------------------------------------------------
     def set_column_types(self, table, decl_types):
         """Register the table's declared column types (one per non-pk column, in cid order): their

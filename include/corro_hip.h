@@ -221,6 +221,25 @@ int corro_value_bytes(corro_ctx *ctx, const uint64_t *handles, uint64_t n, uint8
 int corro_ctx_set_profiling(corro_ctx *ctx, int on);
 int corro_last_timings(corro_ctx *ctx, float *ms, uint32_t cap, uint32_t *count);
 
+/* ------------------------------------------------------------------ metrics */
+
+/* Cumulative counters of a context (the hot path's share of corrosion's metrics: util.rs:534,698,
+ * 1032-1034,1178 -- processing started / time / chunk size / changes committed). */
+typedef struct {
+    uint64_t applies;          /* corro_apply_batch calls that committed */
+    uint64_t changes;          /* changes merged by them (winners and losers) */
+    uint64_t overflow_rounds;  /* applies that ran the device-wide overflow fold */
+    uint64_t deferred_rounds;  /* merge rounds repeated after growing the row store */
+    uint64_t region_growths, heap_growths;
+    uint64_t state_rows, state_records;   /* now */
+    uint64_t max_batch;        /* largest batch (chunk_size) */
+    double apply_seconds;      /* wall time inside corro_apply_batch */
+} corro_metrics;
+int corro_ctx_metrics(corro_ctx *ctx, corro_metrics *out);
+/* corro.changes.committed{table}: changes of complete and partial changesets that
+ * corro_process_multiple_changes / corro_process_fully_buffered committed, per table. */
+int corro_table_committed(corro_ctx *ctx, uint32_t table, uint64_t *count);
+
 /* ------------------------------------------------------------------ multi-GPU ingest */
 
 /* Stable partition of a DEVICE-resident batch by owner rank, rank_of(table, pk) = low 32 bits of

@@ -237,3 +237,23 @@ def test_failed_call_leaves_bookkeeping_untouched():
     r = a.process_multiple_changes([empty, part])
     assert r.known == ["cleared", "partial"]
     assert a.bookie.partial(Y, 1) is not None and a.bookie.last(X) == 5
+
+
+def test_metrics_and_committed_counts():
+    """corro.changes.committed{table} (util.rs:533-535) counts the impactful changes of complete
+    versions (:1254-1258) and every buffered change of an incomplete one (:1101-1105); the context
+    counters (corro_ctx_metrics) follow corro.agent.changes.processing.* (util.rs:698, :1032-1034)."""
+    ta1, ta2 = Node(TA1), agent()
+    ta1.insert_rows(1, 3)
+    m0 = ta2.engine.metrics()
+    assert m0["applies"] == 0 and m0["changes"] == 0
+    ta2.process_multiple_changes(ta1.get_rows([((1, 3), None)]))
+    assert ta2.engine.committed("tests3") == 12 and ta2.engine.committed("tests") == 0
+    m = ta2.engine.metrics()
+    assert m["applies"] >= 1 and m["changes"] >= 12 and m["max_batch"] >= 12
+    assert m["apply_seconds"] > 0 and m["state_records"] >= 12
+    ta2.process_multiple_changes(ta1.get_rows([((1, 3), None)]))  # known: skipped, nothing committed
+    assert ta2.engine.committed("tests3") == 12
+    ta1.insert_rows(4, 4)
+    ta2.process_multiple_changes(ta1.get_rows([((4, 4), (0, 1))]))  # partial: 2 buffered changes
+    assert ta2.engine.committed("tests3") == 14
