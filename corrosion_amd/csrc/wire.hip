@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,8 +41,17 @@
 namespace corro {
 namespace {
 
-constexpr uint32_t WIRE_LDS = 16384;      // frame bytes staged per workgroup
-constexpr uint32_t WIRE_OFFS = 1024;      // change offsets kept in LDS
+#ifndef CORRO_DIAG
+#define CORRO_DIAG 0
+#endif
+#if CORRO_DIAG & 512  // phase times of a few k_wire_decode workgroups (tools/diag_wire.py)
+#define WDIAG(i) const uint64_t t##i = wall_clock64();
+#else
+#define WDIAG(i)
+#endif
+
+constexpr uint32_t WIRE_LDS = 16384;      // at most this many frame bytes staged per workgroup
+constexpr uint32_t WIRE_OFFS = 1024;      // at most this many change offsets kept in LDS
 constexpr int32_t ST_NOT_CHANGESET = 1;   // a frame that is not a changeset message (skipped)
 
 __device__ inline uint64_t wmix(uint64_t x) {
@@ -79,6 +89,7 @@ struct WireDev {
     const uint8_t *interned;  // per table: 1 = rows keyed by interned pk bytes
     uint64_t *pkref;          // per change: 0, or (buffer offset << 32 | length) of an interned pk
     unsigned long long *nref, *nlong;  // interned pk references, long values
+    uint32_t lds_len, off_cap;         // k_wire_decode's dynamic LDS: frame bytes, change offsets
 };
 
 // little-endian / big-endian readers over any byte pointer, bounds-checked against end
@@ -205,15 +216,47 @@ __device__ inline bool name_eq(const uint8_t *a, uint32_t alen, const uint8_t *b
     return true;
 }
 
+// The walk over a frame's variable-length changes, done by the whole wave with wave-uniform
+// (scalar) state: lane i of the window holds the little-endian u32 at base + i, so each length
+// prefix is ONE readlane and a change costs one window load (4 LDS byte reads per lane, VALU) plus
+// ~40 scalar instructions. The scalar unit is shared by every wave of a CU, and a byte-at-a-time
+// walk (~300 scalar instructions per change) saturated it: 90 us per 128-change frame.
+struct WaveWin {
+    const uint8_t *p;
+    uint32_t len, base, word;
+    bool padded;  // p has >= 68 readable bytes past len (the LDS copy): no per-byte bounds checks
+    __device__ inline void load(uint32_t at) {
+        base = at;
+        const uint32_t i = at + threadIdx.x;
+        uint32_t v = 0;
+        if (padded) {
+            v = (uint32_t)p[i] | (uint32_t)p[i + 1] << 8 | (uint32_t)p[i + 2] << 16 | (uint32_t)p[i + 3] << 24;
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++) v |= (i + b < len ? (uint32_t)p[i + b] : 0u) << (8 * b);
+        }
+        word = v;
+    }
+    // the u32 at `at`; the caller has checked at + 4 <= len
+    __device__ inline uint32_t u32(uint32_t at) {
+        if (at - base > 63u) load(at);
+        return (uint32_t)__builtin_amdgcn_readlane((int)word, (int)(at - base));
+    }
+};
+
 __global__ void __launch_bounds__(64) k_wire_decode(WireDev d) {
-    __shared__ uint8_t s_buf[WIRE_LDS];
-    __shared__ uint32_t s_off[WIRE_OFFS];
+    // dynamic LDS: change offsets (off_cap words), then the staged frame (lds_len bytes)
+    extern __shared__ uint32_t s_dyn[];
+    __shared__ uint64_t s_tail;
     __shared__ int32_t s_bad;
+    uint32_t *s_off = s_dyn;
+    uint8_t *s_buf = reinterpret_cast<uint8_t *>(s_dyn + d.off_cap);
     const uint32_t f = blockIdx.x;
     if (d.status[f] || d.cs_kind[f] != 1) return;   // uniform per workgroup
+    WDIAG(0)
     const uint32_t len = d.flen[f], n = d.nchg[f];
     const uint8_t *g = d.buf + d.foff[f];
-    const bool lds = len <= WIRE_LDS;
+    const bool lds = len <= d.lds_len;
     if (lds) {
         // coalesced staging: 8-byte words where aligned, bytes at the ragged ends
         const uintptr_t base = reinterpret_cast<uintptr_t>(g);
@@ -228,43 +271,165 @@ __global__ void __launch_bounds__(64) k_wire_decode(WireDev d) {
         for (uint32_t i = head + 8 * nw + threadIdx.x; i < len; i += 64) s_buf[i] = g[i];
     }
     __syncthreads();
-    const uint8_t *p = lds ? s_buf : g;
-    const bool off_lds = n <= WIRE_OFFS;
+    WDIAG(1)
+    // the rest runs on a pointer of known address space (LDS or global): through a generic pointer
+    // every byte read is a flat load, several hundred cycles each on the walk's dependent chain
+    auto body = [&](const uint8_t *p, const bool padded) __attribute__((always_inline)) {
+    const bool off_lds = n <= d.off_cap;
     const uint64_t co = d.chg_off[f];
-    if (threadIdx.x == 0) {
-        // the walk: offsets of the variable-length changes, then the Full tail
-        Rd r{p, d.chg_start[f], len, false};
-        for (uint32_t k = 0; k < n && !r.bad; k++) {
-            if (off_lds) s_off[k] = r.pos;
-            else d.chg_rel[co + k] = r.pos;
-            for (int s = 0; s < 2; s++) {        // table, pk
-                const uint32_t l = r.u32();
-                if (r.need(l)) r.pos += l;
+    bool walk_bad;
+    uint64_t ts3;
+    if (padded) {
+        // LDS copy: lane 0 walks in vector registers (the four SIMDs' VALUs instead of the CU's
+        // one scalar unit, which the wave-uniform walk saturates at ~15 waves per CU). Lengths are
+        // clamped to len so positions cannot wrap and one check per change is exact: a position
+        // only grows, so a read past the end makes the change's end pass len too. Reads are
+        // clamped into the staged bytes (+80 padding).
+        if (threadIdx.x == 0) {
+            auto rd32 = [&](uint32_t a) -> uint32_t {
+                a = a < len ? a : len;
+                return (uint32_t)p[a] | (uint32_t)p[a + 1] << 8 | (uint32_t)p[a + 2] << 16 | (uint32_t)p[a + 3] << 24;
+            };
+            auto rd8 = [&](uint32_t a) -> uint32_t { return p[a < len ? a : len]; };
+            // speculation: a change's table / pk / cid lengths are predicted to equal the previous
+            // change's, so the four dependent reads (lt -> lp -> lc -> tag) are issued together and
+            // a change costs one LDS round trip when the predictions hold (one table per changeset,
+            // fixed-width pks and equal-length column names are the common case); a miss re-reads
+            // from the first wrong field on, sequentially.
+            uint32_t pos = d.chg_start[f];
+            bool bad = false;
+            uint32_t plt = 0, plp = 0, plc = 0;
+            for (uint32_t k = 0; k < n; k++) {
+                if (off_lds) s_off[k] = pos;
+                else d.chg_rel[co + k] = pos;
+                const uint32_t q1 = pos + 4 + plt, q2 = q1 + 4 + plp, q3 = q2 + 4 + plc;
+                const uint32_t lt = rd32(pos), s1 = rd32(q1), s2 = rd32(q2), st = rd8(q3), sv = rd32(q3 + 1);
+                uint32_t a = pos + 4 + min(lt, len);
+                uint32_t lp, lc, tag, vl;
+                if (lt == plt) {
+                    lp = s1;
+                } else {
+                    lp = rd32(a);
+                }
+                const bool hit1 = lt == plt;
+                a += 4 + min(lp, len);
+                if (hit1 && lp == plp) {
+                    lc = s2;
+                } else {
+                    lc = rd32(a);
+                }
+                const bool hit2 = hit1 && lp == plp;
+                a += 4 + min(lc, len);
+                if (hit2 && lc == plc) {
+                    tag = st;
+                    vl = sv;
+                } else {
+                    tag = rd8(a);
+                    vl = rd32(a + 1);
+                }
+                plt = min(lt, len);
+                plp = min(lp, len);
+                plc = min(lc, len);
+                a += 1;
+                if (tag == 1 || tag == 2) a += 8;
+                else if (tag == 3 || tag == 4) a += 4 + min(vl, len);
+                else if (tag != 0) bad = true;
+                a += 48;                             // col_version, db_version, seq, site_id, cl
+                if (bad || a > len) {
+                    bad = true;
+                    break;
+                }
+                pos = a;
             }
-            const uint32_t lc = r.u32();         // cid
-            if (r.need(lc)) r.pos += lc;
-            const uint32_t tag = (uint32_t)r.le(1);
-            if (tag == 1 || tag == 2) r.pos += 8;
-            else if (tag == 3 || tag == 4) {
-                const uint32_t l = r.u32();
-                if (r.need(l)) r.pos += l;
-            } else if (tag != 0) r.bad = true;
-            r.need(48);                          // col_version, db_version, seq, site_id, cl
-            r.pos += 48;
+            if (!bad && len - pos < 32) bad = true;
+            uint64_t tl[4] = {0, 0, 0, 0};
+            if (!bad)
+                for (int i = 0; i < 4; i++) tl[i] = (uint64_t)rd32(pos + 8 * i) | (uint64_t)rd32(pos + 8 * i + 4) << 32;
+            d.s0[f] = tl[0];
+            d.s1[f] = tl[1];
+            d.last[f] = tl[2];
+            d.ts[f] = tl[3];
+            s_tail = tl[3];
+            s_bad = bad ? 1 : 0;
+            if (!off_lds) __threadfence_block();
         }
-        d.s0[f] = r.u64();
-        d.s1[f] = r.u64();
-        d.last[f] = r.u64();
-        d.ts[f] = r.u64();
-        s_bad = r.bad ? 1 : 0;
-        if (!off_lds) __threadfence_block();
+        __syncthreads();
+        walk_bad = s_bad != 0;
+        ts3 = s_tail;
+    } else {
+        // the walk: offsets of the variable-length changes, then the Full tail (wave-uniform). Lane
+        // k % 64 keeps change k's offset; every 64 changes the wave stores them at once.
+        WaveWin w{p, len, 0, 0, padded};
+        uint32_t pos = d.chg_start[f];
+        w.load(pos);
+        bool bad = false;
+        uint32_t myoff = 0;
+        uint32_t k = 0;
+        const uint32_t lane = threadIdx.x;
+        for (; k < n; k++) {
+            if (lane == (k & 63)) myoff = pos;
+            if ((k & 63) == 63) {
+                if (off_lds) s_off[k - 63 + lane] = myoff;
+                else d.chg_rel[co + k - 63 + lane] = myoff;
+            }
+            // table, pk, cid: u32 length + bytes each (a length must leave room for what follows)
+            uint32_t a = pos;
+    #pragma unroll
+            for (int fld = 0; fld < 3; fld++) {
+                if (a > len - 4 || len < 4) { bad = true; break; }
+                const uint32_t l = w.u32(a);
+                if (l > len - (a + 4)) { bad = true; break; }
+                a += 4 + l;
+            }
+            if (bad) break;
+            if (a > len - 4 || len < 4) { bad = true; break; }  // the tag is followed by >= 48 bytes
+            const uint32_t tw = w.u32(a), tag = tw & 0xFF;
+            a += 1;
+            if (tag == 1 || tag == 2) {
+                a += 8;
+            } else if (tag == 3 || tag == 4) {
+                if (a > len - 4) { bad = true; break; }
+                const uint32_t l = w.u32(a);
+                if (l > len - (a + 4)) { bad = true; break; }
+                a += 4 + l;
+            } else if (tag != 0) {
+                bad = true;
+                break;
+            }
+            if (a > len || len - a < 48) { bad = true; break; }  // col_version, db_version, seq, site_id, cl
+            pos = a + 48;
+        }
+        if (!bad && (n & 63)) {  // the last partial group of offsets
+            const uint32_t g0 = n & ~63u;
+            if (lane < (n & 63)) {
+                if (off_lds) s_off[g0 + lane] = myoff;
+                else d.chg_rel[co + g0 + lane] = myoff;
+            }
+        }
+        uint64_t tl[4] = {0, 0, 0, 0};
+        if (!bad && len - pos >= 32) {
+    #pragma unroll
+            for (int i = 0; i < 4; i++) tl[i] = (uint64_t)w.u32(pos + 8 * i) | (uint64_t)w.u32(pos + 8 * i + 4) << 32;
+        } else {
+            bad = true;
+        }
+        ts3 = tl[3];
+        if (threadIdx.x == 0) {
+            d.s0[f] = tl[0];
+            d.s1[f] = tl[1];
+            d.last[f] = tl[2];
+            d.ts[f] = tl[3];
+            if (!off_lds) __threadfence_block();
+        }
+        walk_bad = bad;
     }
+    WDIAG(2)
     __syncthreads();
-    if (s_bad) {
+    if (walk_bad) {
         if (threadIdx.x == 0) d.status[f] = CORRO_E_INVALID;
         return;
     }
-    const uint64_t ts = d.ts[f];
+    const uint64_t ts = ts3;
     int32_t err = 0;
     for (uint32_t k = threadIdx.x; k < n; k += 64) {
         Rd r{p, off_lds ? s_off[k] : d.chg_rel[co + k], len, false};
@@ -367,6 +532,15 @@ __global__ void __launch_bounds__(64) k_wire_decode(WireDev d) {
         if (o.ts) const_cast<uint64_t *>(o.ts)[q] = ts;
     }
     if (err) atomicMin(&d.status[f], err);
+#if CORRO_DIAG & 512
+    const uint64_t t3 = wall_clock64();
+    if (threadIdx.x == 0 && (f % 997) == 0)
+        printf("WDIAG f=%u len=%u n=%u stage=%lu walk=%lu decode=%lu (x10ns) t0=%lu\n", f, len, n,
+               (unsigned long)(t1 - t0), (unsigned long)(t2 - t1), (unsigned long)(t3 - t2), (unsigned long)t0);
+#endif
+    };
+    if (lds) body(s_buf, true);
+    else body(g, false);
 }
 
 size_t al(size_t b) { return ((b + 255) / 256) * 256; }
@@ -619,7 +793,20 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
         // (device time = header kernel + these two: the host round trip between them is not kernel time)
         if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[2], s));
         hipLaunchKernelGGL(k_wire_sets, dim3((F + 255) / 256), dim3(256), 0, s, d);
-        hipLaunchKernelGGL(k_wire_decode, dim3(F), dim3(64), 0, s, d);
+        {
+            // LDS sized by this call's Full frames (occupancy is LDS-bound: ~10 KB frames fit 15
+            // workgroups per CU where a fixed 20 KB fits 8); longer frames are read from HBM
+            uint32_t ml = 0, mn = 0;
+            for (uint32_t f = 0; f < F; f++)
+                if (!st[f] && kind[f] == 1) {
+                    if (flen[f] <= WIRE_LDS) ml = std::max(ml, flen[f]);
+                    mn = std::max(mn, std::min(nchg[f], WIRE_OFFS));
+                }
+            d.lds_len = (ml + 15) & ~15u;
+            d.off_cap = (mn + 3) & ~3u;
+        }
+        // (+ 80 bytes: the walk's window reads run up to 67 bytes past a frame)
+        hipLaunchKernelGGL(k_wire_decode, dim3(F), dim3(64), (size_t)d.off_cap * 4 + d.lds_len + 80, s, d);
         if (ctx->profiling) CORRO_HIP_TRY(hipEventRecord(ctx->ev[3], s));
         CORRO_HIP_TRY(hipGetLastError());
         CORRO_HIP_TRY(hipMemcpyAsync(cnt3, d.nunknown, 24, hipMemcpyDeviceToHost, s));
