@@ -241,3 +241,34 @@ def test_process_frames_interned_pks_and_long_values():
     assert cx == cy
     assert any(isinstance(row[4], bytes) for row in cx)          # long values present
     assert any(isinstance(row[1], bytes) for row in cx)          # interned pks present
+
+
+def test_decode_corrupt_length_prefixes():
+    """A length prefix past the frame end (table, pk, cid or value length, each set to 2^32 - 16)
+    marks only that frame malformed; the speculative walk's predictions never hide it, and a
+    neighbouring good frame decodes unchanged."""
+    import corrosion_amd as ca
+    import struct
+    rng = np.random.default_rng(21)
+    ch = [Change("users", 5 + k, "name", "abcdefgh", 1, 1, k, ACT[0], 1) for k in range(6)]
+    good = wire.encode_sync_changeset(ChangeV1(ACT[0], Full(1, ch, (0, 5), 5, ts=3)))
+    # change 3's fields: payload offset 40 is change 0; every change here has the same size
+    size = (len(good) - 40 - 32) // 6
+    base = 40 + 3 * size
+    lt = struct.unpack_from("<I", good, base)[0]
+    lp = struct.unpack_from("<I", good, base + 4 + lt)[0]
+    lc = struct.unpack_from("<I", good, base + 8 + lt + lp)[0]
+    offs = [base, base + 4 + lt, base + 8 + lt + lp, base + 12 + lt + lp + lc + 1]  # table, pk, cid, value
+    bad = []
+    for o in offs:
+        b = bytearray(good)
+        struct.pack_into("<I", b, o, 0xFFFFFFF0)
+        bad.append(bytes(b))
+    mixed = wire.encode_sync_changeset(ChangeV1(ACT[1], Full(2, rand_changes(rng, 40, ACT[1], 2), (0, 39), 39, ts=4)))
+    buf = b"".join(wire.frame(x) for x in bad + [good, mixed])
+    eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12)
+    dec = eng.decode_frames(buf)
+    assert list(dec["status"]) == [-1, -1, -1, -1, 0, 0]
+    cs = dec["cs"][4]
+    for k, c in enumerate(ch):
+        assert got_fields(dec, cs.change_off + k) == expected_fields(eng, c, 3)
