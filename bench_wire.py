@@ -6,7 +6,8 @@ INTEGER columns, 1000 actors, INTEGER values, positive pks below 2^22), encoded 
 corrosion_amd/wire.py (speedy layout). One step = one decode call: the device kernels (header
 scan + per-frame walk/decode) are timed with HIP events; the call time includes the H2D copy of
 the frame bytes and the D2H copy of the decoded batch. Algorithmic bytes: the frame bytes read +
-48 B per decoded change written (SURVEY §8(d) SoA). Prints one JSON line.
+48 B per decoded change written (SURVEY §8(d) SoA). `roofline.traffic` is the HBM bytes per decode
+from two rocprofv3 PMC passes over a child run (--no-pmc skips them). Prints one JSON line.
 """
 import argparse
 import json
@@ -25,7 +26,22 @@ def main():
     ap.add_argument("--per-frame", type=int, default=128)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    PMC_RUNS = 3
+    traffic = None
+    if not args.pmc_child and not args.no_pmc:
+        # HBM bytes per decode from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over a child run of this
+        # script doing PMC_RUNS decodes, before this process touches the GPU (bench.py's recipe)
+        from bench import pmc_traffic_live
+        child = [os.path.abspath(__file__), "--pmc-child", "--changes", str(args.changes), "--per-frame",
+                 str(args.per_frame)]
+        tb, note, per = pmc_traffic_live(0, applies=PMC_RUNS, child_cmd=child)
+        if per:  # the decode kernels only
+            per = {k: v for k, v in per.items() if "k_wire" in k}
+            tb = sum(v["fetch"] + v["write"] for v in per.values())
+        traffic = {"bytes": tb, "source": note, "by_kernel": per}
     import numpy as np
     import corrosion_amd as ca
     import synth
@@ -50,6 +66,10 @@ def main():
     enc_s = time.perf_counter() - t0
     eng = ca.MergeEngine({"t": cols}, capacity_hint=args.changes)
     eng.register_sites(sites)
+    if args.pmc_child:  # exactly PMC_RUNS decodes, nothing else on the GPU
+        for _ in range(PMC_RUNS):
+            eng.decode_frames(buf)
+        return
     eng.set_profiling(True)
     for _ in range(args.warmup):
         dec = eng.decode_frames(buf)
@@ -77,7 +97,9 @@ def main():
             "host_encode_s": enc_s,
             "roofline": {"bound": "hbm", "kernel": "k_wire_hdr + k_wire_decode", "achieved": alg / (kt * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "traffic": None}}
+                         "traffic": traffic["bytes"] if traffic else None,
+                         "traffic_ratio": (traffic["bytes"] / alg) if traffic and traffic["bytes"] else None,
+                         "traffic_by_kernel": traffic["by_kernel"] if traffic else None, "alg_bytes": alg}}
     print(json.dumps(line), flush=True)
 
 
