@@ -251,6 +251,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
     achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
     steady = steady_state(eng, prep, n, dev, dt / args.steps * 1e3, cells)
     agent = agent_path(eng, batch, n)
+    e2e_agent = agent_e2e(eng, batch, n, agent["ms"])
     e2e = host_batch_e2e(eng, batch, n)
     cpu = None if args.no_cpu_baseline else cpu_baseline(batch)
     line = {
@@ -280,6 +281,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
         "cpu_baseline": cpu,
         "steady_state": steady,
         "agent_path": agent,
+        "agent_e2e": e2e_agent,
         "end_to_end_h2d": e2e,
     }
     print(json.dumps(line), flush=True)
@@ -352,6 +354,88 @@ def agent_path(eng, batch, n, reps=3):
     del prep
     return {"ms": med, "changes_per_s": n / (med * 1e-3), "merge_ms": stages.get("k_merge"),
             "note": f"config-2 batch with impact flags (the agent path), reset + apply, median of {reps}"}
+
+
+def agent_e2e(eng, batch, n, agent_ms=None, reps=3):
+    """The drop-in entry point end to end: config 2 as ChangeV1-shaped input -- 1000 actors x ~1049
+    versions x 64 changes, changesets arriving interleaved across actors (round-robin by version) and
+    the change batch laid out in that arrival order (as a decoder emits it), every change carrying its
+    changeset's NTP64 ts -- through corro_process_multiple_changes with the
+    batch left in HBM (CORRO_MEM_DEVICE): header dedup passes and gap bookkeeping on the host (actors in
+    parallel), the unknown-name screen, the regroup into ActorId order (gather kernel), the merge with
+    impact flags, and the impactful flags / Current-Cleared outcomes on the device. Each rep resets the
+    state and starts a fresh Bookie (util.rs:691-1037 on an empty node); median of `reps`."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import synth
+    import corrosion_amd as ca
+    from corrosion_amd import _lib as L
+    per_actor = -(-n // N_ACTORS)
+    ids = np.ascontiguousarray(synth.site_ids(N_ACTORS, 1), dtype=np.uint8)   # ordinal a = actor a
+    cs_dt = np.dtype([("actor_id", "<u8"), ("site", "<u4"), ("kind", "<u4"), ("version_start", "<u8"),
+                      ("version_end", "<u8"), ("seq_start", "<u8"), ("seq_end", "<u8"), ("last_seq", "<u8"),
+                      ("ts", "<u8"), ("change_off", "<u8"), ("change_count", "<u8")])
+    assert cs_dt.itemsize == C.sizeof(L.Changeset)
+    a_idx, v_idx = [], []
+    for a in range(N_ACTORS):
+        lo, hi = a * per_actor, min(n, (a + 1) * per_actor)
+        nv = max(0, -(-(hi - lo) // 64))
+        a_idx.append(np.full(nv, a, np.int64))
+        v_idx.append(np.arange(nv, dtype=np.int64))
+    a_idx, v_idx = np.concatenate(a_idx), np.concatenate(v_idx)
+    order = np.lexsort((a_idx, v_idx))                 # arrival: version-major, actors interleaved
+    a_idx, v_idx = a_idx[order], v_idx[order]
+    off = a_idx * per_actor + v_idx * 64
+    cnt = np.minimum(64, np.minimum(n, (a_idx + 1) * per_actor) - off)
+    # the batch laid out in arrival order (as a decoder emits it): changeset j at arr[j]
+    arr = np.cumsum(cnt) - cnt
+    dev = batch["pk"].device
+    idx = (torch.repeat_interleave(torch.from_numpy(off - arr).to(dev), torch.from_numpy(cnt).to(dev))
+           + torch.arange(n, device=dev))
+    cs = np.zeros(len(off), cs_dt)
+    cs["actor_id"] = ids.ctypes.data + 16 * a_idx
+    cs["site"] = a_idx
+    cs["kind"] = L.CORRO_CS_FULL
+    cs["version_start"] = cs["version_end"] = v_idx + 1
+    cs["seq_end"] = cs["last_seq"] = cnt - 1
+    cs["ts"] = ((v_idx + 1) << 32) | a_idx             # NTP64-shaped, per changeset
+    cs["change_off"], cs["change_count"] = arr, cnt
+    full = {k: v[idx].contiguous() for k, v in batch.items()}
+    full["ts"] = ((full["db_version"] << 32) | full["site"].to(torch.int64)).contiguous()
+    del idx
+    s = L.Changes()
+    s.n = n
+    for k in ("pk", "table_cid", "col_version", "db_version", "cl", "seq", "site", "val0", "ts"):
+        setattr(s, k, full[k].data_ptr())
+    known = np.zeros(len(cs), np.int32)
+    imp = torch.zeros(n, dtype=torch.uint8, device=batch["pk"].device)
+    out = L.ProcessOut()
+    out.known, out.impactful = known.ctypes.data, imp.data_ptr()
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(reps):
+        bk = ca.agent.Bookie()
+        eng.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        L.check(L.lib().corro_process_multiple_changes(eng._h, bk._h, cs.ctypes.data, len(cs), C.byref(s),
+                                                       L.CORRO_MEM_DEVICE, C.byref(out)))
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) * 1e3)
+        del bk
+    ms.sort()
+    med = ms[len(ms) // 2]
+    ok = bool((known == 1).all())          # every version Current (empty state: each one impactful)
+    nimp = int(imp.sum().item())
+    del full, imp
+    return {"ms": med, "changes_per_s": n / (med * 1e-3), "changesets": int(len(cs)),
+            "ratio_vs_agent_path": (med / agent_ms) if agent_ms else None, "all_current": ok,
+            "impactful_changes": nimp,
+            "note": "corro_process_multiple_changes (CORRO_MEM_DEVICE) on config 2 as 1000 actors x ~1049 "
+                    "versions x 64 changes arriving interleaved (batch in arrival order), reset + fresh Bookie + "
+                    "call, median of "
+                    f"{reps}"}
 
 
 def run_multi(args, world, rank):

@@ -37,7 +37,8 @@ EXPORTS = [
     "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
     "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity",
-    "corro_ctx_metrics", "corro_table_committed",
+    "corro_ctx_metrics", "corro_table_committed", "corro_ctx_track_touched", "corro_state_export_touched",
+    "corro_ctx_set_store_limit",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -182,6 +183,9 @@ def lib():
         "corro_apply_batch": (i32, [vp, C.POINTER(Changes), i32, C.POINTER(ApplyOut)]),
         "corro_state_count": (i32, [vp, vp]),
         "corro_state_export": (i32, [vp, C.POINTER(Rows), u64, vp]),
+        "corro_state_export_touched": (i32, [vp, C.POINTER(Rows), u64, vp]),
+        "corro_ctx_track_touched": (i32, [vp, i32]),
+        "corro_ctx_set_store_limit": (i32, [vp, u64]),
         "corro_state_reset": (i32, [vp]),
         "corro_db_versions": (i32, [vp, vp, u32]),
         "corro_compute_needs": (i32, [vp, C.POINTER(SyncEntries), i32, C.POINTER(NeedsOut), i32]),
@@ -212,7 +216,7 @@ def lib():
         "corro_last_timings": (i32, [vp, vp, u32, vp]),
         "corro_bookie_new": (i32, [vp]),
         "corro_bookie_free": (None, [vp]),
-        "corro_process_multiple_changes": (i32, [vp, vp, vp, u64, C.POINTER(Changes), C.POINTER(ProcessOut)]),
+        "corro_process_multiple_changes": (i32, [vp, vp, vp, u64, C.POINTER(Changes), i32, C.POINTER(ProcessOut)]),
         "corro_bookie_take_ready": (i32, [vp, vp, vp, u64, vp]),
         "corro_process_fully_buffered": (i32, [vp, vp, vp, u64, vp]),
         "corro_bookie_last": (i32, [vp, vp, vp]),

@@ -255,7 +255,7 @@ class Agent:
         out.known = known.ctypes.data
         out.impactful = imp.ctypes.data
         L.check(L.lib().corro_process_multiple_changes(self.engine._h, self.bookie._h, descs, ncs, C.byref(s),
-                                                       C.byref(out)))
+                                                       L.CORRO_MEM_HOST, C.byref(out)))
         res = Processed(known=[L.KNOWN.get(int(k), int(k)) for k in known[:ncs]])
         for i, cv1 in enumerate(changes):
             cs = cv1.changeset
@@ -268,11 +268,14 @@ class Agent:
         return res
 
     def process_frames(self, buf, payload=0):
-        """Wire bytes -> merge: decode length-delimited changeset frames on the GPU
-        (corro_decode_frames) and feed the decoded batch to process_multiple_changes as it is.
+        """Wire bytes -> merge without leaving the GPU: decode length-delimited changeset frames
+        on the device (corro_decode_frames, CORRO_MEM_DEVICE) and hand the decoded batch to
+        process_multiple_changes where it lies (CORRO_MEM_DEVICE: no change crosses PCIe again).
         Frames with a non-zero decode status are not applied. Returns (Processed over the applied
-        frames, per-frame decode status)."""
-        dec = self.engine.decode_frames(buf, payload)
+        frames, with .impact = per-change impactful flags as a CUDA uint8 tensor, per-frame decode
+        status)."""
+        import torch
+        dec = self.engine.decode_frames(buf, payload, device=True)
         keep = [i for i in range(dec["nframes"]) if dec["status"][i] == 0]
         descs = (L.Changeset * max(1, len(keep)))()
         for j, i in enumerate(keep):
@@ -281,21 +284,22 @@ class Agent:
                 descs[j].change_off = descs[j].change_count = 0
         self.site_ids = dict(enumerate(self.engine.site_ids()))   # the decoder may have registered sites
         ch = dec["changes"]
-        n = len(ch["pk"])
+        n = int(ch["pk"].shape[0])
         s = L.Changes()
         s.n = n
         for k, a in ch.items():
             if k == "val_data":
-                s.val_data, s.val_data_len = a.ctypes.data, a.size
+                s.val_data, s.val_data_len = a.data_ptr(), int(a.numel())
             else:
-                setattr(s, k, a.ctypes.data if n else None)
+                setattr(s, k, a.data_ptr() if n else None)
         known = np.zeros(max(1, len(keep)), np.int32)
-        imp = np.zeros(max(1, n), np.uint8)
+        imp = torch.zeros(max(1, n), dtype=torch.uint8, device="cuda")
         out = L.ProcessOut()
         out.known = known.ctypes.data
-        out.impactful = imp.ctypes.data
+        out.impactful = imp.data_ptr()
+        torch.cuda.current_stream().synchronize()
         L.check(L.lib().corro_process_multiple_changes(self.engine._h, self.bookie._h, descs, len(keep), C.byref(s),
-                                                       C.byref(out)))
+                                                       L.CORRO_MEM_DEVICE, C.byref(out)))
         res = Processed(known=[L.KNOWN.get(int(k), int(k)) for k in known[:len(keep)]])
         res.impact = imp[:n]
         res.ready = self.take_ready()

@@ -88,9 +88,14 @@ __global__ void __launch_bounds__(256) k_affinity(BatchDev in, const uint8_t *__
             const uint32_t ln = in.vl ? in.vl[i] : 0u;
             TextView tv{in.v0[i], in.v1 ? in.v1[i] : 0ULL, nullptr, ln};
             if (ln == VLEN_LONG) {
-                if (!in.voff || !in.vsz || !in.arena) continue;  // malformed: k_validate reports it
-                tv.p = in.arena + in.lbase + in.voff[i];
-                tv.len = in.vsz[i];
+                // a malformed span is skipped here (k_validate / k_scatter report it): the same
+                // bounds long_value() checks before any byte is read
+                if (!in.voff || !in.vsz || !in.arena) continue;
+                const uint64_t off = in.voff[i];
+                const uint32_t sz = in.vsz[i];
+                if (sz <= 16 || sz >= (1u << 24) || off > in.ldata || sz > in.ldata - off) continue;
+                tv.p = in.arena + in.lbase + off;
+                tv.len = sz;
             }
             bad |= numeric_literal(tv);
         }

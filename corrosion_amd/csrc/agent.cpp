@@ -12,14 +12,20 @@
 // and generate_sync (corro-types/src/sync.rs:284-333). The merge itself is corro_apply_batch.
 #include <array>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <optional>
 #include <set>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
+#include "agent_dev.h"
 #include "booked.h"
 #include "corro_hip.h"
 
@@ -30,6 +36,12 @@ namespace corro {
 int fail(int code, const std::string &msg);
 int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version);
 }  // namespace corro
+
+#define TRY_RC(x)                        \
+    do {                                 \
+        int rc_ = (x);                   \
+        if (rc_ != CORRO_OK) return rc_; \
+    } while (0)
 
 using corro::fail;
 using corro::Range;
@@ -145,9 +157,11 @@ struct Staged {
     }
 };
 
-int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset &cs, const corro_changes *in,
+// row(k) = HostRow of the changeset's k-th change
+template <class RowFn>
+int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset &cs, RowFn row,
                        corro::PartialVersion &out) {
-    for (uint64_t k = 0; k < cs.change_count; k++) st.buffered.push_back(row_at(in, cs.change_off + k, cs.ts));
+    for (uint64_t k = 0; k < cs.change_count; k++) st.buffered.push_back(row(k));
     SeqBook &sb = st.seq(bk, cs.site, cs.version_start);
     const uint64_t s = cs.seq_start, e = cs.seq_end;
     RangeSet merged;
@@ -183,6 +197,31 @@ void clear_buffered(corro_bookie *bk, uint32_t site, uint64_t vs, uint64_t ve) {
     }
 }
 
+// f(0) .. f(n - 1) on up to CORRO_HOST_THREADS (default: min(16, hardware)) host threads, at least
+// `per` indices per thread (serial for small n). f must only touch state of its own index.
+template <class F>
+void run_parallel(size_t n, F &&f, size_t per = 8) {
+    static const unsigned cap = [] {
+        const char *e = std::getenv("CORRO_HOST_THREADS");
+        const long v = e ? std::atol(e) : 0;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        return v > 0 ? (unsigned)std::min<long>(v, 256) : std::min(16u, hw);
+    }();
+    const unsigned nth = (unsigned)std::min<size_t>(cap, n / std::max<size_t>(per, 1));
+    if (nth <= 1) {
+        for (size_t k = 0; k < n; k++) f(k);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    auto body = [&] {
+        for (size_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(k);
+    };
+    std::vector<std::thread> ts;
+    for (unsigned t = 1; t < nth; t++) ts.emplace_back(body);
+    body();
+    for (auto &t : ts) t.join();
+}
+
 }  // namespace
 
 extern "C" {
@@ -195,19 +234,68 @@ int corro_bookie_new(corro_bookie **out) {
 
 void corro_bookie_free(corro_bookie *b) { delete b; }
 
+}  // extern "C"
+
+namespace {
+
+// RangeInclusiveMap<Version, Option<PartialVersion>> of the versions one actor has seen in this
+// call (util.rs:762-807): covered versions plus, per version whose latest entry is a partial, that
+// PartialVersion (a later entry over the version replaces it).
+struct SeenMap {
+    RangeSet covered;
+    std::map<uint64_t, corro::PartialVersion> partial_at;
+    void insert(const Range &v, const std::optional<corro::PartialVersion> &p) {
+        covered.insert(v.first, v.second);
+        if (!partial_at.empty()) partial_at.erase(partial_at.lower_bound(v.first), partial_at.upper_bound(v.second));
+        if (p) partial_at[v.first] = *p;
+    }
+    // every version of v seen, and (with seqs) each seen partial holding the seqs
+    bool all_seen(const Range &v, const Range *seqs) const {
+        if (!covered.contains_range(v.first, v.second)) return false;
+        if (!seqs || partial_at.empty()) return true;
+        for (auto it = partial_at.lower_bound(v.first); it != partial_at.end() && it->first <= v.second; ++it)
+            if (!it->second.seqs.contains_range(seqs->first, seqs->second)) return false;
+        return true;
+    }
+};
+
+// One actor's share of a process_multiple_changes call. Actors are independent (util.rs:765-884
+// handles them one at a time under their own booked write lock), so their header passes run in
+// parallel on the host.
+struct ActorWork {
+    ActorId id{};
+    uint32_t site = 0;
+    corro::Booked *booked = nullptr;
+    bool had_max = false;
+    uint64_t max = 0;
+    bool fast = false;                // every changeset a complete Full version, ascending (arrival order)
+    const uint64_t *idx = nullptr;    // (not fast) changesets in arrival order
+    uint64_t nidx = 0;
+    // results (not fast: the per-actor passes; fast ones are counted per chunk)
+    uint64_t nspans = 0, nchanges = 0;
+    bool ts = false;
+    std::vector<uint64_t> set_dbv;    // crsql_set_db_version(site, v)
+    Staged st;                        // buffered rows / seq bookkeeping of incomplete versions
+    std::vector<std::pair<uint64_t, corro::PartialVersion>> partials;
+    bool has_next = false;
+    corro::Booked next;               // the committed VersionsSnapshot
+    std::vector<uint64_t> ready;      // versions now fully buffered
+    int rc = CORRO_OK;
+    std::string err;
+};
+
+}  // namespace
+
+extern "C" {
+
 int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
-                                   const corro_changes *in, corro_process_out *out) {
+                                   const corro_changes *in, int mem, corro_process_out *out) {
     if (!ctx || !bk || (ncs && !cs) || !out) return fail(CORRO_E_INVALID, "NULL argument");
     if (ncs && (!out->known)) return fail(CORRO_E_INVALID, "out->known is required");
+    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
     const uint64_t nchanges = in ? in->n : 0;
-    for (uint64_t i = 0; i < ncs; i++) {
-        out->known[i] = CORRO_KNOWN_SKIPPED;
-        if (cs[i].kind == CORRO_CS_FULL && cs[i].change_count &&
-            (!in || cs[i].change_off + cs[i].change_count > nchanges))
-            return fail(CORRO_E_INVALID, "changeset change span outside the batch");
-    }
-    if (out->impactful)
-        for (uint64_t j = 0; j < nchanges; j++) out->impactful[j] = 0;
+    if (nchanges && !in->table_cid) return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    out->n_ready = 0;
 
     auto versions_of = [](const corro_changeset &c) -> Range {
         if (c.kind == CORRO_CS_EMPTY_SET) return {0, 0};  // Changeset::versions() dummy (broadcast.rs:176-178)
@@ -223,162 +311,403 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     };
     auto is_empty = [](const corro_changeset &c) { return c.kind != CORRO_CS_FULL || c.change_count == 0; };
 
-    // pass 1 (util.rs:704-739): batch-local dedup, then drop already-known versions
-    std::set<std::tuple<ActorId, uint64_t, uint64_t, int, uint64_t, uint64_t>> seen;
-    std::map<ActorId, std::vector<uint64_t>> unknown;  // BTreeMap<ActorId, _>: byte order
-    for (uint64_t i = 0; i < ncs; i++) {
-        const ActorId a = actor_of(cs[i].actor_id);
-        const Range v = versions_of(cs[i]);
-        Range sq;
-        const Range *seqs = seqs_of(cs[i], sq);
-        if (!seen.emplace(a, v.first, v.second, seqs ? 1 : 0, seqs ? sq.first : 0, seqs ? sq.second : 0).second)
-            continue;
-        corro::Booked &booked = bk->actors[a];  // Bookie::ensure
-        bk->site_of[a] = cs[i].site;
-        if (booked.contains_all(v.first, v.second, seqs)) continue;
-        unknown[a].push_back(i);
-    }
+    // CORRO_AGENT_PROFILE=1: host-side stage times of each call on stderr (tools)
+    static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    std::string prof_line;
+    auto stage = [&](const char *name) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        prof_line += std::string(" ") + name + "=" +
+                     std::to_string(std::chrono::duration<double, std::milli>(t - t_last).count()).substr(0, 6);
+        t_last = t;
+    };
+    corro::AgentPinned P{};
+    TRY_RC(corro::agent_dev_begin(ctx, ncs, &P));
+    stage("begin");
 
-    // pass 2 (util.rs:765-884): per actor, in order
-    Staged st;
-    Batch batch;
-    std::vector<std::pair<uint64_t, uint64_t>> applied;  // (changeset, first batch row)
-    std::map<ActorId, std::vector<std::pair<Range, std::optional<corro::PartialVersion>>>> processed;
-    for (auto &[actor, idxs] : unknown) {
-        corro::Booked &booked = bk->actors[actor];
-        const bool had_max = booked.has_max;
-        const uint64_t max = booked.max;
-        std::vector<std::pair<Range, std::optional<corro::PartialVersion>>> seen_local;  // RangeInclusiveMap
-        auto seen_get = [&](uint64_t v) -> const std::optional<corro::PartialVersion> * {
-            for (auto it = seen_local.rbegin(); it != seen_local.rend(); ++it)
-                if (it->first.first <= v && v <= it->first.second) return &it->second;
-            return nullptr;
-        };
-        for (uint64_t i : idxs) {
+    // Host passes walk the headers in ARRIVAL order (sequential chunks in parallel threads): an actor's
+    // changesets are interleaved with everyone else's, so a walk in actor order would miss the cache
+    // on every header. Per-changeset results go to the pinned arrays; the regroup into ActorId order
+    // happens on the device (agent_dev_batch).
+    const uint32_t nsites = corro::agent_site_count(ctx);
+    std::vector<std::array<uint8_t, 16>> site_id(nsites);
+    for (uint32_t k = 0; k < nsites; k++) corro::agent_site_id(ctx, k, site_id[k].data());
+    const size_t nchunk = std::max<size_t>(1, std::min<size_t>(16, ncs / 4096));
+    auto chunk_of = [&](size_t k, uint64_t &lo, uint64_t &hi) {
+        lo = ncs * k / nchunk;
+        hi = ncs * (k + 1) / nchunk;
+    };
+    // per (chunk, site): changesets, first / last version, every one a complete Full ascending
+    struct SiteStat {
+        uint64_t count = 0, first = 0, last = 0;
+        bool ok = true;
+    };
+    std::vector<std::vector<SiteStat>> cstat(nchunk);
+    std::vector<int> cerr(nchunk, CORRO_OK);
+    std::vector<uint64_t> cfull(nchunk, 0);
+    // 1. headers: spans checked, staged for the device, actors checked against the registered ids
+    run_parallel(nchunk, [&](size_t k) {
+        uint64_t lo, hi;
+        chunk_of(k, lo, hi);
+        std::vector<SiteStat> &st = cstat[k];
+        st.assign(nsites, SiteStat{});
+        const uint8_t *last_ptr = nullptr;
+        uint32_t last_site = 0xFFFFFFFFu;
+        for (uint64_t i = lo; i < hi; i++) {
             const corro_changeset &c = cs[i];
-            const Range v = versions_of(c);
-            Range sq;
-            const Range *seqs = seqs_of(c, sq);
-            if (booked.contains_all(v.first, v.second, seqs)) continue;
-            bool all_seen = true;
-            for (uint64_t ver = v.first; ver <= v.second && all_seen; ver++) {
-                const auto *p = seen_get(ver);
-                if (!p) all_seen = false;
-                else if (seqs && p->has_value()) all_seen = (*p)->seqs.contains_range(seqs->first, seqs->second);
-                if (ver == UINT64_MAX) break;
+            out->known[i] = CORRO_KNOWN_SKIPPED;
+            const bool full = c.kind == CORRO_CS_FULL && c.change_count;
+            if (full && (!in || c.change_off > nchanges || c.change_count > nchanges - c.change_off)) {
+                cerr[k] = 1;
+                return;
             }
-            if (all_seen) continue;
-
-            std::optional<corro::PartialVersion> partial;
-            if (is_complete(c) && is_empty(c)) {
-                // process_empty_version only when end > booked max (util.rs:810-824)
-                if (!had_max || v.second > max) st.set_dbv.emplace_back(c.site, v.second);
-                out->known[i] = CORRO_KNOWN_CLEARED;
-            } else {
-                if (seqs && seqs->second < seqs->first) continue;  // invalid seqs (util.rs:826-831)
-                bool bad = false;
-                for (uint64_t k = 0; k < c.change_count; k++)
-                    if (in->table_cid[c.change_off + k] == CORRO_TCID_UNKNOWN) bad = true;
-                if (bad) {  // the INSERT fails, the version's SAVEPOINT rolls back (util.rs:839-860)
-                    out->known[i] = CORRO_E_UNKNOWN_COLUMN;
-                    continue;
+            if (c.site >= nsites || !c.actor_id) {
+                cerr[k] = 2;
+                return;
+            }
+            if (c.actor_id != last_ptr || c.site != last_site) {  // (a run of one actor checks once)
+                if (std::memcmp(site_id[c.site].data(), c.actor_id, 16) != 0) {
+                    cerr[k] = 3;
+                    return;
                 }
-                if (is_complete(c)) {
-                    applied.emplace_back(i, batch.size());
-                    for (uint64_t k = 0; k < c.change_count; k++) batch.push(row_at(in, c.change_off + k, c.ts));
-                    out->known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
+                last_ptr = c.actor_id;
+                last_site = c.site;
+            }
+            P.off[i] = full ? c.change_off : 0;
+            P.cnt[i] = full ? c.change_count : 0;
+            P.ts[i] = c.ts;
+            P.site[i] = c.site;
+            P.flag[i] = 0;
+            cfull[k] += full;
+            SiteStat &t = st[c.site];
+            const bool fast = c.kind == CORRO_CS_FULL && is_complete(c) && (!t.count || c.version_start > t.last);
+            if (!t.count) t.first = c.version_start;
+            t.last = c.version_start;
+            t.ok = t.ok && fast;
+            t.count++;
+        }
+    }, 1);
+    for (int e : cerr) {
+        if (e == 1) return fail(CORRO_E_INVALID, "changeset change span outside the batch");
+        if (e == 2) return fail(CORRO_E_INVALID, "changeset site ordinal is not registered (or actor_id is NULL)");
+        if (e == 3) return fail(CORRO_E_INVALID, "changeset site ordinal does not name its actor_id");
+    }
+    uint64_t nfull = 0;
+    for (uint64_t f : cfull) nfull += f;
+    // actors; the fast ones (every changeset a complete Full version, strictly ascending in arrival
+    // order) need no per-actor walk: no version repeats, so no batch-local dedup and nothing already
+    // seen in this call -- pass 1's contains_all is the only check left, made per changeset below
+    std::vector<ActorWork> work;
+    std::vector<int64_t> work_of(nsites, -1);
+    bool any_slow = false;
+    for (uint32_t t = 0; t < nsites; t++) {
+        uint64_t count = 0, last = 0;
+        bool ok = true;
+        for (size_t k = 0; k < nchunk; k++) {
+            const SiteStat &x = cstat[k][t];
+            if (!x.count) continue;
+            ok = ok && x.ok && (!count || x.first > last);
+            last = x.last;
+            count += x.count;
+        }
+        if (!count) continue;
+        work_of[t] = (int64_t)work.size();
+        work.emplace_back();
+        ActorWork &w = work.back();
+        w.site = t;
+        w.fast = ok;
+        w.nidx = count;
+        std::memcpy(w.id.data(), site_id[t].data(), 16);
+        any_slow |= !ok;
+    }
+    for (ActorWork &w : work) {  // Bookie::ensure (std::map nodes: stable pointers for the workers)
+        w.booked = &bk->actors[w.id];
+        bk->site_of[w.id] = w.site;
+        w.had_max = w.booked->has_max;
+        w.max = w.booked->max;
+    }
+    // the changesets of the other actors, grouped (stable counting sort by site)
+    std::vector<uint64_t> by_actor;
+    if (any_slow) {
+        std::vector<uint64_t> base(work.size() + 1, 0);
+        for (size_t k = 0; k < work.size(); k++) base[k + 1] = base[k] + (work[k].fast ? 0 : work[k].nidx);
+        by_actor.resize(base.back());
+        std::vector<uint64_t> cur(base.begin(), base.end() - 1);
+        for (uint64_t i = 0; i < ncs; i++) {
+            const ActorWork &w = work[(size_t)work_of[cs[i].site]];
+            if (!w.fast) by_actor[cur[(size_t)work_of[cs[i].site]]++] = i;
+        }
+        for (size_t k = 0; k < work.size(); k++) work[k].idx = by_actor.data() + base[k];
+    }
+    stage("headers");
+
+    // 2. the device view of the input and the per-changeset unknown-name screen (one kernel)
+    corro_changes dv{};
+    if (nfull) {
+        TRY_RC(corro::agent_dev_input(ctx, in, mem, &dv));
+        TRY_RC(corro::agent_dev_bad(ctx, &dv, P, ncs));
+    } else {
+        for (uint64_t i = 0; i < ncs; i++) P.bad[i] = 0;
+    }
+    const uint8_t *bad = P.bad;
+    // the changes of incomplete versions are buffered on the host: fetched once (device input)
+    std::map<uint64_t, uint64_t> inc_row;  // changeset -> first fetched row
+    corro::HostSpanRows inc;
+    if (mem == CORRO_MEM_DEVICE && any_slow) {
+        std::vector<corro::AgentSpan> sp;
+        uint64_t r = 0;
+        for (uint64_t i = 0; i < ncs; i++)
+            if (cs[i].kind == CORRO_CS_FULL && cs[i].change_count && !is_complete(cs[i]) && !bad[i]) {
+                inc_row[i] = r;
+                sp.push_back({cs[i].change_off, r, cs[i].change_count, cs[i].ts});
+                r += cs[i].change_count;
+            }
+        if (!sp.empty()) TRY_RC(corro::agent_dev_fetch(ctx, &dv, sp, inc));
+    }
+    auto row_of = [&](const corro_changeset &c, uint64_t ci, uint64_t k) -> HostRow {
+        if (mem == CORRO_MEM_HOST) return row_at(in, c.change_off + k, c.ts);
+        const uint64_t j = inc_row.at(ci) + k;
+        HostRow r;
+        r.pk = inc.pk[j];
+        r.tcid = inc.tcid[j];
+        r.cv = inc.cv[j];
+        r.dbv = inc.dbv[j];
+        r.cl = inc.cl[j];
+        r.seq = inc.seq[j];
+        r.site = inc.site[j];
+        r.v0 = inc.v0[j];
+        r.v1 = in->val1 ? inc.v1[j] : 0;
+        r.vt = inc.vt[j];
+        r.vl = in->val_len ? inc.vl[j] : 0;
+        r.ts = in->ts ? inc.ts[j] : c.ts;
+        if (inc.lv_len[j])
+            r.lv.assign(reinterpret_cast<const char *>(inc.lv_data.data() + inc.lv_off[j]), inc.lv_len[j]);
+        return r;
+    };
+    stage("screen");
+
+    // 3a. the fast actors' changesets, in arrival order (chunks in parallel): each one new to the actor
+    // (contains_all) is merged, or cleared when empty (process_empty_version, util.rs:810-824), or
+    // rolled back alone when it names an unknown table / column (util.rs:839-860). Their version runs
+    // per (chunk, actor) feed the gap bookkeeping.
+    struct ChunkOut {
+        std::vector<std::pair<uint32_t, Range>> runs;  // (work index, versions) in arrival order
+        std::vector<std::pair<uint32_t, uint64_t>> set_dbv;
+        uint64_t nspans = 0, nb = 0;
+        bool ts = false;
+    };
+    std::vector<ChunkOut> cout(nchunk);
+    run_parallel(nchunk, [&](size_t k) {
+        uint64_t lo, hi;
+        chunk_of(k, lo, hi);
+        ChunkOut &o = cout[k];
+        std::vector<int64_t> open(work.size(), -1);  // index into o.runs of the actor's open run
+        for (uint64_t i = lo; i < hi; i++) {
+            const corro_changeset &c = cs[i];
+            const uint32_t wi = (uint32_t)work_of[c.site];
+            const ActorWork &w = work[wi];
+            if (!w.fast) continue;
+            const uint64_t v = c.version_start;
+            Range sq{c.seq_start, c.seq_end};
+            if (w.had_max && v <= w.max && w.booked->contains_all(v, v, &sq)) continue;
+            if (c.change_count == 0) {
+                if (!w.had_max || v > w.max) o.set_dbv.emplace_back(wi, v);
+                out->known[i] = CORRO_KNOWN_CLEARED;
+            } else if (bad[i]) {
+                out->known[i] = CORRO_E_UNKNOWN_COLUMN;
+                continue;
+            } else {
+                P.flag[i] = 1;
+                out->known[i] = CORRO_KNOWN_CURRENT;
+                o.nspans++;
+                o.nb += c.change_count;
+                o.ts |= c.ts != 0;
+            }
+            int64_t &r = open[wi];
+            if (r >= 0 && o.runs[(size_t)r].second.second + 1 == v) {
+                o.runs[(size_t)r].second.second = v;
+            } else {
+                r = (int64_t)o.runs.size();
+                o.runs.emplace_back(wi, Range{v, v});
+            }
+        }
+    }, 1);
+    // 3b. per actor: the other actors' passes 1 and 2 (util.rs:704-884), then every actor's gap
+    // snapshot (:894-932)
+    std::vector<std::vector<Range>> fast_runs(work.size());
+    for (size_t k = 0; k < nchunk; k++)
+        for (auto &[wi, r] : cout[k].runs) fast_runs[wi].push_back(r);
+    auto run_actor = [&](size_t wi) {
+        ActorWork &w = work[wi];
+        corro::Booked &booked = *w.booked;
+        const bool had_max = w.had_max;
+        const uint64_t max = w.max;
+        RangeSet versions;
+        if (w.fast) {
+            for (const Range &r : fast_runs[wi]) versions.insert(r.first, r.second);
+        } else {
+            // pass 1: batch-local dedup of (versions, seqs), then versions the actor already holds
+            std::vector<uint64_t> unknown;
+            unknown.reserve(w.nidx);
+            std::set<std::tuple<uint64_t, uint64_t, int, uint64_t, uint64_t>> seen;
+            for (uint64_t k = 0; k < w.nidx; k++) {
+                const uint64_t i = w.idx[k];
+                const Range v = versions_of(cs[i]);
+                Range sq;
+                const Range *seqs = seqs_of(cs[i], sq);
+                if (!seen.emplace(v.first, v.second, seqs ? 1 : 0, seqs ? sq.first : 0, seqs ? sq.second : 0).second)
+                    continue;
+                if (booked.contains_all(v.first, v.second, seqs)) continue;
+                unknown.push_back(i);
+            }
+            // pass 2 (the bookie is not written until the call commits, so pass 1's contains_all stands)
+            SeenMap seen_local;
+            for (uint64_t i : unknown) {
+                const corro_changeset &c = cs[i];
+                const Range v = versions_of(c);
+                Range sq;
+                const Range *seqs = seqs_of(c, sq);
+                if (seen_local.all_seen(v, seqs)) continue;
+                std::optional<corro::PartialVersion> partial;
+                if (is_complete(c) && is_empty(c)) {
+                    // process_empty_version only when end > booked max (util.rs:810-824)
+                    if (!had_max || v.second > max) w.set_dbv.push_back(v.second);
+                    out->known[i] = CORRO_KNOWN_CLEARED;
                 } else {
-                    corro::PartialVersion p;
-                    if (process_incomplete(bk, st, c, in, p) != CORRO_OK) {
-                        out->known[i] = CORRO_E_INVALID;
+                    if (seqs && seqs->second < seqs->first) continue;  // invalid seqs (util.rs:826-831)
+                    if (bad[i]) {  // the INSERT fails, the version's SAVEPOINT rolls back (util.rs:839-860)
+                        out->known[i] = CORRO_E_UNKNOWN_COLUMN;
                         continue;
                     }
-                    partial = p;
-                    out->known[i] = CORRO_KNOWN_PARTIAL;
+                    if (is_complete(c)) {
+                        P.flag[i] = 1;
+                        w.nspans++;
+                        w.nchanges += c.change_count;
+                        w.ts |= c.ts != 0;
+                        out->known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
+                    } else {
+                        corro::PartialVersion p;
+                        if (process_incomplete(bk, w.st, c, [&](uint64_t k) { return row_of(c, i, k); }, p) !=
+                            CORRO_OK) {
+                            out->known[i] = CORRO_E_INVALID;
+                            continue;
+                        }
+                        partial = p;
+                        out->known[i] = CORRO_KNOWN_PARTIAL;
+                    }
                 }
+                seen_local.insert(v, partial);
+                versions.insert(v.first, v.second);
+                if (partial) w.partials.emplace_back(v.first, *partial);
             }
-            seen_local.emplace_back(v, partial);
-            processed[actor].emplace_back(v, partial);
         }
-    }
-
-    // gap bookkeeping first, on copies of the actors' Booked (VersionsSnapshot, agent.rs:1108-1235): an
-    // INSERT that would violate __corro_bookkeeping_gaps' key fails the whole call before the merge
-    // has touched the state, as the transaction's rollback would undo it (util.rs:894-936)
-    std::map<ActorId, corro::Booked> next;
-    std::vector<std::pair<ActorId, uint64_t>> ready;
-    for (auto &[actor, list] : processed) {
-        corro::Booked nb = bk->actors[actor];
-        RangeSet versions;
-        for (auto &e : list) versions.insert(e.first.first, e.first.second);
-        if (!nb.insert_db(versions, nullptr, nullptr))
-            return fail(CORRO_E_INVALID, "UNIQUE constraint failed: __corro_bookkeeping_gaps.start");
-        for (auto &e : list) {
-            if (!e.second) continue;
-            const uint64_t version = e.first.first;
-            const corro::PartialVersion &p = nb.insert_partial(version, *e.second);
-            if (p.seqs.gaps(0, p.last_seq).empty()) ready.emplace_back(actor, version);
+        if (versions.empty()) return;
+        // gap bookkeeping on a copy of the actor's Booked (VersionsSnapshot, agent.rs:1108-1235): an
+        // INSERT that would violate __corro_bookkeeping_gaps' key fails the whole call before the
+        // merge has touched the state, as the transaction's rollback would undo it (util.rs:894-936)
+        w.next = booked;
+        w.has_next = true;
+        if (!w.next.insert_db(versions, nullptr, nullptr)) {
+            w.rc = CORRO_E_INVALID;
+            w.err = "UNIQUE constraint failed: __corro_bookkeeping_gaps.start";
+            return;
         }
-        next.emplace(actor, std::move(nb));
-    }
-
-    // the merge: one batch in application order
-    std::vector<uint8_t> impact(batch.size(), 0);
-    if (batch.size()) {
-        corro_changes view = batch.view();
-        corro_apply_out ao{};
-        ao.impact = impact.data();
-        int rc = corro_apply_batch(ctx, &view, CORRO_MEM_HOST, &ao);
-        if (rc != CORRO_OK) {  // the transaction fails as a whole (util.rs:849-855)
-            for (uint64_t i = 0; i < ncs; i++) out->known[i] = CORRO_KNOWN_SKIPPED;
-            return rc;
+        for (auto &[version, pv] : w.partials) {
+            const corro::PartialVersion &p = w.next.insert_partial(version, pv);
+            if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
         }
-    }
-    // commit: everything below only records what the successful transaction did
-    for (const auto &[site, version] : st.set_dbv) {
-        int rc = corro::set_db_version(ctx, site, version);
-        if (rc != CORRO_OK) return rc;
-    }
-    // corro.changes.committed{table} (util.rs:533-535): every buffered change of an incomplete
-    // version (:1101-1105), every impactful change of a complete one (:1254-1258, below)
-    std::vector<uint64_t> committed;
-    auto commit_count = [&](uint32_t tcid) {
-        if ((tcid >> 16) >= committed.size()) committed.resize((tcid >> 16) + 1, 0);
-        committed[tcid >> 16]++;
     };
-    for (const HostRow &r : st.buffered) {  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
-        bk->buffered[{r.site, r.dbv}].emplace(r.seq, r);
-        commit_count(r.tcid);
+    run_parallel(work.size(), [&](size_t k) { run_actor(k); });
+    for (ActorWork &w : work)
+        if (w.rc != CORRO_OK) return fail(w.rc, w.err);
+    uint64_t nspans = 0, nb = 0;
+    bool need_ts = false;
+    for (const ChunkOut &o : cout) {
+        nspans += o.nspans;
+        nb += o.nb;
+        need_ts |= o.ts;
     }
-    for (auto &[key, sb] : st.seqbook) bk->seqbook[key] = sb;
-    // impactful changes: crsql_rows_impacted() is cumulative over the transaction, while
-    // last_rows_impacted restarts at 0 for every version (util.rs:1218-1261)
-    uint64_t cum = 0;
-    for (size_t a = 0; a < applied.size(); a++) {
-        const uint64_t ci = applied[a].first, row0 = applied[a].second;
-        const corro_changeset &c = cs[ci];
-        uint64_t last = 0;
-        bool any = false;
-        for (uint64_t k = 0; k < c.change_count; k++) {
-            cum += impact[row0 + k];
-            const bool hit = cum > last;
-            last = cum;
-            if (hit) {
-                any = true;
-                if (out->impactful) out->impactful[c.change_off + k] = 1;
-                commit_count(in->table_cid[c.change_off + k]);
+    for (const ActorWork &w : work) {
+        nspans += w.nspans;
+        nb += w.nchanges;
+        need_ts |= w.ts;
+    }
+    stage("actors");
+
+    // 4. the merge: one batch of every flagged changeset, actors in ActorId byte order (the device
+    // orders and gathers them)
+    const uint32_t ntables = corro::agent_table_count(ctx);
+    std::vector<uint64_t> committed(ntables, 0);
+    if (nb || out->impactful) {
+        corro_changes batch{};
+        const uint8_t *imp = nullptr;
+        if (nb) {
+            bool gathered = false;
+            TRY_RC(corro::agent_dev_batch(ctx, &dv, P, ncs, nspans, nb, need_ts, &batch, &gathered));
+            stage(gathered ? "order+gather" : "order");
+            int rc = CORRO_OK;
+            uint8_t *ib = corro::agent_dev_impact_buf(ctx, nb, &rc);
+            if (rc != CORRO_OK) return rc;
+            corro_apply_out ao{};
+            ao.impact = ib;
+            rc = corro_apply_batch(ctx, &batch, CORRO_MEM_DEVICE, &ao);
+            if (rc != CORRO_OK) {  // the transaction fails as a whole (util.rs:849-855)
+                for (uint64_t i = 0; i < ncs; i++) out->known[i] = CORRO_KNOWN_SKIPPED;
+                return rc;
             }
+            imp = ib;
+            stage("apply");
         }
-        out->known[ci] = any ? CORRO_KNOWN_CURRENT : CORRO_KNOWN_CLEARED;
-        if (!c.change_count) out->known[ci] = CORRO_KNOWN_CLEARED;
-        // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303)
-        clear_buffered(bk, c.site, c.version_start, c.version_start);
+        TRY_RC(corro::agent_dev_impacts(ctx, imp, batch.table_cid, nb, P, ncs, nspans, out->impactful, nchanges, mem,
+                                        ntables));
+        for (uint32_t t = 0; t < ntables; t++) committed[t] += P.committed[t];
+        stage("impacts");
     }
-    // per-actor gap snapshot commit, then partials (util.rs:936-1008)
-    for (auto &[actor, nb] : next) bk->actors[actor] = std::move(nb);
-    for (auto &r : ready) bk->ready.push_back(r);
-    out->n_ready = ready.size();
+
+    // 5. commit: everything below only records what the successful transaction did
+    for (const ChunkOut &o : cout)
+        for (auto &[wi, version] : o.set_dbv) TRY_RC(corro::set_db_version(ctx, work[wi].site, version));
+    for (ActorWork &w : work)
+        for (uint64_t version : w.set_dbv) TRY_RC(corro::set_db_version(ctx, w.site, version));
+    // corro.changes.committed{table} (util.rs:533-535): every buffered change of an incomplete version
+    // (:1101-1105), every impactful change of a complete one (:1254-1258, counted on the device)
+    for (ActorWork &w : work) {
+        for (const HostRow &r : w.st.buffered) {  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
+            bk->buffered[{r.site, r.dbv}].emplace(r.seq, r);
+            if ((r.tcid >> 16) < ntables) committed[r.tcid >> 16]++;
+        }
+        for (auto &[key, sb] : w.st.seqbook) bk->seqbook[key] = sb;
+    }
+    // known: Current when the version had an impactful change, else Cleared (util.rs:1264-1287)
+    const bool clear_meta = !bk->buffered.empty() || !bk->seqbook.empty();
+    if (nspans)
+        run_parallel(nchunk, [&](size_t k) {
+            uint64_t lo, hi;
+            chunk_of(k, lo, hi);
+            for (uint64_t i = lo; i < hi; i++)
+                if (P.flag[i]) out->known[i] = P.any[i] ? CORRO_KNOWN_CURRENT : CORRO_KNOWN_CLEARED;
+        }, 1);
+    // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303)
+    if (clear_meta)
+        for (uint64_t i = 0; i < ncs; i++)
+            if (P.flag[i]) clear_buffered(bk, cs[i].site, cs[i].version_start, cs[i].version_start);
+    // per-actor gap snapshot commit, then partials (util.rs:936-1008), actors in ActorId order
+    std::vector<size_t> order(work.size());
+    for (size_t k = 0; k < order.size(); k++) order[k] = k;
+    std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return work[x].id < work[y].id; });
+    uint64_t nready = 0;
+    for (size_t k : order) {
+        ActorWork &w = work[k];
+        if (w.has_next) *w.booked = std::move(w.next);
+        for (uint64_t v : w.ready) bk->ready.emplace_back(w.id, v);
+        nready += w.ready.size();
+    }
+    out->n_ready = nready;
     corro_detail_add_committed(ctx, committed.data(), committed.size());
+    stage("commit");
+    if (prof) fprintf(stderr, "[corro agent] ncs=%llu spans=%llu changes=%llu ms:%s\n", (unsigned long long)ncs,
+                      (unsigned long long)nspans, (unsigned long long)nb, prof_line.c_str());
     return CORRO_OK;
 }
 

@@ -1,0 +1,85 @@
+// Device half of corro_process_multiple_changes (agent.cpp), in plain C++ types: agent.cpp is host
+// C++ and never sees HIP. Implemented in agent_dev.hip.
+//
+// The call keeps the caller's change batch where it is (device memory, or staged once from host
+// memory) and does its per-change work on the GPU: the bad-cid screen of every changeset (util.rs
+// :839-860), the applied batch (zero-copy when the applied changesets are one contiguous run of the
+// input, else one gather kernel), and the impactful-change flags with the transaction-cumulative
+// crsql_rows_impacted() rule (util.rs:1218-1261). The host only walks changeset headers.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "corro_hip.h"
+
+namespace corro {
+
+// A run of input changes that goes into the applied batch: input [src, src + count) -> batch
+// [dst, dst + count); ts = the changeset timestamp (bound per change when the input has no ts).
+struct AgentSpan {
+    uint64_t src, dst, count, ts;
+};
+
+// Pinned host arrays of one call (agent_dev_begin; valid until the next begin on the context), per
+// changeset in arrival order. The host fills them in sequential parallel passes and each crosses to
+// the device with one copy:
+//   off / cnt  its change span (cnt 0 = not screened: not a non-empty Full)
+//   ts / site  its timestamp and actor (site ordinal)
+//   flag       1 = merged by this call (a complete version that passed every check)
+//   bad        filled by agent_dev_bad; any: filled by agent_dev_impacts (flag set only)
+struct AgentPinned {
+    uint64_t *off, *cnt, *ts;
+    uint32_t *site;
+    uint8_t *flag, *bad, *any;
+    uint64_t *committed;  // per table
+};
+int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, AgentPinned *p);
+
+// Device view of the input: `in` itself for CORRO_MEM_DEVICE, else every field copied to device
+// scratch (val_data too). The view stays valid until the call ends.
+int agent_dev_input(corro_ctx *ctx, const corro_changes *in, int mem, corro_changes *dv);
+
+// p.bad[j] = 1 when changes [off[j], off[j] + cnt[j]) hold a table_cid of CORRO_TCID_UNKNOWN.
+int agent_dev_bad(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &p, uint64_t ncs);
+
+// Host copies of the input changes of `spans` (dst ignored), concatenated: field arrays of
+// sum(count) elements + the bytes of their long values (lv_off/lv_len index lv_data; len 0 = none).
+// (Incomplete versions only: pageable copies, its own device scratch.)
+struct HostSpanRows {
+    std::vector<uint64_t> pk, v0, v1, ts;
+    std::vector<int64_t> cv, dbv;
+    std::vector<uint32_t> tcid, cl, seq, site;
+    std::vector<uint8_t> vt, vl;
+    std::vector<uint64_t> lv_off, lv_len;
+    std::vector<uint8_t> lv_data;
+};
+int agent_dev_fetch(corro_ctx *ctx, const corro_changes *dv, const std::vector<AgentSpan> &spans, HostSpanRows &out);
+
+// The applied batch (device SoA, application order) of the nspans flagged changesets: their order
+// (actors by ActorId bytes = site rank, arrival order within an actor) from a stable device radix
+// sort, their batch offsets from a device scan. Zero-copy (pointers into dv) when the spans are one
+// contiguous, suitably aligned run of the input and every needed field is there; else a gather into
+// device scratch that also fills ts from the changesets when the input has none and some changeset
+// carries one. *gathered says which. The span tables stay on the device for agent_dev_impacts.
+int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &p, uint64_t ncs, uint64_t nspans,
+                    uint64_t nbatch, bool need_ts, corro_changes *batch, bool *gathered);
+
+// Device impact buffer for a batch of n changes (valid until the next call).
+uint8_t *agent_dev_impact_buf(corro_ctx *ctx, uint64_t n, int *rc);
+
+// From the batch's per-change impact growth: impactful[span.src + k] (0/1 over all nin input
+// changes, in `mem` memory; NULL = not wanted), p.any[i] = flagged changeset i had an impactful change,
+// p.committed[t] = impactful changes of table t (tcid = the batch's table_cid array, device). Rule
+// (util.rs:1218-1261): a version's first change is impactful when the transaction's cumulative
+// counter is > 0 after it (any impact at or before it in the batch); its later changes when their
+// own growth is > 0.
+int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tcid, uint64_t nbatch,
+                      const AgentPinned &p, uint64_t ncs, uint64_t nspans, uint8_t *impactful, uint64_t nin, int mem,
+                      uint32_t ntables);
+
+// The registered 16-byte id of a site ordinal (false: not registered).
+bool agent_site_id(corro_ctx *ctx, uint32_t site, uint8_t out[16]);
+uint32_t agent_site_count(corro_ctx *ctx);
+uint32_t agent_table_count(corro_ctx *ctx);
+
+}  // namespace corro

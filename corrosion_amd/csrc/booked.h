@@ -38,7 +38,7 @@ struct Booked {
     bool contains_all(uint64_t s, uint64_t e, const Range *seqs) const {
         if (s > e) return true;
         if (e > max_or_zero()) return false;
-        if (!needed.overlapping(s, e).empty()) return false;
+        if (needed.any_overlap(s, e)) return false;
         if (!seqs || seqs->first > seqs->second) return true;
         for (auto it = partials.lower_bound(s); it != partials.end() && it->first <= e; ++it)
             if (!it->second.seqs.contains_range(seqs->first, seqs->second)) return false;

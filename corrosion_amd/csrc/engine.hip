@@ -339,10 +339,13 @@ static int store_clear(corro_ctx *ctx) {
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_used.p, 0, ctx->B * 4ULL, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_gen.p, 0, ctx->B * 4ULL, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_heap_top.p, 0, 8, s));  // (stream-ordered before the next apply)
+    if (ctx->d_touch_n.p) CORRO_HIP_TRY(hipMemsetAsync(ctx->d_touch_n.p, 0, 8, s));
+    ctx->touch_bound = 0;
     ctx->state_total = 0;
     ctx->state_rows = 0;
     ctx->arena_top = 0;
     ctx->state_epoch++;
+    ctx->poisoned = false;
     return CORRO_OK;
 }
 
@@ -411,6 +414,11 @@ int grow_heap(corro_ctx *ctx, uint64_t want_records) {
     // (heap indices stay below 2^31: the fast bodies mark a new row's heap offset with the top bit)
     if (cap > (1ULL << 31)) cap = 1ULL << 31;
     if (cap < want_records) return fail(CORRO_E_RANGE, "row store heap would exceed 2^31 records");
+    if (ctx->heap_limit && cap > ctx->heap_limit) {
+        if (want_records > ctx->heap_limit)
+            return fail(CORRO_E_NOMEM, "row store heap would exceed the context's store limit");
+        cap = ctx->heap_limit;
+    }
     hipStream_t s = ctx->stream;
     unsigned long long top = 0;
     CORRO_HIP_TRY(hipMemcpyAsync(&top, ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost, s));
@@ -523,9 +531,12 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
-                      &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag};
+                      &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,
+                      &ctx->d_agent_in, &ctx->d_agent_batch, &ctx->d_agent_spans, &ctx->d_agent_imp,
+                      &ctx->d_agent_out, &ctx->d_agent_aux, &ctx->d_agent_fetch, &ctx->d_agent_aux2, &ctx->d_touch, &ctx->d_touch_n, &ctx->d_touch_stamp, &ctx->d_touch_tmp};
     for (DevBuf *b : bufs) b->release();
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
+    if (ctx->h_agent) (void)hipHostFree(ctx->h_agent);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -694,7 +705,8 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_bflags.p, 0, ((B + 31) / 32) * 4ULL, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, MISC_WORDS * 8, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_dbv_batch.p, 0, (size_t)nsites * 8, s));
-    if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 0, n, s));
+    // (1: the INTEGER impact body stores only zero flags; every other body stores each change's)
+    if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 1, n, s));
 
     unsigned long long *misc = ctx->d_misc.as<unsigned long long>();
     const bool prof = ctx->profiling;
@@ -752,21 +764,27 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     a.track_ts = ctx->track_ts ? 1u : 0u;
     a.state_wide = ctx->state_wide ? 1u : 0u;
     a.arena = ctx->d_arena.as<uint8_t>();
+    a.touch = ctx->track_touched ? ctx->d_touch.as<uint4>() : nullptr;
+    a.touch_n = ctx->track_touched ? ctx->d_touch_n.as<unsigned long long>() : nullptr;
     uint32_t nblocks = B;
     float merge_ms = 0.f, ovf_ms = 0.f;
     for (int round = 0;; round++) {
         if (round > 40) return fail(CORRO_E_NOMEM, "internal: the row store did not take the batch's rows");
         // a batch that failed validation (k_scatter's error bits) is never merged
         if (round == 0) {
-            CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, 8, hipMemcpyDeviceToHost, s));
+            CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, (MISC_CVBIG + 1) * 8, hipMemcpyDeviceToHost, s));
             CORRO_HIP_TRY(hipStreamSynchronize(s));
             if (ctx->h_misc[0]) return error_from_bits(ctx->h_misc[0]);
             if (prof)
                 for (int i = 0; i < 4; i++) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[i], ctx->ev[i], ctx->ev[i + 1]));
         }
         mark(4);
+        ctx->apply_wrote = true;  // from here on a failure leaves the state part-merged
         if (a.impact) {
-            hipLaunchKernelGGL(k_merge_fast_int<true>, dim3(nblocks), dim3(FAST_T), 0, s, a);
+            // the packed two-word keys of the INTEGER impact body: col_versions < 2^15, <= 2^16 sites
+            const bool packed = ctx->h_misc[MISC_CVBIG] == 0 && nsites <= 65536;
+            auto kern = packed ? k_merge_fast_int<true, true> : k_merge_fast_int<true, false>;
+            hipLaunchKernelGGL(kern, dim3(nblocks), dim3(FAST_T), 0, s, a);
             CORRO_HIP_TRY(hipGetLastError());
             hipLaunchKernelGGL(k_merge_fast_wide<true>, dim3(std::min(nblocks, LIST_GRID)), dim3(FAST_T), 0, s, a);
         } else {
@@ -825,6 +843,13 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     ctx->state_total += ctx->h_misc[MISC_LIVE];  // (a signed delta in two's complement)
     ctx->state_rows = ctx->h_misc[MISC_ROWS];
+#if CORRO_DIAG & 256
+    fprintf(stderr, "DIAG impact phases (us per bucket): loads %.3f claims %.3f rows %.3f prior %.3f counts %.3f ranks %.3f walk %.3f winners %.3f\n",
+            ctx->h_misc[MISC_DIAG] / 100.0 / B, ctx->h_misc[MISC_DIAG + 1] / 100.0 / B,
+            ctx->h_misc[MISC_DIAG + 2] / 100.0 / B, ctx->h_misc[MISC_DIAG + 3] / 100.0 / B,
+            ctx->h_misc[MISC_DIAG + 4] / 100.0 / B, ctx->h_misc[MISC_DIAG + 5] / 100.0 / B,
+            ctx->h_misc[MISC_DIAG + 6] / 100.0 / B, ctx->h_misc[MISC_DIAG + 7] / 100.0 / B);
+#endif
 #if CORRO_DIAG & 64
     fprintf(stderr, "DIAG phases (us per bucket): load %.3f claims %.3f rows_count %.3f stage1 %.3f stages %.3f fast_rows %.3f winners %.3f publish %.3f\n",
             ctx->h_misc[MISC_DIAG] / 100.0 / B, ctx->h_misc[MISC_DIAG + 1] / 100.0 / B,
@@ -856,13 +881,50 @@ static uint64_t chunk_changes(const corro_ctx *ctx) {
     return std::max<uint64_t>(1ULL << 16, (uint64_t)ctx->B * 2048ULL);
 }
 
+// Room in the touched-row list for a batch of n changes (at most n rows): the bound grows by n per
+// apply; when it would pass the capacity the exact count is read and the list regrown (contents kept).
+static int touch_reserve(corro_ctx *ctx, uint64_t n) {
+    if (!ctx->d_touch_n.p) {
+        TRY(ctx->d_touch_n.ensure(8));
+        CORRO_HIP_TRY(hipMemsetAsync(ctx->d_touch_n.p, 0, 8, ctx->stream));
+    }
+    if (ctx->touch_bound + n > ctx->touch_cap) {
+        unsigned long long cur = 0;
+        CORRO_HIP_TRY(hipMemcpyAsync(&cur, ctx->d_touch_n.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
+        ctx->touch_bound = cur;
+        if (cur + n > ctx->touch_cap) {
+            const uint64_t cap = std::max<uint64_t>(cur + n, std::min<uint64_t>(2 * ctx->touch_cap, cur + 4 * n));
+            DevBuf nb;
+            TRY(nb.ensure(cap * 16));
+            if (cur) CORRO_HIP_TRY(hipMemcpyAsync(nb.p, ctx->d_touch.p, cur * 16, hipMemcpyDeviceToDevice, ctx->stream));
+            CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
+            ctx->d_touch.release();
+            ctx->d_touch = nb;
+            nb.p = nullptr;
+            ctx->touch_cap = cap;
+        }
+    }
+    ctx->touch_bound += n;
+    return CORRO_OK;
+}
+
 static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out);
+static const char *poisoned_msg =
+    "context poisoned: an earlier apply failed after it began writing the state; call corro_state_reset";
 
 int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out) {
     if (!ctx || !in) return fail(CORRO_E_INVALID, "NULL argument");
+    if (ctx->poisoned) return fail(CORRO_E_DEVICE, poisoned_msg);
     if (in->n == 0) return CORRO_OK;
     const auto t0 = std::chrono::steady_clock::now();
+    ctx->apply_wrote = false;
     const int rc = apply_batch_impl(ctx, in, mem, out);
+    if (rc != CORRO_OK && ctx->apply_wrote) {
+        // the merge had begun writing: the state is no longer the pre-call state
+        ctx->poisoned = true;
+        corro::set_error(corro_last_error() + std::string(" (mid-apply: the context is poisoned until corro_state_reset)"));
+    }
     if (rc == CORRO_OK) {
         corro_metrics &m = ctx->metrics;
         m.applies++;
@@ -933,6 +995,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
     uint8_t *imp_buf = !(out && out->impact) ? nullptr : (imp_dev ? out->impact : ctx->d_impact.as<uint8_t>());
 
     TRY(affinity_check(ctx, bd));
+    if (ctx->track_touched) TRY(touch_reserve(ctx, n));
     const uint64_t chunk = chunk_changes(ctx);
     if (n > chunk) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
@@ -1077,6 +1140,7 @@ int corro_state_reset(corro_ctx *ctx) {
 
 int corro_state_export(corro_ctx *ctx, corro_rows *o, uint64_t cap, uint64_t *written) {
     if (!ctx || !o || !written) return fail(CORRO_E_INVALID, "NULL argument");
+    if (ctx->poisoned) return fail(CORRO_E_DEVICE, poisoned_msg);
     const uint64_t m = ctx->state_total;
     *written = 0;
     if (cap < m) return fail(CORRO_E_INVALID, "export capacity too small");
@@ -1165,6 +1229,100 @@ int corro_value_bytes(corro_ctx *ctx, const uint64_t *handles, uint64_t n, uint8
     CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipMemcpyAsync(bytes, dout, total, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+int corro_ctx_track_touched(corro_ctx *ctx, int on) {
+    if (!ctx) return fail(CORRO_E_INVALID, "NULL argument");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    ctx->track_touched = on != 0;
+    TRY(ctx->d_touch_n.ensure(8));
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_touch_n.p, 0, 8, ctx->stream));
+    CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->touch_bound = 0;
+    return CORRO_OK;
+}
+
+int corro_ctx_set_store_limit(corro_ctx *ctx, uint64_t max_heap_records) {
+    if (!ctx) return fail(CORRO_E_INVALID, "NULL argument");
+    ctx->heap_limit = max_heap_records;
+    return CORRO_OK;
+}
+
+int corro_state_export_touched(corro_ctx *ctx, corro_rows *o, uint64_t cap, uint64_t *written) {
+    if (!ctx || !o || !written) return fail(CORRO_E_INVALID, "NULL argument");
+    *written = 0;
+    if (ctx->poisoned) return fail(CORRO_E_DEVICE, poisoned_msg);
+    if (!ctx->track_touched) return fail(CORRO_E_INVALID, "touched-row tracking is off (corro_ctx_track_touched)");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    unsigned long long m = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&m, ctx->d_touch_n.p, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (m == 0) return CORRO_OK;
+    if (m * (uint64_t)ctx->max_stride >= (1ULL << 32))
+        return fail(CORRO_E_RANGE, "touched rows exceed one export (2^32 clock rows): export after every apply");
+    // dedup stamps per region entry: reallocated (zeroed) when the regions changed size
+    const uint64_t nent = (uint64_t)ctx->B << ctx->log2S;
+    if (ctx->touch_stamp_n != nent || ++ctx->touch_epoch == 0) {
+        TRY(ctx->d_touch_stamp.ensure(nent * 4));
+        CORRO_HIP_TRY(hipMemsetAsync(ctx->d_touch_stamp.p, 0, nent * 4, s));
+        ctx->touch_stamp_n = nent;
+        ctx->touch_epoch = 1;
+    }
+    size_t temp = 0;
+    TRY(prim_inclusive_scan_u32(nullptr, &temp, nullptr, nullptr, (uint32_t)m, s));
+    const size_t col = ((m * 4 + 255) / 256) * 256;
+    TRY(ctx->d_touch_tmp.ensure(3 * col + temp + 256));
+    uint32_t *ent = ctx->d_touch_tmp.as<uint32_t>();
+    uint32_t *cnt = (uint32_t *)((uint8_t *)ent + col), *incl = (uint32_t *)((uint8_t *)ent + 2 * col);
+    void *tmp = (uint8_t *)ent + 3 * col;
+    const dim3 grid((uint32_t)std::min<uint64_t>((m + 255) / 256, 8192));
+    hipLaunchKernelGGL(k_touch_count, grid, dim3(256), 0, s, row_store(ctx), ctx->log2B, ctx->d_touch.as<uint4>(), m,
+                       ctx->d_touch_stamp.as<uint32_t>(), ctx->touch_epoch, ent, cnt);
+    CORRO_HIP_TRY(hipGetLastError());
+    TRY(prim_inclusive_scan_u32(tmp, &temp, cnt, incl, (uint32_t)m, s));
+    uint32_t total = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&total, incl + (m - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (total > cap) {  // the list is kept: a retry with room exports the same rows
+        *written = total;
+        return fail(CORRO_E_RANGE, "touched rows exceed cap (*written = the row count)");
+    }
+    const size_t per = 8 * 7 + 4 * 3 + 2;
+    TRY(ctx->d_export.ensure((uint64_t)total * per + 13 * 256 + 256));
+    uint8_t *p = ctx->d_export.as<uint8_t>();
+    corro_rows d{};
+    auto carve = [&](size_t elem) {
+        uint8_t *q = p;
+        p += (((uint64_t)total * elem + 255) / 256) * 256;
+        return q;
+    };
+    d.pk = (uint64_t *)carve(8);
+    d.col_version = (int64_t *)carve(8);
+    d.db_version = (int64_t *)carve(8);
+    d.cl = (int64_t *)carve(8);
+    d.ts = (uint64_t *)carve(8);
+    d.val0 = (uint64_t *)carve(8);
+    d.val1 = (uint64_t *)carve(8);
+    d.table_cid = (uint32_t *)carve(4);
+    d.seq = (uint32_t *)carve(4);
+    d.site = (uint32_t *)carve(4);
+    d.val_type = (uint8_t *)carve(1);
+    d.val_len = (uint8_t *)carve(1);
+    hipLaunchKernelGGL(k_touch_rows, grid, dim3(256), 0, s, row_store(ctx), ent, cnt, incl, m, d);
+    CORRO_HIP_TRY(hipGetLastError());
+    struct C { void *dst; const void *src; size_t elem; } cp[] = {
+        {o->pk, d.pk, 8},         {o->col_version, d.col_version, 8}, {o->db_version, d.db_version, 8},
+        {o->cl, d.cl, 8},         {o->ts, d.ts, 8},                   {o->val0, d.val0, 8},
+        {o->val1, d.val1, 8},     {o->table_cid, d.table_cid, 4},     {o->seq, d.seq, 4},
+        {o->site, d.site, 4},     {o->val_type, d.val_type, 1},       {o->val_len, d.val_len, 1}};
+    for (auto &c : cp)
+        if (c.dst && total) CORRO_HIP_TRY(hipMemcpyAsync(c.dst, c.src, (uint64_t)total * c.elem, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_touch_n.p, 0, 8, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    ctx->touch_bound = 0;
+    *written = total;
     return CORRO_OK;
 }
 

@@ -120,6 +120,19 @@ struct corro_ctx {
     corro_metrics metrics{};      // cumulative counters (corro_ctx_metrics)
     std::vector<uint64_t> committed;  // per table: changes committed by corro_process_multiple_changes
     bool track_ts = false;
+    // rows addressed by the applies since the last corro_state_export_touched (or reset): an
+    // append-only list of (pk, table) written by the merge bodies, deduplicated at export
+    bool track_touched = false;
+    corro::DevBuf d_touch, d_touch_n, d_touch_stamp, d_touch_tmp;
+    uint64_t touch_cap = 0;       // entries d_touch holds
+    uint64_t touch_bound = 0;     // upper bound of the entries written so far (changes applied)
+    uint32_t touch_epoch = 0;     // stamp of the current export (dedup per region entry)
+    uint64_t touch_stamp_n = 0;   // entries d_touch_stamp covers
+    // a failure after an apply's first merge write leaves the state part-merged: every later
+    // call on the context fails until corro_state_reset (corro_hip.h "Failure atomicity")
+    bool poisoned = false;
+    bool apply_wrote = false;     // the current apply has launched its first merge kernel
+    uint64_t heap_limit = 0;      // corro_ctx_set_store_limit (0: none)
     bool state_wide = false;      // some clock row holds a non-INTEGER value
     corro::DevBuf d_defer, d_relist;  // deferred buckets of a merge round, the re-merge list
     corro::DevBuf d_dense, d_dense_ts, d_dense_view;  // materialised state (extraction), its pseudo-buckets
@@ -163,6 +176,13 @@ struct corro_ctx {
     corro::DevBuf d_aff, d_affflag;
     bool aff_any = false;         // some column has an affinity other than BLOB
     corro::DevBuf d_part;         // partition counts
+    // process_multiple_changes on the device (agent_dev.hip): staged host input, gathered batch,
+    // span tables, impact flags, impactful output, and a pinned host staging area
+    corro::DevBuf d_agent_in, d_agent_batch, d_agent_spans, d_agent_imp, d_agent_out, d_agent_aux;
+    corro::DevBuf d_agent_fetch, d_agent_aux2;
+    void *h_agent = nullptr;
+    size_t h_agent_bytes = 0;
+    uint64_t agent_ncs = 0;       // changesets of the current call (d_agent_spans column length)
     uint64_t *h_misc = nullptr;   // pinned, 16 words
     // stage timing
     bool profiling = false;

@@ -70,6 +70,8 @@ struct MergeArgs {
     uint32_t track_ts;
     uint32_t state_wide;       // the state holds non-INTEGER values
     const uint8_t *arena;      // bytes of long TEXT/BLOB values (value handles point into it)
+    uint4 *touch;              // rows the apply addressed, (pk lo, pk hi, table, 0) each (null: not tracked)
+    unsigned long long *touch_n;
 };
 
 // misc words
@@ -163,6 +165,19 @@ __device__ inline bool long_value(const BatchDev &in, uint32_t i, uint64_t &w0, 
     w0 = w;
     w1 = ((in.lbase + off) << 24) | sz;
     return true;
+}
+
+// Append the calling lanes' rows to the touched-row list (corro_state_export_touched): one atomic per
+// wave over its active lanes, so it may be called from divergent code.
+__device__ inline void touch_append(const MergeArgs &a, uint64_t pk, uint32_t table) {
+    const unsigned long long act = __ballot(1);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t leader = (uint32_t)__ffsll(act) - 1;
+    const uint32_t rank = (uint32_t)__popcll(act & ((1ULL << lane) - 1ULL));
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(a.touch_n, (unsigned long long)__popcll(act));
+    base = __shfl(base, leader);
+    a.touch[base + rank] = make_uint4((uint32_t)pk, (uint32_t)(pk >> 32), table, 0u);
 }
 
 __device__ inline uint32_t site_rank_of(const MergeArgs &a, uint32_t site) {
@@ -923,6 +938,7 @@ struct LdsEmit {
             a.rs.ent[e].bits[0] = bits[0];
             a.rs.ent[e].bits[1] = bits[1];
         }
+        if (a.touch) touch_append(a, g.pk[row], g.tc[row] >> 16);
         atomicAdd(emitted, cnt);
         if (gen) *general = 1;
     }
@@ -1560,7 +1576,10 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * FAST_T + tid;
-        if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_k[i];
+        if (ent[k] != ROW_NONE && row[k] == i) {
+            a.rs.ent[ent[k]].bits[0] = s_k[i];
+            if (a.touch) touch_append(a, s_pk[i], s_tc[i] >> 16);
+        }
     }
     if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
     DIAG_MARK(5);
@@ -1784,15 +1803,24 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * FAST_T + tid;
-        if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_v0[i];
+        if (ent[k] != ROW_NONE && row[k] == i) {
+            a.rs.ent[ent[k]].bits[0] = s_v0[i];
+            if (a.touch) touch_append(a, pk[k], tc[k] >> 16);
+        }
     }
     if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
 }
 
-// The INTEGER form of the impact body in 76 KB of LDS (two workgroups per CU instead of one): a
+// The INTEGER form of the impact body in 76 KB of LDS (two workgroups per CU instead of one).
+// PACKED (every col_version < 2^15, at most 2^16 sites: the no-impact body's two-stage condition):
+// a member's key is two words, (col_version | value bits 63..16) and (value bits 15..0 | site rank),
+// so a member slot holds both words and the position in the LDS the unpacked form needs for its
+// three key words -- members are placed once and the walk compares positions directly. Unpacked: a
 // cell's members are placed in application order (each member's rank among its cell's positions),
-// so "earlier" is the member index and no position array is kept for the walk; the hashing arrays
-// are reused for the ordered keys.
+// so "earlier" is the member index and no position array is kept for the walk.
+// Only zero impacts are stored: the apply initialises the flags to 1 (every other body stores each
+// change's flag), which halves the byte scatter into batch order.
+template <bool PACKED>
 __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, const BucketView &v) {
     __shared__ uint64_t s_a[CAP_FAST];      // hashing: pk; then the cell-ordered biased col_versions
     __shared__ uint32_t s_b[CAP_FAST];      // hashing: table_cid; then positions by member slot; then site ranks
@@ -1810,6 +1838,12 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     uint32_t flags = 0;   // bit 2k: beats the prior clock; bit 2k+1: the cell had no prior clock
     bool alive[FAST_R];
     uint4 q[FAST_R][4];
+#if CORRO_DIAG & 256
+    unsigned long long diag_t2 = wall_clock64();
+#define DIAG_MARK2(k) do { if (tid == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&a.misc[MISC_DIAG + (k)], t_ - diag_t2); diag_t2 = t_; } } while (0)
+#else
+#define DIAG_MARK2(k) do { } while (0)
+#endif
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * FAST_T + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
@@ -1843,6 +1877,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) rank[k] = site[k] < a.nsites ? rank[k] : 0u;
     __syncthreads();
+    DIAG_MARK2(0);
     // 1. rows, then cells (row_claim / cell_claim)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1856,8 +1891,10 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     for (int k = 0; k < FAST_R; k++)
         if (alive[k]) cell[k] = cell_claim(s_own, k * FAST_T + tid, row[k], tc[k]);
     __syncthreads();
+    DIAG_MARK2(1);
     // 1b. row lookups, prior clocks: does the change beat its cell's prior?
     if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase, false)) return;
+    DIAG_MARK2(2);
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         hb[k] = 0;
@@ -1872,6 +1909,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
         }
     }
     __syncthreads();
+    DIAG_MARK2(3);
     // 2. member counts per owner, exclusive scan -> offsets
     for (uint32_t i = tid; i < FAST_SLOTS; i += FAST_T) s_own[i] = 0;
     __syncthreads();
@@ -1909,6 +1947,43 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) md[k] = alive[k] ? s_own[cell[k]] : 0u;
     __syncthreads();
+    DIAG_MARK2(4);
+    if constexpr (PACKED) {
+        // 3. keys and positions by member slot
+        uint32_t *s_p = reinterpret_cast<uint32_t *>(s_c);
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++)
+            if (alive[k]) {
+                const uint32_t d = atomicAdd(&s_own[cell[k]], 1u);
+                s_a[d] = ((cv[k] ^ 0x8000000000000000ULL) << 48) | (v0[k] >> 16);
+                s_b[d] = (uint32_t)((v0[k] & 0xFFFFULL) << 16) | rank[k];
+                s_p[d] = pos[k];
+                md[k] |= d << 16;
+            }
+        __syncthreads();
+        DIAG_MARK2(5);
+        // 4. one walk over the cell's members per change: impact and winner as below
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            if (!alive[k]) continue;
+            bool imp = (flags >> (2 * k)) & 1u, win = imp;
+            const uint32_t mb = md[k] & 0xFFFFu, d = md[k] >> 16, me = s_own[cell[k]];
+            const uint64_t k1 = s_a[d];
+            const uint32_t k2 = s_b[d];
+            for (uint32_t m = mb; m < me; m++) {
+                if (m == d) continue;
+                const uint64_t j1 = s_a[m];
+                const uint32_t j2 = s_b[m];
+                const int c = j1 != k1 ? (j1 > k1 ? 1 : -1) : (j2 != k2 ? (j2 > k2 ? 1 : -1) : 0);
+                const bool earlier = s_p[m] < pos[k];
+                if (earlier && c >= 0) imp = false;
+                if (c > 0 || (c == 0 && earlier)) win = false;
+            }
+            if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
+            alive[k] = win;
+        }
+        __syncthreads();
+    } else {
     // 3. positions by member slot, then each member's rank among its cell's positions
 #pragma unroll
     for (int k = 0; k < FAST_R; k++)
@@ -1932,6 +2007,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
             s_b[d] = rank[k];
         }
     __syncthreads();
+    DIAG_MARK2(5);
     // 4. one walk over the cell's members (application order) per change: impact (strict prefix
     // maximum, above the prior clock) and winner (maximum, earliest among equals, above the prior)
 #pragma unroll
@@ -1949,10 +2025,12 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
             if (earlier && c >= 0) imp = false;             // an earlier change already holds >= key
             if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
         }
-        if (a.impact && (pos[k] & BATCH_POS)) a.impact[pos[k] & 0x7FFFFFFFu] = imp ? 1 : 0;
+        if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
         alive[k] = win;
     }
     __syncthreads();
+    }
+    DIAG_MARK2(6);
     // 5. winners: the clock row into its heap slot; presence bits of new cells (s_c per owner)
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -1991,9 +2069,13 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * FAST_T + tid;
-        if (ent[k] != ROW_NONE && row[k] == i) a.rs.ent[ent[k]].bits[0] = s_c[i];
+        if (ent[k] != ROW_NONE && row[k] == i) {
+            a.rs.ent[ent[k]].bits[0] = s_c[i];
+            if (a.touch) touch_append(a, pk[k], tc[k] >> 16);
+        }
     }
     if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
+    DIAG_MARK2(7);
 }
 
 __device__ inline uint32_t bucket_of_block(const MergeArgs &a) {
@@ -2003,7 +2085,9 @@ __device__ inline uint32_t bucket_of_block(const MergeArgs &a) {
 // Bucket triage + the INTEGER fast body (one workgroup per bucket). General buckets and, for a
 // batch or state with non-INTEGER values, every fast bucket are queued for the list-driven kernels
 // below, so those launch a few hundred workgroups instead of one per bucket.
-template <bool IMPACT>
+// IMPACT bodies come as two kernels, PACKED chosen by the host from k_scatter's MISC_CVBIG (one
+// kernel holding both forms would size its registers for the larger and halve the occupancy)
+template <bool IMPACT, bool PACKED = false>
 static __global__ void __launch_bounds__(FAST_T, FAST_WAVES_EU)
 k_merge_fast_int(MergeArgs a) {
     const uint32_t b = bucket_of_block(a);
@@ -2034,10 +2118,12 @@ k_merge_fast_int(MergeArgs a) {
         if (threadIdx.x == 0) a.wide_list[atomicAdd(&a.misc[MISC_WIDEQ], 1ULL)] = b;
         return;
     }
-    if constexpr (IMPACT)
-        fast_body_impact_int(a, b, v);
-    else
+    if constexpr (IMPACT) {
+        (void)cvbig;
+        fast_body_impact_int<PACKED>(a, b, v);
+    } else {
         fast_body<false>(a, b, v, cvbig == 0 && a.nsites <= 65536);
+    }
 }
 
 constexpr uint32_t LIST_GRID = 512;
@@ -2170,22 +2256,58 @@ __device__ inline void for_each_state_record(const RowStore &rs, uint64_t nent, 
     }
 }
 
+// one clock record (heap index h, row causal length L) as crsql_changes row k
+__device__ inline void export_rec(const RowStore &rs, const corro_rows &o, unsigned long long k, uint32_t h, int64_t L) {
+    const Rec r = load_rec(rs.heap + h);
+    o.pk[k] = r.pk;
+    o.table_cid[k] = r.tcid;
+    o.col_version[k] = r.cv;
+    o.db_version[k] = r.dbv;
+    o.cl[k] = L;
+    o.seq[k] = r.seq;
+    o.site[k] = r.site;
+    o.ts[k] = rs.heap_ts ? rs.heap_ts[h] : 0ULL;
+    o.val0[k] = r.v0;
+    o.val1[k] = r.v1;
+    o.val_type[k] = (uint8_t)vtype(r.meta);
+    o.val_len[k] = (uint8_t)vlen(r.meta);
+}
+
 static __global__ void k_export(RowStore rs, uint64_t nent, unsigned long long *count, corro_rows o) {
-    for_each_state_record(rs, nent, count, [&](unsigned long long k, uint32_t h, int64_t L) {
-        const Rec r = load_rec(rs.heap + h);
-        o.pk[k] = r.pk;
-        o.table_cid[k] = r.tcid;
-        o.col_version[k] = r.cv;
-        o.db_version[k] = r.dbv;
-        o.cl[k] = L;
-        o.seq[k] = r.seq;
-        o.site[k] = r.site;
-        o.ts[k] = rs.heap_ts ? rs.heap_ts[h] : 0ULL;
-        o.val0[k] = r.v0;
-        o.val1[k] = r.v1;
-        o.val_type[k] = (uint8_t)vtype(r.meta);
-        o.val_len[k] = (uint8_t)vlen(r.meta);
-    });
+    for_each_state_record(rs, nent, count,
+                          [&](unsigned long long k, uint32_t h, int64_t L) { export_rec(rs, o, k, h, L); });
+}
+
+// corro_state_export_touched, pass 1: each listed row's region entry (looked up in its bucket's
+// region) and, for the first listing of the row in this export (stamp), its clock record count
+static __global__ void k_touch_count(RowStore rs, uint32_t log2B, const uint4 *__restrict__ touch, uint64_t m,
+                                     uint32_t *__restrict__ stamp, uint32_t epoch, uint32_t *__restrict__ ent,
+                                     uint32_t *__restrict__ cnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 t = touch[i];
+        const uint64_t pk = (uint64_t)t.x | ((uint64_t)t.y << 32);
+        const uint32_t e = rs_lookup(rs, bucket_of(t.z, pk, log2B), pk, t.z);
+        uint32_t c = 0;
+        if (e != ROW_NONE && atomicExch(&stamp[e], epoch) != epoch) c = row_popc(rs.ent[e].bits);
+        ent[i] = e;
+        cnt[i] = c;
+    }
+}
+
+// pass 2: the row's records at [incl - cnt, incl), sentinel first then by cid
+static __global__ void k_touch_rows(RowStore rs, const uint32_t *__restrict__ ent, const uint32_t *__restrict__ cnt,
+                                    const uint32_t *__restrict__ incl, uint64_t m, corro_rows o) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!cnt[i]) continue;
+        const RowEnt re = rs.ent[ent[i]];
+        unsigned long long k = incl[i] - cnt[i];
+        const int64_t L = (re.bits[0] & 1ULL) ? rs.heap[re.heap].cv : 1;
+        for (int w = 0; w < 2; w++)
+            for (uint64_t b = re.bits[w]; b; b &= b - 1) {
+                const uint32_t c = 64 * w + (uint32_t)__ffsll((unsigned long long)b) - 1;
+                export_rec(rs, o, k++, re.heap + c, L);
+            }
+    }
 }
 
 // dense copy of the state's clock records (64-B Recs with cl = the row's causal length, pos = the

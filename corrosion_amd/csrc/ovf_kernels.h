@@ -455,6 +455,10 @@ __device__ inline void ovf_publish(const MergeArgs &a, const OvfDev &d, uint32_t
                                    const uint64_t bits[2], uint32_t cnt, bool general) {
     a.rs.ent[e].bits[0] = bits[0];
     a.rs.ent[e].bits[1] = bits[1];
+    if (a.touch) {
+        const uint32_t own = d.rowner[row];
+        touch_append(a, d.pk[own], d.tc[own] >> 16);
+    }
     atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)cnt);
     if (general) a.rs.gen[a.ovf_list[d.rb[row]]] = 1;
 }

@@ -254,6 +254,34 @@ class MergeEngine:
         rows["long_values"] = self.long_values(rows)
         return rows
 
+    def track_touched(self, on=True):
+        """List the rows every apply addresses, for export_touched (corro_ctx_track_touched)."""
+        L.check(L.lib().corro_ctx_track_touched(self._h, 1 if on else 0))
+
+    def export_touched(self):
+        """The complete current clock rows of every row addressed since the previous call
+        (corro_state_export_touched): a dict of numpy arrays like export(), rows of one (table, pk)
+        contiguous. A host persisting the state replaces each exported row's clock rows with these."""
+        lib = L.lib()
+        w = C.c_uint64()
+        empty = L.Rows()
+        rc = lib.corro_state_export_touched(self._h, C.byref(empty), 0, C.byref(w))
+        if rc not in (0, -6):
+            L.check(rc)
+        m = int(w.value)
+        out = {k: np.zeros(max(m, 1), dt) for k, dt in ROW_FIELDS.items()}
+        if m:
+            r = L.Rows()
+            for k, a in out.items():
+                setattr(r, k, a.ctypes.data)
+            L.check(lib.corro_state_export_touched(self._h, C.byref(r), m, C.byref(w)))
+        rows = {k: a[: w.value] for k, a in out.items()}
+        rows["long_values"] = self.long_values(rows)
+        return rows
+
+    def set_store_limit(self, max_heap_records):
+        L.check(L.lib().corro_ctx_set_store_limit(self._h, int(max_heap_records)))
+
     def value_bytes(self, handles):
         """Bytes of long values by their handles (the val1 of rows with val_len == VAL_LONG)."""
         h = np.ascontiguousarray(handles, dtype=np.uint64)
@@ -372,30 +400,47 @@ class MergeEngine:
         return out
 
     # ---- wire decode ------------------------------------------------------------------------
-    def decode_frames(self, buf, payload=0):
+    def decode_frames(self, buf, payload=0, device=False):
         """Decode length-delimited speedy frames (corro_decode_frames; payload 0 = SyncMessage,
         1 = UniPayload) on the GPU. Returns {"cs": ctypes array of corro_changeset (one per
-        frame), "status": int32[], "changes": SoA dict (host numpy), "set_start"/"set_end"}."""
+        frame), "status": int32[], "changes": SoA dict, "set_start"/"set_end"}: host numpy arrays,
+        or with device=True CUDA tensors that stay on the GPU (the batch
+        corro_process_multiple_changes / corro_apply_batch take with CORRO_MEM_DEVICE)."""
         lib = L.lib()
         buf = bytes(buf)
         d = L.Decoded()
-        L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, L.CORRO_MEM_HOST, C.byref(d), 0))
+        mem = L.CORRO_MEM_DEVICE if device else L.CORRO_MEM_HOST
+        L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, mem, C.byref(d), 0))
         F, NC, NS = d.nframes, d.nchanges, d.nsets
         cs = (L.Changeset * max(F, 1))()
         actors = (C.c_uint8 * max(16 * F, 16))()
         status = np.zeros(max(F, 1), np.int32)
-        ch = {k: np.zeros(max(NC, 1), dt) for k, dt in BATCH_FIELDS.items()}
-        ss, se = np.zeros(max(NS, 1), np.uint64), np.zeros(max(NS, 1), np.uint64)
+        if device:
+            import torch
+            tdt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}
+            ch = {k: torch.zeros(max(NC, 1), dtype=tdt[dt], device="cuda") for k, dt in BATCH_FIELDS.items()}
+            ss = torch.zeros(max(NS, 1), dtype=torch.int64, device="cuda")
+            se = torch.zeros(max(NS, 1), dtype=torch.int64, device="cuda")
+            vdata = torch.zeros(max(len(buf), 1), dtype=torch.uint8, device="cuda")
+            ptr = lambda a: a.data_ptr()  # noqa: E731
+            torch.cuda.current_stream().synchronize()
+        else:
+            ch = {k: np.zeros(max(NC, 1), dt) for k, dt in BATCH_FIELDS.items()}
+            ss, se = np.zeros(max(NS, 1), np.uint64), np.zeros(max(NS, 1), np.uint64)
+            vdata = None
+            ptr = lambda a: a.ctypes.data  # noqa: E731
         d.cs, d.actor_ids, d.status = C.addressof(cs), C.addressof(actors), status.ctypes.data
         d.changes.n = NC
         for k, a in ch.items():
-            setattr(d.changes, k, a.ctypes.data)
-        d.set_start, d.set_end = ss.ctypes.data, se.ctypes.data
+            setattr(d.changes, k, ptr(a))
+        if device:
+            d.changes.val_data, d.changes.val_data_len = vdata.data_ptr(), len(buf)
+        d.set_start, d.set_end = ptr(ss), ptr(se)
         if F:
-            L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, L.CORRO_MEM_HOST, C.byref(d), 1))
+            L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, mem, C.byref(d), 1))
         changes = {k: a[:NC] for k, a in ch.items()}
         if d.changes.val_data:  # long values: offsets into the frame bytes
-            changes["val_data"] = np.frombuffer(buf, np.uint8)
+            changes["val_data"] = vdata[:len(buf)] if device else np.frombuffer(buf, np.uint8)
         else:
             for k in LONG_FIELDS:
                 changes.pop(k)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define CORRO_HIP_ABI_VERSION 2
+#define CORRO_HIP_ABI_VERSION 3
 
 typedef enum {
     CORRO_OK = 0,
@@ -202,8 +202,33 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
 int corro_state_count(corro_ctx *ctx, uint64_t *count);
 /* Copy the state out in crsql_changes form, unspecified row order; `cap` = capacity of `out`. */
 int corro_state_export(corro_ctx *ctx, corro_rows *out, uint64_t cap, uint64_t *written);
-/* Drop all merged state (keeps schema, sites and crsql_db_versions). */
+/* Drop all merged state (keeps schema, sites and crsql_db_versions). Also clears a poisoned context. */
 int corro_state_reset(corro_ctx *ctx);
+
+/* Failure atomicity. A failing corro_apply_batch (or corro_process_multiple_changes) that fails
+ * BEFORE its first merge write -- validation, unknown names, affinity, arena or scratch allocation --
+ * leaves the state exactly as it was. One that fails after the merge began writing (a resource limit
+ * hit while growing the row store, a device error, a later chunk of a chunked batch) cannot be undone
+ * in place: the context is then POISONED and every later apply / export / extraction call fails with
+ * CORRO_E_DEVICE until corro_state_reset, after which the caller re-seeds the state from its durable
+ * store (the SQLite tables it persists with corro_state_export_touched). */
+
+/* Per-apply delta for persistence (the writes each reference INSERT INTO crsql_changes makes to the
+ * base table and clock table inside the caller's transaction, util.rs:749-758, :1225-1245). With
+ * tracking on, the merge bodies list every row an apply addresses; corro_state_export_touched returns,
+ * for every row listed since the previous successful call (or reset), the row's COMPLETE current clock
+ * set in crsql_changes form (sentinel first, then cells by cid; rows contiguous, each row once). A
+ * host replaces each exported (table, pk)'s clock rows with these (DELETE ... WHERE key = pk, then
+ * INSERT) in the transaction that commits the apply: a delete drops cells, so the replacement set is
+ * authoritative, and an addressed row whose clocks did not change is rewritten unchanged. The cost
+ * scales with the rows addressed, not the state. cap < rows: CORRO_E_RANGE with *written = the row
+ * count, the list kept for a retry. Long values: val1 handles as in corro_state_export. */
+int corro_ctx_track_touched(corro_ctx *ctx, int on);
+int corro_state_export_touched(corro_ctx *ctx, corro_rows *out, uint64_t cap, uint64_t *written);
+
+/* Upper bound of the row store's heap in clock records (0 = none, the default): growth past it fails
+ * with CORRO_E_NOMEM (a device-memory budget per context). */
+int corro_ctx_set_store_limit(corro_ctx *ctx, uint64_t max_heap_records);
 /* crsql_db_versions: per-site max db_version over every merged change, -1 = never seen. */
 int corro_db_versions(corro_ctx *ctx, int64_t *out, uint32_t nsites);
 /* Bytes of long values named by value handles (the val1 of exported / extracted rows whose val_len
@@ -444,10 +469,17 @@ void corro_bookie_free(corro_bookie *b);
  * order: dedup passes against the bookie, actors in ActorId byte order, empty versions to
  * crsql_set_db_version, incomplete versions buffered, ONE corro_apply_batch for all complete
  * versions, impactful changes with the transaction-cumulative crsql_rows_impacted() semantics,
- * then per-actor gap bookkeeping and partial tracking. `in` holds every change (host arrays);
- * unresolved names carry table_cid = CORRO_TCID_UNKNOWN. */
+ * then per-actor gap bookkeeping and partial tracking. `cs` (headers, host memory) names each
+ * changeset's changes in `in`; cs[i].site must be the registered ordinal of cs[i].actor_id.
+ * `mem` says where `in`'s arrays (val_data included) and out->impactful live: with
+ * CORRO_MEM_DEVICE (e.g. corro_decode_frames' device output) no change crosses PCIe -- the
+ * unknown-name screen, the applied batch (zero-copy when the applied changesets are one contiguous
+ * run of `in`, else one gather kernel) and the impactful flags are device passes, and the host walks
+ * only the headers (actors in parallel host threads). With CORRO_MEM_HOST the arrays are copied to
+ * the device once. Unresolved names carry table_cid = CORRO_TCID_UNKNOWN. out->impactful, if set, has
+ * in->n entries (0 for changes that were not applied). */
 int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
-                                   const corro_changes *in, corro_process_out *out);
+                                   const corro_changes *in, int mem, corro_process_out *out);
 /* (actor, version) pairs whose buffered seqs are complete; cap < count = sizing call */
 int corro_bookie_take_ready(corro_bookie *bk, uint8_t *actors, uint64_t *versions, uint64_t cap, uint64_t *count);
 /* process_fully_buffered_changes (util.rs:541-688) */

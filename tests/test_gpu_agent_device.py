@@ -1,0 +1,209 @@
+"""process_multiple_changes end to end against the CPU restatement (oracle/agent.py, util.rs:691-1037
+over the pinned merge fold), with the change batch in device memory (CORRO_MEM_DEVICE: the
+drop-in path corro_decode_frames feeds) and in host memory.
+
+Random calls mix, from several actors arriving interleaved: complete versions (conflicting cells,
+deletes / resurrects), versions re-sent inside a call and across calls, empty versions, partial
+versions completed later, versions arriving with gaps that are filled later, and versions naming
+an unknown column (rolled back alone). Checked per call: known outcomes and impactful flags; at the
+end: the merged state, crsql_db_versions and every actor's gap bookkeeping. Also: the applied batch
+built zero-copy (one contiguous run) and by the gather kernel give the same result.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = {"t": ["a", "b", "c", "d"], "u": ["x", "y"]}
+NACT = 5
+
+
+def _calls(seed, ncalls=6, per_call=40):
+    from oracle.agent import Changeset, UNKNOWN
+    rng = np.random.default_rng(seed)
+    import synth
+    ids = synth.site_ids(NACT, seed)
+    rng.shuffle(ids)                                   # ordinal order != ActorId order
+    nextv = [1] * NACT
+    sent, held = [], []                                # earlier changesets; second halves of partials
+    cl_of = {}                                         # (table, pk) -> causal length the actors agree on
+
+    def rows(a, version, k):
+        out = []
+        for s in range(k):
+            t = int(rng.integers(0, 2))
+            ncols = 4 if t == 0 else 2
+            pk = int(rng.integers(1, 12))
+            cl = cl_of.get((t, pk), 1)
+            r = rng.random()
+            if r < 0.08:                               # delete
+                cl = cl + 1 if cl % 2 else cl
+                cl_of[(t, pk)] = cl
+                out.append(dict(pk=pk, table_cid=t << 16, col_version=cl, db_version=version, cl=cl, seq=s,
+                                site=a, val0=0, val_type=5))
+                continue
+            if r < 0.14 or cl % 2 == 0:                # pk-only resurrect / insert
+                cl = cl + 1 if cl % 2 == 0 else cl
+                cl_of[(t, pk)] = cl
+                out.append(dict(pk=pk, table_cid=t << 16, col_version=cl, db_version=version, cl=cl, seq=s,
+                                site=a, val0=0, val_type=5))
+                continue
+            out.append(dict(pk=pk, table_cid=(t << 16) | int(rng.integers(1, ncols + 1)),
+                            col_version=int(rng.integers(1, 4)), db_version=version, cl=cl, seq=s, site=a,
+                            val0=int(rng.integers(0, 5)), val_type=1))
+        return out
+
+    calls = []
+    for _c in range(ncalls):
+        call = list(held)
+        held = []
+        for _k in range(per_call):
+            a = int(rng.integers(0, NACT))
+            r = rng.random()
+            if r < 0.12 and sent:                      # re-sent (same call or an earlier one)
+                call.append(sent[int(rng.integers(0, len(sent)))])
+                continue
+            if rng.random() < 0.1:
+                nextv[a] += int(rng.integers(1, 3))    # leave a gap (never filled: stays needed)
+            v = nextv[a]
+            nextv[a] += 1
+            if r < 0.2:
+                n = int(rng.integers(1, 3))
+                cs = Changeset(ids[a], "empty", versions=(v, v + n - 1))
+                nextv[a] += n - 1
+            else:
+                k = int(rng.integers(1, 9))
+                rr = rows(a, v, k)
+                ts = int(rng.integers(1, 1 << 40))
+                if r < 0.26:                           # an unknown column in the version
+                    rr[int(rng.integers(0, k))]["table_cid"] = UNKNOWN
+                if r > 0.9 and k >= 2:                 # partial: first half now, rest next call
+                    h = k // 2
+                    cs = Changeset(ids[a], "full", version=v, seqs=(0, h - 1), last_seq=k - 1, ts=ts, rows=rr[:h])
+                    held.append(Changeset(ids[a], "full", version=v, seqs=(h, k - 1), last_seq=k - 1, ts=ts,
+                                          rows=rr[h:]))
+                else:
+                    cs = Changeset(ids[a], "full", version=v, seqs=(0, k - 1), last_seq=k - 1, ts=ts, rows=rr)
+            call.append(cs)
+            sent.append(cs)
+        calls.append(call)
+    if held:
+        calls.append(held)
+    return ids, calls
+
+
+FIELDS = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64, "db_version": np.int64,
+          "cl": np.uint32, "seq": np.uint32, "site": np.uint32, "val0": np.uint64, "val_type": np.uint8,
+          "ts": np.uint64}
+
+
+def _run(eng, bk, ordinal, call, device, order=None):
+    """corro_process_multiple_changes on one call; the batch laid out in `order` of the changesets
+    (default: arrival order). Returns (known list, impactful per changeset)."""
+    import torch
+    from corrosion_amd import _lib as L
+    order = list(range(len(call))) if order is None else order
+    off, rows = {}, []
+    for i in order:
+        off[i] = len(rows)
+        rows.extend(dict(r, ts=call[i].ts) for r in call[i].rows)
+    n = len(rows)
+    arr = {k: np.array([r[k] for r in rows] or [0], dt) for k, dt in FIELDS.items()}
+    keep = []
+    s = L.Changes()
+    s.n = n
+    for k, a in arr.items():
+        if device:
+            t = torch.from_numpy(a.view({8: np.int64, 4: np.int32, 1: np.uint8}[a.itemsize])).cuda()
+            keep.append(t)
+            setattr(s, k, t.data_ptr())
+        else:
+            keep.append(a)
+            setattr(s, k, a.ctypes.data)
+    descs = (L.Changeset * max(1, len(call)))()
+    abufs = []
+    for i, c in enumerate(call):
+        d = descs[i]
+        ab = C.create_string_buffer(bytes(c.actor), 16)
+        abufs.append(ab)
+        d.actor_id = C.addressof(ab)
+        d.site = ordinal[bytes(c.actor)]
+        d.ts = c.ts
+        if c.kind == "full":
+            d.kind = L.CORRO_CS_FULL
+            d.version_start = d.version_end = c.version
+            d.seq_start, d.seq_end = c.seqs
+            d.last_seq = c.last_seq
+            d.change_off, d.change_count = off[i], len(c.rows)
+        else:
+            d.kind = L.CORRO_CS_EMPTY
+            d.version_start, d.version_end = c.versions
+    known = np.zeros(max(1, len(call)), np.int32)
+    if device:
+        imp = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+        ip = imp.data_ptr()
+        torch.cuda.synchronize()
+    else:
+        imp = np.zeros(max(n, 1), np.uint8)
+        ip = imp.ctypes.data
+    out = L.ProcessOut()
+    out.known, out.impactful = known.ctypes.data, ip
+    L.check(L.lib().corro_process_multiple_changes(eng._h, bk._h, descs, len(call), C.byref(s),
+                                                   L.CORRO_MEM_DEVICE if device else L.CORRO_MEM_HOST, C.byref(out)))
+    imp = imp.cpu().numpy() if device else imp
+    kn = [L.KNOWN.get(int(k), int(k)) for k in known[:len(call)]]
+    return kn, [list(imp[off[i]:off[i] + len(c.rows)]) if c.kind == "full" else [] for i, c in enumerate(call)]
+
+
+def canon_rows(rows):
+    keys = ("table_cid", "pk", "val_type", "val0", "col_version", "db_version", "site", "cl", "seq", "ts")
+    return sorted(zip(*[np.asarray(rows[k]).tolist() for k in keys]))
+
+
+def _check_against_oracle(seed, device, order_fn=None):
+    import corrosion_amd as ca
+    from oracle.agent import AgentOracle
+    ids, calls = _calls(seed)
+    eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12)
+    ords = eng.register_sites(ids)
+    ordinal = {bytes(ids[k]): int(ords[k]) for k in range(NACT)}
+    bk = ca.agent.Bookie()
+    ref = AgentOracle(ids)
+    for call in calls:
+        for c in call:                       # oracle rows name sites by ordinal too
+            for r in c.rows:
+                r["site"] = ordinal[bytes(c.actor)]
+        order = order_fn(call) if order_fn else None
+        got_known, got_imp = _run(eng, bk, ordinal, call, device, order)
+        exp_known, exp_imp = ref.process(call)
+        assert got_known == exp_known
+        assert got_imp == exp_imp
+    assert canon_rows(eng.export()) == canon_rows(ref.export())
+    dbv = list(ref.fold.db_versions())
+    for a, v in ref.set_dbv.items():
+        o = ordinal[a]
+        dbv[o] = max(dbv[o], v)
+    assert list(eng.db_versions()) == dbv
+    for a in ordinal:
+        assert bk.last(a) == ref.last(a)
+        assert bk.needed(a) == ref.needed(a)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_device_batch_matches_restatement(seed):
+    _check_against_oracle(seed, device=True)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_host_batch_matches_restatement(seed):
+    _check_against_oracle(seed, device=False)
+
+
+def test_batch_in_application_order_zero_copy():
+    """The batch laid out in application order (actors by id, arrival order within): the applied
+    changesets are one contiguous run, so the engine merges the caller's arrays in place."""
+    def app_order(call):
+        return sorted(range(len(call)), key=lambda i: (bytes(call[i].actor), i))
+    _check_against_oracle(6, device=True, order_fn=app_order)

@@ -6,6 +6,11 @@
     the oracle's pk-sharded fold (oracle/crsql_fold.c of_apply_sharded, the sequential rules run per
     shard on the host cores): every impact flag, the crsql_changes rows through an order-independent
     digest of every output field (row count, sum and xor of per-row 64-bit hashes), crsql_db_versions;
+  * config 5: the adversarial mix at its stated 64M size (8 tables, Zipf(1.1) hot pks over 2^20 per
+    table, 30 % sentinel deletes / resurrects, mixed INTEGER / REAL / TEXT / BLOB / NULL values), two
+    64M batches folded into one state with impact flags -- the regime where ~57M records per apply
+    take the device-wide overflow fold with the row store's prior-row lookups -- against the same
+    pk-sharded oracle fold;
   * config 4: 1M node pairs x 64 sparse actors from a 100k-actor universe (64M need-diff entries),
     the device need diff against the oracle restatement (oracle/ranges.c, threaded over entry
     chunks), every output array equal.
@@ -71,6 +76,42 @@ def test_config3_512m_one_batch_vs_sharded_oracle():
 
 def test_config3_512m_eight_batch_fold_vs_sharded_oracle():
     _config3(8)
+
+
+def _dev(b):
+    import torch
+    return {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                                (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda() for k, v in b.items()}
+
+
+@pytest.mark.timeout(1200)
+def test_config5_64m_two_batch_fold_vs_sharded_oracle():
+    import torch
+    import corrosion_amd as ca
+    n = 64_000_000
+    seed = synth.config_seed(5)
+    sites = synth.site_ids(1000, seed)
+    eng = ca.MergeEngine(synth.adversarial_schema(8), capacity_hint=n, device=0)
+    eng.register_sites(sites)
+    fold = O.ShardedFold(sites, nshards=64, nthreads=16)
+    for k in range(2):
+        b = synth.adversarial_batch(n, 1000, 8, 1 << 20, seed + k)
+        d = _dev(b)
+        imp = eng.apply(d, impact=True).cpu().numpy()
+        del d
+        torch.cuda.empty_cache()
+        ref = fold.apply(b)
+        assert np.array_equal(imp, ref), f"config 5 batch {k}: impact flags differ"
+        del b, imp, ref
+    m = eng.metrics()
+    assert m["overflow_rounds"] >= 2          # the hot-row regime was exercised
+    rows = eng.export()
+    dg = O.rows_digest(rows)
+    del rows
+    assert dg == fold.digest()
+    assert np.array_equal(eng.db_versions(), fold.db_versions())
+    print(f"config 5, 2 x 64M folded: {dg[0]} clock rows bit-exact")
+    eng.close()
 
 
 def test_config4_full_size_vs_oracle():
