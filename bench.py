@@ -88,6 +88,23 @@ def cpu_baseline(batch_dev, seconds_target=15.0):
                             "sample": f"{n} changes of the config-2 distribution folded sequentially in {dt:.2f} s"}}
 
 
+def cpu_baseline_sample(npk, n=1 << 24, threads=None):
+    """The N > 1 lines' CPU baseline, bounded to a few seconds: the oracle's fold restatement (kind
+    'port') pk-sharded over the host threads on a 16M-change sample of the line's distribution."""
+    from oracle import oracle as O
+    import synth
+    sites = synth.site_ids(N_ACTORS, 1)
+    threads = threads or max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS") or 16)))
+    b = synth.uniform_batch(n, N_ACTORS, npk, N_COLS, 11 + n)
+    g = O.ShardedFold(sites, nshards=4 * threads, nthreads=threads)
+    t0 = time.perf_counter()
+    g.apply(b, impact=False)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "merged column-changes/s", "cores": threads, "kind": "port",
+            "sample": f"{n} changes of the line's distribution (pk space {npk}) folded by oracle/crsql_fold.c "
+                      f"of_apply_sharded ({4 * threads} pk-hash shards, {threads} threads) in {dt:.2f} s"}
+
+
 # ------------------------------------------------------------------------------------- PMC traffic
 def _ours(kernel_name):
     """Kernels of the apply pipeline (the library's own and the rocPRIM sorts it launches), not the
@@ -514,7 +531,22 @@ def run_multi(args, world, rank):
     stats = torch.tensor([dt, dt_own, sum(ex_ms) / max(1, len(ex_ms))], device=sdev, dtype=torch.float64)
     dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     dt, dt_own, exm = (float(x) for x in stats.tolist())
+    cells_t = torch.tensor([eng.count()], device=sdev, dtype=torch.int64)
+    dist.all_reduce(cells_t, op=dist.ReduceOp.SUM)
+    cells = int(cells_t.item())
     if rank == 0:
+        # roofline of the whole step over the node: the SURVEY §8(d) algorithmic bytes of the merge
+        # (48 B per change + 48 B per output cell) plus the exchange's 48 B x (N-1)/N per change
+        # (strong mode: the packed records that leave their rank), against N x the HBM peak
+        moved = ALG_BYTES_PER_CHANGE * G * (world - 1) / world
+        alg = ALG_BYTES_PER_CHANGE * G + ALG_BYTES_PER_CELL * cells + moved
+        achieved = alg / (dt / args.steps) / 1e9
+        roof = {"bound": "hbm", "kernel": "step: partition + all-to-all-v + unpack + merge, all ranks",
+                "achieved": achieved, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                "frac": achieved / (HBM_PEAK_GBS * world), "traffic": None,
+                "traffic_source": "not measured at N > 1 (the N = 1 line carries the PMC passes)",
+                "alg_bytes_per_step": alg, "exchange_bytes_per_step": moved, "cells": cells}
+        cpu = None if args.no_cpu_baseline else cpu_baseline_sample(npk)
         line = {
             "metric": METRIC,
             "value": G / dt * args.steps,
@@ -535,6 +567,8 @@ def run_multi(args, world, rank):
                                     "all-to-all-v + merge"),
                        "total_changes": G, "changes_per_gpu": n_local,
                        "parallelism": f"pk-hash x{world}, {backend} all-to-all"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
             "exchange_ms": exm,
             "owner_routed": {"value": G / dt_own * args.steps, "ms_per_step": dt_own / args.steps * 1e3,
                              "note": "each rank merges only its own rows (the received batch), no collective"},

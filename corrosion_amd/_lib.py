@@ -38,7 +38,7 @@ EXPORTS = [
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
     "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity",
     "corro_ctx_metrics", "corro_table_committed", "corro_ctx_track_touched", "corro_state_export_touched",
-    "corro_ctx_set_store_limit",
+    "corro_ctx_set_store_limit", "corro_partition_var", "corro_unpack_var",
 ]
 
 CORRO_CS_FULL, CORRO_CS_EMPTY, CORRO_CS_EMPTY_SET = 0, 1, 2
@@ -228,6 +228,8 @@ def lib():
         "corro_packed_record_bytes": (i32, [C.POINTER(Changes), vp]),
         "corro_partition_packed": (i32, [vp, C.POINTER(Changes), u32, vp, vp, vp]),
         "corro_unpack_records": (i32, [vp, vp, u64, u32, C.POINTER(Changes)]),
+        "corro_partition_var": (i32, [vp, C.POINTER(Changes), u32, vp, vp, vp, vp, u64, vp]),
+        "corro_unpack_var": (i32, [vp, vp, u64, vp, u64, vp, vp, u32, C.POINTER(Changes)]),
         "corro_table_set_pk_interned": (i32, [vp, u32, i32]),
         "corro_pk_keys": (i32, [vp, u32, vp, vp, u64, vp]),
         "corro_pk_bytes": (i32, [vp, u32, vp, u64, vp, u64, vp]),

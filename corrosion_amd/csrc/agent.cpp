@@ -73,6 +73,7 @@ struct corro_bookie {
     std::map<std::pair<uint32_t, uint64_t>, SeqBook> seqbook;  // (site, version)
     std::vector<std::pair<ActorId, uint64_t>> ready;           // fully buffered, to apply
     std::map<ActorId, uint32_t> site_of;                       // actor -> site ordinal
+    std::vector<uint64_t> scratch_ver;                          // process_multiple_changes scratch
 };
 
 namespace {
@@ -346,10 +347,21 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     std::vector<std::vector<SiteStat>> cstat(nchunk);
     std::vector<int> cerr(nchunk, CORRO_OK);
     std::vector<uint64_t> cfull(nchunk, 0);
+    std::vector<uint8_t> chunk_ts(nchunk, 0);
+    const bool in_ts = in && in->ts;
+    // compact per-changeset copy of what the later host pass reads (8 B instead of the 80-B header);
+    // kept by the bookie between calls (no fresh pages to fault in per call)
+    if (bk->scratch_ver.size() < ncs) bk->scratch_ver.resize(ncs);
+    uint64_t *ver = bk->scratch_ver.data();
     // 1. headers: spans checked, staged for the device, actors checked against the registered ids
     run_parallel(nchunk, [&](size_t k) {
         uint64_t lo, hi;
         chunk_of(k, lo, hi);
+        bool cts = false;
+        struct Flush {
+            std::vector<uint8_t> &v; size_t k; bool &b;
+            ~Flush() { v[k] = b; }
+        } flush{chunk_ts, k, cts};
         std::vector<SiteStat> &st = cstat[k];
         st.assign(nsites, SiteStat{});
         const uint8_t *last_ptr = nullptr;
@@ -376,9 +388,11 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
             }
             P.off[i] = full ? c.change_off : 0;
             P.cnt[i] = full ? c.change_count : 0;
-            P.ts[i] = c.ts;
+            if (!in_ts) P.ts[i] = c.ts;  // (per-change ts in the input: the span ts is never read)
             P.site[i] = c.site;
             P.flag[i] = 0;
+            ver[i] = c.version_start;
+            cts |= c.ts != 0;
             cfull[k] += full;
             SiteStat &t = st[c.site];
             const bool fast = c.kind == CORRO_CS_FULL && is_complete(c) && (!t.count || c.version_start > t.last);
@@ -504,14 +518,15 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
         ChunkOut &o = cout[k];
         std::vector<int64_t> open(work.size(), -1);  // index into o.runs of the actor's open run
         for (uint64_t i = lo; i < hi; i++) {
-            const corro_changeset &c = cs[i];
-            const uint32_t wi = (uint32_t)work_of[c.site];
+            const uint32_t wi = (uint32_t)work_of[P.site[i]];
             const ActorWork &w = work[wi];
             if (!w.fast) continue;
-            const uint64_t v = c.version_start;
-            Range sq{c.seq_start, c.seq_end};
-            if (w.had_max && v <= w.max && w.booked->contains_all(v, v, &sq)) continue;
-            if (c.change_count == 0) {
+            const uint64_t v = ver[i];
+            if (w.had_max && v <= w.max) {
+                Range sq{cs[i].seq_start, cs[i].seq_end};
+                if (w.booked->contains_all(v, v, &sq)) continue;
+            }
+            if (P.cnt[i] == 0) {  // (a fast actor's changesets are all Full: cnt 0 = no changes)
                 if (!w.had_max || v > w.max) o.set_dbv.emplace_back(wi, v);
                 out->known[i] = CORRO_KNOWN_CLEARED;
             } else if (bad[i]) {
@@ -521,8 +536,7 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
                 P.flag[i] = 1;
                 out->known[i] = CORRO_KNOWN_CURRENT;
                 o.nspans++;
-                o.nb += c.change_count;
-                o.ts |= c.ts != 0;
+                o.nb += P.cnt[i];
             }
             int64_t &r = open[wi];
             if (r >= 0 && o.runs[(size_t)r].second.second + 1 == v) {
@@ -623,10 +637,10 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);
     uint64_t nspans = 0, nb = 0;
     bool need_ts = false;
-    for (const ChunkOut &o : cout) {
-        nspans += o.nspans;
-        nb += o.nb;
-        need_ts |= o.ts;
+    for (size_t k = 0; k < nchunk; k++) {
+        nspans += cout[k].nspans;
+        nb += cout[k].nb;
+        need_ts |= chunk_ts[k] != 0;  // (any changeset's ts: a superset of the applied ones')
     }
     for (const ActorWork &w : work) {
         nspans += w.nspans;

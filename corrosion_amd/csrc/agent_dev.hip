@@ -455,7 +455,7 @@ int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &
     const DevCols c = dev_cols(ctx);
     if (nspans) {
         // off / cnt are on the device already (the screen); the rest of the changeset columns once
-        CORRO_HIP_TRY(hipMemcpyAsync(c.ts, p.ts, ncs * 8, hipMemcpyHostToDevice, s));
+        if (!dv->ts) CORRO_HIP_TRY(hipMemcpyAsync(c.ts, p.ts, ncs * 8, hipMemcpyHostToDevice, s));
         CORRO_HIP_TRY(hipMemcpyAsync(c.site, p.site, ncs * 4, hipMemcpyHostToDevice, s));
         CORRO_HIP_TRY(hipMemcpyAsync(c.flag, p.flag, ncs, hipMemcpyHostToDevice, s));
         uint32_t bits = 1;

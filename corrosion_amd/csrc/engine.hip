@@ -70,7 +70,7 @@ int ovf_scan_tiles(void *temp, size_t *temp_bytes, const OvfDev &d, const CsAgg 
 int grow_regions(corro_ctx *ctx, uint32_t new_log2S);
 int grow_heap(corro_ctx *ctx, uint64_t want_records);
 RowStore row_store(corro_ctx *ctx);
-int affinity_check(corro_ctx *ctx, const BatchDev &bd);  // affinity.hip
+int affinity_convert(corro_ctx *ctx, BatchDev &bd);  // affinity.hip
 
 // Oversized buckets (queued by a merge round), all at once and device-wide (the phases of
 // ovf_kernels.h): batch fields + row ids -> region lookups (prior records appended, new rows
@@ -367,7 +367,7 @@ RowStore row_store(corro_ctx *ctx) {
 
 // Room for `add` more bytes in the value arena (contents kept: handles are offsets into it).
 static constexpr uint64_t ARENA_MAX = 1ULL << 40;  // a value handle holds a 40-bit offset
-static int arena_reserve(corro_ctx *ctx, uint64_t add) {
+int arena_reserve(corro_ctx *ctx, uint64_t add) {
     const uint64_t need = ctx->arena_top + add;
     if (need > ARENA_MAX) return fail(CORRO_E_RANGE, "value arena would exceed 2^40 bytes");
     if (need <= ctx->d_arena.bytes && ctx->d_arena.p) return CORRO_OK;
@@ -535,6 +535,13 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_agent_in, &ctx->d_agent_batch, &ctx->d_agent_spans, &ctx->d_agent_imp,
                       &ctx->d_agent_out, &ctx->d_agent_aux, &ctx->d_agent_fetch, &ctx->d_agent_aux2, &ctx->d_touch, &ctx->d_touch_n, &ctx->d_touch_stamp, &ctx->d_touch_tmp};
     for (DevBuf *b : bufs) b->release();
+    ctx->d_pkdir.release();
+    ctx->d_part_var.release();
+    for (PkTable &t : ctx->pk) {
+        t.d_off.release();
+        t.d_bytes.release();
+        t.d_hash.release();
+    }
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     if (ctx->h_agent) (void)hipHostFree(ctx->h_agent);
     for (auto &e : ctx->ev)
@@ -728,7 +735,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     mark(3);
     {
         static const bool nt_stores = std::getenv("CORRO_HIP_NT") && std::atoi(std::getenv("CORRO_HIP_NT")) != 0;
-        const bool plain = !bd.v1 && !bd.vt && !bd.vl;
+        const bool plain = !bd.v1 && !bd.vt && !bd.vl && !bd.conv;
         auto kern = plain ? (nt_stores ? k_scatter<true, true> : k_scatter<true, false>)
                           : (nt_stores ? k_scatter<false, true> : k_scatter<false, false>);
         hipLaunchKernelGGL(kern, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4 + ((B + 31) / 32) * 4, s, bd,
@@ -766,6 +773,10 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     a.arena = ctx->d_arena.as<uint8_t>();
     a.touch = ctx->track_touched ? ctx->d_touch.as<uint4>() : nullptr;
     a.touch_n = ctx->track_touched ? ctx->d_touch_n.as<unsigned long long>() : nullptr;
+    if (bd.conv) {  // converted values: incoming changes compare by their raw values
+        a.raw = bd;
+        a.raw.arena = ctx->d_arena.as<uint8_t>();
+    }
     uint32_t nblocks = B;
     float merge_ms = 0.f, ovf_ms = 0.f;
     for (int round = 0;; round++) {
@@ -994,7 +1005,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
     if (out && out->impact && !imp_dev) TRY(ctx->d_impact.ensure(n));
     uint8_t *imp_buf = !(out && out->impact) ? nullptr : (imp_dev ? out->impact : ctx->d_impact.as<uint8_t>());
 
-    TRY(affinity_check(ctx, bd));
+    TRY(affinity_convert(ctx, bd));
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
     const uint64_t chunk = chunk_changes(ctx);
     if (n > chunk) {
@@ -1016,6 +1027,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         };
         adv(c.pk), adv(c.tcid), adv(c.cv), adv(c.dbv), adv(c.cl), adv(c.seq), adv(c.site), adv(c.v0), adv(c.v1);
         adv(c.vt), adv(c.vl), adv(c.ts), adv(c.voff), adv(c.vsz);
+        adv(c.conv), adv(c.cv0), adv(c.cv1), adv(c.cmeta);
         c.n = m;
         TRY(apply_chunk(ctx, c, imp_buf ? imp_buf + off : nullptr));
         for (int k = 0; k < 6; k++) ms[k] += ctx->last_ms[k];

@@ -82,7 +82,24 @@ struct PkTable {
     bool interned = false;
     std::unordered_map<std::string, uint64_t> ids;
     std::vector<std::string> keys;
+    std::vector<uint64_t> hash;   // pk_route_hash of each key (the owner rank on every engine)
+    uint64_t max_len = 0;         // longest canonical key
+    // device mirror (pk_mirror_sync): canonical bytes, offsets (n + 1), route hashes of ids [0, dev_n)
+    DevBuf d_off, d_bytes, d_hash;
+    uint64_t dev_n = 0, dev_bytes = 0;
 };
+// Device view of one table's interned keys (partition.hip routes and ships interned pks by them).
+struct PkDir {
+    const uint64_t *off;
+    const uint8_t *bytes;
+    const uint64_t *hash;
+    uint64_t n;
+    uint32_t interned;
+    uint32_t pad;
+};
+uint64_t pk_route_hash(const std::string &canon);
+// Bring every interned table's device mirror up to date and upload the directory (ctx->d_pkdir).
+int pk_mirror_sync(corro_ctx *ctx);
 bool pk_canonical(const uint8_t *p, uint64_t len, std::string &out, bool *single_int, int64_t *ival);
 std::string pack_int_pk(int64_t v);
 
@@ -174,8 +191,11 @@ struct corro_ctx {
     corro::DevBuf d_ncols;        // u16 column count per table
     std::vector<uint8_t> aff;     // column affinity per (table, cid), (MAX_COLS + 1) per table
     corro::DevBuf d_aff, d_affflag;
+    corro::DevBuf d_aff_conv, d_aff_vals;  // per change of a batch: converted flag; cv0 | cv1 | cmeta
     bool aff_any = false;         // some column has an affinity other than BLOB
     corro::DevBuf d_part;         // partition counts
+    corro::DevBuf d_pkdir;        // PkDir per table (pk_mirror_sync)
+    corro::DevBuf d_part_var;     // partition_var scratch: per-record var lengths / offsets, perm
     // process_multiple_changes on the device (agent_dev.hip): staged host input, gathered batch,
     // span tables, impact flags, impactful output, and a pinned host staging area
     corro::DevBuf d_agent_in, d_agent_batch, d_agent_spans, d_agent_imp, d_agent_out, d_agent_aux;

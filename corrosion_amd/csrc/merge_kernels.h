@@ -72,6 +72,9 @@ struct MergeArgs {
     const uint8_t *arena;      // bytes of long TEXT/BLOB values (value handles point into it)
     uint4 *touch;              // rows the apply addressed, (pk lo, pk hi, table, 0) each (null: not tracked)
     unsigned long long *touch_n;
+    // column affinity: the batch's raw values (raw.conv[i] = 1: change i was staged with its
+    // converted value; an incoming change still compares by its raw one, App. A.4). conv null: none.
+    BatchDev raw;
 };
 
 // misc words
@@ -501,15 +504,23 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
             Rec &r = rr[u];
             uint32_t idx = 0;
             if (act) {
+                // a value its column's affinity converts is staged converted (affinity.hip); its
+                // bucket takes the general body, which compares it raw as the incoming change
+                const bool cvt = !PLAIN && in.conv && in.conv[i];
+                if (cvt) {
+                    r.v0 = in.cv0[i];
+                    r.v1 = in.cv1[i];
+                    r.meta = in.cmeta[i];
+                }
                 const uint32_t ty = vtype(r.meta), ln = vlen(r.meta);
                 const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
                 const uint32_t b = bucket_of(one_table ? 0u : t, r.pk, log2B);
                 idx = atomicAdd(&cur[b], 1u);
                 // long values: words from the arena; their buckets take the general body
-                const bool lv = !PLAIN && (ty == CORRO_TEXT || ty == CORRO_BLOB) && ln == VLEN_LONG;
+                const bool lv = !PLAIN && !cvt && (ty == CORRO_TEXT || ty == CORRO_BLOB) && ln == VLEN_LONG;
                 if (lv && !long_value(in, i, r.v0, r.v1)) err |= ERR_VALUE;
                 // (the fast bodies keep a row's presence bits in one word: cids 1..63)
-                if (r.cl != 1u || cid == 0 || cid >= 64 || lv) atomicOr(&fl[b >> 5], 1u << (b & 31));
+                if (r.cl != 1u || cid == 0 || cid >= 64 || lv || cvt) atomicOr(&fl[b >> 5], 1u << (b & 31));
                 if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
                 if (r.site >= nsites) err |= ERR_SITE;
                 if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
@@ -700,6 +711,15 @@ __device__ inline void gen_set_cell(const GenArrays &g, uint32_t s, uint32_t &nc
     ncell++;
 }
 
+// the raw (unconverted) value of batch change i into r's value fields
+__device__ inline void raw_value(const BatchDev &in, uint32_t i, Rec &r) {
+    const uint32_t ty = in.vt ? in.vt[i] : (uint32_t)CORRO_INTEGER, ln = in.vl ? in.vl[i] : 0u;
+    r.meta = ty | (ln << 8);
+    r.v0 = in.v0[i];
+    r.v1 = in.v1 ? in.v1[i] : 0ULL;
+    if ((ty == CORRO_TEXT || ty == CORRO_BLOB) && ln == VLEN_LONG) (void)long_value(in, i, r.v0, r.v1);
+}
+
 // Fold one row's records (sorted positions [s, e)) through the cr-sqlite rules,
 // then hand the result to the emitter.
 template <class V, class E>
@@ -772,7 +792,8 @@ __device__ inline void gen_fold_row(const MergeArgs &a, const V &v, E &em, const
                 if (cv != lcv) {
                     win = cv > lcv;
                 } else {
-                    const Rec xr = load_rec(v.at(x));
+                    Rec xr = load_rec(v.at(x));
+                    if (a.raw.conv && a.raw.conv[pos & 0x7FFFFFFFu]) raw_value(a.raw, pos & 0x7FFFFFFFu, xr);
                     const Rec lr = load_rec(v.at(g.csrc[s + found]));
                     const int vc = value_cmp(xr, lr, a.arena);
                     if (vc != 0) win = vc > 0;

@@ -15,7 +15,15 @@
 #include "internal.h"
 #include "rowhash.h"
 
+#define TRY_PART(x)                      \
+    do {                                 \
+        int rc_ = (x);                   \
+        if (rc_ != CORRO_OK) return rc_; \
+    } while (0)
+
 namespace corro {
+int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, uint32_t *out, uint32_t n,
+                            hipStream_t s);
 
 constexpr int PART_THREADS = 256;
 constexpr int PART_MAX_RANKS = 64;
@@ -225,6 +233,151 @@ __global__ void k_unpack(const void *__restrict__ recs, uint32_t n, BatchOut o) 
     }
 }
 
+// ---- every table: interned pks routed by their canonical bytes, variable-length bytes shipped ----
+// Owner of a change: INTEGER-pk rows by rank_of (the pk is the row key on every engine); rows of an
+// interned table by the route hash of their canonical packed pk (the dense row key is per engine).
+__device__ inline uint32_t route_of(const PkDir *dir, uint32_t table, uint64_t key, uint32_t nranks) {
+    if (dir && dir[table].interned) {
+        const uint64_t h = key < dir[table].n ? dir[table].hash[key] : 0ULL;
+        return (uint32_t)(mix64(h ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(table + 1))) & 0xFFFFFFFFULL) % nranks;
+    }
+    return rank_of(table, key, nranks);
+}
+
+__global__ void __launch_bounds__(PART_THREADS)
+k_partv_count(BatchDev in, const PkDir *dir, uint32_t tile, uint32_t nranks, uint32_t *__restrict__ counts) {
+    __shared__ uint32_t c[PART_MAX_RANKS];
+    for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) c[r] = 0;
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * tile, end = min(in.n, begin + tile);
+    for (uint32_t i = begin + threadIdx.x; i < end; i += blockDim.x)
+        atomicAdd(&c[route_of(dir, in.tcid[i] >> 16, in.pk[i], nranks)], 1u);
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) counts[(size_t)blockIdx.x * nranks + r] = c[r];
+}
+
+// bytes change i ships: its canonical pk (interned table) then its long value's bytes
+__device__ inline void var_parts(const BatchDev &in, const PkDir *dir, uint32_t i, uint32_t &pk_len, uint32_t &vsz) {
+    const uint32_t t = in.tcid[i] >> 16;
+    pk_len = 0;
+    if (dir[t].interned && in.pk[i] < dir[t].n) pk_len = (uint32_t)(dir[t].off[in.pk[i] + 1] - dir[t].off[in.pk[i]]);
+    vsz = 0;
+    if (in.voff && in.vsz && in.vt && in.vl && in.vl[i] == CORRO_VAL_LONG && (in.vt[i] == CORRO_TEXT || in.vt[i] == CORRO_BLOB)) {
+        const uint64_t off = in.voff[i];
+        const uint32_t sz = in.vsz[i];
+        if (sz > 16 && sz < (1u << 24) && off <= in.ldata && sz <= in.ldata - off) vsz = sz;
+    }
+}
+
+// stable scatter of 80-B records (route_of), perm[pos] = source, vlen[pos] = bytes it ships
+__global__ void __launch_bounds__(PART_THREADS)
+k_partv_pack(BatchDev in, const PkDir *dir, uint32_t tile, uint32_t nranks, const uint32_t *__restrict__ offs,
+             PackedRec80 *__restrict__ out, uint32_t *__restrict__ perm, uint32_t *__restrict__ vlen) {
+    __shared__ uint32_t run[PART_MAX_RANKS];
+    __shared__ uint32_t wcnt[PART_THREADS / 64][PART_MAX_RANKS];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) run[r] = offs[(size_t)blockIdx.x * nranks + r];
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * tile, end = min(in.n, begin + tile);
+    const uint64_t lt = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+    for (uint32_t base = begin; base < end; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const bool act = i < end;
+        const uint32_t ic = act ? i : begin;
+        const uint64_t pk = in.pk[ic];
+        const uint32_t tc = in.tcid[ic];
+        const uint32_t d = act ? route_of(dir, tc >> 16, pk, nranks) : 0xFFFFFFFFu;
+        uint32_t my_rank = 0;
+        for (uint32_t r = 0; r < nranks; r++) {
+            const uint64_t m = __ballot(d == r);
+            if (d == r) my_rank = __popcll(m & lt);
+            if (lane == 0) wcnt[w][r] = __popcll(m);
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t pos = run[d] + my_rank;
+            for (uint32_t ww = 0; ww < w; ww++) pos += wcnt[ww][d];
+            PackedRec80 r{};
+            r.pk = pk;
+            r.cv = in.cv[i];
+            r.dbv = in.dbv[i];
+            r.v0 = in.v0[i];
+            r.v1 = in.v1 ? in.v1[i] : 0ULL;
+            r.ts = in.ts ? in.ts[i] : 0ULL;
+            r.tcid = tc;
+            r.cl = in.cl[i];
+            r.seq = in.seq[i];
+            r.site = in.site[i];
+            r.meta = (in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER) | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8);
+            uint32_t pl, vs;
+            var_parts(in, dir, i, pl, vs);
+            r.pad[1] = pl;
+            r.pad[2] = vs;
+            out[pos] = r;
+            perm[pos] = i;
+            vlen[pos] = pl + vs;
+        }
+        __syncthreads();
+        if (threadIdx.x < nranks) {
+            uint32_t add = 0;
+            for (uint32_t ww = 0; ww < PART_THREADS / 64; ww++) add += wcnt[ww][threadIdx.x];
+            run[threadIdx.x] += add;
+        }
+        __syncthreads();
+    }
+}
+
+// record pos: its bytes at var[vincl[pos] - vlen[pos]], its offset inside its rank's segment in
+// pad[0] (the receiver adds the segment's base); one wave per record copies the bytes
+__global__ void __launch_bounds__(PART_THREADS)
+k_partv_fill(BatchDev in, const PkDir *dir, uint32_t n, const uint32_t *__restrict__ perm, const uint32_t *__restrict__ vlen,
+             const uint32_t *__restrict__ vincl, const uint64_t *__restrict__ seg_base, const uint64_t *__restrict__ rec_base,
+             uint32_t nranks, PackedRec80 *__restrict__ out, uint8_t *__restrict__ var) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = gridDim.x * blockDim.x / 64;
+    for (uint32_t pos = w0; pos < n; pos += nw) {
+        const uint32_t L = vlen[pos];
+        const uint64_t at = (uint64_t)vincl[pos] - L;
+        uint32_t r = 0;  // destination rank: the last whose first record is at or before pos
+        while (r + 1 < nranks && rec_base[r + 1] <= pos) r++;
+        if (lane == 0) out[pos].pad[0] = (uint32_t)(at - seg_base[r]);
+        if (!L) continue;
+        const uint32_t i = perm[pos];
+        const uint32_t pl = out[pos].pad[1], vs = out[pos].pad[2];
+        if (pl) {
+            const uint8_t *src = dir[in.tcid[i] >> 16].bytes + dir[in.tcid[i] >> 16].off[in.pk[i]];
+            for (uint32_t k = lane; k < pl; k += 64) var[at + k] = src[k];
+        }
+        if (vs) {
+            const uint8_t *src = in.arena + in.voff[i];
+            for (uint32_t k = lane; k < vs; k += 64) var[at + pl + k] = src[k];
+        }
+    }
+}
+
+// received records (source-rank order, var segments concatenated the same way) -> SoA; long
+// values' val_off point into the received var bytes (the batch's val_data); interned records'
+// (pk bytes offset, length) listed in pkref for the host's interning
+__global__ void k_unpackv(const PackedRec80 *__restrict__ recs, uint32_t n, const uint64_t *__restrict__ src_rec,
+                          const uint64_t *__restrict__ src_var, uint32_t nsrc, BatchOut o, uint64_t *__restrict__ voff,
+                          uint32_t *__restrict__ vsz, uint64_t *__restrict__ pkref) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const PackedRec80 r = recs[i];
+        uint32_t s = 0;
+        while (s + 1 < nsrc && src_rec[s + 1] <= i) s++;
+        const uint64_t at = src_var[s] + r.pad[0];
+        o.pk[i] = r.pk; o.cv[i] = r.cv; o.dbv[i] = r.dbv; o.v0[i] = r.v0;
+        o.tcid[i] = r.tcid; o.cl[i] = r.cl; o.seq[i] = r.seq; o.site[i] = r.site;
+        if (o.v1) o.v1[i] = r.v1;
+        if (o.ts) o.ts[i] = r.ts;
+        if (o.vt) o.vt[i] = (uint8_t)(r.meta & 0xFFu);
+        if (o.vl) o.vl[i] = (uint8_t)(r.meta >> 8);
+        voff[i] = at + r.pad[1];
+        vsz[i] = r.pad[2];
+        pkref[i] = r.pad[1] ? ((at << 24) | r.pad[1]) : ~0ULL;
+    }
+}
+
 }  // namespace corro
 
 using namespace corro;
@@ -360,6 +513,143 @@ extern "C" int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n
     else
         hipLaunchKernelGGL(k_unpack<false>, dim3(grid), dim3(256), 0, s, recs, (uint32_t)n, bo);
     CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+// ---------------------------------------------------------------------- exchange for every table
+
+extern "C" int corro_partition_var(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, void *out, uint32_t *perm,
+                                   uint64_t *counts, uint8_t *var, uint64_t var_cap, uint64_t *var_counts) {
+    if (!ctx || !in || !out || !counts || !var_counts) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nranks == 0 || nranks > (uint32_t)PART_MAX_RANKS) return fail(CORRO_E_RANGE, "1..64 ranks");
+    if (in->n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
+    if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
+        !in->val0)
+        return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    if ((uintptr_t)out % 16) return fail(CORRO_E_INVALID, "packed records must be 16-byte aligned");
+    for (uint32_t r = 0; r < nranks; r++) counts[r] = var_counts[r] = 0;
+    const uint32_t n = (uint32_t)in->n;
+    if (n == 0) return CORRO_OK;
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    TRY_PART(pk_mirror_sync(ctx));
+    uint64_t max_pk = 0;
+    for (const PkTable &t : ctx->pk) max_pk = std::max<uint64_t>(max_pk, t.interned ? t.max_len : 0);
+    if (in->val_data_len + (uint64_t)n * max_pk >= (1ULL << 32))
+        return fail(CORRO_E_RANGE, "one exchange ships at most 4 GiB of pk / value bytes: split the batch");
+    BatchDev bd = batch_dev(in, n);
+    bd.voff = in->val_off;
+    bd.vsz = in->val_size;
+    bd.arena = in->val_data;  // (device bytes; lbase 0)
+    bd.lbase = 0;
+    bd.ldata = in->val_data_len;
+    const PkDir *dir = ctx->d_pkdir.as<PkDir>();
+    uint32_t ntiles, tile, *d_counts;
+    uint64_t *d_tot;
+    if (int rc = part_tiles(ctx, n, nranks, ntiles, tile, d_counts, d_tot)) return rc;
+    hipLaunchKernelGGL(k_partv_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, dir, tile, nranks, d_counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, d_tot);
+    // scratch: perm (caller's or ours), vlen, vincl, rocPRIM temp, segment / record bases
+    size_t temp = 0;
+    TRY_PART(prim_inclusive_scan_u32(nullptr, &temp, nullptr, nullptr, n, s));
+    const size_t col = ((size_t)n * 4 + 255) & ~(size_t)255;
+    if (int rc = ctx->d_part_var.ensure(3 * col + temp + 2 * 64 * 8 + 256)) return rc;
+    uint8_t *sp = ctx->d_part_var.as<uint8_t>();
+    uint32_t *d_perm = perm ? perm : reinterpret_cast<uint32_t *>(sp);
+    uint32_t *vlen = reinterpret_cast<uint32_t *>(sp + col), *vincl = reinterpret_cast<uint32_t *>(sp + 2 * col);
+    void *tmp = sp + 3 * col;
+    uint64_t *d_seg = reinterpret_cast<uint64_t *>(sp + 3 * col + ((temp + 255) & ~(size_t)255));
+    uint64_t *d_recb = d_seg + 64;
+    hipLaunchKernelGGL(k_partv_pack, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, dir, tile, nranks, d_counts,
+                       static_cast<PackedRec80 *>(out), d_perm, vlen);
+    CORRO_HIP_TRY(hipGetLastError());
+    TRY_PART(prim_inclusive_scan_u32(tmp, &temp, vlen, vincl, n, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(counts, d_tot, nranks * 8ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    // per-rank record and byte bases: B(x) = bytes of records [0, x) = vincl[x - 1]
+    std::vector<uint64_t> recb(nranks + 1, 0), seg(nranks + 1, 0);
+    for (uint32_t r = 0; r < nranks; r++) recb[r + 1] = recb[r] + counts[r];
+    for (uint32_t r = 1; r <= nranks; r++) {
+        uint32_t b = 0;
+        if (recb[r]) CORRO_HIP_TRY(hipMemcpy(&b, vincl + (recb[r] - 1), 4, hipMemcpyDeviceToHost));
+        seg[r] = b;
+    }
+    for (uint32_t r = 0; r < nranks; r++) var_counts[r] = seg[r + 1] - seg[r];
+    const uint64_t total = seg[nranks];
+    if (total > var_cap || (total && !var)) return fail(CORRO_E_RANGE, "var bytes exceed var_cap (var_counts = the sizes)");
+    CORRO_HIP_TRY(hipMemcpyAsync(d_seg, seg.data(), nranks * 8ULL, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(d_recb, recb.data(), nranks * 8ULL, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_partv_fill, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(PART_THREADS), 0, s, bd, dir, n,
+                       d_perm, vlen, vincl, d_seg, d_recb, nranks, static_cast<PackedRec80 *>(out), var);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+extern "C" int corro_unpack_var(corro_ctx *ctx, const void *recs, uint64_t n, const uint8_t *var, uint64_t var_len,
+                                const uint64_t *src_counts, const uint64_t *src_var, uint32_t nsrc, corro_changes *out) {
+    if (!ctx || (!recs && n) || !out || !src_counts || !src_var) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nsrc == 0 || nsrc > (uint32_t)PART_MAX_RANKS) return fail(CORRO_E_RANGE, "1..64 source ranks");
+    if (n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
+    if (n == 0) return CORRO_OK;
+    if (!out->pk || !out->table_cid || !out->col_version || !out->db_version || !out->cl || !out->seq ||
+        !out->site || !out->val0 || !out->val1 || !out->val_type || !out->val_len || !out->ts || !out->val_off ||
+        !out->val_size)
+        return fail(CORRO_E_INVALID, "every batch array is needed (80-B records carry every field)");
+    uint64_t tot = 0, totv = 0;
+    for (uint32_t r = 0; r < nsrc; r++) {
+        tot += src_counts[r];
+        totv += src_var[r];
+    }
+    if (tot != n || totv > var_len) return fail(CORRO_E_INVALID, "source counts do not add up to the records / bytes");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    std::vector<uint64_t> rb(nsrc), vb(nsrc);
+    uint64_t a = 0, v = 0;
+    for (uint32_t r = 0; r < nsrc; r++) {
+        rb[r] = a;
+        vb[r] = v;
+        a += src_counts[r];
+        v += src_var[r];
+    }
+    const size_t col8 = ((size_t)n * 8 + 255) & ~(size_t)255;
+    if (int rc = ctx->d_part_var.ensure(col8 + 2 * 64 * 8 + 256)) return rc;
+    uint64_t *pkref = ctx->d_part_var.as<uint64_t>();
+    uint64_t *d_rb = reinterpret_cast<uint64_t *>(ctx->d_part_var.as<uint8_t>() + col8), *d_vb = d_rb + 64;
+    CORRO_HIP_TRY(hipMemcpyAsync(d_rb, rb.data(), nsrc * 8ULL, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(d_vb, vb.data(), nsrc * 8ULL, hipMemcpyHostToDevice, s));
+    BatchOut bo{const_cast<uint64_t *>(out->pk),     const_cast<uint32_t *>(out->table_cid),
+                const_cast<int64_t *>(out->col_version), const_cast<int64_t *>(out->db_version),
+                const_cast<uint32_t *>(out->cl),     const_cast<uint32_t *>(out->seq),
+                const_cast<uint32_t *>(out->site),   const_cast<uint64_t *>(out->val0),
+                const_cast<uint64_t *>(out->val1),   const_cast<uint8_t *>(out->val_type),
+                const_cast<uint8_t *>(out->val_len), const_cast<uint64_t *>(out->ts)};
+    hipLaunchKernelGGL(k_unpackv, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
+                       static_cast<const PackedRec80 *>(recs), (uint32_t)n, d_rb, d_vb, nsrc, bo,
+                       const_cast<uint64_t *>(out->val_off), const_cast<uint32_t *>(out->val_size), pkref);
+    CORRO_HIP_TRY(hipGetLastError());
+    // interned pks: this engine's row keys for the shipped canonical bytes (host intern table)
+    bool any_interned = false;
+    for (const PkTable &t : ctx->pk) any_interned |= t.interned;
+    if (any_interned) {
+        std::vector<uint64_t> ref(n);
+        std::vector<uint32_t> tc(n);
+        CORRO_HIP_TRY(hipMemcpyAsync(ref.data(), pkref, n * 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(tc.data(), out->table_cid, n * 4, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        std::vector<uint8_t> hv(var_len);
+        if (var_len) CORRO_HIP_TRY(hipMemcpy(hv.data(), var, var_len, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> pk(n);
+        CORRO_HIP_TRY(hipMemcpy(pk.data(), out->pk, n * 8, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < n; i++) {
+            if (ref[i] == ~0ULL) continue;
+            const uint64_t off[2] = {0, ref[i] & 0xFFFFFFu}, at = ref[i] >> 24;
+            if (at + off[1] > var_len) return fail(CORRO_E_INVALID, "shipped pk bytes outside the var buffer");
+            if (int rc = corro_pk_keys(ctx, tc[i] >> 16, hv.data() + at, off, 1, &pk[i])) return rc;
+        }
+        CORRO_HIP_TRY(hipMemcpy(const_cast<uint64_t *>(out->pk), pk.data(), n * 8, hipMemcpyHostToDevice));
+    }
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;
 }

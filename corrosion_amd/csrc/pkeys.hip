@@ -8,6 +8,7 @@
 // pks are canonicalised before interning (unpacked and re-packed the way pack_columns packs), so
 // non-canonical encodings of one key name one row, as cr-sqlite's re-packing makes them (SURVEY
 // App. A.3).
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -108,6 +109,81 @@ bool pk_canonical(const uint8_t *p, uint64_t len, std::string &out, bool *single
     return true;
 }
 
+// Owner-routing hash of a canonical packed pk: FNV-1a over the bytes, then a 64-bit finaliser. A
+// function of the bytes alone, so every engine routes a row to the same rank whatever dense id its
+// own intern table gave it.
+uint64_t pk_route_hash(const std::string &canon) {
+    uint64_t h = 0xCBF29CE484222325ULL;
+    for (unsigned char c : canon) {
+        h ^= c;
+        h *= 0x100000001B3ULL;
+    }
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDULL;
+    h ^= h >> 33;
+    h *= 0xC4CEB9FE1A85EC53ULL;
+    h ^= h >> 33;
+    return h;
+}
+
+// grow a device buffer to hold `want` bytes, keeping its first `keep` bytes
+static int grow_keep(DevBuf &b, size_t want, size_t keep, hipStream_t s) {
+    if (want <= b.bytes && b.p) return CORRO_OK;
+    DevBuf nb;
+    if (int rc = nb.ensure(std::max<size_t>(want, 2 * b.bytes))) return rc;
+    if (keep) CORRO_HIP_TRY(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    b.release();
+    b = nb;
+    nb.p = nullptr;
+    return CORRO_OK;
+}
+
+int pk_mirror_sync(corro_ctx *ctx) {
+    if (ctx->pk.size() < ctx->tables.size()) ctx->pk.resize(ctx->tables.size());
+    hipStream_t s = ctx->stream;
+    std::vector<PkDir> dir(ctx->tables.size());
+    for (size_t t = 0; t < ctx->tables.size(); t++) {
+        PkTable &pt = ctx->pk[t];
+        PkDir &d = dir[t];
+        d = PkDir{};
+        d.interned = pt.interned ? 1u : 0u;
+        if (!pt.interned) continue;
+        const uint64_t n = pt.keys.size();
+        if (n > pt.dev_n) {  // append ids [dev_n, n)
+            std::vector<uint64_t> off(n - pt.dev_n + 1), hs(n - pt.dev_n);
+            std::string bytes;
+            off[0] = pt.dev_bytes;
+            for (uint64_t i = pt.dev_n; i < n; i++) {
+                bytes += pt.keys[i];
+                off[i - pt.dev_n + 1] = pt.dev_bytes + bytes.size();
+                hs[i - pt.dev_n] = pt.hash[i];
+            }
+            if (int rc = grow_keep(pt.d_off, (n + 1) * 8, (pt.dev_n + 1) * 8 * (pt.dev_n ? 1 : 0), s)) return rc;
+            if (int rc = grow_keep(pt.d_bytes, std::max<size_t>(pt.dev_bytes + bytes.size(), 1), pt.dev_bytes, s)) return rc;
+            if (int rc = grow_keep(pt.d_hash, n * 8, pt.dev_n * 8, s)) return rc;
+            CORRO_HIP_TRY(hipMemcpyAsync(pt.d_off.as<uint64_t>() + pt.dev_n, off.data(), off.size() * 8,
+                                         hipMemcpyHostToDevice, s));
+            if (!bytes.empty())
+                CORRO_HIP_TRY(hipMemcpyAsync(pt.d_bytes.as<uint8_t>() + pt.dev_bytes, bytes.data(), bytes.size(),
+                                             hipMemcpyHostToDevice, s));
+            CORRO_HIP_TRY(hipMemcpyAsync(pt.d_hash.as<uint64_t>() + pt.dev_n, hs.data(), hs.size() * 8,
+                                         hipMemcpyHostToDevice, s));
+            pt.dev_n = n;
+            pt.dev_bytes += bytes.size();
+        }
+        d.off = pt.d_off.as<uint64_t>();
+        d.bytes = pt.d_bytes.as<uint8_t>();
+        d.hash = pt.d_hash.as<uint64_t>();
+        d.n = pt.dev_n;
+    }
+    if (int rc = ctx->d_pkdir.ensure(std::max<size_t>(dir.size(), 1) * sizeof(PkDir))) return rc;
+    if (!dir.empty())
+        CORRO_HIP_TRY(hipMemcpyAsync(ctx->d_pkdir.p, dir.data(), dir.size() * sizeof(PkDir), hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
 std::string pack_int_pk(int64_t v) {
     std::string s;
     s.push_back((char)1);
@@ -168,6 +244,8 @@ int corro_pk_keys(corro_ctx *ctx, uint32_t table, const uint8_t *bytes, const ui
             const uint64_t id = t.keys.size();
             it = t.ids.emplace(canon, id).first;
             t.keys.push_back(canon);
+            t.hash.push_back(pk_route_hash(canon));
+            t.max_len = std::max<uint64_t>(t.max_len, canon.size());
         }
         keys[i] = it->second;
     }

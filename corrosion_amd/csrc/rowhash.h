@@ -26,6 +26,11 @@ struct BatchDev {
     const uint32_t *vsz;
     const uint8_t *arena;
     uint64_t lbase, ldata;
+    // column affinity (affinity.hip): conv[i] = 1 when change i's stored value is its converted
+    // value (cv0[i], cv1[i], cmeta[i] = type | len << 8); null when no value of the batch converts
+    const uint8_t *conv;
+    const uint64_t *cv0, *cv1;
+    const uint32_t *cmeta;
     uint32_t n;
 };
 

@@ -1,7 +1,9 @@
 """Node-level multi-GPU merge: one process per GPU, rows sharded by pk hash.
 
 Ingest on every rank: stable partition by owner rank into whole packed records (HIP kernel,
-corro_partition_packed: 48 B per INTEGER change, the §8(d) record) -> ONE all-to-all-v of records
+corro_partition_packed: 48 B per INTEGER change, the §8(d) record; corro_partition_var for tables
+with interned pks or long values: 80-B records routed by the canonical pk bytes plus a second stream
+of the pk / value bytes, re-keyed on the receiving engine) -> ONE all-to-all-v of records
 (torch.distributed: RCCL over xGMI on the GPU box, gloo in CPU rehearsals) after one all-to-all of
 the per-rank counts -> the received records, concatenated by source rank, unpacked to the SoA batch
 (corro_unpack_records) -> local merge. Concatenation by source rank preserves every row's
@@ -86,6 +88,29 @@ def exchange_records(recs, rec_bytes, counts, group=None):
     return out, rcounts
 
 
+def exchange_var(recs, var, counts, vcounts, group=None):
+    """The every-table exchange: the per-rank (records, bytes) sizes in one small all-to-all, then
+    one all-to-all-v of 80-B records and one of their variable-length bytes. Returns (records,
+    bytes, per-source record counts, per-source byte counts)."""
+    import torch
+    import torch.distributed as dist
+    dev = recs.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        r, v, rc, rv = exchange_var(recs.cpu(), var.cpu(), counts, vcounts, group)
+        return r.to(dev), v.to(dev), rc, rv
+    world = dist.get_world_size(group)
+    send = torch.tensor([x for pair in zip(counts, vcounts) for x in pair], dtype=torch.int64, device=dev)
+    got = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(got, send, group=group)
+    g = [int(x) for x in got.tolist()]
+    rcounts, rvar = g[0::2], g[1::2]
+    out = torch.empty(sum(rcounts) * 80, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(out, recs, [c * 80 for c in rcounts], [int(c) * 80 for c in counts], group=group)
+    vout = torch.empty(sum(rvar), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(vout, var.contiguous(), rvar, [int(c) for c in vcounts], group=group)
+    return out, vout, rcounts, rvar
+
+
 def site_digest(engine):
     """sha256 of the engine's site table (16-byte ids in ordinal order)."""
     return hashlib.sha256(b"".join(engine.site_ids())).digest()
@@ -120,9 +145,15 @@ def distributed_apply(engine, batch, group=None, impact=False, verify=True):
         if getattr(engine, "_sites_verified", None) != n_sites:
             verify_sites(engine, group)
             engine._sites_verified = n_sites
-    recs, rb, counts, perm = engine.partition_packed(batch, world, with_perm=impact)
-    got, rcounts = exchange_records(recs, rb, counts, group)
-    mine = engine.unpack_records(got, rb)
+    if "val_data" in batch or engine.interned:
+        # interned pks (routed and re-keyed by their canonical bytes) or long values: records + bytes
+        recs, var, counts, vcounts, perm = engine.partition_var(batch, world, with_perm=impact)
+        got, gvar, rcounts, rvar = exchange_var(recs, var, counts, vcounts, group)
+        mine = engine.unpack_var(got, gvar, rcounts, rvar)
+    else:
+        recs, rb, counts, perm = engine.partition_packed(batch, world, with_perm=impact)
+        got, rcounts = exchange_records(recs, rb, counts, group)
+        mine = engine.unpack_records(got, rb)
     imp = engine.apply(mine, impact=impact)
     if not impact:
         return None

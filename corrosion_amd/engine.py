@@ -126,8 +126,8 @@ class MergeEngine:
     # ---- column affinity -------------------------------------------------------------------
     def set_column_types(self, table, decl_types):
         """Register the table's declared column types (one per non-pk column, in cid order): their
-        SQLite affinities (corro_affinity_of_type) make the engine refuse values the affinity would
-        convert (corro_table_set_affinity)."""
+        SQLite affinities (corro_affinity_of_type) make the engine store each winning value as the
+        affinity converts it, as SQLite's base table does (corro_table_set_affinity)."""
         t = self.table_index(table)
         aff = np.array([L.lib().corro_affinity_of_type(str(d).encode()) for d in decl_types], np.uint8)
         L.check(L.lib().corro_table_set_affinity(self._h, t, aff.ctypes.data if len(aff) else None, len(aff)))
@@ -380,6 +380,57 @@ class MergeEngine:
         L.check(L.lib().corro_partition_packed(self._h, C.byref(s), nranks, recs.data_ptr(),
                                                perm.data_ptr() if perm is not None else None, counts.ctypes.data))
         return recs[:n * rb.value], rb.value, [int(c) for c in counts[:nranks]], (perm[:n] if perm is not None else None)
+
+    def partition_var(self, batch, nranks, with_perm=False):
+        """The exchange for every table (corro_partition_var): 80-B records grouped by owner rank plus
+        the variable-length bytes they ship (canonical pks of interned tables, long values), routed
+        by canonical pk bytes for interned tables. Returns (records uint8 tensor, var uint8 tensor,
+        per-rank record counts, per-rank byte counts, perm or None)."""
+        import torch
+        s = self._device_changes(batch)
+        data = batch.get("val_data")
+        if data is not None:
+            s.val_data, s.val_data_len = (data.data_ptr() if data.numel() else None), int(data.numel())
+        n = int(s.n)
+        dev = batch["pk"].device
+        recs = torch.empty(max(n, 1) * 80, dtype=torch.uint8, device=dev)
+        perm = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if with_perm else None
+        counts = np.zeros(max(1, nranks), np.uint64)
+        vcounts = np.zeros(max(1, nranks), np.uint64)
+        torch.cuda.current_stream().synchronize()
+        lib = L.lib()
+        pp = perm.data_ptr() if perm is not None else None
+        rc = lib.corro_partition_var(self._h, C.byref(s), nranks, recs.data_ptr(), pp, counts.ctypes.data, None, 0,
+                                     vcounts.ctypes.data)
+        total = int(vcounts[:nranks].sum())
+        var = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+        if rc == -6 and total:
+            rc = lib.corro_partition_var(self._h, C.byref(s), nranks, recs.data_ptr(), pp, counts.ctypes.data,
+                                         var.data_ptr(), total, vcounts.ctypes.data)
+        L.check(rc)
+        return (recs[:n * 80], var[:total], [int(c) for c in counts[:nranks]], [int(c) for c in vcounts[:nranks]],
+                perm[:n] if perm is not None else None)
+
+    def unpack_var(self, recs, var, src_counts, src_var):
+        """Received records + var bytes (concatenated by source rank) -> a device batch with every
+        field, val_data = var (corro_unpack_var; interned pks re-keyed on this engine)."""
+        import torch
+        n = int(recs.numel()) // 80
+        dev = recs.device
+        tdt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}
+        out = {k: torch.empty(max(n, 1), dtype=tdt[dt], device=dev)[:n] for k, dt in BATCH_FIELDS.items()}
+        s = L.Changes()
+        s.n = n
+        for k in BATCH_FIELDS:
+            setattr(s, k, out[k].data_ptr() if n else None)
+        sc = np.ascontiguousarray(src_counts, np.uint64)
+        sv = np.ascontiguousarray(src_var, np.uint64)
+        torch.cuda.current_stream().synchronize()
+        L.check(L.lib().corro_unpack_var(self._h, recs.data_ptr() if n else None, n,
+                                         var.data_ptr() if var.numel() else None, int(var.numel()),
+                                         sc.ctypes.data, sv.ctypes.data, len(sc), C.byref(s)))
+        out["val_data"] = var
+        return out
 
     def unpack_records(self, recs, rec_bytes, out=None):
         """Packed records (a uint8 CUDA tensor) -> SoA device batch (corro_unpack_records)."""

@@ -180,10 +180,12 @@ int corro_pk_bytes(corro_ctx *ctx, uint32_t table, const uint64_t *keys, uint64_
 
 /* SQLite column affinity. cr-sqlite stores a winning value through the base table,
  * whose column affinity may convert it; the next change is then compared unconverted against the
- * converted value. The engine merges values already in the class their column's affinity keeps (what
- * corrosion's writers send) and REFUSES a batch holding a value the affinity would convert
- * (CORRO_E_RANGE, nothing merged) instead of merging it inexactly. Without a registered affinity a
- * column is BLOB (no conversion, no check). */
+ * converted value. The engine does the same: a change's value is stored as its column's affinity
+ * converts it (SQLite 3.37.2's applyAffinity, its x87 long-double decimal scaling emulated bit for
+ * bit: INTEGER -> TEXT '5', REAL -0.0 -> INTEGER 0, INTEGER 5 -> REAL 5.0, numeric TEXT -> number,
+ * REAL -> "%!.15g" TEXT), exported rows carry the stored value, and an incoming change is compared
+ * by its raw value against the stored one. Without a registered affinity a column is BLOB (no
+ * conversion). */
 enum { CORRO_AFF_BLOB = 0, CORRO_AFF_TEXT = 1, CORRO_AFF_NUMERIC = 2, CORRO_AFF_INTEGER = 3, CORRO_AFF_REAL = 4 };
 /* sqlite3AffinityType of a declared column type (schema.rs's column type names): INT -> INTEGER,
  * CHAR/CLOB/TEXT -> TEXT, BLOB or none -> BLOB, REAL/FLOA/DOUB -> REAL, else NUMERIC. Host only. */
@@ -287,6 +289,24 @@ int corro_partition_packed(corro_ctx *ctx, const corro_changes *in, uint32_t nra
 /* Received records (concatenated by source rank) -> the SoA batch corro_apply_batch takes (device
  * arrays, n each; optional arrays may be NULL). rec_bytes = 48 or 80. */
 int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n, uint32_t rec_bytes, corro_changes *out);
+
+/* The exchange for EVERY table (interned pks, long values): 80-B records like corro_partition_packed
+ * plus a second stream of variable-length bytes per record -- the canonical packed pk of a change to
+ * an interned table (so the receiver keys the row in ITS own row-key space) and a long TEXT/BLOB
+ * value's bytes -- grouped by destination rank like the records: var_counts[r] bytes for rank r, in
+ * rank order. Rows of interned tables are routed by a hash of their canonical pk bytes (the same
+ * owner on every rank, whatever dense key each engine gave them); INTEGER-pk rows as in
+ * corro_partition_packed. DEVICE memory (in, out, var, perm); counts / var_counts host. var == NULL
+ * or var_cap too small: CORRO_E_RANGE after counts and var_counts are filled (records written), so
+ * the caller can size var and call again. One call ships < 4 GiB of bytes. */
+int corro_partition_var(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, void *out, uint32_t *perm,
+                        uint64_t *counts, uint8_t *var, uint64_t var_cap, uint64_t *var_counts);
+/* Received 80-B records and var bytes (each concatenated by source rank; src_counts / src_var = what
+ * each source sent, host) -> the SoA batch (device, every array set): long values' val_off / val_size
+ * point into `var`, which becomes the batch's val_data; interned tables' pks are re-keyed from their
+ * shipped canonical bytes (corro_pk_keys on this engine). */
+int corro_unpack_var(corro_ctx *ctx, const void *recs, uint64_t n, const uint8_t *var, uint64_t var_len,
+                     const uint64_t *src_counts, const uint64_t *src_var, uint32_t nsrc, corro_changes *out);
 
 /* ------------------------------------------------------------------ sync need diff */
 

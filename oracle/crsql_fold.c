@@ -67,6 +67,8 @@ struct of_state {
     uint64_t cap, nrows;
     uint8_t *arena;     /* bytes of long values; a long cell's v1 = (offset << 24) | length */
     uint64_t arena_len, arena_cap;
+    uint8_t *aff;       /* column affinity, 257 per table (NULL = none: every column BLOB) */
+    uint32_t aff_tables;
 };
 
 static uint64_t mix64(uint64_t x) {
@@ -90,7 +92,7 @@ of_state *of_new(const uint8_t *site_ids, uint32_t nsites) {
 void of_free(of_state *s) {
     if (!s) return;
     for (uint64_t i = 0; i < s->cap; i++) free(s->rows[i].cells);
-    free(s->rows); free(s->dbv); free(s->site_ids); free(s->arena); free(s);
+    free(s->rows); free(s->dbv); free(s->site_ids); free(s->arena); free(s->aff); free(s);
 }
 
 static of_row *find_row(of_state *s, uint32_t table, uint64_t pk, int create);
@@ -232,6 +234,46 @@ uint64_t of_value_bytes(const of_state *s, uint64_t handle, uint8_t *out, uint64
     return len;
 }
 
+#define OF_AFF_W 257
+void of_set_affinity(of_state *s, uint32_t table, const uint8_t *aff, uint32_t ncols) {
+    if (table >= s->aff_tables) {
+        s->aff = (uint8_t *)realloc(s->aff, (size_t)(table + 1) * OF_AFF_W);
+        memset(s->aff + (size_t)s->aff_tables * OF_AFF_W, OF_AFF_BLOB, (size_t)(table + 1 - s->aff_tables) * OF_AFF_W);
+        s->aff_tables = table + 1;
+    }
+    for (uint32_t c = 0; c < ncols && c + 1 < OF_AFF_W; c++) s->aff[(size_t)table * OF_AFF_W + c + 1] = aff[c];
+}
+
+/* the base table stores the value its column's affinity converts it to (affinity.c) */
+static int convert_cell(of_state *s, of_cell *c, uint32_t table, const of_val *raw) {
+    if (!s->aff || table >= s->aff_tables || c->cid >= OF_AFF_W) return 0;
+    const int aff = s->aff[(size_t)table * OF_AFF_W + c->cid];
+    uint8_t buf[16], out[32];
+    uint64_t len = 0;
+    const uint8_t *p = raw->type == OF_TEXT ? val_bytes(raw, buf, &len) : NULL;
+    int ot;
+    uint64_t ov0;
+    uint32_t olen;
+    if (!of_affinity(aff, raw->type, raw->v0, p, len, &ot, &ov0, out, &olen)) return 0;
+    c->vtype = (uint8_t)ot;
+    c->v0 = c->v1 = 0;
+    c->vlen = 0;
+    if (ot != OF_TEXT) {
+        c->v0 = ov0;
+    } else if (olen <= 16) {
+        for (uint32_t k = 0; k < olen; k++) {
+            if (k < 8) c->v0 |= (uint64_t)out[k] << (56 - 8 * k);
+            else c->v1 |= (uint64_t)out[k] << (56 - 8 * (k - 8));
+        }
+        c->vlen = (uint8_t)olen;
+    } else {
+        for (int k = 0; k < 8; k++) c->v0 = (c->v0 << 8) | out[k];
+        c->v1 = (arena_put(s, out, olen) << 24) | olen;
+        c->vlen = OF_LONG;
+    }
+    return 1;
+}
+
 static void fill_cell(of_state *s, of_cell *c, const of_changes *in, uint64_t i) {
     c->cid = in->table_cid[i] & 0xFFFFu;
     c->cv = in->col_version[i];
@@ -243,6 +285,10 @@ static void fill_cell(of_state *s, of_cell *c, const of_changes *in, uint64_t i)
     c->vlen = in->val_len ? in->val_len[i] : 0;
     c->v0 = in->val0 ? in->val0[i] : 0;
     c->v1 = in->val1 ? in->val1[i] : 0;
+    if (s->aff) {
+        const of_val v = in_val(in, i);
+        if (convert_cell(s, c, in->table_cid[i] >> 16, &v)) return;
+    }
     if (c->vlen == OF_LONG && (c->vtype == OF_TEXT || c->vtype == OF_BLOB)) {
         const of_val v = in_val(in, i);
         c->v0 = v.v0;

@@ -74,6 +74,17 @@ int of_apply_sharded(of_state **shards, uint32_t nshards, const of_changes *in, 
 void of_state_digest(const of_state *s, uint64_t out[3]);
 void of_rows_digest(const of_rows *o, uint64_t n, uint64_t out[3]);
 
+/* ---- column affinity (affinity.c; codes as CORRO_AFF_* in include/corro_hip.h) ---- */
+enum { OF_AFF_BLOB = 0, OF_AFF_TEXT = 1, OF_AFF_NUMERIC = 2, OF_AFF_INTEGER = 3, OF_AFF_REAL = 4 };
+/* The value a column of affinity `aff` stores for (type, v0 = INTEGER / REAL bits, txt/len = TEXT
+ * bytes). Returns 1 if that differs from the input: *otype, and *ov0 (INTEGER / REAL) or otxt/olen
+ * (TEXT, at most 32 bytes). */
+int of_affinity(int aff, int type, uint64_t v0, const uint8_t *txt, uint64_t len, int *otype, uint64_t *ov0,
+                uint8_t *otxt, uint32_t *olen);
+/* the fold stores a winning value as its column's affinity converts it (the incoming change is
+ * still compared unconverted, App. A.4); aff[c] = affinity of cid c + 1 */
+void of_set_affinity(of_state *s, uint32_t table, const uint8_t *aff, uint32_t ncols);
+
 /* ---- sync need diff (corro-types/src/sync.rs:127-249), CSR over (pair, actor) entries ---- */
 typedef struct {
     uint64_t n;                 /* entries */

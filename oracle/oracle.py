@@ -76,6 +76,10 @@ def lib():
         L.of_bytes_hash.restype = C.c_uint64
         L.of_bytes_hash.argtypes = [C.c_char_p, C.c_uint64]
         L.of_needs.argtypes = [C.POINTER(_SyncEntries), C.POINTER(_NeedsOut), C.c_int]
+        L.of_affinity.restype = C.c_int
+        L.of_affinity.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_char_p, C.c_uint64, C.POINTER(C.c_int),
+                                  C.POINTER(C.c_uint64), C.c_char_p, C.POINTER(C.c_uint32)]
+        L.of_set_affinity.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32]
         L.of_booked_new.restype = C.c_void_p
         L.of_booked_free.argtypes = [C.c_void_p]
         L.of_booked_insert_db.restype = C.c_int
@@ -146,6 +150,11 @@ class Fold:
         imp = np.zeros(max(s.n, 1), dtype=np.uint8)
         lib().of_apply(self._h, C.byref(s), imp.ctypes.data)
         return imp[: s.n]
+
+    def set_affinity(self, table, codes):
+        """column affinities of `table` (CORRO_AFF_* per cid 1..): winning values are stored converted"""
+        b = bytes(bytearray(codes))
+        lib().of_set_affinity(self._h, table, b, len(b))
 
     def export(self):
         m = lib().of_count(self._h)
@@ -402,3 +411,30 @@ def extract_changes(rows, needs):
             groups.append((v, last, ts, g))
         out.append(groups)
     return out
+
+
+AFF = {"BLOB": 0, "TEXT": 1, "NUMERIC": 2, "INTEGER": 3, "REAL": 4}
+
+
+def affinity(aff, value):
+    """The value (Python int / float / str / bytes / None) a column of affinity `aff` (AFF code) stores
+    for `value` (affinity.c, SQLite 3.37.2 applyAffinity)."""
+    import struct
+    if value is None or isinstance(value, (bytes, bytearray)):
+        return value
+    txt = b""
+    if isinstance(value, bool) or isinstance(value, int):
+        ty, v0 = OF_INTEGER, value & 0xFFFFFFFFFFFFFFFF
+    elif isinstance(value, float):
+        ty, v0 = OF_REAL, struct.unpack("<Q", struct.pack("<d", value))[0]
+    else:
+        ty, v0, txt = OF_TEXT, 0, value.encode()
+    ot, ov0, olen = C.c_int(), C.c_uint64(), C.c_uint32()
+    buf = C.create_string_buffer(32)
+    if not lib().of_affinity(aff, ty, v0, txt, len(txt), C.byref(ot), C.byref(ov0), buf, C.byref(olen)):
+        return value
+    if ot.value == OF_INTEGER:
+        return ov0.value - (1 << 64) if ov0.value >> 63 else ov0.value
+    if ot.value == OF_REAL:
+        return struct.unpack("<d", struct.pack("<Q", ov0.value))[0]
+    return buf.raw[: olen.value].decode()

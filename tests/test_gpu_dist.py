@@ -92,3 +92,106 @@ def test_exchange_refuses_mismatched_site_tables(tmp_path):
     world = 2
     mp.spawn(_sites_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert [open(tmp_path / f"sites{r}.txt").read() for r in range(world)] == ["refused", "refused"]
+
+
+# ---- every table: interned pks (testsblob, wide) and long values over the exchange ----------------
+NV, SEEDV = 9000, 17
+
+
+def _pk_batch(eng, rows):
+    """rows of tests.test_gpu_pk._changes -> a host batch keyed on THIS engine (interned ids are per
+    engine: the exchange must re-key them from the canonical bytes)."""
+    from tests.test_gpu_pk import INTERNED, SCHEMA
+    from tests._util import encode_values
+    from corrosion_amd.wire import unpack_int_pk
+    tix = {t: i for i, t in enumerate(SCHEMA)}
+    keys = np.zeros(len(rows), np.uint64)
+    for t in SCHEMA:
+        idx = [j for j, r in enumerate(rows) if r[0] == t]
+        if not idx:
+            continue
+        if t in INTERNED:
+            keys[idx] = eng.pk_keys(t, [rows[j][1] for j in idx])
+        else:
+            keys[idx] = [unpack_int_pk(rows[j][1]) & 0xFFFFFFFFFFFFFFFF for j in idx]
+    b = {"pk": keys,
+         "table_cid": np.array([(tix[r[0]] << 16) | r[2] for r in rows], np.uint32),
+         "col_version": np.array([r[4] for r in rows], np.int64),
+         "db_version": np.array([r[5] for r in rows], np.int64),
+         "site": np.array([r[6] for r in rows], np.uint32),
+         "cl": np.array([r[7] for r in rows], np.uint32),
+         "seq": np.array([r[8] % 100 for r in rows], np.uint32),
+         "ts": np.array([r[8] for r in rows], np.uint64)}
+    b.update(encode_values([r[3] for r in rows]))
+    return b
+
+
+def _canon_rows(eng):
+    """the state as comparable tuples: interned row keys by their canonical packed pk, long values
+    by their bytes"""
+    from tests.test_gpu_pk import INTERNED, SCHEMA
+    rows = eng.export()
+    tups = rows_to_tuples(rows, with_ts=True)
+    out = []
+    names = list(SCHEMA)
+    for t in tups:
+        name = names[t[0]]
+        pk = eng.pk_bytes(name, [t[1]])[0] if name in INTERNED else t[1]
+        out.append((t[0], pk) + t[2:])
+    return sorted(out, key=repr)
+
+
+def _var_worker(rank, world, port, outdir):
+    import pickle
+    import torch
+    import torch.distributed as dist
+    import corrosion_amd as ca
+    from corrosion_amd.dist import distributed_apply
+    from tests.test_gpu_pk import INTERNED, SCHEMA, _changes
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(SEEDV)
+    rows = _changes(rng, NV, 6)
+    lo, hi = rank * NV // world, (rank + 1) * NV // world
+    eng = ca.MergeEngine(SCHEMA, capacity_hint=NV, device=0, interned=INTERNED)
+    eng.register_sites(synth.site_ids(6, 3))
+    if rank == 1:  # a different interning order than rank 0: the shipped bytes must re-key rows
+        eng.pk_keys("wide", [r[1] for r in reversed(rows) if r[0] == "wide"][:40])
+    b = _pk_batch(eng, rows[lo:hi])
+    dev = {}
+    for k, v in b.items():
+        v = np.ascontiguousarray(v)
+        dev[k] = torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                                  (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda()
+    imp = distributed_apply(eng, dev, impact=True)
+    np.save(os.path.join(outdir, f"vimp{rank}.npy"), imp.cpu().numpy())
+    with open(os.path.join(outdir, f"vrows{rank}.pkl"), "wb") as f:
+        pickle.dump(_canon_rows(eng), f)
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_two_rank_every_table_with_long_values(tmp_path):
+    """testsblob (BLOB pk) and wide (composite pk) of corro-tests/src/lib.rs:32-52, TEXT / BLOB
+    values longer than 16 bytes: the exchange routes interned rows by their canonical pk bytes,
+    ships the bytes, re-keys them on the owner; the union of the two ranks' states equals one engine's
+    merge of the whole batch, and every sender gets its changes' impacts back in its order."""
+    import pickle
+    import corrosion_amd as ca
+    from tests.test_gpu_pk import INTERNED, SCHEMA, _changes
+    world = 2
+    mp.spawn(_var_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = []
+    for r in range(world):
+        with open(tmp_path / f"vrows{r}.pkl", "rb") as f:
+            got += pickle.load(f)
+    e = ca.MergeEngine(SCHEMA, capacity_hint=NV, interned=INTERNED)
+    e.register_sites(synth.site_ids(6, 3))
+    rows = _changes(np.random.default_rng(SEEDV), NV, 6)
+    want_imp = e.apply(_pk_batch(e, rows), impact=True)
+    want = _canon_rows(e)
+    assert any(isinstance(t[5], bytes) for t in want) and any(isinstance(t[1], bytes) for t in want)
+    assert sorted(got, key=repr) == want
+    got_imp = np.concatenate([np.load(tmp_path / f"vimp{r}.npy") for r in range(world)])
+    assert np.array_equal(got_imp, want_imp)

@@ -127,13 +127,13 @@ def test_failure_before_writes_does_not_poison():
 def test_affinity_check_with_out_of_range_long_value():
     """a long TEXT value whose val_off points past val_data on a table with registered
     affinities is reported as malformed (CORRO_E_INVALID), never read out of bounds."""
-    from tests.test_gpu_affinity import T, _batch, _engine
-    e, _sites = _engine()
-    b = _batch([(1, 3, T, b"abc")])
+    from tests.test_gpu_affinity import _batch, _engine
+    e, _f = _engine()
+    b = _batch([(1, 1, "abc")])
     b["val_len"][0] = 255
     b["val_off"] = np.array([1 << 40], np.uint64)
     b["val_size"] = np.array([40], np.uint32)
     b["val_data"] = np.frombuffer(b"x" * 40, np.uint8).copy()
     with pytest.raises(ca.CorroError, match="CORRO_E_INVALID"):
         e.apply(b)
-    e.apply(_batch([(2, 3, T, b"fine")]))
+    e.apply(_batch([(2, 3, "fine")]))
