@@ -14,6 +14,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -198,29 +200,89 @@ void clear_buffered(corro_bookie *bk, uint32_t site, uint64_t vs, uint64_t ve) {
     }
 }
 
+// A persistent pool of host workers for the per-call parallel passes: spawning threads per pass
+// cost more than the passes themselves (four passes x 15 threads per call). Workers sleep on a
+// condition variable between jobs; one job runs at a time (callers serialise on the pool).
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool *p = new HostPool();  // never destroyed: its workers outlive static teardown
+        return *p;
+    }
+    unsigned threads() const { return cap_; }
+    // fn(arg, k) for k in [0, n) on up to nth threads (the caller is one of them)
+    void run(size_t n, unsigned nth, void (*fn)(void *, size_t), void *arg) {
+        std::lock_guard<std::mutex> one(job_mu_);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = fn;
+            arg_ = arg;
+            n_ = n;
+            next_.store(0, std::memory_order_relaxed);
+            want_ = nth - 1;
+            joined_ = 0;
+            done_ = 0;
+            gen_++;
+        }
+        cv_.notify_all();
+        work(fn, arg, n);
+        std::unique_lock<std::mutex> g(mu_);
+        want_ = 0;  // no worker joins this job any more; wait for the ones that did
+        done_cv_.wait(g, [&] { return done_ == joined_; });
+    }
+
+  private:
+    HostPool() {
+        const char *e = std::getenv("CORRO_HOST_THREADS");
+        const long v = e ? std::atol(e) : 0;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        cap_ = v > 0 ? (unsigned)std::min<long>(v, 256) : std::min(16u, hw);
+        for (unsigned t = 1; t < cap_; t++) std::thread([this] { loop(); }).detach();
+    }
+    void work(void (*fn)(void *, size_t), void *arg, size_t n) {
+        for (size_t k; (k = next_.fetch_add(1, std::memory_order_relaxed)) < n;) fn(arg, k);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(mu_);
+        while (true) {
+            cv_.wait(g, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (joined_ >= want_) continue;  // enough workers for this job
+            joined_++;
+            auto fn = fn_;
+            auto arg = arg_;
+            const size_t n = n_;
+            g.unlock();
+            work(fn, arg, n);
+            g.lock();
+            done_++;
+            done_cv_.notify_all();
+        }
+    }
+    unsigned cap_ = 1;
+    std::mutex job_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    void (*fn_)(void *, size_t) = nullptr;
+    void *arg_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    unsigned want_ = 0, joined_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+};
+
 // f(0) .. f(n - 1) on up to CORRO_HOST_THREADS (default: min(16, hardware)) host threads, at least
 // `per` indices per thread (serial for small n). f must only touch state of its own index.
 template <class F>
 void run_parallel(size_t n, F &&f, size_t per = 8) {
-    static const unsigned cap = [] {
-        const char *e = std::getenv("CORRO_HOST_THREADS");
-        const long v = e ? std::atol(e) : 0;
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        return v > 0 ? (unsigned)std::min<long>(v, 256) : std::min(16u, hw);
-    }();
-    const unsigned nth = (unsigned)std::min<size_t>(cap, n / std::max<size_t>(per, 1));
+    HostPool &pool = HostPool::get();
+    const unsigned nth = (unsigned)std::min<size_t>(pool.threads(), n / std::max<size_t>(per, 1));
     if (nth <= 1) {
         for (size_t k = 0; k < n; k++) f(k);
         return;
     }
-    std::atomic<size_t> next{0};
-    auto body = [&] {
-        for (size_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(k);
-    };
-    std::vector<std::thread> ts;
-    for (unsigned t = 1; t < nth; t++) ts.emplace_back(body);
-    body();
-    for (auto &t : ts) t.join();
+    using FT = typename std::remove_reference<F>::type;
+    pool.run(n, nth, [](void *p, size_t k) { (*static_cast<FT *>(p))(k); }, (void *)&f);
 }
 
 }  // namespace

@@ -94,13 +94,18 @@ def test_config5_64m_two_batch_fold_vs_sharded_oracle():
     eng = ca.MergeEngine(synth.adversarial_schema(8), capacity_hint=n, device=0)
     eng.register_sites(sites)
     fold = O.ShardedFold(sites, nshards=64, nthreads=16)
+    import time
+    t0 = time.time()
     for k in range(2):
         b = synth.adversarial_batch(n, 1000, 8, 1 << 20, seed + k)
+        print(f"batch {k} generated at {time.time() - t0:.0f} s", flush=True)
         d = _dev(b)
         imp = eng.apply(d, impact=True).cpu().numpy()
+        print(f"batch {k} applied on the GPU at {time.time() - t0:.0f} s", flush=True)
         del d
         torch.cuda.empty_cache()
         ref = fold.apply(b)
+        print(f"batch {k} folded by the oracle at {time.time() - t0:.0f} s", flush=True)
         assert np.array_equal(imp, ref), f"config 5 batch {k}: impact flags differ"
         del b, imp, ref
     m = eng.metrics()

@@ -1,6 +1,6 @@
 // Microbenchmark for the staging pass's record width: what does MI355X give when 48-B SoA changes
-// are staged as 64-B records vs 32-B records into per-tile bucket slices (32 K buckets, LDS cursors
-// exactly like k_scatter), and how should a wave lay out the 32-B stores?
+// are staged as 64-B records vs 48-B or 32-B records into per-tile bucket slices (32 K buckets, LDS
+// cursors exactly like k_scatter), and how should a wave lay out the narrower stores?
 // Build: hipcc -O3 --offload-arch=gfx950 tools/micro_stage32.hip -o tools/micro_stage32
 #include <hip/hip_runtime.h>
 
@@ -31,6 +31,9 @@ constexpr uint32_t LGB = 15, NB = 1u << LGB;
 // layout 2: 32-B record, permlane32 transpose: lanes L and L+32 store the two halves of a record
 // layout 3: 32-B record, shuffles so that lanes 2r, 2r+1 store the two halves of one record
 // layout 4: 32-B record as two 16-B SoA planes (quad 0 array, quad 1 array), one dwordx4 each
+// layout 5: 48-B record (a PLAIN batch's record without v1 / meta), each lane stores its own 3 quads
+// layout 6: 48-B record, wave-cooperative: the wave's 64 records are 192 consecutive-per-record
+//           quads; store instruction k has lane L write quad 64k + L (record (64k+L)/3, part %3)
 template <int LAYOUT, bool SEQ>
 __global__ void __launch_bounds__(TH) k_stage(const uint64_t *pk, const int64_t *cv, const int64_t *dbv,
                                                const uint64_t *v0, const uint32_t *tc, const uint32_t *cl,
@@ -43,14 +46,18 @@ __global__ void __launch_bounds__(TH) k_stage(const uint64_t *pk, const int64_t 
     const uint32_t begin = blockIdx.x * tile, end = min(n, begin + tile);
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t base = begin; base < end; base += TH * 4) {
-        uint4 q[4][4];
+        uint4 q[4][4] = {};
         uint32_t d[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const uint32_t i = base + u * TH + threadIdx.x;
             const uint64_t p = pk[i], c = (uint64_t)cv[i], b = (uint64_t)dbv[i], v = v0[i];
             const uint32_t t = tc[i], l = cl[i], s = seq[i], st = site[i];
-            if (LAYOUT == 0) {
+            if (LAYOUT >= 5) {
+                q[u][0] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)c, (uint32_t)(c >> 32));
+                q[u][1] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)v, (uint32_t)(v >> 32));
+                q[u][2] = make_uint4(t, l ^ s, st, i);
+            } else if (LAYOUT == 0) {
                 q[u][0] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)c, (uint32_t)(c >> 32));
                 q[u][1] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)v, (uint32_t)(v >> 32));
                 q[u][2] = make_uint4(0, 0, t, l);
@@ -104,6 +111,21 @@ __global__ void __launch_bounds__(TH) k_stage(const uint64_t *pk, const int64_t 
                     b.x = __shfl(q[u][1].x, src); b.y = __shfl(q[u][1].y, src); b.z = __shfl(q[u][1].z, src); b.w = __shfl(q[u][1].w, src);
                     const uint32_t sidx = __shfl(d[u], src);
                     out[(size_t)sidx * 2 + j] = j ? b : a;
+                }
+            } else if (LAYOUT == 5) {
+                out[(size_t)d[u] * 3] = q[u][0];
+                out[(size_t)d[u] * 3 + 1] = q[u][1];
+                out[(size_t)d[u] * 3 + 2] = q[u][2];
+            } else if (LAYOUT == 6) {
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const uint32_t qi = 64 * k + lane, src = qi / 3, part = qi % 3;
+                    uint4 a0, a1, a2;
+                    a0.x = __shfl(q[u][0].x, (int)src); a0.y = __shfl(q[u][0].y, (int)src); a0.z = __shfl(q[u][0].z, (int)src); a0.w = __shfl(q[u][0].w, (int)src);
+                    a1.x = __shfl(q[u][1].x, (int)src); a1.y = __shfl(q[u][1].y, (int)src); a1.z = __shfl(q[u][1].z, (int)src); a1.w = __shfl(q[u][1].w, (int)src);
+                    a2.x = __shfl(q[u][2].x, (int)src); a2.y = __shfl(q[u][2].y, (int)src); a2.z = __shfl(q[u][2].z, (int)src); a2.w = __shfl(q[u][2].w, (int)src);
+                    const uint32_t sidx = __shfl(d[u], (int)src);
+                    out[(size_t)sidx * 3 + part] = part == 0 ? a0 : (part == 1 ? a1 : a2);
                 }
             } else {
                 out[d[u]] = q[u][0];
@@ -177,6 +199,7 @@ int main() {
                            (uint32_t *)in[6], (uint32_t *)in[7], sink, n);
     });
     time_it("read 32-B records (2 GB)", 32.0 * n, [&] { hipLaunchKernelGGL(k_read_rec, dim3(4096), dim3(256), 0, 0, out, sink, (size_t)n * 2); });
+    time_it("read 48-B records (3 GB)", 48.0 * n, [&] { hipLaunchKernelGGL(k_read_rec, dim3(4096), dim3(256), 0, 0, out, sink, (size_t)n * 3); });
     time_it("read 64-B records (4 GB)", 64.0 * n, [&] { hipLaunchKernelGGL(k_read_rec, dim3(4096), dim3(256), 0, 0, out, sink, (size_t)n * 4); });
     const dim3 g(ntiles), b(TH);
     time_it("stage 64B, sequential", 112.0 * n, [&] { hipLaunchKernelGGL((k_stage<0, true>), g, b, 0, 0, ARGS); });
@@ -188,6 +211,10 @@ int main() {
     time_it("stage 32B adjacent-lane halves, sequential", 80.0 * n, [&] { hipLaunchKernelGGL((k_stage<3, true>), g, b, 0, 0, ARGS); });
     time_it("stage 32B adjacent-lane halves, bucket slices", 80.0 * n, [&] { hipLaunchKernelGGL((k_stage<3, false>), g, b, 0, 0, ARGS); });
     time_it("stage 2x16B SoA planes, sequential", 80.0 * n, [&] { hipLaunchKernelGGL((k_stage<4, true>), g, b, 0, 0, ARGS); });
+    time_it("stage 48B per-lane 3x16B, sequential", 96.0 * n, [&] { hipLaunchKernelGGL((k_stage<5, true>), g, b, 0, 0, ARGS); });
+    time_it("stage 48B per-lane 3x16B, bucket slices", 96.0 * n, [&] { hipLaunchKernelGGL((k_stage<5, false>), g, b, 0, 0, ARGS); });
+    time_it("stage 48B wave-cooperative quads, sequential", 96.0 * n, [&] { hipLaunchKernelGGL((k_stage<6, true>), g, b, 0, 0, ARGS); });
+    time_it("stage 48B wave-cooperative quads, bucket slices", 96.0 * n, [&] { hipLaunchKernelGGL((k_stage<6, false>), g, b, 0, 0, ARGS); });
     time_it("stage 2x16B SoA planes, bucket slices", 80.0 * n, [&] { hipLaunchKernelGGL((k_stage<4, false>), g, b, 0, 0, ARGS); });
     return 0;
 }
