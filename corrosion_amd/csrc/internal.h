@@ -191,7 +191,8 @@ struct corro_ctx {
     corro::DevBuf d_ncols;        // u16 column count per table
     std::vector<uint8_t> aff;     // column affinity per (table, cid), (MAX_COLS + 1) per table
     corro::DevBuf d_aff, d_affflag;
-    corro::DevBuf d_aff_conv, d_aff_vals;  // per change of a batch: converted flag; cv0 | cv1 | cmeta
+    corro::DevBuf d_aff_conv, d_aff_vals;
+    corro::DevBuf d_gaps_big;              // corro_booked_insert_db_batch: counter + long-actor list  // per change of a batch: converted flag; cv0 | cv1 | cmeta
     bool aff_any = false;         // some column has an affinity other than BLOB
     corro::DevBuf d_part;         // partition counts
     corro::DevBuf d_pkdir;        // PkDir per table (pk_mirror_sync)

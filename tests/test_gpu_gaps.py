@@ -73,3 +73,46 @@ def test_non_canonical_input_flagged():
     e = _engine()
     (mx, rm, ins, gaps, status), = insert_db_batch(e, [10], [[(3, 5), (4, 8)]], [[(12, 12)]])
     assert status == -1
+
+
+def _long_state(rng):
+    """An actor with many gaps (a wave each in k_gaps_wave): every other version range applied, then
+    the next call's ranges, some spanning many gaps, some above max."""
+    b = ca.BookedVersions()
+    ng = int(rng.integers(20, 400))
+    hist = [[(int(3 * k + 1), int(3 * k + 1)) for k in range(ng)]]
+    b.insert_db(hist[0])
+    top = 3 * ng + 1
+    k = int(rng.integers(0, 90))
+    st = rng.integers(1, top + 60, size=k)
+    nxt = [(int(s), int(s + rng.integers(0, rng.choice([2, 8, 40])))) for s in st]
+    return b, hist, nxt
+
+
+def test_long_actors_vs_host_and_oracle():
+    rng = np.random.default_rng(32)
+    e = _engine()
+    states = [_long_state(rng) if i % 3 else _random_state(rng) for i in range(3000)]
+    got = insert_db_batch(e, [b.last() for b, _, _ in states], [b.needed() for b, _, _ in states],
+                          [nxt for _, _, nxt in states])
+    nlong = 0
+    for (b, hist, nxt), (mx, rm, ins, gaps, status) in zip(states, got):
+        nlong += len(b.needed()) + len(canonical_ranges(nxt) if nxt else []) > 32
+        assert status == 0
+        rm_h, ins_h = b.insert_db(canonical_ranges(nxt)) if nxt else ([], [])
+        assert sorted(rm) == sorted(set(rm_h))
+        assert ins == ins_h
+        assert gaps == b.needed()
+        assert mx == b.last()
+        f = O.Booked()
+        for h in hist + ([nxt] if nxt else []):
+            f.insert_db(h)
+        assert gaps == f.needed() and mx == f.max()
+    assert nlong > 1000
+
+
+def test_non_canonical_long_actor_flagged():
+    e = _engine()
+    gaps = [(3 * k + 2, 3 * k + 3) for k in range(50)] + [(150, 151)]   # (149, 150) and (150, 151) overlap
+    (mx, rm, ins, gaps_out, status), = insert_db_batch(e, [400], [gaps], [[(402, 402)]])
+    assert status == -1
