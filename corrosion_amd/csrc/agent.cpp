@@ -718,16 +718,20 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     if (nb || out->impactful) {
         corro_changes batch{};
         const uint8_t *imp = nullptr;
+        corro::AgentPositions pm{};
         if (nb) {
             bool gathered = false;
-            TRY_RC(corro::agent_dev_batch(ctx, &dv, P, ncs, nspans, nb, need_ts, &batch, &gathered));
-            stage(gathered ? "order+gather" : "order");
+            TRY_RC(corro::agent_dev_batch(ctx, &dv, P, ncs, nspans, nb, need_ts, &batch, &gathered, &pm));
+            stage(gathered ? "order+gather" : (pm.on ? "order+positions" : "order"));
             int rc = CORRO_OK;
             uint8_t *ib = corro::agent_dev_impact_buf(ctx, nb, &rc);
             if (rc != CORRO_OK) return rc;
             corro_apply_out ao{};
             ao.impact = ib;
+            // (position mode: the input where it lies, each change at its application position)
+            corro::agent_dev_set_positions(ctx, pm.on ? &pm : nullptr);
             rc = corro_apply_batch(ctx, &batch, CORRO_MEM_DEVICE, &ao);
+            corro::agent_dev_set_positions(ctx, nullptr);
             if (rc != CORRO_OK) {  // the transaction fails as a whole (util.rs:849-855)
                 for (uint64_t i = 0; i < ncs; i++) out->known[i] = CORRO_KNOWN_SKIPPED;
                 return rc;
@@ -735,8 +739,8 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
             imp = ib;
             stage("apply");
         }
-        TRY_RC(corro::agent_dev_impacts(ctx, imp, batch.table_cid, nb, P, ncs, nspans, out->impactful, nchanges, mem,
-                                        ntables));
+        TRY_RC(corro::agent_dev_impacts(ctx, imp, batch.table_cid, pm.on, nb, P, ncs, nspans, out->impactful, nchanges,
+                                        mem, ntables));
         for (uint32_t t = 0; t < ntables; t++) committed[t] += P.committed[t];
         stage("impacts");
     }

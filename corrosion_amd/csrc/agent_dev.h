@@ -61,19 +61,31 @@ int agent_dev_fetch(corro_ctx *ctx, const corro_changes *dv, const std::vector<A
 // contiguous, suitably aligned run of the input and every needed field is there; else a gather into
 // device scratch that also fills ts from the changesets when the input has none and some changeset
 // carries one. *gathered says which. The span tables stay on the device for agent_dev_impacts.
+// Position mode (pm non-null, taken when the input is one apply chunk with the apply's alignment):
+// no gather; *batch = the input itself and pm the application position of every input change
+// (ap, AP_SKIP = not applied), the input index of every position (src) and the per-position ts.
+struct AgentPositions {
+    bool on;
+    const uint32_t *ap, *src;
+    const uint64_t *ts;
+    uint64_t n;
+};
 int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &p, uint64_t ncs, uint64_t nspans,
-                    uint64_t nbatch, bool need_ts, corro_changes *batch, bool *gathered);
+                    uint64_t nbatch, bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm);
+// the next corro_apply_batch on ctx runs in position mode (null: back to normal)
+void agent_dev_set_positions(corro_ctx *ctx, const AgentPositions *pm);
 
 // Device impact buffer for a batch of n changes (valid until the next call).
 uint8_t *agent_dev_impact_buf(corro_ctx *ctx, uint64_t n, int *rc);
 
 // From the batch's per-change impact growth: impactful[span.src + k] (0/1 over all nin input
 // changes, in `mem` memory; NULL = not wanted), p.any[i] = flagged changeset i had an impactful change,
-// p.committed[t] = impactful changes of table t (tcid = the batch's table_cid array, device). Rule
+// p.committed[t] = impactful changes of table t (tcid = the batch's table_cid array, device, by batch
+// position -- or by input index with tcid_by_src). Rule
 // (util.rs:1218-1261): a version's first change is impactful when the transaction's cumulative
 // counter is > 0 after it (any impact at or before it in the batch); its later changes when their
 // own growth is > 0.
-int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tcid, uint64_t nbatch,
+int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tcid, bool tcid_by_src, uint64_t nbatch,
                       const AgentPinned &p, uint64_t ncs, uint64_t nspans, uint8_t *impactful, uint64_t nin, int mem,
                       uint32_t ntables);
 

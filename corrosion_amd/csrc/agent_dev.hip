@@ -17,7 +17,11 @@
 #include <cstring>
 
 #include "agent_dev.h"
+#include <cstdlib>
+
 #include "internal.h"
+
+extern "C" uint64_t corro_detail_chunk_changes(const corro_ctx *ctx);  // engine.hip (apply chunk size)
 
 namespace corro {
 
@@ -127,6 +131,7 @@ struct ImpArgs {
     uint8_t *any;                      // per changeset
     unsigned long long *committed;     // per table
     uint32_t ntables;
+    bool tcid_by_src;                  // tcid indexed by input index (position mode), else by batch position
 };
 
 __global__ void __launch_bounds__(AG_T) k_impactful(ImpArgs a) {
@@ -145,7 +150,7 @@ __global__ void __launch_bounds__(AG_T) k_impactful(ImpArgs a) {
             bool hit = false;
             if (act) hit = k == 0 ? first <= d : a.imp[d + k] != 0;
             if (act && a.out) a.out[s + k] = hit ? 1 : 0;
-            const uint32_t t = hit ? a.tcid[d + k] >> 16 : 0xFFFFFFFFu;
+            const uint32_t t = hit ? a.tcid[(a.tcid_by_src ? s : d) + k] >> 16 : 0xFFFFFFFFu;
             unsigned long long m = __ballot(hit && t < a.ntables);
             anyb |= __ballot(hit) != 0;
             while (m) {
@@ -312,6 +317,25 @@ int gather_dev(corro_ctx *ctx, const corro_changes *dv, const uint64_t *src, con
     return CORRO_OK;
 }
 
+// position mode: ap[src + k] = dst + k, src_of[dst + k] = src + k and, when wanted, the ts of
+// application position dst + k (the input's per-change ts, else the changeset's), a wave per span
+__global__ void __launch_bounds__(AG_T) k_span_pos(const uint64_t *__restrict__ s_src, const uint64_t *__restrict__ s_dst,
+                                                    const uint64_t *__restrict__ s_cnt, const uint64_t *__restrict__ s_ts,
+                                                    uint64_t nspans, const uint64_t *__restrict__ in_ts,
+                                                    uint32_t *__restrict__ ap, uint32_t *__restrict__ src_of,
+                                                    uint64_t *__restrict__ ts_out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * AG_T + threadIdx.x) >> 6, nw = (uint64_t)gridDim.x * (AG_T / 64);
+    for (uint64_t j = w0; j < nspans; j += nw) {
+        const uint64_t s = s_src[j], d = s_dst[j], c = s_cnt[j], t = s_ts[j];
+        for (uint64_t k = lane; k < c; k += 64) {
+            ap[s + k] = (uint32_t)(d + k);
+            src_of[d + k] = (uint32_t)(s + k);
+            if (ts_out) ts_out[d + k] = in_ts ? in_ts[s + k] : t;
+        }
+    }
+}
+
 dim3 flat_grid(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + AG_T - 1) / AG_T, 8192))); }
 
 }  // namespace
@@ -449,8 +473,9 @@ int agent_dev_fetch(corro_ctx *ctx, const corro_changes *dv, const std::vector<A
 }
 
 int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &p, uint64_t ncs, uint64_t nspans,
-                    uint64_t nbatch, bool need_ts, corro_changes *batch, bool *gathered) {
+                    uint64_t nbatch, bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm) {
     *gathered = false;
+    if (pm) *pm = AgentPositions{};
     hipStream_t s = ctx->stream;
     const DevCols c = dev_cols(ctx);
     if (nspans) {
@@ -495,6 +520,32 @@ int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &
         *batch = b;
         return CORRO_OK;
     }
+    // position mode: the merge stages the input where it lies, each change with its application
+    // position, instead of a gather of every field into application order (one chunk, the apply's
+    // alignment of device batches)
+    auto aligned = [](const void *q, uintptr_t a) { return !q || ((uintptr_t)q % a) == 0; };
+    const char *fg = std::getenv("CORRO_AGENT_GATHER");  // tests: force the gather path
+    if (pm && nspans && !(fg && fg[0] == '1') && dv->n <= corro_detail_chunk_changes(ctx) && aligned(dv->pk, 16) && aligned(dv->col_version, 16) &&
+        aligned(dv->db_version, 16) && aligned(dv->val0, 16) && aligned(dv->val1, 16) && aligned(dv->table_cid, 8) &&
+        aligned(dv->cl, 8) && aligned(dv->seq, 8) && aligned(dv->site, 8)) {
+        const bool want_ts = need_ts || dv->ts;
+        const size_t o_src = al256(dv->n * 4), o_ts = o_src + al256(nbatch * 4);
+        if (int rc = ctx->d_agent_batch.ensure(o_ts + (want_ts ? nbatch * 8 : 0) + 256)) return rc;
+        uint8_t *base = ctx->d_agent_batch.as<uint8_t>();
+        uint32_t *ap = reinterpret_cast<uint32_t *>(base), *src_of = reinterpret_cast<uint32_t *>(base + o_src);
+        uint64_t *ts = want_ts ? reinterpret_cast<uint64_t *>(base + o_ts) : nullptr;
+        CORRO_HIP_TRY(hipMemsetAsync(ap, 0xFF, dv->n * 4, s));
+        hipLaunchKernelGGL(k_span_pos, wave_grid(nspans), dim3(AG_T), 0, s, c.s_src, c.s_dst, c.s_cnt, c.s_ts, nspans,
+                           dv->ts, ap, src_of, ts);
+        CORRO_HIP_TRY(hipGetLastError());
+        *batch = *dv;
+        pm->on = true;
+        pm->ap = ap;
+        pm->src = src_of;
+        pm->ts = ts;
+        pm->n = nbatch;
+        return CORRO_OK;
+    }
     corro_changes g{};
     if (int rc = gather_dev(ctx, dv, c.s_src, c.s_dst, c.s_cnt, c.s_ts, nspans, nbatch, need_ts, ctx->d_agent_batch, g))
         return rc;
@@ -504,12 +555,19 @@ int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &
     return CORRO_OK;
 }
 
+void agent_dev_set_positions(corro_ctx *ctx, const AgentPositions *pm) {
+    ctx->pm_ap = pm ? pm->ap : nullptr;
+    ctx->pm_src = pm ? pm->src : nullptr;
+    ctx->pm_ts = pm ? pm->ts : nullptr;
+    ctx->pm_n = pm ? pm->n : 0;
+}
+
 uint8_t *agent_dev_impact_buf(corro_ctx *ctx, uint64_t n, int *rc) {
     *rc = ctx->d_agent_imp.ensure(al256(std::max<uint64_t>(n, 1)) + 256);
     return *rc ? nullptr : ctx->d_agent_imp.as<uint8_t>();
 }
 
-int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tcid, uint64_t nbatch,
+int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tcid, bool tcid_by_src, uint64_t nbatch,
                       const AgentPinned &p, uint64_t ncs, uint64_t nspans, uint8_t *impactful, uint64_t nin, int mem,
                       uint32_t ntables) {
     hipStream_t s = ctx->stream;
@@ -546,6 +604,7 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
         a.any = c.any;
         a.committed = reinterpret_cast<unsigned long long *>(base + o_cm);
         a.ntables = ntables;
+        a.tcid_by_src = tcid_by_src;
         hipLaunchKernelGGL(k_impactful, wave_grid(nspans), dim3(AG_T), 0, s, a);
         CORRO_HIP_TRY(hipGetLastError());
         CORRO_HIP_TRY(hipMemcpyAsync(p.any, c.any, ncs, hipMemcpyDeviceToHost, s));

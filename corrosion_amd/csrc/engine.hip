@@ -714,7 +714,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, MISC_WORDS * 8, s));
     CORRO_HIP_TRY(hipMemsetAsync(ctx->d_dbv_batch.p, 0, (size_t)nsites * 8, s));
     // (1: the INTEGER impact body stores only zero flags; every other body stores each change's)
-    if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 1, n, s));
+    if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 1, bd.ap ? ctx->pm_n : n, s));
 
     unsigned long long *misc = ctx->d_misc.as<unsigned long long>();
     const bool prof = ctx->profiling;
@@ -778,6 +778,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         a.raw = bd;
         a.raw.arena = ctx->d_arena.as<uint8_t>();
     }
+    a.pos_src = bd.ap ? ctx->pm_src : nullptr;
     uint32_t nblocks = B;
     float merge_ms = 0.f, ovf_ms = 0.f;
     for (int round = 0;; round++) {
@@ -886,7 +887,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
 // batch is applied as consecutive chunks of it, in application order -- the same result as one
 // apply, since the merge is a left fold over the changes (each INSERT sees the state its
 // predecessors left). The whole batch is validated before the first chunk commits.
-static uint64_t chunk_changes(const corro_ctx *ctx) {
+uint64_t corro_detail_chunk_changes(const corro_ctx *ctx) {
     const char *e = std::getenv("CORRO_HIP_CHUNK");  // tests: force chunking of small batches
     const uint64_t env = e ? (uint64_t)std::atoll(e) : 0ULL;
     if (env) return std::max<uint64_t>(1024, env & ~1023ULL);
@@ -985,6 +986,12 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.vsz = in->val_size;
     }
     bd.n = n;
+    if (ctx->pm_ap) {  // position mode (agent): one chunk, per-position ts
+        if (mem != CORRO_MEM_DEVICE || n > corro_detail_chunk_changes(ctx))
+            return fail(CORRO_E_INVALID, "internal: position mode needs one device-resident chunk");
+        bd.ap = ctx->pm_ap;
+        bd.ts = ctx->pm_ts;
+    }
     // long values: the batch's value bytes are appended to the arena once; every chunk's changes
     // name their bytes relative to that base. A failed batch leaves them unreferenced.
     if (in->val_off) {
@@ -1008,7 +1015,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
 
     TRY(affinity_convert(ctx, bd));
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
-    const uint64_t chunk = chunk_changes(ctx);
+    const uint64_t chunk = corro_detail_chunk_changes(ctx);
     if (n > chunk) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
         hipLaunchKernelGGL(k_validate, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, bd,

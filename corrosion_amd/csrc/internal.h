@@ -148,6 +148,12 @@ struct corro_ctx {
     // a failure after an apply's first merge write leaves the state part-merged: every later
     // call on the context fails until corro_state_reset (corro_hip.h "Failure atomicity")
     bool poisoned = false;
+    // position mode of the next apply (set by the agent around one corro_apply_batch call on its
+    // arrival-order input, agent_dev.hip): application position per input change, input index per
+    // position, per-position ts, applied count
+    const uint32_t *pm_ap = nullptr, *pm_src = nullptr;
+    const uint64_t *pm_ts = nullptr;
+    uint64_t pm_n = 0;
     bool apply_wrote = false;     // the current apply has launched its first merge kernel
     uint64_t heap_limit = 0;      // corro_ctx_set_store_limit (0: none)
     bool state_wide = false;      // some clock row holds a non-INTEGER value

@@ -75,7 +75,12 @@ struct MergeArgs {
     // column affinity: the batch's raw values (raw.conv[i] = 1: change i was staged with its
     // converted value; an incoming change still compares by its raw one, App. A.4). conv null: none.
     BatchDev raw;
+    // position mode: input index of application position p (null: p itself)
+    const uint32_t *pos_src;
 };
+
+// input index of batch position p (position mode maps it, MergeArgs::pos_src)
+__device__ inline uint32_t batch_src(const MergeArgs &a, uint32_t p) { return a.pos_src ? a.pos_src[p] : p; }
 
 // misc words
 constexpr int MISC_ERR = 0, MISC_OVF = 1, MISC_LIVE = 2, MISC_WIDE = 3, MISC_GEN = 4, MISC_WIDEQ = 5,
@@ -205,17 +210,18 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t 
     constexpr int HIST_U = 8;
     for (uint32_t base = begin; base < end; base += blockDim.x * HIST_U) {
         uint64_t pk[HIST_U];
-        uint32_t tc[HIST_U];
+        uint32_t tc[HIST_U], ap[HIST_U];
 #pragma unroll
         for (int k = 0; k < HIST_U; k++) {
             const uint32_t i = min(base + k * blockDim.x + threadIdx.x, end - 1);
             pk[k] = in.pk[i];
             tc[k] = one_table ? 0u : in.tcid[i];
+            ap[k] = in.ap ? in.ap[i] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < HIST_U; k++) {
             const uint32_t i = base + k * blockDim.x + threadIdx.x;
-            if (i < end) atomicAdd(&hist[bucket_of(tc[k] >> 16, pk[k], log2B)], 1u);
+            if (i < end && ap[k] != AP_SKIP) atomicAdd(&hist[bucket_of(tc[k] >> 16, pk[k], log2B)], 1u);
         }
     }
     __syncthreads();
@@ -432,6 +438,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                 const uint2 cl = *reinterpret_cast<const uint2 *>(in.cl + ic);
                 const uint2 sq = *reinterpret_cast<const uint2 *>(in.seq + ic);
                 const uint2 st = *reinterpret_cast<const uint2 *>(in.site + ic);
+                const uint2 ap2 = in.ap ? *reinterpret_cast<const uint2 *>(in.ap + ic) : make_uint2(i, i + 1);
                 const bool ok = i < end;
                 a.pk = pk.x; b.pk = pk.y;
                 a.cv = cv.x; b.cv = cv.y;
@@ -443,8 +450,10 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                 a.seq = sq.x; b.seq = sq.y;
                 a.site = ok ? st.x : 0xFFFFFFFFu; b.site = ok ? st.y : 0xFFFFFFFFu;
                 a.meta = b.meta = (uint32_t)CORRO_INTEGER;
-                a.pos = BATCH_POS | i;
-                b.pos = BATCH_POS | (i + 1);
+                a.pos = BATCH_POS | ap2.x;  // (AP_SKIP: not applied, see act below)
+                b.pos = BATCH_POS | ap2.y;
+                if (ap2.x == AP_SKIP) a.site = 0xFFFFFFFFu;
+                if (ap2.y == AP_SKIP) b.site = 0xFFFFFFFFu;
             }
         } else {
 #pragma unroll
@@ -480,8 +489,11 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                 a.meta = in.vt ? ((uint32_t)in.vt[i] | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8)) : (uint32_t)CORRO_INTEGER;
                 b.meta = in.vt ? ((uint32_t)in.vt[i + 1] | ((in.vl ? (uint32_t)in.vl[i + 1] : 0u) << 8))
                                : (uint32_t)CORRO_INTEGER;
-                a.pos = BATCH_POS | i;
-                b.pos = BATCH_POS | (i + 1);
+                const uint32_t pa = in.ap ? in.ap[i] : i, pb = in.ap ? in.ap[i + 1] : i + 1;
+                a.pos = BATCH_POS | pa;
+                b.pos = BATCH_POS | pb;
+                if (pa == AP_SKIP) a.site = 0xFFFFFFFFu;
+                if (pb == AP_SKIP) b.site = 0xFFFFFFFFu;
             } else if (i < end) {
                 a.pk = in.pk[i];
                 a.cv = in.cv[i];
@@ -492,7 +504,9 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                 a.cl = in.cl[i];
                 a.seq = in.seq[i];
                 a.site = in.site[i];
-                a.pos = BATCH_POS | i;
+                const uint32_t pa = in.ap ? in.ap[i] : i;
+                a.pos = BATCH_POS | pa;
+                if (pa == AP_SKIP) a.site = 0xFFFFFFFFu;
                 a.meta = in.vt ? ((uint32_t)in.vt[i] | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8)) : (uint32_t)CORRO_INTEGER;
             }
         }
@@ -500,8 +514,8 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
 #pragma unroll
         for (int u = 0; u < SCAT_U; u++) {
             const uint32_t i = base + (u / 2) * 2 * blockDim.x + 2 * threadIdx.x + (u & 1);
-            const bool act = i < end;
             Rec &r = rr[u];
+            const bool act = i < end && (!in.ap || (r.pos & 0x7FFFFFFFu) != (AP_SKIP & 0x7FFFFFFFu));
             uint32_t idx = 0;
             if (act) {
                 // a value its column's affinity converts is staged converted (affinity.hip); its
@@ -793,7 +807,10 @@ __device__ inline void gen_fold_row(const MergeArgs &a, const V &v, E &em, const
                     win = cv > lcv;
                 } else {
                     Rec xr = load_rec(v.at(x));
-                    if (a.raw.conv && a.raw.conv[pos & 0x7FFFFFFFu]) raw_value(a.raw, pos & 0x7FFFFFFFu, xr);
+                    if (a.raw.conv) {
+                        const uint32_t bi = batch_src(a, pos & 0x7FFFFFFFu);
+                        if (a.raw.conv[bi]) raw_value(a.raw, bi, xr);
+                    }
                     const Rec lr = load_rec(v.at(g.csrc[s + found]));
                     const int vc = value_cmp(xr, lr, a.arena);
                     if (vc != 0) win = vc > 0;

@@ -315,7 +315,8 @@ static __global__ void k_ovf_classify(MergeArgs a, OvfDev d) {
         if (((cid == 0 || (cl & 1u) == 0) && d.cv[x] != (int64_t)cl) || (!(pos & BATCH_POS) && cid != 0 && !(cl & 1u)))
             atomicOr(&d.rbad[d.rowid[p]], 1u);
         // a converted value compares raw-vs-stored, an order the candidate argmax cannot keep
-        if (a.raw.conv && (pos & BATCH_POS) && a.raw.conv[pos & 0x7FFFFFFFu]) atomicOr(&d.rbad[d.rowid[p]], 1u);
+        if (a.raw.conv && (pos & BATCH_POS) && a.raw.conv[batch_src(a, pos & 0x7FFFFFFFu)])
+            atomicOr(&d.rbad[d.rowid[p]], 1u);
         if (a.impact && (pos & BATCH_POS) && kd != 2)
             a.impact[pos & 0x7FFFFFFFu] = kd == 0 ? 0 : ((cid != 0 && (cl & 1u) && (L > 0 || cl > 1)) ? 2 : 1);
     }

@@ -31,8 +31,12 @@ struct BatchDev {
     const uint8_t *conv;
     const uint64_t *cv0, *cv1;
     const uint32_t *cmeta;
+    // position mode (the agent's batch in arrival order): ap[i] = change i's application position,
+    // AP_SKIP for a change that is not applied; null: position i
+    const uint32_t *ap;
     uint32_t n;
 };
+constexpr uint32_t AP_SKIP = 0xFFFFFFFFu;
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
     x ^= x >> 33;

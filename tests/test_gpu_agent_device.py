@@ -196,6 +196,14 @@ def test_device_batch_matches_restatement(seed):
     _check_against_oracle(seed, device=True)
 
 
+@pytest.mark.parametrize("seed", [7, 8])
+def test_device_batch_gather_path_matches_restatement(seed, monkeypatch):
+    """the applied batch gathered into application order (the path for inputs that are not one
+    aligned apply chunk) instead of staged in place with application positions"""
+    monkeypatch.setenv("CORRO_AGENT_GATHER", "1")
+    _check_against_oracle(seed, device=True)
+
+
 @pytest.mark.parametrize("seed", [4, 5])
 def test_host_batch_matches_restatement(seed):
     _check_against_oracle(seed, device=False)
