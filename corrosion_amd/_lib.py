@@ -16,7 +16,7 @@ CORRO_OK = 0
 ERRORS = {-1: "CORRO_E_INVALID", -2: "CORRO_E_NOMEM", -3: "CORRO_E_DEVICE",
           -4: "CORRO_E_UNKNOWN_TABLE", -5: "CORRO_E_UNKNOWN_COLUMN", -6: "CORRO_E_RANGE",
           -7: "CORRO_E_NO_DEVICE"}
-CORRO_MEM_HOST, CORRO_MEM_DEVICE = 0, 1
+CORRO_MEM_HOST, CORRO_MEM_DEVICE, CORRO_MEM_DEVICE_HEADERS = 0, 1, 2
 CORRO_PAYLOAD_SYNC, CORRO_PAYLOAD_UNI = 0, 1
 
 # every symbol include/corro_hip.h declares (checked by tests/test_abi.py)
@@ -92,7 +92,7 @@ class ExtractOut(C.Structure):
 class Metrics(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("applies", "changes", "overflow_rounds", "deferred_rounds",
                                           "region_growths", "heap_growths", "state_rows", "state_records",
-                                          "max_batch")] + [("apply_seconds", C.c_double)]
+                                          "max_batch")] + [("apply_seconds", C.c_double), ("arena_bytes", C.c_uint64)]
 
 
 class GapsIn(C.Structure):

@@ -347,6 +347,297 @@ struct ActorWork {
     std::string err;
 };
 
+Range versions_of(const corro_changeset &c) {
+    if (c.kind == CORRO_CS_EMPTY_SET) return {0, 0};  // Changeset::versions() dummy (broadcast.rs:176-178)
+    return {c.version_start, c.kind == CORRO_CS_FULL ? c.version_start : c.version_end};
+}
+const Range *seqs_of(const corro_changeset &c, Range &r) {
+    if (c.kind != CORRO_CS_FULL) return nullptr;
+    r = {c.seq_start, c.seq_end};
+    return &r;
+}
+bool is_complete(const corro_changeset &c) { return c.kind != CORRO_CS_FULL || (c.seq_start == 0 && c.seq_end == c.last_seq); }
+bool is_empty(const corro_changeset &c) { return c.kind != CORRO_CS_FULL || c.change_count == 0; }
+
+// Where the per-actor walk reads changeset i and records its outcome: the caller's headers and
+// out->known (host headers), or host copies of the slow actors' changesets (device headers).
+struct CsView {
+    const corro_changeset *cs;
+    const uint8_t *bad;   // unknown-name screen
+    int32_t *known;
+    uint8_t *flag;        // 1 = merged by this call
+};
+
+// One actor's passes 1 and 2 (util.rs:704-884) over its changesets w.idx (arrival order) unless it
+// is fast (its versions are the runs given), then its gap snapshot (:894-932) and partials.
+template <class RowOf>
+void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::vector<Range> &fast_runs, RowOf &&row_of) {
+    corro::Booked &booked = *w.booked;
+    const bool had_max = w.had_max;
+    const uint64_t max = w.max;
+    RangeSet versions;
+    if (w.fast) {
+        for (const Range &r : fast_runs) versions.insert(r.first, r.second);
+    } else {
+        // pass 1: batch-local dedup of (versions, seqs), then versions the actor already holds
+        std::vector<uint64_t> unknown;
+        unknown.reserve(w.nidx);
+        std::set<std::tuple<uint64_t, uint64_t, int, uint64_t, uint64_t>> seen;
+        for (uint64_t k = 0; k < w.nidx; k++) {
+            const uint64_t i = w.idx[k];
+            const Range vr = versions_of(v.cs[i]);
+            Range sq;
+            const Range *seqs = seqs_of(v.cs[i], sq);
+            if (!seen.emplace(vr.first, vr.second, seqs ? 1 : 0, seqs ? sq.first : 0, seqs ? sq.second : 0).second)
+                continue;
+            if (booked.contains_all(vr.first, vr.second, seqs)) continue;
+            unknown.push_back(i);
+        }
+        // pass 2 (the bookie is not written until the call commits, so pass 1's contains_all stands)
+        SeenMap seen_local;
+        for (uint64_t i : unknown) {
+            const corro_changeset &c = v.cs[i];
+            const Range vr = versions_of(c);
+            Range sq;
+            const Range *seqs = seqs_of(c, sq);
+            if (seen_local.all_seen(vr, seqs)) continue;
+            std::optional<corro::PartialVersion> partial;
+            if (is_complete(c) && is_empty(c)) {
+                // process_empty_version only when end > booked max (util.rs:810-824)
+                if (!had_max || vr.second > max) w.set_dbv.push_back(vr.second);
+                v.known[i] = CORRO_KNOWN_CLEARED;
+            } else {
+                if (seqs && seqs->second < seqs->first) continue;  // invalid seqs (util.rs:826-831)
+                if (v.bad[i]) {  // the INSERT fails, the version's SAVEPOINT rolls back (util.rs:839-860)
+                    v.known[i] = CORRO_E_UNKNOWN_COLUMN;
+                    continue;
+                }
+                if (is_complete(c)) {
+                    v.flag[i] = 1;
+                    w.nspans++;
+                    w.nchanges += c.change_count;
+                    w.ts |= c.ts != 0;
+                    v.known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
+                } else {
+                    corro::PartialVersion p;
+                    if (process_incomplete(bk, w.st, c, [&](uint64_t k) { return row_of(c, i, k); }, p) != CORRO_OK) {
+                        v.known[i] = CORRO_E_INVALID;
+                        continue;
+                    }
+                    partial = p;
+                    v.known[i] = CORRO_KNOWN_PARTIAL;
+                }
+            }
+            seen_local.insert(vr, partial);
+            versions.insert(vr.first, vr.second);
+            if (partial) w.partials.emplace_back(vr.first, *partial);
+        }
+    }
+    if (versions.empty()) return;
+    // gap bookkeeping on a copy of the actor's Booked (VersionsSnapshot, agent.rs:1108-1235): an
+    // INSERT that would violate __corro_bookkeeping_gaps' key fails the whole call before the
+    // merge has touched the state, as the transaction's rollback would undo it (util.rs:894-936)
+    w.next = booked;
+    w.has_next = true;
+    if (!w.next.insert_db(versions, nullptr, nullptr)) {
+        w.rc = CORRO_E_INVALID;
+        w.err = "UNIQUE constraint failed: __corro_bookkeeping_gaps.start";
+        return;
+    }
+    for (auto &[version, pv] : w.partials) {
+        const corro::PartialVersion &p = w.next.insert_partial(version, pv);
+        if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
+    }
+}
+
+}  // namespace
+
+
+namespace {
+
+// corro_process_multiple_changes with CORRO_MEM_DEVICE_HEADERS: the header passes on the device
+// (agent_dev_headers), the host walks only slow actors' headers, then the same merge / impacts /
+// commit as the host-header path.
+int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *dcs, uint64_t ncs,
+                        const corro_changes *in, corro_process_out *out) {
+    static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    std::string prof_line;
+    auto stage = [&](const char *name) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        prof_line += std::string(" ") + name + "=" +
+                     std::to_string(std::chrono::duration<double, std::milli>(t - t_last).count()).substr(0, 6);
+        t_last = t;
+    };
+    const uint64_t nchanges = in ? in->n : 0;
+    corro::AgentPinned P{};
+    TRY_RC(corro::agent_dev_begin(ctx, ncs, nchanges, &P));
+    const uint32_t nsites = corro::agent_site_count(ctx);
+    std::vector<ActorId> site_id(nsites);
+    std::vector<int64_t> site_max(nsites, -1);
+    for (uint32_t t = 0; t < nsites; t++) {
+        corro::agent_site_id(ctx, t, site_id[t].data());
+        auto it = bk->actors.find(site_id[t]);
+        if (it != bk->actors.end() && it->second.has_max) site_max[t] = (int64_t)it->second.max;
+    }
+    corro_changes dv{};
+    if (in) dv = *in;
+    corro::DevHdrResult R;
+    TRY_RC(corro::agent_dev_headers(ctx, dcs, ncs, nchanges ? &dv : nullptr, site_max, out->known, R));
+    if (R.err & 1) return fail(CORRO_E_INVALID, "changeset change span outside the batch");
+    if (R.err & 2) return fail(CORRO_E_INVALID, "changeset site ordinal is not registered (or actor_id is NULL)");
+    stage("headers");
+
+    // actors of the call; the slow ones' headers come to the host (sorted order = grouped by actor,
+    // arrival order inside)
+    std::vector<ActorWork> work;
+    std::vector<int64_t> work_of(nsites, -1);
+    std::vector<std::pair<uint32_t, uint32_t>> slow_ranges;
+    for (uint32_t t = 0; t < nsites; t++) {
+        const corro::DevHdrSite &g = R.sites[t];
+        if (g.gstart == 0xFFFFFFFFu) continue;
+        work_of[t] = (int64_t)work.size();
+        work.emplace_back();
+        ActorWork &w = work.back();
+        w.site = t;
+        w.id = site_id[t];
+        w.fast = !g.slow;
+        w.nidx = g.gend - g.gstart + 1;
+        if (g.slow) slow_ranges.emplace_back(g.gstart, g.gend + 1);
+    }
+    for (ActorWork &w : work) {  // Bookie::ensure
+        w.booked = &bk->actors[w.id];
+        bk->site_of[w.id] = w.site;
+        w.had_max = w.booked->has_max;
+        w.max = w.booked->max;
+    }
+    std::vector<corro_changeset> hcs;
+    std::vector<uint32_t> hidx;
+    std::vector<uint8_t> hbad, hflag;
+    std::vector<int32_t> hknown;
+    std::vector<uint64_t> local;
+    std::map<uint64_t, uint64_t> inc_row;  // slow changeset (local index) -> first fetched row
+    corro::HostSpanRows inc;
+    if (!slow_ranges.empty()) {
+        TRY_RC(corro::agent_dev_slow_headers(ctx, dcs, slow_ranges, hcs, hidx, hbad));
+        hflag.assign(hcs.size(), 0);
+        hknown.assign(hcs.size(), CORRO_KNOWN_SKIPPED);
+        local.resize(hcs.size());
+        for (uint64_t k = 0; k < local.size(); k++) local[k] = k;
+        uint64_t o = 0;
+        for (ActorWork &w : work)  // (work and slow_ranges are both in site-ordinal order)
+            if (!w.fast) {
+                w.idx = local.data() + o;
+                o += w.nidx;
+            }
+        std::vector<corro::AgentSpan> sp;
+        uint64_t r = 0;
+        for (uint64_t k = 0; k < hcs.size(); k++)
+            if (hcs[k].kind == CORRO_CS_FULL && hcs[k].change_count && !is_complete(hcs[k]) && !hbad[k]) {
+                inc_row[k] = r;
+                sp.push_back({hcs[k].change_off, r, hcs[k].change_count, hcs[k].ts});
+                r += hcs[k].change_count;
+            }
+        if (!sp.empty()) TRY_RC(corro::agent_dev_fetch(ctx, &dv, sp, inc));
+    }
+    auto row_of = [&](const corro_changeset &c, uint64_t ci, uint64_t k) -> HostRow {
+        const uint64_t j = inc_row.at(ci) + k;
+        HostRow r;
+        r.pk = inc.pk[j];
+        r.tcid = inc.tcid[j];
+        r.cv = inc.cv[j];
+        r.dbv = inc.dbv[j];
+        r.cl = inc.cl[j];
+        r.seq = inc.seq[j];
+        r.site = inc.site[j];
+        r.v0 = inc.v0[j];
+        r.v1 = in->val1 ? inc.v1[j] : 0;
+        r.vt = inc.vt[j];
+        r.vl = in->val_len ? inc.vl[j] : 0;
+        r.ts = in->ts ? inc.ts[j] : c.ts;
+        if (inc.lv_len[j])
+            r.lv.assign(reinterpret_cast<const char *>(inc.lv_data.data() + inc.lv_off[j]), inc.lv_len[j]);
+        return r;
+    };
+    std::vector<std::vector<Range>> fast_runs(work.size());
+    for (size_t r = 0; r < R.run_site.size(); r++)
+        fast_runs[(size_t)work_of[R.run_site[r]]].emplace_back(R.run_start[r], R.run_end[r]);
+    const CsView view{hcs.data(), hbad.data(), hknown.data(), hflag.data()};
+    run_parallel(work.size(), [&](size_t k) { run_actor_walk(bk, work[k], view, fast_runs[k], row_of); });
+    for (ActorWork &w : work)
+        if (w.rc != CORRO_OK) return fail(w.rc, w.err);
+    uint64_t nspans = R.nspans, nb = R.nchanges;
+    for (const ActorWork &w : work) {
+        nspans += w.nspans;
+        nb += w.nchanges;
+    }
+    if (!hcs.empty()) TRY_RC(corro::agent_dev_put_slow(ctx, hidx, hflag, hknown, out->known));
+    stage("actors");
+
+    const uint32_t ntables = corro::agent_table_count(ctx);
+    std::vector<uint64_t> committed(ntables, 0);
+    if (nb || out->impactful) {
+        corro_changes batch{};
+        const uint8_t *imp = nullptr;
+        corro::AgentPositions pm{};
+        if (nb) {
+            bool gathered = false;
+            TRY_RC(corro::agent_dev_batch_sorted(ctx, &dv, ncs, nspans, nb, R.ts_any, &batch, &gathered, &pm));
+            stage(gathered ? "order+gather" : (pm.on ? "order+positions" : "order"));
+            int rc = CORRO_OK;
+            uint8_t *ib = corro::agent_dev_impact_buf(ctx, nb, &rc);
+            if (rc != CORRO_OK) return rc;
+            corro_apply_out ao{};
+            ao.impact = ib;
+            corro::agent_dev_set_positions(ctx, pm.on ? &pm : nullptr);
+            rc = corro_apply_batch(ctx, &batch, CORRO_MEM_DEVICE, &ao);
+            corro::agent_dev_set_positions(ctx, nullptr);
+            if (rc != CORRO_OK) {  // the transaction fails as a whole (util.rs:849-855)
+                (void)corro::agent_dev_clear_known(ctx, out->known, ncs);
+                return rc;
+            }
+            imp = ib;
+            stage("apply");
+        }
+        TRY_RC(corro::agent_dev_impacts(ctx, imp, batch.table_cid, pm.on, nb, P, ncs, nspans, out->impactful, nchanges,
+                                        CORRO_MEM_DEVICE, ntables));
+        for (uint32_t t = 0; t < ntables; t++) committed[t] += P.committed[t];
+        stage("impacts");
+    }
+
+    // commit
+    for (ActorWork &w : work)
+        for (uint64_t version : w.set_dbv) TRY_RC(corro::set_db_version(ctx, w.site, version));
+    for (ActorWork &w : work) {
+        for (const HostRow &r : w.st.buffered) {  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
+            bk->buffered[{r.site, r.dbv}].emplace(r.seq, r);
+            if ((r.tcid >> 16) < ntables) committed[r.tcid >> 16]++;
+        }
+        for (auto &[key, sb] : w.st.seqbook) bk->seqbook[key] = sb;
+    }
+    const bool clear_meta = !bk->buffered.empty() || !bk->seqbook.empty();
+    std::vector<std::pair<uint32_t, uint64_t>> sv;
+    TRY_RC(corro::agent_dev_commit_headers(ctx, ncs, out->known, clear_meta ? &sv : nullptr));
+    for (auto &[site, v] : sv) clear_buffered(bk, site, v, v);  // check_buffered_meta_to_clear
+    std::vector<size_t> order(work.size());
+    for (size_t k = 0; k < order.size(); k++) order[k] = k;
+    std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return work[x].id < work[y].id; });
+    uint64_t nready = 0;
+    for (size_t k : order) {
+        ActorWork &w = work[k];
+        if (w.has_next) *w.booked = std::move(w.next);
+        for (uint64_t v : w.ready) bk->ready.emplace_back(w.id, v);
+        nready += w.ready.size();
+    }
+    out->n_ready = nready;
+    corro_detail_add_committed(ctx, committed.data(), committed.size());
+    stage("commit");
+    if (prof) fprintf(stderr, "[corro agent dev] ncs=%llu spans=%llu changes=%llu slow=%zu ms:%s\n", (unsigned long long)ncs,
+                      (unsigned long long)nspans, (unsigned long long)nb, hcs.size(), prof_line.c_str());
+    return CORRO_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -355,24 +646,12 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
                                    const corro_changes *in, int mem, corro_process_out *out) {
     if (!ctx || !bk || (ncs && !cs) || !out) return fail(CORRO_E_INVALID, "NULL argument");
     if (ncs && (!out->known)) return fail(CORRO_E_INVALID, "out->known is required");
-    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
+    if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE && mem != CORRO_MEM_DEVICE_HEADERS)
+        return fail(CORRO_E_INVALID, "bad mem kind");
     const uint64_t nchanges = in ? in->n : 0;
     if (nchanges && !in->table_cid) return fail(CORRO_E_INVALID, "a required batch array is NULL");
     out->n_ready = 0;
-
-    auto versions_of = [](const corro_changeset &c) -> Range {
-        if (c.kind == CORRO_CS_EMPTY_SET) return {0, 0};  // Changeset::versions() dummy (broadcast.rs:176-178)
-        return {c.version_start, c.kind == CORRO_CS_FULL ? c.version_start : c.version_end};
-    };
-    auto seqs_of = [](const corro_changeset &c, Range &r) -> const Range * {
-        if (c.kind != CORRO_CS_FULL) return nullptr;
-        r = {c.seq_start, c.seq_end};
-        return &r;
-    };
-    auto is_complete = [](const corro_changeset &c) {
-        return c.kind != CORRO_CS_FULL || (c.seq_start == 0 && c.seq_end == c.last_seq);
-    };
-    auto is_empty = [](const corro_changeset &c) { return c.kind != CORRO_CS_FULL || c.change_count == 0; };
+    if (mem == CORRO_MEM_DEVICE_HEADERS) return process_dev_headers(ctx, bk, cs, ncs, in, out);
 
     // CORRO_AGENT_PROFILE=1: host-side stage times of each call on stderr (tools)
     static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;
@@ -386,7 +665,7 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
         t_last = t;
     };
     corro::AgentPinned P{};
-    TRY_RC(corro::agent_dev_begin(ctx, ncs, &P));
+    TRY_RC(corro::agent_dev_begin(ctx, ncs, nchanges, &P));
     stage("begin");
 
     // Host passes walk the headers in ARRIVAL order (sequential chunks in parallel threads): an actor's
@@ -614,86 +893,8 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     std::vector<std::vector<Range>> fast_runs(work.size());
     for (size_t k = 0; k < nchunk; k++)
         for (auto &[wi, r] : cout[k].runs) fast_runs[wi].push_back(r);
-    auto run_actor = [&](size_t wi) {
-        ActorWork &w = work[wi];
-        corro::Booked &booked = *w.booked;
-        const bool had_max = w.had_max;
-        const uint64_t max = w.max;
-        RangeSet versions;
-        if (w.fast) {
-            for (const Range &r : fast_runs[wi]) versions.insert(r.first, r.second);
-        } else {
-            // pass 1: batch-local dedup of (versions, seqs), then versions the actor already holds
-            std::vector<uint64_t> unknown;
-            unknown.reserve(w.nidx);
-            std::set<std::tuple<uint64_t, uint64_t, int, uint64_t, uint64_t>> seen;
-            for (uint64_t k = 0; k < w.nidx; k++) {
-                const uint64_t i = w.idx[k];
-                const Range v = versions_of(cs[i]);
-                Range sq;
-                const Range *seqs = seqs_of(cs[i], sq);
-                if (!seen.emplace(v.first, v.second, seqs ? 1 : 0, seqs ? sq.first : 0, seqs ? sq.second : 0).second)
-                    continue;
-                if (booked.contains_all(v.first, v.second, seqs)) continue;
-                unknown.push_back(i);
-            }
-            // pass 2 (the bookie is not written until the call commits, so pass 1's contains_all stands)
-            SeenMap seen_local;
-            for (uint64_t i : unknown) {
-                const corro_changeset &c = cs[i];
-                const Range v = versions_of(c);
-                Range sq;
-                const Range *seqs = seqs_of(c, sq);
-                if (seen_local.all_seen(v, seqs)) continue;
-                std::optional<corro::PartialVersion> partial;
-                if (is_complete(c) && is_empty(c)) {
-                    // process_empty_version only when end > booked max (util.rs:810-824)
-                    if (!had_max || v.second > max) w.set_dbv.push_back(v.second);
-                    out->known[i] = CORRO_KNOWN_CLEARED;
-                } else {
-                    if (seqs && seqs->second < seqs->first) continue;  // invalid seqs (util.rs:826-831)
-                    if (bad[i]) {  // the INSERT fails, the version's SAVEPOINT rolls back (util.rs:839-860)
-                        out->known[i] = CORRO_E_UNKNOWN_COLUMN;
-                        continue;
-                    }
-                    if (is_complete(c)) {
-                        P.flag[i] = 1;
-                        w.nspans++;
-                        w.nchanges += c.change_count;
-                        w.ts |= c.ts != 0;
-                        out->known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
-                    } else {
-                        corro::PartialVersion p;
-                        if (process_incomplete(bk, w.st, c, [&](uint64_t k) { return row_of(c, i, k); }, p) !=
-                            CORRO_OK) {
-                            out->known[i] = CORRO_E_INVALID;
-                            continue;
-                        }
-                        partial = p;
-                        out->known[i] = CORRO_KNOWN_PARTIAL;
-                    }
-                }
-                seen_local.insert(v, partial);
-                versions.insert(v.first, v.second);
-                if (partial) w.partials.emplace_back(v.first, *partial);
-            }
-        }
-        if (versions.empty()) return;
-        // gap bookkeeping on a copy of the actor's Booked (VersionsSnapshot, agent.rs:1108-1235): an
-        // INSERT that would violate __corro_bookkeeping_gaps' key fails the whole call before the
-        // merge has touched the state, as the transaction's rollback would undo it (util.rs:894-936)
-        w.next = booked;
-        w.has_next = true;
-        if (!w.next.insert_db(versions, nullptr, nullptr)) {
-            w.rc = CORRO_E_INVALID;
-            w.err = "UNIQUE constraint failed: __corro_bookkeeping_gaps.start";
-            return;
-        }
-        for (auto &[version, pv] : w.partials) {
-            const corro::PartialVersion &p = w.next.insert_partial(version, pv);
-            if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
-        }
-    };
+    const CsView view{cs, bad, out->known, P.flag};
+    auto run_actor = [&](size_t wi) { run_actor_walk(bk, work[wi], view, fast_runs[wi], row_of); };
     run_parallel(work.size(), [&](size_t k) { run_actor(k); });
     for (ActorWork &w : work)
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);

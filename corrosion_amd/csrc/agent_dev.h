@@ -33,7 +33,7 @@ struct AgentPinned {
     uint8_t *flag, *bad, *any;
     uint64_t *committed;  // per table
 };
-int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, AgentPinned *p);
+int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, uint64_t nchanges, AgentPinned *p);
 
 // Device view of the input: `in` itself for CORRO_MEM_DEVICE, else every field copied to device
 // scratch (val_data too). The view stays valid until the call ends.
@@ -88,6 +88,48 @@ uint8_t *agent_dev_impact_buf(corro_ctx *ctx, uint64_t n, int *rc);
 int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tcid, bool tcid_by_src, uint64_t nbatch,
                       const AgentPinned &p, uint64_t ncs, uint64_t nspans, uint8_t *impactful, uint64_t nin, int mem,
                       uint32_t ntables);
+
+// ---- device-resident headers (CORRO_MEM_DEVICE_HEADERS) -----------------------------------------
+// The changeset headers, out->known and out->impactful live on the device. One pass per changeset
+// (span check, unknown-name screen, columns), one stable sort by site rank (the application order
+// and the per-actor grouping at once), one pass per sorted slot that decides every "fast" actor
+// (each of its changesets a complete Full version, strictly ascending in arrival order, all above
+// the actor's booked max) on the device: flags, known, empty versions, and the actor's applied
+// version runs for the gap bookkeeping. The host gets per-site summaries and the runs; it walks
+// only the headers of the other ("slow") actors, fetched in sorted order.
+struct DevHdrSite {
+    uint32_t gstart, gend;   // sorted slots [gstart, gend] of the site's changesets (gstart ~0: none)
+    uint8_t slow;            // 1: the host walks this actor's changesets
+};
+struct DevHdrResult {
+    uint32_t err;            // bit 0 span outside the batch, bit 1 site ordinal not registered
+    bool ts_any;             // some changeset has a non-zero ts
+    uint64_t nspans, nchanges;   // flagged (fast actors) changesets and their changes
+    std::vector<DevHdrSite> sites;             // per site ordinal
+    std::vector<uint32_t> run_site;            // fast actors' version runs, grouped by site, ascending
+    std::vector<uint64_t> run_start, run_end;
+};
+// site_max[s] = the actor's booked max (-1: none); dknown: device, ncs entries
+int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, const corro_changes *dv,
+                      const std::vector<int64_t> &site_max, int32_t *dknown, DevHdrResult &res);
+// host copies of the changesets in sorted slots [lo, hi) of each (lo, hi) range, concatenated, with
+// their arrival index and bad flag
+int agent_dev_slow_headers(corro_ctx *ctx, const corro_changeset *dcs, const std::vector<std::pair<uint32_t, uint32_t>> &ranges,
+                           std::vector<corro_changeset> &hcs, std::vector<uint32_t> &idx, std::vector<uint8_t> &bad);
+// the host's decisions for slow changesets: flag[idx[k]] = flag[k], known[idx[k]] = known[k]
+int agent_dev_put_slow(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
+                       const std::vector<int32_t> &known, int32_t *dknown);
+// the applied batch in sorted order (flagged changesets only), like agent_dev_batch
+int agent_dev_batch_sorted(corro_ctx *ctx, const corro_changes *dv, uint64_t ncs, uint64_t nspans, uint64_t nbatch,
+                           bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm);
+// after a successful merge: known of flagged changesets (Current / Cleared by p.any on the device),
+// crsql_set_db_version of the fast actors' empty versions; *flagged_sv (optional) = (site, version)
+// of every flagged changeset (host, for check_buffered_meta_to_clear)
+int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown,
+                             std::vector<std::pair<uint32_t, uint64_t>> *flagged_sv);
+
+// every known entry back to Skipped (a failed call)
+int agent_dev_clear_known(corro_ctx *ctx, int32_t *dknown, uint64_t ncs);
 
 // The registered 16-byte id of a site ordinal (false: not registered).
 bool agent_site_id(corro_ctx *ctx, uint32_t site, uint8_t out[16]);

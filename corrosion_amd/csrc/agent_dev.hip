@@ -3,12 +3,12 @@
 // /root/reference/crates/corro-agent/src/agent/util.rs:765-884 walks every change of every
 // changeset on the host (a SAVEPOINT per version, an INSERT per change). Here the host walks only
 // the changeset headers; each per-change pass is one kernel over the caller's device batch:
-//   k_cs_bad       one wave per changeset: does any change name an unknown table/column (the INSERT
+//   k_cs_bad       one lane per changeset: does any change name an unknown table/column (the INSERT
 //                  would fail and the version's SAVEPOINT roll back, util.rs:839-860)?
 //   k_span_gather  one wave per applied changeset: its changes into the applied batch (skipped when
 //                  the applied changesets are one contiguous run of the input: zero-copy)
 //   k_first_imp    the first batch position whose INSERT grew crsql_rows_impacted()
-//   k_impactful    one wave per applied changeset: impactful flags with the transaction-cumulative
+//   k_impactful    per application position (k_span_blocks): impactful flags with the transaction-cumulative
 //                  counter rule (util.rs:1218-1261), per-changeset "any", per-table committed counts
 #include <hip/hip_runtime.h>
 
@@ -40,18 +40,32 @@ dim3 wave_grid(uint64_t nspans) {
     return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nspans + 3) / 4, AG_GRID_MAX)));
 }
 
+// one lane per changeset: its span's table_cids, 16-B loads when the span start is 4-aligned
+// (a wave per changeset leaves each lane one 4-B load per 64 changes: latency-bound)
+__device__ inline bool span_has_unknown(const uint32_t *__restrict__ tcid, uint64_t o, uint64_t c) {
+    bool b = false;
+    uint64_t k = 0;
+    if ((o & 3) == 0) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(tcid + o);
+        for (; k + 16 <= c; k += 16) {
+            uint4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) x[u] = q[k / 4 + u];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                b |= (x[u].x == CORRO_TCID_UNKNOWN) | (x[u].y == CORRO_TCID_UNKNOWN) | (x[u].z == CORRO_TCID_UNKNOWN) |
+                     (x[u].w == CORRO_TCID_UNKNOWN);
+        }
+    }
+    for (; k < c; k++) b |= tcid[o + k] == CORRO_TCID_UNKNOWN;
+    return b;
+}
+
 __global__ void __launch_bounds__(AG_T) k_cs_bad(const uint32_t *__restrict__ tcid, const uint64_t *__restrict__ off,
                                                   const uint64_t *__restrict__ cnt, uint64_t nspans,
                                                   uint8_t *__restrict__ bad) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w0 = ((uint64_t)blockIdx.x * AG_T + threadIdx.x) >> 6, nw = (uint64_t)gridDim.x * (AG_T / 64);
-    for (uint64_t j = w0; j < nspans; j += nw) {
-        const uint64_t o = off[j], c = cnt[j];
-        bool b = false;
-        for (uint64_t k = lane; k < c; k += 64) b |= tcid[o + k] == CORRO_TCID_UNKNOWN;
-        b = __any(b);
-        if (lane == 0) bad[j] = b ? 1 : 0;
-    }
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < nspans; j += (uint64_t)gridDim.x * AG_T)
+        bad[j] = span_has_unknown(tcid, off[j], cnt[j]) ? 1 : 0;
 }
 
 struct GatherArgs {
@@ -120,55 +134,150 @@ __global__ void __launch_bounds__(AG_T) k_first_imp(const uint8_t *__restrict__ 
     if ((threadIdx.x & 63) == 0 && best != ~0ULL) atomicMin(first, best);
 }
 
+// Per-position passes over the applied batch. Application positions [0, nbatch) are covered by the
+// spans in order (s_dst ascending, every count >= 1). A workgroup takes SPB consecutive positions:
+// k_span_blocks gives it its first span, it stages the spans it overlaps in LDS and each lane finds
+// the span of its positions by binary search there -- loads and stores run along positions (and
+// along input indices inside a span), not one wave-latency chain per span.
+constexpr uint32_t SPB = 2048;                  // positions per workgroup
+constexpr uint32_t SP_PER = SPB / AG_T;         // positions per lane
+
+__global__ void __launch_bounds__(AG_T) k_span_blocks(const uint64_t *__restrict__ s_dst, const uint64_t *__restrict__ s_cnt,
+                                                       uint64_t nspans, uint32_t *__restrict__ first) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < nspans; j += (uint64_t)gridDim.x * AG_T) {
+        const uint64_t d = s_dst[j], c = s_cnt[j];
+        for (uint64_t b = (d + SPB - 1) / SPB; b * SPB < d + c; b++) first[b] = (uint32_t)j;
+    }
+}
+
+struct SpanTile {
+    uint32_t j0, ns;        // first span, spans staged
+    uint64_t p0, p1;        // positions [p0, p1)
+    bool head0;             // the first staged span starts inside [p0, p1)
+};
+
+// stage the spans of workgroup blockIdx.x: dst (relative to p0, clamped at 0), src, and optionally ts / cs
+__device__ inline SpanTile stage_spans(const uint32_t *__restrict__ first, uint64_t nspans, uint64_t nbatch,
+                                       const uint64_t *__restrict__ s_dst, const uint64_t *__restrict__ s_src,
+                                       const uint64_t *__restrict__ s_ts, const uint32_t *__restrict__ s_cs,
+                                       uint32_t *l_dst, uint64_t *l_src, uint64_t *l_ts, uint32_t *l_cs) {
+    const uint64_t nblocks = (nbatch + SPB - 1) / SPB;
+    SpanTile t;
+    t.p0 = (uint64_t)blockIdx.x * SPB;
+    t.p1 = t.p0 + SPB < nbatch ? t.p0 + SPB : nbatch;
+    t.j0 = first[blockIdx.x];
+    const uint32_t j1 = blockIdx.x + 1 < nblocks ? first[blockIdx.x + 1] : (uint32_t)(nspans - 1);
+    t.ns = j1 - t.j0 + 1;
+    t.head0 = s_dst[t.j0] == t.p0;
+    for (uint32_t k = threadIdx.x; k < t.ns; k += AG_T) {
+        const uint64_t d = s_dst[t.j0 + k];
+        l_dst[k] = d > t.p0 ? (uint32_t)(d - t.p0) : 0u;
+        l_src[k] = s_src[t.j0 + k] + (d < t.p0 ? t.p0 - d : 0);  // input index of the span's first position here
+        if (l_ts) l_ts[k] = s_ts[t.j0 + k];
+        if (l_cs) l_cs[k] = s_cs[t.j0 + k];
+    }
+    __syncthreads();
+    return t;
+}
+
+// local span of relative position r: the last k with l_dst[k] <= r
+__device__ inline uint32_t span_of(const uint32_t *l_dst, uint32_t ns, uint32_t r) {
+    uint32_t lo = 0, hi = ns;  // l_dst[lo] <= r < l_dst[hi]
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (l_dst[m] <= r) lo = m;
+        else hi = m;
+    }
+    return lo;
+}
+
 struct ImpArgs {
     const uint8_t *imp;
     const uint32_t *tcid;
-    const uint64_t *s_src, *s_dst, *s_cnt;
+    const uint64_t *s_src, *s_dst;
     const uint32_t *s_cs;              // changeset of each span
-    uint64_t nspans;
+    const uint32_t *first_span;        // k_span_blocks
+    uint64_t nspans, nbatch;
     const unsigned long long *first;
     uint8_t *out;                      // impactful per input change (nullable)
     uint8_t *any;                      // per changeset
-    unsigned long long *committed;     // per table
+    unsigned long long *committed;     // per table (ntables > IMP_TLDS: atomics)
+    unsigned long long *part;          // per (workgroup, table) counts (ntables <= IMP_TLDS)
     uint32_t ntables;
     bool tcid_by_src;                  // tcid indexed by input index (position mode), else by batch position
 };
+constexpr uint32_t IMP_TLDS = 32;
 
+// impactful flag of every applied change: its own growth, except a version's first change, which
+// takes the transaction-cumulative counter (any growth at or before it in the batch)
 __global__ void __launch_bounds__(AG_T) k_impactful(ImpArgs a) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w0 = ((uint64_t)blockIdx.x * AG_T + threadIdx.x) >> 6, nw = (uint64_t)gridDim.x * (AG_T / 64);
+    __shared__ uint32_t l_dst[SPB + 1];
+    __shared__ uint64_t l_src[SPB + 1];
+    __shared__ uint32_t l_cs[SPB + 1];
+    __shared__ uint8_t l_any[SPB + 1];
+    __shared__ uint32_t l_cnt[IMP_TLDS];
+    const SpanTile t = stage_spans(a.first_span, a.nspans, a.nbatch, a.s_dst, a.s_src, nullptr, a.s_cs, l_dst, l_src,
+                                   nullptr, l_cs);
+    for (uint32_t k = threadIdx.x; k < t.ns; k += AG_T) l_any[k] = 0;
+    if (threadIdx.x < IMP_TLDS) l_cnt[threadIdx.x] = 0;
+    __syncthreads();
     const unsigned long long first = *a.first;
-    // committed counts: the wave's running (table, count), one atomic per table change and at the end
-    uint32_t run_t = 0xFFFFFFFFu;
-    unsigned long long run_c = 0;
-    for (uint64_t j = w0; j < a.nspans; j += nw) {
-        const uint64_t s = a.s_src[j], d = a.s_dst[j], c = a.s_cnt[j];
-        bool anyb = false;
-        for (uint64_t base = 0; base < c; base += 64) {  // (wave-uniform trip count)
-            const uint64_t k = base + lane;
-            const bool act = k < c;
-            bool hit = false;
-            if (act) hit = k == 0 ? first <= d : a.imp[d + k] != 0;
-            if (act && a.out) a.out[s + k] = hit ? 1 : 0;
-            const uint32_t t = hit ? a.tcid[(a.tcid_by_src ? s : d) + k] >> 16 : 0xFFFFFFFFu;
-            unsigned long long m = __ballot(hit && t < a.ntables);
-            anyb |= __ballot(hit) != 0;
-            while (m) {
-                const uint32_t leader = (uint32_t)__ffsll(m) - 1;
-                const uint32_t tl = __shfl(t, leader);
-                const unsigned long long mt = __ballot(hit && t == tl);
-                if (tl != run_t) {
-                    if (lane == 0 && run_c) atomicAdd(&a.committed[run_t], run_c);
-                    run_t = tl;
-                    run_c = 0;
-                }
-                run_c += (unsigned long long)__popcll(mt);
-                m &= ~mt;
+    const bool lds_t = a.ntables <= IMP_TLDS;
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll 2
+    for (uint32_t u = 0; u < SP_PER; u++) {
+        const uint32_t r = u * AG_T + threadIdx.x;
+        const uint64_t p = t.p0 + r;
+        const bool act = p < t.p1;
+        bool hit = false;
+        uint32_t tb = 0xFFFFFFFFu;
+        if (act) {
+            const uint32_t k = span_of(l_dst, t.ns, r);
+            const uint64_t src = l_src[k] + (r - l_dst[k]);
+            const bool head = r == l_dst[k] && (k > 0 || t.head0);
+            hit = head ? first <= p : a.imp[p] != 0;
+            if (a.out) a.out[src] = hit ? 1 : 0;
+            if (hit) {
+                l_any[k] = 1;
+                tb = a.tcid[a.tcid_by_src ? src : p] >> 16;
             }
         }
-        if (lane == 0) a.any[a.s_cs[j]] = anyb ? 1 : 0;
+        if (tb >= a.ntables) continue;
+        if (lds_t) {
+            atomicAdd(&l_cnt[tb], 1u);
+        } else {  // wave-aggregated global atomics per table
+            unsigned long long m = __ballot(tb < a.ntables);
+            while (m) {
+                const uint32_t leader = (uint32_t)__ffsll(m) - 1;
+                const uint32_t tl = __shfl(tb, leader);
+                const unsigned long long mt = __ballot(tb == tl);
+                if (lane == leader) atomicAdd(&a.committed[tl], (unsigned long long)__popcll(mt));
+                m &= ~mt;
+                if (tb == tl) tb = 0xFFFFFFFFu;
+            }
+        }
     }
-    if (lane == 0 && run_c) atomicAdd(&a.committed[run_t], run_c);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < t.ns; k += AG_T)
+        if (l_any[k]) a.any[l_cs[k]] = 1;  // (spans straddling workgroups: the same value from each)
+    if (lds_t && threadIdx.x < a.ntables) a.part[(uint64_t)blockIdx.x * a.ntables + threadIdx.x] = l_cnt[threadIdx.x];
+}
+
+// committed[t] += sum over workgroups of part[wg * ntables + t] (one workgroup per table)
+__global__ void __launch_bounds__(AG_T) k_imp_reduce(const unsigned long long *__restrict__ part, uint64_t nwg,
+                                                      uint32_t ntables, unsigned long long *__restrict__ committed) {
+    __shared__ unsigned long long l[AG_T / 64];
+    unsigned long long sum = 0;
+    for (uint64_t w = threadIdx.x; w < nwg; w += AG_T) sum += part[w * ntables + blockIdx.x];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
+    if ((threadIdx.x & 63) == 0) l[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (int k = 0; k < AG_T / 64; k++) s += l[k];
+        committed[blockIdx.x] += s;
+    }
 }
 
 // Application order of the applied changesets: key = site rank (ActorId byte order) for an applied
@@ -207,7 +316,7 @@ __global__ void __launch_bounds__(AG_T) k_span_fin(const uint64_t *__restrict__ 
         s_cnt[j] = cnt32[j];
         if (j && s_src[j] != s_src[j - 1] + cnt32[j - 1]) gap = true;
     }
-    if (__any(gap) && (threadIdx.x & 63) == 0) atomicOr(info, 1u);
+    if (__any(gap) && (threadIdx.x & 63) == 0) *info = 1u;  // (a plain store: every writer stores 1)
 }
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -266,6 +375,7 @@ struct DevCols {
     uint32_t *val, *val2;
     uint64_t *s_src, *s_dst, *s_cnt, *s_ts;
     uint32_t *cnt32, *incl, *info;
+    uint32_t *first_span;    // k_span_blocks: first span of each SPB-position workgroup
     void *temp;
     size_t temp_bytes;
 };
@@ -279,7 +389,7 @@ size_t sort_temp_bytes(uint64_t n) {
 
 DevCols dev_cols(corro_ctx *ctx, size_t *total = nullptr) {
     const uint64_t n = std::max<uint64_t>(ctx->agent_ncs, 1);
-    const size_t elem[] = {8, 8, 8, 4, 1, 1, 1, 8, 8, 4, 4, 8, 8, 8, 8, 4, 4, 4};
+    const size_t elem[] = {8, 8, 8, 4, 1, 1, 1, 8, 8, 4, 4, 8, 8, 8, 8, 4, 4, 4};  // (+ first_span, below)
     DevCols c{};
     void **slot[] = {(void **)&c.off, (void **)&c.cnt, (void **)&c.ts, (void **)&c.site, (void **)&c.flag,
                      (void **)&c.bad, (void **)&c.any, (void **)&c.key, (void **)&c.key2, (void **)&c.val,
@@ -291,6 +401,8 @@ DevCols dev_cols(corro_ctx *ctx, size_t *total = nullptr) {
         *slot[k] = base + o;
         o += al256(n * elem[k]);
     }
+    c.first_span = reinterpret_cast<uint32_t *>(base + o);
+    o += al256((ctx->agent_nbatch_max / SPB + 2) * 4);
     c.temp_bytes = sort_temp_bytes(n);
     c.temp = base + o;
     o += al256(c.temp_bytes);
@@ -317,22 +429,28 @@ int gather_dev(corro_ctx *ctx, const corro_changes *dv, const uint64_t *src, con
     return CORRO_OK;
 }
 
-// position mode: ap[src + k] = dst + k, src_of[dst + k] = src + k and, when wanted, the ts of
-// application position dst + k (the input's per-change ts, else the changeset's), a wave per span
-__global__ void __launch_bounds__(AG_T) k_span_pos(const uint64_t *__restrict__ s_src, const uint64_t *__restrict__ s_dst,
-                                                    const uint64_t *__restrict__ s_cnt, const uint64_t *__restrict__ s_ts,
-                                                    uint64_t nspans, const uint64_t *__restrict__ in_ts,
+// position mode: ap[src] = p, src_of[p] = src and, when wanted, the ts of application position p (the
+// input's per-change ts, else the changeset's), positions along the workgroup's spans
+__global__ void __launch_bounds__(AG_T) k_span_pos(const uint32_t *__restrict__ first_span, const uint64_t *__restrict__ s_src,
+                                                    const uint64_t *__restrict__ s_dst, const uint64_t *__restrict__ s_ts,
+                                                    uint64_t nspans, uint64_t nbatch, const uint64_t *__restrict__ in_ts,
                                                     uint32_t *__restrict__ ap, uint32_t *__restrict__ src_of,
                                                     uint64_t *__restrict__ ts_out) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w0 = ((uint64_t)blockIdx.x * AG_T + threadIdx.x) >> 6, nw = (uint64_t)gridDim.x * (AG_T / 64);
-    for (uint64_t j = w0; j < nspans; j += nw) {
-        const uint64_t s = s_src[j], d = s_dst[j], c = s_cnt[j], t = s_ts[j];
-        for (uint64_t k = lane; k < c; k += 64) {
-            ap[s + k] = (uint32_t)(d + k);
-            src_of[d + k] = (uint32_t)(s + k);
-            if (ts_out) ts_out[d + k] = in_ts ? in_ts[s + k] : t;
-        }
+    __shared__ uint32_t l_dst[SPB + 1];
+    __shared__ uint64_t l_src[SPB + 1];
+    __shared__ uint64_t l_ts[SPB + 1];
+    const SpanTile t = stage_spans(first_span, nspans, nbatch, s_dst, s_src, ts_out && !in_ts ? s_ts : nullptr, nullptr,
+                                   l_dst, l_src, ts_out && !in_ts ? l_ts : nullptr, nullptr);
+#pragma unroll 2
+    for (uint32_t u = 0; u < SP_PER; u++) {
+        const uint32_t r = u * AG_T + threadIdx.x;
+        const uint64_t p = t.p0 + r;
+        if (p >= t.p1) continue;
+        const uint32_t k = span_of(l_dst, t.ns, r);
+        const uint64_t src = l_src[k] + (r - l_dst[k]);
+        ap[src] = (uint32_t)p;
+        src_of[p] = (uint32_t)src;
+        if (ts_out) ts_out[p] = in_ts ? in_ts[src] : l_ts[k];
     }
 }
 
@@ -340,7 +458,7 @@ dim3 flat_grid(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, std::mi
 
 }  // namespace
 
-int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, AgentPinned *p) {
+int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, uint64_t nchanges, AgentPinned *p) {
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
     CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));  // (the pinned area may still feed a copy)
     const uint64_t n = std::max<uint64_t>(ncs, 1);
@@ -364,6 +482,8 @@ int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, AgentPinned *p) {
     p->any = p->bad + c1;
     p->committed = reinterpret_cast<uint64_t *>(p->any + c1);
     ctx->agent_ncs = ncs;
+    ctx->agent_nbatch_max = nchanges;
+    ctx->agent_sorted_mode = false;
     size_t dtotal = 0;
     (void)dev_cols(ctx, &dtotal);
     if (int rc = ctx->d_agent_spans.ensure(dtotal + 256)) return rc;
@@ -405,7 +525,7 @@ int agent_dev_bad(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &p,
     const DevCols c = dev_cols(ctx);
     CORRO_HIP_TRY(hipMemcpyAsync(c.off, p.off, ncs * 8, hipMemcpyHostToDevice, s));
     CORRO_HIP_TRY(hipMemcpyAsync(c.cnt, p.cnt, ncs * 8, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_cs_bad, wave_grid(ncs), dim3(AG_T), 0, s, dv->table_cid, c.off, c.cnt, ncs, c.bad);
+    hipLaunchKernelGGL(k_cs_bad, flat_grid(ncs), dim3(AG_T), 0, s, dv->table_cid, c.off, c.cnt, ncs, c.bad);
     CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipMemcpyAsync(p.bad, c.bad, ncs, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
@@ -472,32 +592,22 @@ int agent_dev_fetch(corro_ctx *ctx, const corro_changes *dv, const std::vector<A
     return CORRO_OK;
 }
 
-int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &p, uint64_t ncs, uint64_t nspans,
-                    uint64_t nbatch, bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm) {
+// spans (s_src, cnt32, s_ts, s_cs written for nspans) -> their batch offsets, workgroup span table,
+// then the batch: zero-copy, position mode or a gather
+int spans_to_batch(corro_ctx *ctx, const corro_changes *dv, uint64_t nspans, uint64_t nbatch, bool need_ts,
+                   corro_changes *batch, bool *gathered, AgentPositions *pm) {
     *gathered = false;
     if (pm) *pm = AgentPositions{};
     hipStream_t s = ctx->stream;
     const DevCols c = dev_cols(ctx);
     if (nspans) {
-        // off / cnt are on the device already (the screen); the rest of the changeset columns once
-        if (!dv->ts) CORRO_HIP_TRY(hipMemcpyAsync(c.ts, p.ts, ncs * 8, hipMemcpyHostToDevice, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(c.site, p.site, ncs * 4, hipMemcpyHostToDevice, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(c.flag, p.flag, ncs, hipMemcpyHostToDevice, s));
-        uint32_t bits = 1;
-        while ((1ULL << bits) <= ctx->sites.size()) bits++;
-        hipLaunchKernelGGL(k_span_keys, flat_grid(ncs), dim3(AG_T), 0, s, c.site, c.flag, ctx->d_site_rank.as<uint32_t>(),
-                           ncs, (uint64_t)((1ULL << bits) - 1), c.key, c.val);
-        CORRO_HIP_TRY(hipGetLastError());
         size_t tb = c.temp_bytes;
-        if (int rc = ovf_sort_pairs(c.temp, &tb, c.key, c.key2, c.val, c.val2, (uint32_t)ncs, bits, s)) return rc;
-        hipLaunchKernelGGL(k_span_build, flat_grid(nspans), dim3(AG_T), 0, s, c.val2, nspans, c.off, c.cnt, c.ts,
-                           c.s_src, c.cnt32, c.s_ts);
-        CORRO_HIP_TRY(hipGetLastError());
-        tb = c.temp_bytes;
         if (int rc = prim_inclusive_scan_u32(c.temp, &tb, c.cnt32, c.incl, (uint32_t)nspans, s)) return rc;
         CORRO_HIP_TRY(hipMemsetAsync(c.info, 0, 4, s));
         hipLaunchKernelGGL(k_span_fin, flat_grid(nspans), dim3(AG_T), 0, s, c.s_src, c.cnt32, c.incl, nspans, c.s_dst,
                            c.s_cnt, c.info);
+        CORRO_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_span_blocks, flat_grid(nspans), dim3(AG_T), 0, s, c.s_dst, c.s_cnt, nspans, c.first_span);
         CORRO_HIP_TRY(hipGetLastError());
     }
     // zero-copy: one contiguous run, pairs of changes 16-B aligned (the scatter's paired loads), and
@@ -535,8 +645,8 @@ int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &
         uint32_t *ap = reinterpret_cast<uint32_t *>(base), *src_of = reinterpret_cast<uint32_t *>(base + o_src);
         uint64_t *ts = want_ts ? reinterpret_cast<uint64_t *>(base + o_ts) : nullptr;
         CORRO_HIP_TRY(hipMemsetAsync(ap, 0xFF, dv->n * 4, s));
-        hipLaunchKernelGGL(k_span_pos, wave_grid(nspans), dim3(AG_T), 0, s, c.s_src, c.s_dst, c.s_cnt, c.s_ts, nspans,
-                           dv->ts, ap, src_of, ts);
+        hipLaunchKernelGGL(k_span_pos, dim3((uint32_t)((nbatch + SPB - 1) / SPB)), dim3(AG_T), 0, s, c.first_span, c.s_src,
+                           c.s_dst, c.s_ts, nspans, nbatch, dv->ts, ap, src_of, ts);
         CORRO_HIP_TRY(hipGetLastError());
         *batch = *dv;
         pm->on = true;
@@ -553,6 +663,29 @@ int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &
     *batch = g;
     *gathered = true;
     return CORRO_OK;
+}
+
+int agent_dev_batch(corro_ctx *ctx, const corro_changes *dv, const AgentPinned &p, uint64_t ncs, uint64_t nspans,
+                    uint64_t nbatch, bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm) {
+    hipStream_t s = ctx->stream;
+    const DevCols c = dev_cols(ctx);
+    if (nspans) {
+        // off / cnt are on the device already (the screen); the rest of the changeset columns once
+        if (!dv->ts) CORRO_HIP_TRY(hipMemcpyAsync(c.ts, p.ts, ncs * 8, hipMemcpyHostToDevice, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(c.site, p.site, ncs * 4, hipMemcpyHostToDevice, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(c.flag, p.flag, ncs, hipMemcpyHostToDevice, s));
+        uint32_t bits = 1;
+        while ((1ULL << bits) <= ctx->sites.size()) bits++;
+        hipLaunchKernelGGL(k_span_keys, flat_grid(ncs), dim3(AG_T), 0, s, c.site, c.flag, ctx->d_site_rank.as<uint32_t>(),
+                           ncs, (uint64_t)((1ULL << bits) - 1), c.key, c.val);
+        CORRO_HIP_TRY(hipGetLastError());
+        size_t tb = c.temp_bytes;
+        if (int rc = ovf_sort_pairs(c.temp, &tb, c.key, c.key2, c.val, c.val2, (uint32_t)ncs, bits, s)) return rc;
+        hipLaunchKernelGGL(k_span_build, flat_grid(nspans), dim3(AG_T), 0, s, c.val2, nspans, c.off, c.cnt, c.ts,
+                           c.s_src, c.cnt32, c.s_ts);
+        CORRO_HIP_TRY(hipGetLastError());
+    }
+    return spans_to_batch(ctx, dv, nspans, nbatch, need_ts, batch, gathered, pm);
 }
 
 void agent_dev_set_positions(corro_ctx *ctx, const AgentPositions *pm) {
@@ -573,9 +706,11 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
     hipStream_t s = ctx->stream;
     if (ntables > 65536) return fail(CORRO_E_RANGE, "at most 65536 tables");
     const DevCols c = dev_cols(ctx);
-    // scratch: first (8 B) | committed (8 per table) | host-mode impactful (nin)
+    // scratch: first (8 B) | committed (8 per table) | host-mode impactful (nin) | per-workgroup table counts
+    const uint64_t nwg = (nbatch + SPB - 1) / SPB;
     const size_t o_cm = 256, o_out = o_cm + 8 * 65536;
-    const size_t total = o_out + (mem == CORRO_MEM_HOST && impactful ? al256(nin) : 0);
+    const size_t o_part = o_out + (mem == CORRO_MEM_HOST && impactful ? al256(nin) : 0);
+    const size_t total = o_part + (ntables <= IMP_TLDS ? al256(nwg * ntables * 8) : 0);
     if (int rc = ctx->d_agent_out.ensure(total)) return rc;
     uint8_t *base = ctx->d_agent_out.as<uint8_t>();
     unsigned long long *first = reinterpret_cast<unsigned long long *>(base);
@@ -583,7 +718,7 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
     CORRO_HIP_TRY(hipMemsetAsync(base + o_cm, 0, 8ULL * std::max<uint32_t>(ntables, 1), s));
     uint8_t *out = nullptr;
     if (impactful) {
-        out = mem == CORRO_MEM_DEVICE ? impactful : base + o_out;
+        out = mem == CORRO_MEM_HOST ? base + o_out : impactful;
         if (nin) CORRO_HIP_TRY(hipMemsetAsync(out, 0, nin, s));
     }
     if (nspans) {
@@ -596,22 +731,455 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
         a.tcid = tcid;
         a.s_src = c.s_src;
         a.s_dst = c.s_dst;
-        a.s_cnt = c.s_cnt;
-        a.s_cs = c.val2;
+        a.s_cs = ctx->agent_sorted_mode ? c.val : c.val2;
+        a.first_span = c.first_span;
         a.nspans = nspans;
+        a.nbatch = nbatch;
         a.first = first;
         a.out = out;
         a.any = c.any;
         a.committed = reinterpret_cast<unsigned long long *>(base + o_cm);
+        a.part = reinterpret_cast<unsigned long long *>(base + o_part);
         a.ntables = ntables;
         a.tcid_by_src = tcid_by_src;
-        hipLaunchKernelGGL(k_impactful, wave_grid(nspans), dim3(AG_T), 0, s, a);
+        hipLaunchKernelGGL(k_impactful, dim3((uint32_t)nwg), dim3(AG_T), 0, s, a);
         CORRO_HIP_TRY(hipGetLastError());
+        if (ntables && ntables <= IMP_TLDS) {
+            hipLaunchKernelGGL(k_imp_reduce, dim3(ntables), dim3(AG_T), 0, s, a.part, nwg, ntables, a.committed);
+            CORRO_HIP_TRY(hipGetLastError());
+        }
         CORRO_HIP_TRY(hipMemcpyAsync(p.any, c.any, ncs, hipMemcpyDeviceToHost, s));
     }
     CORRO_HIP_TRY(hipMemcpyAsync(p.committed, base + o_cm, 8ULL * ntables, hipMemcpyDeviceToHost, s));
     if (out && mem == CORRO_MEM_HOST && nin) CORRO_HIP_TRY(hipMemcpyAsync(impactful, out, nin, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+// ---- device-resident headers ------------------------------------------------------------------
+namespace {
+
+// Header-mode columns in d_agent_hdr (n = changesets, m = sites):
+//   ver u64[n] | comp u8[n] | inrun u8[n] | emp u8[n] | rflag u32[n] | rincl u32[n] | run_site u32[n]
+//   | run_start u64[n] | run_end u64[n] | site_max i64[m] | slow u8[m] | gstart u32[m] | gend u32[m]
+//   | ctl u64[8] (0 err, 1 ts_any, 2 nspans, 3 nchanges)
+struct HdrCols {
+    uint64_t *ver;
+    uint8_t *comp, *inrun, *emp;
+    uint32_t *rflag, *rincl, *run_site;
+    uint64_t *run_start, *run_end;
+    int64_t *site_max;
+    uint8_t *slow;
+    uint32_t *gstart, *gend;
+    unsigned long long *ctl;
+};
+
+HdrCols hdr_cols(corro_ctx *ctx, uint64_t ncs, uint32_t nsites, size_t *total = nullptr) {
+    const uint64_t n = std::max<uint64_t>(ncs, 1), m = std::max<uint32_t>(nsites, 1);
+    const size_t sz[] = {n * 8, n, n, n, n * 4, n * 4, n * 4, n * 8, n * 8, m * 8, m, m * 4, m * 4, 64};
+    void **slot[] = {(void **)nullptr};
+    (void)slot;
+    HdrCols h{};
+    void **dst[] = {(void **)&h.ver, (void **)&h.comp, (void **)&h.inrun, (void **)&h.emp, (void **)&h.rflag,
+                    (void **)&h.rincl, (void **)&h.run_site, (void **)&h.run_start, (void **)&h.run_end,
+                    (void **)&h.site_max, (void **)&h.slow, (void **)&h.gstart, (void **)&h.gend, (void **)&h.ctl};
+    uint8_t *base = ctx->d_agent_hdr.as<uint8_t>();
+    size_t o = 0;
+    for (size_t k = 0; k < sizeof(sz) / sizeof(sz[0]); k++) {
+        if (base) *dst[k] = base + o;
+        o += al256(sz[k]);
+    }
+    if (total) *total = o;
+    return h;
+}
+
+struct HdrArgs {
+    const corro_changeset *cs;
+    uint64_t ncs, nchanges;
+    uint32_t nsites;
+    const uint32_t *tcid;          // the input's table_cid (device)
+    const uint32_t *site_rank;
+    uint64_t *off, *cnt, *ts, *ver, *key;
+    uint32_t *site, *val;
+    uint8_t *flag, *bad, *comp;
+    int32_t *known;
+    unsigned long long *ctl;
+};
+
+// one thread per changeset: span check, unknown-name screen, the per-changeset columns, sort keys
+__global__ void __launch_bounds__(AG_T) k_hdr(HdrArgs a) {
+    bool tsb = false;
+    uint32_t err = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * AG_T + threadIdx.x; i < a.ncs; i += (uint64_t)gridDim.x * AG_T) {
+        const corro_changeset c = a.cs[i];
+        const bool full = c.kind == CORRO_CS_FULL && c.change_count;
+        bool ok = true;
+        if (full && (c.change_off > a.nchanges || c.change_count > a.nchanges - c.change_off)) {
+            err |= 1u;
+            ok = false;
+        }
+        if (c.site >= a.nsites) err |= 2u;
+        a.off[i] = full ? c.change_off : 0;
+        a.cnt[i] = full ? c.change_count : 0;
+        a.ts[i] = c.ts;
+        a.site[i] = c.site;
+        a.ver[i] = c.version_start;
+        a.flag[i] = 0;
+        a.known[i] = CORRO_KNOWN_SKIPPED;
+        a.comp[i] = c.kind == CORRO_CS_FULL && c.seq_start == 0 && c.seq_end == c.last_seq;
+        a.bad[i] = full && ok && span_has_unknown(a.tcid, c.change_off, c.change_count) ? 1 : 0;
+        a.key[i] = c.site < a.nsites ? a.site_rank[c.site] : 0;
+        a.val[i] = (uint32_t)i;
+        tsb |= c.ts != 0;
+    }
+    const unsigned long long anyts = __ballot(tsb);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d);
+    if ((threadIdx.x & 63) == 0) {
+        if (err) atomicOr(&a.ctl[0], (unsigned long long)err);
+        if (anyts) a.ctl[1] = 1;  // (a plain store of 1)
+    }
+}
+
+// per sorted slot: actor groups (gstart / gend) and the fast test; a violation marks the actor slow
+__global__ void __launch_bounds__(AG_T) k_hdr_sites(const uint32_t *__restrict__ order, uint64_t ncs,
+                                                     const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
+                                                     const uint8_t *__restrict__ comp, const int64_t *__restrict__ site_max,
+                                                     uint8_t *__restrict__ slow, uint32_t *__restrict__ gstart,
+                                                     uint32_t *__restrict__ gend) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = order[j], st = site[i];
+        const bool same_prev = j > 0 && site[order[j - 1]] == st;
+        const bool same_next = j + 1 < ncs && site[order[j + 1]] == st;
+        if (!same_prev) gstart[st] = (uint32_t)j;
+        if (!same_next) gend[st] = (uint32_t)j;
+        const int64_t mx = site_max[st];
+        const bool fast = comp[i] && (!same_prev || ver[i] > ver[order[j - 1]]) && (mx < 0 || ver[i] > (uint64_t)mx);
+        if (!fast) slow[st] = 1;
+    }
+}
+
+// per sorted slot of a fast actor: merged (flag), cleared (empty) or rolled back (unknown name);
+// version runs of the merged and cleared ones; counts of the flagged spans and changes
+__global__ void __launch_bounds__(AG_T) k_hdr_fast(const uint32_t *__restrict__ order, uint64_t ncs,
+                                                    const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
+                                                    const uint64_t *__restrict__ cnt, const uint8_t *__restrict__ bad,
+                                                    const uint8_t *__restrict__ slow, uint8_t *__restrict__ flag,
+                                                    int32_t *__restrict__ known, uint8_t *__restrict__ inrun,
+                                                    uint8_t *__restrict__ emp, unsigned long long *ctl) {
+    __shared__ unsigned long long l_sp[AG_T / 64], l_ch[AG_T / 64];
+    unsigned long long nsp = 0, nch = 0;
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = order[j];
+        uint8_t in = 0, e = 0;
+        if (!slow[site[i]]) {
+            if (cnt[i] == 0) {  // process_empty_version (every version of a fast actor is above its max)
+                known[i] = CORRO_KNOWN_CLEARED;
+                in = e = 1;
+            } else if (bad[i]) {  // the version's SAVEPOINT rolls back alone (util.rs:839-860)
+                known[i] = CORRO_E_UNKNOWN_COLUMN;
+            } else {
+                flag[i] = 1;
+                known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
+                in = 1;
+                nsp++;
+                nch += cnt[i];
+            }
+        }
+        inrun[j] = in;
+        emp[j] = e;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        nsp += __shfl_xor(nsp, d);
+        nch += __shfl_xor(nch, d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        l_sp[threadIdx.x >> 6] = nsp;
+        l_ch[threadIdx.x >> 6] = nch;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, b = 0;
+        for (int k = 0; k < AG_T / 64; k++) {
+            a += l_sp[k];
+            b += l_ch[k];
+        }
+        if (a) atomicAdd(&ctl[2], a);
+        if (b) atomicAdd(&ctl[3], b);
+    }
+}
+
+// run starts: a slot in a run whose predecessor (same actor) does not continue it with version - 1
+__global__ void __launch_bounds__(AG_T) k_hdr_runflag(const uint32_t *__restrict__ order, uint64_t ncs,
+                                                       const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
+                                                       const uint8_t *__restrict__ inrun, uint32_t *__restrict__ rflag) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = order[j];
+        const bool cont = j > 0 && inrun[j - 1] && site[order[j - 1]] == site[i] && ver[order[j - 1]] + 1 == ver[i];
+        rflag[j] = inrun[j] && !cont ? 1u : 0u;
+    }
+}
+
+__global__ void __launch_bounds__(AG_T) k_hdr_runs(const uint32_t *__restrict__ order, uint64_t ncs,
+                                                    const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
+                                                    const uint8_t *__restrict__ inrun, const uint32_t *__restrict__ rflag,
+                                                    const uint32_t *__restrict__ rincl, uint32_t *__restrict__ run_site,
+                                                    uint64_t *__restrict__ run_start, uint64_t *__restrict__ run_end) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
+        if (!inrun[j]) continue;
+        const uint32_t i = order[j], r = rincl[j] - 1;
+        if (rflag[j]) {
+            run_site[r] = site[i];
+            run_start[r] = ver[i];
+        }
+        const bool ends = j + 1 >= ncs || !inrun[j + 1] || rflag[j + 1];
+        if (ends) run_end[r] = ver[i];
+    }
+}
+
+__global__ void __launch_bounds__(AG_T) k_hdr_gather(const corro_changeset *__restrict__ cs, const uint32_t *__restrict__ order,
+                                                      const uint8_t *__restrict__ bad, const uint32_t *__restrict__ slot,
+                                                      uint64_t n, corro_changeset *__restrict__ out, uint32_t *__restrict__ idx,
+                                                      uint8_t *__restrict__ obad) {
+    for (uint64_t k = (uint64_t)blockIdx.x * AG_T + threadIdx.x; k < n; k += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = order[slot[k]];
+        out[k] = cs[i];
+        idx[k] = i;
+        obad[k] = bad[i];
+    }
+}
+
+__global__ void __launch_bounds__(AG_T) k_hdr_put(const uint32_t *__restrict__ idx, const uint8_t *__restrict__ f,
+                                                   const int32_t *__restrict__ kn, uint64_t n, uint8_t *__restrict__ flag,
+                                                   int32_t *__restrict__ known) {
+    for (uint64_t k = (uint64_t)blockIdx.x * AG_T + threadIdx.x; k < n; k += (uint64_t)gridDim.x * AG_T) {
+        flag[idx[k]] = f[k];
+        known[idx[k]] = kn[k];
+    }
+}
+
+// applied spans in sorted order: slot j's changeset when flagged -> span rincl[j] - 1
+__global__ void __launch_bounds__(AG_T) k_hdr_flagged(const uint32_t *__restrict__ order, uint64_t ncs,
+                                                       const uint8_t *__restrict__ flag, uint32_t *__restrict__ fl) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T)
+        fl[j] = flag[order[j]];
+}
+
+__global__ void __launch_bounds__(AG_T) k_hdr_spans(const uint32_t *__restrict__ order, uint64_t ncs,
+                                                     const uint8_t *__restrict__ flag, const uint32_t *__restrict__ incl,
+                                                     const uint64_t *__restrict__ off, const uint64_t *__restrict__ cnt,
+                                                     const uint64_t *__restrict__ ts, uint64_t *__restrict__ s_src,
+                                                     uint32_t *__restrict__ cnt32, uint64_t *__restrict__ s_ts,
+                                                     uint32_t *__restrict__ s_cs) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = order[j];
+        if (!flag[i]) continue;
+        const uint32_t k = incl[j] - 1;
+        s_src[k] = off[i];
+        cnt32[k] = (uint32_t)cnt[i];
+        s_ts[k] = ts[i];
+        s_cs[k] = i;
+    }
+}
+
+// commit: known of flagged changesets, crsql_set_db_version of the fast actors' empty versions
+__global__ void __launch_bounds__(AG_T) k_hdr_commit(const uint32_t *__restrict__ order, uint64_t ncs,
+                                                      const uint8_t *__restrict__ flag, const uint8_t *__restrict__ any,
+                                                      const uint8_t *__restrict__ emp, const uint32_t *__restrict__ site,
+                                                      const uint64_t *__restrict__ ver, int32_t *__restrict__ known,
+                                                      unsigned long long *__restrict__ dbv) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = order[j];
+        if (flag[i]) known[i] = any[i] ? CORRO_KNOWN_CURRENT : CORRO_KNOWN_CLEARED;
+        if (emp[j]) atomicMax(&dbv[site[i]], (unsigned long long)(ver[i] + 1));
+    }
+}
+
+}  // namespace
+
+int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, const corro_changes *dv,
+                      const std::vector<int64_t> &site_max, int32_t *dknown, DevHdrResult &res) {
+    hipStream_t s = ctx->stream;
+    const uint32_t nsites = (uint32_t)ctx->sites.size();
+    res = DevHdrResult{};
+    res.sites.assign(nsites, DevHdrSite{0xFFFFFFFFu, 0xFFFFFFFFu, 0});
+    ctx->agent_sorted_mode = true;
+    if (!ncs) return CORRO_OK;
+    size_t total = 0;
+    (void)hdr_cols(ctx, ncs, nsites, &total);
+    if (int rc = ctx->d_agent_hdr.ensure(total + 256)) return rc;
+    const HdrCols h = hdr_cols(ctx, ncs, nsites);
+    const DevCols c = dev_cols(ctx);
+    CORRO_HIP_TRY(hipMemsetAsync(h.ctl, 0, 64, s));
+    CORRO_HIP_TRY(hipMemsetAsync(h.slow, 0, std::max<uint32_t>(nsites, 1), s));
+    CORRO_HIP_TRY(hipMemsetAsync(h.gstart, 0xFF, 4ULL * std::max<uint32_t>(nsites, 1), s));
+    if (nsites) CORRO_HIP_TRY(hipMemcpyAsync(h.site_max, site_max.data(), 8ULL * nsites, hipMemcpyHostToDevice, s));
+    HdrArgs a{};
+    a.cs = dcs;
+    a.ncs = ncs;
+    a.nchanges = dv ? dv->n : 0;
+    a.nsites = nsites;
+    a.tcid = dv ? dv->table_cid : nullptr;
+    a.site_rank = ctx->d_site_rank.as<uint32_t>();
+    a.off = c.off;
+    a.cnt = c.cnt;
+    a.ts = c.ts;
+    a.ver = h.ver;
+    a.key = c.key;
+    a.site = c.site;
+    a.val = c.val;
+    a.flag = c.flag;
+    a.bad = c.bad;
+    a.comp = h.comp;
+    a.known = dknown;
+    a.ctl = h.ctl;
+    hipLaunchKernelGGL(k_hdr, flat_grid(ncs), dim3(AG_T), 0, s, a);
+    CORRO_HIP_TRY(hipGetLastError());
+    unsigned long long ctl0 = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&ctl0, h.ctl, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (ctl0) {  // nothing decided: every changeset stays Skipped
+        res.err = (uint32_t)ctl0;
+        return CORRO_OK;
+    }
+    uint32_t bits = 1;
+    while ((1ULL << bits) <= nsites) bits++;
+    size_t tb = c.temp_bytes;
+    if (int rc = ovf_sort_pairs(c.temp, &tb, c.key, c.key2, c.val, c.val2, (uint32_t)ncs, bits, s)) return rc;
+    const uint32_t *order = c.val2;
+    hipLaunchKernelGGL(k_hdr_sites, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, h.comp, h.site_max,
+                       h.slow, h.gstart, h.gend);
+    CORRO_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_hdr_fast, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, c.cnt, c.bad, h.slow,
+                       c.flag, dknown, h.inrun, h.emp, h.ctl);
+    CORRO_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_hdr_runflag, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, h.inrun, h.rflag);
+    CORRO_HIP_TRY(hipGetLastError());
+    tb = c.temp_bytes;
+    if (int rc = prim_inclusive_scan_u32(c.temp, &tb, h.rflag, h.rincl, (uint32_t)ncs, s)) return rc;
+    hipLaunchKernelGGL(k_hdr_runs, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, h.inrun, h.rflag,
+                       h.rincl, h.run_site, h.run_start, h.run_end);
+    CORRO_HIP_TRY(hipGetLastError());
+    // summaries: counters, run count, per-site groups
+    unsigned long long ctl[4] = {0, 0, 0, 0};
+    uint32_t nruns = 0;
+    std::vector<uint8_t> slow(nsites);
+    std::vector<uint32_t> gs(nsites), ge(nsites);
+    CORRO_HIP_TRY(hipMemcpyAsync(ctl, h.ctl, 32, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&nruns, h.rincl + (ncs - 1), 4, hipMemcpyDeviceToHost, s));
+    if (nsites) {
+        CORRO_HIP_TRY(hipMemcpyAsync(slow.data(), h.slow, nsites, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(gs.data(), h.gstart, 4ULL * nsites, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(ge.data(), h.gend, 4ULL * nsites, hipMemcpyDeviceToHost, s));
+    }
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    res.ts_any = ctl[1] != 0;
+    res.nspans = ctl[2];
+    res.nchanges = ctl[3];
+    for (uint32_t t = 0; t < nsites; t++) res.sites[t] = DevHdrSite{gs[t], ge[t], slow[t]};
+    res.run_site.resize(nruns);
+    res.run_start.resize(nruns);
+    res.run_end.resize(nruns);
+    if (nruns) {
+        CORRO_HIP_TRY(hipMemcpyAsync(res.run_site.data(), h.run_site, 4ULL * nruns, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(res.run_start.data(), h.run_start, 8ULL * nruns, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(res.run_end.data(), h.run_end, 8ULL * nruns, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+    }
+    return CORRO_OK;
+}
+
+int agent_dev_slow_headers(corro_ctx *ctx, const corro_changeset *dcs, const std::vector<std::pair<uint32_t, uint32_t>> &ranges,
+                           std::vector<corro_changeset> &hcs, std::vector<uint32_t> &idx, std::vector<uint8_t> &bad) {
+    hipStream_t s = ctx->stream;
+    std::vector<uint32_t> slots;
+    for (auto &[lo, hi] : ranges)
+        for (uint32_t j = lo; j < hi; j++) slots.push_back(j);
+    const uint64_t n = slots.size();
+    hcs.resize(n);
+    idx.resize(n);
+    bad.resize(n);
+    if (!n) return CORRO_OK;
+    const size_t o_cs = 0, o_idx = al256(n * sizeof(corro_changeset)), o_bad = o_idx + al256(n * 4), o_slot = o_bad + al256(n);
+    if (int rc = ctx->d_agent_fetch.ensure(o_slot + al256(n * 4))) return rc;
+    uint8_t *base = ctx->d_agent_fetch.as<uint8_t>();
+    const DevCols c = dev_cols(ctx);
+    CORRO_HIP_TRY(hipMemcpyAsync(base + o_slot, slots.data(), n * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_hdr_gather, flat_grid(n), dim3(AG_T), 0, s, dcs, c.val2, c.bad,
+                       reinterpret_cast<const uint32_t *>(base + o_slot), n,
+                       reinterpret_cast<corro_changeset *>(base + o_cs), reinterpret_cast<uint32_t *>(base + o_idx),
+                       base + o_bad);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipMemcpyAsync(hcs.data(), base + o_cs, n * sizeof(corro_changeset), hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(idx.data(), base + o_idx, n * 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(bad.data(), base + o_bad, n, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+int agent_dev_put_slow(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
+                       const std::vector<int32_t> &known, int32_t *dknown) {
+    const uint64_t n = idx.size();
+    if (!n) return CORRO_OK;
+    hipStream_t s = ctx->stream;
+    const size_t o_f = al256(n * 4), o_k = o_f + al256(n);
+    if (int rc = ctx->d_agent_aux2.ensure(o_k + al256(n * 4))) return rc;
+    uint8_t *base = ctx->d_agent_aux2.as<uint8_t>();
+    CORRO_HIP_TRY(hipMemcpyAsync(base, idx.data(), n * 4, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(base + o_f, flag.data(), n, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(base + o_k, known.data(), n * 4, hipMemcpyHostToDevice, s));
+    const DevCols c = dev_cols(ctx);
+    hipLaunchKernelGGL(k_hdr_put, flat_grid(n), dim3(AG_T), 0, s, reinterpret_cast<const uint32_t *>(base), base + o_f,
+                       reinterpret_cast<const int32_t *>(base + o_k), n, c.flag, dknown);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipStreamSynchronize(s));  // (host sources)
+    return CORRO_OK;
+}
+
+int agent_dev_batch_sorted(corro_ctx *ctx, const corro_changes *dv, uint64_t ncs, uint64_t nspans, uint64_t nbatch,
+                           bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm) {
+    hipStream_t s = ctx->stream;
+    const DevCols c = dev_cols(ctx);
+    if (nspans) {
+        hipLaunchKernelGGL(k_hdr_flagged, flat_grid(ncs), dim3(AG_T), 0, s, c.val2, ncs, c.flag, c.cnt32);
+        CORRO_HIP_TRY(hipGetLastError());
+        size_t tb = c.temp_bytes;
+        if (int rc = prim_inclusive_scan_u32(c.temp, &tb, c.cnt32, c.incl, (uint32_t)ncs, s)) return rc;
+        hipLaunchKernelGGL(k_hdr_spans, flat_grid(ncs), dim3(AG_T), 0, s, c.val2, ncs, c.flag, c.incl, c.off, c.cnt, c.ts,
+                           c.s_src, c.cnt32, c.s_ts, c.val);
+        CORRO_HIP_TRY(hipGetLastError());
+    }
+    return spans_to_batch(ctx, dv, nspans, nbatch, need_ts, batch, gathered, pm);
+}
+
+int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown,
+                             std::vector<std::pair<uint32_t, uint64_t>> *flagged_sv) {
+    if (!ncs) return CORRO_OK;
+    hipStream_t s = ctx->stream;
+    const HdrCols h = hdr_cols(ctx, ncs, (uint32_t)ctx->sites.size());
+    const DevCols c = dev_cols(ctx);
+    hipLaunchKernelGGL(k_hdr_commit, flat_grid(ncs), dim3(AG_T), 0, s, c.val2, ncs, c.flag, c.any, h.emp, c.site, h.ver,
+                       dknown, ctx->d_dbv.as<unsigned long long>());
+    CORRO_HIP_TRY(hipGetLastError());
+    if (flagged_sv) {
+        std::vector<uint8_t> f(ncs);
+        std::vector<uint32_t> st(ncs);
+        std::vector<uint64_t> v(ncs);
+        CORRO_HIP_TRY(hipMemcpyAsync(f.data(), c.flag, ncs, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(st.data(), c.site, ncs * 4, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(v.data(), h.ver, ncs * 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        for (uint64_t i = 0; i < ncs; i++)
+            if (f[i]) flagged_sv->emplace_back(st[i], v[i]);
+    }
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+int agent_dev_clear_known(corro_ctx *ctx, int32_t *dknown, uint64_t ncs) {
+    if (ncs) CORRO_HIP_TRY(hipMemsetAsync(dknown, 0, ncs * 4, ctx->stream));  // (CORRO_KNOWN_SKIPPED = 0)
+    CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return CORRO_OK;
 }
 

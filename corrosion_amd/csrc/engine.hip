@@ -1133,6 +1133,7 @@ int corro_ctx_metrics(corro_ctx *ctx, corro_metrics *out) {
     *out = ctx->metrics;
     out->state_rows = ctx->state_rows;
     out->state_records = ctx->state_total;
+    out->arena_bytes = ctx->arena_top;
     return CORRO_OK;
 }
 

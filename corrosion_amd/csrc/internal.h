@@ -207,9 +207,12 @@ struct corro_ctx {
     // span tables, impact flags, impactful output, and a pinned host staging area
     corro::DevBuf d_agent_in, d_agent_batch, d_agent_spans, d_agent_imp, d_agent_out, d_agent_aux;
     corro::DevBuf d_agent_fetch, d_agent_aux2;
+    corro::DevBuf d_agent_hdr;    // device-header mode: per-changeset / per-site / run columns
+    bool agent_sorted_mode = false;  // spans compacted from the site-rank sort (s_cs in the val column)
     void *h_agent = nullptr;
     size_t h_agent_bytes = 0;
     uint64_t agent_ncs = 0;       // changesets of the current call (d_agent_spans column length)
+    uint64_t agent_nbatch_max = 0;  // input changes of the current call (bound on the applied batch)
     uint64_t *h_misc = nullptr;   // pinned, 16 words
     // stage timing
     bool profiling = false;

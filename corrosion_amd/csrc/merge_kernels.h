@@ -1489,6 +1489,7 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
             const unsigned long long need = s_ctl[1];
             const bool room = used0 + s_ctl[0] <= a.rs.fill;
             if (!room || (need && hraw + need > a.rs.heap_cap)) {
+                if (room && need) atomicSub(a.rs.heap_top, need);  // (give the failed request back)
                 push_defer(a, b, room ? DEFER_HEAP : DEFER_REGION);
                 s_ctl[2] = 1;
             } else {
@@ -2017,7 +2018,9 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
                 if (earlier && c >= 0) imp = false;
                 if (c > 0 || (c == 0 && earlier)) win = false;
             }
+#if !(CORRO_DIAG & 1024)  // (1024: diagnostics only -- no flag stores, results not valid)
             if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
+#endif
             alive[k] = win;
         }
         __syncthreads();

@@ -130,7 +130,12 @@ __device__ inline uint32_t rs_insert(const RowStore &rs, uint32_t b, uint64_t pk
 // every successful range is disjoint and below the capacity; the host grows the heap past the top.
 __device__ inline unsigned long long rs_heap_alloc(const RowStore &rs, unsigned long long need) {
     const unsigned long long old = atomicAdd(rs.heap_top, need);
-    return old + need <= rs.heap_cap ? old : ~0ULL;
+    if (old + need <= rs.heap_cap) return old;
+    // a failed request gives its records back, so the top the host grows from (and later requests
+    // of this round) do not carry it (a concurrent request may still see the transient excess and
+    // defer: harmless, it merges after the growth)
+    atomicSub(rs.heap_top, need);
+    return ~0ULL;
 }
 
 }  // namespace corro

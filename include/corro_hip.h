@@ -49,6 +49,9 @@ enum { CORRO_INTEGER = 1, CORRO_REAL = 2, CORRO_TEXT = 3, CORRO_BLOB = 4, CORRO_
 
 /* Where a batch's arrays live */
 enum { CORRO_MEM_HOST = 0, CORRO_MEM_DEVICE = 1 };
+/* corro_process_multiple_changes only: like CORRO_MEM_DEVICE, and the changeset headers and
+ * out->known live on the device too (a decoder's device output); cs[i].actor_id is not read. */
+enum { CORRO_MEM_DEVICE_HEADERS = 2 };
 
 typedef struct corro_ctx corro_ctx;
 
@@ -261,6 +264,9 @@ typedef struct {
     uint64_t state_rows, state_records;   /* now */
     uint64_t max_batch;        /* largest batch (chunk_size) */
     double apply_seconds;      /* wall time inside corro_apply_batch */
+    uint64_t arena_bytes;      /* long-value arena in use: append-only (every batch's TEXT/BLOB values
+                                  longer than 16 bytes, winners or not) until corro_state_reset, at most
+                                  2^40 bytes (CORRO_E_RANGE beyond) */
 } corro_metrics;
 int corro_ctx_metrics(corro_ctx *ctx, corro_metrics *out);
 /* corro.changes.committed{table}: changes of complete and partial changesets that
@@ -496,8 +502,13 @@ void corro_bookie_free(corro_bookie *b);
  * unknown-name screen, the applied batch (zero-copy when the applied changesets are one contiguous
  * run of `in`, else one gather kernel) and the impactful flags are device passes, and the host walks
  * only the headers (actors in parallel host threads). With CORRO_MEM_HOST the arrays are copied to
- * the device once. Unresolved names carry table_cid = CORRO_TCID_UNKNOWN. out->impactful, if set, has
- * in->n entries (0 for changes that were not applied). */
+ * the device once. With CORRO_MEM_DEVICE_HEADERS `cs` and out->known are device arrays as well: the
+ * header passes run on the device (one pass per changeset, one stable sort by actor, one pass per
+ * sorted slot decides every actor whose changesets are complete Full versions strictly ascending in
+ * arrival order and above its booked max); the host walks only the other actors' headers (fetched)
+ * and runs the gap bookkeeping on per-actor version runs. Unresolved names carry table_cid =
+ * CORRO_TCID_UNKNOWN. out->impactful, if set, has in->n entries (0 for changes that were not
+ * applied). */
 int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
                                    const corro_changes *in, int mem, corro_process_out *out);
 /* (actor, version) pairs whose buffered seqs are complete; cap < count = sizing call */

@@ -20,7 +20,10 @@ SCHEMA = {"t": ["a", "b", "c", "d"], "u": ["x", "y"]}
 NACT = 5
 
 
-def _calls(seed, ncalls=6, per_call=40):
+def _calls(seed, ncalls=6, per_call=40, clean=()):
+    """Random calls; actors in `clean` never re-send, never send partial or Empty versions (each of
+    their calls is a run of complete Full versions ascending, gaps and empty Full versions allowed:
+    the device-header path decides them without the host)."""
     from oracle.agent import Changeset, UNKNOWN
     rng = np.random.default_rng(seed)
     import synth
@@ -62,6 +65,20 @@ def _calls(seed, ncalls=6, per_call=40):
         for _k in range(per_call):
             a = int(rng.integers(0, NACT))
             r = rng.random()
+            if a in clean:
+                if rng.random() < 0.1:
+                    nextv[a] += int(rng.integers(1, 3))
+                v = nextv[a]
+                nextv[a] += 1
+                k = 0 if rng.random() < 0.05 else int(rng.integers(1, 9))
+                rr = rows(a, v, k)
+                if k and rng.random() < 0.06:
+                    rr[int(rng.integers(0, k))]["table_cid"] = UNKNOWN
+                cs = Changeset(ids[a], "full", version=v, seqs=(0, max(k - 1, 0)), last_seq=max(k - 1, 0),
+                               ts=int(rng.integers(1, 1 << 40)), rows=rr)
+                call.append(cs)
+                sent.append(cs)
+                continue
             if r < 0.12 and sent:                      # re-sent (same call or an earlier one)
                 call.append(sent[int(rng.integers(0, len(sent)))])
                 continue
@@ -101,7 +118,9 @@ FIELDS = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64, "db_
 
 def _run(eng, bk, ordinal, call, device, order=None):
     """corro_process_multiple_changes on one call; the batch laid out in `order` of the changesets
-    (default: arrival order). Returns (known list, impactful per changeset)."""
+    (default: arrival order). device: False (host batch), True (device batch) or "headers" (device
+    batch, headers and known: CORRO_MEM_DEVICE_HEADERS). Returns (known list, impactful per
+    changeset)."""
     import torch
     from corrosion_amd import _lib as L
     order = list(range(len(call))) if order is None else order
@@ -150,8 +169,18 @@ def _run(eng, bk, ordinal, call, device, order=None):
         ip = imp.ctypes.data
     out = L.ProcessOut()
     out.known, out.impactful = known.ctypes.data, ip
-    L.check(L.lib().corro_process_multiple_changes(eng._h, bk._h, descs, len(call), C.byref(s),
-                                                   L.CORRO_MEM_DEVICE if device else L.CORRO_MEM_HOST, C.byref(out)))
+    mem = L.CORRO_MEM_DEVICE if device else L.CORRO_MEM_HOST
+    cs_arg = descs
+    if device == "headers":
+        raw = np.frombuffer(bytes(descs), np.uint8)
+        dcs = torch.from_numpy(raw.copy()).cuda()
+        dknown = torch.full((max(1, len(call)),), -99, dtype=torch.int32, device="cuda")
+        keep += [dcs, dknown]
+        torch.cuda.synchronize()
+        cs_arg, out.known, mem = C.c_void_p(dcs.data_ptr()), dknown.data_ptr(), L.CORRO_MEM_DEVICE_HEADERS
+    L.check(L.lib().corro_process_multiple_changes(eng._h, bk._h, cs_arg, len(call), C.byref(s), mem, C.byref(out)))
+    if device == "headers":
+        known = dknown.cpu().numpy()
     imp = imp.cpu().numpy() if device else imp
     kn = [L.KNOWN.get(int(k), int(k)) for k in known[:len(call)]]
     return kn, [list(imp[off[i]:off[i] + len(c.rows)]) if c.kind == "full" else [] for i, c in enumerate(call)]
@@ -162,10 +191,10 @@ def canon_rows(rows):
     return sorted(zip(*[np.asarray(rows[k]).tolist() for k in keys]))
 
 
-def _check_against_oracle(seed, device, order_fn=None):
+def _check_against_oracle(seed, device, order_fn=None, clean=()):
     import corrosion_amd as ca
     from oracle.agent import AgentOracle
-    ids, calls = _calls(seed)
+    ids, calls = _calls(seed, clean=clean)
     eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12)
     ords = eng.register_sites(ids)
     ordinal = {bytes(ids[k]): int(ords[k]) for k in range(NACT)}
@@ -215,3 +244,22 @@ def test_batch_in_application_order_zero_copy():
     def app_order(call):
         return sorted(range(len(call)), key=lambda i: (bytes(call[i].actor), i))
     _check_against_oracle(6, device=True, order_fn=app_order)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_device_headers_matches_restatement(seed):
+    """CORRO_MEM_DEVICE_HEADERS: headers and known on the device; every actor slow here (re-sends,
+    partials, Empty versions), so the host walks the fetched headers"""
+    _check_against_oracle(seed, device="headers")
+
+
+@pytest.mark.parametrize("seed,clean", [(11, (0, 1, 2)), (12, (0, 1, 2, 3, 4)), (13, (1, 3))])
+def test_device_headers_fast_actors_match_restatement(seed, clean):
+    """actors decided on the device (complete Full versions ascending, gaps, empty Full versions,
+    unknown names) next to slow ones, in one call"""
+    _check_against_oracle(seed, device="headers", clean=clean)
+
+
+def test_device_headers_fast_gather_path(monkeypatch):
+    monkeypatch.setenv("CORRO_AGENT_GATHER", "1")
+    _check_against_oracle(14, device="headers", clean=(0, 2, 4))

@@ -16,7 +16,20 @@ def main():
     ap.add_argument("--sizes", default="1000000,4000000")
     ap.add_argument("--impact", action="store_true")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--pmc", action="store_true",
+                    help="HBM traffic per apply from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over a child run "
+                         "(first size only; before this process touches the GPU)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    traffic = None
+    if args.pmc and not args.pmc_child:
+        import bench
+        n0 = int(args.sizes.split(",")[0])
+        child = [os.path.abspath(__file__), "--pmc-child", "--sizes", str(n0), "--reps", str(args.reps)]
+        if args.impact:
+            child.append("--impact")
+        tb, note, per = bench.pmc_traffic_live(n0, applies=args.reps + 1, timeout=400, child_cmd=child)
+        traffic = {"bytes": tb, "source": note, "by_kernel": per}
     import numpy as np
     import torch
     import synth
@@ -59,7 +72,12 @@ def main():
                           "roofline": {"bound": "hbm", "kernel": "apply pipeline (sum of stages)",
                                        "achieved": alg / (pipe * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
                                        "frac": alg / (pipe * 1e-3) / 1e9 / 8000.0, "alg_bytes": alg,
-                                       "pipeline_ms": pipe, "stages_ms": stages[k]}}), flush=True)
+                                       "pipeline_ms": pipe, "stages_ms": stages[k],
+                                       "traffic": traffic["bytes"] if traffic else None,
+                                       "traffic_ratio": (traffic["bytes"] / alg) if traffic and traffic["bytes"] else None,
+                                       "traffic_source": traffic["source"] if traffic else None,
+                                       "traffic_by_kernel": traffic["by_kernel"] if traffic else None}}), flush=True)
+        traffic = None  # (measured for the first size only)
         eng.close()
 
 
