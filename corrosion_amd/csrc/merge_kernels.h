@@ -1859,7 +1859,8 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
 // so "earlier" is the member index and no position array is kept for the walk.
 // Only zero impacts are stored: the apply initialises the flags to 1 (every other body stores each
 // change's flag), which halves the byte scatter into batch order.
-template <bool PACKED>
+// (three-word keys: col_versions of 2^15 or more, or more than 2^16 sites; fast_body_impact_packed
+// below takes the common case)
 __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, const BucketView &v) {
     __shared__ uint64_t s_a[CAP_FAST];      // hashing: pk; then the cell-ordered biased col_versions
     __shared__ uint32_t s_b[CAP_FAST];      // hashing: table_cid; then positions by member slot; then site ranks
@@ -1987,44 +1988,6 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     for (int k = 0; k < FAST_R; k++) md[k] = alive[k] ? s_own[cell[k]] : 0u;
     __syncthreads();
     DIAG_MARK2(4);
-    if constexpr (PACKED) {
-        // 3. keys and positions by member slot
-        uint32_t *s_p = reinterpret_cast<uint32_t *>(s_c);
-#pragma unroll
-        for (int k = 0; k < FAST_R; k++)
-            if (alive[k]) {
-                const uint32_t d = atomicAdd(&s_own[cell[k]], 1u);
-                s_a[d] = ((cv[k] ^ 0x8000000000000000ULL) << 48) | (v0[k] >> 16);
-                s_b[d] = (uint32_t)((v0[k] & 0xFFFFULL) << 16) | rank[k];
-                s_p[d] = pos[k];
-                md[k] |= d << 16;
-            }
-        __syncthreads();
-        DIAG_MARK2(5);
-        // 4. one walk over the cell's members per change: impact and winner as below
-#pragma unroll
-        for (int k = 0; k < FAST_R; k++) {
-            if (!alive[k]) continue;
-            bool imp = (flags >> (2 * k)) & 1u, win = imp;
-            const uint32_t mb = md[k] & 0xFFFFu, d = md[k] >> 16, me = s_own[cell[k]];
-            const uint64_t k1 = s_a[d];
-            const uint32_t k2 = s_b[d];
-            for (uint32_t m = mb; m < me; m++) {
-                if (m == d) continue;
-                const uint64_t j1 = s_a[m];
-                const uint32_t j2 = s_b[m];
-                const int c = j1 != k1 ? (j1 > k1 ? 1 : -1) : (j2 != k2 ? (j2 > k2 ? 1 : -1) : 0);
-                const bool earlier = s_p[m] < pos[k];
-                if (earlier && c >= 0) imp = false;
-                if (c > 0 || (c == 0 && earlier)) win = false;
-            }
-#if !(CORRO_DIAG & 1024)  // (1024: diagnostics only -- no flag stores, results not valid)
-            if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
-#endif
-            alive[k] = win;
-        }
-        __syncthreads();
-    } else {
     // 3. positions by member slot, then each member's rank among its cell's positions
 #pragma unroll
     for (int k = 0; k < FAST_R; k++)
@@ -2070,7 +2033,6 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
         alive[k] = win;
     }
     __syncthreads();
-    }
     DIAG_MARK2(6);
     // 5. winners: the clock row into its heap slot; presence bits of new cells (s_c per owner)
 #pragma unroll
@@ -2119,6 +2081,284 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
     DIAG_MARK2(7);
 }
 
+// Packed INTEGER impact body (col_versions < 2^15, <= 2^16 sites): each change's key is two words,
+// k1 = cv 15 | value bits 63..16 and k2 = value bits 15..0 | site rank 16, kept in registers with
+// the change's position, cell, row and heap slot only -- the rest of a winner's clock row (db_version,
+// seq, site) is re-read from its staged record at the end (the register budget of two workgroups per
+// CU, no spills). An empty region (the common case of a fresh state) has no prior clocks, so its rows
+// are counted right after the hashing, the heap allocation is issued before the member walk and
+// consumed after it, and the region entries are written at the end; a populated region resolves its
+// rows and prior clocks first (impacts depend on them).
+__device__ inline int prior_cmp_packed(const MergeArgs &a, const Rec &pr, uint64_t k1, uint32_t k2) {
+    const uint64_t cv = k1 >> 48, pcv = (uint64_t)pr.cv ^ 0x8000000000000000ULL;
+    const uint64_t cvb = cv ^ 0x8000000000000000ULL;  // (cv >= 0: biased like pcv)
+    if (cvb != pcv) return cvb > pcv ? 1 : -1;
+    const uint64_t v0b = ((k1 & 0xFFFFFFFFFFFFULL) << 16) | (k2 >> 16), pv = pr.v0 ^ 0x8000000000000000ULL;
+    if (v0b != pv) return v0b > pv ? 1 : -1;
+    const uint32_t rank = k2 & 0xFFFFu, pr_rank = site_rank_of(a, pr.site);
+    return rank != pr_rank ? (rank > pr_rank ? 1 : -1) : 0;
+}
+
+__device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, const BucketView &v) {
+    __shared__ uint64_t s_a[CAP_FAST];      // hashing: pk; then k1 by member slot
+    __shared__ uint32_t s_b[CAP_FAST];      // hashing: table_cid; then k2 by member slot
+    __shared__ uint64_t s_c[CAP_FAST];      // row table; presence words (populated region); positions by member slot; presence words
+    __shared__ uint32_t s_own[FAST_SLOTS];  // cell table; heap words; member counts / offsets / ends
+    __shared__ uint32_t s_wsum[FAST_T / 64];
+    __shared__ uint32_t s_ctl[4];
+    __shared__ unsigned long long s_hbase, s_live;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = v.nn;
+    uint64_t k1[FAST_R];
+    uint32_t k2[FAST_R], cell[FAST_R], pos[FAST_R], tc[FAST_R], md[FAST_R], row[FAST_R], ent[FAST_R], hb[FAST_R];
+    uint32_t flags = 0;   // bit 2k: beats the prior clock; bit 2k+1: the cell had no prior clock
+    bool alive[FAST_R];
+    uint4 q[FAST_R][4];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * FAST_T + (tid & ~63u), n, q[k]);
+    const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
+    if (tid == 0) {
+        s_live = 0;
+        s_ctl[0] = s_ctl[1] = s_ctl[2] = s_ctl[3] = 0;
+    }
+    for (uint32_t i = tid; i < FAST_SLOTS; i += FAST_T) {
+        s_own[i] = 0;
+        reinterpret_cast<uint32_t *>(s_c)[i] = 0;  // the row table of row_claim
+    }
+    uint32_t site[FAST_R];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * FAST_T + tid;
+        alive[k] = i < n;
+        cell[k] = 0;
+        const Rec r = rec_from_wave_quads(q[k]);
+        tc[k] = r.tcid;
+        s_a[i] = r.pk;
+        s_b[i] = r.tcid;
+        const uint64_t v0b = r.v0 ^ 0x8000000000000000ULL;  // INTEGER order as unsigned
+        k1[k] = ((uint64_t)r.cv << 48) | (v0b >> 16);
+        k2[k] = (uint32_t)(v0b & 0xFFFFu) << 16;
+        pos[k] = r.pos;
+        site[k] = r.site;
+    }
+    // site ranks and, for an empty region, row strides: one more batch of loads during the claims
+    uint32_t strd[FAST_R];
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        strd[k] = used0 ? 0u : (uint32_t)a.rs.stride[alive[k] ? tc[k] >> 16 : 0u];
+        k2[k] |= a.site_rank[site[k] < a.nsites ? site[k] : 0u];
+    }
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (site[k] >= a.nsites) k2[k] &= 0xFFFF0000u;
+    __syncthreads();
+    // 1. rows, then cells
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * FAST_T + tid;
+        row[k] = 0;
+        if (!alive[k]) continue;
+        row[k] = row_claim(reinterpret_cast<uint32_t *>(s_c), s_a, s_b, i, s_a[i], tc[k] >> 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) cell[k] = cell_claim(s_own, k * FAST_T + tid, row[k], tc[k]);
+    __syncthreads();
+    unsigned long long hraw = 0;
+    if (!used0) {
+        // 1b (empty region). every row new: heap offsets counted now (s_own: heap words by owner),
+        // the allocation issued now and checked after the walk; no prior clocks
+        fast_rows_count<FAST_R>(n, row, strd, s_own, s_ctl);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            hb[k] = alive[k] ? (s_own[row[k]] & 0x7FFFFFFFu) + (tc[k] & 0xFFFFu) : 0u;  // (+ heap base below)
+            ent[k] = ROW_NONE;
+            if (alive[k]) flags |= 3u << (2 * k);
+        }
+        if (tid == 0 && s_ctl[1] && s_ctl[0] <= a.rs.fill) hraw = atomicAdd(a.rs.heap_top, (unsigned long long)s_ctl[1]);
+    } else {
+        // 1b (populated region). row lookups, prior clocks: does the change beat its cell's prior?
+        if (!fast_rows<FAST_R>(a, b, used0, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase, false)) return;
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            hb[k] = 0;
+            if (!alive[k]) continue;
+            const uint32_t c = tc[k] & 0xFFFFu;
+            hb[k] = row_heap(s_own[row[k]], s_hbase) + c;
+            if ((s_c[row[k]] >> c) & 1ULL) {
+                const Rec pr = load_rec(a.rs.heap + hb[k]);
+                if (prior_cmp_packed(a, pr, k1[k], k2[k]) > 0) flags |= 1u << (2 * k);
+            } else {
+                flags |= 3u << (2 * k);
+            }
+        }
+    }
+    __syncthreads();
+    // 2. member counts per cell, exclusive scan -> offsets
+    for (uint32_t i = tid; i < CAP_FAST; i += FAST_T) s_own[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) atomicAdd(&s_own[cell[k]], 1u);
+    __syncthreads();
+    {
+        const uint32_t i0 = tid * FAST_R;
+        uint32_t c[FAST_R], loc = 0;
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            c[k] = i0 + k < n ? s_own[i0 + k] : 0u;
+            loc += c[k];
+        }
+        const uint32_t lane = tid & 63, w = tid >> 6;
+        const uint32_t inc = wave_incl_scan(loc);
+        if (lane == 63) s_wsum[w] = inc;
+        __syncthreads();
+        uint32_t run = inc - loc;
+        for (uint32_t ww = 0; ww < w; ww++) run += s_wsum[ww];
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++)
+            if (i0 + k < n) {
+                s_own[i0 + k] = run;
+                run += c[k];
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) md[k] = alive[k] ? s_own[cell[k]] : 0u;
+    __syncthreads();
+    // 3. keys and positions by member slot
+    uint32_t *s_p = reinterpret_cast<uint32_t *>(s_c);
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) {
+            const uint32_t d = atomicAdd(&s_own[cell[k]], 1u);
+            s_a[d] = k1[k];
+            s_b[d] = k2[k];
+            s_p[d] = pos[k];
+            md[k] |= d << 16;
+        }
+    __syncthreads();
+    // 4. one walk over the cell's members per change: impact (strict prefix maximum in application
+    // order, above the prior clock) and winner (maximum, earliest among equals, above the prior)
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        if (!alive[k]) continue;
+        bool imp = (flags >> (2 * k)) & 1u, win = imp;
+        const uint32_t mb = md[k] & 0xFFFFu, d = md[k] >> 16, me = s_own[cell[k]];
+        for (uint32_t m = mb; m < me; m++) {
+            if (m == d) continue;
+            const uint64_t j1 = s_a[m];
+            const uint32_t j2 = s_b[m];
+            const int c = j1 != k1[k] ? (j1 > k1[k] ? 1 : -1) : (j2 != k2[k] ? (j2 > k2[k] ? 1 : -1) : 0);
+            const bool earlier = s_p[m] < pos[k];
+            if (earlier && c >= 0) imp = false;             // an earlier change already holds >= key
+            if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
+        }
+#if !(CORRO_DIAG & 1024)  // (1024: diagnostics only -- no flag stores, results not valid)
+        if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
+#endif
+        alive[k] = win;
+    }
+    if (!used0) {
+        // 4b (empty region). the heap allocation issued before the walk: room, or defer (nothing of
+        // the bucket's state written yet; its impact flags depend on the batch only)
+        if (tid == 0) {
+            const unsigned long long need = s_ctl[1];
+            const bool room = s_ctl[0] <= a.rs.fill;
+            if (!room || (need && hraw + need > a.rs.heap_cap)) {
+                if (room && need) atomicSub(a.rs.heap_top, need);
+                push_defer(a, b, room ? DEFER_HEAP : DEFER_REGION);
+                s_ctl[2] = 1;
+            } else {
+                a.rs.used[b] = s_ctl[0];
+                s_hbase = need ? hraw : 0;
+            }
+        }
+        __syncthreads();
+        if (s_ctl[2]) return;
+        // the owners' row keys and heap words again (s_a / s_b / s_own held the member lists),
+        // then the region entries
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            const uint32_t i = k * FAST_T + tid;
+            if (i < n && row[k] == i) {
+                s_a[i] = v.fresh[i].pk;
+                s_b[i] = tc[k];
+                s_own[i] = 0x80000000u | (hb[k] - (tc[k] & 0xFFFFu));
+            }
+        }
+        if (!fast_rows<FAST_R>(a, b, 0u, n, row, ent, s_a, s_b, s_own, s_c, s_ctl, &s_hbase, true)) return;
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) hb[k] += (uint32_t)s_hbase;
+    } else {
+        __syncthreads();
+        // presence words of the populated rows again (s_c held the positions)
+#pragma unroll
+        for (int k = 0; k < FAST_R; k++) {
+            const uint32_t i = k * FAST_T + tid;
+            if (ent[k] != ROW_NONE && row[k] == i) s_c[i] = a.rs.ent[ent[k]].bits[0];
+        }
+    }
+    __syncthreads();
+    // 5. winners: the rest of the clock row from the staged record, into its heap slot; presence bits
+    uint32_t nlive = 0;
+    constexpr int WH = (FAST_R + 1) / 2;  // two halves: the reloads of one half in flight at once
+#pragma unroll
+    for (int h = 0; h < FAST_R; h += WH) {
+        uint2 w0[WH], w16[WH], w48[WH];  // pk | db_version | seq, site
+#pragma unroll
+        for (int u = 0; u < WH && h + u < FAST_R; u++) {
+            const int k = h + u;
+            const uint32_t i = k * FAST_T + tid;
+            const uint2 *src = reinterpret_cast<const uint2 *>(v.fresh + i);
+            if (alive[k]) {
+                w0[u] = src[0];
+                w16[u] = src[2];
+                w48[u] = src[6];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < WH && h + u < FAST_R; u++) {
+            const int k = h + u;
+            Rec x;
+            if (alive[k]) {
+                x.pk = ((uint64_t)w0[u].y << 32) | w0[u].x;
+                x.cv = (int64_t)(k1[k] >> 48);
+                x.dbv = (int64_t)(((uint64_t)w16[u].y << 32) | w16[u].x);
+                x.v0 = (((k1[k] & 0xFFFFFFFFFFFFULL) << 16) | (k2[k] >> 16)) ^ 0x8000000000000000ULL;
+                x.v1 = 0;
+                x.tcid = tc[k];
+                x.seq = w48[u].x;
+                x.site = w48[u].y;
+                x.pos = pos[k];
+                x.meta = CORRO_INTEGER;
+                if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
+                x.cl = 1;
+                x.pos = hb[k];
+                if ((flags >> (2 * k + 1)) & 1u) {
+                    atomicOr(reinterpret_cast<unsigned long long *>(&s_c[row[k]]), 1ULL << (tc[k] & 0xFFFFu));
+                    nlive++;
+                }
+            }
+            store_rec_wave(a.rs.heap, hb[k], x, alive[k]);
+        }
+    }
+    nlive = wave_sum_u32(nlive);
+    if ((tid & 63) == 0 && nlive) atomicAdd(&s_live, (unsigned long long)nlive);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * FAST_T + tid;
+        if (ent[k] != ROW_NONE && row[k] == i) {
+            a.rs.ent[ent[k]].bits[0] = s_c[i];
+            if (a.touch) touch_append(a, v.fresh[i].pk, tc[k] >> 16);
+        }
+    }
+    if (tid == 0 && s_live) atomicAdd(&a.misc[MISC_LIVE], s_live);
+}
+
 __device__ inline uint32_t bucket_of_block(const MergeArgs &a) {
     return a.bucket_list ? a.bucket_list[blockIdx.x] : blockIdx.x;
 }
@@ -2161,7 +2401,8 @@ k_merge_fast_int(MergeArgs a) {
     }
     if constexpr (IMPACT) {
         (void)cvbig;
-        fast_body_impact_int<PACKED>(a, b, v);
+        if constexpr (PACKED) fast_body_impact_packed(a, b, v);
+        else fast_body_impact_int(a, b, v);
     } else {
         fast_body<false>(a, b, v, cvbig == 0 && a.nsites <= 65536);
     }

@@ -706,6 +706,33 @@ struct NullEmit {
     __device__ inline void partial(uint64_t, uint64_t, uint64_t, uint64_t) const {}
     __device__ inline void seq(uint64_t, uint64_t, uint64_t) const {}
 };
+// NEED_NB > 0 (measured, not kept): the count walk keeps a lane's first NEED_NB needs in registers
+// (Full needs only: a lane with a Partial, or with more needs, walks again to write them itself),
+// and after the scan the wave writes the buffered needs of its contiguous output window with
+// coalesced stores (each slot fetched from its lane by a cross-lane permute), without a second walk.
+// At the 6-waves-per-SIMD register budget the buffers spill: config 4 5.52 ms (NEED_NB 0) vs 6.02 /
+// 6.48 / 7.47 ms (2 / 3 / 4), and 10.6 GB written per diff at 4 (profiles/r03_sync_need_nb.log).
+#ifndef NEED_NB
+#define NEED_NB 0
+#endif
+#if NEED_NB > 0
+struct BufEmit {
+    uint64_t (&bs)[NEED_NB];
+    uint64_t (&bt)[NEED_NB];
+    bool &spill;
+    __device__ inline void full(uint64_t q, uint64_t s, uint64_t t, uint64_t) const {
+#pragma unroll
+        for (int k = 0; k < NEED_NB; k++)
+            if (q == (uint64_t)k) {
+                bs[k] = s;
+                bt[k] = t;
+            }
+        if (q >= NEED_NB) spill = true;
+    }
+    __device__ inline void partial(uint64_t, uint64_t, uint64_t, uint64_t) const { spill = true; }
+    __device__ inline void seq(uint64_t, uint64_t, uint64_t) const {}
+};
+#endif
 
 template <bool FILL, class E>
 __device__ inline void walk_inputs(const SyncDev &in, const EntryHdr &h, const NeedsLds &L, const WgSegs &g,
@@ -753,7 +780,16 @@ __global__ void __launch_bounds__(NEEDS_T, NEEDS_PACKED_WAVES) k_needs_packed(Sy
     const uint64_t bs0 = b0.tps + b0.ops, bs1 = b1.tps + b1.ops;
     NDIAG(0);
     uint64_t nn = 0, ns = 0;
+#if NEED_NB > 0
+    uint64_t bs[NEED_NB], bt[NEED_NB];
+#pragma unroll
+    for (int k = 0; k < NEED_NB; k++) bs[k] = bt[k] = 0;
+    bool spill = false;
+    if (live) walk_inputs<true>(in, h, L, g, BufEmit{bs, bt, spill}, 0, 0, nn, ns);
+#else
+    const bool spill = true;  // (diagnostics: every lane walks again and writes its own needs)
     if (live) walk_inputs<false>(in, h, L, g, NullEmit{}, 0, 0, nn, ns);
+#endif
     NDIAG(1);
     // workgroup exclusive scan of (nn, ns)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -793,6 +829,41 @@ __global__ void __launch_bounds__(NEEDS_T, NEEDS_PACKED_WAVES) k_needs_packed(Sy
     if (live) {
         o.need_off[e] = nbase;
         o.need_count[e] = (uint32_t)nn;
+    }
+    // the wave's window [wbase, wbase + wtot): slot rel of lane src (the last lane whose window
+    // offset is <= rel), its k-th buffered need
+#if NEED_NB > 0
+    {
+        const uint32_t wex = (uint32_t)(in_n - nn), wtot = (uint32_t)__shfl(in_n, 63);
+        const uint64_t wbase = bn0 + pre_n;
+        const int buffered = !spill;
+        for (uint32_t r0 = 0; r0 < wtot; r0 += 64) {
+            const uint32_t rel = r0 + (uint32_t)lane;
+            uint32_t src = 0;
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1) {
+                const uint32_t c = src + (uint32_t)st;
+                if ((uint32_t)__shfl((int)wex, (int)c) <= rel) src = c;
+            }
+            const uint32_t k = rel - (uint32_t)__shfl((int)wex, (int)src);
+            const bool sb = __shfl(buffered, (int)src) != 0;
+            uint64_t vs = 0, vt = 0;
+#pragma unroll
+            for (int kk = 0; kk < NEED_NB; kk++) {
+                const uint64_t xs = __shfl(bs[kk], (int)src), xt = __shfl(bt[kk], (int)src);
+                if (k == (uint32_t)kk) {
+                    vs = xs;
+                    vt = xt;
+                }
+            }
+            if (rel < wtot && sb) {
+                *reinterpret_cast<ulonglong2 *>(o.range + 2 * (wbase + rel)) = make_ulonglong2(vs, vt);
+                o.kind[wbase + rel] = 0;
+            }
+        }
+    }
+#endif
+    if (live && spill) {  // a lane the buffer did not hold walks again and writes its own needs
         const PackedEmit em{o.range, o.kind, o.s_start, o.s_end};
         uint64_t n2 = 0, s2 = 0;
         walk_inputs<true>(in, h, L, g, em, nbase, sbase, n2, s2);
