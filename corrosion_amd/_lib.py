@@ -124,7 +124,7 @@ class Changeset(C.Structure):
 class Decoded(C.Structure):
     _fields_ = [("nframes", C.c_uint64), ("nchanges", C.c_uint64), ("nsets", C.c_uint64), ("cs", C.c_void_p),
                 ("actor_ids", C.c_void_p), ("status", C.c_void_p), ("changes", Changes), ("set_start", C.c_void_p),
-                ("set_end", C.c_void_p)]
+                ("set_end", C.c_void_p), ("cs_dev", C.c_void_p), ("n_dev", C.c_uint64)]
 
 
 class ProcessOut(C.Structure):

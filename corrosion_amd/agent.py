@@ -269,19 +269,15 @@ class Agent:
 
     def process_frames(self, buf, payload=0):
         """Wire bytes -> merge without leaving the GPU: decode length-delimited changeset frames
-        on the device (corro_decode_frames, CORRO_MEM_DEVICE) and hand the decoded batch to
-        process_multiple_changes where it lies (CORRO_MEM_DEVICE: no change crosses PCIe again).
-        Frames with a non-zero decode status are not applied. Returns (Processed over the applied
-        frames, with .impact = per-change impactful flags as a CUDA uint8 tensor, per-frame decode
-        status)."""
+        on the device (corro_decode_frames, CORRO_MEM_DEVICE, with the kept frames' headers built on
+        the device too) and hand the decoded batch and headers to process_multiple_changes where
+        they lie (CORRO_MEM_DEVICE_HEADERS: no change or header crosses PCIe again; the known
+        outcomes come back once). Frames with a non-zero decode status are not applied. Returns
+        (Processed over the applied frames, with .impact = per-change impactful flags as a CUDA
+        uint8 tensor, per-frame decode status)."""
         import torch
-        dec = self.engine.decode_frames(buf, payload, device=True)
-        keep = [i for i in range(dec["nframes"]) if dec["status"][i] == 0]
-        descs = (L.Changeset * max(1, len(keep)))()
-        for j, i in enumerate(keep):
-            C.memmove(C.byref(descs[j]), C.byref(dec["cs"][i]), C.sizeof(L.Changeset))
-            if descs[j].kind == L.CORRO_CS_EMPTY_SET:
-                descs[j].change_off = descs[j].change_count = 0
+        dec = self.engine.decode_frames(buf, payload, device=True, device_headers=True)
+        nk = dec["n_dev"]
         self.site_ids = dict(enumerate(self.engine.site_ids()))   # the decoder may have registered sites
         ch = dec["changes"]
         n = int(ch["pk"].shape[0])
@@ -292,15 +288,15 @@ class Agent:
                 s.val_data, s.val_data_len = a.data_ptr(), int(a.numel())
             else:
                 setattr(s, k, a.data_ptr() if n else None)
-        known = np.zeros(max(1, len(keep)), np.int32)
+        known = torch.zeros(max(1, nk), dtype=torch.int32, device="cuda")
         imp = torch.zeros(max(1, n), dtype=torch.uint8, device="cuda")
         out = L.ProcessOut()
-        out.known = known.ctypes.data
+        out.known = known.data_ptr()
         out.impactful = imp.data_ptr()
         torch.cuda.current_stream().synchronize()
-        L.check(L.lib().corro_process_multiple_changes(self.engine._h, self.bookie._h, descs, len(keep), C.byref(s),
-                                                       L.CORRO_MEM_DEVICE, C.byref(out)))
-        res = Processed(known=[L.KNOWN.get(int(k), int(k)) for k in known[:len(keep)]])
+        L.check(L.lib().corro_process_multiple_changes(self.engine._h, self.bookie._h, C.c_void_p(dec["cs_dev"].data_ptr()),
+                                                       nk, C.byref(s), L.CORRO_MEM_DEVICE_HEADERS, C.byref(out)))
+        res = Processed(known=[L.KNOWN.get(int(k), int(k)) for k in known[:nk].cpu().tolist()])
         res.impact = imp[:n]
         res.ready = self.take_ready()
         return res, dec["status"]

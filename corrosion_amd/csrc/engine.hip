@@ -73,7 +73,7 @@ RowStore row_store(corro_ctx *ctx);
 int affinity_convert(corro_ctx *ctx, BatchDev &bd);  // affinity.hip
 
 // Oversized buckets (queued by a merge round), all at once and device-wide (the phases of
-// ovf_kernels.h): batch fields + row ids -> region lookups (prior records appended, new rows
+// ovf_kernels.h): batch fields + row owners (one pass) -> region lookups (prior records appended, new rows
 // counted; the store grows here if they do not fit, before anything is written) -> sort by (row,
 // position) -> L scan -> classify -> epoch scan -> candidate keys -> sort -> argmax / group-start
 // scans -> link -> walk (rows written back to the heap) -> [impacts] -> region fill counts.
@@ -182,8 +182,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         CORRO_HIP_TRY(hipGetLastError());
         return CORRO_OK;
     };
-    hipLaunchKernelGGL(k_ovf_load, gridb, blk, 0, s, a, d);
-    hipLaunchKernelGGL(k_ovf_rowhash, gridb, blk, 0, s, d);
+    hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
     TRY(launched());
     // dense row ids: the row count sizes the sort's key
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.recf, d.epc, d.Kb, s));
@@ -191,7 +190,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     CORRO_HIP_TRY(hipMemcpyAsync(&nrows, d.epc + (Kb - 1), 4, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     d.nrows = nrows;
-    // every row looked up in its region; prior records counted, new rows counted per bucket
+    d.rshift = pbits;
+    // every row looked up in its region; prior records counted, new rows counted per bucket (and
+    // every batch record's sort key)
     hipLaunchKernelGGL(k_ovf_lookup, gridb, blk, 0, s, a, d);
     TRY(launched());
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
@@ -228,7 +229,6 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         fprintf(stderr, "[corro ovf] buckets %llu batch records %llu prior %u rows %u key bits %u (+%u) cand key bits %u\n",
                 (unsigned long long)novf, (unsigned long long)Kb, P, nrows, key_bits, rbits, ckey_bits);
     hipLaunchKernelGGL(k_ovf_pload, grid_for(nrows), blk, 0, s, a, d);
-    hipLaunchKernelGGL(k_ovf_rowkey, gridb, blk, 0, s, d);
     TRY(launched());
     TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.key_s, d.val, d.val_s, d.K, key_bits, s));
     hipLaunchKernelGGL(k_ovf_gather, grid, blk, 0, s, d);
@@ -534,7 +534,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,
                       &ctx->d_agent_in, &ctx->d_agent_batch, &ctx->d_agent_spans, &ctx->d_agent_imp,
                       &ctx->d_agent_out, &ctx->d_agent_aux, &ctx->d_agent_fetch, &ctx->d_agent_aux2, &ctx->d_touch, &ctx->d_touch_n, &ctx->d_touch_stamp, &ctx->d_touch_tmp,
-                      &ctx->d_aff_conv, &ctx->d_aff_vals, &ctx->d_gaps_big};
+                      &ctx->d_aff_conv, &ctx->d_aff_vals, &ctx->d_gaps_big, &ctx->d_agent_hdr, &ctx->d_wire_map};
     for (DevBuf *b : bufs) b->release();
     ctx->d_pkdir.release();
     ctx->d_part_var.release();
@@ -710,9 +710,9 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
 
     TRY(ctx->d_hist.ensure((size_t)ntiles * B * 4));
     TRY(ctx->d_stage.ensure((size_t)n * sizeof(Rec)));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_bflags.p, 0, ((B + 31) / 32) * 4ULL, s));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, MISC_WORDS * 8, s));
-    CORRO_HIP_TRY(hipMemsetAsync(ctx->d_dbv_batch.p, 0, (size_t)nsites * 8, s));
+    // (bucket general bits, misc counters and per-site db_version maxima are zeroed by k_hist)
+    ApplyZero z{ctx->d_bflags.as<uint32_t>(), ctx->d_misc.as<unsigned long long>(),
+                ctx->d_dbv_batch.as<unsigned long long>(), (B + 31) / 32, (uint32_t)MISC_WORDS, nsites};
     // (1: the INTEGER impact body stores only zero flags; every other body stores each change's)
     if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 1, bd.ap ? ctx->pm_n : n, s));
 
@@ -725,7 +725,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     mark(0);
     const uint32_t one_table = ctx->tables.size() == 1 ? 1u : 0u;
     hipLaunchKernelGGL(k_hist, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B, one_table,
-                       ctx->d_hist.as<uint32_t>());
+                       ctx->d_hist.as<uint32_t>(), z);
     CORRO_HIP_TRY(hipGetLastError());
     mark(1);
     hipLaunchKernelGGL(k_colscan, dim3((B + 255) / 256), dim3(256), 0, s, ctx->d_hist.as<uint32_t>(), ntiles, B,
@@ -781,18 +781,20 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     a.pos_src = bd.ap ? ctx->pm_src : nullptr;
     uint32_t nblocks = B;
     float merge_ms = 0.f, ovf_ms = 0.f;
+    // A batch that failed validation (k_scatter's error bits in misc[0]) is never merged: the merge
+    // and the db_version fold check the bits on the device, so the non-impact path needs no host
+    // round trip between the scatter and the merge (the impact path reads MISC_CVBIG first: it picks
+    // one of two kernels). The region fill sum and the db_version fold are launched behind the first
+    // merge round; the host reads everything once, and re-runs the sum only after further rounds.
+    if (a.impact) {
+        CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, (MISC_CVBIG + 1) * 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        if (ctx->h_misc[0]) return error_from_bits(ctx->h_misc[0]);
+    }
+    bool extra_rounds = false;
     for (int round = 0;; round++) {
         if (round > 40) return fail(CORRO_E_NOMEM, "internal: the row store did not take the batch's rows");
-        // a batch that failed validation (k_scatter's error bits) is never merged
-        if (round == 0) {
-            CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, (MISC_CVBIG + 1) * 8, hipMemcpyDeviceToHost, s));
-            CORRO_HIP_TRY(hipStreamSynchronize(s));
-            if (ctx->h_misc[0]) return error_from_bits(ctx->h_misc[0]);
-            if (prof)
-                for (int i = 0; i < 4; i++) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[i], ctx->ev[i], ctx->ev[i + 1]));
-        }
         mark(4);
-        ctx->apply_wrote = true;  // from here on a failure leaves the state part-merged
         if (a.impact) {
             // the packed two-word keys of the INTEGER impact body: col_versions < 2^15, <= 2^16 sites
             const bool packed = ctx->h_misc[MISC_CVBIG] == 0 && nsites <= 65536;
@@ -813,8 +815,21 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         hipLaunchKernelGGL(k_merge_gen, dim3(std::min(nblocks, LIST_GRID)), dim3(MERGE_THREADS), 0, s, a);
         CORRO_HIP_TRY(hipGetLastError());
         mark(5);
+        if (round == 0) {
+            hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
+                               ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites,
+                               (const unsigned long long *)misc);
+            CORRO_HIP_TRY(hipMemsetAsync(misc + MISC_ROWS, 0, 8, s));
+            hipLaunchKernelGGL(k_sum_used, dim3(1), dim3(1024), 0, s, ctx->d_used.as<uint32_t>(), B, misc);
+        }
         CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, MISC_WORDS * 8, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipStreamSynchronize(s));
+        if (round == 0) {
+            if (ctx->h_misc[0]) return error_from_bits(ctx->h_misc[0]);  // (nothing merged)
+            ctx->apply_wrote = true;  // from here on a failure leaves the state part-merged
+            if (prof)
+                for (int i = 0; i < 4; i++) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[i], ctx->ev[i], ctx->ev[i + 1]));
+        }
         if (prof) {
             float ms = 0.f;
             CORRO_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[4], ctx->ev[5]));
@@ -822,12 +837,14 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         }
         const uint64_t novf = ctx->h_misc[MISC_OVF];
         if (novf) {
+            extra_rounds = true;
             TRY(run_overflow(ctx, a, novf, n, prof));
             ctx->metrics.overflow_rounds++;
             ovf_ms += ctx->last_ms[5];
         }
         const uint64_t ndefer = ctx->h_misc[MISC_DEFER];
         if (!ndefer) break;
+        extra_rounds = true;
         // grow what ran out, then merge the deferred buckets again
         const uint64_t why = ctx->h_misc[MISC_DEFER_WHY];
         ctx->metrics.deferred_rounds++;
@@ -848,12 +865,12 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         ctx->last_ms[4] = merge_ms;
         ctx->last_ms[5] = ovf_ms;
     }
-    hipLaunchKernelGGL(k_dbv_fold, dim3((nsites + 255) / 256), dim3(256), 0, s,
-                       ctx->d_dbv.as<unsigned long long>(), ctx->d_dbv_batch.as<unsigned long long>(), nsites);
-    CORRO_HIP_TRY(hipMemsetAsync(misc + MISC_ROWS, 0, 8, s));
-    hipLaunchKernelGGL(k_sum_used, dim3(1), dim3(1024), 0, s, ctx->d_used.as<uint32_t>(), B, misc);
-    CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, MISC_WORDS * 8, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (extra_rounds) {  // the overflow fold / deferred rounds changed the region fills
+        CORRO_HIP_TRY(hipMemsetAsync(misc + MISC_ROWS, 0, 8, s));
+        hipLaunchKernelGGL(k_sum_used, dim3(1), dim3(1024), 0, s, ctx->d_used.as<uint32_t>(), B, misc);
+        CORRO_HIP_TRY(hipMemcpyAsync(ctx->h_misc, misc, MISC_WORDS * 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+    }
     ctx->state_total += ctx->h_misc[MISC_LIVE];  // (a signed delta in two's complement)
     ctx->state_rows = ctx->h_misc[MISC_ROWS];
 #if CORRO_DIAG & 256

@@ -188,6 +188,7 @@ struct corro_ctx {
     corro::DevBuf d_wire;         // wire decode: frame bytes, headers, staged outputs
     corro::DevBuf d_wire_schema;  // wire decode: table / column names
     corro::DevBuf d_wire_sites;   // wire decode: hash of the registered site ids
+    corro::DevBuf d_wire_map;     // wire decode: kept-frame index map (cs_dev output)
     bool wire_schema_ready = false;
     const uint8_t *wire_names = nullptr;
     const uint32_t *wire_toff = nullptr, *wire_tlen = nullptr, *wire_tbase = nullptr, *wire_tn = nullptr,

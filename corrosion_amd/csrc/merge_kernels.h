@@ -196,10 +196,23 @@ __device__ inline uint32_t site_rank_of(const MergeArgs &a, uint32_t site) {
 // Tile histogram of row buckets. Reads only pk + table_cid (12 B per change), or only pk when the
 // schema has one table (every change's bucket then uses table 0; k_scatter does the same and
 // reports a bad table id as an error).
+// The per-apply words the scatter and merge accumulate into (bucket general bits, misc counters,
+// per-site db_version maxima) are zeroed here too: three fills fewer per apply.
+struct ApplyZero {
+    uint32_t *bflags;
+    unsigned long long *misc, *dbv_batch;
+    uint32_t nbflags, nmisc, nsites;
+};
 static __global__ void __launch_bounds__(HIST_THREADS)
-k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t *__restrict__ hist_out) {
+k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t *__restrict__ hist_out, ApplyZero z) {
     extern __shared__ uint32_t hist[];
     const uint32_t B = 1u << log2B;
+    {
+        const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+        for (uint32_t i = t; i < z.nbflags; i += nt) z.bflags[i] = 0;
+        for (uint32_t i = t; i < z.nmisc; i += nt) z.misc[i] = 0;
+        for (uint32_t i = t; i < z.nsites; i += nt) z.dbv_batch[i] = 0;
+    }
     for (uint32_t i = threadIdx.x; i < B; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     const uint32_t begin = blockIdx.x * tile;
@@ -2371,6 +2384,7 @@ __device__ inline uint32_t bucket_of_block(const MergeArgs &a) {
 template <bool IMPACT, bool PACKED = false>
 static __global__ void __launch_bounds__(FAST_T, FAST_WAVES_EU)
 k_merge_fast_int(MergeArgs a) {
+    if (a.misc[0]) return;  // the batch failed k_scatter's validation: nothing is merged
     const uint32_t b = bucket_of_block(a);
     // every per-bucket word is loaded up front (independent scalar loads, one latency)
     BucketView v;
@@ -2497,10 +2511,12 @@ static __global__ void k_validate(BatchDev in, uint32_t nsites, const uint16_t *
     if (__any(wide != 0) && (threadIdx.x & 63) == 0) atomicOr(&misc[3], 1ULL);
 }
 
-// crsql_db_versions fold after a successful batch
+// crsql_db_versions fold after a batch that passed validation (misc[0]: k_scatter's error bits; a
+// batch that fails them is never merged)
 static __global__ void k_dbv_fold(unsigned long long *__restrict__ dbv, const unsigned long long *__restrict__ batch,
-                           uint32_t nsites) {
+                           uint32_t nsites, const unsigned long long *__restrict__ misc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (misc[0]) return;
     if (i < nsites && batch[i] > dbv[i]) dbv[i] = batch[i];
 }
 

@@ -25,11 +25,12 @@
 // (tools/proto_rowfold.py); tests/test_gpu_merge.py checks this implementation.
 //
 // Phases:
-//   k_ovf_load, k_ovf_rowhash       fields; row owners (open addressing per bucket, read-before-CAS)
+//   k_ovf_loadhash                  fields; row owners (open addressing per bucket, read-before-CAS)
 //   scan of owner flags               dense row ids
 //   k_ovf_lookup, scan, k_ovf_pload   each row looked up in its region (new rows counted per bucket
 //                                     for the host's capacity check), prior records appended
-//   k_ovf_rowkey                      compact positions (prior: slot index < pm; batch: pm + i)
+//   (k_ovf_lookup also writes the batch records' sort keys: dense row << rshift | compact position,
+//   prior slots [0, pm), then the batch in application order: log2(rows) + log2(pm + batch) bits)
 //   radix sort by (row, position)                                       [prims.hip, rocPRIM]
 //   k_ovf_gather                    cl in sorted order, row starts
 //   exclusive max-scan of cl by row -> L                                [rocPRIM scan_by_key]
@@ -156,10 +157,17 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b, const uint8_t *
 
 #define OVF_LOOP(i, N) for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (N); i += gridDim.x * blockDim.x)
 
-static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
+// Record fields and row owners in one pass: each batch record's fields are loaded from its staged
+// 64-B record and the record is hashed into its bucket's row table (open addressing per bucket, a
+// slot read before it is claimed); an occupied slot's row key is compared with the claimant's staged
+// record (read-only in this kernel, so no ordering against the claimant's own field writes).
+static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
+    const uint32_t lane = threadIdx.x & 63;
     OVF_LOOP(r, d.Kb) {
         const uint32_t b = ovf_bucket_of(d, r);
-        const uint32_t si = a.stage_off[a.ovf_list[b]] + (r - d.koff[b]);
+        const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
+        const uint32_t sbase = a.stage_off[a.ovf_list[b]];
+        const uint32_t si = sbase + (r - kb);
         const Rec x = load_rec(a.stage + si);
         d.pb[r] = b;
         d.src[r] = si;
@@ -168,19 +176,11 @@ static __global__ void k_ovf_load(MergeArgs a, OvfDev d) {
         d.tc[r] = x.tcid;
         d.cl[r] = x.cl;
         d.pos[r] = x.pos;
-    }
-}
-
-static __global__ void k_ovf_rowhash(OvfDev d) {
-    const uint32_t lane = threadIdx.x & 63;
-    OVF_LOOP(r, d.Kb) {
-        const uint32_t b = d.pb[r];
-        const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
         uint32_t S = 1;
         while (S < 2 * n) S <<= 1;
         uint32_t *slots = d.slots + d.slot_off[b];
-        const uint64_t pk = d.pk[r];
-        const uint32_t t = d.tc[r] >> 16;
+        const uint64_t pk = x.pk;
+        const uint32_t t = x.tcid >> 16;
         auto probe = [&]() -> uint32_t {
             uint32_t slot = row_hash(pk, t) & (S - 1);
             while (true) {
@@ -188,7 +188,8 @@ static __global__ void k_ovf_rowhash(OvfDev d) {
                 uint32_t o = slots[slot];
                 if (o == 0) o = atomicCAS(&slots[slot], 0u, r - kb + 1);
                 if (o == 0) return r - kb;
-                if (d.pk[kb + o - 1] == pk && (d.tc[kb + o - 1] >> 16) == t) return o - 1;
+                const Rec *q = a.stage + sbase + (o - 1);
+                if (q->pk == pk && (q->tcid >> 16) == t) return o - 1;
                 slot = (slot + 1) & (S - 1);
             }
         };
@@ -226,6 +227,12 @@ static __global__ void k_ovf_rowhash(OvfDev d) {
 // adds what it writes back.
 static __global__ void k_ovf_lookup(MergeArgs a, OvfDev d) {
     OVF_LOOP(r, d.Kb) {
+        // every record: its sort key (k_ovf_rowkey's, fused here: dense rows are known by now)
+        {
+            const uint32_t kb = d.koff[d.pb[r]];
+            const uint64_t row = d.epc[kb + d.rowid[r]] - 1u;
+            d.key[r] = (row << d.rshift) | ((uint64_t)d.pm + (d.pos[r] & 0x7FFFFFFFu));
+        }
         if (!d.recf[r]) continue;
         const uint32_t row = d.epc[r] - 1u;
         const uint32_t b = d.pb[r], t = d.tc[r] >> 16;
@@ -273,18 +280,6 @@ static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
                 d.val[r] = r;
                 r++;
             }
-    }
-}
-
-// Sort keys of the batch records: rows numbered densely (inclusive scan of the owner flags, in epc)
-// and positions compacted (prior slots [0, pm), then the batch in application order), so the radix
-// sort goes through log2(rows) + log2(pm + batch) bits instead of 32 + 32.
-static __global__ void k_ovf_rowkey(OvfDev d) {
-    OVF_LOOP(r, d.Kb) {
-        const uint32_t kb = d.koff[d.pb[r]];
-        const uint64_t row = d.epc[kb + d.rowid[r]] - 1u;
-        const uint32_t pos = d.pos[r];
-        d.key[r] = (row << d.rshift) | ((uint64_t)d.pm + (pos & 0x7FFFFFFFu));
     }
 }
 

@@ -684,17 +684,20 @@ __device__ inline WgSegs stage_inputs_b(const SyncDev &in, const WgBound &b0, co
 // the workgroup reads them off its own segment bounds), compacted within the workgroup: count walk
 // over the LDS-staged inputs, workgroup scan, fill walk. Needs are written as one 16-B pair + a kind
 // byte (Partial: {version, first seq slot << 24 | seq ranges}), so a wave's stores cover whole lines.
+#ifndef NEED_DIAG  // diagnostics only (results not valid): 1 = no kind stores, 2 = no range stores
+#define NEED_DIAG 0
+#endif
 struct PackedEmit {
     uint64_t *range;
     uint8_t *kind;
     uint64_t *s_start, *s_end;
     __device__ inline void full(uint64_t q, uint64_t s, uint64_t t, uint64_t) const {
-        *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(s, t);
-        kind[q] = 0;
+        if (!(NEED_DIAG & 2)) *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(s, t);
+        if (!(NEED_DIAG & 1)) kind[q] = 0;
     }
     __device__ inline void partial(uint64_t q, uint64_t v, uint64_t sr, uint64_t cnt) const {
-        *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(v, (sr << 24) | cnt);
-        kind[q] = 1;
+        if (!(NEED_DIAG & 2)) *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(v, (sr << 24) | cnt);
+        if (!(NEED_DIAG & 1)) kind[q] = 1;
     }
     __device__ inline void seq(uint64_t j, uint64_t s, uint64_t t) const {
         s_start[j] = s;

@@ -552,6 +552,26 @@ uint64_t hmix(uint64_t x) {
 }
 
 // device copies of the schema names (once) and of the site hash (whenever sites were added)
+// the kept frames' headers on the device (map[f] = output index, ~0 = dropped)
+__global__ void k_wire_cs(WireDev d, const uint32_t *__restrict__ map, corro_changeset *__restrict__ out) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= d.nframes || map[f] == 0xFFFFFFFFu) return;
+    corro_changeset c;
+    const uint32_t k = d.cs_kind[f];
+    c.actor_id = nullptr;
+    c.site = d.site[f];
+    c.kind = k == 0 ? CORRO_CS_EMPTY : (k == 1 ? CORRO_CS_FULL : CORRO_CS_EMPTY_SET);
+    c.version_start = d.v0[f];
+    c.version_end = d.v1[f];
+    c.seq_start = d.s0[f];
+    c.seq_end = d.s1[f];
+    c.last_seq = d.last[f];
+    c.ts = d.ts[f];
+    c.change_off = k == 2 ? 0 : d.chg_off[f];
+    c.change_count = k == 2 ? 0 : d.nchg[f];
+    out[map[f]] = c;
+}
+
 int wire_tables(corro_ctx *ctx) {
     if (!ctx->wire_schema_ready) {
         std::vector<uint8_t> names;
@@ -891,6 +911,22 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
         if (mem == CORRO_MEM_DEVICE)
             CORRO_HIP_TRY(hipMemcpyAsync(const_cast<uint64_t *>(oc.pk), pk.data(), NC * 8, hipMemcpyHostToDevice, s));
         CORRO_HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (out->cs_dev) {  // the kept headers for CORRO_MEM_DEVICE_HEADERS, built where they lie
+        std::vector<uint32_t> map(F);
+        uint64_t k = 0;
+        for (uint32_t f = 0; f < F; f++) map[f] = st[f] == 0 ? (uint32_t)k++ : 0xFFFFFFFFu;
+        if (int rc = ctx->d_wire_map.ensure(F * 4ULL + 256)) return rc;
+        CORRO_HIP_TRY(hipMemcpyAsync(ctx->d_wire_map.p, map.data(), F * 4ULL, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_wire_cs, dim3((F + 255) / 256), dim3(256), 0, s, d, ctx->d_wire_map.as<uint32_t>(), out->cs_dev);
+        CORRO_HIP_TRY(hipGetLastError());
+        CORRO_HIP_TRY(hipStreamSynchronize(s));  // (map is a host vector)
+        out->n_dev = k;
+    }
+    if (!out->cs) {
+        if (out->status)
+            for (uint32_t f = 0; f < F; f++) out->status[f] = st[f];
+        return CORRO_OK;
     }
     uint64_t coff = 0, soff = 0;
     for (uint32_t f = 0; f < F; f++) {

@@ -451,12 +451,15 @@ class MergeEngine:
         return out
 
     # ---- wire decode ------------------------------------------------------------------------
-    def decode_frames(self, buf, payload=0, device=False):
+    def decode_frames(self, buf, payload=0, device=False, device_headers=False):
         """Decode length-delimited speedy frames (corro_decode_frames; payload 0 = SyncMessage,
         1 = UniPayload) on the GPU. Returns {"cs": ctypes array of corro_changeset (one per
         frame), "status": int32[], "changes": SoA dict, "set_start"/"set_end"}: host numpy arrays,
         or with device=True CUDA tensors that stay on the GPU (the batch
-        corro_process_multiple_changes / corro_apply_batch take with CORRO_MEM_DEVICE)."""
+        corro_process_multiple_changes / corro_apply_batch take with CORRO_MEM_DEVICE). With
+        device_headers=True (and device=True) also "cs_dev": the status-0 frames' headers as a CUDA
+        uint8 tensor of corro_changeset records built on the device, and "n_dev" of them (for
+        CORRO_MEM_DEVICE_HEADERS)."""
         lib = L.lib()
         buf = bytes(buf)
         d = L.Decoded()
@@ -487,6 +490,12 @@ class MergeEngine:
         if device:
             d.changes.val_data, d.changes.val_data_len = vdata.data_ptr(), len(buf)
         d.set_start, d.set_end = ptr(ss), ptr(se)
+        cs_dev = None
+        if device and device_headers:
+            import torch
+            cs_dev = torch.zeros(max(F, 1) * C.sizeof(L.Changeset), dtype=torch.uint8, device="cuda")
+            d.cs_dev = cs_dev.data_ptr()
+            torch.cuda.current_stream().synchronize()
         if F:
             L.check(lib.corro_decode_frames(self._h, buf, len(buf), payload, mem, C.byref(d), 1))
         changes = {k: a[:NC] for k, a in ch.items()}
@@ -495,8 +504,11 @@ class MergeEngine:
         else:
             for k in LONG_FIELDS:
                 changes.pop(k)
-        return {"cs": cs, "nframes": F, "actors": actors, "status": status[:F],
-                "changes": changes, "set_start": ss[:NS], "set_end": se[:NS]}
+        out = {"cs": cs, "nframes": F, "actors": actors, "status": status[:F],
+               "changes": changes, "set_start": ss[:NS], "set_end": se[:NS]}
+        if cs_dev is not None:
+            out["cs_dev"], out["n_dev"] = cs_dev, int(d.n_dev) if F else 0
+        return out
 
     # ---- changeset extraction (server side of a sync need) ---------------------------------
     def extract_changes(self, needs):

@@ -578,11 +578,17 @@ int corro_generate_sync(corro_bookie *bk, const uint8_t *self_actor, corro_sync_
 enum { CORRO_PAYLOAD_SYNC = 0, CORRO_PAYLOAD_UNI = 1 };
 typedef struct {
     uint64_t nframes, nchanges, nsets;      /* pass 0 outputs, pass 1 inputs */
-    corro_changeset *cs;                    /* host, nframes */
-    uint8_t *actor_ids;                     /* host, 16 * nframes */
+    corro_changeset *cs;                    /* host, nframes (optional when cs_dev is set) */
+    uint8_t *actor_ids;                     /* host, 16 * nframes (with cs) */
     int32_t *status;                        /* host, nframes (optional) */
     corro_changes changes;                  /* nchanges each (mem); val1/val_type/val_len/ts optional */
     uint64_t *set_start, *set_end;          /* nsets each (mem) */
+    /* optional, pass 1: the headers of the frames with status 0, in frame order, written on the
+     * device into cs_dev (device, nframes entries) for corro_process_multiple_changes with
+     * CORRO_MEM_DEVICE_HEADERS; EmptySet headers carry change_count 0 there; actor_id is NULL.
+     * n_dev = how many were written. */
+    corro_changeset *cs_dev;
+    uint64_t n_dev;
 } corro_decoded;
 int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t len, int payload, int mem, corro_decoded *out,
                         int pass);
