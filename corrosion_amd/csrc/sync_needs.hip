@@ -754,17 +754,42 @@ __device__ inline void walk_inputs(const SyncDev &in, const EntryHdr &h, const N
     }
 }
 
-// err[0] |= 1: a workgroup's needs exceed its bound slots (overlapping input ranges); 2: a partial
+// err[0] |= 1: an entry's needs exceed its bound slots (overlapping input ranges); 2: a partial
 // with >= 2^24 seq ranges or a seq slot >= 2^40 (not representable in the packed word)
 #ifndef NEEDS_PACKED_WAVES
 #define NEEDS_PACKED_WAVES 6  // waves per SIMD the compiler budgets registers for: LDS allows 6
-                              // workgroups per CU; at 6 (84 B of spills) 5.25 ms vs 6.92 ms at 4 (no spills)
+                              // workgroups per CU
 #endif
+// PackedEmit bounded by the entry's own slots: nothing is written past them (an entry whose needs
+// exceed its bound -- overlapping input ranges -- only sets the error)
+struct BoundedEmit {
+    PackedEmit e;
+    uint64_t qlim, slim;
+    bool *over;
+    __device__ inline void full(uint64_t q, uint64_t s, uint64_t t, uint64_t sr) const {
+        if (q < qlim) e.full(q, s, t, sr);
+        else *over = true;
+    }
+    __device__ inline void partial(uint64_t q, uint64_t v, uint64_t sr, uint64_t cnt) const {
+        if (q < qlim) e.partial(q, v, sr, cnt);
+        else *over = true;
+    }
+    __device__ inline void seq(uint64_t j, uint64_t s, uint64_t t) const {
+        if (j < slim) e.seq(j, s, t);
+        else *over = true;
+    }
+};
+
+// One walk per entry, written straight into the slots its own output bound reserves: entry e's
+// needs start at tn_off[e] + on_off[e] + tp_off[e] + op_off[e] + e (the prefix of the per-entry
+// bound our + their need ranges + their + our partial versions + 1), its seq ranges at
+// tps_off[tp_off[e]] + ops_off[op_off[e]]. Every bound offset is a sum of CSR offsets the lane
+// loads anyway, so there is no count walk and no scan (round 2 compacted the slots within each
+// 256-entry run: a count walk, a workgroup scan, then the fill walk).
 __global__ void __launch_bounds__(NEEDS_T, NEEDS_PACKED_WAVES) k_needs_packed(SyncDev in, corro_needs_packed_out o, uint64_t need_slots,
                                                           uint64_t seq_slots, unsigned long long *err,
                                                           const WgBound *__restrict__ wb) {
     __shared__ NeedsLds L;
-    __shared__ uint64_t s_wn[NEEDS_T / 64], s_ws[NEEDS_T / 64];
 #if defined(CORRO_DIAG) && (CORRO_DIAG & 128)
     unsigned long long dt0 = wall_clock64();
 #define NDIAG(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&err[1 + (k)], t_ - dt0); dt0 = t_; } } while (0)
@@ -772,106 +797,35 @@ __global__ void __launch_bounds__(NEEDS_T, NEEDS_PACKED_WAVES) k_needs_packed(Sy
 #define NDIAG(k) do { } while (0)
 #endif
     const uint64_t e0 = (uint64_t)blockIdx.x * NEEDS_T;
-    const uint64_t e1 = min(in.n, e0 + NEEDS_T);
     const uint64_t e = e0 + threadIdx.x;
     const bool live = e < in.n;
     const EntryHdr h = load_entry(in, live ? e : e0);
-    // the workgroup's CSR window (k_needs_bounds) also fixes its bound slot windows
     const WgBound b0 = wb[blockIdx.x], b1 = wb[blockIdx.x + 1];
     const WgSegs g = stage_inputs_b(in, b0, b1, L);
-    const uint64_t bn0 = g.tn_lo + g.on_lo + g.tp_lo + g.op_lo + e0, bn1 = g.tn_hi + g.on_hi + g.tp_hi + g.op_hi + e1;
-    const uint64_t bs0 = b0.tps + b0.ops, bs1 = b1.tps + b1.ops;
     NDIAG(0);
+    if (!live) return;
+    // this entry's bound windows
+    const uint64_t nbase = h.tne0 + h.one0 + h.tpe0 + h.ope0 + e;
+    const uint64_t nend = h.tne1 + h.one1 + h.tpe1 + h.ope1 + e + 1;
+    // nested seq offsets: staged in LDS for the workgroup's partials [lo, hi] (when it has any)
+    auto soff = [&](const uint64_t *goff, const uint64_t *loff, uint64_t lo, uint64_t hi, uint64_t k) -> uint64_t {
+        return g.lds && hi > lo ? loff[k - lo] : goff[k];
+    };
+    const uint64_t tps0 = in.tps_off ? soff(in.tps_off, L.tpso, g.tp_lo, g.tp_hi, h.tpe0) : 0;
+    const uint64_t tps1 = in.tps_off ? soff(in.tps_off, L.tpso, g.tp_lo, g.tp_hi, h.tpe1) : 0;
+    const uint64_t ops0 = in.ops_off ? soff(in.ops_off, L.opso, g.op_lo, g.op_hi, h.ope0) : 0;
+    const uint64_t ops1 = in.ops_off ? soff(in.ops_off, L.opso, g.op_lo, g.op_hi, h.ope1) : 0;
+    const uint64_t sbase = tps0 + ops0, send = tps1 + ops1;
+    bool over = nend > need_slots || send > seq_slots;
+    const BoundedEmit em{PackedEmit{o.range, o.kind, o.s_start, o.s_end}, over ? nbase : nend, over ? sbase : send,
+                         &over};
     uint64_t nn = 0, ns = 0;
-#if NEED_NB > 0
-    uint64_t bs[NEED_NB], bt[NEED_NB];
-#pragma unroll
-    for (int k = 0; k < NEED_NB; k++) bs[k] = bt[k] = 0;
-    bool spill = false;
-    if (live) walk_inputs<true>(in, h, L, g, BufEmit{bs, bt, spill}, 0, 0, nn, ns);
-#else
-    const bool spill = true;  // (diagnostics: every lane walks again and writes its own needs)
-    if (live) walk_inputs<false>(in, h, L, g, NullEmit{}, 0, 0, nn, ns);
-#endif
+    walk_inputs<true>(in, h, L, g, em, nbase, sbase, nn, ns);
     NDIAG(1);
-    // workgroup exclusive scan of (nn, ns)
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t in_n = nn, in_s = ns;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t yn = __shfl_up(in_n, d), ys = __shfl_up(in_s, d);
-        if (lane >= d) {
-            in_n += yn;
-            in_s += ys;
-        }
-    }
-    if (lane == 63) {
-        s_wn[wv] = in_n;
-        s_ws[wv] = in_s;
-    }
-    __syncthreads();
-    uint64_t pre_n = 0, pre_s = 0, tot_n = 0, tot_s = 0;
-#pragma unroll
-    for (int w = 0; w < (int)(NEEDS_T / 64); w++) {
-        if (w < wv) {
-            pre_n += s_wn[w];
-            pre_s += s_ws[w];
-        }
-        tot_n += s_wn[w];
-        tot_s += s_ws[w];
-    }
-    if (bn0 + tot_n > bn1 || bs0 + tot_s > bs1 || bn1 > need_slots || bs1 > seq_slots) {
-        if (threadIdx.x == 0) atomicOr(err, 1ULL);
-        return;  // uniform
-    }
-    if (bs1 >= (1ULL << 40) || __any(nn > 0xFFFFFFFFULL || ns >= (1ULL << 24))) {
-        if (threadIdx.x == 0) atomicOr(err, 2ULL);
-        return;
-    }
-    const uint64_t nbase = bn0 + pre_n + in_n - nn, sbase = bs0 + pre_s + in_s - ns;
-    NDIAG(2);
-    if (live) {
-        o.need_off[e] = nbase;
-        o.need_count[e] = (uint32_t)nn;
-    }
-    // the wave's window [wbase, wbase + wtot): slot rel of lane src (the last lane whose window
-    // offset is <= rel), its k-th buffered need
-#if NEED_NB > 0
-    {
-        const uint32_t wex = (uint32_t)(in_n - nn), wtot = (uint32_t)__shfl(in_n, 63);
-        const uint64_t wbase = bn0 + pre_n;
-        const int buffered = !spill;
-        for (uint32_t r0 = 0; r0 < wtot; r0 += 64) {
-            const uint32_t rel = r0 + (uint32_t)lane;
-            uint32_t src = 0;
-#pragma unroll
-            for (int st = 32; st >= 1; st >>= 1) {
-                const uint32_t c = src + (uint32_t)st;
-                if ((uint32_t)__shfl((int)wex, (int)c) <= rel) src = c;
-            }
-            const uint32_t k = rel - (uint32_t)__shfl((int)wex, (int)src);
-            const bool sb = __shfl(buffered, (int)src) != 0;
-            uint64_t vs = 0, vt = 0;
-#pragma unroll
-            for (int kk = 0; kk < NEED_NB; kk++) {
-                const uint64_t xs = __shfl(bs[kk], (int)src), xt = __shfl(bt[kk], (int)src);
-                if (k == (uint32_t)kk) {
-                    vs = xs;
-                    vt = xt;
-                }
-            }
-            if (rel < wtot && sb) {
-                *reinterpret_cast<ulonglong2 *>(o.range + 2 * (wbase + rel)) = make_ulonglong2(vs, vt);
-                o.kind[wbase + rel] = 0;
-            }
-        }
-    }
-#endif
-    if (live && spill) {  // a lane the buffer did not hold walks again and writes its own needs
-        const PackedEmit em{o.range, o.kind, o.s_start, o.s_end};
-        uint64_t n2 = 0, s2 = 0;
-        walk_inputs<true>(in, h, L, g, em, nbase, sbase, n2, s2);
-    }
-    NDIAG(3);
+    o.need_off[e] = nbase;
+    o.need_count[e] = (uint32_t)nn;
+    if (over || nbase + nn > nend || sbase + ns > send) atomicOr(err, 1ULL);
+    if (send >= (1ULL << 40) || nn > 0xFFFFFFFFULL || ns >= (1ULL << 24)) atomicOr(err, 2ULL);
 }
 
 }  // namespace corro

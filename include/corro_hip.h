@@ -356,10 +356,12 @@ int corro_compute_needs(corro_ctx *ctx, const corro_sync_entries *in, int mem,
  * re-run with. corro_needs_bound gives caps that always suffice for disjoint need ranges. */
 int corro_compute_needs_onepass(corro_ctx *ctx, const corro_sync_entries *in, corro_needs_out *out,
                               uint64_t need_cap, uint64_t seq_cap, uint64_t *totals);
-/* Packed one-pass form for DEVICE-resident entries and outputs: no count pass, no look-back. Entry
- * e's needs occupy need slots [need_off[e], need_off[e] + need_count[e]) in reference order
- * (sync.rs:164-245); slots are compact within each run of 256 entries and runs start at the slots
- * their output bounds reserve, so need_slots / seq_slots = corro_needs_bound's caps. Per need slot q:
+/* Packed one-pass form for DEVICE-resident entries and outputs: one walk per entry, no count pass,
+ * no scan. Entry e's needs occupy need slots [need_off[e], need_off[e] + need_count[e]) in reference
+ * order (sync.rs:164-245), starting at the slots its own output bound reserves (tn_off[e] +
+ * on_off[e] + tp_off[e] + op_off[e] + e; its seq ranges at tps_off[tp_off[e]] + ops_off[op_off[e]]):
+ * slots past need_count[e] up to the next entry's are left unwritten, and need_slots / seq_slots =
+ * corro_needs_bound's caps. Per need slot q:
  * kind[q] 0 Full{versions: range[2q]..=range[2q+1]}, 1 Partial{version: range[2q], seqs:
  * s_start/s_end[(range[2q+1] >> 24) + j] for j < (range[2q+1] & 0xFFFFFF)}. CORRO_E_RANGE when need
  * ranges overlap (bounds exceeded: use corro_compute_needs) or a partial carries >= 2^24 seq ranges. */

@@ -263,3 +263,89 @@ def test_device_headers_fast_actors_match_restatement(seed, clean):
 def test_device_headers_fast_gather_path(monkeypatch):
     monkeypatch.setenv("CORRO_AGENT_GATHER", "1")
     _check_against_oracle(14, device="headers", clean=(0, 2, 4))
+
+
+def _dev_call(eng, bk, descs, n_cs, batch_arrays, n):
+    """corro_process_multiple_changes with CORRO_MEM_DEVICE_HEADERS on raw descriptors; returns
+    (rc, known list)."""
+    import torch
+    from corrosion_amd import _lib as L
+    s = L.Changes()
+    s.n = n
+    keep = []
+    for k, a in batch_arrays.items():
+        t = torch.from_numpy(a.view({8: np.int64, 4: np.int32, 1: np.uint8}[a.itemsize])).cuda()
+        keep.append(t)
+        setattr(s, k, t.data_ptr())
+    dcs = torch.from_numpy(np.frombuffer(bytes(descs), np.uint8).copy()).cuda()
+    dknown = torch.full((max(1, n_cs),), 77, dtype=torch.int32, device="cuda")
+    out = L.ProcessOut()
+    out.known = dknown.data_ptr()
+    torch.cuda.synchronize()
+    rc = L.lib().corro_process_multiple_changes(eng._h, bk._h, C.c_void_p(dcs.data_ptr()), n_cs, C.byref(s),
+                                                L.CORRO_MEM_DEVICE_HEADERS, C.byref(out))
+    return rc, dknown[:n_cs].cpu().tolist()
+
+
+def _one_full_batch(site, version, k, pk0=1):
+    rows = [dict(pk=pk0 + j, table_cid=(0 << 16) | 1, col_version=1, db_version=version, cl=1, seq=j, site=site,
+                 val0=j, val_type=1, ts=5) for j in range(k)]
+    return {key: np.array([r[key] for r in rows], dt) for key, dt in FIELDS.items()}
+
+
+def test_device_headers_bad_span_and_site_fail_untouched():
+    """A span outside the batch or an unregistered site ordinal fails the call before anything is
+    decided: every outcome Skipped, no state, no bookkeeping (the host-header path's errors)."""
+    import corrosion_amd as ca
+    from corrosion_amd import _lib as L
+    import synth
+    ids = synth.site_ids(2, 5)
+    eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 10)
+    ords = eng.register_sites(ids)
+    bk = ca.agent.Bookie()
+    arrs = _one_full_batch(int(ords[0]), 1, 4)
+    for bad in ("span", "site"):
+        descs = (L.Changeset * 2)()
+        for i in range(2):
+            d = descs[i]
+            d.site, d.kind = int(ords[0]), L.CORRO_CS_FULL
+            d.version_start = d.version_end = i + 1
+            d.seq_start, d.seq_end, d.last_seq = 0, 1, 1
+            d.change_off, d.change_count = 2 * i, 2
+        if bad == "span":
+            descs[1].change_count = 3          # [2, 5) is outside the 4-change batch
+        else:
+            descs[1].site = 99                 # not a registered ordinal
+        rc, known = _dev_call(eng, bk, descs, 2, arrs, 4)
+        assert rc == -1                       # CORRO_E_INVALID
+        assert known == [0, 0]
+        assert eng.count() == 0
+        assert bk.last(bytes(ids[0])) is None
+
+
+def test_device_headers_empty_and_zero_calls():
+    """No changesets at all, and a call of only empty Full versions (no changes): the latter bump
+    crsql_db_versions and the bookkeeping, merge nothing."""
+    import corrosion_amd as ca
+    from corrosion_amd import _lib as L
+    import synth
+    ids = synth.site_ids(2, 6)
+    eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 10)
+    ords = eng.register_sites(ids)
+    bk = ca.agent.Bookie()
+    arrs = _one_full_batch(int(ords[1]), 1, 1)
+    rc, known = _dev_call(eng, bk, (L.Changeset * 1)(), 0, arrs, 1)
+    assert rc == 0 and known == []
+    descs = (L.Changeset * 3)()
+    for i in range(3):
+        d = descs[i]
+        d.site, d.kind = int(ords[1]), L.CORRO_CS_FULL
+        d.version_start = d.version_end = i + 1
+        d.seq_start = d.seq_end = d.last_seq = 0
+        d.change_off, d.change_count = 0, 0
+    rc, known = _dev_call(eng, bk, descs, 3, arrs, 1)
+    assert rc == 0
+    assert known == [2, 2, 2]                  # Cleared (process_empty_version)
+    assert eng.count() == 0
+    assert bk.last(bytes(ids[1])) == 3 and bk.needed(bytes(ids[1])) == []
+    assert list(eng.db_versions())[int(ords[1])] == 3
