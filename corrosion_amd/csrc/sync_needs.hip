@@ -687,16 +687,28 @@ __device__ inline WgSegs stage_inputs_b(const SyncDev &in, const WgBound &b0, co
 #ifndef NEED_DIAG  // diagnostics only (results not valid): 1 = no kind stores, 2 = no range stores
 #define NEED_DIAG 0
 #endif
+#ifndef NEED_NT    // 1: non-temporal range stores (experiment)
+#define NEED_NT 0
+#endif
 struct PackedEmit {
     uint64_t *range;
     uint8_t *kind;
     uint64_t *s_start, *s_end;
+    __device__ inline void put(uint64_t q, uint64_t a, uint64_t b) const {
+#if NEED_NT
+        typedef uint64_t v2u __attribute__((ext_vector_type(2)));
+        const v2u x = {a, b};
+        __builtin_nontemporal_store(x, reinterpret_cast<v2u *>(range + 2 * q));
+#else
+        *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(a, b);
+#endif
+    }
     __device__ inline void full(uint64_t q, uint64_t s, uint64_t t, uint64_t) const {
-        if (!(NEED_DIAG & 2)) *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(s, t);
+        if (!(NEED_DIAG & 2)) put(q, s, t);
         if (!(NEED_DIAG & 1)) kind[q] = 0;
     }
     __device__ inline void partial(uint64_t q, uint64_t v, uint64_t sr, uint64_t cnt) const {
-        if (!(NEED_DIAG & 2)) *reinterpret_cast<ulonglong2 *>(range + 2 * q) = make_ulonglong2(v, (sr << 24) | cnt);
+        if (!(NEED_DIAG & 2)) put(q, v, (sr << 24) | cnt);
         if (!(NEED_DIAG & 1)) kind[q] = 1;
     }
     __device__ inline void seq(uint64_t j, uint64_t s, uint64_t t) const {
