@@ -467,8 +467,9 @@ def agent_e2e(eng, batch, n, agent_ms=None, reps=3):
             "ratio_vs_agent_path": (med / agent_ms) if agent_ms else None, "all_current": ok,
             "impactful_changes": nimp,
             "host_headers": {"ms": med_h, "all_current": ok_h, "impactful_changes": nimp_h,
-                             "note": "the same call with the headers and known in host memory (CORRO_MEM_DEVICE: "
-                                     "header passes in host threads)"},
+                             "note": "the same call with the headers and known in host memory (CORRO_MEM_DEVICE: a "
+                                     "call this large copies the headers in parallel host threads into pinned "
+                                     "memory, uploads them chunk by chunk and runs the device header passes)"},
             "note": "corro_process_multiple_changes (CORRO_MEM_DEVICE_HEADERS: changes, headers, known, impactful "
                     "in HBM) on config 2 as 1000 actors x ~1049 versions x 64 changes arriving interleaved (batch "
                     "in arrival order), reset + fresh Bookie + call, median of "

@@ -638,6 +638,65 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     return CORRO_OK;
 }
 
+// CORRO_MEM_DEVICE with headers in host memory, for large calls: the headers are copied into a
+// pinned area in parallel chunks (each checked against the registered actor ids and uploaded as soon
+// as it is copied), then the device header passes run as with CORRO_MEM_DEVICE_HEADERS and the
+// outcomes come back in one copy. The host header walk (the form below) costs more than the copy
+// once a call carries tens of thousands of changesets.
+int process_staged_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
+                           const corro_changes *in, corro_process_out *out) {
+    corro::HdrStage st{};
+    TRY_RC(corro::agent_dev_stage_begin(ctx, ncs, &st));
+    const uint32_t nsites = corro::agent_site_count(ctx);
+    std::vector<ActorId> site_id(nsites);
+    for (uint32_t k = 0; k < nsites; k++) corro::agent_site_id(ctx, k, site_id[k].data());
+    const size_t nchunk = std::max<size_t>(1, std::min<size_t>(16, ncs / 4096));
+    std::vector<int> cerr(nchunk, CORRO_OK);
+    run_parallel(nchunk, [&](size_t k) {
+        const uint64_t lo = ncs * k / nchunk, hi = ncs * (k + 1) / nchunk;
+        std::memcpy(st.pinned + lo, cs + lo, (hi - lo) * sizeof(corro_changeset));
+        const uint8_t *last_ptr = nullptr;
+        uint32_t last_site = 0xFFFFFFFFu;
+        for (uint64_t i = lo; i < hi; i++) {
+            const corro_changeset &c = st.pinned[i];
+            if (c.site >= nsites || !c.actor_id) {
+                cerr[k] = 2;
+                return;
+            }
+            if (c.actor_id != last_ptr || c.site != last_site) {
+                if (std::memcmp(site_id[c.site].data(), c.actor_id, 16) != 0) {
+                    cerr[k] = 3;
+                    return;
+                }
+                last_ptr = c.actor_id;
+                last_site = c.site;
+            }
+        }
+        cerr[k] = corro::agent_dev_stage_upload(ctx, st, lo, hi) == CORRO_OK ? CORRO_OK : 4;
+    }, 1);
+    auto skip_all = [&]() {
+        for (uint64_t i = 0; i < ncs; i++) out->known[i] = CORRO_KNOWN_SKIPPED;
+    };
+    for (int e : cerr) {
+        if (e == CORRO_OK) continue;
+        skip_all();
+        if (e == 2) return fail(CORRO_E_INVALID, "changeset site ordinal is not registered (or actor_id is NULL)");
+        if (e == 3) return fail(CORRO_E_INVALID, "changeset site ordinal does not name its actor_id");
+        return fail(CORRO_E_DEVICE, "header upload failed");
+    }
+    corro_process_out o2 = *out;
+    o2.known = st.dknown;
+    const int rc = process_dev_headers(ctx, bk, st.dev, ncs, in, &o2);
+    out->n_ready = o2.n_ready;
+    if (rc != CORRO_OK) {
+        const std::string msg = corro_last_error();
+        skip_all();
+        return fail(rc, msg);
+    }
+    TRY_RC(corro::agent_dev_stage_known(ctx, st, out->known, ncs));
+    return CORRO_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -652,6 +711,12 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     if (nchanges && !in->table_cid) return fail(CORRO_E_INVALID, "a required batch array is NULL");
     out->n_ready = 0;
     if (mem == CORRO_MEM_DEVICE_HEADERS) return process_dev_headers(ctx, bk, cs, ncs, in, out);
+    // host headers of a device batch: staged for the device header passes when the call is large
+    // (CORRO_AGENT_STAGE_HEADERS=1 always, =0 never; tests)
+    const char *stage_e = std::getenv("CORRO_AGENT_STAGE_HEADERS");
+    const int stage_env = stage_e ? std::atoi(stage_e) : -1;
+    if (mem == CORRO_MEM_DEVICE && ncs && (stage_env == 1 || (stage_env == -1 && ncs >= 32768)))
+        return process_staged_headers(ctx, bk, cs, ncs, in, out);
 
     // CORRO_AGENT_PROFILE=1: host-side stage times of each call on stderr (tools)
     static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;

@@ -128,6 +128,18 @@ int agent_dev_batch_sorted(corro_ctx *ctx, const corro_changes *dv, uint64_t ncs
 int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown,
                              std::vector<std::pair<uint32_t, uint64_t>> *flagged_sv);
 
+// Host headers staged for the device header passes (CORRO_MEM_DEVICE with host headers, large
+// calls): a pinned area the host fills in parallel chunks, each chunk uploaded as soon as it is
+// copied, and the device outcome array copied back at the end.
+struct HdrStage {
+    corro_changeset *pinned, *dev;
+    int32_t *dknown;
+};
+int agent_dev_stage_begin(corro_ctx *ctx, uint64_t ncs, HdrStage *st);
+// async upload of headers [lo, hi) (callable from pool threads)
+int agent_dev_stage_upload(corro_ctx *ctx, const HdrStage &st, uint64_t lo, uint64_t hi);
+int agent_dev_stage_known(corro_ctx *ctx, const HdrStage &st, int32_t *known, uint64_t ncs);
+
 // every known entry back to Skipped (a failed call)
 int agent_dev_clear_known(corro_ctx *ctx, int32_t *dknown, uint64_t ncs);
 

@@ -1177,6 +1177,37 @@ int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown,
     return CORRO_OK;
 }
 
+int agent_dev_stage_begin(corro_ctx *ctx, uint64_t ncs, HdrStage *st) {
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    const size_t hb = std::max<uint64_t>(ncs, 1) * sizeof(corro_changeset);
+    if (hb > ctx->h_hdr_bytes) {
+        if (ctx->h_hdr) (void)hipHostFree(ctx->h_hdr);
+        ctx->h_hdr = nullptr;
+        ctx->h_hdr_bytes = 0;
+        CORRO_HIP_TRY(hipHostMalloc(&ctx->h_hdr, hb + hb / 4, hipHostMallocDefault));
+        ctx->h_hdr_bytes = hb + hb / 4;
+    }
+    if (int rc = ctx->d_hdr_stage.ensure(al256(hb) + al256(std::max<uint64_t>(ncs, 1) * 4))) return rc;
+    st->pinned = static_cast<corro_changeset *>(ctx->h_hdr);
+    st->dev = ctx->d_hdr_stage.as<corro_changeset>();
+    st->dknown = reinterpret_cast<int32_t *>(ctx->d_hdr_stage.as<uint8_t>() + al256(hb));
+    return CORRO_OK;
+}
+
+int agent_dev_stage_upload(corro_ctx *ctx, const HdrStage &st, uint64_t lo, uint64_t hi) {
+    if (hi <= lo) return CORRO_OK;
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));  // (pool threads have their own current device)
+    CORRO_HIP_TRY(hipMemcpyAsync(st.dev + lo, st.pinned + lo, (hi - lo) * sizeof(corro_changeset), hipMemcpyHostToDevice,
+                                 ctx->stream));
+    return CORRO_OK;
+}
+
+int agent_dev_stage_known(corro_ctx *ctx, const HdrStage &st, int32_t *known, uint64_t ncs) {
+    if (ncs) CORRO_HIP_TRY(hipMemcpyAsync(known, st.dknown, ncs * 4, hipMemcpyDeviceToHost, ctx->stream));
+    CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return CORRO_OK;
+}
+
 int agent_dev_clear_known(corro_ctx *ctx, int32_t *dknown, uint64_t ncs) {
     if (ncs) CORRO_HIP_TRY(hipMemsetAsync(dknown, 0, ncs * 4, ctx->stream));  // (CORRO_KNOWN_SKIPPED = 0)
     CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));

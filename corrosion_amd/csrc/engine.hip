@@ -80,9 +80,10 @@ int affinity_convert(corro_ctx *ctx, BatchDev &bd);  // affinity.hip
 static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nbatch, bool prof) {
     hipStream_t s = ctx->stream;
     const uint32_t B = ctx->B;
-    std::vector<uint32_t> list(novf), nc(B);
+    std::vector<uint32_t> list(novf), nc(B), used0(B);
     CORRO_HIP_TRY(hipMemcpy(list.data(), ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost));
     CORRO_HIP_TRY(hipMemcpy(nc.data(), ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
+    CORRO_HIP_TRY(hipMemcpy(used0.data(), ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost));
     std::vector<uint32_t> koff(novf + 1), soff(novf);
     uint64_t Kb = 0, S = 0;
     for (uint64_t k = 0; k < novf; k++) {
@@ -95,8 +96,13 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         S += sl;
     }
     koff[novf] = (uint32_t)Kb;
-    // prior records: at most one heap row per batch row, at most the whole state
-    const uint64_t Kmax = Kb + std::min<uint64_t>(ctx->state_total, Kb * (uint64_t)ctx->max_stride);
+    // prior records: at most one heap row per batch row, at most the rows the oversized buckets'
+    // regions hold (each at most max_stride records), at most the whole state -- the region bound
+    // keeps a hot-row batch into a large state from sizing (and failing) for the whole state
+    uint64_t region_rows = 0;
+    for (uint64_t k = 0; k < novf; k++) region_rows += used0[list[k]];
+    const uint64_t Kmax = Kb + std::min<uint64_t>(std::min<uint64_t>(ctx->state_total, region_rows * ctx->max_stride),
+                                                  Kb * (uint64_t)ctx->max_stride);
     if (Kmax >= (1ULL << 31) || S >= (1ULL << 32))
         return fail(CORRO_E_RANGE, "oversized buckets hold more than 2^31 records");
     // compact positions: prior slots [0, pm), batch change i -> pm + i
@@ -534,7 +540,8 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,
                       &ctx->d_agent_in, &ctx->d_agent_batch, &ctx->d_agent_spans, &ctx->d_agent_imp,
                       &ctx->d_agent_out, &ctx->d_agent_aux, &ctx->d_agent_fetch, &ctx->d_agent_aux2, &ctx->d_touch, &ctx->d_touch_n, &ctx->d_touch_stamp, &ctx->d_touch_tmp,
-                      &ctx->d_aff_conv, &ctx->d_aff_vals, &ctx->d_gaps_big, &ctx->d_agent_hdr, &ctx->d_wire_map};
+                      &ctx->d_aff_conv, &ctx->d_aff_vals, &ctx->d_gaps_big, &ctx->d_agent_hdr, &ctx->d_wire_map,
+                      &ctx->d_hdr_stage};
     for (DevBuf *b : bufs) b->release();
     ctx->d_pkdir.release();
     ctx->d_part_var.release();
@@ -545,6 +552,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
     }
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     if (ctx->h_agent) (void)hipHostFree(ctx->h_agent);
+    if (ctx->h_hdr) (void)hipHostFree(ctx->h_hdr);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

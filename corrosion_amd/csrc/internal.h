@@ -212,6 +212,9 @@ struct corro_ctx {
     bool agent_sorted_mode = false;  // spans compacted from the site-rank sort (s_cs in the val column)
     void *h_agent = nullptr;
     size_t h_agent_bytes = 0;
+    void *h_hdr = nullptr;           // host ChangeV1 headers staged for the device header passes (pinned)
+    size_t h_hdr_bytes = 0;
+    corro::DevBuf d_hdr_stage;       // their device copy + the device known outcomes
     uint64_t agent_ncs = 0;       // changesets of the current call (d_agent_spans column length)
     uint64_t agent_nbatch_max = 0;  // input changes of the current call (bound on the applied batch)
     uint64_t *h_misc = nullptr;   // pinned, 16 words

@@ -349,3 +349,11 @@ def test_device_headers_empty_and_zero_calls():
     assert eng.count() == 0
     assert bk.last(bytes(ids[1])) == 3 and bk.needed(bytes(ids[1])) == []
     assert list(eng.db_versions())[int(ords[1])] == 3
+
+
+@pytest.mark.parametrize("seed,clean", [(21, ()), (22, (0, 1, 2, 3, 4)), (23, (1, 2))])
+def test_host_headers_staged_to_device_match_restatement(seed, clean, monkeypatch):
+    """CORRO_MEM_DEVICE with host headers staged through the device header passes (the path large
+    calls take; forced here): same outcomes, flags, state and bookkeeping as the restatement"""
+    monkeypatch.setenv("CORRO_AGENT_STAGE_HEADERS", "1")
+    _check_against_oracle(seed, device=True, clean=clean)
