@@ -45,6 +45,9 @@ constexpr int FAST_R = CAP_FAST / FAST_T;              // records per thread
 static_assert(FAST_R * FAST_T == CAP_FAST, "FAST_T must divide CAP_FAST");
 constexpr int FAST_WAVES_EU = 2 * (FAST_T / 64) / 4;  // two workgroups per CU (LDS)
 constexpr int FAST_SLOTS = 4096;                       // cell table (distinct cells <= records)
+#ifndef IMPACT_LISTS
+#define IMPACT_LISTS 1  // packed impact body: per-cell member lists (1) or a counting sort by cell (0)
+#endif
 constexpr int CAP_GEN = 2048;                          // records, general body in LDS
 constexpr int GEN_SLOTS = 4096;
 constexpr uint32_t LONG_ROW = 128;                     // rows this long leave the LDS body
@@ -2209,6 +2212,53 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
         }
     }
     __syncthreads();
+#if IMPACT_LISTS
+    // 2. each cell's members as a list: its claimant heads it, the other members chain in (one LDS
+    // exchange each); keys and positions stay at the members' record indices (no counting sort)
+    uint32_t *s_p = reinterpret_cast<uint32_t *>(s_c), *s_nx = s_p + CAP_FAST;
+    for (uint32_t i = tid; i < CAP_FAST; i += FAST_T) s_own[i] = 0;
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++)
+        if (alive[k]) {
+            const uint32_t i = k * FAST_T + tid;
+            s_a[i] = k1[k];
+            s_b[i] = k2[k];
+            s_p[i] = pos[k];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        const uint32_t i = k * FAST_T + tid;
+        if (alive[k] && cell[k] != i) s_nx[i] = atomicExch(&s_own[cell[k]], i + 1);
+    }
+    __syncthreads();
+    // 4. one walk over the cell's members per change: impact (strict prefix maximum in application
+    // order, above the prior clock) and winner (maximum, earliest among equals, above the prior)
+#pragma unroll
+    for (int k = 0; k < FAST_R; k++) {
+        if (!alive[k]) continue;
+        bool imp = (flags >> (2 * k)) & 1u, win = imp;
+        const uint32_t i = k * FAST_T + tid;
+        uint32_t m = cell[k], nxt = s_own[cell[k]];
+        while (true) {
+            if (m != i) {
+                const uint64_t j1 = s_a[m];
+                const uint32_t j2 = s_b[m];
+                const int c = j1 != k1[k] ? (j1 > k1[k] ? 1 : -1) : (j2 != k2[k] ? (j2 > k2[k] ? 1 : -1) : 0);
+                const bool earlier = s_p[m] < pos[k];
+                if (earlier && c >= 0) imp = false;             // an earlier change already holds >= key
+                if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
+            }
+            if (nxt == 0) break;
+            m = nxt - 1;
+            nxt = s_nx[m];
+        }
+#if !(CORRO_DIAG & 1024)  // (1024: diagnostics only -- no flag stores, results not valid)
+        if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
+#endif
+        alive[k] = win;
+    }
+#else
     // 2. member counts per cell, exclusive scan -> offsets
     for (uint32_t i = tid; i < CAP_FAST; i += FAST_T) s_own[i] = 0;
     __syncthreads();
@@ -2274,6 +2324,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
 #endif
         alive[k] = win;
     }
+#endif
     if (!used0) {
         // 4b (empty region). the heap allocation issued before the walk: room, or defer (nothing of
         // the bucket's state written yet; its impact flags depend on the batch only)
