@@ -360,6 +360,27 @@ def test_config2_full_size_vs_sharded_oracle():
     e.close()
 
 
+@pytest.mark.parametrize("cap,chunk", [(64, None), (1 << 12, None), (1 << 12, "65536")])
+def test_overflow_fold_mixed_buckets_vs_oracle(monkeypatch, cap, chunk):
+    """The device-wide overflow fold against the oracle: every bucket oversized (cap 64), a few
+    Zipf-hot buckets among fast ones (cap 4096), chunked applies; malformed rows, mixed value
+    classes, impacts, a prior state."""
+    if chunk:
+        monkeypatch.setenv("CORRO_HIP_CHUNK", chunk)
+    seed = 91 + cap % 7 + (3 if chunk else 0)
+    sites = synth.site_ids(8, seed)
+    e = engine(synth.adversarial_schema(3), cap=cap, sites=sites)
+    f = O.Fold(sites)
+    for k in range(3):
+        b = synth.adversarial_batch(150000, 8, 3, 4000, seed * 10 + k, zipf=1.1, malformed=k == 1, max_cl=12)
+        if k == 2:
+            e.apply(b)
+            f.apply(b)
+        else:
+            assert np.array_equal(e.apply(b, impact=True), f.apply(b)), f"impacts differ in batch {k}"
+        compare(e, f, with_ts=True)
+
+
 @pytest.mark.parametrize("impact", [False, True])
 def test_chunked_apply_equals_one_apply(monkeypatch, impact):
     """A batch larger than the merge's chunk is applied as consecutive chunks in application order:
