@@ -85,6 +85,34 @@ template <class V> struct VerHolesT {
     }
 };
 
+// The common entry -- a few need ranges of theirs, no partial of theirs -- keeps its holes in
+// registers: the sweep tests every hole at every step, and from LDS that is a chain of dependent
+// reads per step; from registers the tests are a few predicated compares.
+#ifndef NEED_RH
+#define NEED_RH 3
+#endif
+struct RegHoles {
+    uint64_t hs[NEED_RH > 0 ? NEED_RH : 1], he[NEED_RH > 0 ? NEED_RH : 1];
+    uint32_t n;
+    __device__ inline bool covering(uint64_t x, uint64_t &end) const {
+        bool hit = false;
+#pragma unroll
+        for (int k = 0; k < NEED_RH; k++)
+            if ((uint32_t)k < n && hs[k] <= x && x <= he[k] && (!hit || he[k] > end)) {
+                end = he[k];
+                hit = true;
+            }
+        return hit;
+    }
+    __device__ inline uint64_t next_start(uint64_t x) const {
+        uint64_t m = ~0ULL;
+#pragma unroll
+        for (int k = 0; k < NEED_RH; k++)
+            if ((uint32_t)k < n && hs[k] > x && hs[k] < m) m = hs[k];
+        return m;
+    }
+};
+
 template <class V> struct SeqHolesT {
     V hs, he;
     uint64_t h0, h1;
@@ -224,11 +252,10 @@ template <class VK, class VU> struct NeedsEmit {
     }
 };
 
-template <bool FILL, class V, class E>
-__device__ inline void walk_entry(const EntryHdr &h, const InViews<V> &iv, const E &em, uint64_t nbase,
-                                  uint64_t sbase, uint64_t &nn_out, uint64_t &ns_out) {
+template <bool FILL, class V, class E, class H>
+__device__ inline void walk_entry_h(const EntryHdr &h, const InViews<V> &iv, const H &vh, const E &em, uint64_t nbase,
+                                    uint64_t sbase, uint64_t &nn_out, uint64_t &ns_out) {
     const uint64_t head = h.head;
-    VerHolesT<V> vh{iv.tns, iv.tne, h.tne0, h.tne1, iv.tpv, h.tpe0, h.tpe1};
     uint64_t nn = 0, ns = 0;
     auto full = [&](uint64_t s, uint64_t t) {
         if (FILL) em.full(nbase + nn, s, t, sbase + ns);
@@ -302,6 +329,25 @@ __device__ inline void walk_entry(const EntryHdr &h, const InViews<V> &iv, const
     else if (head > (uint64_t)h.ours) full((uint64_t)h.ours + 1, head);
     nn_out = nn;
     ns_out = ns;
+}
+
+template <bool FILL, class V, class E>
+__device__ inline void walk_entry(const EntryHdr &h, const InViews<V> &iv, const E &em, uint64_t nbase,
+                                  uint64_t sbase, uint64_t &nn_out, uint64_t &ns_out) {
+    if (NEED_RH > 0 && h.tpe1 == h.tpe0 && h.tne1 - h.tne0 <= (uint64_t)NEED_RH) {
+        RegHoles rh;
+        rh.n = (uint32_t)(h.tne1 - h.tne0);
+#pragma unroll
+        for (int k = 0; k < (NEED_RH > 0 ? NEED_RH : 1); k++) {
+            const bool in = (uint32_t)k < rh.n;
+            rh.hs[k] = in ? iv.tns[h.tne0 + k] : 0;
+            rh.he[k] = in ? iv.tne[h.tne0 + k] : 0;
+        }
+        walk_entry_h<FILL>(h, iv, rh, em, nbase, sbase, nn_out, ns_out);
+        return;
+    }
+    const VerHolesT<V> vh{iv.tns, iv.tne, h.tne0, h.tne1, iv.tpv, h.tpe0, h.tpe1};
+    walk_entry_h<FILL>(h, iv, vh, em, nbase, sbase, nn_out, ns_out);
 }
 
 // LDS of one need workgroup: the staged inputs ...
@@ -658,6 +704,9 @@ __device__ inline WgSegs stage_inputs_b(const SyncDev &in, const WgBound &b0, co
     g.ops_lo = b0.ops; g.ops_hi = b1.ops;
     g.lds = g.tn_hi - g.tn_lo <= NEEDS_CAP_R && g.on_hi - g.on_lo <= NEEDS_CAP_R && g.tp_hi - g.tp_lo <= NEEDS_CAP_P &&
             g.op_hi - g.op_lo <= NEEDS_CAP_P && g.tps_hi - g.tps_lo <= NEEDS_CAP_S && g.ops_hi - g.ops_lo <= NEEDS_CAP_S;
+#ifdef NEED_NOSTAGE  // experiment: the walk reads global memory (holes in registers)
+    g.lds = false;
+#endif
     if (!g.lds) return g;  // uniform
     stage_ranges(in.tn_start, in.tn_end, g.tn_lo, g.tn_hi - g.tn_lo, L.tns, L.tne);
     stage_ranges(in.on_start, in.on_end, g.on_lo, g.on_hi - g.on_lo, L.ons, L.one);
