@@ -91,6 +91,9 @@ template <class V> struct VerHolesT {
 #ifndef NEED_RH
 #define NEED_RH 3
 #endif
+#ifndef NEED_RO  // > 0: an entry with at most NEED_RO need ranges of ours loads them all up front
+#define NEED_RO 0
+#endif
 struct RegHoles {
     uint64_t hs[NEED_RH > 0 ? NEED_RH : 1], he[NEED_RH > 0 ? NEED_RH : 1];
     uint32_t n;
@@ -261,8 +264,7 @@ __device__ inline void walk_entry_h(const EntryHdr &h, const InViews<V> &iv, con
         if (FILL) em.full(nbase + nn, s, t, sbase + ns);
         nn++;
     };
-    for (uint64_t k = h.one0; k < h.one1; k++) {
-        const uint64_t s = iv.ons[k], t = iv.one[k];
+    auto our_range = [&](uint64_t s, uint64_t t) {
         if (s > t) {
             // an inverted (empty) range, which no RangeInclusiveSet holds but a peer's message may:
             // rangemap's overlapping(s..=t) yields every stored range with end >= s and start <= t,
@@ -271,10 +273,25 @@ __device__ inline void walk_entry_h(const EntryHdr &h, const InViews<V> &iv, con
                 uint64_t dummy;
                 if (!vh.covering(t, dummy) && vh.next_start(t) > s) full(s, t);
             }
-            continue;
+            return;
         }
         sweep(vh, s, t, 1, head, full);
-    }
+    };
+#if NEED_RO > 0
+    if (h.one1 - h.one0 <= (uint64_t)NEED_RO) {  // all loads issued before the first sweep
+        uint64_t os[NEED_RO], oe[NEED_RO];
+        const uint32_t no = (uint32_t)(h.one1 - h.one0);
+#pragma unroll
+        for (int k = 0; k < NEED_RO; k++) {
+            os[k] = (uint32_t)k < no ? iv.ons[h.one0 + k] : 0;
+            oe[k] = (uint32_t)k < no ? iv.one[h.one0 + k] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < NEED_RO; k++)
+            if ((uint32_t)k < no) our_range(os[k], oe[k]);
+    } else
+#endif
+        for (uint64_t k = h.one0; k < h.one1; k++) our_range(iv.ons[k], iv.one[k]);
 
     for (uint64_t k = h.ope0; k < h.ope1; k++) {
         const uint64_t v = iv.opv[k];
