@@ -882,7 +882,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     ctx->state_total += ctx->h_misc[MISC_LIVE];  // (a signed delta in two's complement)
     ctx->state_rows = ctx->h_misc[MISC_ROWS];
 #if CORRO_DIAG & 256
-    fprintf(stderr, "DIAG impact phases (us per bucket): loads %.3f claims %.3f rows %.3f prior %.3f counts %.3f ranks %.3f walk %.3f winners %.3f\n",
+    fprintf(stderr, "DIAG impact phases (us per bucket; packed body: loads claims rows counts place walk region winners): %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f\n",
             ctx->h_misc[MISC_DIAG] / 100.0 / B, ctx->h_misc[MISC_DIAG + 1] / 100.0 / B,
             ctx->h_misc[MISC_DIAG + 2] / 100.0 / B, ctx->h_misc[MISC_DIAG + 3] / 100.0 / B,
             ctx->h_misc[MISC_DIAG + 4] / 100.0 / B, ctx->h_misc[MISC_DIAG + 5] / 100.0 / B,

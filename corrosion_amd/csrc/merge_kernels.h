@@ -2130,6 +2130,9 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
     uint32_t flags = 0;   // bit 2k: beats the prior clock; bit 2k+1: the cell had no prior clock
     bool alive[FAST_R];
     uint4 q[FAST_R][4];
+#if CORRO_DIAG & 256
+    unsigned long long diag_t2 = wall_clock64();
+#endif
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) load_rec_wave_raw(v.fresh, k * FAST_T + (tid & ~63u), n, q[k]);
     const uint32_t used0 = a.rs.used[b];  // (issued with the record loads)
@@ -2168,6 +2171,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
     for (int k = 0; k < FAST_R; k++)
         if (site[k] >= a.nsites) k2[k] &= 0xFFFF0000u;
     __syncthreads();
+    DIAG_MARK2(0);
     // 1. rows, then cells
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
@@ -2181,6 +2185,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
     for (int k = 0; k < FAST_R; k++)
         if (alive[k]) cell[k] = cell_claim(s_own, k * FAST_T + tid, row[k], tc[k]);
     __syncthreads();
+    DIAG_MARK2(1);
     unsigned long long hraw = 0;
     if (!used0) {
         // 1b (empty region). every row new: heap offsets counted now (s_own: heap words by owner),
@@ -2212,6 +2217,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
         }
     }
     __syncthreads();
+    DIAG_MARK2(2);
 #if IMPACT_LISTS
     // 2. each cell's members as a list: its claimant heads it, the other members chain in (one LDS
     // exchange each); keys and positions stay at the members' record indices (no counting sort)
@@ -2288,6 +2294,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
             }
     }
     __syncthreads();
+    DIAG_MARK2(3);
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) md[k] = alive[k] ? s_own[cell[k]] : 0u;
     __syncthreads();
@@ -2303,6 +2310,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
             md[k] |= d << 16;
         }
     __syncthreads();
+    DIAG_MARK2(4);
     // 4. one walk over the cell's members per change: impact (strict prefix maximum in application
     // order, above the prior clock) and winner (maximum, earliest among equals, above the prior)
 #pragma unroll
@@ -2325,6 +2333,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
         alive[k] = win;
     }
 #endif
+    DIAG_MARK2(5);
     if (!used0) {
         // 4b (empty region). the heap allocation issued before the walk: room, or defer (nothing of
         // the bucket's state written yet; its impact flags depend on the batch only)
@@ -2366,6 +2375,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
         }
     }
     __syncthreads();
+    DIAG_MARK2(6);
     // 5. winners: the rest of the clock row from the staged record, into its heap slot; presence bits
     uint32_t nlive = 0;
     constexpr int WH = (FAST_R + 1) / 2;  // two halves: the reloads of one half in flight at once
@@ -2412,6 +2422,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
     nlive = wave_sum_u32(nlive);
     if ((tid & 63) == 0 && nlive) atomicAdd(&s_live, (unsigned long long)nlive);
     __syncthreads();
+    DIAG_MARK2(7);
 #pragma unroll
     for (int k = 0; k < FAST_R; k++) {
         const uint32_t i = k * FAST_T + tid;
