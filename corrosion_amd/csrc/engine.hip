@@ -156,6 +156,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         uint32_t **rows[] = {&d.rowner, &d.rb, &d.rheap, &d.rprior, &d.rpoff};
         for (uint32_t **p : rows) *p = (uint32_t *)take(R * 4);
         d.rbits = (uint64_t *)take(R * 16);
+        d.rmx = (uint32_t *)take(R * 40 + 64);
+        d.cbk = (uint32_t *)take((Kb / 64 + 2) * 4);  // row summaries, laid out once the row count is known
         if (pass == 0) {
             size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
             TRY(ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, d.K, 64, s));
@@ -188,6 +190,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         CORRO_HIP_TRY(hipGetLastError());
         return CORRO_OK;
     };
+    hipLaunchKernelGGL(k_ovf_chunkmap, grid_for((Kb + 63) / 64), blk, 0, s, d);
     hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
     TRY(launched());
     // dense row ids: the row count sizes the sort's key
@@ -197,9 +200,21 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     d.nrows = nrows;
     d.rshift = pbits;
+    // row reduction off with impacts (every epoch's changes get a flag) or when asked (A/B runs)
+    static const bool no_reduce = std::getenv("CORRO_OVF_REDUCE") && std::atoi(std::getenv("CORRO_OVF_REDUCE")) == 0;
+    d.reduce = (!a.impact && !no_reduce) ? 1u : 0u;
+    {
+        uint8_t *blk = (uint8_t *)d.rmx;
+        d.rcall = (uint64_t *)blk;
+        d.rcfin = (uint64_t *)(blk + 16ULL * nrows);
+        d.rmx = (uint32_t *)(blk + 32ULL * nrows);
+        d.rbad0 = (uint32_t *)(blk + 36ULL * nrows);
+        d.nkeep = (uint32_t *)(blk + 40ULL * nrows);
+        if (d.reduce) CORRO_HIP_TRY(hipMemsetAsync(blk, 0, 40ULL * nrows + 4, s));
+    }
     // every row looked up in its region; prior records counted, new rows counted per bucket (and
     // every batch record's sort key)
-    hipLaunchKernelGGL(k_ovf_lookup, gridb, blk, 0, s, a, d);
+    hipLaunchKernelGGL(k_ovf_lookup, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)), dim3(RS_T), 0, s, a, d);
     TRY(launched());
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
     uint32_t P = 0;
@@ -224,7 +239,6 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     if (top + need_heap > ctx->heap_cap) TRY(grow_heap(ctx, top + need_heap));
     a.rs = row_store(ctx);
     d.K = (uint32_t)(Kb + P);
-    const dim3 grid = grid_for(d.K);
     uint32_t rbits = 1;
     while ((1ULL << rbits) < nrows) rbits++;
     const uint32_t key_bits = rbits + pbits;
@@ -236,7 +250,22 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
                 (unsigned long long)novf, (unsigned long long)Kb, P, nrows, key_bits, rbits, ckey_bits);
     hipLaunchKernelGGL(k_ovf_pload, grid_for(nrows), blk, 0, s, a, d);
     TRY(launched());
-    TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.key_s, d.val, d.val_s, d.K, key_bits, s));
+    if (d.reduce) {
+        // rows reduced to their last epoch's records (k_ovf_lookup's comment); the rest sort as before
+        hipLaunchKernelGGL(k_ovf_rfin, dim3((d.K + RS_CHUNK - 1) / RS_CHUNK), dim3(RS_T), 0, s, d);
+        hipLaunchKernelGGL(k_ovf_keep, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK), dim3(KEEP_T), 0, s, d);
+        TRY(launched());
+        uint32_t kept = 0;
+        CORRO_HIP_TRY(hipMemcpyAsync(&kept, d.nkeep, 4, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        if (kept == 0 || kept > d.K) return fail(CORRO_E_DEVICE, "internal: overflow row reduction kept no records");
+        if (dbg) fprintf(stderr, "[corro ovf] row reduction keeps %u of %u records\n", kept, d.K);
+        d.K = kept;
+        TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.key_s, d.cval, d.val_s, d.K, key_bits, s));
+    } else {
+        TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.key_s, d.val, d.val_s, d.K, key_bits, s));
+    }
+    const dim3 grid = grid_for(d.K);
     hipLaunchKernelGGL(k_ovf_gather, grid, blk, 0, s, d);
     TRY(launched());
     TRY(ovf_scans(d_temp, &temp, d, 0, s));

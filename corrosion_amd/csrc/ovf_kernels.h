@@ -29,6 +29,8 @@
 //   scan of owner flags               dense row ids
 //   k_ovf_lookup, scan, k_ovf_pload   each row looked up in its region (new rows counted per bucket
 //                                     for the host's capacity check), prior records appended
+//   [no impacts] k_ovf_rfin, k_ovf_keep  row reduction: a row whose last epoch covers every cid it
+//                                     holds keeps only the records at its largest cl (below)
 //   (k_ovf_lookup also writes the batch records' sort keys: dense row << rshift | compact position,
 //   prior slots [0, pm), then the batch in application order: log2(rows) + log2(pm + batch) bits)
 //   radix sort by (row, position)                                       [prims.hip, rocPRIM]
@@ -98,6 +100,13 @@ struct OvfDev {
     uint32_t *slots;
     uint32_t *bnew, *bnrec;      // [G] new rows / their heap records per bucket
     const uint8_t *arena;        // long value bytes (MergeArgs::arena)
+    // row reduction (no impacts): per row the largest cl, whether any record is outside App. A.3,
+    // the cids of all its column records and of its column records at that cl with col_version > 0
+    uint32_t reduce;             // 1: rows are reduced to their last epoch's records before the sort
+    uint32_t *rmx, *rbad0;
+    uint64_t *rcall, *rcfin;     // [2 * nrows] cid bits
+    uint32_t *nkeep;             // [1] records kept
+    uint32_t *cbk;               // [Kb / 64 + 1] bucket of batch record 64 c (k_ovf_chunkmap)
 };
 
 // a record's 64-B source: the staged batch change or the prior heap record
@@ -161,10 +170,17 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b, const uint8_t *
 // 64-B record and the record is hashed into its bucket's row table (open addressing per bucket, a
 // slot read before it is claimed); an occupied slot's row key is compared with the claimant's staged
 // record (read-only in this kernel, so no ordering against the claimant's own field writes).
+// the bucket of every 64th batch record: a record's bucket is then a step or two from its chunk's
+// (the binary search over koff is one dependent chain of ~15 loads per lookup)
+static __global__ void k_ovf_chunkmap(OvfDev d) {
+    OVF_LOOP(c, (d.Kb + 63) / 64) d.cbk[c] = ovf_bucket_of(d, c * 64);
+}
+
 static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
     const uint32_t lane = threadIdx.x & 63;
     OVF_LOOP(r, d.Kb) {
-        const uint32_t b = ovf_bucket_of(d, r);
+        uint32_t b = d.cbk[r >> 6];
+        while (d.koff[b + 1] <= r) b++;
         const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
         const uint32_t sbase = a.stage_off[a.ovf_list[b]];
         const uint32_t si = sbase + (r - kb);
@@ -225,16 +241,163 @@ static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
 // prior records counted, new rows counted per bucket (the host checks the region and heap have
 // room before anything is written). The removed prior records leave the live count here; the walk
 // adds what it writes back.
-static __global__ void k_ovf_lookup(MergeArgs a, OvfDev d) {
-    OVF_LOOP(r, d.Kb) {
+// Row reduction (no impacts). With Mx the row's largest cl (prior records included), the records at
+// cl == Mx form the row's last epoch: the first of them is its record, every later one a candidate
+// or a no-op, and nothing after it starts another epoch. The walk's result depends on earlier epochs
+// only through the cells they carry: none when Mx is even (a delete), and when Mx is odd only cells
+// of cids without a change of their own in the last epoch -- one with col_version > 0 always beats
+// a carried (zeroed) cell. So a row whose records are all inside App. A.3, with Mx even, or whose
+// cids all have such a change at Mx, folds to the same clock rows from its Mx records alone (the
+// row's sentinel is the epoch record's either way: App. A.1 rules 2-4). The other rows keep every
+// record. Without this, a Zipf-hot row's history (88 % of its records in config 5) goes through
+// the sort, scans and walk only to be dropped by its last delete or overwritten by its last epoch.
+__device__ inline bool ovf_rec_bad(const MergeArgs &a, uint32_t cid, uint32_t cl, int64_t cv, uint32_t pos) {
+    if (((cid == 0 || (cl & 1u) == 0) && cv != (int64_t)cl) || (!(pos & BATCH_POS) && cid != 0 && !(cl & 1u)))
+        return true;
+    return a.raw.conv && (pos & BATCH_POS) && a.raw.conv[batch_src(a, pos & 0x7FFFFFFFu)];
+}
+
+// device-coherent read (past the CU's L1, which does not see other CUs' atomics): a summary word is
+// read before it is updated, and a hot row's lanes mostly find it set
+template <typename T>
+__device__ inline T ovf_ld_dev(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline void ovf_rsum_put(const OvfDev &d, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad) {
+    if (mx > ovf_ld_dev(&d.rmx[row])) atomicMax(&d.rmx[row], mx);
+    unsigned long long *w = (unsigned long long *)&d.rcall[2 * row];
+    if (b0 & ~ovf_ld_dev(&d.rcall[2 * row])) atomicOr(w, (unsigned long long)b0);
+    if (b1 & ~ovf_ld_dev(&d.rcall[2 * row + 1])) atomicOr(w + 1, (unsigned long long)b1);
+    if (bad && !ovf_ld_dev(&d.rbad0[row])) d.rbad0[row] = 1;
+}
+
+// Row summaries aggregated per workgroup first: a workgroup takes RS_CHUNK consecutive records
+// (bucket-major, so a few buckets' rows, a Zipf-hot row's records many times over), folds them into
+// an LDS table keyed by row, then writes each of its rows to the global words once. A record whose
+// row finds no LDS slot updates the global words itself.
+constexpr uint32_t RS_T = 256, RS_E = 8, RS_CHUNK = RS_T * RS_E, RS_HT = 1024;
+struct RsLds {
+    uint32_t key[RS_HT], mx[RS_HT], bad[RS_HT];  // key: row + 1 (0: free)
+    unsigned long long b0[RS_HT], b1[RS_HT];
+};
+
+__device__ inline void rs_lds_clear(RsLds &L) {
+    for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x) {
+        L.key[i] = 0;
+        L.mx[i] = 0;
+        L.bad[i] = 0;
+        L.b0[i] = 0;
+        L.b1[i] = 0;
+    }
+}
+
+__device__ inline bool rs_lds_add(RsLds &L, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad) {
+    const uint32_t h = (row * 2654435761u) >> 22;  // (RS_HT = 2^10)
+    for (uint32_t k = 0; k < 16; k++) {
+        const uint32_t sl = (h + k) & (RS_HT - 1);
+        const uint32_t o = atomicCAS(&L.key[sl], 0u, row + 1);
+        if (o != 0 && o != row + 1) continue;
+        if (mx) atomicMax(&L.mx[sl], mx);
+        if (b0) atomicOr(&L.b0[sl], (unsigned long long)b0);
+        if (b1) atomicOr(&L.b1[sl], (unsigned long long)b1);
+        if (bad) L.bad[sl] = 1;
+        return true;
+    }
+    return false;
+}
+
+__device__ inline uint64_t wave_or64(uint64_t x) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) x |= __shfl_xor(x, o);
+    return x;
+}
+
+__device__ inline uint32_t wave_max32(uint32_t x) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) x = max(x, (uint32_t)__shfl_xor(x, o));
+    return x;
+}
+
+template <bool FIN>
+__device__ inline void rs_put(const OvfDev &d, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad);
+
+// One summary term per `todo` lane (called by every lane of the wave): lanes sharing the first
+// active lane's row -- a Zipf-hot row fills whole waves -- are reduced across the wave and added by
+// that lane (at most two rounds), the rest add their own term; LDS first, the global words when the
+// table has no slot for the row.
+template <bool FIN>
+__device__ inline void rs_wave_add(RsLds &L, const OvfDev &d, bool todo, uint32_t row, uint32_t mx, uint64_t b0,
+                                   uint64_t b1, bool bad) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (int round = 0; round < 2; round++) {
+        const uint64_t act = __ballot(todo);
+        if (!act) break;
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint32_t lrow = __shfl(row, leader);
+        const bool mine = todo && row == lrow;
+        if (__popcll(__ballot(mine)) < 8) break;  // (wave-uniform) not a hot row
+        const uint32_t m = wave_max32(mine ? mx : 0u);
+        const uint64_t o0 = wave_or64(mine ? b0 : 0ULL), o1 = wave_or64(mine ? b1 : 0ULL);
+        const bool bd = __ballot(mine && bad) != 0;
+        if ((int)lane == leader && !rs_lds_add(L, lrow, m, o0, o1, bd)) rs_put<FIN>(d, lrow, m, o0, o1, bd);
+        if (mine) todo = false;
+    }
+    if (todo && !rs_lds_add(L, row, mx, b0, b1, bad)) rs_put<FIN>(d, row, mx, b0, b1, bad);
+}
+
+// FIN: the table holds the cid bits at the row's largest cl (rcfin), else the full summary
+template <bool FIN>
+__device__ inline void rs_put(const OvfDev &d, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad) {
+    if (!FIN) {
+        ovf_rsum_put(d, row, mx, b0, b1, bad);
+        return;
+    }
+    unsigned long long *w = (unsigned long long *)&d.rcfin[2 * row];
+    if (b0 & ~ovf_ld_dev(&d.rcfin[2 * row])) atomicOr(w, (unsigned long long)b0);
+    if (b1 & ~ovf_ld_dev(&d.rcfin[2 * row + 1])) atomicOr(w + 1, (unsigned long long)b1);
+}
+
+template <bool FIN>
+__device__ inline void rs_lds_flush(const RsLds &L, const OvfDev &d) {
+    for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x)
+        if (L.key[i]) rs_put<FIN>(d, L.key[i] - 1, L.mx[i], L.b0[i], L.b1[i], L.bad[i] != 0);
+}
+
+static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev d) {
+    __shared__ RsLds L;
+    if (d.reduce) {
+        rs_lds_clear(L);
+        __syncthreads();
+    }
+    const uint32_t c0 = blockIdx.x * RS_CHUNK;
+    for (uint32_t j = 0; j < RS_E; j++) {  // (wave-uniform: the summary reduces across the wave)
+        const uint32_t r = c0 + j * RS_T + threadIdx.x;
+        const bool valid = r < d.Kb;
         // every record: its sort key (k_ovf_rowkey's, fused here: dense rows are known by now)
-        {
+        uint32_t row = 0, pos = 0;
+        if (valid) {
             const uint32_t kb = d.koff[d.pb[r]];
-            const uint64_t row = d.epc[kb + d.rowid[r]] - 1u;
-            d.key[r] = (row << d.rshift) | ((uint64_t)d.pm + (d.pos[r] & 0x7FFFFFFFu));
+            row = d.epc[kb + d.rowid[r]] - 1u;
+            pos = d.pos[r];
+            d.key[r] = ((uint64_t)row << d.rshift) | ((uint64_t)d.pm + (pos & 0x7FFFFFFFu));
         }
-        if (!d.recf[r]) continue;
-        const uint32_t row = d.epc[r] - 1u;
+        if (d.reduce) {
+            uint32_t cl = 0;
+            uint64_t b0 = 0, b1 = 0;
+            bool bad = false;
+            if (valid) {
+                d.rowid[r] = row;  // (own slot: every other lane reads epc, not rowid)
+                const uint32_t cid = d.tc[r] & 0xFFFFu;
+                cl = d.cl[r];
+                const uint64_t bit = cid != 0 ? 1ULL << (cid & 63) : 0ULL;
+                b0 = cid < 64 ? bit : 0ULL;
+                b1 = cid >= 64 ? bit : 0ULL;
+                bad = ovf_rec_bad(a, cid, cl, d.cv[r], pos);
+            }
+            rs_wave_add<false>(L, d, valid, row, cl, b0, b1, bad);
+        }
+        if (!valid || !d.recf[r]) continue;  // (an owner's row: epc[r] - 1, as computed above)
         const uint32_t b = d.pb[r], t = d.tc[r] >> 16;
         d.rowner[row] = r;
         d.rb[row] = b;
@@ -254,6 +417,10 @@ static __global__ void k_ovf_lookup(MergeArgs a, OvfDev d) {
             d.rbits[2 * row + 1] = re.bits[1];
             atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)(-(long long)pc));
         }
+    }
+    if (d.reduce) {
+        __syncthreads();
+        rs_lds_flush<false>(L, d);
     }
 }
 
@@ -278,8 +445,82 @@ static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
                 d.src[r] = hb + c;
                 d.key[r] = ((uint64_t)row << d.rshift) | c;
                 d.val[r] = r;
+                if (d.reduce) {
+                    d.rowid[r] = row;
+                    const uint32_t cid = pr.tcid & 0xFFFFu;
+                    const uint64_t bit = cid != 0 ? 1ULL << (cid & 63) : 0ULL;
+                    ovf_rsum_put(d, row, pr.cl, cid < 64 ? bit : 0ULL, cid >= 64 ? bit : 0ULL,
+                                 ovf_rec_bad(a, cid, pr.cl, pr.cv, c));
+                }
                 r++;
             }
+    }
+}
+
+// the cids with a change of col_version > 0 at the row's largest cl
+static __global__ void __launch_bounds__(RS_T) k_ovf_rfin(OvfDev d) {
+    __shared__ RsLds L;  // (rs_lds_add's table: key and cid bits used)
+    rs_lds_clear(L);
+    __syncthreads();
+    const uint32_t c0 = blockIdx.x * RS_CHUNK;
+    for (uint32_t j = 0; j < RS_E; j++) {  // (wave-uniform)
+        const uint32_t r = c0 + j * RS_T + threadIdx.x;
+        uint32_t cid = 0, row = 0;
+        bool fin = false;
+        if (r < d.K) {
+            cid = d.tc[r] & 0xFFFFu;
+            row = d.rowid[r];
+            fin = cid != 0 && d.cv[r] > 0 && d.cl[r] == d.rmx[row];
+        }
+        const uint64_t bit = 1ULL << (cid & 63), b0 = cid < 64 ? bit : 0ULL, b1 = cid >= 64 ? bit : 0ULL;
+        rs_wave_add<true>(L, d, fin, row, 0u, b0, b1, false);
+    }
+    __syncthreads();
+    rs_lds_flush<true>(L, d);
+}
+
+// The kept records' (key, record) pairs compacted into (ckey, cval) for the sort: each workgroup
+// takes a contiguous chunk, ranks its kept records by wave ballots and reserves their slots with ONE
+// atomic (the order does not matter: the keys are unique and the sort orders them).
+constexpr uint32_t KEEP_T = 256, KEEP_E = 32, KEEP_CHUNK = KEEP_T * KEEP_E;
+static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(OvfDev d) {
+    __shared__ uint32_t s_cnt[KEEP_T / 64], s_base;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = d.K;
+    const uint32_t c0 = blockIdx.x * KEEP_CHUNK;
+    uint32_t mine = 0, cnt = 0;  // lane's kept bits per step; the wave's kept count
+#pragma unroll 4
+    for (uint32_t j = 0; j < KEEP_E; j++) {
+        const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
+        bool keep = false;
+        if (r < n) {
+            const uint32_t row = d.rowid[r], mx = d.rmx[row], cl = d.cl[r];
+            const bool red = !d.rbad0[row] && (!(mx & 1u) || (d.rcfin[2 * row] == d.rcall[2 * row] &&
+                                                               d.rcfin[2 * row + 1] == d.rcall[2 * row + 1]));
+            keep = !red || cl == mx;
+        }
+        mine |= keep ? 1u << j : 0u;
+        cnt += (uint32_t)__popcll(__ballot(keep));
+    }
+    if (lane == 0) s_cnt[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t v = 0; v < KEEP_T / 64; v++) t += s_cnt[v];
+        s_base = t ? atomicAdd(d.nkeep, t) : 0u;
+    }
+    __syncthreads();
+    uint32_t o = s_base;
+    for (uint32_t v = 0; v < w; v++) o += s_cnt[v];
+    for (uint32_t j = 0; j < KEEP_E; j++) {
+        const bool keep = (mine >> j) & 1u;
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+            const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
+            const uint32_t q = o + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
+            d.ckey[q] = d.key[r];
+            d.cval[q] = d.val[r];
+        }
+        o += (uint32_t)__popcll(m);
     }
 }
 
@@ -439,11 +680,12 @@ struct WalkCells<false> {
 // The row's heap slot: its prior one, or a fresh one for a new row (the host made room), and its
 // region entry: looked up for a row that existed before the apply, inserted for a new one
 // (k_ovf_lookup told them apart; rowstore.h says why the two never interfere). Returns the entry.
+// (rprior, the rows' prior counts until k_ovf_pload, holds a new row's heap slot in the walk.)
 __device__ inline uint32_t ovf_row_slot(const MergeArgs &a, const OvfDev &d, uint32_t row, uint32_t &hb) {
     const uint32_t bb = a.ovf_list[d.rb[row]], own = d.rowner[row], t = d.tc[own] >> 16;
     hb = d.rheap[row];
     if (hb != ROW_NONE) return rs_lookup(a.rs, bb, d.pk[own], t);
-    hb = (uint32_t)atomicAdd(a.rs.heap_top, (unsigned long long)a.rs.stride[t]);
+    hb = d.rprior[row];  // (k_ovf_walk allocated it, one heap request per wave)
     const uint64_t z[2] = {0, 0};
     return rs_insert(a.rs, bb, d.pk[own], t, hb, z);
 }
@@ -457,7 +699,6 @@ __device__ inline void ovf_publish(const MergeArgs &a, const OvfDev &d, uint32_t
         const uint32_t own = d.rowner[row];
         touch_append(a, d.pk[own], d.tc[own] >> 16);
     }
-    atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)cnt);
     if (general) a.rs.gen[a.ovf_list[d.rb[row]]] = 1;
 }
 
@@ -473,12 +714,13 @@ struct OvfEmit {
         bool gen;
         const uint32_t cnt = heap_write_row(a, v, g, s, ncell, hs, scv, ssrc, hb, bits, gen);
         ovf_publish(a, *d, row, e, bits, cnt, gen);
+        atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)cnt);
     }
 };
 
-// clock rows of one walked row (rf_emit on the carried cells) into its heap slot
+// clock rows of one walked row (rf_emit on the carried cells) into its heap slot; returns them
 template <bool REG>
-__device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t row, const WalkCells<REG> &cells_,
+__device__ inline uint32_t ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t row, const WalkCells<REG> &cells_,
                                 uint32_t ncell, uint32_t rpos) {
     const uint32_t xr = d.val_s[rpos];
     const uint32_t clr = d.cl[xr], cidr = d.tc[xr] & 0xFFFFu;
@@ -487,7 +729,7 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t ro
     const int64_t rowcl = hs ? scv : 1;
     const bool cells = (clr & 1u) != 0;
     const uint32_t cnt = (hs ? 1u : 0u) + (cells ? ncell : 0u);
-    if (cnt == 0) return;
+    if (cnt == 0) return 0;
     uint32_t hb;
     const uint32_t e = ovf_row_slot(a, d, row, hb);
     const OvfView v{&a, &d};
@@ -522,6 +764,7 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t ro
         }
     }
     ovf_publish(a, d, row, e, bits, cnt, general);
+    return cnt;
 }
 
 #ifndef OVF_WALK_WAVES
@@ -529,7 +772,27 @@ __device__ inline void ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t ro
 #endif
 template <bool REG>
 static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeArgs a, OvfDev d) {
-    OVF_LOOP(row, d.nrows) {  // one thread per row (dense ids), every lane busy
+    const uint32_t lane = threadIdx.x & 63, stride = gridDim.x * blockDim.x;
+    uint32_t live = 0;  // clock rows written (one atomic per wave at the end)
+    // one thread per row (dense ids), every lane busy; wave-uniform loop for the heap requests
+    for (uint32_t r0 = blockIdx.x * blockDim.x + threadIdx.x - lane; r0 < d.nrows; r0 += stride) {
+        const uint32_t row = r0 + lane;
+        {  // the wave's new rows take their heap records in one request (the host made room)
+            uint32_t need = 0;
+            if (row < d.nrows && d.rheap[row] == ROW_NONE) need = a.rs.stride[d.tc[d.rowner[row]] >> 16];
+            uint32_t incl = need;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t u = __shfl_up(incl, off);
+                if ((int)lane >= off) incl += u;
+            }
+            const uint32_t tot = __shfl(incl, 63);
+            unsigned long long base = 0;
+            if (lane == 63 && tot) base = atomicAdd(a.rs.heap_top, (unsigned long long)tot);
+            base = __shfl(base, 63);
+            if (need) d.rprior[row] = (uint32_t)base + incl - need;
+        }
+        if (row >= d.nrows) continue;
         const uint32_t j0 = d.rstart[row];
         if (d.rbad[row]) {  // outside App. A.3: the sequential fold over the row's sorted records
             GenArrays g{};
@@ -593,8 +856,11 @@ static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeAr
                 if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(a, d, fp, fz != 0), d.arena) > 0) set(cid, d.cval_s[wq], 0);
             }
         }
-        if (nrec) ovf_emit<REG>(a, d, row, cs, ncell, d.recs[j0 + nrec - 1]);
+        if (nrec) live += ovf_emit<REG>(a, d, row, cs, ncell, d.recs[j0 + nrec - 1]);
     }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) live += __shfl_xor(live, off);
+    if (lane == 0 && live) atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)live);
 }
 
 static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {

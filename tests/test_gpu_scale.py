@@ -85,7 +85,10 @@ def _dev(b):
 
 
 @pytest.mark.timeout(1200)
-def test_config5_64m_two_batch_fold_vs_sharded_oracle():
+@pytest.mark.parametrize("impact", [True, False], ids=["impacts", "no_impacts"])
+def test_config5_64m_two_batch_fold_vs_sharded_oracle(impact):
+    """With impacts every change keeps its place in the fold; without them the overflow fold reduces
+    hot rows to their last epoch's changes first (ovf_kernels.h) -- both against the same oracle."""
     import torch
     import corrosion_amd as ca
     n = 64_000_000
@@ -100,13 +103,15 @@ def test_config5_64m_two_batch_fold_vs_sharded_oracle():
         b = synth.adversarial_batch(n, 1000, 8, 1 << 20, seed + k)
         print(f"batch {k} generated at {time.time() - t0:.0f} s", flush=True)
         d = _dev(b)
-        imp = eng.apply(d, impact=True).cpu().numpy()
+        imp = eng.apply(d, impact=impact)
+        imp = imp.cpu().numpy() if impact else None
         print(f"batch {k} applied on the GPU at {time.time() - t0:.0f} s", flush=True)
         del d
         torch.cuda.empty_cache()
-        ref = fold.apply(b)
+        ref = fold.apply(b, impact=impact)
         print(f"batch {k} folded by the oracle at {time.time() - t0:.0f} s", flush=True)
-        assert np.array_equal(imp, ref), f"config 5 batch {k}: impact flags differ"
+        if impact:
+            assert np.array_equal(imp, ref), f"config 5 batch {k}: impact flags differ"
         del b, imp, ref
     m = eng.metrics()
     assert m["overflow_rounds"] >= 2          # the hot-row regime was exercised
