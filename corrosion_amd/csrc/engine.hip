@@ -156,8 +156,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         uint32_t **rows[] = {&d.rowner, &d.rb, &d.rheap, &d.rprior, &d.rpoff};
         for (uint32_t **p : rows) *p = (uint32_t *)take(R * 4);
         d.rbits = (uint64_t *)take(R * 16);
-        d.rmx = (uint32_t *)take(R * 40 + 64);
-        d.cbk = (uint32_t *)take((Kb / 64 + 2) * 4);  // row summaries, laid out once the row count is known
+        d.rw1 = (uint64_t *)take(R * 12 + 64);  // row summaries, laid out once the row count is known
+        d.cbk = (uint32_t *)take((Kb / 64 + 2) * 4);
         if (pass == 0) {
             size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
             TRY(ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, d.K, 64, s));
@@ -202,15 +202,13 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     d.rshift = pbits;
     // row reduction off with impacts (every epoch's changes get a flag) or when asked (A/B runs)
     static const bool no_reduce = std::getenv("CORRO_OVF_REDUCE") && std::atoi(std::getenv("CORRO_OVF_REDUCE")) == 0;
-    d.reduce = (!a.impact && !no_reduce) ? 1u : 0u;
+    // (the summary's cid bits cover cids < 32)
+    d.reduce = (!a.impact && !no_reduce && ctx->max_stride <= 32) ? 1u : 0u;
     {
-        uint8_t *blk = (uint8_t *)d.rmx;
-        d.rcall = (uint64_t *)blk;
-        d.rcfin = (uint64_t *)(blk + 16ULL * nrows);
-        d.rmx = (uint32_t *)(blk + 32ULL * nrows);
-        d.rbad0 = (uint32_t *)(blk + 36ULL * nrows);
-        d.nkeep = (uint32_t *)(blk + 40ULL * nrows);
-        if (d.reduce) CORRO_HIP_TRY(hipMemsetAsync(blk, 0, 40ULL * nrows + 4, s));
+        uint8_t *blk = (uint8_t *)d.rw1;
+        d.rw2 = (uint32_t *)(blk + 8ULL * nrows);
+        d.nkeep = (uint32_t *)(blk + 12ULL * nrows);
+        if (d.reduce) CORRO_HIP_TRY(hipMemsetAsync(blk, 0, 12ULL * nrows + 4, s));
     }
     // every row looked up in its region; prior records counted, new rows counted per bucket (and
     // every batch record's sort key)
@@ -252,7 +250,6 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     TRY(launched());
     if (d.reduce) {
         // rows reduced to their last epoch's records (k_ovf_lookup's comment); the rest sort as before
-        hipLaunchKernelGGL(k_ovf_rfin, dim3((d.K + RS_CHUNK - 1) / RS_CHUNK), dim3(RS_T), 0, s, d);
         hipLaunchKernelGGL(k_ovf_keep, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK), dim3(KEEP_T), 0, s, d);
         TRY(launched());
         uint32_t kept = 0;

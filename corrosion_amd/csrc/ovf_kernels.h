@@ -29,8 +29,9 @@
 //   scan of owner flags               dense row ids
 //   k_ovf_lookup, scan, k_ovf_pload   each row looked up in its region (new rows counted per bucket
 //                                     for the host's capacity check), prior records appended
-//   [no impacts] k_ovf_rfin, k_ovf_keep  row reduction: a row whose last epoch covers every cid it
-//                                     holds keeps only the records at its largest cl (below)
+//   [no impacts] (row summaries in k_ovf_lookup / k_ovf_pload), k_ovf_keep  row reduction: a row
+//                                     whose last epoch covers every cid it holds keeps only the
+//                                     records at its largest cl (below)
 //   (k_ovf_lookup also writes the batch records' sort keys: dense row << rshift | compact position,
 //   prior slots [0, pm), then the batch in application order: log2(rows) + log2(pm + batch) bits)
 //   radix sort by (row, position)                                       [prims.hip, rocPRIM]
@@ -103,8 +104,8 @@ struct OvfDev {
     // row reduction (no impacts): per row the largest cl, whether any record is outside App. A.3,
     // the cids of all its column records and of its column records at that cl with col_version > 0
     uint32_t reduce;             // 1: rows are reduced to their last epoch's records before the sort
-    uint32_t *rmx, *rbad0;
-    uint64_t *rcall, *rcfin;     // [2 * nrows] cid bits
+    uint64_t *rw1;               // [nrows] Mx << 32 | cids at Mx (rs_comb)
+    uint32_t *rw2;               // [nrows] cids | outside App. A.3
     uint32_t *nkeep;             // [1] records kept
     uint32_t *cbk;               // [Kb / 64 + 1] bucket of batch record 64 c (k_ovf_chunkmap)
 };
@@ -264,12 +265,35 @@ __device__ inline T ovf_ld_dev(const T *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ inline void ovf_rsum_put(const OvfDev &d, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad) {
-    if (mx > ovf_ld_dev(&d.rmx[row])) atomicMax(&d.rmx[row], mx);
-    unsigned long long *w = (unsigned long long *)&d.rcall[2 * row];
-    if (b0 & ~ovf_ld_dev(&d.rcall[2 * row])) atomicOr(w, (unsigned long long)b0);
-    if (b1 & ~ovf_ld_dev(&d.rcall[2 * row + 1])) atomicOr(w + 1, (unsigned long long)b1);
-    if (bad && !ovf_ld_dev(&d.rbad0[row])) d.rbad0[row] = 1;
+// A row's summary is two words, each a commutative monoid, so every record's term folds in in any
+// order and in one pass (no second pass once the largest cl is known):
+//   w1 = Mx << 32 | F   Mx the largest cl, F the cids (bit c, c < 32) of the column changes at Mx with
+//                       col_version > 0: (m, f) + (m', f') = (max, f if m is the max | f' if m' is)
+//   w2 = C | bad        C the cids of all column records (bit c), bit 0 (no cid 0 term) a record
+//                       outside App. A.3
+// (tables with 32 or more columns keep every record: the host turns the reduction off for them)
+__device__ inline uint64_t rs_comb(uint64_t x, uint64_t y) {
+    const uint32_t mx = (uint32_t)(x >> 32), my = (uint32_t)(y >> 32), m = max(mx, my);
+    return ((uint64_t)m << 32) | ((mx == m ? (uint32_t)x : 0u) | (my == m ? (uint32_t)y : 0u));
+}
+
+__device__ inline void rs_put(const OvfDev &d, uint32_t row, uint64_t w1, uint32_t w2) {
+    unsigned long long *p = (unsigned long long *)&d.rw1[row];
+    unsigned long long cur = ovf_ld_dev(&d.rw1[row]);
+    for (unsigned long long want = rs_comb(cur, w1); want != cur; want = rs_comb(cur, w1)) {
+        const unsigned long long o = atomicCAS(p, cur, want);
+        if (o == cur) break;
+        cur = o;
+    }
+    if (w2 & ~ovf_ld_dev(&d.rw2[row])) atomicOr(&d.rw2[row], w2);
+}
+
+// a record's terms
+__device__ inline void rs_terms(const MergeArgs &a, uint32_t cid, uint32_t cl, int64_t cv, uint32_t pos, uint64_t &w1,
+                                uint32_t &w2) {
+    const uint32_t bit = cid != 0 ? 1u << (cid & 31) : 0u;
+    w1 = ((uint64_t)cl << 32) | (cv > 0 ? bit : 0u);
+    w2 = bit | (ovf_rec_bad(a, cid, cl, cv, pos) ? 1u : 0u);
 }
 
 // Row summaries aggregated per workgroup first: a workgroup takes RS_CHUNK consecutive records
@@ -278,38 +302,44 @@ __device__ inline void ovf_rsum_put(const OvfDev &d, uint32_t row, uint32_t mx, 
 // row finds no LDS slot updates the global words itself.
 constexpr uint32_t RS_T = 256, RS_E = 8, RS_CHUNK = RS_T * RS_E, RS_HT = 1024;
 struct RsLds {
-    uint32_t key[RS_HT], mx[RS_HT], bad[RS_HT];  // key: row + 1 (0: free)
-    unsigned long long b0[RS_HT], b1[RS_HT];
+    uint32_t key[RS_HT], w2[RS_HT];  // key: row + 1 (0: free)
+    unsigned long long w1[RS_HT];
 };
 
 __device__ inline void rs_lds_clear(RsLds &L) {
     for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x) {
         L.key[i] = 0;
-        L.mx[i] = 0;
-        L.bad[i] = 0;
-        L.b0[i] = 0;
-        L.b1[i] = 0;
+        L.w2[i] = 0;
+        L.w1[i] = 0;
     }
 }
 
-__device__ inline bool rs_lds_add(RsLds &L, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad) {
+__device__ inline bool rs_lds_add(RsLds &L, uint32_t row, uint64_t w1, uint32_t w2) {
     const uint32_t h = (row * 2654435761u) >> 22;  // (RS_HT = 2^10)
     for (uint32_t k = 0; k < 16; k++) {
         const uint32_t sl = (h + k) & (RS_HT - 1);
         const uint32_t o = atomicCAS(&L.key[sl], 0u, row + 1);
         if (o != 0 && o != row + 1) continue;
-        if (mx) atomicMax(&L.mx[sl], mx);
-        if (b0) atomicOr(&L.b0[sl], (unsigned long long)b0);
-        if (b1) atomicOr(&L.b1[sl], (unsigned long long)b1);
-        if (bad) L.bad[sl] = 1;
+        unsigned long long cur = L.w1[sl];
+        for (unsigned long long want = rs_comb(cur, w1); want != cur; want = rs_comb(cur, w1)) {
+            const unsigned long long q = atomicCAS(&L.w1[sl], cur, want);
+            if (q == cur) break;
+            cur = q;
+        }
+        if (w2) atomicOr(&L.w2[sl], w2);
         return true;
     }
     return false;
 }
 
-__device__ inline uint64_t wave_or64(uint64_t x) {
+__device__ inline void rs_lds_flush(const RsLds &L, const OvfDev &d) {
+    for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x)
+        if (L.key[i]) rs_put(d, L.key[i] - 1, L.w1[i], L.w2[i]);
+}
+
+__device__ inline uint32_t wave_or32(uint32_t x) {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) x |= __shfl_xor(x, o);
+    for (int o = 1; o < 64; o <<= 1) x |= (uint32_t)__shfl_xor(x, o);
     return x;
 }
 
@@ -319,16 +349,10 @@ __device__ inline uint32_t wave_max32(uint32_t x) {
     return x;
 }
 
-template <bool FIN>
-__device__ inline void rs_put(const OvfDev &d, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad);
-
-// One summary term per `todo` lane (called by every lane of the wave): lanes sharing the first
-// active lane's row -- a Zipf-hot row fills whole waves -- are reduced across the wave and added by
-// that lane (at most two rounds), the rest add their own term; LDS first, the global words when the
-// table has no slot for the row.
-template <bool FIN>
-__device__ inline void rs_wave_add(RsLds &L, const OvfDev &d, bool todo, uint32_t row, uint32_t mx, uint64_t b0,
-                                   uint64_t b1, bool bad) {
+// One term per `todo` lane (called by every lane of the wave): lanes sharing the first active lane's
+// row -- a Zipf-hot row fills whole waves -- are combined across the wave and added by that lane (at
+// most two rounds), the rest add their own; LDS first, the global words when the table has no slot.
+__device__ inline void rs_wave_add(RsLds &L, const OvfDev &d, bool todo, uint32_t row, uint64_t w1, uint32_t w2) {
     const uint32_t lane = threadIdx.x & 63;
     for (int round = 0; round < 2; round++) {
         const uint64_t act = __ballot(todo);
@@ -337,31 +361,14 @@ __device__ inline void rs_wave_add(RsLds &L, const OvfDev &d, bool todo, uint32_
         const uint32_t lrow = __shfl(row, leader);
         const bool mine = todo && row == lrow;
         if (__popcll(__ballot(mine)) < 8) break;  // (wave-uniform) not a hot row
-        const uint32_t m = wave_max32(mine ? mx : 0u);
-        const uint64_t o0 = wave_or64(mine ? b0 : 0ULL), o1 = wave_or64(mine ? b1 : 0ULL);
-        const bool bd = __ballot(mine && bad) != 0;
-        if ((int)lane == leader && !rs_lds_add(L, lrow, m, o0, o1, bd)) rs_put<FIN>(d, lrow, m, o0, o1, bd);
+        const uint32_t m = wave_max32(mine ? (uint32_t)(w1 >> 32) : 0u);
+        const uint32_t f = wave_or32(mine && (uint32_t)(w1 >> 32) == m ? (uint32_t)w1 : 0u);
+        const uint32_t c = wave_or32(mine ? w2 : 0u);
+        const uint64_t x1 = ((uint64_t)m << 32) | f;
+        if ((int)lane == leader && !rs_lds_add(L, lrow, x1, c)) rs_put(d, lrow, x1, c);
         if (mine) todo = false;
     }
-    if (todo && !rs_lds_add(L, row, mx, b0, b1, bad)) rs_put<FIN>(d, row, mx, b0, b1, bad);
-}
-
-// FIN: the table holds the cid bits at the row's largest cl (rcfin), else the full summary
-template <bool FIN>
-__device__ inline void rs_put(const OvfDev &d, uint32_t row, uint32_t mx, uint64_t b0, uint64_t b1, bool bad) {
-    if (!FIN) {
-        ovf_rsum_put(d, row, mx, b0, b1, bad);
-        return;
-    }
-    unsigned long long *w = (unsigned long long *)&d.rcfin[2 * row];
-    if (b0 & ~ovf_ld_dev(&d.rcfin[2 * row])) atomicOr(w, (unsigned long long)b0);
-    if (b1 & ~ovf_ld_dev(&d.rcfin[2 * row + 1])) atomicOr(w + 1, (unsigned long long)b1);
-}
-
-template <bool FIN>
-__device__ inline void rs_lds_flush(const RsLds &L, const OvfDev &d) {
-    for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x)
-        if (L.key[i]) rs_put<FIN>(d, L.key[i] - 1, L.mx[i], L.b0[i], L.b1[i], L.bad[i] != 0);
+    if (todo && !rs_lds_add(L, row, w1, w2)) rs_put(d, row, w1, w2);
 }
 
 static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev d) {
@@ -383,19 +390,13 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
             d.key[r] = ((uint64_t)row << d.rshift) | ((uint64_t)d.pm + (pos & 0x7FFFFFFFu));
         }
         if (d.reduce) {
-            uint32_t cl = 0;
-            uint64_t b0 = 0, b1 = 0;
-            bool bad = false;
+            uint64_t w1 = 0;
+            uint32_t w2 = 0;
             if (valid) {
                 d.rowid[r] = row;  // (own slot: every other lane reads epc, not rowid)
-                const uint32_t cid = d.tc[r] & 0xFFFFu;
-                cl = d.cl[r];
-                const uint64_t bit = cid != 0 ? 1ULL << (cid & 63) : 0ULL;
-                b0 = cid < 64 ? bit : 0ULL;
-                b1 = cid >= 64 ? bit : 0ULL;
-                bad = ovf_rec_bad(a, cid, cl, d.cv[r], pos);
+                rs_terms(a, d.tc[r] & 0xFFFFu, d.cl[r], d.cv[r], pos, w1, w2);
             }
-            rs_wave_add<false>(L, d, valid, row, cl, b0, b1, bad);
+            rs_wave_add(L, d, valid, row, w1, w2);
         }
         if (!valid || !d.recf[r]) continue;  // (an owner's row: epc[r] - 1, as computed above)
         const uint32_t b = d.pb[r], t = d.tc[r] >> 16;
@@ -420,7 +421,7 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
     }
     if (d.reduce) {
         __syncthreads();
-        rs_lds_flush<false>(L, d);
+        rs_lds_flush(L, d);
     }
 }
 
@@ -447,36 +448,14 @@ static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
                 d.val[r] = r;
                 if (d.reduce) {
                     d.rowid[r] = row;
-                    const uint32_t cid = pr.tcid & 0xFFFFu;
-                    const uint64_t bit = cid != 0 ? 1ULL << (cid & 63) : 0ULL;
-                    ovf_rsum_put(d, row, pr.cl, cid < 64 ? bit : 0ULL, cid >= 64 ? bit : 0ULL,
-                                 ovf_rec_bad(a, cid, pr.cl, pr.cv, c));
+                    uint64_t w1;
+                    uint32_t w2;
+                    rs_terms(a, pr.tcid & 0xFFFFu, pr.cl, pr.cv, c, w1, w2);
+                    rs_put(d, row, w1, w2);
                 }
                 r++;
             }
     }
-}
-
-// the cids with a change of col_version > 0 at the row's largest cl
-static __global__ void __launch_bounds__(RS_T) k_ovf_rfin(OvfDev d) {
-    __shared__ RsLds L;  // (rs_lds_add's table: key and cid bits used)
-    rs_lds_clear(L);
-    __syncthreads();
-    const uint32_t c0 = blockIdx.x * RS_CHUNK;
-    for (uint32_t j = 0; j < RS_E; j++) {  // (wave-uniform)
-        const uint32_t r = c0 + j * RS_T + threadIdx.x;
-        uint32_t cid = 0, row = 0;
-        bool fin = false;
-        if (r < d.K) {
-            cid = d.tc[r] & 0xFFFFu;
-            row = d.rowid[r];
-            fin = cid != 0 && d.cv[r] > 0 && d.cl[r] == d.rmx[row];
-        }
-        const uint64_t bit = 1ULL << (cid & 63), b0 = cid < 64 ? bit : 0ULL, b1 = cid >= 64 ? bit : 0ULL;
-        rs_wave_add<true>(L, d, fin, row, 0u, b0, b1, false);
-    }
-    __syncthreads();
-    rs_lds_flush<true>(L, d);
 }
 
 // The kept records' (key, record) pairs compacted into (ckey, cval) for the sort: each workgroup
@@ -493,9 +472,10 @@ static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(OvfDev d) {
         const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
         bool keep = false;
         if (r < n) {
-            const uint32_t row = d.rowid[r], mx = d.rmx[row], cl = d.cl[r];
-            const bool red = !d.rbad0[row] && (!(mx & 1u) || (d.rcfin[2 * row] == d.rcall[2 * row] &&
-                                                               d.rcfin[2 * row + 1] == d.rcall[2 * row + 1]));
+            const uint32_t row = d.rowid[r], cl = d.cl[r], w2 = d.rw2[row];
+            const uint64_t w1 = d.rw1[row];
+            const uint32_t mx = (uint32_t)(w1 >> 32);
+            const bool red = !(w2 & 1u) && (!(mx & 1u) || (uint32_t)w1 == w2);
             keep = !red || cl == mx;
         }
         mine |= keep ? 1u << j : 0u;
