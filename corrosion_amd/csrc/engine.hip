@@ -80,11 +80,15 @@ int affinity_convert(corro_ctx *ctx, BatchDev &bd);  // affinity.hip
 static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nbatch, bool prof) {
     hipStream_t s = ctx->stream;
     const uint32_t B = ctx->B;
-    std::vector<uint32_t> list(novf), nc(B), used0(B);
-    CORRO_HIP_TRY(hipMemcpy(list.data(), ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost));
-    CORRO_HIP_TRY(hipMemcpy(nc.data(), ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost));
-    CORRO_HIP_TRY(hipMemcpy(used0.data(), ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> koff(novf + 1), soff(novf);
+    // readbacks land in pinned memory: async copies, one wait per group (pageable ones block per copy)
+    if (!ctx->h_ovf) CORRO_HIP_TRY(hipHostMalloc((void **)&ctx->h_ovf, (8ULL * B + 32) * 4, hipHostMallocDefault));
+    uint32_t *const list = ctx->h_ovf, *const nc = list + B, *const used0 = nc + B, *const koff = used0 + B;
+    uint32_t *const soff = koff + B + 1, *const bnew = soff + B, *const bnrec = bnew + B, *const used = bnrec + B;
+    uint32_t *const hw = used + B;
+    CORRO_HIP_TRY(hipMemcpyAsync(list, ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(nc, ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(used0, ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
     uint64_t Kb = 0, S = 0;
     for (uint64_t k = 0; k < novf; k++) {
         const uint64_t n = nc[list[k]];
@@ -178,8 +182,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
             base = ctx->d_ovf_sort.as<uint8_t>();
         }
     }
-    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.koff, koff.data(), (novf + 1) * 4, hipMemcpyHostToDevice, s));
-    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.slot_off, soff.data(), novf * 4, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.koff, koff, (novf + 1) * 4, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.slot_off, soff, novf * 4, hipMemcpyHostToDevice, s));
     CORRO_HIP_TRY(hipMemsetAsync(d.bnew, 0, novf * 4, s));
     CORRO_HIP_TRY(hipMemsetAsync(d.bnrec, 0, novf * 4, s));
     CORRO_HIP_TRY(hipMemsetAsync(d.slots, 0, S * 4, s));
@@ -195,9 +199,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     TRY(launched());
     // dense row ids: the row count sizes the sort's key
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.recf, d.epc, d.Kb, s));
-    uint32_t nrows = 0;
-    CORRO_HIP_TRY(hipMemcpyAsync(&nrows, d.epc + (Kb - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&hw[0], d.epc + (Kb - 1), 4, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t nrows = hw[0];
     d.nrows = nrows;
     d.rshift = pbits;
     // row reduction off with impacts (every epoch's changes get a flag) or when asked (A/B runs)
@@ -215,15 +219,14 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     hipLaunchKernelGGL(k_ovf_lookup, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)), dim3(RS_T), 0, s, a, d);
     TRY(launched());
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
-    uint32_t P = 0;
-    std::vector<uint32_t> bnew(novf), bnrec(novf), used(B);
-    CORRO_HIP_TRY(hipMemcpyAsync(&P, d.rpoff + (nrows - 1), 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(bnew.data(), d.bnew, novf * 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(bnrec.data(), d.bnrec, novf * 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(used.data(), ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost, s));
-    unsigned long long top = 0;
-    CORRO_HIP_TRY(hipMemcpyAsync(&top, ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&hw[0], d.rpoff + (nrows - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(bnew, d.bnew, novf * 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(bnrec, d.bnrec, novf * 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(used, ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&hw[2], ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t P = hw[0];
+    const unsigned long long top = (unsigned long long)hw[2] | ((unsigned long long)hw[3] << 32);
     if (Kb + (uint64_t)P > Kmax) return fail(CORRO_E_DEVICE, "internal: overflow prior records exceed their bound");
     // room for the new rows (region fill, heap) before the walk writes anything
     uint64_t need_heap = 0;
@@ -252,9 +255,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         // rows reduced to their last epoch's records (k_ovf_lookup's comment); the rest sort as before
         hipLaunchKernelGGL(k_ovf_keep, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK), dim3(KEEP_T), 0, s, d);
         TRY(launched());
-        uint32_t kept = 0;
-        CORRO_HIP_TRY(hipMemcpyAsync(&kept, d.nkeep, 4, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(&hw[4], d.nkeep, 4, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipStreamSynchronize(s));
+        const uint32_t kept = hw[4];
         if (kept == 0 || kept > d.K) return fail(CORRO_E_DEVICE, "internal: overflow row reduction kept no records");
         if (dbg) fprintf(stderr, "[corro ovf] row reduction keeps %u of %u records\n", kept, d.K);
         d.K = kept;
@@ -274,9 +277,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     TRY(launched());
     // only the candidates are sorted (a minority of the records): compact them first
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.slots, d.slots + d.K, d.K, s));
-    uint32_t ncand = 0;
-    CORRO_HIP_TRY(hipMemcpyAsync(&ncand, d.slots + d.K + (d.K - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&hw[5], d.slots + d.K + (d.K - 1), 4, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t ncand = hw[5];
     hipLaunchKernelGGL(k_ovf_ccompact, grid, blk, 0, s, d);
     TRY(launched());
     if (ncand) TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.ckey_s, d.val, d.cval_s, ncand, ckey_bits, s));
@@ -577,6 +580,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
         t.d_hash.release();
     }
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
+    if (ctx->h_ovf) (void)hipHostFree(ctx->h_ovf);
     if (ctx->h_agent) (void)hipHostFree(ctx->h_agent);
     if (ctx->h_hdr) (void)hipHostFree(ctx->h_hdr);
     for (auto &e : ctx->ev)

@@ -218,6 +218,7 @@ struct corro_ctx {
     uint64_t agent_ncs = 0;       // changesets of the current call (d_agent_spans column length)
     uint64_t agent_nbatch_max = 0;  // input changes of the current call (bound on the applied batch)
     uint64_t *h_misc = nullptr;   // pinned, 16 words
+    uint32_t *h_ovf = nullptr;    // pinned, 3 B + 16 words: the overflow fold's readbacks (run_overflow)
     // stage timing
     bool profiling = false;
     hipEvent_t ev[8] = {};
