@@ -70,6 +70,7 @@ struct MergeArgs {
     const uint32_t *bucket_list;  // a re-merge: workgroup k takes bucket bucket_list[k] (null: k itself)
     uint32_t B;
     uint32_t force_general;    // route every non-empty bucket through the sequential general body
+    uint32_t gen_ovf_min;      // general buckets of more records than this go to the device-wide fold
     uint32_t track_ts;
     uint32_t state_wide;       // the state holds non-INTEGER values
     const uint8_t *arena;      // bytes of long TEXT/BLOB values (value handles point into it)
@@ -2458,7 +2459,9 @@ k_merge_fast_int(MergeArgs a) {
     if (n == 0) return;
     if (a.force_general || rgen || ((bword >> (b & 31)) & 1u)) {
         if (threadIdx.x == 0) {
-            if (n <= CAP_GEN_SMALL)
+            if (n > a.gen_ovf_min)
+                push_overflow(a, b);
+            else if (n <= CAP_GEN_SMALL)
                 a.gen_list[a.B + atomicAdd(&a.misc[MISC_GEN_SMALL], 1ULL)] = b;
             else if (n <= CAP_GEN_MID)
                 a.gen_list[2 * a.B + atomicAdd(&a.misc[MISC_GEN_MID], 1ULL)] = b;
