@@ -194,6 +194,10 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         CORRO_HIP_TRY(hipGetLastError());
         return CORRO_OK;
     };
+    // row reduction off with impacts (every epoch's changes get a flag) or when asked (A/B runs)
+    static const bool no_reduce = std::getenv("CORRO_OVF_REDUCE") && std::atoi(std::getenv("CORRO_OVF_REDUCE")) == 0;
+    // (the summary's cid bits cover cids < 32)
+    d.reduce = (!a.impact && !no_reduce && ctx->max_stride <= 32) ? 1u : 0u;
     hipLaunchKernelGGL(k_ovf_chunkmap, grid_for((Kb + 63) / 64), blk, 0, s, d);
     hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
     TRY(launched());
@@ -204,10 +208,6 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     const uint32_t nrows = hw[0];
     d.nrows = nrows;
     d.rshift = pbits;
-    // row reduction off with impacts (every epoch's changes get a flag) or when asked (A/B runs)
-    static const bool no_reduce = std::getenv("CORRO_OVF_REDUCE") && std::atoi(std::getenv("CORRO_OVF_REDUCE")) == 0;
-    // (the summary's cid bits cover cids < 32)
-    d.reduce = (!a.impact && !no_reduce && ctx->max_stride <= 32) ? 1u : 0u;
     {
         uint8_t *blk = (uint8_t *)d.rw1;
         d.rw2 = (uint32_t *)(blk + 8ULL * nrows);
@@ -297,7 +297,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         hipLaunchKernelGGL(k_cscan_fix, dim3(ntc), dim3(CS_T), 0, s, d, cs_incl, cs_first);
     }
     TRY(launched());
-    if (ncand) TRY(ovf_scans(d_temp, &temp, d, 2, s));
+    if (ncand && a.impact) TRY(ovf_scans(d_temp, &temp, d, 2, s));  // (group starts: impacts only)
     hipLaunchKernelGGL(k_ovf_link, cgrid, blk, 0, s, d);
     // carried cells in registers when no table has WALK_MAXC or more columns (cids 1..ncols)
     auto walk = ctx->max_stride <= WALK_MAXC ? k_ovf_walk<true> : k_ovf_walk<false>;

@@ -186,7 +186,6 @@ static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
         const uint32_t sbase = a.stage_off[a.ovf_list[b]];
         const uint32_t si = sbase + (r - kb);
         const Rec x = load_rec(a.stage + si);
-        d.pb[r] = b;
         d.src[r] = si;
         d.pk[r] = x.pk;
         d.cv[r] = x.cv;
@@ -234,7 +233,7 @@ static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
         if (todo) owner = probe();
         d.rowid[r] = owner;  // (scratch until the sort)
         d.recf[r] = owner == r - kb ? 1u : 0u;
-        d.val[r] = r;
+        if (!d.reduce) d.val[r] = r;  // (the reduction's compaction writes the sort values)
     }
 }
 
@@ -382,9 +381,12 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
         const uint32_t r = c0 + j * RS_T + threadIdx.x;
         const bool valid = r < d.Kb;
         // every record: its sort key (k_ovf_rowkey's, fused here: dense rows are known by now)
-        uint32_t row = 0, pos = 0;
+        uint32_t row = 0, pos = 0, bk = 0;
         if (valid) {
-            const uint32_t kb = d.koff[d.pb[r]];
+            uint32_t b = d.cbk[r >> 6];
+            while (d.koff[b + 1] <= r) b++;
+            bk = b;
+            const uint32_t kb = d.koff[b];
             row = d.epc[kb + d.rowid[r]] - 1u;
             pos = d.pos[r];
             d.key[r] = ((uint64_t)row << d.rshift) | ((uint64_t)d.pm + (pos & 0x7FFFFFFFu));
@@ -399,7 +401,7 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
             rs_wave_add(L, d, valid, row, w1, w2);
         }
         if (!valid || !d.recf[r]) continue;  // (an owner's row: epc[r] - 1, as computed above)
-        const uint32_t b = d.pb[r], t = d.tc[r] >> 16;
+        const uint32_t b = bk, t = d.tc[r] >> 16;
         d.rowner[row] = r;
         d.rb[row] = b;
         const uint32_t e = rs_lookup(a.rs, a.ovf_list[b], d.pk[r], t);
@@ -498,7 +500,7 @@ static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(OvfDev d) {
             const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
             const uint32_t q = o + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
             d.ckey[q] = d.key[r];
-            d.cval[q] = d.val[r];
+            d.cval[q] = r;
         }
         o += (uint32_t)__popcll(m);
     }
@@ -508,10 +510,9 @@ static __global__ void k_ovf_gather(OvfDev d) {
     OVF_LOOP(p, d.K) {
         const uint32_t row = (uint32_t)(d.key_s[p] >> d.rshift);
         d.rowid[p] = row;
-        d.pb[p] = d.rb[row];
         d.cl_s[p] = d.cl[d.val_s[p]];
         d.head[p] = 0;
-        d.fstg[p] = 0;
+        if (!d.reduce) d.fstg[p] = 0;  // (impacts only; never with the row reduction)
         if (p == 0 || (uint32_t)(d.key_s[p - 1] >> d.rshift) != row) {
             d.rstart[row] = p;
             d.rbad[row] = 0;
@@ -831,7 +832,7 @@ static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeAr
                 const uint32_t cid = (uint32_t)d.ckey_s[qe] & ((1u << d.cid_bits) - 1);
                 const int found = cs.find(cid, ncell);
                 const uint32_t fp = found < 0 ? 0u : cs.pos((uint32_t)found), fz = found < 0 ? 0u : cs.z((uint32_t)found);
-                d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((fp + 1) | (fz << 31));
+                if (a.impact) d.fstg[d.cgs[qe]] = found < 0 ? 0u : ((fp + 1) | (fz << 31));
                 const uint32_t wq = d.cbest[qe];
                 if (found < 0 || ovf_kcmp(ovf_key_q(d, wq), ovf_key_p(a, d, fp, fz != 0), d.arena) > 0) set(cid, d.cval_s[wq], 0);
             }
