@@ -1,0 +1,61 @@
+"""GPU parity of the overflow fold's row reduction (ovf_kernels.h, k_ovf_lookup's comment) at its edges,
+against the sequential oracle (oracle/crsql_fold.c): the cid mask's last bit (cid 31, tables of 32
+columns: reduction on), tables of more columns (reduction off for the batch), and a hot-row batch folded
+into a prior state whose rows hold cids the new batch does not touch (rows that must keep every change)."""
+import numpy as np
+import pytest
+
+import synth
+from oracle import oracle as O
+from tests._util import rows_to_tuples
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(schema, sites, cap=64):
+    import corrosion_amd as ca
+    e = ca.MergeEngine(schema, capacity_hint=cap)  # a small capacity: every bucket overflows
+    e.register_sites(sites)
+    return e
+
+
+def _recid(b, ncols, seed, lo=1):
+    """b with its column changes spread over cids lo..ncols (sentinels keep cid 0)"""
+    rng = np.random.default_rng(seed)
+    tc = np.asarray(b["table_cid"], np.uint32)
+    cid = tc & 0xFFFF
+    new = rng.integers(lo, ncols + 1, size=len(tc)).astype(np.uint32)
+    out = dict(b)
+    out["table_cid"] = np.where(cid != 0, (tc & 0xFFFF0000) | new, tc).astype(np.uint32)
+    return out
+
+
+def _compare(e, f):
+    assert rows_to_tuples(e.export(), with_ts=True) == rows_to_tuples(f.export(), with_ts=True)
+    assert list(e.db_versions()[:f.nsites]) == list(f.db_versions())
+
+
+@pytest.mark.parametrize("ncols,lo", [(31, 25), (40, 28)], ids=["cid31_reduced", "wide_not_reduced"])
+def test_reduction_cid_mask_edges(ncols, lo):
+    seed = 901 + ncols
+    sites = synth.site_ids(8, seed)
+    e, f = _engine({"t0": [f"c{i}" for i in range(ncols)]}, sites), O.Fold(sites)
+    for k in range(3):
+        b = _recid(synth.adversarial_batch(40000, 8, 1, 80, seed * 10 + k, zipf=1.1), ncols, seed + k, lo=lo)
+        e.apply(b)
+        f.apply(b)
+    _compare(e, f)
+
+
+def test_reduction_keeps_rows_with_untouched_prior_cids():
+    """Prior rows hold cids 1..4; the hot batch then only writes cids 1..2 at its largest cl, so rows
+    whose prior cells of cids 3..4 are not covered keep every change (and carry those cells)."""
+    seed = 933
+    sites = synth.site_ids(8, seed)
+    e, f = _engine(synth.adversarial_schema(2), sites), O.Fold(sites)
+    b1 = synth.adversarial_batch(30000, 8, 2, 200, seed, zipf=1.1)
+    b2 = _recid(synth.adversarial_batch(50000, 8, 2, 200, seed + 1, zipf=1.1), 2, seed + 2)
+    for b in (b1, b2, b1):
+        e.apply(b)
+        f.apply(b)
+        _compare(e, f)
