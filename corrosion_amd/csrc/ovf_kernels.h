@@ -299,7 +299,10 @@ __device__ inline void rs_terms(const MergeArgs &a, uint32_t cid, uint32_t cl, i
 // (bucket-major, so a few buckets' rows, a Zipf-hot row's records many times over), folds them into
 // an LDS table keyed by row, then writes each of its rows to the global words once. A record whose
 // row finds no LDS slot updates the global words itself.
-constexpr uint32_t RS_T = 256, RS_E = 8, RS_CHUNK = RS_T * RS_E, RS_HT = 1024;
+#ifndef OVF_RS_E
+#define OVF_RS_E 8  // records per thread of a summary workgroup
+#endif
+constexpr uint32_t RS_T = 256, RS_E = OVF_RS_E, RS_CHUNK = RS_T * RS_E, RS_HT = 1024;
 struct RsLds {
     uint32_t key[RS_HT], w2[RS_HT];  // key: row + 1 (0: free)
     unsigned long long w1[RS_HT];
