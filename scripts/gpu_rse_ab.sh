@@ -7,3 +7,5 @@ for v in default rse4 rse16; do
   echo "$v $(grep '^n=' gpurun_out/rse/$v.log | cut -c1-80)"
   python tools/kstats.py gpurun_out/rse/$v | grep -E "ovf_lookup|ovf_loadhash"
 done
+timeout -k 10 400 python -u bench_sync.py > gpurun_out/rse/sync.log 2>&1 || { tail -20 gpurun_out/rse/sync.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/rse/sync.log | tail -2 | cut -c1-400
