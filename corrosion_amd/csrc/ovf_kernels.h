@@ -77,7 +77,7 @@ struct OvfDev {
     const uint32_t *koff;       // [G + 1] bucket base offsets of the batch records
     const uint32_t *slot_off;   // [G] row-hash slot region, next_pow2(2 n) words each
     // per record (global index)
-    uint64_t *pk;
+    uint64_t *pk;               // (row owners only)
     int64_t *cv;
     uint32_t *tc, *cl, *pos;
     uint32_t *src;              // batch record: its staged index; prior record: its heap index
@@ -187,7 +187,6 @@ static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
         const uint32_t si = sbase + (r - kb);
         const Rec x = load_rec(a.stage + si);
         d.src[r] = si;
-        d.pk[r] = x.pk;
         d.cv[r] = x.cv;
         d.tc[r] = x.tcid;
         d.cl[r] = x.cl;
@@ -233,6 +232,7 @@ static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
         if (todo) owner = probe();
         d.rowid[r] = owner;  // (scratch until the sort)
         d.recf[r] = owner == r - kb ? 1u : 0u;
+        if (owner == r - kb) d.pk[r] = pk;  // (only a row's owner is asked for its pk)
         if (!d.reduce) d.val[r] = r;  // (the reduction's compaction writes the sort values)
     }
 }
@@ -436,13 +436,12 @@ static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
     OVF_LOOP(row, d.nrows) {
         const uint32_t pc = d.rprior[row];
         if (!pc) continue;
-        const uint32_t hb = d.rheap[row], own = d.rowner[row];
+        const uint32_t hb = d.rheap[row];
         uint32_t r = d.Kb + d.rpoff[row] - pc;
         for (int w = 0; w < 2; w++)
             for (uint64_t m = d.rbits[2 * row + w]; m; m &= m - 1) {
                 const uint32_t c = 64 * w + (uint32_t)__ffsll((unsigned long long)m) - 1;
                 const Rec pr = load_rec(a.rs.heap + hb + c);
-                d.pk[r] = d.pk[own];
                 d.cv[r] = pr.cv;
                 d.tc[r] = pr.tcid;
                 d.cl[r] = pr.cl;
