@@ -74,3 +74,18 @@ def test_row_reduction_empty_prior():
     red.apply(_sub(b, keep))
     assert (~keep).sum() > len(keep) // 2
     assert rows_to_tuples(red.export(), with_ts=True) == rows_to_tuples(full.export(), with_ts=True)
+
+
+@pytest.mark.parametrize("max_cl,sentinel_frac", [(12, 0.3), (3, 0.6), (20, 0.1)])
+def test_row_reduction_epoch_mixes(max_cl, sentinel_frac):
+    """Many epochs per row (up to 20 causal lengths), delete-heavy and resurrect-heavy mixes, three
+    batches folded: the reduced batch always gives the full batch's rows."""
+    seed = 40 + max_cl
+    sites = synth.site_ids(12, seed)
+    full, red = O.Fold(sites), O.Fold(sites)
+    for k in range(3):
+        b = synth.adversarial_batch(25000, 12, 2, 128, seed * 7 + k, max_cl=max_cl, sentinel_frac=sentinel_frac)
+        keep, _ = reduce_keep(b, full.export())
+        full.apply(b)
+        red.apply(_sub(b, keep))
+        assert rows_to_tuples(red.export(), with_ts=True) == rows_to_tuples(full.export(), with_ts=True), k
