@@ -43,6 +43,14 @@ ALG_BYTES_PER_CHANGE = 48  # pk 8, table_cid 4, col_version 8, db
 ALG_BYTES_PER_CELL = 48
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8 TB/s spec
 METRIC = "merged column-changes/sec (node) at 1/2/4/8 GPUs + % of HBM BW roofline"
+# The reference's own CPU apply (cr-sqlite 0.17 through SQLite, one writer, per-change INSERT +
+# crsql_rows_impacted()), recorded during the survey in the build container -- not re-run here: the
+# cr-sqlite binary ships prebuilt inside the reference and is never loaded.
+REFERENCE_CPU = {"value_range": [53000.0, 103000.0], "unit": "merged column-changes/s", "cores": 1,
+                 "kind": "reference (survey-recorded)",
+                 "sample": "cr-sqlite 0.17.0 via SQLite 3.37.2, 100k-1M changes, 1 table x 3 INTEGER cols: 103k/s "
+                           "(100k changes, 4 actors), 53-56k/s (1M changes: B-tree growth); recorded in the build "
+                           "container (Intel Xeon, 1 core), SURVEY.md App. D -- not re-run on the GPU box"}
 
 
 def cpu_baseline(batch_dev, seconds_target=15.0):
@@ -85,7 +93,8 @@ def cpu_baseline(batch_dev, seconds_target=15.0):
             "sample": f"the bench's own {n_all}-change batch folded by oracle/crsql_fold.c of_apply_sharded "
                       f"({4 * threads} pk-hash shards, {threads} threads) in {dt_mt:.2f} s",
             "single_core": {"value": n / dt, "cores": 1,
-                            "sample": f"{n} changes of the config-2 distribution folded sequentially in {dt:.2f} s"}}
+                            "sample": f"{n} changes of the config-2 distribution folded sequentially in {dt:.2f} s"},
+            "reference": REFERENCE_CPU}
 
 
 def cpu_baseline_sample(npk, n=1 << 24, threads=None):
@@ -102,7 +111,8 @@ def cpu_baseline_sample(npk, n=1 << 24, threads=None):
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "merged column-changes/s", "cores": threads, "kind": "port",
             "sample": f"{n} changes of the line's distribution (pk space {npk}) folded by oracle/crsql_fold.c "
-                      f"of_apply_sharded ({4 * threads} pk-hash shards, {threads} threads) in {dt:.2f} s"}
+                      f"of_apply_sharded ({4 * threads} pk-hash shards, {threads} threads) in {dt:.2f} s",
+            "reference": REFERENCE_CPU}
 
 
 # ------------------------------------------------------------------------------------- PMC traffic

@@ -36,7 +36,7 @@ EXPORTS = [
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
     "corro_unpack_records", "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
-    "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity",
+    "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity", "corro_set_affinity_policy",
     "corro_ctx_metrics", "corro_table_committed", "corro_ctx_track_touched", "corro_state_export_touched",
     "corro_ctx_set_store_limit", "corro_partition_var", "corro_unpack_var",
 ]
@@ -196,6 +196,7 @@ def lib():
         "corro_ctx_metrics": (i32, [vp, C.POINTER(Metrics)]),
         "corro_table_committed": (i32, [vp, u32, vp]),
         "corro_table_set_affinity": (i32, [vp, u32, vp, u32]),
+        "corro_set_affinity_policy": (i32, [vp, i32]),
         "corro_booked_insert_db_batch": (i32, [vp, C.POINTER(GapsIn), C.POINTER(GapsOut)]),
         "corro_compute_needs_packed": (i32, [vp, C.POINTER(SyncEntries), C.POINTER(NeedsPackedOut), u64, u64]),
         "corro_bookie_seq_bookkeeping": (i32, [vp, vp, u64, vp, vp, u64, vp, vp, vp]),

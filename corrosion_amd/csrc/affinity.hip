@@ -17,6 +17,25 @@
 //   NUMERIC/INTEGER REAL holding an integer in (-2^63, 2^63) -> INTEGER; numeric TEXT -> INTEGER/REAL
 //   REAL            as NUMERIC, then an INTEGER result is read back as REAL
 //   BLOB (none)     nothing; NULL and BLOB values are never converted
+//
+// Version gap: the reference bundles SQLite through libsqlite3-sys 0.31.0
+// (Cargo.lock:2444), a newer SQLite than the 3.37.2 this image holds and the fixtures pin. Newer
+// SQLite rewrote sqlite3AtoF and the REAL -> TEXT rendering, so a conversion whose result hinges on
+// 3.37.2's long-double rounding is not known to match the reference's base table. The default
+// policy (CORRO_AFF_POLICY_PORTABLE) therefore converts only what any correctly rounded
+// implementation of these routines stores identically, and refuses the rest (CORRO_E_RANGE, before
+// any write):
+//   TEXT -> REAL   refused when a nonzero digit past the 19th is dropped, when the result
+//                  overflows / is subnormal / takes the e > 307 double-scaling path, or when the
+//                  long-double value lies within a margin of the double rounding midpoint (1 unit
+//                  of 2^-64 when 10^e is exact, e <= 27; 32 otherwise -- above 3.37.2's scaling
+//                  error, so outside it both 3.37.2 and a correctly rounded conversion pick the
+//                  same double);
+//   REAL -> TEXT   refused unless the "%!.15g" text converts back to the same double (then the
+//                  15-digit rendering is far from a rounding tie and equals the shortest
+//                  round-trip form as well), and for -0.0 (3.37.2 writes "0.0").
+// Integer text, INTEGER -> TEXT / REAL and REAL -> INTEGER are exact and always converted.
+// CORRO_AFF_POLICY_SQLITE_3_37_2 converts everything bit for bit as 3.37.2 does (the fixtures).
 #include <hip/hip_runtime.h>
 
 #include <cctype>
@@ -189,8 +208,10 @@ __device__ inline X87 x_pow10(int E) {
 
 // sqlite3AtoF (UTF-8): 1 = pure integer, 2+ = '.' and/or exponent, <= 0 = not a number (-1: a numeric
 // prefix with '.'/exponent and trailing text)
-__device__ int aff_atof(const TextView &t, double *out) {
+// *sens: the result is not known to be version-independent (the header's PORTABLE rules).
+__device__ int aff_atof(const TextView &t, double *out, bool *sens) {
     constexpr int64_t LARGEST = 0x7fffffffffffffffLL;
+    *sens = false;
     uint64_t z = 0;
     const uint64_t zEnd = t.len;
     int sign = 1, d = 0, esign = 1, e = 0, eValid = 1, nDigit = 0, eType = 1;
@@ -211,6 +232,7 @@ __device__ int aff_atof(const TextView &t, double *out) {
         nDigit++;
         if (s >= ((LARGEST - 9) / 10))
             while (z < zEnd && aff_digit(t.at(z))) {
+                *sens |= t.at(z) != '0';  // a dropped digit
                 z++;
                 d++;
             }
@@ -223,6 +245,8 @@ __device__ int aff_atof(const TextView &t, double *out) {
                 s = s * 10 + (int64_t)(t.at(z) - '0');
                 d--;
                 nDigit++;
+            } else {
+                *sens |= t.at(z) != '0';  // a dropped digit
             }
             z++;
         }
@@ -270,18 +294,27 @@ __device__ int aff_atof(const TextView &t, double *out) {
         if (e == 0) {
             result = (double)(sign < 0 ? -s : s);
         } else if (e > 307 && e >= 342) {
+            *sens = true;
             result = esign < 0 ? (sign < 0 ? -0.0 : 0.0)
                                : __longlong_as_double(sign < 0 ? (long long)0xFFF0000000000000ULL : 0x7FF0000000000000LL);
         } else {
             const X87 S = x_u64((uint64_t)s);  // s > 0 here; the sign is applied to the result
             if (e > 307) {
+                *sens = true;
                 const X87 scale = x_pow10(e - 308);
                 double r = x_to_dbl(esign < 0 ? x_div(S, scale) : x_mul(S, scale));
                 r = esign < 0 ? r / 1.0e+308 : r * 1.0e+308;
                 result = sign < 0 ? -r : r;
             } else {
                 const X87 scale = x_pow10(e);
-                const double r = x_to_dbl(esign < 0 ? x_div(S, scale) : x_mul(S, scale));
+                const X87 q = esign < 0 ? x_div(S, scale) : x_mul(S, scale);
+                const double r = x_to_dbl(q);
+                const int E = q.e + 63;  // the double's exponent
+                const int low = (int)(q.m & 0x7FFu);  // the 11 bits the double drops: tie at 0x400
+                // 3.37.2's error in 2^-64 units: half of one when 10^e is exact (e <= 27: one rounding),
+                // a few per rounding of the binary powering otherwise (margin 32)
+                const int margin = e <= 27 ? 1 : 32;
+                if (E > 1023 || E < -1022 || (low >= 0x400 - margin && low <= 0x400 + margin)) *sens = true;
                 result = sign < 0 ? -r : r;
             }
         }
@@ -423,14 +456,28 @@ __device__ uint32_t aff_real_text(double r, uint8_t *out) {
 
 // The value a column of affinity `aff` stores for (ty, v0, text t). True = converted: *oty, *ov0
 // (INTEGER / REAL bits) or txt/len (TEXT, at most 24 bytes).
+// *sens: the conversion is not known to be version-independent (the header's PORTABLE rules).
 __device__ bool aff_convert(uint32_t aff, uint32_t ty, uint64_t v0, const TextView &t, uint32_t *oty,
-                            uint64_t *ov0, uint8_t *txt, uint32_t *len) {
+                            uint64_t *ov0, uint8_t *txt, uint32_t *len, bool *sens) {
     *len = 0;
+    *sens = false;
     if (aff == CORRO_AFF_BLOB || ty == CORRO_NULL || ty == CORRO_BLOB) return false;
     if (aff == CORRO_AFF_TEXT) {
-        if (ty == CORRO_INTEGER) *len = aff_int_text((int64_t)v0, txt);
-        else if (ty == CORRO_REAL) *len = aff_real_text(__longlong_as_double((long long)v0), txt);
-        else return false;
+        if (ty == CORRO_INTEGER) {
+            *len = aff_int_text((int64_t)v0, txt);
+        } else if (ty == CORRO_REAL) {
+            const double r = __longlong_as_double((long long)v0);
+            *len = aff_real_text(r, txt);
+            TextView back{0, 0, txt, *len};
+            double rb;
+            bool sb;  // (unused: 3.37.2's re-read is enough -- when it gives r back, r lies within
+                      // about half an ulp of the 15-digit text, far from a 15th-digit tie)
+            // must round-trip; -0.0 renders as "0.0" in 3.37.2 (its sign test is r < 0.0), a
+            // rendering later versions need not share
+            *sens = aff_atof(back, &rb, &sb) <= 0 || rb != r || (r == 0.0 && signbit(r));
+        } else {
+            return false;
+        }
         *oty = CORRO_TEXT;
         *ov0 = 0;
         return true;
@@ -440,18 +487,21 @@ __device__ bool aff_convert(uint32_t aff, uint32_t ty, uint64_t v0, const TextVi
     double rv = __longlong_as_double((long long)v0);
     if (ty == CORRO_TEXT) {
         double r;
-        const int rc = aff_atof(t, &r);
+        bool sr;
+        const int rc = aff_atof(t, &r, &sr);
         if (rc <= 0) return false;
         int64_t i;
-        if (rc == 1 && aff_atoi64(t, &i)) {  // alsoAnInt
+        if (rc == 1 && aff_atoi64(t, &i)) {  // alsoAnInt (exact)
             rt = CORRO_INTEGER;
             iv = i;
         } else if (aff_real_int(r, &i)) {
             rt = CORRO_INTEGER;
             iv = i;
+            *sens = sr;
         } else {
             rt = CORRO_REAL;
             rv = r;
+            *sens = sr;
         }
     } else if (ty == CORRO_REAL) {
         int64_t i;
@@ -478,7 +528,7 @@ __global__ void __launch_bounds__(256) k_aff_convert(BatchDev in, const uint8_t 
                                                      uint8_t *conv, uint64_t *cv0, uint64_t *cv1, uint32_t *cmeta,
                                                      uint8_t *arena, uint64_t slot_base,
                                                      unsigned long long *cnt) {
-    uint32_t nconv = 0, nlong = 0;
+    uint32_t nconv = 0, nlong = 0, nsens = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < in.n; i += gridDim.x * blockDim.x) {
         if (WRITE && !conv[i]) continue;
         const uint32_t tc = in.tcid[i], t = tc >> 16, cid = tc & 0xFFFFu;
@@ -508,9 +558,11 @@ __global__ void __launch_bounds__(256) k_aff_convert(BatchDev in, const uint8_t 
             uint32_t oty = 0, olen = 0;
             uint64_t ov0 = 0;
             uint8_t txt[32];
-            if (go && aff_convert(a, ty, in.v0[i], tv, &oty, &ov0, txt, &olen)) {
+            bool sens = false;
+            if (go && aff_convert(a, ty, in.v0[i], tv, &oty, &ov0, txt, &olen, &sens)) {
                 c = 1;
                 nconv++;
+                nsens += sens;
                 nlong += olen > 16;
                 if (WRITE) {
                     uint64_t w0 = 0, w1 = 0;
@@ -540,9 +592,11 @@ __global__ void __launch_bounds__(256) k_aff_convert(BatchDev in, const uint8_t 
     if (!WRITE) {
         nconv = wave_sum_u32(nconv);
         nlong = wave_sum_u32(nlong);
+        nsens = wave_sum_u32(nsens);
         if ((threadIdx.x & 63) == 0 && nconv) {
             atomicAdd(&cnt[0], (unsigned long long)nconv);
             atomicAdd(&cnt[1], (unsigned long long)nlong);
+            if (nsens) atomicAdd(&cnt[3], (unsigned long long)nsens);
         }
     }
 }
@@ -568,10 +622,14 @@ int affinity_convert(corro_ctx *ctx, BatchDev &bd) {
     hipLaunchKernelGGL(k_aff_convert<false>, grid, dim3(256), 0, s, bd, ctx->d_aff.as<uint8_t>(), nt, conv, nullptr,
                        nullptr, nullptr, nullptr, 0ULL, cnt);
     CORRO_HIP_TRY(hipGetLastError());
-    uint64_t h[2] = {0, 0};
-    CORRO_HIP_TRY(hipMemcpyAsync(h, cnt, 16, hipMemcpyDeviceToHost, s));
+    uint64_t h[4] = {0, 0, 0, 0};
+    CORRO_HIP_TRY(hipMemcpyAsync(h, cnt, 32, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     if (!h[0]) return CORRO_OK;
+    if (h[3] && ctx->aff_policy == CORRO_AFF_POLICY_PORTABLE)
+        return fail(CORRO_E_RANGE, std::to_string(h[3]) + " change(s) need a column-affinity conversion whose result "
+                                   "depends on the SQLite version (TEXT <-> REAL rounding): refused under "
+                                   "CORRO_AFF_POLICY_PORTABLE (corro_set_affinity_policy)");
     // 20 bytes per change of the batch: cv0 | cv1 | cmeta
     AFF_TRY(ctx->d_aff_vals.ensure(n * 20));
     uint64_t *cv0 = ctx->d_aff_vals.as<uint64_t>(), *cv1 = cv0 + n;
@@ -629,5 +687,13 @@ extern "C" int corro_table_set_affinity(corro_ctx *ctx, uint32_t table, const ui
     if (int rc = ctx->d_affflag.ensure(64)) return rc;
     CORRO_HIP_TRY(hipMemcpy(ctx->d_aff.p, ctx->aff.data(), ctx->aff.size(), hipMemcpyHostToDevice));
     ctx->aff_any = any;
+    return CORRO_OK;
+}
+
+extern "C" int corro_set_affinity_policy(corro_ctx *ctx, int policy) {
+    if (!ctx) return fail(CORRO_E_INVALID, "NULL argument");
+    if (policy != CORRO_AFF_POLICY_PORTABLE && policy != CORRO_AFF_POLICY_SQLITE_3_37_2)
+        return fail(CORRO_E_INVALID, "unknown affinity policy");
+    ctx->aff_policy = policy;
     return CORRO_OK;
 }

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <exception>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
@@ -210,8 +211,15 @@ class HostPool {
         return *p;
     }
     unsigned threads() const { return cap_; }
-    // fn(arg, k) for k in [0, n) on up to nth threads (the caller is one of them)
+    // fn(arg, k) for k in [0, n) on up to nth threads (the caller is one of them). Exception-safe:
+    // an exception thrown by fn (on the caller or a worker) stops further indices from starting, the
+    // call still waits for every worker that joined, then rethrows the first one on the caller.
+    // A nested call (fn itself calling run) runs serially on the calling thread.
     void run(size_t n, unsigned nth, void (*fn)(void *, size_t), void *arg) {
+        if (in_pool_) {
+            for (size_t k = 0; k < n; k++) fn(arg, k);
+            return;
+        }
         std::lock_guard<std::mutex> one(job_mu_);
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -222,6 +230,7 @@ class HostPool {
             want_ = nth - 1;
             joined_ = 0;
             done_ = 0;
+            err_ = nullptr;
             gen_++;
         }
         cv_.notify_all();
@@ -229,6 +238,12 @@ class HostPool {
         std::unique_lock<std::mutex> g(mu_);
         want_ = 0;  // no worker joins this job any more; wait for the ones that did
         done_cv_.wait(g, [&] { return done_ == joined_; });
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            g.unlock();
+            std::rethrow_exception(e);
+        }
     }
 
   private:
@@ -240,7 +255,15 @@ class HostPool {
         for (unsigned t = 1; t < cap_; t++) std::thread([this] { loop(); }).detach();
     }
     void work(void (*fn)(void *, size_t), void *arg, size_t n) {
-        for (size_t k; (k = next_.fetch_add(1, std::memory_order_relaxed)) < n;) fn(arg, k);
+        in_pool_ = true;
+        try {
+            for (size_t k; (k = next_.fetch_add(1, std::memory_order_relaxed)) < n;) fn(arg, k);
+        } catch (...) {
+            next_.store(n, std::memory_order_relaxed);  // no further index starts
+            std::lock_guard<std::mutex> g(mu_);
+            if (!err_) err_ = std::current_exception();
+        }
+        in_pool_ = false;
     }
     void loop() {
         uint64_t seen = 0;
@@ -269,7 +292,10 @@ class HostPool {
     std::atomic<size_t> next_{0};
     unsigned want_ = 0, joined_ = 0, done_ = 0;
     uint64_t gen_ = 0;
+    std::exception_ptr err_;
+    static thread_local bool in_pool_;
 };
+thread_local bool HostPool::in_pool_ = false;
 
 // f(0) .. f(n - 1) on up to CORRO_HOST_THREADS (default: min(16, hardware)) host threads, at least
 // `per` indices per thread (serial for small n). f must only touch state of its own index.
@@ -699,10 +725,9 @@ int process_staged_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changes
 
 }  // namespace
 
-extern "C" {
-
-int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
-                                   const corro_changes *in, int mem, corro_process_out *out) {
+namespace {
+int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
+                             const corro_changes *in, int mem, corro_process_out *out) {
     if (!ctx || !bk || (ncs && !cs) || !out) return fail(CORRO_E_INVALID, "NULL argument");
     if (ncs && (!out->known)) return fail(CORRO_E_INVALID, "out->known is required");
     if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE && mem != CORRO_MEM_DEVICE_HEADERS)
@@ -1055,6 +1080,26 @@ int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro
     if (prof) fprintf(stderr, "[corro agent] ncs=%llu spans=%llu changes=%llu ms:%s\n", (unsigned long long)ncs,
                       (unsigned long long)nspans, (unsigned long long)nb, prof_line.c_str());
     return CORRO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// The C ABI never lets a C++ exception out (a host allocation failing inside the header walks or the
+// host pool's workers): std::bad_alloc is CORRO_E_NOMEM, anything else CORRO_E_INVALID. A failure
+// that late leaves the call uncommitted (the caller's transaction rolls back).
+int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
+                                   const corro_changes *in, int mem, corro_process_out *out) {
+    try {
+        return process_multiple_changes(ctx, bk, cs, ncs, in, mem, out);
+    } catch (const std::bad_alloc &) {
+        return fail(CORRO_E_NOMEM, "host allocation failed in process_multiple_changes");
+    } catch (const std::exception &e) {
+        return fail(CORRO_E_INVALID, std::string("process_multiple_changes: ") + e.what());
+    } catch (...) {
+        return fail(CORRO_E_INVALID, "process_multiple_changes: unknown host exception");
+    }
 }
 
 int corro_bookie_take_ready(corro_bookie *bk, uint8_t *actors, uint64_t *versions, uint64_t cap, uint64_t *count) {

@@ -201,6 +201,7 @@ struct corro_ctx {
     corro::DevBuf d_aff_conv, d_aff_vals;
     corro::DevBuf d_gaps_big;              // corro_booked_insert_db_batch: counter + long-actor list  // per change of a batch: converted flag; cv0 | cv1 | cmeta
     bool aff_any = false;         // some column has an affinity other than BLOB
+    int aff_policy = CORRO_AFF_POLICY_PORTABLE;  // corro_set_affinity_policy
     corro::DevBuf d_part;         // partition counts
     corro::DevBuf d_pkdir;        // PkDir per table (pk_mirror_sync)
     corro::DevBuf d_part_var;     // partition_var scratch: per-record var lengths / offsets, perm

@@ -669,6 +669,8 @@ __device__ inline uint32_t ovf_row_slot(const MergeArgs &a, const OvfDev &d, uin
     hb = d.rheap[row];
     if (hb != ROW_NONE) return rs_lookup(a.rs, bb, d.pk[own], t);
     hb = d.rprior[row];  // (k_ovf_walk allocated it, one heap request per wave)
+    if (hb == ROW_NONE)  // a new row of the sequential fold: its records now that it emits (the host made room)
+        hb = (uint32_t)atomicAdd(a.rs.heap_top, (unsigned long long)a.rs.stride[t]);
     const uint64_t z[2] = {0, 0};
     return rs_insert(a.rs, bb, d.pk[own], t, hb, z);
 }
@@ -760,9 +762,12 @@ static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeAr
     // one thread per row (dense ids), every lane busy; wave-uniform loop for the heap requests
     for (uint32_t r0 = blockIdx.x * blockDim.x + threadIdx.x - lane; r0 < d.nrows; r0 += stride) {
         const uint32_t row = r0 + lane;
-        {  // the wave's new rows take their heap records in one request (the host made room)
+        {  // the wave's new rows take their heap records in one request (the host made room). Rows of
+           // the sequential fold (rbad) may emit nothing: they allocate only when they emit.
             uint32_t need = 0;
-            if (row < d.nrows && d.rheap[row] == ROW_NONE) need = a.rs.stride[d.tc[d.rowner[row]] >> 16];
+            const bool fresh = row < d.nrows && d.rheap[row] == ROW_NONE;
+            if (fresh && !d.rbad[row]) need = a.rs.stride[d.tc[d.rowner[row]] >> 16];
+            else if (fresh) d.rprior[row] = ROW_NONE;
             uint32_t incl = need;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {

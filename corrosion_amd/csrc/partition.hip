@@ -236,8 +236,10 @@ __global__ void k_unpack(const void *__restrict__ recs, uint32_t n, BatchOut o) 
 // ---- every table: interned pks routed by their canonical bytes, variable-length bytes shipped ----
 // Owner of a change: INTEGER-pk rows by rank_of (the pk is the row key on every engine); rows of an
 // interned table by the route hash of their canonical packed pk (the dense row key is per engine).
-__device__ inline uint32_t route_of(const PkDir *dir, uint32_t table, uint64_t key, uint32_t nranks) {
-    if (dir && dir[table].interned) {
+// A table id at or past ntables (not registered: the receiving merge rejects it) is routed like an
+// INTEGER pk and never dereferences the directory.
+__device__ inline uint32_t route_of(const PkDir *dir, uint32_t ntables, uint32_t table, uint64_t key, uint32_t nranks) {
+    if (dir && table < ntables && dir[table].interned) {
         const uint64_t h = key < dir[table].n ? dir[table].hash[key] : 0ULL;
         return (uint32_t)(mix64(h ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(table + 1))) & 0xFFFFFFFFULL) % nranks;
     }
@@ -245,22 +247,23 @@ __device__ inline uint32_t route_of(const PkDir *dir, uint32_t table, uint64_t k
 }
 
 __global__ void __launch_bounds__(PART_THREADS)
-k_partv_count(BatchDev in, const PkDir *dir, uint32_t tile, uint32_t nranks, uint32_t *__restrict__ counts) {
+k_partv_count(BatchDev in, const PkDir *dir, uint32_t ntables, uint32_t tile, uint32_t nranks, uint32_t *__restrict__ counts) {
     __shared__ uint32_t c[PART_MAX_RANKS];
     for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) c[r] = 0;
     __syncthreads();
     const uint32_t begin = blockIdx.x * tile, end = min(in.n, begin + tile);
     for (uint32_t i = begin + threadIdx.x; i < end; i += blockDim.x)
-        atomicAdd(&c[route_of(dir, in.tcid[i] >> 16, in.pk[i], nranks)], 1u);
+        atomicAdd(&c[route_of(dir, ntables, in.tcid[i] >> 16, in.pk[i], nranks)], 1u);
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < nranks; r += blockDim.x) counts[(size_t)blockIdx.x * nranks + r] = c[r];
 }
 
 // bytes change i ships: its canonical pk (interned table) then its long value's bytes
-__device__ inline void var_parts(const BatchDev &in, const PkDir *dir, uint32_t i, uint32_t &pk_len, uint32_t &vsz) {
+__device__ inline void var_parts(const BatchDev &in, const PkDir *dir, uint32_t ntables, uint32_t i, uint32_t &pk_len,
+                                 uint32_t &vsz) {
     const uint32_t t = in.tcid[i] >> 16;
     pk_len = 0;
-    if (dir[t].interned && in.pk[i] < dir[t].n) pk_len = (uint32_t)(dir[t].off[in.pk[i] + 1] - dir[t].off[in.pk[i]]);
+    if (t < ntables && dir[t].interned && in.pk[i] < dir[t].n) pk_len = (uint32_t)(dir[t].off[in.pk[i] + 1] - dir[t].off[in.pk[i]]);
     vsz = 0;
     if (in.voff && in.vsz && in.vt && in.vl && in.vl[i] == CORRO_VAL_LONG && (in.vt[i] == CORRO_TEXT || in.vt[i] == CORRO_BLOB)) {
         const uint64_t off = in.voff[i];
@@ -271,7 +274,7 @@ __device__ inline void var_parts(const BatchDev &in, const PkDir *dir, uint32_t 
 
 // stable scatter of 80-B records (route_of), perm[pos] = source, vlen[pos] = bytes it ships
 __global__ void __launch_bounds__(PART_THREADS)
-k_partv_pack(BatchDev in, const PkDir *dir, uint32_t tile, uint32_t nranks, const uint32_t *__restrict__ offs,
+k_partv_pack(BatchDev in, const PkDir *dir, uint32_t ntables, uint32_t tile, uint32_t nranks, const uint32_t *__restrict__ offs,
              PackedRec80 *__restrict__ out, uint32_t *__restrict__ perm, uint32_t *__restrict__ vlen) {
     __shared__ uint32_t run[PART_MAX_RANKS];
     __shared__ uint32_t wcnt[PART_THREADS / 64][PART_MAX_RANKS];
@@ -286,7 +289,7 @@ k_partv_pack(BatchDev in, const PkDir *dir, uint32_t tile, uint32_t nranks, cons
         const uint32_t ic = act ? i : begin;
         const uint64_t pk = in.pk[ic];
         const uint32_t tc = in.tcid[ic];
-        const uint32_t d = act ? route_of(dir, tc >> 16, pk, nranks) : 0xFFFFFFFFu;
+        const uint32_t d = act ? route_of(dir, ntables, tc >> 16, pk, nranks) : 0xFFFFFFFFu;
         uint32_t my_rank = 0;
         for (uint32_t r = 0; r < nranks; r++) {
             const uint64_t m = __ballot(d == r);
@@ -310,7 +313,7 @@ k_partv_pack(BatchDev in, const PkDir *dir, uint32_t tile, uint32_t nranks, cons
             r.site = in.site[i];
             r.meta = (in.vt ? (uint32_t)in.vt[i] : (uint32_t)CORRO_INTEGER) | ((in.vl ? (uint32_t)in.vl[i] : 0u) << 8);
             uint32_t pl, vs;
-            var_parts(in, dir, i, pl, vs);
+            var_parts(in, dir, ntables, i, pl, vs);
             r.pad[1] = pl;
             r.pad[2] = vs;
             out[pos] = r;
@@ -545,10 +548,11 @@ extern "C" int corro_partition_var(corro_ctx *ctx, const corro_changes *in, uint
     bd.lbase = 0;
     bd.ldata = in->val_data_len;
     const PkDir *dir = ctx->d_pkdir.as<PkDir>();
+    const uint32_t ntables = (uint32_t)ctx->tables.size();
     uint32_t ntiles, tile, *d_counts;
     uint64_t *d_tot;
     if (int rc = part_tiles(ctx, n, nranks, ntiles, tile, d_counts, d_tot)) return rc;
-    hipLaunchKernelGGL(k_partv_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, dir, tile, nranks, d_counts);
+    hipLaunchKernelGGL(k_partv_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, dir, ntables, tile, nranks, d_counts);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, d_tot);
     // scratch: perm (caller's or ours), vlen, vincl, rocPRIM temp, segment / record bases
     size_t temp = 0;
@@ -561,7 +565,7 @@ extern "C" int corro_partition_var(corro_ctx *ctx, const corro_changes *in, uint
     void *tmp = sp + 3 * col;
     uint64_t *d_seg = reinterpret_cast<uint64_t *>(sp + 3 * col + ((temp + 255) & ~(size_t)255));
     uint64_t *d_recb = d_seg + 64;
-    hipLaunchKernelGGL(k_partv_pack, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, dir, tile, nranks, d_counts,
+    hipLaunchKernelGGL(k_partv_pack, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, dir, ntables, tile, nranks, d_counts,
                        static_cast<PackedRec80 *>(out), d_perm, vlen);
     CORRO_HIP_TRY(hipGetLastError());
     TRY_PART(prim_inclusive_scan_u32(tmp, &temp, vlen, vincl, n, s));

@@ -178,8 +178,8 @@ int pk_mirror_sync(corro_ctx *ctx) {
         d.n = pt.dev_n;
     }
     if (int rc = ctx->d_pkdir.ensure(std::max<size_t>(dir.size(), 1) * sizeof(PkDir))) return rc;
-    if (!dir.empty())
-        CORRO_HIP_TRY(hipMemcpyAsync(ctx->d_pkdir.p, dir.data(), dir.size() * sizeof(PkDir), hipMemcpyHostToDevice, s));
+    if (dir.empty()) dir.push_back(PkDir{});  // (no table: one zeroed entry, never an uninitialised one)
+    CORRO_HIP_TRY(hipMemcpyAsync(ctx->d_pkdir.p, dir.data(), dir.size() * sizeof(PkDir), hipMemcpyHostToDevice, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;
 }

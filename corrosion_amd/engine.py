@@ -132,6 +132,15 @@ class MergeEngine:
         aff = np.array([L.lib().corro_affinity_of_type(str(d).encode()) for d in decl_types], np.uint8)
         L.check(L.lib().corro_table_set_affinity(self._h, t, aff.ctypes.data if len(aff) else None, len(aff)))
 
+    AFFINITY_POLICIES = {"portable": 0, "sqlite-3.37.2": 1}
+
+    def set_affinity_policy(self, policy):
+        """"portable" (default): convert only values whose stored form is the same in every SQLite
+        version with correctly rounded conversions, refuse a batch holding any other (CorroError,
+        CORRO_E_RANGE, before any write). "sqlite-3.37.2": convert every value exactly as SQLite 3.37.2
+        does (corro_set_affinity_policy)."""
+        L.check(L.lib().corro_set_affinity_policy(self._h, self.AFFINITY_POLICIES[policy]))
+
     def pk_keys(self, table, packed):
         """Row keys of packed pks (a list of bytes, pack_columns encoding) of one table."""
         t = self.table_index(table)

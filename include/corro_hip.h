@@ -195,6 +195,14 @@ enum { CORRO_AFF_BLOB = 0, CORRO_AFF_TEXT = 1, CORRO_AFF_NUMERIC = 2, CORRO_AFF_
 int corro_affinity_of_type(const char *decl_type);
 /* aff[c - 1] = affinity of cid c, ncols = the table's column count. */
 int corro_table_set_affinity(corro_ctx *ctx, uint32_t table, const uint8_t *aff, uint32_t ncols);
+/* Which conversions the engine performs. The reference bundles a newer SQLite (libsqlite3-sys 0.31.0,
+ * Cargo.lock:2444) than the 3.37.2 whose conversion routines the engine emulates, and newer SQLite
+ * rewrote TEXT -> REAL (sqlite3AtoF) and REAL -> TEXT rounding. PORTABLE (the default) converts
+ * only values every correctly rounded implementation stores identically and fails a batch holding
+ * any other conversion with CORRO_E_RANGE before it writes (affinity.hip states the rules);
+ * SQLITE_3_37_2 converts every value exactly as SQLite 3.37.2 does. */
+enum { CORRO_AFF_POLICY_PORTABLE = 0, CORRO_AFF_POLICY_SQLITE_3_37_2 = 1 };
+int corro_set_affinity_policy(corro_ctx *ctx, int policy);
 
 /* ------------------------------------------------------------------ merge */
 

@@ -13,9 +13,14 @@ Follows /root/reference/crates/corro-agent/src/agent/util.rs:
              last_rows_impacted restarts at 0 per version
   :894-932   gap bookkeeping of every processed version range (insert_db, agent.rs:1108-1235)
 over the oracle's own restatements: the merge fold (crsql_fold.c, pinned by the cr-sqlite KATs) and
-the RangeInclusiveSet gap bookkeeping (ranges.c, pinned by agent.rs:1605-1868). Scope: Full / Empty
-changesets (EmptySet's dummy versions are not exercised), calls that commit (no UNIQUE-constraint
-rollback), changes given as engine-encoded fields.
+the RangeInclusiveSet gap bookkeeping (ranges.c, pinned by agent.rs:1605-1868). Scope: Full, Empty
+and EmptySet changesets, calls that commit (no UNIQUE-constraint rollback), changes given as
+engine-encoded fields. EmptySet reports the dummy range 0..=0 (broadcast.rs:176), is complete and
+empty (:218, :236) and has no seqs (:201); BookedVersions::contains_version(0) holds for every actor
+(max.unwrap_or_default() >= 0 and no gap holds 0, agent.rs:1353-1361), so pass 1's contains_all
+(util.rs:724-733) always skips it: an EmptySet is never processed (known "skipped", no
+crsql_set_db_version, no gap bookkeeping). The restatement keeps the reference's full control flow
+for it anyway, so a bookkeeping state with 0 in a gap would process it as the reference does.
 """
 from . import oracle as O
 
@@ -75,7 +80,7 @@ class ActorBook:
     def contains_all(self, s, e, seqs):
         if s > e:
             return True
-        mx = self.max() or 0
+        mx = self.max() or 0  # max.unwrap_or_default() (agent.rs:1353-1361)
         if e > mx:
             return False
         if any(not (b < s or a > e) for a, b in self.gaps.needed()):
@@ -86,7 +91,8 @@ class ActorBook:
 
 
 class Changeset:
-    """One ChangeV1: kind 'full' (version, seqs, last_seq, ts, rows) or 'empty' (versions)."""
+    """One ChangeV1: kind 'full' (version, seqs, last_seq, ts, rows), 'empty' (versions) or 'empty_set'
+    (versions: the list of ranges it carries; only its dummy 0..=0 takes part in the apply)."""
 
     def __init__(self, actor, kind, version=None, versions=None, seqs=None, last_seq=None, ts=0, rows=()):
         self.actor, self.kind, self.ts = bytes(actor), kind, ts
@@ -94,6 +100,8 @@ class Changeset:
         self.rows = list(rows)  # dicts of engine fields: pk, table_cid, col_version, db_version, cl, seq, site, val0
 
     def vrange(self):
+        if self.kind == "empty_set":
+            return (0, 0)  # Changeset::versions() dummy (broadcast.rs:176)
         return (self.version, self.version) if self.kind == "full" else tuple(self.versions)
 
     def complete(self):

@@ -39,11 +39,13 @@ def _batch(rows, cv=None, site=None):
     return out
 
 
-def _engine(nsites=2):
+def _engine(nsites=2, policy="sqlite-3.37.2"):
+    """the fixtures pin SQLite 3.37.2's conversions: those tests ask for that policy explicitly"""
     sites = synth.site_ids(nsites, 3)
     e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 16)
     e.register_sites(sites)
     e.set_column_types("t", TYPES)
+    e.set_affinity_policy(policy)
     f = O.Fold(sites)
     f.set_affinity(0, AFF_OF_CID)
     return e, f
@@ -181,3 +183,150 @@ def test_long_numeric_text_converted():
     assert got[(1, 1)] == 1.2345678901234567e+19 and got[(2, 3)] == "-123456789012345678"
     assert got[(3, 3)] == "-1.2345678901234e-300" and got[(4, 2)] == 1.2345678901234567e+19
     assert sorted(rows_to_tuples(e.export())) == sorted(rows_to_tuples(f.export()))
+
+
+# ---- the portable policy (default): only version-independent conversions ------------------------
+def _sqlite_15g(x):
+    """SQLite's "%!.15g" from a correctly rounded '%.15g' (Python's): '.0' when no point, exponent
+    with at least two digits (Python's already has them)"""
+    s = "%.15g" % x
+    m, _, ex = s.partition("e")
+    if "." not in m and m not in ("inf", "-inf"):
+        m += ".0"
+    return m + ("e" + ex if ex else "")
+
+
+def _correct(aff, v):
+    """the value a correctly rounded SQLite stores for v under affinity aff (the conversions the
+    portable policy performs), or the marker None when v stays as it is"""
+    if aff == "BLOB":
+        return None
+    if aff == "TEXT":
+        if isinstance(v, bool) or not isinstance(v, (int, float)):
+            return None
+        return str(v) if isinstance(v, int) else _sqlite_15g(v)
+    if isinstance(v, str):
+        import re
+        if not re.fullmatch(r"\s*[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?\s*", v):
+            return None  # not a number to SQLite (Python's float() also takes 'inf', '1_0', ...)
+        r = float(v.strip())
+        t = v.strip().lstrip("+-")
+        if t.isdigit() and -(1 << 63) <= int(v) < (1 << 63):
+            r = int(v)
+        elif r.is_integer() and -(2.0 ** 63) < r < 2.0 ** 63:
+            r = int(r)
+    elif isinstance(v, float):
+        r = int(v) if v.is_integer() and -(2.0 ** 63) < v < 2.0 ** 63 else v
+    elif isinstance(v, int):
+        r = v
+    else:
+        return None
+    if aff == "REAL" and isinstance(r, int):
+        r = float(r)
+    return r
+
+
+def _real_text_sensitive(v):
+    """a REAL whose '%!.15g' text may differ between SQLite versions: -0.0, infinities, magnitudes
+    past 1e307 or below 1e-307 (their text re-reads through the scaled path), or a 15-digit text
+    that is another double"""
+    return str(v) in ("-0.0", "inf", "-inf") or (v != 0 and not 1e-307 < abs(v) < 1e307) or \
+        float(_sqlite_15g(v)) != v
+
+
+def _text_real_sensitive(v):
+    """a decimal text whose double may differ between SQLite versions: more than 15 significant
+    digits, an extreme magnitude, or an exact value within 2^-50 (relative) of a double rounding midpoint"""
+    import math
+    from fractions import Fraction
+    t = v.strip()
+    mant = t.lstrip("+-").lower().split("e")[0].replace(".", "").lstrip("0").rstrip("0")
+    if len(mant) > 15:
+        return True
+    x = Fraction(t)
+    if x == 0:
+        return False
+    try:
+        d = float(x)
+    except OverflowError:
+        return True
+    if math.isinf(d) or abs(d) < 2.2250738585072014e-308 or abs(d) > 1e300:
+        return True
+    nb = math.nextafter(d, math.inf if Fraction(d) < x else -math.inf)
+    mid = (Fraction(d) + Fraction(nb)) / 2
+    return abs(x - mid) / abs(x) < Fraction(1, 1 << 50)
+
+
+def _one(e, cid, v):
+    """apply one change; the stored value, or the string 'refused'"""
+    e.reset()
+    try:
+        e.apply(_batch([(1, cid, v)]))
+    except ca.CorroError as err:
+        assert err.code == -6 and "SQLite version" in str(err)
+        return "refused"
+    return _stored(e.export()).get((1, cid))
+
+
+def test_portable_policy_converts_only_version_independent_values():
+    """Every fixture case under the default policy: either refused as a whole batch (CORRO_E_RANGE,
+    nothing written), or stored exactly as SQLite 3.37.2 stores it (the fixture) AND as a correctly
+    rounded conversion stores it (Python's float() / '%.15g'). A refusal is only allowed where the
+    15-digit rendering does not round-trip (REAL -> TEXT) or the decimal needs more than 15 digits or
+    an extreme exponent (TEXT -> REAL)."""
+    d = json.load(open(os.path.join(HERE, "golden", "affinity_kats.json")))
+    e, _ = _engine(policy="portable")
+    refused = converted = 0
+    for c in d["cases"]:
+        aff, v, want = c["affinity"], _decode(c["in"]), _decode(c["out"])
+        got = _one(e, CID_OF_AFF[aff], v)
+        if got == "refused":
+            refused += 1
+            if aff == "TEXT":
+                assert isinstance(v, float) and _real_text_sensitive(v), (aff, v)
+            else:
+                assert isinstance(v, str) and _text_real_sensitive(v), (aff, v)
+            continue
+        converted += 1
+        assert _key(got) == _key(want), (aff, v, got, want)
+        cr = _correct(aff, v)
+        if cr is not None:
+            assert _key(got) == _key(cr), (aff, v, got, cr)
+    assert converted > 450 and refused > 0
+
+
+@pytest.mark.parametrize("aff,v,refuse", [
+    ("TEXT", 0.1 + 0.2, True),             # '%!.15g' -> '0.3', which is another double
+    ("TEXT", 0.5, False),
+    ("TEXT", -0.0, True),                  # 3.37.2 writes '0.0'
+    ("TEXT", -2.25, False),
+    ("TEXT", 1e20, False),                 # '1.0e+20'
+    ("TEXT", 1 / 3, True),
+    ("REAL", "0.1000000000000000055511151231257827021181583404541015625", True),  # dropped digits
+    ("REAL", "1e400", True),               # overflow
+    ("REAL", "4.9e-324", True),            # subnormal
+    ("REAL", "2.5", False),
+    ("NUMERIC", " 12.0 ", False),          # INTEGER 12
+    ("INTEGER", "9007199254740993", False),  # integer text: exact
+    ("REAL", "9007199254740993", False),   # int64 -> double: correctly rounded in every version
+    ("NUMERIC", "9007199254740993.0", False),  # an integer after the '.0' is stripped: (double)s
+    ("REAL", "1.000000000000000111", True),  # 19 digits, within the long double's margin of 1 + 2^-53
+])
+def test_portable_policy_known_cases(aff, v, refuse):
+    e, _ = _engine(policy="portable")
+    got = _one(e, CID_OF_AFF[aff], v)
+    assert (got == "refused") == refuse, (aff, v, got)
+    if not refuse:
+        cr = _correct(aff, v)
+        assert _key(got) == _key(cr), (aff, v, got, cr)
+    e37, _ = _engine()
+    assert _one(e37, CID_OF_AFF[aff], v) != "refused"
+
+
+def test_portable_refusal_writes_nothing():
+    e, _ = _engine(policy="portable")
+    e.apply(_batch([(1, 1, 5)]))
+    before = sorted(rows_to_tuples(e.export()))
+    with pytest.raises(ca.CorroError):
+        e.apply(_batch([(2, 2, 7), (3, 3, 0.1 + 0.2)]))
+    assert sorted(rows_to_tuples(e.export())) == before

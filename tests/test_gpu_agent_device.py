@@ -20,7 +20,7 @@ SCHEMA = {"t": ["a", "b", "c", "d"], "u": ["x", "y"]}
 NACT = 5
 
 
-def _calls(seed, ncalls=6, per_call=40, clean=()):
+def _calls(seed, ncalls=6, per_call=40, clean=(), empty_sets=0.0):
     """Random calls; actors in `clean` never re-send, never send partial or Empty versions (each of
     their calls is a run of complete Full versions ascending, gaps and empty Full versions allowed:
     the device-header path decides them without the host)."""
@@ -108,6 +108,15 @@ def _calls(seed, ncalls=6, per_call=40, clean=()):
         calls.append(call)
     if held:
         calls.append(held)
+    if empty_sets:  # Changeset::EmptySet from random actors, at random places (own rng: seeds keep their calls)
+        erng = np.random.default_rng(seed + 1000)
+        for call in calls:
+            for _k in range(int(erng.binomial(len(call), empty_sets))):
+                a = int(erng.integers(0, NACT))
+                v0 = int(erng.integers(1, 50))
+                cs = Changeset(ids[a], "empty_set", versions=[(v0, v0 + int(erng.integers(0, 4)))],
+                               ts=int(erng.integers(1, 1 << 40)))
+                call.insert(int(erng.integers(0, len(call) + 1)), cs)
     return ids, calls
 
 
@@ -156,9 +165,11 @@ def _run(eng, bk, ordinal, call, device, order=None):
             d.seq_start, d.seq_end = c.seqs
             d.last_seq = c.last_seq
             d.change_off, d.change_count = off[i], len(c.rows)
-        else:
+        elif c.kind == "empty":
             d.kind = L.CORRO_CS_EMPTY
             d.version_start, d.version_end = c.versions
+        else:
+            d.kind = L.CORRO_CS_EMPTY_SET  # (its ranges travel beside the header; unused by the apply)
     known = np.zeros(max(1, len(call)), np.int32)
     if device:
         imp = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
@@ -191,10 +202,12 @@ def canon_rows(rows):
     return sorted(zip(*[np.asarray(rows[k]).tolist() for k in keys]))
 
 
-def _check_against_oracle(seed, device, order_fn=None, clean=()):
+def _check_against_oracle(seed, device, order_fn=None, clean=(), empty_sets=0.0):
     import corrosion_amd as ca
     from oracle.agent import AgentOracle
-    ids, calls = _calls(seed, clean=clean)
+    ids, calls = _calls(seed, clean=clean, empty_sets=empty_sets)
+    if empty_sets:
+        assert any(c.kind == "empty_set" for call in calls for c in call)
     eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12)
     ords = eng.register_sites(ids)
     ordinal = {bytes(ids[k]): int(ords[k]) for k in range(NACT)}
@@ -258,6 +271,15 @@ def test_device_headers_fast_actors_match_restatement(seed, clean):
     """actors decided on the device (complete Full versions ascending, gaps, empty Full versions,
     unknown names) next to slow ones, in one call"""
     _check_against_oracle(seed, device="headers", clean=clean)
+
+
+@pytest.mark.parametrize("device,clean", [(True, ()), (False, ()), ("headers", ()), ("headers", (0, 1, 2))])
+def test_empty_set_changesets_match_restatement(device, clean):
+    """Changeset::EmptySet (broadcast.rs:114-148) mixed into random calls: its versions() is the dummy
+    0..=0 (:176), which contains_all always holds, so process_multiple_changes skips it in pass 1
+    (util.rs:724-733): known = skipped, no crsql_set_db_version, no gap rows -- on every header path,
+    next to fast and slow actors"""
+    _check_against_oracle(21, device=device, clean=clean, empty_sets=0.1)
 
 
 def test_device_headers_fast_gather_path(monkeypatch):

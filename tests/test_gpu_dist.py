@@ -195,3 +195,34 @@ def test_two_rank_every_table_with_long_values(tmp_path):
     assert sorted(got, key=repr) == want
     got_imp = np.concatenate([np.load(tmp_path / f"vimp{r}.npy") for r in range(world)])
     assert np.array_equal(got_imp, want_imp)
+
+
+def test_partition_var_routes_unregistered_table_ids():
+    """A change naming a table id past the schema goes through the every-table partition without
+    touching the pk directory: routed like an INTEGER pk (rank_of), its record shipped unchanged, and
+    refused by the owner's merge (cr-sqlite: no such table). Engines with interned tables and with
+    none are both covered."""
+    import torch
+    import corrosion_amd as ca
+    from corrosion_amd.dist import rank_of_np
+    from tests.test_gpu_pk import INTERNED, SCHEMA
+    for schema, interned in ((SCHEMA, INTERNED), ({"t": ["a"]}, ())):
+        eng = ca.MergeEngine(schema, capacity_hint=1024, device=0, interned=interned)
+        eng.register_sites(synth.site_ids(4, 3))
+        n = 512
+        bad_table = len(schema) + 7
+        b = {"pk": np.arange(n, dtype=np.uint64) * 977,
+             "table_cid": np.full(n, (bad_table << 16) | 1, np.uint32),
+             "col_version": np.ones(n, np.int64), "db_version": np.ones(n, np.int64),
+             "site": np.zeros(n, np.uint32), "cl": np.ones(n, np.uint32), "seq": np.zeros(n, np.uint32),
+             "val0": np.arange(n, dtype=np.uint64)}
+        dev = _to_dev(b)
+        recs, var, counts, vcounts, perm = eng.partition_var(dev, 3, with_perm=True)
+        torch.cuda.synchronize()
+        want = np.bincount(rank_of_np(b["table_cid"], b["pk"], 3), minlength=3)
+        assert counts == [int(c) for c in want] and vcounts == [0, 0, 0]
+        got = eng.unpack_var(recs, var, counts, vcounts)
+        assert np.array_equal(np.sort(got["pk"].cpu().numpy().view(np.uint64)), np.sort(b["pk"]))
+        with pytest.raises(ca.CorroError):
+            eng.apply(got)
+        eng.close()

@@ -188,3 +188,21 @@ def test_oracle_long_values_lww_order():
     s = O.ShardedFold(site_table(4), nshards=4, nthreads=2)
     s.apply(b)
     assert s.digest() == O.rows_digest(rows)
+
+
+def test_agent_oracle_empty_set_is_skipped():
+    """Changeset::EmptySet through the process_multiple_changes restatement: versions() = 0..=0
+    (broadcast.rs:176), contains_version(0) holds with or without a max (agent.rs:1353-1361), so pass
+    1 skips it (util.rs:724-733) -- for a fresh actor and for one with bookkeeping alike."""
+    import synth
+    from oracle.agent import AgentOracle, Changeset
+    ids = synth.site_ids(2, 9)
+    ref = AgentOracle(ids)
+    es = Changeset(ids[0], "empty_set", versions=[(3, 5)], ts=7)
+    assert ref.process([es]) == (["skipped"], [[]])
+    assert ref.last(bytes(ids[0])) is None and not ref.set_dbv
+    full = Changeset(ids[1], "full", version=2, seqs=(0, 0), last_seq=0, ts=1,
+                     rows=[dict(pk=1, table_cid=1, col_version=1, db_version=2, cl=1, seq=0, site=1, val0=5)])
+    known, _ = ref.process([full, Changeset(ids[1], "empty_set", versions=[(1, 1)])])
+    assert known == ["current", "skipped"]
+    assert ref.last(bytes(ids[1])) == 2 and ref.needed(bytes(ids[1])) == [(1, 1)]

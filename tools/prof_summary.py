@@ -1,4 +1,4 @@
-"""Summarise a gpurun_out/prof directory (scripts/gpu_prof.sh) into a markdown table:
+"""Summarise a gpurun_out/prof directory (scripts/gpu.sh) into a markdown table:
 per-kernel average duration (rocprofv3 --kernel-trace --stats) and HBM traffic per dispatch from
 the separate --pmc passes: 2 x FETCH_SIZE (gfx950 reports half of wide coalesced reads,
 MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KiB.
