@@ -486,6 +486,110 @@ def agent_e2e(eng, batch, n, agent_ms=None, reps=3):
                     f"{reps}"}
 
 
+def agent_e2e_mixed(eng, batch, n, fast_ms=None, reps=3, resend=0.10, partial=0.05, empty=0.05, seed=5):
+    """agent_e2e's call with the slow cases the reference routes through its per-actor checks
+    (util.rs:704-884): ~10 % of the versions re-sent later in the same call (pass 1's seen set skips
+    them), ~5 % arriving as two partial halves (incomplete: buffered, process_incomplete_version
+    util.rs:1053-1186), ~5 % as Empty versions (cleared, crsql_set_db_version when past the max).
+    Same changes in HBM, headers in HBM (CORRO_MEM_DEVICE_HEADERS), fresh Bookie and empty state per
+    rep; median of `reps`. Reported beside the all-fast figure (ratio_vs_fast)."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import synth
+    import corrosion_amd as ca
+    from corrosion_amd import _lib as L
+    rng = np.random.default_rng(seed)
+    per_actor = -(-n // N_ACTORS)
+    ids = np.ascontiguousarray(synth.site_ids(N_ACTORS, 1), dtype=np.uint8)
+    cs_dt = np.dtype([("actor_id", "<u8"), ("site", "<u4"), ("kind", "<u4"), ("version_start", "<u8"),
+                      ("version_end", "<u8"), ("seq_start", "<u8"), ("seq_end", "<u8"), ("last_seq", "<u8"),
+                      ("ts", "<u8"), ("change_off", "<u8"), ("change_count", "<u8")])
+    a_idx, v_idx = [], []
+    for a in range(N_ACTORS):
+        lo, hi = a * per_actor, min(n, (a + 1) * per_actor)
+        nv = max(0, -(-(hi - lo) // 64))
+        a_idx.append(np.full(nv, a, np.int64))
+        v_idx.append(np.arange(nv, dtype=np.int64))
+    a_idx, v_idx = np.concatenate(a_idx), np.concatenate(v_idx)
+    order = np.lexsort((a_idx, v_idx))
+    a_idx, v_idx = a_idx[order], v_idx[order]
+    off = a_idx * per_actor + v_idx * 64
+    cnt = np.minimum(64, np.minimum(n, (a_idx + 1) * per_actor) - off)
+    arr = np.cumsum(cnt) - cnt
+    dev = batch["pk"].device
+    idx = (torch.repeat_interleave(torch.from_numpy(off - arr).to(dev), torch.from_numpy(cnt).to(dev))
+           + torch.arange(n, device=dev))
+    base = np.zeros(len(off), cs_dt)
+    base["actor_id"] = ids.ctypes.data + 16 * a_idx
+    base["site"] = a_idx
+    base["kind"] = L.CORRO_CS_FULL
+    base["version_start"] = base["version_end"] = v_idx + 1
+    base["seq_end"] = base["last_seq"] = cnt - 1
+    base["ts"] = ((v_idx + 1) << 32) | a_idx
+    base["change_off"], base["change_count"] = arr, cnt
+    u = rng.random(len(base))
+    emp = u < empty
+    par = (u >= empty) & (u < empty + partial) & (cnt >= 2)
+    cs = base.copy()
+    cs["kind"][emp] = L.CORRO_CS_EMPTY
+    cs["change_count"][emp] = 0
+    h = cnt // 2
+    first = cs.copy()[par]
+    first["seq_end"] = h[par] - 1
+    first["change_count"] = h[par]
+    second = base[par].copy()
+    second["seq_start"] = h[par]
+    second["change_off"] = arr[par] + h[par]
+    second["change_count"] = cnt[par] - h[par]
+    cs[par] = first
+    resent = base[rng.random(len(base)) < resend]
+    tail = np.concatenate([second, resent])
+    tail = tail[rng.permutation(len(tail))]
+    # second halves and re-sends arrive later in the call: spread over the back half of the arrival order
+    pos = np.sort(rng.integers(len(cs) // 2, len(cs) + 1, size=len(tail)))
+    cs = np.insert(cs, pos, tail)
+    full = {k: v[idx].contiguous() for k, v in batch.items()}
+    full["ts"] = ((full["db_version"] << 32) | full["site"].to(torch.int64)).contiguous()
+    del idx
+    s = L.Changes()
+    s.n = n
+    for k in ("pk", "table_cid", "col_version", "db_version", "cl", "seq", "site", "val0", "ts"):
+        setattr(s, k, full[k].data_ptr())
+    imp = torch.zeros(n, dtype=torch.uint8, device=dev)
+    dcs = torch.from_numpy(cs.view(np.uint8).copy()).to(dev)
+    dknown = torch.zeros(len(cs), dtype=torch.int32, device=dev)
+    out_ = L.ProcessOut()
+    out_.impactful = imp.data_ptr()
+    out_.known = dknown.data_ptr()
+    ms = []
+    nready = 0
+    for _ in range(reps):
+        bk = ca.agent.Bookie()
+        eng.reset()
+        dknown.fill_(-1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        L.check(L.lib().corro_process_multiple_changes(eng._h, bk._h, C.c_void_p(dcs.data_ptr()), len(cs), C.byref(s),
+                                                       L.CORRO_MEM_DEVICE_HEADERS, C.byref(out_)))
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) * 1e3)
+        nready = int(out_.n_ready)
+        del bk
+    ms.sort()
+    med = ms[len(ms) // 2]
+    known = dknown.cpu().numpy()
+    kinds = {name: int((known == v).sum()) for name, v in (("current", 1), ("cleared", 2), ("partial", 3),
+                                                         ("skipped", 0))}
+    del full, imp, dcs, dknown
+    return {"ms": med, "changes_per_s": n / (med * 1e-3), "changesets": int(len(cs)),
+            "ratio_vs_fast": (med / fast_ms) if fast_ms else None, "known": kinds, "n_ready": nready,
+            "mix": {"resent": float(resend), "partial": float(partial), "empty": float(empty)},
+            "note": "agent_e2e's call with ~10% of versions re-sent later in the call, ~5% as two partial halves "
+                    "(buffered, then ready), ~5% as Empty versions; headers in HBM, reset + fresh Bookie + call, "
+                    f"median of {reps}"}
+
+
 def run_multi(args, world, rank):
     import torch
     import torch.distributed as dist

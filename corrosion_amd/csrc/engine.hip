@@ -72,6 +72,15 @@ int grow_heap(corro_ctx *ctx, uint64_t want_records);
 RowStore row_store(corro_ctx *ctx);
 int affinity_convert(corro_ctx *ctx, BatchDev &bd);  // affinity.hip
 
+// The overflow fold reduces rows to their last epoch (k_ovf_lookup's comment) unless asked not to
+// (CORRO_OVF_REDUCE=0; CORRO_OVF_RIMP=0 only with impacts: A/B runs) or a table has 32 or more
+// columns (the summary's cid bits cover cids < 32).
+static bool ovf_reduce_ok(const corro_ctx *ctx, bool impact) {
+    static const bool no_reduce = std::getenv("CORRO_OVF_REDUCE") && std::atoi(std::getenv("CORRO_OVF_REDUCE")) == 0;
+    static const bool no_rimp = std::getenv("CORRO_OVF_RIMP") && std::atoi(std::getenv("CORRO_OVF_RIMP")) == 0;
+    return !no_reduce && ctx->max_stride <= 32 && !(impact && no_rimp);
+}
+
 // Oversized buckets (queued by a merge round), all at once and device-wide (the phases of
 // ovf_kernels.h): batch fields + row owners (one pass) -> region lookups (prior records appended, new rows
 // counted; the store grows here if they do not fit, before anything is written) -> sort by (row,
@@ -194,10 +203,14 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         CORRO_HIP_TRY(hipGetLastError());
         return CORRO_OK;
     };
-    // row reduction off with impacts (every epoch's changes get a flag) or when asked (A/B runs)
-    static const bool no_reduce = std::getenv("CORRO_OVF_REDUCE") && std::atoi(std::getenv("CORRO_OVF_REDUCE")) == 0;
-    // (the summary's cid bits cover cids < 32)
-    d.reduce = (!a.impact && !no_reduce && ctx->max_stride <= 32) ? 1u : 0u;
+    // Row reduction (k_ovf_lookup's comment), with impacts in its impact form (k_ovf_keep's comment:
+    // the dropped records' flags from per-row causal-length slots, the dropped candidates sorted by
+    // group); off when asked (A/B runs) or when the dropped candidates' key would not fit 64 bits.
+    uint32_t kbits = 1;  // (nrows <= Kb)
+    while ((1ULL << kbits) < Kb) kbits++;
+    const bool rimp_fits = kbits + 3 + cid_bits + pbits <= 64;
+    d.reduce = ovf_reduce_ok(ctx, a.impact != nullptr) && (!a.impact || rimp_fits) ? 1u : 0u;
+    d.rimp = d.reduce && a.impact ? 1u : 0u;
     hipLaunchKernelGGL(k_ovf_chunkmap, grid_for((Kb + 63) / 64), blk, 0, s, d);
     hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
     TRY(launched());
@@ -212,7 +225,13 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         uint8_t *blk = (uint8_t *)d.rw1;
         d.rw2 = (uint32_t *)(blk + 8ULL * nrows);
         d.nkeep = (uint32_t *)(blk + 12ULL * nrows);
-        if (d.reduce) CORRO_HIP_TRY(hipMemsetAsync(blk, 0, 12ULL * nrows + 4, s));
+        if (d.reduce) CORRO_HIP_TRY(hipMemsetAsync(blk, 0, 12ULL * nrows + 8, s));
+    }
+    if (d.rimp) {  // causal-length slots (free = ~0) and their first records
+        TRY(ctx->d_ovf_rcl.ensure((uint64_t)nrows * OVF_NCL * 12 + 256));
+        d.rcl = ctx->d_ovf_rcl.as<uint64_t>();
+        d.rclr = reinterpret_cast<uint32_t *>(d.rcl + (uint64_t)nrows * OVF_NCL);
+        CORRO_HIP_TRY(hipMemsetAsync(d.rcl, 0xFF, (uint64_t)nrows * OVF_NCL * 8, s));
     }
     // every row looked up in its region; prior records counted, new rows counted per bucket (and
     // every batch record's sort key)
@@ -253,13 +272,34 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     TRY(launched());
     if (d.reduce) {
         // rows reduced to their last epoch's records (k_ovf_lookup's comment); the rest sort as before
-        hipLaunchKernelGGL(k_ovf_keep, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK), dim3(KEEP_T), 0, s, d);
+        const uint32_t kcap = d.K;
+        hipLaunchKernelGGL(k_ovf_keep, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK), dim3(KEEP_T), 0, s, a, d, kcap);
         TRY(launched());
-        CORRO_HIP_TRY(hipMemcpyAsync(&hw[4], d.nkeep, 4, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(&hw[4], d.nkeep, 8, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipStreamSynchronize(s));
-        const uint32_t kept = hw[4];
-        if (kept == 0 || kept > d.K) return fail(CORRO_E_DEVICE, "internal: overflow row reduction kept no records");
-        if (dbg) fprintf(stderr, "[corro ovf] row reduction keeps %u of %u records\n", kept, d.K);
+        const uint32_t kept = hw[4], ndc = d.rimp ? hw[5] : 0u;
+        if (kept == 0 || kept + ndc > kcap) return fail(CORRO_E_DEVICE, "internal: overflow row reduction kept no records");
+        if (dbg) fprintf(stderr, "[corro ovf] row reduction keeps %u of %u records (%u dropped candidates)\n", kept, d.K, ndc);
+        if (ndc) {
+            // dropped candidates (impact form): sorted by (row, slot, cid, position), running argmax by
+            // group with the candidate scan's kernels, then their flags -- all before the kept records'
+            // sort reuses key_s / val_s / key / qkey / cbest
+            const uint32_t dbits = kbits + 3 + cid_bits + pbits;
+            TRY(ovf_sort_pairs(d_temp, &temp, d.ckey + (kcap - ndc), d.key_s, d.cval + (kcap - ndc), d.val_s, ndc, dbits, s));
+            const dim3 dgrid = grid_for(ndc);
+            hipLaunchKernelGGL(k_ovf_dgather, dgrid, blk, 0, s, a, d, ndc, d.key_s, d.val_s, d.key, d.qkey);
+            TRY(launched());
+            OvfDev dd = d;  // the scan reads (ckey_s: group keys, qkey: cell keys, K, cbest)
+            dd.ckey_s = d.key;
+            dd.K = ndc;
+            const uint32_t ntc = (ndc + CS_TILE - 1) / CS_TILE;  // <= nt
+            hipLaunchKernelGGL(k_cscan_tile, dim3(ntc), dim3(CS_T), 0, s, dd, cs_agg, cs_first);
+            TRY(launched());
+            TRY(ovf_scan_tiles(d_temp, &temp, dd, cs_agg, cs_incl, ntc, s));
+            hipLaunchKernelGGL(k_cscan_fix, dim3(ntc), dim3(CS_T), 0, s, dd, cs_incl, cs_first);
+            hipLaunchKernelGGL(k_ovf_dimp, dgrid, blk, 0, s, a, d, ndc, d.key, d.val_s, d.qkey, d.cbest);
+            TRY(launched());
+        }
         d.K = kept;
         TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.key_s, d.cval, d.val_s, d.K, key_bits, s));
     } else {
@@ -563,7 +603,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_heap, &ctx->d_heap_ts, &ctx->d_heap_top, &ctx->d_stride, &ctx->d_defer,
                       &ctx->d_relist, &ctx->d_dense, &ctx->d_dense_ts, &ctx->d_dense_view, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_ovf_rcl,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
                       &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,
@@ -812,7 +852,8 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     // config 5 12.3 -> 11.5 ms (256 / 1024 / all: 12.4 / 11.8 / 12.8, profiles/r03_c5_gen_ovf_min.log).
     // A small batch keeps its LDS bodies (one bucket past 512 records would pull in the whole fold).
     static const char *gom = std::getenv("CORRO_GEN_OVF_MIN");  // (A/B knob)
-    a.gen_ovf_min = gom ? (uint32_t)std::atoi(gom) : (!imp_buf && bd.n >= (1ULL << 24) ? 512u : 0xFFFFFFFFu);
+    a.gen_ovf_min = gom ? (uint32_t)std::atoi(gom)
+                        : (ovf_reduce_ok(ctx, imp_buf != nullptr) && bd.n >= (1ULL << 24) ? 512u : 0xFFFFFFFFu);
     a.track_ts = ctx->track_ts ? 1u : 0u;
     a.state_wide = ctx->state_wide ? 1u : 0u;
     a.arena = ctx->d_arena.as<uint8_t>();

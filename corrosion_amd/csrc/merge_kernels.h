@@ -1239,18 +1239,28 @@ __device__ inline uint32_t row_heap(uint32_t w, unsigned long long hbase) {
 // Empty region: every row of the bucket is new, so rows and heap records are counted (and each row's
 // heap offset noted) right after the cell hashing; thread 0 allocates after the next barrier, its
 // latency hidden behind the argmax.
+// (one wave scan of each lane's total over its R records and one LDS atomic per wave: the lane's
+// records take consecutive offsets inside its share -- any disjoint assignment of heap offsets does)
 template <int R>
 __device__ inline void fast_rows_count(uint32_t n, const uint32_t (&row)[R], const uint32_t (&strd)[R], uint32_t *s_heap,
                                        uint32_t *s_ctl) {
     const uint32_t tid = threadIdx.x;
-    uint32_t rows = 0;
+    uint32_t rows = 0, tot = 0;
 #pragma unroll
     for (int k = 0; k < R; k++) {
         const uint32_t i = k * FAST_T + tid;
         const bool own = i < n && row[k] == i;
-        const uint32_t off = wave_lds_add(&s_ctl[1], own ? strd[k] : 0u);
-        if (own) s_heap[i] = 0x80000000u | off;
+        tot += own ? strd[k] : 0u;
         rows += own;
+    }
+    uint32_t off = wave_lds_add(&s_ctl[1], tot);
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        const uint32_t i = k * FAST_T + tid;
+        if (i < n && row[k] == i) {
+            s_heap[i] = 0x80000000u | off;
+            off += strd[k];
+        }
     }
     rows = wave_sum_u32(rows);
     if ((tid & 63) == 0 && rows) atomicAdd(&s_ctl[0], rows);
@@ -1318,15 +1328,22 @@ __device__ inline bool fast_rows(const MergeArgs &a, uint32_t b, uint32_t used0,
             ent[k] = ROW_NONE - 1;  // marks "owner of a new row"
         }
     }
-    if (!counted) {  // heap offsets of the new rows, one LDS atomic per wave and k
-        uint32_t rows = 0;
+    if (!counted) {  // heap offsets of the new rows: one wave scan of the lanes' totals, one LDS atomic per wave
+        uint32_t rows = 0, tot = 0;
 #pragma unroll
         for (int k = 0; k < R; k++) {
             const bool nw = ent[k] == ROW_NONE - 1;
-            const uint32_t off = wave_lds_add(&s_ctl[1], nw ? hw[k] : 0u);
-            if (nw) hw[k] = 0x80000000u | off;
+            tot += nw ? hw[k] : 0u;
             rows += nw;
         }
+        uint32_t off = wave_lds_add(&s_ctl[1], tot);
+#pragma unroll
+        for (int k = 0; k < R; k++)
+            if (ent[k] == ROW_NONE - 1) {
+                const uint32_t st = hw[k];
+                hw[k] = 0x80000000u | off;
+                off += st;
+            }
         rows = wave_sum_u32(rows);
         if ((tid & 63) == 0 && rows) atomicAdd(&s_ctl[0], rows);
     }

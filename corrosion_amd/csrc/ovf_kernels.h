@@ -106,8 +106,14 @@ struct OvfDev {
     uint32_t reduce;             // 1: rows are reduced to their last epoch's records before the sort
     uint64_t *rw1;               // [nrows] Mx << 32 | cids at Mx (rs_comb)
     uint32_t *rw2;               // [nrows] cids | outside App. A.3
-    uint32_t *nkeep;             // [1] records kept
+    uint32_t *nkeep;             // [1] records kept; [1]: dropped candidates (impact form)
     uint32_t *cbk;               // [Kb / 64 + 1] bucket of batch record 64 c (k_ovf_chunkmap)
+    // impact form of the reduction (rimp): per row OVF_NCL causal-length slots, the first compact
+    // position of each causal length (cl << 32 | position, ~0 free) and the record at it; the
+    // dropped candidates' sort key = ((row * OVF_NCL + slot) << cid_bits | cid) << rshift | position
+    uint32_t rimp;
+    uint64_t *rcl;               // [nrows * OVF_NCL]
+    uint32_t *rclr;              // [nrows * OVF_NCL]
 };
 
 // a record's 64-B source: the staged batch change or the prior heap record
@@ -288,11 +294,58 @@ __device__ inline void rs_put(const OvfDev &d, uint32_t row, uint64_t w1, uint32
 }
 
 // a record's terms
+// (impact form: a batch column change with col_version <= 0 also keeps its row whole -- a carried,
+// zeroed cell need not lose to it, and the reduced fold carries none)
 __device__ inline void rs_terms(const MergeArgs &a, uint32_t cid, uint32_t cl, int64_t cv, uint32_t pos, uint64_t &w1,
                                 uint32_t &w2) {
     const uint32_t bit = cid != 0 ? 1u << (cid & 31) : 0u;
     w1 = ((uint64_t)cl << 32) | (cv > 0 ? bit : 0u);
-    w2 = bit | (ovf_rec_bad(a, cid, cl, cv, pos) ? 1u : 0u);
+    const bool zero_col = a.impact && cid != 0 && cv <= 0 && (pos & BATCH_POS);
+    w2 = bit | ((ovf_rec_bad(a, cid, cl, cv, pos) || zero_col) ? 1u : 0u);
+}
+
+// ---- impact form: first position of each causal length per row (F(c) of k_ovf_keep) ----------
+#ifndef OVF_NCL
+#define OVF_NCL 8  // causal-length slots per row; a row with more distinct ones keeps every record
+#endif
+// slots fill in order, so one causal length always lands in one slot; the word's min keeps its
+// first position. cl 0 records are never records nor candidates and take no slot.
+__device__ inline void rcl_put(const OvfDev &d, uint32_t row, uint32_t cl, uint32_t pos) {
+    if (cl == 0) return;
+    unsigned long long *sl = (unsigned long long *)d.rcl + (size_t)row * OVF_NCL;
+    const unsigned long long want = ((unsigned long long)cl << 32) | pos;
+    for (uint32_t k = 0; k < OVF_NCL; k++) {
+        unsigned long long cur = ovf_ld_dev(&sl[k]);
+        if (cur == ~0ULL) {
+            cur = atomicCAS(&sl[k], ~0ULL, want);
+            if (cur == ~0ULL) return;
+        }
+        if ((uint32_t)(cur >> 32) == cl) {
+            if (want < cur) atomicMin(&sl[k], want);
+            return;
+        }
+    }
+    atomicOr(&d.rw2[row], 1u);  // more causal lengths than slots: the row keeps every record
+}
+
+// one (row, cl, position) per `todo` lane, called by every lane of the wave: lanes sharing the first
+// active lane's row and causal length (a Zipf-hot row fills whole waves) take their minimum first
+__device__ inline void rcl_wave_add(const OvfDev &d, bool todo, uint32_t row, uint32_t cl, uint32_t pos) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (int round = 0; round < OVF_NCL; round++) {
+        const uint64_t act = __ballot(todo);
+        if (!act) break;
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint32_t lrow = __shfl(row, leader), lcl = __shfl(cl, leader);
+        const bool mine = todo && row == lrow && cl == lcl;
+        if (__popcll(__ballot(mine)) < 4) break;  // (wave-uniform) not a hot row
+        uint32_t m = mine ? pos : ~0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) m = min(m, (uint32_t)__shfl_xor(m, o));
+        if ((int)lane == leader) rcl_put(d, lrow, lcl, m);
+        if (mine) todo = false;
+    }
+    if (todo) rcl_put(d, row, cl, pos);
 }
 
 // Row summaries aggregated per workgroup first: a workgroup takes RS_CHUNK consecutive records
@@ -397,11 +450,14 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
         if (d.reduce) {
             uint64_t w1 = 0;
             uint32_t w2 = 0;
+            uint32_t cl = 0;
             if (valid) {
                 d.rowid[r] = row;  // (own slot: every other lane reads epc, not rowid)
-                rs_terms(a, d.tc[r] & 0xFFFFu, d.cl[r], d.cv[r], pos, w1, w2);
+                cl = d.cl[r];
+                rs_terms(a, d.tc[r] & 0xFFFFu, cl, d.cv[r], pos, w1, w2);
             }
             rs_wave_add(L, d, valid, row, w1, w2);
+            if (d.rimp) rcl_wave_add(d, valid, row, cl, d.pm + (pos & 0x7FFFFFFFu));
         }
         if (!valid || !d.recf[r]) continue;  // (an owner's row: epc[r] - 1, as computed above)
         const uint32_t b = bk, t = d.tc[r] >> 16;
@@ -456,6 +512,7 @@ static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
                     uint32_t w2;
                     rs_terms(a, pr.tcid & 0xFFFFu, pr.cl, pr.cv, c, w1, w2);
                     rs_put(d, row, w1, w2);
+                    if (d.rimp) rcl_put(d, row, pr.cl, c);
                 }
                 r++;
             }
@@ -465,46 +522,158 @@ static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
 // The kept records' (key, record) pairs compacted into (ckey, cval) for the sort: each workgroup
 // takes a contiguous chunk, ranks its kept records by wave ballots and reserves their slots with ONE
 // atomic (the order does not matter: the keys are unique and the sort orders them).
+//
+// Impact form (rimp; the rule is checked against the sequential oracle on the CPU in
+// tests/test_ovf_reduce_rule.py::test_row_reduction_impacts_equal_full_fold): a dropped record r of a
+// reduced row (cl < Mx) at compact position p, with F = its causal length's first position and H the
+// first position of any larger causal length (the row's OVF_NCL slots), is
+//   a record     p == F < H: flag 1, or 2 for a column change with odd cl > 1 (it resurrects); the
+//                slot notes r (the epoch record a candidate group may be seeded by);
+//   a candidate  F < p < H, odd cl, column change: compacted from the END of (ckey, cval) with its
+//                group key (row, slot, cid) and position, for the sort and running argmax that
+//                decide its flag (k_ovf_dimp);
+//   a no-op      otherwise: flag 0.
+__device__ inline void ovf_drop_class(const MergeArgs &a, const OvfDev &d, uint32_t r, uint32_t row, uint32_t cl,
+                                      bool &cand, uint64_t &dkey) {
+    cand = false;
+    const uint64_t key = d.key[r];
+    const uint32_t p = (uint32_t)(key & ((1ULL << d.rshift) - 1));
+    const uint32_t tc = d.tc[r], cid = tc & 0xFFFFu, pos = d.pos[r];
+    uint32_t F = ~0u, H = ~0u, slot = 0;
+    const unsigned long long *sl = (const unsigned long long *)d.rcl + (size_t)row * OVF_NCL;
+#pragma unroll
+    for (uint32_t k = 0; k < OVF_NCL; k++) {
+        const unsigned long long x = sl[k];
+        if (x == ~0ULL) continue;
+        const uint32_t c = (uint32_t)(x >> 32), fp = (uint32_t)x;
+        if (c == cl) {
+            F = fp;
+            slot = k;
+        } else if (c > cl) {
+            H = min(H, fp);
+        }
+    }
+    uint8_t flag = 0;
+    if (cl != 0 && p == F && p < H) {
+        flag = (cid != 0 && (cl & 1u) && cl > 1) ? 2 : 1;
+        d.rclr[(size_t)row * OVF_NCL + slot] = r;
+    } else if (cl != 0 && F != ~0u && F < p && p < H && (cl & 1u) && cid != 0) {
+        cand = true;
+        dkey = ((((uint64_t)row * OVF_NCL + slot) << d.cid_bits | cid) << d.rshift) | p;
+    }
+    if (!cand && (pos & BATCH_POS)) a.impact[pos & 0x7FFFFFFFu] = flag;
+}
+
 constexpr uint32_t KEEP_T = 256, KEEP_E = 32, KEEP_CHUNK = KEEP_T * KEEP_E;
-static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(OvfDev d) {
-    __shared__ uint32_t s_cnt[KEEP_T / 64], s_base;
+static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(MergeArgs a, OvfDev d, uint32_t kcap) {
+    __shared__ uint32_t s_cnt[KEEP_T / 64], s_base, s_dcnt[KEEP_T / 64], s_dbase;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = d.K;
     const uint32_t c0 = blockIdx.x * KEEP_CHUNK;
     uint32_t mine = 0, cnt = 0;  // lane's kept bits per step; the wave's kept count
+    uint32_t dmine = 0, dcnt = 0;  // (impact form) the same for dropped candidates
 #pragma unroll 4
     for (uint32_t j = 0; j < KEEP_E; j++) {
         const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
-        bool keep = false;
+        bool keep = false, cand = false;
         if (r < n) {
             const uint32_t row = d.rowid[r], cl = d.cl[r], w2 = d.rw2[row];
             const uint64_t w1 = d.rw1[row];
             const uint32_t mx = (uint32_t)(w1 >> 32);
             const bool red = !(w2 & 1u) && (!(mx & 1u) || (uint32_t)w1 == w2);
             keep = !red || cl == mx;
+            if (!keep && d.rimp) {
+                uint64_t dk;
+                ovf_drop_class(a, d, r, row, cl, cand, dk);
+            }
         }
         mine |= keep ? 1u << j : 0u;
         cnt += (uint32_t)__popcll(__ballot(keep));
+        dmine |= cand ? 1u << j : 0u;
+        dcnt += (uint32_t)__popcll(__ballot(cand));
     }
-    if (lane == 0) s_cnt[w] = cnt;
+    if (lane == 0) {
+        s_cnt[w] = cnt;
+        s_dcnt[w] = dcnt;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (uint32_t v = 0; v < KEEP_T / 64; v++) t += s_cnt[v];
+        uint32_t t = 0, u = 0;
+        for (uint32_t v = 0; v < KEEP_T / 64; v++) {
+            t += s_cnt[v];
+            u += s_dcnt[v];
+        }
         s_base = t ? atomicAdd(d.nkeep, t) : 0u;
+        s_dbase = u ? atomicAdd(d.nkeep + 1, u) : 0u;
     }
     __syncthreads();
-    uint32_t o = s_base;
-    for (uint32_t v = 0; v < w; v++) o += s_cnt[v];
+    uint32_t o = s_base, od = s_dbase;
+    for (uint32_t v = 0; v < w; v++) {
+        o += s_cnt[v];
+        od += s_dcnt[v];
+    }
     for (uint32_t j = 0; j < KEEP_E; j++) {
         const bool keep = (mine >> j) & 1u;
         const uint64_t m = __ballot(keep);
+        const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
         if (keep) {
-            const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
             const uint32_t q = o + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
             d.ckey[q] = d.key[r];
             d.cval[q] = r;
         }
         o += (uint32_t)__popcll(m);
+        if (!dcnt) continue;  // (wave-uniform)
+        const bool cand = (dmine >> j) & 1u;
+        const uint64_t dm = __ballot(cand);
+        if (cand) {  // dropped candidates fill (ckey, cval) from the end: kept + dropped <= kcap
+            const uint32_t q = kcap - 1 - (od + (uint32_t)__popcll(dm & ((1ULL << lane) - 1)));
+            bool c2;
+            uint64_t dk;
+            ovf_drop_class(a, d, r, d.rowid[r], d.cl[r], c2, dk);  // (recomputed: the key, no flag written)
+            d.ckey[q] = dk;
+            d.cval[q] = r;
+        }
+        od += (uint32_t)__popcll(dm);
+    }
+}
+
+// the cell key of record x (a batch record's staged copy, a prior record's key read before the walk)
+__device__ inline OvfKey ovf_key_x(const MergeArgs &a, const OvfDev &d, uint32_t x) {
+    if (x >= d.Kb) return d.pkey[x - d.Kb];
+    const Rec r = load_rec(ovf_rec(a, d, x));
+    return OvfKey{r.cv, r.v0, r.v1, r.meta, site_rank_of(a, r.site)};
+}
+
+// dropped candidates sorted by (group, position): their group keys (for the running argmax's group
+// starts) and cell keys in sorted order
+static __global__ void k_ovf_dgather(MergeArgs a, OvfDev d, uint32_t ndc, const uint64_t *__restrict__ dkey_s,
+                                     const uint32_t *__restrict__ dval_s, uint64_t *__restrict__ dgroup,
+                                     OvfKey *__restrict__ dq) {
+    OVF_LOOP(q, ndc) {
+        dgroup[q] = dkey_s[q] >> d.rshift;
+        dq[q] = ovf_key_x(a, d, dval_s[q]);
+    }
+}
+
+// a dropped candidate's flag: strictly greater than every earlier candidate of its (row, causal
+// length, cid) group (dbest[q - 1]: the running argmax) and than its epoch record's own cell when
+// that record is a column change of the same cid (a carried, zeroed cell loses to col_version > 0)
+static __global__ void k_ovf_dimp(MergeArgs a, OvfDev d, uint32_t ndc, const uint64_t *__restrict__ dgroup,
+                                  const uint32_t *__restrict__ dval_s, const OvfKey *__restrict__ dq,
+                                  const uint32_t *__restrict__ dbest) {
+    OVF_LOOP(q, ndc) {
+        const uint32_t x = dval_s[q];
+        const uint32_t pos = d.pos[x];
+        if (!(pos & BATCH_POS)) continue;
+        const uint64_t g = dgroup[q];
+        const OvfKey k = dq[q];
+        bool imp = q == 0 || dgroup[q - 1] != g || ovf_kcmp(k, dq[dbest[q - 1]], d.arena) > 0;
+        if (imp) {
+            const uint32_t cid = (uint32_t)(g & ((1ULL << d.cid_bits) - 1));
+            const uint64_t rs = g >> d.cid_bits;  // row * OVF_NCL + slot
+            const uint32_t R = d.rclr[rs];
+            if ((d.tc[R] & 0xFFFFu) == cid) imp = ovf_kcmp(k, ovf_key_x(a, d, R), d.arena) > 0;
+        }
+        a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
     }
 }
 
@@ -514,7 +683,7 @@ static __global__ void k_ovf_gather(OvfDev d) {
         d.rowid[p] = row;
         d.cl_s[p] = d.cl[d.val_s[p]];
         d.head[p] = 0;
-        if (!d.reduce) d.fstg[p] = 0;  // (impacts only; never with the row reduction)
+        if (!d.reduce || d.rimp) d.fstg[p] = 0;  // (impacts only)
         if (p == 0 || (uint32_t)(d.key_s[p - 1] >> d.rshift) != row) {
             d.rstart[row] = p;
             d.rbad[row] = 0;

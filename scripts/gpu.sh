@@ -57,6 +57,11 @@ for s in "$@"; do
     agenttrace) step agenttrace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/agenttrace" -o run -- \
                   python tools/bench_agent.py
                 kstats "$OUT/agenttrace" ;;
+    agentsplit) for w in path e2e; do  # separate kernel traces of agent_path and agent_e2e
+                  CORRO_AGENT_ONLY=$w step "agent_$w" 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                    -d "$OUT/agent_$w" -o run -- python tools/bench_agent.py
+                  kstats "$OUT/agent_$w"
+                done ;;
     sync) step sync 400 python -u bench_sync.py ;;
     synctrace) step synctrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/synctrace" -o run -- $SY
                kstats "$OUT/synctrace" ;;

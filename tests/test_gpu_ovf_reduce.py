@@ -35,19 +35,30 @@ def _compare(e, f):
     assert list(e.db_versions()[:f.nsites]) == list(f.db_versions())
 
 
+def _apply(e, f, b, impact):
+    if impact:
+        got = e.apply(b, impact=True)
+        want = f.apply(b)
+        assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
+    else:
+        e.apply(b)
+        f.apply(b)
+
+
+@pytest.mark.parametrize("impact", [False, True])
 @pytest.mark.parametrize("ncols,lo", [(31, 25), (40, 28)], ids=["cid31_reduced", "wide_not_reduced"])
-def test_reduction_cid_mask_edges(ncols, lo):
+def test_reduction_cid_mask_edges(ncols, lo, impact):
     seed = 901 + ncols
     sites = synth.site_ids(8, seed)
     e, f = _engine({"t0": [f"c{i}" for i in range(ncols)]}, sites), O.Fold(sites)
     for k in range(3):
         b = _recid(synth.adversarial_batch(40000, 8, 1, 80, seed * 10 + k, zipf=1.1), ncols, seed + k, lo=lo)
-        e.apply(b)
-        f.apply(b)
+        _apply(e, f, b, impact)
     _compare(e, f)
 
 
-def test_reduction_keeps_rows_with_untouched_prior_cids():
+@pytest.mark.parametrize("impact", [False, True])
+def test_reduction_keeps_rows_with_untouched_prior_cids(impact):
     """Prior rows hold cids 1..4; the hot batch then only writes cids 1..2 at its largest cl, so rows
     whose prior cells of cids 3..4 are not covered keep every change (and carry those cells)."""
     seed = 933
@@ -56,6 +67,23 @@ def test_reduction_keeps_rows_with_untouched_prior_cids():
     b1 = synth.adversarial_batch(30000, 8, 2, 200, seed, zipf=1.1)
     b2 = _recid(synth.adversarial_batch(50000, 8, 2, 200, seed + 1, zipf=1.1), 2, seed + 2)
     for b in (b1, b2, b1):
-        e.apply(b)
-        f.apply(b)
+        _apply(e, f, b, impact)
+        _compare(e, f)
+
+
+@pytest.mark.parametrize("max_cl,sent,wide", [(6, 0.3, True), (7, 0.3, False), (3, 0.6, True), (12, 0.3, False),
+                                              (5, 0.1, True)])
+def test_reduction_impact_form_vs_oracle(max_cl, sent, wide):
+    """The impact form of the reduction (k_ovf_keep's comment): a dropped change's flag from its row's
+    causal-length slots -- records, no-ops, and candidates by a running argmax over their (row, cl,
+    cid) group seeded by a same-cid epoch record -- against the sequential oracle's
+    crsql_rows_impacted() growth, three batches folded (prior records in the slots too); max_cl 12
+    passes the 8 slots for many rows (those keep every change)."""
+    seed = 950 + max_cl
+    sites = synth.site_ids(12, seed)
+    e, f = _engine(synth.adversarial_schema(3), sites), O.Fold(sites)
+    for k in range(3):
+        b = synth.adversarial_batch(60000, 12, 3, 96, seed * 10 + k, zipf=1.1, max_cl=max_cl, sentinel_frac=sent,
+                                    wide=wide)
+        _apply(e, f, b, True)
         _compare(e, f)

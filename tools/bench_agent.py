@@ -22,9 +22,12 @@ def main():
                                       device=dev)
     torch.cuda.synchronize()
     eng.set_profiling(True)
-    path = bench.agent_path(eng, batch, n, reps=reps)
-    e2e = bench.agent_e2e(eng, batch, n, path["ms"], reps=reps)
-    print(json.dumps({"agent_path": path, "agent_e2e": e2e}), flush=True)
+    only = os.environ.get("CORRO_AGENT_ONLY")  # "path" / "e2e": one of the two (separate kernel traces)
+    path = bench.agent_path(eng, batch, n, reps=reps) if only != "e2e" else {"ms": None}
+    e2e = bench.agent_e2e(eng, batch, n, path["ms"], reps=reps) if only not in ("path", "mixed") else None
+    mixed = bench.agent_e2e_mixed(eng, batch, n, e2e["ms"] if e2e else None, reps=reps) \
+        if only in (None, "mixed") else None
+    print(json.dumps({"agent_path": path, "agent_e2e": e2e, "agent_e2e_mixed": mixed}), flush=True)
     eng.close()
 
 
