@@ -235,7 +235,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     }
     // every row looked up in its region; prior records counted, new rows counted per bucket (and
     // every batch record's sort key)
-    hipLaunchKernelGGL(k_ovf_lookup, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)), dim3(RS_T), 0, s, a, d);
+    hipLaunchKernelGGL(d.rimp ? k_ovf_lookup<true> : k_ovf_lookup<false>, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)),
+                       dim3(RS_T), 0, s, a, d);
     TRY(launched());
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
     CORRO_HIP_TRY(hipMemcpyAsync(&hw[0], d.rpoff + (nrows - 1), 4, hipMemcpyDeviceToHost, s));
@@ -791,8 +792,9 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     // (bucket general bits, misc counters and per-site db_version maxima are zeroed by k_hist)
     ApplyZero z{ctx->d_bflags.as<uint32_t>(), ctx->d_misc.as<unsigned long long>(),
                 ctx->d_dbv_batch.as<unsigned long long>(), (B + 31) / 32, (uint32_t)MISC_WORDS, nsites};
-    // (1: the INTEGER impact body stores only zero flags; every other body stores each change's)
-    if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 1, bd.ap ? ctx->pm_n : n, s));
+    // (0: every body stores only the nonzero flags -- in Zipf-hot batches most changes are no-ops,
+    // and each flag store is a random byte)
+    if (imp_buf) CORRO_HIP_TRY(hipMemsetAsync(imp_buf, 0, bd.ap ? ctx->pm_n : n, s));
 
     unsigned long long *misc = ctx->d_misc.as<unsigned long long>();
     const bool prof = ctx->profiling;
@@ -1088,10 +1090,14 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.vsz = in->val_size;
     }
     bd.n = n;
+    // (a slot layout -- corro_apply_mapped -- may pass the chunk size by its padding: one chunk still)
+    const uint64_t chunk_cap = corro_detail_chunk_changes(ctx) + (ctx->pm_slack ? corro_detail_chunk_changes(ctx) / 4 : 0);
     if (ctx->pm_ap) {  // position mode (agent): one chunk, per-position ts
-        if (mem != CORRO_MEM_DEVICE || n > corro_detail_chunk_changes(ctx))
+        if (mem != CORRO_MEM_DEVICE || n > chunk_cap)
             return fail(CORRO_E_INVALID, "internal: position mode needs one device-resident chunk");
         bd.ap = ctx->pm_ap;
+        // (positions [0, pm_n) cover every input change; a mapped apply's skips are anywhere)
+        bd.ap_all = ctx->pm_n == n && !ctx->pm_slack ? 1u : 0u;
         bd.ts = ctx->pm_ts;
     }
     // long values: the batch's value bytes are appended to the arena once; every chunk's changes
@@ -1117,7 +1123,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
 
     TRY(affinity_convert(ctx, bd));
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
-    const uint64_t chunk = corro_detail_chunk_changes(ctx);
+    const uint64_t chunk = ctx->pm_ap ? std::max<uint64_t>(n, 1) : corro_detail_chunk_changes(ctx);
     if (n > chunk) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
         hipLaunchKernelGGL(k_validate, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, bd,
@@ -1148,6 +1154,23 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         CORRO_HIP_TRY(hipStreamSynchronize(s));
     }
     return CORRO_OK;
+}
+
+int corro_apply_mapped(corro_ctx *ctx, const corro_changes *in, const uint32_t *ap, corro_apply_out *out) {
+    if (!ctx || !in || !ap) return fail(CORRO_E_INVALID, "NULL argument");
+    if (ctx->pm_ap) return fail(CORRO_E_INVALID, "a position map is already set on this context");
+    // position mode with position = index: skipped changes are not applied, the rest in index order
+    ctx->pm_ap = ap;
+    ctx->pm_src = nullptr;
+    ctx->pm_ts = in->ts;
+    ctx->pm_n = in->n;
+    ctx->pm_slack = true;
+    const int rc = corro_apply_batch(ctx, in, CORRO_MEM_DEVICE, out);
+    ctx->pm_ap = nullptr;
+    ctx->pm_ts = nullptr;
+    ctx->pm_n = 0;
+    ctx->pm_slack = false;
+    return rc;
 }
 
 }  // extern "C"

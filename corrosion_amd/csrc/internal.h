@@ -154,6 +154,7 @@ struct corro_ctx {
     const uint32_t *pm_ap = nullptr, *pm_src = nullptr;
     const uint64_t *pm_ts = nullptr;
     uint64_t pm_n = 0;
+    bool pm_slack = false;  // corro_apply_mapped: a slot layout's padding may pass the chunk size
     bool apply_wrote = false;     // the current apply has launched its first merge kernel
     uint64_t heap_limit = 0;      // corro_ctx_set_store_limit (0: none)
     bool state_wide = false;      // some clock row holds a non-INTEGER value

@@ -233,7 +233,7 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t 
             const uint32_t i = min(base + k * blockDim.x + threadIdx.x, end - 1);
             pk[k] = in.pk[i];
             tc[k] = one_table ? 0u : in.tcid[i];
-            ap[k] = in.ap ? in.ap[i] : 0u;
+            ap[k] = in.ap && !in.ap_all ? in.ap[i] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < HIST_U; k++) {
@@ -839,7 +839,7 @@ __device__ inline void gen_fold_row(const MergeArgs &a, const V &v, E &em, const
                 imp = 1;
             }
         }
-        if (a.impact && (pos & BATCH_POS)) a.impact[pos & 0x7FFFFFFFu] = (uint8_t)imp;
+        if (a.impact && (pos & BATCH_POS) && imp) a.impact[pos & 0x7FFFFFFFu] = (uint8_t)imp;
     }
     em.emit(a, v, g, s, row, ncell, hs, scv, ssrc);
 }
@@ -1834,7 +1834,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
             if (earlier && c >= 0) imp = false;             // an earlier change already holds >= key
             if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
         }
-        if (a.impact && (pos[k] & BATCH_POS)) a.impact[pos[k] & 0x7FFFFFFFu] = imp ? 1 : 0;
+        if (a.impact && (pos[k] & BATCH_POS) && imp) a.impact[pos[k] & 0x7FFFFFFFu] = 1;
         alive[k] = win;
     }
     __syncthreads();
@@ -2063,7 +2063,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
             if (earlier && c >= 0) imp = false;             // an earlier change already holds >= key
             if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
         }
-        if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
+        if (a.impact && (pos[k] & BATCH_POS) && imp) a.impact[pos[k] & 0x7FFFFFFFu] = 1;
         alive[k] = win;
     }
     __syncthreads();
@@ -2278,7 +2278,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
             nxt = s_nx[m];
         }
 #if !(CORRO_DIAG & 1024)  // (1024: diagnostics only -- no flag stores, results not valid)
-        if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
+        if (a.impact && (pos[k] & BATCH_POS) && imp) a.impact[pos[k] & 0x7FFFFFFFu] = 1;
 #endif
         alive[k] = win;
     }
@@ -2346,7 +2346,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
             if (c > 0 || (c == 0 && earlier)) win = false;  // a greater key, or an equal earlier one
         }
 #if !(CORRO_DIAG & 1024)  // (1024: diagnostics only -- no flag stores, results not valid)
-        if (a.impact && (pos[k] & BATCH_POS) && !imp) a.impact[pos[k] & 0x7FFFFFFFu] = 0;
+        if (a.impact && (pos[k] & BATCH_POS) && imp) a.impact[pos[k] & 0x7FFFFFFFu] = 1;
 #endif
         alive[k] = win;
     }

@@ -328,11 +328,47 @@ __device__ inline void rcl_put(const OvfDev &d, uint32_t row, uint32_t cl, uint3
     atomicOr(&d.rw2[row], 1u);  // more causal lengths than slots: the row keeps every record
 }
 
+// Per workgroup first (k_ovf_lookup's chunk of RS_CHUNK bucket-major records: a few buckets' rows, a
+// hot row's records many times over): an LDS table keyed (row, cl) keeps the minimum position, and
+// each entry goes to the row's global slots once at the end. A key without an LDS slot goes straight
+// to the global slots.
+constexpr uint32_t RCL_HT = 2048;
+struct RclLds {
+    unsigned long long key[RCL_HT];  // row << 32 | cl, ~0: free
+    uint32_t pos[RCL_HT];
+};
+
+__device__ inline void rcl_lds_clear(RclLds &L) {
+    for (uint32_t i = threadIdx.x; i < RCL_HT; i += blockDim.x) {
+        L.key[i] = ~0ULL;
+        L.pos[i] = ~0u;
+    }
+}
+
+__device__ inline bool rcl_lds_add(RclLds &L, uint32_t row, uint32_t cl, uint32_t pos) {
+    const unsigned long long k = ((unsigned long long)row << 32) | cl;
+    const uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ULL) >> 53);  // (RCL_HT = 2^11)
+    for (uint32_t j = 0; j < 16; j++) {
+        const uint32_t sl = (h + j) & (RCL_HT - 1);
+        unsigned long long o = L.key[sl];
+        if (o == ~0ULL) o = atomicCAS(&L.key[sl], ~0ULL, k);
+        if (o != ~0ULL && o != k) continue;
+        atomicMin(&L.pos[sl], pos);
+        return true;
+    }
+    return false;
+}
+
+__device__ inline void rcl_lds_flush(const RclLds &L, const OvfDev &d) {
+    for (uint32_t i = threadIdx.x; i < RCL_HT; i += blockDim.x)
+        if (L.key[i] != ~0ULL) rcl_put(d, (uint32_t)(L.key[i] >> 32), (uint32_t)L.key[i], L.pos[i]);
+}
+
 // one (row, cl, position) per `todo` lane, called by every lane of the wave: lanes sharing the first
 // active lane's row and causal length (a Zipf-hot row fills whole waves) take their minimum first
-__device__ inline void rcl_wave_add(const OvfDev &d, bool todo, uint32_t row, uint32_t cl, uint32_t pos) {
+__device__ inline void rcl_wave_add(RclLds &L, const OvfDev &d, bool todo, uint32_t row, uint32_t cl, uint32_t pos) {
     const uint32_t lane = threadIdx.x & 63;
-    for (int round = 0; round < OVF_NCL; round++) {
+    for (int round = 0; round < 2; round++) {  // (two rounds, as for the summaries: the rest go to LDS)
         const uint64_t act = __ballot(todo);
         if (!act) break;
         const int leader = __ffsll((unsigned long long)act) - 1;
@@ -342,10 +378,10 @@ __device__ inline void rcl_wave_add(const OvfDev &d, bool todo, uint32_t row, ui
         uint32_t m = mine ? pos : ~0u;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) m = min(m, (uint32_t)__shfl_xor(m, o));
-        if ((int)lane == leader) rcl_put(d, lrow, lcl, m);
+        if ((int)lane == leader && lcl != 0 && !rcl_lds_add(L, lrow, lcl, m)) rcl_put(d, lrow, lcl, m);
         if (mine) todo = false;
     }
-    if (todo) rcl_put(d, row, cl, pos);
+    if (todo && cl != 0 && !rcl_lds_add(L, row, cl, pos)) rcl_put(d, row, cl, pos);
 }
 
 // Row summaries aggregated per workgroup first: a workgroup takes RS_CHUNK consecutive records
@@ -426,10 +462,15 @@ __device__ inline void rs_wave_add(RsLds &L, const OvfDev &d, bool todo, uint32_
     if (todo && !rs_lds_add(L, row, w1, w2)) rs_put(d, row, w1, w2);
 }
 
+// (RIMP: the impact form's causal-length slots too; its LDS table only in that instantiation, so the
+// plain form keeps its occupancy)
+template <bool RIMP>
 static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev d) {
     __shared__ RsLds L;
+    __shared__ typename std::conditional<RIMP, RclLds, char>::type LC_;
     if (d.reduce) {
         rs_lds_clear(L);
+        if constexpr (RIMP) rcl_lds_clear(LC_);
         __syncthreads();
     }
     const uint32_t c0 = blockIdx.x * RS_CHUNK;
@@ -457,7 +498,7 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
                 rs_terms(a, d.tc[r] & 0xFFFFu, cl, d.cv[r], pos, w1, w2);
             }
             rs_wave_add(L, d, valid, row, w1, w2);
-            if (d.rimp) rcl_wave_add(d, valid, row, cl, d.pm + (pos & 0x7FFFFFFFu));
+            if constexpr (RIMP) rcl_wave_add(LC_, d, valid, row, cl, d.pm + (pos & 0x7FFFFFFFu));
         }
         if (!valid || !d.recf[r]) continue;  // (an owner's row: epc[r] - 1, as computed above)
         const uint32_t b = bk, t = d.tc[r] >> 16;
@@ -483,6 +524,7 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
     if (d.reduce) {
         __syncthreads();
         rs_lds_flush(L, d);
+        if constexpr (RIMP) rcl_lds_flush(LC_, d);
     }
 }
 
@@ -561,7 +603,7 @@ __device__ inline void ovf_drop_class(const MergeArgs &a, const OvfDev &d, uint3
         cand = true;
         dkey = ((((uint64_t)row * OVF_NCL + slot) << d.cid_bits | cid) << d.rshift) | p;
     }
-    if (!cand && (pos & BATCH_POS)) a.impact[pos & 0x7FFFFFFFu] = flag;
+    if (!cand && (pos & BATCH_POS) && flag) a.impact[pos & 0x7FFFFFFFu] = flag;
 }
 
 constexpr uint32_t KEEP_T = 256, KEEP_E = 32, KEEP_CHUNK = KEEP_T * KEEP_E;
@@ -673,7 +715,7 @@ static __global__ void k_ovf_dimp(MergeArgs a, OvfDev d, uint32_t ndc, const uin
             const uint32_t R = d.rclr[rs];
             if ((d.tc[R] & 0xFFFFu) == cid) imp = ovf_kcmp(k, ovf_key_x(a, d, R), d.arena) > 0;
         }
-        a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
+        if (imp) a.impact[pos & 0x7FFFFFFFu] = 1;
     }
 }
 
@@ -705,8 +747,8 @@ static __global__ void k_ovf_classify(MergeArgs a, OvfDev d) {
         // a converted value compares raw-vs-stored, an order the candidate argmax cannot keep
         if (a.raw.conv && (pos & BATCH_POS) && a.raw.conv[batch_src(a, pos & 0x7FFFFFFFu)])
             atomicOr(&d.rbad[d.rowid[p]], 1u);
-        if (a.impact && (pos & BATCH_POS) && kd != 2)
-            a.impact[pos & 0x7FFFFFFFu] = kd == 0 ? 0 : ((cid != 0 && (cl & 1u) && (L > 0 || cl > 1)) ? 2 : 1);
+        if (a.impact && (pos & BATCH_POS) && kd == 1)
+            a.impact[pos & 0x7FFFFFFFu] = (cid != 0 && (cl & 1u) && (L > 0 || cl > 1)) ? 2 : 1;
     }
 }
 
@@ -1032,7 +1074,7 @@ static __global__ void k_ovf_impacts(MergeArgs a, OvfDev d) {
         bool imp = first || ovf_kcmp(kq, ovf_key_q(d, d.cbest[q - 1]), d.arena) > 0;
         const uint32_t fs = d.fstg[d.cgs[q]];
         if (imp && fs) imp = ovf_kcmp(kq, ovf_key_p(a, d, (fs & 0x7FFFFFFFu) - 1, (fs >> 31) != 0), d.arena) > 0;
-        a.impact[pos & 0x7FFFFFFFu] = imp ? 1 : 0;
+        if (imp) a.impact[pos & 0x7FFFFFFFu] = 1;
     }
 }
 

@@ -47,9 +47,9 @@ k_part_count(BatchDev in, uint32_t tile, uint32_t nranks, uint32_t *__restrict__
 }
 
 // one workgroup: counts[t][r] -> absolute output position of tile t's first change for rank r;
-// totals[r] = changes for rank r
+// totals[r] = changes for rank r. cap > 0: rank r's group starts at r * cap (the slot layout)
 __global__ void k_part_scan(uint32_t *__restrict__ counts, uint32_t ntiles, uint32_t nranks,
-                            uint64_t *__restrict__ totals) {
+                            uint64_t *__restrict__ totals, uint64_t cap = 0) {
     __shared__ uint64_t base[PART_MAX_RANKS];
     if (threadIdx.x < nranks) {
         const uint32_t r = threadIdx.x;
@@ -65,7 +65,7 @@ __global__ void k_part_scan(uint32_t *__restrict__ counts, uint32_t ntiles, uint
     if (threadIdx.x == 0) {
         uint64_t run = 0;
         for (uint32_t r = 0; r < nranks; r++) {
-            base[r] = run;
+            base[r] = cap ? (uint64_t)r * cap : run;
             run += totals[r];
         }
     }
@@ -158,7 +158,7 @@ static_assert(sizeof(PackedRec48) == 48 && sizeof(PackedRec80) == 80, "packed re
 template <bool PLAIN>
 __global__ void __launch_bounds__(PART_THREADS)
 k_part_pack(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restrict__ offs, void *__restrict__ out,
-            uint32_t *__restrict__ perm) {
+            uint32_t *__restrict__ perm, uint64_t cap = 0) {
     __shared__ uint32_t run[PART_MAX_RANKS];
     __shared__ uint32_t wcnt[PART_THREADS / 64][PART_MAX_RANKS];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -183,6 +183,9 @@ k_part_pack(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restr
         if (act) {
             uint32_t pos = run[d] + my_rank;
             for (uint32_t ww = 0; ww < w; ww++) pos += wcnt[ww][d];
+            // (slot layout: a record past rank d's slot is counted, not written -- the receiver sees
+            // the count and the caller repeats the exchange with exact sizes)
+            if (cap && pos >= (uint64_t)(d + 1) * cap) goto next;
             if (PLAIN) {
                 PackedRec48 r{pk, in.cv[i], in.dbv[i], in.v0[i], tc, in.cl[i], in.seq[i], in.site[i]};
                 static_cast<PackedRec48 *>(out)[pos] = r;
@@ -203,6 +206,7 @@ k_part_pack(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restr
             }
             if (perm) perm[pos] = i;
         }
+    next:
         __syncthreads();
         if (threadIdx.x < nranks) {
             uint32_t add = 0;
@@ -211,6 +215,30 @@ k_part_pack(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restr
         }
         __syncthreads();
     }
+}
+
+// received slots -> SoA at the same indices, ap[i] = i (received) / AP_SKIP (padding, or every slot
+// when a source overflowed its slot: the apply is then a no-op and the caller repeats the exchange)
+__global__ void k_unpack_slots(const PackedRec48 *__restrict__ recs, uint32_t nsrc, uint64_t cap,
+                               const uint64_t *__restrict__ cnt, BatchOut o, uint32_t *__restrict__ ap,
+                               uint32_t *__restrict__ overflow) {
+    bool over = false;
+    for (uint32_t s = 0; s < nsrc; s++) over |= cnt[s] > cap;
+    const uint64_t n = (uint64_t)nsrc * cap;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)(i / cap);
+        const bool valid = !over && i - (uint64_t)s * cap < cnt[s];
+        if (valid) {
+            const PackedRec48 r = recs[i];
+            o.pk[i] = r.pk; o.cv[i] = r.cv; o.dbv[i] = r.dbv; o.v0[i] = r.v0;
+            o.tcid[i] = r.tcid; o.cl[i] = r.cl; o.seq[i] = r.seq; o.site[i] = r.site;
+        } else {  // padding: fields no check trips over (never merged: ap = skip)
+            o.pk[i] = 0; o.cv[i] = 1; o.dbv[i] = 0; o.v0[i] = 0;
+            o.tcid[i] = 0xFFFFFFFFu; o.cl[i] = 1; o.seq[i] = 0; o.site[i] = 0xFFFFFFFFu;
+        }
+        ap[i] = valid ? (uint32_t)i : AP_SKIP;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = over ? 1u : 0u;
 }
 
 // received records (source-rank order) -> the SoA batch corro_apply_batch takes
@@ -517,6 +545,63 @@ extern "C" int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n
         hipLaunchKernelGGL(k_unpack<false>, dim3(grid), dim3(256), 0, s, recs, (uint32_t)n, bo);
     CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
+// ---------------------------------------------------------------------- stream-ordered slots
+extern "C" void *corro_ctx_stream(corro_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+extern "C" int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, uint64_t cap, void *out,
+                                     uint64_t *counts_dev) {
+    if (!ctx || !in || !out || !counts_dev) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nranks == 0 || nranks > (uint32_t)PART_MAX_RANKS) return fail(CORRO_E_RANGE, "1..64 ranks");
+    if (in->n >= (1ULL << 31) || cap == 0 || (uint64_t)nranks * cap >= (1ULL << 31))
+        return fail(CORRO_E_RANGE, "slots: 1 <= cap, nranks * cap < 2^31 records");
+    if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
+        !in->val0)
+        return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    if (in->val1 || in->val_type || in->val_len || in->ts || in->val_off)
+        return fail(CORRO_E_RANGE, "slots carry 48-B records: INTEGER batches without val1/val_type/val_len/ts");
+    if ((uintptr_t)out % 16) return fail(CORRO_E_INVALID, "packed records must be 16-byte aligned");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const uint32_t n = (uint32_t)in->n;
+    if (n == 0) {
+        CORRO_HIP_TRY(hipMemsetAsync(counts_dev, 0, nranks * 8ULL, s));
+        return CORRO_OK;
+    }
+    const BatchDev bd = batch_dev(in, n);
+    uint32_t ntiles, tile, *d_counts;
+    uint64_t *d_tot;
+    if (int rc = part_tiles(ctx, n, nranks, ntiles, tile, d_counts, d_tot)) return rc;
+    hipLaunchKernelGGL(k_part_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, counts_dev, cap);
+    hipLaunchKernelGGL(k_part_pack<true>, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts, out,
+                       (uint32_t *)nullptr, cap);
+    CORRO_HIP_TRY(hipGetLastError());
+    (void)d_tot;
+    return CORRO_OK;  // (no host wait: everything is queued on ctx->stream)
+}
+
+extern "C" int corro_unpack_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t cap,
+                                  const uint64_t *src_counts_dev, corro_changes *out, uint32_t *ap, uint32_t *overflow_dev) {
+    if (!ctx || !recs || !src_counts_dev || !out || !ap || !overflow_dev) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nsrc == 0 || nsrc > (uint32_t)PART_MAX_RANKS) return fail(CORRO_E_RANGE, "1..64 source ranks");
+    if (cap == 0 || (uint64_t)nsrc * cap >= (1ULL << 31)) return fail(CORRO_E_RANGE, "slots: nsrc * cap < 2^31 records");
+    if (!out->pk || !out->table_cid || !out->col_version || !out->db_version || !out->cl || !out->seq ||
+        !out->site || !out->val0)
+        return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    BatchOut bo{const_cast<uint64_t *>(out->pk),     const_cast<uint32_t *>(out->table_cid),
+                const_cast<int64_t *>(out->col_version), const_cast<int64_t *>(out->db_version),
+                const_cast<uint32_t *>(out->cl),     const_cast<uint32_t *>(out->seq),
+                const_cast<uint32_t *>(out->site),   const_cast<uint64_t *>(out->val0),
+                nullptr, nullptr, nullptr, nullptr};
+    const uint64_t n = (uint64_t)nsrc * cap;
+    hipLaunchKernelGGL(k_unpack_slots, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
+                       static_cast<const PackedRec48 *>(recs), nsrc, cap, src_counts_dev, bo, ap, overflow_dev);
+    CORRO_HIP_TRY(hipGetLastError());
     return CORRO_OK;
 }
 

@@ -35,6 +35,7 @@ struct BatchDev {
     // AP_SKIP for a change that is not applied; null: position i
     const uint32_t *ap;
     uint32_t n;
+    uint32_t ap_all;  // position mode with every change applied: the histogram need not read ap
 };
 constexpr uint32_t AP_SKIP = 0xFFFFFFFFu;
 

@@ -111,6 +111,59 @@ def exchange_var(recs, var, counts, vcounts, group=None):
     return out, vout, rcounts, rvar
 
 
+def slot_cap(n_max, world):
+    """Records per (source, destination) slot of the stream-ordered exchange: the even share of the
+    largest rank's batch plus 8 standard deviations of a uniform hash split and a small floor, so a
+    slot overflows only under skew (then the exchange repeats with exact sizes)."""
+    share = n_max / world
+    return int(share + 8.0 * share ** 0.5 + 256)
+
+
+def distributed_apply_slots(engine, batch, cap, group=None):
+    """The stream-ordered form of distributed_apply for INTEGER batches (no impact flags): partition
+    into fixed slots of `cap` 48-B records per destination (slot_cap; the same cap on every rank), the
+    per-slot counts and the slots in two all-to-alls with EQUAL splits, unpack at the same indices and
+    a mapped merge that skips the padding -- every step queued on the engine's stream (the collectives
+    run under torch.cuda.stream(engine.stream())), so no host wait separates partition and merge.
+    A rank whose incoming slot overflowed merges nothing in that pass; after it, one tiny all-reduce
+    tells every rank, and the exact-size exchange (distributed_apply) repeats for those ranks only.
+    Returns the number of ranks that overflowed (0 in the common case)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if world == 1:
+        engine.apply(batch)
+        return 0
+    st = engine.stream()
+    st.wait_stream(torch.cuda.current_stream())  # the batch's producer (device-side wait)
+    gloo = dist.get_backend(group) == "gloo"
+    with torch.cuda.stream(st):
+        recs, cnt = engine.partition_slots(batch, world, cap)
+        if gloo:  # (no device all-to-all in gloo: rehearsals stage through host memory)
+            rc = torch.empty(world, dtype=torch.int64)
+            dist.all_to_all_single(rc, cnt.cpu(), group=group)
+            got = torch.empty(recs.numel(), dtype=torch.uint8)
+            dist.all_to_all_single(got, recs.cpu(), group=group)
+            rcnt, got = rc.to(recs.device), got.to(recs.device)
+        else:
+            rcnt = torch.empty_like(cnt)
+            dist.all_to_all_single(rcnt, cnt, group=group)
+            got = torch.empty_like(recs)
+            dist.all_to_all_single(got, recs, group=group)
+        mine = engine.unpack_slots(got, world, cap, rcnt)
+        engine.apply_mapped(mine)
+    over = mine["overflow"].to(torch.int64)  # (after the merge: the apply has returned)
+    tot = over.cpu() if gloo else over.clone()
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
+    nover = int(tot.item())
+    if nover:
+        recs2, rb, counts, _ = engine.partition_packed(batch, world)
+        got2, _rc2 = exchange_records(recs2, rb, counts, group)
+        if int(over.item()):
+            engine.apply(engine.unpack_records(got2, rb))
+    return nover
+
+
 def site_digest(engine):
     """sha256 of the engine's site table (16-byte ids in ordinal order)."""
     return hashlib.sha256(b"".join(engine.site_ids())).digest()

@@ -441,6 +441,59 @@ class MergeEngine:
         out["val_data"] = var
         return out
 
+    # ---- stream-ordered slot exchange (corro_partition_slots / corro_unpack_slots) ------------
+    def stream(self):
+        """The engine's HIP stream as a torch stream: collectives issued under
+        `torch.cuda.stream(engine.stream())` are ordered with the engine's kernels without a host wait."""
+        import torch
+        if getattr(self, "_tstream", None) is None:
+            self._tstream = torch.cuda.ExternalStream(L.lib().corro_ctx_stream(self._h), device=self.device)
+        return self._tstream
+
+    def partition_slots(self, batch, nranks, cap, out=None, counts=None):
+        """Stable pk-hash partition of an INTEGER device batch into fixed slots of `cap` 48-B records
+        per destination (corro_partition_slots): returns (uint8 tensor of nranks * cap * 48, int64
+        tensor of the true per-destination counts) -- both written on the engine's stream, nothing
+        read back (a count past cap means that slot lost records: corro_unpack_slots reports it)."""
+        import torch
+        s = self._device_changes(batch)
+        dev = batch["pk"].device
+        if out is None:
+            out = torch.empty(nranks * cap * 48, dtype=torch.uint8, device=dev)
+        if counts is None:
+            counts = torch.empty(nranks, dtype=torch.int64, device=dev)
+        L.check(L.lib().corro_partition_slots(self._h, C.byref(s), nranks, cap, out.data_ptr(), counts.data_ptr()))
+        return out, counts
+
+    def unpack_slots(self, recs, nsrc, cap, src_counts, out=None):
+        """Received slots -> (SoA device batch of nsrc * cap changes at the same indices, ap int32
+        tensor: i for a received change, -1 for padding, overflow int32 tensor [1]) on the engine's
+        stream (corro_unpack_slots); merge with apply_mapped."""
+        import torch
+        n = nsrc * cap
+        dev = recs.device
+        if out is None:
+            tdt = {np.uint64: torch.int64, np.int64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}
+            out = {k: torch.empty(max(n, 1), dtype=tdt[BATCH_FIELDS[k]], device=dev)[:n] for k in REQUIRED}
+            out["ap"] = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+            out["overflow"] = torch.zeros(1, dtype=torch.int32, device=dev)
+        s = L.Changes()
+        s.n = n
+        for k in BATCH_FIELDS:
+            a = out.get(k) if k in REQUIRED else None
+            setattr(s, k, a.data_ptr() if (a is not None and n) else None)
+        L.check(L.lib().corro_unpack_slots(self._h, recs.data_ptr(), nsrc, cap, src_counts.data_ptr(), C.byref(s),
+                                           out["ap"].data_ptr(), out["overflow"].data_ptr()))
+        return out
+
+    def apply_mapped(self, batch, impact=False):
+        """corro_apply_mapped: merge a device batch whose changes with ap == -1 (batch["ap"]) are
+        skipped, the rest in index order (the slot layout of unpack_slots)."""
+        fields = {k: v for k, v in batch.items() if k in BATCH_FIELDS}
+        s, o, _keep, imp, n, _on_dev, impact = self.prepare(fields, impact)
+        L.check(L.lib().corro_apply_mapped(self._h, C.byref(s), batch["ap"].data_ptr(), C.byref(o)))
+        return imp[:n] if impact else None
+
     def unpack_records(self, recs, rec_bytes, out=None):
         """Packed records (a uint8 CUDA tensor) -> SoA device batch (corro_unpack_records)."""
         import torch

@@ -304,6 +304,28 @@ int corro_partition_packed(corro_ctx *ctx, const corro_changes *in, uint32_t nra
  * arrays, n each; optional arrays may be NULL). rec_bytes = 48 or 80. */
 int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n, uint32_t rec_bytes, corro_changes *out);
 
+/* Stream-ordered form of the packed exchange (no host round trip between partition and merge):
+ * destination r's 48-B records go to the fixed slot out[r * cap, r * cap + cap) (in input order,
+ * records past cap are not written), and counts_dev[r] (DEVICE u64) receives the true count. Every
+ * launch is queued on the context's stream (corro_ctx_stream), so an all-to-all with EQUAL splits
+ * of cap records (RCCL on that stream) needs no host-side sizes. PLAIN batches only (48-B records). */
+int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, uint64_t cap, void *out,
+                          uint64_t *counts_dev);
+/* Received slots (nsrc slots of cap records, src_counts_dev[s] = DEVICE count source s sent) ->
+ * the SoA batch at the same indices (device, nsrc * cap each) and ap[i] = i for a received record,
+ * CORRO_AP_SKIP for a slot's padding; *overflow_dev (device u32) = 1 when a source sent more than
+ * cap (its records past cap are lost: every ap is then CORRO_AP_SKIP, so the apply is a no-op and
+ * the caller repeats the exchange with exact sizes). Queued on the context's stream. */
+#define CORRO_AP_SKIP 0xFFFFFFFFu
+int corro_unpack_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t cap, const uint64_t *src_counts_dev,
+                       corro_changes *out, uint32_t *ap, uint32_t *overflow_dev);
+/* corro_apply_batch over a DEVICE batch whose changes i with ap[i] == CORRO_AP_SKIP are not applied
+ * (the others apply in index order): the slot layout above, merged without compacting it. */
+int corro_apply_mapped(corro_ctx *ctx, const corro_changes *in, const uint32_t *ap, corro_apply_out *out);
+/* The HIP stream every launch of the context is queued on (a hipStream_t), for callers that order
+ * their own collectives (RCCL) with the engine's kernels without a host wait. */
+void *corro_ctx_stream(corro_ctx *ctx);
+
 /* The exchange for EVERY table (interned pks, long values): 80-B records like corro_partition_packed
  * plus a second stream of variable-length bytes per record -- the canonical packed pk of a change to
  * an interned table (so the receiver keys the row in ITS own row-key space) and a long TEXT/BLOB

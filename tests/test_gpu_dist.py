@@ -226,3 +226,52 @@ def test_partition_var_routes_unregistered_table_ids():
         with pytest.raises(ca.CorroError):
             eng.apply(got)
         eng.close()
+
+
+# ---- stream-ordered slot exchange (distributed_apply_slots) -------------------------------------
+NS = 50000
+
+
+def _slots_worker(rank, world, port, outdir, cap_scale):
+    import torch.distributed as dist
+    import corrosion_amd as ca
+    from corrosion_amd.dist import distributed_apply_slots, rank_of_np, slot_cap
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = synth.uniform_batch(NS, 16, 4000, 4, 77)
+    lo, hi = rank * NS // world, (rank + 1) * NS // world
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS, device=0)
+    eng.register_sites(synth.site_ids(16, 5))
+    cap = max(1, int(slot_cap(hi - lo, world) * cap_scale))
+    nover = distributed_apply_slots(eng, _to_dev({k: v[lo:hi] for k, v in full.items()}), cap)
+    rows = eng.export()
+    assert (rank_of_np(rows["table_cid"], rows["pk"], world) == rank).all()
+    np.save(os.path.join(outdir, f"srows{rank}.npy"), np.array(rows_to_tuples(rows, with_ts=True), dtype=object),
+            allow_pickle=True)
+    np.save(os.path.join(outdir, f"sover{rank}.npy"), np.array([nover]))
+    np.save(os.path.join(outdir, f"sdbv{rank}.npy"), np.asarray(eng.db_versions()))
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cap_scale", [1.0, 0.3], ids=["slots_fit", "slots_overflow_repeat"])
+def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale):
+    """distributed_apply_slots: fixed slots, equal-split all-to-alls on the engine's stream, a mapped
+    merge that skips the padding; with slots too small (0.3 x) every rank overflows, merges nothing in
+    the slot pass and repeats with the exact-size exchange -- the union of the rank states equals one
+    engine's merge of the whole batch either way."""
+    import corrosion_amd as ca
+    world = 2
+    mp.spawn(_slots_worker, args=(world, _free_port(), str(tmp_path), cap_scale), nprocs=world, join=True)
+    got = []
+    for r in range(world):
+        got += [tuple(x) for x in np.load(tmp_path / f"srows{r}.npy", allow_pickle=True)]
+    nover = int(np.load(tmp_path / "sover0.npy")[0])
+    assert (nover == 0) == (cap_scale == 1.0)
+    e = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS)
+    e.register_sites(synth.site_ids(16, 5))
+    e.apply(synth.uniform_batch(NS, 16, 4000, 4, 77))
+    assert sorted(got) == rows_to_tuples(e.export(), with_ts=True)
+    dbv = np.max([np.load(tmp_path / f"sdbv{r}.npy") for r in range(world)], axis=0)
+    assert list(dbv) == list(e.db_versions())
