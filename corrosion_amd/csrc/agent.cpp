@@ -38,6 +38,7 @@ void corro_detail_add_committed(corro_ctx *ctx, const uint64_t *counts, size_t n
 namespace corro {
 int fail(int code, const std::string &msg);
 int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version);
+int set_db_versions(corro_ctx *ctx, const std::vector<std::pair<uint32_t, uint64_t>> &sv);
 }  // namespace corro
 
 #define TRY_RC(x)                        \
@@ -68,11 +69,43 @@ struct SeqBook {  // __corro_seq_bookkeeping rows of one (site, version)
     uint64_t last_seq = 0, ts = 0;
 };
 
+// The __corro_buffered_changes rows of one (site, db_version): one vector sorted by seq, unique seqs
+// (a node per version, not per row: a call can buffer millions of rows).
+using BufRows = std::vector<HostRow>;
+
+bool seq_less(const HostRow &a, const HostRow &b) { return a.seq < b.seq; }
+
+// INSERT ... ON CONFLICT (site_id, db_version, seq) DO NOTHING of rows [first, last) into dst:
+// the first row of each seq wins (rows already stored, then earlier rows of the batch)
+void buf_insert(BufRows &dst, HostRow *first, HostRow *last) {
+    std::stable_sort(first, last, seq_less);
+    BufRows out;
+    out.reserve(dst.size() + (size_t)(last - first));
+    auto a = dst.begin();
+    for (HostRow *b = first; b != last;) {
+        if (a != dst.end() && a->seq <= b->seq) {
+            if (a->seq == b->seq)  // the stored row wins; drop every batch row of that seq
+                for (const uint32_t q = b->seq; b != last && b->seq == q;) ++b;
+            out.push_back(std::move(*a++));
+            continue;
+        }
+        out.push_back(std::move(*b));
+        const uint32_t q = b->seq;
+        for (++b; b != last && b->seq == q;) ++b;  // later rows of the same seq
+    }
+    for (; a != dst.end(); ++a) out.push_back(std::move(*a));
+    dst.swap(out);
+}
+
+BufRows::const_iterator buf_lower(const BufRows &v, uint32_t seq) {
+    return std::lower_bound(v.begin(), v.end(), seq, [](const HostRow &r, uint32_t q) { return r.seq < q; });
+}
+
 }  // namespace
 
 struct corro_bookie {
     std::map<ActorId, corro::Booked> actors;                  // Bookie (agent.rs:1546-1598)
-    std::map<std::pair<uint32_t, int64_t>, std::map<uint32_t, HostRow>> buffered;  // (site, dbv) -> seq -> row
+    std::map<std::pair<uint32_t, int64_t>, BufRows> buffered;  // (site, dbv) -> rows by seq
     std::map<std::pair<uint32_t, uint64_t>, SeqBook> seqbook;  // (site, version)
     std::vector<std::pair<ActorId, uint64_t>> ready;           // fully buffered, to apply
     std::map<ActorId, uint32_t> site_of;                       // actor -> site ordinal
@@ -188,6 +221,33 @@ int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset
     out.last_seq = cs.last_seq;
     out.ts = cs.ts;
     return CORRO_OK;
+}
+
+// a call's buffered rows (rows of one changeset are consecutive) into the bookie, per (site, dbv)
+// key; committed[t] counts every buffered change of table t (util.rs:1101-1105)
+void commit_buffered(corro_bookie *bk, std::vector<HostRow> &rows, std::vector<uint64_t> &committed) {
+    const size_t ntables = committed.size();
+    for (size_t a = 0; a < rows.size();) {
+        size_t b = a + 1;
+        while (b < rows.size() && rows[b].site == rows[a].site && rows[b].dbv == rows[a].dbv) b++;
+        for (size_t k = a; k < b; k++)
+            if ((rows[k].tcid >> 16) < ntables) committed[rows[k].tcid >> 16]++;
+        buf_insert(bk->buffered[{rows[a].site, rows[a].dbv}], rows.data() + a, rows.data() + b);
+        a = b;
+    }
+}
+
+// sorted site << 40 | version keys of every (site, version) holding buffered rows or seq bookkeeping
+std::vector<uint64_t> buffered_keys(const corro_bookie *bk) {
+    std::vector<uint64_t> k;
+    k.reserve(bk->buffered.size() + bk->seqbook.size());
+    for (const auto &[key, rows] : bk->buffered)
+        if (key.second >= 0 && (uint64_t)key.second < (1ULL << 40)) k.push_back((uint64_t)key.first << 40 | (uint64_t)key.second);
+    for (const auto &[key, sb] : bk->seqbook)
+        if (key.second < (1ULL << 40)) k.push_back((uint64_t)key.first << 40 | key.second);
+    std::sort(k.begin(), k.end());
+    k.erase(std::unique(k.begin(), k.end()), k.end());
+    return k;
 }
 
 void clear_buffered(corro_bookie *bk, uint32_t site, uint64_t vs, uint64_t ve) {
@@ -358,7 +418,7 @@ struct ActorWork {
     bool had_max = false;
     uint64_t max = 0;
     bool fast = false;                // every changeset a complete Full version, ascending (arrival order)
-    const uint64_t *idx = nullptr;    // (not fast) changesets in arrival order
+    const uint64_t *idx = nullptr;    // (not fast) changesets the walk takes, in arrival order
     uint64_t nidx = 0;
     // results (not fast: the per-actor passes; fast ones are counted per chunk)
     uint64_t nspans = 0, nchanges = 0;
@@ -395,16 +455,17 @@ struct CsView {
 };
 
 // One actor's passes 1 and 2 (util.rs:704-884) over its changesets w.idx (arrival order) unless it
-// is fast (its versions are the runs given), then its gap snapshot (:894-932) and partials.
+// is fast, plus the versions of the runs given (decided elsewhere: a fast actor's, or the device's
+// isolated changesets, which share no version with w.idx), then its gap snapshot (:894-932) and
+// partials.
 template <class RowOf>
 void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::vector<Range> &fast_runs, RowOf &&row_of) {
     corro::Booked &booked = *w.booked;
     const bool had_max = w.had_max;
     const uint64_t max = w.max;
     RangeSet versions;
-    if (w.fast) {
-        for (const Range &r : fast_runs) versions.insert(r.first, r.second);
-    } else {
+    for (const Range &r : fast_runs) versions.insert(r.first, r.second);
+    if (!w.fast) {
         // pass 1: batch-local dedup of (versions, seqs), then versions the actor already holds
         std::vector<uint64_t> unknown;
         unknown.reserve(w.nidx);
@@ -482,8 +543,8 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
 namespace {
 
 // corro_process_multiple_changes with CORRO_MEM_DEVICE_HEADERS: the header passes on the device
-// (agent_dev_headers), the host walks only slow actors' headers, then the same merge / impacts /
-// commit as the host-header path.
+// (agent_dev_headers decides every changeset its actor's other changesets do not overlap), the host
+// walks only the rest, then the same merge / impacts / commit as the host-header path.
 int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *dcs, uint64_t ncs,
                         const corro_changes *in, corro_process_out *out) {
     static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;
@@ -515,22 +576,16 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     if (R.err & 2) return fail(CORRO_E_INVALID, "changeset site ordinal is not registered (or actor_id is NULL)");
     stage("headers");
 
-    // actors of the call; the slow ones' headers come to the host (sorted order = grouped by actor,
-    // arrival order inside)
+    // actors of the call, each with its host changesets (R.hcs: grouped by actor in site-rank order)
     std::vector<ActorWork> work;
     std::vector<int64_t> work_of(nsites, -1);
-    std::vector<std::pair<uint32_t, uint32_t>> slow_ranges;
     for (uint32_t t = 0; t < nsites; t++) {
-        const corro::DevHdrSite &g = R.sites[t];
-        if (g.gstart == 0xFFFFFFFFu) continue;
+        if (R.sites[t].gstart == 0xFFFFFFFFu) continue;
         work_of[t] = (int64_t)work.size();
         work.emplace_back();
         ActorWork &w = work.back();
         w.site = t;
         w.id = site_id[t];
-        w.fast = !g.slow;
-        w.nidx = g.gend - g.gstart + 1;
-        if (g.slow) slow_ranges.emplace_back(g.gstart, g.gend + 1);
     }
     for (ActorWork &w : work) {  // Bookie::ensure
         w.booked = &bk->actors[w.id];
@@ -538,34 +593,33 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         w.had_max = w.booked->has_max;
         w.max = w.booked->max;
     }
-    std::vector<corro_changeset> hcs;
-    std::vector<uint32_t> hidx;
-    std::vector<uint8_t> hbad, hflag;
-    std::vector<int32_t> hknown;
-    std::vector<uint64_t> local;
-    std::map<uint64_t, uint64_t> inc_row;  // slow changeset (local index) -> first fetched row
+    std::vector<corro_changeset> &hcs = R.hcs;
+    std::vector<uint8_t> hflag(hcs.size(), 0);
+    std::vector<int32_t> hknown(hcs.size(), CORRO_KNOWN_SKIPPED);
+    std::vector<uint64_t> local(hcs.size());
+    std::map<uint64_t, uint64_t> inc_row;  // host changeset (local index) -> first fetched row
     corro::HostSpanRows inc;
-    if (!slow_ranges.empty()) {
-        TRY_RC(corro::agent_dev_slow_headers(ctx, dcs, slow_ranges, hcs, hidx, hbad));
-        hflag.assign(hcs.size(), 0);
-        hknown.assign(hcs.size(), CORRO_KNOWN_SKIPPED);
-        local.resize(hcs.size());
+    if (!hcs.empty()) {
         for (uint64_t k = 0; k < local.size(); k++) local[k] = k;
-        uint64_t o = 0;
-        for (ActorWork &w : work)  // (work and slow_ranges are both in site-ordinal order)
-            if (!w.fast) {
-                w.idx = local.data() + o;
-                o += w.nidx;
-            }
+        for (uint64_t k = 0; k < hcs.size();) {
+            uint64_t e = k + 1;
+            while (e < hcs.size() && hcs[e].site == hcs[k].site) e++;
+            ActorWork &w = work[(size_t)work_of[hcs[k].site]];
+            w.idx = local.data() + k;
+            w.nidx = e - k;
+            k = e;
+        }
         std::vector<corro::AgentSpan> sp;
         uint64_t r = 0;
         for (uint64_t k = 0; k < hcs.size(); k++)
-            if (hcs[k].kind == CORRO_CS_FULL && hcs[k].change_count && !is_complete(hcs[k]) && !hbad[k]) {
+            if (hcs[k].kind == CORRO_CS_FULL && hcs[k].change_count && !is_complete(hcs[k]) && !R.hbad[k]) {
                 inc_row[k] = r;
                 sp.push_back({hcs[k].change_off, r, hcs[k].change_count, hcs[k].ts});
                 r += hcs[k].change_count;
             }
+        stage("host_headers");
         if (!sp.empty()) TRY_RC(corro::agent_dev_fetch(ctx, &dv, sp, inc));
+        stage("partial_rows");
     }
     auto row_of = [&](const corro_changeset &c, uint64_t ci, uint64_t k) -> HostRow {
         const uint64_t j = inc_row.at(ci) + k;
@@ -586,11 +640,11 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             r.lv.assign(reinterpret_cast<const char *>(inc.lv_data.data() + inc.lv_off[j]), inc.lv_len[j]);
         return r;
     };
-    std::vector<std::vector<Range>> fast_runs(work.size());
+    std::vector<std::vector<Range>> dev_runs(work.size());
     for (size_t r = 0; r < R.run_site.size(); r++)
-        fast_runs[(size_t)work_of[R.run_site[r]]].emplace_back(R.run_start[r], R.run_end[r]);
-    const CsView view{hcs.data(), hbad.data(), hknown.data(), hflag.data()};
-    run_parallel(work.size(), [&](size_t k) { run_actor_walk(bk, work[k], view, fast_runs[k], row_of); });
+        dev_runs[(size_t)work_of[R.run_site[r]]].emplace_back(R.run_start[r], R.run_end[r]);
+    const CsView view{hcs.data(), R.hbad.data(), hknown.data(), hflag.data()};
+    run_parallel(work.size(), [&](size_t k) { run_actor_walk(bk, work[k], view, dev_runs[k], row_of); });
     for (ActorWork &w : work)
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);
     uint64_t nspans = R.nspans, nb = R.nchanges;
@@ -598,7 +652,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         nspans += w.nspans;
         nb += w.nchanges;
     }
-    if (!hcs.empty()) TRY_RC(corro::agent_dev_put_slow(ctx, hidx, hflag, hknown, out->known));
+    if (!hcs.empty()) TRY_RC(corro::agent_dev_put_host(ctx, R.hidx, hflag, hknown, out->known));
     stage("actors");
 
     const uint32_t ntables = corro::agent_table_count(ctx);
@@ -633,19 +687,23 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     }
 
     // commit
-    for (ActorWork &w : work)
-        for (uint64_t version : w.set_dbv) TRY_RC(corro::set_db_version(ctx, w.site, version));
+    {  // crsql_set_db_version of every processed empty version, one device pass
+        std::vector<std::pair<uint32_t, uint64_t>> sv;
+        for (ActorWork &w : work)
+            for (uint64_t version : w.set_dbv) sv.emplace_back(w.site, version);
+        TRY_RC(corro::set_db_versions(ctx, sv));
+    }
     for (ActorWork &w : work) {
-        for (const HostRow &r : w.st.buffered) {  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
-            bk->buffered[{r.site, r.dbv}].emplace(r.seq, r);
-            if ((r.tcid >> 16) < ntables) committed[r.tcid >> 16]++;
-        }
+        commit_buffered(bk, w.st.buffered, committed);
         for (auto &[key, sb] : w.st.seqbook) bk->seqbook[key] = sb;
     }
-    const bool clear_meta = !bk->buffered.empty() || !bk->seqbook.empty();
+    stage("commit_buffered");
+    // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303): the merged versions that hold
+    // buffered rows or seq bookkeeping, found on the device against the (small) set of such keys
+    std::vector<uint64_t> bkeys = buffered_keys(bk);
     std::vector<std::pair<uint32_t, uint64_t>> sv;
-    TRY_RC(corro::agent_dev_commit_headers(ctx, ncs, out->known, clear_meta ? &sv : nullptr));
-    for (auto &[site, v] : sv) clear_buffered(bk, site, v, v);  // check_buffered_meta_to_clear
+    TRY_RC(corro::agent_dev_commit_headers(ctx, ncs, out->known, bkeys.empty() ? nullptr : &bkeys, &sv));
+    for (auto &[site, v] : sv) clear_buffered(bk, site, v, v);
     std::vector<size_t> order(work.size());
     for (size_t k = 0; k < order.size(); k++) order[k] = k;
     std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return work[x].id < work[y].id; });
@@ -659,7 +717,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     out->n_ready = nready;
     corro_detail_add_committed(ctx, committed.data(), committed.size());
     stage("commit");
-    if (prof) fprintf(stderr, "[corro agent dev] ncs=%llu spans=%llu changes=%llu slow=%zu ms:%s\n", (unsigned long long)ncs,
+    if (prof) fprintf(stderr, "[corro agent dev] ncs=%llu spans=%llu changes=%llu host=%zu ms:%s\n", (unsigned long long)ncs,
                       (unsigned long long)nspans, (unsigned long long)nb, hcs.size(), prof_line.c_str());
     return CORRO_OK;
 }
@@ -908,7 +966,9 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
                 sp.push_back({cs[i].change_off, r, cs[i].change_count, cs[i].ts});
                 r += cs[i].change_count;
             }
+        stage("slow_headers");
         if (!sp.empty()) TRY_RC(corro::agent_dev_fetch(ctx, &dv, sp, inc));
+        stage("partial_rows");
     }
     auto row_of = [&](const corro_changeset &c, uint64_t ci, uint64_t k) -> HostRow {
         if (mem == CORRO_MEM_HOST) return row_at(in, c.change_off + k, c.ts);
@@ -1037,21 +1097,22 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
     }
 
     // 5. commit: everything below only records what the successful transaction did
-    for (const ChunkOut &o : cout)
-        for (auto &[wi, version] : o.set_dbv) TRY_RC(corro::set_db_version(ctx, work[wi].site, version));
-    for (ActorWork &w : work)
-        for (uint64_t version : w.set_dbv) TRY_RC(corro::set_db_version(ctx, w.site, version));
+    {  // crsql_set_db_version of every processed empty version, one device pass
+        std::vector<std::pair<uint32_t, uint64_t>> sv;
+        for (const ChunkOut &o : cout)
+            for (auto &[wi, version] : o.set_dbv) sv.emplace_back(work[wi].site, version);
+        for (ActorWork &w : work)
+            for (uint64_t version : w.set_dbv) sv.emplace_back(w.site, version);
+        TRY_RC(corro::set_db_versions(ctx, sv));
+    }
     // corro.changes.committed{table} (util.rs:533-535): every buffered change of an incomplete version
     // (:1101-1105), every impactful change of a complete one (:1254-1258, counted on the device)
     for (ActorWork &w : work) {
-        for (const HostRow &r : w.st.buffered) {  // ON CONFLICT (site_id, db_version, seq) DO NOTHING
-            bk->buffered[{r.site, r.dbv}].emplace(r.seq, r);
-            if ((r.tcid >> 16) < ntables) committed[r.tcid >> 16]++;
-        }
+        commit_buffered(bk, w.st.buffered, committed);
         for (auto &[key, sb] : w.st.seqbook) bk->seqbook[key] = sb;
     }
     // known: Current when the version had an impactful change, else Cleared (util.rs:1264-1287)
-    const bool clear_meta = !bk->buffered.empty() || !bk->seqbook.empty();
+    const std::vector<uint64_t> bkeys = buffered_keys(bk);
     if (nspans)
         run_parallel(nchunk, [&](size_t k) {
             uint64_t lo, hi;
@@ -1060,9 +1121,11 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
                 if (P.flag[i]) out->known[i] = P.any[i] ? CORRO_KNOWN_CURRENT : CORRO_KNOWN_CLEARED;
         }, 1);
     // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303)
-    if (clear_meta)
+    if (!bkeys.empty())
         for (uint64_t i = 0; i < ncs; i++)
-            if (P.flag[i]) clear_buffered(bk, cs[i].site, cs[i].version_start, cs[i].version_start);
+            if (P.flag[i] && cs[i].version_start < (1ULL << 40) &&
+                std::binary_search(bkeys.begin(), bkeys.end(), (uint64_t)cs[i].site << 40 | cs[i].version_start))
+                clear_buffered(bk, cs[i].site, cs[i].version_start, cs[i].version_start);
     // per-actor gap snapshot commit, then partials (util.rs:936-1008), actors in ActorId order
     std::vector<size_t> order(work.size());
     for (size_t k = 0; k < order.size(); k++) order[k] = k;
@@ -1132,7 +1195,7 @@ int corro_process_fully_buffered(corro_ctx *ctx, corro_bookie *bk, const uint8_t
     Batch batch;
     auto rows = bk->buffered.find({site, (int64_t)version});
     if (rows != bk->buffered.end())
-        for (auto &kv : rows->second) batch.push(kv.second);  // ORDER BY db_version, seq
+        for (const HostRow &r : rows->second) batch.push(r);  // ORDER BY db_version, seq
     RangeSet v;
     v.insert(version, version);
     corro::Booked nb = booked;  // committed only with the merge (one transaction, util.rs:560-676)
@@ -1253,9 +1316,9 @@ int corro_bookie_buffered(corro_bookie *bk, const uint8_t *actor_id, uint64_t ve
     if (it == bk->buffered.end() || seq_start > seq_end || seq_start > 0xFFFFFFFFULL) return CORRO_OK;
     const uint32_t hi = seq_end > 0xFFFFFFFFULL ? 0xFFFFFFFFu : (uint32_t)seq_end;
     uint64_t k = 0;
-    for (auto r = it->second.lower_bound((uint32_t)seq_start); r != it->second.end() && r->first <= hi; ++r, ++k) {
+    for (auto r = buf_lower(it->second, (uint32_t)seq_start); r != it->second.end() && r->seq <= hi; ++r, ++k) {
         if (k >= cap) continue;
-        const HostRow &h = r->second;
+        const HostRow &h = *r;
         if (o->pk) o->pk[k] = h.pk;
         if (o->table_cid) o->table_cid[k] = h.tcid;
         if (o->col_version) o->col_version[k] = h.cv;
@@ -1282,9 +1345,9 @@ int corro_bookie_buffered_value(corro_bookie *bk, const uint8_t *actor_id, uint6
     if (so == bk->site_of.end() || seq > 0xFFFFFFFFULL) return CORRO_OK;
     auto it = bk->buffered.find({so->second, (int64_t)version});
     if (it == bk->buffered.end()) return CORRO_OK;
-    auto r = it->second.find((uint32_t)seq);
-    if (r == it->second.end()) return CORRO_OK;
-    const std::string &lv = r->second.lv;
+    auto r = buf_lower(it->second, (uint32_t)seq);
+    if (r == it->second.end() || r->seq != (uint32_t)seq) return CORRO_OK;
+    const std::string &lv = r->lv;
     *len = lv.size();
     std::memcpy(out, lv.data(), std::min<uint64_t>(cap, lv.size()));
     return CORRO_OK;

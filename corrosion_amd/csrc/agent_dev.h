@@ -92,41 +92,43 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
 // ---- device-resident headers (CORRO_MEM_DEVICE_HEADERS) -----------------------------------------
 // The changeset headers, out->known and out->impactful live on the device. One pass per changeset
 // (span check, unknown-name screen, columns), one stable sort by site rank (the application order
-// and the per-actor grouping at once), one pass per sorted slot that decides every "fast" actor
-// (each of its changesets a complete Full version, strictly ascending in arrival order, all above
-// the actor's booked max) on the device: flags, known, empty versions, and the actor's applied
-// version runs for the gap bookkeeping. The host gets per-site summaries and the runs; it walks
-// only the headers of the other ("slow") actors, fetched in sorted order.
+// and the per-actor grouping at once), a second by (site rank, version start) that decides every
+// changeset nothing else of its actor in the call overlaps and whose versions are all above the
+// actor's booked max (a complete Full version: merged / rolled back; an empty one or an Empty range:
+// cleared; later copies of its dedup key: skipped), and the decided versions' runs for the gap
+// bookkeeping. The host gets per-site summaries, the runs, and the headers of the other ("host")
+// changesets, which it walks with the reference's per-actor passes.
 struct DevHdrSite {
     uint32_t gstart, gend;   // sorted slots [gstart, gend] of the site's changesets (gstart ~0: none)
-    uint8_t slow;            // 1: the host walks this actor's changesets
 };
 struct DevHdrResult {
     uint32_t err;            // bit 0 span outside the batch, bit 1 site ordinal not registered
     bool ts_any;             // some changeset has a non-zero ts
-    uint64_t nspans, nchanges;   // flagged (fast actors) changesets and their changes
+    uint64_t nspans, nchanges;   // changesets merged by a device decision and their changes
     std::vector<DevHdrSite> sites;             // per site ordinal
-    std::vector<uint32_t> run_site;            // fast actors' version runs, grouped by site, ascending
+    std::vector<uint32_t> run_site;            // decided version runs, grouped by site, ascending
     std::vector<uint64_t> run_start, run_end;
+    // the host's changesets in sorted order (grouped by actor, arrival order inside): header, arrival
+    // index, unknown-name flag
+    std::vector<corro_changeset> hcs;
+    std::vector<uint32_t> hidx;
+    std::vector<uint8_t> hbad;
 };
 // site_max[s] = the actor's booked max (-1: none); dknown: device, ncs entries
 int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, const corro_changes *dv,
                       const std::vector<int64_t> &site_max, int32_t *dknown, DevHdrResult &res);
-// host copies of the changesets in sorted slots [lo, hi) of each (lo, hi) range, concatenated, with
-// their arrival index and bad flag
-int agent_dev_slow_headers(corro_ctx *ctx, const corro_changeset *dcs, const std::vector<std::pair<uint32_t, uint32_t>> &ranges,
-                           std::vector<corro_changeset> &hcs, std::vector<uint32_t> &idx, std::vector<uint8_t> &bad);
-// the host's decisions for slow changesets: flag[idx[k]] = flag[k], known[idx[k]] = known[k]
-int agent_dev_put_slow(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
+// the host's decisions for its changesets: flag[idx[k]] = flag[k], known[idx[k]] = known[k]
+int agent_dev_put_host(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
                        const std::vector<int32_t> &known, int32_t *dknown);
 // the applied batch in sorted order (flagged changesets only), like agent_dev_batch
 int agent_dev_batch_sorted(corro_ctx *ctx, const corro_changes *dv, uint64_t ncs, uint64_t nspans, uint64_t nbatch,
                            bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm);
 // after a successful merge: known of flagged changesets (Current / Cleared by p.any on the device),
-// crsql_set_db_version of the fast actors' empty versions; *flagged_sv (optional) = (site, version)
-// of every flagged changeset (host, for check_buffered_meta_to_clear)
-int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown,
-                             std::vector<std::pair<uint32_t, uint64_t>> *flagged_sv);
+// crsql_set_db_version of the device-decided empty versions; with `keys` (sorted site << 40 | version
+// keys holding buffered meta) *hits = the (site, version) of every flagged changeset among them (a
+// device binary search per changeset, for check_buffered_meta_to_clear)
+int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown, const std::vector<uint64_t> *keys,
+                             std::vector<std::pair<uint32_t, uint64_t>> *hits);
 
 // Host headers staged for the device header passes (CORRO_MEM_DEVICE with host headers, large
 // calls): a pinned area the host fills in parallel chunks, each chunk uploaded as soon as it is

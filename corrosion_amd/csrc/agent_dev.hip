@@ -30,6 +30,8 @@ int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t 
                    uint32_t *vo, uint32_t n, uint32_t end_bit, hipStream_t s);
 int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, uint32_t *out, uint32_t n,
                             hipStream_t s);
+int prim_segmax_scan_u64(void *temp, size_t *temp_bytes, const uint32_t *keys, const uint64_t *in, uint64_t *out,
+                         uint32_t n, hipStream_t s);
 
 namespace {
 
@@ -381,10 +383,12 @@ struct DevCols {
 };
 
 size_t sort_temp_bytes(uint64_t n) {
-    size_t t0 = 0, t1 = 0;
-    ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, (uint32_t)std::max<uint64_t>(n, 1), 32, nullptr);
-    prim_inclusive_scan_u32(nullptr, &t1, nullptr, nullptr, (uint32_t)std::max<uint64_t>(n, 1), nullptr);
-    return std::max(t0, t1);
+    size_t t0 = 0, t1 = 0, t2 = 0;
+    const uint32_t m = (uint32_t)std::max<uint64_t>(n, 1);
+    ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, m, 64, nullptr);
+    prim_inclusive_scan_u32(nullptr, &t1, nullptr, nullptr, m, nullptr);
+    prim_segmax_scan_u64(nullptr, &t2, nullptr, nullptr, nullptr, m, nullptr);
+    return std::max(std::max(t0, t1), t2);
 }
 
 DevCols dev_cols(corro_ctx *ctx, size_t *total = nullptr) {
@@ -759,30 +763,40 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
 // ---- device-resident headers ------------------------------------------------------------------
 namespace {
 
-// Header-mode columns in d_agent_hdr (n = changesets, m = sites):
-//   ver u64[n] | comp u8[n] | inrun u8[n] | emp u8[n] | rflag u32[n] | rincl u32[n] | run_site u32[n]
-//   | run_start u64[n] | run_end u64[n] | site_max i64[m] | slow u8[m] | gstart u32[m] | gend u32[m]
-//   | ctl u64[8] (0 err, 1 ts_any, 2 nspans, 3 nchanges)
+// Header-mode columns in d_agent_hdr (n = changesets, m = sites), per changeset i unless noted:
+//   ver u64 (version start) | vend u64 | kd u8 (kind, seqs flag) | dec u8 (decided on the device) |
+//   inrun u8 [slot of order2] | emp u8 (set_db_version(vend) at commit) | rflag u32 [order2] |
+//   rincl u32 [order2] | run_site u32 | run_start u64 | run_end u64 | key2 u64 | key2' u64 |
+//   val2 u32 | val2' u32 (the (rank, version) sort: order2) | segk u32 [order2] | vend2 u64 [order2] |
+//   rmax u64 [order2] | ghead u32 [order2] | gincl u32 [order2] | gfirst u32 | glast u32 |
+//   site_max i64[m] | gstart u32[m] | gend u32[m] | ctl u64[8] (0 err, 1 ts_any, 2 nspans, 3 nchanges)
 struct HdrCols {
-    uint64_t *ver;
-    uint8_t *comp, *inrun, *emp;
+    uint64_t *ver, *vend;
+    uint8_t *kd, *dec, *inrun, *emp;
     uint32_t *rflag, *rincl, *run_site;
     uint64_t *run_start, *run_end;
+    uint64_t *key2, *key2b;
+    uint32_t *val2, *val2b, *segk;
+    uint64_t *vend2, *rmax;
+    uint32_t *ghead, *gincl, *gfirst, *glast;
     int64_t *site_max;
-    uint8_t *slow;
     uint32_t *gstart, *gend;
     unsigned long long *ctl;
 };
 
 HdrCols hdr_cols(corro_ctx *ctx, uint64_t ncs, uint32_t nsites, size_t *total = nullptr) {
     const uint64_t n = std::max<uint64_t>(ncs, 1), m = std::max<uint32_t>(nsites, 1);
-    const size_t sz[] = {n * 8, n, n, n, n * 4, n * 4, n * 4, n * 8, n * 8, m * 8, m, m * 4, m * 4, 64};
-    void **slot[] = {(void **)nullptr};
-    (void)slot;
+    const size_t sz[] = {n * 8, n * 8, n, n, n, n, n * 4, n * 4, n * 4, n * 8, n * 8, n * 8, n * 8, n * 4, n * 4, n * 4,
+                         n * 8, n * 8, n * 4, n * 4, n * 4, n * 4, m * 8, m * 4, m * 4, 64};
     HdrCols h{};
-    void **dst[] = {(void **)&h.ver, (void **)&h.comp, (void **)&h.inrun, (void **)&h.emp, (void **)&h.rflag,
-                    (void **)&h.rincl, (void **)&h.run_site, (void **)&h.run_start, (void **)&h.run_end,
-                    (void **)&h.site_max, (void **)&h.slow, (void **)&h.gstart, (void **)&h.gend, (void **)&h.ctl};
+    void **dst[] = {(void **)&h.ver,   (void **)&h.vend,     (void **)&h.kd,      (void **)&h.dec,
+                    (void **)&h.inrun, (void **)&h.emp,      (void **)&h.rflag,   (void **)&h.rincl,
+                    (void **)&h.run_site, (void **)&h.run_start, (void **)&h.run_end, (void **)&h.key2,
+                    (void **)&h.key2b, (void **)&h.val2,     (void **)&h.val2b,   (void **)&h.segk,
+                    (void **)&h.vend2, (void **)&h.rmax,     (void **)&h.ghead,   (void **)&h.gincl,
+                    (void **)&h.gfirst, (void **)&h.glast,   (void **)&h.site_max,
+                    (void **)&h.gstart, (void **)&h.gend,    (void **)&h.ctl};
+    static_assert(sizeof(sz) / sizeof(sz[0]) == sizeof(dst) / sizeof(dst[0]), "one size per column");
     uint8_t *base = ctx->d_agent_hdr.as<uint8_t>();
     size_t o = 0;
     for (size_t k = 0; k < sizeof(sz) / sizeof(sz[0]); k++) {
@@ -801,10 +815,18 @@ struct HdrArgs {
     const uint32_t *site_rank;
     uint64_t *off, *cnt, *ts, *ver, *key;
     uint32_t *site, *val;
-    uint8_t *flag, *bad, *comp;
+    uint8_t *flag, *bad, *emp;
     int32_t *known;
     unsigned long long *ctl;
+    uint64_t *vend, *key2;
+    uint32_t *val2;
+    uint8_t *kd, *dec;
 };
+
+// kind byte: bits 0-1 the CORRO_CS_* kind, bit 2 a complete Full version
+constexpr uint8_t KD_COMPLETE = 4;
+// versions at or above 2^40 - 1 share one sort key (arrival order among them): never decided
+constexpr uint64_t VCLAMP = (1ULL << 40) - 1;
 
 // one thread per changeset: span check, unknown-name screen, the per-changeset columns, sort keys
 __global__ void __launch_bounds__(AG_T) k_hdr(HdrArgs a) {
@@ -823,13 +845,23 @@ __global__ void __launch_bounds__(AG_T) k_hdr(HdrArgs a) {
         a.cnt[i] = full ? c.change_count : 0;
         a.ts[i] = c.ts;
         a.site[i] = c.site;
-        a.ver[i] = c.version_start;
         a.flag[i] = 0;
+        a.emp[i] = 0;
+        a.dec[i] = 0;
         a.known[i] = CORRO_KNOWN_SKIPPED;
-        a.comp[i] = c.kind == CORRO_CS_FULL && c.seq_start == 0 && c.seq_end == c.last_seq;
+        const bool comp = c.kind == CORRO_CS_FULL && c.seq_start == 0 && c.seq_end == c.last_seq;
+        a.kd[i] = (uint8_t)((c.kind & 3u) | (comp ? KD_COMPLETE : 0));
+        // versions(): Full v..=v, Empty its range, EmptySet the dummy 0..=0 (broadcast.rs:170-178)
+        const uint64_t vs = c.kind == CORRO_CS_EMPTY_SET ? 0 : c.version_start;
+        const uint64_t ve = c.kind == CORRO_CS_EMPTY_SET ? 0 : (c.kind == CORRO_CS_EMPTY ? c.version_end : c.version_start);
+        a.ver[i] = vs;
+        a.vend[i] = ve;
         a.bad[i] = full && ok && span_has_unknown(a.tcid, c.change_off, c.change_count) ? 1 : 0;
-        a.key[i] = c.site < a.nsites ? a.site_rank[c.site] : 0;
+        const uint64_t rank = c.site < a.nsites ? a.site_rank[c.site] : 0;
+        a.key[i] = rank;
         a.val[i] = (uint32_t)i;
+        a.key2[i] = rank << 40 | (vs < VCLAMP ? vs : VCLAMP);
+        a.val2[i] = (uint32_t)i;
         tsb |= c.ts != 0;
     }
     const unsigned long long anyts = __ballot(tsb);
@@ -841,53 +873,112 @@ __global__ void __launch_bounds__(AG_T) k_hdr(HdrArgs a) {
     }
 }
 
-// per sorted slot: actor groups (gstart / gend) and the fast test; a violation marks the actor slow
+// per sorted slot (order: site rank, arrival): each actor's slots [gstart, gend]
 __global__ void __launch_bounds__(AG_T) k_hdr_sites(const uint32_t *__restrict__ order, uint64_t ncs,
-                                                     const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
-                                                     const uint8_t *__restrict__ comp, const int64_t *__restrict__ site_max,
-                                                     uint8_t *__restrict__ slow, uint32_t *__restrict__ gstart,
+                                                     const uint32_t *__restrict__ site, uint32_t *__restrict__ gstart,
                                                      uint32_t *__restrict__ gend) {
     for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
-        const uint32_t i = order[j], st = site[i];
-        const bool same_prev = j > 0 && site[order[j - 1]] == st;
-        const bool same_next = j + 1 < ncs && site[order[j + 1]] == st;
-        if (!same_prev) gstart[st] = (uint32_t)j;
-        if (!same_next) gend[st] = (uint32_t)j;
-        const int64_t mx = site_max[st];
-        const bool fast = comp[i] && (!same_prev || ver[i] > ver[order[j - 1]]) && (mx < 0 || ver[i] > (uint64_t)mx);
-        if (!fast) slow[st] = 1;
+        const uint32_t st = site[order[j]];
+        if (j == 0 || site[order[j - 1]] != st) gstart[st] = (uint32_t)j;
+        if (j + 1 == ncs || site[order[j + 1]] != st) gend[st] = (uint32_t)j;
     }
 }
 
-// per sorted slot of a fast actor: merged (flag), cleared (empty) or rolled back (unknown name);
-// version runs of the merged and cleared ones; counts of the flagged spans and changes
-__global__ void __launch_bounds__(AG_T) k_hdr_fast(const uint32_t *__restrict__ order, uint64_t ncs,
-                                                    const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
-                                                    const uint64_t *__restrict__ cnt, const uint8_t *__restrict__ bad,
-                                                    const uint8_t *__restrict__ slow, uint8_t *__restrict__ flag,
-                                                    int32_t *__restrict__ known, uint8_t *__restrict__ inrun,
-                                                    uint8_t *__restrict__ emp, unsigned long long *ctl) {
+// ---- per-changeset decisions (order2: site rank, version start, arrival) ------------------------
+// A changeset is decided on the device when nothing else of its actor in the call touches its
+// versions and they are all above the actor's booked max: then util.rs:704-884 treats it on its
+// own -- contains_all is false (no version above max is known), no earlier changeset of the actor
+// has seen a version of it -- so a complete Full version merges (or rolls back on an unknown name),
+// an empty one or an Empty range clears (crsql_set_db_version of its end, :810-824). Changesets with
+// the same dedup key (actor, versions, seqs: util.rs:711) form one group: the first to arrive is the
+// one processed, the rest are skipped by pass 1's seen set. versions() == 0..=0 (EmptySet, and any
+// changeset of version 0) is always contained (agent.rs:1353-1361): skipped. Everything else -- an
+// overlap, an incomplete (partial) version, a version at or below the max -- is walked by the host
+// with the reference's per-actor code, and never touches the versions of a decided changeset.
+__device__ inline bool same_key(const corro_changeset *cs, const uint64_t *ver, const uint64_t *vend,
+                                const uint8_t *kd, uint32_t a, uint32_t b) {
+    if (ver[a] != ver[b] || vend[a] != vend[b]) return false;
+    const bool sa = (kd[a] & 3u) == CORRO_CS_FULL, sb = (kd[b] & 3u) == CORRO_CS_FULL;  // seqs: Full only
+    if (sa != sb) return false;
+    return !sa || (cs[a].seq_start == cs[b].seq_start && cs[a].seq_end == cs[b].seq_end);
+}
+
+__global__ void __launch_bounds__(AG_T) k_iso_prep(const corro_changeset *__restrict__ cs, const uint32_t *__restrict__ order2,
+                                                    uint64_t n, const uint32_t *__restrict__ site,
+                                                    const uint64_t *__restrict__ ver, const uint64_t *__restrict__ vend,
+                                                    const uint8_t *__restrict__ kd, uint32_t *__restrict__ segk,
+                                                    uint64_t *__restrict__ vend2, uint32_t *__restrict__ ghead) {
+    for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < n; q += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = order2[q];
+        segk[q] = site[i];
+        vend2[q] = vend[i];
+        const uint32_t p = q ? order2[q - 1] : 0u;
+        ghead[q] = (q == 0 || site[p] != site[i] || !same_key(cs, ver, vend, kd, p, i)) ? 1u : 0u;
+    }
+}
+
+__global__ void __launch_bounds__(AG_T) k_iso_groups(uint64_t n, const uint32_t *__restrict__ ghead,
+                                                      const uint32_t *__restrict__ gincl, uint32_t *__restrict__ gfirst,
+                                                      uint32_t *__restrict__ glast) {
+    for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < n; q += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t g = gincl[q] - 1;
+        if (ghead[q]) gfirst[g] = (uint32_t)q;
+        if (q + 1 == n || ghead[q + 1]) glast[g] = (uint32_t)q;
+    }
+}
+
+struct IsoArgs {
+    const uint32_t *order2, *segk, *gincl, *gfirst, *glast;
+    const uint64_t *ver, *vend, *rmax, *cnt;
+    const uint8_t *kd, *bad;
+    const int64_t *site_max;
+    uint8_t *dec, *flag, *emp, *inrun;
+    int32_t *known;
+    unsigned long long *ctl;
+    uint64_t n;
+};
+
+__global__ void __launch_bounds__(AG_T) k_iso_decide(IsoArgs a) {
     __shared__ unsigned long long l_sp[AG_T / 64], l_ch[AG_T / 64];
     unsigned long long nsp = 0, nch = 0;
-    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
-        const uint32_t i = order[j];
-        uint8_t in = 0, e = 0;
-        if (!slow[site[i]]) {
-            if (cnt[i] == 0) {  // process_empty_version (every version of a fast actor is above its max)
-                known[i] = CORRO_KNOWN_CLEARED;
-                in = e = 1;
-            } else if (bad[i]) {  // the version's SAVEPOINT rolls back alone (util.rs:839-860)
-                known[i] = CORRO_E_UNKNOWN_COLUMN;
-            } else {
-                flag[i] = 1;
-                known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
-                in = 1;
-                nsp++;
-                nch += cnt[i];
+    for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < a.n; q += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = a.order2[q];
+        uint8_t in = 0;
+        if (a.ver[i] == 0 && a.vend[i] == 0) {
+            a.dec[i] = 1;  // versions() == 0..=0: always contained (pass 1 skips it)
+        } else if (a.ver[i] != 0 && a.ver[i] <= a.vend[i] && a.ver[i] < VCLAMP) {
+            const uint32_t g = a.gincl[q] - 1, f = a.gfirst[g], l = a.glast[g], fi = a.order2[f];
+            const uint64_t vs = a.ver[fi], ve = a.vend[fi];
+            const bool prev_ov = f > 0 && a.segk[f - 1] == a.segk[f] && a.rmax[f - 1] >= vs;
+            bool next_ov = false;
+            if (l + 1 < a.n && a.segk[l + 1] == a.segk[l]) {
+                const uint64_t nv = a.ver[a.order2[l + 1]];
+                next_ov = nv <= ve || (nv >= VCLAMP && ve >= VCLAMP);
             }
-        }
-        inrun[j] = in;
-        emp[j] = e;
+            const int64_t mx = a.site_max[a.segk[q]];
+            const uint32_t kind = a.kd[fi] & 3u;
+            const bool decidable = !prev_ov && !next_ov && (mx < 0 || vs > (uint64_t)mx) &&
+                                   (kind == CORRO_CS_EMPTY || (kind == CORRO_CS_FULL && (a.kd[fi] & KD_COMPLETE)));
+            if (decidable && q != f) {
+                a.dec[i] = 1;  // a later copy of the group's key: pass 1's seen set skips it
+            } else if (decidable) {
+                a.dec[i] = 1;
+                if (kind == CORRO_CS_EMPTY || a.cnt[i] == 0) {  // process_empty_version (above the max)
+                    a.known[i] = CORRO_KNOWN_CLEARED;
+                    a.emp[i] = 1;
+                    in = 1;
+                } else if (a.bad[i]) {  // the version's SAVEPOINT rolls back alone (util.rs:839-860)
+                    a.known[i] = CORRO_E_UNKNOWN_COLUMN;
+                } else {
+                    a.flag[i] = 1;
+                    a.known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
+                    in = 1;
+                    nsp++;
+                    nch += a.cnt[i];
+                }
+            }
+        }  // (else: a range from version 0, an inverted or clamped range -- the host walks it)
+        a.inrun[q] = in;
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -900,42 +991,57 @@ __global__ void __launch_bounds__(AG_T) k_hdr_fast(const uint32_t *__restrict__ 
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long a = 0, b = 0;
+        unsigned long long x = 0, y = 0;
         for (int k = 0; k < AG_T / 64; k++) {
-            a += l_sp[k];
-            b += l_ch[k];
+            x += l_sp[k];
+            y += l_ch[k];
         }
-        if (a) atomicAdd(&ctl[2], a);
-        if (b) atomicAdd(&ctl[3], b);
+        if (x) atomicAdd(&a.ctl[2], x);
+        if (y) atomicAdd(&a.ctl[3], y);
     }
 }
 
-// run starts: a slot in a run whose predecessor (same actor) does not continue it with version - 1
-__global__ void __launch_bounds__(AG_T) k_hdr_runflag(const uint32_t *__restrict__ order, uint64_t ncs,
-                                                       const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
-                                                       const uint8_t *__restrict__ inrun, uint32_t *__restrict__ rflag) {
-    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
-        const uint32_t i = order[j];
-        const bool cont = j > 0 && inrun[j - 1] && site[order[j - 1]] == site[i] && ver[order[j - 1]] + 1 == ver[i];
-        rflag[j] = inrun[j] && !cont ? 1u : 0u;
+// version runs of the decided (merged or cleared) changesets, in order2: a slot starts a run unless
+// the previous slot is in a run of the same actor ending right before it
+__global__ void __launch_bounds__(AG_T) k_hdr_runflag(const uint32_t *__restrict__ order2, uint64_t n,
+                                                       const uint32_t *__restrict__ segk, const uint64_t *__restrict__ ver,
+                                                       const uint64_t *__restrict__ vend, const uint8_t *__restrict__ inrun,
+                                                       uint32_t *__restrict__ rflag) {
+    for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < n; q += (uint64_t)gridDim.x * AG_T) {
+        const bool cont = q > 0 && inrun[q - 1] && segk[q - 1] == segk[q] && vend[order2[q - 1]] + 1 == ver[order2[q]];
+        rflag[q] = inrun[q] && !cont ? 1u : 0u;
     }
 }
 
-__global__ void __launch_bounds__(AG_T) k_hdr_runs(const uint32_t *__restrict__ order, uint64_t ncs,
-                                                    const uint32_t *__restrict__ site, const uint64_t *__restrict__ ver,
-                                                    const uint8_t *__restrict__ inrun, const uint32_t *__restrict__ rflag,
-                                                    const uint32_t *__restrict__ rincl, uint32_t *__restrict__ run_site,
-                                                    uint64_t *__restrict__ run_start, uint64_t *__restrict__ run_end) {
-    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
-        if (!inrun[j]) continue;
-        const uint32_t i = order[j], r = rincl[j] - 1;
-        if (rflag[j]) {
-            run_site[r] = site[i];
+__global__ void __launch_bounds__(AG_T) k_hdr_runs(const uint32_t *__restrict__ order2, uint64_t n,
+                                                    const uint32_t *__restrict__ segk, const uint64_t *__restrict__ ver,
+                                                    const uint64_t *__restrict__ vend, const uint8_t *__restrict__ inrun,
+                                                    const uint32_t *__restrict__ rflag, const uint32_t *__restrict__ rincl,
+                                                    uint32_t *__restrict__ run_site, uint64_t *__restrict__ run_start,
+                                                    uint64_t *__restrict__ run_end) {
+    for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < n; q += (uint64_t)gridDim.x * AG_T) {
+        if (!inrun[q]) continue;
+        const uint32_t i = order2[q], r = rincl[q] - 1;
+        if (rflag[q]) {
+            run_site[r] = segk[q];
             run_start[r] = ver[i];
         }
-        const bool ends = j + 1 >= ncs || !inrun[j + 1] || rflag[j + 1];
-        if (ends) run_end[r] = ver[i];
+        const bool ends = q + 1 >= n || !inrun[q + 1] || rflag[q + 1];
+        if (ends) run_end[r] = vend[i];
     }
+}
+
+// the host's changesets (dec 0) among the sorted slots (order: site rank, arrival): flags for the scan
+__global__ void __launch_bounds__(AG_T) k_hdr_hmark(const uint32_t *__restrict__ order, uint64_t n,
+                                                     const uint8_t *__restrict__ dec, uint32_t *__restrict__ hm) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < n; j += (uint64_t)gridDim.x * AG_T)
+        hm[j] = dec[order[j]] ? 0u : 1u;
+}
+
+__global__ void __launch_bounds__(AG_T) k_hdr_hlist(uint64_t n, const uint32_t *__restrict__ hm,
+                                                     const uint32_t *__restrict__ hincl, uint32_t *__restrict__ hslot) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < n; j += (uint64_t)gridDim.x * AG_T)
+        if (hm[j]) hslot[hincl[j] - 1] = (uint32_t)j;
 }
 
 __global__ void __launch_bounds__(AG_T) k_hdr_gather(const corro_changeset *__restrict__ cs, const uint32_t *__restrict__ order,
@@ -983,16 +1089,33 @@ __global__ void __launch_bounds__(AG_T) k_hdr_spans(const uint32_t *__restrict__
     }
 }
 
-// commit: known of flagged changesets, crsql_set_db_version of the fast actors' empty versions
-__global__ void __launch_bounds__(AG_T) k_hdr_commit(const uint32_t *__restrict__ order, uint64_t ncs,
-                                                      const uint8_t *__restrict__ flag, const uint8_t *__restrict__ any,
-                                                      const uint8_t *__restrict__ emp, const uint32_t *__restrict__ site,
-                                                      const uint64_t *__restrict__ ver, int32_t *__restrict__ known,
-                                                      unsigned long long *__restrict__ dbv) {
-    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < ncs; j += (uint64_t)gridDim.x * AG_T) {
-        const uint32_t i = order[j];
+// commit: known of flagged changesets, crsql_set_db_version of the decided empty versions / ranges
+__global__ void __launch_bounds__(AG_T) k_hdr_commit(uint64_t ncs, const uint8_t *__restrict__ flag,
+                                                      const uint8_t *__restrict__ any, const uint8_t *__restrict__ emp,
+                                                      const uint32_t *__restrict__ site, const uint64_t *__restrict__ vend,
+                                                      int32_t *__restrict__ known, unsigned long long *__restrict__ dbv) {
+    for (uint64_t i = (uint64_t)blockIdx.x * AG_T + threadIdx.x; i < ncs; i += (uint64_t)gridDim.x * AG_T) {
         if (flag[i]) known[i] = any[i] ? CORRO_KNOWN_CURRENT : CORRO_KNOWN_CLEARED;
-        if (emp[j]) atomicMax(&dbv[site[i]], (unsigned long long)(ver[i] + 1));
+        if (emp[i]) atomicMax(&dbv[site[i]], (unsigned long long)(vend[i] + 1));
+    }
+}
+
+// flagged changeset i whose site << 40 | version is among the sorted keys -> hit list
+__global__ void __launch_bounds__(AG_T) k_hdr_clearprobe(uint64_t ncs, const uint8_t *__restrict__ flag,
+                                                          const uint32_t *__restrict__ site,
+                                                          const uint64_t *__restrict__ ver, const uint64_t *__restrict__ keys,
+                                                          uint64_t nk, uint64_t *__restrict__ hit,
+                                                          unsigned long long *__restrict__ nhit) {
+    for (uint64_t i = (uint64_t)blockIdx.x * AG_T + threadIdx.x; i < ncs; i += (uint64_t)gridDim.x * AG_T) {
+        if (!flag[i] || ver[i] >= (1ULL << 40)) continue;
+        const uint64_t k = (uint64_t)site[i] << 40 | ver[i];
+        uint64_t lo = 0, hi = nk;  // first key >= k
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (keys[m] < k) lo = m + 1;
+            else hi = m;
+        }
+        if (lo < nk && keys[lo] == k) hit[atomicAdd(nhit, 1ULL)] = k;
     }
 }
 
@@ -1003,7 +1126,7 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     hipStream_t s = ctx->stream;
     const uint32_t nsites = (uint32_t)ctx->sites.size();
     res = DevHdrResult{};
-    res.sites.assign(nsites, DevHdrSite{0xFFFFFFFFu, 0xFFFFFFFFu, 0});
+    res.sites.assign(nsites, DevHdrSite{0xFFFFFFFFu, 0xFFFFFFFFu});
     ctx->agent_sorted_mode = true;
     if (!ncs) return CORRO_OK;
     size_t total = 0;
@@ -1012,7 +1135,6 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     const HdrCols h = hdr_cols(ctx, ncs, nsites);
     const DevCols c = dev_cols(ctx);
     CORRO_HIP_TRY(hipMemsetAsync(h.ctl, 0, 64, s));
-    CORRO_HIP_TRY(hipMemsetAsync(h.slow, 0, std::max<uint32_t>(nsites, 1), s));
     CORRO_HIP_TRY(hipMemsetAsync(h.gstart, 0xFF, 4ULL * std::max<uint32_t>(nsites, 1), s));
     if (nsites) CORRO_HIP_TRY(hipMemcpyAsync(h.site_max, site_max.data(), 8ULL * nsites, hipMemcpyHostToDevice, s));
     HdrArgs a{};
@@ -1031,9 +1153,14 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     a.val = c.val;
     a.flag = c.flag;
     a.bad = c.bad;
-    a.comp = h.comp;
+    a.emp = h.emp;
     a.known = dknown;
     a.ctl = h.ctl;
+    a.vend = h.vend;
+    a.key2 = h.key2;
+    a.val2 = h.val2;
+    a.kd = h.kd;
+    a.dec = h.dec;
     hipLaunchKernelGGL(k_hdr, flat_grid(ncs), dim3(AG_T), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
     unsigned long long ctl0 = 0;
@@ -1045,31 +1172,76 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     }
     uint32_t bits = 1;
     while ((1ULL << bits) <= nsites) bits++;
+    const uint32_t n32 = (uint32_t)ncs;
+    // the application order (site rank, arrival) and each actor's slots in it
     size_t tb = c.temp_bytes;
-    if (int rc = ovf_sort_pairs(c.temp, &tb, c.key, c.key2, c.val, c.val2, (uint32_t)ncs, bits, s)) return rc;
+    if (int rc = ovf_sort_pairs(c.temp, &tb, c.key, c.key2, c.val, c.val2, n32, bits, s)) return rc;
     const uint32_t *order = c.val2;
-    hipLaunchKernelGGL(k_hdr_sites, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, h.comp, h.site_max,
-                       h.slow, h.gstart, h.gend);
+    hipLaunchKernelGGL(k_hdr_sites, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.gstart, h.gend);
     CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_hdr_fast, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, c.cnt, c.bad, h.slow,
-                       c.flag, dknown, h.inrun, h.emp, h.ctl);
-    CORRO_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_hdr_runflag, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, h.inrun, h.rflag);
+    // per-changeset decisions over (site rank, version start, arrival): dedup groups, the running max
+    // of version ends per actor (overlaps), then the decided changesets' version runs
+    const bool decide = bits <= 24;  // (rank << 40 | version in one 64-bit key; else the host walks all)
+    if (decide) {
+        tb = c.temp_bytes;
+        if (int rc = ovf_sort_pairs(c.temp, &tb, h.key2, h.key2b, h.val2, h.val2b, n32, bits + 40, s)) return rc;
+        const uint32_t *order2 = h.val2b;
+        hipLaunchKernelGGL(k_iso_prep, flat_grid(ncs), dim3(AG_T), 0, s, dcs, order2, ncs, c.site, h.ver, h.vend, h.kd,
+                           h.segk, h.vend2, h.ghead);
+        CORRO_HIP_TRY(hipGetLastError());
+        tb = c.temp_bytes;
+        if (int rc = prim_inclusive_scan_u32(c.temp, &tb, h.ghead, h.gincl, n32, s)) return rc;
+        hipLaunchKernelGGL(k_iso_groups, flat_grid(ncs), dim3(AG_T), 0, s, ncs, h.ghead, h.gincl, h.gfirst, h.glast);
+        CORRO_HIP_TRY(hipGetLastError());
+        tb = c.temp_bytes;
+        if (int rc = prim_segmax_scan_u64(c.temp, &tb, h.segk, h.vend2, h.rmax, n32, s)) return rc;
+        IsoArgs d{};
+        d.order2 = order2;
+        d.segk = h.segk;
+        d.gincl = h.gincl;
+        d.gfirst = h.gfirst;
+        d.glast = h.glast;
+        d.ver = h.ver;
+        d.vend = h.vend;
+        d.rmax = h.rmax;
+        d.cnt = c.cnt;
+        d.kd = h.kd;
+        d.bad = c.bad;
+        d.site_max = h.site_max;
+        d.dec = h.dec;
+        d.flag = c.flag;
+        d.emp = h.emp;
+        d.inrun = h.inrun;
+        d.known = dknown;
+        d.ctl = h.ctl;
+        d.n = ncs;
+        hipLaunchKernelGGL(k_iso_decide, flat_grid(ncs), dim3(AG_T), 0, s, d);
+        CORRO_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_hdr_runflag, flat_grid(ncs), dim3(AG_T), 0, s, order2, ncs, h.segk, h.ver, h.vend, h.inrun,
+                           h.rflag);
+        CORRO_HIP_TRY(hipGetLastError());
+        tb = c.temp_bytes;
+        if (int rc = prim_inclusive_scan_u32(c.temp, &tb, h.rflag, h.rincl, n32, s)) return rc;
+        hipLaunchKernelGGL(k_hdr_runs, flat_grid(ncs), dim3(AG_T), 0, s, order2, ncs, h.segk, h.ver, h.vend, h.inrun,
+                           h.rflag, h.rincl, h.run_site, h.run_start, h.run_end);
+        CORRO_HIP_TRY(hipGetLastError());
+    }
+    // the host's changesets: their sorted slots (grouped by actor, arrival order inside)
+    hipLaunchKernelGGL(k_hdr_hmark, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, h.dec, c.cnt32);
     CORRO_HIP_TRY(hipGetLastError());
     tb = c.temp_bytes;
-    if (int rc = prim_inclusive_scan_u32(c.temp, &tb, h.rflag, h.rincl, (uint32_t)ncs, s)) return rc;
-    hipLaunchKernelGGL(k_hdr_runs, flat_grid(ncs), dim3(AG_T), 0, s, order, ncs, c.site, h.ver, h.inrun, h.rflag,
-                       h.rincl, h.run_site, h.run_start, h.run_end);
+    if (int rc = prim_inclusive_scan_u32(c.temp, &tb, c.cnt32, c.incl, n32, s)) return rc;
+    uint32_t *hslot = h.gfirst;  // (free once the decisions are made)
+    hipLaunchKernelGGL(k_hdr_hlist, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.cnt32, c.incl, hslot);
     CORRO_HIP_TRY(hipGetLastError());
-    // summaries: counters, run count, per-site groups
+    // summaries: counters, run count, host changeset count, per-site groups
     unsigned long long ctl[4] = {0, 0, 0, 0};
-    uint32_t nruns = 0;
-    std::vector<uint8_t> slow(nsites);
+    uint32_t nruns = 0, nh = 0;
     std::vector<uint32_t> gs(nsites), ge(nsites);
     CORRO_HIP_TRY(hipMemcpyAsync(ctl, h.ctl, 32, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(&nruns, h.rincl + (ncs - 1), 4, hipMemcpyDeviceToHost, s));
+    if (decide) CORRO_HIP_TRY(hipMemcpyAsync(&nruns, h.rincl + (ncs - 1), 4, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(&nh, c.incl + (ncs - 1), 4, hipMemcpyDeviceToHost, s));
     if (nsites) {
-        CORRO_HIP_TRY(hipMemcpyAsync(slow.data(), h.slow, nsites, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipMemcpyAsync(gs.data(), h.gstart, 4ULL * nsites, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipMemcpyAsync(ge.data(), h.gend, 4ULL * nsites, hipMemcpyDeviceToHost, s));
     }
@@ -1077,7 +1249,7 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     res.ts_any = ctl[1] != 0;
     res.nspans = ctl[2];
     res.nchanges = ctl[3];
-    for (uint32_t t = 0; t < nsites; t++) res.sites[t] = DevHdrSite{gs[t], ge[t], slow[t]};
+    for (uint32_t t = 0; t < nsites; t++) res.sites[t] = DevHdrSite{gs[t], ge[t]};
     res.run_site.resize(nruns);
     res.run_start.resize(nruns);
     res.run_end.resize(nruns);
@@ -1085,40 +1257,27 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         CORRO_HIP_TRY(hipMemcpyAsync(res.run_site.data(), h.run_site, 4ULL * nruns, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipMemcpyAsync(res.run_start.data(), h.run_start, 8ULL * nruns, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipMemcpyAsync(res.run_end.data(), h.run_end, 8ULL * nruns, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
     }
+    res.hcs.resize(nh);
+    res.hidx.resize(nh);
+    res.hbad.resize(nh);
+    if (nh) {  // their headers, arrival index and unknown-name flag
+        const size_t o_cs = 0, o_idx = al256((uint64_t)nh * sizeof(corro_changeset)), o_bad = o_idx + al256(nh * 4ULL);
+        if (int rc = ctx->d_agent_fetch.ensure(o_bad + al256(nh))) return rc;
+        uint8_t *base = ctx->d_agent_fetch.as<uint8_t>();
+        hipLaunchKernelGGL(k_hdr_gather, flat_grid(nh), dim3(AG_T), 0, s, dcs, order, c.bad, hslot, (uint64_t)nh,
+                           reinterpret_cast<corro_changeset *>(base + o_cs), reinterpret_cast<uint32_t *>(base + o_idx),
+                           base + o_bad);
+        CORRO_HIP_TRY(hipGetLastError());
+        CORRO_HIP_TRY(hipMemcpyAsync(res.hcs.data(), base + o_cs, nh * sizeof(corro_changeset), hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(res.hidx.data(), base + o_idx, nh * 4ULL, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(res.hbad.data(), base + o_bad, nh, hipMemcpyDeviceToHost, s));
+    }
+    if (nruns || nh) CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;
 }
 
-int agent_dev_slow_headers(corro_ctx *ctx, const corro_changeset *dcs, const std::vector<std::pair<uint32_t, uint32_t>> &ranges,
-                           std::vector<corro_changeset> &hcs, std::vector<uint32_t> &idx, std::vector<uint8_t> &bad) {
-    hipStream_t s = ctx->stream;
-    std::vector<uint32_t> slots;
-    for (auto &[lo, hi] : ranges)
-        for (uint32_t j = lo; j < hi; j++) slots.push_back(j);
-    const uint64_t n = slots.size();
-    hcs.resize(n);
-    idx.resize(n);
-    bad.resize(n);
-    if (!n) return CORRO_OK;
-    const size_t o_cs = 0, o_idx = al256(n * sizeof(corro_changeset)), o_bad = o_idx + al256(n * 4), o_slot = o_bad + al256(n);
-    if (int rc = ctx->d_agent_fetch.ensure(o_slot + al256(n * 4))) return rc;
-    uint8_t *base = ctx->d_agent_fetch.as<uint8_t>();
-    const DevCols c = dev_cols(ctx);
-    CORRO_HIP_TRY(hipMemcpyAsync(base + o_slot, slots.data(), n * 4, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_hdr_gather, flat_grid(n), dim3(AG_T), 0, s, dcs, c.val2, c.bad,
-                       reinterpret_cast<const uint32_t *>(base + o_slot), n,
-                       reinterpret_cast<corro_changeset *>(base + o_cs), reinterpret_cast<uint32_t *>(base + o_idx),
-                       base + o_bad);
-    CORRO_HIP_TRY(hipGetLastError());
-    CORRO_HIP_TRY(hipMemcpyAsync(hcs.data(), base + o_cs, n * sizeof(corro_changeset), hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(idx.data(), base + o_idx, n * 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(bad.data(), base + o_bad, n, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipStreamSynchronize(s));
-    return CORRO_OK;
-}
-
-int agent_dev_put_slow(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
+int agent_dev_put_host(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
                        const std::vector<int32_t> &known, int32_t *dknown) {
     const uint64_t n = idx.size();
     if (!n) return CORRO_OK;
@@ -1153,25 +1312,39 @@ int agent_dev_batch_sorted(corro_ctx *ctx, const corro_changes *dv, uint64_t ncs
     return spans_to_batch(ctx, dv, nspans, nbatch, need_ts, batch, gathered, pm);
 }
 
-int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown,
-                             std::vector<std::pair<uint32_t, uint64_t>> *flagged_sv) {
+int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown, const std::vector<uint64_t> *keys,
+                             std::vector<std::pair<uint32_t, uint64_t>> *hits) {
+    if (hits) hits->clear();
     if (!ncs) return CORRO_OK;
     hipStream_t s = ctx->stream;
     const HdrCols h = hdr_cols(ctx, ncs, (uint32_t)ctx->sites.size());
     const DevCols c = dev_cols(ctx);
-    hipLaunchKernelGGL(k_hdr_commit, flat_grid(ncs), dim3(AG_T), 0, s, c.val2, ncs, c.flag, c.any, h.emp, c.site, h.ver,
-                       dknown, ctx->d_dbv.as<unsigned long long>());
+    hipLaunchKernelGGL(k_hdr_commit, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.flag, c.any, h.emp, c.site, h.vend, dknown,
+                       ctx->d_dbv.as<unsigned long long>());
     CORRO_HIP_TRY(hipGetLastError());
-    if (flagged_sv) {
-        std::vector<uint8_t> f(ncs);
-        std::vector<uint32_t> st(ncs);
-        std::vector<uint64_t> v(ncs);
-        CORRO_HIP_TRY(hipMemcpyAsync(f.data(), c.flag, ncs, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(st.data(), c.site, ncs * 4, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(v.data(), h.ver, ncs * 8, hipMemcpyDeviceToHost, s));
+    if (keys && !keys->empty() && hits) {
+        // the merged changesets whose (site, version) holds buffered meta: keys uploaded once, a
+        // binary search per flagged changeset, the hits appended (a few) and read back
+        const uint64_t nk = keys->size();
+        const size_t o_hit = al256(nk * 8), o_cnt = o_hit + al256(ncs * 8);
+        if (int rc = ctx->d_agent_aux2.ensure(o_cnt + 256)) return rc;
+        uint8_t *base = ctx->d_agent_aux2.as<uint8_t>();
+        uint64_t *dk = reinterpret_cast<uint64_t *>(base);
+        uint64_t *dh = reinterpret_cast<uint64_t *>(base + o_hit);  // the hits' keys
+        unsigned long long *dc = reinterpret_cast<unsigned long long *>(base + o_cnt);
+        CORRO_HIP_TRY(hipMemcpyAsync(dk, keys->data(), nk * 8, hipMemcpyHostToDevice, s));
+        CORRO_HIP_TRY(hipMemsetAsync(dc, 0, 8, s));
+        hipLaunchKernelGGL(k_hdr_clearprobe, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.flag, c.site, h.ver, dk, nk, dh, dc);
+        CORRO_HIP_TRY(hipGetLastError());
+        unsigned long long nh = 0;
+        CORRO_HIP_TRY(hipMemcpyAsync(&nh, dc, 8, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipStreamSynchronize(s));
-        for (uint64_t i = 0; i < ncs; i++)
-            if (f[i]) flagged_sv->emplace_back(st[i], v[i]);
+        if (nh) {
+            std::vector<uint64_t> hk(nh);
+            CORRO_HIP_TRY(hipMemcpyAsync(hk.data(), dh, nh * 8, hipMemcpyDeviceToHost, s));
+            CORRO_HIP_TRY(hipStreamSynchronize(s));
+            for (uint64_t k : hk) hits->emplace_back((uint32_t)(k >> 40), k & ((1ULL << 40) - 1));
+        }
     }
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;

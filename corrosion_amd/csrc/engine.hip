@@ -604,7 +604,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_heap, &ctx->d_heap_ts, &ctx->d_heap_top, &ctx->d_stride, &ctx->d_defer,
                       &ctx->d_relist, &ctx->d_dense, &ctx->d_dense_ts, &ctx->d_dense_view, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_ovf_rcl,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_ovf_rcl, &ctx->d_setdbv,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
                       &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,
@@ -1217,6 +1217,35 @@ int state_dense_view(corro_ctx *ctx, DenseView &v) {
 }
 
 // crsql_set_db_version(site, v) for an empty complete changeset (util.rs:1040-1050)
+// crsql_set_db_version for many (site, version) pairs at once: the per-site maxima on the host, one
+// atomicMax per site on the device (d_dbv holds version + 1), queued on the context's stream
+static __global__ void k_set_dbv(const uint64_t *__restrict__ sv, uint32_t n, unsigned long long *__restrict__ dbv) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+        atomicMax(&dbv[(uint32_t)(sv[2 * k])], (unsigned long long)sv[2 * k + 1]);
+}
+
+int set_db_versions(corro_ctx *ctx, const std::vector<std::pair<uint32_t, uint64_t>> &sv) {
+    if (sv.empty()) return CORRO_OK;
+    std::vector<uint64_t> best(ctx->sites.size(), 0);
+    for (const auto &[site, v] : sv) {
+        if (site >= ctx->sites.size()) return fail(CORRO_E_INVALID, "unregistered site ordinal");
+        best[site] = std::max<uint64_t>(best[site], v + 1);
+    }
+    std::vector<uint64_t> flat;
+    for (uint32_t t = 0; t < best.size(); t++)
+        if (best[t]) flat.insert(flat.end(), {(uint64_t)t, best[t]});
+    const uint32_t n = (uint32_t)(flat.size() / 2);
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    TRY(ctx->d_setdbv.ensure(flat.size() * 8 + 256));
+    hipStream_t s = ctx->stream;
+    CORRO_HIP_TRY(hipMemcpyAsync(ctx->d_setdbv.p, flat.data(), flat.size() * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_set_dbv, dim3((n + 255) / 256), dim3(256), 0, s, ctx->d_setdbv.as<uint64_t>(), n,
+                       ctx->d_dbv.as<unsigned long long>());
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipStreamSynchronize(s));  // (the host vector is the copy's source)
+    return CORRO_OK;
+}
+
 int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version) {
     if (site >= ctx->sites.size()) return fail(CORRO_E_INVALID, "unregistered site ordinal");
     CORRO_HIP_TRY(hipSetDevice(ctx->device));

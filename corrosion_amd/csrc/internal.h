@@ -175,6 +175,7 @@ struct corro_ctx {
     corro::DevBuf d_wide_list;    // buckets queued for the mixed-type fast body
     corro::DevBuf d_ovf_sort;     // overflow path: its device-wide arrays, offsets, rocPRIM temp
     corro::DevBuf d_ovf_rcl;      // overflow path, impact form of the row reduction: per-row cl slots
+    corro::DevBuf d_setdbv;       // set_db_versions: (site, version + 1) pairs
     corro::DevBuf d_scan_tmp;     // corro_scan_offsets: rocPRIM temp
     corro::DevBuf d_impact;
     corro::DevBuf d_export;

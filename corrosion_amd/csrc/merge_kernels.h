@@ -1503,7 +1503,11 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
         __syncthreads();
         DIAG_MARK(7);
         // the bucket's heap allocation: issued now, its result consumed after the second stage
+#if CORRO_DIAG & 8  // (diagnostics: no global heap atomic -- a fixed offset per bucket, results not valid)
+        if (!used0 && tid == 0 && s_ctl[1] && used0 + s_ctl[0] <= a.rs.fill) hraw = (unsigned long long)b * 640u;
+#else
         if (!used0 && tid == 0 && s_ctl[1] && used0 + s_ctl[0] <= a.rs.fill) hraw = atomicAdd(a.rs.heap_top, (unsigned long long)s_ctl[1]);
+#endif
 #pragma unroll
         for (int k = 0; k < FAST_R; k++)
             if (alive[k]) alive[k] = s_k[cell[k]] == w[k];

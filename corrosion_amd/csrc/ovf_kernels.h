@@ -994,6 +994,12 @@ static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeAr
         if (row >= d.nrows) continue;
         const uint32_t j0 = d.rstart[row];
         if (d.rbad[row]) {  // outside App. A.3: the sequential fold over the row's sorted records
+            if (a.impact)  // (k_ovf_classify flagged its records before the row was known to be bad;
+                           // the fold stores only nonzero flags)
+                for (uint32_t p = j0; p < d.K && (uint32_t)(d.key_s[p] >> d.rshift) == row; p++) {
+                    const uint32_t pos = d.pos[d.val_s[p]];
+                    if (pos & BATCH_POS) a.impact[pos & 0x7FFFFFFFu] = 0;
+                }
             GenArrays g{};
             g.key = d.key_s;
             g.val = d.val_s;

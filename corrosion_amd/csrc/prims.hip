@@ -27,6 +27,16 @@ int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t 
     return CORRO_OK;
 }
 
+// inclusive max-scan of u64 values segmented by equal consecutive u32 keys (the agent's per-actor
+// running max of version ends); temp == nullptr -> *temp_bytes = size needed
+int prim_segmax_scan_u64(void *temp, size_t *temp_bytes, const uint32_t *keys, const uint64_t *in, uint64_t *out,
+                         uint32_t n, hipStream_t s) {
+    const hipError_t e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, keys, in, out, (size_t)n,
+                                                        rocprim::maximum<uint64_t>(), rocprim::equal_to<uint32_t>(), s);
+    if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("segmented scan: ") + hipGetErrorString(e));
+    return CORRO_OK;
+}
+
 // inclusive scan of u32 (extraction index group ids); temp == nullptr -> *temp_bytes = size needed
 int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, uint32_t *out, uint32_t n,
                             hipStream_t s) {

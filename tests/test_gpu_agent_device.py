@@ -202,10 +202,60 @@ def canon_rows(rows):
     return sorted(zip(*[np.asarray(rows[k]).tolist() for k in keys]))
 
 
-def _check_against_oracle(seed, device, order_fn=None, clean=(), empty_sets=0.0):
+def _overlap_calls(seed, ncalls=5, per_call=60, base=0):
+    """Adversarial calls for the per-changeset device decisions: versions from a small window per
+    actor (base + 0..14 or 0..39, a window near 2^40 with base), so ranges overlap all the time -- complete
+    and partial Full versions, Empty ranges crossing each other and Full versions, exact duplicates
+    (same and different content), EmptySet, version 0 -- in random arrival order, over calls that move
+    each actor's booked max."""
+    from oracle.agent import Changeset
+    rng = np.random.default_rng(seed)
+    import synth
+    ids = synth.site_ids(NACT, seed)
+    calls, prev = [], []
+    win = 15 if seed % 2 else 40
+    for c in range(ncalls):
+        call = []
+        lo = base + 3 * c                                 # the window climbs: some versions go below max
+        for _k in range(per_call):
+            a = int(rng.integers(0, NACT))
+            v = lo + int(rng.integers(0, win))
+            r = rng.random()
+            if r < 0.08 and prev:
+                call.append(prev[int(rng.integers(0, len(prev)))])
+                continue
+            if r < 0.12:
+                cs = Changeset(ids[a], "empty_set", versions=[(v, v + 1)], ts=int(rng.integers(1, 1 << 30)))
+            elif r < 0.3:
+                vs = int(rng.integers(0, 2)) * v if base == 0 else v  # (ranges from 0 too)
+                cs = Changeset(ids[a], "empty", versions=(vs, v + int(rng.integers(0, 4))))
+            else:
+                if base == 0 and rng.random() < 0.03:
+                    v = 0
+                k = int(rng.integers(0, 5))
+                rr = [dict(pk=int(rng.integers(1, 6)), table_cid=(0 << 16) | int(rng.integers(1, 5)),
+                           col_version=int(rng.integers(1, 4)), db_version=v, cl=1, seq=s, site=a,
+                           val0=int(rng.integers(0, 4)), val_type=1) for s in range(k)]
+                ts = int(rng.integers(1, 1 << 30))
+                if k >= 2 and rng.random() < 0.25:       # a partial (some halves never arrive)
+                    h = k // 2
+                    part = (rr[:h], (0, h - 1)) if rng.random() < 0.5 else (rr[h:], (h, k - 1))
+                    cs = Changeset(ids[a], "full", version=v, seqs=part[1], last_seq=k - 1, ts=ts, rows=part[0])
+                else:
+                    cs = Changeset(ids[a], "full", version=v, seqs=(0, max(k - 1, 0)), last_seq=max(k - 1, 0),
+                                   ts=ts, rows=rr)
+            call.append(cs)
+            if rng.random() < 0.1:
+                call.append(cs)                           # an exact duplicate in the same call
+        prev = list(call)
+        calls.append(call)
+    return ids, calls
+
+
+def _check_against_oracle(seed, device, order_fn=None, clean=(), empty_sets=0.0, calls_fn=None):
     import corrosion_amd as ca
     from oracle.agent import AgentOracle
-    ids, calls = _calls(seed, clean=clean, empty_sets=empty_sets)
+    ids, calls = calls_fn(seed) if calls_fn else _calls(seed, clean=clean, empty_sets=empty_sets)
     if empty_sets:
         assert any(c.kind == "empty_set" for call in calls for c in call)
     eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12)
@@ -280,6 +330,21 @@ def test_empty_set_changesets_match_restatement(device, clean):
     (util.rs:724-733): known = skipped, no crsql_set_db_version, no gap rows -- on every header path,
     next to fast and slow actors"""
     _check_against_oracle(21, device=device, clean=clean, empty_sets=0.1)
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33])
+@pytest.mark.parametrize("device", ["headers", True])
+def test_overlapping_versions_match_restatement(seed, device):
+    """The per-changeset device decisions next to the host walk: only changesets no other changeset of
+    their actor overlaps, above the booked max, are decided on the device; everything else (overlaps,
+    duplicates with other content, partials, ranges from version 0) must come out as the reference's
+    per-actor passes say -- on the device-header path and the host-header one"""
+    _check_against_oracle(seed, device=device, calls_fn=_overlap_calls)
+
+
+def test_overlapping_versions_near_2_40_match_restatement():
+    """versions at and above 2^40 - 1 share the decision sort's key: they always go to the host walk"""
+    _check_against_oracle(34, device="headers", calls_fn=lambda s: _overlap_calls(s, base=(1 << 40) - 9))
 
 
 def test_device_headers_fast_gather_path(monkeypatch):
