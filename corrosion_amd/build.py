@@ -11,7 +11,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcorro_hip.so")
 SOURCES = ["engine.hip", "sync_needs.hip", "partition.hip", "prims.hip", "extract.hip", "wire.hip", "booked.cpp", "agent.cpp",
-           "pkeys.hip", "gaps.hip", "affinity.hip", "agent_dev.hip"]
+           "pkeys.hip", "gaps.hip", "affinity.hip", "agent_dev.hip", "bufpool.hip"]
 HEADERS = ["internal.h", "merge_kernels.h", "ovf_kernels.h", "ranges.h", "booked.h", "rowhash.h", "rowstore.h", "agent_dev.h"]
 ARCH = "gfx950"
 

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <exception>
+#include <functional>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
@@ -23,6 +24,7 @@
 #include <map>
 #include <optional>
 #include <set>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <tuple>
@@ -101,12 +103,87 @@ BufRows::const_iterator buf_lower(const BufRows &v, uint32_t seq) {
     return std::lower_bound(v.begin(), v.end(), seq, [](const HostRow &r, uint32_t q) { return r.seq < q; });
 }
 
+// Rows of one (site, db_version) in the bookie's device pool (bufpool.hip): pool rows [off, off + n)
+// hold seqs seq0 .. seq0 + n - 1 in order. A key's segments are sorted by seq0 and disjoint.
+struct PoolSeg {
+    uint64_t off;
+    uint32_t seq0, n;
+};
+constexpr uint64_t SEG_PENDING = 1ULL << 63;  // off = SEG_PENDING | copy job (until the copy runs)
+
+// __corro_buffered_changes rows of one (site, db_version): host rows, or (every row of the key came
+// from canonical partial changesets of a device batch) pool segments -- never both
+struct BufEntry {
+    BufRows rows;
+    std::vector<PoolSeg> segs;
+    bool empty() const { return rows.empty() && segs.empty(); }
+};
+
+// A sorted vector map for the bookie's per-(site, version) tables: a call inserts its new keys as one
+// sorted batch (merge, O(n + m)) instead of one tree node each, lookups are binary searches (safe
+// from the parallel actor walks), erased keys are tombstones dropped at the next merge.
+template <class K, class V>
+class FlatMap {
+  public:
+    struct Slot {
+        K key;
+        V val;
+        bool dead;
+    };
+    size_t lower(const K &k) const {
+        return (size_t)(std::lower_bound(v_.begin(), v_.end(), k, [](const Slot &s, const K &x) { return s.key < x; }) -
+                        v_.begin());
+    }
+    V *find(const K &k) {
+        const size_t i = lower(k);
+        return i < v_.size() && !(k < v_[i].key) && !v_[i].dead ? &v_[i].val : nullptr;
+    }
+    const V *find(const K &k) const { return const_cast<FlatMap *>(this)->find(k); }
+    void erase_at(size_t i) {
+        if (v_[i].dead) return;
+        v_[i].dead = true;
+        v_[i].val = V{};
+        dead_++;
+    }
+    // `add`: keys ascending, unique, none live in the map
+    void merge(std::vector<std::pair<K, V>> &&add) {
+        if (add.empty() && dead_ * 2 <= v_.size()) return;
+        std::vector<Slot> out;
+        out.reserve(v_.size() - dead_ + add.size());
+        size_t a = 0;
+        for (Slot &x : v_) {
+            for (; a < add.size() && add[a].first < x.key; a++) out.push_back(Slot{add[a].first, std::move(add[a].second), false});
+            if (a < add.size() && !(x.key < add[a].first)) {  // (a dead slot of the same key)
+                out.push_back(Slot{add[a].first, std::move(add[a].second), false});
+                a++;
+                continue;
+            }
+            if (!x.dead) out.push_back(std::move(x));
+        }
+        for (; a < add.size(); a++) out.push_back(Slot{add[a].first, std::move(add[a].second), false});
+        v_.swap(out);
+        dead_ = 0;
+    }
+    size_t slots() const { return v_.size(); }
+    Slot &at(size_t i) { return v_[i]; }
+    const Slot &at(size_t i) const { return v_[i]; }
+
+  private:
+    std::vector<Slot> v_;
+    size_t dead_ = 0;
+};
+
+using BufKey = std::pair<uint32_t, int64_t>;   // (site, db_version)
+using SeqKey = std::pair<uint32_t, uint64_t>;  // (site, version)
+
 }  // namespace
 
 struct corro_bookie {
-    std::map<ActorId, corro::Booked> actors;                  // Bookie (agent.rs:1546-1598)
-    std::map<std::pair<uint32_t, int64_t>, BufRows> buffered;  // (site, dbv) -> rows by seq
-    std::map<std::pair<uint32_t, uint64_t>, SeqBook> seqbook;  // (site, version)
+    ~corro_bookie() { corro::bufpool_free(pool); }
+    std::map<ActorId, corro::Booked> actors;                   // Bookie (agent.rs:1546-1598)
+    FlatMap<BufKey, BufEntry> buffered;                         // (site, dbv) -> rows by seq
+    corro::DevBufPool *pool = nullptr;                          // device rows of BufEntry::segs
+    FlatMap<SeqKey, SeqBook> seqbook;                           // (site, version)
     std::vector<std::pair<ActorId, uint64_t>> ready;           // fully buffered, to apply
     std::map<ActorId, uint32_t> site_of;                       // actor -> site ordinal
     std::vector<uint64_t> scratch_ver;                          // process_multiple_changes scratch
@@ -181,24 +258,39 @@ HostRow row_at(const corro_changes *in, uint64_t i, uint64_t ts) {
 // Writes of one process_multiple_changes call that must not outlive a failed call: the reference
 // makes them inside the call's single transaction (util.rs:749, :936), so they are staged here and
 // applied only once the merge and the gap bookkeeping have succeeded.
+struct StagedBuf {  // one partial changeset's __corro_buffered_changes INSERTs, in walk order
+    bool dev;           // canonical changeset of a device batch: its rows stay in HBM
+    uint64_t a, b;      // (host) rows [a, b) of Staged::buffered
+    uint64_t src, ts;   // (dev) input span start, the changeset ts
+    uint32_t seq0, n, site;
+    int64_t dbv;
+};
 struct Staged {
     std::vector<std::pair<uint32_t, uint64_t>> set_dbv;                      // crsql_set_db_version
     std::vector<HostRow> buffered;                                            // __corro_buffered_changes
+    std::vector<StagedBuf> items;
     std::map<std::pair<uint32_t, uint64_t>, SeqBook> seqbook;                 // __corro_seq_bookkeeping
     SeqBook &seq(const corro_bookie *bk, uint32_t site, uint64_t version) {
         auto it = seqbook.find({site, version});
         if (it != seqbook.end()) return it->second;
-        auto b = bk->seqbook.find({site, version});
-        return seqbook.emplace(std::make_pair(site, version), b == bk->seqbook.end() ? SeqBook{} : b->second)
-            .first->second;
+        const SeqBook *b = bk->seqbook.find({site, version});
+        return seqbook.emplace(std::make_pair(site, version), b ? *b : SeqBook{}).first->second;
     }
 };
 
 // row(k) = HostRow of the changeset's k-th change
+// canon: the changeset's rows are canonical in a device batch (bufpool.hip): staged as a span
 template <class RowFn>
-int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset &cs, RowFn row,
+int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset &cs, bool canon, RowFn row,
                        corro::PartialVersion &out) {
-    for (uint64_t k = 0; k < cs.change_count; k++) st.buffered.push_back(row(k));
+    if (canon) {
+        st.items.push_back(StagedBuf{true, 0, 0, cs.change_off, cs.ts, (uint32_t)cs.seq_start,
+                                     (uint32_t)cs.change_count, cs.site, (int64_t)cs.version_start});
+    } else {
+        const uint64_t a = st.buffered.size();
+        for (uint64_t k = 0; k < cs.change_count; k++) st.buffered.push_back(row(k));
+        st.items.push_back(StagedBuf{false, a, st.buffered.size(), 0, 0, 0, 0, 0, 0});
+    }
     SeqBook &sb = st.seq(bk, cs.site, cs.version_start);
     const uint64_t s = cs.seq_start, e = cs.seq_end;
     RangeSet merged;
@@ -223,42 +315,302 @@ int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset
     return CORRO_OK;
 }
 
-// a call's buffered rows (rows of one changeset are consecutive) into the bookie, per (site, dbv)
-// key; committed[t] counts every buffered change of table t (util.rs:1101-1105)
-void commit_buffered(corro_bookie *bk, std::vector<HostRow> &rows, std::vector<uint64_t> &committed) {
-    const size_t ntables = committed.size();
-    for (size_t a = 0; a < rows.size();) {
-        size_t b = a + 1;
-        while (b < rows.size() && rows[b].site == rows[a].site && rows[b].dbv == rows[a].dbv) b++;
-        for (size_t k = a; k < b; k++)
-            if ((rows[k].tcid >> 16) < ntables) committed[rows[k].tcid >> 16]++;
-        buf_insert(bk->buffered[{rows[a].site, rows[a].dbv}], rows.data() + a, rows.data() + b);
-        a = b;
+// f(0) .. f(n - 1) on the host pool (defined below)
+template <class F>
+void run_parallel(size_t n, F &&f, size_t per = 8);
+
+// a device entry's segments -> host rows (seq order), the pool rows left dead
+int materialize(corro_bookie *bk, BufEntry &e) {
+    if (e.segs.empty()) return CORRO_OK;
+    for (const PoolSeg &g : e.segs) {
+        corro::HostSpanRows r;
+        TRY_RC(corro::bufpool_read(bk->pool, g.off, g.n, r));
+        for (uint64_t j = 0; j < g.n; j++) {
+            HostRow h;
+            h.pk = r.pk[j];
+            h.v0 = r.v0[j];
+            h.v1 = r.v1[j];
+            h.ts = r.ts[j];
+            h.cv = r.cv[j];
+            h.dbv = r.dbv[j];
+            h.tcid = r.tcid[j];
+            h.cl = r.cl[j];
+            h.seq = r.seq[j];
+            h.site = r.site[j];
+            h.vt = r.vt[j];
+            h.vl = r.vl[j];
+            e.rows.push_back(std::move(h));
+        }
     }
+    e.segs.clear();
+    return CORRO_OK;
+}
+
+// [s, e] minus the (sorted, disjoint) segments: the seqs not buffered yet, ascending
+std::vector<Range> seq_pieces(const std::vector<PoolSeg> &segs, uint64_t s, uint64_t e) {
+    std::vector<Range> out;
+    uint64_t x = s;
+    for (const PoolSeg &g : segs) {
+        const uint64_t gs = g.seq0, ge = (uint64_t)g.seq0 + g.n - 1;
+        if (ge < x) continue;
+        if (gs > e) break;
+        if (gs > x) out.emplace_back(x, gs - 1);
+        x = ge + 1;
+        if (x > e) break;
+    }
+    if (x <= e) out.emplace_back(x, e);
+    return out;
+}
+
+// The call's staged __corro_buffered_changes INSERTs into the bookie; ON CONFLICT (site_id,
+// db_version, seq) DO NOTHING: the first row of a key wins. Keys are independent, so the INSERTs are
+// grouped by key, each key's in call order (actors in `order` = ActorId order, as util.rs:765 walks
+// them, each actor's in walk order). committed[t] counts every buffered change of table t
+// (util.rs:1101-1105). A key stays in the device pool while all its rows come from canonical
+// changesets (segments trimmed against the key's earlier ones); a key that receives host rows is
+// brought to the host first. dv: the call's device batch (null: host rows only).
+int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, const std::vector<Staged *> &order,
+                  std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage = nullptr) {
+    auto mark = [&](const char *n) {
+        if (stage) stage(n);
+    };
+    const size_t ntables = committed.size();
+    struct Sub {  // one key's share of one staged INSERT batch
+        BufKey key;
+        uint64_t call;
+        const StagedBuf *it;
+        Staged *st;
+        uint64_t a, b;  // (host) rows [a, b) of st->buffered, all of this key
+        uint64_t fr;    // (dev, fetched) first row in the fetched rows
+    };
+    // per actor (in parallel): its subs sorted by (key, call), call = ActorId rank << 40 | walk index;
+    // the actors' blocks concatenated by first key are globally sorted unless two actors share a key
+    std::vector<std::vector<Sub>> per(order.size());
+    std::vector<std::vector<uint64_t>> ptab(order.size(), std::vector<uint64_t>(ntables, 0));
+    run_parallel(order.size(), [&](size_t ai) {
+        Staged *st = order[ai];
+        std::vector<Sub> &v = per[ai];
+        uint64_t call = (uint64_t)ai << 40;
+        const std::vector<HostRow> &rows = st->buffered;
+        for (const StagedBuf &it : st->items) {
+            if (it.dev) {
+                v.push_back(Sub{{it.site, it.dbv}, call++, &it, st, 0, 0, 0});
+                continue;
+            }
+            for (uint64_t a = it.a; a < it.b;) {
+                uint64_t b = a + 1;
+                while (b < it.b && rows[b].site == rows[a].site && rows[b].dbv == rows[a].dbv) b++;
+                v.push_back(Sub{{rows[a].site, rows[a].dbv}, call++, &it, st, a, b, 0});
+                for (uint64_t k = a; k < b; k++)
+                    if ((rows[k].tcid >> 16) < ntables) ptab[ai][rows[k].tcid >> 16]++;
+                a = b;
+            }
+        }
+        auto less = [](const Sub &x, const Sub &y) { return x.key < y.key || (x.key == y.key && x.call < y.call); };
+        if (!std::is_sorted(v.begin(), v.end(), less)) std::sort(v.begin(), v.end(), less);
+    });
+    for (const auto &t : ptab)
+        for (size_t k = 0; k < ntables; k++) committed[k] += t[k];
+    std::vector<size_t> blk;
+    for (size_t ai = 0; ai < per.size(); ai++)
+        if (!per[ai].empty()) blk.push_back(ai);
+    std::sort(blk.begin(), blk.end(), [&](size_t x, size_t y) { return per[x][0].key < per[y][0].key; });
+    std::vector<Sub *> sp;  // every sub in (key, call) order
+    size_t nsub = 0;
+    for (size_t ai : blk) nsub += per[ai].size();
+    if (!nsub) return CORRO_OK;
+    sp.reserve(nsub);
+    for (size_t ai : blk)
+        for (Sub &u : per[ai]) sp.push_back(&u);
+    auto sless = [](const Sub *x, const Sub *y) { return x->key < y->key || (x->key == y->key && x->call < y->call); };
+    if (!std::is_sorted(sp.begin(), sp.end(), sless)) std::sort(sp.begin(), sp.end(), sless);
+    const bool pool_ok = dv && (bk->pool ? corro::bufpool_usable(ctx, bk->pool) : true);
+    // per key group: host at the end of the call (it holds host rows, or receives some, or there is no
+    // pool for it)? Its device segments come to the host first; its canonical changesets' rows are
+    // fetched from the batch.
+    std::vector<std::pair<size_t, size_t>> groups;
+    std::vector<uint8_t> ghost;
+    std::vector<corro::AgentSpan> fsp, all_dev;
+    uint64_t fr_n = 0;
+    for (size_t g0 = 0; g0 < sp.size();) {
+        size_t g1 = g0 + 1;
+        while (g1 < sp.size() && sp[g1]->key == sp[g0]->key) g1++;
+        BufEntry *e = bk->buffered.find(sp[g0]->key);
+        bool host = !pool_ok || (e && !e->rows.empty());
+        for (size_t q = g0; q < g1 && !host; q++) host = !sp[q]->it->dev;
+        if (host && e) TRY_RC(materialize(bk, *e));
+        for (size_t q = g0; q < g1; q++) {
+            Sub &u = *sp[q];
+            if (!u.it->dev) continue;
+            all_dev.push_back({u.it->src, 0, u.it->n, u.it->ts});
+            if (host) {
+                u.fr = fr_n;
+                fsp.push_back({u.it->src, fr_n, u.it->n, u.it->ts});
+                fr_n += u.it->n;
+            }
+        }
+        groups.emplace_back(g0, g1);
+        ghost.push_back(host);
+        g0 = g1;
+    }
+    corro::HostSpanRows fr;
+    if (!fsp.empty()) TRY_RC(corro::agent_dev_fetch(ctx, dv, fsp, fr));
+    mark("cb_fetch");
+    if (!all_dev.empty()) {
+        std::vector<uint64_t> tc;
+        TRY_RC(corro::agent_dev_table_counts(ctx, dv, all_dev, (uint32_t)ntables, tc));
+        for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
+    }
+    mark("cb_tables");
+    if (!all_dev.empty() && pool_ok && !bk->pool) bk->pool = corro::bufpool_new();
+    std::vector<corro::PoolCopy> jobs;
+    std::vector<std::pair<BufKey, BufEntry>> add;
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+        const BufKey key = sp[groups[gi].first]->key;
+        BufEntry local;
+        BufEntry *e = bk->buffered.find(key);
+        const bool fresh = !e;
+        if (fresh) e = &local;
+        for (size_t q = groups[gi].first; q < groups[gi].second; q++) {
+            const Sub &u = *sp[q];
+            const StagedBuf &it = *u.it;
+            if (!it.dev) {
+                buf_insert(e->rows, u.st->buffered.data() + u.a, u.st->buffered.data() + u.b);
+            } else if (ghost[gi]) {
+                std::vector<HostRow> hr(it.n);
+                for (uint64_t j = 0; j < it.n; j++) {
+                    const uint64_t x = u.fr + j;
+                    HostRow &h = hr[j];
+                    h.pk = fr.pk[x];
+                    h.v0 = fr.v0[x];
+                    h.v1 = fr.v1[x];
+                    h.ts = dv->ts ? fr.ts[x] : it.ts;
+                    h.cv = fr.cv[x];
+                    h.dbv = fr.dbv[x];
+                    h.tcid = fr.tcid[x];
+                    h.cl = fr.cl[x];
+                    h.seq = fr.seq[x];
+                    h.site = fr.site[x];
+                    h.vt = fr.vt[x];
+                    h.vl = fr.vl[x];
+                }
+                buf_insert(e->rows, hr.data(), hr.data() + hr.size());
+            } else {
+                for (const Range &r : seq_pieces(e->segs, it.seq0, (uint64_t)it.seq0 + it.n - 1)) {
+                    const PoolSeg g{SEG_PENDING | jobs.size(), (uint32_t)r.first, (uint32_t)(r.second - r.first + 1)};
+                    jobs.push_back({it.src + (r.first - it.seq0), r.second - r.first + 1, it.ts, 0});
+                    e->segs.insert(std::lower_bound(e->segs.begin(), e->segs.end(), g,
+                                                    [](const PoolSeg &x, const PoolSeg &y) { return x.seq0 < y.seq0; }),
+                                   g);
+                }
+            }
+        }
+        if (fresh && !local.empty()) add.emplace_back(key, std::move(local));
+    }
+    bk->buffered.merge(std::move(add));
+    mark("cb_trim");
+    if (jobs.empty()) return CORRO_OK;
+    uint64_t need = 0;
+    for (const corro::PoolCopy &j : jobs) need += j.count;
+    std::vector<uint64_t *> offs;
+    std::vector<uint64_t> lens;
+    for (size_t i = 0; i < bk->buffered.slots(); i++) {
+        auto &x = bk->buffered.at(i);
+        if (x.dead) continue;
+        for (PoolSeg &g : x.val.segs)
+            if (!(g.off & SEG_PENDING)) {
+                offs.push_back(&g.off);
+                lens.push_back(g.n);
+            }
+    }
+    mark("cb_offs");
+    TRY_RC(corro::bufpool_reserve(ctx, bk->pool, need, offs, lens));
+    mark("cb_reserve");
+    TRY_RC(corro::bufpool_append(ctx, bk->pool, dv, jobs));
+    mark("cb_append");
+    for (size_t i = 0; i < bk->buffered.slots(); i++)  // (one sequential pass: no per-key searches)
+        for (PoolSeg &g : bk->buffered.at(i).val.segs)
+            if (g.off & SEG_PENDING) g.off = jobs[g.off & ~SEG_PENDING].dst;
+    mark("cb_fix");
+    return CORRO_OK;
+}
+
+// the call's __corro_seq_bookkeeping rows (one per (site, version): the actors' keys are disjoint)
+void commit_seqbook(corro_bookie *bk, const std::vector<Staged *> &order) {
+    std::vector<Staged *> blk;
+    for (Staged *st : order)
+        if (!st->seqbook.empty()) blk.push_back(st);
+    if (blk.empty()) return;
+    std::sort(blk.begin(), blk.end(), [](Staged *x, Staged *y) { return x->seqbook.begin()->first < y->seqbook.begin()->first; });
+    std::vector<size_t> base(blk.size() + 1, 0);
+    for (size_t b = 0; b < blk.size(); b++) base[b + 1] = base[b] + blk[b]->seqbook.size();
+    // gathered in parallel (one actor's map per task), each item with the slot it updates, if any
+    std::vector<std::pair<SeqKey, SeqBook>> items(base.back());
+    std::vector<SeqBook *> hit(base.back());
+    run_parallel(blk.size(), [&](size_t b) {
+        size_t q = base[b];
+        for (auto &[k, sb] : blk[b]->seqbook) {
+            items[q].first = k;
+            items[q].second = std::move(sb);
+            hit[q] = bk->seqbook.find(k);  // (read-only lookups)
+            q++;
+        }
+    }, 16);
+    bool sorted = true;
+    for (size_t q = 1; q < items.size() && sorted; q++) sorted = items[q - 1].first < items[q].first;
+    std::vector<std::pair<SeqKey, SeqBook>> add;
+    if (!sorted) {  // (two actors' keys interleave: plain path)
+        std::sort(items.begin(), items.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+        for (auto &[k, sb] : items) {
+            if (SeqBook *x = bk->seqbook.find(k)) *x = std::move(sb);
+            else add.emplace_back(k, std::move(sb));
+        }
+    } else {
+        add.reserve(items.size());
+        for (size_t q = 0; q < items.size(); q++) {
+            if (hit[q]) *hit[q] = std::move(items[q].second);
+            else add.push_back(std::move(items[q]));
+        }
+    }
+    bk->seqbook.merge(std::move(add));
 }
 
 // sorted site << 40 | version keys of every (site, version) holding buffered rows or seq bookkeeping
 std::vector<uint64_t> buffered_keys(const corro_bookie *bk) {
-    std::vector<uint64_t> k;
-    k.reserve(bk->buffered.size() + bk->seqbook.size());
-    for (const auto &[key, rows] : bk->buffered)
-        if (key.second >= 0 && (uint64_t)key.second < (1ULL << 40)) k.push_back((uint64_t)key.first << 40 | (uint64_t)key.second);
-    for (const auto &[key, sb] : bk->seqbook)
-        if (key.second < (1ULL << 40)) k.push_back((uint64_t)key.first << 40 | key.second);
-    std::sort(k.begin(), k.end());
+    std::vector<uint64_t> a, b, k;
+    for (size_t i = 0; i < bk->buffered.slots(); i++) {
+        const auto &x = bk->buffered.at(i);
+        if (!x.dead && !x.val.empty() && x.key.second >= 0 && (uint64_t)x.key.second < (1ULL << 40))
+            a.push_back((uint64_t)x.key.first << 40 | (uint64_t)x.key.second);
+    }
+    for (size_t i = 0; i < bk->seqbook.slots(); i++) {
+        const auto &x = bk->seqbook.at(i);
+        if (!x.dead && x.key.second < (1ULL << 40)) b.push_back((uint64_t)x.key.first << 40 | x.key.second);
+    }
+    k.resize(a.size() + b.size());  // (both ascending: the maps' key order is (site, version))
+    std::merge(a.begin(), a.end(), b.begin(), b.end(), k.begin());
     k.erase(std::unique(k.begin(), k.end()), k.end());
     return k;
 }
 
 void clear_buffered(corro_bookie *bk, uint32_t site, uint64_t vs, uint64_t ve) {
-    for (auto it = bk->buffered.lower_bound({site, (int64_t)vs}); it != bk->buffered.end();) {
-        if (it->first.first != site || (uint64_t)it->first.second > ve) break;
-        it = bk->buffered.erase(it);
+    if (vs <= (uint64_t)INT64_MAX)
+        for (size_t i = bk->buffered.lower({site, (int64_t)vs}); i < bk->buffered.slots(); i++) {
+            const auto &x = bk->buffered.at(i);
+            if (x.key.first != site || (uint64_t)x.key.second > ve) break;
+            bk->buffered.erase_at(i);
+        }
+    for (size_t i = bk->seqbook.lower({site, vs}); i < bk->seqbook.slots(); i++) {
+        const auto &x = bk->seqbook.at(i);
+        if (x.key.first != site || x.key.second > ve) break;
+        bk->seqbook.erase_at(i);
     }
-    for (auto it = bk->seqbook.lower_bound({site, vs}); it != bk->seqbook.end();) {
-        if (it->first.first != site || it->first.second > ve) break;
-        it = bk->seqbook.erase(it);
-    }
+}
+
+// tombstones of cleared keys dropped once they are half of a table
+void compact_tables(corro_bookie *bk) {
+    bk->buffered.merge({});
+    bk->seqbook.merge({});
 }
 
 // A persistent pool of host workers for the per-call parallel passes: spawning threads per pass
@@ -360,7 +712,7 @@ thread_local bool HostPool::in_pool_ = false;
 // f(0) .. f(n - 1) on up to CORRO_HOST_THREADS (default: min(16, hardware)) host threads, at least
 // `per` indices per thread (serial for small n). f must only touch state of its own index.
 template <class F>
-void run_parallel(size_t n, F &&f, size_t per = 8) {
+void run_parallel(size_t n, F &&f, size_t per) {
     HostPool &pool = HostPool::get();
     const unsigned nth = (unsigned)std::min<size_t>(pool.threads(), n / std::max<size_t>(per, 1));
     if (nth <= 1) {
@@ -452,6 +804,7 @@ struct CsView {
     const uint8_t *bad;   // unknown-name screen
     int32_t *known;
     uint8_t *flag;        // 1 = merged by this call
+    const uint8_t *canon; // canonical partial changeset of a device batch (bufpool.hip; null: none)
 };
 
 // One actor's passes 1 and 2 (util.rs:704-884) over its changesets w.idx (arrival order) unless it
@@ -507,7 +860,9 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
                     v.known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
                 } else {
                     corro::PartialVersion p;
-                    if (process_incomplete(bk, w.st, c, [&](uint64_t k) { return row_of(c, i, k); }, p) != CORRO_OK) {
+                    const bool canon = v.canon && v.canon[i];
+                    if (process_incomplete(bk, w.st, c, canon, [&](uint64_t k) { return row_of(c, i, k); }, p) !=
+                        CORRO_OK) {
                         v.known[i] = CORRO_E_INVALID;
                         continue;
                     }
@@ -560,6 +915,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     const uint64_t nchanges = in ? in->n : 0;
     corro::AgentPinned P{};
     TRY_RC(corro::agent_dev_begin(ctx, ncs, nchanges, &P));
+    stage("begin");
     const uint32_t nsites = corro::agent_site_count(ctx);
     std::vector<ActorId> site_id(nsites);
     std::vector<int64_t> site_max(nsites, -1);
@@ -593,17 +949,22 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         w.had_max = w.booked->has_max;
         w.max = w.booked->max;
     }
-    std::vector<corro_changeset> &hcs = R.hcs;
-    std::vector<uint8_t> hflag(hcs.size(), 0);
-    std::vector<int32_t> hknown(hcs.size(), CORRO_KNOWN_SKIPPED);
-    std::vector<uint64_t> local(hcs.size());
-    std::map<uint64_t, uint64_t> inc_row;  // host changeset (local index) -> first fetched row
+    const uint64_t nh = R.nh;
+    const corro_changeset *hcs = R.hcs;
+    std::vector<uint8_t> hflag(nh, 0);
+    std::vector<int32_t> hknown(nh, CORRO_KNOWN_SKIPPED);
+    std::vector<uint64_t> local(nh);
+    std::vector<uint64_t> inc_row(nh, ~0ULL);  // host changeset (local index) -> first fetched row
+    // partial changesets: canonical ones keep their rows in HBM (bufpool.hip) when the bookie's pool
+    // can take them, the others' rows come to the host
+    const bool pool_ok = !bk->pool || corro::bufpool_usable(ctx, bk->pool);
+    const uint8_t *canon = pool_ok ? R.hcanon : nullptr;
     corro::HostSpanRows inc;
-    if (!hcs.empty()) {
-        for (uint64_t k = 0; k < local.size(); k++) local[k] = k;
-        for (uint64_t k = 0; k < hcs.size();) {
+    if (nh) {
+        for (uint64_t k = 0; k < nh; k++) local[k] = k;
+        for (uint64_t k = 0; k < nh;) {
             uint64_t e = k + 1;
-            while (e < hcs.size() && hcs[e].site == hcs[k].site) e++;
+            while (e < nh && hcs[e].site == hcs[k].site) e++;
             ActorWork &w = work[(size_t)work_of[hcs[k].site]];
             w.idx = local.data() + k;
             w.nidx = e - k;
@@ -611,8 +972,9 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         }
         std::vector<corro::AgentSpan> sp;
         uint64_t r = 0;
-        for (uint64_t k = 0; k < hcs.size(); k++)
-            if (hcs[k].kind == CORRO_CS_FULL && hcs[k].change_count && !is_complete(hcs[k]) && !R.hbad[k]) {
+        for (uint64_t k = 0; k < nh; k++)
+            if (hcs[k].kind == CORRO_CS_FULL && hcs[k].change_count && !is_complete(hcs[k]) && !R.hbad[k] &&
+                !(canon && canon[k])) {
                 inc_row[k] = r;
                 sp.push_back({hcs[k].change_off, r, hcs[k].change_count, hcs[k].ts});
                 r += hcs[k].change_count;
@@ -622,7 +984,8 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         stage("partial_rows");
     }
     auto row_of = [&](const corro_changeset &c, uint64_t ci, uint64_t k) -> HostRow {
-        const uint64_t j = inc_row.at(ci) + k;
+        if (inc_row[ci] == ~0ULL) throw std::logic_error("partial changeset rows not fetched");
+        const uint64_t j = inc_row[ci] + k;
         HostRow r;
         r.pk = inc.pk[j];
         r.tcid = inc.tcid[j];
@@ -643,7 +1006,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     std::vector<std::vector<Range>> dev_runs(work.size());
     for (size_t r = 0; r < R.run_site.size(); r++)
         dev_runs[(size_t)work_of[R.run_site[r]]].emplace_back(R.run_start[r], R.run_end[r]);
-    const CsView view{hcs.data(), R.hbad.data(), hknown.data(), hflag.data()};
+    const CsView view{hcs, R.hbad, hknown.data(), hflag.data(), canon};
     run_parallel(work.size(), [&](size_t k) { run_actor_walk(bk, work[k], view, dev_runs[k], row_of); });
     for (ActorWork &w : work)
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);
@@ -652,7 +1015,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         nspans += w.nspans;
         nb += w.nchanges;
     }
-    if (!hcs.empty()) TRY_RC(corro::agent_dev_put_host(ctx, R.hidx, hflag, hknown, out->known));
+    if (nh) TRY_RC(corro::agent_dev_put_host(ctx, R.hidx, nh, hflag, hknown, out->known));
     stage("actors");
 
     const uint32_t ntables = corro::agent_table_count(ctx);
@@ -693,20 +1056,25 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             for (uint64_t version : w.set_dbv) sv.emplace_back(w.site, version);
         TRY_RC(corro::set_db_versions(ctx, sv));
     }
-    for (ActorWork &w : work) {
-        commit_buffered(bk, w.st.buffered, committed);
-        for (auto &[key, sb] : w.st.seqbook) bk->seqbook[key] = sb;
-    }
-    stage("commit_buffered");
-    // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303): the merged versions that hold
-    // buffered rows or seq bookkeeping, found on the device against the (small) set of such keys
-    std::vector<uint64_t> bkeys = buffered_keys(bk);
-    std::vector<std::pair<uint32_t, uint64_t>> sv;
-    TRY_RC(corro::agent_dev_commit_headers(ctx, ncs, out->known, bkeys.empty() ? nullptr : &bkeys, &sv));
-    for (auto &[site, v] : sv) clear_buffered(bk, site, v, v);
     std::vector<size_t> order(work.size());
     for (size_t k = 0; k < order.size(); k++) order[k] = k;
     std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return work[x].id < work[y].id; });
+    {
+        std::vector<Staged *> sto;
+        for (size_t k : order) sto.push_back(&work[k].st);
+        TRY_RC(commit_staged(ctx, bk, nchanges ? &dv : nullptr, sto, committed, stage));
+        commit_seqbook(bk, sto);
+    }
+    stage("seqbook");
+    // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303): the merged versions that hold
+    // buffered rows or seq bookkeeping, found on the device against the (small) set of such keys
+    std::vector<uint64_t> bkeys = buffered_keys(bk);
+    stage("bkeys");
+    std::vector<std::pair<uint32_t, uint64_t>> sv;
+    TRY_RC(corro::agent_dev_commit_headers(ctx, ncs, out->known, bkeys.empty() ? nullptr : &bkeys, &sv));
+    stage("commit_hdr");
+    for (auto &[site, v] : sv) clear_buffered(bk, site, v, v);
+    compact_tables(bk);
     uint64_t nready = 0;
     for (size_t k : order) {
         ActorWork &w = work[k];
@@ -717,8 +1085,10 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     out->n_ready = nready;
     corro_detail_add_committed(ctx, committed.data(), committed.size());
     stage("commit");
+    run_parallel(work.size(), [&](size_t k) { ActorWork gone = std::move(work[k]); }, 16);  // (frees in parallel)
+    stage("free");
     if (prof) fprintf(stderr, "[corro agent dev] ncs=%llu spans=%llu changes=%llu host=%zu ms:%s\n", (unsigned long long)ncs,
-                      (unsigned long long)nspans, (unsigned long long)nb, hcs.size(), prof_line.c_str());
+                      (unsigned long long)nspans, (unsigned long long)nb, (size_t)nh, prof_line.c_str());
     return CORRO_OK;
 }
 
@@ -1043,7 +1413,7 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
     std::vector<std::vector<Range>> fast_runs(work.size());
     for (size_t k = 0; k < nchunk; k++)
         for (auto &[wi, r] : cout[k].runs) fast_runs[wi].push_back(r);
-    const CsView view{cs, bad, out->known, P.flag};
+    const CsView view{cs, bad, out->known, P.flag, nullptr};
     auto run_actor = [&](size_t wi) { run_actor_walk(bk, work[wi], view, fast_runs[wi], row_of); };
     run_parallel(work.size(), [&](size_t k) { run_actor(k); });
     for (ActorWork &w : work)
@@ -1107,9 +1477,14 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
     }
     // corro.changes.committed{table} (util.rs:533-535): every buffered change of an incomplete version
     // (:1101-1105), every impactful change of a complete one (:1254-1258, counted on the device)
-    for (ActorWork &w : work) {
-        commit_buffered(bk, w.st.buffered, committed);
-        for (auto &[key, sb] : w.st.seqbook) bk->seqbook[key] = sb;
+    std::vector<size_t> order(work.size());
+    for (size_t k = 0; k < order.size(); k++) order[k] = k;
+    std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return work[x].id < work[y].id; });
+    {
+        std::vector<Staged *> sto;
+        for (size_t k : order) sto.push_back(&work[k].st);
+        TRY_RC(commit_staged(ctx, bk, nullptr, sto, committed));
+        commit_seqbook(bk, sto);
     }
     // known: Current when the version had an impactful change, else Cleared (util.rs:1264-1287)
     const std::vector<uint64_t> bkeys = buffered_keys(bk);
@@ -1126,10 +1501,8 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
             if (P.flag[i] && cs[i].version_start < (1ULL << 40) &&
                 std::binary_search(bkeys.begin(), bkeys.end(), (uint64_t)cs[i].site << 40 | cs[i].version_start))
                 clear_buffered(bk, cs[i].site, cs[i].version_start, cs[i].version_start);
+    compact_tables(bk);
     // per-actor gap snapshot commit, then partials (util.rs:936-1008), actors in ActorId order
-    std::vector<size_t> order(work.size());
-    for (size_t k = 0; k < order.size(); k++) order[k] = k;
-    std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return work[x].id < work[y].id; });
     uint64_t nready = 0;
     for (size_t k : order) {
         ActorWork &w = work[k];
@@ -1193,9 +1566,10 @@ int corro_process_fully_buffered(corro_ctx *ctx, corro_bookie *bk, const uint8_t
     if (!pit->second.seqs.gaps(0, pit->second.last_seq).empty()) return CORRO_OK;  // gaps: abort
     const uint32_t site = sit->second;
     Batch batch;
-    auto rows = bk->buffered.find({site, (int64_t)version});
-    if (rows != bk->buffered.end())
-        for (const HostRow &r : rows->second) batch.push(r);  // ORDER BY db_version, seq
+    if (BufEntry *rows = bk->buffered.find({site, (int64_t)version})) {
+        TRY_RC(materialize(bk, *rows));
+        for (const HostRow &r : rows->rows) batch.push(r);  // ORDER BY db_version, seq
+    }
     RangeSet v;
     v.insert(version, version);
     corro::Booked nb = booked;  // committed only with the merge (one transaction, util.rs:560-676)
@@ -1210,6 +1584,7 @@ int corro_process_fully_buffered(corro_ctx *ctx, corro_bookie *bk, const uint8_t
         if (rc != CORRO_OK) return rc;
     }
     clear_buffered(bk, site, version, version);
+    compact_tables(bk);
     booked = std::move(nb);
     uint64_t total = 0;
     for (uint8_t x : impact) total += x;
@@ -1267,9 +1642,9 @@ int corro_bookie_seq_bookkeeping(corro_bookie *bk, const uint8_t *actor_id, uint
     *ts = 0;
     auto so = bk->site_of.find(actor_of(actor_id));
     if (so == bk->site_of.end()) return CORRO_OK;
-    auto it = bk->seqbook.find({so->second, version});
-    if (it == bk->seqbook.end()) return CORRO_OK;
-    std::vector<Range> rs = it->second.ranges;
+    const SeqBook *sb = bk->seqbook.find({so->second, version});
+    if (!sb) return CORRO_OK;
+    std::vector<Range> rs = sb->ranges;
     std::sort(rs.begin(), rs.end());
     uint64_t k = 0;
     for (const Range &r : rs) {
@@ -1280,8 +1655,8 @@ int corro_bookie_seq_bookkeeping(corro_bookie *bk, const uint8_t *actor_id, uint
         k++;
     }
     *count = k;
-    *last_seq = (int64_t)it->second.last_seq;
-    *ts = it->second.ts;
+    *last_seq = (int64_t)sb->last_seq;
+    *ts = sb->ts;
     return CORRO_OK;
 }
 
@@ -1294,10 +1669,11 @@ int corro_bookie_buffered_versions(corro_bookie *bk, const uint8_t *actor_id, ui
     auto so = bk->site_of.find(actor_of(actor_id));
     if (so == bk->site_of.end() || vstart > vend || vstart > (uint64_t)INT64_MAX) return CORRO_OK;
     uint64_t k = 0;
-    for (auto it = bk->buffered.lower_bound({so->second, (int64_t)vstart}); it != bk->buffered.end(); ++it) {
-        if (it->first.first != so->second || (uint64_t)it->first.second > vend) break;
-        if (it->second.empty()) continue;
-        if (k < cap) versions[k] = (uint64_t)it->first.second;
+    for (size_t i = bk->buffered.lower({so->second, (int64_t)vstart}); i < bk->buffered.slots(); i++) {
+        const auto &x = bk->buffered.at(i);
+        if (x.key.first != so->second || (uint64_t)x.key.second > vend) break;
+        if (x.dead || x.val.empty()) continue;
+        if (k < cap) versions[k] = (uint64_t)x.key.second;
         k++;
     }
     *count = k;
@@ -1312,11 +1688,13 @@ int corro_bookie_buffered(corro_bookie *bk, const uint8_t *actor_id, uint64_t ve
     *count = 0;
     auto so = bk->site_of.find(actor_of(actor_id));
     if (so == bk->site_of.end()) return CORRO_OK;
-    auto it = bk->buffered.find({so->second, (int64_t)version});
-    if (it == bk->buffered.end() || seq_start > seq_end || seq_start > 0xFFFFFFFFULL) return CORRO_OK;
+    BufEntry *it = version <= (uint64_t)INT64_MAX ? bk->buffered.find({so->second, (int64_t)version}) : nullptr;
+    if (!it || seq_start > seq_end || seq_start > 0xFFFFFFFFULL) return CORRO_OK;
+    TRY_RC(materialize(bk, *it));
+    const BufRows &rows = it->rows;
     const uint32_t hi = seq_end > 0xFFFFFFFFULL ? 0xFFFFFFFFu : (uint32_t)seq_end;
     uint64_t k = 0;
-    for (auto r = buf_lower(it->second, (uint32_t)seq_start); r != it->second.end() && r->seq <= hi; ++r, ++k) {
+    for (auto r = buf_lower(rows, (uint32_t)seq_start); r != rows.end() && r->seq <= hi; ++r, ++k) {
         if (k >= cap) continue;
         const HostRow &h = *r;
         if (o->pk) o->pk[k] = h.pk;
@@ -1343,10 +1721,11 @@ int corro_bookie_buffered_value(corro_bookie *bk, const uint8_t *actor_id, uint6
     *len = 0;
     auto so = bk->site_of.find(actor_of(actor_id));
     if (so == bk->site_of.end() || seq > 0xFFFFFFFFULL) return CORRO_OK;
-    auto it = bk->buffered.find({so->second, (int64_t)version});
-    if (it == bk->buffered.end()) return CORRO_OK;
-    auto r = buf_lower(it->second, (uint32_t)seq);
-    if (r == it->second.end() || r->seq != (uint32_t)seq) return CORRO_OK;
+    BufEntry *it = version <= (uint64_t)INT64_MAX ? bk->buffered.find({so->second, (int64_t)version}) : nullptr;
+    if (!it) return CORRO_OK;
+    TRY_RC(materialize(bk, *it));
+    auto r = buf_lower(it->rows, (uint32_t)seq);
+    if (r == it->rows.end() || r->seq != (uint32_t)seq) return CORRO_OK;
     const std::string &lv = r->lv;
     *len = lv.size();
     std::memcpy(out, lv.data(), std::min<uint64_t>(cap, lv.size()));

@@ -109,16 +109,17 @@ struct DevHdrResult {
     std::vector<uint32_t> run_site;            // decided version runs, grouped by site, ascending
     std::vector<uint64_t> run_start, run_end;
     // the host's changesets in sorted order (grouped by actor, arrival order inside): header, arrival
-    // index, unknown-name flag
-    std::vector<corro_changeset> hcs;
-    std::vector<uint32_t> hidx;
-    std::vector<uint8_t> hbad;
+    // index, unknown-name flag, canonical partial (bufpool.hip); pinned, valid until the next call
+    uint64_t nh;
+    const corro_changeset *hcs;
+    const uint32_t *hidx;
+    const uint8_t *hbad, *hcanon;
 };
 // site_max[s] = the actor's booked max (-1: none); dknown: device, ncs entries
 int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, const corro_changes *dv,
                       const std::vector<int64_t> &site_max, int32_t *dknown, DevHdrResult &res);
 // the host's decisions for its changesets: flag[idx[k]] = flag[k], known[idx[k]] = known[k]
-int agent_dev_put_host(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
+int agent_dev_put_host(corro_ctx *ctx, const uint32_t *idx, uint64_t n, const std::vector<uint8_t> &flag,
                        const std::vector<int32_t> &known, int32_t *dknown);
 // the applied batch in sorted order (flagged changesets only), like agent_dev_batch
 int agent_dev_batch_sorted(corro_ctx *ctx, const corro_changes *dv, uint64_t ncs, uint64_t nspans, uint64_t nbatch,
@@ -141,6 +142,30 @@ int agent_dev_stage_begin(corro_ctx *ctx, uint64_t ncs, HdrStage *st);
 // async upload of headers [lo, hi) (callable from pool threads)
 int agent_dev_stage_upload(corro_ctx *ctx, const HdrStage &st, uint64_t lo, uint64_t hi);
 int agent_dev_stage_known(corro_ctx *ctx, const HdrStage &st, int32_t *known, uint64_t ncs);
+
+// ---- device-resident buffered rows (bufpool.hip) ------------------------------------------------
+// A bookie's pool of __corro_buffered_changes rows in HBM (columns of corro_changes without long
+// values), on the device of the first context that writes it.
+struct DevBufPool;
+DevBufPool *bufpool_new();
+void bufpool_free(DevBufPool *p);
+bool bufpool_usable(corro_ctx *ctx, const DevBufPool *p);
+uint64_t bufpool_top(const DevBufPool *p);
+// per-table counts of the changes of the spans (src, count)
+int agent_dev_table_counts(corro_ctx *ctx, const corro_changes *dv, const std::vector<AgentSpan> &spans,
+                           uint32_t ntables, std::vector<uint64_t> &counts);
+// room for `need` more rows at the top: grows, or compacts the live segments (*offs[k], lens[k]),
+// rewriting their offsets, when at least half of the rows below the top are dead
+int bufpool_reserve(corro_ctx *ctx, DevBufPool *p, uint64_t need, std::vector<uint64_t *> &offs,
+                    const std::vector<uint64_t> &lens);
+// input changes [src, src + count) -> pool rows at the top (dst set per job); ts = the changeset's
+// when the input has no ts
+struct PoolCopy {
+    uint64_t src, count, ts, dst;
+};
+int bufpool_append(corro_ctx *ctx, DevBufPool *p, const corro_changes *dv, std::vector<PoolCopy> &jobs);
+// pool rows [off, off + n) to the host (no long values)
+int bufpool_read(const DevBufPool *p, uint64_t off, uint64_t n, HostSpanRows &out);
 
 // every known entry back to Skipped (a failed call)
 int agent_dev_clear_known(corro_ctx *ctx, int32_t *dknown, uint64_t ncs);

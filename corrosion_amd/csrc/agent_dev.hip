@@ -1044,15 +1044,40 @@ __global__ void __launch_bounds__(AG_T) k_hdr_hlist(uint64_t n, const uint32_t *
         if (hm[j]) hslot[hincl[j] - 1] = (uint32_t)j;
 }
 
-__global__ void __launch_bounds__(AG_T) k_hdr_gather(const corro_changeset *__restrict__ cs, const uint32_t *__restrict__ order,
-                                                      const uint8_t *__restrict__ bad, const uint32_t *__restrict__ slot,
-                                                      uint64_t n, corro_changeset *__restrict__ out, uint32_t *__restrict__ idx,
-                                                      uint8_t *__restrict__ obad) {
-    for (uint64_t k = (uint64_t)blockIdx.x * AG_T + threadIdx.x; k < n; k += (uint64_t)gridDim.x * AG_T) {
-        const uint32_t i = order[slot[k]];
-        out[k] = cs[i];
-        idx[k] = i;
-        obad[k] = bad[i];
+// the host's changesets: header, arrival index, unknown-name flag, and whether a partial one is
+// canonical (bufpool.hip: its k-th change has seq = seq_start + k, its own site and version, no long
+// value -- its rows then stay in HBM)
+struct HGatherArgs {
+    const corro_changeset *cs;
+    const uint32_t *order, *slot;
+    const uint8_t *bad;
+    corro_changes in;
+    uint64_t n;
+    corro_changeset *out;
+    uint32_t *idx;
+    uint8_t *obad, *ocanon;
+};
+
+__global__ void __launch_bounds__(AG_T) k_hdr_gather(HGatherArgs a) {
+    for (uint64_t k = (uint64_t)blockIdx.x * AG_T + threadIdx.x; k < a.n; k += (uint64_t)gridDim.x * AG_T) {
+        const uint32_t i = a.order[a.slot[k]];
+        const corro_changeset c = a.cs[i];
+        a.out[k] = c;
+        a.idx[k] = i;
+        a.obad[k] = a.bad[i];
+        bool canon = c.kind == CORRO_CS_FULL && c.change_count && !(c.seq_start == 0 && c.seq_end == c.last_seq) &&
+                     !a.bad[i] && c.seq_start <= c.seq_end && c.seq_end < 0xFFFFFFFFULL &&
+                     c.change_count == c.seq_end - c.seq_start + 1 && c.version_start <= (uint64_t)INT64_MAX &&
+                     a.in.seq && a.in.site && a.in.db_version;
+        for (uint64_t q = 0; canon && q < c.change_count; q++) {
+            const uint64_t r = c.change_off + q;
+            const uint8_t vt = a.in.val_type ? a.in.val_type[r] : (uint8_t)CORRO_INTEGER;
+            const uint8_t vl = a.in.val_len ? a.in.val_len[r] : 0;
+            canon = a.in.seq[r] == c.seq_start + q && a.in.site[r] == c.site &&
+                    (uint64_t)a.in.db_version[r] == c.version_start &&
+                    !(vl == CORRO_VAL_LONG && (vt == CORRO_TEXT || vt == CORRO_BLOB));
+        }
+        a.ocanon[k] = canon ? 1 : 0;
     }
 }
 
@@ -1258,34 +1283,51 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         CORRO_HIP_TRY(hipMemcpyAsync(res.run_start.data(), h.run_start, 8ULL * nruns, hipMemcpyDeviceToHost, s));
         CORRO_HIP_TRY(hipMemcpyAsync(res.run_end.data(), h.run_end, 8ULL * nruns, hipMemcpyDeviceToHost, s));
     }
-    res.hcs.resize(nh);
-    res.hidx.resize(nh);
-    res.hbad.resize(nh);
-    if (nh) {  // their headers, arrival index and unknown-name flag
-        const size_t o_cs = 0, o_idx = al256((uint64_t)nh * sizeof(corro_changeset)), o_bad = o_idx + al256(nh * 4ULL);
-        if (int rc = ctx->d_agent_fetch.ensure(o_bad + al256(nh))) return rc;
+    res.nh = nh;
+    if (nh) {  // their headers, arrival index, unknown-name and canonical flags: one pinned readback
+        const size_t o_idx = al256((uint64_t)nh * sizeof(corro_changeset)), o_bad = o_idx + al256(nh * 4ULL),
+                     o_can = o_bad + al256(nh), total_b = o_can + al256(nh);
+        if (int rc = ctx->d_agent_fetch.ensure(total_b + 256)) return rc;
+        if (total_b > ctx->h_hfetch_bytes) {
+            if (ctx->h_hfetch) (void)hipHostFree(ctx->h_hfetch);
+            ctx->h_hfetch = nullptr;
+            ctx->h_hfetch_bytes = 0;
+            CORRO_HIP_TRY(hipHostMalloc(&ctx->h_hfetch, total_b + total_b / 4, hipHostMallocDefault));
+            ctx->h_hfetch_bytes = total_b + total_b / 4;
+        }
         uint8_t *base = ctx->d_agent_fetch.as<uint8_t>();
-        hipLaunchKernelGGL(k_hdr_gather, flat_grid(nh), dim3(AG_T), 0, s, dcs, order, c.bad, hslot, (uint64_t)nh,
-                           reinterpret_cast<corro_changeset *>(base + o_cs), reinterpret_cast<uint32_t *>(base + o_idx),
-                           base + o_bad);
+        HGatherArgs g{};
+        g.cs = dcs;
+        g.order = order;
+        g.slot = hslot;
+        g.bad = c.bad;
+        if (dv) g.in = *dv;
+        g.n = nh;
+        g.out = reinterpret_cast<corro_changeset *>(base);
+        g.idx = reinterpret_cast<uint32_t *>(base + o_idx);
+        g.obad = base + o_bad;
+        g.ocanon = base + o_can;
+        hipLaunchKernelGGL(k_hdr_gather, flat_grid(nh), dim3(AG_T), 0, s, g);
         CORRO_HIP_TRY(hipGetLastError());
-        CORRO_HIP_TRY(hipMemcpyAsync(res.hcs.data(), base + o_cs, nh * sizeof(corro_changeset), hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(res.hidx.data(), base + o_idx, nh * 4ULL, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(res.hbad.data(), base + o_bad, nh, hipMemcpyDeviceToHost, s));
+        uint8_t *hp = static_cast<uint8_t *>(ctx->h_hfetch);
+        CORRO_HIP_TRY(hipMemcpyAsync(hp, base, total_b, hipMemcpyDeviceToHost, s));
+        res.hcs = reinterpret_cast<const corro_changeset *>(hp);
+        res.hidx = reinterpret_cast<const uint32_t *>(hp + o_idx);
+        res.hbad = hp + o_bad;
+        res.hcanon = hp + o_can;
     }
     if (nruns || nh) CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;
 }
 
-int agent_dev_put_host(corro_ctx *ctx, const std::vector<uint32_t> &idx, const std::vector<uint8_t> &flag,
+int agent_dev_put_host(corro_ctx *ctx, const uint32_t *idx, uint64_t n, const std::vector<uint8_t> &flag,
                        const std::vector<int32_t> &known, int32_t *dknown) {
-    const uint64_t n = idx.size();
     if (!n) return CORRO_OK;
     hipStream_t s = ctx->stream;
     const size_t o_f = al256(n * 4), o_k = o_f + al256(n);
     if (int rc = ctx->d_agent_aux2.ensure(o_k + al256(n * 4))) return rc;
     uint8_t *base = ctx->d_agent_aux2.as<uint8_t>();
-    CORRO_HIP_TRY(hipMemcpyAsync(base, idx.data(), n * 4, hipMemcpyHostToDevice, s));
+    CORRO_HIP_TRY(hipMemcpyAsync(base, idx, n * 4, hipMemcpyHostToDevice, s));
     CORRO_HIP_TRY(hipMemcpyAsync(base + o_f, flag.data(), n, hipMemcpyHostToDevice, s));
     CORRO_HIP_TRY(hipMemcpyAsync(base + o_k, known.data(), n * 4, hipMemcpyHostToDevice, s));
     const DevCols c = dev_cols(ctx);

@@ -624,6 +624,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
     if (ctx->h_ovf) (void)hipHostFree(ctx->h_ovf);
     if (ctx->h_agent) (void)hipHostFree(ctx->h_agent);
     if (ctx->h_hdr) (void)hipHostFree(ctx->h_hdr);
+    if (ctx->h_hfetch) (void)hipHostFree(ctx->h_hfetch);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -444,3 +444,110 @@ def test_host_headers_staged_to_device_match_restatement(seed, clean, monkeypatc
     calls take; forced here): same outcomes, flags, state and bookkeeping as the restatement"""
     monkeypatch.setenv("CORRO_AGENT_STAGE_HEADERS", "1")
     _check_against_oracle(seed, device=True, clean=clean)
+
+
+def _buffer_calls(seed, nact=3, nver=6, ncalls=5):
+    """Partial versions sent in overlapping pieces across calls: re-sent seqs carry different
+    contents (the stored row must win), some pieces are non-canonical (rows out of seq order, or a
+    row missing), some versions arrive complete."""
+    from oracle.agent import Changeset
+    rng = np.random.default_rng(seed)
+    import synth
+    ids = synth.site_ids(nact, seed)
+    pieces = []
+    for a in range(nact):
+        for v in range(1, nver + 1):
+            k = int(rng.integers(3, 11))
+            ts = int(rng.integers(1, 1 << 30))
+
+            def rows(s, e, a=a, v=v):
+                return [dict(pk=int(rng.integers(1, 7)), table_cid=(0 << 16) | int(rng.integers(1, 5)),
+                             col_version=int(rng.integers(1, 4)), db_version=v, cl=1, seq=q, site=a,
+                             val0=int(rng.integers(0, 1000)), val_type=1) for q in range(s, e + 1)]
+            if rng.random() < 0.15:
+                pieces.append(Changeset(ids[a], "full", version=v, seqs=(0, k - 1), last_seq=k - 1, ts=ts,
+                                        rows=rows(0, k - 1)))
+                continue
+            for _p in range(int(rng.integers(2, 5))):
+                s = int(rng.integers(0, k))
+                e = int(rng.integers(s, k))
+                rr = rows(s, e)
+                r = rng.random()
+                if r < 0.15 and len(rr) > 1:
+                    rr = rr[::-1]                      # out of seq order
+                elif r < 0.25 and len(rr) > 1:
+                    rr = rr[:-1]                       # a row short of the seq range
+                pieces.append(Changeset(ids[a], "full", version=v, seqs=(s, e), last_seq=k - 1, ts=ts, rows=rr))
+            pieces.append(Changeset(ids[a], "full", version=v, seqs=(0, k - 1), last_seq=k - 1, ts=ts,
+                                    rows=rows(0, k - 1)) if rng.random() < 0.1 else
+                          Changeset(ids[a], "full", version=v, seqs=(0, 0), last_seq=k - 1, ts=ts, rows=rows(0, 0)))
+    order = rng.permutation(len(pieces))
+    calls = [[] for _ in range(ncalls)]
+    for j in order:
+        calls[int(rng.integers(0, ncalls))].append(pieces[j])
+    return ids, calls
+
+
+def _bookie_buffers(bk, ids, nver):
+    from corrosion_amd import serve
+    out = {}
+    for a in ids:
+        for v in range(1, nver + 1):
+            rows, n = serve._buffered_rows(bk, bytes(a), v, 0, (1 << 32) - 1)
+            out[(bytes(a), v)] = sorted(zip(*[rows[k][:n].tolist() for k in sorted(rows)]))
+    return out
+
+
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_device_buffered_rows_match_host_path(seed):
+    """Partial changesets of a device-header call keep their rows in HBM (bufpool.hip): pieces re-sent
+    with other contents (ON CONFLICT DO NOTHING: the stored row wins), non-canonical pieces next to
+    canonical ones of the same version (the key goes to the host), buffered rows read back, and
+    process_fully_buffered_changes of every ready version -- outcomes, buffered rows, committed
+    counts, merged state and bookkeeping equal to the host-memory path's"""
+    import corrosion_amd as ca
+    from corrosion_amd import _lib as L
+    nver = 6
+    ids, calls = _buffer_calls(seed, nver=nver)
+    sides = []
+    for _k in range(2):
+        eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12)
+        ords = eng.register_sites(ids)
+        sides.append((eng, ca.agent.Bookie(), {bytes(ids[q]): int(ords[q]) for q in range(len(ids))}))
+    for c in (c for call in calls for c in call):
+        for r in c.rows:
+            r["site"] = sides[0][2][bytes(c.actor)]
+    assert sides[0][2] == sides[1][2]
+
+    def ready(bk):
+        n = C.c_uint64()
+        L.check(L.lib().corro_bookie_take_ready(bk._h, None, None, 0, C.byref(n)))
+        act = (C.c_uint8 * (16 * max(1, n.value)))()
+        ver = (C.c_uint64 * max(1, n.value))()
+        L.check(L.lib().corro_bookie_take_ready(bk._h, act, ver, n.value, C.byref(n)))
+        return [(bytes(act[16 * k:16 * k + 16]), int(ver[k])) for k in range(n.value)]
+
+    for ci, call in enumerate(calls):
+        got = [_run(eng, bk, o, call, dev)[0] for (eng, bk, o), dev in zip(sides, ("headers", False))]
+        assert got[0] == got[1]
+        if ci == 2:   # a read in the middle: device keys come to the host, later pieces mix with them
+            assert _bookie_buffers(sides[0][1], ids, nver) == _bookie_buffers(sides[1][1], ids, nver)
+        rd = [ready(bk) for _e, bk, _o in sides]
+        assert rd[0] == rd[1]
+        for a, v in rd[0]:
+            imp = []
+            for eng, bk, _o in sides:
+                r = C.c_int()
+                L.check(L.lib().corro_process_fully_buffered(eng._h, bk._h, a, v, C.byref(r)))
+                imp.append(r.value)
+            assert imp[0] == imp[1]
+    assert _bookie_buffers(sides[0][1], ids, nver) == _bookie_buffers(sides[1][1], ids, nver)
+    (ea, ba, _), (eb, bb, _) = sides
+    assert canon_rows(ea.export()) == canon_rows(eb.export())
+    assert list(ea.db_versions()) == list(eb.db_versions())
+    assert ea.committed("t") == eb.committed("t")
+    for a in ids:
+        assert ba.last(bytes(a)) == bb.last(bytes(a))
+        assert ba.needed(bytes(a)) == bb.needed(bytes(a))
+        for v in range(1, nver + 1):
+            assert ba.partial(bytes(a), v) == bb.partial(bytes(a), v)
