@@ -216,7 +216,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-rank-child", type=int, default=0, help=argparse.SUPPRESS)  # world size emulated
     args = ap.parse_args()
+    if args.pmc_rank_child:
+        run_rank_child(args, args.pmc_rank_child)
+        return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
@@ -229,10 +233,44 @@ def main():
     if world == 1 and not args.pmc_child and not args.no_pmc and rank == 0:
         traffic, traffic_note, traffic_kern = pmc_traffic_live(args.changes or N_CHANGES)
 
+    if world > 1 and not args.no_pmc and rank == 0:
+        # per-rank traffic of the step's local kernels, before this rank touches its GPU (the other
+        # ranks wait in the process-group rendezvous meanwhile)
+        G = (args.changes or N_GLOBAL_C3) if args.mode == "strong" else (args.changes or N_CHANGES) * world
+        child = [os.path.abspath(__file__), "--pmc-rank-child", str(world), "--changes", str(G), "--mode", args.mode,
+                 "--steps", "2", "--warmup", "1"]
+        traffic, traffic_note, traffic_kern = pmc_traffic_live(G // world, applies=3, child_cmd=child)
+
     if world == 1:
         run_single(args, traffic, traffic_note, traffic_kern)
     else:
-        run_multi(args, world, rank)
+        run_multi(args, world, rank, (traffic, traffic_note, traffic_kern))
+
+
+def run_rank_child(args, world):
+    """(PMC child) one rank's local kernels of the N > 1 step on one GPU: rank 0's slice, the slot
+    partition for `world` destinations, the unpack of an equal-size received slot buffer (its own
+    slots stand in for the peers': the same bytes and counts) and the mapped merge. The all-to-alls
+    are not run: RCCL's copies are not the library's kernels."""
+    import torch
+    import synth
+    import corrosion_amd as ca
+    from corrosion_amd.dist import slot_cap
+    strong = args.mode == "strong"
+    G = args.changes
+    n_local = G // world
+    npk = N_PK_C3 if strong else N_PK * world
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=max(n_local, 1), device=0)
+    eng.register_sites(synth.site_ids(N_ACTORS, 1))
+    batch = synth.uniform_batch_torch(n_local, N_ACTORS, npk, N_COLS, seed=synth.config_seed(3), device="cuda:0",
+                                      offset=0, global_n=G)
+    cap = slot_cap(n_local, world)
+    for _ in range(args.warmup + args.steps):
+        eng.reset()
+        recs, cnt = eng.partition_slots(batch, world, cap)
+        eng.apply_mapped(eng.unpack_slots(recs, world, cap, cnt))
+    torch.cuda.synchronize()
+    eng.close()
 
 
 def run_single(args, traffic, traffic_note, traffic_kern=None):
@@ -590,7 +628,7 @@ def agent_e2e_mixed(eng, batch, n, fast_ms=None, reps=3, resend=0.10, partial=0.
                     f"median of {reps}"}
 
 
-def run_multi(args, world, rank):
+def run_multi(args, world, rank, pmc=(None, "not measured (--no-pmc)", None)):
     import torch
     import torch.distributed as dist
     import synth
@@ -691,8 +729,15 @@ def run_multi(args, world, rank):
         achieved = alg / (dt / args.steps) / 1e9
         roof = {"bound": "hbm", "kernel": "step: slot partition + two equal-split all-to-alls + unpack + mapped merge, all ranks",
                 "achieved": achieved, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
-                "frac": achieved / (HBM_PEAK_GBS * world), "traffic": None,
-                "traffic_source": "not measured at N > 1 (the N = 1 line carries the PMC passes)",
+                "frac": achieved / (HBM_PEAK_GBS * world),
+                "traffic": pmc[0] * world if pmc[0] else None,
+                "traffic_per_rank": pmc[0],
+                "traffic_source": (pmc[1] + "; per rank: rank 0's slice through the slot partition, unpack and "
+                                   "mapped merge on one GPU (RCCL's copies excluded), x N for the node")
+                if pmc[0] else pmc[1],
+                "traffic_ratio": (pmc[0] * world / alg) if pmc[0] else None,
+                "traffic_by_kernel_per_rank": ({k: {"fetch": round(v["fetch"]), "write": round(v["write"])}
+                                                for k, v in sorted(pmc[2].items())} if pmc[2] else None),
                 "alg_bytes_per_step": alg, "exchange_bytes_per_step": moved, "cells": cells}
         cpu = None if args.no_cpu_baseline else cpu_baseline_sample(npk)
         line = {

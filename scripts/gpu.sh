@@ -9,6 +9,7 @@
 #   smoke      __graft_entry__.smoke()
 #   tests      every -m gpu test (TESTS= narrows it, e.g. TESTS="tests/test_gpu_agent_device.py")
 #   bench      python bench.py (defaults: config 2, live PMC traffic, cpu baseline)
+#   multi2     the N > 1 line rehearsed with 2 gloo ranks on the one GPU (2^26 global changes)
 #   quick      python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-pmc
 #   trace      kernel trace + stats of a short bench run (gpurun_out/$OUT/trace)
 #   pmc        FETCH_SIZE / WRITE_SIZE / SQ groups over a short bench run, one pass each
@@ -42,6 +43,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1100 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python -u bench.py ;;
+    multi2) CORRO_BENCH_BACKEND=gloo step multi2 600 python -u bench.py --gpus 2 --changes $((1 << 26)) --steps 3 --warmup 1 ;;
     quick) step quick 300 $B ;;
     trace) step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $B
            kstats "$OUT/trace" ;;
