@@ -383,6 +383,9 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
         uint64_t a, b;  // (host) rows [a, b) of st->buffered, all of this key
         uint64_t fr;    // (dev, fetched) first row in the fetched rows
     };
+    bool any_items = false;
+    for (Staged *st : order) any_items |= !st->items.empty();
+    if (!any_items) return CORRO_OK;
     // per actor (in parallel): its subs sorted by (key, call), call = ActorId rank << 40 | walk index;
     // the actors' blocks concatenated by first key are globally sorted unless two actors share a key
     std::vector<std::vector<Sub>> per(order.size());
@@ -1085,7 +1088,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     out->n_ready = nready;
     corro_detail_add_committed(ctx, committed.data(), committed.size());
     stage("commit");
-    run_parallel(work.size(), [&](size_t k) { ActorWork gone = std::move(work[k]); }, 16);  // (frees in parallel)
+    if (nh >= 4096) run_parallel(work.size(), [&](size_t k) { ActorWork gone = std::move(work[k]); }, 16);  // (frees in parallel)
     stage("free");
     if (prof) fprintf(stderr, "[corro agent dev] ncs=%llu spans=%llu changes=%llu host=%zu ms:%s\n", (unsigned long long)ncs,
                       (unsigned long long)nspans, (unsigned long long)nb, (size_t)nh, prof_line.c_str());

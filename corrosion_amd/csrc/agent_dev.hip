@@ -17,6 +17,8 @@
 #include <cstring>
 
 #include "agent_dev.h"
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 
 #include "internal.h"
@@ -133,7 +135,13 @@ __global__ void __launch_bounds__(AG_T) k_first_imp(const uint8_t *__restrict__ 
         const unsigned long long y = __shfl_xor(best, d);
         best = y < best ? y : best;
     }
-    if ((threadIdx.x & 63) == 0 && best != ~0ULL) atomicMin(first, best);
+    __shared__ unsigned long long l_b[AG_T / 64];
+    if ((threadIdx.x & 63) == 0) l_b[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one atomic per workgroup (same-address atomics serialise at the L2)
+        for (int k = 1; k < AG_T / 64; k++) best = l_b[k] < best ? l_b[k] : best;
+        if (best != ~0ULL) atomicMin(first, best);
+    }
 }
 
 // Per-position passes over the applied batch. Application positions [0, nbatch) are covered by the
@@ -463,8 +471,12 @@ dim3 flat_grid(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, std::mi
 }  // namespace
 
 int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, uint64_t nchanges, AgentPinned *p) {
+    static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
     CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));  // (the pinned area may still feed a copy)
+    const double t_sync = ms();
     const uint64_t n = std::max<uint64_t>(ncs, 1);
     const size_t c8 = al256(n * 8), c4 = al256(n * 4), c1 = al256(n);
     const size_t total = 3 * c8 + c4 + 3 * c1 + 8 * 65536;
@@ -488,10 +500,16 @@ int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, uint64_t nchanges, AgentPinned
     ctx->agent_ncs = ncs;
     ctx->agent_nbatch_max = nchanges;
     ctx->agent_sorted_mode = false;
+    const double t_pin = ms();
     size_t dtotal = 0;
     (void)dev_cols(ctx, &dtotal);
+    const double t_cols = ms();
     if (int rc = ctx->d_agent_spans.ensure(dtotal + 256)) return rc;
-    return ctx->d_agent_out.ensure(256 + 8 * 65536);
+    const int rc = ctx->d_agent_out.ensure(256 + 8 * 65536);
+    if (prof)
+        fprintf(stderr, "[corro agent dev begin] sync=%.3f pinned=%.3f cols=%.3f ensure=%.3f ms\n", t_sync, t_pin - t_sync,
+                t_cols - t_pin, ms() - t_cols);
+    return rc;
 }
 
 int agent_dev_input(corro_ctx *ctx, const corro_changes *in, int mem, corro_changes *dv) {
@@ -763,39 +781,60 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
 // ---- device-resident headers ------------------------------------------------------------------
 namespace {
 
-// Header-mode columns in d_agent_hdr (n = changesets, m = sites), per changeset i unless noted:
-//   ver u64 (version start) | vend u64 | kd u8 (kind, seqs flag) | dec u8 (decided on the device) |
-//   inrun u8 [slot of order2] | emp u8 (set_db_version(vend) at commit) | rflag u32 [order2] |
-//   rincl u32 [order2] | run_site u32 | run_start u64 | run_end u64 | key2 u64 | key2' u64 |
-//   val2 u32 | val2' u32 (the (rank, version) sort: order2) | segk u32 [order2] | vend2 u64 [order2] |
-//   rmax u64 [order2] | ghead u32 [order2] | gincl u32 [order2] | gfirst u32 | glast u32 |
-//   site_max i64[m] | gstart u32[m] | gend u32[m] | ctl u64[8] (0 err, 1 ts_any, 2 nspans, 3 nchanges)
+// One changeset's header fields the decision passes read, packed (32 B: one line fetch per gather)
+struct HdrPack {
+    uint64_t vs, ve;     // versions(): Full v..=v, Empty its range, EmptySet the dummy 0..=0
+    uint32_t site, cnt;  // site ordinal; change count of a non-empty Full (clamped to 32 bits)
+    uint32_t kd;         // kind byte (KD_*)
+    uint32_t pad;
+};
+static_assert(sizeof(HdrPack) == 32, "HdrPack is 32 B");
+struct RunRec {          // a version run of decided changesets
+    uint64_t start, end;
+    uint32_t site, pad;
+};
+static_assert(sizeof(RunRec) == 24, "RunRec is 24 B");
+
+// kind byte: bits 0-1 the CORRO_CS_* kind, bit 2 a complete Full version, bit 3 the unknown-name screen
+constexpr uint32_t KD_COMPLETE = 4, KD_BAD = 8;
+
+// Header-mode columns in d_agent_hdr (n = changesets, m = sites), per changeset i unless noted
+// ([q]: per slot of order2, the (site rank, version start) sort):
+//   pack HdrPack | dec u8 (decided on the device) | inrun u8 [q] | emp u8 (set_db_version(ve) at
+//   commit) | rflag u32 [q] | rincl u32 [q] | runs RunRec | key2 u64 | key2' u64 | val2 u32 | val2'
+//   u32 (order2) | segk u32 [q] | ver2 u64 [q] | vend2 u64 [q] | rmax u64 [q] | kd2 u8 [q] | cnt2 u32
+//   [q] | ghead u32 [q] | gincl u32 [q] | gfirst u32 | glast u32 | site_max i64[m] | then, adjacent
+//   (one readback): ctl u64[8] (0 err, 1 ts_any, 2 nspans, 3 nchanges, 4 max version start, 6 runs,
+//   7 host changesets) | gstart u32[m] | gend u32[m]
 struct HdrCols {
-    uint64_t *ver, *vend;
-    uint8_t *kd, *dec, *inrun, *emp;
-    uint32_t *rflag, *rincl, *run_site;
-    uint64_t *run_start, *run_end;
+    HdrPack *pack;
+    uint8_t *dec, *inrun, *emp;
+    uint32_t *rflag, *rincl;
+    RunRec *runs;
     uint64_t *key2, *key2b;
     uint32_t *val2, *val2b, *segk;
-    uint64_t *vend2, *rmax;
+    uint64_t *ver2, *vend2, *rmax;
+    uint8_t *kd2;
+    uint32_t *cnt2;
     uint32_t *ghead, *gincl, *gfirst, *glast;
     int64_t *site_max;
-    uint32_t *gstart, *gend;
+    unsigned long long *part;  // per-workgroup partials: [0, 8192) max version start, then nspans, nchanges
     unsigned long long *ctl;
+    uint32_t *gstart, *gend;
+    size_t summary_bytes;  // ctl .. gend
 };
 
 HdrCols hdr_cols(corro_ctx *ctx, uint64_t ncs, uint32_t nsites, size_t *total = nullptr) {
     const uint64_t n = std::max<uint64_t>(ncs, 1), m = std::max<uint32_t>(nsites, 1);
-    const size_t sz[] = {n * 8, n * 8, n, n, n, n, n * 4, n * 4, n * 4, n * 8, n * 8, n * 8, n * 8, n * 4, n * 4, n * 4,
-                         n * 8, n * 8, n * 4, n * 4, n * 4, n * 4, m * 8, m * 4, m * 4, 64};
+    const size_t sz[] = {n * 32, n, n, n, n * 4, n * 4, n * 24, n * 8, n * 8, n * 4, n * 4, n * 4, n * 8, n * 8, n * 8,
+                         n, n * 4, n * 4, n * 4, n * 4, n * 4, m * 8, 3 * 8192 * 8, 64, m * 4, m * 4};
     HdrCols h{};
-    void **dst[] = {(void **)&h.ver,   (void **)&h.vend,     (void **)&h.kd,      (void **)&h.dec,
-                    (void **)&h.inrun, (void **)&h.emp,      (void **)&h.rflag,   (void **)&h.rincl,
-                    (void **)&h.run_site, (void **)&h.run_start, (void **)&h.run_end, (void **)&h.key2,
-                    (void **)&h.key2b, (void **)&h.val2,     (void **)&h.val2b,   (void **)&h.segk,
-                    (void **)&h.vend2, (void **)&h.rmax,     (void **)&h.ghead,   (void **)&h.gincl,
-                    (void **)&h.gfirst, (void **)&h.glast,   (void **)&h.site_max,
-                    (void **)&h.gstart, (void **)&h.gend,    (void **)&h.ctl};
+    void **dst[] = {(void **)&h.pack,  (void **)&h.dec,   (void **)&h.inrun, (void **)&h.emp,   (void **)&h.rflag,
+                    (void **)&h.rincl, (void **)&h.runs,  (void **)&h.key2,  (void **)&h.key2b, (void **)&h.val2,
+                    (void **)&h.val2b, (void **)&h.segk,  (void **)&h.ver2,  (void **)&h.vend2, (void **)&h.rmax,
+                    (void **)&h.kd2,   (void **)&h.cnt2,  (void **)&h.ghead, (void **)&h.gincl, (void **)&h.gfirst,
+                    (void **)&h.glast, (void **)&h.site_max, (void **)&h.part, (void **)&h.ctl, (void **)&h.gstart,
+                    (void **)&h.gend};
     static_assert(sizeof(sz) / sizeof(sz[0]) == sizeof(dst) / sizeof(dst[0]), "one size per column");
     uint8_t *base = ctx->d_agent_hdr.as<uint8_t>();
     size_t o = 0;
@@ -803,6 +842,7 @@ HdrCols hdr_cols(corro_ctx *ctx, uint64_t ncs, uint32_t nsites, size_t *total = 
         if (base) *dst[k] = base + o;
         o += al256(sz[k]);
     }
+    h.summary_bytes = al256(64) + 2 * al256(m * 4);
     if (total) *total = o;
     return h;
 }
@@ -813,25 +853,23 @@ struct HdrArgs {
     uint32_t nsites;
     const uint32_t *tcid;          // the input's table_cid (device)
     const uint32_t *site_rank;
-    uint64_t *off, *cnt, *ts, *ver, *key;
+    uint64_t *off, *cnt, *ts, *key;
     uint32_t *site, *val;
-    uint8_t *flag, *bad, *emp;
+    uint8_t *flag, *bad, *emp, *dec;
     int32_t *known;
-    unsigned long long *ctl;
-    uint64_t *vend, *key2;
-    uint32_t *val2;
-    uint8_t *kd, *dec;
+    unsigned long long *ctl, *part;
+    HdrPack *pack;
 };
 
-// kind byte: bits 0-1 the CORRO_CS_* kind, bit 2 a complete Full version
-constexpr uint8_t KD_COMPLETE = 4;
 // versions at or above 2^40 - 1 share one sort key (arrival order among them): never decided
-constexpr uint64_t VCLAMP = (1ULL << 40) - 1;
+constexpr uint64_t VCLAMP40 = (1ULL << 40) - 1;
 
-// one thread per changeset: span check, unknown-name screen, the per-changeset columns, sort keys
+// one thread per changeset: span check, unknown-name screen, the per-changeset columns, the first
+// sort's key, the largest version start below 2^40 - 1 (sizes the second sort's key)
 __global__ void __launch_bounds__(AG_T) k_hdr(HdrArgs a) {
     bool tsb = false;
     uint32_t err = 0;
+    unsigned long long vmax = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * AG_T + threadIdx.x; i < a.ncs; i += (uint64_t)gridDim.x * AG_T) {
         const corro_changeset c = a.cs[i];
         const bool full = c.kind == CORRO_CS_FULL && c.change_count;
@@ -850,26 +888,95 @@ __global__ void __launch_bounds__(AG_T) k_hdr(HdrArgs a) {
         a.dec[i] = 0;
         a.known[i] = CORRO_KNOWN_SKIPPED;
         const bool comp = c.kind == CORRO_CS_FULL && c.seq_start == 0 && c.seq_end == c.last_seq;
-        a.kd[i] = (uint8_t)((c.kind & 3u) | (comp ? KD_COMPLETE : 0));
-        // versions(): Full v..=v, Empty its range, EmptySet the dummy 0..=0 (broadcast.rs:170-178)
-        const uint64_t vs = c.kind == CORRO_CS_EMPTY_SET ? 0 : c.version_start;
-        const uint64_t ve = c.kind == CORRO_CS_EMPTY_SET ? 0 : (c.kind == CORRO_CS_EMPTY ? c.version_end : c.version_start);
-        a.ver[i] = vs;
-        a.vend[i] = ve;
-        a.bad[i] = full && ok && span_has_unknown(a.tcid, c.change_off, c.change_count) ? 1 : 0;
-        const uint64_t rank = c.site < a.nsites ? a.site_rank[c.site] : 0;
-        a.key[i] = rank;
+        const bool bad = full && ok && span_has_unknown(a.tcid, c.change_off, c.change_count);
+        a.bad[i] = bad ? 1 : 0;
+        HdrPack pk;
+        pk.vs = c.kind == CORRO_CS_EMPTY_SET ? 0 : c.version_start;
+        pk.ve = c.kind == CORRO_CS_EMPTY_SET ? 0 : (c.kind == CORRO_CS_EMPTY ? c.version_end : c.version_start);
+        pk.site = c.site;
+        pk.cnt = full ? (uint32_t)(c.change_count < 0xFFFFFFFFULL ? c.change_count : 0xFFFFFFFFULL) : 0u;
+        pk.kd = (c.kind & 3u) | (comp ? KD_COMPLETE : 0u) | (bad ? KD_BAD : 0u);
+        pk.pad = 0;
+        a.pack[i] = pk;
+        if (pk.vs < VCLAMP40 && pk.vs > vmax) vmax = pk.vs;
+        a.key[i] = c.site < a.nsites ? a.site_rank[c.site] : 0;
         a.val[i] = (uint32_t)i;
-        a.key2[i] = rank << 40 | (vs < VCLAMP ? vs : VCLAMP);
-        a.val2[i] = (uint32_t)i;
         tsb |= c.ts != 0;
     }
+    __shared__ unsigned long long l_v[AG_T / 64];
     const unsigned long long anyts = __ballot(tsb);
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d);
+    for (int d = 32; d >= 1; d >>= 1) {
+        err |= __shfl_xor(err, d);
+        const unsigned long long y = __shfl_xor(vmax, d);
+        vmax = y > vmax ? y : vmax;
+    }
     if ((threadIdx.x & 63) == 0) {
-        if (err) atomicOr(&a.ctl[0], (unsigned long long)err);
-        if (anyts) a.ctl[1] = 1;  // (a plain store of 1)
+        if (err) atomicOr(&a.ctl[0], (unsigned long long)err);  // (rare: a malformed call)
+        if (anyts) a.ctl[1] = 1;                                // (a plain store of 1)
+        l_v[threadIdx.x >> 6] = vmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one partial per workgroup (no same-address atomics), k_hdr_reduce folds them
+        unsigned long long m = 0;
+        for (int k = 0; k < AG_T / 64; k++) m = l_v[k] > m ? l_v[k] : m;
+        a.part[blockIdx.x] = m;
+    }
+}
+
+// fold per-workgroup partials: ctl[4] = max of part[0, nb); with sums, ctl[2] += sum part[8192 + ..],
+// ctl[3] += sum part[16384 + ..]
+__global__ void __launch_bounds__(1024) k_hdr_reduce(const unsigned long long *__restrict__ part, uint32_t nb, int sums,
+                                                      unsigned long long *__restrict__ ctl) {
+    __shared__ unsigned long long l[3][1024 / 64];
+    unsigned long long m = 0, x = 0, y = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+        if (sums) {
+            x += part[8192 + b];
+            y += part[16384 + b];
+        } else {
+            m = part[b] > m ? part[b] : m;
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long q = __shfl_xor(m, d);
+        m = q > m ? q : m;
+        x += __shfl_xor(x, d);
+        y += __shfl_xor(y, d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        l[0][threadIdx.x >> 6] = m;
+        l[1][threadIdx.x >> 6] = x;
+        l[2][threadIdx.x >> 6] = y;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 1024 / 64; k++) {
+            m = l[0][k] > l[0][0] ? l[0][k] : l[0][0];
+            l[0][0] = m;
+            l[1][0] += l[1][k];
+            l[2][0] += l[2][k];
+        }
+        if (sums) {
+            ctl[2] += l[1][0];
+            ctl[3] += l[2][0];
+        } else {
+            ctl[4] = l[0][0];
+        }
+    }
+}
+
+// the second sort's key: site rank << vbits | version start (clamped at vclamp = 2^vbits - 1)
+__global__ void __launch_bounds__(AG_T) k_hdr_key2(uint64_t ncs, const HdrPack *__restrict__ pack,
+                                                    const uint32_t *__restrict__ site_rank, uint32_t nsites,
+                                                    uint32_t vbits, uint64_t *__restrict__ key2, uint32_t *__restrict__ val2) {
+    const uint64_t vclamp = (1ULL << vbits) - 1;
+    for (uint64_t i = (uint64_t)blockIdx.x * AG_T + threadIdx.x; i < ncs; i += (uint64_t)gridDim.x * AG_T) {
+        const HdrPack pk = pack[i];
+        const uint64_t rank = pk.site < nsites ? site_rank[pk.site] : 0;
+        key2[i] = rank << vbits | (pk.vs < vclamp ? pk.vs : vclamp);
+        val2[i] = (uint32_t)i;
     }
 }
 
@@ -895,25 +1002,34 @@ __global__ void __launch_bounds__(AG_T) k_hdr_sites(const uint32_t *__restrict__
 // changeset of version 0) is always contained (agent.rs:1353-1361): skipped. Everything else -- an
 // overlap, an incomplete (partial) version, a version at or below the max -- is walked by the host
 // with the reference's per-actor code, and never touches the versions of a decided changeset.
-__device__ inline bool same_key(const corro_changeset *cs, const uint64_t *ver, const uint64_t *vend,
-                                const uint8_t *kd, uint32_t a, uint32_t b) {
-    if (ver[a] != ver[b] || vend[a] != vend[b]) return false;
-    const bool sa = (kd[a] & 3u) == CORRO_CS_FULL, sb = (kd[b] & 3u) == CORRO_CS_FULL;  // seqs: Full only
+__device__ inline bool same_key(const corro_changeset *cs, const HdrPack &x, const HdrPack &y, uint32_t a, uint32_t b) {
+    if (x.vs != y.vs || x.ve != y.ve) return false;
+    const bool sa = (x.kd & 3u) == CORRO_CS_FULL, sb = (y.kd & 3u) == CORRO_CS_FULL;  // seqs: Full only
     if (sa != sb) return false;
     return !sa || (cs[a].seq_start == cs[b].seq_start && cs[a].seq_end == cs[b].seq_end);
 }
 
+// the slot-ordered copies the decision reads (one 32-B gather per slot) and the dedup-group heads
 __global__ void __launch_bounds__(AG_T) k_iso_prep(const corro_changeset *__restrict__ cs, const uint32_t *__restrict__ order2,
-                                                    uint64_t n, const uint32_t *__restrict__ site,
-                                                    const uint64_t *__restrict__ ver, const uint64_t *__restrict__ vend,
-                                                    const uint8_t *__restrict__ kd, uint32_t *__restrict__ segk,
-                                                    uint64_t *__restrict__ vend2, uint32_t *__restrict__ ghead) {
+                                                    uint64_t n, const HdrPack *__restrict__ pack, uint32_t *__restrict__ segk,
+                                                    uint64_t *__restrict__ ver2, uint64_t *__restrict__ vend2,
+                                                    uint8_t *__restrict__ kd2, uint32_t *__restrict__ cnt2,
+                                                    uint32_t *__restrict__ ghead) {
     for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < n; q += (uint64_t)gridDim.x * AG_T) {
         const uint32_t i = order2[q];
-        segk[q] = site[i];
-        vend2[q] = vend[i];
-        const uint32_t p = q ? order2[q - 1] : 0u;
-        ghead[q] = (q == 0 || site[p] != site[i] || !same_key(cs, ver, vend, kd, p, i)) ? 1u : 0u;
+        const HdrPack x = pack[i];
+        segk[q] = x.site;
+        ver2[q] = x.vs;
+        vend2[q] = x.ve;
+        kd2[q] = (uint8_t)x.kd;
+        cnt2[q] = x.cnt;
+        bool head = q == 0;
+        if (!head) {
+            const uint32_t p = order2[q - 1];
+            const HdrPack y = pack[p];
+            head = y.site != x.site || !same_key(cs, y, x, p, i);
+        }
+        ghead[q] = head ? 1u : 0u;
     }
 }
 
@@ -928,14 +1044,14 @@ __global__ void __launch_bounds__(AG_T) k_iso_groups(uint64_t n, const uint32_t 
 }
 
 struct IsoArgs {
-    const uint32_t *order2, *segk, *gincl, *gfirst, *glast;
-    const uint64_t *ver, *vend, *rmax, *cnt;
-    const uint8_t *kd, *bad;
+    const uint32_t *order2, *segk, *gincl, *gfirst, *glast, *cnt2;
+    const uint64_t *ver2, *vend2, *rmax;
+    const uint8_t *kd2;
     const int64_t *site_max;
     uint8_t *dec, *flag, *emp, *inrun;
     int32_t *known;
-    unsigned long long *ctl;
-    uint64_t n;
+    unsigned long long *part;
+    uint64_t n, vclamp;
 };
 
 __global__ void __launch_bounds__(AG_T) k_iso_decide(IsoArgs a) {
@@ -943,38 +1059,39 @@ __global__ void __launch_bounds__(AG_T) k_iso_decide(IsoArgs a) {
     unsigned long long nsp = 0, nch = 0;
     for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < a.n; q += (uint64_t)gridDim.x * AG_T) {
         const uint32_t i = a.order2[q];
+        const uint64_t vs_q = a.ver2[q], ve_q = a.vend2[q];
         uint8_t in = 0;
-        if (a.ver[i] == 0 && a.vend[i] == 0) {
+        if (vs_q == 0 && ve_q == 0) {
             a.dec[i] = 1;  // versions() == 0..=0: always contained (pass 1 skips it)
-        } else if (a.ver[i] != 0 && a.ver[i] <= a.vend[i] && a.ver[i] < VCLAMP) {
-            const uint32_t g = a.gincl[q] - 1, f = a.gfirst[g], l = a.glast[g], fi = a.order2[f];
-            const uint64_t vs = a.ver[fi], ve = a.vend[fi];
+        } else if (vs_q != 0 && vs_q <= ve_q && vs_q < a.vclamp) {
+            const uint32_t g = a.gincl[q] - 1, f = a.gfirst[g], l = a.glast[g];
+            const uint64_t vs = a.ver2[f], ve = a.vend2[f];
             const bool prev_ov = f > 0 && a.segk[f - 1] == a.segk[f] && a.rmax[f - 1] >= vs;
             bool next_ov = false;
             if (l + 1 < a.n && a.segk[l + 1] == a.segk[l]) {
-                const uint64_t nv = a.ver[a.order2[l + 1]];
-                next_ov = nv <= ve || (nv >= VCLAMP && ve >= VCLAMP);
+                const uint64_t nv = a.ver2[l + 1];
+                next_ov = nv <= ve || (nv >= a.vclamp && ve >= a.vclamp);
             }
             const int64_t mx = a.site_max[a.segk[q]];
-            const uint32_t kind = a.kd[fi] & 3u;
+            const uint32_t kd = a.kd2[f], kind = kd & 3u;
             const bool decidable = !prev_ov && !next_ov && (mx < 0 || vs > (uint64_t)mx) &&
-                                   (kind == CORRO_CS_EMPTY || (kind == CORRO_CS_FULL && (a.kd[fi] & KD_COMPLETE)));
+                                   (kind == CORRO_CS_EMPTY || (kind == CORRO_CS_FULL && (kd & KD_COMPLETE)));
             if (decidable && q != f) {
                 a.dec[i] = 1;  // a later copy of the group's key: pass 1's seen set skips it
             } else if (decidable) {
                 a.dec[i] = 1;
-                if (kind == CORRO_CS_EMPTY || a.cnt[i] == 0) {  // process_empty_version (above the max)
+                if (kind == CORRO_CS_EMPTY || a.cnt2[q] == 0) {  // process_empty_version (above the max)
                     a.known[i] = CORRO_KNOWN_CLEARED;
                     a.emp[i] = 1;
                     in = 1;
-                } else if (a.bad[i]) {  // the version's SAVEPOINT rolls back alone (util.rs:839-860)
+                } else if (kd & KD_BAD) {  // the version's SAVEPOINT rolls back alone (util.rs:839-860)
                     a.known[i] = CORRO_E_UNKNOWN_COLUMN;
                 } else {
                     a.flag[i] = 1;
                     a.known[i] = CORRO_KNOWN_CURRENT;  // final value decided after the merge
                     in = 1;
                     nsp++;
-                    nch += a.cnt[i];
+                    nch += a.cnt2[q];
                 }
             }
         }  // (else: a range from version 0, an inverted or clamped range -- the host walks it)
@@ -990,44 +1107,41 @@ __global__ void __launch_bounds__(AG_T) k_iso_decide(IsoArgs a) {
         l_ch[threadIdx.x >> 6] = nch;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // one partial per workgroup (k_hdr_reduce)
         unsigned long long x = 0, y = 0;
         for (int k = 0; k < AG_T / 64; k++) {
             x += l_sp[k];
             y += l_ch[k];
         }
-        if (x) atomicAdd(&a.ctl[2], x);
-        if (y) atomicAdd(&a.ctl[3], y);
+        a.part[8192 + blockIdx.x] = x;
+        a.part[16384 + blockIdx.x] = y;
     }
 }
 
 // version runs of the decided (merged or cleared) changesets, in order2: a slot starts a run unless
 // the previous slot is in a run of the same actor ending right before it
-__global__ void __launch_bounds__(AG_T) k_hdr_runflag(const uint32_t *__restrict__ order2, uint64_t n,
-                                                       const uint32_t *__restrict__ segk, const uint64_t *__restrict__ ver,
-                                                       const uint64_t *__restrict__ vend, const uint8_t *__restrict__ inrun,
-                                                       uint32_t *__restrict__ rflag) {
+__global__ void __launch_bounds__(AG_T) k_hdr_runflag(uint64_t n, const uint32_t *__restrict__ segk,
+                                                       const uint64_t *__restrict__ ver2, const uint64_t *__restrict__ vend2,
+                                                       const uint8_t *__restrict__ inrun, uint32_t *__restrict__ rflag) {
     for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < n; q += (uint64_t)gridDim.x * AG_T) {
-        const bool cont = q > 0 && inrun[q - 1] && segk[q - 1] == segk[q] && vend[order2[q - 1]] + 1 == ver[order2[q]];
+        const bool cont = q > 0 && inrun[q - 1] && segk[q - 1] == segk[q] && vend2[q - 1] + 1 == ver2[q];
         rflag[q] = inrun[q] && !cont ? 1u : 0u;
     }
 }
 
-__global__ void __launch_bounds__(AG_T) k_hdr_runs(const uint32_t *__restrict__ order2, uint64_t n,
-                                                    const uint32_t *__restrict__ segk, const uint64_t *__restrict__ ver,
-                                                    const uint64_t *__restrict__ vend, const uint8_t *__restrict__ inrun,
-                                                    const uint32_t *__restrict__ rflag, const uint32_t *__restrict__ rincl,
-                                                    uint32_t *__restrict__ run_site, uint64_t *__restrict__ run_start,
-                                                    uint64_t *__restrict__ run_end) {
+__global__ void __launch_bounds__(AG_T) k_hdr_runs(uint64_t n, const uint32_t *__restrict__ segk,
+                                                    const uint64_t *__restrict__ ver2, const uint64_t *__restrict__ vend2,
+                                                    const uint8_t *__restrict__ inrun, const uint32_t *__restrict__ rflag,
+                                                    const uint32_t *__restrict__ rincl, RunRec *__restrict__ runs) {
     for (uint64_t q = (uint64_t)blockIdx.x * AG_T + threadIdx.x; q < n; q += (uint64_t)gridDim.x * AG_T) {
         if (!inrun[q]) continue;
-        const uint32_t i = order2[q], r = rincl[q] - 1;
+        const uint32_t r = rincl[q] - 1;
         if (rflag[q]) {
-            run_site[r] = segk[q];
-            run_start[r] = ver[i];
+            runs[r].site = segk[q];
+            runs[r].start = ver2[q];
         }
         const bool ends = q + 1 >= n || !inrun[q + 1] || rflag[q + 1];
-        if (ends) run_end[r] = vend[i];
+        if (ends) runs[r].end = vend2[q];
     }
 }
 
@@ -1042,6 +1156,15 @@ __global__ void __launch_bounds__(AG_T) k_hdr_hlist(uint64_t n, const uint32_t *
                                                      const uint32_t *__restrict__ hincl, uint32_t *__restrict__ hslot) {
     for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < n; j += (uint64_t)gridDim.x * AG_T)
         if (hm[j]) hslot[hincl[j] - 1] = (uint32_t)j;
+}
+
+// run and host-changeset counts into ctl[6], ctl[7] (read back with the summary)
+__global__ void k_hdr_counts(uint64_t n, const uint32_t *__restrict__ rincl, const uint32_t *__restrict__ hincl,
+                             unsigned long long *__restrict__ ctl) {
+    if (threadIdx.x == 0) {
+        ctl[6] = rincl ? rincl[n - 1] : 0u;
+        ctl[7] = hincl[n - 1];
+    }
 }
 
 // the host's changesets: header, arrival index, unknown-name flag, and whether a partial one is
@@ -1068,7 +1191,8 @@ __global__ void __launch_bounds__(AG_T) k_hdr_gather(HGatherArgs a) {
         bool canon = c.kind == CORRO_CS_FULL && c.change_count && !(c.seq_start == 0 && c.seq_end == c.last_seq) &&
                      !a.bad[i] && c.seq_start <= c.seq_end && c.seq_end < 0xFFFFFFFFULL &&
                      c.change_count == c.seq_end - c.seq_start + 1 && c.version_start <= (uint64_t)INT64_MAX &&
-                     a.in.seq && a.in.site && a.in.db_version;
+                     c.change_off <= a.in.n && c.change_count <= a.in.n - c.change_off && a.in.seq && a.in.site &&
+                     a.in.db_version;
         for (uint64_t q = 0; canon && q < c.change_count; q++) {
             const uint64_t r = c.change_off + q;
             const uint8_t vt = a.in.val_type ? a.in.val_type[r] : (uint8_t)CORRO_INTEGER;
@@ -1117,23 +1241,27 @@ __global__ void __launch_bounds__(AG_T) k_hdr_spans(const uint32_t *__restrict__
 // commit: known of flagged changesets, crsql_set_db_version of the decided empty versions / ranges
 __global__ void __launch_bounds__(AG_T) k_hdr_commit(uint64_t ncs, const uint8_t *__restrict__ flag,
                                                       const uint8_t *__restrict__ any, const uint8_t *__restrict__ emp,
-                                                      const uint32_t *__restrict__ site, const uint64_t *__restrict__ vend,
-                                                      int32_t *__restrict__ known, unsigned long long *__restrict__ dbv) {
+                                                      const HdrPack *__restrict__ pack, int32_t *__restrict__ known,
+                                                      unsigned long long *__restrict__ dbv) {
     for (uint64_t i = (uint64_t)blockIdx.x * AG_T + threadIdx.x; i < ncs; i += (uint64_t)gridDim.x * AG_T) {
         if (flag[i]) known[i] = any[i] ? CORRO_KNOWN_CURRENT : CORRO_KNOWN_CLEARED;
-        if (emp[i]) atomicMax(&dbv[site[i]], (unsigned long long)(vend[i] + 1));
+        if (emp[i]) {
+            const HdrPack pk = pack[i];
+            atomicMax(&dbv[pk.site], (unsigned long long)(pk.ve + 1));
+        }
     }
 }
 
 // flagged changeset i whose site << 40 | version is among the sorted keys -> hit list
 __global__ void __launch_bounds__(AG_T) k_hdr_clearprobe(uint64_t ncs, const uint8_t *__restrict__ flag,
-                                                          const uint32_t *__restrict__ site,
-                                                          const uint64_t *__restrict__ ver, const uint64_t *__restrict__ keys,
+                                                          const HdrPack *__restrict__ pack, const uint64_t *__restrict__ keys,
                                                           uint64_t nk, uint64_t *__restrict__ hit,
                                                           unsigned long long *__restrict__ nhit) {
     for (uint64_t i = (uint64_t)blockIdx.x * AG_T + threadIdx.x; i < ncs; i += (uint64_t)gridDim.x * AG_T) {
-        if (!flag[i] || ver[i] >= (1ULL << 40)) continue;
-        const uint64_t k = (uint64_t)site[i] << 40 | ver[i];
+        if (!flag[i]) continue;
+        const HdrPack pk = pack[i];
+        if (pk.vs >= (1ULL << 40)) continue;
+        const uint64_t k = (uint64_t)pk.site << 40 | pk.vs;
         uint64_t lo = 0, hi = nk;  // first key >= k
         while (lo < hi) {
             const uint64_t m = (lo + hi) >> 1;
@@ -1150,6 +1278,11 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
                       const std::vector<int64_t> &site_max, int32_t *dknown, DevHdrResult &res) {
     hipStream_t s = ctx->stream;
     const uint32_t nsites = (uint32_t)ctx->sites.size();
+    // CORRO_AGENT_PROFILE: host-visible phase times of this pass on stderr
+    static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    double t_launch = 0, t_ctl0 = 0, t_sum = 0;
     res = DevHdrResult{};
     res.sites.assign(nsites, DevHdrSite{0xFFFFFFFFu, 0xFFFFFFFFu});
     ctx->agent_sorted_mode = true;
@@ -1172,31 +1305,35 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     a.off = c.off;
     a.cnt = c.cnt;
     a.ts = c.ts;
-    a.ver = h.ver;
     a.key = c.key;
     a.site = c.site;
     a.val = c.val;
     a.flag = c.flag;
     a.bad = c.bad;
     a.emp = h.emp;
+    a.dec = h.dec;
     a.known = dknown;
     a.ctl = h.ctl;
-    a.vend = h.vend;
-    a.key2 = h.key2;
-    a.val2 = h.val2;
-    a.kd = h.kd;
-    a.dec = h.dec;
+    a.part = h.part;
+    a.pack = h.pack;
+    t_launch = ms();
     hipLaunchKernelGGL(k_hdr, flat_grid(ncs), dim3(AG_T), 0, s, a);
     CORRO_HIP_TRY(hipGetLastError());
-    unsigned long long ctl0 = 0;
-    CORRO_HIP_TRY(hipMemcpyAsync(&ctl0, h.ctl, 8, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_hdr_reduce, dim3(1), dim3(1024), 0, s, h.part, flat_grid(ncs).x, 0, h.ctl);
+    CORRO_HIP_TRY(hipGetLastError());
+    unsigned long long ctl0[5] = {0, 0, 0, 0, 0};
+    CORRO_HIP_TRY(hipMemcpyAsync(ctl0, h.ctl, sizeof(ctl0), hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
-    if (ctl0) {  // nothing decided: every changeset stays Skipped
-        res.err = (uint32_t)ctl0;
+    t_ctl0 = ms();
+    if (ctl0[0]) {  // nothing decided: every changeset stays Skipped
+        res.err = (uint32_t)ctl0[0];
         return CORRO_OK;
     }
     uint32_t bits = 1;
     while ((1ULL << bits) <= nsites) bits++;
+    // the second sort's version field: wide enough that only versions >= 2^40 - 1 reach its clamp
+    uint32_t vbits = 1;
+    while (vbits < 40 && (1ULL << vbits) - 1 <= ctl0[4]) vbits++;
     const uint32_t n32 = (uint32_t)ncs;
     // the application order (site rank, arrival) and each actor's slots in it
     size_t tb = c.temp_bytes;
@@ -1206,13 +1343,16 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     CORRO_HIP_TRY(hipGetLastError());
     // per-changeset decisions over (site rank, version start, arrival): dedup groups, the running max
     // of version ends per actor (overlaps), then the decided changesets' version runs
-    const bool decide = bits <= 24;  // (rank << 40 | version in one 64-bit key; else the host walks all)
+    const bool decide = bits + vbits <= 64;  // (else the host walks every changeset)
     if (decide) {
+        hipLaunchKernelGGL(k_hdr_key2, flat_grid(ncs), dim3(AG_T), 0, s, ncs, h.pack, a.site_rank, nsites, vbits, h.key2,
+                           h.val2);
+        CORRO_HIP_TRY(hipGetLastError());
         tb = c.temp_bytes;
-        if (int rc = ovf_sort_pairs(c.temp, &tb, h.key2, h.key2b, h.val2, h.val2b, n32, bits + 40, s)) return rc;
+        if (int rc = ovf_sort_pairs(c.temp, &tb, h.key2, h.key2b, h.val2, h.val2b, n32, bits + vbits, s)) return rc;
         const uint32_t *order2 = h.val2b;
-        hipLaunchKernelGGL(k_iso_prep, flat_grid(ncs), dim3(AG_T), 0, s, dcs, order2, ncs, c.site, h.ver, h.vend, h.kd,
-                           h.segk, h.vend2, h.ghead);
+        hipLaunchKernelGGL(k_iso_prep, flat_grid(ncs), dim3(AG_T), 0, s, dcs, order2, ncs, h.pack, h.segk, h.ver2, h.vend2,
+                           h.kd2, h.cnt2, h.ghead);
         CORRO_HIP_TRY(hipGetLastError());
         tb = c.temp_bytes;
         if (int rc = prim_inclusive_scan_u32(c.temp, &tb, h.ghead, h.gincl, n32, s)) return rc;
@@ -1226,29 +1366,30 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         d.gincl = h.gincl;
         d.gfirst = h.gfirst;
         d.glast = h.glast;
-        d.ver = h.ver;
-        d.vend = h.vend;
+        d.cnt2 = h.cnt2;
+        d.ver2 = h.ver2;
+        d.vend2 = h.vend2;
         d.rmax = h.rmax;
-        d.cnt = c.cnt;
-        d.kd = h.kd;
-        d.bad = c.bad;
+        d.kd2 = h.kd2;
         d.site_max = h.site_max;
         d.dec = h.dec;
         d.flag = c.flag;
         d.emp = h.emp;
         d.inrun = h.inrun;
         d.known = dknown;
-        d.ctl = h.ctl;
+        d.part = h.part;
         d.n = ncs;
+        d.vclamp = vbits >= 40 ? VCLAMP40 : (1ULL << vbits) - 1;
         hipLaunchKernelGGL(k_iso_decide, flat_grid(ncs), dim3(AG_T), 0, s, d);
         CORRO_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_hdr_runflag, flat_grid(ncs), dim3(AG_T), 0, s, order2, ncs, h.segk, h.ver, h.vend, h.inrun,
-                           h.rflag);
+        hipLaunchKernelGGL(k_hdr_reduce, dim3(1), dim3(1024), 0, s, h.part, flat_grid(ncs).x, 1, h.ctl);
+        CORRO_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_hdr_runflag, flat_grid(ncs), dim3(AG_T), 0, s, ncs, h.segk, h.ver2, h.vend2, h.inrun, h.rflag);
         CORRO_HIP_TRY(hipGetLastError());
         tb = c.temp_bytes;
         if (int rc = prim_inclusive_scan_u32(c.temp, &tb, h.rflag, h.rincl, n32, s)) return rc;
-        hipLaunchKernelGGL(k_hdr_runs, flat_grid(ncs), dim3(AG_T), 0, s, order2, ncs, h.segk, h.ver, h.vend, h.inrun,
-                           h.rflag, h.rincl, h.run_site, h.run_start, h.run_end);
+        hipLaunchKernelGGL(k_hdr_runs, flat_grid(ncs), dim3(AG_T), 0, s, ncs, h.segk, h.ver2, h.vend2, h.inrun, h.rflag,
+                           h.rincl, h.runs);
         CORRO_HIP_TRY(hipGetLastError());
     }
     // the host's changesets: their sorted slots (grouped by actor, arrival order inside)
@@ -1259,30 +1400,26 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     uint32_t *hslot = h.gfirst;  // (free once the decisions are made)
     hipLaunchKernelGGL(k_hdr_hlist, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.cnt32, c.incl, hslot);
     CORRO_HIP_TRY(hipGetLastError());
-    // summaries: counters, run count, host changeset count, per-site groups
-    unsigned long long ctl[4] = {0, 0, 0, 0};
-    uint32_t nruns = 0, nh = 0;
-    std::vector<uint32_t> gs(nsites), ge(nsites);
-    CORRO_HIP_TRY(hipMemcpyAsync(ctl, h.ctl, 32, hipMemcpyDeviceToHost, s));
-    if (decide) CORRO_HIP_TRY(hipMemcpyAsync(&nruns, h.rincl + (ncs - 1), 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(&nh, c.incl + (ncs - 1), 4, hipMemcpyDeviceToHost, s));
-    if (nsites) {
-        CORRO_HIP_TRY(hipMemcpyAsync(gs.data(), h.gstart, 4ULL * nsites, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(ge.data(), h.gend, 4ULL * nsites, hipMemcpyDeviceToHost, s));
-    }
+    hipLaunchKernelGGL(k_hdr_counts, dim3(1), dim3(64), 0, s, ncs, decide ? h.rincl : nullptr, c.incl, h.ctl);
+    CORRO_HIP_TRY(hipGetLastError());
+    // one readback: counters, run count, host changeset count, per-site groups
+    std::vector<uint8_t> sum(h.summary_bytes);
+    CORRO_HIP_TRY(hipMemcpyAsync(sum.data(), h.ctl, h.summary_bytes, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    t_sum = ms();
+    const unsigned long long *ctl = reinterpret_cast<const unsigned long long *>(sum.data());
+    const uint32_t *gs = reinterpret_cast<const uint32_t *>(sum.data() + al256(64));
+    const uint32_t *ge = reinterpret_cast<const uint32_t *>(sum.data() + al256(64) + al256(std::max<uint32_t>(nsites, 1) * 4ULL));
     res.ts_any = ctl[1] != 0;
     res.nspans = ctl[2];
     res.nchanges = ctl[3];
+    const uint64_t nruns = ctl[6], nh = ctl[7];
     for (uint32_t t = 0; t < nsites; t++) res.sites[t] = DevHdrSite{gs[t], ge[t]};
     res.run_site.resize(nruns);
     res.run_start.resize(nruns);
     res.run_end.resize(nruns);
-    if (nruns) {
-        CORRO_HIP_TRY(hipMemcpyAsync(res.run_site.data(), h.run_site, 4ULL * nruns, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(res.run_start.data(), h.run_start, 8ULL * nruns, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(res.run_end.data(), h.run_end, 8ULL * nruns, hipMemcpyDeviceToHost, s));
-    }
+    std::vector<RunRec> runs(nruns);
+    if (nruns) CORRO_HIP_TRY(hipMemcpyAsync(runs.data(), h.runs, nruns * sizeof(RunRec), hipMemcpyDeviceToHost, s));
     res.nh = nh;
     if (nh) {  // their headers, arrival index, unknown-name and canonical flags: one pinned readback
         const size_t o_idx = al256((uint64_t)nh * sizeof(corro_changeset)), o_bad = o_idx + al256(nh * 4ULL),
@@ -1317,6 +1454,14 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         res.hcanon = hp + o_can;
     }
     if (nruns || nh) CORRO_HIP_TRY(hipStreamSynchronize(s));
+    for (uint64_t r = 0; r < nruns; r++) {
+        res.run_site[r] = runs[r].site;
+        res.run_start[r] = runs[r].start;
+        res.run_end[r] = runs[r].end;
+    }
+    if (prof)
+        fprintf(stderr, "[corro agent dev headers] setup=%.3f k_hdr+sync=%.3f passes+sync=%.3f fetch=%.3f ms\n", t_launch,
+                t_ctl0 - t_launch, t_sum - t_ctl0, ms() - t_sum);
     return CORRO_OK;
 }
 
@@ -1361,7 +1506,7 @@ int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown, cons
     hipStream_t s = ctx->stream;
     const HdrCols h = hdr_cols(ctx, ncs, (uint32_t)ctx->sites.size());
     const DevCols c = dev_cols(ctx);
-    hipLaunchKernelGGL(k_hdr_commit, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.flag, c.any, h.emp, c.site, h.vend, dknown,
+    hipLaunchKernelGGL(k_hdr_commit, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.flag, c.any, h.emp, h.pack, dknown,
                        ctx->d_dbv.as<unsigned long long>());
     CORRO_HIP_TRY(hipGetLastError());
     if (keys && !keys->empty() && hits) {
@@ -1376,7 +1521,7 @@ int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown, cons
         unsigned long long *dc = reinterpret_cast<unsigned long long *>(base + o_cnt);
         CORRO_HIP_TRY(hipMemcpyAsync(dk, keys->data(), nk * 8, hipMemcpyHostToDevice, s));
         CORRO_HIP_TRY(hipMemsetAsync(dc, 0, 8, s));
-        hipLaunchKernelGGL(k_hdr_clearprobe, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.flag, c.site, h.ver, dk, nk, dh, dc);
+        hipLaunchKernelGGL(k_hdr_clearprobe, flat_grid(ncs), dim3(AG_T), 0, s, ncs, c.flag, h.pack, dk, nk, dh, dc);
         CORRO_HIP_TRY(hipGetLastError());
         unsigned long long nh = 0;
         CORRO_HIP_TRY(hipMemcpyAsync(&nh, dc, 8, hipMemcpyDeviceToHost, s));
