@@ -234,37 +234,55 @@ __global__ void __launch_bounds__(AG_T) k_impactful(ImpArgs a) {
     const unsigned long long first = *a.first;
     const bool lds_t = a.ntables <= IMP_TLDS;
     const uint32_t lane = threadIdx.x & 63;
-#pragma unroll 2
+    // the lane's SP_PER positions: spans from LDS first, then every flag load in flight at once,
+    // then the table loads of the hits, then the stores (memory-level parallelism per lane)
+    uint32_t kk[SP_PER];
+    uint64_t src[SP_PER];
+    uint8_t st[SP_PER];  // bit 0 active, bit 1 head of its span, bit 2 hit
+#pragma unroll
     for (uint32_t u = 0; u < SP_PER; u++) {
         const uint32_t r = u * AG_T + threadIdx.x;
         const uint64_t p = t.p0 + r;
-        const bool act = p < t.p1;
-        bool hit = false;
-        uint32_t tb = 0xFFFFFFFFu;
-        if (act) {
+        st[u] = 0;
+        kk[u] = 0;
+        src[u] = 0;
+        if (p < t.p1) {
             const uint32_t k = span_of(l_dst, t.ns, r);
-            const uint64_t src = l_src[k] + (r - l_dst[k]);
-            const bool head = r == l_dst[k] && (k > 0 || t.head0);
-            hit = head ? first <= p : a.imp[p] != 0;
-            if (a.out) a.out[src] = hit ? 1 : 0;
-            if (hit) {
-                l_any[k] = 1;
-                tb = a.tcid[a.tcid_by_src ? src : p] >> 16;
-            }
+            kk[u] = k;
+            src[u] = l_src[k] + (r - l_dst[k]);
+            st[u] = 1 | ((r == l_dst[k] && (k > 0 || t.head0)) ? 2 : 0);
         }
-        if (tb >= a.ntables) continue;
-        if (lds_t) {
-            atomicAdd(&l_cnt[tb], 1u);
-        } else {  // wave-aggregated global atomics per table
-            unsigned long long m = __ballot(tb < a.ntables);
-            while (m) {
-                const uint32_t leader = (uint32_t)__ffsll(m) - 1;
-                const uint32_t tl = __shfl(tb, leader);
-                const unsigned long long mt = __ballot(tb == tl);
-                if (lane == leader) atomicAdd(&a.committed[tl], (unsigned long long)__popcll(mt));
-                m &= ~mt;
-                if (tb == tl) tb = 0xFFFFFFFFu;
+    }
+    uint8_t im[SP_PER];
+#pragma unroll
+    for (uint32_t u = 0; u < SP_PER; u++) im[u] = (st[u] & 1) && !(st[u] & 2) ? a.imp[t.p0 + u * AG_T + threadIdx.x] : 0;
+    uint32_t tb[SP_PER];
+#pragma unroll
+    for (uint32_t u = 0; u < SP_PER; u++) {
+        const uint64_t p = t.p0 + u * AG_T + threadIdx.x;
+        const bool hit = (st[u] & 1) && ((st[u] & 2) ? first <= p : im[u] != 0);
+        if (hit) st[u] |= 4;
+        tb[u] = hit ? a.tcid[a.tcid_by_src ? src[u] : p] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < SP_PER; u++) {
+        const bool hit = st[u] & 4;
+        if (a.out && (st[u] & 1)) a.out[src[u]] = hit ? 1 : 0;
+        if (hit) l_any[kk[u]] = 1;
+        uint32_t t_ = hit ? tb[u] >> 16 : 0xFFFFFFFFu;
+        if (t_ >= a.ntables) t_ = 0xFFFFFFFFu;
+        // one atomic per (wave, table): LDS counters when the tables fit, else global
+        unsigned long long m = __ballot(t_ != 0xFFFFFFFFu);
+        while (m) {
+            const uint32_t leader = (uint32_t)__ffsll(m) - 1;
+            const uint32_t tl = __shfl(t_, leader);
+            const unsigned long long mt = __ballot(t_ == tl);
+            if (lane == leader) {
+                if (lds_t) atomicAdd(&l_cnt[tl], (uint32_t)__popcll(mt));
+                else atomicAdd(&a.committed[tl], (unsigned long long)__popcll(mt));
             }
+            m &= ~mt;
+            if (t_ == tl) t_ = 0xFFFFFFFFu;
         }
     }
     __syncthreads();
@@ -453,16 +471,28 @@ __global__ void __launch_bounds__(AG_T) k_span_pos(const uint32_t *__restrict__ 
     __shared__ uint64_t l_ts[SPB + 1];
     const SpanTile t = stage_spans(first_span, nspans, nbatch, s_dst, s_src, ts_out && !in_ts ? s_ts : nullptr, nullptr,
                                    l_dst, l_src, ts_out && !in_ts ? l_ts : nullptr, nullptr);
-#pragma unroll 2
+    // spans from LDS for all of the lane's positions, then every ts load in flight, then the stores
+    uint64_t src[SP_PER], tv[SP_PER];
+    uint32_t kk[SP_PER];
+#pragma unroll
     for (uint32_t u = 0; u < SP_PER; u++) {
         const uint32_t r = u * AG_T + threadIdx.x;
-        const uint64_t p = t.p0 + r;
+        const uint32_t k = t.p0 + r < t.p1 ? span_of(l_dst, t.ns, r) : 0u;
+        kk[u] = k;
+        src[u] = l_src[k] + (r - l_dst[k]);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < SP_PER; u++) {
+        const bool act = t.p0 + u * AG_T + threadIdx.x < t.p1;
+        tv[u] = ts_out && act ? (in_ts ? in_ts[src[u]] : l_ts[kk[u]]) : 0ULL;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < SP_PER; u++) {
+        const uint64_t p = t.p0 + u * AG_T + threadIdx.x;
         if (p >= t.p1) continue;
-        const uint32_t k = span_of(l_dst, t.ns, r);
-        const uint64_t src = l_src[k] + (r - l_dst[k]);
-        ap[src] = (uint32_t)p;
-        src_of[p] = (uint32_t)src;
-        if (ts_out) ts_out[p] = in_ts ? in_ts[src] : l_ts[k];
+        ap[src[u]] = (uint32_t)p;
+        src_of[p] = (uint32_t)src[u];
+        if (ts_out) ts_out[p] = tv[u];
     }
 }
 

@@ -551,3 +551,72 @@ def test_device_buffered_rows_match_host_path(seed):
         assert ba.needed(bytes(a)) == bb.needed(bytes(a))
         for v in range(1, nver + 1):
             assert ba.partial(bytes(a), v) == bb.partial(bytes(a), v)
+
+
+def _mixed_scale_calls(seed, nact=64, nver=120, per=8, ncalls=3):
+    """agent_e2e_mixed's shape at a test size: versions arriving round-robin across actors, ~10 %
+    re-sent later in the call, ~5 % as two partial halves (the second half later), ~5 % Empty, over
+    calls whose versions continue (each call's versions above the previous call's)."""
+    from oracle.agent import Changeset
+    rng = np.random.default_rng(seed)
+    import synth
+    ids = synth.site_ids(nact, seed)
+    calls, v0 = [], 0
+    for _c in range(ncalls):
+        head, tail = [], []
+        for v in range(v0 + 1, v0 + nver + 1):
+            for a in range(nact):
+                rr = [dict(pk=int(rng.integers(1, 4000)), table_cid=(0 << 16) | int(rng.integers(1, 5)),
+                           col_version=int(rng.integers(1, 6)), db_version=v, cl=1, seq=q, site=a,
+                           val0=int(rng.integers(0, 1 << 40)), val_type=1) for q in range(per)]
+                ts = int(rng.integers(1, 1 << 40))
+                u = rng.random()
+                if u < 0.05:
+                    cs = Changeset(ids[a], "empty", versions=(v, v))
+                elif u < 0.10:
+                    h = per // 2
+                    cs = Changeset(ids[a], "full", version=v, seqs=(0, h - 1), last_seq=per - 1, ts=ts, rows=rr[:h])
+                    tail.append(Changeset(ids[a], "full", version=v, seqs=(h, per - 1), last_seq=per - 1, ts=ts,
+                                          rows=rr[h:]))
+                else:
+                    cs = Changeset(ids[a], "full", version=v, seqs=(0, per - 1), last_seq=per - 1, ts=ts, rows=rr)
+                    if rng.random() < 0.10:
+                        tail.append(cs)
+                head.append(cs)
+        order = rng.permutation(len(tail))
+        call = list(head)
+        for j in order:   # re-sends and second halves into the back half of the call
+            call.insert(int(rng.integers(len(call) // 2, len(call) + 1)), tail[j])
+        calls.append(call)
+        v0 += nver
+    return ids, calls
+
+
+def test_mixed_call_at_scale_matches_host_path():
+    """The mixed drop-in call at ~8.7 K changesets x 3 calls: device-resident headers (per-changeset
+    device decisions, host walk of the rest, partial rows in the device pool) against the
+    host-memory path -- outcomes, impactful flags, merged state, db_versions, committed counts, gap
+    bookkeeping and partials"""
+    import corrosion_amd as ca
+    ids, calls = _mixed_scale_calls(51)
+    sides = []
+    for _k in range(2):
+        eng = ca.MergeEngine(SCHEMA, capacity_hint=1 << 18)
+        ords = eng.register_sites(ids)
+        sides.append((eng, ca.agent.Bookie(), {bytes(ids[q]): int(ords[q]) for q in range(len(ids))}))
+    assert sides[0][2] == sides[1][2]
+    for c in (c for call in calls for c in call):
+        for r in c.rows:
+            r["site"] = sides[0][2][bytes(c.actor)]
+    for call in calls:
+        got = [_run(eng, bk, o, call, dev) for (eng, bk, o), dev in zip(sides, ("headers", False))]
+        assert got[0][0] == got[1][0]
+        assert got[0][1] == got[1][1]
+        assert "partial" in got[0][0] and "skipped" in got[0][0] and "cleared" in got[0][0]
+    (ea, ba, _), (eb, bb, _) = sides
+    assert canon_rows(ea.export()) == canon_rows(eb.export())
+    assert list(ea.db_versions()) == list(eb.db_versions())
+    assert ea.committed("t") == eb.committed("t")
+    for a in ids:
+        assert ba.last(bytes(a)) == bb.last(bytes(a))
+        assert ba.needed(bytes(a)) == bb.needed(bytes(a))
