@@ -190,15 +190,15 @@ __device__ inline SpanTile stage_spans(const uint32_t *__restrict__ first, uint6
     return t;
 }
 
-// local span of relative position r: the last k with l_dst[k] <= r
-__device__ inline uint32_t span_of(const uint32_t *l_dst, uint32_t ns, uint32_t r) {
-    uint32_t lo = 0, hi = ns;  // l_dst[lo] <= r < l_dst[hi]
-    while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (l_dst[m] <= r) lo = m;
-        else hi = m;
+// position -> local span map of the tile: each wave writes the positions of every 4th span (no
+// per-position binary search: one LDS read per position afterwards)
+__device__ inline void fill_pspan(const uint32_t *l_dst, const SpanTile &t, uint16_t *pspan) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63, len = (uint32_t)(t.p1 - t.p0);
+    for (uint32_t k = w; k < t.ns; k += AG_T / 64) {
+        const uint32_t a = l_dst[k], b = k + 1 < t.ns ? l_dst[k + 1] : len;
+        for (uint32_t r = a + lane; r < b && r < len; r += 64) pspan[r] = (uint16_t)k;
     }
-    return lo;
+    __syncthreads();
 }
 
 struct ImpArgs {
@@ -226,8 +226,10 @@ __global__ void __launch_bounds__(AG_T) k_impactful(ImpArgs a) {
     __shared__ uint32_t l_cs[SPB + 1];
     __shared__ uint8_t l_any[SPB + 1];
     __shared__ uint32_t l_cnt[IMP_TLDS];
+    __shared__ uint16_t pspan[SPB];
     const SpanTile t = stage_spans(a.first_span, a.nspans, a.nbatch, a.s_dst, a.s_src, nullptr, a.s_cs, l_dst, l_src,
                                    nullptr, l_cs);
+    fill_pspan(l_dst, t, pspan);
     for (uint32_t k = threadIdx.x; k < t.ns; k += AG_T) l_any[k] = 0;
     if (threadIdx.x < IMP_TLDS) l_cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -247,7 +249,7 @@ __global__ void __launch_bounds__(AG_T) k_impactful(ImpArgs a) {
         kk[u] = 0;
         src[u] = 0;
         if (p < t.p1) {
-            const uint32_t k = span_of(l_dst, t.ns, r);
+            const uint32_t k = pspan[r];
             kk[u] = k;
             src[u] = l_src[k] + (r - l_dst[k]);
             st[u] = 1 | ((r == l_dst[k] && (k > 0 || t.head0)) ? 2 : 0);
@@ -469,15 +471,17 @@ __global__ void __launch_bounds__(AG_T) k_span_pos(const uint32_t *__restrict__ 
     __shared__ uint32_t l_dst[SPB + 1];
     __shared__ uint64_t l_src[SPB + 1];
     __shared__ uint64_t l_ts[SPB + 1];
+    __shared__ uint16_t pspan[SPB];
     const SpanTile t = stage_spans(first_span, nspans, nbatch, s_dst, s_src, ts_out && !in_ts ? s_ts : nullptr, nullptr,
                                    l_dst, l_src, ts_out && !in_ts ? l_ts : nullptr, nullptr);
+    fill_pspan(l_dst, t, pspan);
     // spans from LDS for all of the lane's positions, then every ts load in flight, then the stores
     uint64_t src[SP_PER], tv[SP_PER];
     uint32_t kk[SP_PER];
 #pragma unroll
     for (uint32_t u = 0; u < SP_PER; u++) {
         const uint32_t r = u * AG_T + threadIdx.x;
-        const uint32_t k = t.p0 + r < t.p1 ? span_of(l_dst, t.ns, r) : 0u;
+        const uint32_t k = t.p0 + r < t.p1 ? pspan[r] : 0u;
         kk[u] = k;
         src[u] = l_src[k] + (r - l_dst[k]);
     }
@@ -800,7 +804,8 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
             hipLaunchKernelGGL(k_imp_reduce, dim3(ntables), dim3(AG_T), 0, s, a.part, nwg, ntables, a.committed);
             CORRO_HIP_TRY(hipGetLastError());
         }
-        CORRO_HIP_TRY(hipMemcpyAsync(p.any, c.any, ncs, hipMemcpyDeviceToHost, s));
+        // (device-resident headers: the outcome pass reads c.any on the device)
+        if (!ctx->agent_sorted_mode) CORRO_HIP_TRY(hipMemcpyAsync(p.any, c.any, ncs, hipMemcpyDeviceToHost, s));
     }
     CORRO_HIP_TRY(hipMemcpyAsync(p.committed, base + o_cm, 8ULL * ntables, hipMemcpyDeviceToHost, s));
     if (out && mem == CORRO_MEM_HOST && nin) CORRO_HIP_TRY(hipMemcpyAsync(impactful, out, nin, hipMemcpyDeviceToHost, s));
