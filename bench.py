@@ -317,6 +317,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
     steady = steady_state(eng, prep, n, dev, dt / args.steps * 1e3, cells)
     agent = agent_path(eng, batch, n)
     e2e_agent = agent_e2e(eng, batch, n, agent["ms"])
+    mixed_agent = agent_e2e_mixed(eng, batch, n, e2e_agent["ms"], reps=3)
     e2e = host_batch_e2e(eng, batch, n)
     cpu = None if args.no_cpu_baseline else cpu_baseline(batch)
     line = {
@@ -347,6 +348,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
         "steady_state": steady,
         "agent_path": agent,
         "agent_e2e": e2e_agent,
+        "agent_e2e_mixed": mixed_agent,
         "end_to_end_h2d": e2e,
     }
     print(json.dumps(line), flush=True)
