@@ -825,14 +825,37 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
         // pass 1: batch-local dedup of (versions, seqs), then versions the actor already holds
         std::vector<uint64_t> unknown;
         unknown.reserve(w.nidx);
-        std::set<std::tuple<uint64_t, uint64_t, int, uint64_t, uint64_t>> seen;
+        // the seen set of (versions, seqs) keys: the first changeset of each key in arrival order
+        // (one sort of the actor's keys instead of a tree node per changeset)
+        struct SeenKey {
+            uint64_t vs, ve, ss, se;
+            uint32_t has_seqs, k;
+        };
+        std::vector<SeenKey> keys(w.nidx);
         for (uint64_t k = 0; k < w.nidx; k++) {
+            const corro_changeset &c = v.cs[w.idx[k]];
+            const Range vr = versions_of(c);
+            Range sq;
+            const Range *seqs = seqs_of(c, sq);
+            keys[k] = SeenKey{vr.first, vr.second, seqs ? sq.first : 0, seqs ? sq.second : 0, seqs ? 1u : 0u, (uint32_t)k};
+        }
+        auto kless = [](const SeenKey &x, const SeenKey &y) {
+            return std::tie(x.vs, x.ve, x.has_seqs, x.ss, x.se, x.k) < std::tie(y.vs, y.ve, y.has_seqs, y.ss, y.se, y.k);
+        };
+        std::sort(keys.begin(), keys.end(), kless);
+        std::vector<uint8_t> first_of_key(w.nidx, 0);
+        for (uint64_t q = 0; q < keys.size(); q++) {
+            const SeenKey &x = keys[q];
+            if (q == 0 || std::tie(x.vs, x.ve, x.has_seqs, x.ss, x.se) !=
+                              std::tie(keys[q - 1].vs, keys[q - 1].ve, keys[q - 1].has_seqs, keys[q - 1].ss, keys[q - 1].se))
+                first_of_key[x.k] = 1;
+        }
+        for (uint64_t k = 0; k < w.nidx; k++) {
+            if (!first_of_key[k]) continue;
             const uint64_t i = w.idx[k];
             const Range vr = versions_of(v.cs[i]);
             Range sq;
             const Range *seqs = seqs_of(v.cs[i], sq);
-            if (!seen.emplace(vr.first, vr.second, seqs ? 1 : 0, seqs ? sq.first : 0, seqs ? sq.second : 0).second)
-                continue;
             if (booked.contains_all(vr.first, vr.second, seqs)) continue;
             unknown.push_back(i);
         }
@@ -869,7 +892,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
                         v.known[i] = CORRO_E_INVALID;
                         continue;
                     }
-                    partial = p;
+                    partial = std::move(p);
                     v.known[i] = CORRO_KNOWN_PARTIAL;
                 }
             }
