@@ -784,6 +784,8 @@ struct ActorWork {
     bool has_next = false;
     corro::Booked next;               // the committed VersionsSnapshot
     std::vector<uint64_t> ready;      // versions now fully buffered
+    bool defer_gaps = false;          // the call's gap bookkeeping runs batched on the device (gaps_batch)
+    RangeSet versions;                // (deferred) the versions this call adds
     int rc = CORRO_OK;
     std::string err;
 };
@@ -902,6 +904,10 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
         }
     }
     if (versions.empty()) return;
+    if (w.defer_gaps) {  // (many actors: one device pass for all of them, gaps_batch)
+        w.versions = std::move(versions);
+        return;
+    }
     // gap bookkeeping on a copy of the actor's Booked (VersionsSnapshot, agent.rs:1108-1235): an
     // INSERT that would violate __corro_bookkeeping_gaps' key fails the whole call before the
     // merge has touched the state, as the transaction's rollback would undo it (util.rs:894-936)
@@ -916,6 +922,95 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
         const corro::PartialVersion &p = w.next.insert_partial(version, pv);
         if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
     }
+}
+
+// Whether the call's gap bookkeeping goes through the batched device form (corro_booked_insert_db_batch)
+// instead of insert_db inside each actor's (parallel) walk: CORRO_AGENT_GAPS_BATCH=1, and only when
+// every booked max fits its signed input. Off by default: with the Bookie on the host, the CSR
+// round trip and the per-actor rebuild of the gap lists cost more than the host pass at every size
+// measured (tools/bench_agent_actors.py: 100 K actors x 2 gaps 90 vs 109 ms, 20 K x 31 gaps 28 vs
+// 67 ms, 4 K x 199 gaps 20 vs 48 ms for the whole call); it pays only for gap lists kept on the device.
+bool want_gaps_batch(const std::vector<ActorWork> &work) {
+    const char *e = std::getenv("CORRO_AGENT_GAPS_BATCH");  // (read per call: tests switch it)
+    if (!e || std::atoi(e) != 1 || work.empty()) return false;
+    for (const ActorWork &w : work)
+        if (w.booked->has_max && w.booked->max > (uint64_t)INT64_MAX) return false;
+    return true;
+}
+
+// The deferred actors' insert_db (agent.rs:1108-1235) in one device pass: new max and gap lists from
+// the device, the partials inside a deleted gap dropped, the UNIQUE (actor_id, start) check on the
+// host (an INSERT row starting where a gap the pass kept starts), then insert_partial as in the walk.
+int gaps_batch(corro_ctx *ctx, std::vector<ActorWork> &work) {
+    std::vector<size_t> A;
+    for (size_t k = 0; k < work.size(); k++)
+        if (work[k].defer_gaps && !work[k].versions.empty() && work[k].rc == CORRO_OK) A.push_back(k);
+    if (A.empty()) return CORRO_OK;
+    const size_t n = A.size();
+    corro::GapsHost in;
+    in.max.resize(n);
+    in.gap_off.assign(n + 1, 0);
+    in.ver_off.assign(n + 1, 0);
+    for (size_t q = 0; q < n; q++) {
+        const ActorWork &w = work[A[q]];
+        in.max[q] = w.booked->has_max ? (int64_t)w.booked->max : -1;
+        in.gap_off[q + 1] = in.gap_off[q] + w.booked->needed.ranges().size();
+        in.ver_off[q + 1] = in.ver_off[q] + w.versions.ranges().size();
+    }
+    in.gap_start.resize(in.gap_off[n]);
+    in.gap_end.resize(in.gap_off[n]);
+    in.ver_start.resize(in.ver_off[n]);
+    in.ver_end.resize(in.ver_off[n]);
+    for (size_t q = 0; q < n; q++) {
+        const ActorWork &w = work[A[q]];
+        uint64_t o = in.gap_off[q];
+        for (const Range &r : w.booked->needed.ranges()) {
+            in.gap_start[o] = r.first;
+            in.gap_end[o++] = r.second;
+        }
+        o = in.ver_off[q];
+        for (const Range &r : w.versions.ranges()) {
+            in.ver_start[o] = r.first;
+            in.ver_end[o++] = r.second;
+        }
+    }
+    corro::GapsHostOut out;
+    TRY_RC(corro::agent_dev_gaps(ctx, in, out));
+    run_parallel(n, [&](size_t q) {
+        ActorWork &w = work[A[q]];
+        if (out.status[q] != 0) {
+            w.rc = CORRO_E_INVALID;
+            w.err = "gap bookkeeping input not canonical";
+            return;
+        }
+        const corro::Booked &old = *w.booked;
+        const uint64_t rb = in.gap_off[q], ib = in.gap_off[q] + in.ver_off[q] + q;
+        std::vector<uint64_t> removed(out.rm_start.begin() + rb, out.rm_start.begin() + rb + out.rm_count[q]);
+        std::sort(removed.begin(), removed.end());
+        for (uint64_t k = 0; k < out.ins_count[q]; k++) {
+            const uint64_t st = out.ins_start[ib + k];
+            uint64_t a0 = 0, b0 = 0;
+            if (old.needed.get(st, a0, b0) && a0 == st && !std::binary_search(removed.begin(), removed.end(), st)) {
+                w.rc = CORRO_E_INVALID;
+                w.err = "UNIQUE constraint failed: __corro_bookkeeping_gaps.start";
+                return;
+            }
+        }
+        w.next.needed = RangeSet();
+        for (uint64_t k = 0; k < out.gap_count[q]; k++) w.next.needed.insert(out.new_start[ib + k], out.new_end[ib + k]);
+        w.next.has_max = out.max[q] >= 0;
+        w.next.max = out.max[q] >= 0 ? (uint64_t)out.max[q] : 0;
+        w.next.partials = old.partials;
+        for (uint64_t k = 0; k < out.rm_count[q]; k++)
+            w.next.partials.erase(w.next.partials.lower_bound(out.rm_start[rb + k]),
+                                  w.next.partials.upper_bound(out.rm_end[rb + k]));
+        w.has_next = true;
+        for (auto &[version, pv] : w.partials) {
+            const corro::PartialVersion &p = w.next.insert_partial(version, pv);
+            if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
+        }
+    }, 16);
+    return CORRO_OK;
 }
 
 }  // namespace
@@ -1033,7 +1128,10 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     for (size_t r = 0; r < R.run_site.size(); r++)
         dev_runs[(size_t)work_of[R.run_site[r]]].emplace_back(R.run_start[r], R.run_end[r]);
     const CsView view{hcs, R.hbad, hknown.data(), hflag.data(), canon};
+    if (want_gaps_batch(work))
+        for (ActorWork &w : work) w.defer_gaps = true;
     run_parallel(work.size(), [&](size_t k) { run_actor_walk(bk, work[k], view, dev_runs[k], row_of); });
+    TRY_RC(gaps_batch(ctx, work));
     for (ActorWork &w : work)
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);
     uint64_t nspans = R.nspans, nb = R.nchanges;
@@ -1441,7 +1539,10 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
         for (auto &[wi, r] : cout[k].runs) fast_runs[wi].push_back(r);
     const CsView view{cs, bad, out->known, P.flag, nullptr};
     auto run_actor = [&](size_t wi) { run_actor_walk(bk, work[wi], view, fast_runs[wi], row_of); };
+    if (want_gaps_batch(work))
+        for (ActorWork &w : work) w.defer_gaps = true;
     run_parallel(work.size(), [&](size_t k) { run_actor(k); });
+    TRY_RC(gaps_batch(ctx, work));
     for (ActorWork &w : work)
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);
     uint64_t nspans = 0, nb = 0;

@@ -167,6 +167,20 @@ int bufpool_append(corro_ctx *ctx, DevBufPool *p, const corro_changes *dv, std::
 // pool rows [off, off + n) to the host (no long values)
 int bufpool_read(const DevBufPool *p, uint64_t off, uint64_t n, HostSpanRows &out);
 
+// Batched gap bookkeeping (corro_booked_insert_db_batch, gaps.hip) for a call with many actors:
+// host CSR in (per actor: booked max or -1, needed gaps, this call's versions), host arrays out
+// (per actor: new max, DELETE rows, INSERT rows, new gaps, status).
+struct GapsHost {
+    std::vector<int64_t> max;
+    std::vector<uint64_t> gap_off, gap_start, gap_end, ver_off, ver_start, ver_end;
+};
+struct GapsHostOut {
+    std::vector<int64_t> max;
+    std::vector<uint64_t> rm_count, ins_count, gap_count, rm_start, rm_end, ins_start, ins_end, new_start, new_end;
+    std::vector<int32_t> status;
+};
+int agent_dev_gaps(corro_ctx *ctx, const GapsHost &in, GapsHostOut &out);
+
 // every known entry back to Skipped (a failed call)
 int agent_dev_clear_known(corro_ctx *ctx, int32_t *dknown, uint64_t ncs);
 

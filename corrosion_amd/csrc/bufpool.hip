@@ -313,4 +313,66 @@ int bufpool_read(const DevBufPool *p, uint64_t off, uint64_t n, HostSpanRows &o)
     return CORRO_OK;
 }
 
+int agent_dev_gaps(corro_ctx *ctx, const GapsHost &in, GapsHostOut &out) {
+    const uint64_t n = in.max.size();
+    out = GapsHostOut{};
+    if (!n) return CORRO_OK;
+    const uint64_t ng = in.gap_off[n], nv = in.ver_off[n], nw = ng + nv + n;
+    // one device area: inputs, then outputs
+    const size_t sz[] = {n * 8, (n + 1) * 8, ng * 8, ng * 8, (n + 1) * 8, nv * 8, nv * 8,                // in
+                         n * 8, n * 8, n * 8, n * 8, ng * 8, ng * 8, nw * 8, nw * 8, nw * 8, nw * 8, n * 4};  // out
+    size_t off[18], total = 0;
+    for (int k = 0; k < 18; k++) {
+        off[k] = total;
+        total += al256(std::max<size_t>(sz[k], 8));
+    }
+    if (int rc = ctx->d_agent_aux2.ensure(total + 256)) return rc;
+    uint8_t *d = ctx->d_agent_aux2.as<uint8_t>();
+    hipStream_t s = ctx->stream;
+    const void *src[7] = {in.max.data(), in.gap_off.data(), in.gap_start.data(), in.gap_end.data(),
+                          in.ver_off.data(), in.ver_start.data(), in.ver_end.data()};
+    for (int k = 0; k < 7; k++)
+        if (sz[k]) CORRO_HIP_TRY(hipMemcpyAsync(d + off[k], src[k], sz[k], hipMemcpyHostToDevice, s));
+    corro_gaps_in gi{};
+    gi.n = n;
+    gi.max = reinterpret_cast<const int64_t *>(d + off[0]);
+    gi.gap_off = reinterpret_cast<const uint64_t *>(d + off[1]);
+    gi.gap_start = reinterpret_cast<const uint64_t *>(d + off[2]);
+    gi.gap_end = reinterpret_cast<const uint64_t *>(d + off[3]);
+    gi.ver_off = reinterpret_cast<const uint64_t *>(d + off[4]);
+    gi.ver_start = reinterpret_cast<const uint64_t *>(d + off[5]);
+    gi.ver_end = reinterpret_cast<const uint64_t *>(d + off[6]);
+    corro_gaps_out go{};
+    go.max = reinterpret_cast<int64_t *>(d + off[7]);
+    go.rm_count = reinterpret_cast<uint64_t *>(d + off[8]);
+    go.ins_count = reinterpret_cast<uint64_t *>(d + off[9]);
+    go.gap_count = reinterpret_cast<uint64_t *>(d + off[10]);
+    go.rm_start = reinterpret_cast<uint64_t *>(d + off[11]);
+    go.rm_end = reinterpret_cast<uint64_t *>(d + off[12]);
+    go.ins_start = reinterpret_cast<uint64_t *>(d + off[13]);
+    go.ins_end = reinterpret_cast<uint64_t *>(d + off[14]);
+    go.new_start = reinterpret_cast<uint64_t *>(d + off[15]);
+    go.new_end = reinterpret_cast<uint64_t *>(d + off[16]);
+    go.status = reinterpret_cast<int32_t *>(d + off[17]);
+    if (int rc = corro_booked_insert_db_batch(ctx, &gi, &go)) return rc;
+    out.max.resize(n);
+    out.rm_count.resize(n);
+    out.ins_count.resize(n);
+    out.gap_count.resize(n);
+    out.rm_start.resize(ng);
+    out.rm_end.resize(ng);
+    out.ins_start.resize(nw);
+    out.ins_end.resize(nw);
+    out.new_start.resize(nw);
+    out.new_end.resize(nw);
+    out.status.resize(n);
+    void *dst[11] = {out.max.data(), out.rm_count.data(), out.ins_count.data(), out.gap_count.data(),
+                     out.rm_start.data(), out.rm_end.data(), out.ins_start.data(), out.ins_end.data(),
+                     out.new_start.data(), out.new_end.data(), out.status.data()};
+    for (int k = 0; k < 11; k++)
+        if (sz[7 + k]) CORRO_HIP_TRY(hipMemcpyAsync(dst[k], d + off[7 + k], sz[7 + k], hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    return CORRO_OK;
+}
+
 }  // namespace corro

@@ -620,3 +620,19 @@ def test_mixed_call_at_scale_matches_host_path():
     for a in ids:
         assert ba.last(bytes(a)) == bb.last(bytes(a))
         assert ba.needed(bytes(a)) == bb.needed(bytes(a))
+
+
+@pytest.mark.parametrize("device,seed,clean", [("headers", 1, ()), ("headers", 12, (0, 1, 2, 3, 4)), (True, 2, ()),
+                                               (False, 4, ())])
+def test_batched_gap_bookkeeping_route_matches_restatement(device, seed, clean, monkeypatch):
+    """Calls with many actors take the batched device gap pass (corro_booked_insert_db_batch) instead
+    of the per-actor host insert_db; forced here on small calls: the same outcomes, bookkeeping and
+    partials as the restatement, on every header path"""
+    monkeypatch.setenv("CORRO_AGENT_GAPS_BATCH", "1")
+    _check_against_oracle(seed, device=device, clean=clean)
+
+
+def test_batched_gap_bookkeeping_route_overlaps_and_buffers(monkeypatch):
+    monkeypatch.setenv("CORRO_AGENT_GAPS_BATCH", "1")
+    _check_against_oracle(31, device="headers", calls_fn=_overlap_calls)
+    test_device_buffered_rows_match_host_path(42)
