@@ -186,10 +186,37 @@ struct corro_bookie {
     FlatMap<SeqKey, SeqBook> seqbook;                           // (site, version)
     std::vector<std::pair<ActorId, uint64_t>> ready;           // fully buffered, to apply
     std::map<ActorId, uint32_t> site_of;                       // actor -> site ordinal
+    // site ordinal -> its actor's Booked (a map node: stable), checked against the ordinal's id: the
+    // per-call Bookie::ensure without a tree search per actor
+    std::vector<corro::Booked *> site_booked;
+    std::vector<ActorId> site_booked_id;
     std::vector<uint64_t> scratch_ver;                          // process_multiple_changes scratch
 };
 
 namespace {
+
+// Bookie::ensure (agent.rs:1546-1598) through the site cache; create = false: nullptr for an actor
+// the bookie does not hold
+corro::Booked *booked_of_site(corro_bookie *bk, uint32_t site, const ActorId &id, bool create) {
+    if (site < bk->site_booked.size() && bk->site_booked[site] && bk->site_booked_id[site] == id)
+        return bk->site_booked[site];
+    corro::Booked *b = nullptr;
+    if (create) {
+        b = &bk->actors[id];
+        bk->site_of[id] = site;
+    } else {
+        auto it = bk->actors.find(id);
+        if (it == bk->actors.end()) return nullptr;
+        b = &it->second;
+    }
+    if (site >= bk->site_booked.size()) {
+        bk->site_booked.resize((size_t)site + 1, nullptr);
+        bk->site_booked_id.resize((size_t)site + 1);
+    }
+    bk->site_booked[site] = b;
+    bk->site_booked_id[site] = id;
+    return b;
+}
 
 ActorId actor_of(const uint8_t *p) {
     ActorId a;
@@ -1042,8 +1069,8 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     std::vector<int64_t> site_max(nsites, -1);
     for (uint32_t t = 0; t < nsites; t++) {
         corro::agent_site_id(ctx, t, site_id[t].data());
-        auto it = bk->actors.find(site_id[t]);
-        if (it != bk->actors.end() && it->second.has_max) site_max[t] = (int64_t)it->second.max;
+        const corro::Booked *b = booked_of_site(bk, t, site_id[t], false);
+        if (b && b->has_max) site_max[t] = (int64_t)b->max;
     }
     corro_changes dv{};
     if (in) dv = *in;
@@ -1056,6 +1083,11 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     // actors of the call, each with its host changesets (R.hcs: grouped by actor in site-rank order)
     std::vector<ActorWork> work;
     std::vector<int64_t> work_of(nsites, -1);
+    {
+        size_t na = 0;
+        for (uint32_t t = 0; t < nsites; t++) na += R.sites[t].gstart != 0xFFFFFFFFu;
+        work.reserve(na);  // (no reallocation moves of the per-actor state)
+    }
     for (uint32_t t = 0; t < nsites; t++) {
         if (R.sites[t].gstart == 0xFFFFFFFFu) continue;
         work_of[t] = (int64_t)work.size();
@@ -1065,8 +1097,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         w.id = site_id[t];
     }
     for (ActorWork &w : work) {  // Bookie::ensure
-        w.booked = &bk->actors[w.id];
-        bk->site_of[w.id] = w.site;
+        w.booked = booked_of_site(bk, w.site, w.id, true);
         w.had_max = w.booked->has_max;
         w.max = w.booked->max;
     }
@@ -1180,9 +1211,11 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             for (uint64_t version : w.set_dbv) sv.emplace_back(w.site, version);
         TRY_RC(corro::set_db_versions(ctx, sv));
     }
+    // actors in ActorId order: the device sort's site-rank order (each actor's first sorted slot)
     std::vector<size_t> order(work.size());
     for (size_t k = 0; k < order.size(); k++) order[k] = k;
-    std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return work[x].id < work[y].id; });
+    std::sort(order.begin(), order.end(),
+              [&](size_t x, size_t y) { return R.sites[work[x].site].gstart < R.sites[work[y].site].gstart; });
     {
         std::vector<Staged *> sto;
         for (size_t k : order) sto.push_back(&work[k].st);
@@ -1202,7 +1235,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     uint64_t nready = 0;
     for (size_t k : order) {
         ActorWork &w = work[k];
-        if (w.has_next) *w.booked = std::move(w.next);
+        if (w.has_next) std::swap(*w.booked, w.next);  // (the old state is freed with the call's work)
         for (uint64_t v : w.ready) bk->ready.emplace_back(w.id, v);
         nready += w.ready.size();
     }
@@ -1396,6 +1429,7 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
     // order) need no per-actor walk: no version repeats, so no batch-local dedup and nothing already
     // seen in this call -- pass 1's contains_all is the only check left, made per changeset below
     std::vector<ActorWork> work;
+    work.reserve(std::min<uint64_t>(nsites, ncs));  // (no reallocation moves of the per-actor state)
     std::vector<int64_t> work_of(nsites, -1);
     bool any_slow = false;
     for (uint32_t t = 0; t < nsites; t++) {
@@ -1419,8 +1453,7 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
         any_slow |= !ok;
     }
     for (ActorWork &w : work) {  // Bookie::ensure (std::map nodes: stable pointers for the workers)
-        w.booked = &bk->actors[w.id];
-        bk->site_of[w.id] = w.site;
+        w.booked = booked_of_site(bk, w.site, w.id, true);
         w.had_max = w.booked->has_max;
         w.max = w.booked->max;
     }
@@ -1633,7 +1666,7 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
     uint64_t nready = 0;
     for (size_t k : order) {
         ActorWork &w = work[k];
-        if (w.has_next) *w.booked = std::move(w.next);
+        if (w.has_next) std::swap(*w.booked, w.next);  // (the old state is freed with the call's work)
         for (uint64_t v : w.ready) bk->ready.emplace_back(w.id, v);
         nready += w.ready.size();
     }
