@@ -111,11 +111,57 @@ struct PoolSeg {
 };
 constexpr uint64_t SEG_PENDING = 1ULL << 63;  // off = SEG_PENDING | copy job (until the copy runs)
 
+// A key's segments: sorted by seq0; the first two inline (a version arrives in a few pieces, and a
+// call buffers tens of thousands of keys: no allocation per key)
+class SegList {
+  public:
+    SegList() = default;
+    SegList(const SegList &o) : n_(o.n_), more_(o.more_) { std::copy(o.in_, o.in_ + 2, in_); }
+    SegList(SegList &&o) noexcept : n_(o.n_), more_(std::move(o.more_)) {
+        std::copy(o.in_, o.in_ + 2, in_);
+        o.n_ = 0;
+    }
+    SegList &operator=(SegList o) noexcept {
+        n_ = o.n_;
+        std::copy(o.in_, o.in_ + 2, in_);
+        more_.swap(o.more_);
+        return *this;
+    }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    PoolSeg *begin() { return n_ <= 2 ? in_ : more_.data(); }
+    PoolSeg *end() { return begin() + n_; }
+    const PoolSeg *begin() const { return n_ <= 2 ? in_ : more_.data(); }
+    const PoolSeg *end() const { return begin() + n_; }
+    void clear() {
+        n_ = 0;
+        more_.clear();
+    }
+    // insert keeping seq0 order
+    void insert_sorted(const PoolSeg &g) {
+        if (n_ < 2) {
+            in_[n_++] = g;
+            if (n_ == 2 && in_[1].seq0 < in_[0].seq0) std::swap(in_[0], in_[1]);
+            return;
+        }
+        if (n_ == 2) more_.assign(in_, in_ + 2);
+        more_.insert(std::lower_bound(more_.begin(), more_.end(), g,
+                                      [](const PoolSeg &x, const PoolSeg &y) { return x.seq0 < y.seq0; }),
+                     g);
+        n_++;
+    }
+
+  private:
+    size_t n_ = 0;
+    PoolSeg in_[2] = {};
+    std::vector<PoolSeg> more_;  // (all of them once there are more than two)
+};
+
 // __corro_buffered_changes rows of one (site, db_version): host rows, or (every row of the key came
 // from canonical partial changesets of a device batch) pool segments -- never both
 struct BufEntry {
     BufRows rows;
-    std::vector<PoolSeg> segs;
+    SegList segs;
     bool empty() const { return rows.empty() && segs.empty(); }
 };
 
@@ -374,8 +420,8 @@ int materialize(corro_bookie *bk, BufEntry &e) {
 }
 
 // [s, e] minus the (sorted, disjoint) segments: the seqs not buffered yet, ascending
-std::vector<Range> seq_pieces(const std::vector<PoolSeg> &segs, uint64_t s, uint64_t e) {
-    std::vector<Range> out;
+void seq_pieces(const SegList &segs, uint64_t s, uint64_t e, std::vector<Range> &out) {
+    out.clear();
     uint64_t x = s;
     for (const PoolSeg &g : segs) {
         const uint64_t gs = g.seq0, ge = (uint64_t)g.seq0 + g.n - 1;
@@ -386,7 +432,6 @@ std::vector<Range> seq_pieces(const std::vector<PoolSeg> &segs, uint64_t s, uint
         if (x > e) break;
     }
     if (x <= e) out.emplace_back(x, e);
-    return out;
 }
 
 // The call's staged __corro_buffered_changes INSERTs into the bookie; ON CONFLICT (site_id,
@@ -495,6 +540,9 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     if (!all_dev.empty() && pool_ok && !bk->pool) bk->pool = corro::bufpool_new();
     std::vector<corro::PoolCopy> jobs;
     std::vector<std::pair<BufKey, BufEntry>> add;
+    std::vector<Range> pieces;
+    jobs.reserve(all_dev.size());
+    add.reserve(groups.size());
     for (size_t gi = 0; gi < groups.size(); gi++) {
         const BufKey key = sp[groups[gi].first]->key;
         BufEntry local;
@@ -526,12 +574,11 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
                 }
                 buf_insert(e->rows, hr.data(), hr.data() + hr.size());
             } else {
-                for (const Range &r : seq_pieces(e->segs, it.seq0, (uint64_t)it.seq0 + it.n - 1)) {
+                seq_pieces(e->segs, it.seq0, (uint64_t)it.seq0 + it.n - 1, pieces);
+                for (const Range &r : pieces) {
                     const PoolSeg g{SEG_PENDING | jobs.size(), (uint32_t)r.first, (uint32_t)(r.second - r.first + 1)};
                     jobs.push_back({it.src + (r.first - it.seq0), r.second - r.first + 1, it.ts, 0});
-                    e->segs.insert(std::lower_bound(e->segs.begin(), e->segs.end(), g,
-                                                    [](const PoolSeg &x, const PoolSeg &y) { return x.seq0 < y.seq0; }),
-                                   g);
+                    e->segs.insert_sorted(g);
                 }
             }
         }
