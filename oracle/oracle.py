@@ -157,33 +157,93 @@ class Fold:
         lib().of_set_affinity(self._h, table, b, len(b))
 
     def export(self):
-        m = lib().of_count(self._h)
-        out = {"pk": np.zeros(m, np.uint64), "table_cid": np.zeros(m, np.uint32),
-               "col_version": np.zeros(m, np.int64), "db_version": np.zeros(m, np.int64),
-               "cl": np.zeros(m, np.int64), "seq": np.zeros(m, np.uint32),
-               "site": np.zeros(m, np.uint32), "ts": np.zeros(m, np.uint64),
-               "val0": np.zeros(m, np.uint64), "val1": np.zeros(m, np.uint64),
-               "val_type": np.zeros(m, np.uint8), "val_len": np.zeros(m, np.uint8)}
-        r = _Rows()
-        for k, a in out.items():
-            setattr(r, k, a.ctypes.data if m else None)
-        if m:
-            got = lib().of_export(self._h, C.byref(r))
-            assert got == m
-        out["long_values"] = {int(i): self.value_bytes(int(out["val1"][i]))
-                              for i in np.nonzero(out["val_len"] == OF_LONG)[0]}
-        return out
+        return _export_handle(self._h)
 
     def value_bytes(self, handle):
-        n = lib().of_value_bytes(self._h, handle, None, 0)
-        buf = C.create_string_buffer(max(n, 1))
-        lib().of_value_bytes(self._h, handle, buf, n)
-        return buf.raw[:n]
+        return _value_bytes(self._h, handle)
 
     def db_versions(self):
         out = np.zeros(max(self.nsites, 1), np.int64)
         lib().of_db_versions(self._h, out.ctypes.data)
         return out[: self.nsites]
+
+
+def _value_bytes(h, handle):
+    n = lib().of_value_bytes(h, handle, None, 0)
+    buf = C.create_string_buffer(max(n, 1))
+    lib().of_value_bytes(h, handle, buf, n)
+    return buf.raw[:n]
+
+
+def _export_handle(h):
+    """crsql_changes rows of one fold state (the layout MergeEngine.export() returns)"""
+    m = lib().of_count(h)
+    out = {"pk": np.zeros(m, np.uint64), "table_cid": np.zeros(m, np.uint32),
+           "col_version": np.zeros(m, np.int64), "db_version": np.zeros(m, np.int64),
+           "cl": np.zeros(m, np.int64), "seq": np.zeros(m, np.uint32),
+           "site": np.zeros(m, np.uint32), "ts": np.zeros(m, np.uint64),
+           "val0": np.zeros(m, np.uint64), "val1": np.zeros(m, np.uint64),
+           "val_type": np.zeros(m, np.uint8), "val_len": np.zeros(m, np.uint8)}
+    r = _Rows()
+    for k, a in out.items():
+        setattr(r, k, a.ctypes.data if m else None)
+    if m:
+        got = lib().of_export(h, C.byref(r))
+        assert got == m
+    out["long_values"] = {int(i): _value_bytes(h, int(out["val1"][i]))
+                          for i in np.nonzero(out["val_len"] == OF_LONG)[0]}
+    return out
+
+
+ROW_KEYS = ("table_cid", "pk")  # a clock row's identity (cid is in table_cid's low half)
+ROW_VALUE_FIELDS = ("col_version", "db_version", "cl", "seq", "site", "ts", "val0", "val1", "val_type", "val_len")
+
+
+def rows_diff(got, ref, limit=5):
+    """Row-by-row comparison of two crsql_changes exports (MergeEngine.export() / Fold.export() /
+    ShardedFold.export()): None when equal, else a report of the row counts and the first `limit`
+    differing rows, keyed by (table, cid, pk), so a failed full-size parity check says where. Long
+    values compare by their bytes (rows["long_values"]), not by their handles."""
+    kdt = np.dtype([("tc", "<u4"), ("pk", "<u8")])
+
+    def keyed(r):
+        o = np.lexsort((np.asarray(r["pk"]), np.asarray(r["table_cid"])))
+        k = np.empty(len(o), kdt)
+        k["tc"] = np.asarray(r["table_cid"])[o]
+        k["pk"] = np.asarray(r["pk"])[o]
+        return o, k
+
+    def name(k):
+        return f"table {int(k['tc']) >> 16} cid {int(k['tc']) & 0xFFFF} pk {int(k['pk'])}"
+
+    og, kg = keyed(got)
+    orf, kr = keyed(ref)
+    if len(og) != len(orf) or not np.array_equal(kg, kr):
+        lines = [f"row sets differ: got {len(og)} rows, expected {len(orf)}"]
+        lines += [f"  extra row ({name(k)})" for k in np.setdiff1d(kg, kr)[:limit]]
+        lines += [f"  missing row ({name(k)})" for k in np.setdiff1d(kr, kg)[:limit]]
+        return "\n".join(lines)
+    lg, lr = got.get("long_values") or {}, ref.get("long_values") or {}
+    bad = np.zeros(len(og), bool)
+    for f in ROW_VALUE_FIELDS:
+        a, b = np.asarray(got[f])[og], np.asarray(ref[f])[orf]
+        if f == "val1" and (lg or lr):  # long values: handles differ between stores, bytes must not
+            is_long = np.asarray(got["val_len"])[og] == OF_LONG
+            d = (a != b) & ~is_long
+            for j in np.nonzero(is_long)[0]:
+                d[j] = lg.get(int(og[j])) != lr.get(int(orf[j]))
+            bad |= d
+        else:
+            bad |= a != b
+    idx = np.nonzero(bad)[0]
+    if not len(idx):
+        return None
+    lines = [f"{len(idx)} of {len(og)} rows differ; the first {min(limit, len(idx))}:"]
+    for j in idx[:limit]:
+        g = {f: int(np.asarray(got[f])[og[j]]) for f in ROW_VALUE_FIELDS}
+        r = {f: int(np.asarray(ref[f])[orf[j]]) for f in ROW_VALUE_FIELDS}
+        lines.append(f"  {name(kg[j])}: (got, expected) " + str({f: (g[f], r[f]) for f in ROW_VALUE_FIELDS if g[f] != r[f]}))
+    return "\n".join(lines)
 
 
 class ShardedFold:
@@ -218,6 +278,16 @@ class ShardedFold:
         for h in self._hs:
             lib().of_state_digest(h, out.ctypes.data)
         return tuple(int(x) for x in out)
+
+    def export(self):
+        """every shard's rows, concatenated (long-value indices re-based)"""
+        parts = [_export_handle(h) for h in self._hs]
+        out = {k: np.concatenate([p[k] for p in parts]) for k in parts[0] if k != "long_values"}
+        out["long_values"], base = {}, 0
+        for p in parts:
+            out["long_values"].update({i + base: v for i, v in p["long_values"].items()})
+            base += len(p["pk"])
+        return out
 
     def db_versions(self):
         acc = np.full(max(self.nsites, 1), -1, np.int64)

@@ -5,12 +5,13 @@
     state (each batch into the state the previous ones left: the in-place row store), checked against
     the oracle's pk-sharded fold (oracle/crsql_fold.c of_apply_sharded, the sequential rules run per
     shard on the host cores): every impact flag, the crsql_changes rows through an order-independent
-    digest of every output field (row count, sum and xor of per-row 64-bit hashes), crsql_db_versions;
+    digest of every output field (row count, sum and xor of per-row 64-bit hashes; a mismatch prints
+    the row-by-row report of oracle.rows_diff), crsql_db_versions;
   * config 5: the adversarial mix at its stated 64M size (8 tables, Zipf(1.1) hot pks over 2^20 per
     table, 30 % sentinel deletes / resurrects, mixed INTEGER / REAL / TEXT / BLOB / NULL values), two
     64M batches folded into one state with impact flags -- the regime where ~57M records per apply
     take the device-wide overflow fold with the row store's prior-row lookups -- against the same
-    pk-sharded oracle fold;
+    pk-sharded oracle fold, every output row compared field by field (oracle.rows_diff) and by digest;
   * config 4: 1M node pairs x 64 sparse actors from a 100k-actor universe (64M need-diff entries),
     the device need diff against the oracle restatement (oracle/ranges.c, threaded over entry
     chunks), every output array equal.
@@ -62,8 +63,9 @@ def _config3(batches):
         del hb, imp, ref
     rows = eng.export()
     dg = O.rows_digest(rows)
+    if dg != fold.digest():  # (where: the row-by-row report)
+        pytest.fail("config 3 state differs from the oracle:\n" + str(O.rows_diff(rows, fold.export())))
     del rows
-    assert dg == fold.digest()
     assert np.array_equal(eng.db_versions(), fold.db_versions())
     print(f"config 3, {batches} batch(es): {dg[0]} clock rows bit-exact; GPU apply s per batch "
           + ", ".join(f"{t:.3f}" for t in t_gpu))
@@ -117,10 +119,13 @@ def test_config5_64m_two_batch_fold_vs_sharded_oracle(impact):
     assert m["overflow_rounds"] >= 2          # the hot-row regime was exercised
     rows = eng.export()
     dg = O.rows_digest(rows)
+    # every row compared field by field against the oracle's rows (8 M rows), and the digest too
+    rep = O.rows_diff(rows, fold.export())
+    assert rep is None, "config 5 state differs from the oracle:\n" + rep
     del rows
     assert dg == fold.digest()
     assert np.array_equal(eng.db_versions(), fold.db_versions())
-    print(f"config 5, 2 x 64M folded: {dg[0]} clock rows bit-exact")
+    print(f"config 5, 2 x 64M folded: {dg[0]} clock rows bit-exact, row by row")
     eng.close()
 
 
