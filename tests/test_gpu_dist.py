@@ -1,6 +1,7 @@
 """Two ranks on one GPU box: device pk-hash partition (HIP) + all-to-all exchange (gloo through host
 memory here; RCCL on a multi-GPU node) + per-rank device merge. The union of the rank states must
-equal the single-engine merge of the whole batch, bit for bit."""
+equal the single-engine merge of the whole batch, bit for bit, and that merge the oracle's
+sequential fold (rows, impact flags, db_versions)."""
 import os
 import socket
 
@@ -59,13 +60,19 @@ def test_two_rank_device_merge_equals_single_engine(tmp_path):
     got = []
     for r in range(world):
         got += [tuple(x) for x in np.load(tmp_path / f"rows{r}.npy", allow_pickle=True)]
+    from oracle import oracle as O
     e = ca.MergeEngine(synth.adversarial_schema(NT), capacity_hint=N)
     e.register_sites(synth.site_ids(8, SEED))
-    want_imp = e.apply(synth.adversarial_batch(N, 8, NT, 500, SEED), impact=True)
+    batch = synth.adversarial_batch(N, 8, NT, 500, SEED)
+    want_imp = e.apply(batch, impact=True)
     assert sorted(got) == rows_to_tuples(e.export(), with_ts=True)
     # per-change impacts come back to each sender in its own order (reverse all-to-all + permutation)
     got_imp = np.concatenate([np.load(tmp_path / f"imp{r}.npy") for r in range(world)])
     assert np.array_equal(got_imp, want_imp)
+    # and the single engine (so the union of the ranks) against the oracle's sequential fold
+    f = O.Fold(synth.site_ids(8, SEED))
+    assert np.array_equal(want_imp, f.apply(batch))
+    assert O.rows_diff(e.export(), f.export()) is None
 
 
 def _sites_worker(rank, world, port, outdir):
@@ -269,9 +276,15 @@ def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale):
         got += [tuple(x) for x in np.load(tmp_path / f"srows{r}.npy", allow_pickle=True)]
     nover = int(np.load(tmp_path / "sover0.npy")[0])
     assert (nover == 0) == (cap_scale == 1.0)
+    from oracle import oracle as O
     e = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS)
     e.register_sites(synth.site_ids(16, 5))
-    e.apply(synth.uniform_batch(NS, 16, 4000, 4, 77))
+    batch = synth.uniform_batch(NS, 16, 4000, 4, 77)
+    e.apply(batch)
     assert sorted(got) == rows_to_tuples(e.export(), with_ts=True)
     dbv = np.max([np.load(tmp_path / f"sdbv{r}.npy") for r in range(world)], axis=0)
     assert list(dbv) == list(e.db_versions())
+    f = O.Fold(synth.site_ids(16, 5))  # (the single engine, so the ranks' union, against the oracle)
+    f.apply(batch)
+    assert O.rows_diff(e.export(), f.export()) is None
+    assert list(e.db_versions()) == list(f.db_versions())
