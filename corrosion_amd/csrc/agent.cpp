@@ -1148,6 +1148,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         w.had_max = w.booked->has_max;
         w.max = w.booked->max;
     }
+    stage("act_setup");
     const uint64_t nh = R.nh;
     const corro_changeset *hcs = R.hcs;
     std::vector<uint8_t> hflag(nh, 0);
@@ -1208,10 +1209,12 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     const CsView view{hcs, R.hbad, hknown.data(), hflag.data(), canon};
     if (want_gaps_batch(work))
         for (ActorWork &w : work) w.defer_gaps = true;
+    stage("act_runs");
     run_parallel(work.size(), [&](size_t k) { run_actor_walk(bk, work[k], view, dev_runs[k], row_of); });
     TRY_RC(gaps_batch(ctx, work));
     for (ActorWork &w : work)
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);
+    stage("act_walk");
     uint64_t nspans = R.nspans, nb = R.nchanges;
     for (const ActorWork &w : work) {
         nspans += w.nspans;

@@ -694,7 +694,9 @@ int spans_to_batch(corro_ctx *ctx, const corro_changes *dv, uint64_t nspans, uin
     if (pm && nspans && !(fg && fg[0] == '1') && dv->n <= corro_detail_chunk_changes(ctx) && aligned(dv->pk, 16) && aligned(dv->col_version, 16) &&
         aligned(dv->db_version, 16) && aligned(dv->val0, 16) && aligned(dv->val1, 16) && aligned(dv->table_cid, 8) &&
         aligned(dv->cl, 8) && aligned(dv->seq, 8) && aligned(dv->site, 8)) {
-        const bool want_ts = need_ts || dv->ts;
+        // per-position ts only from the changesets: an input with per-change ts is staged with them
+        // (the apply puts an INTEGER batch's ts in its staged records, else gathers them by position)
+        const bool want_ts = need_ts && !dv->ts;
         const size_t o_src = al256(dv->n * 4), o_ts = o_src + al256(nbatch * 4);
         if (int rc = ctx->d_agent_batch.ensure(o_ts + (want_ts ? nbatch * 8 : 0) + 256)) return rc;
         uint8_t *base = ctx->d_agent_batch.as<uint8_t>();

@@ -611,7 +611,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_agent_in, &ctx->d_agent_batch, &ctx->d_agent_spans, &ctx->d_agent_imp,
                       &ctx->d_agent_out, &ctx->d_agent_aux, &ctx->d_agent_fetch, &ctx->d_agent_aux2, &ctx->d_touch, &ctx->d_touch_n, &ctx->d_touch_stamp, &ctx->d_touch_tmp,
                       &ctx->d_aff_conv, &ctx->d_aff_vals, &ctx->d_gaps_big, &ctx->d_agent_hdr, &ctx->d_wire_map,
-                      &ctx->d_hdr_stage};
+                      &ctx->d_hdr_stage, &ctx->d_pm_ts};
     for (DevBuf *b : bufs) b->release();
     ctx->d_pkdir.release();
     ctx->d_part_var.release();
@@ -752,6 +752,13 @@ static int stage_host_batch(corro_ctx *ctx, const corro_changes *in, BatchDev &b
     return CORRO_OK;
 }
 
+// position mode, value words in the batch: ts[p] = input ts of application position p
+static __global__ void k_ts_by_pos(const uint64_t *__restrict__ in_ts, const uint32_t *__restrict__ src_of, uint64_t n,
+                                   uint64_t *__restrict__ out) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x)
+        out[p] = in_ts[src_of[p]];
+}
+
 static int error_from_bits(uint64_t bits) {
     if (bits & ERR_NAME) return fail(CORRO_E_UNKNOWN_COLUMN, "batch references an unknown table or cid");
     if (bits & ERR_SITE) return fail(CORRO_E_INVALID, "batch references an unregistered site ordinal");
@@ -818,6 +825,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     {
         static const bool nt_stores = std::getenv("CORRO_HIP_NT") && std::atoi(std::getenv("CORRO_HIP_NT")) != 0;
         const bool plain = !bd.v1 && !bd.vt && !bd.vl && !bd.conv;
+        if (bd.ts_v1 && !plain) return fail(CORRO_E_INVALID, "internal: ts_v1 on a batch with value words");
         auto kern = plain ? (nt_stores ? k_scatter<true, true> : k_scatter<true, false>)
                           : (nt_stores ? k_scatter<false, true> : k_scatter<false, false>);
         hipLaunchKernelGGL(kern, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4 + ((B + 31) / 32) * 4, s, bd,
@@ -867,6 +875,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         a.raw.arena = ctx->d_arena.as<uint8_t>();
     }
     a.pos_src = bd.ap ? ctx->pm_src : nullptr;
+    a.ts_v1 = bd.ts_v1;
     uint32_t nblocks = B;
     float merge_ms = 0.f, ovf_ms = 0.f;
     // A batch that failed validation (k_scatter's error bits in misc[0]) is never merged: the merge
@@ -1099,7 +1108,9 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.ap = ctx->pm_ap;
         // (positions [0, pm_n) cover every input change; a mapped apply's skips are anywhere)
         bd.ap_all = ctx->pm_n == n && !ctx->pm_slack ? 1u : 0u;
-        bd.ts = ctx->pm_ts;
+        // per-position timestamps (pm_ts), else the input's own per-change ones (by input index)
+        bd.ts = ctx->pm_ts ? ctx->pm_ts : in->ts;
+        bd.ts_pos = ctx->pm_ts ? 1u : 0u;
     }
     // long values: the batch's value bytes are appended to the arena once; every chunk's changes
     // name their bytes relative to that base. A failed batch leaves them unreferenced.
@@ -1123,6 +1134,21 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
     uint8_t *imp_buf = !(out && out->impact) ? nullptr : (imp_dev ? out->impact : ctx->d_impact.as<uint8_t>());
 
     TRY(affinity_convert(ctx, bd));
+    // INTEGER-only batch: the scatter stages each change's ts in its record's v1 word (BatchDev::ts_v1;
+    // CORRO_TS_V1=0 keeps the per-position ts array, A/B). Otherwise ts must be per position: a
+    // position-mode batch that brought its input's per-change ts gets them gathered into that order.
+    static const bool no_ts_v1 = std::getenv("CORRO_TS_V1") && std::atoi(std::getenv("CORRO_TS_V1")) == 0;
+    const bool plain = !bd.v1 && !bd.vt && !bd.vl && !bd.conv;
+    bd.ts_v1 = bd.ts && plain && !no_ts_v1 ? 1u : 0u;
+    if (bd.ap && bd.ts && !bd.ts_pos && !bd.ts_v1) {
+        if (!ctx->pm_src) return fail(CORRO_E_INVALID, "internal: position mode without a position -> input map");
+        TRY(ctx->d_pm_ts.ensure(ctx->pm_n * 8 + 8));
+        hipLaunchKernelGGL(k_ts_by_pos, dim3((uint32_t)std::min<uint64_t>((ctx->pm_n + 255) / 256, 8192)), dim3(256), 0,
+                           ctx->stream, bd.ts, ctx->pm_src, ctx->pm_n, ctx->d_pm_ts.as<uint64_t>());
+        CORRO_HIP_TRY(hipGetLastError());
+        bd.ts = ctx->d_pm_ts.as<uint64_t>();
+        bd.ts_pos = 1;
+    }
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
     const uint64_t chunk = ctx->pm_ap ? std::max<uint64_t>(n, 1) : corro_detail_chunk_changes(ctx);
     if (n > chunk) {

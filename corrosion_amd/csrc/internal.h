@@ -178,6 +178,7 @@ struct corro_ctx {
     corro::DevBuf d_setdbv;       // set_db_versions: (site, version + 1) pairs
     corro::DevBuf d_scan_tmp;     // corro_scan_offsets: rocPRIM temp
     corro::DevBuf d_impact;
+    corro::DevBuf d_pm_ts;        // position mode: the input's per-change ts in application order (k_ts_by_pos)
     corro::DevBuf d_export;
     corro::DevBuf d_needs;        // sync-need scratch
     corro::DevBuf d_needs1;       // one-pass need diff: look-back status words + ticket

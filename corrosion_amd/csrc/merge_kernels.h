@@ -81,6 +81,8 @@ struct MergeArgs {
     BatchDev raw;
     // position mode: input index of application position p (null: p itself)
     const uint32_t *pos_src;
+    // batch records carry their ts in v1 (BatchDev::ts_v1); their value's v1 word is 0
+    uint32_t ts_v1;
 };
 
 // input index of batch position p (position mode maps it, MergeArgs::pos_src)
@@ -471,6 +473,15 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                 b.pos = BATCH_POS | ap2.y;
                 if (ap2.x == AP_SKIP) a.site = 0xFFFFFFFFu;
                 if (ap2.y == AP_SKIP) b.site = 0xFFFFFFFFu;
+                if (in.ts_v1) {  // (loads issued with the others: consumed at the store)
+                    if (in.ts_pos) {
+                        a.v1 = ap2.x != AP_SKIP ? in.ts[ap2.x] : 0ULL;
+                        b.v1 = ap2.y != AP_SKIP ? in.ts[ap2.y] : 0ULL;
+                    } else {
+                        a.v1 = in.ts[ic];
+                        b.v1 = in.ts[ic + 1];
+                    }
+                }
             }
         } else {
 #pragma unroll
@@ -535,6 +546,8 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
             const bool act = i < end && (!in.ap || (r.pos & 0x7FFFFFFFu) != (AP_SKIP & 0x7FFFFFFFu));
             uint32_t idx = 0;
             if (act) {
+                // (the unpaired path of an INTEGER batch: its ts into v1 here)
+                if (PLAIN && !plain && in.ts_v1) r.v1 = in.ts[in.ts_pos ? (r.pos & 0x7FFFFFFFu) : i];
                 // a value its column's affinity converts is staged converted (affinity.hip); its
                 // bucket takes the general body, which compares it raw as the incoming change
                 const bool cvt = !PLAIN && in.conv && in.conv[i];
@@ -638,8 +651,19 @@ __device__ inline Rec rec_from_wave_quads(uint4 q[4]) {
 
 template <class V>
 __device__ inline uint64_t rec_ts(const MergeArgs &a, const V &v, const Rec &r) {
-    if (r.pos & BATCH_POS) return a.batch_ts ? a.batch_ts[r.pos & 0x7FFFFFFFu] : 0ULL;
+    if (r.pos & BATCH_POS) return a.ts_v1 ? r.v1 : (a.batch_ts ? a.batch_ts[r.pos & 0x7FFFFFFFu] : 0ULL);
     return v.prior_ts(r);
+}
+// a batch record about to be stored as a clock row: its value's v1 word back to 0 under ts_v1 (call
+// after rec_ts, before pos is rewritten)
+__device__ inline void rec_clear_ts(const MergeArgs &a, Rec &r) {
+    if (a.ts_v1 && (r.pos & BATCH_POS)) r.v1 = 0;
+}
+// ts of the fast bodies' winner x (built in registers without v1), staged at stage index i
+template <class V>
+__device__ inline uint64_t win_ts(const MergeArgs &a, const V &v, const Rec &x, uint32_t i) {
+    if (a.ts_v1 && (x.pos & BATCH_POS)) return v.fresh[i].v1;
+    return rec_ts(a, v, x);
 }
 
 __device__ inline void push_overflow(const MergeArgs &a, uint32_t b) {
@@ -713,6 +737,7 @@ __device__ inline uint32_t heap_write_row(const MergeArgs &a, const V &v, const 
         for (uint32_t u = 0; u < EU; u++) {
             if (c0 + u >= ncell) break;
             const uint64_t ts = a.track_ts ? rec_ts(a, v, r[u]) : 0ULL;
+            rec_clear_ts(a, r[u]);
             const uint32_t cid = r[u].tcid & 0xFFFFu;
             r[u].cv = g.ccv[s + c0 + u];
             r[u].cl = (uint32_t)L;
@@ -1629,7 +1654,8 @@ __device__ inline void fast_body(const MergeArgs &a, uint32_t b, const BucketVie
                 x.pos = ~(uint32_t)rp[k];
                 x.meta = CORRO_INTEGER;
             }
-            if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
+            if (a.track_ts) a.rs.heap_ts[hb[k]] = win_ts(a, v, x, i);
+            rec_clear_ts(a, x);
             x.cl = 1;
             x.pos = hb[k];
         }
@@ -1865,6 +1891,7 @@ __device__ inline void fast_body_impact_wide(const MergeArgs &a, uint32_t b, con
             x.pos = pos[k];
             x.meta = meta[k];
             if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
+            rec_clear_ts(a, x);
             x.cl = 1;
             x.pos = hb[k];
             if ((flags >> (2 * k + 1)) & 1u) {
@@ -2094,7 +2121,7 @@ __device__ inline void fast_body_impact_int(const MergeArgs &a, uint32_t b, cons
             x.site = site[k];
             x.pos = pos[k];
             x.meta = CORRO_INTEGER;
-            if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
+            if (a.track_ts) a.rs.heap_ts[hb[k]] = win_ts(a, v, x, k * FAST_T + tid);
             x.cl = 1;
             x.pos = hb[k];
             if ((flags >> (2 * k + 1)) & 1u) {
@@ -2403,7 +2430,8 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
     constexpr int WH = (FAST_R + 1) / 2;  // two halves: the reloads of one half in flight at once
 #pragma unroll
     for (int h = 0; h < FAST_R; h += WH) {
-        uint2 w0[WH], w16[WH], w48[WH];  // pk | db_version | seq, site
+        uint2 w0[WH], w16[WH], w48[WH], w32[WH];  // pk | db_version | seq, site | ts (ts_v1)
+        const bool tsv = a.track_ts && a.ts_v1;
 #pragma unroll
         for (int u = 0; u < WH && h + u < FAST_R; u++) {
             const int k = h + u;
@@ -2413,6 +2441,7 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
                 w0[u] = src[0];
                 w16[u] = src[2];
                 w48[u] = src[6];
+                if (tsv) w32[u] = src[4];
             }
         }
 #pragma unroll
@@ -2430,7 +2459,8 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
                 x.site = w48[u].y;
                 x.pos = pos[k];
                 x.meta = CORRO_INTEGER;
-                if (a.track_ts) a.rs.heap_ts[hb[k]] = rec_ts(a, v, x);
+                if (a.track_ts)
+                    a.rs.heap_ts[hb[k]] = tsv && (x.pos & BATCH_POS) ? ((uint64_t)w32[u].y << 32) | w32[u].x : rec_ts(a, v, x);
                 x.cl = 1;
                 x.pos = hb[k];
                 if ((flags >> (2 * k + 1)) & 1u) {

@@ -949,6 +949,7 @@ __device__ inline uint32_t ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_
         for (uint32_t c = 0; c < ncell; c++) {
             Rec r = load_rec(ovf_rec(a, d, d.val_s[cells_.pos(c)]));
             const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+            rec_clear_ts(a, r);
             const uint32_t cid = r.tcid & 0xFFFFu;
             if (cells_.z(c)) r.cv = 0;
             r.cl = (uint32_t)rowcl;
