@@ -378,11 +378,11 @@ int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset
     merged.insert(s, e);
     if (merged.size() != 1) return fail(CORRO_E_INVALID, "deleted non-contiguous seq ranges");
     keep.push_back(*merged.ranges().begin());
-    sb.ranges = keep;
+    sb.ranges = std::move(keep);
     sb.last_seq = cs.last_seq;
     sb.ts = cs.ts;
     out = corro::PartialVersion();
-    out.seqs = merged;
+    out.seqs = std::move(merged);
     out.last_seq = cs.last_seq;
     out.ts = cs.ts;
     return CORRO_OK;
@@ -484,6 +484,7 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
         auto less = [](const Sub &x, const Sub &y) { return x.key < y.key || (x.key == y.key && x.call < y.call); };
         if (!std::is_sorted(v.begin(), v.end(), less)) std::sort(v.begin(), v.end(), less);
     });
+    mark("cb_subs");
     for (const auto &t : ptab)
         for (size_t k = 0; k < ntables; k++) committed[k] += t[k];
     std::vector<size_t> blk;
@@ -528,6 +529,7 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
         ghost.push_back(host);
         g0 = g1;
     }
+    mark("cb_groups");
     corro::HostSpanRows fr;
     if (!fsp.empty()) TRY_RC(corro::agent_dev_fetch(ctx, dv, fsp, fr));
     mark("cb_fetch");
@@ -584,8 +586,9 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
         }
         if (fresh && !local.empty()) add.emplace_back(key, std::move(local));
     }
-    bk->buffered.merge(std::move(add));
     mark("cb_trim");
+    bk->buffered.merge(std::move(add));
+    mark("cb_merge");
     if (jobs.empty()) return CORRO_OK;
     uint64_t need = 0;
     for (const corro::PoolCopy &j : jobs) need += j.count;
@@ -974,7 +977,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
             }
             seen_local.insert(vr, partial);
             versions.insert(vr.first, vr.second);
-            if (partial) w.partials.emplace_back(vr.first, *partial);
+            if (partial) w.partials.emplace_back(vr.first, std::move(*partial));
         }
     }
     if (versions.empty()) return;
@@ -992,8 +995,8 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::
         w.err = "UNIQUE constraint failed: __corro_bookkeeping_gaps.start";
         return;
     }
-    for (auto &[version, pv] : w.partials) {
-        const corro::PartialVersion &p = w.next.insert_partial(version, pv);
+    for (auto &[version, pv] : w.partials) {  // (w.partials is done with: moved into the snapshot)
+        const corro::PartialVersion &p = w.next.insert_partial(version, std::move(pv));
         if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
     }
 }
@@ -1080,7 +1083,7 @@ int gaps_batch(corro_ctx *ctx, std::vector<ActorWork> &work) {
                                   w.next.partials.upper_bound(out.rm_end[rb + k]));
         w.has_next = true;
         for (auto &[version, pv] : w.partials) {
-            const corro::PartialVersion &p = w.next.insert_partial(version, pv);
+            const corro::PartialVersion &p = w.next.insert_partial(version, std::move(pv));
             if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
         }
     }, 16);

@@ -92,14 +92,15 @@ struct Booked {
     }
 
     // insert_partial (agent.rs:1414-1432)
-    const PartialVersion &insert_partial(uint64_t version, const PartialVersion &p) {
+    // (by value: a caller done with its PartialVersion moves it in, no copy of its ranges)
+    const PartialVersion &insert_partial(uint64_t version, PartialVersion p) {
         auto it = partials.find(version);
         if (it == partials.end()) {
             if (!has_max || version > max) {
                 max = version;
                 has_max = true;
             }
-            return partials.emplace(version, p).first->second;
+            return partials.emplace_hint(it, version, std::move(p))->second;
         }
         for (const auto &r : p.seqs.ranges()) it->second.seqs.insert(r.first, r.second);
         return it->second;

@@ -382,8 +382,10 @@ static int ctx_prepare_device(corro_ctx *ctx) {
     CORRO_HIP_TRY(hipHostMalloc((void **)&ctx->h_misc, MISC_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     for (auto &e : ctx->ev) CORRO_HIP_TRY(hipEventCreate(&e));
     const size_t lds_max = 160 * 1024;
-    CORRO_HIP_TRY(hipFuncSetAttribute((const void *)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
+    for (const void *f : {(const void *)k_hist<8>, (const void *)k_hist<16>, (const void *)k_hist<32>})
+        CORRO_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
     for (const void *f : {(const void *)k_scatter<true, true>, (const void *)k_scatter<true, false>,
+                          (const void *)k_scatter<true, false, 8>,
                           (const void *)k_scatter<false, true>, (const void *)k_scatter<false, false>})
         CORRO_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
     return CORRO_OK;
@@ -812,7 +814,10 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     for (int k = 0; k < 6; k++) ctx->last_ms[k] = 0.f;
     mark(0);
     const uint32_t one_table = ctx->tables.size() == 1 ? 1u : 0u;
-    hipLaunchKernelGGL(k_hist, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B, one_table,
+    // changes per lane in flight (CORRO_HIST_U: A/B knob)
+    static const int hist_u = std::getenv("CORRO_HIST_U") ? std::atoi(std::getenv("CORRO_HIST_U")) : 16;
+    auto hk = hist_u == 8 ? k_hist<8> : hist_u == 32 ? k_hist<32> : k_hist<16>;
+    hipLaunchKernelGGL(hk, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B, one_table,
                        ctx->d_hist.as<uint32_t>(), z);
     CORRO_HIP_TRY(hipGetLastError());
     mark(1);
@@ -826,7 +831,8 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
         static const bool nt_stores = std::getenv("CORRO_HIP_NT") && std::atoi(std::getenv("CORRO_HIP_NT")) != 0;
         const bool plain = !bd.v1 && !bd.vt && !bd.vl && !bd.conv;
         if (bd.ts_v1 && !plain) return fail(CORRO_E_INVALID, "internal: ts_v1 on a batch with value words");
-        auto kern = plain ? (nt_stores ? k_scatter<true, true> : k_scatter<true, false>)
+        static const bool scat8 = std::getenv("CORRO_SCAT_U") && std::atoi(std::getenv("CORRO_SCAT_U")) == 8;  // A/B knob
+        auto kern = plain ? (nt_stores ? k_scatter<true, true> : scat8 ? k_scatter<true, false, 8> : k_scatter<true, false>)
                           : (nt_stores ? k_scatter<false, true> : k_scatter<false, false>);
         hipLaunchKernelGGL(kern, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4 + ((B + 31) / 32) * 4, s, bd,
                            tile, log2B, one_table, ctx->d_hist.as<uint32_t>(), ctx->d_stage_off.as<uint32_t>(),

@@ -209,6 +209,7 @@ struct ApplyZero {
     unsigned long long *misc, *dbv_batch;
     uint32_t nbflags, nmisc, nsites;
 };
+template <int HIST_U>
 static __global__ void __launch_bounds__(HIST_THREADS)
 k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t *__restrict__ hist_out, ApplyZero z) {
     extern __shared__ uint32_t hist[];
@@ -223,10 +224,9 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t 
     __syncthreads();
     const uint32_t begin = blockIdx.x * tile;
     const uint32_t end = min(in.n, begin + tile);
-    // HIST_U changes per lane in flight: one CU holds a single 128-KB-LDS workgroup, so memory
-    // level parallelism has to come from each lane. Loads are unconditional (clamped index) so
-    // that all of them are issued before the first wait.
-    constexpr int HIST_U = 8;
+    // HIST_U changes per lane in flight: one CU holds a single 128-KB-LDS workgroup (8 waves), so
+    // memory level parallelism has to come from each lane. Loads are unconditional (clamped index)
+    // so that all of them are issued before the first wait.
     for (uint32_t base = begin; base < end; base += blockDim.x * HIST_U) {
         uint64_t pk[HIST_U];
         uint32_t tc[HIST_U], ap[HIST_U];
@@ -413,7 +413,7 @@ __device__ inline unsigned long long wave_max_u64(unsigned long long x) {
 // "general" bits (a change with cl != 1 or a sentinel), crsql_db_versions maxima and validation.
 // PLAIN: the batch has no val1/val_type/val_len arrays (INTEGER values) -- loads are unconditional
 // (clamped) so all of an iteration's loads are in flight together. NT: non-temporal record stores.
-template <bool PLAIN, bool NT>
+template <bool PLAIN, bool NT, int SCAT_U = 4>
 static __global__ void __launch_bounds__(HIST_THREADS)
 k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const uint32_t *__restrict__ hist_off,
           const uint32_t *__restrict__ stage_off, Rec *__restrict__ stage, uint32_t *__restrict__ bflags,
@@ -437,7 +437,6 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
     unsigned long long run_max = 0;
     // SCAT_U changes per lane: all their loads are issued before any is consumed (one 132-KB-LDS
     // workgroup per CU, so memory-level parallelism must come from each lane)
-    constexpr int SCAT_U = 4;
     // (tiles start at multiples of 2 * blockDim.x, so pairs (2t, 2t+1) are 16-B aligned)
     // the PLAIN path needs an even tile length (pairs never straddle the tile end)
     const bool plain = PLAIN && ((end - begin) & 1u) == 0;
