@@ -447,13 +447,16 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
         if (stage) stage(n);
     };
     const size_t ntables = committed.size();
-    struct Sub {  // one key's share of one staged INSERT batch
+    struct Sub {  // one key's share of one staged INSERT batch (the item's fields copied in: the
+                  // passes below walk the subs in key order without chasing pointers)
         BufKey key;
         uint64_t call;
-        const StagedBuf *it;
         Staged *st;
         uint64_t a, b;  // (host) rows [a, b) of st->buffered, all of this key
         uint64_t fr;    // (dev, fetched) first row in the fetched rows
+        uint64_t src, ts;  // (dev) the item's input span start and ts
+        uint32_t seq0, n;  // (dev) its first seq and change count
+        bool dev;
     };
     bool any_items = false;
     for (Staged *st : order) any_items |= !st->items.empty();
@@ -469,13 +472,13 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
         const std::vector<HostRow> &rows = st->buffered;
         for (const StagedBuf &it : st->items) {
             if (it.dev) {
-                v.push_back(Sub{{it.site, it.dbv}, call++, &it, st, 0, 0, 0});
+                v.push_back(Sub{{it.site, it.dbv}, call++, st, 0, 0, 0, it.src, it.ts, it.seq0, it.n, true});
                 continue;
             }
             for (uint64_t a = it.a; a < it.b;) {
                 uint64_t b = a + 1;
                 while (b < it.b && rows[b].site == rows[a].site && rows[b].dbv == rows[a].dbv) b++;
-                v.push_back(Sub{{rows[a].site, rows[a].dbv}, call++, &it, st, a, b, 0});
+                v.push_back(Sub{{rows[a].site, rows[a].dbv}, call++, st, a, b, 0, 0, 0, 0, 0, false});
                 for (uint64_t k = a; k < b; k++)
                     if ((rows[k].tcid >> 16) < ntables) ptab[ai][rows[k].tcid >> 16]++;
                 a = b;
@@ -491,14 +494,16 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     for (size_t ai = 0; ai < per.size(); ai++)
         if (!per[ai].empty()) blk.push_back(ai);
     std::sort(blk.begin(), blk.end(), [&](size_t x, size_t y) { return per[x][0].key < per[y][0].key; });
-    std::vector<Sub *> sp;  // every sub in (key, call) order
+    std::vector<Sub> sp;  // every sub in (key, call) order, contiguous
     size_t nsub = 0;
     for (size_t ai : blk) nsub += per[ai].size();
     if (!nsub) return CORRO_OK;
     sp.reserve(nsub);
-    for (size_t ai : blk)
-        for (Sub &u : per[ai]) sp.push_back(&u);
-    auto sless = [](const Sub *x, const Sub *y) { return x->key < y->key || (x->key == y->key && x->call < y->call); };
+    for (size_t ai : blk) {
+        sp.insert(sp.end(), per[ai].begin(), per[ai].end());
+        std::vector<Sub>().swap(per[ai]);
+    }
+    auto sless = [](const Sub &x, const Sub &y) { return x.key < y.key || (x.key == y.key && x.call < y.call); };
     if (!std::is_sorted(sp.begin(), sp.end(), sless)) std::sort(sp.begin(), sp.end(), sless);
     const bool pool_ok = dv && (bk->pool ? corro::bufpool_usable(ctx, bk->pool) : true);
     // per key group: host at the end of the call (it holds host rows, or receives some, or there is no
@@ -506,27 +511,34 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     // fetched from the batch.
     std::vector<std::pair<size_t, size_t>> groups;
     std::vector<uint8_t> ghost;
+    std::vector<BufEntry *> gent;  // the key's entry before this call (null: a new key)
     std::vector<corro::AgentSpan> fsp, all_dev;
+    all_dev.reserve(sp.size());
+    groups.reserve(sp.size());
+    ghost.reserve(sp.size());
+    gent.reserve(sp.size());
     uint64_t fr_n = 0;
+    const bool any_buffered = bk->buffered.slots() != 0;
     for (size_t g0 = 0; g0 < sp.size();) {
         size_t g1 = g0 + 1;
-        while (g1 < sp.size() && sp[g1]->key == sp[g0]->key) g1++;
-        BufEntry *e = bk->buffered.find(sp[g0]->key);
+        while (g1 < sp.size() && sp[g1].key == sp[g0].key) g1++;
+        BufEntry *e = any_buffered ? bk->buffered.find(sp[g0].key) : nullptr;
         bool host = !pool_ok || (e && !e->rows.empty());
-        for (size_t q = g0; q < g1 && !host; q++) host = !sp[q]->it->dev;
+        for (size_t q = g0; q < g1 && !host; q++) host = !sp[q].dev;
         if (host && e) TRY_RC(materialize(bk, *e));
         for (size_t q = g0; q < g1; q++) {
-            Sub &u = *sp[q];
-            if (!u.it->dev) continue;
-            all_dev.push_back({u.it->src, 0, u.it->n, u.it->ts});
+            Sub &u = sp[q];
+            if (!u.dev) continue;
+            all_dev.push_back({u.src, 0, u.n, u.ts});
             if (host) {
                 u.fr = fr_n;
-                fsp.push_back({u.it->src, fr_n, u.it->n, u.it->ts});
-                fr_n += u.it->n;
+                fsp.push_back({u.src, fr_n, u.n, u.ts});
+                fr_n += u.n;
             }
         }
         groups.emplace_back(g0, g1);
         ghost.push_back(host);
+        gent.push_back(e);
         g0 = g1;
     }
     mark("cb_groups");
@@ -546,25 +558,24 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     jobs.reserve(all_dev.size());
     add.reserve(groups.size());
     for (size_t gi = 0; gi < groups.size(); gi++) {
-        const BufKey key = sp[groups[gi].first]->key;
+        const BufKey key = sp[groups[gi].first].key;
         BufEntry local;
-        BufEntry *e = bk->buffered.find(key);
+        BufEntry *e = gent[gi];  // (materialize keeps the entry where it is)
         const bool fresh = !e;
         if (fresh) e = &local;
         for (size_t q = groups[gi].first; q < groups[gi].second; q++) {
-            const Sub &u = *sp[q];
-            const StagedBuf &it = *u.it;
-            if (!it.dev) {
+            const Sub &u = sp[q];
+            if (!u.dev) {
                 buf_insert(e->rows, u.st->buffered.data() + u.a, u.st->buffered.data() + u.b);
             } else if (ghost[gi]) {
-                std::vector<HostRow> hr(it.n);
-                for (uint64_t j = 0; j < it.n; j++) {
+                std::vector<HostRow> hr(u.n);
+                for (uint64_t j = 0; j < u.n; j++) {
                     const uint64_t x = u.fr + j;
                     HostRow &h = hr[j];
                     h.pk = fr.pk[x];
                     h.v0 = fr.v0[x];
                     h.v1 = fr.v1[x];
-                    h.ts = dv->ts ? fr.ts[x] : it.ts;
+                    h.ts = dv->ts ? fr.ts[x] : u.ts;
                     h.cv = fr.cv[x];
                     h.dbv = fr.dbv[x];
                     h.tcid = fr.tcid[x];
@@ -576,10 +587,10 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
                 }
                 buf_insert(e->rows, hr.data(), hr.data() + hr.size());
             } else {
-                seq_pieces(e->segs, it.seq0, (uint64_t)it.seq0 + it.n - 1, pieces);
+                seq_pieces(e->segs, u.seq0, (uint64_t)u.seq0 + u.n - 1, pieces);
                 for (const Range &r : pieces) {
                     const PoolSeg g{SEG_PENDING | jobs.size(), (uint32_t)r.first, (uint32_t)(r.second - r.first + 1)};
-                    jobs.push_back({it.src + (r.first - it.seq0), r.second - r.first + 1, it.ts, 0});
+                    jobs.push_back({u.src + (r.first - u.seq0), r.second - r.first + 1, u.ts, 0});
                     e->segs.insert_sorted(g);
                 }
             }
@@ -893,13 +904,23 @@ struct CsView {
 // is fast, plus the versions of the runs given (decided elsewhere: a fast actor's, or the device's
 // isolated changesets, which share no version with w.idx), then its gap snapshot (:894-932) and
 // partials.
+// (the version runs an actor's changesets decided elsewhere add -- device decisions: columns of the
+// header result; host fast path: Range pairs)
+struct RunView {
+    const uint64_t *s = nullptr, *e = nullptr;
+    const Range *r = nullptr;
+    size_t n = 0;
+};
 template <class RowOf>
-void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const std::vector<Range> &fast_runs, RowOf &&row_of) {
+void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunView &fast_runs, RowOf &&row_of) {
     corro::Booked &booked = *w.booked;
     const bool had_max = w.had_max;
     const uint64_t max = w.max;
     RangeSet versions;
-    for (const Range &r : fast_runs) versions.insert(r.first, r.second);
+    for (size_t k = 0; k < fast_runs.n; k++) {
+        if (fast_runs.r) versions.insert(fast_runs.r[k].first, fast_runs.r[k].second);
+        else versions.insert(fast_runs.s[k], fast_runs.e[k]);
+    }
     if (!w.fast) {
         // pass 1: batch-local dedup of (versions, seqs), then versions the actor already holds
         std::vector<uint64_t> unknown;
@@ -1206,9 +1227,16 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             r.lv.assign(reinterpret_cast<const char *>(inc.lv_data.data() + inc.lv_off[j]), inc.lv_len[j]);
         return r;
     };
-    std::vector<std::vector<Range>> dev_runs(work.size());
-    for (size_t r = 0; r < R.run_site.size(); r++)
-        dev_runs[(size_t)work_of[R.run_site[r]]].emplace_back(R.run_start[r], R.run_end[r]);
+    // (R's runs are grouped by site: each actor's are one slice of the columns)
+    std::vector<RunView> dev_runs(work.size());
+    for (size_t r = 0; r < R.run_site.size();) {
+        size_t q = r + 1;
+        while (q < R.run_site.size() && R.run_site[q] == R.run_site[r]) q++;
+        RunView &rv = dev_runs[(size_t)work_of[R.run_site[r]]];
+        if (rv.n) throw std::logic_error("device runs not grouped by site");
+        rv = RunView{R.run_start.data() + r, R.run_end.data() + r, nullptr, q - r};
+        r = q;
+    }
     const CsView view{hcs, R.hbad, hknown.data(), hflag.data(), canon};
     if (want_gaps_batch(work))
         for (ActorWork &w : work) w.defer_gaps = true;
@@ -1624,7 +1652,9 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
     for (size_t k = 0; k < nchunk; k++)
         for (auto &[wi, r] : cout[k].runs) fast_runs[wi].push_back(r);
     const CsView view{cs, bad, out->known, P.flag, nullptr};
-    auto run_actor = [&](size_t wi) { run_actor_walk(bk, work[wi], view, fast_runs[wi], row_of); };
+    auto run_actor = [&](size_t wi) {
+        run_actor_walk(bk, work[wi], view, RunView{nullptr, nullptr, fast_runs[wi].data(), fast_runs[wi].size()}, row_of);
+    };
     if (want_gaps_batch(work))
         for (ActorWork &w : work) w.defer_gaps = true;
     run_parallel(work.size(), [&](size_t k) { run_actor(k); });
