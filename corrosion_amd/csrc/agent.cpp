@@ -465,6 +465,7 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     // the actors' blocks concatenated by first key are globally sorted unless two actors share a key
     std::vector<std::vector<Sub>> per(order.size());
     std::vector<std::vector<uint64_t>> ptab(order.size(), std::vector<uint64_t>(ntables, 0));
+    std::vector<uint8_t> host_rows(order.size(), 0);  // the actor staged host rows
     run_parallel(order.size(), [&](size_t ai) {
         Staged *st = order[ai];
         std::vector<Sub> &v = per[ai];
@@ -479,6 +480,7 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
                 uint64_t b = a + 1;
                 while (b < it.b && rows[b].site == rows[a].site && rows[b].dbv == rows[a].dbv) b++;
                 v.push_back(Sub{{rows[a].site, rows[a].dbv}, call++, st, a, b, 0, 0, 0, 0, 0, false});
+                host_rows[ai] = 1;
                 for (uint64_t k = a; k < b; k++)
                     if ((rows[k].tcid >> 16) < ntables) ptab[ai][rows[k].tcid >> 16]++;
                 a = b;
@@ -494,6 +496,95 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     for (size_t ai = 0; ai < per.size(); ai++)
         if (!per[ai].empty()) blk.push_back(ai);
     std::sort(blk.begin(), blk.end(), [&](size_t x, size_t y) { return per[x][0].key < per[y][0].key; });
+    const bool pool_ok = dv && (bk->pool ? corro::bufpool_usable(ctx, bk->pool) : true);
+    const bool any_buffered = bk->buffered.slots() != 0;
+    std::vector<corro::PoolCopy> jobs;
+    std::vector<std::pair<BufKey, BufEntry>> add;
+    // Fast path -- the common shape: every sub a canonical device changeset, the actors' key ranges
+    // disjoint (each actor's keys carry its own site) and no key holding host rows. Then no group is
+    // host, nothing is fetched or materialized, and each actor's groups, segment trims and copy jobs
+    // are built in parallel (pending segment offsets name (actor, local job)), concatenated in key
+    // order afterwards.
+    bool fast = pool_ok && !blk.empty();
+    for (size_t k = 0; k < blk.size() && fast; k++) {
+        fast = !host_rows[blk[k]];
+        if (fast && k + 1 < blk.size()) fast = per[blk[k]].back().key < per[blk[k + 1]][0].key;
+    }
+    if (fast && any_buffered) {  // (read-only check: a key of this call that holds host rows)
+        std::vector<uint8_t> hostkey(blk.size(), 0);
+        run_parallel(blk.size(), [&](size_t k) {
+            const std::vector<Sub> &v = per[blk[k]];
+            for (size_t q = 0; q < v.size(); q++) {
+                if (q && v[q].key == v[q - 1].key) continue;
+                const BufEntry *e = bk->buffered.find(v[q].key);
+                if (e && !e->rows.empty()) {
+                    hostkey[k] = 1;
+                    return;
+                }
+            }
+        });
+        for (uint8_t h : hostkey) fast = fast && !h;
+    }
+    std::vector<size_t> jbase;  // fast path: first global job of each block
+    if (fast) {
+        struct Out {
+            std::vector<corro::AgentSpan> dev;
+            std::vector<corro::PoolCopy> jobs;
+            std::vector<std::pair<BufKey, BufEntry>> add;
+        };
+        std::vector<Out> outs(blk.size());
+        run_parallel(blk.size(), [&](size_t k) {
+            const std::vector<Sub> &v = per[blk[k]];
+            Out &o = outs[k];
+            o.dev.reserve(v.size());
+            std::vector<Range> pieces;
+            for (size_t g0 = 0; g0 < v.size();) {
+                size_t g1 = g0 + 1;
+                while (g1 < v.size() && v[g1].key == v[g0].key) g1++;
+                BufEntry local;
+                BufEntry *e = any_buffered ? bk->buffered.find(v[g0].key) : nullptr;  // (keys of this block only)
+                const bool fresh = !e;
+                if (fresh) e = &local;
+                for (size_t q = g0; q < g1; q++) {
+                    const Sub &u = v[q];
+                    o.dev.push_back({u.src, 0, u.n, u.ts});
+                    seq_pieces(e->segs, u.seq0, (uint64_t)u.seq0 + u.n - 1, pieces);
+                    for (const Range &r : pieces) {
+                        const PoolSeg g{SEG_PENDING | ((uint64_t)k << 32) | o.jobs.size(), (uint32_t)r.first,
+                                        (uint32_t)(r.second - r.first + 1)};
+                        o.jobs.push_back({u.src + (r.first - u.seq0), r.second - r.first + 1, u.ts, 0});
+                        e->segs.insert_sorted(g);
+                    }
+                }
+                if (fresh && !local.empty()) o.add.emplace_back(v[g0].key, std::move(local));
+                g0 = g1;
+            }
+        });
+        mark("cb_groups");
+        std::vector<corro::AgentSpan> all_dev;
+        size_t nd = 0, nj = 0, na = 0;
+        for (const Out &o : outs) {
+            nd += o.dev.size();
+            nj += o.jobs.size();
+            na += o.add.size();
+        }
+        all_dev.reserve(nd);
+        jobs.reserve(nj);
+        add.reserve(na);
+        jbase.resize(blk.size());
+        for (size_t k = 0; k < outs.size(); k++) {
+            all_dev.insert(all_dev.end(), outs[k].dev.begin(), outs[k].dev.end());
+            jbase[k] = jobs.size();
+            jobs.insert(jobs.end(), outs[k].jobs.begin(), outs[k].jobs.end());
+            for (auto &x : outs[k].add) add.push_back(std::move(x));
+        }
+        std::vector<uint64_t> tc;
+        TRY_RC(corro::agent_dev_table_counts(ctx, dv, all_dev, (uint32_t)ntables, tc));
+        for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
+        mark("cb_tables");
+        if (!bk->pool) bk->pool = corro::bufpool_new();
+        mark("cb_trim");
+    } else {
     std::vector<Sub> sp;  // every sub in (key, call) order, contiguous
     size_t nsub = 0;
     for (size_t ai : blk) nsub += per[ai].size();
@@ -505,7 +596,6 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     }
     auto sless = [](const Sub &x, const Sub &y) { return x.key < y.key || (x.key == y.key && x.call < y.call); };
     if (!std::is_sorted(sp.begin(), sp.end(), sless)) std::sort(sp.begin(), sp.end(), sless);
-    const bool pool_ok = dv && (bk->pool ? corro::bufpool_usable(ctx, bk->pool) : true);
     // per key group: host at the end of the call (it holds host rows, or receives some, or there is no
     // pool for it)? Its device segments come to the host first; its canonical changesets' rows are
     // fetched from the batch.
@@ -518,7 +608,6 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     ghost.reserve(sp.size());
     gent.reserve(sp.size());
     uint64_t fr_n = 0;
-    const bool any_buffered = bk->buffered.slots() != 0;
     for (size_t g0 = 0; g0 < sp.size();) {
         size_t g1 = g0 + 1;
         while (g1 < sp.size() && sp[g1].key == sp[g0].key) g1++;
@@ -552,8 +641,6 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     }
     mark("cb_tables");
     if (!all_dev.empty() && pool_ok && !bk->pool) bk->pool = corro::bufpool_new();
-    std::vector<corro::PoolCopy> jobs;
-    std::vector<std::pair<BufKey, BufEntry>> add;
     std::vector<Range> pieces;
     jobs.reserve(all_dev.size());
     add.reserve(groups.size());
@@ -598,6 +685,7 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
         if (fresh && !local.empty()) add.emplace_back(key, std::move(local));
     }
     mark("cb_trim");
+    }  // (serial path)
     bk->buffered.merge(std::move(add));
     mark("cb_merge");
     if (jobs.empty()) return CORRO_OK;
@@ -619,9 +707,14 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     mark("cb_reserve");
     TRY_RC(corro::bufpool_append(ctx, bk->pool, dv, jobs));
     mark("cb_append");
-    for (size_t i = 0; i < bk->buffered.slots(); i++)  // (one sequential pass: no per-key searches)
+    // (one sequential pass: no per-key searches; a pending offset names (block, job) on the fast
+    // path, the global job on the serial one)
+    for (size_t i = 0; i < bk->buffered.slots(); i++)
         for (PoolSeg &g : bk->buffered.at(i).val.segs)
-            if (g.off & SEG_PENDING) g.off = jobs[g.off & ~SEG_PENDING].dst;
+            if (g.off & SEG_PENDING) {
+                const uint64_t x = g.off & ~SEG_PENDING;
+                g.off = jobs[fast ? jbase[x >> 32] + (x & 0xFFFFFFFFULL) : x].dst;
+            }
     mark("cb_fix");
     return CORRO_OK;
 }
