@@ -926,22 +926,29 @@ namespace {
 // RangeInclusiveMap<Version, Option<PartialVersion>> of the versions one actor has seen in this
 // call (util.rs:762-807): covered versions plus, per version whose latest entry is a partial, that
 // PartialVersion (a later entry over the version replaces it).
+// (a partial is held by index into the actor's partial list, which keeps every one in walk order: no
+// copy of its seq ranges)
 struct SeenMap {
+    using Parts = std::vector<std::pair<uint64_t, corro::PartialVersion>>;
+    explicit SeenMap(const Parts &parts) : parts_(parts) {}
     RangeSet covered;
-    std::map<uint64_t, corro::PartialVersion> partial_at;
-    void insert(const Range &v, const std::optional<corro::PartialVersion> &p) {
+    std::map<uint64_t, size_t> partial_at;
+    void insert(const Range &v, size_t part = SIZE_MAX) {  // part: index in parts, SIZE_MAX = none
         covered.insert(v.first, v.second);
         if (!partial_at.empty()) partial_at.erase(partial_at.lower_bound(v.first), partial_at.upper_bound(v.second));
-        if (p) partial_at[v.first] = *p;
+        if (part != SIZE_MAX) partial_at[v.first] = part;
     }
     // every version of v seen, and (with seqs) each seen partial holding the seqs
     bool all_seen(const Range &v, const Range *seqs) const {
         if (!covered.contains_range(v.first, v.second)) return false;
         if (!seqs || partial_at.empty()) return true;
         for (auto it = partial_at.lower_bound(v.first); it != partial_at.end() && it->first <= v.second; ++it)
-            if (!it->second.seqs.contains_range(seqs->first, seqs->second)) return false;
+            if (!parts_[it->second].second.seqs.contains_range(seqs->first, seqs->second)) return false;
         return true;
     }
+
+  private:
+    const Parts &parts_;
 };
 
 // One actor's share of a process_multiple_changes call. Actors are independent (util.rs:765-884
@@ -1053,7 +1060,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
             unknown.push_back(i);
         }
         // pass 2 (the bookie is not written until the call commits, so pass 1's contains_all stands)
-        SeenMap seen_local;
+        SeenMap seen_local(w.partials);
         for (uint64_t i : unknown) {
             const corro_changeset &c = v.cs[i];
             const Range vr = versions_of(c);
@@ -1089,9 +1096,9 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
                     v.known[i] = CORRO_KNOWN_PARTIAL;
                 }
             }
-            seen_local.insert(vr, partial);
-            versions.insert(vr.first, vr.second);
             if (partial) w.partials.emplace_back(vr.first, std::move(*partial));
+            seen_local.insert(vr, partial ? w.partials.size() - 1 : SIZE_MAX);
+            versions.insert(vr.first, vr.second);
         }
     }
     if (versions.empty()) return;
