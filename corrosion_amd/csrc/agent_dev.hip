@@ -310,6 +310,85 @@ __global__ void __launch_bounds__(AG_T) k_imp_reduce(const unsigned long long *_
     }
 }
 
+// Position mode: the impactful flags streamed along the positions (no span staging): src_of gives
+// each position's input index and whether it heads its span (a version's first change), so a lane
+// needs only imp[p], src_of[p] and, for a hit, its table. Hits are stored into the zeroed output
+// (out[src] = 1) and into a per-position byte map for k_span_any; table counts per (workgroup,
+// table) in LDS (global atomics past IMP_TLDS tables).
+constexpr uint32_t IP_U = 8;      // positions per lane per iteration
+constexpr uint32_t IP_GRID = 2048;
+__global__ void __launch_bounds__(AG_T) k_imp_pos(const uint8_t *__restrict__ imp, const uint32_t *__restrict__ src_of,
+                                                  const uint32_t *__restrict__ tcid, uint64_t nbatch,
+                                                  const unsigned long long *first_p, uint8_t *__restrict__ out,
+                                                  uint8_t *__restrict__ hitp, unsigned long long *committed,
+                                                  unsigned long long *part, uint32_t ntables) {
+    __shared__ uint32_t l_cnt[IMP_TLDS];
+    if (threadIdx.x < IMP_TLDS) l_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned long long first = *first_p;
+    const bool lds_t = ntables <= IMP_TLDS;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t step = (uint64_t)gridDim.x * AG_T * IP_U;
+    for (uint64_t base = (uint64_t)blockIdx.x * AG_T * IP_U; base < nbatch; base += step) {
+        uint32_t sv[IP_U];
+        uint8_t im[IP_U];
+#pragma unroll
+        for (uint32_t u = 0; u < IP_U; u++) {
+            const uint64_t p = base + u * AG_T + threadIdx.x;
+            const uint64_t pc = p < nbatch ? p : nbatch - 1;
+            sv[u] = src_of[pc];
+            im[u] = imp[pc];
+        }
+        uint32_t tb[IP_U];
+        bool hit[IP_U];
+#pragma unroll
+        for (uint32_t u = 0; u < IP_U; u++) {
+            const uint64_t p = base + u * AG_T + threadIdx.x;
+            hit[u] = p < nbatch && ((sv[u] >> 31) ? first <= p : im[u] != 0);
+            tb[u] = hit[u] ? tcid[sv[u] & 0x7FFFFFFFu] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < IP_U; u++) {
+            const uint64_t p = base + u * AG_T + threadIdx.x;
+            if (hit[u]) {
+                if (out) out[sv[u] & 0x7FFFFFFFu] = 1;
+                hitp[p] = 1;
+            }
+            uint32_t t_ = hit[u] ? tb[u] >> 16 : 0xFFFFFFFFu;
+            if (t_ >= ntables) t_ = 0xFFFFFFFFu;
+            unsigned long long m = __ballot(t_ != 0xFFFFFFFFu);
+            while (m) {
+                const uint32_t leader = (uint32_t)__ffsll(m) - 1;
+                const uint32_t tl = __shfl(t_, leader);
+                const unsigned long long mt = __ballot(t_ == tl);
+                if (lane == leader) {
+                    if (lds_t) atomicAdd(&l_cnt[tl], (uint32_t)__popcll(mt));
+                    else atomicAdd(&committed[tl], (unsigned long long)__popcll(mt));
+                }
+                m &= ~mt;
+                if (t_ == tl) t_ = 0xFFFFFFFFu;
+            }
+        }
+    }
+    __syncthreads();
+    if (lds_t && threadIdx.x < ntables) part[(uint64_t)blockIdx.x * ntables + threadIdx.x] = l_cnt[threadIdx.x];
+}
+
+// any[cs of span j] = 1 when a position of span j was a hit (k_imp_pos's byte map)
+__global__ void __launch_bounds__(AG_T) k_span_any(const uint8_t *__restrict__ hitp, const uint64_t *__restrict__ s_dst,
+                                                   const uint64_t *__restrict__ s_cnt, const uint32_t *__restrict__ s_cs,
+                                                   uint64_t nspans, uint8_t *__restrict__ any) {
+    for (uint64_t j = (uint64_t)blockIdx.x * AG_T + threadIdx.x; j < nspans; j += (uint64_t)gridDim.x * AG_T) {
+        const uint64_t d = s_dst[j], e = d + s_cnt[j];
+        uint32_t acc = 0;
+        uint64_t q = d;
+        for (; q < e && (q & 3); q++) acc |= hitp[q];
+        for (; q + 4 <= e && !acc; q += 4) acc |= *reinterpret_cast<const uint32_t *>(hitp + q);
+        for (; q < e && !acc; q++) acc |= hitp[q];
+        if (acc) any[s_cs[j]] = 1;
+    }
+}
+
 // Application order of the applied changesets: key = site rank (ActorId byte order) for an applied
 // changeset, past every rank otherwise; value = arrival index. A stable radix sort keeps arrival
 // order inside an actor.
@@ -461,8 +540,9 @@ int gather_dev(corro_ctx *ctx, const corro_changes *dv, const uint64_t *src, con
     return CORRO_OK;
 }
 
-// position mode: ap[src] = p, src_of[p] = src and, when wanted, the ts of application position p (the
-// input's per-change ts, else the changeset's), positions along the workgroup's spans
+// position mode: ap[src] = p, src_of[p] = src | (first position of its span) << 31 and, when wanted,
+// the ts of application position p (the input's per-change ts, else the changeset's), positions along
+// the workgroup's spans (position mode takes inputs of < 2^31 changes)
 __global__ void __launch_bounds__(AG_T) k_span_pos(const uint32_t *__restrict__ first_span, const uint64_t *__restrict__ s_src,
                                                     const uint64_t *__restrict__ s_dst, const uint64_t *__restrict__ s_ts,
                                                     uint64_t nspans, uint64_t nbatch, const uint64_t *__restrict__ in_ts,
@@ -477,13 +557,14 @@ __global__ void __launch_bounds__(AG_T) k_span_pos(const uint32_t *__restrict__ 
     fill_pspan(l_dst, t, pspan);
     // spans from LDS for all of the lane's positions, then every ts load in flight, then the stores
     uint64_t src[SP_PER], tv[SP_PER];
-    uint32_t kk[SP_PER];
+    uint32_t kk[SP_PER], hd[SP_PER];
 #pragma unroll
     for (uint32_t u = 0; u < SP_PER; u++) {
         const uint32_t r = u * AG_T + threadIdx.x;
         const uint32_t k = t.p0 + r < t.p1 ? pspan[r] : 0u;
         kk[u] = k;
         src[u] = l_src[k] + (r - l_dst[k]);
+        hd[u] = (r == l_dst[k] && (k > 0 || t.head0)) ? 0x80000000u : 0u;
     }
 #pragma unroll
     for (uint32_t u = 0; u < SP_PER; u++) {
@@ -495,7 +576,7 @@ __global__ void __launch_bounds__(AG_T) k_span_pos(const uint32_t *__restrict__ 
         const uint64_t p = t.p0 + u * AG_T + threadIdx.x;
         if (p >= t.p1) continue;
         ap[src[u]] = (uint32_t)p;
-        src_of[p] = (uint32_t)src[u];
+        src_of[p] = (uint32_t)src[u] | hd[u];
         if (ts_out) ts_out[p] = tv[u];
     }
 }
@@ -654,6 +735,7 @@ int spans_to_batch(corro_ctx *ctx, const corro_changes *dv, uint64_t nspans, uin
                    corro_changes *batch, bool *gathered, AgentPositions *pm) {
     *gathered = false;
     if (pm) *pm = AgentPositions{};
+    ctx->agent_src_of = nullptr;
     hipStream_t s = ctx->stream;
     const DevCols c = dev_cols(ctx);
     if (nspans) {
@@ -691,7 +773,8 @@ int spans_to_batch(corro_ctx *ctx, const corro_changes *dv, uint64_t nspans, uin
     // alignment of device batches)
     auto aligned = [](const void *q, uintptr_t a) { return !q || ((uintptr_t)q % a) == 0; };
     const char *fg = std::getenv("CORRO_AGENT_GATHER");  // tests: force the gather path
-    if (pm && nspans && !(fg && fg[0] == '1') && dv->n <= corro_detail_chunk_changes(ctx) && aligned(dv->pk, 16) && aligned(dv->col_version, 16) &&
+    if (pm && nspans && !(fg && fg[0] == '1') && dv->n <= corro_detail_chunk_changes(ctx) && dv->n < (1ULL << 31) &&
+        aligned(dv->pk, 16) && aligned(dv->col_version, 16) &&
         aligned(dv->db_version, 16) && aligned(dv->val0, 16) && aligned(dv->val1, 16) && aligned(dv->table_cid, 8) &&
         aligned(dv->cl, 8) && aligned(dv->seq, 8) && aligned(dv->site, 8)) {
         // per-position ts only from the changesets: an input with per-change ts is staged with them
@@ -707,6 +790,7 @@ int spans_to_batch(corro_ctx *ctx, const corro_changes *dv, uint64_t nspans, uin
                            c.s_dst, c.s_ts, nspans, nbatch, dv->ts, ap, src_of, ts);
         CORRO_HIP_TRY(hipGetLastError());
         *batch = *dv;
+        ctx->agent_src_of = src_of;
         pm->on = true;
         pm->ap = ap;
         pm->src = src_of;
@@ -765,10 +849,14 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
     if (ntables > 65536) return fail(CORRO_E_RANGE, "at most 65536 tables");
     const DevCols c = dev_cols(ctx);
     // scratch: first (8 B) | committed (8 per table) | host-mode impactful (nin) | per-workgroup table counts
-    const uint64_t nwg = (nbatch + SPB - 1) / SPB;
+    // position mode with span-head flags: the streamed pass (k_imp_pos + k_span_any)
+    const bool streamed = tcid_by_src && ctx->agent_src_of && !std::getenv("CORRO_IMP_SPANS");  // (env: A/B)
+    const uint64_t nwg = streamed ? std::max<uint64_t>(1, std::min<uint64_t>(IP_GRID, (nbatch + AG_T * IP_U - 1) / (AG_T * IP_U)))
+                                  : (nbatch + SPB - 1) / SPB;
     const size_t o_cm = 256, o_out = o_cm + 8 * 65536;
     const size_t o_part = o_out + (mem == CORRO_MEM_HOST && impactful ? al256(nin) : 0);
-    const size_t total = o_part + (ntables <= IMP_TLDS ? al256(nwg * ntables * 8) : 0);
+    const size_t o_hit = o_part + (ntables <= IMP_TLDS ? al256(nwg * ntables * 8) : 0);
+    const size_t total = o_hit + (streamed ? al256(nbatch) : 0);
     if (int rc = ctx->d_agent_out.ensure(total)) return rc;
     uint8_t *base = ctx->d_agent_out.as<uint8_t>();
     unsigned long long *first = reinterpret_cast<unsigned long long *>(base);
@@ -800,7 +888,17 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
         a.part = reinterpret_cast<unsigned long long *>(base + o_part);
         a.ntables = ntables;
         a.tcid_by_src = tcid_by_src;
-        hipLaunchKernelGGL(k_impactful, dim3((uint32_t)nwg), dim3(AG_T), 0, s, a);
+        if (streamed) {
+            uint8_t *hitp = base + o_hit;
+            CORRO_HIP_TRY(hipMemsetAsync(hitp, 0, nbatch, s));
+            hipLaunchKernelGGL(k_imp_pos, dim3((uint32_t)nwg), dim3(AG_T), 0, s, impact, ctx->agent_src_of, tcid, nbatch,
+                               first, out, hitp, a.committed, a.part, ntables);
+            CORRO_HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(k_span_any, flat_grid(nspans), dim3(AG_T), 0, s, hitp, c.s_dst, c.s_cnt, a.s_cs, nspans,
+                               c.any);
+        } else {
+            hipLaunchKernelGGL(k_impactful, dim3((uint32_t)nwg), dim3(AG_T), 0, s, a);
+        }
         CORRO_HIP_TRY(hipGetLastError());
         if (ntables && ntables <= IMP_TLDS) {
             hipLaunchKernelGGL(k_imp_reduce, dim3(ntables), dim3(AG_T), 0, s, a.part, nwg, ntables, a.committed);

@@ -758,7 +758,7 @@ static int stage_host_batch(corro_ctx *ctx, const corro_changes *in, BatchDev &b
 static __global__ void k_ts_by_pos(const uint64_t *__restrict__ in_ts, const uint32_t *__restrict__ src_of, uint64_t n,
                                    uint64_t *__restrict__ out) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x)
-        out[p] = in_ts[src_of[p]];
+        out[p] = in_ts[src_of[p] & 0x7FFFFFFFu];  // (bit 31: span head flag)
 }
 
 static int error_from_bits(uint64_t bits) {

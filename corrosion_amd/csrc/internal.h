@@ -215,6 +215,9 @@ struct corro_ctx {
     corro::DevBuf d_agent_fetch, d_agent_aux2;
     corro::DevBuf d_agent_hdr;    // device-header mode: per-changeset / per-site / run columns
     bool agent_sorted_mode = false;  // spans compacted from the site-rank sort (s_cs in the val column)
+    // position mode: input index of every application position, bit 31 = the first position of its
+    // span (k_span_pos; null when the call's batch is not in position mode)
+    const uint32_t *agent_src_of = nullptr;
     void *h_agent = nullptr;
     size_t h_agent_bytes = 0;
     void *h_hdr = nullptr;           // host ChangeV1 headers staged for the device header passes (pinned)

@@ -86,7 +86,8 @@ struct MergeArgs {
 };
 
 // input index of batch position p (position mode maps it, MergeArgs::pos_src)
-__device__ inline uint32_t batch_src(const MergeArgs &a, uint32_t p) { return a.pos_src ? a.pos_src[p] : p; }
+// (bit 31 of a position-mode entry marks the first position of its span, agent_dev.hip k_span_pos)
+__device__ inline uint32_t batch_src(const MergeArgs &a, uint32_t p) { return a.pos_src ? a.pos_src[p] & 0x7FFFFFFFu : p; }
 
 // misc words
 constexpr int MISC_ERR = 0, MISC_OVF = 1, MISC_LIVE = 2, MISC_WIDE = 3, MISC_GEN = 4, MISC_WIDEQ = 5,
