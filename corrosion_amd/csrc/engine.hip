@@ -1145,7 +1145,10 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
     // position-mode batch that brought its input's per-change ts gets them gathered into that order.
     static const bool no_ts_v1 = std::getenv("CORRO_TS_V1") && std::atoi(std::getenv("CORRO_TS_V1")) == 0;
     const bool plain = !bd.v1 && !bd.vt && !bd.vl && !bd.conv;
+    static const bool no_ts_pair = std::getenv("CORRO_TS_PAIR") && std::atoi(std::getenv("CORRO_TS_PAIR")) == 0;  // (A/B)
     bd.ts_v1 = bd.ts && plain && !no_ts_v1 ? 1u : 0u;
+    // (chunks start at multiples of the chunk size, a multiple of 1024 changes: alignment carries over)
+    if (bd.ts_v1 && !no_ts_pair && ((uintptr_t)bd.ts % 16) == 0) bd.ts_v1 |= 2u;
     if (bd.ap && bd.ts && !bd.ts_pos && !bd.ts_v1) {
         if (!ctx->pm_src) return fail(CORRO_E_INVALID, "internal: position mode without a position -> input map");
         TRY(ctx->d_pm_ts.ensure(ctx->pm_n * 8 + 8));

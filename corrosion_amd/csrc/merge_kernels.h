@@ -477,6 +477,10 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
                     if (in.ts_pos) {
                         a.v1 = ap2.x != AP_SKIP ? in.ts[ap2.x] : 0ULL;
                         b.v1 = ap2.y != AP_SKIP ? in.ts[ap2.y] : 0ULL;
+                    } else if (in.ts_v1 & 2u) {  // (16-B aligned ts array: one paired load)
+                        const ulonglong2 t2 = *reinterpret_cast<const ulonglong2 *>(in.ts + ic);
+                        a.v1 = t2.x;
+                        b.v1 = t2.y;
                     } else {
                         a.v1 = in.ts[ic];
                         b.v1 = in.ts[ic + 1];

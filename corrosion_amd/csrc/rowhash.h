@@ -39,7 +39,7 @@ struct BatchDev {
     // ts_v1 (INTEGER-only batches, k_scatter<PLAIN>): every staged record carries its change's ts in
     // its v1 word (unused by INTEGER values), so the merge reads a winner's ts from the record it
     // already holds instead of a random load from a per-position array. ts_pos: ts is indexed by
-    // application position (ap), else by input index.
+    // application position (ap), else by input index. (ts_v1 bit 1: ts is 16-B aligned, paired loads)
     uint32_t ts_v1, ts_pos;
 };
 constexpr uint32_t AP_SKIP = 0xFFFFFFFFu;
