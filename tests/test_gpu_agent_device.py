@@ -125,11 +125,12 @@ FIELDS = {"pk": np.uint64, "table_cid": np.uint32, "col_version": np.int64, "db_
           "ts": np.uint64}
 
 
-def _run(eng, bk, ordinal, call, device, order=None):
+def _run(eng, bk, ordinal, call, device, order=None, drop=()):
     """corro_process_multiple_changes on one call; the batch laid out in `order` of the changesets
     (default: arrival order). device: False (host batch), True (device batch) or "headers" (device
     batch, headers and known: CORRO_MEM_DEVICE_HEADERS). Returns (known list, impactful per
-    changeset)."""
+    changeset). drop: batch fields left out (val_type: an INTEGER-only batch, every column value here
+    is INTEGER and a sentinel's value is not stored; ts: the changesets' ts only)."""
     import torch
     from corrosion_amd import _lib as L
     order = list(range(len(call))) if order is None else order
@@ -138,7 +139,7 @@ def _run(eng, bk, ordinal, call, device, order=None):
         off[i] = len(rows)
         rows.extend(dict(r, ts=call[i].ts) for r in call[i].rows)
     n = len(rows)
-    arr = {k: np.array([r[k] for r in rows] or [0], dt) for k, dt in FIELDS.items()}
+    arr = {k: np.array([r[k] for r in rows] or [0], dt) for k, dt in FIELDS.items() if k not in drop}
     keep = []
     s = L.Changes()
     s.n = n
@@ -252,7 +253,7 @@ def _overlap_calls(seed, ncalls=5, per_call=60, base=0):
     return ids, calls
 
 
-def _check_against_oracle(seed, device, order_fn=None, clean=(), empty_sets=0.0, calls_fn=None):
+def _check_against_oracle(seed, device, order_fn=None, clean=(), empty_sets=0.0, calls_fn=None, drop=()):
     import corrosion_amd as ca
     from oracle.agent import AgentOracle
     ids, calls = calls_fn(seed) if calls_fn else _calls(seed, clean=clean, empty_sets=empty_sets)
@@ -268,7 +269,7 @@ def _check_against_oracle(seed, device, order_fn=None, clean=(), empty_sets=0.0,
             for r in c.rows:
                 r["site"] = ordinal[bytes(c.actor)]
         order = order_fn(call) if order_fn else None
-        got_known, got_imp = _run(eng, bk, ordinal, call, device, order)
+        got_known, got_imp = _run(eng, bk, ordinal, call, device, order, drop)
         exp_known, exp_imp = ref.process(call)
         assert got_known == exp_known
         assert got_imp == exp_imp
@@ -286,6 +287,15 @@ def _check_against_oracle(seed, device, order_fn=None, clean=(), empty_sets=0.0,
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_device_batch_matches_restatement(seed):
     _check_against_oracle(seed, device=True)
+
+
+@pytest.mark.parametrize("device", [True, "headers"])
+@pytest.mark.parametrize("drop", [("val_type",), ("ts",), ("val_type", "ts")])
+def test_integer_batch_and_changeset_ts_match_restatement(drop, device):
+    # the ts routes of the apply: an INTEGER-only batch stages each change's ts in its record (by
+    # input index, or by application position when only the changesets carry one); a batch with
+    # value words keeps the per-position ts array
+    _check_against_oracle(4, device=device, drop=drop)
 
 
 @pytest.mark.parametrize("seed", [7, 8])
