@@ -93,7 +93,8 @@ class ExtractOut(C.Structure):
 class Metrics(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("applies", "changes", "overflow_rounds", "deferred_rounds",
                                           "region_growths", "heap_growths", "state_rows", "state_records",
-                                          "max_batch")] + [("apply_seconds", C.c_double), ("arena_bytes", C.c_uint64)]
+                                          "max_batch")] + [("apply_seconds", C.c_double), ("arena_bytes", C.c_uint64),
+                                                                   ("aff_sensitive", C.c_uint64)]
 
 
 class GapsIn(C.Structure):

@@ -22,9 +22,11 @@
 // (Cargo.lock:2444), a newer SQLite than the 3.37.2 this image holds and the fixtures pin. Newer
 // SQLite rewrote sqlite3AtoF and the REAL -> TEXT rendering, so a conversion whose result hinges on
 // 3.37.2's long-double rounding is not known to match the reference's base table. The default
-// policy (CORRO_AFF_POLICY_PORTABLE) therefore converts only what any correctly rounded
-// implementation of these routines stores identically, and refuses the rest (CORRO_E_RANGE, before
-// any write):
+// policy (CORRO_AFF_POLICY_SQLITE_3_37_2) converts every value as 3.37.2 does -- SQLite never
+// refuses a change, and a refused batch would stall an actor's sync for good -- and counts such
+// version-sensitive conversions (corro_metrics.aff_sensitive). The strict opt-in policy
+// (CORRO_AFF_POLICY_PORTABLE) converts only what any correctly rounded implementation of these
+// routines stores identically, and refuses the rest (CORRO_E_RANGE, before any write):
 //   TEXT -> REAL   refused when a nonzero digit past the 19th is dropped, when the result
 //                  overflows / is subnormal / takes the e > 307 double-scaling path, or when the
 //                  long-double value lies within a margin of the double rounding midpoint (1 unit
@@ -36,6 +38,7 @@
 //                  round-trip form as well), and for -0.0 (3.37.2 writes "0.0").
 // Integer text, INTEGER -> TEXT / REAL and REAL -> INTEGER are exact and always converted.
 // CORRO_AFF_POLICY_SQLITE_3_37_2 converts everything bit for bit as 3.37.2 does (the fixtures).
+// The sensitive count is taken in the counting pass either way (one word per wave).
 #include <hip/hip_runtime.h>
 
 #include <cctype>
@@ -630,6 +633,7 @@ int affinity_convert(corro_ctx *ctx, BatchDev &bd) {
         return fail(CORRO_E_RANGE, std::to_string(h[3]) + " change(s) need a column-affinity conversion whose result "
                                    "depends on the SQLite version (TEXT <-> REAL rounding): refused under "
                                    "CORRO_AFF_POLICY_PORTABLE (corro_set_affinity_policy)");
+    ctx->metrics.aff_sensitive += h[3];  // (counted at staging: a batch that later fails is counted too)
     // 20 bytes per change of the batch: cv0 | cv1 | cmeta
     AFF_TRY(ctx->d_aff_vals.ensure(n * 20));
     uint64_t *cv0 = ctx->d_aff_vals.as<uint64_t>(), *cv1 = cv0 + n;

@@ -41,6 +41,9 @@ namespace corro {
 int fail(int code, const std::string &msg);
 int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version);
 int set_db_versions(corro_ctx *ctx, const std::vector<std::pair<uint32_t, uint64_t>> &sv);
+uint64_t ctx_write_mark(const corro_ctx *ctx);   // engine.hip: committed applies + set_db_version passes
+void ctx_poison(corro_ctx *ctx, const char *why);  // engine.hip
+bool ctx_poisoned(const corro_ctx *ctx);            // engine.hip
 }  // namespace corro
 
 #define TRY_RC(x)                        \
@@ -65,6 +68,15 @@ struct HostRow {  // one buffered change (__corro_buffered_changes row)
 };
 
 bool is_long(uint8_t vt, uint8_t vl) { return vl == CORRO_VAL_LONG && (vt == CORRO_TEXT || vt == CORRO_BLOB); }
+
+// Failure injection for the atomicity tests: CORRO_FAULT names the steps that fail (comma-separated;
+// read on every call, so a test arms and disarms it around one call).
+bool fault_armed(const char *name) {
+    const char *e = std::getenv("CORRO_FAULT");
+    if (!e || !*e) return false;
+    const std::string s = std::string(",") + e + ",";
+    return s.find(std::string(",") + name + ",") != std::string::npos;
+}
 
 struct SeqBook {  // __corro_seq_bookkeeping rows of one (site, version)
     std::vector<Range> ranges;
@@ -149,6 +161,19 @@ class SegList {
                                       [](const PoolSeg &x, const PoolSeg &y) { return x.seq0 < y.seq0; }),
                      g);
         n_++;
+    }
+    // drop the segments whose copy never ran (a failed commit_staged); order is kept
+    void drop_pending() {
+        std::vector<PoolSeg> keep;
+        for (const PoolSeg &g : *this)
+            if (!(g.off & SEG_PENDING)) keep.push_back(g);
+        clear();
+        for (const PoolSeg &g : keep) insert_sorted(g);
+    }
+    bool any_pending() const {
+        for (const PoolSeg &g : *this)
+            if (g.off & SEG_PENDING) return true;
+        return false;
     }
 
   private:
@@ -441,8 +466,8 @@ void seq_pieces(const SegList &segs, uint64_t s, uint64_t e, std::vector<Range> 
 // (util.rs:1101-1105). A key stays in the device pool while all its rows come from canonical
 // changesets (segments trimmed against the key's earlier ones); a key that receives host rows is
 // brought to the host first. dv: the call's device batch (null: host rows only).
-int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, const std::vector<Staged *> &order,
-                  std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage = nullptr) {
+int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, const std::vector<Staged *> &order,
+                       std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage) {
     auto mark = [&](const char *n) {
         if (stage) stage(n);
     };
@@ -703,6 +728,7 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
             }
     }
     mark("cb_offs");
+    if (fault_armed("bufpool_reserve")) return fail(CORRO_E_NOMEM, "injected fault (CORRO_FAULT): bufpool_reserve");
     TRY_RC(corro::bufpool_reserve(ctx, bk->pool, need, offs, lens));
     mark("cb_reserve");
     TRY_RC(corro::bufpool_append(ctx, bk->pool, dv, jobs));
@@ -717,6 +743,23 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
             }
     mark("cb_fix");
     return CORRO_OK;
+}
+
+// A failure inside commit_staged_impl (table counts, pool reserve or copy: HBM or HIP errors) can come
+// after segments were inserted into the bookie with pending offsets naming this call's copy jobs.
+// They are dropped again (keys left without rows are erased), so the bookie never names pool rows
+// that were not copied and no seq counts as buffered that is not: a re-sent piece buffers again.
+int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, const std::vector<Staged *> &order,
+                  std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage = nullptr) {
+    const int rc = commit_staged_impl(ctx, bk, dv, order, committed, stage);
+    if (rc == CORRO_OK) return rc;
+    for (size_t i = 0; i < bk->buffered.slots(); i++) {
+        auto &x = bk->buffered.at(i);
+        if (x.dead || !x.val.segs.any_pending()) continue;
+        x.val.segs.drop_pending();
+        if (x.val.empty()) bk->buffered.erase_at(i);
+    }
+    return rc;
 }
 
 // the call's __corro_seq_bookkeeping rows (one per (site, version): the actors' keys are disjoint)
@@ -1866,19 +1909,34 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
 extern "C" {
 
 // The C ABI never lets a C++ exception out (a host allocation failing inside the header walks or the
-// host pool's workers): std::bad_alloc is CORRO_E_NOMEM, anything else CORRO_E_INVALID. A failure
-// that late leaves the call uncommitted (the caller's transaction rolls back).
+// host pool's workers): std::bad_alloc is CORRO_E_NOMEM, anything else CORRO_E_INVALID.
+// Failure atomicity of the call: a failure BEFORE the merge or any crsql_set_db_version wrote the state
+// leaves the state, the bookie's Booked versions and its buffered rows as they were (the caller's
+// transaction rolls back, util.rs:849-855). A failure AFTER one of them (the buffered-row commit, the
+// header commit, a host exception in the bookkeeping) cannot be undone on the device: the context is
+// poisoned (every later call fails until corro_state_reset, as for a mid-apply failure) and the bookie
+// keeps no pending buffered segment of the failed call (commit_staged), but its Booked versions do not
+// include the call either, so the caller re-seeds both from its durable store (corro_hip.h, "Failure
+// atomicity").
 int corro_process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_changeset *cs, uint64_t ncs,
                                    const corro_changes *in, int mem, corro_process_out *out) {
+    if (ctx && corro::ctx_poisoned(ctx))
+        return fail(CORRO_E_DEVICE, "context poisoned: an earlier call failed after it began writing the state; "
+                                    "call corro_state_reset");
+    const uint64_t mark0 = ctx ? corro::ctx_write_mark(ctx) : 0;
+    int rc;
     try {
-        return process_multiple_changes(ctx, bk, cs, ncs, in, mem, out);
+        rc = process_multiple_changes(ctx, bk, cs, ncs, in, mem, out);
     } catch (const std::bad_alloc &) {
-        return fail(CORRO_E_NOMEM, "host allocation failed in process_multiple_changes");
+        rc = fail(CORRO_E_NOMEM, "host allocation failed in process_multiple_changes");
     } catch (const std::exception &e) {
-        return fail(CORRO_E_INVALID, std::string("process_multiple_changes: ") + e.what());
+        rc = fail(CORRO_E_INVALID, std::string("process_multiple_changes: ") + e.what());
     } catch (...) {
-        return fail(CORRO_E_INVALID, "process_multiple_changes: unknown host exception");
+        rc = fail(CORRO_E_INVALID, "process_multiple_changes: unknown host exception");
     }
+    if (rc != CORRO_OK && ctx && corro::ctx_write_mark(ctx) != mark0)
+        corro::ctx_poison(ctx, " (after the merge: the context is poisoned until corro_state_reset)");
+    return rc;
 }
 
 int corro_bookie_take_ready(corro_bookie *bk, uint8_t *actors, uint64_t *versions, uint64_t cap, uint64_t *count) {

@@ -1278,8 +1278,19 @@ int set_db_versions(corro_ctx *ctx, const std::vector<std::pair<uint32_t, uint64
     hipLaunchKernelGGL(k_set_dbv, dim3((n + 255) / 256), dim3(256), 0, s, ctx->d_setdbv.as<uint64_t>(), n,
                        ctx->d_dbv.as<unsigned long long>());
     CORRO_HIP_TRY(hipGetLastError());
+    ctx->dbv_writes++;
     CORRO_HIP_TRY(hipStreamSynchronize(s));  // (the host vector is the copy's source)
     return CORRO_OK;
+}
+
+uint64_t ctx_write_mark(const corro_ctx *ctx) { return ctx->metrics.applies + ctx->dbv_writes; }
+
+bool ctx_poisoned(const corro_ctx *ctx) { return ctx->poisoned; }
+
+void ctx_poison(corro_ctx *ctx, const char *why) {
+    if (ctx->poisoned) return;
+    ctx->poisoned = true;
+    set_error(corro_last_error() + std::string(why));
 }
 
 int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version) {
@@ -1290,6 +1301,7 @@ int set_db_version(corro_ctx *ctx, uint32_t site, uint64_t version) {
     CORRO_HIP_TRY(hipMemcpy(&cur, p, 8, hipMemcpyDeviceToHost));
     if (version + 1 > cur) {
         const uint64_t nv = version + 1;
+        ctx->dbv_writes++;
         CORRO_HIP_TRY(hipMemcpy(p, &nv, 8, hipMemcpyHostToDevice));
     }
     return CORRO_OK;
@@ -1324,6 +1336,7 @@ int corro_ctx_metrics(corro_ctx *ctx, corro_metrics *out) {
     out->state_rows = ctx->state_rows;
     out->state_records = ctx->state_total;
     out->arena_bytes = ctx->arena_top;
+    out->aff_sensitive = ctx->metrics.aff_sensitive;
     return CORRO_OK;
 }
 

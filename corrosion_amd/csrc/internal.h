@@ -148,6 +148,7 @@ struct corro_ctx {
     // a failure after an apply's first merge write leaves the state part-merged: every later
     // call on the context fails until corro_state_reset (corro_hip.h "Failure atomicity")
     bool poisoned = false;
+    uint64_t dbv_writes = 0;      // crsql_set_db_version passes run (a late agent failure after one poisons)
     // position mode of the next apply (set by the agent around one corro_apply_batch call on its
     // arrival-order input, agent_dev.hip): application position per input change, input index per
     // position, per-position ts, applied count
@@ -205,7 +206,7 @@ struct corro_ctx {
     corro::DevBuf d_aff_conv, d_aff_vals;
     corro::DevBuf d_gaps_big;              // corro_booked_insert_db_batch: counter + long-actor list  // per change of a batch: converted flag; cv0 | cv1 | cmeta
     bool aff_any = false;         // some column has an affinity other than BLOB
-    int aff_policy = CORRO_AFF_POLICY_PORTABLE;  // corro_set_affinity_policy
+    int aff_policy = CORRO_AFF_POLICY_SQLITE_3_37_2;  // corro_set_affinity_policy (never refuse by default)
     corro::DevBuf d_part;         // partition counts
     corro::DevBuf d_pkdir;        // PkDir per table (pk_mirror_sync)
     corro::DevBuf d_part_var;     // partition_var scratch: per-record var lengths / offsets, perm

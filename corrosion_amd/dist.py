@@ -152,7 +152,8 @@ def distributed_apply_slots(engine, batch, cap, group=None):
             dist.all_to_all_single(got, recs, group=group)
         mine = engine.unpack_slots(got, world, cap, rcnt)
         engine.apply_mapped(mine)
-    over = mine["overflow"].to(torch.int64)  # (after the merge: the apply has returned)
+        over = mine["overflow"].to(torch.int64)  # (on the engine's stream, where unpack_slots wrote it)
+    torch.cuda.current_stream().wait_stream(st)  # (the caller's stream reads `over` and the state next)
     tot = over.cpu() if gloo else over.clone()
     dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
     nover = int(tot.item())

@@ -135,10 +135,12 @@ class MergeEngine:
     AFFINITY_POLICIES = {"portable": 0, "sqlite-3.37.2": 1}
 
     def set_affinity_policy(self, policy):
-        """"portable" (default): convert only values whose stored form is the same in every SQLite
-        version with correctly rounded conversions, refuse a batch holding any other (CorroError,
-        CORRO_E_RANGE, before any write). "sqlite-3.37.2": convert every value exactly as SQLite 3.37.2
-        does (corro_set_affinity_policy)."""
+        """"sqlite-3.37.2" (default): convert every value exactly as SQLite 3.37.2 does, never refusing a
+        change (as SQLite does), and count the conversions whose stored form may differ in another SQLite
+        version (metrics()["aff_sensitive"]). "portable" (strict, opt-in): convert only values whose
+        stored form is the same in every SQLite version with correctly rounded conversions, refuse a
+        batch holding any other (CorroError, CORRO_E_RANGE, before any write)
+        (corro_set_affinity_policy)."""
         L.check(L.lib().corro_set_affinity_policy(self._h, self.AFFINITY_POLICIES[policy]))
 
     def pk_keys(self, table, packed):

@@ -197,10 +197,12 @@ int corro_affinity_of_type(const char *decl_type);
 int corro_table_set_affinity(corro_ctx *ctx, uint32_t table, const uint8_t *aff, uint32_t ncols);
 /* Which conversions the engine performs. The reference bundles a newer SQLite (libsqlite3-sys 0.31.0,
  * Cargo.lock:2444) than the 3.37.2 whose conversion routines the engine emulates, and newer SQLite
- * rewrote TEXT -> REAL (sqlite3AtoF) and REAL -> TEXT rounding. PORTABLE (the default) converts
- * only values every correctly rounded implementation stores identically and fails a batch holding
- * any other conversion with CORRO_E_RANGE before it writes (affinity.hip states the rules);
- * SQLITE_3_37_2 converts every value exactly as SQLite 3.37.2 does. */
+ * rewrote TEXT -> REAL (sqlite3AtoF) and REAL -> TEXT rounding. SQLITE_3_37_2 (the default) converts
+ * every value exactly as SQLite 3.37.2 does -- like SQLite, it never refuses a change -- and counts
+ * the conversions whose result may differ in another SQLite version in corro_metrics.aff_sensitive.
+ * PORTABLE (opt-in, strict) converts only values every correctly rounded implementation stores
+ * identically and fails a batch holding any other conversion with CORRO_E_RANGE before it writes
+ * (affinity.hip states the rules). */
 enum { CORRO_AFF_POLICY_PORTABLE = 0, CORRO_AFF_POLICY_SQLITE_3_37_2 = 1 };
 int corro_set_affinity_policy(corro_ctx *ctx, int policy);
 
@@ -224,7 +226,12 @@ int corro_state_reset(corro_ctx *ctx);
  * hit while growing the row store, a device error, a later chunk of a chunked batch) cannot be undone
  * in place: the context is then POISONED and every later apply / export / extraction call fails with
  * CORRO_E_DEVICE until corro_state_reset, after which the caller re-seeds the state from its durable
- * store (the SQLite tables it persists with corro_state_export_touched). */
+ * store (the SQLite tables it persists with corro_state_export_touched).
+ * corro_process_multiple_changes adds its bookkeeping after the merge: a failure there (the buffered
+ * rows' pool reserve or copy, the header commit, a host allocation) also poisons the context once the
+ * call's merge or any crsql_set_db_version has run; the bookie then keeps none of the call's pending
+ * buffered segments and none of its Booked versions, and the caller rebuilds it with the state
+ * (CORRO_FAULT=bufpool_reserve injects such a failure in tests). */
 
 /* Per-apply delta for persistence (the writes each reference INSERT INTO crsql_changes makes to the
  * base table and clock table inside the caller's transaction, util.rs:749-758, :1225-1245). With
@@ -275,6 +282,9 @@ typedef struct {
     uint64_t arena_bytes;      /* long-value arena in use: append-only (every batch's TEXT/BLOB values
                                   longer than 16 bytes, winners or not) until corro_state_reset, at most
                                   2^40 bytes (CORRO_E_RANGE beyond) */
+    uint64_t aff_sensitive;    /* changes converted by a column affinity whose stored value may differ
+                                  between SQLite versions (TEXT <-> REAL rounding), under
+                                  CORRO_AFF_POLICY_SQLITE_3_37_2 (the default); PORTABLE refuses them */
 } corro_metrics;
 int corro_ctx_metrics(corro_ctx *ctx, corro_metrics *out);
 /* corro.changes.committed{table}: changes of complete and partial changesets that

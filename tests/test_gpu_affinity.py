@@ -185,7 +185,26 @@ def test_long_numeric_text_converted():
     assert sorted(rows_to_tuples(e.export())) == sorted(rows_to_tuples(f.export()))
 
 
-# ---- the portable policy (default): only version-independent conversions ------------------------
+# ---- the default policy never refuses; the portable policy (opt-in, strict) ----------
+def test_default_policy_converts_version_sensitive_values_and_counts_them():
+    """A REAL whose '%!.15g' text is another double (0.1 + 0.2) written into a TEXT column applies under
+    the default policy -- SQLite stores a converted value and never refuses a change -- and is counted
+    in the aff_sensitive metric; a plain conversion is not counted."""
+    sites = synth.site_ids(2, 3)
+    e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 16)
+    e.register_sites(sites)
+    e.set_column_types("t", TYPES)
+    f = O.Fold(sites)
+    f.set_affinity(0, AFF_OF_CID)
+    b = _batch([(1, 3, 0.1 + 0.2), (2, 3, 0.5), (3, 1, "12"), (4, 3, 1 / 3)])
+    assert np.array_equal(e.apply(b, impact=True), f.apply(b))
+    got = _stored(e.export())
+    assert got[(1, 3)] == "0.3" and got[(2, 3)] == "0.5" and got[(3, 1)] == 12
+    assert sorted(rows_to_tuples(e.export())) == sorted(rows_to_tuples(f.export()))
+    assert e.metrics()["aff_sensitive"] == 2
+
+
+
 def _sqlite_15g(x):
     """SQLite's "%!.15g" from a correctly rounded '%.15g' (Python's): '.0' when no point, exponent
     with at least two digits (Python's already has them)"""
@@ -269,7 +288,7 @@ def _one(e, cid, v):
 
 
 def test_portable_policy_converts_only_version_independent_values():
-    """Every fixture case under the default policy: either refused as a whole batch (CORRO_E_RANGE,
+    """Every fixture case under the portable policy: either refused as a whole batch (CORRO_E_RANGE,
     nothing written), or stored exactly as SQLite 3.37.2 stores it (the fixture) AND as a correctly
     rounded conversion stores it (Python's float() / '%.15g'). A refusal is only allowed where the
     15-digit rendering does not round-trip (REAL -> TEXT) or the decimal needs more than 15 digits or
