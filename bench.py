@@ -39,6 +39,8 @@ N_ACTORS = 1000
 N_PK = 1 << 22
 N_PK_C3 = 1 << 25
 N_COLS = 4
+N_C5 = 64_000_000          # BASELINE configs[4] at the size config 2's bench uses
+C5_PMC_APPLIES = 3
 ALG_BYTES_PER_CHANGE = 48  # pk 8, table_cid 4, col_version 8, db_version 8, cl 4, seq 4, site 4, value 8
 ALG_BYTES_PER_CELL = 48
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8 TB/s spec
@@ -217,9 +219,14 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-rank-child", type=int, default=0, help=argparse.SUPPRESS)  # world size emulated
+    ap.add_argument("--pmc-c5-child", type=int, default=-1, help=argparse.SUPPRESS)  # 0 / 1: config 5 (impacts)
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 figure of the N = 1 line")
     args = ap.parse_args()
     if args.pmc_rank_child:
         run_rank_child(args, args.pmc_rank_child)
+        return
+    if args.pmc_c5_child >= 0:
+        config5(bool(args.pmc_c5_child), reps=args.steps, child=True)
         return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -230,8 +237,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
 
     traffic, traffic_note, traffic_kern = None, "not measured (--no-pmc)", None
+    c5_traffic = {}
     if world == 1 and not args.pmc_child and not args.no_pmc and rank == 0:
         traffic, traffic_note, traffic_kern = pmc_traffic_live(args.changes or N_CHANGES)
+        if not args.no_config5:
+            for imp in (0, 1):
+                child = [os.path.abspath(__file__), "--pmc-c5-child", str(imp), "--steps", str(C5_PMC_APPLIES - 1)]
+                c5_traffic[imp] = pmc_traffic_live(N_C5, applies=C5_PMC_APPLIES, timeout=300, child_cmd=child)
 
     if world > 1 and not args.no_pmc and rank == 0:
         # per-rank traffic of the step's local kernels, before this rank touches its GPU (the other
@@ -242,7 +254,7 @@ def main():
         traffic, traffic_note, traffic_kern = pmc_traffic_live(G // world, applies=3, child_cmd=child)
 
     if world == 1:
-        run_single(args, traffic, traffic_note, traffic_kern)
+        run_single(args, traffic, traffic_note, traffic_kern, c5_traffic)
     else:
         run_multi(args, world, rank, (traffic, traffic_note, traffic_kern))
 
@@ -273,7 +285,62 @@ def run_rank_child(args, world):
     eng.close()
 
 
-def run_single(args, traffic, traffic_note, traffic_kern=None):
+def config5(impact, reps=3, child=False, traffic=None):
+    """BASELINE configs[4] (adversarial mix) on one GPU: 64M changes generated in HBM
+    (synth.adversarial_batch_torch: 8 tables of (INTEGER, INTEGER, BLOB, BLOB) columns, Zipf(1.1) pks
+    over 2^20, 30 % sentinel deletes / resurrects, mixed value classes), one apply into an empty state
+    per rep, with or without impact flags. Returns (median ms, cells, stage ms). child: the PMC child
+    (warm-up + `reps` applies, nothing printed)."""
+    import torch
+    import synth
+    import corrosion_amd as ca
+    seed = synth.config_seed(5)
+    batch = synth.adversarial_batch_torch(N_C5, N_ACTORS, 8, 1 << 20, seed, device="cuda:0")
+    eng = ca.MergeEngine(synth.adversarial_schema(8), capacity_hint=N_C5, device=0)
+    eng.register_sites(synth.site_ids(N_ACTORS, seed))
+    eng.set_profiling(True)
+    prep = eng.prepare(batch, impact=impact)
+    times, stages = [], []
+    for rep in range(reps + 1):
+        eng.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.apply_prepared(prep)
+        torch.cuda.synchronize()
+        if rep:
+            times.append((time.perf_counter() - t0) * 1e3)
+            stages.append(eng.last_timings())
+    cells = eng.count()
+    eng.close()
+    if child:
+        return None
+    k = sorted(range(len(times)), key=times.__getitem__)[len(times) // 2]
+    return times[k], cells, stages[k]
+
+
+def config5_figures(reps, c5_traffic):
+    """The config-5 object of the N = 1 line: ms per apply without and with impact flags, traffic
+    ratio (live PMC bytes per apply over SURVEY §8(d)'s 56 B per change and per output cell)."""
+    out = {"workload": "config 5: 64M changes, 8 tables, Zipf(1.1) pks over 2^20, 30 percent sentinels, mixed "
+                       f"values; one apply into an empty state (median of {reps})", "changes": N_C5}
+    for imp in (0, 1):
+        ms, cells, st = config5(bool(imp), reps=reps)
+        alg = 56 * (N_C5 + cells)
+        tr = c5_traffic.get(imp, (None, "not measured", None))
+        key = "impact" if imp else "no_impact"
+        out[key] = {"ms": ms, "changes_per_s": N_C5 / (ms * 1e-3), "cells": int(cells), "alg_bytes": alg,
+                    "roofline_frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "stages_ms": st,
+                    "traffic": tr[0], "traffic_ratio": (tr[0] / alg) if tr[0] else None, "traffic_source": tr[1],
+                    "traffic_by_kernel": ({k: {"fetch": round(v["fetch"]), "write": round(v["write"])}
+                                           for k, v in sorted(tr[2].items())} if tr[2] else None)}
+    out["ms"] = out["no_impact"]["ms"]
+    out["ms_impact"] = out["impact"]["ms"]
+    out["traffic_ratio"] = out["no_impact"]["traffic_ratio"]
+    out["traffic_ratio_impact"] = out["impact"]["traffic_ratio"]
+    return out
+
+
+def run_single(args, traffic, traffic_note, traffic_kern=None, c5_traffic=None):
     import torch
     import synth
     import corrosion_amd as ca
@@ -320,6 +387,10 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
     mixed_agent = agent_e2e_mixed(eng, batch, n, e2e_agent["ms"], reps=5)
     e2e = host_batch_e2e(eng, batch, n)
     cpu = None if args.no_cpu_baseline else cpu_baseline(batch)
+    eng.close()
+    del batch, prep
+    torch.cuda.empty_cache()
+    c5 = None if args.no_config5 else config5_figures(3, c5_traffic or {})
     line = {
         "metric": METRIC,
         "value": n / dt * args.steps,
@@ -350,9 +421,9 @@ def run_single(args, traffic, traffic_note, traffic_kern=None):
         "agent_e2e": e2e_agent,
         "agent_e2e_mixed": mixed_agent,
         "end_to_end_h2d": e2e,
+        "config5": c5,
     }
     print(json.dumps(line), flush=True)
-    eng.close()
 
 
 def host_batch_e2e(eng, batch, n, reps=3):

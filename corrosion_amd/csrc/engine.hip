@@ -606,7 +606,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_heap, &ctx->d_heap_ts, &ctx->d_heap_top, &ctx->d_stride, &ctx->d_defer,
                       &ctx->d_relist, &ctx->d_dense, &ctx->d_dense_ts, &ctx->d_dense_view, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_ovf_sort, &ctx->d_ovf_rcl, &ctx->d_setdbv,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_fast_of, &ctx->d_ovf_sort, &ctx->d_ovf_rcl, &ctx->d_setdbv,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
                       &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,
@@ -898,6 +898,15 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     for (int round = 0;; round++) {
         if (round > 40) return fail(CORRO_E_NOMEM, "internal: the row store did not take the batch's rows");
         mark(4);
+        // triage in one pass, queue appends per wave (k_triage); the fast body's workgroups skip it
+        static const bool no_triage = std::getenv("CORRO_TRIAGE") && std::atoi(std::getenv("CORRO_TRIAGE")) == 0;
+        if (!no_triage) {
+            TRY(ctx->d_fast_of.ensure(B + 256));
+            a.fast_of = ctx->d_fast_of.as<uint8_t>();
+            hipLaunchKernelGGL(k_triage, dim3(std::min<uint32_t>((nblocks + 255) / 256, 1024)), dim3(256), 0, s, a, nblocks,
+                               ctx->d_fast_of.as<uint8_t>());
+            CORRO_HIP_TRY(hipGetLastError());
+        }
         if (a.impact) {
             // the packed two-word keys of the INTEGER impact body: col_versions < 2^15, <= 2^16 sites
             const bool packed = ctx->h_misc[MISC_CVBIG] == 0 && nsites <= 65536;

@@ -174,6 +174,7 @@ struct corro_ctx {
     corro::DevBuf d_ovf_list;     // overflow buckets
     corro::DevBuf d_gen_list;     // buckets queued for the general body
     corro::DevBuf d_wide_list;    // buckets queued for the mixed-type fast body
+    corro::DevBuf d_fast_of;      // k_triage: per merged bucket, 1 = INTEGER fast body
     corro::DevBuf d_ovf_sort;     // overflow path: its device-wide arrays, offsets, rocPRIM temp
     corro::DevBuf d_ovf_rcl;      // overflow path, impact form of the row reduction: per-row cl slots
     corro::DevBuf d_setdbv;       // set_db_versions: (site, version + 1) pairs

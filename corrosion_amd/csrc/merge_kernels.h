@@ -66,6 +66,7 @@ struct MergeArgs {
     uint32_t *ovf_list;
     uint32_t *gen_list;        // [B] buckets for k_merge_gen, then k_merge_gen_small, k_merge_gen_mid
     uint32_t *wide_list;       // buckets for k_merge_fast_wide
+    const uint8_t *fast_of;    // k_triage ran: per launched block, 1 = INTEGER fast body (null: fast_int triages)
     uint32_t *defer_list;      // buckets that could not take their new rows (re-merged after growth)
     const uint32_t *bucket_list;  // a re-merge: workgroup k takes bucket bucket_list[k] (null: k itself)
     uint32_t B;
@@ -2499,9 +2500,55 @@ __device__ inline uint32_t bucket_of_block(const MergeArgs &a) {
 // below, so those launch a few hundred workgroups instead of one per bucket.
 // IMPACT bodies come as two kernels, PACKED chosen by the host from k_scatter's MISC_CVBIG (one
 // kernel holding both forms would size its registers for the larger and halve the occupancy)
+// The triage as its own pass (k_triage: one lane per bucket, each queue append aggregated per wave)
+// when a batch is mostly general (config 5: 32 K one-workgroup triages of k_merge_fast_int, each one
+// same-address queue atomic, cost 0.4 ms): a_fast[b] = 1 for the buckets left to the INTEGER fast
+// body, whose workgroups then skip the triage. Queue q: 0 ovf, 1 gen_small, 2 gen_mid, 3 gen, 4 wide.
+__device__ inline void queue_append_wave(const MergeArgs &a, int q, bool mine, uint32_t b) {
+    const uint64_t m = __ballot(mine);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int word = q == 0 ? MISC_OVF : q == 1 ? MISC_GEN_SMALL : q == 2 ? MISC_GEN_MID : q == 3 ? MISC_GEN : MISC_WIDEQ;
+    unsigned long long base = 0;
+    if ((int)lane == leader) base = atomicAdd(&a.misc[word], (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (!mine) return;
+    const uint32_t k = (uint32_t)base + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
+    if (q == 0) a.ovf_list[k] = b;
+    else if (q == 1) a.gen_list[a.B + k] = b;
+    else if (q == 2) a.gen_list[2 * a.B + k] = b;
+    else if (q == 3) a.gen_list[k] = b;
+    else a.wide_list[k] = b;
+}
+
+static __global__ void __launch_bounds__(256) k_triage(MergeArgs a, uint32_t nb, uint8_t *__restrict__ fast) {
+    if (a.misc[0]) return;
+    const unsigned long long wide = a.misc[MISC_WIDE];
+    for (uint32_t base = blockIdx.x * blockDim.x; base < nb; base += gridDim.x * blockDim.x) {  // (wave-uniform)
+        const uint32_t j = base + threadIdx.x;
+        int q = -1;  // -1: nothing (empty / past the end), 5: fast body
+        uint32_t b = 0;
+        if (j < nb) {
+            b = a.bucket_list ? a.bucket_list[j] : j;
+            const uint32_t n = a.new_cnt[b];
+            if (n) {
+                if (a.force_general || a.rs.gen[b] || ((a.bflags[b >> 5] >> (b & 31)) & 1u))
+                    q = n > a.gen_ovf_min ? 0 : n <= CAP_GEN_SMALL ? 1 : n <= CAP_GEN_MID ? 2 : 3;
+                else if (n > (uint32_t)CAP_FAST) q = 0;
+                else if (a.state_wide || wide != 0) q = 4;
+                else q = 5;
+            }
+            fast[j] = q == 5 ? 1 : 0;
+        }
+        for (int k = 0; k < 5; k++) queue_append_wave(a, k, q == k, b);
+    }
+}
+
 template <bool IMPACT, bool PACKED = false>
 static __global__ void __launch_bounds__(FAST_T, FAST_WAVES_EU)
 k_merge_fast_int(MergeArgs a) {
+    if (a.fast_of && !a.fast_of[blockIdx.x]) return;  // (k_triage queued it, or it is empty)
     if (a.misc[0]) return;  // the batch failed k_scatter's validation: nothing is merged
     const uint32_t b = bucket_of_block(a);
     // every per-bucket word is loaded up front (independent scalar loads, one latency)
@@ -2512,7 +2559,7 @@ k_merge_fast_int(MergeArgs a) {
     const unsigned long long wide = a.misc[MISC_WIDE], cvbig = a.misc[MISC_CVBIG];
     const uint32_t n = v.nn;
     if (n == 0) return;
-    if (a.force_general || rgen || ((bword >> (b & 31)) & 1u)) {
+    if (!a.fast_of && (a.force_general || rgen || ((bword >> (b & 31)) & 1u))) {
         if (threadIdx.x == 0) {
             if (n > a.gen_ovf_min)
                 push_overflow(a, b);
@@ -2525,11 +2572,11 @@ k_merge_fast_int(MergeArgs a) {
         }
         return;
     }
-    if (n > (uint32_t)CAP_FAST) {
+    if (!a.fast_of && n > (uint32_t)CAP_FAST) {
         if (threadIdx.x == 0) push_overflow(a, b);
         return;
     }
-    if (a.state_wide || wide != 0) {
+    if (!a.fast_of && (a.state_wide || wide != 0)) {
         if (threadIdx.x == 0) a.wide_list[atomicAdd(&a.misc[MISC_WIDEQ], 1ULL)] = b;
         return;
     }

@@ -127,6 +127,76 @@ def adversarial_batch(n, nactors, ntables, npk, seed, zipf=1.1, sentinel_frac=0.
             "val_type": vt, "val_len": vl, "ts": (dbv.astype(np.uint64) << np.uint64(20)) + site.astype(np.uint64)}
 
 
+def adversarial_batch_torch(n, nactors, ntables, npk, seed, device="cuda", zipf=1.1, sentinel_frac=0.3,
+                            per_version=50, max_cl=6):
+    """Config 5 generated in HBM (torch): the distribution of adversarial_batch(wide=True), not its
+    bytes (bench.py's config-5 figure; parity tests use the numpy batch). Zipf pks by inverse CDF,
+    30 % sentinels (col_version == cl, NULL), column changes at odd cl with INTEGER / 16-B BLOB /
+    REAL / TEXT (<= 16 B inline) / NULL values."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
+    i64 = torch.int64
+    per_actor = -(-n // nactors)
+    i = torch.arange(n, device=device, dtype=i64)
+    site = (i // per_actor).to(torch.int32)
+    local = i % per_actor
+    dbv = local // per_version + 1
+    seq = (local % per_version).to(torch.int32)
+    table = torch.randint(0, ntables, (n,), device=device, generator=g, dtype=i64)
+    w = torch.arange(1, npk + 1, device=device, dtype=torch.float64) ** (-zipf)
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    pk = (torch.searchsorted(cdf, torch.rand(n, device=device, generator=g, dtype=torch.float64)) + 1).clamp(max=npk)
+    sent = torch.rand(n, device=device, generator=g) < sentinel_frac
+    cid = torch.where(sent, torch.zeros_like(table), torch.randint(1, 5, (n,), device=device, generator=g, dtype=i64))
+    cl = torch.randint(1, max_cl + 1, (n,), device=device, generator=g, dtype=i64)
+    cl = torch.where(sent, cl, cl | 1)
+    cv = torch.where(sent, cl, torch.randint(1, 6, (n,), device=device, generator=g, dtype=i64))
+    vt = torch.ones(n, device=device, dtype=torch.uint8)
+    v0 = torch.randint(-(1 << 62), 1 << 62, (n,), device=device, generator=g, dtype=i64)
+    ties = torch.rand(n, device=device, generator=g) < 0.3
+    v0 = torch.where(ties, torch.randint(0, 4, (n,), device=device, generator=g, dtype=i64), v0)
+    v1 = torch.zeros(n, device=device, dtype=i64)
+    vl = torch.zeros(n, device=device, dtype=torch.uint8)
+    blob = (cid == 3) | (cid == 4)
+    vt = torch.where(blob, torch.full_like(vt, 4), vt)
+    vl = torch.where(blob, torch.full_like(vl, 16), vl)
+    v1 = torch.where(blob, torch.randint(0, 1 << 62, (n,), device=device, generator=g, dtype=i64), v1)
+    bt = blob & (torch.rand(n, device=device, generator=g) < 0.3)
+    v1 = torch.where(bt, torch.randint(0, 3, (n,), device=device, generator=g, dtype=i64), v1)
+    v0 = torch.where(bt, torch.randint(0, 3, (n,), device=device, generator=g, dtype=i64), v0)
+    r = torch.rand(n, device=device, generator=g)
+    real = (~blob) & (r < 0.1)
+    reals = torch.tensor([0.0, -0.0, 1.5, -2.25, 5.0], device=device, dtype=torch.float64).view(i64)
+    v0 = torch.where(real, reals[torch.randint(0, 5, (n,), device=device, generator=g)], v0)
+    vt = torch.where(real, torch.full_like(vt, 2), vt)
+    text = (~blob) & (r >= 0.1) & (r < 0.2)
+    lens = torch.randint(0, 17, (n,), device=device, generator=g, dtype=i64)
+    raw = torch.randint(97, 100, (n, 16), device=device, generator=g, dtype=i64)
+    raw = torch.where(torch.arange(16, device=device)[None, :] < lens[:, None], raw, torch.zeros_like(raw))
+    sh = (8 * (7 - torch.arange(8, device=device, dtype=i64)))[None, :]
+    tw0 = (raw[:, :8] << sh).sum(1)
+    tw1 = (raw[:, 8:] << sh).sum(1)
+    del raw
+    v0 = torch.where(text, tw0, v0)
+    v1 = torch.where(text, tw1, v1)
+    vt = torch.where(text, torch.full_like(vt, 3), vt)
+    vl = torch.where(text, lens.to(torch.uint8), vl)
+    nul = (~blob) & (r >= 0.2) & (r < 0.25)
+    vt = torch.where(nul, torch.full_like(vt, 5), vt)
+    v0 = torch.where(nul, torch.zeros_like(v0), v0)
+    vt = torch.where(sent, torch.full_like(vt, 5), vt)
+    zero = torch.zeros_like(v0)
+    v0, v1 = torch.where(sent, zero, v0), torch.where(sent, zero, v1)
+    vl = torch.where(sent, torch.zeros_like(vl), vl)
+    tcid = ((table << 16) | cid).to(torch.int32)
+    return {"pk": pk.contiguous(), "table_cid": tcid.contiguous(), "col_version": cv.contiguous(),
+            "db_version": dbv.contiguous(), "cl": cl.to(torch.int32).contiguous(), "seq": seq.contiguous(),
+            "site": site.contiguous(), "val0": v0.contiguous(), "val1": v1.contiguous(),
+            "val_type": vt.contiguous(), "val_len": vl.contiguous(), "ts": ((dbv << 20) + site.to(i64)).contiguous()}
+
+
 ADV_COLS = ["i0", "i1", "b0", "b1"]
 
 

@@ -236,7 +236,38 @@ def agent_kats():
          "expect": [full(5, flat[2:3], [2, 2], last), full(5, flat[15:25], [15, 24], last)]},
     ]
     handle = {"source": "corro-agent/src/api/peer/mod.rs:1729-2321", "actor": "ab" * 16, "ts": 7, "steps": steps}
-    return {"process_failed_changes": failed, "handle_need": handle}
+    return {"process_failed_changes": failed, "handle_need": handle, "clear_empty_versions": clear_empty_versions()}
+
+
+def clear_empty_versions():
+    """test_clear_empty_versions (corro-agent/src/agent/tests.rs:777-875). ta1 writes rows 1..50 of
+    tests3, one INSERT OR REPLACE transaction each (insert_rows, tests.rs:1326-1349: text
+    'service-name', text2 'second text', num i + 20, num2 i + 100), so version i holds row i's four
+    column changes (seqs 0..=3, the range check_bookie_versions asks contains_all for, :1207); then it
+    overwrites rows 1..=5, 10, 23..=25, 30..=31 in that order, versions 51..=61 (the same INSERT OR
+    REPLACE on an existing row: every column clock bumped to col_version 2). ta2 processes versions
+    1..=50 in one process_multiple_changes call and 51..=60 in a second (get_rows, :813-829: version
+    61 is not sent); check_bookie_versions then asserts 1..=50 complete (not in gaps); a sync from
+    ta2 to ta1 (parallel_sync over generate_sync, :841-849) brings what ta2 needs, and the second
+    check asserts that crsql_changes holds no row of site ta1 at versions 1..=5, 10, 23..=25, 30..=31
+    (:855-867)."""
+    rows = list(range(1, 51))
+    over = [1, 2, 3, 4, 5, 10, 23, 24, 25, 30, 31]
+
+    def version(v, row, cv):
+        vals = [T("service-name"), T("second text"), I(row + 20), I(row + 100)]
+        return {"kind": "full", "version": v, "seqs": [0, 3], "last_seq": 3,
+                "changes": [["tests3", row, col, val, cv, v, seq, 1]
+                            for seq, (col, val) in enumerate(zip(["text", "text2", "num", "num2"], vals))]}
+    ta1_versions = [version(i, r, 1) for i, r in enumerate(rows, 1)] + \
+                   [version(51 + k, r, 2) for k, r in enumerate(over)]
+    return {"source": "corro-agent/src/agent/tests.rs:777-875 (helpers :1184-1262, :1264-1349)",
+            "ta1": "c1" * 16, "ta2": "c2" * 16, "ts": 11,
+            "ta1_versions": ta1_versions,
+            "calls": [[1, 50], [51, 60]],
+            "after_calls": {"complete": [[1, 50]], "gaps": [], "partials": [], "last": 60},
+            "sync_needs": [["full", 61, 61]],
+            "cleared": [[1, 5], [10, 10], [23, 25], [30, 31]]}
 
 
 def main():

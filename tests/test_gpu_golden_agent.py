@@ -98,3 +98,46 @@ def test_handle_need_fixture():
         else:
             exp = [_msg(m, actor, ts) for m in st["expect_prefix"]]
             assert got[:len(exp)] == exp, n
+
+
+def test_clear_empty_versions_fixture():
+    """test_clear_empty_versions (agent/tests.rs:777-875) in-process: ta1's 61 versions land in its own
+    agent (its bookie books them, as local writes do); ta2 processes 1..=50, then 51..=60; the first
+    check_bookie_versions (1..=50 complete: not needed, no gap; no partial); then the sync: ta2's
+    generate_sync against ta1's, compute_available_needs on the GPU, ta1's handle_need serving those
+    needs from its state, and ta2's process_multiple_changes of what it sent; the second check: no row
+    of site ta1 in ta2's crsql_changes at the cleared versions."""
+    from corrosion_amd.agent import Agent, ChangeV1, Full
+    f = K["clear_empty_versions"]
+    ta1, ta2 = bytes.fromhex(f["ta1"]), bytes.fromhex(f["ta2"])
+    vers = {v["version"]: v for v in f["ta1_versions"]}
+
+    def msg(v):
+        x = vers[v]
+        return ChangeV1(ta1, Full(v, [_change(c, ta1) for c in x["changes"]], tuple(x["seqs"]), x["last_seq"],
+                                  ts=f["ts"]))
+    a1 = Agent(SCHEMA, capacity_hint=1 << 12, actor_id=ta1, interned=INTERNED)
+    a2 = Agent(SCHEMA, capacity_hint=1 << 12, actor_id=ta2, interned=INTERNED)
+    r = a1.process_multiple_changes([msg(v) for v in sorted(vers)])
+    assert r.known == ["current"] * len(vers)
+    for s, e in f["calls"]:
+        r = a2.process_multiple_changes([msg(v) for v in range(s, e + 1)])
+        assert r.known == ["current"] * (e - s + 1)
+    ac = f["after_calls"]
+    assert a2.bookie.last(ta1) == ac["last"] and a2.bookie.needed(ta1) == [tuple(g) for g in ac["gaps"]]
+    for s, e in ac["complete"]:
+        assert a2.bookie.contains_all(ta1, (s, e), (0, 3))
+        assert all(a2.bookie.partial(ta1, v) is None for v in range(s, e + 1))
+    ours, theirs = a2.generate_sync(), a1.generate_sync()
+    needs = ours.compute_available_needs(theirs, a2.engine)
+    from corrosion_amd.sync import Full as NFull
+    assert needs == {ta1: [NFull(s, e) for _k, s, e in f["sync_needs"]]}
+    served = a1.handle_needs([(ta1, n) for n in needs[ta1]])
+    r = a2.process_multiple_changes([m for msgs in served for m in msgs])
+    assert r.known and all(k == "current" for k in r.known)
+    rows = a2.engine.export()
+    site = a2.site(ta1)
+    dbv = {int(rows["db_version"][i]) for i in range(len(rows["pk"])) if int(rows["site"][i]) == site}
+    for s, e in f["cleared"]:
+        assert not dbv & set(range(s, e + 1)), (s, e, sorted(dbv & set(range(s, e + 1))))
+    assert max(dbv) == 61 and a2.bookie.last(ta1) == 61 and a2.bookie.needed(ta1) == []

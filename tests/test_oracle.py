@@ -206,3 +206,49 @@ def test_agent_oracle_empty_set_is_skipped():
     known, _ = ref.process([full, Changeset(ids[1], "empty_set", versions=[(1, 1)])])
     assert known == ["current", "skipped"]
     assert ref.last(bytes(ids[1])) == 2 and ref.needed(bytes(ids[1])) == [(1, 1)]
+
+
+def _clear_empty_versions_oracle_rows(v, site):
+    """a fixture version's changes as oracle rows (tests3 = table 0, columns text/text2/num/num2 =
+    cids 1..4; TEXT values as small INTEGER stand-ins: the test asserts bookkeeping and db_versions)"""
+    cols = {"text": 1, "text2": 2, "num": 3, "num2": 4}
+    out = []
+    for _t, pk, col, val, cv, dbv, seq, cl in v["changes"]:
+        x = int(val["v"]) if val["t"] == "int" else len(val["v"])
+        out.append(dict(pk=pk, table_cid=cols[col], col_version=cv, db_version=dbv, cl=cl, seq=seq, site=site,
+                        val0=x & ((1 << 64) - 1), val_type=1))
+    return out
+
+
+def test_clear_empty_versions_fixture_on_the_restatement():
+    """test_clear_empty_versions (agent/tests.rs:777-875) through oracle/agent.py: the two calls leave
+    1..=50 complete, no gaps, last 60; ta2's sync state against ta1's needs exactly 61..=61 (the
+    restated compute_available_needs); after it lands no row of ta1's is left at the cleared versions."""
+    from oracle.agent import AgentOracle, Changeset
+    f = load_golden("agent_kats.json")["clear_empty_versions"]
+    ta1, ta2 = bytes.fromhex(f["ta1"]), bytes.fromhex(f["ta2"])
+    ids = np.frombuffer(ta1 + ta2, np.uint8).reshape(2, 16)
+    vers = {v["version"]: v for v in f["ta1_versions"]}
+
+    def cs(v):
+        x = vers[v]
+        return Changeset(ta1, "full", version=v, seqs=tuple(x["seqs"]), last_seq=x["last_seq"], ts=f["ts"],
+                         rows=_clear_empty_versions_oracle_rows(x, 0))
+    src, dst = AgentOracle(ids), AgentOracle(ids)
+    known, _ = src.process([cs(v) for v in sorted(vers)])
+    assert known == ["current"] * len(vers)
+    for a, b in f["calls"]:
+        known, _ = dst.process([cs(v) for v in range(a, b + 1)])
+        assert known == ["current"] * (b - a + 1)
+    assert dst.last(ta1) == f["after_calls"]["last"] and dst.needed(ta1) == []
+    ent = entries_from_pairs([({"head": dst.last(ta1), "need": dst.needed(ta1)},
+                               {"head": src.last(ta1), "need": src.needed(ta1)})])
+    got = decode_needs(O.needs(ent), 1)[0]
+    assert got == [tuple(n) for n in f["sync_needs"]]
+    for kind, s, e in got:
+        dst.process([cs(v) for v in range(s, e + 1)])
+    rows = dst.export()
+    dbv = {int(rows["db_version"][i]) for i in range(len(rows["pk"])) if int(rows["site"][i]) == 0}
+    for s, e in f["cleared"]:
+        assert not dbv & set(range(s, e + 1)), (s, e)
+    assert dbv == set(range(1, 62)) - {v for s, e in f["cleared"] for v in range(s, e + 1)} - {31}
