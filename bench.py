@@ -340,6 +340,50 @@ def config5_figures(reps, c5_traffic):
     return out
 
 
+def blob_pk_figures(int_ms, reps=5):
+    """Config 2 over a testsblob-shaped table (corro-tests/src/lib.rs:32-35): the same 2^26 changes with
+    every pk a 16-byte BLOB packed in HBM (19 bytes, synth.blob_pks_torch), interned on the device
+    (corro_pk_keys_device) and applied. `cold`: the first intern of the batch's 4.2 M keys into an
+    empty table; `intern_ms`: a warm intern (every key already held, a node's steady state); `apply_ms`:
+    reset + apply with the interned keys; `e2e_ms`: warm intern + reset + apply, against the INTEGER-pk
+    step (`int_ms`)."""
+    import torch
+    import synth
+    import corrosion_amd as ca
+    n = N_CHANGES
+    b = synth.uniform_batch_torch(n, N_ACTORS, N_PK, N_COLS, seed=synth.config_seed(2), device="cuda:0")
+    data, off = synth.blob_pks_torch(b["pk"])
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=n, device=0, interned=("t",))
+    eng.register_sites(synth.site_ids(N_ACTORS, 1))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    keys = eng.pk_keys_device("t", data, off)
+    torch.cuda.synchronize()
+    cold = (time.perf_counter() - t0) * 1e3
+    b["pk"] = keys
+    prep = eng.prepare(b)
+    it, ap, ee = [], [], []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.pk_keys_device("t", data, off)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        eng.reset()
+        eng.apply_prepared(prep)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        it.append((t1 - t0) * 1e3)
+        ap.append((t2 - t1) * 1e3)
+        ee.append((t2 - t0) * 1e3)
+    med = lambda x: sorted(x[1:])[len(x[1:]) // 2]
+    out = {"workload": "config 2 with 16-byte BLOB pks (testsblob shape), packed in HBM", "changes": n,
+           "keys": int(keys.max().item()) + 1, "intern_cold_ms": cold, "intern_ms": med(it), "apply_ms": med(ap),
+           "e2e_ms": med(ee), "int_pk_ms": int_ms, "apply_ratio": med(ap) / int_ms, "e2e_ratio": med(ee) / int_ms}
+    eng.close()
+    return out
+
+
 def run_single(args, traffic, traffic_note, traffic_kern=None, c5_traffic=None):
     import torch
     import synth
@@ -390,6 +434,8 @@ def run_single(args, traffic, traffic_note, traffic_kern=None, c5_traffic=None):
     eng.close()
     del batch, prep
     torch.cuda.empty_cache()
+    blob = blob_pk_figures(dt / args.steps * 1e3)
+    torch.cuda.empty_cache()
     c5 = None if args.no_config5 else config5_figures(3, c5_traffic or {})
     line = {
         "metric": METRIC,
@@ -421,6 +467,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None, c5_traffic=None):
         "agent_e2e": e2e_agent,
         "agent_e2e_mixed": mixed_agent,
         "end_to_end_h2d": e2e,
+        "blob_pk": blob,
         "config5": c5,
     }
     print(json.dumps(line), flush=True)

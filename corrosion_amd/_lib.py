@@ -35,7 +35,7 @@ EXPORTS = [
     "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
     "corro_unpack_records", "corro_partition_slots", "corro_unpack_slots", "corro_apply_mapped", "corro_ctx_stream",
-    "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_bytes",
+    "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_keys_device", "corro_pk_bytes",
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
     "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity", "corro_set_affinity_policy",
     "corro_ctx_metrics", "corro_table_committed", "corro_ctx_track_touched", "corro_state_export_touched",
@@ -239,6 +239,7 @@ def lib():
         "corro_unpack_var": (i32, [vp, vp, u64, vp, u64, vp, vp, u32, C.POINTER(Changes)]),
         "corro_table_set_pk_interned": (i32, [vp, u32, i32]),
         "corro_pk_keys": (i32, [vp, u32, vp, vp, u64, vp]),
+        "corro_pk_keys_device": (i32, [vp, u32, vp, vp, u64, vp]),
         "corro_pk_bytes": (i32, [vp, u32, vp, u64, vp, u64, vp]),
         "corro_pk_canonical": (i32, [C.c_char_p, u64, vp, u64, vp]),
     }

@@ -171,7 +171,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         d.rbits = (uint64_t *)take(R * 16);
         d.rw1 = (uint64_t *)take(R * 12 + 64);  // row summaries, laid out once the row count is known
         d.cbk = (uint32_t *)take((Kb / 64 + 2) * 4);
-        if (pass == 0) {
+        if (pass == 0 && K <= ctx->ovf_temp_k) {
+            temp = ctx->ovf_temp;  // (rocPRIM's temp sizes grow with n; the 64-bit sort bounds the others)
+        } else if (pass == 0) {
             size_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
             TRY(ovf_sort_pairs(nullptr, &t0, nullptr, nullptr, nullptr, nullptr, d.K, 64, s));
             TRY(ovf_sort_pairs(nullptr, &t1, nullptr, nullptr, nullptr, nullptr, d.K, ckey_bits, s));
@@ -180,6 +182,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
             size_t t4 = 0;
             TRY(ovf_scan_tiles(nullptr, &t4, d, nullptr, nullptr, (uint32_t)((K + CS_TILE - 1) / CS_TILE), s));
             temp = std::max(std::max(std::max(t0, t1), std::max(t2, t3)), t4);
+            ctx->ovf_temp_k = K;
+            ctx->ovf_temp = temp;
         }
         nt = (uint32_t)((K + CS_TILE - 1) / CS_TILE);
         cs_agg = (CsAgg *)take(nt * 8ULL);
@@ -616,11 +620,14 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_hdr_stage, &ctx->d_pm_ts};
     for (DevBuf *b : bufs) b->release();
     ctx->d_pkdir.release();
+    ctx->d_pk_scratch.release();
+    ctx->d_pk_bad.release();
     ctx->d_part_var.release();
     for (PkTable &t : ctx->pk) {
         t.d_off.release();
         t.d_bytes.release();
         t.d_hash.release();
+        t.d_slots.release();
     }
     if (ctx->h_misc) (void)hipHostFree(ctx->h_misc);
     if (ctx->h_ovf) (void)hipHostFree(ctx->h_ovf);

@@ -76,17 +76,18 @@ struct Table {
     std::vector<std::string> cols;
 };
 
-// Row keys of one table's primary keys (pkeys.cpp): interned tables key rows by a dense id of the
+// Row keys of one table's primary keys (pkeys.hip): interned tables key rows by a dense id of the
 // canonical packed pk (cr-sqlite's __crsql_key / <t>__crsql_pks), others by the INTEGER pk itself.
+// The intern table lives on the device (authoritative since round 5): canonical bytes of ids [0, n)
+// at d_bytes[d_off[id], d_off[id + 1]), their route hashes, and open-addressing slots
+// (tag << 32 | id; 0 = empty) that k_pk_probe claims with one 64-bit CAS.
 struct PkTable {
     bool interned = false;
-    std::unordered_map<std::string, uint64_t> ids;
-    std::vector<std::string> keys;
-    std::vector<uint64_t> hash;   // pk_route_hash of each key (the owner rank on every engine)
-    uint64_t max_len = 0;         // longest canonical key
-    // device mirror (pk_mirror_sync): canonical bytes, offsets (n + 1), route hashes of ids [0, dev_n)
-    DevBuf d_off, d_bytes, d_hash;
-    uint64_t dev_n = 0, dev_bytes = 0;
+    DevBuf d_off, d_bytes, d_hash, d_slots;
+    uint64_t n = 0, nbytes = 0;             // keys, arena bytes
+    uint64_t cap_off = 0, cap_bytes = 0;    // capacities of d_off / d_hash (keys) and d_bytes
+    uint64_t nslots = 0;                    // power of two (0: no table yet)
+    uint64_t max_len = 0;                   // bound on the longest canonical key
 };
 // Device view of one table's interned keys (partition.hip routes and ships interned pks by them).
 struct PkDir {
@@ -98,8 +99,24 @@ struct PkDir {
     uint32_t pad;
 };
 uint64_t pk_route_hash(const std::string &canon);
-// Bring every interned table's device mirror up to date and upload the directory (ctx->d_pkdir).
+// Upload the directory of every table's intern arrays (ctx->d_pkdir).
 int pk_mirror_sync(corro_ctx *ctx);
+// Row keys of packed pks on the device (pkeys.hip): for every change i with (tcid[i] >> 16) == table and
+// a reference (ref[i] != none: bytes at base + (ref >> len_bits), length ref & (2^len_bits - 1); or with
+// off != null: bytes [off[i], off[i + 1]) of base), keys[i] = the row key -- the INTEGER pk of a table
+// not interned, else the interned id (new canonical keys get the next ids, in no particular order).
+// bad (optional, n bytes): 1 for a malformed encoding or a non-INTEGER pk of a table not interned
+// (keys[i] untouched); *nbad = their count. All pointers device memory; synchronous.
+struct PkRefs {
+    const uint8_t *base = nullptr;
+    const uint64_t *ref = nullptr;
+    const uint64_t *off = nullptr;
+    uint64_t none = 0;
+    uint32_t len_bits = 32;
+    const uint32_t *tcid = nullptr;  // null: every change is of `table`
+};
+int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, uint64_t *keys, uint8_t *bad,
+                   uint64_t *nbad);
 bool pk_canonical(const uint8_t *p, uint64_t len, std::string &out, bool *single_int, int64_t *ival);
 std::string pack_int_pk(int64_t v);
 
@@ -177,6 +194,8 @@ struct corro_ctx {
     corro::DevBuf d_fast_of;      // k_triage: per merged bucket, 1 = INTEGER fast body
     corro::DevBuf d_ovf_sort;     // overflow path: its device-wide arrays, offsets, rocPRIM temp
     corro::DevBuf d_ovf_rcl;      // overflow path, impact form of the row reduction: per-row cl slots
+    uint64_t ovf_temp_k = 0;      // overflow path: the record count its cached rocPRIM temp size was queried for
+    size_t ovf_temp = 0;
     corro::DevBuf d_setdbv;       // set_db_versions: (site, version + 1) pairs
     corro::DevBuf d_scan_tmp;     // corro_scan_offsets: rocPRIM temp
     corro::DevBuf d_impact;
@@ -210,6 +229,8 @@ struct corro_ctx {
     int aff_policy = CORRO_AFF_POLICY_SQLITE_3_37_2;  // corro_set_affinity_policy (never refuse by default)
     corro::DevBuf d_part;         // partition counts
     corro::DevBuf d_pkdir;        // PkDir per table (pk_mirror_sync)
+    corro::DevBuf d_pk_scratch;   // pk_keys_device: per-change columns, staged host inputs, rocPRIM temp
+    corro::DevBuf d_pk_bad;       // wire decode: per change, a malformed interned pk
     corro::DevBuf d_part_var;     // partition_var scratch: per-record var lengths / offsets, perm
     // process_multiple_changes on the device (agent_dev.hip): staged host input, gathered batch,
     // span tables, impact flags, impactful output, and a pinned host staging area

@@ -718,26 +718,17 @@ extern "C" int corro_unpack_var(corro_ctx *ctx, const void *recs, uint64_t n, co
                        static_cast<const PackedRec80 *>(recs), (uint32_t)n, d_rb, d_vb, nsrc, bo,
                        const_cast<uint64_t *>(out->val_off), const_cast<uint32_t *>(out->val_size), pkref);
     CORRO_HIP_TRY(hipGetLastError());
-    // interned pks: this engine's row keys for the shipped canonical bytes (host intern table)
-    bool any_interned = false;
-    for (const PkTable &t : ctx->pk) any_interned |= t.interned;
-    if (any_interned) {
-        std::vector<uint64_t> ref(n);
-        std::vector<uint32_t> tc(n);
-        CORRO_HIP_TRY(hipMemcpyAsync(ref.data(), pkref, n * 8, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(tc.data(), out->table_cid, n * 4, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
-        std::vector<uint8_t> hv(var_len);
-        if (var_len) CORRO_HIP_TRY(hipMemcpy(hv.data(), var, var_len, hipMemcpyDeviceToHost));
-        std::vector<uint64_t> pk(n);
-        CORRO_HIP_TRY(hipMemcpy(pk.data(), out->pk, n * 8, hipMemcpyDeviceToHost));
-        for (uint64_t i = 0; i < n; i++) {
-            if (ref[i] == ~0ULL) continue;
-            const uint64_t off[2] = {0, ref[i] & 0xFFFFFFu}, at = ref[i] >> 24;
-            if (at + off[1] > var_len) return fail(CORRO_E_INVALID, "shipped pk bytes outside the var buffer");
-            if (int rc = corro_pk_keys(ctx, tc[i] >> 16, hv.data() + at, off, 1, &pk[i])) return rc;
-        }
-        CORRO_HIP_TRY(hipMemcpy(const_cast<uint64_t *>(out->pk), pk.data(), n * 8, hipMemcpyHostToDevice));
+    // interned pks: this engine's row keys for the shipped canonical bytes, interned on the device
+    // (pkref: var offset << 24 | length, ~0 for a change of a table that is not interned)
+    for (uint32_t t = 0; t < (uint32_t)ctx->pk.size(); t++) {
+        if (!ctx->pk[t].interned) continue;
+        PkRefs pr;
+        pr.base = static_cast<const uint8_t *>(var);
+        pr.ref = pkref;
+        pr.none = ~0ULL;
+        pr.len_bits = 24;
+        pr.tcid = out->table_cid;
+        if (int rc = pk_keys_device(ctx, t, pr, n, const_cast<uint64_t *>(out->pk), nullptr, nullptr)) return rc;
     }
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     return CORRO_OK;

@@ -45,6 +45,19 @@ int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, 
     return CORRO_OK;
 }
 
+// inclusive scan of u32 counts into u64 sums (the pk intern's byte offsets); temp == nullptr ->
+// *temp_bytes = size needed
+struct Widen64 {
+    __host__ __device__ inline uint64_t operator()(uint32_t x) const { return x; }
+};
+int prim_inclusive_scan_u32_u64(void *temp, size_t *temp_bytes, const uint32_t *in, uint64_t *out, uint64_t n,
+                                hipStream_t s) {
+    const auto wide = rocprim::make_transform_iterator(in, Widen64{});
+    const hipError_t e = rocprim::inclusive_scan(temp, *temp_bytes, wide, out, (size_t)n, rocprim::plus<uint64_t>(), s);
+    if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("scan: ") + hipGetErrorString(e));
+    return CORRO_OK;
+}
+
 struct OvfMax {
     __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return x > y ? x : y; }
 };

@@ -847,6 +847,38 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
         if (int rc = corro_site_register(ctx, ids.data(), take, nullptr)) return rc;
         if (nu > ucap) attempt = -1;  // more unknown ids than one pass collects: keep going
     }
+    // interned pks: their packed bytes -> row keys on the device (pk_keys_device), patched into the
+    // decoded pk column before anything is copied out; a malformed pk fails its frame
+    if (cnt3[1] && NC) {
+        if (int rc = ctx->d_pk_bad.ensure(NC + 256)) return rc;
+        uint8_t *dbad = ctx->d_pk_bad.as<uint8_t>();
+        bool any_bad = false;
+        for (uint32_t t = 0; t < (uint32_t)ctx->pk.size(); t++) {
+            if (!ctx->pk[t].interned) continue;
+            PkRefs pr;
+            pr.base = dbuf;
+            pr.ref = d.pkref;
+            pr.none = 0;
+            pr.len_bits = 32;
+            pr.tcid = o.table_cid;
+            uint64_t nbad = 0;
+            if (int rc = pk_keys_device(ctx, t, pr, NC, const_cast<uint64_t *>(o.pk), dbad + 0, &nbad)) return rc;
+            if (nbad) {
+                if (!any_bad) CORRO_HIP_TRY(hipMemcpy(st.data(), d.status, F * 4ULL, hipMemcpyDeviceToHost));
+                std::vector<uint8_t> hb(NC);
+                CORRO_HIP_TRY(hipMemcpy(hb.data(), dbad, NC, hipMemcpyDeviceToHost));
+                uint32_t f = 0;
+                for (uint64_t q = 0; q < NC; q++) {
+                    if (!hb[q]) continue;
+                    while (cofs[f + 1] <= q) f++;
+                    st[f] = std::min(st[f], (int32_t)CORRO_E_INVALID);
+                }
+                any_bad = true;
+            }
+        }
+        if (any_bad)  // (the frames' status words on the device, read back with the headers below)
+            CORRO_HIP_TRY(hipMemcpy(d.status, st.data(), F * 4ULL, hipMemcpyHostToDevice));
+    }
     // headers -> host
     std::vector<uint64_t> v0(F), v1(F), s0(F), s1(F), last(F), ts(F);
     std::vector<uint8_t> actor(F * 16ULL);
@@ -887,30 +919,6 @@ extern "C" int corro_decode_frames(corro_ctx *ctx, const uint8_t *buf, uint64_t 
         oc.val_size = nullptr;
         oc.val_data = nullptr;
         oc.val_data_len = 0;
-    }
-    // interned pks: their packed bytes -> row keys (corro_pk_keys), patched into the pk array
-    if (cnt3[1]) {
-        std::vector<uint64_t> ref(NC), pk(NC);
-        std::vector<uint32_t> tc(NC);
-        CORRO_HIP_TRY(hipMemcpyAsync(ref.data(), d.pkref, NC * 8, hipMemcpyDeviceToHost, s));
-        if (mem == CORRO_MEM_DEVICE) {
-            CORRO_HIP_TRY(hipMemcpyAsync(tc.data(), o.table_cid, NC * 4, hipMemcpyDeviceToHost, s));
-            CORRO_HIP_TRY(hipMemcpyAsync(pk.data(), o.pk, NC * 8, hipMemcpyDeviceToHost, s));
-        }
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
-        uint64_t *hp = mem == CORRO_MEM_HOST ? const_cast<uint64_t *>(oc.pk) : pk.data();
-        const uint32_t *ht = mem == CORRO_MEM_HOST ? oc.table_cid : tc.data();
-        uint32_t f = 0;
-        for (uint64_t q = 0; q < NC; q++) {
-            if (!ref[q]) continue;
-            while (cofs[f + 1] <= q) f++;
-            const uint64_t off[2] = {0, ref[q] & 0xFFFFFFFFu};
-            if (corro_pk_keys(ctx, ht[q] >> 16, buf + (ref[q] >> 32), off, 1, hp + q) != CORRO_OK)
-                st[f] = std::min(st[f], (int32_t)CORRO_E_INVALID);
-        }
-        if (mem == CORRO_MEM_DEVICE)
-            CORRO_HIP_TRY(hipMemcpyAsync(const_cast<uint64_t *>(oc.pk), pk.data(), NC * 8, hipMemcpyHostToDevice, s));
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
     }
     if (out->cs_dev) {  // the kept headers for CORRO_MEM_DEVICE_HEADERS, built where they lie
         std::vector<uint32_t> map(F);

@@ -154,6 +154,19 @@ class MergeEngine:
         L.check(L.lib().corro_pk_keys(self._h, t, buf.ctypes.data, off.ctypes.data, len(packed), keys.ctypes.data))
         return keys[:len(packed)]
 
+    def pk_keys_device(self, table, data, off):
+        """Row keys of n packed pks held in device memory: `data` a uint8 CUDA tensor of the packed
+        bytes, `off` an int64 CUDA tensor of n + 1 offsets into it (corro_pk_keys_device: interned in
+        the HBM intern table, nothing crosses PCIe). Returns an int64 CUDA tensor of n keys (uint64
+        bits)."""
+        import torch
+        t = self.table_index(table)
+        n = int(off.numel()) - 1
+        keys = torch.empty(max(n, 1), dtype=torch.int64, device=off.device)
+        torch.cuda.current_stream().synchronize()
+        L.check(L.lib().corro_pk_keys_device(self._h, t, data.data_ptr(), off.data_ptr(), n, keys.data_ptr()))
+        return keys[:n]
+
     def pk_bytes(self, table, keys):
         """Canonical packed pk bytes of row keys of one table."""
         t = self.table_index(table)

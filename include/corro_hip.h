@@ -174,6 +174,12 @@ int corro_pk_canonical(const uint8_t *bytes, uint64_t len, uint8_t *out, uint64_
  * CORRO_E_INVALID for a malformed encoding, CORRO_E_RANGE for a non-INTEGER pk of a table not interned. */
 int corro_pk_keys(corro_ctx *ctx, uint32_t table, const uint8_t *bytes, const uint64_t *off, uint64_t n,
                   uint64_t *keys);
+/* The same with bytes, off (n + 1) and keys in device memory (a decoder that leaves packed pks in HBM):
+ * the intern table is an open-addressing table in HBM, so no pk crosses PCIe. Ids are dense per table
+ * and persist across calls (a new key's id is the table's size at the call plus its rank among the
+ * call's new keys, in no particular order). Synchronous. */
+int corro_pk_keys_device(corro_ctx *ctx, uint32_t table, const uint8_t *bytes, const uint64_t *off, uint64_t n,
+                         uint64_t *keys);
 /* Row keys of `table` -> canonical packed pk bytes (export, extraction): key i's bytes at
  * [out_off[i], out_off[i+1]); out_off holds n + 1 entries; CORRO_E_RANGE if cap < out_off[n]. */
 int corro_pk_bytes(corro_ctx *ctx, uint32_t table, const uint64_t *keys, uint64_t n, uint8_t *bytes, uint64_t cap,

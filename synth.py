@@ -197,6 +197,28 @@ def adversarial_batch_torch(n, nactors, ntables, npk, seed, device="cuda", zipf=
             "val_type": vt.contiguous(), "val_len": vl.contiguous(), "ts": ((dbv << 20) + site.to(i64)).contiguous()}
 
 
+def blob_pks_torch(ids, device="cuda"):
+    """testsblob-shaped packed pks (pack_columns of one 16-byte BLOB, corro-tests/src/lib.rs:32-35)
+    generated in HBM from integer row ids: 19 bytes each -- column count 1, type byte (1 << 3 | BLOB),
+    length 16, then the id big-endian and a 64-bit mix of it -- so distinct ids are distinct keys.
+    Returns (uint8 bytes, int64 offsets of n + 1)."""
+    import torch
+    ids = ids.to(device=device, dtype=torch.int64)
+    n = ids.numel()
+    x = ids.clone()
+    m = ids * -7046029254386353131 + 0x165667B19E3779F9  # (wrapping int64 arithmetic)
+    m = m ^ ((m >> 29) & 0x7FFFFFFFF)
+    out = torch.empty((n, 19), dtype=torch.uint8, device=device)
+    out[:, 0] = 1
+    out[:, 1] = (1 << 3) | 4
+    out[:, 2] = 16
+    for k in range(8):
+        out[:, 3 + k] = ((x >> (8 * (7 - k))) & 0xFF).to(torch.uint8)
+        out[:, 11 + k] = ((m >> (8 * (7 - k))) & 0xFF).to(torch.uint8)
+    off = torch.arange(0, 19 * (n + 1), 19, dtype=torch.int64, device=device)
+    return out.reshape(-1), off
+
+
 ADV_COLS = ["i0", "i1", "b0", "b1"]
 
 

@@ -133,3 +133,134 @@ def test_noncanonical_pk_encodings_name_one_row():
     with pytest.raises(ca.CorroError):
         e.pk_keys("tests", [canon])  # a composite pk on a single-INTEGER-pk table
     e.close()
+
+
+def _canon(b):
+    import ctypes as C
+    from corrosion_amd import _lib as L
+    out = (C.c_uint8 * (9 * len(b) + 16))()
+    n = C.c_uint64()
+    L.check(L.lib().corro_pk_canonical(bytes(b), len(b), out, len(out), C.byref(n)))
+    return bytes(out[:n.value])
+
+
+def _noncanonical(rng, b):
+    """another encoding of the same key: an INTEGER column's value sign-extended from more bytes, or a
+    BLOB / TEXT length written with a wider length prefix (unpack_columns reads both)"""
+    ncol, pos, out = b[0], 1, bytearray([b[0]])
+    for _c in range(ncol):
+        tb = b[pos]
+        t, n = tb & 7, tb >> 3
+        if t == 1:
+            v = int.from_bytes(b[pos + 1:pos + 1 + n], "big", signed=True) if n else 0
+            m = min(8, n + 1 + int(rng.integers(0, 2)))
+            out += bytes([(m << 3) | 1]) + (v & ((1 << (8 * m)) - 1)).to_bytes(m, "big")
+            pos += 1 + n
+        elif t in (3, 4):
+            ln = int.from_bytes(b[pos + 1:pos + 1 + n], "big") if n else 0
+            m = min(4, n + 1)
+            out += bytes([(m << 3) | t]) + ln.to_bytes(m, "big") + b[pos + 1 + n:pos + 1 + n + ln]
+            pos += 1 + n + ln
+        else:
+            sz = 8 if t == 2 else 0
+            out += b[pos:pos + 1 + sz]
+            pos += 1 + sz
+    return bytes(out)
+
+
+@pytest.mark.parametrize("device_api", [False, True])
+def test_intern_table_keys_are_a_persistent_bijection(device_api):
+    """The HBM intern table (corro_pk_keys stages host pks into it; corro_pk_keys_device takes them
+    where they lie): over three calls of random testsblob / wide pks -- duplicates inside a call, keys
+    re-sent in later calls, non-canonical encodings -- equal canonical pks get one key, distinct ones
+    distinct keys, the keys are dense (0 .. n-1 over the calls) and stable across calls, and every key
+    maps back to its canonical bytes (corro_pk_bytes)."""
+    import torch
+    import corrosion_amd as ca
+    rng = np.random.default_rng(5 + device_api)
+    e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12, interned=INTERNED)
+    seen = {}
+    for call in range(3):
+        for table in ("testsblob", "wide"):
+            pool = [_pack([bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))]) if table == "testsblob"
+                    else _pack([int(rng.integers(-2**40, 2**40)).to_bytes(8, "big", signed=True), str(int(rng.integers(0, 50)))])
+                    for _ in range(3000)]
+            pks = [pool[int(rng.integers(0, len(pool)))] for _ in range(8000)]
+            pks = [_noncanonical(rng, p) if rng.random() < 0.1 else p for p in pks]
+            if device_api:
+                buf = torch.tensor(list(b"".join(pks)) or [0], dtype=torch.uint8, device="cuda")
+                off = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pks])]), dtype=torch.int64,
+                                   device="cuda")
+                keys = e.pk_keys_device(table, buf, off).cpu().numpy().view(np.uint64)
+            else:
+                keys = e.pk_keys(table, pks)
+            got = seen.setdefault(table, {})
+            for p, k in zip(pks, keys.tolist()):
+                c = _canon(p)
+                assert got.setdefault(c, k) == k, (table, call)
+            inv = {}
+            for c, k in got.items():
+                assert inv.setdefault(k, c) == c
+            assert sorted(inv) == list(range(len(inv)))
+    for table, got in seen.items():
+        ks = np.array(list(got.values()), np.uint64)
+        assert e.pk_bytes(table, ks) == list(got.keys())
+
+
+def test_device_intern_rejects_malformed_pk():
+    import torch
+    import corrosion_amd as ca
+    e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12, interned=INTERNED)
+    good = _pack([b"abc"])
+    bad = bytes([1, (5 << 3) | 4, 200, 1, 2])   # a 200-byte BLOB with 2 bytes
+    buf = torch.tensor(list(good + bad), dtype=torch.uint8, device="cuda")
+    off = torch.tensor([0, len(good), len(good) + len(bad)], dtype=torch.int64, device="cuda")
+    with pytest.raises(ca.CorroError):
+        e.pk_keys_device("testsblob", buf, off)
+    with pytest.raises(ca.CorroError):   # a composite pk on a table keyed by one INTEGER
+        e.pk_keys_device("tests", buf[:len(good)], off[:2])
+
+
+@pytest.mark.slow
+def test_blob_pk_config2_size_vs_sharded_oracle():
+    """Config 2 at its full size (2^26 changes, 2^22 rows, 1000 actors) over a testsblob-shaped table:
+    every pk a 16-byte BLOB packed in HBM (19 bytes), interned on the device (corro_pk_keys_device),
+    then applied with impacts. The keys are a bijection of the row ids, stable when the same pks come
+    again; impacts, every output row (pk mapped back to its row id) and db_versions equal the oracle's
+    pk-sharded fold of the batch keyed by the row ids."""
+    import torch
+    import corrosion_amd as ca
+    sites = synth.site_ids(1000, 1)
+    b = synth.uniform_batch_torch(1 << 26, 1000, 1 << 22, 4, seed=synth.config_seed(2), device="cuda")
+    ids = b["pk"]
+    data, off = synth.blob_pks_torch(ids)
+    e = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=1 << 26, interned=("t",))
+    e.register_sites(sites)
+    keys = e.pk_keys_device("t", data, off)
+    uid, inv = torch.unique(ids, return_inverse=True)
+    kmax = torch.full((uid.numel(),), -1, dtype=torch.int64, device="cuda").scatter_reduce(0, inv, keys, "amax")
+    kmin = torch.full((uid.numel(),), 1 << 62, dtype=torch.int64, device="cuda").scatter_reduce(0, inv, keys, "amin")
+    assert torch.equal(kmax, kmin)                                   # one key per row id
+    assert torch.unique(kmax).numel() == uid.numel() == int(kmax.max()) + 1  # distinct, dense
+    again = e.pk_keys_device("t", data[:19 * 4096], off[:4097])
+    assert torch.equal(again, keys[:4096])                           # stable across calls
+    bb = dict(b)
+    bb["pk"] = keys
+    imp = e.apply(bb, impact=True).cpu().numpy()
+    hb = {k: v.cpu().numpy() for k, v in b.items()}
+    id_of_key = torch.empty(uid.numel(), dtype=torch.int64, device="cuda")
+    id_of_key[kmax] = uid
+    del b, bb, data, off, keys, kmax, kmin, inv
+    torch.cuda.empty_cache()
+    for k in ("table_cid", "cl", "seq", "site"):
+        hb[k] = hb[k].view(np.uint32)
+    for k in ("pk", "val0"):
+        hb[k] = hb[k].view(np.uint64)
+    f = O.ShardedFold(sites, nshards=64, nthreads=16)
+    ref = f.apply(hb)
+    assert np.array_equal(imp, ref)
+    rows = e.export()
+    rows["pk"] = id_of_key.cpu().numpy().view(np.uint64)[rows["pk"].astype(np.int64)]
+    assert O.rows_digest(rows) == f.digest()
+    assert np.array_equal(e.db_versions(), f.db_versions())
+    e.close()
