@@ -259,6 +259,15 @@ def main():
         run_multi(args, world, rank, (traffic, traffic_note, traffic_kern))
 
 
+def rank_capacity(n_local, G, npk, world):
+    """A rank engine's capacity hint: its batch, or enough for the rows it will own (npk pks drawn G
+    times, 1/world of them owned; the row store sizes its regions for hint / 16 rows), so the store
+    does not grow (k_rehash) inside the timed step."""
+    import math
+    rows = npk * (1.0 - math.exp(-G / max(1, npk))) / world
+    return int(max(n_local, 16 * rows * 1.1, 1))
+
+
 def run_rank_child(args, world):
     """(PMC child) one rank's local kernels of the N > 1 step on one GPU: rank 0's slice, the slot
     partition for `world` destinations, the unpack of an equal-size received slot buffer (its own
@@ -272,7 +281,7 @@ def run_rank_child(args, world):
     G = args.changes
     n_local = G // world
     npk = N_PK_C3 if strong else N_PK * world
-    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=max(n_local, 1), device=0)
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=rank_capacity(n_local, G, npk, world), device=0)
     eng.register_sites(synth.site_ids(N_ACTORS, 1))
     batch = synth.uniform_batch_torch(n_local, N_ACTORS, npk, N_COLS, seed=synth.config_seed(3), device="cuda:0",
                                       offset=0, global_n=G)
@@ -280,7 +289,7 @@ def run_rank_child(args, world):
     for _ in range(args.warmup + args.steps):
         eng.reset()
         recs, cnt = eng.partition_slots(batch, world, cap)
-        eng.apply_mapped(eng.unpack_slots(recs, world, cap, cnt))
+        eng.apply_slots(recs, world, cap, cnt)
     torch.cuda.synchronize()
     eng.close()
 
@@ -777,7 +786,7 @@ def run_multi(args, world, rank, pmc=(None, "not measured (--no-pmc)", None)):
         lo, hi = rank * G // world, (rank + 1) * G // world
         npk = N_PK * world
     n_local = hi - lo
-    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=max(n_local, 1), device=local)
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=rank_capacity(n_local, G, npk, world), device=local)
     eng.register_sites(synth.site_ids(N_ACTORS, 1))
     verify_sites(eng)
     # rank r holds the global batch's slice r (rank-major = application order)
@@ -797,8 +806,9 @@ def run_multi(args, world, rank, pmc=(None, "not measured (--no-pmc)", None)):
     overflows = []
 
     def step():
-        # stream-ordered: partition -> counts + slots all-to-all -> unpack -> merge, all queued on
-        # the engine's stream (no host wait between partition and merge)
+        # stream-ordered: partition -> counts + slots all-to-all -> merge from the received slots
+        # (corro_apply_slots: no unpack pass), all queued on the engine's stream (no host wait between
+        # partition and merge)
         eng.reset()
         overflows.append(distributed_apply_slots(eng, batch, cap))
 

@@ -35,6 +35,7 @@ EXPORTS = [
     "corro_bookie_seq_bookkeeping", "corro_bookie_buffered", "corro_bookie_buffered_versions",
     "corro_decode_frames", "corro_site_ids", "corro_packed_record_bytes", "corro_partition_packed",
     "corro_unpack_records", "corro_partition_slots", "corro_unpack_slots", "corro_apply_mapped", "corro_ctx_stream",
+    "corro_apply_slots", "corro_slots_flags_back",
     "corro_table_set_pk_interned", "corro_pk_keys", "corro_pk_keys_device", "corro_pk_bytes",
     "corro_pk_canonical", "corro_bookie_buffered_value", "corro_compute_needs_packed",
     "corro_booked_insert_db_batch", "corro_affinity_of_type", "corro_table_set_affinity", "corro_set_affinity_policy",
@@ -231,7 +232,9 @@ def lib():
         "corro_packed_record_bytes": (i32, [C.POINTER(Changes), vp]),
         "corro_partition_packed": (i32, [vp, C.POINTER(Changes), u32, vp, vp, vp]),
         "corro_unpack_records": (i32, [vp, vp, u64, u32, C.POINTER(Changes)]),
-        "corro_partition_slots": (i32, [vp, C.POINTER(Changes), u32, u64, vp, vp]),
+        "corro_partition_slots": (i32, [vp, C.POINTER(Changes), u32, u64, vp, vp, vp]),
+        "corro_apply_slots": (i32, [vp, vp, u32, u64, vp, C.POINTER(ApplyOut), vp]),
+        "corro_slots_flags_back": (i32, [vp, vp, u32, u64, vp, vp, vp, u64]),
         "corro_unpack_slots": (i32, [vp, vp, u32, u64, vp, C.POINTER(Changes), vp, vp]),
         "corro_apply_mapped": (i32, [vp, C.POINTER(Changes), vp, C.POINTER(ApplyOut)]),
         "corro_ctx_stream": (vp, [vp]),

@@ -1086,8 +1086,8 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
 
 static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, corro_apply_out *out) {
     if (in->n >= (1ULL << 31)) return fail(CORRO_E_RANGE, "at most 2^31-1 changes per batch");
-    if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
-        !in->val0)
+    if (!ctx->slot_rec && (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq ||
+                           !in->site || !in->val0))
         return fail(CORRO_E_INVALID, "a required batch array is NULL");
     if (mem != CORRO_MEM_HOST && mem != CORRO_MEM_DEVICE) return fail(CORRO_E_INVALID, "bad mem kind");
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
@@ -1122,6 +1122,13 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.vsz = in->val_size;
     }
     bd.n = n;
+    if (ctx->slot_rec) {  // slot mode (corro_apply_slots): one chunk, positions = slot indices
+        bd.slot_rec = static_cast<const SlotRec *>(ctx->slot_rec);
+        bd.slot_cnt = ctx->slot_cnt;
+        bd.slot_cap = ctx->slot_cap;
+        bd.slot_nsrc = ctx->slot_nsrc;
+        bd.slot_over = ctx->slot_over;
+    }
     // (a slot layout -- corro_apply_mapped -- may pass the chunk size by its padding: one chunk still)
     const uint64_t chunk_cap = corro_detail_chunk_changes(ctx) + (ctx->pm_slack ? corro_detail_chunk_changes(ctx) / 4 : 0);
     if (ctx->pm_ap) {  // position mode (agent): one chunk, per-position ts
@@ -1175,7 +1182,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.ts_pos = 1;
     }
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
-    const uint64_t chunk = ctx->pm_ap ? std::max<uint64_t>(n, 1) : corro_detail_chunk_changes(ctx);
+    const uint64_t chunk = ctx->pm_ap || ctx->slot_rec ? std::max<uint64_t>(n, 1) : corro_detail_chunk_changes(ctx);
     if (n > chunk) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
         hipLaunchKernelGGL(k_validate, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, bd,
@@ -1206,6 +1213,30 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         CORRO_HIP_TRY(hipStreamSynchronize(s));
     }
     return CORRO_OK;
+}
+
+// The received slots of the stream-ordered exchange merged where they lie: k_hist / k_scatter read the
+// 48-B records themselves (BatchDev slot mode), so the receiver runs no unpack pass.
+int corro_apply_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t cap, const uint64_t *src_counts_dev,
+                      corro_apply_out *out, uint32_t *overflow_dev) {
+    if (!ctx || !recs || !src_counts_dev) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nsrc == 0 || nsrc > 64) return fail(CORRO_E_RANGE, "1..64 source ranks");
+    if (cap == 0 || (uint64_t)nsrc * cap >= (1ULL << 31)) return fail(CORRO_E_RANGE, "slots: nsrc * cap < 2^31 records");
+    if ((uintptr_t)recs % 16) return fail(CORRO_E_INVALID, "slot records must be 16-byte aligned");
+    if (ctx->pm_ap || ctx->slot_rec) return fail(CORRO_E_INVALID, "a position map is already set on this context");
+    if (ctx->aff_any) return fail(CORRO_E_INVALID, "slots carry INTEGER values: no column affinity may convert them");
+    corro_changes in{};
+    in.n = (uint64_t)nsrc * cap;
+    ctx->slot_rec = recs;
+    ctx->slot_cnt = src_counts_dev;
+    ctx->slot_cap = (uint32_t)cap;
+    ctx->slot_nsrc = nsrc;
+    ctx->slot_over = overflow_dev;
+    const int rc = corro_apply_batch(ctx, &in, CORRO_MEM_DEVICE, out);
+    ctx->slot_rec = nullptr;
+    ctx->slot_cnt = nullptr;
+    ctx->slot_over = nullptr;
+    return rc;
 }
 
 int corro_apply_mapped(corro_ctx *ctx, const corro_changes *in, const uint32_t *ap, corro_apply_out *out) {

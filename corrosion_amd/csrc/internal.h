@@ -173,6 +173,11 @@ struct corro_ctx {
     const uint64_t *pm_ts = nullptr;
     uint64_t pm_n = 0;
     bool pm_slack = false;  // corro_apply_mapped: a slot layout's padding may pass the chunk size
+    // slot mode of the next apply (corro_apply_slots): the received slots merged where they lie
+    const void *slot_rec = nullptr;
+    const uint64_t *slot_cnt = nullptr;
+    uint32_t slot_cap = 0, slot_nsrc = 0;
+    uint32_t *slot_over = nullptr;
     bool apply_wrote = false;     // the current apply has launched its first merge kernel
     uint64_t heap_limit = 0;      // corro_ctx_set_store_limit (0: none)
     bool state_wide = false;      // some clock row holds a non-INTEGER value

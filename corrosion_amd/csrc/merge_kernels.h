@@ -223,6 +223,8 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t 
         for (uint32_t i = t; i < z.nsites; i += nt) z.dbv_batch[i] = 0;
     }
     for (uint32_t i = threadIdx.x; i < B; i += blockDim.x) hist[i] = 0;
+    const bool sover = in.slot_rec && slot_overflowed(in);
+    if (in.slot_rec && in.slot_over && blockIdx.x == 0 && threadIdx.x == 0) *in.slot_over = sover ? 1u : 0u;
     __syncthreads();
     const uint32_t begin = blockIdx.x * tile;
     const uint32_t end = min(in.n, begin + tile);
@@ -235,6 +237,12 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t 
 #pragma unroll
         for (int k = 0; k < HIST_U; k++) {
             const uint32_t i = min(base + k * blockDim.x + threadIdx.x, end - 1);
+            if (in.slot_rec) {  // (slot mode: the received record itself)
+                pk[k] = in.slot_rec[i].pk;
+                tc[k] = one_table ? 0u : in.slot_rec[i].tcid;
+                ap[k] = slot_valid(in, i, sover) ? 0u : AP_SKIP;
+                continue;
+            }
             pk[k] = in.pk[i];
             tc[k] = one_table ? 0u : in.tcid[i];
             ap[k] = in.ap && !in.ap_all ? in.ap[i] : 0u;
@@ -442,9 +450,31 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
     // (tiles start at multiples of 2 * blockDim.x, so pairs (2t, 2t+1) are 16-B aligned)
     // the PLAIN path needs an even tile length (pairs never straddle the tile end)
     const bool plain = PLAIN && ((end - begin) & 1u) == 0;
+    const bool sover = in.slot_rec && slot_overflowed(in);
     for (uint32_t base = begin; base < end; base += blockDim.x * SCAT_U) {
         Rec rr[SCAT_U];
-        if (plain) {
+        if (in.slot_rec) {  // slot mode: each lane's records straight from the received slots (3 x 16 B)
+#pragma unroll
+            for (int u = 0; u < SCAT_U; u++) {
+                const uint32_t i = base + (u / 2) * 2 * blockDim.x + 2 * threadIdx.x + (u & 1);
+                Rec &r = rr[u];
+                const uint32_t ic = min(i, end - 1);
+                const uint4 *q = reinterpret_cast<const uint4 *>(in.slot_rec + ic);
+                const uint4 x0 = q[0], x1 = q[1], x2 = q[2];
+                const bool ok = i < end && slot_valid(in, i, sover);
+                r.pk = ((uint64_t)x0.y << 32) | x0.x;
+                r.cv = (int64_t)(((uint64_t)x0.w << 32) | x0.z);
+                r.dbv = ok ? (int64_t)(((uint64_t)x1.y << 32) | x1.x) : 0;
+                r.v0 = ((uint64_t)x1.w << 32) | x1.z;
+                r.v1 = 0;
+                r.tcid = x2.x;
+                r.cl = x2.y;
+                r.seq = x2.z;
+                r.site = ok ? x2.w : 0xFFFFFFFFu;
+                r.meta = (uint32_t)CORRO_INTEGER;
+                r.pos = BATCH_POS | (ok ? i : AP_SKIP);
+            }
+        } else if (plain) {
 #pragma unroll
             for (int p = 0; p < SCAT_U / 2; p++) {
                 const uint32_t i = base + p * 2 * blockDim.x + 2 * threadIdx.x;
@@ -548,7 +578,7 @@ k_scatter(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, const 
         for (int u = 0; u < SCAT_U; u++) {
             const uint32_t i = base + (u / 2) * 2 * blockDim.x + 2 * threadIdx.x + (u & 1);
             Rec &r = rr[u];
-            const bool act = i < end && (!in.ap || (r.pos & 0x7FFFFFFFu) != (AP_SKIP & 0x7FFFFFFFu));
+            const bool act = i < end && (!(in.ap || in.slot_rec) || (r.pos & 0x7FFFFFFFu) != (AP_SKIP & 0x7FFFFFFFu));
             uint32_t idx = 0;
             if (act) {
                 // (the unpaired path of an INTEGER batch: its ts into v1 here)

@@ -140,12 +140,7 @@ k_part_scatter(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__re
 // Packed-record exchange format (one all-to-all of whole records instead of one per SoA field):
 // PLAIN batches (INTEGER values, no val1/val_type/val_len/ts arrays) use the 48-B record of
 // SURVEY §8(d); others a 80-B record that carries every optional field.
-struct __attribute__((aligned(16))) PackedRec48 {
-    uint64_t pk;
-    int64_t cv, dbv;
-    uint64_t v0;
-    uint32_t tcid, cl, seq, site;
-};
+using PackedRec48 = SlotRec;  // (rowhash.h: the receiver's apply reads it in slot mode)
 struct __attribute__((aligned(16))) PackedRec80 {
     uint64_t pk;
     int64_t cv, dbv;
@@ -552,7 +547,7 @@ extern "C" int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n
 extern "C" void *corro_ctx_stream(corro_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
 extern "C" int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, uint64_t cap, void *out,
-                                     uint64_t *counts_dev) {
+                                     uint64_t *counts_dev, uint32_t *perm_dev) {
     if (!ctx || !in || !out || !counts_dev) return fail(CORRO_E_INVALID, "NULL argument");
     if (nranks == 0 || nranks > (uint32_t)PART_MAX_RANKS) return fail(CORRO_E_RANGE, "1..64 ranks");
     if (in->n >= (1ULL << 31) || cap == 0 || (uint64_t)nranks * cap >= (1ULL << 31))
@@ -577,10 +572,36 @@ extern "C" int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, ui
     hipLaunchKernelGGL(k_part_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, counts_dev, cap);
     hipLaunchKernelGGL(k_part_pack<true>, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts, out,
-                       (uint32_t *)nullptr, cap);
+                       perm_dev, cap);
     CORRO_HIP_TRY(hipGetLastError());
     (void)d_tot;
     return CORRO_OK;  // (no host wait: everything is queued on ctx->stream)
+}
+
+// received impact flags -> the sender's input order: slot position p of destination d (p - d * cap <
+// counts[d]) held input change perm[p]
+__global__ void k_slots_back(const uint8_t *__restrict__ back, uint32_t nranks, uint64_t cap,
+                             const uint64_t *__restrict__ cnt, const uint32_t *__restrict__ perm, uint8_t *__restrict__ flags,
+                             uint64_t n) {
+    const uint64_t m = (uint64_t)nranks * cap;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < m; p += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = p / cap;
+        if (p - d * cap >= cnt[d]) continue;
+        const uint32_t i = perm[p];
+        if (i < n) flags[i] = back[p];
+    }
+}
+
+extern "C" int corro_slots_flags_back(corro_ctx *ctx, const uint8_t *back, uint32_t nranks, uint64_t cap,
+                                      const uint64_t *counts_dev, const uint32_t *perm_dev, uint8_t *flags, uint64_t n) {
+    if (!ctx || !back || !counts_dev || !perm_dev || (!flags && n)) return fail(CORRO_E_INVALID, "NULL argument");
+    if (nranks == 0 || nranks > (uint32_t)PART_MAX_RANKS || cap == 0) return fail(CORRO_E_RANGE, "1..64 ranks, cap >= 1");
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t m = (uint64_t)nranks * cap;
+    hipLaunchKernelGGL(k_slots_back, dim3((uint32_t)std::min<uint64_t>((m + 255) / 256, 8192)), dim3(256), 0, ctx->stream,
+                       back, nranks, cap, counts_dev, perm_dev, flags, n);
+    CORRO_HIP_TRY(hipGetLastError());
+    return CORRO_OK;  // (queued on ctx->stream)
 }
 
 extern "C" int corro_unpack_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t cap,

@@ -23,8 +23,10 @@
 //                everything a later prober compares against.
 //   scans        claims -> new ids (table size + rank), their bytes -> arena offsets
 //   k_pk_commit  keys; each claim's canonical bytes, offset and hash appended, its slot -> the id
-// The slots are sized at twice the keys the table may hold after the call; a probe that runs past
-// PK_MAX_PROBE slots marks the call for a retry with a larger table (rebuilt from the arena).
+// The slots (32 B: claim word, length, up to 23 canonical bytes inline) are sized by the keys the
+// table holds (load <= 1/2 with a share of new ones), not by the changes of a call; a probe that runs
+// past PK_MAX_PROBE slots marks the call for a retry with a table four times larger (rebuilt from the
+// arena).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -194,7 +196,18 @@ int prim_inclusive_scan_u32_u64(void *temp, size_t *temp_bytes, const uint32_t *
 namespace {
 
 constexpr uint32_t PK_NEW = 0x80000000u;   // slot / owner word: a claim by change (word & ~PK_NEW)
-constexpr uint32_t PK_MAX_PROBE = 1024;    // past this many slots a probe asks for a larger table
+constexpr uint32_t PK_INLINE = 23;         // canonical keys of at most this many bytes live in their slot
+
+// One slot, 32 B (one half of a cache line): the claim word (tag << 32 | id, or | PK_NEW | change while a
+// call's new key is being interned) and, once committed, the key's length and -- for a short key -- its
+// canonical bytes, so a lookup of an existing key reads one line (the arena only for longer keys).
+struct alignas(32) PkSlot {
+    unsigned long long w;
+    uint8_t len;
+    uint8_t b[PK_INLINE];
+};
+static_assert(sizeof(PkSlot) == 32, "pk slot size");
+constexpr uint32_t PK_MAX_PROBE = 256;     // past this many slots a probe asks for a larger table
 constexpr uint64_t PK_SCRATCH = 1ULL << 63;  // cref: canonical bytes in the scratch, not the input
 
 __device__ inline uint32_t pk_wave_sum(uint32_t x) {
@@ -330,7 +343,7 @@ struct PkArgs {
     uint64_t *noff;     // inclusive scan of newl
     unsigned long long *ctl;  // [0] bad [1] max canonical length [2] non-canonical inputs [3] probe overflow
     // the table
-    unsigned long long *slots;
+    PkSlot *slots;
     uint64_t smask;
     uint64_t *koff;
     uint8_t *kbytes;
@@ -359,17 +372,36 @@ __device__ inline const uint8_t *pk_cbytes(const PkArgs &a, uint64_t j) {
 
 #define PK_LOOP(i) for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x)
 
+// A pk of at most PK_STAGE bytes is parsed from a copy in LDS: the parse reads its bytes in a data-
+// dependent order (column types, then lengths), which from HBM is a chain of dependent loads per byte
+// (2.1 ms for config 2's 2^26 pks); the copy's loads are independent and issue at once.
+constexpr uint32_t PK_STAGE = 32;
+
 __global__ void __launch_bounds__(256) k_pk_parse(PkArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_pk[256 * PK_STAGE];
+    uint8_t *mine_lds = s_pk + threadIdx.x * PK_STAGE;
     uint32_t nbad = 0, mx = 0, nnc = 0;
     PK_LOOP(i) {
         const uint8_t *p = nullptr;
         uint64_t len = 0;
         uint32_t cl = 0, nc = 0;
         if (pk_src(a, i, p, len)) {
-            CanonOut<false> co{p, len, nullptr};
+            const uint8_t *q = p;
+            if (len <= PK_STAGE) {
+                uint8_t b[PK_STAGE];
+#pragma unroll
+                for (uint32_t k = 0; k < PK_STAGE; k++) b[k] = k < len ? p[k] : 0;
+                uint32_t *w = reinterpret_cast<uint32_t *>(mine_lds);
+#pragma unroll
+                for (uint32_t k = 0; k < PK_STAGE / 4; k++)
+                    w[k] = (uint32_t)b[4 * k] | ((uint32_t)b[4 * k + 1] << 8) | ((uint32_t)b[4 * k + 2] << 16) |
+                           ((uint32_t)b[4 * k + 3] << 24);
+                q = mine_lds;
+            }
+            CanonOut<false> co{q, len, nullptr};
             bool one = false;
             int64_t v = 0;
-            const bool ok = pk_canon_dev<false>(p, len, co, one, v) && co.o < (1ULL << 24);
+            const bool ok = pk_canon_dev<false>(q, len, co, one, v) && co.o < (1ULL << 24);
             if (!ok || (!a.interned && !one)) {
                 nbad++;
                 if (a.bad) a.bad[i] = 1;
@@ -425,22 +457,61 @@ __device__ inline bool pk_eq(const uint8_t *x, const uint8_t *y, uint32_t n) {
 __device__ inline uint64_t pk_slot_of(uint64_t h, uint64_t mask) { return (h ^ (h >> 31)) & mask; }
 __device__ inline uint32_t pk_tag(uint64_t h) { return (uint32_t)(h >> 32) | 1u; }
 
+// A short key (<= PK_INLINE bytes) as the three words of a slot's bytes 8..31: length, then the bytes,
+// zero past the length. Its byte loads are independent (predicated, all issued at once), and a key is
+// then compared by three word compares instead of a loop of dependent byte loads.
+struct PkWords {
+    uint64_t q[3];
+};
+__device__ inline PkWords pk_words(const uint8_t *p, uint32_t cl) {
+    uint8_t b[PK_INLINE];
+#pragma unroll
+    for (uint32_t k = 0; k < PK_INLINE; k++) b[k] = k < cl ? p[k] : 0;
+    PkWords w;
+    w.q[0] = cl;
+#pragma unroll
+    for (uint32_t k = 0; k < 7; k++) w.q[0] |= (uint64_t)b[k] << (8 * (k + 1));
+    w.q[1] = w.q[2] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        w.q[1] |= (uint64_t)b[7 + k] << (8 * k);
+        w.q[2] |= (uint64_t)b[15 + k] << (8 * k);
+    }
+    return w;
+}
+__device__ inline bool pk_words_eq(const PkWords &x, const PkSlot *ps) {
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(ps) + 1;  // (bytes 8..31: len, b[0..22])
+    return q[0] == x.q[0] && q[1] == x.q[1] && q[2] == x.q[2];
+}
+
+// a committed key against my canonical bytes: inline in the slot (the line the claim word is on) or in
+// the arena
+__device__ inline bool pk_eq_slot(const PkArgs &a, const PkSlot *ps, uint32_t id, const uint8_t *mine, const PkWords &mw,
+                                  uint32_t cl, uint64_t h) {
+    if (cl <= PK_INLINE) return pk_words_eq(mw, ps);
+    return a.koff[id + 1] - a.koff[id] == cl && a.khash[id] == h && pk_eq(a.kbytes + a.koff[id], mine, cl);
+}
+
 __global__ void __launch_bounds__(256) k_pk_probe(PkArgs a) {
     PK_LOOP(i) {
         a.newf[i] = 0;
         a.newl[i] = 0;
         const uint32_t cl = a.clen[i];
         if (!cl) continue;
+        if (*(volatile unsigned long long *)&a.ctl[3]) continue;  // (retrying: a cached read, seen late is fine)
         const uint64_t h = a.h[i];
         const uint32_t tag = pk_tag(h);
         const uint8_t *mine = pk_cbytes(a, i);
+        PkWords mw{};
+        if (cl <= PK_INLINE) mw = pk_words(mine, cl);
         uint64_t sl = pk_slot_of(h, a.smask);
         uint32_t owner = ~0u;
         for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = (sl + 1) & a.smask) {
-            unsigned long long w = __hip_atomic_load(&a.slots[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            PkSlot *ps = a.slots + sl;
+            unsigned long long w = __hip_atomic_load(&ps->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (w == 0) {
                 const unsigned long long want = ((unsigned long long)tag << 32) | (PK_NEW | (uint32_t)i);
-                w = atomicCAS(&a.slots[sl], 0ULL, want);
+                w = atomicCAS(&ps->w, 0ULL, want);
                 if (w == 0) {  // claimed: a new key, its canonical bytes already where cref says
                     owner = PK_NEW | (uint32_t)i;
                     a.slotix[i] = (uint32_t)sl;
@@ -454,9 +525,15 @@ __global__ void __launch_bounds__(256) k_pk_probe(PkArgs a) {
             bool eq;
             if (v & PK_NEW) {
                 const uint32_t j = v & ~PK_NEW;
-                eq = a.clen[j] == cl && a.h[j] == h && pk_eq(pk_cbytes(a, j), mine, cl);
+                eq = a.clen[j] == cl && a.h[j] == h;
+                if (eq && cl <= PK_INLINE) {
+                    const PkWords jw = pk_words(pk_cbytes(a, j), cl);
+                    eq = jw.q[0] == mw.q[0] && jw.q[1] == mw.q[1] && jw.q[2] == mw.q[2];
+                } else if (eq) {
+                    eq = pk_eq(pk_cbytes(a, j), mine, cl);
+                }
             } else {
-                eq = a.koff[v + 1] - a.koff[v] == cl && a.khash[v] == h && pk_eq(a.kbytes + a.koff[v], mine, cl);
+                eq = pk_eq_slot(a, ps, v, mine, mw, cl, h);  // (committed by an earlier kernel: plain loads)
             }
             if (eq) {
                 owner = v;
@@ -466,6 +543,12 @@ __global__ void __launch_bounds__(256) k_pk_probe(PkArgs a) {
         if (owner == ~0u) atomicOr(&a.ctl[3], 1ULL);  // (the table is too full: the call retries)
         a.owner[i] = owner;
     }
+}
+
+__device__ inline void pk_slot_fill(PkSlot &sl, const uint8_t *src, uint32_t cl) {
+    sl.len = (uint8_t)min(cl, 255u);
+    if (cl <= PK_INLINE)
+        for (uint32_t k = 0; k < cl; k++) sl.b[k] = src[k];
 }
 
 __global__ void __launch_bounds__(256) k_pk_commit(PkArgs a) {
@@ -481,18 +564,23 @@ __global__ void __launch_bounds__(256) k_pk_commit(PkArgs a) {
         for (uint32_t k = 0; k < cl; k++) a.kbytes[at + k] = src[k];
         a.koff[id + 1] = at + cl;
         a.khash[id] = a.h[i];
-        a.slots[a.slotix[i]] = ((unsigned long long)pk_tag(a.h[i]) << 32) | id;
+        PkSlot &sl = a.slots[a.slotix[i]];
+        pk_slot_fill(sl, src, cl);
+        sl.w = ((unsigned long long)pk_tag(a.h[i]) << 32) | id;
     }
 }
 
 // the slots rebuilt from the keys (a larger table, or a retry after a probe overflow)
-__global__ void __launch_bounds__(256) k_pk_rehash(unsigned long long *slots, uint64_t mask, const uint64_t *khash,
-                                                   uint64_t nkeys) {
+__global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t mask, const uint64_t *khash,
+                                                   const uint64_t *koff, const uint8_t *kbytes, uint64_t nkeys) {
     for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < nkeys; id += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t h = khash[id];
         const unsigned long long w = ((unsigned long long)pk_tag(h) << 32) | id;
         for (uint64_t sl = pk_slot_of(h, mask);; sl = (sl + 1) & mask)
-            if (atomicCAS(&slots[sl], 0ULL, w) == 0ULL) break;
+            if (atomicCAS(&slots[sl].w, 0ULL, w) == 0ULL) {
+                pk_slot_fill(slots[sl], kbytes + koff[id], (uint32_t)(koff[id + 1] - koff[id]));
+                break;
+            }
     }
 }
 
@@ -500,17 +588,17 @@ __global__ void __launch_bounds__(256) k_pk_rehash(unsigned long long *slots, ui
 
 dim3 pk_grid(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 16384))); }
 
-// slots for `want` keys at load <= 1/2, rebuilt from the arena
-int pk_slots_resize(corro_ctx *ctx, PkTable &t, uint64_t want) {
+// slots for `want` keys at load <= 1/2 (at least `min_slots`), rebuilt from the arena
+int pk_slots_resize(corro_ctx *ctx, PkTable &t, uint64_t want, uint64_t min_slots = 0) {
     uint64_t ns = 1ULL << 12;
-    while (ns < 2 * want) ns <<= 1;
+    while (ns < 2 * want || ns < min_slots) ns <<= 1;
     if (ns >= (1ULL << 32)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
     hipStream_t s = ctx->stream;
     DevBuf nb;
-    if (int rc = nb.ensure(ns * 8)) return rc;
-    CORRO_HIP_TRY(hipMemsetAsync(nb.p, 0, ns * 8, s));
-    if (t.n) hipLaunchKernelGGL(k_pk_rehash, pk_grid(t.n), dim3(256), 0, s, nb.as<unsigned long long>(), ns - 1,
-                                t.d_hash.as<uint64_t>(), t.n);
+    if (int rc = nb.ensure(ns * sizeof(PkSlot))) return rc;
+    CORRO_HIP_TRY(hipMemsetAsync(nb.p, 0, ns * sizeof(PkSlot), s));
+    if (t.n) hipLaunchKernelGGL(k_pk_rehash, pk_grid(t.n), dim3(256), 0, s, nb.as<PkSlot>(), ns - 1,
+                                t.d_hash.as<uint64_t>(), t.d_off.as<uint64_t>(), t.d_bytes.as<uint8_t>(), t.n);
     CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     t.d_slots.release();
@@ -595,9 +683,15 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
         CORRO_HIP_TRY(hipGetLastError());
     }
     if (t.n + n > ((uint64_t)PK_NEW - 1)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
-    // slots for every key the call might add (at load <= 1/2)
-    if (t.nslots < 2 * (t.n + n)) TRY_PK(pk_slots_resize(ctx, t, t.n + n));
-    a.slots = t.d_slots.as<unsigned long long>();
+    // slots for the held keys and a share of the call's (load <= 1/2); a call that brings more new keys
+    // than that overflows a probe and retries with a table four times larger (rebuilt from the arena).
+    // Sized by keys, not by changes: a warm call (every key held) probes a table that stays in the MALL.
+    // (load <= 1/2 for the held keys, <= 3/4 with the call's estimated new keys: a sixteenth of its
+    // changes into an empty table, a sixty-fourth into one that holds keys)
+    const uint64_t est_new = std::max<uint64_t>(t.n ? n / 64 : n / 16, 1ULL << 16);
+    const uint64_t want = std::max<uint64_t>(t.n, (t.n + est_new) * 2 / 3);
+    if (t.nslots < 2 * want) TRY_PK(pk_slots_resize(ctx, t, want));
+    a.slots = t.d_slots.as<PkSlot>();
     a.smask = t.nslots - 1;
     a.koff = t.d_off.as<uint64_t>();
     a.kbytes = t.d_bytes.as<uint8_t>();
@@ -611,19 +705,22 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
         CORRO_HIP_TRY(hipStreamSynchronize(s));
         if (!ctl[3]) break;
         // a probe ran long: rebuild a table four times larger from the committed keys and probe again
-        if (attempt == 2) return fail(CORRO_E_DEVICE, "internal: interned pk probes do not terminate");
-        TRY_PK(pk_slots_resize(ctx, t, 4 * (t.n + n)));
-        a.slots = t.d_slots.as<unsigned long long>();
+        if (attempt == 6) return fail(CORRO_E_DEVICE, "internal: interned pk probes do not terminate");
+        TRY_PK(pk_slots_resize(ctx, t, t.n, 4 * t.nslots));
+        a.slots = t.d_slots.as<PkSlot>();
         a.smask = t.nslots - 1;
         CORRO_HIP_TRY(hipMemsetAsync(a.ctl + 3, 0, 8, s));
     }
     TRY_PK(prim_inclusive_scan_u32(d_temp, &temp, a.newf, a.rank, (uint32_t)n, s));
-    TRY_PK(prim_inclusive_scan_u32_u64(d_temp, &temp, a.newl, a.noff, n, s));
     uint32_t nnew = 0;
     uint64_t nb = 0;
     CORRO_HIP_TRY(hipMemcpyAsync(&nnew, a.rank + (n - 1), 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(&nb, a.noff + (n - 1), 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (nnew) {  // (a warm call -- every key held -- needs no byte offsets)
+        TRY_PK(prim_inclusive_scan_u32_u64(d_temp, &temp, a.newl, a.noff, n, s));
+        CORRO_HIP_TRY(hipMemcpyAsync(&nb, a.noff + (n - 1), 8, hipMemcpyDeviceToHost, s));
+        CORRO_HIP_TRY(hipStreamSynchronize(s));
+    }
     // room for the new keys (offsets n + 1, hashes, bytes), keeping the committed ones
     const uint64_t nk = t.n + nnew, nbytes = t.nbytes + nb;
     if (int rc = grow_keep(t.d_off, (nk + 1) * 8, (t.n + 1) * 8 * (t.d_off.p ? 1 : 0), s)) return rc;
@@ -638,6 +735,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     t.n = nk;
     t.nbytes = nbytes;
+    if (2 * t.n > t.nslots) TRY_PK(pk_slots_resize(ctx, t, 2 * t.n));  // (the next call starts at load <= 1/4)
     return CORRO_OK;
 }
 

@@ -7,6 +7,14 @@
 
 namespace corro {
 
+// One change as the multi-GPU exchange ships it (SURVEY §8(d)'s 48 B; partition.hip PackedRec48).
+struct alignas(16) SlotRec {
+    uint64_t pk;
+    int64_t cv, dbv;
+    uint64_t v0;
+    uint32_t tcid, cl, seq, site;
+};
+
 struct BatchDev {
     const uint64_t *pk;
     const uint32_t *tcid;
@@ -41,7 +49,26 @@ struct BatchDev {
     // already holds instead of a random load from a per-position array. ts_pos: ts is indexed by
     // application position (ap), else by input index. (ts_v1 bit 1: ts is 16-B aligned, paired loads)
     uint32_t ts_v1, ts_pos;
+    // slot mode (corro_apply_slots: the receiver of the stream-ordered exchange merges the received
+    // 48-B records where they lie): change i is slot_rec[i], applied at position i when its source's
+    // slot holds it (i % cap < slot_cnt[i / cap]) and no source overflowed its slot; the SoA arrays
+    // above are not read. k_hist reports an overflow in *slot_over.
+    const SlotRec *slot_rec;
+    const uint64_t *slot_cnt;
+    uint32_t slot_cap, slot_nsrc;
+    uint32_t *slot_over;
 };
+
+// slot mode: does any source's count pass the slot (every record is then skipped)?
+__device__ inline bool slot_overflowed(const BatchDev &in) {
+    bool over = false;
+    for (uint32_t s = 0; s < in.slot_nsrc; s++) over |= in.slot_cnt[s] > in.slot_cap;
+    return over;
+}
+__device__ inline bool slot_valid(const BatchDev &in, uint32_t i, bool over) {
+    const uint32_t s = i / in.slot_cap;
+    return !over && s < in.slot_nsrc && (uint64_t)(i - s * in.slot_cap) < in.slot_cnt[s];
+}
 constexpr uint32_t AP_SKIP = 0xFFFFFFFFu;
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

@@ -119,50 +119,86 @@ def slot_cap(n_max, world):
     return int(share + 8.0 * share ** 0.5 + 256)
 
 
-def distributed_apply_slots(engine, batch, cap, group=None):
-    """The stream-ordered form of distributed_apply for INTEGER batches (no impact flags): partition
-    into fixed slots of `cap` 48-B records per destination (slot_cap; the same cap on every rank), the
-    per-slot counts and the slots in two all-to-alls with EQUAL splits, unpack at the same indices and
-    a mapped merge that skips the padding -- every step queued on the engine's stream (the collectives
-    run under torch.cuda.stream(engine.stream())), so no host wait separates partition and merge.
+def distributed_apply_slots(engine, batch, cap, group=None, impact=False):
+    """The stream-ordered form of distributed_apply for INTEGER batches: partition into fixed slots of
+    `cap` 48-B records per destination (slot_cap; the same cap on every rank), the per-slot counts and
+    the slots in two all-to-alls with EQUAL splits, and the receiver's merge straight from the received
+    slots (corro_apply_slots: its histogram and scatter read the records themselves -- no unpack pass)
+    -- every step queued on the engine's stream (the collectives run under
+    torch.cuda.stream(engine.stream())), so no host wait separates partition, exchange and merge.
+    impact=True (process_multiple_changes always asks for crsql_rows_impacted(), util.rs:1247): the
+    receiver's flags come out at slot positions, go back to their senders with a third equal-split
+    all-to-all on the same stream, and the partition's permutation puts them in the caller's order
+    (corro_slots_flags_back) -- still no host wait.
     A rank whose incoming slot overflowed merges nothing in that pass; after it, one tiny all-reduce
     tells every rank, and the exact-size exchange (distributed_apply) repeats for those ranks only.
-    Returns the number of ranks that overflowed (0 in the common case)."""
+    Returns the number of ranks that overflowed (0 in the common case), and with impact=True the flags
+    (uint8 CUDA tensor, this rank's changes in its own order) as a second value."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     if world == 1:
-        engine.apply(batch)
-        return 0
+        imp = engine.apply(batch, impact=impact)
+        return (0, imp) if impact else 0
+    n = int(batch["pk"].shape[0])
     st = engine.stream()
     st.wait_stream(torch.cuda.current_stream())  # the batch's producer (device-side wait)
     gloo = dist.get_backend(group) == "gloo"
-    with torch.cuda.stream(st):
-        recs, cnt = engine.partition_slots(batch, world, cap)
+
+    def a2a(dst, src):
         if gloo:  # (no device all-to-all in gloo: rehearsals stage through host memory)
-            rc = torch.empty(world, dtype=torch.int64)
-            dist.all_to_all_single(rc, cnt.cpu(), group=group)
-            got = torch.empty(recs.numel(), dtype=torch.uint8)
-            dist.all_to_all_single(got, recs.cpu(), group=group)
-            rcnt, got = rc.to(recs.device), got.to(recs.device)
+            h = torch.empty(src.numel(), dtype=src.dtype)
+            dist.all_to_all_single(h, src.cpu(), group=group)
+            dst.copy_(h.to(dst.device))
         else:
-            rcnt = torch.empty_like(cnt)
-            dist.all_to_all_single(rcnt, cnt, group=group)
-            got = torch.empty_like(recs)
-            dist.all_to_all_single(got, recs, group=group)
-        mine = engine.unpack_slots(got, world, cap, rcnt)
-        engine.apply_mapped(mine)
-        over = mine["overflow"].to(torch.int64)  # (on the engine's stream, where unpack_slots wrote it)
-    torch.cuda.current_stream().wait_stream(st)  # (the caller's stream reads `over` and the state next)
+            dist.all_to_all_single(dst, src, group=group)
+
+    with torch.cuda.stream(st):
+        perm = torch.empty(world * cap, dtype=torch.int32, device=batch["pk"].device) if impact else None
+        recs, cnt = engine.partition_slots(batch, world, cap, perm=perm)
+        rcnt = torch.empty_like(cnt)
+        a2a(rcnt, cnt)
+        got = torch.empty_like(recs)
+        a2a(got, recs)
+        imp_slots, over = engine.apply_slots(got, world, cap, rcnt, impact=impact)
+        flags = None
+        if impact:
+            back = torch.empty_like(imp_slots)
+            a2a(back, imp_slots)
+            flags = engine.slots_flags_back(back, world, cap, cnt, perm, n)
+        over = over.to(torch.int64)  # (on the engine's stream, where the apply wrote it)
+    torch.cuda.current_stream().wait_stream(st)  # (the caller's stream reads `over`, the flags and the state next)
     tot = over.cpu() if gloo else over.clone()
     dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
     nover = int(tot.item())
     if nover:
-        recs2, rb, counts, _ = engine.partition_packed(batch, world)
-        got2, _rc2 = exchange_records(recs2, rb, counts, group)
-        if int(over.item()):
-            engine.apply(engine.unpack_records(got2, rb))
-    return nover
+        recs2, rb, counts, perm2 = engine.partition_packed(batch, world, with_perm=impact)
+        got2, rc2 = exchange_records(recs2, rb, counts, group)
+        mine = int(over.item())
+        imp2 = engine.apply(engine.unpack_records(got2, rb), impact=impact) if mine else None
+        if impact:  # every rank takes part in the flags' way back (the overflowed ones send real flags)
+            dev = batch["pk"].device
+            send = imp2[:sum(rc2)].contiguous() if mine else torch.zeros(sum(rc2), dtype=torch.uint8, device=dev)
+            back2 = torch.empty(sum(counts), dtype=torch.uint8, device=dev)
+            if gloo:
+                b2 = torch.empty(sum(counts), dtype=torch.uint8)
+                dist.all_to_all_single(b2, send.cpu(), [int(c) for c in counts], rc2, group=group)
+                back2 = b2.to(dev)
+            else:
+                dist.all_to_all_single(back2, send, [int(c) for c in counts], rc2, group=group)
+            # flags from destinations that overflowed replace the slot pass's (which applied nothing there)
+            dst_over = torch.zeros(world, dtype=torch.int64)
+            ov = over.cpu() if gloo else over
+            allov = [torch.zeros_like(ov) for _ in range(world)]
+            dist.all_gather(allov, ov, group=group)
+            dst_over = torch.cat([x.cpu() for x in allov]).tolist()
+            start = 0
+            p2 = perm2.long()
+            for d, c in enumerate(counts):
+                if dst_over[d]:
+                    flags[p2[start:start + int(c)]] = back2[start:start + int(c)]
+                start += int(c)
+    return (nover, flags) if impact else nover
 
 
 def site_digest(engine):

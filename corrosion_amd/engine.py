@@ -465,7 +465,7 @@ class MergeEngine:
             self._tstream = torch.cuda.ExternalStream(L.lib().corro_ctx_stream(self._h), device=self.device)
         return self._tstream
 
-    def partition_slots(self, batch, nranks, cap, out=None, counts=None):
+    def partition_slots(self, batch, nranks, cap, out=None, counts=None, perm=None):
         """Stable pk-hash partition of an INTEGER device batch into fixed slots of `cap` 48-B records
         per destination (corro_partition_slots): returns (uint8 tensor of nranks * cap * 48, int64
         tensor of the true per-destination counts) -- both written on the engine's stream, nothing
@@ -477,8 +477,37 @@ class MergeEngine:
             out = torch.empty(nranks * cap * 48, dtype=torch.uint8, device=dev)
         if counts is None:
             counts = torch.empty(nranks, dtype=torch.int64, device=dev)
-        L.check(L.lib().corro_partition_slots(self._h, C.byref(s), nranks, cap, out.data_ptr(), counts.data_ptr()))
+        L.check(L.lib().corro_partition_slots(self._h, C.byref(s), nranks, cap, out.data_ptr(), counts.data_ptr(),
+                                              perm.data_ptr() if perm is not None else None))
         return out, counts
+
+    def apply_slots(self, recs, nsrc, cap, src_counts, impact=False, overflow=None):
+        """corro_apply_slots: merge received slots (nsrc * cap 48-B records, a uint8 CUDA tensor) where
+        they lie -- no unpack pass. Returns (impact flags by slot position, a uint8 CUDA tensor of
+        nsrc * cap, or None; overflow int32 CUDA tensor [1]: 1 when a source overflowed its slot and
+        nothing was applied)."""
+        import torch
+        n = nsrc * cap
+        dev = recs.device
+        if overflow is None:
+            overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+        o = L.ApplyOut()
+        imp = None
+        if impact:
+            imp = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+            o.impact = imp.data_ptr()
+        L.check(L.lib().corro_apply_slots(self._h, recs.data_ptr(), nsrc, cap, src_counts.data_ptr(), C.byref(o),
+                                          overflow.data_ptr()))
+        return (imp[:n] if impact else None), overflow
+
+    def slots_flags_back(self, back, nranks, cap, counts, perm, n):
+        """corro_slots_flags_back: the all-to-all of the receivers' slot-position flags -> this sender's
+        per-input-change flags (uint8 CUDA tensor of n), queued on the engine's stream."""
+        import torch
+        flags = torch.zeros(max(n, 1), dtype=torch.uint8, device=back.device)
+        L.check(L.lib().corro_slots_flags_back(self._h, back.data_ptr(), nranks, cap, counts.data_ptr(), perm.data_ptr(),
+                                               flags.data_ptr(), n))
+        return flags[:n]
 
     def unpack_slots(self, recs, nsrc, cap, src_counts, out=None):
         """Received slots -> (SoA device batch of nsrc * cap changes at the same indices, ap int32

@@ -326,7 +326,9 @@ int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n, uint32_t 
  * launch is queued on the context's stream (corro_ctx_stream), so an all-to-all with EQUAL splits
  * of cap records (RCCL on that stream) needs no host-side sizes. PLAIN batches only (48-B records). */
 int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, uint64_t cap, void *out,
-                          uint64_t *counts_dev);
+                          uint64_t *counts_dev, uint32_t *perm_dev);
+/* (perm_dev, optional DEVICE u32 of nranks * cap: perm_dev[slot position] = the input index packed there,
+ * for the impact flags coming back, corro_slots_flags_back.) */
 /* Received slots (nsrc slots of cap records, src_counts_dev[s] = DEVICE count source s sent) ->
  * the SoA batch at the same indices (device, nsrc * cap each) and ap[i] = i for a received record,
  * CORRO_AP_SKIP for a slot's padding; *overflow_dev (device u32) = 1 when a source sent more than
@@ -338,6 +340,18 @@ int corro_unpack_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t
 /* corro_apply_batch over a DEVICE batch whose changes i with ap[i] == CORRO_AP_SKIP are not applied
  * (the others apply in index order): the slot layout above, merged without compacting it. */
 int corro_apply_mapped(corro_ctx *ctx, const corro_changes *in, const uint32_t *ap, corro_apply_out *out);
+/* The receiver's merge without the unpack: the received slots (recs: nsrc * cap 48-B records, DEVICE) are
+ * read by the apply itself (equal to corro_unpack_slots + corro_apply_mapped). out->impact (DEVICE, nsrc *
+ * cap bytes) gets each received record's flag at its slot position -- padding 0 -- ready to go back to
+ * the senders with one more equal-split all-to-all. *overflow_dev (DEVICE u32) = 1 when a source overflowed
+ * its slot (nothing is then applied). Synchronous, like corro_apply_batch. INTEGER batches, no affinity. */
+int corro_apply_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t cap, const uint64_t *src_counts_dev,
+                      corro_apply_out *out, uint32_t *overflow_dev);
+/* The senders' side of those flags: back (DEVICE, nranks * cap, the all-to-all of every receiver's
+ * out->impact) -> flags[i] (DEVICE, n) of input change i, through the partition's perm_dev and counts_dev.
+ * Queued on the context's stream. */
+int corro_slots_flags_back(corro_ctx *ctx, const uint8_t *back, uint32_t nranks, uint64_t cap, const uint64_t *counts_dev,
+                           const uint32_t *perm_dev, uint8_t *flags, uint64_t n);
 /* The HIP stream every launch of the context is queued on (a hipStream_t), for callers that order
  * their own collectives (RCCL) with the engine's kernels without a host wait. */
 void *corro_ctx_stream(corro_ctx *ctx);

@@ -239,7 +239,7 @@ def test_partition_var_routes_unregistered_table_ids():
 NS = 50000
 
 
-def _slots_worker(rank, world, port, outdir, cap_scale):
+def _slots_worker(rank, world, port, outdir, cap_scale, impact=False):
     import torch.distributed as dist
     import corrosion_amd as ca
     from corrosion_amd.dist import distributed_apply_slots, rank_of_np, slot_cap
@@ -251,7 +251,10 @@ def _slots_worker(rank, world, port, outdir, cap_scale):
     eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS, device=0)
     eng.register_sites(synth.site_ids(16, 5))
     cap = max(1, int(slot_cap(hi - lo, world) * cap_scale))
-    nover = distributed_apply_slots(eng, _to_dev({k: v[lo:hi] for k, v in full.items()}), cap)
+    res = distributed_apply_slots(eng, _to_dev({k: v[lo:hi] for k, v in full.items()}), cap, impact=impact)
+    nover = res[0] if impact else res
+    if impact:
+        np.save(os.path.join(outdir, f"simp{rank}.npy"), res[1].cpu().numpy())
     rows = eng.export()
     assert (rank_of_np(rows["table_cid"], rows["pk"], world) == rank).all()
     np.save(os.path.join(outdir, f"srows{rank}.npy"), np.array(rows_to_tuples(rows, with_ts=True), dtype=object),
@@ -262,15 +265,18 @@ def _slots_worker(rank, world, port, outdir, cap_scale):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("impact", [False, True], ids=["no_impacts", "impacts"])
 @pytest.mark.parametrize("cap_scale", [1.0, 0.3], ids=["slots_fit", "slots_overflow_repeat"])
-def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale):
-    """distributed_apply_slots: fixed slots, equal-split all-to-alls on the engine's stream, a mapped
-    merge that skips the padding; with slots too small (0.3 x) every rank overflows, merges nothing in
-    the slot pass and repeats with the exact-size exchange -- the union of the rank states equals one
-    engine's merge of the whole batch either way."""
+def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale, impact):
+    """distributed_apply_slots: fixed slots, equal-split all-to-alls on the engine's stream, the merge
+    straight from the received slots (corro_apply_slots: no unpack pass, padding skipped); with slots
+    too small (0.3 x) every rank overflows, merges nothing in the slot pass and repeats with the
+    exact-size exchange -- the union of the rank states equals one engine's merge of the whole batch
+    either way. With impacts the flags come back to their senders on the stream (a third equal-split
+    all-to-all + the partition's permutation) and equal the single engine's, in each rank's order."""
     import corrosion_amd as ca
     world = 2
-    mp.spawn(_slots_worker, args=(world, _free_port(), str(tmp_path), cap_scale), nprocs=world, join=True)
+    mp.spawn(_slots_worker, args=(world, _free_port(), str(tmp_path), cap_scale, impact), nprocs=world, join=True)
     got = []
     for r in range(world):
         got += [tuple(x) for x in np.load(tmp_path / f"srows{r}.npy", allow_pickle=True)]
@@ -280,8 +286,11 @@ def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale):
     e = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS)
     e.register_sites(synth.site_ids(16, 5))
     batch = synth.uniform_batch(NS, 16, 4000, 4, 77)
-    e.apply(batch)
+    want_imp = e.apply(batch, impact=True)
     assert sorted(got) == rows_to_tuples(e.export(), with_ts=True)
+    if impact:
+        got_imp = np.concatenate([np.load(tmp_path / f"simp{r}.npy") for r in range(world)])
+        assert np.array_equal(got_imp, want_imp)
     dbv = np.max([np.load(tmp_path / f"sdbv{r}.npy") for r in range(world)], axis=0)
     assert list(dbv) == list(e.db_versions())
     f = O.Fold(synth.site_ids(16, 5))  # (the single engine, so the ranks' union, against the oracle)
