@@ -629,28 +629,31 @@ def agent_e2e(eng, batch, n, agent_ms=None, reps=3):
             torch.cuda.synchronize()
             ms.append((time.perf_counter() - t0) * 1e3)
             del bk
+        first = ms[0]
         ms.sort()
         if mem == L.CORRO_MEM_DEVICE_HEADERS:
             known = dknown.cpu().numpy()
         ok = bool((known == 1).all())      # every version Current (empty state: each one impactful)
-        return ms[len(ms) // 2], ok
+        return ms[len(ms) // 2], ok, first
 
-    med_h, ok_h = timed(L.CORRO_MEM_DEVICE)
+    # (the process's first agent calls: the pinned areas and pools grow in the first call of each mode)
+    med_h, ok_h, first_h = timed(L.CORRO_MEM_DEVICE)
     nimp_h = int(imp.sum().item())
-    med, ok = timed(L.CORRO_MEM_DEVICE_HEADERS)
+    med, ok, first = timed(L.CORRO_MEM_DEVICE_HEADERS)
     nimp = int(imp.sum().item())
     del full, imp, dcs, dknown
     return {"ms": med, "changes_per_s": n / (med * 1e-3), "changesets": int(len(cs)),
             "ratio_vs_agent_path": (med / agent_ms) if agent_ms else None, "all_current": ok,
-            "impactful_changes": nimp,
-            "host_headers": {"ms": med_h, "all_current": ok_h, "impactful_changes": nimp_h,
+            "impactful_changes": nimp, "first_call_ms": first,
+            "host_headers": {"ms": med_h, "all_current": ok_h, "impactful_changes": nimp_h, "first_call_ms": first_h,
                              "note": "the same call with the headers and known in host memory (CORRO_MEM_DEVICE: a "
                                      "call this large copies the headers in parallel host threads into pinned "
                                      "memory, uploads them chunk by chunk and runs the device header passes)"},
             "note": "corro_process_multiple_changes (CORRO_MEM_DEVICE_HEADERS: changes, headers, known, impactful "
                     "in HBM) on config 2 as 1000 actors x ~1049 versions x 64 changes arriving interleaved (batch "
                     "in arrival order), reset + fresh Bookie + call, median of "
-                    f"{reps}"}
+                    f"{reps}; first_call_ms: the first call of the mode (host_headers' is the process's first agent "
+                    "call: its pinned areas and the bookie's pool are allocated inside it)"}
 
 
 def agent_e2e_mixed(eng, batch, n, fast_ms=None, reps=3, resend=0.10, partial=0.05, empty=0.05, seed=5):
@@ -742,6 +745,8 @@ def agent_e2e_mixed(eng, batch, n, fast_ms=None, reps=3, resend=0.10, partial=0.
         torch.cuda.synchronize()
         if r:
             ms.append((time.perf_counter() - t0) * 1e3)
+        else:
+            first = (time.perf_counter() - t0) * 1e3
         nready = int(out_.n_ready)
         del bk
     ms.sort()
@@ -751,7 +756,8 @@ def agent_e2e_mixed(eng, batch, n, fast_ms=None, reps=3, resend=0.10, partial=0.
                                                          ("skipped", 0))}
     del full, imp, dcs, dknown
     return {"ms": med, "changes_per_s": n / (med * 1e-3), "changesets": int(len(cs)),
-            "ratio_vs_fast": (med / fast_ms) if fast_ms else None, "known": kinds, "n_ready": nready,
+            "ratio_vs_fast": (med / fast_ms) if fast_ms else None, "first_call_ms": first, "known": kinds,
+            "n_ready": nready,
             "mix": {"resent": float(resend), "partial": float(partial), "empty": float(empty)},
             "note": "agent_e2e's call with ~10% of versions re-sent later in the call, ~5% as two partial halves "
                     "(buffered, then ready), ~5% as Empty versions; headers in HBM, reset + fresh Bookie + call, "

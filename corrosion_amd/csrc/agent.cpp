@@ -362,6 +362,7 @@ struct StagedBuf {  // one partial changeset's __corro_buffered_changes INSERTs,
     uint64_t src, ts;   // (dev) input span start, the changeset ts
     uint32_t seq0, n, site;
     int64_t dbv;
+    uint32_t tab;       // (dev) the table index of all its changes, or HDR_TAB_MIXED
 };
 struct Staged {
     std::vector<std::pair<uint32_t, uint64_t>> set_dbv;                      // crsql_set_db_version
@@ -378,16 +379,17 @@ struct Staged {
 
 // row(k) = HostRow of the changeset's k-th change
 // canon: the changeset's rows are canonical in a device batch (bufpool.hip): staged as a span
+// tab: (canon) the table index of all its changes, or HDR_TAB_MIXED
 template <class RowFn>
-int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset &cs, bool canon, RowFn row,
-                       corro::PartialVersion &out) {
+int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset &cs, bool canon, uint32_t tab,
+                       RowFn row, corro::PartialVersion &out) {
     if (canon) {
         st.items.push_back(StagedBuf{true, 0, 0, cs.change_off, cs.ts, (uint32_t)cs.seq_start,
-                                     (uint32_t)cs.change_count, cs.site, (int64_t)cs.version_start});
+                                     (uint32_t)cs.change_count, cs.site, (int64_t)cs.version_start, tab});
     } else {
         const uint64_t a = st.buffered.size();
         for (uint64_t k = 0; k < cs.change_count; k++) st.buffered.push_back(row(k));
-        st.items.push_back(StagedBuf{false, a, st.buffered.size(), 0, 0, 0, 0, 0, 0});
+        st.items.push_back(StagedBuf{false, a, st.buffered.size(), 0, 0, 0, 0, 0, 0, corro::HDR_TAB_MIXED});
     }
     SeqBook &sb = st.seq(bk, cs.site, cs.version_start);
     const uint64_t s = cs.seq_start, e = cs.seq_end;
@@ -482,6 +484,7 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
         uint64_t src, ts;  // (dev) the item's input span start and ts
         uint32_t seq0, n;  // (dev) its first seq and change count
         bool dev;
+        bool tc;           // (dev) its changes' tables are counted on the device (k_tab_count)
     };
     bool any_items = false;
     for (Staged *st : order) any_items |= !st->items.empty();
@@ -497,14 +500,16 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
         uint64_t call = (uint64_t)ai << 40;
         const std::vector<HostRow> &rows = st->buffered;
         for (const StagedBuf &it : st->items) {
-            if (it.dev) {
-                v.push_back(Sub{{it.site, it.dbv}, call++, st, 0, 0, 0, it.src, it.ts, it.seq0, it.n, true});
+            if (it.dev) {  // a single-table changeset counts here, the others on the device
+                const bool tc = it.tab == corro::HDR_TAB_MIXED;
+                if (!tc && it.tab < ntables) ptab[ai][it.tab] += it.n;
+                v.push_back(Sub{{it.site, it.dbv}, call++, st, 0, 0, 0, it.src, it.ts, it.seq0, it.n, true, tc});
                 continue;
             }
             for (uint64_t a = it.a; a < it.b;) {
                 uint64_t b = a + 1;
                 while (b < it.b && rows[b].site == rows[a].site && rows[b].dbv == rows[a].dbv) b++;
-                v.push_back(Sub{{rows[a].site, rows[a].dbv}, call++, st, a, b, 0, 0, 0, 0, 0, false});
+                v.push_back(Sub{{rows[a].site, rows[a].dbv}, call++, st, a, b, 0, 0, 0, 0, 0, false, false});
                 host_rows[ai] = 1;
                 for (uint64_t k = a; k < b; k++)
                     if ((rows[k].tcid >> 16) < ntables) ptab[ai][rows[k].tcid >> 16]++;
@@ -572,7 +577,7 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
                 if (fresh) e = &local;
                 for (size_t q = g0; q < g1; q++) {
                     const Sub &u = v[q];
-                    o.dev.push_back({u.src, 0, u.n, u.ts});
+                    if (u.tc) o.dev.push_back({u.src, 0, u.n, u.ts});
                     seq_pieces(e->segs, u.seq0, (uint64_t)u.seq0 + u.n - 1, pieces);
                     for (const Range &r : pieces) {
                         const PoolSeg g{SEG_PENDING | ((uint64_t)k << 32) | o.jobs.size(), (uint32_t)r.first,
@@ -603,9 +608,11 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
             jobs.insert(jobs.end(), outs[k].jobs.begin(), outs[k].jobs.end());
             for (auto &x : outs[k].add) add.push_back(std::move(x));
         }
-        std::vector<uint64_t> tc;
-        TRY_RC(corro::agent_dev_table_counts(ctx, dv, all_dev, (uint32_t)ntables, tc));
-        for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
+        if (!all_dev.empty()) {
+            std::vector<uint64_t> tc;
+            TRY_RC(corro::agent_dev_table_counts(ctx, dv, all_dev, (uint32_t)ntables, tc));
+            for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
+        }
         mark("cb_tables");
         if (!bk->pool) bk->pool = corro::bufpool_new();
         mark("cb_trim");
@@ -633,6 +640,7 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
     ghost.reserve(sp.size());
     gent.reserve(sp.size());
     uint64_t fr_n = 0;
+    bool any_dev = false;
     for (size_t g0 = 0; g0 < sp.size();) {
         size_t g1 = g0 + 1;
         while (g1 < sp.size() && sp[g1].key == sp[g0].key) g1++;
@@ -643,7 +651,8 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
         for (size_t q = g0; q < g1; q++) {
             Sub &u = sp[q];
             if (!u.dev) continue;
-            all_dev.push_back({u.src, 0, u.n, u.ts});
+            any_dev = true;
+            if (u.tc) all_dev.push_back({u.src, 0, u.n, u.ts});
             if (host) {
                 u.fr = fr_n;
                 fsp.push_back({u.src, fr_n, u.n, u.ts});
@@ -665,7 +674,7 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
         for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
     }
     mark("cb_tables");
-    if (!all_dev.empty() && pool_ok && !bk->pool) bk->pool = corro::bufpool_new();
+    if (any_dev && pool_ok && !bk->pool) bk->pool = corro::bufpool_new();
     std::vector<Range> pieces;
     jobs.reserve(all_dev.size());
     add.reserve(groups.size());
@@ -957,6 +966,7 @@ extern "C" {
 int corro_bookie_new(corro_bookie **out) {
     if (!out) return fail(CORRO_E_INVALID, "out is NULL");
     *out = new corro_bookie();
+    (void)HostPool::get();  // the walk's worker threads start now, not inside the first call
     return CORRO_OK;
 }
 
@@ -1041,6 +1051,7 @@ struct CsView {
     int32_t *known;
     uint8_t *flag;        // 1 = merged by this call
     const uint8_t *canon; // canonical partial changeset of a device batch (bufpool.hip; null: none)
+    const uint32_t *ctab; // a canonical one's table index, or HDR_TAB_MIXED (null: all mixed)
 };
 
 // One actor's passes 1 and 2 (util.rs:704-884) over its changesets w.idx (arrival order) unless it
@@ -1130,8 +1141,9 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
                 } else {
                     corro::PartialVersion p;
                     const bool canon = v.canon && v.canon[i];
-                    if (process_incomplete(bk, w.st, c, canon, [&](uint64_t k) { return row_of(c, i, k); }, p) !=
-                        CORRO_OK) {
+                    const uint32_t tab = canon && v.ctab ? v.ctab[i] : corro::HDR_TAB_MIXED;
+                    if (process_incomplete(bk, w.st, c, canon, tab, [&](uint64_t k) { return row_of(c, i, k); },
+                                           p) != CORRO_OK) {
                         v.known[i] = CORRO_E_INVALID;
                         continue;
                     }
@@ -1380,7 +1392,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         rv = RunView{R.run_start.data() + r, R.run_end.data() + r, nullptr, q - r};
         r = q;
     }
-    const CsView view{hcs, R.hbad, hknown.data(), hflag.data(), canon};
+    const CsView view{hcs, R.hbad, hknown.data(), hflag.data(), canon, canon ? R.hctab : nullptr};
     if (want_gaps_batch(work))
         for (ActorWork &w : work) w.defer_gaps = true;
     stage("act_runs");
@@ -1794,7 +1806,7 @@ int process_multiple_changes(corro_ctx *ctx, corro_bookie *bk, const corro_chang
     std::vector<std::vector<Range>> fast_runs(work.size());
     for (size_t k = 0; k < nchunk; k++)
         for (auto &[wi, r] : cout[k].runs) fast_runs[wi].push_back(r);
-    const CsView view{cs, bad, out->known, P.flag, nullptr};
+    const CsView view{cs, bad, out->known, P.flag, nullptr, nullptr};
     auto run_actor = [&](size_t wi) {
         run_actor_walk(bk, work[wi], view, RunView{nullptr, nullptr, fast_runs[wi].data(), fast_runs[wi].size()}, row_of);
     };

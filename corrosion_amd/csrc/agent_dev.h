@@ -98,6 +98,7 @@ int agent_dev_impacts(corro_ctx *ctx, const uint8_t *impact, const uint32_t *tci
 // cleared; later copies of its dedup key: skipped), and the decided versions' runs for the gap
 // bookkeeping. The host gets per-site summaries, the runs, and the headers of the other ("host")
 // changesets, which it walks with the reference's per-actor passes.
+constexpr uint32_t HDR_TAB_MIXED = 0xFFFFFFFFu;  // (DevHdrResult::hctab) tables differ, or not canonical
 struct DevHdrSite {
     uint32_t gstart, gend;   // sorted slots [gstart, gend] of the site's changesets (gstart ~0: none)
 };
@@ -114,6 +115,7 @@ struct DevHdrResult {
     const corro_changeset *hcs;
     const uint32_t *hidx;
     const uint8_t *hbad, *hcanon;
+    const uint32_t *hctab;  // per host changeset: its table index when canonical and single-table, else HDR_TAB_MIXED
 };
 // site_max[s] = the actor's booked max (-1: none); dknown: device, ncs entries
 int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, const corro_changes *dv,

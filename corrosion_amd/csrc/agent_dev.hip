@@ -1314,6 +1314,7 @@ struct HGatherArgs {
     corro_changeset *out;
     uint32_t *idx;
     uint8_t *obad, *ocanon;
+    uint32_t *otab;  // a canonical one's table index when all its changes share it, else HDR_TAB_MIXED
 };
 
 __global__ void __launch_bounds__(AG_T) k_hdr_gather(HGatherArgs a) {
@@ -1328,8 +1329,11 @@ __global__ void __launch_bounds__(AG_T) k_hdr_gather(HGatherArgs a) {
                      c.change_count == c.seq_end - c.seq_start + 1 && c.version_start <= (uint64_t)INT64_MAX &&
                      c.change_off <= a.in.n && c.change_count <= a.in.n - c.change_off && a.in.seq && a.in.site &&
                      a.in.db_version;
+        uint32_t tab = HDR_TAB_MIXED;
+        if (canon && a.in.table_cid) tab = a.in.table_cid[c.change_off] >> 16;
         for (uint64_t q = 0; canon && q < c.change_count; q++) {
             const uint64_t r = c.change_off + q;
+            if (tab != HDR_TAB_MIXED && (a.in.table_cid[r] >> 16) != tab) tab = HDR_TAB_MIXED;
             const uint8_t vt = a.in.val_type ? a.in.val_type[r] : (uint8_t)CORRO_INTEGER;
             const uint8_t vl = a.in.val_len ? a.in.val_len[r] : 0;
             canon = a.in.seq[r] == c.seq_start + q && a.in.site[r] == c.site &&
@@ -1337,6 +1341,7 @@ __global__ void __launch_bounds__(AG_T) k_hdr_gather(HGatherArgs a) {
                     !(vl == CORRO_VAL_LONG && (vt == CORRO_TEXT || vt == CORRO_BLOB));
         }
         a.ocanon[k] = canon ? 1 : 0;
+        a.otab[k] = canon ? tab : HDR_TAB_MIXED;
     }
 }
 
@@ -1558,7 +1563,7 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     res.nh = nh;
     if (nh) {  // their headers, arrival index, unknown-name and canonical flags: one pinned readback
         const size_t o_idx = al256((uint64_t)nh * sizeof(corro_changeset)), o_bad = o_idx + al256(nh * 4ULL),
-                     o_can = o_bad + al256(nh), total_b = o_can + al256(nh);
+                     o_can = o_bad + al256(nh), o_tab = o_can + al256(nh), total_b = o_tab + al256(nh * 4ULL);
         if (int rc = ctx->d_agent_fetch.ensure(total_b + 256)) return rc;
         if (total_b > ctx->h_hfetch_bytes) {
             if (ctx->h_hfetch) (void)hipHostFree(ctx->h_hfetch);
@@ -1579,6 +1584,7 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         g.idx = reinterpret_cast<uint32_t *>(base + o_idx);
         g.obad = base + o_bad;
         g.ocanon = base + o_can;
+        g.otab = reinterpret_cast<uint32_t *>(base + o_tab);
         hipLaunchKernelGGL(k_hdr_gather, flat_grid(nh), dim3(AG_T), 0, s, g);
         CORRO_HIP_TRY(hipGetLastError());
         uint8_t *hp = static_cast<uint8_t *>(ctx->h_hfetch);
@@ -1587,6 +1593,7 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         res.hidx = reinterpret_cast<const uint32_t *>(hp + o_idx);
         res.hbad = hp + o_bad;
         res.hcanon = hp + o_can;
+        res.hctab = reinterpret_cast<const uint32_t *>(hp + o_tab);
     }
     if (nruns || nh) CORRO_HIP_TRY(hipStreamSynchronize(s));
     for (uint64_t r = 0; r < nruns; r++) {

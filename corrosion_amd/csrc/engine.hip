@@ -594,6 +594,7 @@ int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t 
              hipMemcpy(ctx->d_stride.p, stride.data(), stride.size() * 2, hipMemcpyHostToDevice) != hipSuccess))
             rc = fail(CORRO_E_DEVICE, "upload of the schema failed");
         if (rc == CORRO_OK) rc = store_clear(ctx);
+        if (rc == CORRO_OK) rc = prims_warm(ctx);
         if (rc != CORRO_OK) {
             corro_ctx_destroy(ctx);
             return rc;

@@ -120,6 +120,9 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
 bool pk_canonical(const uint8_t *p, uint64_t len, std::string &out, bool *single_int, int64_t *ival);
 std::string pack_int_pk(int64_t v);
 
+// the rocPRIM kernels' first-use cost paid once per process and device (prims.hip)
+int prims_warm(corro_ctx *ctx);
+
 }  // namespace corro
 
 struct corro_ctx {

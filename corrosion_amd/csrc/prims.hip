@@ -14,6 +14,10 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
 #include "internal.h"
 #include "merge_kernels.h"
 
@@ -105,6 +109,59 @@ int ovf_scan_tiles(void *temp, size_t *temp_bytes, const OvfDev &d, const CsAgg 
                    hipStream_t s) {
     const hipError_t e = rocprim::inclusive_scan(temp, *temp_bytes, in, out, (size_t)n, CsComb{d.qkey, d.arena}, s);
     if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("tile scan: ") + hipGetErrorString(e));
+    return CORRO_OK;
+}
+
+// First launches of the rocPRIM kernels (the sorts and scans the agent's header passes and the
+// overflow fold run) cost tens of milliseconds each: the code objects load and the dispatch
+// resolves on first use. Once per process and device, each primitive runs here on a small and a
+// large size (the radix sort takes a different kernel set for each), so a node's first gossip batch
+// does not pay it. Errors are returned; the inputs are scratch (results discarded).
+int prims_warm(corro_ctx *ctx) {
+    static std::mutex mu;
+    static std::vector<int> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (std::find(done.begin(), done.end(), ctx->device) != done.end()) return CORRO_OK;
+    hipStream_t s = ctx->stream;
+    const uint32_t sizes[2] = {1000u, 1u << 20};
+    const uint32_t N = sizes[1];
+    DevBuf buf;
+    size_t temp = 0;
+    for (uint32_t n : sizes) {
+        size_t t = 0;
+        ovf_sort_pairs(nullptr, &t, nullptr, nullptr, nullptr, nullptr, n, 64, s);
+        temp = std::max(temp, t);
+        prim_segmax_scan_u64(nullptr, &t, nullptr, nullptr, nullptr, n, s);
+        temp = std::max(temp, t);
+        prim_inclusive_scan_u32(nullptr, &t, nullptr, nullptr, n, s);
+        temp = std::max(temp, t);
+        prim_inclusive_scan_u32_u64(nullptr, &t, nullptr, nullptr, n, s);
+        temp = std::max(temp, t);
+    }
+    // keys in/out (u64), values in/out (u32), u32 keys/flags, u64 scan outputs
+    const size_t k8 = (size_t)N * 8, k4 = (size_t)N * 4;
+    const size_t o_ko = k8, o_vi = 2 * k8, o_vo = o_vi + k4, o_u = o_vo + k4, o_w = o_u + k4, o_t = o_w + k8;
+    if (int rc = buf.ensure(o_t + temp + 256)) return rc;
+    uint8_t *b = buf.as<uint8_t>();
+    CORRO_HIP_TRY(hipMemsetAsync(b, 0, o_t, s));
+    auto *ki = reinterpret_cast<uint64_t *>(b), *ko = reinterpret_cast<uint64_t *>(b + o_ko),
+         *wo = reinterpret_cast<uint64_t *>(b + o_w);
+    auto *vi = reinterpret_cast<uint32_t *>(b + o_vi), *vo = reinterpret_cast<uint32_t *>(b + o_vo),
+         *u = reinterpret_cast<uint32_t *>(b + o_u);
+    void *tp = b + o_t;
+    for (uint32_t n : sizes) {
+        size_t t = temp;
+        if (int rc = ovf_sort_pairs(tp, &t, ki, ko, vi, vo, n, 64, s)) return rc;
+        t = temp;
+        if (int rc = prim_segmax_scan_u64(tp, &t, u, ki, wo, n, s)) return rc;
+        t = temp;
+        if (int rc = prim_inclusive_scan_u32(tp, &t, u, vo, n, s)) return rc;
+        t = temp;
+        if (int rc = prim_inclusive_scan_u32_u64(tp, &t, u, wo, n, s)) return rc;
+    }
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    buf.release();
+    done.push_back(ctx->device);
     return CORRO_OK;
 }
 
