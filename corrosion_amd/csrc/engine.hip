@@ -239,8 +239,11 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     }
     // every row looked up in its region; prior records counted, new rows counted per bucket (and
     // every batch record's sort key)
+    static const bool split = !std::getenv("CORRO_OVF_SPLIT") || std::atoi(std::getenv("CORRO_OVF_SPLIT")) != 0;
+    d.split = split ? 1u : 0u;
     hipLaunchKernelGGL(d.rimp ? k_ovf_lookup<true> : k_ovf_lookup<false>, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)),
                        dim3(RS_T), 0, s, a, d);
+    if (split) hipLaunchKernelGGL(k_ovf_rlook, grid_for(nrows), blk, 0, s, a, d);
     TRY(launched());
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
     CORRO_HIP_TRY(hipMemcpyAsync(&hw[0], d.rpoff + (nrows - 1), 4, hipMemcpyDeviceToHost, s));

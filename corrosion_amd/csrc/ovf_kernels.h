@@ -112,6 +112,7 @@ struct OvfDev {
     // position of each causal length (cl << 32 | position, ~0 free) and the record at it; the
     // dropped candidates' sort key = ((row * OVF_NCL + slot) << cid_bits | cid) << rshift | position
     uint32_t rimp;
+    uint32_t split;              // 1: the rows' region lookups run in k_ovf_rlook (one lane per row)
     uint64_t *rcl;               // [nrows * OVF_NCL]
     uint32_t *rclr;              // [nrows * OVF_NCL]
 };
@@ -504,6 +505,7 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
         const uint32_t b = bk, t = d.tc[r] >> 16;
         d.rowner[row] = r;
         d.rb[row] = b;
+        if (d.split) continue;
         const uint32_t e = rs_lookup(a.rs, a.ovf_list[b], d.pk[r], t);
         if (e == ROW_NONE) {
             d.rheap[row] = ROW_NONE;
@@ -526,6 +528,61 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
         rs_lds_flush(L, d);
         if constexpr (RIMP) rcl_lds_flush(LC_, d);
     }
+}
+
+// Each row looked up in its region, one lane per row (k_ovf_lookup's lanes walk RS_E records each,
+// so a lookup there is a chain of dependent probes per record group; here every row's probe is in
+// flight at once). New rows and their heap records counted per bucket, the found rows' prior records
+// leave the live count -- both summed per wave first (rows are bucket-major: a wave's rows share one
+// or two buckets).
+static __global__ void k_ovf_rlook(MergeArgs a, OvfDev d) {
+    const uint32_t lane = threadIdx.x & 63;
+    unsigned long long gone = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < d.nrows; base += gridDim.x * blockDim.x) {  // (wave-uniform)
+        const uint32_t row = base + threadIdx.x;
+        const bool ok = row < d.nrows;
+        uint32_t b = 0, nrec = 0;
+        bool isnew = false;
+        if (ok) {
+            const uint32_t r = d.rowner[row], t = d.tc[r] >> 16;
+            b = d.rb[row];
+            const uint32_t e = rs_lookup(a.rs, a.ovf_list[b], d.pk[r], t);
+            if (e == ROW_NONE) {
+                d.rheap[row] = ROW_NONE;
+                d.rprior[row] = 0;
+                d.rbits[2 * row] = d.rbits[2 * row + 1] = 0;
+                isnew = true;
+                nrec = (uint32_t)a.rs.stride[t];
+            } else {
+                const RowEnt re = a.rs.ent[e];
+                const uint32_t pc = row_popc(re.bits);
+                d.rheap[row] = re.heap;
+                d.rprior[row] = pc;
+                d.rbits[2 * row] = re.bits[0];
+                d.rbits[2 * row + 1] = re.bits[1];
+                gone += pc;
+            }
+        }
+        // per-bucket counts: the wave's new rows of the first active lane's bucket in one atomic each
+        bool todo = isnew;
+        while (true) {
+            const uint64_t act = __ballot(todo);
+            if (!act) break;
+            const int leader = __ffsll((unsigned long long)act) - 1;
+            const uint32_t lb = __shfl(b, leader);
+            const bool mine = todo && b == lb;
+            const uint32_t rows = (uint32_t)__popcll(__ballot(mine));
+            const uint32_t recs = wave_sum_u32(mine ? nrec : 0u);
+            if ((int)lane == leader) {
+                atomicAdd(&d.bnew[lb], rows);
+                atomicAdd(&d.bnrec[lb], recs);
+            }
+            if (mine) todo = false;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) gone += __shfl_xor(gone, o);
+    if (lane == 0 && gone) atomicAdd(&a.misc[MISC_LIVE], (unsigned long long)(-(long long)gone));
 }
 
 // prior records of every found row appended at [Kb + rpoff[row] - pc, Kb + rpoff[row]) (rpoff:
