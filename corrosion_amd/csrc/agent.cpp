@@ -1029,6 +1029,43 @@ struct ActorWork {
     RangeSet versions;                // (deferred) the versions this call adds
     int rc = CORRO_OK;
     std::string err;
+    double t_walk[4] = {0, 0, 0, 0};  // (CORRO_AGENT_PROFILE) runs, pass 1, pass 2, gaps + partials: ms
+};
+
+// A call's per-actor work is freed on a background thread after the call returns (a large mixed
+// call's buffered rows, seq maps and snapshots are ~1 ms of frees; nothing in them refers to the
+// bookie). One thread, a queue of batches; like HostPool it is never joined.
+class Reaper {
+  public:
+    static Reaper &get() {
+        static Reaper *r = new Reaper();
+        return *r;
+    }
+    void give(std::vector<ActorWork> &&w) {
+        auto *p = new std::vector<ActorWork>(std::move(w));
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(p);
+        }
+        cv_.notify_one();
+    }
+
+  private:
+    Reaper() { std::thread([this] { loop(); }).detach(); }
+    void loop() {
+        while (true) {
+            std::vector<std::vector<ActorWork> *> batch;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return !q_.empty(); });
+                batch.swap(q_);
+            }
+            for (auto *p : batch) delete p;
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<std::vector<ActorWork> *> q_;
 };
 
 Range versions_of(const corro_changeset &c) {
@@ -1067,6 +1104,14 @@ struct RunView {
 };
 template <class RowOf>
 void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunView &fast_runs, RowOf &&row_of) {
+    static const bool prof = std::getenv("CORRO_AGENT_PROFILE") != nullptr;
+    auto t_prev = std::chrono::steady_clock::now();
+    auto lap = [&](int k) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        w.t_walk[k] += std::chrono::duration<double, std::milli>(t - t_prev).count();
+        t_prev = t;
+    };
     corro::Booked &booked = *w.booked;
     const bool had_max = w.had_max;
     const uint64_t max = w.max;
@@ -1075,6 +1120,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
         if (fast_runs.r) versions.insert(fast_runs.r[k].first, fast_runs.r[k].second);
         else versions.insert(fast_runs.s[k], fast_runs.e[k]);
     }
+    lap(0);
     if (!w.fast) {
         // pass 1: batch-local dedup of (versions, seqs), then versions the actor already holds
         std::vector<uint64_t> unknown;
@@ -1113,6 +1159,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
             if (booked.contains_all(vr.first, vr.second, seqs)) continue;
             unknown.push_back(i);
         }
+        lap(1);
         // pass 2 (the bookie is not written until the call commits, so pass 1's contains_all stands)
         SeenMap seen_local(w.partials);
         for (uint64_t i : unknown) {
@@ -1155,6 +1202,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
             seen_local.insert(vr, partial ? w.partials.size() - 1 : SIZE_MAX);
             versions.insert(vr.first, vr.second);
         }
+        lap(2);
     }
     if (versions.empty()) return;
     if (w.defer_gaps) {  // (many actors: one device pass for all of them, gaps_batch)
@@ -1175,6 +1223,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
         const corro::PartialVersion &p = w.next.insert_partial(version, std::move(pv));
         if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
     }
+    lap(3);
 }
 
 // Whether the call's gap bookkeeping goes through the batched device form (corro_booked_insert_db_batch)
@@ -1401,6 +1450,14 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     for (ActorWork &w : work)
         if (w.rc != CORRO_OK) return fail(w.rc, w.err);
     stage("act_walk");
+    if (prof) {  // the walk's parts summed over actors (thread-ms; the pool runs up to 16 at once)
+        double tw[4] = {0, 0, 0, 0};
+        for (const ActorWork &w : work)
+            for (int k = 0; k < 4; k++) tw[k] += w.t_walk[k];
+        char buf[160];
+        snprintf(buf, sizeof buf, " [walk thread-ms: runs=%.2f pass1=%.2f pass2=%.2f gaps=%.2f]", tw[0], tw[1], tw[2], tw[3]);
+        prof_line += buf;
+    }
     uint64_t nspans = R.nspans, nb = R.nchanges;
     for (const ActorWork &w : work) {
         nspans += w.nspans;
@@ -1478,7 +1535,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     out->n_ready = nready;
     corro_detail_add_committed(ctx, committed.data(), committed.size());
     stage("commit");
-    if (nh >= 4096) run_parallel(work.size(), [&](size_t k) { ActorWork gone = std::move(work[k]); }, 16);  // (frees in parallel)
+    if (nh >= 4096) Reaper::get().give(std::move(work));  // (freed after the call returns)
     stage("free");
     if (prof) fprintf(stderr, "[corro agent dev] ncs=%llu spans=%llu changes=%llu host=%zu ms:%s\n", (unsigned long long)ncs,
                       (unsigned long long)nspans, (unsigned long long)nb, (size_t)nh, prof_line.c_str());
