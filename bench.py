@@ -281,7 +281,9 @@ def run_rank_child(args, world):
     G = args.changes
     n_local = G // world
     npk = N_PK_C3 if strong else N_PK * world
-    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=rank_capacity(n_local, G, npk, world), device=0)
+    # (its own slots stand in for the received ones, so it merges every row of its slice -- more distinct
+    # rows than the rank owns: the engine is presized for those, as a real rank's is for its own)
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=rank_capacity(n_local, n_local, npk, 1), device=0)
     eng.register_sites(synth.site_ids(N_ACTORS, 1))
     batch = synth.uniform_batch_torch(n_local, N_ACTORS, npk, N_COLS, seed=synth.config_seed(3), device="cuda:0",
                                       offset=0, global_n=G)
