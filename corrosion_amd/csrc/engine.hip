@@ -1126,7 +1126,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.vsz = in->val_size;
     }
     bd.n = n;
-    if (ctx->slot_rec) {  // slot mode (corro_apply_slots): one chunk, positions = slot indices
+    if (ctx->slot_rec) {  // slot mode (corro_apply_slots): positions = slot indices (chunk-relative)
         bd.slot_rec = static_cast<const SlotRec *>(ctx->slot_rec);
         bd.slot_cnt = ctx->slot_cnt;
         bd.slot_cap = ctx->slot_cap;
@@ -1186,7 +1186,7 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.ts_pos = 1;
     }
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
-    const uint64_t chunk = ctx->pm_ap || ctx->slot_rec ? std::max<uint64_t>(n, 1) : corro_detail_chunk_changes(ctx);
+    const uint64_t chunk = ctx->pm_ap ? std::max<uint64_t>(n, 1) : corro_detail_chunk_changes(ctx);
     if (n > chunk) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
         hipLaunchKernelGGL(k_validate, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, bd,
@@ -1206,7 +1206,8 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         };
         adv(c.pk), adv(c.tcid), adv(c.cv), adv(c.dbv), adv(c.cl), adv(c.seq), adv(c.site), adv(c.v0), adv(c.v1);
         adv(c.vt), adv(c.vl), adv(c.ts), adv(c.voff), adv(c.vsz);
-        adv(c.conv), adv(c.cv0), adv(c.cv1), adv(c.cmeta);
+        adv(c.conv), adv(c.cv0), adv(c.cv1), adv(c.cmeta), adv(c.slot_rec);
+        c.slot_base = (uint32_t)off;
         c.n = m;
         TRY(apply_chunk(ctx, c, imp_buf ? imp_buf + off : nullptr));
         for (int k = 0; k < 6; k++) ms[k] += ctx->last_ms[k];

@@ -2680,7 +2680,18 @@ static __global__ void __launch_bounds__(1024) k_sum_used(const uint32_t *__rest
 static __global__ void k_validate(BatchDev in, uint32_t nsites, const uint16_t *__restrict__ ncols, uint32_t ntables,
                                   unsigned long long *misc) {
     uint32_t err = 0, wide = 0;
+    const bool sover = in.slot_rec && slot_overflowed(in);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < in.n; i += gridDim.x * blockDim.x) {
+        if (in.slot_rec) {  // slot mode: the received records that will be applied (INTEGER values)
+            if (!slot_valid(in, i, sover)) continue;
+            const SlotRec &r = in.slot_rec[i];
+            const uint32_t t = r.tcid >> 16, cid = r.tcid & 0xFFFFu;
+            if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;
+            if (r.site >= nsites) err |= ERR_SITE;
+            if ((cid == 0 || (r.cl & 1u) == 0) && (r.cv < 0 || r.cv > 0xFFFFFFFFLL)) err |= ERR_RANGE;
+            if (r.dbv < 0) err |= ERR_RANGE;
+            continue;
+        }
         const uint32_t tc = in.tcid[i], t = tc >> 16, cid = tc & 0xFFFFu, cl = in.cl[i];
         const int64_t cv = in.cv[i];
         if (t >= ntables || cid > ncols[t]) err |= ERR_NAME;

@@ -52,11 +52,14 @@ struct BatchDev {
     // slot mode (corro_apply_slots: the receiver of the stream-ordered exchange merges the received
     // 48-B records where they lie): change i is slot_rec[i], applied at position i when its source's
     // slot holds it (i % cap < slot_cnt[i / cap]) and no source overflowed its slot; the SoA arrays
-    // above are not read. k_hist reports an overflow in *slot_over.
+    // above are not read. k_hist reports an overflow in *slot_over. A batch larger than one apply
+    // chunk is applied as consecutive index ranges of the slot layout: slot_rec then points at the
+    // chunk's first record, whose index in the whole layout is slot_base.
     const SlotRec *slot_rec;
     const uint64_t *slot_cnt;
     uint32_t slot_cap, slot_nsrc;
     uint32_t *slot_over;
+    uint32_t slot_base;
 };
 
 // slot mode: does any source's count pass the slot (every record is then skipped)?
@@ -65,9 +68,9 @@ __device__ inline bool slot_overflowed(const BatchDev &in) {
     for (uint32_t s = 0; s < in.slot_nsrc; s++) over |= in.slot_cnt[s] > in.slot_cap;
     return over;
 }
-__device__ inline bool slot_valid(const BatchDev &in, uint32_t i, bool over) {
-    const uint32_t s = i / in.slot_cap;
-    return !over && s < in.slot_nsrc && (uint64_t)(i - s * in.slot_cap) < in.slot_cnt[s];
+__device__ inline bool slot_valid(const BatchDev &in, uint32_t i, bool over) {  // (i: index in the chunk)
+    const uint32_t g = in.slot_base + i, s = g / in.slot_cap;
+    return !over && s < in.slot_nsrc && (uint64_t)(g - s * in.slot_cap) < in.slot_cnt[s];
 }
 constexpr uint32_t AP_SKIP = 0xFFFFFFFFu;
 

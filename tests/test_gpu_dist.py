@@ -239,10 +239,12 @@ def test_partition_var_routes_unregistered_table_ids():
 NS = 50000
 
 
-def _slots_worker(rank, world, port, outdir, cap_scale, impact=False):
+def _slots_worker(rank, world, port, outdir, cap_scale, impact=False, chunk=0):
     import torch.distributed as dist
     import corrosion_amd as ca
     from corrosion_amd.dist import distributed_apply_slots, rank_of_np, slot_cap
+    if chunk:  # (the received slots applied as several index-range chunks)
+        os.environ["CORRO_HIP_CHUNK"] = str(chunk)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -266,17 +268,21 @@ def _slots_worker(rank, world, port, outdir, cap_scale, impact=False):
 
 
 @pytest.mark.parametrize("impact", [False, True], ids=["no_impacts", "impacts"])
-@pytest.mark.parametrize("cap_scale", [1.0, 0.3], ids=["slots_fit", "slots_overflow_repeat"])
-def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale, impact):
+@pytest.mark.parametrize("cap_scale,chunk", [(1.0, 0), (0.3, 0), (1.0, 4096)],
+                         ids=["slots_fit", "slots_overflow_repeat", "slots_fit_chunked"])
+def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale, chunk, impact):
     """distributed_apply_slots: fixed slots, equal-split all-to-alls on the engine's stream, the merge
     straight from the received slots (corro_apply_slots: no unpack pass, padding skipped); with slots
     too small (0.3 x) every rank overflows, merges nothing in the slot pass and repeats with the
     exact-size exchange -- the union of the rank states equals one engine's merge of the whole batch
     either way. With impacts the flags come back to their senders on the stream (a third equal-split
-    all-to-all + the partition's permutation) and equal the single engine's, in each rank's order."""
+    all-to-all + the partition's permutation) and equal the single engine's, in each rank's order.
+    `chunked`: the receivers apply their slot layout in 4096-record index ranges (a batch larger than
+    one apply chunk), whose boundaries fall inside the slots."""
     import corrosion_amd as ca
     world = 2
-    mp.spawn(_slots_worker, args=(world, _free_port(), str(tmp_path), cap_scale, impact), nprocs=world, join=True)
+    mp.spawn(_slots_worker, args=(world, _free_port(), str(tmp_path), cap_scale, impact, chunk), nprocs=world,
+             join=True)
     got = []
     for r in range(world):
         got += [tuple(x) for x in np.load(tmp_path / f"srows{r}.npy", allow_pickle=True)]
