@@ -1134,7 +1134,8 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.slot_over = ctx->slot_over;
     }
     // (a slot layout -- corro_apply_mapped -- may pass the chunk size by its padding: one chunk still)
-    const uint64_t chunk_cap = corro_detail_chunk_changes(ctx) + (ctx->pm_slack ? corro_detail_chunk_changes(ctx) / 4 : 0);
+    const uint64_t chunk_cap = corro_detail_chunk_changes(ctx) +
+                               (ctx->pm_slack || ctx->slot_rec ? corro_detail_chunk_changes(ctx) / 4 : 0);
     if (ctx->pm_ap) {  // position mode (agent): one chunk, per-position ts
         if (mem != CORRO_MEM_DEVICE || n > chunk_cap)
             return fail(CORRO_E_INVALID, "internal: position mode needs one device-resident chunk");
@@ -1186,7 +1187,8 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
         bd.ts_pos = 1;
     }
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
-    const uint64_t chunk = ctx->pm_ap ? std::max<uint64_t>(n, 1) : corro_detail_chunk_changes(ctx);
+    // (a slot layout carries its padding: up to a quarter more slots than applied records, one chunk still)
+    const uint64_t chunk = ctx->pm_ap ? std::max<uint64_t>(n, 1) : ctx->slot_rec ? chunk_cap : corro_detail_chunk_changes(ctx);
     if (n > chunk) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
         hipLaunchKernelGGL(k_validate, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, bd,

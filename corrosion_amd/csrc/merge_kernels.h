@@ -2402,6 +2402,12 @@ __device__ inline void fast_body_impact_packed(const MergeArgs &a, uint32_t b, c
         if (!alive[k]) continue;
         bool imp = (flags >> (2 * k)) & 1u, win = imp;
         const uint32_t mb = md[k] & 0xFFFFu, d = md[k] >> 16, me = s_own[cell[k]];
+#if CORRO_DIAG & 2048  // (diagnostics only: no member walk -- the cell's claimant wins, results not valid)
+        win = cell[k] == k * FAST_T + tid;
+        if (a.impact && (pos[k] & BATCH_POS) && imp) a.impact[pos[k] & 0x7FFFFFFFu] = 1;
+        alive[k] = win;
+        continue;
+#endif
         for (uint32_t m = mb; m < me; m++) {
             if (m == d) continue;
             const uint64_t j1 = s_a[m];
