@@ -590,6 +590,8 @@ int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, uint64_t nchanges, AgentPinned
     const auto t0 = std::chrono::steady_clock::now();
     auto ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    const double t_set = ms();
+    const bool busy = prof && hipStreamQuery(ctx->stream) == hipErrorNotReady;
     CORRO_HIP_TRY(hipStreamSynchronize(ctx->stream));  // (the pinned area may still feed a copy)
     const double t_sync = ms();
     const uint64_t n = std::max<uint64_t>(ncs, 1);
@@ -622,8 +624,8 @@ int agent_dev_begin(corro_ctx *ctx, uint64_t ncs, uint64_t nchanges, AgentPinned
     if (int rc = ctx->d_agent_spans.ensure(dtotal + 256)) return rc;
     const int rc = ctx->d_agent_out.ensure(256 + 8 * 65536);
     if (prof)
-        fprintf(stderr, "[corro agent dev begin] sync=%.3f pinned=%.3f cols=%.3f ensure=%.3f ms\n", t_sync, t_pin - t_sync,
-                t_cols - t_pin, ms() - t_cols);
+        fprintf(stderr, "[corro agent dev begin] set=%.3f sync=%.3f (stream busy %d) pinned=%.3f cols=%.3f ensure=%.3f ms\n",
+                t_set, t_sync - t_set, (int)busy, t_pin - t_sync, t_cols - t_pin, ms() - t_cols);
     return rc;
 }
 
