@@ -79,7 +79,7 @@ bool fault_armed(const char *name) {
 }
 
 struct SeqBook {  // __corro_seq_bookkeeping rows of one (site, version)
-    std::vector<Range> ranges;
+    corro::SmallVec<Range, 2> ranges;  // (one or two ranges inline: no allocation per partial version)
     uint64_t last_seq = 0, ts = 0;
 };
 
@@ -368,12 +368,21 @@ struct Staged {
     std::vector<std::pair<uint32_t, uint64_t>> set_dbv;                      // crsql_set_db_version
     std::vector<HostRow> buffered;                                            // __corro_buffered_changes
     std::vector<StagedBuf> items;
-    std::map<std::pair<uint32_t, uint64_t>, SeqBook> seqbook;                 // __corro_seq_bookkeeping
+    // __corro_seq_bookkeeping rows of the call, sorted by key: one vector (an actor's versions mostly
+    // arrive ascending, so a new key is usually appended; no tree node per partial version)
+    std::vector<std::pair<std::pair<uint32_t, uint64_t>, SeqBook>> seqbook;
     SeqBook &seq(const corro_bookie *bk, uint32_t site, uint64_t version) {
-        auto it = seqbook.find({site, version});
-        if (it != seqbook.end()) return it->second;
-        const SeqBook *b = bk->seqbook.find({site, version});
-        return seqbook.emplace(std::make_pair(site, version), b ? *b : SeqBook{}).first->second;
+        const std::pair<uint32_t, uint64_t> key{site, version};
+        auto it = seqbook.end();
+        if (seqbook.empty() || seqbook.back().first < key) {
+            it = seqbook.end();
+        } else {
+            it = std::lower_bound(seqbook.begin(), seqbook.end(), key,
+                                  [](const auto &x, const std::pair<uint32_t, uint64_t> &k) { return x.first < k; });
+            if (it != seqbook.end() && it->first == key) return it->second;
+        }
+        const SeqBook *b = bk->seqbook.find(key);
+        return seqbook.emplace(it, key, b ? *b : SeqBook{})->second;
     }
 };
 
@@ -394,7 +403,7 @@ int process_incomplete(const corro_bookie *bk, Staged &st, const corro_changeset
     SeqBook &sb = st.seq(bk, cs.site, cs.version_start);
     const uint64_t s = cs.seq_start, e = cs.seq_end;
     RangeSet merged;
-    std::vector<Range> keep;
+    corro::SmallVec<Range, 2> keep;
     for (const Range &r : sb.ranges) {
         const bool hit = (r.first >= s && r.first <= e) || (r.first <= s && r.second >= e) ||
                          (r.first <= e && r.second >= e) || (r.second >= s && r.second <= e) ||
@@ -607,8 +616,7 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
             jbase[k] = jobs.size();
             jobs.insert(jobs.end(), outs[k].jobs.begin(), outs[k].jobs.end());
             for (auto &x : outs[k].add) add.push_back(std::move(x));
-        }
-        if (!all_dev.empty()) {
+        }        if (!all_dev.empty()) {
             std::vector<uint64_t> tc;
             TRY_RC(corro::agent_dev_table_counts(ctx, dv, all_dev, (uint32_t)ntables, tc));
             for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
@@ -985,22 +993,31 @@ struct SeenMap {
     using Parts = std::vector<std::pair<uint64_t, corro::PartialVersion>>;
     explicit SeenMap(const Parts &parts) : parts_(parts) {}
     RangeSet covered;
-    std::map<uint64_t, size_t> partial_at;
+    std::vector<std::pair<uint64_t, size_t>> partial_at;  // version -> part, sorted (no tree node per partial)
     void insert(const Range &v, size_t part = SIZE_MAX) {  // part: index in parts, SIZE_MAX = none
         covered.insert(v.first, v.second);
-        if (!partial_at.empty()) partial_at.erase(partial_at.lower_bound(v.first), partial_at.upper_bound(v.second));
-        if (part != SIZE_MAX) partial_at[v.first] = part;
+        auto lo = first_at(v.first);
+        auto hi = lo;
+        while (hi != partial_at.end() && hi->first <= v.second) ++hi;
+        lo = partial_at.erase(lo, hi);
+        if (part != SIZE_MAX) partial_at.insert(lo, {v.first, part});
     }
     // every version of v seen, and (with seqs) each seen partial holding the seqs
     bool all_seen(const Range &v, const Range *seqs) const {
         if (!covered.contains_range(v.first, v.second)) return false;
         if (!seqs || partial_at.empty()) return true;
-        for (auto it = partial_at.lower_bound(v.first); it != partial_at.end() && it->first <= v.second; ++it)
+        for (auto it = first_at(v.first); it != partial_at.end() && it->first <= v.second; ++it)
             if (!parts_[it->second].second.seqs.contains_range(seqs->first, seqs->second)) return false;
         return true;
     }
 
   private:
+    std::vector<std::pair<uint64_t, size_t>>::iterator first_at(uint64_t v) {
+        return std::lower_bound(partial_at.begin(), partial_at.end(), v, [](const auto &x, uint64_t k) { return x.first < k; });
+    }
+    std::vector<std::pair<uint64_t, size_t>>::const_iterator first_at(uint64_t v) const {
+        return std::lower_bound(partial_at.begin(), partial_at.end(), v, [](const auto &x, uint64_t k) { return x.first < k; });
+    }
     const Parts &parts_;
 };
 
@@ -1221,7 +1238,7 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
     }
     for (auto &[version, pv] : w.partials) {  // (w.partials is done with: moved into the snapshot)
         const corro::PartialVersion &p = w.next.insert_partial(version, std::move(pv));
-        if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
+        if (!p.seqs.has_gap(0, p.last_seq)) w.ready.push_back(version);
     }
     lap(3);
 }
@@ -1309,7 +1326,7 @@ int gaps_batch(corro_ctx *ctx, std::vector<ActorWork> &work) {
         w.has_next = true;
         for (auto &[version, pv] : w.partials) {
             const corro::PartialVersion &p = w.next.insert_partial(version, std::move(pv));
-            if (p.seqs.gaps(0, p.last_seq).empty()) w.ready.push_back(version);
+            if (!p.seqs.has_gap(0, p.last_seq)) w.ready.push_back(version);
         }
     }, 16);
     return CORRO_OK;
@@ -2033,7 +2050,7 @@ int corro_process_fully_buffered(corro_ctx *ctx, corro_bookie *bk, const uint8_t
     corro::Booked &booked = bit->second;
     auto pit = booked.partials.find(version);
     if (pit == booked.partials.end()) return CORRO_OK;
-    if (!pit->second.seqs.gaps(0, pit->second.last_seq).empty()) return CORRO_OK;  // gaps: abort
+    if (pit->second.seqs.has_gap(0, pit->second.last_seq)) return CORRO_OK;  // gaps: abort
     const uint32_t site = sit->second;
     Batch batch;
     if (BufEntry *rows = bk->buffered.find({site, (int64_t)version})) {
@@ -2114,7 +2131,7 @@ int corro_bookie_seq_bookkeeping(corro_bookie *bk, const uint8_t *actor_id, uint
     if (so == bk->site_of.end()) return CORRO_OK;
     const SeqBook *sb = bk->seqbook.find({so->second, version});
     if (!sb) return CORRO_OK;
-    std::vector<Range> rs = sb->ranges;
+    std::vector<Range> rs(sb->ranges.begin(), sb->ranges.end());
     std::sort(rs.begin(), rs.end());
     uint64_t k = 0;
     for (const Range &r : rs) {

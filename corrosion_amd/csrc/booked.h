@@ -20,7 +20,7 @@ struct PartialVersion {
     uint64_t last_seq = 0;
     uint64_t ts = 0;
     // quirk kept from the reference: completeness is checked over 1..=last_seq, not 0..=last_seq
-    bool is_complete() const { return seqs.gaps(1, last_seq).empty(); }
+    bool is_complete() const { return !seqs.has_gap(1, last_seq); }
 };
 
 struct Booked {

@@ -5,6 +5,9 @@
 // Stored as one sorted vector of (start, end): lookups are binary searches, copies are one
 // allocation (a call's per-actor snapshot, VersionsSnapshot, copies the needed set), and the common
 // insert -- versions arriving in ascending order -- appends or extends the last range in O(1).
+// The vector keeps up to two ranges inline: a partial version's seq set or a seq book is one or two
+// ranges, and a mixed gossip call builds hundreds of thousands of them (a heap allocation each was
+// most of the host walk's time).
 #pragma once
 #include <algorithm>
 #include <cstdint>
@@ -13,10 +16,109 @@
 
 namespace corro {
 
+// a vector of small copyable T with N elements inline (the subset of std::vector the range code uses)
+template <class T, unsigned N>
+class SmallVec {
+  public:
+    SmallVec() = default;
+    SmallVec(const SmallVec &o) { assign(o.begin(), o.end()); }
+    SmallVec(SmallVec &&o) noexcept { take(o); }
+    ~SmallVec() { release(); }
+    SmallVec &operator=(const SmallVec &o) {
+        if (this != &o) {
+            n_ = 0;
+            assign(o.begin(), o.end());
+        }
+        return *this;
+    }
+    SmallVec &operator=(SmallVec &&o) noexcept {
+        if (this != &o) {
+            release();
+            take(o);
+        }
+        return *this;
+    }
+    T *begin() { return p_; }
+    T *end() { return p_ + n_; }
+    const T *begin() const { return p_; }
+    const T *end() const { return p_ + n_; }
+    T *data() { return p_; }
+    const T *data() const { return p_; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    T &back() { return p_[n_ - 1]; }
+    const T &back() const { return p_[n_ - 1]; }
+    T &operator[](size_t i) { return p_[i]; }
+    const T &operator[](size_t i) const { return p_[i]; }
+    void clear() { n_ = 0; }
+    void reserve(size_t c) {
+        if (c > cap_) grow(c);
+    }
+    void push_back(const T &x) {
+        if (n_ == cap_) grow(cap_ * 2);
+        p_[n_++] = x;
+    }
+    template <class... A>
+    void emplace_back(A &&...a) {
+        push_back(T{std::forward<A>(a)...});
+    }
+    T *insert(T *at, const T &x) {
+        const size_t k = at - p_;
+        if (n_ == cap_) grow(cap_ * 2);
+        std::copy_backward(p_ + k, p_ + n_, p_ + n_ + 1);
+        p_[k] = x;
+        n_++;
+        return p_ + k;
+    }
+    T *erase(T *a, T *b) {
+        std::copy(b, end(), a);
+        n_ -= b - a;
+        return a;
+    }
+
+  private:
+    void assign(const T *a, const T *b) {
+        reserve(b - a);
+        std::copy(a, b, p_);
+        n_ = b - a;
+    }
+    void grow(size_t c) {
+        T *q = new T[c];
+        std::copy(p_, p_ + n_, q);
+        const size_t n = n_;
+        release();
+        n_ = n;
+        p_ = q;
+        cap_ = c;
+    }
+    void release() {
+        if (p_ != in_) delete[] p_;
+        p_ = in_;
+        cap_ = N;
+    }
+    void take(SmallVec &o) {
+        if (o.p_ == o.in_) {
+            std::copy(o.in_, o.in_ + o.n_, in_);
+            p_ = in_;
+            cap_ = N;
+        } else {
+            p_ = o.p_;
+            cap_ = o.cap_;
+            o.p_ = o.in_;
+            o.cap_ = N;
+        }
+        n_ = o.n_;
+        o.n_ = 0;
+    }
+    T in_[N];
+    T *p_ = in_;
+    size_t n_ = 0, cap_ = N;
+};
+
 class RangeSet {
   public:
     using R = std::pair<uint64_t, uint64_t>;
-    using Vec = std::vector<R>;
+    using Vec = SmallVec<R, 2>;
 
     void insert(uint64_t s, uint64_t e) {
         if (s > e) return;
@@ -100,6 +202,13 @@ class RangeSet {
         }
         out.emplace_back(x, e);
         return out;
+    }
+
+    // gaps(s, e) non-empty, without building them
+    bool has_gap(uint64_t s, uint64_t e) const {
+        if (s > e) return false;
+        uint64_t a, b;
+        return !(get(s, a, b) && b >= e);  // (touching ranges coalesce: [s, e] covered = one range holds it)
     }
 
     bool contains_range(uint64_t s, uint64_t e) const {
