@@ -616,7 +616,8 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
             jbase[k] = jobs.size();
             jobs.insert(jobs.end(), outs[k].jobs.begin(), outs[k].jobs.end());
             for (auto &x : outs[k].add) add.push_back(std::move(x));
-        }        if (!all_dev.empty()) {
+        }
+        if (!all_dev.empty()) {
             std::vector<uint64_t> tc;
             TRY_RC(corro::agent_dev_table_counts(ctx, dv, all_dev, (uint32_t)ntables, tc));
             for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
