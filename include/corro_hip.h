@@ -344,7 +344,9 @@ int corro_apply_mapped(corro_ctx *ctx, const corro_changes *in, const uint32_t *
  * read by the apply itself (equal to corro_unpack_slots + corro_apply_mapped). out->impact (DEVICE, nsrc *
  * cap bytes) gets each received record's flag at its slot position -- padding 0 -- ready to go back to
  * the senders with one more equal-split all-to-all. *overflow_dev (DEVICE u32) = 1 when a source overflowed
- * its slot (nothing is then applied). Synchronous, like corro_apply_batch. INTEGER batches, no affinity. */
+ * its slot (nothing is then applied). Synchronous, like corro_apply_batch. INTEGER batches, no affinity.
+ * A layout larger than one apply chunk is validated whole, then applied as consecutive index ranges
+ * (application order = index order, so the result is that of one apply). */
 int corro_apply_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t cap, const uint64_t *src_counts_dev,
                       corro_apply_out *out, uint32_t *overflow_dev);
 /* The senders' side of those flags: back (DEVICE, nranks * cap, the all-to-all of every receiver's
