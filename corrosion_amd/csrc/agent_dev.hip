@@ -1319,13 +1319,15 @@ struct HGatherArgs {
     uint32_t *otab;  // a canonical one's table index when all its changes share it, else HDR_TAB_MIXED
 };
 
+// one wave per changeset: lane 0 copies the header, the lanes check its changes 64 at a time (the
+// canonical test reads five fields of every change: a lane-serial loop of them was a chain of
+// dependent latencies per changeset)
 __global__ void __launch_bounds__(AG_T) k_hdr_gather(HGatherArgs a) {
-    for (uint64_t k = (uint64_t)blockIdx.x * AG_T + threadIdx.x; k < a.n; k += (uint64_t)gridDim.x * AG_T) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * AG_T + threadIdx.x) >> 6, nw = (uint64_t)gridDim.x * (AG_T / 64);
+    for (uint64_t k = w0; k < a.n; k += nw) {  // (wave-uniform)
         const uint32_t i = a.order[a.slot[k]];
         const corro_changeset c = a.cs[i];
-        a.out[k] = c;
-        a.idx[k] = i;
-        a.obad[k] = a.bad[i];
         bool canon = c.kind == CORRO_CS_FULL && c.change_count && !(c.seq_start == 0 && c.seq_end == c.last_seq) &&
                      !a.bad[i] && c.seq_start <= c.seq_end && c.seq_end < 0xFFFFFFFFULL &&
                      c.change_count == c.seq_end - c.seq_start + 1 && c.version_start <= (uint64_t)INT64_MAX &&
@@ -1333,17 +1335,28 @@ __global__ void __launch_bounds__(AG_T) k_hdr_gather(HGatherArgs a) {
                      a.in.db_version;
         uint32_t tab = HDR_TAB_MIXED;
         if (canon && a.in.table_cid) tab = a.in.table_cid[c.change_off] >> 16;
-        for (uint64_t q = 0; canon && q < c.change_count; q++) {
-            const uint64_t r = c.change_off + q;
-            if (tab != HDR_TAB_MIXED && (a.in.table_cid[r] >> 16) != tab) tab = HDR_TAB_MIXED;
-            const uint8_t vt = a.in.val_type ? a.in.val_type[r] : (uint8_t)CORRO_INTEGER;
-            const uint8_t vl = a.in.val_len ? a.in.val_len[r] : 0;
-            canon = a.in.seq[r] == c.seq_start + q && a.in.site[r] == c.site &&
-                    (uint64_t)a.in.db_version[r] == c.version_start &&
-                    !(vl == CORRO_VAL_LONG && (vt == CORRO_TEXT || vt == CORRO_BLOB));
+        for (uint64_t q0 = 0; canon && q0 < c.change_count; q0 += 64) {  // (canon is wave-uniform)
+            const uint64_t q = q0 + lane;
+            bool ok = true;
+            if (q < c.change_count) {
+                const uint64_t r = c.change_off + q;
+                const uint8_t vt = a.in.val_type ? a.in.val_type[r] : (uint8_t)CORRO_INTEGER;
+                const uint8_t vl = a.in.val_len ? a.in.val_len[r] : 0;
+                ok = a.in.seq[r] == c.seq_start + q && a.in.site[r] == c.site &&
+                     (uint64_t)a.in.db_version[r] == c.version_start &&
+                     !(vl == CORRO_VAL_LONG && (vt == CORRO_TEXT || vt == CORRO_BLOB));
+                if (tab != HDR_TAB_MIXED && a.in.table_cid && (a.in.table_cid[r] >> 16) != tab) tab = HDR_TAB_MIXED;
+            }
+            canon = __all(ok);
+            if (!__all(tab != HDR_TAB_MIXED)) tab = HDR_TAB_MIXED;
         }
-        a.ocanon[k] = canon ? 1 : 0;
-        a.otab[k] = canon ? tab : HDR_TAB_MIXED;
+        if (lane == 0) {
+            a.out[k] = c;
+            a.idx[k] = i;
+            a.obad[k] = a.bad[i];
+            a.ocanon[k] = canon ? 1 : 0;
+            a.otab[k] = canon ? tab : HDR_TAB_MIXED;
+        }
     }
 }
 
@@ -1587,7 +1600,7 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         g.obad = base + o_bad;
         g.ocanon = base + o_can;
         g.otab = reinterpret_cast<uint32_t *>(base + o_tab);
-        hipLaunchKernelGGL(k_hdr_gather, flat_grid(nh), dim3(AG_T), 0, s, g);
+        hipLaunchKernelGGL(k_hdr_gather, wave_grid(nh), dim3(AG_T), 0, s, g);
         CORRO_HIP_TRY(hipGetLastError());
         uint8_t *hp = static_cast<uint8_t *>(ctx->h_hfetch);
         CORRO_HIP_TRY(hipMemcpyAsync(hp, base, total_b, hipMemcpyDeviceToHost, s));
