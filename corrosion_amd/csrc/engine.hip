@@ -1190,7 +1190,9 @@ static int apply_batch_impl(corro_ctx *ctx, const corro_changes *in, int mem, co
     if (ctx->track_touched) TRY(touch_reserve(ctx, n));
     // (a slot layout carries its padding: up to a quarter more slots than applied records, one chunk still)
     const uint64_t chunk = ctx->pm_ap ? std::max<uint64_t>(n, 1) : ctx->slot_rec ? chunk_cap : corro_detail_chunk_changes(ctx);
-    if (n > chunk) {
+    // (slot mode: corro_partition_slots validated the records it packed and marks a failed batch's
+    // counts, so the layout needs no validation pass before its first chunk commits)
+    if (n > chunk && !bd.slot_rec) {
         CORRO_HIP_TRY(hipMemsetAsync(ctx->d_misc.p, 0, 8 * 8, s));
         hipLaunchKernelGGL(k_validate, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, bd,
                            nsites, ctx->d_ncols.as<uint16_t>(), (uint32_t)ctx->tables.size(),

@@ -49,8 +49,9 @@ k_part_count(BatchDev in, uint32_t tile, uint32_t nranks, uint32_t *__restrict__
 // one workgroup: counts[t][r] -> absolute output position of tile t's first change for rank r;
 // totals[r] = changes for rank r. cap > 0: rank r's group starts at r * cap (the slot layout)
 __global__ void k_part_scan(uint32_t *__restrict__ counts, uint32_t ntiles, uint32_t nranks,
-                            uint64_t *__restrict__ totals, uint64_t cap = 0) {
+                            uint64_t *__restrict__ totals, uint64_t cap = 0, unsigned long long *err = nullptr) {
     __shared__ uint64_t base[PART_MAX_RANKS];
+    if (err && threadIdx.x == 0) *err = 0;  // (the slot partition's validation word, set by k_part_pack)
     if (threadIdx.x < nranks) {
         const uint32_t r = threadIdx.x;
         uint64_t run = 0;
@@ -149,11 +150,20 @@ struct __attribute__((aligned(16))) PackedRec80 {
 };
 static_assert(sizeof(PackedRec48) == 48 && sizeof(PackedRec80) == 80, "packed record sizes");
 
+// The slot partition validates what it packs (the checks corro_apply_batch makes before its first
+// write: names, site ordinal, causal-length ranges, db_version), so the receiver can apply the slots
+// in several chunks without a whole-layout validation pass first; err != null turns it on.
+struct PartCheck {
+    const uint16_t *ncols;
+    uint32_t ntables, nsites;
+    unsigned long long *err;
+};
+
 // stable scatter of whole records (same ranking as k_part_scatter); perm[pos] = source index
 template <bool PLAIN>
 __global__ void __launch_bounds__(PART_THREADS)
 k_part_pack(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restrict__ offs, void *__restrict__ out,
-            uint32_t *__restrict__ perm, uint64_t cap = 0) {
+            uint32_t *__restrict__ perm, uint64_t cap = 0, PartCheck chk = PartCheck{}) {
     __shared__ uint32_t run[PART_MAX_RANKS];
     __shared__ uint32_t wcnt[PART_THREADS / 64][PART_MAX_RANKS];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -173,6 +183,16 @@ k_part_pack(BatchDev in, uint32_t tile, uint32_t nranks, const uint32_t *__restr
             const uint64_t m = __ballot(d == r);
             if (d == r) my_rank = __popcll(m & lt);
             if (lane == 0) wcnt[w][r] = __popcll(m);
+        }
+        if (PLAIN && chk.err) {
+            bool bad = false;
+            if (act) {
+                const uint32_t t = tc >> 16, cid = tc & 0xFFFFu, cl = in.cl[i];
+                const int64_t cv = in.cv[i];
+                bad = t >= chk.ntables || cid > chk.ncols[t] || in.site[i] >= chk.nsites ||
+                      ((cid == 0 || (cl & 1u) == 0) && (cv < 0 || cv > 0xFFFFFFFFLL)) || in.dbv[i] < 0;
+            }
+            if (__ballot(bad) && lane == 0) atomicOr(chk.err, 1ULL);
         }
         __syncthreads();
         if (act) {
@@ -453,7 +473,7 @@ extern "C" int corro_partition_ranks(corro_ctx *ctx, const corro_changes *in, ui
     uint32_t tile = (n + ntiles - 1) / ntiles;
     tile = (tile + PART_THREADS - 1) / PART_THREADS * PART_THREADS;
     ntiles = (n + tile - 1) / tile;
-    if (int rc = ctx->d_part.ensure((size_t)ntiles * nranks * 4 + nranks * 8 + 256)) return rc;
+    if (int rc = ctx->d_part.ensure((size_t)ntiles * nranks * 4 + (PART_MAX_RANKS + 1) * 8 + 512)) return rc;
     uint32_t *d_counts = ctx->d_part.as<uint32_t>();
     uint64_t *d_tot = reinterpret_cast<uint64_t *>(ctx->d_part.as<uint8_t>() + (((size_t)ntiles * nranks * 4 + 255) / 256) * 256);
     hipLaunchKernelGGL(k_part_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts);
@@ -471,7 +491,7 @@ static int part_tiles(corro_ctx *ctx, uint32_t n, uint32_t nranks, uint32_t &nti
     tile = (n + ntiles - 1) / ntiles;
     tile = (tile + PART_THREADS - 1) / PART_THREADS * PART_THREADS;
     ntiles = (n + tile - 1) / tile;
-    if (int rc = ctx->d_part.ensure((size_t)ntiles * nranks * 4 + nranks * 8 + 256)) return rc;
+    if (int rc = ctx->d_part.ensure((size_t)ntiles * nranks * 4 + (PART_MAX_RANKS + 1) * 8 + 512)) return rc;
     d_counts = ctx->d_part.as<uint32_t>();
     d_tot = reinterpret_cast<uint64_t *>(ctx->d_part.as<uint8_t>() + (((size_t)ntiles * nranks * 4 + 255) / 256) * 256);
     return CORRO_OK;
@@ -546,6 +566,13 @@ extern "C" int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n
 // ---------------------------------------------------------------------- stream-ordered slots
 extern "C" void *corro_ctx_stream(corro_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+// a batch that failed the partition's validation marks every destination's count (bit 63): each
+// receiver then sees an overflowed slot, applies nothing from the slot pass, and the exchange repeats
+// with exact sizes through the validating apply, which reports the error
+__global__ void k_part_mark(uint64_t *__restrict__ counts, uint32_t nranks, const unsigned long long *__restrict__ err) {
+    if (*err && threadIdx.x < nranks) counts[threadIdx.x] |= 1ULL << 63;
+}
+
 extern "C" int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, uint64_t cap, void *out,
                                      uint64_t *counts_dev, uint32_t *perm_dev) {
     if (!ctx || !in || !out || !counts_dev) return fail(CORRO_E_INVALID, "NULL argument");
@@ -570,11 +597,13 @@ extern "C" int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, ui
     uint64_t *d_tot;
     if (int rc = part_tiles(ctx, n, nranks, ntiles, tile, d_counts, d_tot)) return rc;
     hipLaunchKernelGGL(k_part_count, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, counts_dev, cap);
+    unsigned long long *err = reinterpret_cast<unsigned long long *>(d_tot + PART_MAX_RANKS);
+    const PartCheck chk{ctx->d_ncols.as<uint16_t>(), (uint32_t)ctx->tables.size(), (uint32_t)ctx->sites.size(), err};
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, d_counts, ntiles, nranks, counts_dev, cap, err);
     hipLaunchKernelGGL(k_part_pack<true>, dim3(ntiles), dim3(PART_THREADS), 0, s, bd, tile, nranks, d_counts, out,
-                       perm_dev, cap);
+                       perm_dev, cap, chk);
+    hipLaunchKernelGGL(k_part_mark, dim3(1), dim3(64), 0, s, counts_dev, nranks, (const unsigned long long *)err);
     CORRO_HIP_TRY(hipGetLastError());
-    (void)d_tot;
     return CORRO_OK;  // (no host wait: everything is queued on ctx->stream)
 }
 
@@ -586,7 +615,7 @@ __global__ void k_slots_back(const uint8_t *__restrict__ back, uint32_t nranks, 
     const uint64_t m = (uint64_t)nranks * cap;
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < m; p += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t d = p / cap;
-        if (p - d * cap >= cnt[d]) continue;
+        if (p - d * cap >= (cnt[d] & ~(1ULL << 63))) continue;  // (bit 63: the partition's validation mark)
         const uint32_t i = perm[p];
         if (i < n) flags[i] = back[p];
     }

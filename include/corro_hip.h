@@ -328,7 +328,10 @@ int corro_unpack_records(corro_ctx *ctx, const void *recs, uint64_t n, uint32_t 
 int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, uint32_t nranks, uint64_t cap, void *out,
                           uint64_t *counts_dev, uint32_t *perm_dev);
 /* (perm_dev, optional DEVICE u32 of nranks * cap: perm_dev[slot position] = the input index packed there,
- * for the impact flags coming back, corro_slots_flags_back.) */
+ * for the impact flags coming back, corro_slots_flags_back.) The partition validates the records it
+ * packs as corro_apply_batch would before writing (names, site ordinals, causal-length ranges,
+ * db_version); a batch that fails sets bit 63 of every count, which every receiver reads as an
+ * overflowed slot: nothing is applied from the slots and the exact-size exchange reports the error. */
 /* Received slots (nsrc slots of cap records, src_counts_dev[s] = DEVICE count source s sent) ->
  * the SoA batch at the same indices (device, nsrc * cap each) and ap[i] = i for a received record,
  * CORRO_AP_SKIP for a slot's padding; *overflow_dev (device u32) = 1 when a source sent more than
@@ -345,8 +348,9 @@ int corro_apply_mapped(corro_ctx *ctx, const corro_changes *in, const uint32_t *
  * cap bytes) gets each received record's flag at its slot position -- padding 0 -- ready to go back to
  * the senders with one more equal-split all-to-all. *overflow_dev (DEVICE u32) = 1 when a source overflowed
  * its slot (nothing is then applied). Synchronous, like corro_apply_batch. INTEGER batches, no affinity.
- * A layout larger than one apply chunk is validated whole, then applied as consecutive index ranges
- * (application order = index order, so the result is that of one apply). */
+ * A layout larger than one apply chunk is applied as consecutive index ranges (application order =
+ * index order, so the result is that of one apply); the records must come from corro_partition_slots,
+ * which validated them: a source whose batch failed marks its counts and the receiver applies nothing. */
 int corro_apply_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t cap, const uint64_t *src_counts_dev,
                       corro_apply_out *out, uint32_t *overflow_dev);
 /* The senders' side of those flags: back (DEVICE, nranks * cap, the all-to-all of every receiver's

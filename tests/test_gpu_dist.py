@@ -303,3 +303,49 @@ def test_two_rank_slot_exchange_equals_single_engine(tmp_path, cap_scale, chunk,
     f.apply(batch)
     assert O.rows_diff(e.export(), f.export()) is None
     assert list(e.db_versions()) == list(f.db_versions())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad", ["site", "table", "col_version", None])
+def test_slot_partition_validates_and_marks_counts(bad):
+    """corro_partition_slots validates what it packs (the apply's pre-write checks) and marks every
+    destination's count (bit 63) when the batch fails them: the receiver then sees an overflowed slot
+    and applies nothing -- even when its slots span several apply chunks, whose whole-layout validation
+    pass it no longer runs -- and the exchange repeats through the validating apply. A valid batch is
+    unmarked and merges as one engine would."""
+    import torch
+    import corrosion_amd as ca
+    from corrosion_amd.dist import slot_cap
+    full = synth.uniform_batch(NS, 16, 4000, 4, 77)
+    if bad == "site":
+        full["site"][NS // 3] = 999
+    elif bad == "table":
+        full["table_cid"][NS // 2] = (7 << 16) | 1
+    elif bad == "col_version":
+        full["cl"][NS // 4] = 2
+        full["col_version"][NS // 4] = -5
+    dev = _to_dev(full)
+    world = 2
+    cap = slot_cap(NS, world)
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS, device=0)
+    eng.register_sites(synth.site_ids(16, 5))
+    recs, cnt = eng.partition_slots(dev, world, cap)
+    torch.cuda.synchronize()
+    marked = (cnt.cpu() < 0).tolist()  # (bit 63 reads as a negative int64)
+    assert all(marked) == (bad is not None) and any(marked) == (bad is not None)
+    os.environ["CORRO_HIP_CHUNK"] = "4096"  # (the slot layout as several chunks)
+    try:
+        _, over = eng.apply_slots(recs, world, cap, cnt)
+    finally:
+        del os.environ["CORRO_HIP_CHUNK"]
+    torch.cuda.synchronize()
+    assert int(over.item()) == (1 if bad else 0)
+    if bad:
+        assert eng.count() == 0
+        with pytest.raises(ca.CorroError):
+            eng.apply(dev)
+    else:
+        e = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS)
+        e.register_sites(synth.site_ids(16, 5))
+        e.apply(full)
+        assert rows_to_tuples(eng.export(), with_ts=True) == rows_to_tuples(e.export(), with_ts=True)
