@@ -470,6 +470,38 @@ void seq_pieces(const SegList &segs, uint64_t s, uint64_t e, std::vector<Range> 
     if (x <= e) out.emplace_back(x, e);
 }
 
+// One key's share of one staged INSERT batch (the item's fields copied in: the commit passes walk
+// the subs in key order without chasing pointers)
+struct CommitSub {
+    BufKey key;
+    uint64_t call;
+    Staged *st;
+    uint64_t a, b;     // (host) rows [a, b) of st->buffered, all of this key
+    uint64_t fr;       // (dev, fetched) first row in the fetched rows
+    uint64_t src, ts;  // (dev) the item's input span start and ts
+    uint32_t seq0, n;  // (dev) its first seq and change count
+    bool dev;
+    bool tc;           // (dev) its changes' tables are counted on the device (k_tab_count)
+};
+
+// What commit_prepare computes without writing the bookie (so it can run on another host thread while
+// the merge runs): the subs by actor, and on the fast path the copy jobs, the new keys and, for keys
+// the bookie already holds, their entries with this call's segments added (copies, swapped in by
+// commit_prepared). Pending segment offsets name (block, local job) until the pool append.
+struct CommitPrep {
+    bool any = false;                          // some staged item
+    bool fast = false;                         // the fast path below applies
+    std::vector<std::vector<CommitSub>> per;   // per actor, sorted by (key, call)
+    std::vector<size_t> blk;                   // actors with subs, by first key
+    std::vector<uint64_t> committed;           // per table: the buffered changes counted on the host
+    std::vector<corro::AgentSpan> all_dev;     // (fast) mixed-table spans, counted on the device
+    std::vector<corro::PoolCopy> jobs;         // (fast) pool copy jobs, block-major
+    std::vector<size_t> jbase;                 // (fast) first job of each block
+    std::vector<std::pair<BufKey, BufEntry>> add;  // (fast) new keys, ascending
+    std::vector<std::pair<BufKey, BufEntry>> upd;  // (fast) held keys: their updated entries
+    std::string prof;                          // stage marks (CORRO_AGENT_PROFILE)
+};
+
 // The call's staged __corro_buffered_changes INSERTs into the bookie; ON CONFLICT (site_id,
 // db_version, seq) DO NOTHING: the first row of a key wins. Keys are independent, so the INSERTs are
 // grouped by key, each key's in call order (actors in `order` = ActorId order, as util.rs:765 walks
@@ -477,30 +509,17 @@ void seq_pieces(const SegList &segs, uint64_t s, uint64_t e, std::vector<Range> 
 // (util.rs:1101-1105). A key stays in the device pool while all its rows come from canonical
 // changesets (segments trimmed against the key's earlier ones); a key that receives host rows is
 // brought to the host first. dv: the call's device batch (null: host rows only).
-int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, const std::vector<Staged *> &order,
-                       std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage) {
-    auto mark = [&](const char *n) {
-        if (stage) stage(n);
-    };
-    const size_t ntables = committed.size();
-    struct Sub {  // one key's share of one staged INSERT batch (the item's fields copied in: the
-                  // passes below walk the subs in key order without chasing pointers)
-        BufKey key;
-        uint64_t call;
-        Staged *st;
-        uint64_t a, b;  // (host) rows [a, b) of st->buffered, all of this key
-        uint64_t fr;    // (dev, fetched) first row in the fetched rows
-        uint64_t src, ts;  // (dev) the item's input span start and ts
-        uint32_t seq0, n;  // (dev) its first seq and change count
-        bool dev;
-        bool tc;           // (dev) its changes' tables are counted on the device (k_tab_count)
-    };
-    bool any_items = false;
-    for (Staged *st : order) any_items |= !st->items.empty();
-    if (!any_items) return CORRO_OK;
+// commit_prepare: the part that only READS the bookie (thread-safe against the merge).
+void commit_prepare(corro_ctx *ctx, const corro_bookie *bk, bool have_dv, const std::vector<Staged *> &order,
+                    size_t ntables, CommitPrep &P, const std::function<void(const char *)> &mark) {
+    using Sub = CommitSub;
+    P.committed.assign(ntables, 0);
+    for (Staged *st : order) P.any |= !st->items.empty();
+    if (!P.any) return;
     // per actor (in parallel): its subs sorted by (key, call), call = ActorId rank << 40 | walk index;
     // the actors' blocks concatenated by first key are globally sorted unless two actors share a key
-    std::vector<std::vector<Sub>> per(order.size());
+    std::vector<std::vector<Sub>> &per = P.per;
+    per.assign(order.size(), {});
     std::vector<std::vector<uint64_t>> ptab(order.size(), std::vector<uint64_t>(ntables, 0));
     std::vector<uint8_t> host_rows(order.size(), 0);  // the actor staged host rows
     run_parallel(order.size(), [&](size_t ai) {
@@ -530,15 +549,13 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
     });
     mark("cb_subs");
     for (const auto &t : ptab)
-        for (size_t k = 0; k < ntables; k++) committed[k] += t[k];
-    std::vector<size_t> blk;
+        for (size_t k = 0; k < ntables; k++) P.committed[k] += t[k];
+    std::vector<size_t> &blk = P.blk;
     for (size_t ai = 0; ai < per.size(); ai++)
         if (!per[ai].empty()) blk.push_back(ai);
     std::sort(blk.begin(), blk.end(), [&](size_t x, size_t y) { return per[x][0].key < per[y][0].key; });
-    const bool pool_ok = dv && (bk->pool ? corro::bufpool_usable(ctx, bk->pool) : true);
+    const bool pool_ok = have_dv && (bk->pool ? corro::bufpool_usable(ctx, bk->pool) : true);
     const bool any_buffered = bk->buffered.slots() != 0;
-    std::vector<corro::PoolCopy> jobs;
-    std::vector<std::pair<BufKey, BufEntry>> add;
     // Fast path -- the common shape: every sub a canonical device changeset, the actors' key ranges
     // disjoint (each actor's keys carry its own site) and no key holding host rows. Then no group is
     // host, nothing is fetched or materialized, and each actor's groups, segment trims and copy jobs
@@ -564,68 +581,114 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
         });
         for (uint8_t h : hostkey) fast = fast && !h;
     }
-    std::vector<size_t> jbase;  // fast path: first global job of each block
-    if (fast) {
-        struct Out {
-            std::vector<corro::AgentSpan> dev;
-            std::vector<corro::PoolCopy> jobs;
-            std::vector<std::pair<BufKey, BufEntry>> add;
-        };
-        std::vector<Out> outs(blk.size());
-        run_parallel(blk.size(), [&](size_t k) {
-            const std::vector<Sub> &v = per[blk[k]];
-            Out &o = outs[k];
-            o.dev.reserve(v.size());
-            std::vector<Range> pieces;
-            for (size_t g0 = 0; g0 < v.size();) {
-                size_t g1 = g0 + 1;
-                while (g1 < v.size() && v[g1].key == v[g0].key) g1++;
-                BufEntry local;
-                BufEntry *e = any_buffered ? bk->buffered.find(v[g0].key) : nullptr;  // (keys of this block only)
-                const bool fresh = !e;
-                if (fresh) e = &local;
-                for (size_t q = g0; q < g1; q++) {
-                    const Sub &u = v[q];
-                    if (u.tc) o.dev.push_back({u.src, 0, u.n, u.ts});
-                    seq_pieces(e->segs, u.seq0, (uint64_t)u.seq0 + u.n - 1, pieces);
-                    for (const Range &r : pieces) {
-                        const PoolSeg g{SEG_PENDING | ((uint64_t)k << 32) | o.jobs.size(), (uint32_t)r.first,
-                                        (uint32_t)(r.second - r.first + 1)};
-                        o.jobs.push_back({u.src + (r.first - u.seq0), r.second - r.first + 1, u.ts, 0});
-                        e->segs.insert_sorted(g);
-                    }
+    P.fast = fast;
+    if (!fast) return;
+    struct Out {
+        std::vector<corro::AgentSpan> dev;
+        std::vector<corro::PoolCopy> jobs;
+        std::vector<std::pair<BufKey, BufEntry>> add, upd;
+    };
+    std::vector<Out> outs(blk.size());
+    run_parallel(blk.size(), [&](size_t k) {
+        const std::vector<Sub> &v = per[blk[k]];
+        Out &o = outs[k];
+        o.dev.reserve(v.size());
+        std::vector<Range> pieces;
+        for (size_t g0 = 0; g0 < v.size();) {
+            size_t g1 = g0 + 1;
+            while (g1 < v.size() && v[g1].key == v[g0].key) g1++;
+            // a held key works on a copy of its entry (swapped in after the merge); a new key on a fresh one
+            const BufEntry *held = any_buffered ? bk->buffered.find(v[g0].key) : nullptr;  // (keys of this block only)
+            BufEntry local;
+            if (held) local = *held;
+            for (size_t q = g0; q < g1; q++) {
+                const Sub &u = v[q];
+                if (u.tc) o.dev.push_back({u.src, 0, u.n, u.ts});
+                seq_pieces(local.segs, u.seq0, (uint64_t)u.seq0 + u.n - 1, pieces);
+                for (const Range &r : pieces) {
+                    const PoolSeg g{SEG_PENDING | ((uint64_t)k << 32) | o.jobs.size(), (uint32_t)r.first,
+                                    (uint32_t)(r.second - r.first + 1)};
+                    o.jobs.push_back({u.src + (r.first - u.seq0), r.second - r.first + 1, u.ts, 0});
+                    local.segs.insert_sorted(g);
                 }
-                if (fresh && !local.empty()) o.add.emplace_back(v[g0].key, std::move(local));
-                g0 = g1;
             }
-        });
-        mark("cb_groups");
-        std::vector<corro::AgentSpan> all_dev;
-        size_t nd = 0, nj = 0, na = 0;
-        for (const Out &o : outs) {
-            nd += o.dev.size();
-            nj += o.jobs.size();
-            na += o.add.size();
+            if (held) o.upd.emplace_back(v[g0].key, std::move(local));
+            else if (!local.empty()) o.add.emplace_back(v[g0].key, std::move(local));
+            g0 = g1;
         }
-        all_dev.reserve(nd);
-        jobs.reserve(nj);
-        add.reserve(na);
-        jbase.resize(blk.size());
-        for (size_t k = 0; k < outs.size(); k++) {
-            all_dev.insert(all_dev.end(), outs[k].dev.begin(), outs[k].dev.end());
-            jbase[k] = jobs.size();
-            jobs.insert(jobs.end(), outs[k].jobs.begin(), outs[k].jobs.end());
-            for (auto &x : outs[k].add) add.push_back(std::move(x));
-        }
-        if (!all_dev.empty()) {
-            std::vector<uint64_t> tc;
-            TRY_RC(corro::agent_dev_table_counts(ctx, dv, all_dev, (uint32_t)ntables, tc));
-            for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
-        }
-        mark("cb_tables");
-        if (!bk->pool) bk->pool = corro::bufpool_new();
-        mark("cb_trim");
-    } else {
+    });
+    mark("cb_groups");
+    size_t nd = 0, nj = 0, na = 0, nu = 0;
+    for (const Out &o : outs) {
+        nd += o.dev.size();
+        nj += o.jobs.size();
+        na += o.add.size();
+        nu += o.upd.size();
+    }
+    P.all_dev.reserve(nd);
+    P.jobs.reserve(nj);
+    P.add.reserve(na);
+    P.upd.reserve(nu);
+    P.jbase.resize(blk.size());
+    for (size_t k = 0; k < outs.size(); k++) {
+        P.all_dev.insert(P.all_dev.end(), outs[k].dev.begin(), outs[k].dev.end());
+        P.jbase[k] = P.jobs.size();
+        P.jobs.insert(P.jobs.end(), outs[k].jobs.begin(), outs[k].jobs.end());
+        for (auto &x : outs[k].add) P.add.push_back(std::move(x));
+        for (auto &x : outs[k].upd) P.upd.push_back(std::move(x));
+    }
+    mark("cb_tables");
+}
+
+// the pool copy of the jobs and the pending offsets resolved (both paths)
+int commit_pool(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, std::vector<corro::PoolCopy> &jobs, bool fast,
+                const std::vector<size_t> &jbase, const std::function<void(const char *)> &mark);
+
+// The fast path's writes, after the merge: the device table counts of mixed-table spans, the held
+// keys' updated entries swapped in, the new keys merged, then the pool copy.
+int commit_prepared(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, CommitPrep &P, std::vector<uint64_t> &committed,
+                    const std::function<void(const char *)> &mark) {
+    const size_t ntables = committed.size();
+    for (size_t t = 0; t < ntables; t++) committed[t] += P.committed[t];
+    if (!P.all_dev.empty()) {
+        std::vector<uint64_t> tc;
+        TRY_RC(corro::agent_dev_table_counts(ctx, dv, P.all_dev, (uint32_t)ntables, tc));
+        for (size_t t = 0; t < ntables; t++) committed[t] += tc[t];
+    }
+    if (!bk->pool) bk->pool = corro::bufpool_new();
+    for (auto &[key, e] : P.upd) {
+        BufEntry *x = bk->buffered.find(key);
+        if (!x) throw std::logic_error("buffered key vanished between prepare and commit");
+        *x = std::move(e);
+    }
+    mark("cb_trim");
+    bk->buffered.merge(std::move(P.add));
+    mark("cb_merge");
+    return commit_pool(ctx, bk, dv, P.jobs, true, P.jbase, mark);
+}
+
+int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, const std::vector<Staged *> &order,
+                       std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage,
+                       CommitPrep *prepared = nullptr) {
+    using Sub = CommitSub;
+    auto mark = [&](const char *n) {
+        if (stage) stage(n);
+    };
+    const size_t ntables = committed.size();
+    CommitPrep own;
+    CommitPrep &P = prepared ? *prepared : own;
+    if (!prepared) commit_prepare(ctx, bk, dv != nullptr, order, ntables, P, mark);
+    if (!P.any) return CORRO_OK;
+    if (P.fast) return commit_prepared(ctx, bk, dv, P, committed, mark);
+    for (size_t t = 0; t < ntables; t++) committed[t] += P.committed[t];
+    std::vector<std::vector<Sub>> &per = P.per;
+    const std::vector<size_t> &blk = P.blk;
+    const bool pool_ok = dv && (bk->pool ? corro::bufpool_usable(ctx, bk->pool) : true);
+    const bool any_buffered = bk->buffered.slots() != 0;
+    std::vector<corro::PoolCopy> jobs;
+    std::vector<std::pair<BufKey, BufEntry>> add;
+    const std::vector<size_t> jbase;
+    {
     std::vector<Sub> sp;  // every sub in (key, call) order, contiguous
     size_t nsub = 0;
     for (size_t ai : blk) nsub += per[ai].size();
@@ -731,6 +794,11 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
     }  // (serial path)
     bk->buffered.merge(std::move(add));
     mark("cb_merge");
+    return commit_pool(ctx, bk, dv, jobs, false, jbase, mark);
+}
+
+int commit_pool(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, std::vector<corro::PoolCopy> &jobs, bool fast,
+                const std::vector<size_t> &jbase, const std::function<void(const char *)> &mark) {
     if (jobs.empty()) return CORRO_OK;
     uint64_t need = 0;
     for (const corro::PoolCopy &j : jobs) need += j.count;
@@ -768,8 +836,9 @@ int commit_staged_impl(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv
 // They are dropped again (keys left without rows are erased), so the bookie never names pool rows
 // that were not copied and no seq counts as buffered that is not: a re-sent piece buffers again.
 int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, const std::vector<Staged *> &order,
-                  std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage = nullptr) {
-    const int rc = commit_staged_impl(ctx, bk, dv, order, committed, stage);
+                  std::vector<uint64_t> &committed, const std::function<void(const char *)> &stage = nullptr,
+                  CommitPrep *prepared = nullptr) {
+    const int rc = commit_staged_impl(ctx, bk, dv, order, committed, stage, prepared);
     if (rc == CORRO_OK) return rc;
     for (size_t i = 0; i < bk->buffered.slots(); i++) {
         auto &x = bk->buffered.at(i);
@@ -1487,6 +1556,46 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
 
     const uint32_t ntables = corro::agent_table_count(ctx);
     std::vector<uint64_t> committed(ntables, 0);
+    // actors in ActorId order: the device sort's site-rank order (each actor's first sorted slot)
+    std::vector<size_t> order(work.size());
+    for (size_t k = 0; k < order.size(); k++) order[k] = k;
+    std::sort(order.begin(), order.end(),
+              [&](size_t x, size_t y) { return R.sites[work[x].site].gstart < R.sites[work[y].site].gstart; });
+    std::vector<Staged *> sto;
+    for (size_t k : order) sto.push_back(&work[k].st);
+    // The buffered-row commit's preparation only reads the bookie and the staged rows, so it runs on a
+    // host thread while the merge runs on the device (its writes wait for the merge: a failed merge
+    // leaves the bookie as it was).
+    CommitPrep prep;
+    std::string prep_err;
+    bool prep_started = false;
+    std::thread prep_thread;
+    if (nh >= 4096) {
+        prep_started = true;
+        prep_thread = std::thread([&, have_dv = nchanges != 0] {
+            auto t0 = std::chrono::steady_clock::now();
+            auto markp = [&](const char *name) {
+                if (!prof) return;
+                const auto t = std::chrono::steady_clock::now();
+                prep.prof += std::string(" ") + name + "=" +
+                             std::to_string(std::chrono::duration<double, std::milli>(t - t0).count()).substr(0, 6);
+                t0 = t;
+            };
+            try {
+                commit_prepare(ctx, bk, have_dv, sto, ntables, prep, markp);
+            } catch (const std::exception &e) {
+                prep_err = e.what();
+            } catch (...) {
+                prep_err = "unknown host exception";
+            }
+        });
+    }
+    struct JoinPrep {  // (every return path waits for the preparation thread)
+        std::thread &t;
+        ~JoinPrep() {
+            if (t.joinable()) t.join();
+        }
+    } join_prep{prep_thread};
     if (nb || out->impactful) {
         corro_changes batch{};
         const uint8_t *imp = nullptr;
@@ -1523,17 +1632,13 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             for (uint64_t version : w.set_dbv) sv.emplace_back(w.site, version);
         TRY_RC(corro::set_db_versions(ctx, sv));
     }
-    // actors in ActorId order: the device sort's site-rank order (each actor's first sorted slot)
-    std::vector<size_t> order(work.size());
-    for (size_t k = 0; k < order.size(); k++) order[k] = k;
-    std::sort(order.begin(), order.end(),
-              [&](size_t x, size_t y) { return R.sites[work[x].site].gstart < R.sites[work[y].site].gstart; });
-    {
-        std::vector<Staged *> sto;
-        for (size_t k : order) sto.push_back(&work[k].st);
-        TRY_RC(commit_staged(ctx, bk, nchanges ? &dv : nullptr, sto, committed, stage));
-        commit_seqbook(bk, sto);
+    if (prep_started) {
+        prep_thread.join();
+        if (!prep_err.empty()) return fail(CORRO_E_INVALID, "process_multiple_changes: " + prep_err);
+        if (prof) prof_line += " [prepared alongside the merge:" + prep.prof + "]";
     }
+    TRY_RC(commit_staged(ctx, bk, nchanges ? &dv : nullptr, sto, committed, stage, prep_started ? &prep : nullptr));
+    commit_seqbook(bk, sto);
     stage("seqbook");
     // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303): the merged versions that hold
     // buffered rows or seq bookkeeping, found on the device against the (small) set of such keys

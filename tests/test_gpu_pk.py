@@ -264,3 +264,31 @@ def test_blob_pk_config2_size_vs_sharded_oracle():
     assert O.rows_digest(rows) == f.digest()
     assert np.array_equal(e.db_versions(), f.db_versions())
     e.close()
+
+
+def test_intern_table_grows_past_its_probe_bound():
+    """A call bringing far more new keys than the table was sized for (1.5 M after 1000): probes run
+    past PK_MAX_PROBE, the call retries on tables four times larger (rebuilt from the keys on the
+    device) until every key finds a slot -- the earlier keys keep their ids, the new ones are dense
+    after them, duplicates inside the call share one id, and ids map back to their bytes."""
+    import torch
+    import corrosion_amd as ca
+    import synth
+    e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12, interned=INTERNED)
+    ids1 = torch.arange(1000, device="cuda")
+    b1, o1 = synth.blob_pks_torch(ids1)
+    k1 = e.pk_keys_device("testsblob", b1, o1).cpu().numpy().view(np.uint64)
+    assert sorted(k1.tolist()) == list(range(1000))
+    n2 = 1_500_000
+    ids2 = torch.cat([torch.arange(n2, device="cuda"), torch.arange(0, n2, 7, device="cuda")])  # (with repeats)
+    b2, o2 = synth.blob_pks_torch(ids2)
+    k2 = e.pk_keys_device("testsblob", b2, o2).cpu().numpy().view(np.uint64)
+    assert np.array_equal(k2[:1000], k1)                      # earlier keys keep their ids
+    first = k2[:n2]
+    assert np.unique(first).size == n2 and int(first.max()) == n2 - 1  # dense, one id per distinct key
+    assert np.array_equal(k2[n2:], first[::7])                # repeats inside the call share the id
+    rng = np.random.default_rng(3)
+    pick = rng.integers(0, n2, 200)
+    got = e.pk_bytes("testsblob", first[pick])
+    raw = b2.cpu().numpy()
+    assert got == [bytes(raw[19 * i:19 * i + 19]) for i in pick.tolist()]
