@@ -114,3 +114,37 @@ def test_failure_after_the_merge_poisons_the_context(monkeypatch):
     eng.reset()                                        # the caller re-seeds state and bookie
     bk = ca.agent.Bookie()
     _run(eng, bk, ords, full + first, "headers")
+
+
+def test_failed_merge_leaves_the_bookie_as_it_was():
+    """A call large enough that its buffered-row commit is prepared on a host thread alongside the
+    merge (>= 4096 host-walked changesets): when the merge fails (a sentinel with a negative
+    col_version: CORRO_E_RANGE before anything is written) the call fails as a whole -- the bookie holds
+    nothing of it, the context is not poisoned, and the same call without the bad changeset then gives
+    what a twin that never saw the failure gives."""
+    import corrosion_amd as ca
+    import synth
+    from oracle.agent import Changeset
+    nver = 40
+    ids = synth.site_ids(64, 29)
+    eng, bk, ords = _side(ids)
+    twin, tbk, tords = _side(ids)
+    first, second, full = _pieces(ids, ords, nver, 7)
+    call = [x for pair in zip(first, second) for x in pair] + full
+    assert len(first) + len(second) >= 4096
+    aid = ids[0]
+    bad = Changeset(aid, "full", version=nver + 2, seqs=(0, 0), last_seq=0, ts=9,
+                    rows=[dict(pk=3, table_cid=0, col_version=-1, db_version=nver + 2, cl=1, seq=0,
+                               site=ords[bytes(aid)], val0=0, val_type=1)])
+    before = _state(bk, ids, nver)
+    with pytest.raises(ca.CorroError):
+        _run(eng, bk, ords, call + [bad], "headers")
+    assert _ready(bk) == []
+    assert _state(bk, ids, nver) == before
+    assert eng.count() == 0
+    got = _run(eng, bk, ords, call, "headers")
+    want = _run(twin, tbk, tords, call, "headers")
+    assert got == want
+    assert _state(bk, ids, nver) == _state(tbk, ids, nver)
+    assert sorted(_ready(bk)) == sorted(_ready(tbk))
+    assert canon_rows(eng.export()) == canon_rows(twin.export())
