@@ -306,6 +306,9 @@ __device__ inline void rs_terms(const MergeArgs &a, uint32_t cid, uint32_t cl, i
 }
 
 // ---- impact form: first position of each causal length per row (F(c) of k_ovf_keep) ----------
+#ifndef OVF_RCL_BATCH
+#define OVF_RCL_BATCH 0
+#endif
 #ifndef OVF_NCL
 #define OVF_NCL 8  // causal-length slots per row; a row with more distinct ones keeps every record
 #endif
@@ -315,8 +318,19 @@ __device__ inline void rcl_put(const OvfDev &d, uint32_t row, uint32_t cl, uint3
     if (cl == 0) return;
     unsigned long long *sl = (unsigned long long *)d.rcl + (size_t)row * OVF_NCL;
     const unsigned long long want = ((unsigned long long)cl << 32) | pos;
+#if OVF_RCL_BATCH
+    // every slot read at once (a claimed slot's causal length never changes, so a stale snapshot
+    // only misses later claims, which the CAS below then sees)
+    unsigned long long snap[OVF_NCL];
+#pragma unroll
+    for (uint32_t k = 0; k < OVF_NCL; k++) snap[k] = ovf_ld_dev(&sl[k]);
+#endif
     for (uint32_t k = 0; k < OVF_NCL; k++) {
+#if OVF_RCL_BATCH
+        unsigned long long cur = snap[k];
+#else
         unsigned long long cur = ovf_ld_dev(&sl[k]);
+#endif
         if (cur == ~0ULL) {
             cur = atomicCAS(&sl[k], ~0ULL, want);
             if (cur == ~0ULL) return;
@@ -333,7 +347,10 @@ __device__ inline void rcl_put(const OvfDev &d, uint32_t row, uint32_t cl, uint3
 // hot row's records many times over): an LDS table keyed (row, cl) keeps the minimum position, and
 // each entry goes to the row's global slots once at the end. A key without an LDS slot goes straight
 // to the global slots.
-constexpr uint32_t RCL_HT = 2048;
+#ifndef OVF_RCL_BITS
+#define OVF_RCL_BITS 11
+#endif
+constexpr uint32_t RCL_HT = 1u << OVF_RCL_BITS;
 struct RclLds {
     unsigned long long key[RCL_HT];  // row << 32 | cl, ~0: free
     uint32_t pos[RCL_HT];
@@ -348,7 +365,7 @@ __device__ inline void rcl_lds_clear(RclLds &L) {
 
 __device__ inline bool rcl_lds_add(RclLds &L, uint32_t row, uint32_t cl, uint32_t pos) {
     const unsigned long long k = ((unsigned long long)row << 32) | cl;
-    const uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ULL) >> 53);  // (RCL_HT = 2^11)
+    const uint32_t h = (uint32_t)((k * 0x9E3779B97F4A7C15ULL) >> (64 - OVF_RCL_BITS));
     for (uint32_t j = 0; j < 16; j++) {
         const uint32_t sl = (h + j) & (RCL_HT - 1);
         unsigned long long o = L.key[sl];
@@ -392,7 +409,10 @@ __device__ inline void rcl_wave_add(RclLds &L, const OvfDev &d, bool todo, uint3
 #ifndef OVF_RS_E
 #define OVF_RS_E 16  // records per thread of a summary workgroup (4 / 8 / 16: lookup 1.57 / 1.34 / 1.15 ms at config 5)
 #endif
-constexpr uint32_t RS_T = 256, RS_E = OVF_RS_E, RS_CHUNK = RS_T * RS_E, RS_HT = 1024;
+#ifndef OVF_RS_BITS
+#define OVF_RS_BITS 10
+#endif
+constexpr uint32_t RS_T = 256, RS_E = OVF_RS_E, RS_CHUNK = RS_T * RS_E, RS_HT = 1u << OVF_RS_BITS;
 struct RsLds {
     uint32_t key[RS_HT], w2[RS_HT];  // key: row + 1 (0: free)
     unsigned long long w1[RS_HT];
@@ -407,7 +427,7 @@ __device__ inline void rs_lds_clear(RsLds &L) {
 }
 
 __device__ inline bool rs_lds_add(RsLds &L, uint32_t row, uint64_t w1, uint32_t w2) {
-    const uint32_t h = (row * 2654435761u) >> 22;  // (RS_HT = 2^10)
+    const uint32_t h = (row * 2654435761u) >> (32 - OVF_RS_BITS);
     for (uint32_t k = 0; k < 16; k++) {
         const uint32_t sl = (h + k) & (RS_HT - 1);
         const uint32_t o = atomicCAS(&L.key[sl], 0u, row + 1);

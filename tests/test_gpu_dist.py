@@ -349,3 +349,76 @@ def test_slot_partition_validates_and_marks_counts(bad):
         e.register_sites(synth.site_ids(16, 5))
         e.apply(full)
         assert rows_to_tuples(eng.export(), with_ts=True) == rows_to_tuples(e.export(), with_ts=True)
+
+
+# ---- the multi-rank path at scale, against the oracle ---------------------------------------------
+# (the tests above pin the exchange at 6,000-50,000 changes; here a config-5-shaped adversarial batch
+# of 4M changes -- Zipf-hot rows, so every rank's merge runs the device-wide overflow fold -- and a
+# config-2-shaped INTEGER batch of 2^24 changes through the stream-ordered slot path, with impacts,
+# each against the oracle's pk-sharded fold of the whole batch: every impact flag in each sender's
+# order, the union of the rank states by the order-independent digest of every output field (a
+# mismatch prints the row-by-row report), crsql_db_versions)
+NL_ADV, NL_INT = 4_000_000, 1 << 24
+
+
+def _large_worker(rank, world, port, outdir, kind):
+    import torch
+    import torch.distributed as dist
+    import corrosion_amd as ca
+    from corrosion_amd.dist import distributed_apply, distributed_apply_slots, rank_of_np, slot_cap
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if kind == "adversarial":
+        n, seed = NL_ADV, synth.config_seed(5)
+        schema, sites = synth.adversarial_schema(8), synth.site_ids(1000, seed)
+        full = synth.adversarial_batch(n, 1000, 8, 1 << 20, seed)
+    else:
+        n, seed = NL_INT, synth.config_seed(2)
+        schema, sites = {"t": ["a", "b", "c", "d"]}, synth.site_ids(1000, 1)
+        full = synth.uniform_batch(n, 1000, 1 << 22, 4, seed)
+    lo, hi = rank * n // world, (rank + 1) * n // world
+    eng = ca.MergeEngine(schema, capacity_hint=n // world, device=0)
+    eng.register_sites(sites)
+    part = _to_dev({k: v[lo:hi] for k, v in full.items()})
+    del full
+    if kind == "adversarial":
+        imp = distributed_apply(eng, part, impact=True)
+        assert eng.metrics()["overflow_rounds"] >= 1  # the hot-row regime on this rank
+    else:
+        nover, imp = distributed_apply_slots(eng, part, slot_cap(hi - lo, world), impact=True)
+        assert nover == 0
+    torch.cuda.synchronize()
+    np.save(os.path.join(outdir, f"limp{rank}.npy"), imp.cpu().numpy())
+    rows = eng.export()
+    assert (rank_of_np(rows["table_cid"], rows["pk"], world) == rank).all()
+    assert not rows.get("long_values")  # (values of at most 16 bytes: the rows are plain arrays)
+    np.savez(os.path.join(outdir, f"lrows{rank}.npz"), **{k: v for k, v in rows.items() if k != "long_values"})
+    np.save(os.path.join(outdir, f"ldbv{rank}.npy"), np.asarray(eng.db_versions()))
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("kind", ["adversarial", "integer_slots"])
+def test_two_rank_large_batch_vs_sharded_oracle(tmp_path, kind):
+    from oracle import oracle as O
+    world = 2
+    mp.spawn(_large_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True)
+    if kind == "adversarial":
+        n, seed = NL_ADV, synth.config_seed(5)
+        sites, batch = synth.site_ids(1000, seed), synth.adversarial_batch(NL_ADV, 1000, 8, 1 << 20, seed)
+    else:
+        n, seed = NL_INT, synth.config_seed(2)
+        sites, batch = synth.site_ids(1000, 1), synth.uniform_batch(NL_INT, 1000, 1 << 22, 4, seed)
+    fold = O.ShardedFold(sites, nshards=64, nthreads=16)
+    want_imp = fold.apply(batch, impact=True)
+    got_imp = np.concatenate([np.load(tmp_path / f"limp{r}.npy") for r in range(world)])
+    assert np.array_equal(got_imp, want_imp), "impact flags differ from the oracle"
+    parts = [dict(np.load(tmp_path / f"lrows{r}.npz")) for r in range(world)]
+    rows = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    if O.rows_digest(rows) != fold.digest():
+        pytest.fail(f"{kind}: the ranks' union differs from the oracle:\n" + str(O.rows_diff(rows, fold.export())))
+    dbv = np.max([np.load(tmp_path / f"ldbv{r}.npy") for r in range(world)], axis=0)
+    assert np.array_equal(dbv, fold.db_versions())
+    print(f"{kind}: {n} changes over {world} ranks, {len(rows['pk'])} clock rows bit-exact")
