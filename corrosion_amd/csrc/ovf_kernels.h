@@ -306,41 +306,23 @@ __device__ inline void rs_terms(const MergeArgs &a, uint32_t cid, uint32_t cl, i
 }
 
 // ---- impact form: first position of each causal length per row (F(c) of k_ovf_keep) ----------
-#ifndef OVF_RCL_BATCH
-#define OVF_RCL_BATCH 0
+#ifndef OVF_DIAG
+#define OVF_DIAG 0
 #endif
 #ifndef OVF_NCL
-#define OVF_NCL 8  // causal-length slots per row; a row with more distinct ones keeps every record
+#define OVF_NCL 8  // causal-length slots per row; a row whose causal lengths collide keeps every record
 #endif
-// slots fill in order, so one causal length always lands in one slot; the word's min keeps its
-// first position. cl 0 records are never records nor candidates and take no slot.
+// Slot cl mod OVF_NCL holds causal length cl (a row's causal lengths are mostly a short run of
+// consecutive values, which never collide), and one atomicMin both claims a free slot (~0) and keeps
+// the first position. Two causal lengths that share a slot corrupt it -- the min of the two words --
+// but whichever of them comes second sees the other's word come back and marks the row, which then
+// keeps every record and never reads its slots (k_ovf_keep). cl 0 records are never records nor
+// candidates and take no slot.
 __device__ inline void rcl_put(const OvfDev &d, uint32_t row, uint32_t cl, uint32_t pos) {
     if (cl == 0) return;
-    unsigned long long *sl = (unsigned long long *)d.rcl + (size_t)row * OVF_NCL;
-    const unsigned long long want = ((unsigned long long)cl << 32) | pos;
-#if OVF_RCL_BATCH
-    // every slot read at once (a claimed slot's causal length never changes, so a stale snapshot
-    // only misses later claims, which the CAS below then sees)
-    unsigned long long snap[OVF_NCL];
-#pragma unroll
-    for (uint32_t k = 0; k < OVF_NCL; k++) snap[k] = ovf_ld_dev(&sl[k]);
-#endif
-    for (uint32_t k = 0; k < OVF_NCL; k++) {
-#if OVF_RCL_BATCH
-        unsigned long long cur = snap[k];
-#else
-        unsigned long long cur = ovf_ld_dev(&sl[k]);
-#endif
-        if (cur == ~0ULL) {
-            cur = atomicCAS(&sl[k], ~0ULL, want);
-            if (cur == ~0ULL) return;
-        }
-        if ((uint32_t)(cur >> 32) == cl) {
-            if (want < cur) atomicMin(&sl[k], want);
-            return;
-        }
-    }
-    atomicOr(&d.rw2[row], 1u);  // more causal lengths than slots: the row keeps every record
+    unsigned long long *sl = (unsigned long long *)d.rcl + (size_t)row * OVF_NCL + cl % OVF_NCL;
+    const unsigned long long o = atomicMin(sl, ((unsigned long long)cl << 32) | pos);
+    if (o != ~0ULL && (uint32_t)(o >> 32) != cl) atomicOr(&d.rw2[row], 1u);
 }
 
 // Per workgroup first (k_ovf_lookup's chunk of RS_CHUNK bucket-major records: a few buckets' rows, a
@@ -519,7 +501,9 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
                 rs_terms(a, d.tc[r] & 0xFFFFu, cl, d.cv[r], pos, w1, w2);
             }
             rs_wave_add(L, d, valid, row, w1, w2);
+#if !(OVF_DIAG & 1)  // (diagnostic builds only: OVF_DIAG 1 drops the causal-length slots, results not valid)
             if constexpr (RIMP) rcl_wave_add(LC_, d, valid, row, cl, d.pm + (pos & 0x7FFFFFFFu));
+#endif
         }
         if (!valid || !d.recf[r]) continue;  // (an owner's row: epc[r] - 1, as computed above)
         const uint32_t b = bk, t = d.tc[r] >> 16;
@@ -546,7 +530,9 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
     if (d.reduce) {
         __syncthreads();
         rs_lds_flush(L, d);
+#if !(OVF_DIAG & 3)  // (OVF_DIAG 2: the LDS table kept, its flush to the rows' slots dropped)
         if constexpr (RIMP) rcl_lds_flush(LC_, d);
+#endif
     }
 }
 

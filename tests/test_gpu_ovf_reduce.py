@@ -77,8 +77,9 @@ def test_reduction_impact_form_vs_oracle(max_cl, sent, wide):
     """The impact form of the reduction (k_ovf_keep's comment): a dropped change's flag from its row's
     causal-length slots -- records, no-ops, and candidates by a running argmax over their (row, cl,
     cid) group seeded by a same-cid epoch record -- against the sequential oracle's
-    crsql_rows_impacted() growth, three batches folded (prior records in the slots too); max_cl 12
-    passes the 8 slots for many rows (those keep every change)."""
+    crsql_rows_impacted() growth, three batches folded (prior records in the slots too); with max_cl 12
+    many rows hold causal lengths that share a slot (cl mod 8: 1 and 9, ...; those rows keep every
+    change)."""
     seed = 950 + max_cl
     sites = synth.site_ids(12, seed)
     e, f = _engine(synth.adversarial_schema(3), sites), O.Fold(sites)
