@@ -237,7 +237,7 @@ static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
             }
         }
         if (todo) owner = probe();
-        d.rowid[r] = owner;  // (scratch until the sort)
+        d.rowid[r] = kb + owner;  // the owner's record (scratch until the sort)
         d.recf[r] = owner == r - kb ? 1u : 0u;
         if (owner == r - kb) d.pk[r] = pk;  // (only a row's owner is asked for its pk)
         if (!d.reduce) d.val[r] = r;  // (the reduction's compaction writes the sort values)
@@ -481,13 +481,12 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
         const uint32_t r = c0 + j * RS_T + threadIdx.x;
         const bool valid = r < d.Kb;
         // every record: its sort key (k_ovf_rowkey's, fused here: dense rows are known by now)
-        uint32_t row = 0, pos = 0, bk = 0;
+        uint32_t row = 0, pos = 0;
+        bool owner = false;
         if (valid) {
-            uint32_t b = d.cbk[r >> 6];
-            while (d.koff[b + 1] <= r) b++;
-            bk = b;
-            const uint32_t kb = d.koff[b];
-            row = d.epc[kb + d.rowid[r]] - 1u;
+            const uint32_t o = d.rowid[r];  // the row's owner record (k_ovf_loadhash)
+            owner = o == r;
+            row = d.epc[o] - 1u;
             pos = d.pos[r];
             d.key[r] = ((uint64_t)row << d.rshift) | ((uint64_t)d.pm + (pos & 0x7FFFFFFFu));
         }
@@ -505,8 +504,10 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
             if constexpr (RIMP) rcl_wave_add(LC_, d, valid, row, cl, d.pm + (pos & 0x7FFFFFFFu));
 #endif
         }
-        if (!valid || !d.recf[r]) continue;  // (an owner's row: epc[r] - 1, as computed above)
-        const uint32_t b = bk, t = d.tc[r] >> 16;
+        if (!owner) continue;  // (an owner's row: epc[r] - 1, as computed above)
+        uint32_t b = d.cbk[r >> 6];  // (its bucket: only the owners look it up)
+        while (d.koff[b + 1] <= r) b++;
+        const uint32_t t = d.tc[r] >> 16;
         d.rowner[row] = r;
         d.rb[row] = b;
         if (d.split) continue;
