@@ -170,7 +170,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         for (uint32_t **p : rows) *p = (uint32_t *)take(R * 4);
         d.rbits = (uint64_t *)take(R * 16);
         d.rw1 = (uint64_t *)take(R * 12 + 64);  // row summaries, laid out once the row count is known
-        d.cbk = (uint32_t *)take((Kb / 64 + 2) * 4);
+        d.cbk = (uint32_t *)take((Kb / 64 + 2) * 32);
         if (pass == 0 && K <= ctx->ovf_temp_k) {
             temp = ctx->ovf_temp;  // (rocPRIM's temp sizes grow with n; the 64-bit sort bounds the others)
         } else if (pass == 0) {
@@ -215,7 +215,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     const bool rimp_fits = kbits + 3 + cid_bits + pbits <= 64;
     d.reduce = ovf_reduce_ok(ctx, a.impact != nullptr) && (!a.impact || rimp_fits) ? 1u : 0u;
     d.rimp = d.reduce && a.impact ? 1u : 0u;
-    hipLaunchKernelGGL(k_ovf_chunkmap, grid_for((Kb + 63) / 64), blk, 0, s, d);
+    hipLaunchKernelGGL(k_ovf_chunkmap, grid_for((Kb + 63) / 64), blk, 0, s, a, d);
     hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
     TRY(launched());
     // dense row ids: the row count sizes the sort's key

@@ -107,7 +107,7 @@ struct OvfDev {
     uint64_t *rw1;               // [nrows] Mx << 32 | cids at Mx (rs_comb)
     uint32_t *rw2;               // [nrows] cids | outside App. A.3
     uint32_t *nkeep;             // [1] records kept; [1]: dropped candidates (impact form)
-    uint32_t *cbk;               // [Kb / 64 + 1] bucket of batch record 64 c (k_ovf_chunkmap)
+    uint32_t *cbk;               // [8 (Kb / 64 + 1)] bucket of batch record 64 c and its words (k_ovf_chunkmap)
     // impact form of the reduction (rimp): per row OVF_NCL causal-length slots, the first compact
     // position of each causal length (cl << 32 | position, ~0 free) and the record at it; the
     // dropped candidates' sort key = ((row * OVF_NCL + slot) << cid_bits | cid) << rshift | position
@@ -174,23 +174,55 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b, const uint8_t *
 
 #define OVF_LOOP(i, N) for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (N); i += gridDim.x * blockDim.x)
 
+// the bucket of every 64th batch record and the words its records need (a record's bucket is then
+// its chunk's, or a step or two past it: the binary search over koff is one dependent chain of ~15
+// loads, and the bucket's words -- record range, staged base, row-table slice -- another three)
+// chunk c: b, koff[b], koff[b + 1], staged base, row-table offset, row-table size, -, -
+struct ChunkB {
+    uint32_t b, kb, ke, sbase, soff, S;
+};
+
+__device__ inline ChunkB ovf_chunk_words(const MergeArgs &a, const OvfDev &d, uint32_t b) {
+    ChunkB c;
+    c.b = b;
+    c.kb = d.koff[b];
+    c.ke = d.koff[b + 1];
+    c.sbase = a.stage_off[a.ovf_list[b]];
+    c.soff = d.slot_off[b];
+    uint32_t S = 1;
+    while (S < 2 * (c.ke - c.kb)) S <<= 1;
+    c.S = S;
+    return c;
+}
+
+static __global__ void k_ovf_chunkmap(MergeArgs a, OvfDev d) {
+    OVF_LOOP(c, (d.Kb + 63) / 64) {
+        const ChunkB x = ovf_chunk_words(a, d, ovf_bucket_of(d, c * 64));
+        uint4 *o = (uint4 *)d.cbk + 2 * c;
+        o[0] = make_uint4(x.b, x.kb, x.ke, x.sbase);
+        o[1] = make_uint4(x.soff, x.S, 0u, 0u);
+    }
+}
+
+// a batch record's bucket words: its chunk's, unless the chunk crosses into a later bucket
+__device__ inline ChunkB ovf_chunk_of(const MergeArgs &a, const OvfDev &d, uint32_t r) {
+    const uint4 *m = (const uint4 *)d.cbk + 2 * (r >> 6);
+    const uint4 x = m[0], y = m[1];
+    if (r < x.z) return ChunkB{x.x, x.y, x.z, x.w, y.x, y.y};
+    uint32_t b = x.x + 1;
+    while (d.koff[b + 1] <= r) b++;
+    return ovf_chunk_words(a, d, b);
+}
+
 // Record fields and row owners in one pass: each batch record's fields are loaded from its staged
 // 64-B record and the record is hashed into its bucket's row table (open addressing per bucket, a
 // slot read before it is claimed); an occupied slot's row key is compared with the claimant's staged
 // record (read-only in this kernel, so no ordering against the claimant's own field writes).
-// the bucket of every 64th batch record: a record's bucket is then a step or two from its chunk's
-// (the binary search over koff is one dependent chain of ~15 loads per lookup)
-static __global__ void k_ovf_chunkmap(OvfDev d) {
-    OVF_LOOP(c, (d.Kb + 63) / 64) d.cbk[c] = ovf_bucket_of(d, c * 64);
-}
-
 static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
     const uint32_t lane = threadIdx.x & 63;
     OVF_LOOP(r, d.Kb) {
-        uint32_t b = d.cbk[r >> 6];
-        while (d.koff[b + 1] <= r) b++;
-        const uint32_t kb = d.koff[b], n = d.koff[b + 1] - kb;
-        const uint32_t sbase = a.stage_off[a.ovf_list[b]];
+        const ChunkB cb = ovf_chunk_of(a, d, r);
+        const uint32_t kb = cb.kb, sbase = cb.sbase;
         const uint32_t si = sbase + (r - kb);
         const Rec x = load_rec(a.stage + si);
         d.src[r] = si;
@@ -198,9 +230,8 @@ static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
         d.tc[r] = x.tcid;
         d.cl[r] = x.cl;
         d.pos[r] = x.pos;
-        uint32_t S = 1;
-        while (S < 2 * n) S <<= 1;
-        uint32_t *slots = d.slots + d.slot_off[b];
+        const uint32_t S = cb.S;
+        uint32_t *slots = d.slots + cb.soff;
         const uint64_t pk = x.pk;
         const uint32_t t = x.tcid >> 16;
         auto probe = [&]() -> uint32_t {
@@ -505,7 +536,7 @@ static __global__ void __launch_bounds__(RS_T) k_ovf_lookup(MergeArgs a, OvfDev 
 #endif
         }
         if (!owner) continue;  // (an owner's row: epc[r] - 1, as computed above)
-        uint32_t b = d.cbk[r >> 6];  // (its bucket: only the owners look it up)
+        uint32_t b = d.cbk[8 * (r >> 6)];  // (its bucket: only the owners look it up)
         while (d.koff[b + 1] <= r) b++;
         const uint32_t t = d.tc[r] >> 16;
         d.rowner[row] = r;
