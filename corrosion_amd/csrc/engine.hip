@@ -91,29 +91,35 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     const uint32_t B = ctx->B;
     // readbacks land in pinned memory: async copies, one wait per group (pageable ones block per copy)
     if (!ctx->h_ovf) CORRO_HIP_TRY(hipHostMalloc((void **)&ctx->h_ovf, (8ULL * B + 32) * 4, hipHostMallocDefault));
-    uint32_t *const list = ctx->h_ovf, *const nc = list + B, *const used0 = nc + B, *const koff = used0 + B;
-    uint32_t *const soff = koff + B + 1, *const bnew = soff + B, *const bnrec = bnew + B, *const used = bnrec + B;
-    uint32_t *const hw = used + B;
-    CORRO_HIP_TRY(hipMemcpyAsync(list, ctx->d_ovf_list.p, novf * 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(nc, ctx->d_new_cnt.p, B * 4ULL, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(used0, ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost, s));
+    uint32_t *const hw = ctx->h_ovf + 8ULL * B;  // (32 readback words; hw + 8: the plan's totals, 8-B aligned)
+    // the plan (k_ovf_plan): bucket offsets and row-table slices on the device, totals back
+    if (novf > (uint64_t)PLAN_T * PLAN_PER) return fail(CORRO_E_RANGE, "internal: more oversized buckets than k_ovf_plan takes");
+    TRY(ctx->d_ovf_plan.ensure((2ULL * B + 2) * 4 + 16 * 8 + 256));
+    uint32_t *const p_koff = ctx->d_ovf_plan.as<uint32_t>(), *const p_soff = p_koff + B + 1;
+    unsigned long long *const p_tot = (unsigned long long *)(((uintptr_t)(p_soff + B) + 15) & ~(uintptr_t)15);
+    unsigned long long *const hq = (unsigned long long *)(hw + 8);  // (pinned: tot[0..4])
+    hipLaunchKernelGGL(k_ovf_plan, dim3(1), dim3(PLAN_T), 0, s, ctx->d_ovf_list.as<uint32_t>(), ctx->d_new_cnt.as<uint32_t>(),
+                       ctx->d_used.as<uint32_t>(), (uint32_t)novf, p_koff, p_soff, p_tot);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipMemcpyAsync(hq, p_tot, 3 * 8, hipMemcpyDeviceToHost, s));
+    // CORRO_OVF_HOSTPROF=1: the host's own time between the fold's waits, to stderr (diagnostics)
+    static const bool hostprof = std::getenv("CORRO_OVF_HOSTPROF") != nullptr;
+    auto hp_t0 = std::chrono::steady_clock::now();
+    std::string hp_line;
+    auto hp = [&](const char *what) {
+        if (!hostprof) return;
+        const auto t = std::chrono::steady_clock::now();
+        hp_line += std::string(" ") + what + "=" +
+                   std::to_string(std::chrono::duration<double, std::micro>(t - hp_t0).count()).substr(0, 6);
+        hp_t0 = t;
+    };
     CORRO_HIP_TRY(hipStreamSynchronize(s));
-    uint64_t Kb = 0, S = 0;
-    for (uint64_t k = 0; k < novf; k++) {
-        const uint64_t n = nc[list[k]];
-        uint64_t sl = 1;
-        while (sl < 2 * n) sl <<= 1;
-        koff[k] = (uint32_t)Kb;
-        soff[k] = (uint32_t)S;
-        Kb += n;
-        S += sl;
-    }
-    koff[novf] = (uint32_t)Kb;
+    hp("wait1");
+    const uint64_t Kb = hq[0], S = hq[1];
     // prior records: at most one heap row per batch row, at most the rows the oversized buckets'
     // regions hold (each at most max_stride records), at most the whole state -- the region bound
     // keeps a hot-row batch into a large state from sizing (and failing) for the whole state
-    uint64_t region_rows = 0;
-    for (uint64_t k = 0; k < novf; k++) region_rows += used0[list[k]];
+    const uint64_t region_rows = hq[2];
     const uint64_t Kmax = Kb + std::min<uint64_t>(std::min<uint64_t>(ctx->state_total, region_rows * ctx->max_stride),
                                                   Kb * (uint64_t)ctx->max_stride);
     if (Kmax >= (1ULL << 31) || S >= (1ULL << 32))
@@ -127,6 +133,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     uint32_t cid_bits = 1;
     while ((1u << cid_bits) <= ctx->max_stride - 1) cid_bits++;
     const uint32_t ckey_bits = rb + cid_bits;
+    hp("koff");
     auto al = [](uint64_t x) { return (x + 255) & ~255ULL; };
     // pass 0 sizes the arrays, pass 1 carves them out of d_ovf_sort
     OvfDev d{};
@@ -150,8 +157,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     const uint64_t K = Kmax, R = std::max<uint64_t>(Kb, 1);
     for (int pass = 0; pass < 2; pass++) {
         bytes = 0;
-        d.koff = (const uint32_t *)take((novf + 1) * 4);
-        d.slot_off = (const uint32_t *)take(novf * 4);
+        d.koff = p_koff;
+        d.slot_off = p_soff;
         d.bnew = (uint32_t *)take(novf * 4);
         d.bnrec = (uint32_t *)take(novf * 4);
         d.slots = (uint32_t *)take(std::max<uint64_t>(S, 2 * K) * 4);
@@ -195,8 +202,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
             base = ctx->d_ovf_sort.as<uint8_t>();
         }
     }
-    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.koff, koff, (novf + 1) * 4, hipMemcpyHostToDevice, s));
-    CORRO_HIP_TRY(hipMemcpyAsync((void *)d.slot_off, soff, novf * 4, hipMemcpyHostToDevice, s));
+    hp("carve");
     CORRO_HIP_TRY(hipMemsetAsync(d.bnew, 0, novf * 4, s));
     CORRO_HIP_TRY(hipMemsetAsync(d.bnrec, 0, novf * 4, s));
     CORRO_HIP_TRY(hipMemsetAsync(d.slots, 0, S * 4, s));
@@ -215,13 +221,16 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     const bool rimp_fits = kbits + 3 + cid_bits + pbits <= 64;
     d.reduce = ovf_reduce_ok(ctx, a.impact != nullptr) && (!a.impact || rimp_fits) ? 1u : 0u;
     d.rimp = d.reduce && a.impact ? 1u : 0u;
+    hp("h2d");
     hipLaunchKernelGGL(k_ovf_chunkmap, grid_for((Kb + 63) / 64), blk, 0, s, a, d);
     hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
     TRY(launched());
     // dense row ids: the row count sizes the sort's key
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.recf, d.epc, d.Kb, s));
     CORRO_HIP_TRY(hipMemcpyAsync(&hw[0], d.epc + (Kb - 1), 4, hipMemcpyDeviceToHost, s));
+    hp("enq2");
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    hp("wait2");
     const uint32_t nrows = hw[0];
     d.nrows = nrows;
     d.rshift = pbits;
@@ -247,22 +256,21 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     TRY(launched());
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
     CORRO_HIP_TRY(hipMemcpyAsync(&hw[0], d.rpoff + (nrows - 1), 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(bnew, d.bnew, novf * 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(bnrec, d.bnrec, novf * 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipMemcpyAsync(used, ctx->d_used.p, B * 4ULL, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_ovf_room, dim3(1), dim3(PLAN_T), 0, s, ctx->d_ovf_list.as<uint32_t>(), ctx->d_used.as<uint32_t>(),
+                       d.bnew, d.bnrec, (uint32_t)novf, p_tot);
+    CORRO_HIP_TRY(hipGetLastError());
+    CORRO_HIP_TRY(hipMemcpyAsync(hq + 3, p_tot + 3, 2 * 8, hipMemcpyDeviceToHost, s));
     CORRO_HIP_TRY(hipMemcpyAsync(&hw[2], ctx->d_heap_top.p, 8, hipMemcpyDeviceToHost, s));
+    hp("enq3");
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    hp("wait3");
     const uint32_t P = hw[0];
     const unsigned long long top = (unsigned long long)hw[2] | ((unsigned long long)hw[3] << 32);
     if (Kb + (uint64_t)P > Kmax) return fail(CORRO_E_DEVICE, "internal: overflow prior records exceed their bound");
     // room for the new rows (region fill, heap) before the walk writes anything
-    uint64_t need_heap = 0;
+    const uint64_t need_heap = hq[4], want = hq[3];  // (k_ovf_room: the largest fill asked of a region)
     uint32_t need_log2S = ctx->log2S;
-    for (uint64_t k = 0; k < novf; k++) {
-        need_heap += bnrec[k];
-        const uint64_t want = (uint64_t)used[list[k]] + bnew[k];
-        while (want > ((7ULL << need_log2S) >> 3)) need_log2S++;
-    }
+    while (want > ((7ULL << need_log2S) >> 3)) need_log2S++;
     if (need_log2S != ctx->log2S) TRY(grow_regions(ctx, need_log2S));
     if (top + need_heap > ctx->heap_cap) TRY(grow_heap(ctx, top + need_heap));
     a.rs = row_store(ctx);
@@ -276,6 +284,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     if (dbg)
         fprintf(stderr, "[corro ovf] buckets %llu batch records %llu prior %u rows %u key bits %u (+%u) cand key bits %u\n",
                 (unsigned long long)novf, (unsigned long long)Kb, P, nrows, key_bits, rbits, ckey_bits);
+    hp("room");
     hipLaunchKernelGGL(k_ovf_pload, grid_for(nrows), blk, 0, s, a, d);
     TRY(launched());
     if (d.reduce) {
@@ -284,7 +293,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         hipLaunchKernelGGL(k_ovf_keep, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK), dim3(KEEP_T), 0, s, a, d, kcap);
         TRY(launched());
         CORRO_HIP_TRY(hipMemcpyAsync(&hw[4], d.nkeep, 8, hipMemcpyDeviceToHost, s));
+        hp("enq4");
         CORRO_HIP_TRY(hipStreamSynchronize(s));
+        hp("wait4");
         const uint32_t kept = hw[4], ndc = d.rimp ? hw[5] : 0u;
         if (kept == 0 || kept + ndc > kcap) return fail(CORRO_E_DEVICE, "internal: overflow row reduction kept no records");
         if (dbg) fprintf(stderr, "[corro ovf] row reduction keeps %u of %u records (%u dropped candidates)\n", kept, d.K, ndc);
@@ -326,7 +337,9 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     // only the candidates are sorted (a minority of the records): compact them first
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.slots, d.slots + d.K, d.K, s));
     CORRO_HIP_TRY(hipMemcpyAsync(&hw[5], d.slots + d.K + (d.K - 1), 4, hipMemcpyDeviceToHost, s));
+    hp("enq5");
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    hp("wait5");
     const uint32_t ncand = hw[5];
     hipLaunchKernelGGL(k_ovf_ccompact, grid, blk, 0, s, d);
     TRY(launched());
@@ -353,6 +366,8 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     if (a.impact) hipLaunchKernelGGL(k_ovf_impacts, cgrid, blk, 0, s, a, d);
     hipLaunchKernelGGL(k_ovf_finish, grid_for(novf), blk, 0, s, a, d);
     TRY(launched());
+    hp("enq6");
+    if (hostprof) fprintf(stderr, "[corro ovf host us]%s\n", hp_line.c_str());
     if (prof) (void)hipEventRecord(ctx->ev[7], s);
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     if (prof) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[5], ctx->ev[6], ctx->ev[7]));
@@ -615,7 +630,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_heap, &ctx->d_heap_ts, &ctx->d_heap_top, &ctx->d_stride, &ctx->d_defer,
                       &ctx->d_relist, &ctx->d_dense, &ctx->d_dense_ts, &ctx->d_dense_view, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_fast_of, &ctx->d_ovf_sort, &ctx->d_ovf_rcl, &ctx->d_setdbv,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_fast_of, &ctx->d_ovf_sort, &ctx->d_ovf_rcl, &ctx->d_ovf_plan, &ctx->d_setdbv,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
                       &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,

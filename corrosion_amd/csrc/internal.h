@@ -202,6 +202,7 @@ struct corro_ctx {
     corro::DevBuf d_fast_of;      // k_triage: per merged bucket, 1 = INTEGER fast body
     corro::DevBuf d_ovf_sort;     // overflow path: its device-wide arrays, offsets, rocPRIM temp
     corro::DevBuf d_ovf_rcl;      // overflow path, impact form of the row reduction: per-row cl slots
+    corro::DevBuf d_ovf_plan;     // overflow path: bucket offsets, row-table slices, totals (k_ovf_plan)
     uint64_t ovf_temp_k = 0;      // overflow path: the record count its cached rocPRIM temp size was queried for
     size_t ovf_temp = 0;
     corro::DevBuf d_setdbv;       // set_db_versions: (site, version + 1) pairs

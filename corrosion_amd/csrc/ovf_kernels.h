@@ -174,6 +174,114 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b, const uint8_t *
 
 #define OVF_LOOP(i, N) for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (N); i += gridDim.x * blockDim.x)
 
+// ---- the fold's plan, on the device (one workgroup each; these were host loops over pinned
+// readbacks of the bucket lists: ~0.25 ms and ~0.06 ms at 32 K buckets, the GPU idle meanwhile) ----
+constexpr uint32_t PLAN_T = 1024;  // (x PLAN_PER buckets per thread: up to 32 K queued buckets)
+
+__device__ inline unsigned long long ovf_slots_for(unsigned long long n) {
+    unsigned long long sl = 1;
+    while (sl < 2 * n) sl <<= 1;
+    return sl;
+}
+
+// exclusive scan across the 1024-thread workgroup; `total` = the sum of every x
+__device__ inline unsigned long long plan_scan(unsigned long long x, unsigned long long *s_w, unsigned long long &total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        unsigned long long v = lane < PLAN_T / 64 ? s_w[lane] : 0ULL;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const unsigned long long y = __shfl_up(v, o);
+            if ((int)lane >= o) v += y;
+        }
+        if (lane < PLAN_T / 64) s_w[lane] = v;
+    }
+    __syncthreads();
+    total = s_w[PLAN_T / 64 - 1];
+    return (w ? s_w[w - 1] : 0ULL) + incl - x;
+}
+
+// per queued bucket k (b = list[k]): its batch records at koff[k] (exclusive scan of the counts), its
+// row-table slots next_pow2(2 n) at soff[k]; tot[0..2] = records, slots, the buckets' region rows
+static __global__ void __launch_bounds__(PLAN_T) k_ovf_plan(const uint32_t *__restrict__ list, const uint32_t *__restrict__ nc,
+                                                            const uint32_t *__restrict__ used, uint32_t novf,
+                                                            uint32_t *__restrict__ koff, uint32_t *__restrict__ soff,
+                                                            unsigned long long *__restrict__ tot) {
+    __shared__ unsigned long long s_a[PLAN_T / 64], s_b[PLAN_T / 64], s_c[PLAN_T / 64];
+    const uint32_t per = (novf + PLAN_T - 1) / PLAN_T;  // <= PLAN_PER (the host checks)
+    const uint32_t k0 = min(novf, threadIdx.x * per), k1 = min(novf, k0 + per);
+    // the buckets' counts staged in LDS by coalesced strided loads (independent, so they overlap),
+    // then each thread scans its contiguous range from LDS
+    __shared__ uint32_t s_n[PLAN_T * PLAN_PER];
+    unsigned long long sn = 0, ss = 0, su = 0;
+#pragma unroll 8
+    for (uint32_t k = threadIdx.x; k < novf; k += PLAN_T) {
+        const uint32_t b = list[k];
+        s_n[k] = nc[b];
+        su += used[b];
+    }
+    __syncthreads();
+    for (uint32_t k = k0; k < k1; k++) {
+        sn += s_n[k];
+        ss += ovf_slots_for(s_n[k]);
+    }
+    unsigned long long tn, ts, tu;
+    unsigned long long bn = plan_scan(sn, s_a, tn), bs = plan_scan(ss, s_b, ts);
+    plan_scan(su, s_c, tu);
+    for (uint32_t k = k0; k < k1; k++) {
+        koff[k] = (uint32_t)bn;
+        soff[k] = (uint32_t)bs;
+        bn += s_n[k];
+        bs += ovf_slots_for(s_n[k]);
+    }
+    if (threadIdx.x == 0) {
+        koff[novf] = (uint32_t)tn;
+        tot[0] = tn;
+        tot[1] = ts;
+        tot[2] = tu;
+    }
+}
+
+// room for the new rows: tot[3] = the largest region fill the buckets' new rows ask for, tot[4] =
+// their heap records
+static __global__ void __launch_bounds__(PLAN_T) k_ovf_room(const uint32_t *__restrict__ list, const uint32_t *__restrict__ used,
+                                                            const uint32_t *__restrict__ bnew, const uint32_t *__restrict__ bnrec,
+                                                            uint32_t novf, unsigned long long *__restrict__ tot) {
+    __shared__ unsigned long long s_m[PLAN_T / 64], s_r[PLAN_T / 64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long mx = 0, sr = 0;
+    for (uint32_t k = threadIdx.x; k < novf; k += PLAN_T) {
+        mx = max(mx, (unsigned long long)used[list[k]] + bnew[k]);
+        sr += bnrec[k];
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mx = max(mx, (unsigned long long)__shfl_xor(mx, o));
+        sr += __shfl_xor(sr, o);
+    }
+    if (lane == 0) {
+        s_m[w] = mx;
+        s_r[w] = sr;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t v = 1; v < PLAN_T / 64; v++) {
+            mx = max(mx, s_m[v]);
+            sr += s_r[v];
+        }
+        tot[3] = mx;
+        tot[4] = sr;
+    }
+}
+
 // the bucket of every 64th batch record and the words its records need (a record's bucket is then
 // its chunk's, or a step or two past it: the binary search over koff is one dependent chain of ~15
 // loads, and the bucket's words -- record range, staged base, row-table slice -- another three)
