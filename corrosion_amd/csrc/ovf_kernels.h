@@ -178,10 +178,9 @@ __device__ inline int ovf_kcmp(const OvfKey &a, const OvfKey &b, const uint8_t *
 // readbacks of the bucket lists: ~0.25 ms and ~0.06 ms at 32 K buckets, the GPU idle meanwhile) ----
 constexpr uint32_t PLAN_T = 1024;  // (x PLAN_PER buckets per thread: up to 32 K queued buckets)
 
+// next_pow2(2 n), 1 for n = 0 (the host's former `while (sl < 2 n) sl <<= 1` from sl = 1)
 __device__ inline unsigned long long ovf_slots_for(unsigned long long n) {
-    unsigned long long sl = 1;
-    while (sl < 2 * n) sl <<= 1;
-    return sl;
+    return n ? 1ULL << (64 - __clzll((long long)(2 * n - 1))) : 1ULL;
 }
 
 // exclusive scan across the 1024-thread workgroup; `total` = the sum of every x
@@ -829,6 +828,7 @@ static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(MergeArgs a, OvfDev 
             if (!keep && d.rimp) {
                 uint64_t dk;
                 ovf_drop_class(a, d, r, row, cl, cand, dk);
+                if (cand) d.key[r] = dk;  // (its own slot, read by nothing else: the compaction copies it)
             }
         }
         mine |= keep ? 1u << j : 0u;
@@ -871,10 +871,7 @@ static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(MergeArgs a, OvfDev 
         const uint64_t dm = __ballot(cand);
         if (cand) {  // dropped candidates fill (ckey, cval) from the end: kept + dropped <= kcap
             const uint32_t q = kcap - 1 - (od + (uint32_t)__popcll(dm & ((1ULL << lane) - 1)));
-            bool c2;
-            uint64_t dk;
-            ovf_drop_class(a, d, r, d.rowid[r], d.cl[r], c2, dk);  // (recomputed: the key, no flag written)
-            d.ckey[q] = dk;
+            d.ckey[q] = d.key[r];  // (the group key the first pass left there)
             d.cval[q] = r;
         }
         od += (uint32_t)__popcll(dm);
