@@ -808,7 +808,10 @@ __device__ inline void ovf_drop_class(const MergeArgs &a, const OvfDev &d, uint3
     if (!cand && (pos & BATCH_POS) && flag) a.impact[pos & 0x7FFFFFFFu] = flag;
 }
 
-constexpr uint32_t KEEP_T = 256, KEEP_E = 32, KEEP_CHUNK = KEEP_T * KEEP_E;
+#ifndef OVF_KEEP_E
+#define OVF_KEEP_E 32  // records per thread (<= 32: one bit each in a lane's masks)
+#endif
+constexpr uint32_t KEEP_T = 256, KEEP_E = OVF_KEEP_E, KEEP_CHUNK = KEEP_T * KEEP_E;
 static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(MergeArgs a, OvfDev d, uint32_t kcap) {
     __shared__ uint32_t s_cnt[KEEP_T / 64], s_base, s_dcnt[KEEP_T / 64], s_dbase;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = d.K;
