@@ -435,7 +435,10 @@ def run_single(args, traffic, traffic_note, traffic_kern=None, c5_traffic=None):
     kern = {k: v / args.steps for k, v in kern.items()}
     pipe_ms = sum(kern.values())
     alg_bytes = ALG_BYTES_PER_CHANGE * n + ALG_BYTES_PER_CELL * cells
-    achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
+    step_ms = dt / args.steps * 1e3
+    # (the fraction is over the whole step, reset included; the pipeline-only figure beside it)
+    achieved = alg_bytes / (step_ms * 1e-3) / 1e9
+    achieved_pipe = alg_bytes / (pipe_ms * 1e-3) / 1e9
     steady = steady_state(eng, prep, n, dev, dt / args.steps * 1e3, cells)
     agent = agent_path(eng, batch, n)
     e2e_agent = agent_e2e(eng, batch, n, agent["ms"])
@@ -457,7 +460,7 @@ def run_single(args, traffic, traffic_note, traffic_kern=None, c5_traffic=None):
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "none",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded, generated in HBM)",
@@ -470,6 +473,8 @@ def run_single(args, traffic, traffic_note, traffic_kern=None, c5_traffic=None):
                      "traffic_ratio": (traffic / alg_bytes) if traffic else None,
                      "traffic_by_kernel": ({k: {"fetch": round(v["fetch"]), "write": round(v["write"])}
                                             for k, v in sorted(traffic_kern.items())} if traffic_kern else None),
+                     "achieved_basis": "algorithmic bytes / ms_per_step (reset + apply)",
+                     "pipeline_achieved": achieved_pipe, "pipeline_frac": achieved_pipe / HBM_PEAK_GBS,
                      "alg_bytes_per_apply": alg_bytes, "pipeline_ms": pipe_ms, "kernels_ms": kern,
                      "dominant": max(kern, key=kern.get)},
         "cpu_baseline": cpu,

@@ -70,7 +70,8 @@ struct HostRow {  // one buffered change (__corro_buffered_changes row)
 bool is_long(uint8_t vt, uint8_t vl) { return vl == CORRO_VAL_LONG && (vt == CORRO_TEXT || vt == CORRO_BLOB); }
 
 // Failure injection for the atomicity tests: CORRO_FAULT names the steps that fail (comma-separated;
-// read on every call, so a test arms and disarms it around one call).
+// read on every call, so a test arms and disarms it around one call). (internal.h holds the same
+// helper for the HIP translation units; this one is compiled without the HIP headers.)
 bool fault_armed(const char *name) {
     const char *e = std::getenv("CORRO_FAULT");
     if (!e || !*e) return false;

@@ -1086,6 +1086,7 @@ int corro_apply_batch(corro_ctx *ctx, const corro_changes *in, int mem, corro_ap
     if (!ctx || !in) return fail(CORRO_E_INVALID, "NULL argument");
     if (ctx->poisoned) return fail(CORRO_E_DEVICE, poisoned_msg);
     if (in->n == 0) return CORRO_OK;
+    if (fault_armed("apply")) return fail(CORRO_E_NOMEM, "injected fault (CORRO_FAULT): apply");
     const auto t0 = std::chrono::steady_clock::now();
     ctx->apply_wrote = false;
     const int rc = apply_batch_impl(ctx, in, mem, out);
@@ -1250,6 +1251,7 @@ int corro_apply_slots(corro_ctx *ctx, const void *recs, uint32_t nsrc, uint64_t 
     if ((uintptr_t)recs % 16) return fail(CORRO_E_INVALID, "slot records must be 16-byte aligned");
     if (ctx->pm_ap || ctx->slot_rec) return fail(CORRO_E_INVALID, "a position map is already set on this context");
     if (ctx->aff_any) return fail(CORRO_E_INVALID, "slots carry INTEGER values: no column affinity may convert them");
+    if (fault_armed("apply_slots")) return fail(CORRO_E_NOMEM, "injected fault (CORRO_FAULT): apply_slots");
     corro_changes in{};
     in.n = (uint64_t)nsrc * cap;
     ctx->slot_rec = recs;

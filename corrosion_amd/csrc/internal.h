@@ -4,6 +4,7 @@
 
 #include <array>
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -12,6 +13,15 @@
 #include "corro_hip.h"
 
 namespace corro {
+
+// Failure injection for the atomicity / multi-rank failure tests: CORRO_FAULT names the steps that fail
+// (comma-separated; read on every call, so a test arms and disarms it around one call).
+inline bool fault_armed(const char *name) {
+    const char *e = std::getenv("CORRO_FAULT");
+    if (!e || !*e) return false;
+    const std::string s = std::string(",") + e + ",";
+    return s.find(std::string(",") + name + ",") != std::string::npos;
+}
 
 // Thread-local last error (corro_last_error).
 void set_error(const std::string &msg);
@@ -104,9 +114,11 @@ int pk_mirror_sync(corro_ctx *ctx);
 // Row keys of packed pks on the device (pkeys.hip): for every change i with (tcid[i] >> 16) == table and
 // a reference (ref[i] != none: bytes at base + (ref >> len_bits), length ref & (2^len_bits - 1); or with
 // off != null: bytes [off[i], off[i + 1]) of base), keys[i] = the row key -- the INTEGER pk of a table
-// not interned, else the interned id (new canonical keys get the next ids, in no particular order).
-// bad (optional, n bytes): 1 for a malformed encoding or a non-INTEGER pk of a table not interned
-// (keys[i] untouched); *nbad = their count. All pointers device memory; synchronous.
+// not interned, else the interned id (new canonical keys get the next ids in first-seen order: by the
+// index of the first change of each new key, as cr-sqlite numbers __crsql_key rows in insertion order).
+// bad (optional, n bytes): 1 for a malformed encoding, a reference past `limit` bytes of base, or a
+// non-INTEGER pk of a table not interned (keys[i] untouched); *nbad = their count. All pointers device
+// memory; synchronous. A failed call leaves the table as it was (its claims are dropped).
 struct PkRefs {
     const uint8_t *base = nullptr;
     const uint64_t *ref = nullptr;
@@ -114,6 +126,7 @@ struct PkRefs {
     uint64_t none = 0;
     uint32_t len_bits = 32;
     const uint32_t *tcid = nullptr;  // null: every change is of `table`
+    uint64_t limit = ~0ULL;          // bytes readable from base: a reference past it is a bad pk
 };
 int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, uint64_t *keys, uint8_t *bad,
                    uint64_t *nbad);

@@ -406,12 +406,22 @@ k_partv_fill(BatchDev in, const PkDir *dir, uint32_t n, const uint32_t *__restri
 // (pk bytes offset, length) listed in pkref for the host's interning
 __global__ void k_unpackv(const PackedRec80 *__restrict__ recs, uint32_t n, const uint64_t *__restrict__ src_rec,
                           const uint64_t *__restrict__ src_var, uint32_t nsrc, BatchOut o, uint64_t *__restrict__ voff,
-                          uint32_t *__restrict__ vsz, uint64_t *__restrict__ pkref) {
+                          uint32_t *__restrict__ vsz, uint64_t *__restrict__ pkref, uint64_t var_len,
+                          unsigned long long *__restrict__ nbad) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const PackedRec80 r = recs[i];
         uint32_t s = 0;
         while (s + 1 < nsrc && src_rec[s + 1] <= i) s++;
         const uint64_t at = src_var[s] + r.pad[0];
+        //  the shipped pk and value bytes must lie inside the received bytes, and a pk length
+        // must fit the 24-bit reference: a corrupt or mis-sized exchange is refused, not read past
+        if (r.pad[1] >= (1u << 24) || at + (uint64_t)r.pad[1] + r.pad[2] > var_len) {
+            atomicAdd(nbad, 1ULL);
+            pkref[i] = ~0ULL;
+            voff[i] = 0;
+            vsz[i] = 0;
+            continue;
+        }
         o.pk[i] = r.pk; o.cv[i] = r.cv; o.dbv[i] = r.dbv; o.v0[i] = r.v0;
         o.tcid[i] = r.tcid; o.cl[i] = r.cl; o.seq[i] = r.seq; o.site[i] = r.site;
         if (o.v1) o.v1[i] = r.v1;
@@ -582,6 +592,7 @@ extern "C" int corro_partition_slots(corro_ctx *ctx, const corro_changes *in, ui
     if (!in->pk || !in->table_cid || !in->col_version || !in->db_version || !in->cl || !in->seq || !in->site ||
         !in->val0)
         return fail(CORRO_E_INVALID, "a required batch array is NULL");
+    if (fault_armed("partition_slots")) return fail(CORRO_E_NOMEM, "injected fault (CORRO_FAULT): partition_slots");
     if (in->val1 || in->val_type || in->val_len || in->ts || in->val_off)
         return fail(CORRO_E_RANGE, "slots carry 48-B records: INTEGER batches without val1/val_type/val_len/ts");
     if ((uintptr_t)out % 16) return fail(CORRO_E_INVALID, "packed records must be 16-byte aligned");
@@ -764,10 +775,19 @@ extern "C" int corro_unpack_var(corro_ctx *ctx, const void *recs, uint64_t n, co
                 const_cast<uint32_t *>(out->site),   const_cast<uint64_t *>(out->val0),
                 const_cast<uint64_t *>(out->val1),   const_cast<uint8_t *>(out->val_type),
                 const_cast<uint8_t *>(out->val_len), const_cast<uint64_t *>(out->ts)};
+    unsigned long long *d_nbad = reinterpret_cast<unsigned long long *>(d_vb + 64);
+    CORRO_HIP_TRY(hipMemsetAsync(d_nbad, 0, 8, s));
     hipLaunchKernelGGL(k_unpackv, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
                        static_cast<const PackedRec80 *>(recs), (uint32_t)n, d_rb, d_vb, nsrc, bo,
-                       const_cast<uint64_t *>(out->val_off), const_cast<uint32_t *>(out->val_size), pkref);
+                       const_cast<uint64_t *>(out->val_off), const_cast<uint32_t *>(out->val_size), pkref, var_len,
+                       d_nbad);
     CORRO_HIP_TRY(hipGetLastError());
+    unsigned long long h_nbad = 0;
+    CORRO_HIP_TRY(hipMemcpyAsync(&h_nbad, d_nbad, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (h_nbad)
+        return fail(CORRO_E_INVALID, "shipped pk / value bytes outside the received var buffer (" +
+                                         std::to_string(h_nbad) + " records)");
     // interned pks: this engine's row keys for the shipped canonical bytes, interned on the device
     // (pkref: var offset << 24 | length, ~0 for a change of a table that is not interned)
     for (uint32_t t = 0; t < (uint32_t)ctx->pk.size(); t++) {
@@ -778,6 +798,7 @@ extern "C" int corro_unpack_var(corro_ctx *ctx, const void *recs, uint64_t n, co
         pr.none = ~0ULL;
         pr.len_bits = 24;
         pr.tcid = out->table_cid;
+        pr.limit = var_len;
         if (int rc = pk_keys_device(ctx, t, pr, n, const_cast<uint64_t *>(out->pk), nullptr, nullptr)) return rc;
     }
     CORRO_HIP_TRY(hipStreamSynchronize(s));

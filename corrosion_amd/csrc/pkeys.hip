@@ -10,23 +10,25 @@
 // non-canonical encodings of one key name one row, as cr-sqlite's re-packing makes them (SURVEY
 // App. A.3).
 //
-// Device intern (pk_keys_device), per table, over the changes that reference packed bytes:
-//   k_pk_parse   unpack_columns + pack_columns restated per change without writing: canonical length,
-//                route hash of the canonical bytes (pk_route_hash), whether the input already is
-//                canonical (the common case: pack_columns output), the value of a one-INTEGER pk
-//   [k_pk_canon] only when some input is not canonical: its canonical bytes into a scratch (scan of
-//                their lengths), the change's reference redirected there
-//   k_pk_probe   each change probes the table's slots by its hash: a slot whose tag matches names an
-//                existing id (bytes compared with the arena) or another change's claim of a new key
-//                (bytes compared with that change's canonical bytes); an empty slot is claimed with
-//                one 64-bit CAS of (tag, NEW | change). No change waits for another: a claim carries
-//                everything a later prober compares against.
-//   scans        claims -> new ids (table size + rank), their bytes -> arena offsets
-//   k_pk_commit  keys; each claim's canonical bytes, offset and hash appended, its slot -> the id
+// Device intern (pk_keys_device), per table, over the changes that reference packed bytes (round 6:
+// one fused pass for the common case):
+//   k_pk_find    per wave, the 64 changes' packed bytes staged in LDS with 16-B loads along the bytes;
+//                per change unpack_columns + pack_columns restated without writing (canonical length,
+//                route hash pk_route_hash, whether the input already is canonical, the value of a
+//                one-INTEGER pk), then the probe of the table's slots (plain 32-B slot loads): a held key
+//                writes its id straight into keys[] (a warm call is this one kernel); an empty slot is
+//                claimed with one 64-bit CAS of (tag, NEW | change); a change that finds another's claim
+//                compares against the claimant's input bytes and raises the claim's first-seen word
+//   [k_pk_canon, k_pk_probe_slow]  only for inputs that are not canonical: their canonical bytes into a
+//                scratch, then the same probe through the claimants' recorded bytes
+//   k_pk_mark + scans  each claim's first-seen position flagged -> new ids (table size + rank) in
+//                first-seen order, their bytes -> arena offsets
+//   k_pk_commit  keys of the new keys; each claim's canonical bytes, offset and hash appended, its slot
+//                -> the id and the key's inline words
 // The slots (32 B: claim word, length, up to 23 canonical bytes inline) are sized by the keys the
 // table holds (load <= 1/2 with a share of new ones), not by the changes of a call; a probe that runs
 // past PK_MAX_PROBE slots marks the call for a retry with a table four times larger (rebuilt from the
-// arena).
+// arena). Any failed call drops its claims (the slots rebuilt from the committed keys).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -321,27 +323,30 @@ __device__ bool pk_canon_dev(const uint8_t *p, uint64_t len, CanonOut<WRITE> &co
     return true;
 }
 
+constexpr uint64_t PK_PENDING = 1ULL << 63;  // keys[i] during a call: a new key, claimed by change (key & ~bit)
+
 struct PkArgs {
     PkRefs r;
     uint32_t table;
     uint32_t interned;
     uint64_t n;
-    uint64_t *keys;
+    uint64_t *keys;     // the row keys (PK_PENDING | claimant while a new key is unresolved)
     uint8_t *bad;
-    // per change
-    uint32_t *clen;     // canonical length (0: no reference of this table, or malformed)
+    // per change, written only for the changes that need them (claimants and slow-path changes)
+    uint32_t *clen;     // canonical length
     uint64_t *cref;     // where its canonical bytes are: input offset, or PK_SCRATCH | scratch offset
     uint64_t *h;        // route hash
-    uint32_t *ncl;      // (non-canonical inputs) canonical length, for the scratch scan
-    uint64_t *nclo;     // inclusive scan of ncl
-    uint8_t *scratch;
-    uint32_t *owner;    // id, or PK_NEW | claimant
     uint32_t *slotix;   // a claimant's slot
-    uint32_t *newf;     // 1: a claimant (a new key)
-    uint32_t *newl;     // a claimant's canonical length
+    uint32_t *claims;   // the call's claimants (ctl[4] of them)
+    uint32_t *slow;     // changes whose input is not canonical (ctl[2] of them): canonicalised, then probed
+    uint32_t *newf;     // at each new key's first-seen position: 1
+    uint32_t *newl;     // at each new key's first-seen position: its canonical length
     uint32_t *rank;     // inclusive scan of newf
     uint64_t *noff;     // inclusive scan of newl
-    unsigned long long *ctl;  // [0] bad [1] max canonical length [2] non-canonical inputs [3] probe overflow
+    uint8_t *scratch;
+    // [0] bad [1] max canonical length [2] slow changes [3] probe overflow [4] claims
+    // [5] canonical bytes of the slow changes [6] scratch cursor
+    unsigned long long *ctl;
     // the table
     PkSlot *slots;
     uint64_t smask;
@@ -351,101 +356,28 @@ struct PkArgs {
     uint64_t nkeys, nbytes;
 };
 
-__device__ inline bool pk_src(const PkArgs &a, uint64_t i, const uint8_t *&p, uint64_t &len) {
-    if (a.r.tcid && (a.r.tcid[i] >> 16) != a.table) return false;
+// change i's packed bytes: 1 with (offset from base, length), 0 when it is not a change of this table
+// (or has no reference), -1 when its reference lies outside the buffer (a corrupt exchange
+// must not read past the received bytes)
+__device__ inline int pk_src(const PkArgs &a, uint64_t i, uint64_t &at, uint64_t &len) {
+    if (a.r.tcid && (a.r.tcid[i] >> 16) != a.table) return 0;
     if (a.r.off) {
-        p = a.r.base + a.r.off[i];
-        len = a.r.off[i + 1] - a.r.off[i];
-        return true;
+        at = a.r.off[i];
+        const uint64_t e = a.r.off[i + 1];
+        if (e < at || e > a.r.limit) return -1;
+        len = e - at;
+        return 1;
     }
     const uint64_t x = a.r.ref[i];
-    if (x == a.r.none) return false;
-    p = a.r.base + (x >> a.r.len_bits);
+    if (x == a.r.none) return 0;
+    at = x >> a.r.len_bits;
     len = x & ((1ULL << a.r.len_bits) - 1);
-    return true;
+    return at + len > a.r.limit ? -1 : 1;
 }
 
 __device__ inline const uint8_t *pk_cbytes(const PkArgs &a, uint64_t j) {
     const uint64_t c = a.cref[j];
     return (c & PK_SCRATCH) ? a.scratch + (c & ~PK_SCRATCH) : a.r.base + c;
-}
-
-#define PK_LOOP(i) for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x)
-
-// A pk of at most PK_STAGE bytes is parsed from a copy in LDS: the parse reads its bytes in a data-
-// dependent order (column types, then lengths), which from HBM is a chain of dependent loads per byte
-// (2.1 ms for config 2's 2^26 pks); the copy's loads are independent and issue at once.
-constexpr uint32_t PK_STAGE = 32;
-
-__global__ void __launch_bounds__(256) k_pk_parse(PkArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_pk[256 * PK_STAGE];
-    uint8_t *mine_lds = s_pk + threadIdx.x * PK_STAGE;
-    uint32_t nbad = 0, mx = 0, nnc = 0;
-    PK_LOOP(i) {
-        const uint8_t *p = nullptr;
-        uint64_t len = 0;
-        uint32_t cl = 0, nc = 0;
-        if (pk_src(a, i, p, len)) {
-            const uint8_t *q = p;
-            if (len <= PK_STAGE) {
-                uint8_t b[PK_STAGE];
-#pragma unroll
-                for (uint32_t k = 0; k < PK_STAGE; k++) b[k] = k < len ? p[k] : 0;
-                uint32_t *w = reinterpret_cast<uint32_t *>(mine_lds);
-#pragma unroll
-                for (uint32_t k = 0; k < PK_STAGE / 4; k++)
-                    w[k] = (uint32_t)b[4 * k] | ((uint32_t)b[4 * k + 1] << 8) | ((uint32_t)b[4 * k + 2] << 16) |
-                           ((uint32_t)b[4 * k + 3] << 24);
-                q = mine_lds;
-            }
-            CanonOut<false> co{q, len, nullptr};
-            bool one = false;
-            int64_t v = 0;
-            const bool ok = pk_canon_dev<false>(q, len, co, one, v) && co.o < (1ULL << 24);
-            if (!ok || (!a.interned && !one)) {
-                nbad++;
-                if (a.bad) a.bad[i] = 1;
-            } else if (!a.interned) {
-                a.keys[i] = (uint64_t)v;
-            } else {
-                cl = (uint32_t)co.o;
-                mx = max(mx, cl);
-                a.h[i] = co.hash();
-                const bool canon = co.same && co.o == len;
-                a.cref[i] = canon ? (uint64_t)(p - a.r.base) : PK_SCRATCH;
-                if (!canon) {
-                    nc = cl;
-                    nnc++;
-                }
-            }
-        }
-        a.clen[i] = cl;
-        a.ncl[i] = nc;
-    }
-    nbad = pk_wave_sum(nbad);
-    nnc = pk_wave_sum(nnc);
-    mx = pk_wave_max(mx);
-    if ((threadIdx.x & 63) == 0) {
-        if (nbad) atomicAdd(&a.ctl[0], (unsigned long long)nbad);
-        if (mx) atomicMax(&a.ctl[1], (unsigned long long)mx);
-        if (nnc) atomicAdd(&a.ctl[2], (unsigned long long)nnc);
-    }
-}
-
-// (non-canonical inputs only) their canonical bytes into the scratch at the scan of their lengths
-__global__ void __launch_bounds__(256) k_pk_canon(PkArgs a) {
-    PK_LOOP(i) {
-        if (!a.ncl[i]) continue;
-        const uint8_t *p = nullptr;
-        uint64_t len = 0;
-        pk_src(a, i, p, len);
-        const uint64_t o = a.nclo[i] - a.ncl[i];
-        CanonOut<true> co{p, len, a.scratch + o};
-        bool one = false;
-        int64_t v = 0;
-        pk_canon_dev<true>(p, len, co, one, v);
-        a.cref[i] = PK_SCRATCH | o;
-    }
 }
 
 __device__ inline bool pk_eq(const uint8_t *x, const uint8_t *y, uint32_t n) {
@@ -479,90 +411,334 @@ __device__ inline PkWords pk_words(const uint8_t *p, uint32_t cl) {
     }
     return w;
 }
-__device__ inline bool pk_words_eq(const PkWords &x, const PkSlot *ps) {
-    const uint64_t *q = reinterpret_cast<const uint64_t *>(ps) + 1;  // (bytes 8..31: len, b[0..22])
-    return q[0] == x.q[0] && q[1] == x.q[1] && q[2] == x.q[2];
+__device__ inline bool pk_words_eq(const PkWords &x, const PkWords &y) {
+    return x.q[0] == y.q[0] && x.q[1] == y.q[1] && x.q[2] == y.q[2];
 }
 
-// a committed key against my canonical bytes: inline in the slot (the line the claim word is on) or in
-// the arena
-__device__ inline bool pk_eq_slot(const PkArgs &a, const PkSlot *ps, uint32_t id, const uint8_t *mine, const PkWords &mw,
-                                  uint32_t cl, uint64_t h) {
-    if (cl <= PK_INLINE) return pk_words_eq(mw, ps);
+// One 32-B slot read as two 16-B plain loads: the claim word and the three inline words. Plain loads
+// are exact here: inside a probe kernel a slot's claim word only goes 0 -> claim (a stale 0 is settled
+// by the CAS that follows it), and committed words were written by an earlier kernel.
+__device__ inline void pk_slot_read(const PkSlot *ps, unsigned long long &w, PkWords &q) {
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(ps);
+    const uint4 x0 = s4[0], x1 = s4[1];
+    w = (unsigned long long)x0.x | ((unsigned long long)x0.y << 32);
+    q.q[0] = (uint64_t)x0.z | ((uint64_t)x0.w << 32);
+    q.q[1] = (uint64_t)x1.x | ((uint64_t)x1.y << 32);
+    q.q[2] = (uint64_t)x1.z | ((uint64_t)x1.w << 32);
+}
+
+// First-seen order of a new key (ids in first-seen order, as cr-sqlite's __crsql_key rowids
+// are assigned): while a slot is claimed its inline bytes are still zero, so its first 32-bit inline
+// word holds ~(the smallest index of a change of that key), raised by atomicMax from every change that
+// finds the claim (a plain read first: the word only grows, so a read at or above ~i skips the atomic).
+__device__ inline uint32_t *pk_first_word(PkSlot *ps) { return reinterpret_cast<uint32_t *>(ps) + 2; }
+__device__ inline void pk_first_seen(PkSlot *ps, uint32_t i) {
+    uint32_t *f = pk_first_word(ps);
+    if (*(volatile uint32_t *)f < ~i) atomicMax(f, ~i);
+}
+
+__device__ inline uint64_t pk_wave_min64(uint64_t x) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = (uint64_t)__shfl_xor((unsigned long long)x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+__device__ inline uint64_t pk_wave_max64(uint64_t x) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = (uint64_t)__shfl_xor((unsigned long long)x, o);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+// wave-aggregated append: one atomic per wave; every lane of the wave calls it
+__device__ inline uint32_t pk_wave_append(unsigned long long *ctr, bool take) {
+    const uint64_t m = __ballot(take);
+    if (!m) return 0;
+    const uint32_t lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = (uint32_t)atomicAdd(ctr, (unsigned long long)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    return base + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
+}
+
+// a committed key (claim word w = tag << 32 | id, inline words q) against my canonical bytes
+__device__ inline bool pk_eq_committed(const PkArgs &a, uint32_t id, const PkWords &q, const uint8_t *mine,
+                                       const PkWords &mw, uint32_t cl, uint64_t h) {
+    if (cl <= PK_INLINE) return pk_words_eq(mw, q);
     return a.koff[id + 1] - a.koff[id] == cl && a.khash[id] == h && pk_eq(a.kbytes + a.koff[id], mine, cl);
 }
 
-__global__ void __launch_bounds__(256) k_pk_probe(PkArgs a) {
-    PK_LOOP(i) {
-        a.newf[i] = 0;
-        a.newl[i] = 0;
-        const uint32_t cl = a.clen[i];
-        if (!cl) continue;
-        if (*(volatile unsigned long long *)&a.ctl[3]) continue;  // (retrying: a cached read, seen late is fine)
-        const uint64_t h = a.h[i];
-        const uint32_t tag = pk_tag(h);
-        const uint8_t *mine = pk_cbytes(a, i);
-        PkWords mw{};
-        if (cl <= PK_INLINE) mw = pk_words(mine, cl);
-        uint64_t sl = pk_slot_of(h, a.smask);
-        uint32_t owner = ~0u;
-        for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = (sl + 1) & a.smask) {
-            PkSlot *ps = a.slots + sl;
-            unsigned long long w = __hip_atomic_load(&ps->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (w == 0) {
-                const unsigned long long want = ((unsigned long long)tag << 32) | (PK_NEW | (uint32_t)i);
-                w = atomicCAS(&ps->w, 0ULL, want);
-                if (w == 0) {  // claimed: a new key, its canonical bytes already where cref says
-                    owner = PK_NEW | (uint32_t)i;
-                    a.slotix[i] = (uint32_t)sl;
-                    a.newf[i] = 1;
-                    a.newl[i] = cl;
-                    break;
-                }
-            }
-            if ((uint32_t)(w >> 32) != tag) continue;
-            const uint32_t v = (uint32_t)w;
-            bool eq;
-            if (v & PK_NEW) {
-                const uint32_t j = v & ~PK_NEW;
-                eq = a.clen[j] == cl && a.h[j] == h;
-                if (eq && cl <= PK_INLINE) {
-                    const PkWords jw = pk_words(pk_cbytes(a, j), cl);
-                    eq = jw.q[0] == mw.q[0] && jw.q[1] == mw.q[1] && jw.q[2] == mw.q[2];
-                } else if (eq) {
-                    eq = pk_eq(pk_cbytes(a, j), mine, cl);
-                }
-            } else {
-                eq = pk_eq_slot(a, ps, v, mine, mw, cl, h);  // (committed by an earlier kernel: plain loads)
-            }
-            if (eq) {
-                owner = v;
-                break;
+// The wave's staging window: 64 consecutive changes whose packed bytes lie within one window (the
+// common case: pack_columns output back to back, or a decoded frame) are copied into LDS with 16-B
+// loads along the bytes; lanes then parse from LDS. Larger windows read their bytes from HBM.
+constexpr uint32_t PK_WAVE_STAGE = 2048;
+constexpr uint32_t PK_FIND_THREADS = 256;
+
+// k_pk_find: the fused parse + probe (round 6; it replaces a parse kernel that wrote four columns per
+// change and a probe kernel that re-read them and the key bytes): per change, the canonical check, the
+// route hash and the key's slot words from the staged bytes, then the probe of the table with plain
+// slot loads. A held key writes its id into keys[] here -- the warm call (every key held) is this one
+// kernel. A new key is claimed by one 64-bit CAS of (tag, NEW | i); the changes that find the claim
+// compare against the claimant's input bytes (read-only: a claimant here always has canonical input),
+// take keys[i] = PENDING | claimant and raise the claim's first-seen word. Inputs that are not
+// canonical are listed for the slow path (canonicalised into a scratch, then probed).
+__global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_st[PK_FIND_THREADS / 64][PK_WAVE_STAGE];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t *st = s_st[wv];
+    const uint64_t wstride = (uint64_t)gridDim.x * (PK_FIND_THREADS / 64) * 64;
+    uint32_t nbad = 0, mx = 0;
+    unsigned long long slowb = 0;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(a.r.base);
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (PK_FIND_THREADS / 64) + wv) * 64; w0 < a.n; w0 += wstride) {
+        const uint64_t i = w0 + lane;
+        uint64_t at = 0, len = 0;
+        const int src = i < a.n ? pk_src(a, i, at, len) : 0;
+        const uint64_t lo = pk_wave_min64(src == 1 ? at : ~0ULL), hi = pk_wave_max64(src == 1 ? at + len : 0);
+        uintptr_t a0 = 0;
+        bool staged = false;
+        __builtin_amdgcn_wave_barrier();  // (the previous window's LDS reads are done)
+        if (lo < hi) {
+            a0 = (base + lo) & ~(uintptr_t)15;
+            const uintptr_t span = base + hi - a0;
+            if (span <= PK_WAVE_STAGE) {
+                staged = true;
+                // (an aligned 16-B chunk holding one byte of the buffer lies in that byte's page)
+                const uint4 *src4 = reinterpret_cast<const uint4 *>(a.r.base + (intptr_t)(a0 - base));
+                for (uint32_t c = lane; (uintptr_t)c * 16 < span; c += 64)
+                    *reinterpret_cast<uint4 *>(st + 16 * c) = src4[c];
             }
         }
-        if (owner == ~0u) atomicOr(&a.ctl[3], 1ULL);  // (the table is too full: the call retries)
-        a.owner[i] = owner;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        bool slow = false, claimed = false;
+        uint32_t cl = 0;
+        uint64_t hh = 0, sl = 0;
+        if (src < 0) {
+            nbad++;
+            if (a.bad) a.bad[i] = 1;
+        } else if (src == 1) {
+            const uint8_t *p = staged ? st + (base + at - a0) : a.r.base + at;
+            CanonOut<false> co{p, len, nullptr};
+            bool one = false;
+            int64_t v = 0;
+            const bool ok = pk_canon_dev<false>(p, len, co, one, v) && co.o < (1ULL << 24);
+            if (!ok || (!a.interned && !one)) {
+                nbad++;
+                if (a.bad) a.bad[i] = 1;
+            } else if (!a.interned) {
+                a.keys[i] = (uint64_t)v;
+            } else {
+                cl = (uint32_t)co.o;
+                mx = max(mx, cl);
+                hh = co.hash();
+                if (!(co.same && co.o == len)) {
+                    slow = true;
+                    a.clen[i] = cl;
+                    a.h[i] = hh;
+                    slowb += cl;
+                } else if (!*(volatile unsigned long long *)&a.ctl[3]) {  // (retrying: seen late is fine)
+                    const uint32_t tag = pk_tag(hh);
+                    PkWords mw{};
+                    if (cl <= PK_INLINE) mw = pk_words(p, cl);
+                    sl = pk_slot_of(hh, a.smask);
+                    uint64_t res = ~0ULL;
+                    for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = (sl + 1) & a.smask) {
+                        PkSlot *ps = a.slots + sl;
+                        unsigned long long w;
+                        PkWords q;
+                        pk_slot_read(ps, w, q);
+                        if (w == 0) {
+                            const unsigned long long want = ((unsigned long long)tag << 32) | (PK_NEW | (uint32_t)i);
+                            w = atomicCAS(&ps->w, 0ULL, want);
+                            if (w == 0) {
+                                claimed = true;
+                                res = PK_PENDING | i;
+                                break;
+                            }
+                            q = PkWords{};  // (claimed by another change meanwhile: its inline words are not read)
+                        }
+                        if ((uint32_t)(w >> 32) != tag) continue;
+                        const uint32_t vv = (uint32_t)w;
+                        if (vv & PK_NEW) {
+                            const uint32_t j = vv & ~PK_NEW;
+                            uint64_t jat = 0, jlen = 0;
+                            bool eq = pk_src(a, j, jat, jlen) == 1 && jlen == cl;  // (a claimant's input is canonical)
+                            if (eq) {
+                                const uint8_t *pj = a.r.base + jat;
+                                eq = cl <= PK_INLINE ? pk_words_eq(pk_words(pj, cl), mw) : pk_eq(pj, p, cl);
+                            }
+                            if (eq) {
+                                pk_first_seen(ps, (uint32_t)i);
+                                res = PK_PENDING | j;
+                                break;
+                            }
+                        } else if (pk_eq_committed(a, vv, q, p, mw, cl, hh)) {
+                            res = vv;
+                            break;
+                        }
+                    }
+                    if (res == ~0ULL) {
+                        atomicOr(&a.ctl[3], 1ULL);  // (the table is too full: the call retries)
+                    } else {
+                        a.keys[i] = res;
+                    }
+                }
+            }
+        }
+        // claimants and slow changes listed (one atomic per wave each)
+        const uint32_t ck = pk_wave_append(&a.ctl[4], claimed);
+        if (claimed) {
+            a.claims[ck] = (uint32_t)i;
+            a.clen[i] = cl;
+            a.h[i] = hh;
+            a.cref[i] = at;
+            a.slotix[i] = (uint32_t)sl;
+            pk_first_seen(a.slots + sl, (uint32_t)i);
+        }
+        const uint32_t sk = pk_wave_append(&a.ctl[2], slow);
+        if (slow) a.slow[sk] = (uint32_t)i;
+    }
+    nbad = pk_wave_sum(nbad);
+    mx = pk_wave_max(mx);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) slowb += (unsigned long long)__shfl_xor(slowb, o);
+    if ((threadIdx.x & 63) == 0) {
+        if (nbad) atomicAdd(&a.ctl[0], (unsigned long long)nbad);
+        if (mx) atomicMax(&a.ctl[1], (unsigned long long)mx);
+        if (slowb) atomicAdd(&a.ctl[5], slowb);
     }
 }
 
+#define PK_LIST(k, cnt) for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < (cnt); k += (uint64_t)gridDim.x * blockDim.x)
+
+// (slow path) the listed changes' canonical bytes into the scratch
+__global__ void __launch_bounds__(256) k_pk_canon(PkArgs a, uint64_t nslow) {
+    PK_LIST(k, nslow) {
+        const uint32_t i = a.slow[k];
+        uint64_t at = 0, len = 0;
+        pk_src(a, i, at, len);
+        const uint64_t o = atomicAdd(&a.ctl[6], (unsigned long long)a.clen[i]);
+        CanonOut<true> co{a.r.base + at, len, a.scratch + o};
+        bool one = false;
+        int64_t v = 0;
+        pk_canon_dev<true>(a.r.base + at, len, co, one, v);
+        a.cref[i] = PK_SCRATCH | o;
+    }
+}
+
+// (slow path) the listed changes probe the table; every claimant's canonical bytes, length and hash were
+// written by an earlier kernel, so a claim is compared through cref / clen / h
+__global__ void __launch_bounds__(256) k_pk_probe_slow(PkArgs a, uint64_t nslow) {
+    const uint32_t lane = threadIdx.x & 63;
+    (void)lane;
+    for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < nslow; k0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = k0 + threadIdx.x;
+        bool claimed = false;
+        uint32_t i = 0;
+        uint64_t sl = 0;
+        if (k < nslow && !*(volatile unsigned long long *)&a.ctl[3]) {
+            i = a.slow[k];
+            const uint32_t cl = a.clen[i];
+            const uint64_t h = a.h[i];
+            const uint32_t tag = pk_tag(h);
+            const uint8_t *mine = pk_cbytes(a, i);
+            PkWords mw{};
+            if (cl <= PK_INLINE) mw = pk_words(mine, cl);
+            sl = pk_slot_of(h, a.smask);
+            uint64_t res = ~0ULL;
+            for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = (sl + 1) & a.smask) {
+                PkSlot *ps = a.slots + sl;
+                unsigned long long w;
+                PkWords q;
+                pk_slot_read(ps, w, q);
+                if (w == 0) {
+                    w = atomicCAS(&ps->w, 0ULL, ((unsigned long long)tag << 32) | (PK_NEW | i));
+                    if (w == 0) {
+                        claimed = true;
+                        res = PK_PENDING | i;
+                        break;
+                    }
+                    q = PkWords{};
+                }
+                if ((uint32_t)(w >> 32) != tag) continue;
+                const uint32_t vv = (uint32_t)w;
+                bool eq;
+                if (vv & PK_NEW) {
+                    const uint32_t j = vv & ~PK_NEW;
+                    eq = a.clen[j] == cl && a.h[j] == h;
+                    if (eq) eq = cl <= PK_INLINE ? pk_words_eq(pk_words(pk_cbytes(a, j), cl), mw) : pk_eq(pk_cbytes(a, j), mine, cl);
+                    if (eq) {
+                        pk_first_seen(ps, i);
+                        res = PK_PENDING | j;
+                        break;
+                    }
+                } else if (pk_eq_committed(a, vv, q, mine, mw, cl, h)) {
+                    res = vv;
+                    break;
+                }
+            }
+            if (res == ~0ULL)
+                atomicOr(&a.ctl[3], 1ULL);
+            else
+                a.keys[i] = res;
+        }
+        const uint32_t ck = pk_wave_append(&a.ctl[4], claimed);
+        if (claimed) {
+            a.claims[ck] = i;
+            a.slotix[i] = (uint32_t)sl;
+            pk_first_seen(a.slots + sl, i);
+        }
+    }
+}
+
+// each claim's first-seen position gets its new-key flag and length (the scans then number the new keys
+// in first-seen order)
+__global__ void __launch_bounds__(256) k_pk_mark(PkArgs a, uint64_t nclaims) {
+    PK_LIST(k, nclaims) {
+        const uint32_t c = a.claims[k];
+        const uint32_t f = ~*pk_first_word(a.slots + a.slotix[c]);
+        a.newf[f] = 1;
+        a.newl[f] = a.clen[c];
+    }
+}
+
+// the slot's inline words from a key's canonical bytes (zero past the length; a key longer than the
+// inline bytes keeps only its length there)
 __device__ inline void pk_slot_fill(PkSlot &sl, const uint8_t *src, uint32_t cl) {
-    sl.len = (uint8_t)min(cl, 255u);
-    if (cl <= PK_INLINE)
-        for (uint32_t k = 0; k < cl; k++) sl.b[k] = src[k];
+    PkWords w{};
+    if (cl <= PK_INLINE) {
+        w = pk_words(src, cl);
+    } else {
+        w.q[0] = min(cl, 255u);
+    }
+    uint64_t *q = reinterpret_cast<uint64_t *>(&sl) + 1;
+    q[0] = w.q[0];
+    q[1] = w.q[1];
+    q[2] = w.q[2];
 }
 
 __global__ void __launch_bounds__(256) k_pk_commit(PkArgs a) {
-    PK_LOOP(i) {
-        const uint32_t cl = a.clen[i];
-        if (!cl) continue;
-        const uint32_t o = a.owner[i];
-        const uint32_t id = (o & PK_NEW) ? (uint32_t)a.nkeys + a.rank[o & ~PK_NEW] - 1u : o;
+    PK_LIST(i, a.n) {
+        const uint64_t key = a.keys[i];
+        if (!(key & PK_PENDING)) continue;
+        uint64_t at = 0, len = 0;
+        if (pk_src(a, i, at, len) != 1 || (a.bad && a.bad[i])) continue;  // (another table's key, or a bad pk)
+        const uint32_t c = (uint32_t)(key & ~PK_PENDING);
+        const uint32_t f = ~*pk_first_word(a.slots + a.slotix[c]);
+        const uint32_t id = (uint32_t)a.nkeys + a.rank[f] - 1u;
         a.keys[i] = id;
-        if (!a.newf[i]) continue;
-        const uint64_t at = a.nbytes + a.noff[i] - cl;
+        if (c != i) continue;
+        const uint32_t cl = a.clen[i];
+        const uint64_t o = a.nbytes + a.noff[f] - cl;
         const uint8_t *src = pk_cbytes(a, i);
-        for (uint32_t k = 0; k < cl; k++) a.kbytes[at + k] = src[k];
-        a.koff[id + 1] = at + cl;
+        for (uint32_t k = 0; k < cl; k++) a.kbytes[o + k] = src[k];
+        a.koff[id + 1] = o + cl;
         a.khash[id] = a.h[i];
         PkSlot &sl = a.slots[a.slotix[i]];
         pk_slot_fill(sl, src, cl);
@@ -570,7 +746,8 @@ __global__ void __launch_bounds__(256) k_pk_commit(PkArgs a) {
     }
 }
 
-// the slots rebuilt from the keys (a larger table, or a retry after a probe overflow)
+// the slots rebuilt from the keys (a larger table, a retry after a probe overflow, or the cleanup of a
+// failed call's claims)
 __global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t mask, const uint64_t *khash,
                                                    const uint64_t *koff, const uint8_t *kbytes, uint64_t nkeys) {
     for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < nkeys; id += (uint64_t)gridDim.x * blockDim.x) {
@@ -584,7 +761,7 @@ __global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t mask,
     }
 }
 
-#undef PK_LOOP
+#undef PK_LIST
 
 dim3 pk_grid(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 16384))); }
 
@@ -608,6 +785,19 @@ int pk_slots_resize(corro_ctx *ctx, PkTable &t, uint64_t want, uint64_t min_slot
     return CORRO_OK;
 }
 
+// A failed call leaves claim words (tag | NEW | change) and first-seen words in the slots; the next call
+// would read them as claims of its own changes. Rebuild the slots from the committed keys;
+// if even that fails, drop them so the next call builds them afresh.
+void pk_drop_claims(corro_ctx *ctx, PkTable &t) {
+    const std::string err = corro_last_error();
+    if (pk_slots_resize(ctx, t, t.n, t.nslots) != CORRO_OK) {
+        (void)hipStreamSynchronize(ctx->stream);
+        t.d_slots.release();
+        t.nslots = 0;
+    }
+    set_error(err);
+}
+
 }  // namespace
 
 int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, uint64_t *keys, uint8_t *bad,
@@ -627,7 +817,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     if (int rc = prim_inclusive_scan_u32_u64(nullptr, &t1, nullptr, nullptr, n, s)) return rc;
     temp = std::max(temp, t1);
     const uint64_t c4 = al(n * 4), c8 = al(n * 8);
-    const uint64_t need = 7 * c4 + 4 * c8 + 256 + al(temp);
+    const uint64_t need = 7 * c4 + 3 * c8 + 256 + al(temp);
     if (int rc = ctx->d_pk_scratch.ensure(need)) return rc;
     uint8_t *base = ctx->d_pk_scratch.as<uint8_t>();
     PkArgs a{};
@@ -644,97 +834,117 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
         return p;
     };
     a.clen = (uint32_t *)take(c4);
-    a.ncl = (uint32_t *)take(c4);
-    a.owner = (uint32_t *)take(c4);
     a.slotix = (uint32_t *)take(c4);
+    a.claims = (uint32_t *)take(c4);
+    a.slow = (uint32_t *)take(c4);
     a.newf = (uint32_t *)take(c4);
     a.newl = (uint32_t *)take(c4);
     a.rank = (uint32_t *)take(c4);
     a.cref = (uint64_t *)take(c8);
     a.h = (uint64_t *)take(c8);
-    a.nclo = (uint64_t *)take(c8);
     a.noff = (uint64_t *)take(c8);
     a.ctl = (unsigned long long *)take(256);
     void *d_temp = take(al(temp));
-    CORRO_HIP_TRY(hipMemsetAsync(a.ctl, 0, 64, s));
-    if (bad) CORRO_HIP_TRY(hipMemsetAsync(bad, 0, n, s));
-    hipLaunchKernelGGL(k_pk_parse, pk_grid(n), dim3(256), 0, s, a);
-    CORRO_HIP_TRY(hipGetLastError());
-    unsigned long long ctl[4] = {0, 0, 0, 0};
-    CORRO_HIP_TRY(hipMemcpyAsync(ctl, a.ctl, 32, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipStreamSynchronize(s));
-    if (nbad) *nbad = ctl[0];
-    if (ctl[0] && !bad) {
-        return t.interned ? fail(CORRO_E_INVALID, "malformed packed primary key (unpack_columns)")
-                          : fail(CORRO_E_RANGE, "table " + ctx->tables[table].name +
-                                                    " keys rows by one INTEGER pk (or a pk is malformed): mark it interned");
+    if (t.interned) {
+        if (t.n + n > ((uint64_t)PK_NEW - 1)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
+        // slots for the held keys and a share of the call's (load <= 1/2); a call that brings more new keys
+        // than that overflows a probe and retries with a table four times larger (rebuilt from the arena).
+        // Sized by keys, not by changes: a warm call (every key held) probes a table sized by its keys.
+        // (load <= 1/2 for the held keys, <= 3/4 with the call's estimated new keys: a sixteenth of its
+        // changes into an empty table, a sixty-fourth into one that holds keys)
+        const uint64_t est_new = std::max<uint64_t>(t.n ? n / 64 : n / 16, 1ULL << 16);
+        const uint64_t want = std::max<uint64_t>(t.n, (t.n + est_new) * 2 / 3);
+        if (t.nslots < 2 * want) TRY_PK(pk_slots_resize(ctx, t, want));
+        a.koff = t.d_off.as<uint64_t>();
+        a.kbytes = t.d_bytes.as<uint8_t>();
+        a.khash = t.d_hash.as<uint64_t>();
+        a.nkeys = t.n;
+        a.nbytes = t.nbytes;
     }
-    if (!t.interned) return CORRO_OK;
-    t.max_len = std::max<uint64_t>(t.max_len, ctl[1]);
+    // from the first probe on, an error return drops this call's claims from the slots
+    auto failc = [&](int rc) {
+        if (t.interned && t.nslots) pk_drop_claims(ctx, t);
+        return rc;
+    };
+#define TRY_PKC(x)                            \
+    do {                                      \
+        int rc_ = (x);                        \
+        if (rc_ != CORRO_OK) return failc(rc_); \
+    } while (0)
+#define HIP_PKC(x)                                                                                   \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) return failc(fail(CORRO_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_))); \
+    } while (0)
+    unsigned long long ctl[8] = {};
     DevBuf scratch;  // (non-canonical inputs: their canonical bytes)
-    if (ctl[2]) {
-        TRY_PK(prim_inclusive_scan_u32_u64(d_temp, &temp, a.ncl, a.nclo, n, s));
-        uint64_t tot = 0;
-        CORRO_HIP_TRY(hipMemcpyAsync(&tot, a.nclo + (n - 1), 8, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
-        if (int rc = scratch.ensure(std::max<uint64_t>(tot, 1))) return rc;
-        a.scratch = scratch.as<uint8_t>();
-        hipLaunchKernelGGL(k_pk_canon, pk_grid(n), dim3(256), 0, s, a);
-        CORRO_HIP_TRY(hipGetLastError());
-    }
-    if (t.n + n > ((uint64_t)PK_NEW - 1)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
-    // slots for the held keys and a share of the call's (load <= 1/2); a call that brings more new keys
-    // than that overflows a probe and retries with a table four times larger (rebuilt from the arena).
-    // Sized by keys, not by changes: a warm call (every key held) probes a table that stays in the MALL.
-    // (load <= 1/2 for the held keys, <= 3/4 with the call's estimated new keys: a sixteenth of its
-    // changes into an empty table, a sixty-fourth into one that holds keys)
-    const uint64_t est_new = std::max<uint64_t>(t.n ? n / 64 : n / 16, 1ULL << 16);
-    const uint64_t want = std::max<uint64_t>(t.n, (t.n + est_new) * 2 / 3);
-    if (t.nslots < 2 * want) TRY_PK(pk_slots_resize(ctx, t, want));
-    a.slots = t.d_slots.as<PkSlot>();
-    a.smask = t.nslots - 1;
-    a.koff = t.d_off.as<uint64_t>();
-    a.kbytes = t.d_bytes.as<uint8_t>();
-    a.khash = t.d_hash.as<uint64_t>();
-    a.nkeys = t.n;
-    a.nbytes = t.nbytes;
     for (int attempt = 0;; attempt++) {
-        hipLaunchKernelGGL(k_pk_probe, pk_grid(n), dim3(256), 0, s, a);
-        CORRO_HIP_TRY(hipGetLastError());
-        CORRO_HIP_TRY(hipMemcpyAsync(&ctl[3], a.ctl + 3, 8, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
+        a.slots = t.d_slots.as<PkSlot>();
+        a.smask = t.nslots ? t.nslots - 1 : 0;
+        HIP_PKC(hipMemsetAsync(a.ctl, 0, 64, s));
+        if (bad) HIP_PKC(hipMemsetAsync(bad, 0, n, s));
+        const uint32_t nwaves = (uint32_t)((n + 63) / 64);
+        const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((nwaves + 3) / 4, 8192));
+        if (fault_armed("pk_find")) return failc(fail(CORRO_E_DEVICE, "injected fault (CORRO_FAULT): pk_find"));
+        hipLaunchKernelGGL(k_pk_find, dim3(grid), dim3(PK_FIND_THREADS), 0, s, a);
+        HIP_PKC(hipGetLastError());
+        HIP_PKC(hipMemcpyAsync(ctl, a.ctl, 64, hipMemcpyDeviceToHost, s));
+        HIP_PKC(hipStreamSynchronize(s));
+        if (nbad) *nbad = ctl[0];
+        if (ctl[0] && !bad) {
+            return failc(t.interned ? fail(CORRO_E_INVALID, "malformed packed primary key (unpack_columns, or bytes "
+                                                            "outside the buffer)")
+                                    : fail(CORRO_E_RANGE, "table " + ctx->tables[table].name +
+                                                              " keys rows by one INTEGER pk (or a pk is malformed): mark "
+                                                              "it interned"));
+        }
+        if (!t.interned) return CORRO_OK;
+        t.max_len = std::max<uint64_t>(t.max_len, ctl[1]);
+        if (ctl[2] && !ctl[3]) {  // slow path: non-canonical inputs canonicalised, then probed
+            HIP_PKC((scratch.ensure(std::max<uint64_t>(ctl[5], 1)) == CORRO_OK) ? hipSuccess : hipErrorOutOfMemory);
+            a.scratch = scratch.as<uint8_t>();
+            hipLaunchKernelGGL(k_pk_canon, pk_grid(ctl[2]), dim3(256), 0, s, a, (uint64_t)ctl[2]);
+            hipLaunchKernelGGL(k_pk_probe_slow, pk_grid(ctl[2]), dim3(256), 0, s, a, (uint64_t)ctl[2]);
+            HIP_PKC(hipGetLastError());
+            HIP_PKC(hipMemcpyAsync(ctl + 3, a.ctl + 3, 16, hipMemcpyDeviceToHost, s));
+            HIP_PKC(hipStreamSynchronize(s));
+        }
         if (!ctl[3]) break;
         // a probe ran long: rebuild a table four times larger from the committed keys and probe again
-        if (attempt == 6) return fail(CORRO_E_DEVICE, "internal: interned pk probes do not terminate");
-        TRY_PK(pk_slots_resize(ctx, t, t.n, 4 * t.nslots));
-        a.slots = t.d_slots.as<PkSlot>();
-        a.smask = t.nslots - 1;
-        CORRO_HIP_TRY(hipMemsetAsync(a.ctl + 3, 0, 8, s));
+        if (attempt == 6) return failc(fail(CORRO_E_DEVICE, "internal: interned pk probes do not terminate"));
+        TRY_PKC(pk_slots_resize(ctx, t, t.n, 4 * t.nslots));
     }
-    TRY_PK(prim_inclusive_scan_u32(d_temp, &temp, a.newf, a.rank, (uint32_t)n, s));
+    const uint64_t nclaims = ctl[4];
+    if (!nclaims) return CORRO_OK;  // (a warm call: every key held, ids already in keys[])
+    HIP_PKC(hipMemsetAsync(a.newf, 0, 4 * n, s));
+    HIP_PKC(hipMemsetAsync(a.newl, 0, 4 * n, s));
+    hipLaunchKernelGGL(k_pk_mark, pk_grid(nclaims), dim3(256), 0, s, a, nclaims);
+    HIP_PKC(hipGetLastError());
+    TRY_PKC(prim_inclusive_scan_u32(d_temp, &temp, a.newf, a.rank, (uint32_t)n, s));
+    TRY_PKC(prim_inclusive_scan_u32_u64(d_temp, &temp, a.newl, a.noff, n, s));
     uint32_t nnew = 0;
     uint64_t nb = 0;
-    CORRO_HIP_TRY(hipMemcpyAsync(&nnew, a.rank + (n - 1), 4, hipMemcpyDeviceToHost, s));
-    CORRO_HIP_TRY(hipStreamSynchronize(s));
-    if (nnew) {  // (a warm call -- every key held -- needs no byte offsets)
-        TRY_PK(prim_inclusive_scan_u32_u64(d_temp, &temp, a.newl, a.noff, n, s));
-        CORRO_HIP_TRY(hipMemcpyAsync(&nb, a.noff + (n - 1), 8, hipMemcpyDeviceToHost, s));
-        CORRO_HIP_TRY(hipStreamSynchronize(s));
-    }
+    HIP_PKC(hipMemcpyAsync(&nnew, a.rank + (n - 1), 4, hipMemcpyDeviceToHost, s));
+    HIP_PKC(hipMemcpyAsync(&nb, a.noff + (n - 1), 8, hipMemcpyDeviceToHost, s));
+    HIP_PKC(hipStreamSynchronize(s));
+    if (nnew != nclaims) return failc(fail(CORRO_E_DEVICE, "internal: interned pk claims and first-seen marks differ"));
     // room for the new keys (offsets n + 1, hashes, bytes), keeping the committed ones
     const uint64_t nk = t.n + nnew, nbytes = t.nbytes + nb;
-    if (int rc = grow_keep(t.d_off, (nk + 1) * 8, (t.n + 1) * 8 * (t.d_off.p ? 1 : 0), s)) return rc;
-    if (int rc = grow_keep(t.d_hash, std::max<uint64_t>(nk, 1) * 8, t.n * 8, s)) return rc;
-    if (int rc = grow_keep(t.d_bytes, std::max<uint64_t>(nbytes, 1), t.nbytes, s)) return rc;
-    if (t.n == 0) CORRO_HIP_TRY(hipMemsetAsync(t.d_off.p, 0, 8, s));
+    TRY_PKC(grow_keep(t.d_off, (nk + 1) * 8, (t.n + 1) * 8 * (t.d_off.p ? 1 : 0), s));
+    TRY_PKC(grow_keep(t.d_hash, std::max<uint64_t>(nk, 1) * 8, t.n * 8, s));
+    TRY_PKC(grow_keep(t.d_bytes, std::max<uint64_t>(nbytes, 1), t.nbytes, s));
+    if (t.n == 0) HIP_PKC(hipMemsetAsync(t.d_off.p, 0, 8, s));
     a.koff = t.d_off.as<uint64_t>();
     a.kbytes = t.d_bytes.as<uint8_t>();
     a.khash = t.d_hash.as<uint64_t>();
+    if (fault_armed("pk_commit")) return failc(fail(CORRO_E_DEVICE, "injected fault (CORRO_FAULT): pk_commit"));
     hipLaunchKernelGGL(k_pk_commit, pk_grid(n), dim3(256), 0, s, a);
-    CORRO_HIP_TRY(hipGetLastError());
-    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    HIP_PKC(hipGetLastError());
+    HIP_PKC(hipStreamSynchronize(s));
     t.n = nk;
     t.nbytes = nbytes;
+#undef TRY_PKC
+#undef HIP_PKC
     if (2 * t.n > t.nslots) TRY_PK(pk_slots_resize(ctx, t, 2 * t.n));  // (the next call starts at load <= 1/4)
     return CORRO_OK;
 }
@@ -798,6 +1008,7 @@ int corro_pk_keys(corro_ctx *ctx, uint32_t table, const uint8_t *bytes, const ui
     PkRefs r;
     r.base = dbytes;
     r.off = doff;
+    r.limit = nb;
     if (int rc = pk_keys_device(ctx, table, r, n, dkeys, nullptr, nullptr)) return rc;
     CORRO_HIP_TRY(hipMemcpy(keys, dkeys, n * 8, hipMemcpyDeviceToHost));
     return CORRO_OK;

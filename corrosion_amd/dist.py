@@ -119,6 +119,40 @@ def slot_cap(n_max, world):
     return int(share + 8.0 * share ** 0.5 + 256)
 
 
+FAILED = -(1 << 63)  # a slot count with bit 63 set: the sender's batch failed (partition.hip's mark)
+
+
+def _local(err, fn, *args, **kw):
+    """Run one rank-local step of a multi-rank call unless an earlier step of this rank failed.
+    Returns (result or None, the first error). A rank-local CorroError must not leave this rank
+    outside the collectives its peers are about to enter (they would block in them, or see the
+    connection drop): the caller goes on with empty contributions and reports the error in the
+    call's last all-reduce, after which every rank raises (util.rs:849-855: the whole call fails)."""
+    from ._lib import CorroError
+    if err is not None:
+        return None, err
+    try:
+        return fn(*args, **kw), None
+    except CorroError as e:
+        return None, e
+
+
+def _raise_if_failed(err, nerr, world):
+    """Every rank raises when any rank failed: its own error, or one naming the peers'."""
+    from ._lib import CorroError
+    if err is not None:
+        raise err
+    if nerr:
+        raise CorroError(-3, f"multi-rank apply failed on {nerr} of {world} rank(s); this rank's own steps "
+                             "succeeded (rows it merged stay merged: re-applying the same changes is a no-op)")
+
+
+def _stream_ctx(engine, dev):
+    import contextlib
+    import torch
+    return torch.cuda.stream(engine.stream()) if dev.type == "cuda" else contextlib.nullcontext()
+
+
 def distributed_apply_slots(engine, batch, cap, group=None, impact=False):
     """The stream-ordered form of distributed_apply for INTEGER batches: partition into fixed slots of
     `cap` 48-B records per destination (slot_cap; the same cap on every rank), the per-slot counts and
@@ -132,6 +166,10 @@ def distributed_apply_slots(engine, batch, cap, group=None, impact=False):
     (corro_slots_flags_back) -- still no host wait.
     A rank whose incoming slot overflowed merges nothing in that pass; after it, one tiny all-reduce
     tells every rank, and the exact-size exchange (distributed_apply) repeats for those ranks only.
+    Failure (round 6): a rank whose partition, merge or flag pass raises still takes part in every
+    collective of the call -- its counts marked failed (bit 63, so its receivers merge nothing from it),
+    zero flags -- and the same all-reduce that carries the overflow count carries an error count, after
+    which EVERY rank raises (the reference fails the whole call, util.rs:849-855), none blocks.
     Returns the number of ranks that overflowed (0 in the common case), and with impact=True the flags
     (uint8 CUDA tensor, this rank's changes in its own order) as a second value."""
     import torch
@@ -141,63 +179,93 @@ def distributed_apply_slots(engine, batch, cap, group=None, impact=False):
         imp = engine.apply(batch, impact=impact)
         return (0, imp) if impact else 0
     n = int(batch["pk"].shape[0])
-    st = engine.stream()
-    st.wait_stream(torch.cuda.current_stream())  # the batch's producer (device-side wait)
+    dev = batch["pk"].device
+    cuda = dev.type == "cuda"
+    if cuda:
+        engine.stream().wait_stream(torch.cuda.current_stream())  # the batch's producer (device-side wait)
     gloo = dist.get_backend(group) == "gloo"
 
     def a2a(dst, src):
-        if gloo:  # (no device all-to-all in gloo: rehearsals stage through host memory)
+        if gloo and cuda:  # (no device all-to-all in gloo: rehearsals stage through host memory)
             h = torch.empty(src.numel(), dtype=src.dtype)
             dist.all_to_all_single(h, src.cpu(), group=group)
             dst.copy_(h.to(dst.device))
         else:
             dist.all_to_all_single(dst, src, group=group)
 
-    with torch.cuda.stream(st):
-        perm = torch.empty(world * cap, dtype=torch.int32, device=batch["pk"].device) if impact else None
-        recs, cnt = engine.partition_slots(batch, world, cap, perm=perm)
+    err = None
+    with _stream_ctx(engine, dev):
+        perm = torch.empty(world * cap, dtype=torch.int32, device=dev) if impact else None
+        got_p, err = _local(err, engine.partition_slots, batch, world, cap, perm=perm)
+        if got_p is None:  # (failed here: empty slots, every count marked failed)
+            recs = torch.zeros(world * cap * 48, dtype=torch.uint8, device=dev)
+            cnt = torch.full((world,), FAILED, dtype=torch.int64, device=dev)
+        else:
+            recs, cnt = got_p
         rcnt = torch.empty_like(cnt)
         a2a(rcnt, cnt)
         got = torch.empty_like(recs)
         a2a(got, recs)
-        imp_slots, over = engine.apply_slots(got, world, cap, rcnt, impact=impact)
+        res, err = _local(err, engine.apply_slots, got, world, cap, rcnt, impact=impact)
+        imp_slots, over = res if res is not None else (None, None)
+        if over is None:
+            over = torch.zeros(1, dtype=torch.int32, device=dev)
         flags = None
         if impact:
+            if imp_slots is None:
+                imp_slots = torch.zeros(world * cap, dtype=torch.uint8, device=dev)
             back = torch.empty_like(imp_slots)
             a2a(back, imp_slots)
-            flags = engine.slots_flags_back(back, world, cap, cnt, perm, n)
-        over = over.to(torch.int64)  # (on the engine's stream, where the apply wrote it)
-    torch.cuda.current_stream().wait_stream(st)  # (the caller's stream reads `over`, the flags and the state next)
-    tot = over.cpu() if gloo else over.clone()
+            flags, err = _local(err, engine.slots_flags_back, back, world, cap, cnt, perm, n)
+        over = over.to(torch.int64).reshape(1)  # (on the engine's stream, where the apply wrote it)
+    if cuda:
+        torch.cuda.current_stream().wait_stream(engine.stream())  # (the caller reads `over`, the flags, the state)
+    # one all-reduce: [ranks that overflowed, ranks that failed]
+    tot = torch.cat([over.cpu() if (gloo or not cuda) else over,
+                     torch.tensor([1 if err is not None else 0], dtype=torch.int64,
+                                  device="cpu" if (gloo or not cuda) else dev)])
     dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
-    nover = int(tot.item())
+    nover, nerr = (int(x) for x in tot.tolist())
+    _raise_if_failed(err, nerr, world)
     if nover:
-        recs2, rb, counts, perm2 = engine.partition_packed(batch, world, with_perm=impact)
-        got2, rc2 = exchange_records(recs2, rb, counts, group)
         mine = int(over.item())
-        imp2 = engine.apply(engine.unpack_records(got2, rb), impact=impact) if mine else None
+        res, err = _local(None, engine.partition_packed, batch, world, with_perm=impact)
+        if res is None:
+            recs2, rb, counts, perm2 = torch.zeros(0, dtype=torch.uint8, device=dev), 48, [0] * world, None
+        else:
+            recs2, rb, counts, perm2 = res
+        got2, rc2 = exchange_records(recs2, rb, counts, group)
+        imp2 = None
+        if mine:
+            unp, err = _local(err, engine.unpack_records, got2, rb)
+            if unp is not None:
+                imp2, err = _local(err, engine.apply, unp, impact=impact)
         if impact:  # every rank takes part in the flags' way back (the overflowed ones send real flags)
-            dev = batch["pk"].device
-            send = imp2[:sum(rc2)].contiguous() if mine else torch.zeros(sum(rc2), dtype=torch.uint8, device=dev)
+            send = imp2[:sum(rc2)].contiguous() if imp2 is not None else torch.zeros(sum(rc2), dtype=torch.uint8,
+                                                                                     device=dev)
             back2 = torch.empty(sum(counts), dtype=torch.uint8, device=dev)
-            if gloo:
+            if gloo and cuda:
                 b2 = torch.empty(sum(counts), dtype=torch.uint8)
                 dist.all_to_all_single(b2, send.cpu(), [int(c) for c in counts], rc2, group=group)
                 back2 = b2.to(dev)
             else:
                 dist.all_to_all_single(back2, send, [int(c) for c in counts], rc2, group=group)
             # flags from destinations that overflowed replace the slot pass's (which applied nothing there)
-            dst_over = torch.zeros(world, dtype=torch.int64)
-            ov = over.cpu() if gloo else over
+            ov = over.cpu() if (gloo or not cuda) else over
             allov = [torch.zeros_like(ov) for _ in range(world)]
             dist.all_gather(allov, ov, group=group)
             dst_over = torch.cat([x.cpu() for x in allov]).tolist()
-            start = 0
-            p2 = perm2.long()
-            for d, c in enumerate(counts):
-                if dst_over[d]:
-                    flags[p2[start:start + int(c)]] = back2[start:start + int(c)]
-                start += int(c)
+            if err is None and perm2 is not None:
+                start = 0
+                p2 = perm2.long()
+                for d, c in enumerate(counts):
+                    if dst_over[d]:
+                        flags[p2[start:start + int(c)]] = back2[start:start + int(c)]
+                    start += int(c)
+        e2 = torch.tensor([1 if err is not None else 0], dtype=torch.int64,
+                          device="cpu" if (gloo or not cuda) else dev)
+        dist.all_reduce(e2, op=dist.ReduceOp.SUM, group=group)
+        _raise_if_failed(err, int(e2.item()), world)
     return (nover, flags) if impact else nover
 
 
@@ -224,7 +292,9 @@ def distributed_apply(engine, batch, group=None, impact=False, verify=True):
     """Partition by owner rank into packed records, exchange them with one all-to-all, merge the
     owned rows into this rank's engine. With impact=True returns the crsql_rows_impacted() growth
     of THIS rank's input changes, in the caller's order (a second, 1-byte-per-change all-to-all
-    sends every flag back to its sender, and the partition's permutation restores the order)."""
+    sends every flag back to its sender, and the partition's permutation restores the order).
+    A rank-local failure (partition, unpack, merge) still joins every collective with empty
+    contributions; one all-reduce of an error count at the end makes every rank raise."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -235,27 +305,47 @@ def distributed_apply(engine, batch, group=None, impact=False, verify=True):
         if getattr(engine, "_sites_verified", None) != n_sites:
             verify_sites(engine, group)
             engine._sites_verified = n_sites
+    dev = batch["pk"].device
+    err = None
+    n_in = int(batch["pk"].shape[0])
     if "val_data" in batch or engine.interned:
         # interned pks (routed and re-keyed by their canonical bytes) or long values: records + bytes
-        recs, var, counts, vcounts, perm = engine.partition_var(batch, world, with_perm=impact)
+        res, err = _local(err, engine.partition_var, batch, world, with_perm=impact)
+        if res is None:
+            z = torch.zeros(0, dtype=torch.uint8, device=dev)
+            recs, var, counts, vcounts, perm = z, z, [0] * world, [0] * world, None
+        else:
+            recs, var, counts, vcounts, perm = res
         got, gvar, rcounts, rvar = exchange_var(recs, var, counts, vcounts, group)
-        mine = engine.unpack_var(got, gvar, rcounts, rvar)
+        mine, err = _local(err, engine.unpack_var, got, gvar, rcounts, rvar)
     else:
-        recs, rb, counts, perm = engine.partition_packed(batch, world, with_perm=impact)
+        res, err = _local(err, engine.partition_packed, batch, world, with_perm=impact)
+        if res is None:
+            recs, rb, counts, perm = torch.zeros(0, dtype=torch.uint8, device=dev), 48, [0] * world, None
+        else:
+            recs, rb, counts, perm = res
         got, rcounts = exchange_records(recs, rb, counts, group)
-        mine = engine.unpack_records(got, rb)
-    imp = engine.apply(mine, impact=impact)
-    if not impact:
-        return None
-    # flags back to the senders (reverse split sizes), then into the caller's order
-    dev = imp.device
-    back = torch.empty(sum(counts), dtype=torch.uint8, device=dev)
-    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
-        b2 = torch.empty(sum(counts), dtype=torch.uint8)
-        dist.all_to_all_single(b2, imp[:sum(rcounts)].cpu(), [int(c) for c in counts], rcounts, group=group)
-        back = b2.to(dev)
-    else:
-        dist.all_to_all_single(back, imp[:sum(rcounts)].contiguous(), [int(c) for c in counts], rcounts, group=group)
-    out = torch.empty_like(back)
-    out[perm.long()] = back
+        mine, err = _local(err, engine.unpack_records, got, rb)
+    imp = None
+    if mine is not None:
+        imp, err = _local(err, engine.apply, mine, impact=impact)
+    out = None
+    if impact:
+        # flags back to the senders (reverse split sizes), then into the caller's order
+        send = imp[:sum(rcounts)].contiguous() if imp is not None else torch.zeros(sum(rcounts), dtype=torch.uint8,
+                                                                                   device=dev)
+        back = torch.empty(sum(counts), dtype=torch.uint8, device=dev)
+        if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+            b2 = torch.empty(sum(counts), dtype=torch.uint8)
+            dist.all_to_all_single(b2, send.cpu(), [int(c) for c in counts], rcounts, group=group)
+            back = b2.to(dev)
+        else:
+            dist.all_to_all_single(back, send, [int(c) for c in counts], rcounts, group=group)
+        if perm is not None:
+            out = torch.zeros(n_in, dtype=torch.uint8, device=dev)
+            out[perm.long()] = back
+    cpu_red = dev.type != "cuda" or dist.get_backend(group) == "gloo"
+    e = torch.tensor([1 if err is not None else 0], dtype=torch.int64, device="cpu" if cpu_red else dev)
+    dist.all_reduce(e, op=dist.ReduceOp.SUM, group=group)
+    _raise_if_failed(err, int(e.item()), world)
     return out

@@ -358,7 +358,8 @@ def test_slot_partition_validates_and_marks_counts(bad):
 # each against the oracle's pk-sharded fold of the whole batch: every impact flag in each sender's
 # order, the union of the rank states by the order-independent digest of every output field (a
 # mismatch prints the row-by-row report), crsql_db_versions)
-NL_ADV, NL_INT = 4_000_000, 1 << 24
+NL_ADV, NL_INT, NL_CHUNKED = 4_000_000, 1 << 24, 1 << 26
+CHUNK_FORCED = 1 << 23
 
 
 def _large_worker(rank, world, port, outdir, kind):
@@ -369,12 +370,14 @@ def _large_worker(rank, world, port, outdir, kind):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if kind == "integer_slots_chunked":  # (each receiver applies its slot layout in index-range chunks)
+        os.environ["CORRO_HIP_CHUNK"] = str(CHUNK_FORCED)
     if kind == "adversarial":
         n, seed = NL_ADV, synth.config_seed(5)
         schema, sites = synth.adversarial_schema(8), synth.site_ids(1000, seed)
         full = synth.adversarial_batch(n, 1000, 8, 1 << 20, seed)
     else:
-        n, seed = NL_INT, synth.config_seed(2)
+        n, seed = (NL_CHUNKED if kind == "integer_slots_chunked" else NL_INT), synth.config_seed(2)
         schema, sites = {"t": ["a", "b", "c", "d"]}, synth.site_ids(1000, 1)
         full = synth.uniform_batch(n, 1000, 1 << 22, 4, seed)
     lo, hi = rank * n // world, (rank + 1) * n // world
@@ -386,8 +389,10 @@ def _large_worker(rank, world, port, outdir, kind):
         imp = distributed_apply(eng, part, impact=True)
         assert eng.metrics()["overflow_rounds"] >= 1  # the hot-row regime on this rank
     else:
-        nover, imp = distributed_apply_slots(eng, part, slot_cap(hi - lo, world), impact=True)
+        cap = slot_cap(hi - lo, world)
+        nover, imp = distributed_apply_slots(eng, part, cap, impact=True)
         assert nover == 0
+        np.save(os.path.join(outdir, f"lchunks{rank}.npy"), np.array(-(-(world * cap) // CHUNK_FORCED)))
     torch.cuda.synchronize()
     np.save(os.path.join(outdir, f"limp{rank}.npy"), imp.cpu().numpy())
     rows = eng.export()
@@ -422,3 +427,107 @@ def test_two_rank_large_batch_vs_sharded_oracle(tmp_path, kind):
     dbv = np.max([np.load(tmp_path / f"ldbv{r}.npy") for r in range(world)], axis=0)
     assert np.array_equal(dbv, fold.db_versions())
     print(f"{kind}: {n} changes over {world} ranks, {len(rows['pk'])} clock rows bit-exact")
+
+
+# ---- failure on one rank fails the call on every rank ----------------
+def _fail_worker(rank, world, port, outdir, case):
+    import datetime
+    import torch.distributed as dist
+    import corrosion_amd as ca
+    from corrosion_amd.dist import distributed_apply, distributed_apply_slots, slot_cap
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    full = synth.uniform_batch(NS, 16, 4000, 4, 77)
+    lo, hi = rank * NS // world, (rank + 1) * NS // world
+    mine = {k: v[lo:hi].copy() for k, v in full.items()}
+    if case.startswith("invalid") and rank == 0:
+        mine["site"][len(mine["site"]) // 2] = 999  # (an unregistered site ordinal: the receiver refuses it)
+    eng = ca.MergeEngine({"t": ["a", "b", "c", "d"]}, capacity_hint=NS, device=0)
+    eng.register_sites(synth.site_ids(16, 5))
+    if case == "apply_slots_rank1" and rank == 1:
+        os.environ["CORRO_FAULT"] = "apply_slots"
+    if case == "partition_slots_rank0" and rank == 0:
+        os.environ["CORRO_FAULT"] = "partition_slots"
+    try:
+        if case == "invalid_exact":
+            distributed_apply(eng, _to_dev(mine), impact=True)
+        else:
+            distributed_apply_slots(eng, _to_dev(mine), slot_cap(hi - lo, world), impact=True)
+        out = "ok"
+    except ca.CorroError as e:
+        out = "raised: " + str(e)
+    except RuntimeError as e:
+        out = "hung: " + str(e)
+    os.environ.pop("CORRO_FAULT", None)
+    open(os.path.join(outdir, f"f{rank}.txt"), "w").write(out)
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["apply_slots_rank1", "partition_slots_rank0", "invalid_slots", "invalid_exact"])
+def test_one_rank_failure_raises_on_every_rank(tmp_path, case):
+    """A rank-local failure inside the multi-rank step (an injected CORRO_FAULT in the slot merge or
+    the slot partition, or an invalid change: the sender's validation marks its slots, the receivers
+    repeat through the exact-size exchange whose merge refuses it -- with impact flags, whose
+    collectives follow that merge) makes every rank raise CorroError; none blocks in a collective."""
+    world = 2
+    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path), case), nprocs=world, join=True)
+    got = [open(tmp_path / f"f{r}.txt").read() for r in range(world)]
+    assert all(g.startswith("raised") for g in got), got
+
+
+def test_unpack_var_refuses_bytes_outside_the_received_buffer():
+    """corro_unpack_var checks each record's shipped pk / value span against the received
+    bytes (and a pk length against the 24-bit reference) on the device: a corrupt record is
+    CORRO_E_INVALID, never a read past the buffer."""
+    import torch
+    import corrosion_amd as ca
+    from tests.test_gpu_pk import INTERNED, SCHEMA, _changes
+    rows = _changes(np.random.default_rng(4), 400, 4)
+    eng = ca.MergeEngine(SCHEMA, capacity_hint=4096, device=0, interned=INTERNED)
+    eng.register_sites(synth.site_ids(6, 3))
+    dev = {}
+    for k, v in _pk_batch(eng, rows).items():
+        v = np.ascontiguousarray(v)
+        dev[k] = torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else
+                                  (v.view(np.int32) if v.dtype == np.uint32 else v)).cuda()
+    recs, var, counts, vcounts, _ = eng.partition_var(dev, 1)
+    assert vcounts[0] > 0
+    eng.unpack_var(recs.clone(), var, counts, vcounts)  # (intact: accepted)
+    r = recs.cpu().numpy().view(np.uint32).reshape(-1, 20)
+    j = int(np.nonzero(r[:, 18])[0][0])  # a record shipping pk bytes (pad[1] = its pk length)
+    for word, val in ((17, 1 << 30), (18, 1 << 24), (19, 1 << 28)):  # pad[0] offset, pad[1] pk length, pad[2] value size
+        bad = r.copy()
+        bad[j, word] = val
+        with pytest.raises(ca.CorroError):
+            eng.unpack_var(torch.from_numpy(bad.view(np.uint8).reshape(-1)).cuda(), var, counts, vcounts)
+    eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_two_rank_chunked_slot_receiver_vs_sharded_oracle(tmp_path):
+    """the chunked slot receiver config 3 runs at full size, pinned to the oracle at
+    2^26 global changes -- each receiver's ~2^25 slot records applied as index-range chunks of 2^23
+    (CORRO_HIP_CHUNK; >= 4 chunks, each merging into the state the earlier ones wrote), with impacts,
+    against the oracle's pk-sharded fold: every flag in each sender's order, the ranks' union row by
+    row, db_versions."""
+    from oracle import oracle as O
+    world = 2
+    mp.spawn(_large_worker, args=(world, _free_port(), str(tmp_path), "integer_slots_chunked"), nprocs=world,
+             join=True)
+    n = NL_CHUNKED
+    sites, batch = synth.site_ids(1000, 1), synth.uniform_batch(n, 1000, 1 << 22, 4, synth.config_seed(2))
+    fold = O.ShardedFold(sites, nshards=64, nthreads=16)
+    want_imp = fold.apply(batch, impact=True)
+    del batch
+    got_imp = np.concatenate([np.load(tmp_path / f"limp{r}.npy") for r in range(world)])
+    assert np.array_equal(got_imp, want_imp), "impact flags differ from the oracle"
+    parts = [dict(np.load(tmp_path / f"lrows{r}.npz")) for r in range(world)]
+    rows = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    chunks = [int(np.load(tmp_path / f"lchunks{r}.npy")) for r in range(world)]
+    assert min(chunks) >= 4, chunks
+    diff = O.rows_diff(rows, fold.export())
+    assert diff is None, str(diff)
+    dbv = np.max([np.load(tmp_path / f"ldbv{r}.npy") for r in range(world)], axis=0)
+    assert np.array_equal(dbv, fold.db_versions())

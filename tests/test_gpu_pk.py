@@ -5,6 +5,7 @@ interned row keys (corro_pk_keys) and checked against the oracle on the same key
 keys map back to the canonical packed pks (corro_pk_bytes). TEXT / BLOB column values have any
 length (SqliteValue, corro-api-types/src/lib.rs:419-429): values longer than 16 bytes go through
 the value arena and compare by their whole bytes."""
+import os
 import numpy as np
 import pytest
 
@@ -292,3 +293,69 @@ def test_intern_table_grows_past_its_probe_bound():
     got = e.pk_bytes("testsblob", first[pick])
     raw = b2.cpu().numpy()
     assert got == [bytes(raw[19 * i:19 * i + 19]) for i in pick.tolist()]
+
+
+def test_intern_ids_follow_first_seen_order():
+    """New keys get ids in first-seen order (cr-sqlite numbers __crsql_key rows in insertion
+    order; the device claims are won by whichever change's CAS lands first, so the ids are ranked by
+    each key's first change instead): over two calls with repeats, non-canonical encodings and keys
+    longer than a slot's inline bytes, a key's id is the table size before the call plus the rank of its
+    first occurrence among the call's new keys -- the same on a fresh engine, run after run."""
+    import torch
+    import corrosion_amd as ca
+    rng = np.random.default_rng(11)
+    pool = [_pack([bytes(rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8))]) for _ in range(5000)]
+    calls = []
+    for _ in range(2):
+        pks = [pool[int(rng.integers(0, len(pool)))] for _ in range(20000)]
+        calls.append([_noncanonical(rng, p) if rng.random() < 0.1 else p for p in pks])
+    want, ids = [], {}
+    for pks in calls:
+        got = []
+        for p in pks:
+            c = _canon(p)
+            if c not in ids:
+                ids[c] = len(ids)
+            got.append(ids[c])
+        want.append(got)
+    for run in range(2):
+        e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12, interned=INTERNED)
+        for pks, w in zip(calls, want):
+            buf = torch.tensor(list(b"".join(pks)), dtype=torch.uint8, device="cuda")
+            off = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pks])]), dtype=torch.int64, device="cuda")
+            keys = e.pk_keys_device("testsblob", buf, off).cpu().numpy().view(np.uint64)
+            assert keys.tolist() == w, run
+        e.close()
+
+
+@pytest.mark.parametrize("fault", ["pk_find", "pk_commit"])
+def test_failed_intern_leaves_the_table_as_it_was(fault):
+    """a call that fails after its probe pass has claimed slots (injected: CORRO_FAULT
+    pk_find before the probe, pk_commit after it) leaves no claim behind -- a retry of the same batch, and
+    a shorter batch whose indices a stale claim would point past, intern exactly as on a fresh table."""
+    import torch
+    import corrosion_amd as ca
+    rng = np.random.default_rng(13)
+    e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12, interned=INTERNED)
+    held = torch.arange(500, device="cuda")
+    bh, oh = synth.blob_pks_torch(held)
+    kh = e.pk_keys_device("testsblob", bh, oh).cpu().numpy().view(np.uint64)
+    ids = torch.tensor(rng.integers(0, 3000, 40000), device="cuda")
+    b, o = synth.blob_pks_torch(ids)
+    os.environ["CORRO_FAULT"] = fault
+    try:
+        with pytest.raises(ca.CorroError):
+            e.pk_keys_device("testsblob", b, o)
+    finally:
+        del os.environ["CORRO_FAULT"]
+    short = synth.blob_pks_torch(ids[:1000])
+    ks = e.pk_keys_device("testsblob", *short).cpu().numpy().view(np.uint64)
+    k = e.pk_keys_device("testsblob", b, o).cpu().numpy().view(np.uint64)
+    f = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12, interned=INTERNED)
+    assert np.array_equal(f.pk_keys_device("testsblob", bh, oh).cpu().numpy().view(np.uint64), kh)
+    assert np.array_equal(f.pk_keys_device("testsblob", *short).cpu().numpy().view(np.uint64), ks)
+    assert np.array_equal(f.pk_keys_device("testsblob", b, o).cpu().numpy().view(np.uint64), k)
+    idn = ids.cpu().numpy()
+    assert all(k[i] == kh[idn[i]] for i in range(len(idn)) if idn[i] < 500)  # held keys keep their ids
+    e.close()
+    f.close()
