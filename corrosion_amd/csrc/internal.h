@@ -96,7 +96,7 @@ struct PkTable {
     DevBuf d_off, d_bytes, d_hash, d_slots;
     uint64_t n = 0, nbytes = 0;             // keys, arena bytes
     uint64_t cap_off = 0, cap_bytes = 0;    // capacities of d_off / d_hash (keys) and d_bytes
-    uint64_t nslots = 0;                    // power of two (0: no table yet)
+    uint64_t nslots = 0;                    // a multiple of 8 (0: no table yet)
     uint64_t max_len = 0;                   // bound on the longest canonical key
 };
 // Device view of one table's interned keys (partition.hip routes and ships interned pks by them).

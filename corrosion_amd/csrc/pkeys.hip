@@ -337,6 +337,7 @@ struct PkArgs {
     uint64_t *cref;     // where its canonical bytes are: input offset, or PK_SCRATCH | scratch offset
     uint64_t *h;        // route hash
     uint32_t *slotix;   // a claimant's slot
+    uint32_t *firstof;  // a claimant's first-seen position (k_pk_mark: read before any commit overwrites the word)
     uint32_t *claims;   // the call's claimants (ctl[4] of them)
     uint32_t *slow;     // changes whose input is not canonical (ctl[2] of them): canonicalised, then probed
     uint32_t *newf;     // at each new key's first-seen position: 1
@@ -349,7 +350,7 @@ struct PkArgs {
     unsigned long long *ctl;
     // the table
     PkSlot *slots;
-    uint64_t smask;
+    uint64_t nsl;       // slots (a multiple of 8, not a power of two: sized for the MALL, see pk_slots_for)
     uint64_t *koff;
     uint8_t *kbytes;
     uint64_t *khash;
@@ -386,7 +387,12 @@ __device__ inline bool pk_eq(const uint8_t *x, const uint8_t *y, uint32_t n) {
     return true;
 }
 
-__device__ inline uint64_t pk_slot_of(uint64_t h, uint64_t mask) { return (h ^ (h >> 31)) & mask; }
+// home slot: the hash's low mixed word scaled to the table size (multiply-high); probes run linearly
+// and wrap at the end
+__device__ inline uint64_t pk_slot_of(uint64_t h, uint64_t nsl) {
+    return ((uint64_t)(uint32_t)(h ^ (h >> 31)) * nsl) >> 32;
+}
+__device__ inline uint64_t pk_next(uint64_t sl, uint64_t nsl) { return sl + 1 == nsl ? 0 : sl + 1; }
 __device__ inline uint32_t pk_tag(uint64_t h) { return (uint32_t)(h >> 32) | 1u; }
 
 // A short key (<= PK_INLINE bytes) as the three words of a slot's bytes 8..31: length, then the bytes,
@@ -395,30 +401,44 @@ __device__ inline uint32_t pk_tag(uint64_t h) { return (uint32_t)(h >> 32) | 1u;
 struct PkWords {
     uint64_t q[3];
 };
+// (round 6: read as the aligned 8-B words that hold the key's bytes -- at most four loads, none of them
+// past the word of the key's last byte -- instead of 23 predicated byte loads)
 __device__ inline PkWords pk_words(const uint8_t *p, uint32_t cl) {
-    uint8_t b[PK_INLINE];
-#pragma unroll
-    for (uint32_t k = 0; k < PK_INLINE; k++) b[k] = k < cl ? p[k] : 0;
-    PkWords w;
+    PkWords w{};
     w.q[0] = cl;
+    if (cl == 0) return w;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint64_t *ap = reinterpret_cast<const uint64_t *>(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7) * 8;
+    const uint32_t nw = (uint32_t)(((a + cl - 1) >> 3) - (a >> 3)) + 1;  // (1..4 words for cl <= 23)
+    uint64_t v[4];
 #pragma unroll
-    for (uint32_t k = 0; k < 7; k++) w.q[0] |= (uint64_t)b[k] << (8 * (k + 1));
-    w.q[1] = w.q[2] = 0;
+    for (uint32_t k = 0; k < 4; k++) v[k] = k < nw ? ap[k] : 0;
+    uint64_t x[3];  // bytes [8k, 8k + 8) of the key, zero past its length
 #pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-        w.q[1] |= (uint64_t)b[7 + k] << (8 * k);
-        w.q[2] |= (uint64_t)b[15 + k] << (8 * k);
+    for (uint32_t k = 0; k < 3; k++) {
+        uint64_t y = v[k] >> sh;
+        if (sh) y |= v[k + 1] << (64 - sh);
+        const uint32_t have = cl > 8 * k ? min(cl - 8 * k, 8u) : 0u;
+        x[k] = have == 8 ? y : (y & ((1ULL << (8 * have)) - 1));
     }
+    w.q[0] = (uint64_t)cl | (x[0] << 8);
+    w.q[1] = (x[0] >> 56) | (x[1] << 8);
+    w.q[2] = (x[1] >> 56) | (x[2] << 8);
     return w;
 }
 __device__ inline bool pk_words_eq(const PkWords &x, const PkWords &y) {
     return x.q[0] == y.q[0] && x.q[1] == y.q[1] && x.q[2] == y.q[2];
 }
 
-// One 32-B slot read as two 16-B plain loads: the claim word and the three inline words. Plain loads
+// One 32-B slot read with plain loads: the claim word and the three inline words. Plain loads
 // are exact here: inside a probe kernel a slot's claim word only goes 0 -> claim (a stale 0 is settled
 // by the CAS that follows it), and committed words were written by an earlier kernel.
 __device__ inline void pk_slot_read(const PkSlot *ps, unsigned long long &w, PkWords &q) {
+    // (two 16-B loads, not four 8-B ones: a probe's lanes all read different lines, and the vector
+    // memory pipeline's cost is per line per load instruction -- 4 x 8-B loads made the warm intern
+    // 4.5 ms even with every slot in a 32-MB, cache-resident corner of the table. A 16-B load reads its
+    // line once, so the 8-B claim word in it is never seen torn.)
     const uint4 *s4 = reinterpret_cast<const uint4 *>(ps);
     const uint4 x0 = s4[0], x1 = s4[1];
     w = (unsigned long long)x0.x | ((unsigned long long)x0.y << 32);
@@ -476,6 +496,9 @@ __device__ inline bool pk_eq_committed(const PkArgs &a, uint32_t id, const PkWor
 // common case: pack_columns output back to back, or a decoded frame) are copied into LDS with 16-B
 // loads along the bytes; lanes then parse from LDS. Larger windows read their bytes from HBM.
 constexpr uint32_t PK_WAVE_STAGE = 2048;
+#ifndef PK_DIAG
+#define PK_DIAG 0  // diagnostic builds: 1 no probe, 2 no canonical parse, 4 no LDS staging
+#endif
 constexpr uint32_t PK_FIND_THREADS = 256;
 
 // k_pk_find: the fused parse + probe (round 6; it replaces a parse kernel that wrote four columns per
@@ -510,7 +533,15 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
                 // (an aligned 16-B chunk holding one byte of the buffer lies in that byte's page)
                 const uint4 *src4 = reinterpret_cast<const uint4 *>(a.r.base + (intptr_t)(a0 - base));
                 for (uint32_t c = lane; (uintptr_t)c * 16 < span; c += 64)
+#if PK_DIAG & 16  // (the streamed bytes non-temporal: the slot table keeps the MALL)
+                {
+                    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                    const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(src4) + c);
+                    *reinterpret_cast<v4u *>(st + 16 * c) = x;
+                }
+#else
                     *reinterpret_cast<uint4 *>(st + 16 * c) = src4[c];
+#endif
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -523,11 +554,20 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
             nbad++;
             if (a.bad) a.bad[i] = 1;
         } else if (src == 1) {
+#if PK_DIAG & 4
+            const uint8_t *p = a.r.base + at;
+#else
             const uint8_t *p = staged ? st + (base + at - a0) : a.r.base + at;
+#endif
             CanonOut<false> co{p, len, nullptr};
             bool one = false;
             int64_t v = 0;
+#if PK_DIAG & 2  // (diagnostic: the hash of the input bytes only, no canonical parse -- canonical inputs)
+            for (uint64_t k = 0; k < len; k++) co.put(p[k]);
+            const bool ok = true;
+#else
             const bool ok = pk_canon_dev<false>(p, len, co, one, v) && co.o < (1ULL << 24);
+#endif
             if (!ok || (!a.interned && !one)) {
                 nbad++;
                 if (a.bad) a.bad[i] = 1;
@@ -542,17 +582,33 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
                     a.clen[i] = cl;
                     a.h[i] = hh;
                     slowb += cl;
+                } else if (PK_DIAG & 1) {  // (diagnostic: no probe, results not valid)
+                    a.keys[i] = hh;
                 } else if (!*(volatile unsigned long long *)&a.ctl[3]) {  // (retrying: seen late is fine)
                     const uint32_t tag = pk_tag(hh);
                     PkWords mw{};
                     if (cl <= PK_INLINE) mw = pk_words(p, cl);
-                    sl = pk_slot_of(hh, a.smask);
+                    sl = pk_slot_of(hh, a.nsl);
+#if PK_DIAG & 40  // (diagnostic, results not valid: ONE slot read, at the home slot (32) or inside the
+                  // first 2^20 slots (8), no compare, no claim)
+                    if (PK_DIAG & 8) sl = pk_slot_of(hh, min(a.nsl, (uint64_t)1 << 20));
+                    {
+                        unsigned long long w;
+                        PkWords q;
+                        pk_slot_read(a.slots + sl, w, q);
+                        a.keys[i] = w ^ q.q[0] ^ mw.q[0];
+                    }
+                    if (true) continue;
+#endif
                     uint64_t res = ~0ULL;
-                    for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = (sl + 1) & a.smask) {
+                    for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = pk_next(sl, a.nsl)) {
                         PkSlot *ps = a.slots + sl;
                         unsigned long long w;
                         PkWords q;
                         pk_slot_read(ps, w, q);
+                        // (a plain read that shows an empty slot may be a stale L2 line -- the claims are
+                        // atomics at the memory side: read the word coherently before paying for a CAS)
+                        if (w == 0) w = __hip_atomic_load(&ps->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         if (w == 0) {
                             const unsigned long long want = ((unsigned long long)tag << 32) | (PK_NEW | (uint32_t)i);
                             w = atomicCAS(&ps->w, 0ULL, want);
@@ -574,7 +630,7 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
                                 eq = cl <= PK_INLINE ? pk_words_eq(pk_words(pj, cl), mw) : pk_eq(pj, p, cl);
                             }
                             if (eq) {
-                                pk_first_seen(ps, (uint32_t)i);
+                                if ((uint32_t)i < j) pk_first_seen(ps, (uint32_t)i);  // (only a change before the claimant can be first)
                                 res = PK_PENDING | j;
                                 break;
                             }
@@ -586,7 +642,11 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
                     if (res == ~0ULL) {
                         atomicOr(&a.ctl[3], 1ULL);  // (the table is too full: the call retries)
                     } else {
+#if PK_DIAG & 16
+                        __builtin_nontemporal_store(res, &a.keys[i]);
+#else
                         a.keys[i] = res;
+#endif
                     }
                 }
             }
@@ -650,13 +710,14 @@ __global__ void __launch_bounds__(256) k_pk_probe_slow(PkArgs a, uint64_t nslow)
             const uint8_t *mine = pk_cbytes(a, i);
             PkWords mw{};
             if (cl <= PK_INLINE) mw = pk_words(mine, cl);
-            sl = pk_slot_of(h, a.smask);
+            sl = pk_slot_of(h, a.nsl);
             uint64_t res = ~0ULL;
-            for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = (sl + 1) & a.smask) {
+            for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = pk_next(sl, a.nsl)) {
                 PkSlot *ps = a.slots + sl;
                 unsigned long long w;
                 PkWords q;
                 pk_slot_read(ps, w, q);
+                if (w == 0) w = __hip_atomic_load(&ps->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (w == 0) {
                     w = atomicCAS(&ps->w, 0ULL, ((unsigned long long)tag << 32) | (PK_NEW | i));
                     if (w == 0) {
@@ -674,7 +735,7 @@ __global__ void __launch_bounds__(256) k_pk_probe_slow(PkArgs a, uint64_t nslow)
                     eq = a.clen[j] == cl && a.h[j] == h;
                     if (eq) eq = cl <= PK_INLINE ? pk_words_eq(pk_words(pk_cbytes(a, j), cl), mw) : pk_eq(pk_cbytes(a, j), mine, cl);
                     if (eq) {
-                        pk_first_seen(ps, i);
+                        if (i < j) pk_first_seen(ps, i);
                         res = PK_PENDING | j;
                         break;
                     }
@@ -703,6 +764,7 @@ __global__ void __launch_bounds__(256) k_pk_mark(PkArgs a, uint64_t nclaims) {
     PK_LIST(k, nclaims) {
         const uint32_t c = a.claims[k];
         const uint32_t f = ~*pk_first_word(a.slots + a.slotix[c]);
+        a.firstof[c] = f;
         a.newf[f] = 1;
         a.newl[f] = a.clen[c];
     }
@@ -723,37 +785,45 @@ __device__ inline void pk_slot_fill(PkSlot &sl, const uint8_t *src, uint32_t cl)
     q[2] = w.q[2];
 }
 
+// per claim: its id (the table size + the rank of its first-seen position), its canonical bytes, offset
+// and hash appended, its slot -> the id and the key's inline words; firstof[c] becomes the id
+__global__ void __launch_bounds__(256) k_pk_newkeys(PkArgs a, uint64_t nclaims) {
+    PK_LIST(k, nclaims) {
+        const uint32_t c = a.claims[k];
+        const uint32_t f = a.firstof[c];
+        const uint32_t id = (uint32_t)a.nkeys + a.rank[f] - 1u;
+        const uint32_t cl = a.clen[c];
+        const uint64_t o = a.nbytes + a.noff[f] - cl;
+        const uint8_t *src = pk_cbytes(a, c);
+        for (uint32_t b = 0; b < cl; b++) a.kbytes[o + b] = src[b];
+        a.koff[id + 1] = o + cl;
+        a.khash[id] = a.h[c];
+        PkSlot &sl = a.slots[a.slotix[c]];
+        pk_slot_fill(sl, src, cl);
+        sl.w = ((unsigned long long)pk_tag(a.h[c]) << 32) | id;
+        a.firstof[c] = id;
+    }
+}
+
+// every change of a new key: keys[i] = its claim's id
 __global__ void __launch_bounds__(256) k_pk_commit(PkArgs a) {
     PK_LIST(i, a.n) {
         const uint64_t key = a.keys[i];
         if (!(key & PK_PENDING)) continue;
         uint64_t at = 0, len = 0;
         if (pk_src(a, i, at, len) != 1 || (a.bad && a.bad[i])) continue;  // (another table's key, or a bad pk)
-        const uint32_t c = (uint32_t)(key & ~PK_PENDING);
-        const uint32_t f = ~*pk_first_word(a.slots + a.slotix[c]);
-        const uint32_t id = (uint32_t)a.nkeys + a.rank[f] - 1u;
-        a.keys[i] = id;
-        if (c != i) continue;
-        const uint32_t cl = a.clen[i];
-        const uint64_t o = a.nbytes + a.noff[f] - cl;
-        const uint8_t *src = pk_cbytes(a, i);
-        for (uint32_t k = 0; k < cl; k++) a.kbytes[o + k] = src[k];
-        a.koff[id + 1] = o + cl;
-        a.khash[id] = a.h[i];
-        PkSlot &sl = a.slots[a.slotix[i]];
-        pk_slot_fill(sl, src, cl);
-        sl.w = ((unsigned long long)pk_tag(a.h[i]) << 32) | id;
+        a.keys[i] = a.firstof[(uint32_t)(key & ~PK_PENDING)];
     }
 }
 
 // the slots rebuilt from the keys (a larger table, a retry after a probe overflow, or the cleanup of a
 // failed call's claims)
-__global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t mask, const uint64_t *khash,
+__global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t nsl, const uint64_t *khash,
                                                    const uint64_t *koff, const uint8_t *kbytes, uint64_t nkeys) {
     for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < nkeys; id += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t h = khash[id];
         const unsigned long long w = ((unsigned long long)pk_tag(h) << 32) | id;
-        for (uint64_t sl = pk_slot_of(h, mask);; sl = (sl + 1) & mask)
+        for (uint64_t sl = pk_slot_of(h, nsl);; sl = pk_next(sl, nsl))
             if (atomicCAS(&slots[sl].w, 0ULL, w) == 0ULL) {
                 pk_slot_fill(slots[sl], kbytes + koff[id], (uint32_t)(koff[id + 1] - koff[id]));
                 break;
@@ -765,16 +835,24 @@ __global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t mask,
 
 dim3 pk_grid(uint64_t n) { return dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 16384))); }
 
-// slots for `want` keys at load <= 1/2 (at least `min_slots`), rebuilt from the arena
+// Slots for `keys` keys at load `num / den`, a multiple of 8 (two 128-B lines), at least 4096. The table
+// is not a power of two (round 6): a config-2-sized table (4.2 M keys) at load 3/4 is 179 MB, which the
+// 256-MiB MALL holds beside the call's streamed bytes, where the round-5 table (load <= 1/2 rounded up
+// to 2^23 slots: 268 MB) missed to HBM on nearly every probe.
+uint64_t pk_slots_for(uint64_t keys, uint64_t num, uint64_t den) {
+    const uint64_t ns = (keys * den + num - 1) / num;
+    return std::max<uint64_t>(4096, (ns + 7) & ~7ULL);
+}
+
+// slots for `want` keys at load <= 3/4 (at least `min_slots`), rebuilt from the arena
 int pk_slots_resize(corro_ctx *ctx, PkTable &t, uint64_t want, uint64_t min_slots = 0) {
-    uint64_t ns = 1ULL << 12;
-    while (ns < 2 * want || ns < min_slots) ns <<= 1;
+    const uint64_t ns = std::max<uint64_t>(pk_slots_for(want, 3, 4), (min_slots + 7) & ~7ULL);
     if (ns >= (1ULL << 32)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
     hipStream_t s = ctx->stream;
     DevBuf nb;
     if (int rc = nb.ensure(ns * sizeof(PkSlot))) return rc;
     CORRO_HIP_TRY(hipMemsetAsync(nb.p, 0, ns * sizeof(PkSlot), s));
-    if (t.n) hipLaunchKernelGGL(k_pk_rehash, pk_grid(t.n), dim3(256), 0, s, nb.as<PkSlot>(), ns - 1,
+    if (t.n) hipLaunchKernelGGL(k_pk_rehash, pk_grid(t.n), dim3(256), 0, s, nb.as<PkSlot>(), ns,
                                 t.d_hash.as<uint64_t>(), t.d_off.as<uint64_t>(), t.d_bytes.as<uint8_t>(), t.n);
     CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipStreamSynchronize(s));
@@ -817,7 +895,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     if (int rc = prim_inclusive_scan_u32_u64(nullptr, &t1, nullptr, nullptr, n, s)) return rc;
     temp = std::max(temp, t1);
     const uint64_t c4 = al(n * 4), c8 = al(n * 8);
-    const uint64_t need = 7 * c4 + 3 * c8 + 256 + al(temp);
+    const uint64_t need = 8 * c4 + 3 * c8 + 256 + al(temp);
     if (int rc = ctx->d_pk_scratch.ensure(need)) return rc;
     uint8_t *base = ctx->d_pk_scratch.as<uint8_t>();
     PkArgs a{};
@@ -835,6 +913,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     };
     a.clen = (uint32_t *)take(c4);
     a.slotix = (uint32_t *)take(c4);
+    a.firstof = (uint32_t *)take(c4);
     a.claims = (uint32_t *)take(c4);
     a.slow = (uint32_t *)take(c4);
     a.newf = (uint32_t *)take(c4);
@@ -847,14 +926,14 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     void *d_temp = take(al(temp));
     if (t.interned) {
         if (t.n + n > ((uint64_t)PK_NEW - 1)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
-        // slots for the held keys and a share of the call's (load <= 1/2); a call that brings more new keys
-        // than that overflows a probe and retries with a table four times larger (rebuilt from the arena).
-        // Sized by keys, not by changes: a warm call (every key held) probes a table sized by its keys.
-        // (load <= 1/2 for the held keys, <= 3/4 with the call's estimated new keys: a sixteenth of its
-        // changes into an empty table, a sixty-fourth into one that holds keys)
+        // slots for the held keys and a share of the call's at load <= 3/4; a call that brings more new
+        // keys than that overflows a probe and retries with a table four times larger (rebuilt from the
+        // arena). Sized by keys, not by changes: a warm call (every key held) probes a table sized by its
+        // keys. (The call's estimated new keys: a sixteenth of its changes into an empty table, a
+        // sixty-fourth into one that holds keys.)
         const uint64_t est_new = std::max<uint64_t>(t.n ? n / 64 : n / 16, 1ULL << 16);
-        const uint64_t want = std::max<uint64_t>(t.n, (t.n + est_new) * 2 / 3);
-        if (t.nslots < 2 * want) TRY_PK(pk_slots_resize(ctx, t, want));
+        const uint64_t want = t.n + est_new;
+        if (t.nslots < pk_slots_for(want, 3, 4)) TRY_PK(pk_slots_resize(ctx, t, want));
         a.koff = t.d_off.as<uint64_t>();
         a.kbytes = t.d_bytes.as<uint8_t>();
         a.khash = t.d_hash.as<uint64_t>();
@@ -880,7 +959,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     DevBuf scratch;  // (non-canonical inputs: their canonical bytes)
     for (int attempt = 0;; attempt++) {
         a.slots = t.d_slots.as<PkSlot>();
-        a.smask = t.nslots ? t.nslots - 1 : 0;
+        a.nsl = t.nslots;
         HIP_PKC(hipMemsetAsync(a.ctl, 0, 64, s));
         if (bad) HIP_PKC(hipMemsetAsync(bad, 0, n, s));
         const uint32_t nwaves = (uint32_t)((n + 63) / 64);
@@ -938,6 +1017,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     a.kbytes = t.d_bytes.as<uint8_t>();
     a.khash = t.d_hash.as<uint64_t>();
     if (fault_armed("pk_commit")) return failc(fail(CORRO_E_DEVICE, "injected fault (CORRO_FAULT): pk_commit"));
+    hipLaunchKernelGGL(k_pk_newkeys, pk_grid(nclaims), dim3(256), 0, s, a, nclaims);
     hipLaunchKernelGGL(k_pk_commit, pk_grid(n), dim3(256), 0, s, a);
     HIP_PKC(hipGetLastError());
     HIP_PKC(hipStreamSynchronize(s));
@@ -945,7 +1025,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     t.nbytes = nbytes;
 #undef TRY_PKC
 #undef HIP_PKC
-    if (2 * t.n > t.nslots) TRY_PK(pk_slots_resize(ctx, t, 2 * t.n));  // (the next call starts at load <= 1/4)
+    if (4 * t.n > 3 * t.nslots) TRY_PK(pk_slots_resize(ctx, t, t.n + t.n / 4));  // (the next call starts at load <= 0.6)
     return CORRO_OK;
 }
 
