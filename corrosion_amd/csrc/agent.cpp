@@ -980,6 +980,31 @@ class HostPool {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         cap_ = v > 0 ? (unsigned)std::min<long>(v, 256) : std::min(16u, hw);
         for (unsigned t = 1; t < cap_; t++) std::thread([this] { loop(); }).detach();
+        warm_heap();  // (this thread's; each worker warms its own before its first wait)
+    }
+    // The first call of a process paid its host threads' first heap growth (the allocator's mmap
+    // threshold starts at 128 KB, so every large per-actor vector was a fresh mmap + page faults that
+    // later calls reuse from the arena: the first mixed call's walk 9.3 vs 3.2 ms,
+    // profiles/r05_agent_cold_first_call.log). Each worker grows its arena once here: one 16-MB block
+    // freed raises its mmap / trim thresholds, then a spread of smaller blocks is touched and freed so
+    // the arena keeps the pages. (CORRO_HEAP_WARM=0 skips it.)
+    static void warm_heap() {
+        const char *e = std::getenv("CORRO_HEAP_WARM");
+        if (e && std::atoi(e) == 0) return;
+        const size_t big = 16u << 20;
+        if (void *p = std::malloc(big)) {
+            std::memset(p, 0, big);
+            std::free(p);
+        }
+        std::vector<void *> blocks;
+        for (size_t sz = 4096, tot = 0; tot < (24u << 20); sz = sz < (1u << 20) ? 2 * sz : 4096) {
+            void *p = std::malloc(sz);
+            if (!p) break;
+            std::memset(p, 0, sz);
+            blocks.push_back(p);
+            tot += sz;
+        }
+        for (void *p : blocks) std::free(p);
     }
     void work(void (*fn)(void *, size_t), void *arg, size_t n) {
         in_pool_ = true;
@@ -993,6 +1018,7 @@ class HostPool {
         in_pool_ = false;
     }
     void loop() {
+        warm_heap();
         uint64_t seen = 0;
         std::unique_lock<std::mutex> g(mu_);
         while (true) {

@@ -1694,6 +1694,32 @@ int agent_dev_commit_headers(corro_ctx *ctx, uint64_t ncs, int32_t *dknown, cons
     return CORRO_OK;
 }
 
+// The pinned host areas a call of `ncs` changesets uses (the per-changeset columns and the staged host
+// headers), allocated ahead of the first call: hipHostMalloc of ~100 MB inside a call doubled the
+// process's first host-header call. corro_ctx_create reserves them from its capacity hint.
+int agent_dev_reserve(corro_ctx *ctx, uint64_t ncs) {
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t n = std::max<uint64_t>(ncs, 1);
+    const size_t c8 = al256(n * 8), c4 = al256(n * 4), c1 = al256(n);
+    const size_t total = 3 * c8 + c4 + 3 * c1 + 8 * 65536;
+    if (total > ctx->h_agent_bytes) {
+        if (ctx->h_agent) (void)hipHostFree(ctx->h_agent);
+        ctx->h_agent = nullptr;
+        ctx->h_agent_bytes = 0;
+        CORRO_HIP_TRY(hipHostMalloc(&ctx->h_agent, total + total / 4, hipHostMallocDefault));
+        ctx->h_agent_bytes = total + total / 4;
+    }
+    const size_t hb = n * sizeof(corro_changeset);
+    if (hb > ctx->h_hdr_bytes) {
+        if (ctx->h_hdr) (void)hipHostFree(ctx->h_hdr);
+        ctx->h_hdr = nullptr;
+        ctx->h_hdr_bytes = 0;
+        CORRO_HIP_TRY(hipHostMalloc(&ctx->h_hdr, hb + hb / 4, hipHostMallocDefault));
+        ctx->h_hdr_bytes = hb + hb / 4;
+    }
+    return CORRO_OK;
+}
+
 int agent_dev_stage_begin(corro_ctx *ctx, uint64_t ncs, HdrStage *st) {
     CORRO_HIP_TRY(hipSetDevice(ctx->device));
     const size_t hb = std::max<uint64_t>(ncs, 1) * sizeof(corro_changeset);

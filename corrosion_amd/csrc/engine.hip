@@ -614,6 +614,8 @@ int corro_ctx_create(const corro_table_desc *tables, uint32_t ntables, uint64_t 
             rc = fail(CORRO_E_DEVICE, "upload of the schema failed");
         if (rc == CORRO_OK) rc = store_clear(ctx);
         if (rc == CORRO_OK) rc = prims_warm(ctx);
+        // (the agent's pinned host areas for a call of the hinted size: ~64 changes per changeset)
+        if (rc == CORRO_OK) rc = agent_dev_reserve(ctx, std::max<uint64_t>(4096, capacity_hint / 64));
         if (rc != CORRO_OK) {
             corro_ctx_destroy(ctx);
             return rc;

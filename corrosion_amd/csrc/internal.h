@@ -135,6 +135,8 @@ std::string pack_int_pk(int64_t v);
 
 // the rocPRIM kernels' first-use cost paid once per process and device (prims.hip)
 int prims_warm(corro_ctx *ctx);
+// the agent's pinned host areas for a call of `ncs` changesets (agent_dev.hip), ahead of the first call
+int agent_dev_reserve(corro_ctx *ctx, uint64_t ncs);
 
 }  // namespace corro
 

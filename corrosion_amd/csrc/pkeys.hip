@@ -453,6 +453,9 @@ __device__ inline void pk_slot_read(const PkSlot *ps, unsigned long long &w, PkW
 // finds the claim (a plain read first: the word only grows, so a read at or above ~i skips the atomic).
 __device__ inline uint32_t *pk_first_word(PkSlot *ps) { return reinterpret_cast<uint32_t *>(ps) + 2; }
 __device__ inline void pk_first_seen(PkSlot *ps, uint32_t i) {
+#if PK_DIAG & 64  // (diagnostic: no first-seen atomics from the finders, ids not first-seen)
+    if (true) return;
+#endif
     uint32_t *f = pk_first_word(ps);
     if (*(volatile uint32_t *)f < ~i) atomicMax(f, ~i);
 }
@@ -608,7 +611,9 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
                         pk_slot_read(ps, w, q);
                         // (a plain read that shows an empty slot may be a stale L2 line -- the claims are
                         // atomics at the memory side: read the word coherently before paying for a CAS)
+#if !(PK_DIAG & 128)
                         if (w == 0) w = __hip_atomic_load(&ps->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
                         if (w == 0) {
                             const unsigned long long want = ((unsigned long long)tag << 32) | (PK_NEW | (uint32_t)i);
                             w = atomicCAS(&ps->w, 0ULL, want);
@@ -659,7 +664,7 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
             a.h[i] = hh;
             a.cref[i] = at;
             a.slotix[i] = (uint32_t)sl;
-            pk_first_seen(a.slots + sl, (uint32_t)i);
+            atomicMax(pk_first_word(a.slots + sl), ~(uint32_t)i);  // (its own: always, the finders' only below it)
         }
         const uint32_t sk = pk_wave_append(&a.ctl[2], slow);
         if (slow) a.slow[sk] = (uint32_t)i;
@@ -753,7 +758,7 @@ __global__ void __launch_bounds__(256) k_pk_probe_slow(PkArgs a, uint64_t nslow)
         if (claimed) {
             a.claims[ck] = i;
             a.slotix[i] = (uint32_t)sl;
-            pk_first_seen(a.slots + sl, i);
+            atomicMax(pk_first_word(a.slots + sl), ~i);
         }
     }
 }
