@@ -1595,6 +1595,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     // leaves the bookie as it was).
     CommitPrep prep;
     std::string prep_err;
+    int prep_rc = CORRO_OK;
     bool prep_started = false;
     std::thread prep_thread;
     if (nh >= 4096) {
@@ -1610,9 +1611,14 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             };
             try {
                 commit_prepare(ctx, bk, have_dv, sto, ntables, prep, markp);
+            } catch (const std::bad_alloc &) {  // (same code as the serial path's host OOM)
+                prep_rc = CORRO_E_NOMEM;
+                prep_err = "host allocation failed preparing the commit";
             } catch (const std::exception &e) {
+                prep_rc = CORRO_E_INVALID;
                 prep_err = e.what();
             } catch (...) {
+                prep_rc = CORRO_E_INVALID;
                 prep_err = "unknown host exception";
             }
         });
@@ -1661,7 +1667,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     }
     if (prep_started) {
         prep_thread.join();
-        if (!prep_err.empty()) return fail(CORRO_E_INVALID, "process_multiple_changes: " + prep_err);
+        if (prep_rc != CORRO_OK) return fail(prep_rc, "process_multiple_changes: " + prep_err);
         if (prof) prof_line += " [prepared alongside the merge:" + prep.prof + "]";
     }
     TRY_RC(commit_staged(ctx, bk, nchanges ? &dv : nullptr, sto, committed, stage, prep_started ? &prep : nullptr));

@@ -153,6 +153,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     void *d_temp = nullptr;
     size_t temp = 0;
     uint32_t nt = 0, *cs_first = nullptr;
+    uint8_t *rowblk = nullptr;
     CsAgg *cs_agg = nullptr, *cs_incl = nullptr;
     const uint64_t K = Kmax, R = std::max<uint64_t>(Kb, 1);
     for (int pass = 0; pass < 2; pass++) {
@@ -176,7 +177,7 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
         uint32_t **rows[] = {&d.rowner, &d.rb, &d.rheap, &d.rprior, &d.rpoff};
         for (uint32_t **p : rows) *p = (uint32_t *)take(R * 4);
         d.rbits = (uint64_t *)take(R * 16);
-        d.rw1 = (uint64_t *)take(R * 12 + 64);  // row summaries, laid out once the row count is known
+        rowblk = take(R * 20 + 64);  // row summaries, laid out once the row count is known
         d.cbk = (uint32_t *)take((Kb / 64 + 2) * 32);
         if (pass == 0 && K <= ctx->ovf_temp_k) {
             temp = ctx->ovf_temp;  // (rocPRIM's temp sizes grow with n; the 64-bit sort bounds the others)
@@ -221,9 +222,30 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     const bool rimp_fits = kbits + 3 + cid_bits + pbits <= 64;
     d.reduce = ovf_reduce_ok(ctx, a.impact != nullptr) && (!a.impact || rimp_fits) ? 1u : 0u;
     d.rimp = d.reduce && a.impact ? 1u : 0u;
+    static const bool split = !std::getenv("CORRO_OVF_SPLIT") || std::atoi(std::getenv("CORRO_OVF_SPLIT")) != 0;
+    // fused plain form (OvfDev::fuse; CORRO_OVF_FUSE=0: the separate summary pass, A/B runs)
+    static const bool no_fuse = std::getenv("CORRO_OVF_FUSE") && std::atoi(std::getenv("CORRO_OVF_FUSE")) == 0;
+    d.fuse = d.reduce && !d.rimp && split && !no_fuse ? 1u : 0u;
+    if (d.fuse) {
+        // summaries by owner record: zero between applies (each walk clears its rows' words); a fresh
+        // area, or one an apply left before its walk (an error return), is cleared here
+        void *const was = ctx->d_ovf_sum.p;
+        const size_t was_bytes = ctx->d_ovf_sum.bytes;  // (a regrown area may come back at the same address)
+        TRY(ctx->d_ovf_sum.ensure(Kb * sizeof(OvfSum) + 256));
+        if (ctx->d_ovf_sum.p != was || ctx->d_ovf_sum.bytes != was_bytes || ctx->ovf_sum_dirty)
+            CORRO_HIP_TRY(hipMemsetAsync(ctx->d_ovf_sum.p, 0, ctx->d_ovf_sum.bytes, s));
+        ctx->ovf_sum_dirty = true;  // (until this apply's walk has run)
+        d.osum = ctx->d_ovf_sum.as<OvfSum>();
+        d.cstride = ctx->max_stride;
+        d.obits = 1;
+        while ((1ULL << d.obits) < Kb) d.obits++;
+    }
     hp("h2d");
     hipLaunchKernelGGL(k_ovf_chunkmap, grid_for((Kb + 63) / 64), blk, 0, s, a, d);
-    hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
+    if (d.fuse)
+        hipLaunchKernelGGL(k_ovf_loadsum, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)), dim3(RS_T), 0, s, a, d);
+    else
+        hipLaunchKernelGGL(k_ovf_loadhash, gridb, blk, 0, s, a, d);
     TRY(launched());
     // dense row ids: the row count sizes the sort's key
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.recf, d.epc, d.Kb, s));
@@ -234,8 +256,19 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     const uint32_t nrows = hw[0];
     d.nrows = nrows;
     d.rshift = pbits;
-    {
-        uint8_t *blk = (uint8_t *)d.rw1;
+    if (d.fuse) {  // (summaries by owner record: the per-row block holds the counters)
+        d.nkeep = (uint32_t *)rowblk;
+        CORRO_HIP_TRY(hipMemsetAsync(d.nkeep, 0, 16, s));
+        TRY(ctx->d_ovf_rcl.ensure((uint64_t)nrows * 4 * 7 + 256));
+        d.rsum = ctx->d_ovf_rcl.as<uint64_t>();
+        d.rowE = reinterpret_cast<uint32_t *>(d.rsum + nrows);
+        d.rlist = d.rowE + nrows;
+        d.flist = d.rlist + nrows;
+        d.rhb = d.flist + nrows;
+        d.rclw = d.rhb + nrows;
+    } else {
+        uint8_t *blk = rowblk;
+        d.rw1 = (uint64_t *)blk;
         d.rw2 = (uint32_t *)(blk + 8ULL * nrows);
         d.nkeep = (uint32_t *)(blk + 12ULL * nrows);
         if (d.reduce) CORRO_HIP_TRY(hipMemsetAsync(blk, 0, 12ULL * nrows + 8, s));
@@ -248,10 +281,12 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     }
     // every row looked up in its region; prior records counted, new rows counted per bucket (and
     // every batch record's sort key)
-    static const bool split = !std::getenv("CORRO_OVF_SPLIT") || std::atoi(std::getenv("CORRO_OVF_SPLIT")) != 0;
     d.split = split ? 1u : 0u;
-    hipLaunchKernelGGL(d.rimp ? k_ovf_lookup<true> : k_ovf_lookup<false>, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)),
-                       dim3(RS_T), 0, s, a, d);
+    if (d.fuse)
+        hipLaunchKernelGGL(k_ovf_owners, gridb, blk, 0, s, a, d);
+    else
+        hipLaunchKernelGGL(d.rimp ? k_ovf_lookup<true> : k_ovf_lookup<false>, dim3((uint32_t)((Kb + RS_CHUNK - 1) / RS_CHUNK)),
+                           dim3(RS_T), 0, s, a, d);
     if (split) hipLaunchKernelGGL(k_ovf_rlook, grid_for(nrows), blk, 0, s, a, d);
     TRY(launched());
     TRY(prim_inclusive_scan_u32(d_temp, &temp, d.rprior, d.rpoff, nrows, s));
@@ -290,15 +325,48 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     if (d.reduce) {
         // rows reduced to their last epoch's records (k_ovf_lookup's comment); the rest sort as before
         const uint32_t kcap = d.K;
-        hipLaunchKernelGGL(k_ovf_keep, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK), dim3(KEEP_T), 0, s, a, d, kcap);
+        hipLaunchKernelGGL(d.fuse ? k_ovf_keep<true> : k_ovf_keep<false>, dim3((d.K + KEEP_CHUNK - 1) / KEEP_CHUNK),
+                           dim3(KEEP_T), 0, s, a, d, kcap);
         TRY(launched());
         CORRO_HIP_TRY(hipMemcpyAsync(&hw[4], d.nkeep, 8, hipMemcpyDeviceToHost, s));
         hp("enq4");
         CORRO_HIP_TRY(hipStreamSynchronize(s));
         hp("wait4");
-        const uint32_t kept = hw[4], ndc = d.rimp ? hw[5] : 0u;
-        if (kept == 0 || kept + ndc > kcap) return fail(CORRO_E_DEVICE, "internal: overflow row reduction kept no records");
-        if (dbg) fprintf(stderr, "[corro ovf] row reduction keeps %u of %u records (%u dropped candidates)\n", kept, d.K, ndc);
+        const uint32_t kept = hw[4], ndc = d.rimp ? hw[5] : 0u, nc = d.fuse ? hw[5] : 0u;
+        if ((kept == 0 && !d.fuse) || (uint64_t)kept + ndc + nc > kcap)
+            return fail(CORRO_E_DEVICE, "internal: overflow row reduction kept no records");
+        if (dbg)
+            fprintf(stderr, "[corro ovf] row reduction keeps %u of %u records (%u dropped candidates, %u reduced rows' cell records)\n",
+                    kept, d.K, ndc, nc);
+        if (nc) {
+            // fused form: the reduced rows' cells -- sorted by (owner record, cid), each cell's winner by the
+            // argmax scan with the position as the last tie-break -- before the kept records' sort
+            // reuses key_s / val_s / qkey / cbest
+            TRY(ovf_sort_pairs(d_temp, &temp, d.ckey + (kcap - nc), d.key_s, d.cval + (kcap - nc), d.val_s, nc,
+                               d.obits + cid_bits, s));
+            const dim3 rgrid = grid_for(nc);
+            hipLaunchKernelGGL(k_ovf_rgather, rgrid, blk, 0, s, a, d, nc, d.pb);
+            TRY(launched());
+            OvfDev dd = d;
+            dd.ckey_s = d.key_s;
+            dd.K = nc;
+            dd.qpos = d.pb;
+            const uint32_t ntc = (nc + CS_TILE - 1) / CS_TILE;  // <= nt
+            hipLaunchKernelGGL(k_cscan_tile<true>, dim3(ntc), dim3(CS_T), 0, s, dd, cs_agg, cs_first);
+            TRY(launched());
+            TRY(ovf_scan_tiles(d_temp, &temp, dd, cs_agg, cs_incl, ntc, s));
+            hipLaunchKernelGGL(k_cscan_fix<true>, dim3(ntc), dim3(CS_T), 0, s, dd, cs_incl, cs_first);
+            TRY(launched());
+        }
+        // the reduced rows written now (their sentinels and slots, then their cells, one lane per cell),
+        // while the cell sort's results are in key_s / val_s / cbest; the other rows' pipeline below
+        // reads no heap or region word these write
+        if (d.fuse) {
+            void (*const walk1)(MergeArgs, OvfDev) = ctx->max_stride <= WALK_MAXC ? k_ovf_walk<true, 1> : k_ovf_walk<false, 1>;
+            hipLaunchKernelGGL(walk1, grid_for(nrows), blk, 0, s, a, d);
+            if (nc) hipLaunchKernelGGL(k_ovf_rcells, grid_for(nc), blk, 0, s, a, d, nc);
+            TRY(launched());
+        }
         if (ndc) {
             // dropped candidates (impact form): sorted by (row, slot, cid, position), running argmax by
             // group with the candidate scan's kernels, then their flags -- all before the kept records'
@@ -312,18 +380,20 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
             dd.ckey_s = d.key;
             dd.K = ndc;
             const uint32_t ntc = (ndc + CS_TILE - 1) / CS_TILE;  // <= nt
-            hipLaunchKernelGGL(k_cscan_tile, dim3(ntc), dim3(CS_T), 0, s, dd, cs_agg, cs_first);
+            hipLaunchKernelGGL(k_cscan_tile<false>, dim3(ntc), dim3(CS_T), 0, s, dd, cs_agg, cs_first);
             TRY(launched());
             TRY(ovf_scan_tiles(d_temp, &temp, dd, cs_agg, cs_incl, ntc, s));
-            hipLaunchKernelGGL(k_cscan_fix, dim3(ntc), dim3(CS_T), 0, s, dd, cs_incl, cs_first);
+            hipLaunchKernelGGL(k_cscan_fix<false>, dim3(ntc), dim3(CS_T), 0, s, dd, cs_incl, cs_first);
             hipLaunchKernelGGL(k_ovf_dimp, dgrid, blk, 0, s, a, d, ndc, d.key, d.val_s, d.qkey, d.cbest);
             TRY(launched());
         }
         d.K = kept;
-        TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.key_s, d.cval, d.val_s, d.K, key_bits, s));
+        if (kept) TRY(ovf_sort_pairs(d_temp, &temp, d.ckey, d.key_s, d.cval, d.val_s, d.K, key_bits, s));
     } else {
         TRY(ovf_sort_pairs(d_temp, &temp, d.key, d.key_s, d.val, d.val_s, d.K, key_bits, s));
     }
+    d.ncand = 0;
+    if (d.K) {  // (fused form: none when every row reduced)
     const dim3 grid = grid_for(d.K);
     hipLaunchKernelGGL(k_ovf_gather, grid, blk, 0, s, d);
     TRY(launched());
@@ -352,24 +422,33 @@ static int run_overflow(corro_ctx *ctx, MergeArgs &a, uint64_t novf, uint64_t nb
     TRY(launched());
     if (ncand) {
         const uint32_t ntc = (ncand + CS_TILE - 1) / CS_TILE;  // <= nt
-        hipLaunchKernelGGL(k_cscan_tile, dim3(ntc), dim3(CS_T), 0, s, d, cs_agg, cs_first);
+        hipLaunchKernelGGL(k_cscan_tile<false>, dim3(ntc), dim3(CS_T), 0, s, d, cs_agg, cs_first);
         TRY(launched());
         TRY(ovf_scan_tiles(d_temp, &temp, d, cs_agg, cs_incl, ntc, s));
-        hipLaunchKernelGGL(k_cscan_fix, dim3(ntc), dim3(CS_T), 0, s, d, cs_incl, cs_first);
+        hipLaunchKernelGGL(k_cscan_fix<false>, dim3(ntc), dim3(CS_T), 0, s, d, cs_incl, cs_first);
     }
     TRY(launched());
     if (ncand && a.impact) TRY(ovf_scans(d_temp, &temp, d, 2, s));  // (group starts: impacts only)
     hipLaunchKernelGGL(k_ovf_link, cgrid, blk, 0, s, d);
+    }
     // carried cells in registers when no table has WALK_MAXC or more columns (cids 1..ncols)
-    auto walk = ctx->max_stride <= WALK_MAXC ? k_ovf_walk<true> : k_ovf_walk<false>;
-    hipLaunchKernelGGL(walk, grid_for(nrows), blk, 0, s, a, d);
-    if (a.impact) hipLaunchKernelGGL(k_ovf_impacts, cgrid, blk, 0, s, a, d);
+    const bool wreg = ctx->max_stride <= WALK_MAXC;
+    using WalkK = void (*)(MergeArgs, OvfDev);
+    const WalkK walk0 = wreg ? k_ovf_walk<true, 0> : k_ovf_walk<false, 0>;
+    const WalkK walk2 = wreg ? k_ovf_walk<true, 2> : k_ovf_walk<false, 2>;
+    if (d.fuse) {  // the rows that are not reduced (the reduced ones were written after the cell scan)
+        hipLaunchKernelGGL(walk2, grid_for(nrows), blk, 0, s, a, d);
+    } else {
+        hipLaunchKernelGGL(walk0, grid_for(nrows), blk, 0, s, a, d);
+    }
+    if (a.impact && d.ncand) hipLaunchKernelGGL(k_ovf_impacts, grid_for(d.ncand), blk, 0, s, a, d);
     hipLaunchKernelGGL(k_ovf_finish, grid_for(novf), blk, 0, s, a, d);
     TRY(launched());
     hp("enq6");
     if (hostprof) fprintf(stderr, "[corro ovf host us]%s\n", hp_line.c_str());
     if (prof) (void)hipEventRecord(ctx->ev[7], s);
     CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (d.fuse) ctx->ovf_sum_dirty = false;  // (the walk cleared every row's summary words)
     if (prof) CORRO_HIP_TRY(hipEventElapsedTime(&ctx->last_ms[5], ctx->ev[6], ctx->ev[7]));
     return CORRO_OK;
 }
@@ -632,7 +711,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
                       &ctx->d_heap, &ctx->d_heap_ts, &ctx->d_heap_top, &ctx->d_stride, &ctx->d_defer,
                       &ctx->d_relist, &ctx->d_dense, &ctx->d_dense_ts, &ctx->d_dense_view, &ctx->d_in,
                       &ctx->d_hist, &ctx->d_new_cnt, &ctx->d_stage_off, &ctx->d_bflags, &ctx->d_stage,
-                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_fast_of, &ctx->d_ovf_sort, &ctx->d_ovf_rcl, &ctx->d_ovf_plan, &ctx->d_setdbv,
+                      &ctx->d_misc, &ctx->d_ovf_list, &ctx->d_gen_list, &ctx->d_wide_list, &ctx->d_fast_of, &ctx->d_ovf_sort, &ctx->d_ovf_rcl, &ctx->d_ovf_sum, &ctx->d_ovf_plan, &ctx->d_setdbv,
                       &ctx->d_scan_tmp, &ctx->d_impact, &ctx->d_export, &ctx->d_needs, &ctx->d_needs1,
                       &ctx->d_xidx, &ctx->d_xout, &ctx->d_wire, &ctx->d_wire_schema, &ctx->d_wire_sites,
                       &ctx->d_ncols, &ctx->d_part, &ctx->d_arena, &ctx->d_aff, &ctx->d_affflag,

@@ -217,6 +217,8 @@ struct corro_ctx {
     corro::DevBuf d_fast_of;      // k_triage: per merged bucket, 1 = INTEGER fast body
     corro::DevBuf d_ovf_sort;     // overflow path: its device-wide arrays, offsets, rocPRIM temp
     corro::DevBuf d_ovf_rcl;      // overflow path, impact form of the row reduction: per-row cl slots
+    corro::DevBuf d_ovf_sum;      // overflow path, fused plain form: row summaries by owner record (zero between applies)
+    bool ovf_sum_dirty = false;   // d_ovf_sum may hold words of an apply that failed before its walk cleared them
     corro::DevBuf d_ovf_plan;     // overflow path: bucket offsets, row-table slices, totals (k_ovf_plan)
     uint64_t ovf_temp_k = 0;      // overflow path: the record count its cached rocPRIM temp size was queried for
     size_t ovf_temp = 0;

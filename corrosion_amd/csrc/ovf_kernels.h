@@ -66,6 +66,14 @@ struct alignas(16) OvfKey {
     uint32_t m, sr;
 };
 
+// a row's summary words by its owner record (the fused form; one 32-B line: k_ovf_keep<true> reads
+// them, and the row's dense id, with two 16-B loads)
+struct alignas(32) OvfSum {
+    unsigned long long w1, w3;  // rs_comb's word; Mx << 32 | ~(first compact position at Mx)
+    uint32_t w2, row;           // cids | outside App. A.3; the dense row (k_ovf_owners)
+    uint32_t pad[2];
+};
+
 struct OvfDev {
     uint32_t G, K;              // oversized buckets, their records (batch + prior)
     uint32_t Kb;                // batch records [0, Kb); prior records [Kb, K)
@@ -115,6 +123,23 @@ struct OvfDev {
     uint32_t split;              // 1: the rows' region lookups run in k_ovf_rlook (one lane per row)
     uint64_t *rcl;               // [nrows * OVF_NCL]
     uint32_t *rclr;              // [nrows * OVF_NCL]
+    // fused plain form (fuse = 1: row reduction without impacts). The summaries are built in the
+    // pass that loads the records and finds their row owners, keyed by the owner record's index
+    // (dense rows are not known yet): osum is a persistent [Kb] area that is zero between applies
+    // (the walks clear each row's words after use). w3 = Mx << 32 | ~(first compact position at Mx)
+    // (max monoid): the epoch record of a reduced row. Reduced rows then go around the
+    // (row, position) sort: their column records at Mx are sorted by (owner record, cid) only and each
+    // cell's winner is an argmax with the position as the last tie-break (earliest wins), so their
+    // order in the sort does not matter.
+    uint32_t fuse;
+    OvfSum *osum;                // [Kb] (fuse; rs_put writes here when set)
+    uint32_t obits;              // (fuse) bits of an owner record index: the cell key is owner << cid_bits | cid
+    uint32_t *rlist, *flist;     // [nrows] reduced rows / the others (k_ovf_keep<true>), counts at nkeep[2..3]
+    uint64_t *rsum;              // [nrows] a reduced row's Mx << 32 | cids (fuse)
+    uint32_t *rowE;              // [nrows] a reduced row's epoch record (fuse)
+    uint32_t *rhb, *rclw;        // [nrows] a reduced row's heap slot and clock-row cl (k_ovf_walk mode 1, for k_ovf_rcells)
+    uint32_t cstride;
+    const uint32_t *qpos;        // argmax tie-break positions, by sorted index (fuse; nullptr: order decides)
 };
 
 // a record's 64-B source: the staged batch change or the prior heap record
@@ -321,63 +346,68 @@ __device__ inline ChunkB ovf_chunk_of(const MergeArgs &a, const OvfDev &d, uint3
     return ovf_chunk_words(a, d, b);
 }
 
-// Record fields and row owners in one pass: each batch record's fields are loaded from its staged
-// 64-B record and the record is hashed into its bucket's row table (open addressing per bucket, a
-// slot read before it is claimed); an occupied slot's row key is compared with the claimant's staged
-// record (read-only in this kernel, so no ordering against the claimant's own field writes).
-static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
+// A batch record's row owner (the bucket-local index of the row's first claimant): open addressing
+// per bucket, a slot read before it is claimed; an occupied slot's row key is compared with the
+// claimant's staged record (read-only while owners are found, so no ordering against the claimant's
+// own field writes). Called by every lane of the wave (`todo`: the lane has a record).
+__device__ inline uint32_t ovf_find_owner(const MergeArgs &a, const OvfDev &d, bool todo, uint32_t r, const ChunkB &cb,
+                                          uint64_t pk, uint32_t t) {
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t kb = cb.kb, sbase = cb.sbase, S = cb.S;
+    uint32_t *slots = d.slots + cb.soff;
+    auto probe = [&]() -> uint32_t {
+        uint32_t slot = row_hash(pk, t) & (S - 1);
+        while (true) {
+            // a plain read first: a claimed slot is only read afterwards
+            uint32_t o = slots[slot];
+            if (o == 0) o = atomicCAS(&slots[slot], 0u, r - kb + 1);
+            if (o == 0) return r - kb;
+            const Rec *q = a.stage + sbase + (o - 1);
+            if (q->pk == pk && (q->tcid >> 16) == t) return o - 1;
+            slot = (slot + 1) & (S - 1);
+        }
+    };
+    // A Zipf-hot row fills whole waves, and all of its lanes start at once: every one of them
+    // would read the unclaimed slot and CAS it, a chain of serialised same-address atomics
+    // as long as the row. Lanes of one wave that share a row let one leader probe for them.
+    uint32_t owner = 0;
+    for (int round = 0; round < 2; round++) {
+        const uint64_t act = __ballot(todo);
+        if (!act) break;
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint64_t lpk = __shfl(pk, leader);
+        const uint32_t lt = __shfl(t, leader);
+        const bool mine = todo && pk == lpk && t == lt;
+        if (__popcll(__ballot(mine)) < 8) break;  // (wave-uniform) not a hot row
+        uint32_t o = 0;
+        if ((int)lane == leader) o = probe();
+        o = __shfl(o, leader);
+        if (mine) {
+            owner = o;
+            todo = false;
+        }
+    }
+    if (todo) owner = probe();
+    return owner;
+}
+
+// Record fields and row owners in one pass: each batch record's fields are loaded from its staged
+// 64-B record and the record is hashed into its bucket's row table (ovf_find_owner).
+static __global__ void k_ovf_loadhash(MergeArgs a, OvfDev d) {
     OVF_LOOP(r, d.Kb) {
         const ChunkB cb = ovf_chunk_of(a, d, r);
-        const uint32_t kb = cb.kb, sbase = cb.sbase;
-        const uint32_t si = sbase + (r - kb);
+        const uint32_t kb = cb.kb;
+        const uint32_t si = cb.sbase + (r - kb);
         const Rec x = load_rec(a.stage + si);
         d.src[r] = si;
         d.cv[r] = x.cv;
         d.tc[r] = x.tcid;
         d.cl[r] = x.cl;
         d.pos[r] = x.pos;
-        const uint32_t S = cb.S;
-        uint32_t *slots = d.slots + cb.soff;
-        const uint64_t pk = x.pk;
-        const uint32_t t = x.tcid >> 16;
-        auto probe = [&]() -> uint32_t {
-            uint32_t slot = row_hash(pk, t) & (S - 1);
-            while (true) {
-                // a plain read first: a claimed slot is only read afterwards
-                uint32_t o = slots[slot];
-                if (o == 0) o = atomicCAS(&slots[slot], 0u, r - kb + 1);
-                if (o == 0) return r - kb;
-                const Rec *q = a.stage + sbase + (o - 1);
-                if (q->pk == pk && (q->tcid >> 16) == t) return o - 1;
-                slot = (slot + 1) & (S - 1);
-            }
-        };
-        // A Zipf-hot row fills whole waves, and all of its lanes start at once: every one of them
-        // would read the unclaimed slot and CAS it, a chain of serialised same-address atomics
-        // as long as the row. Lanes of one wave that share a row let one leader probe for them.
-        bool todo = true;
-        uint32_t owner = 0;
-        for (int round = 0; round < 2; round++) {
-            const uint64_t act = __ballot(todo);
-            if (!act) break;
-            const int leader = __ffsll((unsigned long long)act) - 1;
-            const uint64_t lpk = __shfl(pk, leader);
-            const uint32_t lt = __shfl(t, leader);
-            const bool mine = todo && pk == lpk && t == lt;
-            if (__popcll(__ballot(mine)) < 8) break;  // (wave-uniform) not a hot row
-            uint32_t o = 0;
-            if ((int)lane == leader) o = probe();
-            o = __shfl(o, leader);
-            if (mine) {
-                owner = o;
-                todo = false;
-            }
-        }
-        if (todo) owner = probe();
+        const uint32_t owner = ovf_find_owner(a, d, true, r, cb, x.pk, x.tcid >> 16);
         d.rowid[r] = kb + owner;  // the owner's record (scratch until the sort)
         d.recf[r] = owner == r - kb ? 1u : 0u;
-        if (owner == r - kb) d.pk[r] = pk;  // (only a row's owner is asked for its pk)
+        if (owner == r - kb) d.pk[r] = x.pk;  // (only a row's owner is asked for its pk)
         if (!d.reduce) d.val[r] = r;  // (the reduction's compaction writes the sort values)
     }
 }
@@ -421,16 +451,23 @@ __device__ inline uint64_t rs_comb(uint64_t x, uint64_t y) {
     return ((uint64_t)m << 32) | ((mx == m ? (uint32_t)x : 0u) | (my == m ? (uint32_t)y : 0u));
 }
 
-__device__ inline void rs_put(const OvfDev &d, uint32_t row, uint64_t w1, uint32_t w2) {
-    unsigned long long *p = (unsigned long long *)&d.rw1[row];
-    unsigned long long cur = ovf_ld_dev(&d.rw1[row]);
+__device__ inline void rs_put(const OvfDev &d, uint32_t row, uint64_t w1, uint32_t w2, uint64_t w3 = 0) {
+    OvfSum *const S = d.osum ? d.osum + row : nullptr;  // (fused form: by owner record)
+    unsigned long long *p = S ? &S->w1 : (unsigned long long *)&d.rw1[row];
+    uint32_t *const p2 = S ? &S->w2 : &d.rw2[row];
+    unsigned long long cur = ovf_ld_dev(p);
     for (unsigned long long want = rs_comb(cur, w1); want != cur; want = rs_comb(cur, w1)) {
         const unsigned long long o = atomicCAS(p, cur, want);
         if (o == cur) break;
         cur = o;
     }
-    if (w2 & ~ovf_ld_dev(&d.rw2[row])) atomicOr(&d.rw2[row], w2);
+    if (w2 & ~ovf_ld_dev(p2)) atomicOr(p2, w2);
+    if (S && w3 > ovf_ld_dev(&S->w3)) atomicMax(&S->w3, (unsigned long long)w3);
 }
+
+// fused form: a record's epoch term, cl << 32 | ~(compact position) (max: the largest cl, then the
+// earliest position at it)
+__device__ inline uint64_t rs_w3(uint32_t cl, uint32_t p) { return ((uint64_t)cl << 32) | (uint32_t)~p; }
 
 // a record's terms
 // (impact form: a batch column change with col_version <= 0 also keeps its row whole -- a carried,
@@ -533,20 +570,26 @@ __device__ inline void rcl_wave_add(RclLds &L, const OvfDev &d, bool todo, uint3
 #define OVF_RS_BITS 10
 #endif
 constexpr uint32_t RS_T = 256, RS_E = OVF_RS_E, RS_CHUNK = RS_T * RS_E, RS_HT = 1u << OVF_RS_BITS;
-struct RsLds {
+template <bool W3>
+struct RsLdsT {
     uint32_t key[RS_HT], w2[RS_HT];  // key: row + 1 (0: free)
     unsigned long long w1[RS_HT];
+    unsigned long long w3[W3 ? RS_HT : 1];  // (fused form only)
 };
+using RsLds = RsLdsT<false>;
 
-__device__ inline void rs_lds_clear(RsLds &L) {
+template <bool W3>
+__device__ inline void rs_lds_clear(RsLdsT<W3> &L) {
     for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x) {
         L.key[i] = 0;
         L.w2[i] = 0;
         L.w1[i] = 0;
+        if constexpr (W3) L.w3[i] = 0;
     }
 }
 
-__device__ inline bool rs_lds_add(RsLds &L, uint32_t row, uint64_t w1, uint32_t w2) {
+template <bool W3>
+__device__ inline bool rs_lds_add(RsLdsT<W3> &L, uint32_t row, uint64_t w1, uint32_t w2, uint64_t w3 = 0) {
     const uint32_t h = (row * 2654435761u) >> (32 - OVF_RS_BITS);
     for (uint32_t k = 0; k < 16; k++) {
         const uint32_t sl = (h + k) & (RS_HT - 1);
@@ -559,14 +602,16 @@ __device__ inline bool rs_lds_add(RsLds &L, uint32_t row, uint64_t w1, uint32_t 
             cur = q;
         }
         if (w2) atomicOr(&L.w2[sl], w2);
+        if constexpr (W3) atomicMax(&L.w3[sl], (unsigned long long)w3);
         return true;
     }
     return false;
 }
 
-__device__ inline void rs_lds_flush(const RsLds &L, const OvfDev &d) {
+template <bool W3>
+__device__ inline void rs_lds_flush(const RsLdsT<W3> &L, const OvfDev &d) {
     for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x)
-        if (L.key[i]) rs_put(d, L.key[i] - 1, L.w1[i], L.w2[i]);
+        if (L.key[i]) rs_put(d, L.key[i] - 1, L.w1[i], L.w2[i], W3 ? L.w3[W3 ? i : 0] : 0ULL);
 }
 
 __device__ inline uint32_t wave_or32(uint32_t x) {
@@ -584,7 +629,18 @@ __device__ inline uint32_t wave_max32(uint32_t x) {
 // One term per `todo` lane (called by every lane of the wave): lanes sharing the first active lane's
 // row -- a Zipf-hot row fills whole waves -- are combined across the wave and added by that lane (at
 // most two rounds), the rest add their own; LDS first, the global words when the table has no slot.
-__device__ inline void rs_wave_add(RsLds &L, const OvfDev &d, bool todo, uint32_t row, uint64_t w1, uint32_t w2) {
+__device__ inline uint64_t wave_max64(uint64_t x) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_xor(x, o);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+template <bool W3>
+__device__ inline void rs_wave_add(RsLdsT<W3> &L, const OvfDev &d, bool todo, uint32_t row, uint64_t w1, uint32_t w2,
+                                   uint64_t w3 = 0) {
     const uint32_t lane = threadIdx.x & 63;
     for (int round = 0; round < 2; round++) {
         const uint64_t act = __ballot(todo);
@@ -596,12 +652,69 @@ __device__ inline void rs_wave_add(RsLds &L, const OvfDev &d, bool todo, uint32_
         const uint32_t m = wave_max32(mine ? (uint32_t)(w1 >> 32) : 0u);
         const uint32_t f = wave_or32(mine && (uint32_t)(w1 >> 32) == m ? (uint32_t)w1 : 0u);
         const uint32_t c = wave_or32(mine ? w2 : 0u);
+        const uint64_t x3 = W3 ? wave_max64(mine ? w3 : 0ULL) : 0ULL;
         const uint64_t x1 = ((uint64_t)m << 32) | f;
-        if ((int)lane == leader && !rs_lds_add(L, lrow, x1, c)) rs_put(d, lrow, x1, c);
+        if ((int)lane == leader && !rs_lds_add(L, lrow, x1, c, x3)) rs_put(d, lrow, x1, c, x3);
         if (mine) todo = false;
     }
-    if (todo && !rs_lds_add(L, row, w1, w2)) rs_put(d, row, w1, w2);
+    if (todo && !rs_lds_add(L, row, w1, w2, w3)) rs_put(d, row, w1, w2, w3);
 }
+
+// Fused plain form (d.fuse): the same pass also folds every record's summary terms (rs_terms, rs_w3)
+// into its row's words, keyed by the owner record -- per wave, then per workgroup in LDS, then once
+// into HBM, as k_ovf_lookup does by dense row. That pass then has nothing left to do: its sort keys
+// are written by k_ovf_keep<true> for the records it keeps, and the rows' owners by k_ovf_owners.
+static __global__ void __launch_bounds__(RS_T) k_ovf_loadsum(MergeArgs a, OvfDev d) {
+    __shared__ RsLdsT<true> L;
+    const OvfDev &od = d;
+    rs_lds_clear(L);
+    __syncthreads();
+    const uint32_t c0 = blockIdx.x * RS_CHUNK;
+    for (uint32_t j = 0; j < RS_E; j++) {  // (wave-uniform: owners and summaries reduce across the wave)
+        const uint32_t r = c0 + j * RS_T + threadIdx.x;
+        const bool valid = r < d.Kb;
+        ChunkB cb{};
+        Rec x{};
+        if (valid) {
+            cb = ovf_chunk_of(a, d, r);
+            const uint32_t si = cb.sbase + (r - cb.kb);
+            x = load_rec(a.stage + si);
+            d.src[r] = si;
+            d.cv[r] = x.cv;
+            d.tc[r] = x.tcid;
+            d.cl[r] = x.cl;
+            d.pos[r] = x.pos;
+        }
+        const uint32_t owner = ovf_find_owner(a, d, valid, r, cb, x.pk, x.tcid >> 16);
+        const uint32_t o = cb.kb + owner;
+        uint64_t w1 = 0, w3 = 0;
+        uint32_t w2 = 0;
+        if (valid) {
+            d.rowid[r] = o;  // the owner's record (k_ovf_keep<true> reads its summary there)
+            d.recf[r] = o == r ? 1u : 0u;
+            if (o == r) d.pk[r] = x.pk;
+            rs_terms(a, x.tcid & 0xFFFFu, x.cl, x.cv, x.pos, w1, w2);
+            w3 = rs_w3(x.cl, d.pm + (x.pos & 0x7FFFFFFFu));
+        }
+        rs_wave_add(L, od, valid, o, w1, w2, w3);
+    }
+    __syncthreads();
+    rs_lds_flush(L, od);
+}
+
+// fused form: each row's owner record and bucket (k_ovf_lookup's part for owners)
+static __global__ void k_ovf_owners(MergeArgs a, OvfDev d) {
+    OVF_LOOP(r, d.Kb) {
+        if (!d.recf[r]) continue;
+        const uint32_t row = d.epc[r] - 1u;
+        uint32_t b = d.cbk[8 * (r >> 6)];
+        while (d.koff[b + 1] <= r) b++;
+        d.rowner[row] = r;
+        d.rb[row] = b;
+        d.osum[r].row = row;
+    }
+}
+
 
 // (RIMP: the impact form's causal-length slots too; its LDS table only in that instantiation, so the
 // plain form keeps its occupancy)
@@ -751,11 +864,13 @@ static __global__ void k_ovf_pload(MergeArgs a, OvfDev d) {
                 d.key[r] = ((uint64_t)row << d.rshift) | c;
                 d.val[r] = r;
                 if (d.reduce) {
-                    d.rowid[r] = row;
+                    // (fused form: summaries and rowid by the row's owner record, as for the batch)
+                    const uint32_t sk = d.fuse ? d.rowner[row] : row;
+                    d.rowid[r] = sk;
                     uint64_t w1;
                     uint32_t w2;
                     rs_terms(a, pr.tcid & 0xFFFFu, pr.cl, pr.cv, c, w1, w2);
-                    rs_put(d, row, w1, w2);
+                    rs_put(d, sk, w1, w2, rs_w3(pr.cl, c));
                     if (d.rimp) rcl_put(d, row, pr.cl, c);
                 }
                 r++;
@@ -812,17 +927,61 @@ __device__ inline void ovf_drop_class(const MergeArgs &a, const OvfDev &d, uint3
 #define OVF_KEEP_E 32  // records per thread (<= 32: one bit each in a lane's masks)
 #endif
 constexpr uint32_t KEEP_T = 256, KEEP_E = OVF_KEEP_E, KEEP_CHUNK = KEEP_T * KEEP_E;
+// FUSE (the fused plain form, d.fuse): summaries are read at the owner record (rowid[r]) and the
+// sort keys are made here -- a kept record of a row that is not reduced gets (row, position); a
+// reduced row keeps nothing for the (row, position) sort: its epoch record (the first at Mx, rw3)
+// goes to rowE and lists the row for the reduced walk, and its column records at an odd Mx are
+// compacted from the END with the cell key (owner record, cid) for the cell sort (their winners:
+// k_cscan_*<true>, k_ovf_rcells); a row that is not reduced is listed for the walk by its owner
+// record. Only those records look up the dense row (epc): the rest read two words.
+template <bool FUSE>
 static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(MergeArgs a, OvfDev d, uint32_t kcap) {
-    __shared__ uint32_t s_cnt[KEEP_T / 64], s_base, s_dcnt[KEEP_T / 64], s_dbase;
+    __shared__ uint32_t s_cnt[KEEP_T / 64], s_base, s_dcnt[KEEP_T / 64], s_dbase, s_ecnt[KEEP_T / 64], s_ebase,
+        s_fcnt[KEEP_T / 64], s_fbase;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = d.K;
     const uint32_t c0 = blockIdx.x * KEEP_CHUNK;
     uint32_t mine = 0, cnt = 0;  // lane's kept bits per step; the wave's kept count
     uint32_t dmine = 0, dcnt = 0;  // (impact form) the same for dropped candidates
+    uint32_t emine = 0, ecnt = 0;  // (fused form) the same for the reduced rows' epoch records
+    uint32_t fmine = 0, fcnt = 0;  // (fused form) and for the other rows' owner records
 #pragma unroll 4
     for (uint32_t j = 0; j < KEEP_E; j++) {
         const uint32_t r = c0 + j * KEEP_T + threadIdx.x;
         bool keep = false, cand = false;
-        if (r < n) {
+        bool isE = false, isF = false;
+        if (FUSE && r < n) {
+            // (every load unconditional: two dependent levels, batched over the unrolled steps)
+            const uint32_t o = d.rowid[r], cl = d.cl[r], pos = d.pos[r], tcr = d.tc[r];
+            const uint4 *sp = reinterpret_cast<const uint4 *>(d.osum + o);
+            const uint4 s0 = sp[0], s1 = sp[1];
+            const uint64_t w1 = ((uint64_t)s0.y << 32) | s0.x, w3 = ((uint64_t)s0.w << 32) | s0.z;
+            const uint32_t w2 = s1.x, eo = s1.y + 1u;
+            const uint32_t mx = (uint32_t)(w1 >> 32);
+            const bool red = !(w2 & 1u) && (!(mx & 1u) || (uint32_t)w1 == w2);
+            const uint32_t p = r < d.Kb ? d.pm + (pos & 0x7FFFFFFFu) : pos;
+            if (!red) {
+                keep = true;
+                const uint32_t row = eo - 1u;
+                d.key[r] = ((uint64_t)row << d.rshift) | p;  // (its own slot, copied by the compaction)
+                if (o == r) {  // the owner lists the row for the walk
+                    d.rowid[r] = row;  // (its own slot: the list write below reads it back)
+                    isF = true;
+                }
+            } else if (cl == mx) {
+                if ((uint32_t)~(uint32_t)w3 == p) {
+                    const uint32_t row = eo - 1u;
+                    d.rowE[row] = r;
+                    d.rsum[row] = ((uint64_t)mx << 32) | w2;
+                    d.rowid[r] = row;  // (its own slot: the list write below reads it back)
+                    isE = true;
+                }
+                const uint32_t cid = tcr & 0xFFFFu;
+                if ((mx & 1u) && cid != 0) {
+                    cand = true;
+                    d.key[r] = ((uint64_t)o << d.cid_bits) | cid;
+                }
+            }
+        } else if (r < n) {
             const uint32_t row = d.rowid[r], cl = d.cl[r], w2 = d.rw2[row];
             const uint64_t w1 = d.rw1[row];
             const uint32_t mx = (uint32_t)(w1 >> 32);
@@ -834,6 +993,12 @@ static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(MergeArgs a, OvfDev 
                 if (cand) d.key[r] = dk;  // (its own slot, read by nothing else: the compaction copies it)
             }
         }
+        if (FUSE) {
+            emine |= isE ? 1u << j : 0u;
+            ecnt += (uint32_t)__popcll(__ballot(isE));
+            fmine |= isF ? 1u << j : 0u;
+            fcnt += (uint32_t)__popcll(__ballot(isF));
+        }
         mine |= keep ? 1u << j : 0u;
         cnt += (uint32_t)__popcll(__ballot(keep));
         dmine |= cand ? 1u << j : 0u;
@@ -842,23 +1007,45 @@ static __global__ void __launch_bounds__(KEEP_T) k_ovf_keep(MergeArgs a, OvfDev 
     if (lane == 0) {
         s_cnt[w] = cnt;
         s_dcnt[w] = dcnt;
+        s_ecnt[w] = ecnt;
+        s_fcnt[w] = fcnt;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0, u = 0;
+        uint32_t t = 0, u = 0, e = 0, f = 0;
         for (uint32_t v = 0; v < KEEP_T / 64; v++) {
             t += s_cnt[v];
             u += s_dcnt[v];
+            e += s_ecnt[v];
+            f += s_fcnt[v];
         }
         s_base = t ? atomicAdd(d.nkeep, t) : 0u;
         s_dbase = u ? atomicAdd(d.nkeep + 1, u) : 0u;
+        if (FUSE) {
+            s_ebase = e ? atomicAdd(d.nkeep + 2, e) : 0u;
+            s_fbase = f ? atomicAdd(d.nkeep + 3, f) : 0u;
+        }
     }
     __syncthreads();
-    uint32_t o = s_base, od = s_dbase;
+    uint32_t o = s_base, od = s_dbase, oe = FUSE ? s_ebase : 0u, of = FUSE ? s_fbase : 0u;
     for (uint32_t v = 0; v < w; v++) {
         o += s_cnt[v];
         od += s_dcnt[v];
+        oe += s_ecnt[v];
+        of += s_fcnt[v];
     }
+    if (FUSE && (ecnt | fcnt))  // the rows' lists (k_ovf_walk modes 1 and 2)
+        for (uint32_t j = 0; j < KEEP_E; j++) {
+            const bool e = (emine >> j) & 1u, f = (fmine >> j) & 1u;
+            const uint64_t m = __ballot(e), mf = __ballot(f);
+            if (e || f) {
+                const uint32_t row = d.rowid[c0 + j * KEEP_T + threadIdx.x];
+                if (e) d.rlist[oe + (uint32_t)__popcll(m & ((1ULL << lane) - 1))] = row;
+                else d.flist[of + (uint32_t)__popcll(mf & ((1ULL << lane) - 1))] = row;
+            }
+            oe += (uint32_t)__popcll(m);
+            of += (uint32_t)__popcll(mf);
+        }
     for (uint32_t j = 0; j < KEEP_E; j++) {
         const bool keep = (mine >> j) & 1u;
         const uint64_t m = __ballot(keep);
@@ -1117,13 +1304,14 @@ struct OvfEmit {
     }
 };
 
-// clock rows of one walked row (rf_emit on the carried cells) into its heap slot; returns them
-template <bool REG>
-__device__ inline uint32_t ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t row, const WalkCells<REG> &cells_,
-                                uint32_t ncell, uint32_t rpos) {
-    const uint32_t xr = d.val_s[rpos];
+// clock rows of one walked row (rf_emit on the carried cells) into its heap slot; returns them.
+// xr: the row's last epoch record, L: the running max of cl before it; cell c's record is
+// cx(c, z) (z: the cell was carried through a resurrection, col_version zeroed)
+template <class CellX>
+__device__ inline uint32_t ovf_emit_x(const MergeArgs &a, const OvfDev &d, uint32_t row, uint32_t xr, uint32_t L,
+                                      uint32_t ncell, const CellX &cx) {
     const uint32_t clr = d.cl[xr], cidr = d.tc[xr] & 0xFFFFu;
-    const bool hs = !(cidr != 0 && clr == 1 && d.lx[rpos] == 0);
+    const bool hs = !(cidr != 0 && clr == 1 && L == 0);
     const int64_t scv = cidr == 0 ? d.cv[xr] : (int64_t)clr;
     const int64_t rowcl = hs ? scv : 1;
     const bool cells = (clr & 1u) != 0;
@@ -1150,11 +1338,13 @@ __device__ inline uint32_t ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_
     }
     if (cells) {
         for (uint32_t c = 0; c < ncell; c++) {
-            Rec r = load_rec(ovf_rec(a, d, d.val_s[cells_.pos(c)]));
+            uint32_t z = 0;
+            const uint32_t x = cx(c, z);
+            Rec r = load_rec(ovf_rec(a, d, x));
             const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
             rec_clear_ts(a, r);
             const uint32_t cid = r.tcid & 0xFFFFu;
-            if (cells_.z(c)) r.cv = 0;
+            if (z) r.cv = 0;
             r.cl = (uint32_t)rowcl;
             r.pos = hb + cid;
             store_rec(a.rs.heap + hb + cid, r);
@@ -1167,21 +1357,87 @@ __device__ inline uint32_t ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_
     return cnt;
 }
 
+template <bool REG>
+__device__ inline uint32_t ovf_emit(const MergeArgs &a, const OvfDev &d, uint32_t row, const WalkCells<REG> &cells_,
+                                    uint32_t ncell, uint32_t rpos) {
+    return ovf_emit_x(a, d, row, d.val_s[rpos], d.lx[rpos], ncell, [&](uint32_t c, uint32_t &z) {
+        z = cells_.z(c);
+        return d.val_s[cells_.pos(c)];
+    });
+}
+
+// fused form, a reduced row: its epoch record (rowE; nothing before it at a causal length > 0, so
+// L = 0) gives the sentinel and the row's causal length, and at an odd Mx the row holds one cell per
+// cid of C (all changed at Mx: C == F). Here: the row's heap slot and region entry, the sentinel and
+// the presence bits; the cells themselves are written by k_ovf_rcells, one lane per cell, from the
+// slot and cl left in rhb / rclw (a row's cells are independent stores: no per-row chain of loads).
+__device__ inline uint32_t ovf_emit_redhead(const MergeArgs &a, const OvfDev &d, uint32_t row, uint32_t C) {
+    const uint32_t xr = d.rowE[row];
+    const uint32_t clr = d.cl[xr], cidr = d.tc[xr] & 0xFFFFu;
+    const bool hs = !(cidr != 0 && clr == 1);
+    const int64_t scv = cidr == 0 ? d.cv[xr] : (int64_t)clr;
+    const int64_t rowcl = hs ? scv : 1;
+    const uint32_t cids = (clr & 1u) ? (C & ~1u) : 0u;  // (cids < 32: reduction only runs below 32 columns)
+    const uint32_t cnt = (hs ? 1u : 0u) + (uint32_t)__popc(cids);
+    if (cnt == 0) return 0;
+    uint32_t hb;
+    const uint32_t e = ovf_row_slot(a, d, row, hb);
+    uint64_t bits[2] = {(uint64_t)cids | (hs ? 1ULL : 0ULL), 0ULL};
+    if (hs) {
+        const OvfView v{&a, &d};
+        Rec r = load_rec(ovf_rec(a, d, xr));
+        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+        r.tcid &= 0xFFFF0000u;
+        r.cv = scv;
+        r.cl = (uint32_t)rowcl;
+        r.v0 = 0;
+        r.v1 = 0;
+        r.meta = CORRO_NULL;
+        r.pos = hb;
+        store_rec(a.rs.heap + hb, r);
+        if (a.track_ts) a.rs.heap_ts[hb] = ts;
+    }
+    d.rhb[row] = hb;
+    d.rclw[row] = (uint32_t)rowcl;
+    ovf_publish(a, d, row, e, bits, cnt, hs);  // (a long winner value marks the region in k_ovf_rcells)
+    return cnt;
+}
+
 #ifndef OVF_WALK_WAVES
 #define OVF_WALK_WAVES 4  // 6 or 8 (spilling) measured no faster on config 5
 #endif
-template <bool REG>
+// mode 0: every row (dense ids); fused form: 1 the reduced rows (rlist), 2 the others (flist) -- in
+// separate launches, so no wave runs both the reduced emission and the walk
+template <bool REG, int mode>
 static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeArgs a, OvfDev d) {
     const uint32_t lane = threadIdx.x & 63, stride = gridDim.x * blockDim.x;
+    const uint32_t nr = mode == 0 ? d.nrows : d.nkeep[mode + 1];
+    const uint32_t *const list = mode == 1 ? d.rlist : d.flist;
     uint32_t live = 0;  // clock rows written (one atomic per wave at the end)
-    // one thread per row (dense ids), every lane busy; wave-uniform loop for the heap requests
-    for (uint32_t r0 = blockIdx.x * blockDim.x + threadIdx.x - lane; r0 < d.nrows; r0 += stride) {
-        const uint32_t row = r0 + lane;
+    // one thread per row, every lane busy; wave-uniform loop for the heap requests
+    for (uint32_t r0 = blockIdx.x * blockDim.x + threadIdx.x - lane; r0 < nr; r0 += stride) {
+        const bool inr = r0 + lane < nr;
+        const uint32_t row = !inr ? d.nrows : (mode == 0 ? r0 + lane : list[r0 + lane]);
+        // fused form: a reduced row's summary (k_ovf_keep<true>); the owner record's words cleared for
+        // the next apply (this row's last use of them)
+        const bool red = mode == 1 && inr;
+        uint32_t rmx = 0, rC = 0;
+        if (red) {
+            const uint64_t w = d.rsum[row];
+            rmx = (uint32_t)(w >> 32);
+            rC = (uint32_t)w;
+        }
+        if (mode != 0 && inr) {
+            const uint32_t o = d.rowner[row];
+            uint4 *sp = reinterpret_cast<uint4 *>(d.osum + o);
+            sp[0] = make_uint4(0u, 0u, 0u, 0u);
+            sp[1] = make_uint4(0u, 0u, 0u, 0u);
+        }
         {  // the wave's new rows take their heap records in one request (the host made room). Rows of
            // the sequential fold (rbad) may emit nothing: they allocate only when they emit.
             uint32_t need = 0;
             const bool fresh = row < d.nrows && d.rheap[row] == ROW_NONE;
-            if (fresh && !d.rbad[row]) need = a.rs.stride[d.tc[d.rowner[row]] >> 16];
+            if (fresh && (red || !d.rbad[row])) need = a.rs.stride[d.tc[d.rowner[row]] >> 16];
             else if (fresh) d.rprior[row] = ROW_NONE;
             uint32_t incl = need;
 #pragma unroll
@@ -1196,6 +1452,10 @@ static __global__ void __launch_bounds__(256, OVF_WALK_WAVES) k_ovf_walk(MergeAr
             if (need) d.rprior[row] = (uint32_t)base + incl - need;
         }
         if (row >= d.nrows) continue;
+        if constexpr (mode == 1) {  // (a row whose every record has cl 0 has no record and emits nothing, as below)
+            if (rmx) live += ovf_emit_redhead(a, d, row, rC);
+            continue;
+        }
         const uint32_t j0 = d.rstart[row];
         if (d.rbad[row]) {  // outside App. A.3: the sequential fold over the row's sorted records
             if (a.impact)  // (k_ovf_classify flagged its records before the row was known to be bad;
@@ -1305,18 +1565,26 @@ struct CsAgg {
     uint32_t best;  // running argmax of the last group (~0u: none)
 };
 
-// x precedes y; ~0u = none. The later one only when strictly greater (earliest on ties).
-__device__ inline uint32_t cs_pick(const OvfKey *qk, uint32_t x, uint32_t y, const uint8_t *arena) {
+// a beats b: strictly greater, or (pos: the fused form's cells, whose sort order is not the
+// application order) equal and earlier
+__device__ inline bool cs_beats(const OvfKey &a, uint32_t ap, const OvfKey &b, uint32_t bp, const uint8_t *arena, bool pos) {
+    const int c = ovf_kcmp(a, b, arena);
+    return c > 0 || (pos && c == 0 && ap < bp);
+}
+
+// x precedes y; ~0u = none. The later one only when it beats the earlier (earliest on ties).
+__device__ inline uint32_t cs_pick(const OvfKey *qk, const uint32_t *qp, uint32_t x, uint32_t y, const uint8_t *arena) {
     if (x == ~0u) return y;
     if (y == ~0u) return x;
-    return ovf_kcmp(qk[y], qk[x], arena) > 0 ? y : x;
+    return cs_beats(qk[y], qp ? qp[y] : 0u, qk[x], qp ? qp[x] : 0u, arena, qp != nullptr) ? y : x;
 }
 
 struct CsComb {
     const OvfKey *qk;
     const uint8_t *arena;
+    const uint32_t *qp;  // (nullptr: order decides ties)
     __device__ inline CsAgg operator()(const CsAgg &a, const CsAgg &b) const {
-        return b.head ? b : CsAgg{a.head, cs_pick(qk, a.best, b.best, arena)};
+        return b.head ? b : CsAgg{a.head, cs_pick(qk, qp, a.best, b.best, arena)};
     }
 };
 
@@ -1340,9 +1608,11 @@ __device__ inline OvfKey shfl_key(const OvfKey &k, int src) {
     return r;
 }
 
+template <bool POS>
 static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tagg, uint32_t *tfirst) {
-    __shared__ uint32_t s_head[CS_W], s_best[CS_W], s_first[CS_W];
+    __shared__ uint32_t s_head[CS_W], s_best[CS_W], s_first[CS_W], s_pos[CS_W];
     __shared__ OvfKey s_key[CS_W];
+    const uint32_t *const qp = POS ? d.qpos : nullptr;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t t0 = blockIdx.x * CS_TILE, base = t0 + w * (CS_C * 64);
     if (d.ckey_s[t0] == ~0ULL) {  // the non-candidates' key sorts last: no cbest is read there
@@ -1354,48 +1624,54 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tag
     }
     uint32_t res[CS_C];
     bool open[CS_C];
-    uint32_t ch = 0, cb = ~0u, first = CS_C * 64;  // wave carry: head seen, best; first head offset
+    uint32_t ch = 0, cb = ~0u, cp = 0, first = CS_C * 64;  // wave carry: head seen, best (+ its position); first head offset
     OvfKey ck{};
 #pragma unroll
     for (uint32_t c = 0; c < CS_C; c++) {
         const uint32_t q = base + c * 64 + lane;
         const bool valid = q < d.K;
-        uint32_t h = 0, b = ~0u;
+        uint32_t h = 0, b = ~0u, kp = 0;
         OvfKey k{};
         if (valid) {
             const uint64_t kk = d.ckey_s[q];
             h = (q == 0 || d.ckey_s[q - 1] != kk) ? 1u : 0u;
             b = q;
             k = d.qkey[q];
+            if (POS) kp = qp[q];
         }
         const uint64_t hb = __ballot(h != 0);
         if (hb && first == CS_C * 64) first = c * 64 + (uint32_t)(__ffsll((unsigned long long)hb) - 1);
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t lh = __shfl_up(h, off), lb = __shfl_up(b, off);
+            const uint32_t lp = POS ? (uint32_t)__shfl_up(kp, off) : 0u;
             const OvfKey lk = shfl_up_key(k, off);
             if ((int)lane >= off && !h) {
                 h = lh;
-                if (lb != ~0u && (b == ~0u || !(ovf_kcmp(k, lk, d.arena) > 0))) {
+                if (lb != ~0u && (b == ~0u || !cs_beats(k, kp, lk, lp, d.arena, POS))) {
                     b = lb;
                     k = lk;
+                    kp = lp;
                 }
             }
         }
-        if (!h && cb != ~0u && (b == ~0u || !(ovf_kcmp(k, ck, d.arena) > 0))) {
+        if (!h && cb != ~0u && (b == ~0u || !cs_beats(k, kp, ck, cp, d.arena, POS))) {
             b = cb;
             k = ck;
+            kp = cp;
         }
         res[c] = b;
         open[c] = !h && !ch;
         ch |= __shfl(h, 63);
         cb = __shfl(b, 63);
+        if (POS) cp = __shfl(kp, 63);
         ck = shfl_key(k, 63);
     }
     if (lane == 0) {
         s_head[w] = ch;
         s_best[w] = cb;
         s_key[w] = ck;
+        s_pos[w] = cp;
         s_first[w] = w * (CS_C * 64) + first;
     }
     __syncthreads();
@@ -1403,13 +1679,15 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tag
     uint32_t pb = ~0u;
     for (uint32_t v = 0; v < w; v++) {
         if (s_head[v]) pb = s_best[v];
-        else if (s_best[v] != ~0u && (pb == ~0u || ovf_kcmp(s_key[v], d.qkey[pb], d.arena) > 0)) pb = s_best[v];
+        else if (s_best[v] != ~0u &&
+                 (pb == ~0u || cs_beats(s_key[v], s_pos[v], d.qkey[pb], POS ? qp[pb] : 0u, d.arena, POS)))
+            pb = s_best[v];
     }
 #pragma unroll
     for (uint32_t c = 0; c < CS_C; c++) {
         const uint32_t q = base + c * 64 + lane;
         if (q >= d.K) continue;
-        d.cbest[q] = open[c] ? cs_pick(d.qkey, pb, res[c], d.arena) : res[c];
+        d.cbest[q] = open[c] ? cs_pick(d.qkey, qp, pb, res[c], d.arena) : res[c];
     }
     if (threadIdx.x == 0) {
         CsAgg agg{0u, ~0u};
@@ -1420,7 +1698,7 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tag
                 agg.best = s_best[v];
                 if (f == CS_TILE) f = s_first[v];
             } else {
-                agg.best = cs_pick(d.qkey, agg.best, s_best[v], d.arena);
+                agg.best = cs_pick(d.qkey, qp, agg.best, s_best[v], d.arena);
             }
         }
         tagg[blockIdx.x] = agg;
@@ -1429,6 +1707,7 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_tile(OvfDev d, CsAgg *tag
 }
 
 // tincl: inclusive scan of the tile aggregates; tile t's leading open group takes tincl[t - 1]
+template <bool POS>
 static __global__ void __launch_bounds__(CS_T) k_cscan_fix(OvfDev d, const CsAgg *tincl, const uint32_t *tfirst) {
     const uint32_t t = blockIdx.x;
     if (t == 0) return;
@@ -1436,7 +1715,38 @@ static __global__ void __launch_bounds__(CS_T) k_cscan_fix(OvfDev d, const CsAgg
     const uint32_t t0 = t * CS_TILE;
     if (c == ~0u || d.ckey_s[t0] == ~0ULL) return;
     const uint32_t e = min(d.K, t0 + tfirst[t]);
-    for (uint32_t q = t0 + threadIdx.x; q < e; q += CS_T) d.cbest[q] = cs_pick(d.qkey, c, d.cbest[q], d.arena);
+    for (uint32_t q = t0 + threadIdx.x; q < e; q += CS_T) d.cbest[q] = cs_pick(d.qkey, POS ? d.qpos : nullptr, c, d.cbest[q], d.arena);
+}
+
+// fused form: the reduced rows' column records at Mx sorted by cell key (owner << cid_bits | cid) in
+// (key_s, val_s): their cell keys and positions in sorted order for the argmax
+static __global__ void k_ovf_rgather(MergeArgs a, OvfDev d, uint32_t nc, uint32_t *qpos) {
+    OVF_LOOP(q, nc) {
+        const uint32_t x = d.val_s[q];
+        d.qkey[q] = ovf_key_x(a, d, x);
+        qpos[q] = d.pos[x];  // (prior records' slots < BATCH_POS | batch index: application order)
+    }
+}
+
+// each reduced cell's winner (the running argmax at its last sorted record) written to its heap slot
+// (after k_ovf_walk mode 1 gave the row its slot and cl; one lane per cell)
+static __global__ void k_ovf_rcells(MergeArgs a, OvfDev d, uint32_t nc) {
+    OVF_LOOP(q, nc) {
+        const uint64_t k = d.key_s[q];
+        if (q + 1 < nc && d.key_s[q + 1] == k) continue;
+        const uint32_t o = (uint32_t)(k >> d.cid_bits), row = d.epc[o] - 1u;
+        const uint32_t hb = d.rhb[row];
+        Rec r = load_rec(ovf_rec(a, d, d.val_s[d.cbest[q]]));
+        const OvfView v{&a, &d};
+        const uint64_t ts = a.track_ts ? rec_ts(a, v, r) : 0ULL;
+        rec_clear_ts(a, r);
+        const uint32_t cid = r.tcid & 0xFFFFu;
+        r.cl = d.rclw[row];
+        r.pos = hb + cid;
+        store_rec(a.rs.heap + hb + cid, r);
+        if (a.track_ts) a.rs.heap_ts[hb + cid] = ts;
+        if (is_long(r.meta)) a.rs.gen[a.ovf_list[d.rb[row]]] = 1;
+    }
 }
 
 #undef OVF_LOOP

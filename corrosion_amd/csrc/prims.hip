@@ -107,7 +107,7 @@ int ovf_scans(void *temp, size_t *temp_bytes, const OvfDev &d, int which, hipStr
 // inclusive segmented scan of the candidate argmax's tile aggregates (k_cscan_tile)
 int ovf_scan_tiles(void *temp, size_t *temp_bytes, const OvfDev &d, const CsAgg *in, CsAgg *out, uint32_t n,
                    hipStream_t s) {
-    const hipError_t e = rocprim::inclusive_scan(temp, *temp_bytes, in, out, (size_t)n, CsComb{d.qkey, d.arena}, s);
+    const hipError_t e = rocprim::inclusive_scan(temp, *temp_bytes, in, out, (size_t)n, CsComb{d.qkey, d.arena, d.qpos}, s);
     if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("tile scan: ") + hipGetErrorString(e));
     return CORRO_OK;
 }
