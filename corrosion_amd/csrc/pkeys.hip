@@ -338,7 +338,9 @@ struct PkArgs {
     uint64_t *h;        // route hash
     uint32_t *slotix;   // a claimant's slot
     uint32_t *firstof;  // a claimant's first-seen position (k_pk_mark: read before any commit overwrites the word)
-    uint32_t *claims;   // the call's claimants (ctl[4] of them)
+    // (the claimants are not listed: one same-address append per wave of a cold call -- a million of them
+    // at config 2 -- serialised at the memory side for ~20 ms; k_pk_mark / k_pk_newkeys find them by
+    // keys[i] == PENDING | i in one streaming pass instead)
     uint32_t *slow;     // changes whose input is not canonical (ctl[2] of them): canonicalised, then probed
     uint32_t *newf;     // at each new key's first-seen position: 1
     uint32_t *newl;     // at each new key's first-seen position: its canonical length
@@ -517,7 +519,7 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t *st = s_st[wv];
     const uint64_t wstride = (uint64_t)gridDim.x * (PK_FIND_THREADS / 64) * 64;
-    uint32_t nbad = 0, mx = 0;
+    uint32_t nbad = 0, mx = 0, nclaim = 0;  // (nclaim: wave-uniform)
     unsigned long long slowb = 0;
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.r.base);
     for (uint64_t w0 = ((uint64_t)blockIdx.x * (PK_FIND_THREADS / 64) + wv) * 64; w0 < a.n; w0 += wstride) {
@@ -656,10 +658,9 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
                 }
             }
         }
-        // claimants and slow changes listed (one atomic per wave each)
-        const uint32_t ck = pk_wave_append(&a.ctl[4], claimed);
+        // claimants counted (one atomic per wave at the end), slow changes listed (rare)
+        nclaim += (uint32_t)__popcll(__ballot(claimed));
         if (claimed) {
-            a.claims[ck] = (uint32_t)i;
             a.clen[i] = cl;
             a.h[i] = hh;
             a.cref[i] = at;
@@ -674,6 +675,7 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) slowb += (unsigned long long)__shfl_xor(slowb, o);
     if ((threadIdx.x & 63) == 0) {
+        if (nclaim) atomicAdd(&a.ctl[4], (unsigned long long)nclaim);
         if (nbad) atomicAdd(&a.ctl[0], (unsigned long long)nbad);
         if (mx) atomicMax(&a.ctl[1], (unsigned long long)mx);
         if (slowb) atomicAdd(&a.ctl[5], slowb);
@@ -754,9 +756,10 @@ __global__ void __launch_bounds__(256) k_pk_probe_slow(PkArgs a, uint64_t nslow)
             else
                 a.keys[i] = res;
         }
-        const uint32_t ck = pk_wave_append(&a.ctl[4], claimed);
+        const uint32_t nc = (uint32_t)__popcll(__ballot(claimed));  // (rare: the slow path's claims)
+        if (nc && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)__ballot(claimed)) - 1))
+            atomicAdd(&a.ctl[4], (unsigned long long)nc);
         if (claimed) {
-            a.claims[ck] = i;
             a.slotix[i] = (uint32_t)sl;
             atomicMax(pk_first_word(a.slots + sl), ~i);
         }
@@ -765,9 +768,16 @@ __global__ void __launch_bounds__(256) k_pk_probe_slow(PkArgs a, uint64_t nslow)
 
 // each claim's first-seen position gets its new-key flag and length (the scans then number the new keys
 // in first-seen order)
-__global__ void __launch_bounds__(256) k_pk_mark(PkArgs a, uint64_t nclaims) {
-    PK_LIST(k, nclaims) {
-        const uint32_t c = a.claims[k];
+// a change that claimed a slot for a new key (keys[c] == PENDING | c, of this table, well formed)
+__device__ inline bool pk_is_claimant(const PkArgs &a, uint64_t c) {
+    if (a.keys[c] != (PK_PENDING | c)) return false;
+    uint64_t at = 0, len = 0;
+    return pk_src(a, c, at, len) == 1 && !(a.bad && a.bad[c]);
+}
+
+__global__ void __launch_bounds__(256) k_pk_mark(PkArgs a) {
+    PK_LIST(c, a.n) {
+        if (!pk_is_claimant(a, c)) continue;
         const uint32_t f = ~*pk_first_word(a.slots + a.slotix[c]);
         a.firstof[c] = f;
         a.newf[f] = 1;
@@ -792,9 +802,9 @@ __device__ inline void pk_slot_fill(PkSlot &sl, const uint8_t *src, uint32_t cl)
 
 // per claim: its id (the table size + the rank of its first-seen position), its canonical bytes, offset
 // and hash appended, its slot -> the id and the key's inline words; firstof[c] becomes the id
-__global__ void __launch_bounds__(256) k_pk_newkeys(PkArgs a, uint64_t nclaims) {
-    PK_LIST(k, nclaims) {
-        const uint32_t c = a.claims[k];
+__global__ void __launch_bounds__(256) k_pk_newkeys(PkArgs a) {
+    PK_LIST(c, a.n) {
+        if (!pk_is_claimant(a, c)) continue;
         const uint32_t f = a.firstof[c];
         const uint32_t id = (uint32_t)a.nkeys + a.rank[f] - 1u;
         const uint32_t cl = a.clen[c];
@@ -919,7 +929,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     a.clen = (uint32_t *)take(c4);
     a.slotix = (uint32_t *)take(c4);
     a.firstof = (uint32_t *)take(c4);
-    a.claims = (uint32_t *)take(c4);
+    (void)take(c4);  // (was the claimants' list)
     a.slow = (uint32_t *)take(c4);
     a.newf = (uint32_t *)take(c4);
     a.newl = (uint32_t *)take(c4);
@@ -1002,7 +1012,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     if (!nclaims) return CORRO_OK;  // (a warm call: every key held, ids already in keys[])
     HIP_PKC(hipMemsetAsync(a.newf, 0, 4 * n, s));
     HIP_PKC(hipMemsetAsync(a.newl, 0, 4 * n, s));
-    hipLaunchKernelGGL(k_pk_mark, pk_grid(nclaims), dim3(256), 0, s, a, nclaims);
+    hipLaunchKernelGGL(k_pk_mark, pk_grid(n), dim3(256), 0, s, a);
     HIP_PKC(hipGetLastError());
     TRY_PKC(prim_inclusive_scan_u32(d_temp, &temp, a.newf, a.rank, (uint32_t)n, s));
     TRY_PKC(prim_inclusive_scan_u32_u64(d_temp, &temp, a.newl, a.noff, n, s));
@@ -1022,7 +1032,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     a.kbytes = t.d_bytes.as<uint8_t>();
     a.khash = t.d_hash.as<uint64_t>();
     if (fault_armed("pk_commit")) return failc(fail(CORRO_E_DEVICE, "injected fault (CORRO_FAULT): pk_commit"));
-    hipLaunchKernelGGL(k_pk_newkeys, pk_grid(nclaims), dim3(256), 0, s, a, nclaims);
+    hipLaunchKernelGGL(k_pk_newkeys, pk_grid(n), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pk_commit, pk_grid(n), dim3(256), 0, s, a);
     HIP_PKC(hipGetLastError());
     HIP_PKC(hipStreamSynchronize(s));
