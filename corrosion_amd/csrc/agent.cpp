@@ -1017,7 +1017,7 @@ class HostPool {
     // The first call of a process paid its host threads' first heap growth (the allocator's mmap
     // threshold starts at 128 KB, so every large per-actor vector was a fresh mmap + page faults that
     // later calls reuse from the arena: the first mixed call's walk 9.3 vs 3.2 ms,
-    // profiles/r05_agent_cold_first_call.log). Each worker grows its arena once here: one 16-MB block
+    // profiles/history/r05_agent_cold_first_call.log). Each worker grows its arena once here: one 16-MB block
     // freed raises its mmap / trim thresholds, then a spread of smaller blocks is touched and freed so
     // the arena keeps the pages. (CORRO_HEAP_WARM=0 skips it.)
     static void warm_heap() {

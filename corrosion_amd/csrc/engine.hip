@@ -974,7 +974,7 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     a.force_general = force_general ? 1u : 0u;
     // General buckets of more than 512 records go to the device-wide fold when the batch is large
     // enough that the fold runs anyway and no impacts are asked for (the fold then reduces hot rows):
-    // config 5 12.3 -> 11.5 ms (256 / 1024 / all: 12.4 / 11.8 / 12.8, profiles/r03_c5_gen_ovf_min.log).
+    // config 5 12.3 -> 11.5 ms (256 / 1024 / all: 12.4 / 11.8 / 12.8, profiles/history/r03_c5_gen_ovf_min.log).
     // A small batch keeps its LDS bodies (one bucket past 512 records would pull in the whole fold).
     static const char *gom = std::getenv("CORRO_GEN_OVF_MIN");  // (A/B knob)
     a.gen_ovf_min = gom ? (uint32_t)std::atoi(gom)

@@ -792,7 +792,7 @@ struct NullEmit {
 // and after the scan the wave writes the buffered needs of its contiguous output window with
 // coalesced stores (each slot fetched from its lane by a cross-lane permute), without a second walk.
 // At the 6-waves-per-SIMD register budget the buffers spill: config 4 5.52 ms (NEED_NB 0) vs 6.02 /
-// 6.48 / 7.47 ms (2 / 3 / 4), and 10.6 GB written per diff at 4 (profiles/r03_sync_need_nb.log).
+// 6.48 / 7.47 ms (2 / 3 / 4), and 10.6 GB written per diff at 4 (profiles/history/r03_sync_need_nb.log).
 #ifndef NEED_NB
 #define NEED_NB 0
 #endif

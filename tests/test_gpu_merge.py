@@ -339,7 +339,7 @@ def test_config2_full_size_vs_sharded_oracle():
     """Config 2 at its full size (2^26 changes, pk space 2^22, 1000 actors) generated in HBM, with
     impact flags: all 2^26 impacts equal, rows equal through the order-independent digest of every
     output field, db_versions equal (checker: the oracle's pk-sharded fold on the host cores).
-    tools/parity_scale.py runs the same check at 2^29 changes (profiles/r01_parity_512m.json)."""
+    tools/parity_scale.py runs the same check at 2^29 changes (profiles/history/r01_parity_512m.json)."""
     import torch
     sites = synth.site_ids(1000, 1)
     b = synth.uniform_batch_torch(1 << 26, 1000, 1 << 22, 4, seed=synth.config_seed(2), device="cuda")
