@@ -1573,20 +1573,30 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
     res.run_site.resize(nruns);
     res.run_start.resize(nruns);
     res.run_end.resize(nruns);
-    std::vector<RunRec> runs(nruns);
-    if (nruns) CORRO_HIP_TRY(hipMemcpyAsync(runs.data(), h.runs, nruns * sizeof(RunRec), hipMemcpyDeviceToHost, s));
     res.nh = nh;
-    if (nh) {  // their headers, arrival index, unknown-name and canonical flags: one pinned readback
-        const size_t o_idx = al256((uint64_t)nh * sizeof(corro_changeset)), o_bad = o_idx + al256(nh * 4ULL),
-                     o_can = o_bad + al256(nh), o_tab = o_can + al256(nh), total_b = o_tab + al256(nh * 4ULL);
+    // one pinned readback area for the version runs and (when there are host changesets) their headers,
+    // arrival index, unknown-name and canonical flags; one wait for both copies (a pageable copy of the
+    // runs blocked on its own)
+    size_t o_idx = 0, o_bad = 0, o_can = 0, o_tab = 0, total_b = 0;
+    if (nh) {
+        o_idx = al256((uint64_t)nh * sizeof(corro_changeset));
+        o_bad = o_idx + al256(nh * 4ULL);
+        o_can = o_bad + al256(nh);
+        o_tab = o_can + al256(nh);
+        total_b = o_tab + al256(nh * 4ULL);
+    }
+    const size_t o_runs = total_b, pin_b = o_runs + al256(nruns * sizeof(RunRec));
+    if (pin_b > ctx->h_hfetch_bytes) {
+        if (ctx->h_hfetch) (void)hipHostFree(ctx->h_hfetch);
+        ctx->h_hfetch = nullptr;
+        ctx->h_hfetch_bytes = 0;
+        CORRO_HIP_TRY(hipHostMalloc(&ctx->h_hfetch, pin_b + pin_b / 4, hipHostMallocDefault));
+        ctx->h_hfetch_bytes = pin_b + pin_b / 4;
+    }
+    uint8_t *hp = static_cast<uint8_t *>(ctx->h_hfetch);
+    if (nruns) CORRO_HIP_TRY(hipMemcpyAsync(hp + o_runs, h.runs, nruns * sizeof(RunRec), hipMemcpyDeviceToHost, s));
+    if (nh) {
         if (int rc = ctx->d_agent_fetch.ensure(total_b + 256)) return rc;
-        if (total_b > ctx->h_hfetch_bytes) {
-            if (ctx->h_hfetch) (void)hipHostFree(ctx->h_hfetch);
-            ctx->h_hfetch = nullptr;
-            ctx->h_hfetch_bytes = 0;
-            CORRO_HIP_TRY(hipHostMalloc(&ctx->h_hfetch, total_b + total_b / 4, hipHostMallocDefault));
-            ctx->h_hfetch_bytes = total_b + total_b / 4;
-        }
         uint8_t *base = ctx->d_agent_fetch.as<uint8_t>();
         HGatherArgs g{};
         g.cs = dcs;
@@ -1602,7 +1612,6 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         g.otab = reinterpret_cast<uint32_t *>(base + o_tab);
         hipLaunchKernelGGL(k_hdr_gather, wave_grid(nh), dim3(AG_T), 0, s, g);
         CORRO_HIP_TRY(hipGetLastError());
-        uint8_t *hp = static_cast<uint8_t *>(ctx->h_hfetch);
         CORRO_HIP_TRY(hipMemcpyAsync(hp, base, total_b, hipMemcpyDeviceToHost, s));
         res.hcs = reinterpret_cast<const corro_changeset *>(hp);
         res.hidx = reinterpret_cast<const uint32_t *>(hp + o_idx);
@@ -1610,6 +1619,7 @@ int agent_dev_headers(corro_ctx *ctx, const corro_changeset *dcs, uint64_t ncs, 
         res.hcanon = hp + o_can;
         res.hctab = reinterpret_cast<const uint32_t *>(hp + o_tab);
     }
+    const RunRec *runs = reinterpret_cast<const RunRec *>(hp + o_runs);
     if (nruns || nh) CORRO_HIP_TRY(hipStreamSynchronize(s));
     for (uint64_t r = 0; r < nruns; r++) {
         res.run_site[r] = runs[r].site;
@@ -1708,6 +1718,16 @@ int agent_dev_reserve(corro_ctx *ctx, uint64_t ncs) {
         ctx->h_agent_bytes = 0;
         CORRO_HIP_TRY(hipHostMalloc(&ctx->h_agent, total + total / 4, hipHostMallocDefault));
         ctx->h_agent_bytes = total + total / 4;
+    }
+    // the readback of the decided version runs and of the host changesets' headers (agent_dev_headers):
+    // sized for runs of a quarter of the changesets and headers of an eighth
+    const size_t fb = al256(n / 4 * 24) + al256(n / 8 * (sizeof(corro_changeset) + 10));
+    if (fb > ctx->h_hfetch_bytes) {
+        if (ctx->h_hfetch) (void)hipHostFree(ctx->h_hfetch);
+        ctx->h_hfetch = nullptr;
+        ctx->h_hfetch_bytes = 0;
+        CORRO_HIP_TRY(hipHostMalloc(&ctx->h_hfetch, fb, hipHostMallocDefault));
+        ctx->h_hfetch_bytes = fb;
     }
     const size_t hb = n * sizeof(corro_changeset);
     if (hb > ctx->h_hdr_bytes) {
