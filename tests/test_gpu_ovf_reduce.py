@@ -88,3 +88,37 @@ def test_reduction_impact_form_vs_oracle(max_cl, sent, wide):
                                     wide=wide)
         _apply(e, f, b, True)
         _compare(e, f)
+
+
+def _tie_batch(n, npk, sites_n, seed, dbv0=1, cl_max=3):
+    """Hot rows whose changes at the largest causal length tie on (col_version, value, site) in every
+    cell: only db_version / seq / ts tell them apart, so the winner must be the earliest change."""
+    rng = np.random.default_rng(seed)
+    i = np.arange(n, dtype=np.int64)
+    pk = rng.integers(1, npk + 1, size=n).astype(np.uint64)
+    site = rng.integers(0, sites_n, size=n).astype(np.uint32)
+    cid = rng.integers(1, 5, size=n).astype(np.uint32)
+    cl = (2 * rng.integers(0, (cl_max + 1) // 2, size=n) + 1).astype(np.uint32)  # odd: column changes
+    cv = np.full(n, 3, np.int64)
+    v0 = np.full(n, 7, np.uint64)
+    dbv = (dbv0 + i // 16).astype(np.int64)
+    seq = (i % 16).astype(np.uint32)
+    vt = np.full(n, 1, np.uint8)
+    return {"pk": pk, "table_cid": cid, "col_version": cv, "db_version": dbv, "cl": cl, "seq": seq, "site": site,
+            "val0": v0, "val1": np.zeros(n, np.uint64), "val_type": vt, "val_len": np.zeros(n, np.uint8),
+            "ts": (dbv.astype(np.uint64) << np.uint64(20)) + site.astype(np.uint64)}
+
+
+def test_reduced_cells_settle_exact_ties_by_position():
+    """Round 6's fused plain fold: a reduced row's cells are sorted by (owner record, cid) only, so the
+    sort's order inside a cell is not the application order and exact ties -- equal col_version, value
+    and site -- are settled by the position tie-break of the argmax (the earliest change wins, its
+    db_version / seq / ts kept). Two batches: the second ties against the prior clocks too (a prior
+    record comes first in application order)."""
+    seed = 977
+    sites = synth.site_ids(2, seed)
+    e, f = _engine({"t0": list(synth.ADV_COLS)}, sites), O.Fold(sites)
+    for k, dbv0 in enumerate((1, 100000)):
+        b = _tie_batch(30000, 40, 1 if k else 2, seed + k, dbv0=dbv0)
+        _apply(e, f, b, False)
+        _compare(e, f)
