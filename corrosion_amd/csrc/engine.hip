@@ -484,7 +484,7 @@ static int ctx_prepare_device(corro_ctx *ctx) {
     for (auto &e : ctx->ev) CORRO_HIP_TRY(hipEventCreate(&e));
     const size_t lds_max = 160 * 1024;
     for (const void *f : {(const void *)k_hist<8>, (const void *)k_hist<16>, (const void *)k_hist<32>,
-                          (const void *)k_hist<16, true>})
+                          (const void *)k_hist<16, true>, (const void *)k_hist<16, false, true>})
         CORRO_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
     for (const void *f : {(const void *)k_scatter<true, true>, (const void *)k_scatter<true, false>,
                           (const void *)k_scatter<true, false, 8>,
@@ -924,7 +924,10 @@ static int apply_chunk(corro_ctx *ctx, BatchDev bd, uint8_t *imp_buf) {
     const uint32_t one_table = ctx->tables.size() == 1 ? 1u : 0u;
     // changes per lane in flight (CORRO_HIST_U: A/B knob)
     static const int hist_u = std::getenv("CORRO_HIST_U") ? std::atoi(std::getenv("CORRO_HIST_U")) : 16;
-    auto hk = bd.slot_rec ? k_hist<16, true> : hist_u == 8 ? k_hist<8> : hist_u == 32 ? k_hist<32> : k_hist<16>;
+    using HistK = void (*)(BatchDev, uint32_t, uint32_t, uint32_t, uint32_t *, ApplyZero);
+    const HistK hk = bd.slot_rec ? k_hist<16, true>
+                     : !one_table ? (HistK)k_hist<16, false, true>
+                     : hist_u == 8 ? k_hist<8> : hist_u == 32 ? k_hist<32> : k_hist<16>;
     hipLaunchKernelGGL(hk, dim3(ntiles), dim3(HIST_THREADS), (size_t)B * 4, s, bd, tile, log2B, one_table,
                        ctx->d_hist.as<uint32_t>(), z);
     CORRO_HIP_TRY(hipGetLastError());

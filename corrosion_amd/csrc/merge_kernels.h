@@ -214,7 +214,10 @@ struct ApplyZero {
 // SLOT: slot mode (corro_apply_slots) -- its own instantiation, so the SoA form keeps every load of a
 // lane's HIST_U changes issued before the first use (a slot-mode branch inside that loop cost the
 // config-2 histogram 0.145 -> 0.32 ms)
-template <int HIST_U, bool SLOT = false>
+// MT: the schema has several tables (tables read with the pks) -- a compile-time choice, so the lane's
+// table loads are issued with its pk loads (a runtime `one_table` test between them kept the compiler
+// from batching the loads: config 5's histogram ran 0.36 ms against config 2's 0.15)
+template <int HIST_U, bool SLOT = false, bool MT = false>
 static __global__ void __launch_bounds__(HIST_THREADS)
 k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t *__restrict__ hist_out, ApplyZero z) {
     extern __shared__ uint32_t hist[];
@@ -249,7 +252,7 @@ k_hist(BatchDev in, uint32_t tile, uint32_t log2B, uint32_t one_table, uint32_t 
                 ap[k] = slot_valid(in, i, sover) ? 0u : AP_SKIP;
             } else {
                 pk[k] = in.pk[i];
-                tc[k] = one_table ? 0u : in.tcid[i];
+                tc[k] = MT ? in.tcid[i] : 0u;
                 ap[k] = in.ap && !in.ap_all ? in.ap[i] : 0u;
             }
         }
