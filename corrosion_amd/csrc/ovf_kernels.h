@@ -570,11 +570,18 @@ __device__ inline void rcl_wave_add(RclLds &L, const OvfDev &d, bool todo, uint3
 #define OVF_RS_BITS 10
 #endif
 constexpr uint32_t RS_T = 256, RS_E = OVF_RS_E, RS_CHUNK = RS_T * RS_E, RS_HT = 1u << OVF_RS_BITS;
+// (the fused form's w3 words only in its own table: an extra word in the others' would cost
+// k_ovf_lookup<true> a workgroup per CU -- its two LDS tables sit just under a quarter of the CU's LDS)
 template <bool W3>
-struct RsLdsT {
+struct RsLdsT;
+template <>
+struct RsLdsT<false> {
     uint32_t key[RS_HT], w2[RS_HT];  // key: row + 1 (0: free)
     unsigned long long w1[RS_HT];
-    unsigned long long w3[W3 ? RS_HT : 1];  // (fused form only)
+};
+template <>
+struct RsLdsT<true> : RsLdsT<false> {
+    unsigned long long w3[RS_HT];
 };
 using RsLds = RsLdsT<false>;
 
@@ -611,7 +618,10 @@ __device__ inline bool rs_lds_add(RsLdsT<W3> &L, uint32_t row, uint64_t w1, uint
 template <bool W3>
 __device__ inline void rs_lds_flush(const RsLdsT<W3> &L, const OvfDev &d) {
     for (uint32_t i = threadIdx.x; i < RS_HT; i += blockDim.x)
-        if (L.key[i]) rs_put(d, L.key[i] - 1, L.w1[i], L.w2[i], W3 ? L.w3[W3 ? i : 0] : 0ULL);
+        if (L.key[i]) {
+            if constexpr (W3) rs_put(d, L.key[i] - 1, L.w1[i], L.w2[i], L.w3[i]);
+            else rs_put(d, L.key[i] - 1, L.w1[i], L.w2[i]);
+        }
 }
 
 __device__ inline uint32_t wave_or32(uint32_t x) {
