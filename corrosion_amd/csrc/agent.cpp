@@ -207,6 +207,20 @@ class FlatMap {
         return (size_t)(std::lower_bound(v_.begin(), v_.end(), k, [](const Slot &s, const K &x) { return s.key < x; }) -
                         v_.begin());
     }
+    // lower(k) for a k at or past the key of slot `from` (galloping from there: a sorted run of
+    // lookups walks the map once)
+    size_t lower_from(size_t from, const K &k) const {
+        const size_t n = v_.size();
+        if (from >= n || !(v_[from].key < k)) return from;
+        size_t lo = from, step = 1;
+        while (lo + step < n && v_[lo + step].key < k) {
+            lo += step;
+            step *= 2;
+        }
+        const auto e = v_.begin() + (ptrdiff_t)std::min(n, lo + step + 1);
+        return (size_t)(std::lower_bound(v_.begin() + (ptrdiff_t)lo + 1, e, k,
+                                         [](const Slot &s, const K &x) { return s.key < x; }) - v_.begin());
+    }
     V *find(const K &k) {
         const size_t i = lower(k);
         return i < v_.size() && !(k < v_[i].key) && !v_[i].dead ? &v_[i].val : nullptr;
@@ -922,22 +936,56 @@ void commit_seqbook(corro_bookie *bk, const std::vector<Staged *> &order) {
 
 // sorted site << 40 | version keys of every (site, version) holding buffered rows or seq bookkeeping
 std::vector<uint64_t> buffered_keys(const corro_bookie *bk) {
-    std::vector<uint64_t> a, b, k;
-    a.reserve(bk->buffered.live());
-    b.reserve(bk->seqbook.live());
-    for (size_t i = 0; i < bk->buffered.slots(); i++) {
+    // (each map's slots scanned in parallel chunks, the chunks' keys concatenated in order)
+    auto scan = [](size_t n, auto &&key_of) {
+        constexpr size_t CH = 8192;
+        const size_t nch = (n + CH - 1) / CH;
+        std::vector<std::vector<uint64_t>> part(nch);
+        run_parallel(nch, [&](size_t c) {
+            for (size_t i = c * CH; i < std::min(n, (c + 1) * CH); i++) {
+                uint64_t x;
+                if (key_of(i, x)) part[c].push_back(x);
+            }
+        }, 1);
+        size_t tot = 0;
+        for (const auto &p : part) tot += p.size();
+        std::vector<uint64_t> out;
+        out.reserve(tot);
+        for (const auto &p : part) out.insert(out.end(), p.begin(), p.end());
+        return out;
+    };
+    const std::vector<uint64_t> a = scan(bk->buffered.slots(), [&](size_t i, uint64_t &key) {
         const auto &x = bk->buffered.at(i);
-        if (!x.dead && !x.val.empty() && x.key.second >= 0 && (uint64_t)x.key.second < (1ULL << 40))
-            a.push_back((uint64_t)x.key.first << 40 | (uint64_t)x.key.second);
-    }
-    for (size_t i = 0; i < bk->seqbook.slots(); i++) {
+        if (x.dead || x.val.empty() || x.key.second < 0 || (uint64_t)x.key.second >= (1ULL << 40)) return false;
+        key = (uint64_t)x.key.first << 40 | (uint64_t)x.key.second;
+        return true;
+    });
+    const std::vector<uint64_t> b = scan(bk->seqbook.slots(), [&](size_t i, uint64_t &key) {
         const auto &x = bk->seqbook.at(i);
-        if (!x.dead && x.key.second < (1ULL << 40)) b.push_back((uint64_t)x.key.first << 40 | x.key.second);
-    }
-    k.resize(a.size() + b.size());  // (both ascending: the maps' key order is (site, version))
+        if (x.dead || x.key.second >= (1ULL << 40)) return false;
+        key = (uint64_t)x.key.first << 40 | x.key.second;
+        return true;
+    });
+    std::vector<uint64_t> k(a.size() + b.size());  // (both ascending: the maps' key order is (site, version))
     std::merge(a.begin(), a.end(), b.begin(), b.end(), k.begin());
     k.erase(std::unique(k.begin(), k.end()), k.end());
     return k;
+}
+
+// clear_buffered of single versions, many at once: sorted, then each map walked once
+void clear_buffered_each(corro_bookie *bk, std::vector<std::pair<uint32_t, uint64_t>> &sv) {
+    std::sort(sv.begin(), sv.end());
+    size_t i = 0, j = 0;
+    for (const auto &[site, v] : sv) {
+        if (v <= (uint64_t)INT64_MAX) {
+            const BufKey k{site, (int64_t)v};
+            for (i = bk->buffered.lower_from(i, k); i < bk->buffered.slots() && !(k < bk->buffered.at(i).key); i++)
+                bk->buffered.erase_at(i);
+        }
+        const SeqKey k{site, v};
+        for (j = bk->seqbook.lower_from(j, k); j < bk->seqbook.slots() && !(k < bk->seqbook.at(j).key); j++)
+            bk->seqbook.erase_at(j);
+    }
 }
 
 void clear_buffered(corro_bookie *bk, uint32_t site, uint64_t vs, uint64_t ve) {
@@ -1308,6 +1356,10 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
         lap(1);
         // pass 2 (the bookie is not written until the call commits, so pass 1's contains_all stands)
         SeenMap seen_local(w.partials);
+        // (the versions pass 2 adds are collected and merged with the runs' in one linear pass at the
+        // end: inserted one by one they filled holes between the runs, a shift of the range list each)
+        std::vector<Range> added;
+        added.reserve(unknown.size());
         for (uint64_t i : unknown) {
             const corro_changeset &c = v.cs[i];
             const Range vr = versions_of(c);
@@ -1346,7 +1398,18 @@ void run_actor_walk(corro_bookie *bk, ActorWork &w, const CsView &v, const RunVi
             }
             if (partial) w.partials.emplace_back(vr.first, std::move(*partial));
             seen_local.insert(vr, partial ? w.partials.size() - 1 : SIZE_MAX);
-            versions.insert(vr.first, vr.second);
+            added.push_back(vr);
+        }
+        if (!added.empty()) {
+            std::sort(added.begin(), added.end());
+            RangeSet all;  // (ascending starts: every insert appends or extends the last range)
+            const auto &fr = versions.ranges();
+            size_t x = 0, y = 0;
+            while (x < fr.size() || y < added.size()) {
+                const Range &r = (y == added.size() || (x < fr.size() && fr[x].first <= added[y].first)) ? fr[x++] : added[y++];
+                all.insert(r.first, r.second);
+            }
+            versions = std::move(all);
         }
         lap(2);
     }
@@ -1537,18 +1600,34 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     if (nh) {
         // one pass over the headers (they arrive by DMA: each pass is a DRAM read of 80 B per changeset):
         // the per-actor groups and the partial changesets whose rows come to the host
-        std::vector<corro::AgentSpan> sp;
-        uint64_t r = 0, g0 = 0;
-        for (uint64_t k = 0; k < nh; k++) {
-            const corro_changeset &c = hcs[k];
-            local[k] = k;
-            if (k + 1 == nh || hcs[k + 1].site != c.site) {  // (the next header is read next anyway)
-                ActorWork &w = work[(size_t)work_of[c.site]];
-                w.idx = local.data() + g0;
-                w.nidx = k + 1 - g0;
-                g0 = k + 1;
+        // (in parallel chunks: a mixed call's 10^5 headers were 0.6 ms of one thread's reads)
+        const auto fetched = [&](const corro_changeset &c, uint64_t k) {
+            return c.kind == CORRO_CS_FULL && c.change_count && !is_complete(c) && !R.hbad[k] && !(canon && canon[k]);
+        };
+        constexpr uint64_t HCH = 4096;
+        const uint64_t nch = (nh + HCH - 1) / HCH;
+        std::vector<uint64_t> gend(work.size(), 0);
+        std::vector<uint8_t> any_fetch(nch, 0);
+        run_parallel(nch, [&](size_t ch) {
+            const uint64_t lo = ch * HCH, hi = std::min<uint64_t>(nh, lo + HCH);
+            for (uint64_t k = lo; k < hi; k++) {
+                const corro_changeset &c = hcs[k];
+                local[k] = k;
+                const size_t wk = (size_t)work_of[c.site];
+                if (k == 0 || hcs[k - 1].site != c.site) work[wk].idx = local.data() + k;  // (one group per actor)
+                if (k + 1 == nh || hcs[k + 1].site != c.site) gend[wk] = k + 1;
+                if (fetched(c, k)) any_fetch[ch] = 1;
             }
-            if (c.kind == CORRO_CS_FULL && c.change_count && !is_complete(c) && !R.hbad[k] && !(canon && canon[k])) {
+        }, 1);
+        for (size_t q = 0; q < work.size(); q++)
+            if (work[q].idx) work[q].nidx = gend[q] - (uint64_t)(work[q].idx - local.data());
+        std::vector<corro::AgentSpan> sp;
+        uint64_t r = 0;
+        for (uint64_t ch = 0; ch < nch; ch++) {
+            if (!any_fetch[ch]) continue;
+            for (uint64_t k = ch * HCH; k < std::min<uint64_t>(nh, (ch + 1) * HCH); k++) {
+                const corro_changeset &c = hcs[k];
+                if (!fetched(c, k)) continue;
                 inc_row[k] = r;
                 sp.push_back({c.change_off, r, c.change_count, c.ts});
                 r += c.change_count;
@@ -1712,7 +1791,7 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     std::vector<std::pair<uint32_t, uint64_t>> sv;
     TRY_RC(corro::agent_dev_commit_headers(ctx, ncs, out->known, bkeys.empty() ? nullptr : &bkeys, &sv));
     stage("commit_hdr");
-    for (auto &[site, v] : sv) clear_buffered(bk, site, v, v);
+    clear_buffered_each(bk, sv);
     compact_tables(bk);
     uint64_t nready = 0;
     for (size_t k : order) {
