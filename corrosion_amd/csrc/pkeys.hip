@@ -810,11 +810,22 @@ __global__ void __launch_bounds__(256) k_pk_newkeys(PkArgs a) {
         const uint32_t cl = a.clen[c];
         const uint64_t o = a.nbytes + a.noff[f] - cl;
         const uint8_t *src = pk_cbytes(a, c);
-        for (uint32_t b = 0; b < cl; b++) a.kbytes[o + b] = src[b];
+        PkSlot &sl = a.slots[a.slotix[c]];
+        if (cl <= PK_INLINE) {
+            // (a short key's bytes read once as its slot words -- independent aligned loads -- then
+            // stored from registers: a byte loop alternating loads and stores waited on every load)
+            const PkWords w = pk_words(src, cl);
+            for (uint32_t b = 0; b < cl; b++) a.kbytes[o + b] = (uint8_t)(w.q[(b + 1) >> 3] >> (8 * ((b + 1) & 7)));
+            uint64_t *q = reinterpret_cast<uint64_t *>(&sl) + 1;
+            q[0] = w.q[0];
+            q[1] = w.q[1];
+            q[2] = w.q[2];
+        } else {
+            for (uint32_t b = 0; b < cl; b++) a.kbytes[o + b] = src[b];
+            pk_slot_fill(sl, src, cl);
+        }
         a.koff[id + 1] = o + cl;
         a.khash[id] = a.h[c];
-        PkSlot &sl = a.slots[a.slotix[c]];
-        pk_slot_fill(sl, src, cl);
         sl.w = ((unsigned long long)pk_tag(a.h[c]) << 32) | id;
         a.firstof[c] = id;
     }
