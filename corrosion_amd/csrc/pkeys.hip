@@ -194,6 +194,9 @@ int prim_inclusive_scan_u32(void *temp, size_t *temp_bytes, const uint32_t *in, 
                             hipStream_t s);
 int prim_inclusive_scan_u32_u64(void *temp, size_t *temp_bytes, const uint32_t *in, uint64_t *out, uint64_t n,
                                 hipStream_t s);
+int prim_inclusive_max_u64(void *temp, size_t *temp_bytes, const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s);
+int ovf_sort_pairs(void *temp, size_t *temp_bytes, const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uint32_t *vo,
+                   uint32_t n, uint32_t end_bit, hipStream_t s);
 
 namespace {
 
@@ -210,6 +213,9 @@ struct alignas(32) PkSlot {
 };
 static_assert(sizeof(PkSlot) == 32, "pk slot size");
 constexpr uint32_t PK_MAX_PROBE = 256;     // past this many slots a probe asks for a larger table
+// Homes lie in the first PkTable::nslots slots; PK_PAD more follow them before a probe wraps to slot 0,
+// so a table rebuilt in home order (pk_place_ordered) holds every key between its home and the end.
+constexpr uint64_t PK_PAD = 1024;
 constexpr uint64_t PK_SCRATCH = 1ULL << 63;  // cref: canonical bytes in the scratch, not the input
 
 __device__ inline uint32_t pk_wave_sum(uint32_t x) {
@@ -352,7 +358,8 @@ struct PkArgs {
     unsigned long long *ctl;
     // the table
     PkSlot *slots;
-    uint64_t nsl;       // slots (a multiple of 8, not a power of two: sized for the MALL, see pk_slots_for)
+    uint64_t nsl;       // slots, PK_PAD past the homes: a probe wraps here
+    uint64_t nhome;     // home slots (a multiple of 8, not a power of two: sized for the MALL, see pk_slots_for)
     uint64_t *koff;
     uint8_t *kbytes;
     uint64_t *khash;
@@ -593,10 +600,10 @@ __global__ void __launch_bounds__(PK_FIND_THREADS) k_pk_find(PkArgs a) {
                     const uint32_t tag = pk_tag(hh);
                     PkWords mw{};
                     if (cl <= PK_INLINE) mw = pk_words(p, cl);
-                    sl = pk_slot_of(hh, a.nsl);
+                    sl = pk_slot_of(hh, a.nhome);
 #if PK_DIAG & 40  // (diagnostic, results not valid: ONE slot read, at the home slot (32) or inside the
                   // first 2^20 slots (8), no compare, no claim)
-                    if (PK_DIAG & 8) sl = pk_slot_of(hh, min(a.nsl, (uint64_t)1 << 20));
+                    if (PK_DIAG & 8) sl = pk_slot_of(hh, min(a.nhome, (uint64_t)1 << 20));
                     {
                         unsigned long long w;
                         PkWords q;
@@ -717,7 +724,7 @@ __global__ void __launch_bounds__(256) k_pk_probe_slow(PkArgs a, uint64_t nslow)
             const uint8_t *mine = pk_cbytes(a, i);
             PkWords mw{};
             if (cl <= PK_INLINE) mw = pk_words(mine, cl);
-            sl = pk_slot_of(h, a.nsl);
+            sl = pk_slot_of(h, a.nhome);
             uint64_t res = ~0ULL;
             for (uint32_t step = 0; step < PK_MAX_PROBE; step++, sl = pk_next(sl, a.nsl)) {
                 PkSlot *ps = a.slots + sl;
@@ -844,16 +851,46 @@ __global__ void __launch_bounds__(256) k_pk_commit(PkArgs a) {
 
 // the slots rebuilt from the keys (a larger table, a retry after a probe overflow, or the cleanup of a
 // failed call's claims)
-__global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t nsl, const uint64_t *khash,
+__global__ void __launch_bounds__(256) k_pk_rehash(PkSlot *slots, uint64_t nsl, uint64_t nhome, const uint64_t *khash,
                                                    const uint64_t *koff, const uint8_t *kbytes, uint64_t nkeys) {
     for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < nkeys; id += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t h = khash[id];
         const unsigned long long w = ((unsigned long long)pk_tag(h) << 32) | id;
-        for (uint64_t sl = pk_slot_of(h, nsl);; sl = pk_next(sl, nsl))
+        for (uint64_t sl = pk_slot_of(h, nhome);; sl = pk_next(sl, nsl))
             if (atomicCAS(&slots[sl].w, 0ULL, w) == 0ULL) {
                 pk_slot_fill(slots[sl], kbytes + koff[id], (uint32_t)(koff[id + 1] - koff[id]));
                 break;
             }
+    }
+}
+
+// Ordered rebuild (round 6): the keys placed in home order, each at p_i = max(h_i, p_{i-1} + 1) =
+// i + max_{j <= i}(h_j - j) over the home-sorted keys -- a max-scan, then one plain store per key. A
+// key's probe then passes only keys of smaller or equal home: in a table filled by concurrent claims the
+// longest probe of a wave's 64 lanes runs ~10 slots at load 0.6, in home order ~5
+// (tools/sim_probe_order.py), and a wave waits for its longest lane (warm intern 5.48 -> 5.07 ms).
+__global__ void __launch_bounds__(256) k_pk_homes(const uint64_t *khash, uint64_t nkeys, uint64_t nhome, uint64_t *home,
+                                                  uint32_t *ids) {
+    PK_LIST(id, nkeys) {
+        home[id] = pk_slot_of(khash[id], nhome);
+        ids[id] = (uint32_t)id;
+    }
+}
+__global__ void __launch_bounds__(256) k_pk_shift(const uint64_t *home_s, uint64_t nkeys, uint64_t *v) {
+    PK_LIST(i, nkeys) v[i] = home_s[i] + nkeys - i;  // (h_i - i, biased to stay positive)
+}
+__global__ void __launch_bounds__(256) k_pk_place(PkSlot *slots, uint64_t nsl, const uint64_t *vmax, const uint32_t *ids,
+                                                  uint64_t nkeys, const uint64_t *khash, const uint64_t *koff,
+                                                  const uint8_t *kbytes, unsigned long long *past) {
+    PK_LIST(i, nkeys) {
+        const uint64_t p = vmax[i] - nkeys + i;
+        if (p >= nsl) {  // (the pad ran out: the caller rebuilds by claims instead)
+            atomicOr(past, 1ULL);
+            continue;
+        }
+        const uint32_t id = ids[i];
+        pk_slot_fill(slots[p], kbytes + koff[id], (uint32_t)(koff[id + 1] - koff[id]));
+        slots[p].w = ((unsigned long long)pk_tag(khash[id]) << 32) | id;
     }
 }
 
@@ -870,16 +907,67 @@ uint64_t pk_slots_for(uint64_t keys, uint64_t num, uint64_t den) {
     return std::max<uint64_t>(4096, (ns + 7) & ~7ULL);
 }
 
-// slots for `want` keys at load <= 3/4 (at least `min_slots`), rebuilt from the arena
+// The committed keys placed into `slots` (nsl slots, homes in the first nhome) in home order; false
+// when its scratch is not available or the pad runs out (the slots are then zero again).
+int pk_place_ordered(corro_ctx *ctx, const PkTable &t, PkSlot *slots, uint64_t nsl, uint64_t nhome, bool &placed) {
+    placed = false;
+    hipStream_t s = ctx->stream;
+    const uint64_t n = t.n;
+    if (n >= (1ULL << 31)) return CORRO_OK;
+    uint32_t bits = 1;
+    while ((1ULL << bits) < nhome) bits++;
+    size_t temp = 0, t1 = 0;
+    if (int rc = ovf_sort_pairs(nullptr, &temp, nullptr, nullptr, nullptr, nullptr, (uint32_t)n, bits, s)) return rc;
+    if (int rc = prim_inclusive_max_u64(nullptr, &t1, nullptr, nullptr, n, s)) return rc;
+    temp = std::max(temp, t1);
+    auto al = [](uint64_t x) { return (x + 255) & ~255ULL; };
+    const uint64_t c8 = al(n * 8), c4 = al(n * 4);
+    DevBuf sc;
+    if (sc.ensure(2 * c8 + 2 * c4 + 256 + al(temp)) != CORRO_OK) return CORRO_OK;  // (no room: rebuild by claims)
+    uint8_t *b = sc.as<uint8_t>();
+    uint64_t *ki = reinterpret_cast<uint64_t *>(b), *ko = reinterpret_cast<uint64_t *>(b + c8);
+    uint32_t *vi = reinterpret_cast<uint32_t *>(b + 2 * c8), *vo = reinterpret_cast<uint32_t *>(b + 2 * c8 + c4);
+    auto *past = reinterpret_cast<unsigned long long *>(b + 2 * c8 + 2 * c4);
+    void *tp = b + 2 * c8 + 2 * c4 + 256;
+    CORRO_HIP_TRY(hipMemsetAsync(past, 0, 8, s));
+    hipLaunchKernelGGL(k_pk_homes, pk_grid(n), dim3(256), 0, s, t.d_hash.as<uint64_t>(), n, nhome, ki, vi);
+    CORRO_HIP_TRY(hipGetLastError());
+    size_t tb = temp;
+    if (int rc = ovf_sort_pairs(tp, &tb, ki, ko, vi, vo, (uint32_t)n, bits, s)) return rc;
+    hipLaunchKernelGGL(k_pk_shift, pk_grid(n), dim3(256), 0, s, ko, n, ki);
+    CORRO_HIP_TRY(hipGetLastError());
+    tb = temp;
+    if (int rc = prim_inclusive_max_u64(tp, &tb, ki, ko, n, s)) return rc;
+    hipLaunchKernelGGL(k_pk_place, pk_grid(n), dim3(256), 0, s, slots, nsl, ko, vo, n, t.d_hash.as<uint64_t>(),
+                       t.d_off.as<uint64_t>(), t.d_bytes.as<uint8_t>(), past);
+    CORRO_HIP_TRY(hipGetLastError());
+    unsigned long long h_past = 1;
+    CORRO_HIP_TRY(hipMemcpyAsync(&h_past, past, 8, hipMemcpyDeviceToHost, s));
+    CORRO_HIP_TRY(hipStreamSynchronize(s));
+    if (h_past) {
+        CORRO_HIP_TRY(hipMemsetAsync(slots, 0, nsl * sizeof(PkSlot), s));
+        return CORRO_OK;
+    }
+    placed = true;
+    return CORRO_OK;
+}
+
+// slots for `want` keys at load <= 3/4 (at least `min_slots` homes), rebuilt from the arena
 int pk_slots_resize(corro_ctx *ctx, PkTable &t, uint64_t want, uint64_t min_slots = 0) {
     const uint64_t ns = std::max<uint64_t>(pk_slots_for(want, 3, 4), (min_slots + 7) & ~7ULL);
-    if (ns >= (1ULL << 32)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
+    if (ns + PK_PAD >= (1ULL << 32)) return fail(CORRO_E_RANGE, "interned pk table past 2^31 keys");
+    const uint64_t nsl = ns + PK_PAD;
     hipStream_t s = ctx->stream;
     DevBuf nb;
-    if (int rc = nb.ensure(ns * sizeof(PkSlot))) return rc;
-    CORRO_HIP_TRY(hipMemsetAsync(nb.p, 0, ns * sizeof(PkSlot), s));
-    if (t.n) hipLaunchKernelGGL(k_pk_rehash, pk_grid(t.n), dim3(256), 0, s, nb.as<PkSlot>(), ns,
-                                t.d_hash.as<uint64_t>(), t.d_off.as<uint64_t>(), t.d_bytes.as<uint8_t>(), t.n);
+    if (int rc = nb.ensure(nsl * sizeof(PkSlot))) return rc;
+    CORRO_HIP_TRY(hipMemsetAsync(nb.p, 0, nsl * sizeof(PkSlot), s));
+    bool placed = false;
+    static const bool ordered = !std::getenv("CORRO_PK_ORDERED") || std::atoi(std::getenv("CORRO_PK_ORDERED")) != 0;
+    if (t.n && ordered)
+        if (int rc = pk_place_ordered(ctx, t, nb.as<PkSlot>(), nsl, ns, placed)) return rc;
+    if (t.n && !placed)
+        hipLaunchKernelGGL(k_pk_rehash, pk_grid(t.n), dim3(256), 0, s, nb.as<PkSlot>(), nsl, ns,
+                           t.d_hash.as<uint64_t>(), t.d_off.as<uint64_t>(), t.d_bytes.as<uint8_t>(), t.n);
     CORRO_HIP_TRY(hipGetLastError());
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     t.d_slots.release();
@@ -985,7 +1073,8 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     DevBuf scratch;  // (non-canonical inputs: their canonical bytes)
     for (int attempt = 0;; attempt++) {
         a.slots = t.d_slots.as<PkSlot>();
-        a.nsl = t.nslots;
+        a.nsl = t.nslots + PK_PAD;
+        a.nhome = t.nslots;
         HIP_PKC(hipMemsetAsync(a.ctl, 0, 64, s));
         if (bad) HIP_PKC(hipMemsetAsync(bad, 0, n, s));
         const uint32_t nwaves = (uint32_t)((n + 63) / 64);
@@ -1051,7 +1140,11 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     t.nbytes = nbytes;
 #undef TRY_PKC
 #undef HIP_PKC
-    if (4 * t.n > 3 * t.nslots) TRY_PK(pk_slots_resize(ctx, t, t.n + t.n / 4));  // (the next call starts at load <= 0.6)
+    if (4 * t.n > 3 * t.nslots) {
+        TRY_PK(pk_slots_resize(ctx, t, t.n + t.n / 4));  // (the next call starts at load <= 0.6)
+    } else if (nnew >= 65536 && 4ULL * nnew >= t.n) {
+        TRY_PK(pk_slots_resize(ctx, t, t.n, t.nslots));  // (many keys placed by claims: rebuilt in home order)
+    }
     return CORRO_OK;
 }
 

@@ -62,6 +62,13 @@ int prim_inclusive_scan_u32_u64(void *temp, size_t *temp_bytes, const uint32_t *
     return CORRO_OK;
 }
 
+// inclusive max-scan of u64 (the pk table's ordered rebuild); temp == nullptr -> *temp_bytes = size needed
+int prim_inclusive_max_u64(void *temp, size_t *temp_bytes, const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s) {
+    const hipError_t e = rocprim::inclusive_scan(temp, *temp_bytes, in, out, (size_t)n, rocprim::maximum<uint64_t>(), s);
+    if (e != hipSuccess) return fail(CORRO_E_DEVICE, std::string("scan: ") + hipGetErrorString(e));
+    return CORRO_OK;
+}
+
 struct OvfMax {
     __device__ inline uint32_t operator()(uint32_t x, uint32_t y) const { return x > y ? x : y; }
 };
@@ -137,6 +144,8 @@ int prims_warm(corro_ctx *ctx) {
         temp = std::max(temp, t);
         prim_inclusive_scan_u32_u64(nullptr, &t, nullptr, nullptr, n, s);
         temp = std::max(temp, t);
+        prim_inclusive_max_u64(nullptr, &t, nullptr, nullptr, n, s);
+        temp = std::max(temp, t);
     }
     // keys in/out (u64), values in/out (u32), u32 keys/flags, u64 scan outputs
     const size_t k8 = (size_t)N * 8, k4 = (size_t)N * 4;
@@ -158,6 +167,8 @@ int prims_warm(corro_ctx *ctx) {
         if (int rc = prim_inclusive_scan_u32(tp, &t, u, vo, n, s)) return rc;
         t = temp;
         if (int rc = prim_inclusive_scan_u32_u64(tp, &t, u, wo, n, s)) return rc;
+        t = temp;
+        if (int rc = prim_inclusive_max_u64(tp, &t, ki, wo, n, s)) return rc;
     }
     CORRO_HIP_TRY(hipStreamSynchronize(s));
     buf.release();
