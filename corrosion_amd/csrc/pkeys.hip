@@ -1140,11 +1140,9 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
     t.nbytes = nbytes;
 #undef TRY_PKC
 #undef HIP_PKC
-    if (4 * t.n > 3 * t.nslots) {
-        TRY_PK(pk_slots_resize(ctx, t, t.n + t.n / 4));  // (the next call starts at load <= 0.6)
-    } else if (nnew >= 65536 && 4ULL * nnew >= t.n) {
-        TRY_PK(pk_slots_resize(ctx, t, t.n, t.nslots));  // (many keys placed by claims: rebuilt in home order)
-    }
+    // the next call starts at load <= 0.6; a call that placed a quarter of the keys by claims leaves
+    // them rebuilt in home order (sized the same way: the next call's own pre-sizing would rebuild again)
+    if (4 * t.n > 3 * t.nslots || (nnew >= 65536 && 4ULL * nnew >= t.n)) TRY_PK(pk_slots_resize(ctx, t, t.n + t.n / 4));
     return CORRO_OK;
 }
 
