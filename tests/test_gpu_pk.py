@@ -359,3 +359,36 @@ def test_failed_intern_leaves_the_table_as_it_was(fault):
     assert all(k[i] == kh[idn[i]] for i in range(len(idn)) if idn[i] < 500)  # held keys keep their ids
     e.close()
     f.close()
+
+
+def _rebuild_digest():
+    """Keys of three calls on one table: 200 K new keys (a rebuild after the call: a quarter of the table
+    new), a call with 600 K more (growth), then every key again (a warm call through the rebuilt table)."""
+    import hashlib
+    import torch
+    import corrosion_amd as ca
+    e = ca.MergeEngine(SCHEMA, capacity_hint=1 << 12, interned=INTERNED)
+    h = hashlib.sha256()
+    for ids in (torch.arange(200_000, device="cuda"), torch.arange(100_000, 800_000, device="cuda"),
+                torch.arange(800_000, device="cuda").flip(0)):
+        k = e.pk_keys_device("testsblob", *synth.blob_pks_torch(ids)).cpu().numpy().view(np.uint64)
+        h.update(k.tobytes())
+    e.close()
+    return h.hexdigest()
+
+
+def test_intern_rebuild_in_home_order_matches_rebuild_by_claims():
+    """The table rebuilt from the arena in home order (sorted homes, max-scan positions; the default)
+    and by claims (CORRO_PK_ORDERED=0, also the fallback when the pad runs out) intern every call to
+    the same keys: ids are first-seen ranks whatever the slot layout, and a warm call re-finds every key
+    through the rebuilt table."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    ordered = _rebuild_digest()
+    code = ("import sys; sys.path[:0] = [%r, %r]; import test_gpu_pk as t; print(t._rebuild_digest())" % (root, here))
+    env = dict(os.environ, CORRO_PK_ORDERED="0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == ordered
