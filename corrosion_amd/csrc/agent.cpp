@@ -1604,6 +1604,40 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     if (R.err & 2) return fail(CORRO_E_INVALID, "changeset site ordinal is not registered (or actor_id is NULL)");
     stage("headers");
 
+    // A call whose every changeset the device decided (no host changesets) knows its batch now: the
+    // order pass (agent_dev_batch_sorted: the applied spans in ActorId order and their positions --
+    // device scratch only, neither the state nor the bookie) runs on a second thread while this one
+    // walks the actors' bookkeeping. The merge still waits for the walk (a gap conflict fails the call
+    // before the state is touched). This thread makes no device call until it joins the other.
+    struct EarlyOrder {
+        std::thread t;
+        int rc = CORRO_OK;
+        std::string err;
+        corro_changes batch{};
+        bool gathered = false;
+        corro::AgentPositions pm{};
+        ~EarlyOrder() {
+            if (t.joinable()) t.join();
+        }
+    } early;
+    {
+        const char *gb = std::getenv("CORRO_AGENT_GAPS_BATCH");  // (the batched gap pass uses the device)
+        if (R.nh == 0 && nchanges && R.nspans && !(gb && std::atoi(gb) == 1))
+            early.t = std::thread([&] {
+                try {
+                    early.rc = corro::agent_dev_batch_sorted(ctx, &dv, ncs, R.nspans, R.nchanges, R.ts_any, &early.batch,
+                                                             &early.gathered, &early.pm);
+                    if (early.rc != CORRO_OK) early.err = corro_last_error();
+                } catch (const std::bad_alloc &) {
+                    early.rc = CORRO_E_NOMEM;
+                    early.err = "host allocation failed ordering the batch";
+                } catch (const std::exception &e) {
+                    early.rc = CORRO_E_INVALID;
+                    early.err = e.what();
+                }
+            });
+    }
+
     // actors of the call, each with its host changesets (R.hcs: grouped by actor in site-rank order)
     std::vector<ActorWork> work;
     std::vector<int64_t> work_of(nsites, -1);
@@ -1786,8 +1820,18 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         corro::AgentPositions pm{};
         if (nb) {
             bool gathered = false;
-            TRY_RC(corro::agent_dev_batch_sorted(ctx, &dv, ncs, nspans, nb, R.ts_any, &batch, &gathered, &pm));
-            stage(gathered ? "order+gather" : (pm.on ? "order+positions" : "order"));
+            if (early.t.joinable()) {  // (ordered alongside the walk)
+                early.t.join();
+                if (early.rc != CORRO_OK) return fail(early.rc, early.err);
+                if (nspans != R.nspans || nb != R.nchanges) throw std::logic_error("early order: the walk added spans");
+                batch = early.batch;
+                gathered = early.gathered;
+                pm = early.pm;
+                stage("order_joined");
+            } else {
+                TRY_RC(corro::agent_dev_batch_sorted(ctx, &dv, ncs, nspans, nb, R.ts_any, &batch, &gathered, &pm));
+                stage(gathered ? "order+gather" : (pm.on ? "order+positions" : "order"));
+            }
             int rc = CORRO_OK;
             uint8_t *ib = corro::agent_dev_impact_buf(ctx, nb, &rc);
             if (rc != CORRO_OK) return rc;

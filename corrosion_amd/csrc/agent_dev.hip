@@ -1652,6 +1652,7 @@ int agent_dev_put_host(corro_ctx *ctx, const uint32_t *idx, uint64_t n, const st
 
 int agent_dev_batch_sorted(corro_ctx *ctx, const corro_changes *dv, uint64_t ncs, uint64_t nspans, uint64_t nbatch,
                            bool need_ts, corro_changes *batch, bool *gathered, AgentPositions *pm) {
+    CORRO_HIP_TRY(hipSetDevice(ctx->device));  // (callable from a second host thread)
     hipStream_t s = ctx->stream;
     const DevCols c = dev_cols(ctx);
     if (nspans) {
