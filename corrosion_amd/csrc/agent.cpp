@@ -899,8 +899,15 @@ int commit_staged(corro_ctx *ctx, corro_bookie *bk, const corro_changes *dv, con
     return rc;
 }
 
-// the call's __corro_seq_bookkeeping rows (one per (site, version): the actors' keys are disjoint)
-void commit_seqbook(corro_bookie *bk, const std::vector<Staged *> &order) {
+// The call's __corro_seq_bookkeeping rows (one per (site, version): the actors' keys are disjoint), in
+// two parts: seqbook_prepare only READS the bookie (it runs alongside the merge on the commit
+// preparation thread) and moves the call's books out of the staged maps into new entries and updates
+// of held slots; seqbook_apply writes them after the merge.
+struct SeqPrep {
+    FlatMap<SeqKey, SeqBook>::Entries add;            // new keys, ascending
+    std::vector<std::pair<SeqBook *, SeqBook>> upd;   // held keys: their slots and new books
+};
+void seqbook_prepare(corro_bookie *bk, const std::vector<Staged *> &order, SeqPrep &S) {
     std::vector<Staged *> blk;
     for (Staged *st : order)
         if (!st->seqbook.empty()) blk.push_back(st);
@@ -911,7 +918,8 @@ void commit_seqbook(corro_bookie *bk, const std::vector<Staged *> &order) {
     if (bk->seqbook.live() == 0) {
         // no seq books held (every earlier partial version completed or was cleared): the call's books,
         // one actor's (sorted, disjoint) keys per task, are written in place into the map's new storage
-        FlatMap<SeqKey, SeqBook>::Entries add(base.back());
+        FlatMap<SeqKey, SeqBook>::Entries &add = S.add;
+        add.resize(base.back());
         run_parallel(blk.size(), [&](size_t b) {
             size_t q = base[b];
             for (auto &[k, sb] : blk[b]->seqbook) {
@@ -924,7 +932,6 @@ void commit_seqbook(corro_bookie *bk, const std::vector<Staged *> &order) {
         bool sorted = true;
         for (size_t q = 1; q < add.size() && sorted; q++) sorted = add[q - 1].key < add[q].key;
         if (!sorted) std::sort(add.begin(), add.end(), [](const auto &x, const auto &y) { return x.key < y.key; });
-        bk->seqbook.merge(std::move(add));
         return;
     }
     // gathered in parallel (one actor's map per task), each item with the slot it updates, if any
@@ -941,21 +948,28 @@ void commit_seqbook(corro_bookie *bk, const std::vector<Staged *> &order) {
     }, 16);
     bool sorted = true;
     for (size_t q = 1; q < items.size() && sorted; q++) sorted = items[q - 1].first < items[q].first;
-    FlatMap<SeqKey, SeqBook>::Entries add;
     if (!sorted) {  // (two actors' keys interleave: plain path)
         std::sort(items.begin(), items.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
         for (auto &[k, sb] : items) {
-            if (SeqBook *x = bk->seqbook.find(k)) *x = std::move(sb);
-            else add.push_back({k, std::move(sb), false});
+            if (SeqBook *x = bk->seqbook.find(k)) S.upd.emplace_back(x, std::move(sb));
+            else S.add.push_back({k, std::move(sb), false});
         }
     } else {
-        add.reserve(items.size());
+        S.add.reserve(items.size());
         for (size_t q = 0; q < items.size(); q++) {
-            if (hit[q]) *hit[q] = std::move(items[q].second);
-            else add.push_back({items[q].first, std::move(items[q].second), false});
+            if (hit[q]) S.upd.emplace_back(hit[q], std::move(items[q].second));
+            else S.add.push_back({items[q].first, std::move(items[q].second), false});
         }
     }
-    bk->seqbook.merge(std::move(add));
+}
+void seqbook_apply(corro_bookie *bk, SeqPrep &S) {
+    for (auto &[x, sb] : S.upd) *x = std::move(sb);
+    bk->seqbook.merge(std::move(S.add));
+}
+void commit_seqbook(corro_bookie *bk, const std::vector<Staged *> &order) {
+    SeqPrep S;
+    seqbook_prepare(bk, order, S);
+    seqbook_apply(bk, S);
 }
 
 // sorted site << 40 | version keys of every (site, version) holding buffered rows or seq bookkeeping
@@ -994,6 +1008,35 @@ std::vector<uint64_t> buffered_keys(const corro_bookie *bk) {
     std::merge(a.begin(), a.end(), b.begin(), b.end(), k.begin());
     k.erase(std::unique(k.begin(), k.end()), k.end());
     return k;
+}
+
+// buffered_keys as it will read once the prepared commit (fast path, or nothing staged) and the prepared
+// seq books are written: the bookie's keys now plus the ones those writes add (the writes only add
+// keys or fill held ones), computed alongside the merge
+std::vector<uint64_t> buffered_keys_after(const corro_bookie *bk, const CommitPrep &P, const SeqPrep &S) {
+    // (every list ascending: the tables, the prepared new and updated keys -- actors' disjoint key
+    // ranges in key order on the fast path -- and the new seq books; merged, not sorted)
+    std::vector<uint64_t> a, b, c;
+    a.reserve(P.add.size());
+    b.reserve(P.upd.size());
+    c.reserve(S.add.size());
+    auto buf_key = [](std::vector<uint64_t> &v, const BufKey &key, const BufEntry &e) {
+        if (!e.empty() && key.second >= 0 && (uint64_t)key.second < (1ULL << 40))
+            v.push_back((uint64_t)key.first << 40 | (uint64_t)key.second);
+    };
+    for (const auto &x : P.add) buf_key(a, x.key, x.val);
+    for (const auto &[key, e] : P.upd) buf_key(b, key, e);
+    for (const auto &x : S.add)
+        if (x.key.second < (1ULL << 40)) c.push_back((uint64_t)x.key.first << 40 | x.key.second);
+    auto merge2 = [](const std::vector<uint64_t> &x, const std::vector<uint64_t> &y) {
+        std::vector<uint64_t> o(x.size() + y.size());
+        std::merge(x.begin(), x.end(), y.begin(), y.end(), o.begin());
+        return o;
+    };
+    if (!std::is_sorted(b.begin(), b.end())) std::sort(b.begin(), b.end());
+    std::vector<uint64_t> out = merge2(merge2(buffered_keys(bk), a), merge2(b, c));
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
 }
 
 // clear_buffered of single versions, many at once: sorted, then each map walked once per slice of the
@@ -1778,7 +1821,11 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     // The buffered-row commit's preparation only reads the bookie and the staged rows, so it runs on a
     // host thread while the merge runs on the device (its writes wait for the merge: a failed merge
     // leaves the bookie as it was).
+    // (and the seq books' moves and the buffered-meta keys the commit will leave, both read-only too)
     CommitPrep prep;
+    SeqPrep seqp;
+    std::vector<uint64_t> pre_keys;
+    bool seq_ready = false, keys_ready = false;
     std::string prep_err;
     int prep_rc = CORRO_OK;
     bool prep_started = false;
@@ -1796,6 +1843,14 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             };
             try {
                 commit_prepare(ctx, bk, have_dv, sto, ntables, prep, markp);
+                seqbook_prepare(bk, sto, seqp);
+                seq_ready = true;
+                markp("seq_prep");
+                if (!prep.any || prep.fast) {
+                    pre_keys = buffered_keys_after(bk, prep, seqp);
+                    keys_ready = true;
+                    markp("keys_prep");
+                }
             } catch (const std::bad_alloc &) {  // (same code as the serial path's host OOM)
                 prep_rc = CORRO_E_NOMEM;
                 prep_err = "host allocation failed preparing the commit";
@@ -1866,11 +1921,12 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
         if (prof) prof_line += " [prepared alongside the merge:" + prep.prof + "]";
     }
     TRY_RC(commit_staged(ctx, bk, nchanges ? &dv : nullptr, sto, committed, stage, prep_started ? &prep : nullptr));
-    commit_seqbook(bk, sto);
+    if (seq_ready) seqbook_apply(bk, seqp);
+    else commit_seqbook(bk, sto);
     stage("seqbook");
     // check_buffered_meta_to_clear (util.rs:513-520, :1292-1303): the merged versions that hold
     // buffered rows or seq bookkeeping, found on the device against the (small) set of such keys
-    std::vector<uint64_t> bkeys = buffered_keys(bk);
+    std::vector<uint64_t> bkeys = keys_ready ? std::move(pre_keys) : buffered_keys(bk);
     stage("bkeys");
     std::vector<std::pair<uint32_t, uint64_t>> sv;
     TRY_RC(corro::agent_dev_commit_headers(ctx, ncs, out->known, bkeys.empty() ? nullptr : &bkeys, &sv));
