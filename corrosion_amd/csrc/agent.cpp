@@ -1869,15 +1869,16 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
             if (t.joinable()) t.join();
         }
     } join_prep{prep_thread};
+    const bool early_ran = early.t.joinable();
+    if (early_ran) early.t.join();  // (before this thread's next device call: one thread on ctx at a time)
+    if (early_ran && early.rc != CORRO_OK) return fail(early.rc, early.err);
     if (nb || out->impactful) {
         corro_changes batch{};
         const uint8_t *imp = nullptr;
         corro::AgentPositions pm{};
         if (nb) {
             bool gathered = false;
-            if (early.t.joinable()) {  // (ordered alongside the walk)
-                early.t.join();
-                if (early.rc != CORRO_OK) return fail(early.rc, early.err);
+            if (early_ran) {  // (ordered alongside the walk)
                 if (nspans != R.nspans || nb != R.nchanges) throw std::logic_error("early order: the walk added spans");
                 batch = early.batch;
                 gathered = early.gathered;
