@@ -1830,7 +1830,9 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
     int prep_rc = CORRO_OK;
     bool prep_started = false;
     std::thread prep_thread;
-    if (nh >= 4096) {
+    const char *pm_env = std::getenv("CORRO_AGENT_PREP_MIN");  // (read per call: tests run small calls through it)
+    const uint64_t prep_min = pm_env ? std::strtoull(pm_env, nullptr, 10) : 4096;
+    if (nh >= prep_min) {
         prep_started = true;
         prep_thread = std::thread([&, have_dv = nchanges != 0] {
             auto t0 = std::chrono::steady_clock::now();

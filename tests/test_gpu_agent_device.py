@@ -602,12 +602,17 @@ def _mixed_scale_calls(seed, nact=64, nver=120, per=8, ncalls=3):
     return ids, calls
 
 
-def test_mixed_call_at_scale_matches_host_path():
+@pytest.mark.parametrize("prep_min", [None, "0"])
+def test_mixed_call_at_scale_matches_host_path(prep_min, monkeypatch):
     """The mixed drop-in call at ~8.7 K changesets x 3 calls: device-resident headers (per-changeset
     device decisions, host walk of the rest, partial rows in the device pool) against the
     host-memory path -- outcomes, impactful flags, merged state, db_versions, committed counts, gap
-    bookkeeping and partials"""
+    bookkeeping and partials. prep_min "0": the commit's read-only parts (buffered-row groups, seq-book
+    moves, the buffered-meta keys the commit leaves) on the preparation thread alongside the merge, as
+    calls of 4096 host changesets or more take them (CORRO_AGENT_PREP_MIN)."""
     import corrosion_amd as ca
+    if prep_min is not None:
+        monkeypatch.setenv("CORRO_AGENT_PREP_MIN", prep_min)
     ids, calls = _mixed_scale_calls(51)
     sides = []
     for _k in range(2):
