@@ -1738,6 +1738,15 @@ int agent_dev_reserve(corro_ctx *ctx, uint64_t ncs) {
         CORRO_HIP_TRY(hipHostMalloc(&ctx->h_hdr, hb + hb / 4, hipHostMallocDefault));
         ctx->h_hdr_bytes = hb + hb / 4;
     }
+    // the buffered-row pool's copy jobs (bufpool_append): sized for jobs of a sixteenth of the changesets
+    const size_t pb = 5 * al256(std::max<uint64_t>(n / 16, 1) * 8);
+    if (pb > ctx->h_pool_bytes) {
+        if (ctx->h_pool) (void)hipHostFree(ctx->h_pool);
+        ctx->h_pool = nullptr;
+        ctx->h_pool_bytes = 0;
+        CORRO_HIP_TRY(hipHostMalloc(&ctx->h_pool, pb, hipHostMallocDefault));
+        ctx->h_pool_bytes = pb;
+    }
     return CORRO_OK;
 }
 

@@ -255,17 +255,32 @@ int bufpool_append(corro_ctx *ctx, DevBufPool *p, const corro_changes *dv, std::
     uint64_t total = 0;
     for (const PoolCopy &j : jobs) total += j.count;
     if (p->top + total > p->cap) return fail(CORRO_E_INVALID, "buffered-row pool not reserved");
-    std::vector<uint64_t> src(n), dst(n), cnt(n), ts(n);
+    // the four job columns written straight into one pinned area and sent up in one copy (four pageable
+    // copies of a mixed call's 5 x 10^4 jobs cost ~0.4 ms)
+    const size_t col = al256(n * 8);
+    if (4 * col > ctx->h_pool_bytes) {
+        if (ctx->h_pool) (void)hipHostFree(ctx->h_pool);  // (the previous append synchronised before returning)
+        ctx->h_pool = nullptr;
+        ctx->h_pool_bytes = 0;
+        CORRO_HIP_TRY(hipHostMalloc(&ctx->h_pool, 4 * col + col, hipHostMallocDefault));
+        ctx->h_pool_bytes = 4 * col + col;
+    }
+    if (int rc = ctx->d_agent_fetch.ensure(4 * col + 256)) return rc;
+    uint8_t *hp = static_cast<uint8_t *>(ctx->h_pool);
+    uint64_t *hc[4];
+    for (int q = 0; q < 4; q++) hc[q] = reinterpret_cast<uint64_t *>(hp + q * col);
     for (uint64_t k = 0; k < n; k++) {
         jobs[k].dst = p->top;
         p->top += jobs[k].count;
-        src[k] = jobs[k].src;
-        dst[k] = jobs[k].dst;
-        cnt[k] = jobs[k].count;
-        ts[k] = jobs[k].ts;
+        hc[0][k] = jobs[k].src;
+        hc[1][k] = jobs[k].dst;
+        hc[2][k] = jobs[k].count;
+        hc[3][k] = jobs[k].ts;
     }
+    uint8_t *db = ctx->d_agent_fetch.as<uint8_t>();
+    CORRO_HIP_TRY(hipMemcpyAsync(db, hp, 4 * col, hipMemcpyHostToDevice, ctx->stream));
     uint64_t *d[4];
-    if (int rc = stage_cols(ctx, {&src, &dst, &cnt, &ts}, n, d)) return rc;
+    for (int q = 0; q < 4; q++) d[q] = reinterpret_cast<uint64_t *>(db + q * col);
     PoolGatherArgs g{};
     g.in = *dv;
     g.out = pool_view(p->buf.p, p->cap);

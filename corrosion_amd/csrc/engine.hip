@@ -735,6 +735,7 @@ void corro_ctx_destroy(corro_ctx *ctx) {
     if (ctx->h_agent) (void)hipHostFree(ctx->h_agent);
     if (ctx->h_hdr) (void)hipHostFree(ctx->h_hdr);
     if (ctx->h_hfetch) (void)hipHostFree(ctx->h_hfetch);
+    if (ctx->h_pool) (void)hipHostFree(ctx->h_pool);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

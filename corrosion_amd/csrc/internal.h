@@ -273,6 +273,8 @@ struct corro_ctx {
     size_t h_hdr_bytes = 0;
     void *h_hfetch = nullptr;        // the host changesets' headers read back (pinned, agent_dev_headers)
     size_t h_hfetch_bytes = 0;
+    void *h_pool = nullptr;          // the buffered-row pool's copy jobs on their way up (pinned, bufpool_append)
+    size_t h_pool_bytes = 0;
     corro::DevBuf d_hdr_stage;       // their device copy + the device known outcomes
     uint64_t agent_ncs = 0;       // changesets of the current call (d_agent_spans column length)
     uint64_t agent_nbatch_max = 0;  // input changes of the current call (bound on the applied batch)
