@@ -1844,8 +1844,29 @@ int process_dev_headers(corro_ctx *ctx, corro_bookie *bk, const corro_changeset 
                 t0 = t;
             };
             try {
-                commit_prepare(ctx, bk, have_dv, sto, ntables, prep, markp);
-                seqbook_prepare(bk, sto, seqp);
+                // (the seq books' moves on a third thread: they read other staged data and other bookie
+                // tables than the buffered-row preparation, and both have serial stretches)
+                std::string seq_err;
+                bool seq_ok = false, seq_oom = false;
+                std::thread seq_thread([&] {
+                    try {
+                        seqbook_prepare(bk, sto, seqp);
+                        seq_ok = true;
+                    } catch (const std::bad_alloc &) {
+                        seq_oom = true;
+                    } catch (const std::exception &e) {
+                        seq_err = e.what();
+                    }
+                });
+                try {
+                    commit_prepare(ctx, bk, have_dv, sto, ntables, prep, markp);
+                } catch (...) {
+                    seq_thread.join();
+                    throw;
+                }
+                seq_thread.join();
+                if (seq_oom) throw std::bad_alloc();
+                if (!seq_ok) throw std::runtime_error(seq_err);
                 seq_ready = true;
                 markp("seq_prep");
                 if (!prep.any || prep.fast) {
