@@ -508,6 +508,12 @@ __device__ inline bool pk_eq_committed(const PkArgs &a, uint32_t id, const PkWor
 // common case: pack_columns output back to back, or a decoded frame) are copied into LDS with 16-B
 // loads along the bytes; lanes then parse from LDS. Larger windows read their bytes from HBM.
 constexpr uint32_t PK_WAVE_STAGE = 2048;
+#ifndef PK_GRID_MAX
+// k_pk_find workgroups (grid-stride beyond): four per CU of the MI355X's 256. More waves in flight only
+// queue more random slot reads in the fabric -- warm intern 3.2 ms at 1024 workgroups, 3.4 at 2048, 4.0
+// at 4096, 5.3 at the former 8192, 8.3 at 16384, and 5.1 at 512 (profiles/r06_pk_grid_ab.log)
+#define PK_GRID_MAX 1024
+#endif
 #ifndef PK_DIAG
 #define PK_DIAG 0  // diagnostic builds: 1 no probe, 2 no canonical parse, 4 no LDS staging
 #endif
@@ -1078,7 +1084,7 @@ int pk_keys_device(corro_ctx *ctx, uint32_t table, const PkRefs &r, uint64_t n, 
         HIP_PKC(hipMemsetAsync(a.ctl, 0, 64, s));
         if (bad) HIP_PKC(hipMemsetAsync(bad, 0, n, s));
         const uint32_t nwaves = (uint32_t)((n + 63) / 64);
-        const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((nwaves + 3) / 4, 8192));
+        const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((nwaves + 3) / 4, PK_GRID_MAX));
         if (fault_armed("pk_find")) return failc(fail(CORRO_E_DEVICE, "injected fault (CORRO_FAULT): pk_find"));
         hipLaunchKernelGGL(k_pk_find, dim3(grid), dim3(PK_FIND_THREADS), 0, s, a);
         HIP_PKC(hipGetLastError());
